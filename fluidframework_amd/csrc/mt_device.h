@@ -1,0 +1,113 @@
+// mt_device.h — shared constants and record layouts of the MI355X merge-tree replay engine.
+//
+// Used by the HIP kernels (mt_engine.hip) and the host side of the C-ABI library
+// (mt_host.cpp).  Everything here is plain data; no torch types, no STL.
+#pragma once
+
+#include <stdint.h>
+
+namespace mt {
+
+// status codes (include/mtreplay.h MT_STATUS_*; the first six match the oracle's)
+enum : int32_t {
+    ST_OK = 0,
+    ST_INVALID_POS = 1,  // "MergeTree insert failed" (merge-tree/src/mergeTree.ts:2210-2216)
+    ST_SEQ_ORDER = 2,    // client.ts:461-462, 824
+    ST_MSN_ORDER = 3,    // client.ts:463-464, mergeTree.ts:1719-1722
+    ST_UNSUPPORTED = 4,  // outside the observer path / device limits (e.g. > 32 clients)
+    ST_BAD_INPUT = 5,
+    ST_CAPACITY = 6,     // per-document LDS/HBM capacity exceeded: re-run with larger caps
+    ST_INTERNAL = 7
+};
+
+constexpr int kWave = 64;
+constexpr int kMaxNodes = 8;            // MaxNodesInBlock, mergeTree.ts:334
+constexpr uint32_t kGranularity = 256;  // TextSegmentGranularity, mergeTree.ts:1059
+constexpr int kZamboniMax = 2;          // zamboniSegmentsMaxCount, mergeTree.ts:1061
+constexpr int kMaxClients = 32;         // overlap mask width
+constexpr int32_t kNoneSeq = 0x7FFFFFFF;  // removedSeq === undefined
+constexpr uint32_t kMarkerSlot = 0xFFFFu; // oe entry that ends a leaf block
+constexpr uint32_t kNoClient = 63u;
+
+// needsScour tri-state (mergeTree.ts:63, 1279, 1438)
+constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
+
+// segment meta word
+//   [0,6)  clientId (short id)         [6,12) removedClientId (63 = none)
+//   [12]   Marker                       [13]   text ends with '\n'
+//   [14]   linked (in the tree)         [16,32) slot generation (heap entry validity)
+constexpr uint32_t kMetaMarker = 1u << 12;
+constexpr uint32_t kMetaEndsNL = 1u << 13;
+constexpr uint32_t kMetaLinked = 1u << 14;
+
+// one output record per oe entry (doc order), 8 x u32
+struct OutRec {
+    uint32_t len;    // cachedLength (0 for a block marker)
+    int32_t seq;
+    int32_t rseq;    // kNoneSeq when not removed
+    uint32_t meta;
+    uint32_t ovl;    // removedClientOverlap as a bit mask
+    uint32_t props;  // prop-set id in the doc's pool (0 = undefined)
+    uint32_t toff;   // text offset in the doc's text region (Marker: refType)
+    uint32_t blk;    // leaf block id << 16 | slot (slot 0xFFFF: end-of-block marker)
+};
+static_assert(sizeof(OutRec) == 32, "OutRec");
+
+// per-document scalar results
+struct DocOut {
+    int32_t status;
+    int32_t min_seq;
+    int32_t cur_seq;
+    int32_t depth;
+    int32_t n_out;      // OutRec count
+    uint32_t text_top;  // text region high-water mark (code units)
+    uint32_t pool_top;  // prop pool high-water mark (words)
+    int32_t ops_done;   // ops applied before status != OK
+    int32_t max_oe;     // high-water marks (capacity planning)
+    int32_t max_slots;
+    int32_t max_blocks;
+    int32_t max_heap;
+    int32_t fail_op;    // index of the op that failed (-1)
+    int32_t cap_kind;   // ST_CAPACITY cause: 1 LDS tables, 2 text arena, 3 prop pool, 4 out records
+    int32_t gen_text;   // generator: payload code units written
+    int32_t gen_props;  // generator: prop records written
+};
+static_assert(sizeof(DocOut) == 64, "DocOut");
+
+// per-document capacities of the LDS-resident state
+struct Caps {
+    int32_t seg;   // segment slots
+    int32_t oe;    // ordered entries (segments + one end marker per leaf block)
+    int32_t blk;   // blocks
+    int32_t heap;  // zamboni heap entries
+};
+
+// kernel parameters
+struct ReplayParams {
+    const void *ops;              // mt_op[]
+    const int64_t *doc_op_off;    // [n_docs+1]
+    uint16_t *text;               // text heap (code units)
+    const uint64_t *doc_text_base;
+    const uint32_t *doc_text_len; // payload length (arena starts here)
+    const uint32_t *doc_text_cap;
+    uint32_t *pool;               // prop-set pool (words)
+    const uint64_t *doc_pool_base;
+    const uint32_t *doc_pool_cap;
+    const void *props_in;         // mt_prop[] (op prop records, batch-global offsets)
+    const uint8_t *value_flags;   // per value id: bit0 = JS-falsy (rewrite semantics)
+    uint32_t n_values;
+    OutRec *out;                  // [n_docs * out_cap]
+    DocOut *doc_out;
+    int64_t n_docs;               // workgroups in this launch
+    int64_t doc_first;            // generator: global doc index of blockIdx.x == 0
+    const int32_t *doc_list;      // non-null: blockIdx.x replays doc doc_list[blockIdx.x]
+                                  // (capacity escalation); out/doc_out stay indexed by blockIdx.x
+    int32_t out_cap;
+    Caps caps;
+    // generator mode (non-null gen): ops/text/props are written, not read
+    const void *gen;              // mt_gen_params*
+    void *gen_ops;                // mt_op[n_docs * n_ops]
+    void *gen_props;              // mt_prop[n_docs * 2 * n_ops] (doc-local offsets rebased by host)
+};
+
+}  // namespace mt

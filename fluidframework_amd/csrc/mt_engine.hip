@@ -1,0 +1,1298 @@
+// mt_engine.hip — MI355X (gfx950) batch replay of sequenced merge-tree ops.
+//
+// One 64-lane wavefront (= one workgroup) owns one document for the whole op log; the
+// document's merge-tree lives in LDS as a flat, wave-scannable structure:
+//
+//   oe[]        document order of the tree's leaves: each entry is (leaf block id << 16 | slot);
+//               every leaf block ends with a marker entry (slot 0xFFFF), so empty leaf blocks
+//               (pack can create them, mergeTree.ts:1383-1386) stay addressable.
+//   s_*[slot]   segment fields (SoA): length, seq, removedSeq, client ids, overlap mask,
+//               prop-set id, text offset/capacity.
+//   b_*[block]  B-tree blocks (MaxNodesInBlock = 8): parent, child count, needsScour,
+//               interior child lists.  Leaf membership is implicit in oe.
+//   h_*         the zamboni heap (collections.ts:213-265), same algorithm, same tie order.
+//
+// Position resolution replaces PartialSequenceLengths (partialLengths.ts) by a per-op,
+// lane-parallel visibility test of every leaf (nodeLength, mergeTree.ts:1659-1699) and a
+// wave prefix scan; the B-tree walk of insertingWalk (mergeTree.ts:2345-2474) reduces to
+// "first entry that satisfies the leaf tie rule, else the end of the first leaf block whose
+// cumulative length reaches pos" (DESIGN.md "Flat insertingWalk").  Block splits, pack and
+// zamboni follow mergeTree.ts:1289-1478, 2476-2489 exactly, so leaf-block membership — and
+// hence SnapshotV1 bytes — match the reference.
+//
+// No MFMA: the path is integer scan / compaction work bound by LDS latency and HBM.
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/mt_gen.h"
+#include "../../include/mt_oplog.h"
+#include "mt_device.h"
+
+namespace mt {
+
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int32_t rfl(int32_t x) { return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)x); }
+__device__ __forceinline__ uint32_t rdl(uint32_t x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ int32_t rdl(int32_t x, int l) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)x, l); }
+
+__device__ __forceinline__ uint32_t scan_incl(uint32_t v) {
+    const int l = threadIdx.x;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, kWave);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int first_lane(uint64_t b) { return __builtin_ctzll(b); }
+
+// single-wave workgroup: orders LDS traffic between lanes
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+__device__ __forceinline__ uint32_t hash_pair(uint32_t k, uint32_t v) {
+    uint32_t h = k * 0x9E3779B1u ^ (v + 0x7F4A7C15u) * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    return h | 1u;
+}
+
+struct Loc {
+    int32_t idx;    // oe index
+    uint32_t excl;  // view position before entry idx
+    int32_t found;
+    int32_t marker;
+};
+
+struct Engine {
+    // ---- LDS state
+    uint32_t *oe;
+    uint32_t *s_len, *s_meta, *s_ovl, *s_props, *s_toff, *s_tcap, *s_phash;
+    int32_t *s_seq, *s_rseq;
+    uint16_t *s_free;
+    uint16_t *b_parent, *b_free, *b_child;
+    uint8_t *b_count, *b_leaf;
+    int8_t *b_scour;
+    uint32_t *h_key;
+    int32_t *h_seq;
+    uint32_t *scratch;  // 256 words
+    Caps cap;
+    // ---- uniform scalars
+    int32_t n_oe, slot_top, n_free, blk_top, n_bfree, root, depth, hn;
+    int32_t min_seq, cur_seq, status;
+    uint32_t arena_top, pool_top;
+    int32_t max_oe, max_heap;
+    // ---- global
+    uint16_t *text;
+    uint32_t text_cap;
+    uint32_t *pool;
+    uint32_t pool_cap;
+    const mt_prop *props_in;
+    const uint8_t *value_flags;
+    uint32_t n_values;
+    int lane;
+
+    // ------------------------------------------------------------------ layout
+    __device__ static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+    __host__ __device__ static size_t lds_bytes(const Caps &c) {
+        size_t o = 0;
+        auto take = [&](size_t n) { o = (o + n + 15) & ~(size_t)15; };
+        take(4u * c.oe);
+        for (int i = 0; i < 9; i++) take(4u * c.seg);
+        take(2u * c.seg);
+        take(2u * c.blk);
+        take(2u * c.blk);
+        take(2u * 8 * c.blk);
+        take(c.blk);
+        take(c.blk);
+        take(c.blk);
+        take(4u * (c.heap + 1));
+        take(4u * (c.heap + 1));
+        take(4u * 256);
+        return o;
+    }
+    __device__ void carve(uint8_t *base, const Caps &c) {
+        size_t o = 0;
+        auto take = [&](size_t n) {
+            uint8_t *p = base + o;
+            o = (o + n + 15) & ~(size_t)15;
+            return p;
+        };
+        cap = c;
+        oe = (uint32_t *)take(4u * c.oe);
+        s_len = (uint32_t *)take(4u * c.seg);
+        s_seq = (int32_t *)take(4u * c.seg);
+        s_rseq = (int32_t *)take(4u * c.seg);
+        s_meta = (uint32_t *)take(4u * c.seg);
+        s_ovl = (uint32_t *)take(4u * c.seg);
+        s_props = (uint32_t *)take(4u * c.seg);
+        s_toff = (uint32_t *)take(4u * c.seg);
+        s_tcap = (uint32_t *)take(4u * c.seg);
+        s_phash = (uint32_t *)take(4u * c.seg);
+        s_free = (uint16_t *)take(2u * c.seg);
+        b_parent = (uint16_t *)take(2u * c.blk);
+        b_free = (uint16_t *)take(2u * c.blk);
+        b_child = (uint16_t *)take(2u * 8 * c.blk);
+        b_count = (uint8_t *)take(c.blk);
+        b_leaf = (uint8_t *)take(c.blk);
+        b_scour = (int8_t *)take(c.blk);
+        h_key = (uint32_t *)take(4u * (c.heap + 1));
+        h_seq = (int32_t *)take(4u * (c.heap + 1));
+        scratch = (uint32_t *)take(4u * 256);
+    }
+
+    int32_t cap_kind;
+    __device__ void set_fail(int32_t st) {
+        if (status == ST_OK) status = st;
+    }
+    __device__ void cap_fail(int32_t kind) {
+        if (status == ST_OK) {
+            status = ST_CAPACITY;
+            cap_kind = kind;
+        }
+    }
+
+    // ------------------------------------------------------------------ init
+    __device__ void init() {
+        n_oe = 0;
+        slot_top = 0;
+        n_free = 0;
+        blk_top = 0;
+        n_bfree = 0;
+        hn = 0;
+        min_seq = 0;
+        cur_seq = 0;
+        status = ST_OK;
+        cap_kind = 0;
+        max_oe = 0;
+        max_heap = 0;
+        // initialNode (mergeTree.ts:1125): an empty root leaf block
+        root = alloc_block(1);
+        depth = 1;
+        b_parent[root] = 0xFFFF;  // lane-uniform writes (every lane stores the same value)
+        oe_insert(0, (uint32_t)root << 16 | kMarkerSlot);
+        // heap sentinel LRUSegmentComparer.min = { maxSeq: -2 }
+        h_key[0] = 0;
+        h_seq[0] = -2;
+        wsync();
+    }
+
+    // ------------------------------------------------------------------ allocation
+    __device__ int32_t alloc_slot() {
+        int32_t s;
+        if (n_free > 0) {
+            s = rfl((int32_t)s_free[n_free - 1]);
+            n_free--;
+        } else {
+            if (slot_top >= cap.seg) {
+                cap_fail(1);
+                return -1;
+            }
+            s = slot_top++;
+            s_meta[s] = 0;  // generation 0
+        }
+        return s;
+    }
+    __device__ void free_slot(int32_t s) {
+        uint32_t m = s_meta[s];
+        uint32_t gen = (m >> 16) + 1;
+        s_meta[s] = (gen << 16);  // unlinked, next generation
+        s_free[n_free] = (uint16_t)s;
+        n_free++;
+    }
+    __device__ int32_t alloc_block(int leaf) {
+        int32_t b;
+        if (n_bfree > 0) {
+            b = rfl((int32_t)b_free[n_bfree - 1]);
+            n_bfree--;
+        } else {
+            if (blk_top >= cap.blk || blk_top >= 0xFFFF) {
+                cap_fail(1);
+                return 0;
+            }
+            b = blk_top++;
+        }
+        b_leaf[b] = (uint8_t)leaf;
+        b_count[b] = 0;
+        b_scour[b] = kScourUndef;
+        b_parent[b] = 0xFFFF;
+        return b;
+    }
+    __device__ void free_block(int32_t b) {
+        b_free[n_bfree] = (uint16_t)b;
+        n_bfree++;
+    }
+
+    // ------------------------------------------------------------------ oe shifting
+    // insert entry e before index p (lane-parallel shift right by one)
+    __device__ void oe_insert(int32_t p, uint32_t e) {
+        if (n_oe + 1 > cap.oe) {
+            cap_fail(1);
+            return;
+        }
+        wsync();
+        for (int32_t base = ((n_oe - 1 - p) / kWave) * kWave + p; base >= p; base -= kWave) {
+            int32_t j = base + lane;
+            uint32_t v = 0;
+            bool ok = j < n_oe;
+            if (ok) v = oe[j];
+            wsync();
+            if (ok) oe[j + 1] = v;
+            wsync();
+        }
+        if (lane == 0) oe[p] = e;
+        n_oe++;
+        if (n_oe > max_oe) max_oe = n_oe;
+        wsync();
+    }
+    // move oe[from, n_oe) to start at `to` (to < from: left shift; to > from: right shift)
+    __device__ void oe_move_tail(int32_t from, int32_t to) {
+        int32_t cnt = n_oe - from;
+        int32_t new_n = to + cnt;
+        if (new_n > cap.oe) {
+            cap_fail(1);
+            return;
+        }
+        wsync();
+        if (to < from) {
+            for (int32_t base = 0; base < cnt; base += kWave) {
+                int32_t j = base + lane;
+                uint32_t v = 0;
+                if (j < cnt) v = oe[from + j];
+                wsync();
+                if (j < cnt) oe[to + j] = v;
+                wsync();
+            }
+        } else if (to > from) {
+            for (int32_t base = ((cnt - 1) / kWave) * kWave; base >= 0; base -= kWave) {
+                int32_t j = base + lane;
+                uint32_t v = 0;
+                if (j < cnt) v = oe[from + j];
+                wsync();
+                if (j < cnt) oe[to + j] = v;
+                wsync();
+            }
+        }
+        n_oe = new_n;
+        if (n_oe > max_oe) max_oe = n_oe;
+        wsync();
+    }
+
+    // ------------------------------------------------------------------ visibility
+    // nodeLength of one leaf for (refSeq, clientId) + breakTie's leaf rule (mergeTree.ts:2248-2277)
+    __device__ __forceinline__ void view_of(uint32_t e, int32_t ref, uint32_t c, uint32_t &vlen, bool &tie,
+                                            bool &mk) const {
+        uint32_t slot = e & 0xFFFFu;
+        if (slot == kMarkerSlot) {
+            vlen = 0;
+            tie = false;
+            mk = true;
+            return;
+        }
+        mk = false;
+        uint32_t meta = s_meta[slot];
+        int32_t seq = s_seq[slot];
+        int32_t rseq = s_rseq[slot];
+        uint32_t ovl = s_ovl[slot];
+        uint32_t len = s_len[slot];
+        uint32_t cli = meta & 63u, rcli = (meta >> 6) & 63u;
+        bool vis = (cli == c) || (seq <= ref);
+        bool rem = (rcli == c) || ((ovl >> c) & 1u) || (rseq <= ref);
+        vlen = (vis && !rem) ? len : 0u;
+        tie = !(rseq <= ref);
+    }
+
+    // insertingWalk target for pos under (ref, c): see header comment
+    __device__ Loc locate(uint32_t pos, int32_t ref, uint32_t c) {
+        Loc L;
+        L.found = 0;
+        L.idx = -1;
+        L.excl = 0;
+        L.marker = 0;
+        uint32_t carry = 0;
+        for (int32_t base = 0; base < n_oe; base += kWave) {
+            int32_t j = base + lane;
+            bool valid = j < n_oe;
+            uint32_t vlen = 0;
+            bool tie = false, mk = false;
+            if (valid) view_of(oe[j], ref, c, vlen, tie, mk);
+            uint32_t incl = scan_incl(vlen) + carry;
+            uint32_t excl = incl - vlen;
+            bool cond = valid && !mk && (incl > pos || (excl == pos && vlen == 0 && tie));
+            bool mhit = valid && mk && incl >= pos;
+            uint64_t b = ballot(cond || mhit);
+            if (b) {
+                int f = first_lane(b);
+                L.found = 1;
+                L.idx = base + f;
+                L.excl = rdl(excl, f);
+                L.marker = (int32_t)((ballot(mhit) >> f) & 1ull);
+                return L;
+            }
+            carry = rdl(incl, 63);
+        }
+        return L;
+    }
+
+    // MergeTree.getLength(refSeq, clientId) (generator)
+    __device__ uint32_t view_length(int32_t ref, uint32_t c) {
+        uint32_t carry = 0;
+        for (int32_t base = 0; base < n_oe; base += kWave) {
+            int32_t j = base + lane;
+            uint32_t vlen = 0;
+            bool tie, mk;
+            if (j < n_oe) view_of(oe[j], ref, c, vlen, tie, mk);
+            carry = rdl(scan_incl(vlen) + carry, 63);
+        }
+        return carry;
+    }
+
+    // first oe index with entry predicate; kind 0: slot == key, kind 1: block == key
+    __device__ int32_t find_entry(uint32_t key, int kind, int32_t from = 0) {
+        for (int32_t base = from; base < n_oe; base += kWave) {
+            int32_t j = base + lane;
+            bool hit = false;
+            if (j < n_oe) {
+                uint32_t e = oe[j];
+                hit = kind == 0 ? ((e & 0xFFFFu) == key) : ((e >> 16) == key);
+            }
+            uint64_t b = ballot(hit);
+            if (b) return base + first_lane(b);
+        }
+        return -1;
+    }
+    // first index of block `blk`'s range, given an index inside it (ranges are <= 9 entries)
+    __device__ int32_t block_start_near(uint32_t blk, int32_t inside) {
+        int32_t j = inside - 8 + lane;
+        bool hit = lane < 17 && j >= 0 && j < n_oe && (oe[j] >> 16) == blk;
+        uint64_t b = ballot(hit);
+        return inside - 8 + first_lane(b);
+    }
+
+    // ------------------------------------------------------------------ text helpers
+    __device__ bool text_ends_nl(uint32_t toff, uint32_t len) const {
+        return len > 0 && text[toff + len - 1] == (uint16_t)'\n';
+    }
+    // lane-parallel copy of n code units inside the doc's text region
+    __device__ void text_copy(uint32_t dst, uint32_t src, uint32_t n) {
+        for (uint32_t i = lane; i < n; i += kWave) text[dst + i] = text[src + i];
+    }
+    __device__ uint32_t arena_alloc(uint32_t n) {
+        uint32_t n16 = (n + 15u) & ~15u;
+        if (arena_top + n16 > text_cap) {
+            cap_fail(2);
+            return 0;
+        }
+        uint32_t o = arena_top;
+        arena_top += n16;
+        return o;
+    }
+
+    // ------------------------------------------------------------------ block tree
+    __device__ int32_t child_index(int32_t p, int32_t c) {
+        int32_t n = b_count[p];
+        bool hit = lane < n && b_child[p * 8 + lane] == (uint16_t)c;
+        uint64_t b = ballot(hit);
+        return b ? first_lane(b) : -1;
+    }
+
+    // updateRoot (mergeTree.ts:1876-1887)
+    __device__ void update_root(int32_t split_node) {
+        int32_t nr = alloc_block(0);
+        if (status) return;
+        b_child[nr * 8 + 0] = (uint16_t)root;
+        b_child[nr * 8 + 1] = (uint16_t)split_node;
+        b_count[nr] = 2;
+        b_parent[root] = (uint16_t)nr;
+        b_parent[split_node] = (uint16_t)nr;
+        root = nr;
+        depth++;
+    }
+
+    // insertingWalk's "insert the split-off node after its source" (mergeTree.ts:2446-2453),
+    // cascading MergeTree.split (2476-2489) up the interior levels and updateRoot at the top.
+    __device__ void insert_child_after(int32_t p, int32_t after, int32_t nc) {
+        for (;;) {
+            int32_t i = child_index(p, after);
+            int32_t n = b_count[p];
+            wsync();
+            uint16_t v = 0;
+            if (lane > i && lane < n) v = b_child[p * 8 + lane];
+            wsync();
+            if (lane > i && lane < n) b_child[p * 8 + lane + 1] = v;
+            wsync();
+            b_child[p * 8 + i + 1] = (uint16_t)nc;
+            b_parent[nc] = (uint16_t)p;
+            b_count[p] = (uint8_t)(n + 1);
+            wsync();
+            if (n + 1 < kMaxNodes) return;
+            // split the interior block p: children 4..7 move to m
+            int32_t m = alloc_block(0);
+            if (status) return;
+            wsync();
+            if (lane < 4) {
+                uint16_t c = b_child[p * 8 + 4 + lane];
+                b_child[m * 8 + lane] = c;
+                b_parent[c] = (uint16_t)m;
+            }
+            wsync();
+            b_count[m] = 4;
+            b_count[p] = 4;
+            wsync();
+            if (p == root) {
+                update_root(m);
+                return;
+            }
+            after = p;
+            nc = m;
+            p = b_parent[p];
+        }
+    }
+
+    // MergeTree.split on a leaf block whose range starts at s and now holds 8 children.
+    // Returns the new right block.
+    __device__ int32_t split_leaf(int32_t blk, int32_t s) {
+        int32_t nb = alloc_block(1);
+        if (status) return blk;
+        wsync();
+        // children 4..7 and the block's end marker move to the new block
+        if (lane >= 4 && lane <= 8) {
+            uint32_t e = oe[s + lane];
+            oe[s + lane] = ((uint32_t)nb << 16) | (e & 0xFFFFu);
+        }
+        wsync();
+        b_count[nb] = 4;
+        b_count[blk] = 4;
+        oe_insert(s + 4, ((uint32_t)blk << 16) | kMarkerSlot);
+        if (status) return nb;
+        if (blk == root) update_root(nb);
+        else insert_child_after(b_parent[blk], blk, nb);
+        return nb;
+    }
+
+    // ------------------------------------------------------------------ split / insert leaves
+    // insert a leaf before oe index idx into the leaf block owning oe[idx]; returns the
+    // block the new leaf ends up in (after a possible split)
+    __device__ int32_t insert_leaf(int32_t idx, uint32_t slot) {
+        uint32_t blk = rfl(oe[idx] >> 16);
+        oe_insert(idx, (blk << 16) | slot);
+        if (status) return (int32_t)blk;
+        int32_t cnt = b_count[blk] + 1;
+        b_count[blk] = (uint8_t)cnt;
+        wsync();
+        if (cnt >= kMaxNodes) {
+            int32_t s = block_start_near(blk, idx);
+            int32_t nb = split_leaf((int32_t)blk, s);
+            if (idx - s >= 4) return nb;
+        }
+        return (int32_t)blk;
+    }
+
+    // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568,
+    // textSegment.ts:103-111): the right part becomes a new leaf right after the left one
+    __device__ void split_at(int32_t idx, uint32_t r) {
+        uint32_t slot = rfl(oe[idx] & 0xFFFFu);
+        uint32_t meta = s_meta[slot];
+        if (meta & kMetaMarker) return;  // Marker.createSplitSegmentAt returns undefined
+        int32_t ns = alloc_slot();
+        if (ns < 0) return;
+        uint32_t len = s_len[slot], toff = s_toff[slot], tcap = s_tcap[slot];
+        bool left_nl = text_ends_nl(toff, r);
+        s_len[ns] = len - r;
+        s_seq[ns] = s_seq[slot];
+        s_rseq[ns] = s_rseq[slot];
+        s_ovl[ns] = s_ovl[slot];
+        s_props[ns] = s_props[slot];
+        s_phash[ns] = s_phash[slot];
+        s_toff[ns] = toff + r;
+        s_tcap[ns] = tcap - r;
+        uint32_t gen = s_meta[ns] & 0xFFFF0000u;
+        s_meta[ns] = (meta & 0x0000FFFFu) | gen;  // inherits ends-NL of the original tail
+        s_len[slot] = r;
+        s_tcap[slot] = r;
+        s_meta[slot] = left_nl ? (meta | kMetaEndsNL) : (meta & ~kMetaEndsNL);
+        wsync();
+        insert_leaf(idx + 1, (uint32_t)ns);
+    }
+
+    // ensureIntervalBoundary (mergeTree.ts:2241-2245)
+    __device__ void ensure_boundary(uint32_t pos, int32_t ref, uint32_t c) {
+        Loc L = locate(pos, ref, c);
+        if (L.found && !L.marker && L.excl < pos) split_at(L.idx, pos - L.excl);
+    }
+
+    // addToLRUSet (mergeTree.ts:1273-1283); seq > currentSeq holds for sequenced remote ops
+    __device__ void add_to_lru(int32_t blk, uint32_t slot, int32_t seq) {
+        if (b_scour[blk] != kScourTrue && seq > cur_seq) {
+            b_scour[blk] = kScourTrue;
+            heap_add(slot | (s_meta[slot] & 0xFFFF0000u), seq);
+        }
+    }
+
+    // ------------------------------------------------------------------ heap (collections.ts:213-265)
+    __device__ void heap_add(uint32_t key, int32_t seq) {
+        if (hn + 1 > cap.heap) {
+            cap_fail(1);
+            return;
+        }
+        hn++;
+        int32_t k = hn;
+        h_key[k] = key;
+        h_seq[k] = seq;
+        while (k > 1 && h_seq[k >> 1] - h_seq[k] > 0) {
+            uint32_t tk = h_key[k >> 1];
+            int32_t ts = h_seq[k >> 1];
+            h_key[k >> 1] = h_key[k];
+            h_seq[k >> 1] = h_seq[k];
+            h_key[k] = tk;
+            h_seq[k] = ts;
+            k >>= 1;
+        }
+        if (hn > max_heap) max_heap = hn;
+    }
+    __device__ void heap_get(uint32_t &key, int32_t &seq) {
+        key = h_key[1];
+        seq = h_seq[1];
+        h_key[1] = h_key[hn];
+        h_seq[1] = h_seq[hn];
+        hn--;
+        int32_t k = 1;
+        while ((k << 1) <= hn) {
+            int32_t j = k << 1;
+            if (j < hn && h_seq[j] - h_seq[j + 1] > 0) j++;
+            if (h_seq[k] - h_seq[j] <= 0) break;
+            uint32_t tk = h_key[k];
+            int32_t ts = h_seq[k];
+            h_key[k] = h_key[j];
+            h_seq[k] = h_seq[j];
+            h_key[j] = tk;
+            h_seq[j] = ts;
+            k = j;
+        }
+    }
+
+    // ------------------------------------------------------------------ properties
+    // prop-set record in the doc pool: [n, hash, (key, value) x n] in insertion order
+    __device__ bool props_match(uint32_t a, uint32_t ha, uint32_t b, uint32_t hb) {
+        if (a == b) return true;
+        if (a == 0 || b == 0) return false;
+        if (ha != hb) return false;
+        uint32_t na = pool[a], nb = pool[b];
+        if (na != nb) return false;
+        bool ok = true;
+        if ((uint32_t)lane < na) {
+            uint32_t k = pool[a + 2 + 2 * lane], v = pool[a + 3 + 2 * lane];
+            bool f = false;
+            for (uint32_t i = 0; i < nb; i++)
+                if (pool[b + 2 + 2 * i] == k && pool[b + 3 + 2 * i] == v) f = true;
+            ok = f;
+        }
+        return ballot(!ok) == 0;
+    }
+
+    // SegmentPropertiesManager.addProperties for a sequenced remote op (or insert-time props):
+    // start from `old` (0 = undefined -> new empty map), apply rewrite then the op's pairs in
+    // order (null deletes: properties.ts:95-116).  Returns the new set id (hash in hout).
+    __device__ uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout) {
+        uint32_t *keys = scratch;
+        uint32_t *vals = scratch + 128;
+        uint32_t n = old ? pool[old] : 0u;
+        if (n > 64u || nop > 64u) {
+            cap_fail(3);
+            return 0;
+        }
+        wsync();
+        if ((uint32_t)lane < n) {
+            keys[lane] = pool[old + 2 + 2 * lane];
+            vals[lane] = pool[old + 3 + 2 * lane];
+        }
+        uint32_t ok_k = 0, ok_v = 0;
+        if ((uint32_t)lane < nop) {
+            ok_k = op[lane].key;
+            ok_v = op[lane].value;
+        }
+        wsync();
+        if (rewrite) {
+            // delete existing keys whose new value is absent or falsy (segmentPropertiesManager.ts:70-80)
+            bool keep = false;
+            if ((uint32_t)lane < n) {
+                uint32_t k = keys[lane];
+                for (uint32_t i = 0; i < nop; i++) {
+                    uint32_t kk = rdl(ok_k, (int)i), vv = rdl(ok_v, (int)i);
+                    if (kk == k && vv < n_values && !(value_flags[vv] & 1u)) keep = true;
+                }
+            }
+            uint64_t kb = ballot(keep && (uint32_t)lane < n);
+            uint32_t nk = 0, kv = 0, vv2 = 0;
+            if ((uint32_t)lane < n) {
+                kv = keys[lane];
+                vv2 = vals[lane];
+            }
+            wsync();
+            if (keep) {
+                uint32_t dst = __popcll(kb & ((1ull << lane) - 1ull));
+                keys[dst] = kv;
+                vals[dst] = vv2;
+            }
+            nk = __popcll(kb);
+            n = nk;
+            wsync();
+        }
+        for (uint32_t i = 0; i < nop; i++) {
+            uint32_t k = rdl(ok_k, (int)i), v = rdl(ok_v, (int)i);
+            bool hit = (uint32_t)lane < n && keys[lane] == k;
+            uint64_t b = ballot(hit);
+            if (v == MT_VALUE_NULL) {
+                if (b) {
+                    int at = first_lane(b);
+                    uint32_t kk = 0, vv = 0;
+                    bool mv = (uint32_t)lane > (uint32_t)at && (uint32_t)lane < n;
+                    if (mv) {
+                        kk = keys[lane];
+                        vv = vals[lane];
+                    }
+                    wsync();
+                    if (mv) {
+                        keys[lane - 1] = kk;
+                        vals[lane - 1] = vv;
+                    }
+                    n--;
+                    wsync();
+                }
+            } else if (b) {
+                int at = first_lane(b);
+                if (lane == 0) vals[at] = v;
+                wsync();
+            } else {
+                if (n >= 64u) {
+                    cap_fail(3);
+                    return 0;
+                }
+                if (lane == 0) {
+                    keys[n] = k;
+                    vals[n] = v;
+                }
+                n++;
+                wsync();
+            }
+        }
+        uint32_t words = 2 + 2 * n;
+        if (pool_top + words > pool_cap) {
+            cap_fail(3);
+            return 0;
+        }
+        uint32_t id = pool_top;
+        pool_top += words;
+        uint32_t h = 0;
+        if ((uint32_t)lane < n) {
+            uint32_t k = keys[lane], v = vals[lane];
+            h = hash_pair(k, v);
+            pool[id + 2 + 2 * lane] = k;
+            pool[id + 3 + 2 * lane] = v;
+        }
+        // order-insensitive content hash (matchProperties ignores key order)
+        for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, kWave);
+        h = rfl(h);
+        if (lane == 0) {
+            pool[id] = n;
+            pool[id + 1] = h;
+        }
+        hout = h;
+        wsync();
+        return id;
+    }
+
+    // ------------------------------------------------------------------ scour / pack / zamboni
+    // scourNode (mergeTree.ts:1289-1365) over leaf block entries oe[s, s+cnt): appends the kept
+    // slots to hold[nh..], unlinks removed-below-minSeq leaves and appends mergeable neighbours.
+    __device__ int32_t scour_leaves(int32_t s, int32_t cnt, uint32_t *hold, int32_t nh) {
+        int32_t prev = -1;
+        for (int32_t k = 0; k < cnt; k++) {
+            uint32_t slot = rfl(oe[s + k] & 0xFFFFu);
+            int32_t rseq = s_rseq[slot];
+            if (rseq != kNoneSeq) {
+                if (rseq > min_seq) hold[nh++] = slot;
+                else free_slot((int32_t)slot);
+                prev = -1;
+            } else if (s_seq[slot] <= min_seq) {
+                bool can = false;
+                if (prev >= 0) {
+                    uint32_t pm = s_meta[prev], sm = s_meta[slot];
+                    uint32_t pl = s_len[prev], sl = s_len[slot];
+                    // TextSegment.canAppend (textSegment.ts:63-68)
+                    can = !(pm & kMetaMarker) && !(sm & kMetaMarker) && !(pm & kMetaEndsNL) &&
+                          (pl <= kGranularity || sl <= kGranularity);
+                    if (can) can = props_match(s_props[prev], s_phash[prev], s_props[slot], s_phash[slot]);
+                }
+                if (can) {
+                    // TextSegment.append: prev.text += segment.text
+                    uint32_t pl = s_len[prev], sl = s_len[slot];
+                    uint32_t need = pl + sl;
+                    if (s_tcap[prev] >= need) {
+                        text_copy(s_toff[prev] + pl, s_toff[slot], sl);
+                    } else {
+                        uint32_t ncap = 2 * need;
+                        uint32_t dst = arena_alloc(ncap);
+                        if (status) return nh;
+                        text_copy(dst, s_toff[prev], pl);
+                        text_copy(dst + pl, s_toff[slot], sl);
+                        s_toff[prev] = dst;
+                        s_tcap[prev] = (ncap + 15u) & ~15u;
+                    }
+                    s_len[prev] = need;
+                    s_meta[prev] = (s_meta[prev] & ~kMetaEndsNL) | (s_meta[slot] & kMetaEndsNL);
+                    free_slot((int32_t)slot);
+                } else {
+                    hold[nh++] = slot;
+                    prev = (int32_t)slot;
+                }
+            } else {
+                hold[nh++] = slot;
+                prev = -1;
+            }
+        }
+        wsync();
+        return nh;
+    }
+
+    // pack for an interior block `blk` (its parent's children are interior blocks);
+    // repeats upward while the parent underflows (mergeTree.ts:1414-1419)
+    __device__ void pack_interior(int32_t blk) {
+        for (;;) {
+            int32_t parent = b_parent[blk];
+            int32_t pn = b_count[parent];
+            uint32_t *hold = scratch;  // grandchildren block ids
+            int32_t total = 0;
+            for (int32_t ci = 0; ci < pn; ci++) {
+                int32_t cb = b_child[parent * 8 + ci];
+                int32_t cn = b_count[cb];
+                wsync();
+                if (lane < cn) hold[total + lane] = b_child[cb * 8 + lane];
+                total += cn;
+                wsync();
+            }
+            int32_t child_count = total / (kMaxNodes / 2);
+            if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
+            if (child_count < 1) child_count = 1;
+            int32_t base = total / child_count, extra = total % child_count;
+            int32_t nb[kMaxNodes];
+            for (int32_t i = 0; i < pn; i++) free_block(b_child[parent * 8 + i]);
+            for (int32_t i = 0; i < child_count; i++) nb[i] = alloc_block(0);
+            if (status) return;
+            int32_t read = 0;
+            for (int32_t i = 0; i < child_count; i++) {
+                int32_t cnt = base + (i < extra ? 1 : 0);
+                wsync();
+                if (lane < cnt) {
+                    uint16_t g = (uint16_t)hold[read + lane];
+                    b_child[nb[i] * 8 + lane] = g;
+                    b_parent[g] = (uint16_t)nb[i];
+                }
+                wsync();
+                b_count[nb[i]] = (uint8_t)cnt;
+                b_parent[nb[i]] = (uint16_t)parent;
+                b_child[parent * 8 + i] = (uint16_t)nb[i];
+                read += cnt;
+            }
+            b_count[parent] = (uint8_t)child_count;
+            wsync();
+            if (child_count < kMaxNodes / 2 && parent != root) blk = parent;
+            else return;
+        }
+    }
+
+    // pack for a leaf block (mergeTree.ts:1368-1420)
+    __device__ void pack_leaf(int32_t blk, int32_t hint) {
+        int32_t parent = b_parent[blk];
+        int32_t pn = b_count[parent];
+        int32_t first = b_child[parent * 8 + 0];
+        int32_t s0 = find_entry((uint32_t)first, 1, 0);
+        if (s0 < 0) {
+            set_fail(ST_INTERNAL);
+            return;
+        }
+        (void)hint;
+        uint32_t *hold = scratch + 128;
+        int32_t total = 0;
+        int32_t s = s0;
+        for (int32_t ci = 0; ci < pn; ci++) {
+            int32_t cb = b_child[parent * 8 + ci];
+            int32_t cn = b_count[cb];
+            total = scour_leaves(s, cn, hold, total);
+            if (status) return;
+            s += cn + 1;  // skip its marker
+        }
+        int32_t old_end = s;  // one past the last marker
+        int32_t child_count = total / (kMaxNodes / 2);
+        if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
+        if (child_count < 1) child_count = 1;
+        int32_t base = total / child_count, extra = total % child_count;
+        int32_t nb[kMaxNodes];
+        for (int32_t i = 0; i < pn; i++) free_block(b_child[parent * 8 + i]);
+        for (int32_t i = 0; i < child_count; i++) nb[i] = alloc_block(1);
+        if (status) return;
+        int32_t new_len = total + child_count;
+        oe_move_tail(old_end, s0 + new_len);
+        if (status) return;
+        // write the regrouped range
+        int32_t read = 0, w = s0;
+        for (int32_t i = 0; i < child_count; i++) {
+            int32_t cnt = base + (i < extra ? 1 : 0);
+            wsync();
+            if (lane < cnt) oe[w + lane] = ((uint32_t)nb[i] << 16) | hold[read + lane];
+            if (lane == cnt) oe[w + lane] = ((uint32_t)nb[i] << 16) | kMarkerSlot;
+            wsync();
+            b_count[nb[i]] = (uint8_t)cnt;
+            b_parent[nb[i]] = (uint16_t)parent;
+            b_child[parent * 8 + i] = (uint16_t)nb[i];
+            read += cnt;
+            w += cnt + 1;
+        }
+        b_count[parent] = (uint8_t)child_count;
+        wsync();
+        if (child_count < kMaxNodes / 2 && parent != root) pack_interior(parent);
+    }
+
+    // zamboniSegments (mergeTree.ts:1422-1478)
+    __device__ void zamboni() {
+        for (int it = 0; it < kZamboniMax; it++) {
+            if (hn < 1 || h_seq[1] > min_seq) break;
+            uint32_t key;
+            int32_t mseq;
+            heap_get(key, mseq);
+            uint32_t slot = key & 0xFFFFu;
+            uint32_t meta = s_meta[slot];
+            if ((meta & 0xFFFF0000u) != (key & 0xFFFF0000u) || !(meta & kMetaLinked)) continue;  // parent undefined
+            int32_t idx = find_entry(slot, 0, 0);
+            if (idx < 0) {
+                set_fail(ST_INTERNAL);
+                return;
+            }
+            int32_t blk = rfl((int32_t)(oe[idx] >> 16));
+            if (b_scour[blk] == kScourFalse) continue;
+            int32_t s = block_start_near((uint32_t)blk, idx);
+            int32_t cnt = b_count[blk];
+            uint32_t *hold = scratch;
+            int32_t nk = scour_leaves(s, cnt, hold, 0);
+            if (status) return;
+            b_scour[blk] = kScourFalse;
+            if (nk < cnt) {
+                wsync();
+                if (lane < nk) oe[s + lane] = ((uint32_t)blk << 16) | hold[lane];
+                if (lane == nk) oe[s + lane] = ((uint32_t)blk << 16) | kMarkerSlot;
+                wsync();
+                oe_move_tail(s + cnt + 1, s + nk + 1);
+                b_count[blk] = (uint8_t)nk;
+                wsync();
+                if (nk < kMaxNodes / 2 && blk != root) pack_leaf(blk, s);
+                if (status) return;
+            }
+        }
+    }
+
+    // setMinSeq (mergeTree.ts:1718-1736) via Client.updateSeqNumbers (client.ts:821-828)
+    __device__ void update_seq_numbers(int32_t msn, int32_t seq) {
+        if (!(cur_seq <= seq)) {
+            set_fail(ST_SEQ_ORDER);
+            return;
+        }
+        cur_seq = seq;
+        if (!(msn <= seq)) {
+            set_fail(ST_MSN_ORDER);
+            return;
+        }
+        if (!(min_seq <= msn)) {
+            set_fail(ST_MSN_ORDER);
+            return;
+        }
+        if (msn > min_seq) {
+            min_seq = msn;
+            zamboni();
+        }
+    }
+
+    // ------------------------------------------------------------------ ops
+    // insertSegments + blockInsert for one remote segment (mergeTree.ts:1968-1998, 2141-2224)
+    __device__ void op_insert(const mt_op &op) {
+        uint32_t c = op.client;
+        uint32_t pos = (uint32_t)op.pos1;
+        ensure_boundary(pos, op.ref_seq, c);
+        if (status) return;
+        bool marker = (op.flags & MT_OPF_MARKER) != 0;
+        uint32_t len = marker ? 1u : op.payload_len;
+        if (len > 0) {
+            Loc L = locate(pos, op.ref_seq, c);
+            if (!L.found) {
+                set_fail(ST_INVALID_POS);
+                return;
+            }
+            int32_t slot = alloc_slot();
+            if (slot < 0) return;
+            uint32_t props = 0, ph = 0;
+            if (op.flags & MT_OPF_HAS_PROPS) {
+                props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
+                if (status) return;
+            }
+            uint32_t gen = s_meta[slot] & 0xFFFF0000u;
+            uint32_t meta = gen | kMetaLinked | (c & 63u) | (kNoClient << 6);
+            if (marker) meta |= kMetaMarker;
+            if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
+            s_len[slot] = len;
+            s_seq[slot] = op.seq;
+            s_rseq[slot] = kNoneSeq;
+            s_ovl[slot] = 0;
+            s_props[slot] = props;
+            s_phash[slot] = ph;
+            s_toff[slot] = marker ? op.payload : op.payload;
+            s_tcap[slot] = marker ? 0u : len;
+            s_meta[slot] = meta;
+            wsync();
+            int32_t blk = insert_leaf(L.idx, (uint32_t)slot);
+            if (status) return;
+            // saveIfLocal (mergeTree.ts:2164-2179)
+            if (op.seq > min_seq) add_to_lru(blk, (uint32_t)slot, op.seq);
+        }
+        zamboni();
+    }
+
+    // markRangeRemoved / annotateRange range walk (nodeMap, mergeTree.ts:2903-2965)
+    __device__ void op_range(const mt_op &op) {
+        uint32_t c = op.client;
+        int32_t ref = op.ref_seq;
+        uint32_t start = (uint32_t)op.pos1, end = (uint32_t)op.pos2;
+        ensure_boundary(start, ref, c);
+        if (status) return;
+        ensure_boundary(end, ref, c);
+        if (status) return;
+        const bool is_remove = op.type == MT_OP_REMOVE;
+        const bool rewrite = (op.flags & MT_OPF_REWRITE) != 0;
+        // per-op memo old prop-set -> new prop-set (annotate)
+        uint32_t memo_n = 0;
+        uint32_t memo_old = 0, memo_new = 0, memo_h = 0;  // lane i holds entry i
+        uint32_t carry = 0;
+        for (int32_t base = 0; base < n_oe; base += kWave) {
+            int32_t j = base + lane;
+            bool valid = j < n_oe;
+            uint32_t e = valid ? oe[j] : 0u;
+            uint32_t vlen = 0;
+            bool tie, mk;
+            if (valid) view_of(e, ref, c, vlen, tie, mk);
+            uint32_t incl = scan_incl(vlen) + carry;
+            uint32_t excl = incl - vlen;
+            bool hit = valid && vlen > 0 && excl < end && incl > start;
+            uint64_t hb = ballot(hit);
+            bool past = valid && excl >= end;
+            uint64_t pb = ballot(past);
+            if (is_remove && hit) {
+                uint32_t slot = e & 0xFFFFu;
+                if (s_rseq[slot] != kNoneSeq) {
+                    s_ovl[slot] |= 1u << c;  // addOverlappingClient (mergeTree.ts:2544-2552)
+                } else {
+                    s_rseq[slot] = op.seq;
+                    s_meta[slot] = (s_meta[slot] & ~(63u << 6)) | ((c & 63u) << 6);
+                }
+            }
+            wsync();
+            // in document order: properties (annotate) and addToLRUSet
+            while (hb) {
+                int f = first_lane(hb);
+                hb &= hb - 1;
+                uint32_t e2 = rdl(e, f);
+                uint32_t slot = e2 & 0xFFFFu;
+                int32_t blk = (int32_t)(e2 >> 16);
+                if (!is_remove) {
+                    uint32_t old = s_props[slot];
+                    uint64_t mb = ballot((uint32_t)lane < memo_n && memo_old == old);
+                    uint32_t nid, nh;
+                    if (mb) {
+                        int m = first_lane(mb);
+                        nid = rdl(memo_new, m);
+                        nh = rdl(memo_h, m);
+                    } else {
+                        nid = props_extend(old, props_in + op.payload, op.payload_len, rewrite, nh);
+                        if (status) return;
+                        if (memo_n < 64u) {
+                            if ((uint32_t)lane == memo_n) {
+                                memo_old = old;
+                                memo_new = nid;
+                                memo_h = nh;
+                            }
+                            memo_n++;
+                        }
+                    }
+                    s_props[slot] = nid;
+                    s_phash[slot] = nh;
+                }
+                add_to_lru(blk, slot, op.seq);
+                if (status) return;
+            }
+            wsync();
+            if (pb) break;
+            carry = rdl(incl, 63);
+        }
+        zamboni();
+    }
+
+    __device__ void apply(const mt_op &op) {
+        if (op.client >= kMaxClients || (op.client == 0 && op.type != MT_OP_NOOP)) {
+            set_fail(ST_UNSUPPORTED);
+            return;
+        }
+        switch (op.type) {
+            case MT_OP_INSERT: op_insert(op); break;
+            case MT_OP_REMOVE:
+            case MT_OP_ANNOTATE: op_range(op); break;
+            case MT_OP_NOOP: break;
+            default: set_fail(ST_BAD_INPUT); return;
+        }
+        if (status) return;
+        if (op.type != MT_OP_NOOP) {
+            // completeAndLogOp (client.ts:461-464)
+            if (!(cur_seq < op.seq)) {
+                set_fail(ST_SEQ_ORDER);
+                return;
+            }
+            if (!(min_seq <= op.msn)) {
+                set_fail(ST_MSN_ORDER);
+                return;
+            }
+        }
+        if (!(op.flags & MT_OPF_GROUP_CONT)) update_seq_numbers(op.msn, op.seq);
+    }
+
+    // ------------------------------------------------------------------ output
+    __device__ void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op) {
+        wsync();
+        int32_t n = n_oe <= out_cap ? n_oe : out_cap;
+        for (int32_t j = lane; j < n; j += kWave) {
+            uint32_t e = oe[j];
+            uint32_t slot = e & 0xFFFFu;
+            OutRec r;
+            if (slot == kMarkerSlot) {
+                r.len = 0;
+                r.seq = 0;
+                r.rseq = kNoneSeq;
+                r.meta = 0;
+                r.ovl = 0;
+                r.props = 0;
+                r.toff = 0;
+            } else {
+                r.len = s_len[slot];
+                r.seq = s_seq[slot];
+                r.rseq = s_rseq[slot];
+                r.meta = s_meta[slot];
+                r.ovl = s_ovl[slot];
+                r.props = s_props[slot];
+                r.toff = s_toff[slot];
+            }
+            r.blk = e;
+            out[j] = r;
+        }
+        if (lane == 0) {
+            DocOut o;
+            o.status = (n_oe > out_cap && status == ST_OK) ? ST_CAPACITY : status;
+            o.cap_kind = (n_oe > out_cap && status == ST_OK) ? 4 : cap_kind;
+            o.min_seq = min_seq;
+            o.cur_seq = cur_seq;
+            o.depth = depth;
+            o.n_out = n;
+            o.text_top = arena_top;
+            o.pool_top = pool_top;
+            o.ops_done = ops_done;
+            o.max_oe = max_oe;
+            o.max_slots = slot_top;
+            o.max_blocks = blk_top;
+            o.max_heap = max_heap;
+            o.fail_op = fail_op;
+            o.gen_text = 0;
+            o.gen_props = 0;
+            *dout = o;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------- kernels
+__device__ __forceinline__ mt_op load_op_lane(const mt_op *ops, int64_t i, int64_t end) {
+    mt_op o;
+    if (i < end) {
+        const uint4 *p = (const uint4 *)(ops + i);
+        uint4 a = p[0], b = p[1];
+        __builtin_memcpy(&o, &a, 16);
+        __builtin_memcpy((char *)&o + 16, &b, 16);
+    } else {
+        __builtin_memset(&o, 0, sizeof o);
+    }
+    return o;
+}
+
+__device__ __forceinline__ mt_op bcast_op(const mt_op &o, int l) {
+    uint32_t w[8];
+    __builtin_memcpy(w, &o, 32);
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = rdl(w[i], l);
+    mt_op r;
+    __builtin_memcpy(&r, w, 32);
+    return r;
+}
+
+__device__ void engine_setup(Engine &E, const ReplayParams &P, int64_t d, uint8_t *smem) {
+    E.lane = threadIdx.x;
+    E.carve(smem, P.caps);
+    E.text = P.text + P.doc_text_base[d];
+    E.text_cap = P.doc_text_cap[d];
+    E.arena_top = (P.doc_text_len[d] + 15u) & ~15u;
+    E.pool = P.pool + P.doc_pool_base[d];
+    E.pool_cap = P.doc_pool_cap[d];
+    E.pool_top = 1;  // id 0 = undefined
+    E.props_in = (const mt_prop *)P.props_in;
+    E.value_flags = P.value_flags;
+    E.n_values = P.n_values;
+    E.init();
+}
+
+extern "C" __global__ __launch_bounds__(64) void mt_replay_kernel(ReplayParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int64_t w = (int64_t)blockIdx.x;
+    if (w >= P.n_docs) return;
+    const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
+    Engine E;
+    engine_setup(E, P, d, smem);
+    const mt_op *ops = (const mt_op *)P.ops;
+    const int64_t b0 = P.doc_op_off[d], b1 = P.doc_op_off[d + 1];
+    int32_t done = 0, fail_op = -1;
+    // ops stream through registers 64 at a time (coalesced 2 KiB loads), broadcast by readlane
+    mt_op cur = load_op_lane(ops, b0 + E.lane, b1);
+    for (int64_t base = b0; base < b1 && E.status == ST_OK; base += kWave) {
+        mt_op nxt = load_op_lane(ops, base + kWave + E.lane, b1);
+        int64_t n = b1 - base < kWave ? b1 - base : kWave;
+        for (int i = 0; i < n; i++) {
+            mt_op op = bcast_op(cur, i);
+            E.apply(op);
+            if (E.status != ST_OK) {
+                fail_op = (int32_t)(base - b0 + i);
+                break;
+            }
+            done++;
+        }
+        cur = nxt;
+    }
+    E.write_out(P.out + w * (int64_t)P.out_cap, P.out_cap, P.doc_out + w, done, fail_op);
+}
+
+// Generator: draws each op from the issuer's view (include/mt_gen.h, DESIGN.md
+// "Synthetic op logs"), writes the record + payload, then applies it as the observer.
+extern "C" __global__ __launch_bounds__(64) void mt_generate_kernel(ReplayParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int64_t d = (int64_t)blockIdx.x;
+    if (d >= P.n_docs) return;
+    const mt_gen_params g = *(const mt_gen_params *)P.gen;
+    Engine E;
+    engine_setup(E, P, d, smem);
+    mt_op *ops_out = (mt_op *)P.gen_ops + d * (int64_t)g.n_ops;
+    mt_prop *props_out = (mt_prop *)P.gen_props;
+    const int64_t prop_base = d * (int64_t)(2 * g.n_ops);
+    E.props_in = props_out;
+    uint64_t x = mt_rng_seed(g.seed, (uint64_t)(P.doc_first + d));
+    __shared__ int32_t lref[64];  // last refSeq per client (160 B static + 16-aligned dynamic base)
+    lref[E.lane] = 0;
+    wsync();
+    uint32_t pay_top = 0, np = 0;
+    int32_t done = 0, fail_op = -1;
+    for (int32_t k = 1; k <= g.n_ops; k++) {
+        mt_op op;
+        op.seq = k;
+        int32_t c = 1 + (int32_t)mt_rng_below(&x, (uint32_t)g.n_clients);
+        int32_t lag = (int32_t)mt_rng_below(&x, (uint32_t)g.max_lag + 1u);
+        int32_t ref = k - 1 - lag;
+        int32_t lr = lref[c];
+        if (ref < lr) ref = lr;
+        wsync();
+        lref[c] = ref;
+        wsync();
+        int32_t msn = lref[1];
+        for (int32_t i = 2; i <= g.n_clients; i++) {
+            int32_t v = lref[i];
+            if (v < msn) msn = v;
+        }
+        uint32_t len = rfl(E.view_length(ref, (uint32_t)c));
+        uint32_t u = mt_rng_below(&x, 100);
+        int type;
+        if ((int32_t)len < g.min_len || (int32_t)u < g.pct_insert) type = MT_OP_INSERT;
+        else if ((int32_t)u < g.pct_insert + g.pct_remove) type = MT_OP_REMOVE;
+        else type = MT_OP_ANNOTATE;
+        op.type = (uint8_t)type;
+        op.client = (uint8_t)c;
+        op.flags = 0;
+        op.ref_seq = ref;
+        op.msn = msn;
+        op.pos1 = op.pos2 = 0;
+        op.payload = op.payload_len = 0;
+        if (type == MT_OP_INSERT) {
+            op.pos1 = (int32_t)mt_rng_below(&x, len + 1u);
+            uint32_t n = 1u + mt_rng_below(&x, (uint32_t)g.max_insert);
+            if (pay_top + n > P.doc_text_len[d]) {
+                E.cap_fail(2);
+                fail_op = k - 1;
+                break;
+            }
+            op.payload = pay_top;
+            op.payload_len = n;
+            uint16_t ch = 0;
+            for (uint32_t i = 0; i < n; i++) {
+                uint32_t r = mt_rng_below(&x, 100);
+                if ((int32_t)r < g.pct_newline) {
+                    ch = (uint16_t)'\n';
+                } else {
+                    uint32_t a = mt_rng_below(&x, 27);  // "abcdefghijklmnopqrstuvwxyz "
+                    ch = a < 26u ? (uint16_t)('a' + a) : (uint16_t)' ';
+                }
+                if (E.lane == 0) E.text[pay_top + i] = ch;
+            }
+            if (ch == (uint16_t)'\n') op.flags |= MT_OPF_INTERNAL_ENDS_NL;
+            pay_top += n;
+        } else {
+            uint32_t rl = 1;
+            while (rl < len && mt_rng_below(&x, 4) != 0) rl++;
+            uint32_t start = mt_rng_below(&x, len - rl + 1u);
+            op.pos1 = (int32_t)start;
+            op.pos2 = (int32_t)(start + rl);
+            if (type == MT_OP_ANNOTATE) {
+                uint32_t nk = 1u + mt_rng_below(&x, 2);
+                uint32_t k0 = mt_rng_below(&x, 4);
+                uint32_t keys[2] = {k0, (k0 + 1u + mt_rng_below(&x, 3)) % 4u};
+                op.payload = (uint32_t)(prop_base + np);
+                op.payload_len = nk;
+                for (uint32_t i = 0; i < nk; i++) {
+                    uint32_t v;
+                    if (mt_rng_below(&x, 10) == 0) v = 0;
+                    else if (keys[i] <= 1) v = 1;
+                    else if (keys[i] == 2) v = 2 + mt_rng_below(&x, 3);
+                    else v = 5 + mt_rng_below(&x, 17);
+                    if (E.lane == 0) {
+                        props_out[prop_base + np].key = keys[i];
+                        props_out[prop_base + np].value = v;
+                    }
+                    np++;
+                }
+            }
+        }
+        if (E.lane == 0) ops_out[k - 1] = op;
+        __threadfence_block();
+        wsync();
+        E.apply(op);
+        if (E.status != ST_OK) {
+            fail_op = k - 1;
+            break;
+        }
+        done++;
+    }
+    E.write_out(P.out + d * (int64_t)P.out_cap, P.out_cap, P.doc_out + d, done, fail_op);
+    if (E.lane == 0) {
+        P.doc_out[d].gen_text = (int32_t)pay_top;
+        P.doc_out[d].gen_props = (int32_t)np;
+    }
+}
+
+}  // namespace mt

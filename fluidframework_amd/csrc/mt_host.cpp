@@ -1,0 +1,1221 @@
+// mt_host.cpp — host side of libmtreplay.so: the C ABI declared in include/mtreplay.h.
+//
+// Owns a batch of documents on one HIP device: stages packed op logs into per-document
+// HBM regions, launches the replay kernels (mt_engine.hip, compiled into this TU), escalates
+// documents that overflow their LDS capacity class, and serializes per-document results
+// (text, properties, SnapshotV1 blobs, digest) from the device's final segment tables.
+//
+// Nothing here replays ops: every op is applied by mt_replay_kernel on the GPU.  Without a
+// usable HIP device mt_batch_create fails with MT_ERR_NO_DEVICE (there is no CPU path).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mtreplay.h"
+#include "mt_engine.hip"
+
+using mt::Caps;
+using mt::DocOut;
+using mt::OutRec;
+
+namespace {
+
+#define HIPCHK(x)                                                                                 \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) {                                                                   \
+            fprintf(stderr, "mtreplay: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                                    \
+            return MT_ERR_HIP;                                                                    \
+        }                                                                                         \
+    } while (0)
+
+template <class T>
+static hipError_t dalloc(T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc((void **)p, n * sizeof(T));
+}
+
+struct Launch {
+    std::vector<int32_t> docs;  // empty: identity over all docs
+    Caps caps;
+    int32_t out_cap = 0;
+    OutRec *d_out = nullptr;
+    DocOut *d_docout = nullptr;
+    int32_t *d_list = nullptr;
+    size_t lds = 0;
+};
+
+struct DocRes {  // per-document result location
+    int32_t launch = -1;
+    int32_t idx = -1;
+};
+
+// ---------------------------------------------------------------- JSON helpers (JS semantics)
+static void put_cp(std::string &o, uint32_t cp) {
+    if (cp < 0x80) {
+        o.push_back((char)cp);
+    } else if (cp < 0x800) {
+        o.push_back((char)(0xC0 | (cp >> 6)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+        o.push_back((char)(0xE0 | (cp >> 12)));
+        o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+        o.push_back((char)(0xF0 | (cp >> 18)));
+        o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+        o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+}
+
+// UTF-16 -> UTF-8 (raw text; lone surrogates become U+FFFD)
+static void utf16_to_utf8(std::string &o, const uint16_t *s, size_t n) {
+    for (size_t i = 0; i < n; i++) {
+        uint32_t c = s[i];
+        if (c >= 0xD800 && c <= 0xDBFF && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+            put_cp(o, 0x10000 + ((c - 0xD800) << 10) + (uint32_t)(s[i + 1] - 0xDC00));
+            i++;
+        } else if (c >= 0xD800 && c <= 0xDFFF) {
+            put_cp(o, 0xFFFD);
+        } else {
+            put_cp(o, c);
+        }
+    }
+}
+
+// JSON.stringify(string) of UTF-16 code units (well-formed: lone surrogates escaped)
+static void json_quote16(std::string &o, const uint16_t *s, size_t n) {
+    static const char *hex = "0123456789abcdef";
+    o.push_back('"');
+    for (size_t i = 0; i < n; i++) {
+        uint32_t c = s[i];
+        switch (c) {
+            case 0x22: o += "\\\""; continue;
+            case 0x5C: o += "\\\\"; continue;
+            case 0x08: o += "\\b"; continue;
+            case 0x0C: o += "\\f"; continue;
+            case 0x0A: o += "\\n"; continue;
+            case 0x0D: o += "\\r"; continue;
+            case 0x09: o += "\\t"; continue;
+            default: break;
+        }
+        if (c < 0x20) {
+            o += "\\u00";
+            o.push_back(hex[c >> 4]);
+            o.push_back(hex[c & 15]);
+        } else if (c >= 0xD800 && c <= 0xDBFF && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+            put_cp(o, 0x10000 + ((c - 0xD800) << 10) + (uint32_t)(s[i + 1] - 0xDC00));
+            i++;
+        } else if (c >= 0xD800 && c <= 0xDFFF) {
+            o += "\\u";
+            o.push_back(hex[c >> 12]);
+            o.push_back(hex[(c >> 8) & 15]);
+            o.push_back(hex[(c >> 4) & 15]);
+            o.push_back(hex[c & 15]);
+        } else {
+            put_cp(o, c);
+        }
+    }
+    o.push_back('"');
+}
+
+static std::vector<uint16_t> utf8_to_utf16(const std::string &s) {
+    std::vector<uint16_t> out;
+    size_t i = 0, L = s.size();
+    const unsigned char *q = (const unsigned char *)s.data();
+    while (i < L) {
+        uint32_t c = q[i];
+        int len = 1;
+        if (c < 0x80) len = 1;
+        else if ((c & 0xE0) == 0xC0) { len = 2; c &= 0x1F; }
+        else if ((c & 0xF0) == 0xE0) { len = 3; c &= 0x0F; }
+        else if ((c & 0xF8) == 0xF0) { len = 4; c &= 0x07; }
+        else { out.push_back(0xFFFD); i++; continue; }
+        if (i + (size_t)len > L) { out.push_back(0xFFFD); break; }
+        bool bad = false;
+        for (int m = 1; m < len; m++) {
+            if ((q[i + m] & 0xC0) != 0x80) { bad = true; break; }
+            c = (c << 6) | (q[i + m] & 0x3F);
+        }
+        if (bad) { out.push_back(0xFFFD); i++; continue; }
+        i += (size_t)len;
+        if (c >= 0x10000) {
+            c -= 0x10000;
+            out.push_back((uint16_t)(0xD800 + (c >> 10)));
+            out.push_back((uint16_t)(0xDC00 + (c & 0x3FF)));
+        } else {
+            out.push_back((uint16_t)c);
+        }
+    }
+    return out;
+}
+
+static void json_quote8(std::string &o, const std::string &s) {
+    std::vector<uint16_t> u = utf8_to_utf16(s);
+    json_quote16(o, u.data(), u.size());
+}
+
+// canonical array index (ordinary-object key enumeration puts these first, ascending)
+static bool array_index(const std::string &k, uint32_t *idx) {
+    if (k.empty() || k.size() > 10) return false;
+    if (k[0] == '0') {
+        if (k.size() != 1) return false;
+        *idx = 0;
+        return true;
+    }
+    uint64_t v = 0;
+    for (char ch : k) {
+        if (ch < '0' || ch > '9') return false;
+        v = v * 10 + (uint64_t)(ch - '0');
+    }
+    if (v > 4294967294ull) return false;
+    *idx = (uint32_t)v;
+    return true;
+}
+
+static bool json_falsy(const std::string &v) {
+    size_t a = v.find_first_not_of(" \t\r\n"), b = v.find_last_not_of(" \t\r\n");
+    if (a == std::string::npos) return true;
+    std::string t = v.substr(a, b - a + 1);
+    if (t == "null" || t == "false" || t == "\"\"") return true;
+    if (!t.empty() && (t[0] == '-' || (t[0] >= '0' && t[0] <= '9'))) {
+        char *end = nullptr;
+        double d = strtod(t.c_str(), &end);
+        if (end && *end == 0 && d == 0.0) return true;
+    }
+    return false;
+}
+
+struct Fnv {
+    uint64_t h = 0xcbf29ce484222325ull;
+    void bytes(const void *p, size_t n) {
+        const unsigned char *q = (const unsigned char *)p;
+        for (size_t i = 0; i < n; i++) {
+            h ^= q[i];
+            h *= 0x100000001b3ull;
+        }
+    }
+    void u32(uint32_t x) {
+        unsigned char b[4] = {(unsigned char)x, (unsigned char)(x >> 8), (unsigned char)(x >> 16),
+                              (unsigned char)(x >> 24)};
+        bytes(b, 4);
+    }
+    void u64(uint64_t x) {
+        u32((uint32_t)x);
+        u32((uint32_t)(x >> 32));
+    }
+};
+static uint64_t fnv_name(const std::string &s) {
+    Fnv f;
+    f.bytes(s.data(), s.size());
+    return f.h;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- batch
+struct mt_batch {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int64_t n_docs = 0;
+    mt_batch_options opt{};
+    // tables
+    std::vector<std::string> keys, values;
+    std::vector<uint8_t> key_is_index;
+    std::vector<uint32_t> key_index;
+    std::vector<uint8_t> value_flags;
+    std::vector<std::string> clients;  // shared table
+    std::unordered_map<int64_t, std::vector<std::string>> doc_clients;
+    // log (device) + host mirror of the layout
+    bool have_log = false, generated = false;
+    int64_t total_ops = 0, total_props = 0;
+    int32_t max_ops_per_doc = 0;
+    std::vector<int64_t> h_off;
+    std::vector<uint64_t> h_text_base, h_pool_base;
+    std::vector<uint32_t> h_text_len, h_text_cap, h_pool_cap;
+    uint64_t text_words = 0, pool_words = 0;
+    mt_op *d_ops = nullptr;
+    int64_t *d_off = nullptr;
+    uint16_t *d_text = nullptr;
+    uint64_t *d_text_base = nullptr, *d_pool_base = nullptr;
+    uint32_t *d_text_len = nullptr, *d_text_cap = nullptr, *d_pool_cap = nullptr;
+    uint32_t *d_pool = nullptr;
+    mt_prop *d_props = nullptr;
+    uint8_t *d_vflags = nullptr;
+    double payload_units = 0, prop_records = 0;
+    // launches / results
+    std::vector<Launch> launches;
+    std::vector<DocRes> where;
+    std::vector<DocOut> docout;  // gathered per doc
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float kernel_ms = 0, total_ms = 0;
+    bool ran = false;
+    hipStream_t run_stream = nullptr;
+    std::chrono::steady_clock::time_point t_launch;
+    // single-document result cache
+    int64_t cached_doc = -1;
+    std::vector<OutRec> c_recs;
+    std::vector<uint16_t> c_text;
+    std::vector<uint32_t> c_pool;
+    DocOut c_out{};
+    std::vector<std::string> c_blob_names, c_blobs;
+    int64_t c_blob_doc = -1;
+};
+
+static void free_launches(mt_batch *b) {
+    for (auto &L : b->launches) {
+        (void)hipFree(L.d_out);
+        (void)hipFree(L.d_docout);
+        (void)hipFree(L.d_list);
+    }
+    b->launches.clear();
+}
+
+static void free_log(mt_batch *b) {
+    (void)hipFree(b->d_ops);
+    (void)hipFree(b->d_off);
+    (void)hipFree(b->d_text);
+    (void)hipFree(b->d_text_base);
+    (void)hipFree(b->d_text_len);
+    (void)hipFree(b->d_text_cap);
+    (void)hipFree(b->d_pool);
+    (void)hipFree(b->d_pool_base);
+    (void)hipFree(b->d_pool_cap);
+    (void)hipFree(b->d_props);
+    b->d_ops = nullptr;
+    b->d_off = nullptr;
+    b->d_text = nullptr;
+    b->d_text_base = b->d_pool_base = nullptr;
+    b->d_text_len = b->d_text_cap = b->d_pool_cap = nullptr;
+    b->d_pool = nullptr;
+    b->d_props = nullptr;
+    b->have_log = false;
+}
+
+extern "C" {
+
+MT_API const char *mt_status_string(int code) {
+    switch (code) {
+        case MT_OK: return "ok";
+        case MT_INVALID_POS: return "MergeTree insert failed (invalid position)";
+        case MT_SEQ_ORDER: return "sequence number order violated";
+        case MT_MSN_ORDER: return "minimum sequence number order violated";
+        case MT_UNSUPPORTED: return "unsupported op for the observer replay path";
+        case MT_BAD_INPUT: return "bad input";
+        case MT_CAPACITY: return "document exceeds device capacity";
+        case MT_INTERNAL: return "internal error";
+        case MT_ERR_HIP: return "HIP runtime error";
+        case MT_ERR_ARG: return "invalid argument";
+        case MT_ERR_STATE: return "invalid batch state";
+        case MT_ERR_NO_DEVICE: return "no HIP device";
+        default: return "unknown";
+    }
+}
+
+MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_options *opts) {
+    if (!out || n_docs <= 0 || n_docs > (int64_t)0x7FFFFFFF) return MT_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MT_ERR_NO_DEVICE;
+    mt_batch *b = new mt_batch();
+    HIPCHK(hipGetDevice(&b->device));
+    b->n_docs = n_docs;
+    if (opts) b->opt = *opts;
+    if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
+    if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
+    if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
+    if (b->opt.max_retries <= 0) b->opt.max_retries = 3;
+    if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
+        delete b;
+        return MT_ERR_HIP;
+    }
+    b->clients = {"readonly"};
+    b->values = {"null"};
+    b->value_flags = {1};
+    *out = b;
+    return MT_OK;
+}
+
+MT_API void mt_batch_destroy(mt_batch *b) {
+    if (!b) return;
+    free_launches(b);
+    free_log(b);
+    (void)hipFree(b->d_vflags);
+    if (b->ev0) (void)hipEventDestroy(b->ev0);
+    if (b->ev1) (void)hipEventDestroy(b->ev1);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_keys, const char *const *values_json,
+                               int32_t n_values) {
+    if (!b || n_keys < 0 || n_values < 1) return MT_ERR_ARG;
+    b->keys.assign(keys, keys + n_keys);
+    b->key_is_index.assign(n_keys, 0);
+    b->key_index.assign(n_keys, 0);
+    for (int i = 0; i < n_keys; i++) {
+        uint32_t idx = 0;
+        if (array_index(b->keys[i], &idx)) {
+            b->key_is_index[i] = 1;
+            b->key_index[i] = idx;
+        }
+    }
+    b->values.resize(n_values);
+    b->value_flags.resize(n_values);
+    for (int i = 0; i < n_values; i++) {
+        b->values[i] = (i == 0 || !values_json[i]) ? std::string("null") : std::string(values_json[i]);
+        b->value_flags[i] = json_falsy(b->values[i]) ? 1 : 0;
+    }
+    (void)hipFree(b->d_vflags);
+    b->d_vflags = nullptr;
+    HIPCHK(dalloc(&b->d_vflags, b->value_flags.size()));
+    HIPCHK(hipMemcpy(b->d_vflags, b->value_flags.data(), b->value_flags.size(), hipMemcpyHostToDevice));
+    return MT_OK;
+}
+
+MT_API int mt_batch_set_clients(mt_batch *b, int64_t doc, const char *const *names, int32_t n) {
+    if (!b || n < 1 || n > 64 || doc >= b->n_docs) return MT_ERR_ARG;
+    std::vector<std::string> v(names, names + n);
+    if (doc < 0) {
+        b->clients = v;
+        b->doc_clients.clear();
+    } else {
+        b->doc_clients[doc] = v;
+    }
+    return MT_OK;
+}
+
+static const std::vector<std::string> &clients_of(mt_batch *b, int64_t doc) {
+    auto it = b->doc_clients.find(doc);
+    return it == b->doc_clients.end() ? b->clients : it->second;
+}
+
+static int ensure_tables(mt_batch *b) {
+    if (!b->d_vflags) {
+        HIPCHK(dalloc(&b->d_vflags, b->value_flags.size()));
+        HIPCHK(hipMemcpy(b->d_vflags, b->value_flags.data(), b->value_flags.size(), hipMemcpyHostToDevice));
+    }
+    return MT_OK;
+}
+
+static uint32_t align16u(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
+
+MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_off, const uint16_t *text,
+                           int64_t n_text, const mt_prop *props, int64_t n_props) {
+    if (!b || !ops || !doc_op_off || doc_op_off[0] != 0) return MT_ERR_ARG;
+    int rc = ensure_tables(b);
+    if (rc) return rc;
+    const int64_t D = b->n_docs;
+    const int64_t N = doc_op_off[D];
+    // stage: per-doc text regions (payload in op order, then the merge arena), prop pools
+    std::vector<mt_op> h_ops(ops, ops + N);
+    b->h_off.assign(doc_op_off, doc_op_off + D + 1);
+    b->h_text_base.assign(D, 0);
+    b->h_text_len.assign(D, 0);
+    b->h_text_cap.assign(D, 0);
+    b->h_pool_base.assign(D, 0);
+    b->h_pool_cap.assign(D, 0);
+    uint64_t tbase = 0, pbase = 0;
+    int32_t max_ops = 0;
+    b->payload_units = 0;
+    b->prop_records = 0;
+    for (int64_t d = 0; d < D; d++) {
+        int64_t a = doc_op_off[d], e = doc_op_off[d + 1];
+        if (e < a) return MT_ERR_ARG;
+        max_ops = std::max<int32_t>(max_ops, (int32_t)(e - a));
+        uint64_t pay = 0, nprop_ops = 0;
+        for (int64_t i = a; i < e; i++) {
+            const mt_op &o = ops[i];
+            if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
+                if ((int64_t)o.payload + (int64_t)o.payload_len > n_text) return MT_ERR_ARG;
+                pay += o.payload_len;
+            }
+            if (o.type == MT_OP_ANNOTATE) {
+                if ((int64_t)o.payload + (int64_t)o.payload_len > n_props) return MT_ERR_ARG;
+                nprop_ops++;
+                b->prop_records += o.payload_len;
+            }
+            if (o.type == MT_OP_INSERT && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
+                if ((int64_t)o.pos2 + (int64_t)MT_OPF_NPROPS(o.flags) > n_props) return MT_ERR_ARG;
+                nprop_ops++;
+                b->prop_records += MT_OPF_NPROPS(o.flags);
+            }
+        }
+        b->payload_units += (double)pay;
+        uint64_t cap = (uint64_t)align16u(pay) + (uint64_t)b->opt.arena_factor * pay + 4096;
+        if (cap > 0xFFFFFFF0ull) return MT_ERR_ARG;
+        b->h_text_base[d] = tbase;
+        b->h_text_len[d] = (uint32_t)pay;
+        b->h_text_cap[d] = (uint32_t)cap;
+        tbase += align16u(cap);
+        uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * nprop_ops;
+        b->h_pool_base[d] = pbase;
+        b->h_pool_cap[d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
+        pbase += align16u(pc);
+    }
+    b->text_words = tbase;
+    b->pool_words = pbase;
+    std::vector<uint16_t> h_text(tbase ? tbase : 1, 0);
+    for (int64_t d = 0; d < D; d++) {
+        uint32_t w = 0;
+        for (int64_t i = doc_op_off[d]; i < doc_op_off[d + 1]; i++) {
+            mt_op &o = h_ops[i];
+            if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
+                if (o.payload_len) memcpy(&h_text[b->h_text_base[d] + w], text + o.payload, 2ull * o.payload_len);
+                o.flags &= (uint16_t)~MT_OPF_INTERNAL_ENDS_NL;
+                if (o.payload_len && text[o.payload + o.payload_len - 1] == (uint16_t)'\n')
+                    o.flags |= (uint16_t)MT_OPF_INTERNAL_ENDS_NL;
+                o.payload = w;
+                w += o.payload_len;
+            }
+        }
+    }
+    free_launches(b);
+    free_log(b);
+    b->total_ops = N;
+    b->total_props = n_props;
+    b->max_ops_per_doc = max_ops;
+    HIPCHK(dalloc(&b->d_ops, (size_t)N));
+    HIPCHK(dalloc(&b->d_off, (size_t)D + 1));
+    HIPCHK(dalloc(&b->d_text, (size_t)h_text.size()));
+    HIPCHK(dalloc(&b->d_text_base, (size_t)D));
+    HIPCHK(dalloc(&b->d_text_len, (size_t)D));
+    HIPCHK(dalloc(&b->d_text_cap, (size_t)D));
+    HIPCHK(dalloc(&b->d_pool, (size_t)pbase));
+    HIPCHK(dalloc(&b->d_pool_base, (size_t)D));
+    HIPCHK(dalloc(&b->d_pool_cap, (size_t)D));
+    HIPCHK(dalloc(&b->d_props, (size_t)std::max<int64_t>(n_props, 1)));
+    HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_off, doc_op_off, sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text, h_text.data(), 2 * h_text.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_base, b->h_text_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_len, b->h_text_len.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_cap, b->h_text_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_pool_base, b->h_pool_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_pool_cap, b->h_pool_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    if (n_props > 0) HIPCHK(hipMemcpy(b->d_props, props, sizeof(mt_prop) * (size_t)n_props, hipMemcpyHostToDevice));
+    b->have_log = true;
+    b->generated = false;
+    b->ran = false;
+    return MT_OK;
+}
+
+// capacity classes: derived from ops per document unless given
+static Caps caps_for(const mt_batch *b, int32_t ops_per_doc, int level) {
+    Caps c;
+    int32_t seg = b->opt.seg_cap;
+    if (seg <= 0) {
+        seg = 64;
+        while (seg < ops_per_doc / 16 + 64 && seg < 2048) seg *= 2;
+    }
+    seg <<= level;
+    if (seg > 4096) seg = 4096;
+    c.seg = seg;
+    c.oe = b->opt.oe_cap > 0 ? (b->opt.oe_cap << level) : seg + seg / 2 + 16;
+    c.blk = b->opt.blk_cap > 0 ? (b->opt.blk_cap << level) : seg / 2 + 16;
+    c.heap = b->opt.heap_cap > 0 ? (b->opt.heap_cap << level) : seg / 2 + 64;
+    return c;
+}
+
+static int max_lds_bytes() {
+    static int v = -1;
+    if (v < 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        hipDeviceProp_t p;
+        v = 65536;
+        if (hipGetDeviceProperties(&p, dev) == hipSuccess) {
+            size_t m = std::max(p.sharedMemPerBlock, p.sharedMemPerBlockOptin);
+            if (p.maxSharedMemoryPerMultiProcessor > m) m = p.maxSharedMemoryPerMultiProcessor;
+            v = (int)m;
+        }
+        if (v > 160 * 1024) v = 160 * 1024;
+        v -= 1024;  // static LDS of the generator kernel + margin
+    }
+    return v;
+}
+
+static mt::ReplayParams base_params(mt_batch *b) {
+    mt::ReplayParams P{};
+    P.ops = b->d_ops;
+    P.doc_op_off = b->d_off;
+    P.text = b->d_text;
+    P.doc_text_base = b->d_text_base;
+    P.doc_text_len = b->d_text_len;
+    P.doc_text_cap = b->d_text_cap;
+    P.pool = b->d_pool;
+    P.doc_pool_base = b->d_pool_base;
+    P.doc_pool_cap = b->d_pool_cap;
+    P.props_in = b->d_props;
+    P.value_flags = b->d_vflags;
+    P.n_values = (uint32_t)b->value_flags.size();
+    return P;
+}
+
+static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
+    int64_t n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+    L.out_cap = L.caps.oe;
+    L.lds = mt::Engine::lds_bytes(L.caps);
+    HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
+    HIPCHK(dalloc(&L.d_docout, (size_t)n));
+    if (!L.docs.empty()) {
+        HIPCHK(dalloc(&L.d_list, L.docs.size()));
+        HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
+    }
+    mt::ReplayParams P = base_params(b);
+    P.out = L.d_out;
+    P.doc_out = L.d_docout;
+    P.n_docs = n;
+    P.doc_list = L.d_list;
+    P.out_cap = L.out_cap;
+    P.caps = L.caps;
+    if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)mt::mt_replay_kernel,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
+    hipLaunchKernelGGL(mt::mt_replay_kernel, dim3((unsigned)n), dim3(64), L.lds, s, P);
+    HIPCHK(hipGetLastError());
+    return MT_OK;
+}
+
+MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
+    if (!b || !b->have_log) return MT_ERR_STATE;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->stream;
+    free_launches(b);
+    b->ran = false;
+    b->cached_doc = -1;
+    b->c_blob_doc = -1;
+    b->t_launch = std::chrono::steady_clock::now();
+    Launch L;
+    L.caps = caps_for(b, b->max_ops_per_doc, 0);
+    while (mt::Engine::lds_bytes(L.caps) > (size_t)max_lds_bytes() && L.caps.seg > 64) {
+        L.caps.seg /= 2;
+        L.caps.oe = L.caps.seg + L.caps.seg / 2 + 16;
+        L.caps.blk = L.caps.seg / 2 + 16;
+        L.caps.heap = L.caps.seg / 2 + 64;
+    }
+    b->launches.push_back(L);
+    HIPCHK(hipEventRecord(b->ev0, s));
+    int rc = launch_replay(b, s, b->launches.back());
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(b->ev1, s));
+    b->run_stream = s;
+    return MT_OK;
+}
+
+static int gather_launch(mt_batch *b, int li) {
+    Launch &L = b->launches[li];
+    int64_t n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+    std::vector<DocOut> tmp((size_t)n);
+    HIPCHK(hipMemcpy(tmp.data(), L.d_docout, sizeof(DocOut) * (size_t)n, hipMemcpyDeviceToHost));
+    if (b->docout.size() != (size_t)b->n_docs) {
+        b->docout.assign((size_t)b->n_docs, DocOut{});
+        b->where.assign((size_t)b->n_docs, DocRes{});
+    }
+    for (int64_t i = 0; i < n; i++) {
+        int64_t d = L.docs.empty() ? i : L.docs[i];
+        b->docout[d] = tmp[i];
+        b->where[d].launch = li;
+        b->where[d].idx = (int32_t)i;
+    }
+    return MT_OK;
+}
+
+MT_API int mt_batch_sync(mt_batch *b) {
+    if (!b || b->launches.empty()) return MT_ERR_STATE;
+    HIPCHK(hipEventSynchronize(b->ev1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    b->kernel_ms = ms;
+    int rc = gather_launch(b, 0);
+    if (rc) return rc;
+    // capacity escalation: documents whose LDS tables overflowed re-run in a larger class
+    for (int level = 1; level <= b->opt.max_retries; level++) {
+        Launch L;
+        for (int64_t d = 0; d < b->n_docs; d++)
+            if (b->docout[d].status == MT_CAPACITY && (b->docout[d].cap_kind == 1 || b->docout[d].cap_kind == 4))
+                L.docs.push_back((int32_t)d);
+        if (L.docs.empty()) break;
+        L.caps = caps_for(b, b->max_ops_per_doc, level);
+        if (mt::Engine::lds_bytes(L.caps) > (size_t)max_lds_bytes()) break;  // largest LDS class reached
+        b->launches.push_back(L);
+        HIPCHK(hipEventRecord(b->ev0, b->run_stream));
+        rc = launch_replay(b, b->run_stream, b->launches.back());
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(b->ev1, b->run_stream));
+        HIPCHK(hipEventSynchronize(b->ev1));
+        HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+        b->kernel_ms += ms;
+        rc = gather_launch(b, (int)b->launches.size() - 1);
+        if (rc) return rc;
+    }
+    b->total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count();
+    b->ran = true;
+    return MT_OK;
+}
+
+MT_API int mt_batch_run(mt_batch *b, void *hip_stream) {
+    int rc = mt_batch_launch(b, hip_stream);
+    if (rc) return rc;
+    return mt_batch_sync(b);
+}
+
+MT_API int mt_batch_get_stats(mt_batch *b, mt_batch_stats *o) {
+    if (!b || !o) return MT_ERR_ARG;
+    memset(o, 0, sizeof *o);
+    o->n_docs = b->n_docs;
+    o->n_ops = b->total_ops;
+    o->launches = (int32_t)b->launches.size();
+    o->kernel_ms = b->kernel_ms;
+    o->total_ms = b->total_ms;
+    if (!b->launches.empty()) o->lds_bytes = (int32_t)b->launches[0].lds;
+    if (!b->ran) return MT_OK;
+    for (int64_t d = 0; d < b->n_docs; d++) {
+        const DocOut &x = b->docout[d];
+        o->ops_applied += x.ops_done;
+        if (x.status != MT_OK) o->docs_failed++;
+        o->max_oe = std::max(o->max_oe, x.max_oe);
+        o->max_slots = std::max(o->max_slots, x.max_slots);
+        o->max_blocks = std::max(o->max_blocks, x.max_blocks);
+        o->max_heap = std::max(o->max_heap, x.max_heap);
+    }
+    return MT_OK;
+}
+
+// DESIGN.md "Roofline": per document 32 B per op record + 2 B per inserted code unit + 8 B per
+// prop record (read) + 32 B per final table entry + 2 B per final text code unit (written).
+MT_API int mt_batch_algorithmic_bytes(mt_batch *b, double *bytes) {
+    if (!b || !bytes || !b->ran) return MT_ERR_STATE;
+    double t = 32.0 * (double)b->total_ops + 2.0 * b->payload_units + 8.0 * b->prop_records;
+    for (int64_t d = 0; d < b->n_docs; d++) t += 32.0 * (double)b->docout[d].n_out;
+    // final text: visible code units == sum of live lengths; bounded by the payload, use the
+    // device-reported table (exact) when cached per doc would cost a download — estimate with
+    // the table's live segment lengths is done by callers that need it exactly.
+    *bytes = t;
+    return MT_OK;
+}
+
+MT_API int32_t mt_doc_status(mt_batch *b, int64_t doc) {
+    if (!b || !b->ran || doc < 0 || doc >= b->n_docs) return -MT_ERR_ARG;
+    return b->docout[doc].status;
+}
+
+// ---------------------------------------------------------------- per-document results
+static int load_doc(mt_batch *b, int64_t d) {
+    if (!b->ran) return MT_ERR_STATE;
+    if (d < 0 || d >= b->n_docs) return MT_ERR_ARG;
+    if (b->cached_doc == d) return MT_OK;
+    const DocRes &w = b->where[d];
+    const Launch &L = b->launches[w.launch];
+    b->c_out = b->docout[d];
+    b->c_recs.resize((size_t)b->c_out.n_out);
+    if (b->c_out.n_out)
+        HIPCHK(hipMemcpy(b->c_recs.data(), L.d_out + (size_t)w.idx * L.out_cap, sizeof(OutRec) * b->c_recs.size(),
+                         hipMemcpyDeviceToHost));
+    uint32_t tt = std::min<uint32_t>(b->c_out.text_top, b->h_text_cap[d]);
+    b->c_text.resize(tt);
+    if (tt) HIPCHK(hipMemcpy(b->c_text.data(), b->d_text + b->h_text_base[d], 2ull * tt, hipMemcpyDeviceToHost));
+    uint32_t pt = std::min<uint32_t>(b->c_out.pool_top, b->h_pool_cap[d]);
+    b->c_pool.resize(pt);
+    if (pt) HIPCHK(hipMemcpy(b->c_pool.data(), b->d_pool + b->h_pool_base[d], 4ull * pt, hipMemcpyDeviceToHost));
+    b->cached_doc = d;
+    return MT_OK;
+}
+
+static bool rec_is_marker(const OutRec &r) { return (r.blk & 0xFFFFu) == mt::kMarkerSlot; }
+static bool rec_removed(const OutRec &r) { return r.rseq != mt::kNoneSeq; }
+static bool rec_is_text(const OutRec &r) { return !(r.meta & mt::kMetaMarker); }
+
+static const std::string &client_name(mt_batch *b, int64_t d, uint32_t id, std::string &tmp) {
+    const auto &t = clients_of(b, d);
+    if (id < t.size()) return t[id];
+    tmp = "undefined";
+    return tmp;
+}
+
+// JSON.stringify(properties): ordinary-object key order (array indices ascending, then
+// insertion order), values as given in the value table
+static void props_json(mt_batch *b, uint32_t id, std::string &o) {
+    const uint32_t *p = b->c_pool.data() + id;
+    uint32_t n = p[0];
+    std::vector<std::pair<uint64_t, uint32_t>> order;
+    order.reserve(n);
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t k = p[2 + 2 * i];
+        uint64_t rank = (k < b->key_is_index.size() && b->key_is_index[k]) ? (uint64_t)b->key_index[k]
+                                                                            : (1ull << 32) + i;
+        order.push_back({rank, i});
+    }
+    std::sort(order.begin(), order.end());
+    o.push_back('{');
+    for (size_t j = 0; j < order.size(); j++) {
+        uint32_t i = order[j].second;
+        uint32_t k = p[2 + 2 * i], v = p[3 + 2 * i];
+        if (j) o.push_back(',');
+        json_quote8(o, k < b->keys.size() ? b->keys[k] : std::string("?"));
+        o.push_back(':');
+        o += v < b->values.size() ? b->values[v] : std::string("null");
+    }
+    o.push_back('}');
+}
+
+static bool props_match_host(mt_batch *b, uint32_t a, uint32_t c) {
+    if (a == c) return true;
+    if (!a || !c) return false;
+    const uint32_t *pa = b->c_pool.data() + a, *pc = b->c_pool.data() + c;
+    if (pa[0] != pc[0]) return false;
+    for (uint32_t i = 0; i < pa[0]; i++) {
+        bool f = false;
+        for (uint32_t j = 0; j < pc[0]; j++)
+            if (pa[2 + 2 * i] == pc[2 + 2 * j] && pa[3 + 2 * i] == pc[3 + 2 * j]) f = true;
+        if (!f) return false;
+    }
+    return true;
+}
+
+static int out_str(const std::string &s, char *buf, int64_t cap, int64_t *len) {
+    if (len) *len = (int64_t)s.size();
+    if (buf && cap > 0) {
+        int64_t m = std::min<int64_t>((int64_t)s.size(), cap - 1);
+        memcpy(buf, s.data(), (size_t)m);
+        buf[m] = 0;
+    }
+    return MT_OK;
+}
+
+MT_API int mt_doc_text(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len) {
+    if (!b) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    std::string o;
+    for (const OutRec &r : b->c_recs)
+        if (!rec_is_marker(r) && !rec_removed(r) && rec_is_text(r))
+            utf16_to_utf8(o, b->c_text.data() + r.toff, r.len);
+    return out_str(o, buf, cap, len);
+}
+
+MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len) {
+    if (!b) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    std::string o = "[";
+    std::string run_props;
+    int64_t pos = 0, run_start = 0, run_len = 0;
+    bool first = true;
+    auto flush = [&]() {
+        if (run_len <= 0) return;
+        if (!first) o.push_back(',');
+        first = false;
+        o += "[" + std::to_string(run_start) + "," + std::to_string(run_len) + "," + run_props + "]";
+    };
+    for (const OutRec &r : b->c_recs) {
+        if (rec_is_marker(r) || rec_removed(r)) continue;
+        std::string pj;
+        if (!r.props) {
+            pj = "null";
+        } else {
+            std::string j;
+            props_json(b, r.props, j);
+            std::vector<uint16_t> u = utf8_to_utf16(j);
+            json_quote16(pj, u.data(), u.size());
+        }
+        if (run_len > 0 && pj == run_props) {
+            run_len += r.len;
+        } else {
+            flush();
+            run_props = pj;
+            run_start = pos;
+            run_len = r.len;
+        }
+        pos += r.len;
+    }
+    flush();
+    o.push_back(']');
+    return out_str(o, buf, cap, len);
+}
+
+// segment.toJSONObject() (textSegment.ts:48-54, mergeTree.ts:652-656)
+static void seg_json(mt_batch *b, bool text, const uint16_t *t, size_t n, uint32_t ref_type, uint32_t props,
+                     std::string &o) {
+    if (text) {
+        if (props) {
+            o += "{\"text\":";
+            json_quote16(o, t, n);
+            o += ",\"props\":";
+            props_json(b, props, o);
+            o.push_back('}');
+        } else {
+            json_quote16(o, t, n);
+        }
+    } else {
+        o += "{\"marker\":{\"refType\":" + std::to_string(ref_type) + "}";
+        if (props) {
+            o += ",\"props\":";
+            props_json(b, props, o);
+        }
+        o.push_back('}');
+    }
+}
+
+// SnapshotV1.extractSync + emit (snapshotV1.ts:85-247, snapshotChunks.ts:122-131)
+MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs) {
+    if (!b) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    const int32_t min_seq = b->c_out.min_seq, cur_seq = b->c_out.cur_seq;
+    std::vector<std::string> segs;
+    std::vector<int64_t> lens;
+    // coalescing candidate (a clone in the reference: snapshotV1.ts:191-210)
+    bool have_prev = false, prev_text = true;
+    std::vector<uint16_t> ptext;
+    uint32_t pref = 0, pprops = 0;
+    auto push_prev = [&]() {
+        if (!have_prev) return;
+        std::string j;
+        seg_json(b, prev_text, ptext.data(), ptext.size(), pref, pprops, j);
+        segs.push_back(j);
+        lens.push_back(prev_text ? (int64_t)ptext.size() : 1);
+        have_prev = false;
+    };
+    auto set_prev = [&](const OutRec &r) {
+        have_prev = true;
+        prev_text = rec_is_text(r);
+        pref = r.toff;
+        pprops = r.props;
+        ptext.clear();
+        if (prev_text) ptext.assign(b->c_text.begin() + r.toff, b->c_text.begin() + r.toff + r.len);
+    };
+    std::string tmp;
+    for (const OutRec &r : b->c_recs) {
+        if (rec_is_marker(r)) continue;
+        bool removed = rec_removed(r);
+        if (removed && r.rseq <= min_seq) continue;
+        if (r.seq <= min_seq && !removed) {
+            if (!have_prev) {
+                set_prev(r);
+            } else {
+                bool can = prev_text && rec_is_text(r) && !(!ptext.empty() && ptext.back() == (uint16_t)'\n') &&
+                           (ptext.size() <= mt::kGranularity || r.len <= mt::kGranularity);
+                if (can && props_match_host(b, pprops, r.props)) {
+                    ptext.insert(ptext.end(), b->c_text.begin() + r.toff, b->c_text.begin() + r.toff + r.len);
+                } else {
+                    push_prev();
+                    set_prev(r);
+                }
+            }
+        } else {
+            push_prev();
+            std::string j = "{\"json\":";
+            seg_json(b, rec_is_text(r), b->c_text.data() + (rec_is_text(r) ? r.toff : 0), rec_is_text(r) ? r.len : 0,
+                     r.toff, r.props, j);
+            if (r.seq > min_seq) {
+                j += ",\"seq\":" + std::to_string(r.seq) + ",\"client\":";
+                json_quote8(j, client_name(b, doc, r.meta & 63u, tmp));
+            }
+            if (removed) {
+                j += ",\"removedSeq\":" + std::to_string(r.rseq) + ",\"removedClient\":";
+                json_quote8(j, client_name(b, doc, (r.meta >> 6) & 63u, tmp));
+            }
+            j.push_back('}');
+            segs.push_back(j);
+            lens.push_back(r.len);
+        }
+    }
+    push_prev();
+    // emit: chunks of >= chunk_size code units (each chunk includes the segment that crosses)
+    struct Chunk {
+        int64_t start, count, length;
+    };
+    std::vector<Chunk> chunks;
+    int64_t total_count = 0, total_length = 0;
+    do {
+        int64_t length = 0, count = 0;
+        while (length < b->opt.chunk_size && total_count + count < (int64_t)segs.size()) {
+            length += lens[total_count + count];
+            count++;
+        }
+        chunks.push_back({total_count, count, length});
+        total_count += count;
+        total_length += length;
+    } while (total_count < (int64_t)segs.size());
+    b->c_blob_names.clear();
+    b->c_blobs.clear();
+    for (size_t ci = 0; ci < chunks.size(); ci++) {
+        std::string j = "{\"version\":\"1\",\"segmentCount\":" + std::to_string(chunks[ci].count) +
+                        ",\"length\":" + std::to_string(chunks[ci].length) + ",\"segments\":[";
+        for (int64_t k = 0; k < chunks[ci].count; k++) {
+            if (k) j.push_back(',');
+            j += segs[chunks[ci].start + k];
+        }
+        j += "],\"startIndex\":" + std::to_string(chunks[ci].start);
+        if (ci == 0) {
+            j += ",\"headerMetadata\":{\"minSequenceNumber\":" + std::to_string(min_seq) +
+                 ",\"sequenceNumber\":" + std::to_string(cur_seq) + ",\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+            for (size_t bi = 1; bi < chunks.size(); bi++) j += ",{\"id\":\"body_" + std::to_string(bi - 1) + "\"}";
+            j += "],\"totalLength\":" + std::to_string(total_length) +
+                 ",\"totalSegmentCount\":" + std::to_string(total_count) + "}";
+        }
+        j.push_back('}');
+        b->c_blob_names.push_back(ci == 0 ? std::string("header") : "body_" + std::to_string(ci - 1));
+        b->c_blobs.push_back(j);
+    }
+    b->c_blob_doc = doc;
+    if (n_blobs) *n_blobs = (int32_t)b->c_blobs.size();
+    return MT_OK;
+}
+
+MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name, int64_t name_cap, char *buf,
+                                int64_t cap, int64_t *len) {
+    if (!b) return MT_ERR_ARG;
+    if (b->c_blob_doc != doc) {
+        int rc = mt_doc_snapshot_v1(b, doc, nullptr);
+        if (rc) return rc;
+    }
+    if (i < 0 || i >= (int32_t)b->c_blobs.size()) return MT_ERR_ARG;
+    if (name && name_cap > 0) snprintf(name, (size_t)name_cap, "%s", b->c_blob_names[i].c_str());
+    return out_str(b->c_blobs[i], buf, cap, len);
+}
+
+MT_API int mt_doc_shape(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len) {
+    if (!b) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    std::string o = "D" + std::to_string(b->c_out.depth) + ":";
+    int cnt = 0;
+    bool first = true;
+    for (const OutRec &r : b->c_recs) {
+        if (rec_is_marker(r)) {
+            if (!first) o.push_back(',');
+            first = false;
+            o += std::to_string(cnt);
+            cnt = 0;
+        } else {
+            cnt++;
+        }
+    }
+    return out_str(o, buf, cap, len);
+}
+
+// DESIGN.md "State digest" (same definition as the test oracle's mto_state_digest)
+MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out) {
+    if (!b || !out) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    Fnv f;
+    std::string tmp;
+    f.u32((uint32_t)b->c_out.depth);
+    size_t i = 0, n = b->c_recs.size();
+    while (i < n) {
+        size_t j = i;
+        while (j < n && !rec_is_marker(b->c_recs[j])) j++;
+        f.u32(0xB10CB10Cu);
+        f.u32((uint32_t)(j - i));
+        for (size_t k = i; k < j; k++) {
+            const OutRec &r = b->c_recs[k];
+            bool text = rec_is_text(r), removed = rec_removed(r);
+            uint64_t ovl = 0;
+            for (uint32_t c = 0; c < 32; c++)
+                if (r.ovl & (1u << c)) ovl += fnv_name(client_name(b, doc, c, tmp));
+            f.u32(text ? 0u : 1u);
+            f.u32(r.len);
+            f.u32((uint32_t)r.seq);
+            f.u64(fnv_name(client_name(b, doc, r.meta & 63u, tmp)));
+            f.u32(removed ? (uint32_t)r.rseq : 0xFFFFFFFFu);
+            f.u64(removed ? fnv_name(client_name(b, doc, (r.meta >> 6) & 63u, tmp)) : 0ull);
+            f.u64(ovl);
+            if (!r.props) {
+                f.u32(0xFFFFFFFFu);
+            } else {
+                std::string pj;
+                props_json(b, r.props, pj);
+                f.u32((uint32_t)pj.size());
+                f.bytes(pj.data(), pj.size());
+            }
+            if (text) {
+                for (uint32_t q = 0; q < r.len; q++) {
+                    uint16_t c = b->c_text[r.toff + q];
+                    unsigned char b2[2] = {(unsigned char)c, (unsigned char)(c >> 8)};
+                    f.bytes(b2, 2);
+                }
+            } else {
+                f.u32(r.toff);
+            }
+        }
+        i = j + 1;
+    }
+    f.u32((uint32_t)b->c_out.min_seq);
+    f.u32((uint32_t)b->c_out.cur_seq);
+    f.u32((uint32_t)b->c_out.status);
+    *out = f.h;
+    return MT_OK;
+}
+
+// ---------------------------------------------------------------- logs
+MT_API int mt_batch_log_sizes(mt_batch *b, int64_t *n_ops, int64_t *n_text, int64_t *n_props) {
+    if (!b || !b->have_log) return MT_ERR_STATE;
+    if (n_ops) *n_ops = b->total_ops;
+    if (n_text) {
+        int64_t t = 0;
+        for (int64_t d = 0; d < b->n_docs; d++) t += b->h_text_len[d];
+        *n_text = t;
+    }
+    if (n_props) *n_props = b->total_props;
+    return MT_OK;
+}
+
+// batch-global layout: text of doc d follows doc d-1; prop offsets unchanged
+MT_API int mt_batch_download_log(mt_batch *b, mt_op *ops, int64_t *doc_op_off, uint16_t *text, mt_prop *props) {
+    if (!b || !b->have_log) return MT_ERR_STATE;
+    if (ops) {
+        HIPCHK(hipMemcpy(ops, b->d_ops, sizeof(mt_op) * (size_t)b->total_ops, hipMemcpyDeviceToHost));
+        int64_t tb = 0;
+        for (int64_t d = 0; d < b->n_docs; d++) {
+            for (int64_t i = b->h_off[d]; i < b->h_off[d + 1]; i++) {
+                mt_op &o = ops[i];
+                o.flags &= (uint16_t)~MT_OPF_INTERNAL_ENDS_NL;
+                if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) o.payload += (uint32_t)tb;
+            }
+            tb += b->h_text_len[d];
+        }
+    }
+    if (doc_op_off) memcpy(doc_op_off, b->h_off.data(), sizeof(int64_t) * (size_t)(b->n_docs + 1));
+    if (text) {
+        int64_t tb = 0;
+        for (int64_t d = 0; d < b->n_docs; d++) {
+            if (b->h_text_len[d])
+                HIPCHK(hipMemcpy(text + tb, b->d_text + b->h_text_base[d], 2ull * b->h_text_len[d], hipMemcpyDeviceToHost));
+            tb += b->h_text_len[d];
+        }
+    }
+    if (props && b->total_props > 0)
+        HIPCHK(hipMemcpy(props, b->d_props, sizeof(mt_prop) * (size_t)b->total_props, hipMemcpyDeviceToHost));
+    return MT_OK;
+}
+
+// ---------------------------------------------------------------- generator
+static const char *GEN_KEYS[MT_GEN_N_KEYS] = {"bold", "italic", "color", "size"};
+static const char *GEN_CLIENTS[] = {"readonly", "A", "B", "C", "D", "E", "F", "G", "H", "I", "J", "K", "L", "M",
+                                    "N", "O", "P", "Q", "R", "S", "T", "U", "V", "W", "X", "Y", "Z"};
+
+MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_first) {
+    if (!b || !p || p->n_ops < 1 || p->n_clients < 1 || p->n_clients > 26 || p->max_insert < 1) return MT_ERR_ARG;
+    // fixed generator tables (include/mt_gen.h)
+    std::vector<std::string> vals = {"null", "true", "\"red\"", "\"green\"", "\"blue\""};
+    for (int s = 8; s <= 24; s++) vals.push_back(std::to_string(s));
+    std::vector<const char *> vp, kp(GEN_KEYS, GEN_KEYS + MT_GEN_N_KEYS);
+    for (auto &v : vals) vp.push_back(v.c_str());
+    int rc = mt_batch_set_tables(b, kp.data(), MT_GEN_N_KEYS, vp.data(), (int32_t)vp.size());
+    if (rc) return rc;
+    rc = mt_batch_set_clients(b, -1, GEN_CLIENTS, p->n_clients + 1);
+    if (rc) return rc;
+    const int64_t D = b->n_docs;
+    const int64_t N = (int64_t)p->n_ops * D;
+    free_launches(b);
+    free_log(b);
+    b->h_off.resize(D + 1);
+    for (int64_t d = 0; d <= D; d++) b->h_off[d] = d * p->n_ops;
+    b->h_text_base.assign(D, 0);
+    b->h_text_len.assign(D, 0);
+    b->h_text_cap.assign(D, 0);
+    b->h_pool_base.assign(D, 0);
+    b->h_pool_cap.assign(D, 0);
+    const uint64_t pay_cap = (uint64_t)p->n_ops * (uint64_t)p->max_insert;
+    const uint64_t cap = align16u(pay_cap) + (uint64_t)b->opt.arena_factor * pay_cap / 2 + 4096;
+    const int64_t ann = (int64_t)p->n_ops * std::max(0, 100 - p->pct_insert - p->pct_remove) / 100;
+    const uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * (uint64_t)(ann + ann / 2 + 16);
+    if (cap > 0xFFFFFFF0ull || pc > 0xFFFFFFF0ull) return MT_ERR_ARG;
+    for (int64_t d = 0; d < D; d++) {
+        b->h_text_base[d] = (uint64_t)d * align16u(cap);
+        b->h_text_len[d] = (uint32_t)pay_cap;  // payload capacity: the arena starts after it
+        b->h_text_cap[d] = (uint32_t)cap;
+        b->h_pool_base[d] = (uint64_t)d * align16u(pc);
+        b->h_pool_cap[d] = (uint32_t)pc;
+    }
+    b->text_words = (uint64_t)D * align16u(cap);
+    b->pool_words = (uint64_t)D * align16u(pc);
+    b->total_ops = N;
+    b->total_props = 2 * N;
+    b->max_ops_per_doc = p->n_ops;
+    int rc2 = ensure_tables(b);
+    if (rc2) return rc2;
+    HIPCHK(dalloc(&b->d_ops, (size_t)N));
+    HIPCHK(dalloc(&b->d_off, (size_t)D + 1));
+    HIPCHK(dalloc(&b->d_text, (size_t)b->text_words));
+    HIPCHK(dalloc(&b->d_text_base, (size_t)D));
+    HIPCHK(dalloc(&b->d_text_len, (size_t)D));
+    HIPCHK(dalloc(&b->d_text_cap, (size_t)D));
+    HIPCHK(dalloc(&b->d_pool, (size_t)b->pool_words));
+    HIPCHK(dalloc(&b->d_pool_base, (size_t)D));
+    HIPCHK(dalloc(&b->d_pool_cap, (size_t)D));
+    HIPCHK(dalloc(&b->d_props, (size_t)(2 * N)));
+    HIPCHK(hipMemcpy(b->d_off, b->h_off.data(), 8 * (size_t)(D + 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_base, b->h_text_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_len, b->h_text_len.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_cap, b->h_text_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_pool_base, b->h_pool_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_pool_cap, b->h_pool_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    mt_gen_params *d_gen = nullptr;
+    HIPCHK(dalloc(&d_gen, 1));
+    HIPCHK(hipMemcpy(d_gen, p, sizeof(mt_gen_params), hipMemcpyHostToDevice));
+    // generation runs in the largest LDS class so no document overflows during synthesis
+    Launch L;
+    L.caps = caps_for(b, p->n_ops, 0);
+    for (int lvl = 1; lvl <= 3; lvl++) {
+        Caps c2 = caps_for(b, p->n_ops, lvl);
+        if (mt::Engine::lds_bytes(c2) <= (size_t)max_lds_bytes()) L.caps = c2;
+    }
+    L.out_cap = L.caps.oe;
+    L.lds = mt::Engine::lds_bytes(L.caps);
+    HIPCHK(dalloc(&L.d_out, (size_t)D * (size_t)L.out_cap));
+    HIPCHK(dalloc(&L.d_docout, (size_t)D));
+    mt::ReplayParams P = base_params(b);
+    P.out = L.d_out;
+    P.doc_out = L.d_docout;
+    P.n_docs = D;
+    P.doc_first = doc_first;
+    P.out_cap = L.out_cap;
+    P.caps = L.caps;
+    P.gen = d_gen;
+    P.gen_ops = b->d_ops;
+    P.gen_props = b->d_props;
+    if (L.lds > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void *)mt::mt_generate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)L.lds));
+    hipLaunchKernelGGL(mt::mt_generate_kernel, dim3((unsigned)D), dim3(64), L.lds, b->stream, P);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(b->stream));
+    std::vector<DocOut> outs((size_t)D);
+    HIPCHK(hipMemcpy(outs.data(), L.d_docout, sizeof(DocOut) * (size_t)D, hipMemcpyDeviceToHost));
+    (void)hipFree(L.d_out);
+    (void)hipFree(L.d_docout);
+    (void)hipFree(d_gen);
+    b->payload_units = 0;
+    b->prop_records = 0;
+    int bad = 0;
+    for (int64_t d = 0; d < D; d++) {
+        if (outs[d].status != MT_OK) bad++;
+        b->payload_units += outs[d].gen_text;
+        b->prop_records += outs[d].gen_props;
+    }
+    b->have_log = true;
+    b->generated = true;
+    b->ran = false;
+    if (bad) {
+        fprintf(stderr, "mtreplay: generator: %d documents failed (first status %d)\n", bad, outs[0].status);
+        return MT_INTERNAL;
+    }
+    return MT_OK;
+}
+
+}  // extern "C"

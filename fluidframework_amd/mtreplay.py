@@ -1,0 +1,295 @@
+"""Python host layer over libmtreplay.so (include/mtreplay.h).
+
+Mirrors the reference's per-document surface so tests read like the reference's own:
+
+    reference (packages/dds/merge-tree/src, sequence/src)      here
+    ------------------------------------------------------      ---------------------------------
+    new Client(...); client.startOrUpdateCollaboration(id)      ReplayBatch(n_docs, observer=id)
+    client.applyMsg(msg) for msg in log                         batch.ingest_messages(logs); batch.run()
+    sharedString.getText()                                      batch.doc(i).get_text()
+    client.getPropertiesAtPosition(pos)                         batch.doc(i).get_properties_at_position(pos)
+    new SnapshotV1(mt, logger).extractSync(); emit()            batch.doc(i).snapshot_v1()
+    thrown Error from applyMsg                                  batch.doc(i).status (MT_* code)
+
+Every op is applied by the HIP kernel; this module only marshals.  Loading fails loudly
+when the compiled library is missing or no GPU is present (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+from pathlib import Path
+
+import numpy as np
+
+from .oplog import OP_DTYPE, PROP_DTYPE, PackedBatch, Packer
+
+LIB_PATH = Path(__file__).resolve().parent / "libmtreplay.so"
+
+MT_OK, MT_INVALID_POS, MT_SEQ_ORDER, MT_MSN_ORDER, MT_UNSUPPORTED, MT_BAD_INPUT, MT_CAPACITY, MT_INTERNAL = range(8)
+MT_ERR_HIP, MT_ERR_ARG, MT_ERR_STATE, MT_ERR_NO_DEVICE = 100, 101, 102, 103
+
+# every entry point declared in include/mtreplay.h
+EXPORTS = [
+    "mt_status_string", "mt_batch_create", "mt_batch_destroy", "mt_batch_set_tables", "mt_batch_set_clients",
+    "mt_batch_ingest", "mt_batch_generate", "mt_batch_run", "mt_batch_launch", "mt_batch_sync",
+    "mt_batch_get_stats", "mt_batch_algorithmic_bytes", "mt_doc_status", "mt_doc_text", "mt_doc_props_runs",
+    "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_batch_log_sizes",
+    "mt_batch_download_log",
+]
+
+
+class MtError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what}: {status_string(code)} ({code})")
+        self.code = code
+
+
+class GenParams(C.Structure):
+    """mt_gen_params (include/mt_gen.h)"""
+
+    _fields_ = [("n_ops", C.c_int32), ("n_clients", C.c_int32), ("max_lag", C.c_int32),
+                ("pct_insert", C.c_int32), ("pct_remove", C.c_int32), ("min_len", C.c_int32),
+                ("max_insert", C.c_int32), ("pct_newline", C.c_int32), ("seed", C.c_uint64)]
+
+
+class BatchOptions(C.Structure):
+    _fields_ = [("chunk_size", C.c_int32), ("seg_cap", C.c_int32), ("oe_cap", C.c_int32), ("blk_cap", C.c_int32),
+                ("heap_cap", C.c_int32), ("arena_factor", C.c_int32), ("pool_per_op", C.c_int32),
+                ("max_retries", C.c_int32)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("n_docs", C.c_int64), ("n_ops", C.c_int64), ("ops_applied", C.c_int64),
+                ("docs_failed", C.c_int64), ("max_oe", C.c_int32), ("max_slots", C.c_int32),
+                ("max_blocks", C.c_int32), ("max_heap", C.c_int32), ("lds_bytes", C.c_int32),
+                ("launches", C.c_int32), ("kernel_ms", C.c_float), ("total_ms", C.c_float)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def gen_params(n_ops, n_clients=8, max_lag=32, pct_insert=60, pct_remove=40, min_len=4, max_insert=8,
+               pct_newline=2, seed=0xDEADBEEF) -> GenParams:
+    return GenParams(n_ops, n_clients, max_lag, pct_insert, pct_remove, min_len, max_insert, pct_newline, seed)
+
+
+_lib = None
+
+
+def lib():
+    """Load libmtreplay.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise FileNotFoundError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(str(LIB_PATH))
+    vp, i32, i64, cp = C.c_void_p, C.c_int32, C.c_int64, C.c_char_p
+    P = C.POINTER
+    L.mt_status_string.argtypes = [C.c_int]
+    L.mt_status_string.restype = cp
+    L.mt_batch_create.argtypes = [P(vp), i64, P(BatchOptions)]
+    L.mt_batch_destroy.argtypes = [vp]
+    L.mt_batch_destroy.restype = None
+    L.mt_batch_set_tables.argtypes = [vp, P(cp), i32, P(cp), i32]
+    L.mt_batch_set_clients.argtypes = [vp, i64, P(cp), i32]
+    L.mt_batch_ingest.argtypes = [vp, vp, vp, vp, i64, vp, i64]
+    L.mt_batch_generate.argtypes = [vp, P(GenParams), i64]
+    L.mt_batch_run.argtypes = [vp, vp]
+    L.mt_batch_launch.argtypes = [vp, vp]
+    L.mt_batch_sync.argtypes = [vp]
+    L.mt_batch_get_stats.argtypes = [vp, P(BatchStats)]
+    L.mt_batch_algorithmic_bytes.argtypes = [vp, P(C.c_double)]
+    L.mt_doc_status.argtypes = [vp, i64]
+    L.mt_doc_status.restype = i32
+    for fn in ("mt_doc_text", "mt_doc_props_runs", "mt_doc_shape"):
+        getattr(L, fn).argtypes = [vp, i64, C.c_char_p, i64, P(i64)]
+    L.mt_doc_snapshot_v1.argtypes = [vp, i64, P(i32)]
+    L.mt_doc_snapshot_blob.argtypes = [vp, i64, i32, C.c_char_p, i64, C.c_char_p, i64, P(i64)]
+    L.mt_doc_digest.argtypes = [vp, i64, P(C.c_uint64)]
+    L.mt_batch_log_sizes.argtypes = [vp, P(i64), P(i64), P(i64)]
+    L.mt_batch_download_log.argtypes = [vp, vp, vp, vp, vp]
+    _lib = L
+    return L
+
+
+def status_string(code: int) -> str:
+    return lib().mt_status_string(code).decode()
+
+
+def _chk(rc: int, what: str):
+    if rc != MT_OK:
+        raise MtError(rc, what)
+
+
+def _cstrs(strs):
+    arr = (C.c_char_p * max(1, len(strs)))()
+    for k, s in enumerate(strs):
+        arr[k] = s.encode("utf-8")
+    return arr
+
+
+class DocView:
+    """Read-out of one replayed document (a merge-tree Client after its last applyMsg)."""
+
+    def __init__(self, batch: "ReplayBatch", index: int):
+        self.batch, self.index = batch, index
+
+    @property
+    def status(self) -> int:
+        return int(lib().mt_doc_status(self.batch.h, self.index))
+
+    def _string(self, fn) -> str:
+        n = C.c_int64(0)
+        _chk(fn(self.batch.h, self.index, None, 0, C.byref(n)), fn.__name__)
+        buf = C.create_string_buffer(n.value + 1)
+        _chk(fn(self.batch.h, self.index, buf, n.value + 1, C.byref(n)), fn.__name__)
+        return buf.raw[: n.value].decode("utf-8")
+
+    def get_text(self) -> str:
+        return self._string(lib().mt_doc_text)
+
+    def props_runs(self) -> list:
+        return json.loads(self._string(lib().mt_doc_props_runs))
+
+    def get_properties_at_position(self, pos: int):
+        for start, length, props in self.props_runs():
+            if start <= pos < start + length:
+                return None if props is None else json.loads(props)
+        return None
+
+    def shape(self) -> str:
+        return self._string(lib().mt_doc_shape)
+
+    def digest(self) -> int:
+        out = C.c_uint64(0)
+        _chk(lib().mt_doc_digest(self.batch.h, self.index, C.byref(out)), "mt_doc_digest")
+        return int(out.value)
+
+    def snapshot_v1(self) -> dict:
+        L = lib()
+        n = C.c_int32(0)
+        _chk(L.mt_doc_snapshot_v1(self.batch.h, self.index, C.byref(n)), "mt_doc_snapshot_v1")
+        out = {}
+        for i in range(n.value):
+            name = C.create_string_buffer(64)
+            size = C.c_int64(0)
+            _chk(L.mt_doc_snapshot_blob(self.batch.h, self.index, i, name, 64, None, 0, C.byref(size)), "blob")
+            buf = C.create_string_buffer(size.value + 1)
+            _chk(L.mt_doc_snapshot_blob(self.batch.h, self.index, i, name, 64, buf, size.value + 1, C.byref(size)),
+                 "blob")
+            out[name.value.decode()] = buf.raw[: size.value].decode("utf-8")
+        return out
+
+
+class ReplayBatch:
+    """A batch of SharedString documents replayed on one MI355X (the current HIP device)."""
+
+    def __init__(self, n_docs: int, **options):
+        self.n_docs = int(n_docs)
+        opts = BatchOptions(**options)
+        h = C.c_void_p()
+        _chk(lib().mt_batch_create(C.byref(h), self.n_docs, C.byref(opts)), "mt_batch_create")
+        self.h = h
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mt_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- input
+    def set_tables(self, keys, values):
+        k, v = _cstrs(keys), _cstrs(values)
+        self._keep += [k, v]
+        _chk(lib().mt_batch_set_tables(self.h, k, len(keys), v, len(values)), "mt_batch_set_tables")
+
+    def set_clients(self, names, doc: int = -1):
+        a = _cstrs(names)
+        _chk(lib().mt_batch_set_clients(self.h, doc, a, len(names)), "mt_batch_set_clients")
+
+    def ingest(self, ops, doc_op_off, text, props):
+        ops = np.ascontiguousarray(ops, OP_DTYPE)
+        off = np.ascontiguousarray(doc_op_off, np.int64)
+        text = np.ascontiguousarray(text if len(text) else np.zeros(1, np.uint16), np.uint16)
+        props = np.ascontiguousarray(props if len(props) else np.zeros(1, PROP_DTYPE), PROP_DTYPE)
+        if len(off) != self.n_docs + 1:
+            raise ValueError("doc_op_off must have n_docs + 1 entries")
+        _chk(lib().mt_batch_ingest(self.h, ops.ctypes.data, off.ctypes.data, text.ctypes.data, len(text),
+                                   props.ctypes.data, len(props)), "mt_batch_ingest")
+
+    def ingest_packed(self, pb: PackedBatch):
+        self.set_tables(pb.keys or ["_"], pb.values)
+        shared = pb.clients[0] if pb.clients and all(c == pb.clients[0] for c in pb.clients) else None
+        if shared is not None:
+            self.set_clients(shared)
+        else:
+            for i, names in enumerate(pb.clients):
+                self.set_clients(names, i)
+        self.ingest(pb.ops, pb.doc_op_off, pb.text, pb.props)
+
+    def ingest_messages(self, docs, observer: str = "readonly"):
+        """docs: one ISequencedDocumentMessage list (dicts or JSON strings) per document."""
+        p = Packer(observer=observer)
+        for msgs in docs:
+            p.add_document(msgs)
+        pb = p.finish()
+        if len(pb.doc_op_off) != self.n_docs + 1:
+            raise ValueError("expected one message list per document")
+        self.ingest_packed(pb)
+        return pb
+
+    def generate(self, params: GenParams, doc_first: int = 0):
+        _chk(lib().mt_batch_generate(self.h, C.byref(params), doc_first), "mt_batch_generate")
+
+    # -- run
+    def run(self, stream=None):
+        _chk(lib().mt_batch_run(self.h, stream), "mt_batch_run")
+
+    def launch(self, stream=None):
+        _chk(lib().mt_batch_launch(self.h, stream), "mt_batch_launch")
+
+    def sync(self):
+        _chk(lib().mt_batch_sync(self.h), "mt_batch_sync")
+
+    def stats(self) -> dict:
+        s = BatchStats()
+        _chk(lib().mt_batch_get_stats(self.h, C.byref(s)), "mt_batch_get_stats")
+        return s.as_dict()
+
+    def algorithmic_bytes(self) -> float:
+        b = C.c_double(0)
+        _chk(lib().mt_batch_algorithmic_bytes(self.h, C.byref(b)), "mt_batch_algorithmic_bytes")
+        return b.value
+
+    def doc(self, i: int) -> DocView:
+        if not 0 <= i < self.n_docs:
+            raise IndexError(i)
+        return DocView(self, i)
+
+    def statuses(self) -> np.ndarray:
+        L = lib()
+        return np.array([L.mt_doc_status(self.h, i) for i in range(self.n_docs)], np.int32)
+
+    def download_log(self):
+        """(ops, doc_op_off, text, props) with batch-global offsets."""
+        L = lib()
+        n_ops, n_text, n_props = C.c_int64(), C.c_int64(), C.c_int64()
+        _chk(L.mt_batch_log_sizes(self.h, C.byref(n_ops), C.byref(n_text), C.byref(n_props)), "log sizes")
+        ops = np.zeros(n_ops.value, OP_DTYPE)
+        off = np.zeros(self.n_docs + 1, np.int64)
+        text = np.zeros(max(1, n_text.value), np.uint16)
+        props = np.zeros(max(1, n_props.value), PROP_DTYPE)
+        _chk(L.mt_batch_download_log(self.h, ops.ctypes.data, off.ctypes.data, text.ctypes.data, props.ctypes.data),
+             "mt_batch_download_log")
+        return ops, off, text[: n_text.value], props[: n_props.value]

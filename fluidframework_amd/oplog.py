@@ -1,0 +1,242 @@
+"""Pack ISequencedDocumentMessage streams into the device op-log format (include/mt_oplog.h).
+
+The reference consumes messages one at a time through ``Client.applyMsg(msg)``
+(packages/dds/merge-tree/src/client.ts:797-819).  A message is
+
+    {"clientId": str, "sequenceNumber": int, "referenceSequenceNumber": int,
+     "minimumSequenceNumber": int, "type": "op", "contents": IMergeTreeOp}
+
+(server/routerlicious/packages/protocol-definitions/src/protocol.ts:132-172) with
+IMergeTreeOp one of insert {type:0,pos1,seg}, remove {type:1,pos1,pos2},
+annotate {type:2,pos1,pos2,props,combiningOp?} or group {type:3,ops:[...]}
+(merge-tree/src/ops.ts:29-110).  This module turns a batch of such streams into
+the flat arrays that ``mt_batch_ingest`` takes: fixed 32-byte records, a UTF-16 text
+arena, interned property keys/values and per-document client tables.
+
+Short client ids are assigned per document in first-appearance order with the
+observer first, exactly as ``Client.getOrAddShortClientId`` does (client.ts:636-660).
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+
+import numpy as np
+
+OP_DTYPE = np.dtype(
+    [("type", "u1"), ("client", "u1"), ("flags", "<u2"), ("seq", "<i4"), ("ref_seq", "<i4"),
+     ("msn", "<i4"), ("pos1", "<i4"), ("pos2", "<i4"), ("payload", "<u4"), ("payload_len", "<u4")]
+)
+PROP_DTYPE = np.dtype([("key", "<u4"), ("value", "<u4")])
+assert OP_DTYPE.itemsize == 32
+
+OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 15
+OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
+MAX_INSERT_PROPS = 2047
+
+
+class UnsupportedOp(ValueError):
+    """An op shape outside the observer replay path (relative positions, registers,
+    combining ops other than "rewrite")."""
+
+
+def js_stringify(value) -> str:
+    """JSON.stringify for JSON-parsed values: integer-index keys first (ascending), then
+    insertion order; no whitespace.  Python's json keeps insertion order, so only the
+    integer-key hoisting needs doing."""
+    if isinstance(value, dict):
+        items = list(value.items())
+        idx = [(int(k), k, v) for k, v in items if _is_array_index(k)]
+        rest = [(k, v) for k, v in items if not _is_array_index(k)]
+        ordered = [(k, v) for _, k, v in sorted(idx)] + rest
+        return "{" + ",".join(json.dumps(k, ensure_ascii=False) + ":" + js_stringify(v) for k, v in ordered) + "}"
+    if isinstance(value, list):
+        return "[" + ",".join(js_stringify(v) for v in value) + "]"
+    if isinstance(value, bool) or value is None:
+        return json.dumps(value)
+    if isinstance(value, float):
+        if value != value or value in (float("inf"), float("-inf")):
+            return "null"
+        if value == int(value) and abs(value) < 1e21:
+            return str(int(value))
+        return repr(value)
+    if isinstance(value, int):
+        return str(value)
+    return json.dumps(value, ensure_ascii=False)
+
+
+def _is_array_index(k: str) -> bool:
+    if not k or len(k) > 10 or not k.isdigit() or (k[0] == "0" and len(k) > 1):
+        return False
+    return int(k) <= 4294967294
+
+
+def _utf16(s: str) -> np.ndarray:
+    return np.frombuffer(s.encode("utf-16-le"), dtype="<u2")
+
+
+def _js_keys(obj: dict) -> list:
+    """Object.keys order of a JSON-parsed object."""
+    ks = list(obj.keys())
+    idx = sorted((k for k in ks if _is_array_index(k)), key=int)
+    return idx + [k for k in ks if not _is_array_index(k)]
+
+
+@dataclass
+class PackedBatch:
+    ops: np.ndarray
+    doc_op_off: np.ndarray
+    text: np.ndarray
+    props: np.ndarray
+    keys: list
+    values: list
+    clients: list  # per-document list of long client ids (index = short id)
+
+
+@dataclass
+class Packer:
+    """Incrementally packs documents.  ``observer`` is the replica's own long id
+    (``startOrUpdateCollaboration(observer)``), short id 0 in every document."""
+
+    observer: str = "readonly"
+    keys: list = field(default_factory=list)
+    values: list = field(default_factory=lambda: ["null"])
+    _key_ids: dict = field(default_factory=dict)
+    _value_ids: dict = field(default_factory=lambda: {"null": 0})
+    _ops: list = field(default_factory=list)
+    _text: list = field(default_factory=list)
+    _text_len: int = 0
+    _props: list = field(default_factory=list)
+    _off: list = field(default_factory=lambda: [0])
+    _clients: list = field(default_factory=list)
+
+    def _key(self, k: str) -> int:
+        i = self._key_ids.get(k)
+        if i is None:
+            i = self._key_ids[k] = len(self.keys)
+            self.keys.append(k)
+        return i
+
+    def _value(self, v) -> int:
+        if v is None:
+            return 0
+        s = js_stringify(v)
+        i = self._value_ids.get(s)
+        if i is None:
+            i = self._value_ids[s] = len(self.values)
+            self.values.append(s)
+        return i
+
+    def _prop_records(self, props: dict) -> tuple[int, int]:
+        if not isinstance(props, dict):
+            raise UnsupportedOp("props must be an object")
+        off = len(self._props)
+        for k in _js_keys(props):
+            self._props.append((self._key(k), self._value(props[k])))
+        return off, len(self._props) - off
+
+    def add_document(self, messages) -> int:
+        """Append one document's message stream; returns its index."""
+        names = [self.observer]
+        short = {self.observer: 0}
+        recs = []
+        for msg in messages:
+            if isinstance(msg, str):
+                msg = json.loads(msg)
+            cid = msg["clientId"]
+            if cid not in short:  # getOrAddShortClientId (client.ts:636-641)
+                short[cid] = len(names)
+                names.append(cid)
+            c = short[cid]
+            base = dict(client=c, seq=msg["sequenceNumber"], ref_seq=msg["referenceSequenceNumber"],
+                        msn=msg["minimumSequenceNumber"])
+            if msg.get("type") != "op":
+                recs.append(dict(base, type=OP_NOOP, flags=0, pos1=0, pos2=0, payload=0, payload_len=0))
+                continue
+            if c == 0:
+                raise UnsupportedOp("ack of the observer's own op (local path)")
+            members = self._flatten(msg["contents"])
+            for j, op in enumerate(members):
+                r = self._pack_op(op, base)
+                if j + 1 < len(members):
+                    r["flags"] |= OPF_GROUP_CONT
+                recs.append(r)
+            if not members:  # empty group: updateSeqNumbers only
+                recs.append(dict(base, type=OP_NOOP, flags=0, pos1=0, pos2=0, payload=0, payload_len=0))
+        self._ops.extend(recs)
+        self._off.append(self._off[-1] + len(recs))
+        self._clients.append(names)
+        return len(self._clients) - 1
+
+    @staticmethod
+    def _flatten(op) -> list:
+        if op.get("type") == 3:
+            out = []
+            for m in op.get("ops", []):
+                out.extend(Packer._flatten(m))
+            return out
+        return [op]
+
+    def _pack_op(self, op: dict, base: dict) -> dict:
+        t = op.get("type")
+        if "pos1" not in op or op.get("relativePos1") is not None or op.get("register") is not None:
+            raise UnsupportedOp("relative positions / registers are not on the observer fast path")
+        r = dict(base, type=t, flags=0, pos1=int(op["pos1"]), pos2=0, payload=0, payload_len=0)
+        if t == 0:
+            seg = op.get("seg")
+            props = None
+            if isinstance(seg, str):
+                text = seg
+            elif isinstance(seg, dict) and "text" in seg:
+                text, props = seg["text"], seg.get("props")
+            elif isinstance(seg, dict) and "marker" in seg:
+                r["flags"] |= OPF_MARKER
+                r["payload"] = int(seg["marker"].get("refType", 0))
+                r["payload_len"] = 1
+                props = seg.get("props")
+                text = None
+            else:
+                raise UnsupportedOp("unknown segment spec")
+            if text is not None:
+                u = _utf16(text)
+                r["payload"] = self._text_len
+                r["payload_len"] = len(u)
+                self._text.append(u)
+                self._text_len += len(u)
+            if props:  # TextSegment.make: `if (props) addProperties(props)`
+                off, n = self._prop_records(props)
+                if n > MAX_INSERT_PROPS:
+                    raise UnsupportedOp("too many insert props")
+                r["flags"] |= OPF_HAS_PROPS | (n << 4)
+                r["pos2"] = off
+            elif isinstance(props, dict):  # {} is truthy: an empty map is created
+                r["flags"] |= OPF_HAS_PROPS
+                r["pos2"] = len(self._props)
+        elif t in (1, 2):
+            r["pos2"] = int(op.get("pos2", 0))
+            if t == 2:
+                cop = op.get("combiningOp")
+                if cop is not None:
+                    if cop.get("name") != "rewrite":
+                        raise UnsupportedOp("combiningOp other than rewrite")
+                    r["flags"] |= OPF_REWRITE
+                r["payload"], r["payload_len"] = self._prop_records(op.get("props") or {})
+        else:
+            raise UnsupportedOp(f"op type {t}")
+        return r
+
+    def finish(self) -> PackedBatch:
+        ops = np.zeros(len(self._ops), OP_DTYPE)
+        for name in OP_DTYPE.names:
+            ops[name] = [r[name] for r in self._ops] if self._ops else []
+        text = np.concatenate(self._text) if self._text else np.zeros(0, np.uint16)
+        props = np.array(self._props, PROP_DTYPE) if self._props else np.zeros(0, PROP_DTYPE)
+        return PackedBatch(ops=ops, doc_op_off=np.array(self._off, np.int64), text=text.astype(np.uint16),
+                           props=props, keys=list(self.keys), values=list(self.values), clients=self._clients)
+
+
+def pack_documents(docs, observer: str = "readonly") -> PackedBatch:
+    p = Packer(observer=observer)
+    for msgs in docs:
+        p.add_document(msgs)
+    return p.finish()

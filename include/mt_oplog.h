@@ -1,0 +1,84 @@
+/*
+ * mt_oplog.h — packed sequenced merge-tree op log (shared by the C-ABI library,
+ * the HIP kernels, the host layers and the test oracle).
+ *
+ * One record = one ISequencedDocumentMessage carrying one IMergeTreeDeltaOp:
+ *   message fields  : server/routerlicious/packages/protocol-definitions/src/protocol.ts:132-172
+ *                     (clientId, sequenceNumber, referenceSequenceNumber,
+ *                      minimumSequenceNumber, type "op", contents)
+ *   op contents     : packages/dds/merge-tree/src/ops.ts:29-110
+ *                     insert {type:0,pos1,seg}, remove {type:1,pos1,pos2},
+ *                     annotate {type:2,pos1,pos2,props}, group {type:3,ops:[...]}
+ *
+ * A GROUP message is encoded as consecutive records sharing seq/ref_seq/msn;
+ * every member except the last carries MT_OPF_GROUP_CONT (Client.applyRemoteOp
+ * applies the members, then Client.applyMsg runs updateSeqNumbers once:
+ * merge-tree/src/client.ts:782-790, 797-819).
+ *
+ * Strings never enter a record: text lives in a UTF-16 code-unit arena and
+ * property keys/values are interned ids (value id 0 == JSON null == delete key,
+ * merge-tree/src/properties.ts:95-116).
+ */
+#ifndef MT_OPLOG_H
+#define MT_OPLOG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mt_op_type {
+    MT_OP_INSERT = 0,   /* MergeTreeDeltaType.INSERT   */
+    MT_OP_REMOVE = 1,   /* MergeTreeDeltaType.REMOVE   */
+    MT_OP_ANNOTATE = 2, /* MergeTreeDeltaType.ANNOTATE */
+    MT_OP_NOOP = 15     /* non-"op" message: only client registration + updateSeqNumbers */
+};
+
+/* mt_op.flags: bits 0-3 public flags, bits 4-14 the prop count of an insert (<= 2047),
+   bit 15 is internal to the library (set at ingest: the insert's last code unit is '\n') */
+enum mt_op_flags {
+    MT_OPF_GROUP_CONT = 1u, /* more members of the same GROUP message follow          */
+    MT_OPF_MARKER = 2u,     /* insert of a Marker: payload = refType, payload_len = 1  */
+    MT_OPF_HAS_PROPS = 4u,  /* insert seg carries a props object (may be empty {})     */
+    MT_OPF_REWRITE = 8u     /* annotate with combiningOp {name:"rewrite"}              */
+};
+#define MT_OPF_BITS(f) ((f) & 0xFu)
+#define MT_OPF_NPROPS(f) (((uint32_t)(f) >> 4) & 0x7FFu)
+#define MT_OPF_MAKE(bits, nprops) ((uint16_t)((((nprops) & 0x7FFu) << 4) | ((bits) & 0xFu)))
+#define MT_OPF_MAX_INSERT_PROPS 2047u
+#define MT_OPF_INTERNAL_ENDS_NL 0x8000u
+
+typedef struct mt_op {
+    uint8_t type;         /* enum mt_op_type                                             */
+    uint8_t client;       /* short client id (index in the doc's client table, 1..63; 0 is
+                             the observer itself, as Client.startOrUpdateCollaboration
+                             assigns it first: client.ts:1051-1062)                       */
+    uint16_t flags;       /* enum mt_op_flags | nprops<<4                                  */
+    int32_t seq;          /* sequenceNumber                                                */
+    int32_t ref_seq;      /* referenceSequenceNumber                                       */
+    int32_t msn;          /* minimumSequenceNumber                                         */
+    int32_t pos1;         /* insert: pos; remove/annotate: start                           */
+    int32_t pos2;         /* remove/annotate: end; insert with props: prop record offset   */
+    uint32_t payload;     /* insert: text offset (code units); annotate: prop record offset;
+                             marker insert: refType                                         */
+    uint32_t payload_len; /* insert: text length; annotate: prop count                     */
+} mt_op;
+
+typedef struct mt_prop {
+    uint32_t key;   /* interned key id                       */
+    uint32_t value; /* interned value id; 0 = null (delete)  */
+} mt_prop;
+
+#define MT_VALUE_NULL 0u
+
+#ifdef __cplusplus
+static_assert(sizeof(mt_op) == 32, "mt_op is 32 bytes");
+#else
+_Static_assert(sizeof(mt_op) == 32, "mt_op is 32 bytes");
+#endif
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MT_OPLOG_H */

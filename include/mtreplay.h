@@ -1,0 +1,128 @@
+/*
+ * mtreplay.h — C ABI of libmtreplay.so, the MI355X batch replay engine for sequenced
+ * merge-tree ops (the drop-in for the reference's Client.applyMsg observer path).
+ *
+ * Boundary (reference interface each entry point replaces):
+ *   mt_batch_create/destroy     new Client(specToSegment, logger, {newMergeTreeSnapshotFormat:true})
+ *                               + startOrUpdateCollaboration("readonly") per document
+ *                               (merge-tree/src/client.ts:74-83, 1051-1071)
+ *   mt_batch_set_clients        Client.getOrAddShortClientId / getLongClientId
+ *                               (client.ts:636-652): long ids for short ids 0..n-1
+ *   mt_batch_set_tables         property keys/values as they appear in IMergeTreeAnnotateMsg.props /
+ *                               IJSONSegment.props (ops.ts:63-97); values are JSON.stringify texts
+ *   mt_batch_ingest             the ISequencedDocumentMessage streams Client.applyMsg consumes
+ *                               (client.ts:797-819; protocol.ts:132-172), packed (mt_oplog.h)
+ *   mt_batch_run / mt_batch_sync
+ *                               for each doc: for (msg of log) client.applyMsg(msg)
+ *   mt_doc_status               the exception an applyMsg would throw (mergeTree.ts:2210-2216,
+ *                               client.ts:461-464, 824-826) as a per-document code
+ *   mt_doc_text                 SharedString.getText() (sequence/src/sharedString.ts:211-214 ->
+ *                               MergeTreeTextHelper.getText, textSegment.ts:154-172)
+ *   mt_doc_props_runs           Client.getPropertiesAtPosition(pos) for every pos (client.ts:1009-1023),
+ *                               run-length encoded
+ *   mt_doc_snapshot_v1/_blob    new SnapshotV1(mergeTree, logger).extractSync(); emit()
+ *                               (merge-tree/src/snapshotV1.ts:85-247): blob path + contents
+ *   mt_doc_digest               FNV-1a-64 over the final segment table (DESIGN.md "State digest")
+ *
+ * Conventions: every call returns an int status (MT_OK = 0); output buffers are caller
+ * owned and sized by calling with cap = 0 (the required length is returned in *len).
+ * Strings are UTF-8.  No torch types cross this boundary; device memory is owned by the
+ * batch.  A batch is bound to the HIP device current at mt_batch_create.
+ */
+#ifndef MTREPLAY_H
+#define MTREPLAY_H
+
+#include <stdint.h>
+
+#include "mt_gen.h"
+#include "mt_oplog.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MT_API __attribute__((visibility("default")))
+
+enum mt_status_code {
+    MT_OK = 0,
+    MT_INVALID_POS = 1,  /* "MergeTree insert failed" */
+    MT_SEQ_ORDER = 2,    /* sequence number went backwards */
+    MT_MSN_ORDER = 3,    /* minimumSequenceNumber went backwards / above seq */
+    MT_UNSUPPORTED = 4,  /* op outside the observer path or device limits (> 32 clients) */
+    MT_BAD_INPUT = 5,
+    MT_CAPACITY = 6,     /* document exceeded the largest device capacity class */
+    MT_INTERNAL = 7,
+    MT_ERR_HIP = 100,
+    MT_ERR_ARG = 101,
+    MT_ERR_STATE = 102,
+    MT_ERR_NO_DEVICE = 103
+};
+
+typedef struct mt_batch mt_batch;
+
+typedef struct mt_batch_options {
+    int32_t chunk_size;      /* SnapshotV1 chunk size; 0 -> 10000 (snapshotV1.ts:40)              */
+    int32_t seg_cap;         /* per-doc LDS capacities; 0 -> derived from the ops per document     */
+    int32_t oe_cap;
+    int32_t blk_cap;
+    int32_t heap_cap;
+    int32_t arena_factor;    /* text arena = factor * payload + 4096 code units; 0 -> 4            */
+    int32_t pool_per_op;     /* prop pool words per annotate / props insert; 0 -> 96               */
+    int32_t max_retries;     /* capacity-class escalations for docs that overflow; 0 -> 3          */
+} mt_batch_options;
+
+typedef struct mt_batch_stats {
+    int64_t n_docs;
+    int64_t n_ops;          /* ops in the log                                                   */
+    int64_t ops_applied;    /* ops applied before a document stopped                            */
+    int64_t docs_failed;
+    int32_t max_oe, max_slots, max_blocks, max_heap; /* high-water marks over all docs         */
+    int32_t lds_bytes;      /* per-doc LDS of the first launch                                  */
+    int32_t launches;       /* replay launches incl. capacity escalations                       */
+    float kernel_ms;        /* device time of the replay launch(es) (hipEvents, batch stream)    */
+    float total_ms;         /* mt_batch_run wall time incl. escalations                         */
+} mt_batch_stats;
+
+MT_API const char *mt_status_string(int code);
+
+MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_options *opts);
+MT_API void mt_batch_destroy(mt_batch *b);
+
+MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_keys,
+                               const char *const *values_json, int32_t n_values);
+/* doc < 0: the table for every document */
+MT_API int mt_batch_set_clients(mt_batch *b, int64_t doc, const char *const *names, int32_t n);
+
+/* host arrays; ops of doc d are ops[doc_op_off[d] .. doc_op_off[d+1]); insert payload offsets
+   index `text`, annotate / insert-props offsets index `props` */
+MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_off, const uint16_t *text,
+                           int64_t n_text, const mt_prop *props, int64_t n_props);
+/* synthesize logs on the device (include/mt_gen.h); doc_first = global index of doc 0 */
+MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_first);
+
+/* launch the replay on `hip_stream` (NULL = the batch's own stream) and wait for it */
+MT_API int mt_batch_run(mt_batch *b, void *hip_stream);
+/* launch without waiting; mt_batch_sync waits and collects per-doc results */
+MT_API int mt_batch_launch(mt_batch *b, void *hip_stream);
+MT_API int mt_batch_sync(mt_batch *b);
+MT_API int mt_batch_get_stats(mt_batch *b, mt_batch_stats *out);
+/* algorithmic HBM bytes of one replay (DESIGN.md "Roofline"): ops, payloads, final table, text */
+MT_API int mt_batch_algorithmic_bytes(mt_batch *b, double *bytes);
+
+MT_API int32_t mt_doc_status(mt_batch *b, int64_t doc);
+MT_API int mt_doc_text(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
+MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
+MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs);
+MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name, int64_t name_cap, char *buf,
+                                int64_t cap, int64_t *len);
+MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out);
+MT_API int mt_doc_shape(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
+
+/* the (ingested or generated) log in host memory, batch-global offsets (CPU baseline / parity) */
+MT_API int mt_batch_log_sizes(mt_batch *b, int64_t *n_ops, int64_t *n_text, int64_t *n_props);
+MT_API int mt_batch_download_log(mt_batch *b, mt_op *ops, int64_t *doc_op_off, uint16_t *text, mt_prop *props);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1916 @@
+/*
+ * mergetree.c — CPU restatement of merge-tree observer replay (TEST INFRASTRUCTURE ONLY).
+ *
+ * Follows packages/dds/merge-tree/src (reference v0.29.0) structure-for-structure:
+ * an explicit B-tree of MergeBlocks (MaxNodesInBlock = 8, mergeTree.ts:334) whose
+ * leaves are TextSegment / Marker objects.  The one deliberate substitution:
+ * PartialSequenceLengths (partialLengths.ts) is replaced by the exact leaf sum of
+ * nodeLength() under the same (refSeq, clientId) view — the quantity the partial
+ * lengths cache (partialLengths.ts:433-487; see DESIGN.md "Block lengths").
+ *
+ * Scope: the passive-observer path (every op remote, client.ts:797-819) plus the
+ * non-collaborating local edit path that the reference's golden SnapshotV1 files
+ * were generated with (sequence/src/test/generateSharedStrings.ts:24-97).
+ */
+#include <pthread.h>
+#include <setjmp.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "jsv.h"
+#include "mt_oracle.h"
+
+/* constants.ts:11-15 */
+#define UNIVERSAL_SEQ 0
+#define UNASSIGNED_SEQ (-1)
+#define TREE_MAINT_SEQ (-2)
+#define LOCAL_CLIENT (-1)
+#define NONCOLLAB_CLIENT (-2)
+/* mergeTree.ts:334, 1059, 1061 */
+#define MAX_NODES 8
+#define TEXT_GRANULARITY 256
+#define ZAMBONI_MAX 2
+
+#define SCOUR_UNDEF (-1)
+#define SCOUR_FALSE 0
+#define SCOUR_TRUE 1
+
+enum { SEG_TEXT = 0, SEG_MARKER = 1 };
+
+typedef struct Block Block;
+
+typedef struct Node {
+    int is_leaf;
+    Block *parent;
+    int index;
+    int cached_length;
+} Node;
+
+struct Block { /* MergeBlock / HierMergeBlock, mergeTree.ts:336-420 */
+    Node n;
+    int child_count;
+    Node *children[MAX_NODES];
+    int needs_scour; /* undefined / true / false (mergeTree.ts:63, 1279, 1438) */
+    Block *all_next;
+};
+
+typedef struct Seg { /* BaseSegment, mergeTree.ts:429-573 */
+    Node n;
+    int kind;
+    u16 *text; /* TextSegment.text; length == n.cached_length */
+    int tcap;
+    int ref_type; /* Marker.refType */
+    int seq;
+    int client_id;
+    int removed; /* removedSeq !== undefined */
+    int removed_seq;
+    int removed_client;
+    int *ovl; /* removedClientOverlap, push order */
+    int novl, covl;
+    jv *props; /* properties (NULL = undefined) */
+    struct Seg *all_next;
+} Seg;
+
+typedef struct { /* LRUSegment, mergeTree.ts:918-926 */
+    Seg *seg;
+    int max_seq;
+} HeapEnt;
+
+struct mto_tables {
+    char **keys;
+    u16 **keys16;
+    int *keylen16;
+    int n_keys;
+    jv **values;
+    int n_values;
+};
+
+struct mto_doc {
+    Block *root;
+    struct {
+        int client_id, collaborating, min_seq, current_seq;
+    } cw; /* CollaborationWindow, mergeTree.ts:822-839 */
+    HeapEnt *heap; /* Heap.L, collections.ts:213-265; heap[0] is the min sentinel */
+    int hn, hcap;
+    char **long_ids; /* shortClientIdMap (client.ts:70) */
+    int n_ids, cap_ids;
+    char *long_client_id;
+    Seg *all_segs;
+    Block *all_blocks;
+    int status;
+    char err[256];
+    jmp_buf jb;
+    int jb_armed;
+    /* SnapshotV1 output */
+    char **blob_names;
+    sb *blobs;
+    int n_blobs;
+    /* packed-op client index -> short id cache */
+    int pk_map[256];
+};
+
+/* ------------------------------------------------------------------ errors */
+static void fail(mto_doc *d, int code, const char *fmt, ...) {
+    if (d->status == MTO_OK) {
+        d->status = code;
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(d->err, sizeof d->err, fmt, ap);
+        va_end(ap);
+    }
+    if (d->jb_armed) longjmp(d->jb, 1);
+}
+
+/* ------------------------------------------------------------------ alloc */
+static Block *make_block(mto_doc *d, int child_count) { /* MergeTree.makeBlock, mergeTree.ts:1114 */
+    Block *b = (Block *)calloc(1, sizeof(Block));
+    b->n.is_leaf = 0;
+    b->child_count = child_count;
+    b->needs_scour = SCOUR_UNDEF;
+    b->all_next = d->all_blocks;
+    d->all_blocks = b;
+    return b;
+}
+
+static Seg *new_seg(mto_doc *d, int kind) {
+    Seg *s = (Seg *)calloc(1, sizeof(Seg));
+    s->n.is_leaf = 1;
+    s->kind = kind;
+    s->seq = UNIVERSAL_SEQ;     /* BaseSegment.seq default, mergeTree.ts:434 */
+    s->client_id = LOCAL_CLIENT; /* BaseSegment.clientId default, mergeTree.ts:433 */
+    s->all_next = d->all_segs;
+    d->all_segs = s;
+    return s;
+}
+
+static Seg *new_text_seg(mto_doc *d, const u16 *t, int n) { /* TextSegment ctor, textSegment.ts:44-47 */
+    Seg *s = new_seg(d, SEG_TEXT);
+    s->tcap = n > 8 ? n : 8;
+    s->text = (u16 *)malloc(sizeof(u16) * (size_t)s->tcap);
+    if (n) memcpy(s->text, t, sizeof(u16) * (size_t)n);
+    s->n.cached_length = n;
+    return s;
+}
+
+static Seg *new_marker(mto_doc *d, int ref_type) { /* Marker ctor, mergeTree.ts:647-650 */
+    Seg *s = new_seg(d, SEG_MARKER);
+    s->ref_type = ref_type;
+    s->n.cached_length = 1;
+    return s;
+}
+
+static void seg_text_append(Seg *s, const u16 *t, int n) {
+    int len = s->n.cached_length;
+    if (len + n > s->tcap) {
+        int c = s->tcap ? s->tcap : 8;
+        while (c < len + n) c *= 2;
+        s->text = (u16 *)realloc(s->text, sizeof(u16) * (size_t)c);
+        s->tcap = c;
+    }
+    memcpy(s->text + len, t, sizeof(u16) * (size_t)n);
+    s->n.cached_length = len + n;
+}
+
+static void assign_child(Block *b, Node *child, int index) { /* MergeBlock.assignChild, mergeTree.ts:375 */
+    child->parent = b;
+    child->index = index;
+    b->children[index] = child;
+}
+
+/* ------------------------------------------------------------------ lengths */
+static int local_net_length(const Seg *s) { /* mergeTree.ts:1161-1172 (single branch) */
+    return s->removed ? 0 : s->n.cached_length;
+}
+
+static int node_total_length(const Node *n) { /* mergeTree.ts:422-427 */
+    return n->is_leaf ? local_net_length((const Seg *)n) : n->cached_length;
+}
+
+static void block_update(Block *b) { /* mergeTree.ts:2748-2768 (cachedLength part) */
+    int len = 0;
+    for (int i = 0; i < b->child_count; i++) len += node_total_length(b->children[i]);
+    b->n.cached_length = len;
+}
+
+static int seg_has_overlap(const Seg *s, int client) {
+    for (int i = 0; i < s->novl; i++)
+        if (s->ovl[i] == client) return 1;
+    return 0;
+}
+
+static int node_length(mto_doc *d, Node *node, int ref_seq, int client_id);
+
+/* PartialSequenceLengths.getPartialLength substitute: exact leaf sum of nodeLength */
+static int block_partial_length(mto_doc *d, Block *b, int ref_seq, int client_id) {
+    int len = 0;
+    for (int i = 0; i < b->child_count; i++) len += node_length(d, b->children[i], ref_seq, client_id);
+    return len;
+}
+
+static int node_length(mto_doc *d, Node *node, int ref_seq, int client_id) { /* mergeTree.ts:1659-1699 */
+    if (!d->cw.collaborating || d->cw.client_id == client_id) {
+        if (!node->is_leaf) return node->cached_length;
+        return local_net_length((Seg *)node);
+    }
+    if (!node->is_leaf) return block_partial_length(d, (Block *)node, ref_seq, client_id);
+    Seg *s = (Seg *)node;
+    if (s->client_id == client_id || (s->seq != UNASSIGNED_SEQ && s->seq <= ref_seq)) {
+        if (s->removed) {
+            if (s->removed_client == client_id || seg_has_overlap(s, client_id) ||
+                (s->removed_seq != UNASSIGNED_SEQ && s->removed_seq <= ref_seq))
+                return 0;
+            return s->n.cached_length;
+        }
+        return s->n.cached_length;
+    }
+    return 0;
+}
+
+static int block_length(mto_doc *d, Block *b, int ref_seq, int client_id) { /* mergeTree.ts:1636-1642 */
+    if (d->cw.collaborating && client_id != d->cw.client_id) return block_partial_length(d, b, ref_seq, client_id);
+    return b->n.cached_length;
+}
+
+/* blockUpdateLength / nodeUpdateLengthNewStructure / blockUpdatePathLengths
+   (mergeTree.ts:2721, 2770, 2781): with partial lengths substituted, only the
+   local-view cachedLength needs maintenance. */
+static void block_update_length(Block *b) { block_update(b); }
+static void node_update_length_new_structure(Block *b) { block_update(b); }
+static void block_update_path_lengths(Block *b) {
+    while (b) {
+        node_update_length_new_structure(b);
+        b = b->n.parent;
+    }
+}
+
+/* ------------------------------------------------------------------ heap (collections.ts:213-265) */
+static int heap_count(mto_doc *d) { return d->hn - 1; }
+static void heap_push_raw(mto_doc *d, HeapEnt e) {
+    if (d->hn == d->hcap) {
+        d->hcap = d->hcap ? d->hcap * 2 : 64;
+        d->heap = (HeapEnt *)realloc(d->heap, sizeof(HeapEnt) * (size_t)d->hcap);
+    }
+    d->heap[d->hn++] = e;
+}
+static void heap_init(mto_doc *d) {
+    d->hn = 0;
+    HeapEnt min = {NULL, -2}; /* LRUSegmentComparer.min = { maxSeq: -2 } */
+    heap_push_raw(d, min);
+}
+static int heap_cmp(const HeapEnt *a, const HeapEnt *b) { return a->max_seq - b->max_seq; }
+static void heap_fixup(mto_doc *d, int k) {
+    while (k > 1 && heap_cmp(&d->heap[k >> 1], &d->heap[k]) > 0) {
+        HeapEnt t = d->heap[k >> 1];
+        d->heap[k >> 1] = d->heap[k];
+        d->heap[k] = t;
+        k >>= 1;
+    }
+}
+static void heap_fixdown(mto_doc *d, int k) {
+    while ((k << 1) <= heap_count(d)) {
+        int j = k << 1;
+        if (j < heap_count(d) && heap_cmp(&d->heap[j], &d->heap[j + 1]) > 0) j++;
+        if (heap_cmp(&d->heap[k], &d->heap[j]) <= 0) break;
+        HeapEnt t = d->heap[k];
+        d->heap[k] = d->heap[j];
+        d->heap[j] = t;
+        k = j;
+    }
+}
+static void heap_add(mto_doc *d, Seg *s, int max_seq) {
+    HeapEnt e = {s, max_seq};
+    heap_push_raw(d, e);
+    heap_fixup(d, heap_count(d));
+}
+static HeapEnt *heap_peek(mto_doc *d) { return heap_count(d) >= 1 ? &d->heap[1] : NULL; }
+static HeapEnt heap_get(mto_doc *d) {
+    HeapEnt x = d->heap[1];
+    d->heap[1] = d->heap[heap_count(d)];
+    d->hn--;
+    heap_fixdown(d, 1);
+    return x;
+}
+
+/* ------------------------------------------------------------------ properties */
+/* SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111) for
+   seq !== UnassignedSequenceNumber and no pending local state; combiningOp limited to
+   undefined / {name:"rewrite"} (other combining ops: MTO_UNSUPPORTED). */
+static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewrite) {
+    if (!s->props) s->props = jv_new(JV_OBJ);
+    if (!new_props || new_props->kind != JV_OBJ) fail(d, MTO_BAD_INPUT, "props is not an object");
+    if (rewrite) {
+        int *ord = (int *)malloc(sizeof(int) * (size_t)(s->props->n + 1));
+        int n = jv_obj_enum(s->props, ord);
+        /* collect keys first: deleting while enumerating */
+        u16 **ks = (u16 **)malloc(sizeof(u16 *) * (size_t)(n + 1));
+        int *kl = (int *)malloc(sizeof(int) * (size_t)(n + 1));
+        int m = 0;
+        for (int i = 0; i < n; i++) {
+            const jv *nv = jv_obj_get(new_props, s->props->keys[ord[i]], s->props->klens[ord[i]]);
+            int truthy = nv && !(nv->kind == JV_NULL || nv->kind == JV_FALSE || nv->kind == JV_UNDEF ||
+                                 (nv->kind == JV_NUM && (nv->num == 0 || nv->num != nv->num)) ||
+                                 (nv->kind == JV_STR && nv->slen == 0));
+            if (!truthy) {
+                ks[m] = (u16 *)malloc(sizeof(u16) * (size_t)(s->props->klens[ord[i]] + 1));
+                memcpy(ks[m], s->props->keys[ord[i]], sizeof(u16) * (size_t)s->props->klens[ord[i]]);
+                kl[m++] = s->props->klens[ord[i]];
+            }
+        }
+        for (int i = 0; i < m; i++) {
+            jv_obj_del(s->props, ks[i], kl[i]);
+            free(ks[i]);
+        }
+        free(ks);
+        free(kl);
+        free(ord);
+    }
+    int *ord = (int *)malloc(sizeof(int) * (size_t)(new_props->n + 1));
+    int n = jv_obj_enum(new_props, ord);
+    for (int i = 0; i < n; i++) {
+        const u16 *k = new_props->keys[ord[i]];
+        int kl = new_props->klens[ord[i]];
+        jv *v = new_props->vals[ord[i]];
+        if (v->kind == JV_NULL) jv_obj_del(s->props, k, kl);
+        else jv_obj_set(s->props, k, kl, jv_ref(v));
+    }
+    free(ord);
+}
+
+/* TextSegment.make(text, props) / Marker.make: `if (props) addProperties(props)` */
+static void seg_init_props(mto_doc *d, Seg *s, const jv *props) {
+    if (!props || props->kind == JV_NULL) return;
+    if (props->kind == JV_FALSE || (props->kind == JV_NUM && props->num == 0) ||
+        (props->kind == JV_STR && props->slen == 0))
+        return;
+    seg_add_properties(d, s, props, 0);
+}
+
+/* ------------------------------------------------------------------ split / append */
+/* BaseSegment.splitAt (mergeTree.ts:524-568) + TextSegment.createSplitSegmentAt
+   (textSegment.ts:103-111); Marker.createSplitSegmentAt returns undefined. */
+static Seg *seg_split_at(mto_doc *d, Seg *s, int pos) {
+    if (!(pos > 0)) return NULL;
+    if (s->kind != SEG_TEXT) return NULL;
+    int len = s->n.cached_length;
+    Seg *leaf = new_text_seg(d, s->text + pos, len - pos);
+    s->n.cached_length = pos;
+    if (s->props) leaf->props = jv_obj_clone(s->props); /* propertyManager.copyTo */
+    leaf->n.parent = s->n.parent;
+    leaf->removed_client = s->removed_client;
+    leaf->removed_seq = s->removed_seq;
+    leaf->removed = s->removed;
+    leaf->seq = s->seq;
+    leaf->client_id = s->client_id;
+    if (s->novl) {
+        leaf->ovl = (int *)malloc(sizeof(int) * (size_t)s->novl);
+        memcpy(leaf->ovl, s->ovl, sizeof(int) * (size_t)s->novl);
+        leaf->novl = leaf->covl = s->novl;
+    }
+    return leaf;
+}
+
+/* TextSegment.canAppend (textSegment.ts:63-68); Marker.canAppend is false */
+static int seg_can_append(const Seg *prev, const Seg *seg) {
+    if (prev->kind != SEG_TEXT) return 0;
+    int len = prev->n.cached_length;
+    if (len > 0 && prev->text[len - 1] == '\n') return 0;
+    if (seg->kind != SEG_TEXT) return 0;
+    return prev->n.cached_length <= TEXT_GRANULARITY || seg->n.cached_length <= TEXT_GRANULARITY;
+}
+
+/* ------------------------------------------------------------------ tree structure */
+static Block *split_block(mto_doc *d, Block *node) { /* MergeTree.split, mergeTree.ts:2476-2489 */
+    int half = MAX_NODES / 2;
+    Block *nn = make_block(d, half);
+    node->child_count = half;
+    for (int i = 0; i < half; i++) {
+        assign_child(nn, node->children[half + i], i);
+        node->children[half + i] = NULL;
+    }
+    node_update_length_new_structure(node);
+    node_update_length_new_structure(nn);
+    return nn;
+}
+
+static void update_root(mto_doc *d, Block *split_node) { /* mergeTree.ts:1876-1887 */
+    if (split_node) {
+        Block *nr = make_block(d, 2);
+        nr->n.index = 0;
+        assign_child(nr, &d->root->n, 0);
+        assign_child(nr, &split_node->n, 1);
+        d->root = nr;
+        node_update_length_new_structure(d->root);
+    }
+}
+
+/* ------------------------------------------------------------------ nodeMap (mergeTree.ts:2903-2965) */
+typedef struct MapActions {
+    int (*leaf)(mto_doc *d, Seg *s, int pos, int ref_seq, int client_id, int start, int end, void *ctx);
+    int (*post)(mto_doc *d, Block *b, void *ctx);
+    void *ctx;
+} MapActions;
+
+static int node_map(mto_doc *d, Block *node, MapActions *a, int pos, int ref_seq, int client_id, int start,
+                    int end, int has_end) {
+    if (!has_end) end = block_length(d, node, ref_seq, client_id);
+    int go = 1;
+    for (int ci = 0; ci < node->child_count; ci++) {
+        Node *child = node->children[ci];
+        int len = node_length(d, child, ref_seq, client_id);
+        if (go && end > 0 && len > 0 && start < len) {
+            if (!child->is_leaf) go = node_map(d, (Block *)child, a, pos, ref_seq, client_id, start, end, 1);
+            else go = a->leaf(d, (Seg *)child, pos, ref_seq, client_id, start, end, a->ctx);
+        }
+        if (!go) break;
+        pos += len;
+        start -= len;
+        end -= len;
+    }
+    if (go && a->post) go = a->post(d, node, a->ctx);
+    return go;
+}
+
+/* rightExcursion (mergeTree.ts:2313-2343) used by blockInsert.continueFrom (2154-2161) */
+static int check_seg_is_local(mto_doc *d, Seg *s, int pos, int r, int c, int st, int en, void *ctx) {
+    (void)d; (void)pos; (void)r; (void)c; (void)st; (void)en;
+    if (s->seq == UNASSIGNED_SEQ) *(int *)ctx = 1;
+    return 0;
+}
+static int continue_from(mto_doc *d, Block *node) {
+    int seg_is_local = 0;
+    MapActions a = {check_seg_is_local, NULL, &seg_is_local};
+    Node *start = &node->n;
+    Block *parent = start->parent;
+    while (parent) {
+        int matched = 0;
+        for (int ci = 0; ci < parent->child_count; ci++) {
+            Node *c = parent->children[ci];
+            if (matched) {
+                int go;
+                if (!c->is_leaf) go = node_map(d, (Block *)c, &a, 0, UNIVERSAL_SEQ, d->cw.client_id, 0, 0, 0);
+                else go = check_seg_is_local(d, (Seg *)c, 0, UNIVERSAL_SEQ, d->cw.client_id, 0, 0, &seg_is_local);
+                if (!go) return seg_is_local;
+            } else {
+                matched = (start == c);
+            }
+        }
+        start = &parent->n;
+        parent = parent->n.parent;
+    }
+    return seg_is_local;
+}
+
+/* ------------------------------------------------------------------ insertingWalk (mergeTree.ts:2345-2474) */
+enum { LEAF_SPLIT = 0, LEAF_INSERT = 1 };
+typedef struct {
+    int kind;
+    Seg *candidate;
+    int has_continue;
+} ICtx;
+
+static Block UNFINISHED_NODE; /* MergeTree.theUnfinishedNode */
+
+/* breakTie, mergeTree.ts:2248-2277 */
+static int break_tie(mto_doc *d, int pos, Node *node, int ref_seq, int client_id) {
+    if (node->is_leaf) {
+        if (pos == 0) {
+            Seg *s = (Seg *)node;
+            if (s->removed && s->removed_seq != 0 && s->removed_seq <= ref_seq && s->removed_seq != UNASSIGNED_SEQ)
+                return 0;
+            if (client_id == d->cw.client_id) return 1;
+            if (s->seq != UNASSIGNED_SEQ) return 1;
+        }
+        return 0;
+    }
+    return 1;
+}
+
+static Block *inserting_walk(mto_doc *d, Block *block, int pos, int ref_seq, int client_id, int seq, ICtx *ctx) {
+    int ci;
+    Node *new_node = NULL;
+    Block *from_split = NULL;
+    (void)from_split;
+    for (ci = 0; ci < block->child_count; ci++) {
+        Node *child = block->children[ci];
+        int len = node_length(d, child, ref_seq, client_id);
+        if (pos < len || (pos == len && break_tie(d, pos, child, ref_seq, client_id))) {
+            if (!child->is_leaf) {
+                Block *split_node = inserting_walk(d, (Block *)child, pos, ref_seq, client_id, seq, ctx);
+                if (split_node == NULL) {
+                    block_update_length(block);
+                    return NULL;
+                } else if (split_node == &UNFINISHED_NODE) {
+                    pos -= len;
+                    continue;
+                } else {
+                    new_node = &split_node->n;
+                    from_split = split_node;
+                    ci++;
+                }
+            } else {
+                Seg *seg = (Seg *)child;
+                /* context.leaf: splitLeafSegment (2225) or blockInsert.onLeaf (2180) */
+                Node *next = NULL;
+                if (ctx->kind == LEAF_SPLIT) {
+                    Seg *n2 = seg_split_at(d, seg, pos);
+                    next = n2 ? &n2->n : NULL;
+                } else {
+                    assign_child(block, &ctx->candidate->n, ci); /* replaceCurrent */
+                    next = &seg->n;
+                }
+                if (next) {
+                    new_node = next;
+                    ci++;
+                } else {
+                    return NULL;
+                }
+            }
+            break;
+        } else {
+            pos -= len;
+        }
+    }
+    if (!new_node) {
+        if (pos == 0) {
+            if (seq != UNASSIGNED_SEQ && ctx->has_continue && continue_from(d, block)) return &UNFINISHED_NODE;
+            if (ctx->kind == LEAF_INSERT) new_node = &ctx->candidate->n;
+        }
+    }
+    if (new_node) {
+        for (int i = block->child_count; i > ci; i--) {
+            block->children[i] = block->children[i - 1];
+            block->children[i]->index = i;
+        }
+        assign_child(block, new_node, ci);
+        block->child_count++;
+        if (block->child_count < MAX_NODES) {
+            block_update_length(block);
+            return NULL;
+        }
+        return split_block(d, block);
+    }
+    return NULL;
+}
+
+/* ensureIntervalBoundary, mergeTree.ts:2241-2245 */
+static void ensure_interval_boundary(mto_doc *d, int pos, int ref_seq, int client_id) {
+    ICtx ctx = {LEAF_SPLIT, NULL, 0};
+    Block *sn = inserting_walk(d, d->root, pos, ref_seq, client_id, TREE_MAINT_SEQ, &ctx);
+    update_root(d, sn);
+}
+
+/* addToLRUSet, mergeTree.ts:1273-1283 */
+static void add_to_lru_set(mto_doc *d, Seg *s, int seq) {
+    if (s->n.parent->needs_scour != SCOUR_TRUE && seq > d->cw.current_seq) {
+        s->n.parent->needs_scour = SCOUR_TRUE;
+        heap_add(d, s, seq);
+    }
+}
+
+/* ------------------------------------------------------------------ zamboni */
+typedef struct {
+    Node **p;
+    int n, cap;
+} NodeVec;
+static void nv_push(NodeVec *v, Node *x) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 16;
+        v->p = (Node **)realloc(v->p, sizeof(Node *) * (size_t)v->cap);
+    }
+    v->p[v->n++] = x;
+}
+
+/* scourNode, mergeTree.ts:1289-1365 (segmentGroups / trackingCollection are empty on this path) */
+static void scour_node(mto_doc *d, Block *node, NodeVec *hold) {
+    Seg *prev = NULL;
+    for (int k = 0; k < node->child_count; k++) {
+        Node *child = node->children[k];
+        if (child->is_leaf) {
+            Seg *s = (Seg *)child;
+            if (s->removed) {
+                if (s->removed_seq > d->cw.min_seq) {
+                    nv_push(hold, child);
+                } else {
+                    s->n.parent = NULL; /* unlink */
+                }
+                prev = NULL;
+            } else {
+                if (s->seq <= d->cw.min_seq) {
+                    int can_append = prev && seg_can_append(prev, s) && jv_match_properties(prev->props, s->props) &&
+                                     local_net_length(s) > 0;
+                    if (can_append) {
+                        seg_text_append(prev, s->text, s->n.cached_length); /* TextSegment.append */
+                        s->n.parent = NULL;
+                    } else {
+                        nv_push(hold, child);
+                        prev = local_net_length(s) > 0 ? s : NULL;
+                    }
+                } else {
+                    nv_push(hold, child);
+                    prev = NULL;
+                }
+            }
+        } else {
+            nv_push(hold, child);
+            prev = NULL;
+        }
+    }
+}
+
+static int underflow(const Block *b) { return b->child_count < MAX_NODES / 2; } /* mergeTree.ts:1285 */
+
+/* pack, mergeTree.ts:1368-1420 */
+static void pack(mto_doc *d, Block *block) {
+    Block *parent = block->n.parent;
+    NodeVec hold = {0, 0, 0};
+    for (int ci = 0; ci < parent->child_count; ci++) {
+        Block *cb = (Block *)parent->children[ci];
+        scour_node(d, cb, &hold);
+        cb->n.parent = NULL;
+    }
+    int total = hold.n;
+    int half = MAX_NODES / 2;
+    int child_count = total / half;
+    if (child_count > MAX_NODES - 1) child_count = MAX_NODES - 1;
+    if (child_count < 1) child_count = 1;
+    int base = total / child_count;
+    int extra = total % child_count;
+    Block *packed[MAX_NODES];
+    int read = 0;
+    for (int ni = 0; ni < child_count; ni++) {
+        int cnt = base;
+        if (extra > 0) {
+            cnt++;
+            extra--;
+        }
+        Block *pb = make_block(d, cnt);
+        for (int j = 0; j < cnt; j++) assign_child(pb, hold.p[read++], j);
+        pb->n.parent = parent;
+        packed[ni] = pb;
+        node_update_length_new_structure(pb);
+    }
+    free(hold.p);
+    for (int j = 0; j < MAX_NODES; j++) parent->children[j] = NULL;
+    for (int j = 0; j < child_count; j++) assign_child(parent, &packed[j]->n, j);
+    parent->child_count = child_count;
+    if (underflow(parent) && parent->n.parent) {
+        pack(d, parent);
+    } else {
+        block_update_path_lengths(parent);
+    }
+}
+
+/* zamboniSegments, mergeTree.ts:1422-1478 */
+static void zamboni_segments(mto_doc *d) {
+    if (!d->cw.collaborating) return;
+    for (int i = 0; i < ZAMBONI_MAX; i++) {
+        HeapEnt *top = heap_peek(d);
+        if (!top || top->max_seq > d->cw.min_seq) break;
+        HeapEnt e = heap_get(d);
+        if (e.seg->n.parent && e.seg->n.parent->needs_scour != SCOUR_FALSE) {
+            Block *block = e.seg->n.parent;
+            NodeVec copy = {0, 0, 0};
+            scour_node(d, block, &copy);
+            block->needs_scour = SCOUR_FALSE;
+            int nc = copy.n;
+            if (nc < block->child_count) {
+                block->child_count = nc;
+                for (int j = 0; j < MAX_NODES; j++) block->children[j] = NULL;
+                for (int j = 0; j < nc; j++) assign_child(block, copy.p[j], j);
+                if (underflow(block) && block->n.parent) {
+                    pack(d, block);
+                } else {
+                    block_update_path_lengths(block);
+                }
+            }
+            free(copy.p);
+        }
+    }
+}
+
+/* setMinSeq, mergeTree.ts:1718-1736 */
+static void set_min_seq(mto_doc *d, int min_seq) {
+    if (!(min_seq <= d->cw.current_seq)) fail(d, MTO_MSN_ORDER, "minSeq %d > currentSeq %d", min_seq, d->cw.current_seq);
+    if (!(d->cw.min_seq <= min_seq)) fail(d, MTO_MSN_ORDER, "minSeq moved backwards %d -> %d", d->cw.min_seq, min_seq);
+    if (min_seq > d->cw.min_seq) {
+        d->cw.min_seq = min_seq;
+        zamboni_segments(d);
+    }
+}
+
+/* ------------------------------------------------------------------ edits */
+/* insertSegments (mergeTree.ts:1968-1998) + blockInsert (2141-2224), one segment */
+static void insert_segment(mto_doc *d, int pos, Seg *seg, int ref_seq, int client_id, int seq) {
+    ensure_interval_boundary(d, pos, ref_seq, client_id);
+    if (seg && seg->n.cached_length > 0) {
+        seg->seq = seq;
+        seg->client_id = client_id;
+        ICtx ctx = {LEAF_INSERT, seg, 1};
+        Block *sn = inserting_walk(d, d->root, pos, ref_seq, client_id, seq, &ctx);
+        if (seg->n.parent == NULL)
+            fail(d, MTO_INVALID_POS, "MergeTree insert failed: {\"currentSeq\":%d,\"minSeq\":%d,\"segSeq\":%d}",
+                 d->cw.current_seq, d->cw.min_seq, seg->seq);
+        update_root(d, sn);
+        /* saveIfLocal (2164-2179) */
+        if (d->cw.collaborating) {
+            if (seg->seq == UNASSIGNED_SEQ && client_id == d->cw.client_id) {
+                fail(d, MTO_UNSUPPORTED, "pending local segment");
+            } else if (seg->seq > d->cw.min_seq) {
+                add_to_lru_set(d, seg, seg->seq);
+            }
+        }
+    }
+    if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
+}
+
+typedef struct {
+    int seq;
+    int client_id;
+    int overwrite;
+} RemoveCtx;
+
+/* markRangeRemoved.markRemoved (mergeTree.ts:2614-2660), single branch */
+static int mark_removed(mto_doc *d, Seg *s, int pos, int r, int c, int st, int en, void *vctx) {
+    (void)pos; (void)r; (void)c; (void)st; (void)en;
+    RemoveCtx *ctx = (RemoveCtx *)vctx;
+    if (s->removed) {
+        ctx->overwrite = 1;
+        if (s->removed_seq == UNASSIGNED_SEQ) {
+            fail(d, MTO_UNSUPPORTED, "pending local remove");
+        } else {
+            if (s->novl == s->covl) {
+                s->covl = s->covl ? s->covl * 2 : 4;
+                s->ovl = (int *)realloc(s->ovl, sizeof(int) * (size_t)s->covl);
+            }
+            s->ovl[s->novl++] = ctx->client_id; /* addOverlappingClient, 2544-2552 */
+        }
+    } else {
+        s->removed_client = ctx->client_id;
+        s->removed_seq = ctx->seq;
+        s->removed = 1;
+    }
+    if (d->cw.collaborating) {
+        if (s->removed_seq == UNASSIGNED_SEQ && ctx->client_id == d->cw.client_id) {
+            fail(d, MTO_UNSUPPORTED, "pending local remove");
+        } else {
+            add_to_lru_set(d, s, ctx->seq);
+        }
+    }
+    return 1;
+}
+static int after_mark_removed(mto_doc *d, Block *b, void *ctx) {
+    (void)d; (void)ctx;
+    block_update_length(b); /* or nodeUpdateLengthNewStructure: same cachedLength */
+    return 1;
+}
+
+static void mark_range_removed(mto_doc *d, int start, int end, int ref_seq, int client_id, int seq) {
+    ensure_interval_boundary(d, start, ref_seq, client_id);
+    ensure_interval_boundary(d, end, ref_seq, client_id);
+    RemoveCtx ctx = {seq, client_id, 0};
+    MapActions a = {mark_removed, after_mark_removed, &ctx};
+    node_map(d, d->root, &a, 0, ref_seq, client_id, start, end, 1);
+    if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
+}
+
+typedef struct {
+    const jv *props;
+    int rewrite;
+    int seq;
+} AnnotateCtx;
+
+static int annotate_segment(mto_doc *d, Seg *s, int pos, int r, int c, int st, int en, void *vctx) {
+    (void)pos; (void)r; (void)c; (void)st; (void)en;
+    AnnotateCtx *ctx = (AnnotateCtx *)vctx;
+    seg_add_properties(d, s, ctx->props, ctx->rewrite);
+    if (d->cw.collaborating) {
+        if (ctx->seq == UNASSIGNED_SEQ) fail(d, MTO_UNSUPPORTED, "pending local annotate");
+        else add_to_lru_set(d, s, ctx->seq);
+    }
+    return 1;
+}
+
+/* annotateRange, mergeTree.ts:2565-2605 */
+static void annotate_range(mto_doc *d, int start, int end, const jv *props, int rewrite, int ref_seq, int client_id,
+                           int seq) {
+    ensure_interval_boundary(d, start, ref_seq, client_id);
+    ensure_interval_boundary(d, end, ref_seq, client_id);
+    AnnotateCtx ctx = {props, rewrite, seq};
+    MapActions a = {annotate_segment, NULL, &ctx};
+    node_map(d, d->root, &a, 0, ref_seq, client_id, start, end, 1);
+    if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
+}
+
+/* ------------------------------------------------------------------ client */
+static int get_short_client_id(mto_doc *d, const char *long_id) {
+    for (int i = 0; i < d->n_ids; i++)
+        if (!strcmp(d->long_ids[i], long_id)) return i;
+    return -1;
+}
+static int add_long_client_id(mto_doc *d, const char *long_id) { /* client.ts:653-660 */
+    if (d->n_ids == d->cap_ids) {
+        d->cap_ids = d->cap_ids ? d->cap_ids * 2 : 16;
+        d->long_ids = (char **)realloc(d->long_ids, sizeof(char *) * (size_t)d->cap_ids);
+    }
+    d->long_ids[d->n_ids] = strdup(long_id);
+    return d->n_ids++;
+}
+static int get_or_add_short_client_id(mto_doc *d, const char *long_id) { /* client.ts:636-641 */
+    int id = get_short_client_id(d, long_id);
+    return id >= 0 ? id : add_long_client_id(d, long_id);
+}
+static const char *get_long_client_id(mto_doc *d, int short_id) { /* client.ts:645-652 */
+    if (short_id >= 0) return short_id < d->n_ids ? d->long_ids[short_id] : "undefined";
+    return "original";
+}
+
+mto_doc *mto_new(void) {
+    mto_doc *d = (mto_doc *)calloc(1, sizeof(mto_doc));
+    d->root = make_block(d, 0); /* initialNode, mergeTree.ts:1125-1129 */
+    d->root->n.cached_length = 0;
+    d->cw.client_id = LOCAL_CLIENT;
+    heap_init(d);
+    for (int i = 0; i < 256; i++) d->pk_map[i] = -1;
+    return d;
+}
+
+static void free_blobs(mto_doc *d) {
+    for (int i = 0; i < d->n_blobs; i++) {
+        free(d->blob_names[i]);
+        sb_free(&d->blobs[i]);
+    }
+    free(d->blob_names);
+    free(d->blobs);
+    d->blob_names = NULL;
+    d->blobs = NULL;
+    d->n_blobs = 0;
+}
+
+void mto_free(mto_doc *d) {
+    if (!d) return;
+    for (Seg *s = d->all_segs; s;) {
+        Seg *n = s->all_next;
+        free(s->text);
+        free(s->ovl);
+        jv_unref(s->props);
+        free(s);
+        s = n;
+    }
+    for (Block *b = d->all_blocks; b;) {
+        Block *n = b->all_next;
+        free(b);
+        b = n;
+    }
+    for (int i = 0; i < d->n_ids; i++) free(d->long_ids[i]);
+    free(d->long_ids);
+    free(d->long_client_id);
+    free(d->heap);
+    free_blobs(d);
+    free(d);
+}
+
+int mto_status(const mto_doc *d) { return d->status; }
+const char *mto_error(const mto_doc *d) { return d->err; }
+
+#define GUARD(d)                                       \
+    if ((d)->status != MTO_OK) return (d)->status;     \
+    (d)->jb_armed = 1;                                 \
+    if (setjmp((d)->jb)) {                             \
+        (d)->jb_armed = 0;                             \
+        return (d)->status;                            \
+    }
+#define UNGUARD(d) ((d)->jb_armed = 0)
+
+/* Client.startOrUpdateCollaboration (client.ts:1051-1071) → MergeTree.startCollaboration (1254-1271) */
+int mto_start_collab(mto_doc *d, const char *long_id, int min_seq, int cur_seq) {
+    GUARD(d);
+    if (d->long_client_id == NULL) {
+        d->long_client_id = strdup(long_id);
+        int sid = add_long_client_id(d, long_id);
+        d->cw.client_id = sid;
+        d->cw.min_seq = min_seq;
+        d->cw.collaborating = 1;
+        d->cw.current_seq = cur_seq;
+        heap_init(d);
+    } else {
+        int sid = get_short_client_id(d, d->long_client_id);
+        free(d->long_ids[sid]);
+        d->long_ids[sid] = strdup(long_id);
+        free(d->long_client_id);
+        d->long_client_id = strdup(long_id);
+    }
+    UNGUARD(d);
+    return d->status;
+}
+
+/* completeAndLogOp asserts for remote ops (client.ts:461-464) */
+static void complete_remote_op(mto_doc *d, int seq, int msn) {
+    if (!(d->cw.current_seq < seq)) fail(d, MTO_SEQ_ORDER, "Incoming remote op sequence# <= local collabWindow's currentSequence#");
+    if (!(d->cw.min_seq <= msn)) fail(d, MTO_MSN_ORDER, "Incoming remote op minSequence# < local collabWindow's minSequence#");
+}
+
+/* Client.updateSeqNumbers (client.ts:821-828) */
+static void update_seq_numbers(mto_doc *d, int min, int seq) {
+    if (!(d->cw.current_seq <= seq)) fail(d, MTO_SEQ_ORDER, "Incoming op sequence# < local collabWindow's currentSequence#");
+    d->cw.current_seq = seq;
+    if (!(min <= seq)) fail(d, MTO_MSN_ORDER, "Incoming op sequence# < minSequence#");
+    set_min_seq(d, min);
+}
+
+static int jv_int(const jv *v, int *out) {
+    if (!v || v->kind != JV_NUM) return 0;
+    *out = (int)v->num;
+    return 1;
+}
+
+/* specToSegment (sequence/src/sequenceFactory.ts:31-37): TextSegment.fromJSONObject
+   (textSegment.ts:30-39) then Marker.fromJSONObject (mergeTree.ts:658-665) */
+static Seg *spec_to_segment(mto_doc *d, const jv *spec) {
+    if (spec && spec->kind == JV_STR) return new_text_seg(d, spec->s, spec->slen);
+    if (spec && spec->kind == JV_OBJ) {
+        const jv *t = jv_obj_get_ascii(spec, "text");
+        if (t) {
+            if (t->kind != JV_STR) fail(d, MTO_BAD_INPUT, "text is not a string");
+            Seg *s = new_text_seg(d, t->s, t->slen);
+            seg_init_props(d, s, jv_obj_get_ascii(spec, "props"));
+            return s;
+        }
+        const jv *m = jv_obj_get_ascii(spec, "marker");
+        if (m) {
+            int rt = 0;
+            if (m->kind == JV_OBJ) jv_int(jv_obj_get_ascii(m, "refType"), &rt);
+            Seg *s = new_marker(d, rt);
+            seg_init_props(d, s, jv_obj_get_ascii(spec, "props"));
+            return s;
+        }
+    }
+    fail(d, MTO_BAD_INPUT, "unrecognized segment spec");
+    return NULL;
+}
+
+/* Client.applyRemoteOp (client.ts:768-795) */
+static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int ref_seq, int msn) {
+    int type = -1;
+    if (!op || op->kind != JV_OBJ || !jv_int(jv_obj_get_ascii(op, "type"), &type)) fail(d, MTO_BAD_INPUT, "bad op");
+    int pos1 = 0, pos2 = 0;
+    int has1 = jv_int(jv_obj_get_ascii(op, "pos1"), &pos1);
+    int has2 = jv_int(jv_obj_get_ascii(op, "pos2"), &pos2);
+    if (type != 3 && !has1) fail(d, MTO_UNSUPPORTED, "relative positions are not supported");
+    switch (type) {
+        case 0: { /* applyInsertOp, client.ts:393-441 */
+            const jv *segspec = jv_obj_get_ascii(op, "seg");
+            if (!segspec) fail(d, MTO_UNSUPPORTED, "register insert");
+            Seg *s = spec_to_segment(d, segspec);
+            insert_segment(d, pos1, s, ref_seq, short_id, seq);
+            complete_remote_op(d, seq, msn);
+            break;
+        }
+        case 1: /* applyRemoveRangeOp, client.ts:320-351 */
+            if (jv_obj_get_ascii(op, "register")) fail(d, MTO_UNSUPPORTED, "register remove");
+            if (!has2) pos2 = 0; /* undefined end: nodeMap never matches (end > 0 fails) */
+            mark_range_removed(d, pos1, pos2, ref_seq, short_id, seq);
+            complete_remote_op(d, seq, msn);
+            break;
+        case 2: { /* applyAnnotateRangeOp, client.ts:358-386 */
+            const jv *props = jv_obj_get_ascii(op, "props");
+            const jv *cop = jv_obj_get_ascii(op, "combiningOp");
+            int rewrite = 0;
+            if (cop && cop->kind == JV_OBJ) {
+                const jv *nm = jv_obj_get_ascii(cop, "name");
+                static const u16 RW[7] = {'r', 'e', 'w', 'r', 'i', 't', 'e'};
+                if (nm && nm->kind == JV_STR && u16_eq(nm->s, nm->slen, RW, 7)) rewrite = 1;
+                else fail(d, MTO_UNSUPPORTED, "combiningOp other than rewrite");
+            }
+            if (!has2) pos2 = 0;
+            annotate_range(d, pos1, pos2, props, rewrite, ref_seq, short_id, seq);
+            complete_remote_op(d, seq, msn);
+            break;
+        }
+        case 3: { /* GROUP */
+            const jv *ops = jv_obj_get_ascii(op, "ops");
+            if (!ops || ops->kind != JV_ARR) fail(d, MTO_BAD_INPUT, "group without ops");
+            for (int i = 0; i < ops->n; i++) apply_remote_op(d, ops->vals[i], short_id, seq, ref_seq, msn);
+            break;
+        }
+        default: break;
+    }
+}
+
+int mto_apply_msg_json(mto_doc *d, const char *msg_json) {
+    GUARD(d);
+    jv *msg = jv_parse(msg_json, strlen(msg_json));
+    if (!msg || msg->kind != JV_OBJ) fail(d, MTO_BAD_INPUT, "message is not a JSON object");
+    const jv *cid = jv_obj_get_ascii(msg, "clientId");
+    if (!cid || cid->kind != JV_STR) fail(d, MTO_BAD_INPUT, "clientId");
+    sb name;
+    sb_init(&name);
+    sb_put_u16_utf8(&name, cid->s, cid->slen);
+    int seq = 0, ref = 0, msn = 0;
+    if (!jv_int(jv_obj_get_ascii(msg, "sequenceNumber"), &seq) ||
+        !jv_int(jv_obj_get_ascii(msg, "referenceSequenceNumber"), &ref) ||
+        !jv_int(jv_obj_get_ascii(msg, "minimumSequenceNumber"), &msn)) {
+        sb_free(&name);
+        fail(d, MTO_BAD_INPUT, "sequence numbers");
+    }
+    int short_id = get_or_add_short_client_id(d, name.p ? name.p : "");
+    const jv *type = jv_obj_get_ascii(msg, "type");
+    static const u16 OP[2] = {'o', 'p'};
+    if (type && type->kind == JV_STR && u16_eq(type->s, type->slen, OP, 2)) {
+        if (d->long_client_id && !strcmp(name.p ? name.p : "", d->long_client_id)) {
+            sb_free(&name);
+            fail(d, MTO_UNSUPPORTED, "ack of a local op (observer path only)");
+        }
+        apply_remote_op(d, jv_obj_get_ascii(msg, "contents"), short_id, seq, ref, msn);
+    }
+    sb_free(&name);
+    update_seq_numbers(d, msn, seq);
+    jv_unref(msg);
+    UNGUARD(d);
+    return d->status;
+}
+
+/* Client.insertSegmentLocal on a non-collaborating client (client.ts:201-210, 393-441, 485-547) */
+int mto_insert_local_json(mto_doc *d, int pos, const char *seg_json) {
+    GUARD(d);
+    jv *spec = jv_parse(seg_json, strlen(seg_json));
+    if (!spec) fail(d, MTO_BAD_INPUT, "segment spec");
+    Seg *s = spec_to_segment(d, spec);
+    jv_unref(spec);
+    if (s->n.cached_length <= 0) {
+        UNGUARD(d);
+        return d->status;
+    }
+    if (d->cw.collaborating) fail(d, MTO_UNSUPPORTED, "local edits on a collaborating client");
+    int len = d->root->n.cached_length;
+    if (pos < 0 || pos > len) fail(d, MTO_INVALID_POS, "InvalidOpRange");
+    insert_segment(d, pos, s, d->cw.current_seq, d->cw.client_id, UNIVERSAL_SEQ);
+    UNGUARD(d);
+    return d->status;
+}
+
+int mto_annotate_local_json(mto_doc *d, int start, int end, const char *props_json) {
+    GUARD(d);
+    if (d->cw.collaborating) fail(d, MTO_UNSUPPORTED, "local edits on a collaborating client");
+    int len = d->root->n.cached_length;
+    if (start < 0 || start >= len || end <= start) fail(d, MTO_INVALID_POS, "InvalidOpRange");
+    jv *props = jv_parse(props_json, strlen(props_json));
+    if (!props) fail(d, MTO_BAD_INPUT, "props");
+    annotate_range(d, start, end, props, 0, d->cw.current_seq, d->cw.client_id, UNIVERSAL_SEQ);
+    jv_unref(props);
+    UNGUARD(d);
+    return d->status;
+}
+
+int mto_remove_local(mto_doc *d, int start, int end) {
+    GUARD(d);
+    if (d->cw.collaborating) fail(d, MTO_UNSUPPORTED, "local edits on a collaborating client");
+    int len = d->root->n.cached_length;
+    if (start < 0 || start >= len || end <= start) fail(d, MTO_INVALID_POS, "InvalidOpRange");
+    mark_range_removed(d, start, end, d->cw.current_seq, d->cw.client_id, UNIVERSAL_SEQ);
+    UNGUARD(d);
+    return d->status;
+}
+
+int mto_get_length(mto_doc *d) { return d->root->n.cached_length; }
+int mto_view_length(mto_doc *d, int ref_seq, int short_client) { return block_length(d, d->root, ref_seq, short_client); }
+int mto_current_seq(mto_doc *d) { return d->cw.current_seq; }
+int mto_min_seq(mto_doc *d) { return d->cw.min_seq; }
+
+/* ------------------------------------------------------------------ read-out */
+typedef struct {
+    sb *out;
+} TextCtx;
+/* MergeTreeTextHelper.gatherText (textSegment.ts:188-275) with placeholder "" over the
+   full local view */
+static int gather_text(mto_doc *d, Seg *s, int pos, int r, int c, int start, int end, void *vctx) {
+    (void)d; (void)pos; (void)r; (void)c;
+    TextCtx *ctx = (TextCtx *)vctx;
+    if (s->kind == SEG_TEXT) {
+        int len = s->n.cached_length;
+        int a = start < 0 ? 0 : start;
+        int b = end >= len ? len : end;
+        if (start <= 0 && end >= len) { a = 0; b = len; }
+        sb_put_u16_utf8(ctx->out, s->text + a, b - a);
+    }
+    return 1;
+}
+
+static void build_text(mto_doc *d, sb *out) {
+    TextCtx ctx = {out};
+    MapActions a = {gather_text, NULL, &ctx};
+    int len = block_length(d, d->root, d->cw.current_seq, d->cw.client_id);
+    node_map(d, d->root, &a, 0, d->cw.current_seq, d->cw.client_id, 0, len, 1);
+}
+
+static long copy_out(const sb *s, char *buf, long cap) {
+    long n = (long)s->n;
+    if (buf && cap > 0) {
+        long m = n < cap - 1 ? n : cap - 1;
+        if (m > 0) memcpy(buf, s->p, (size_t)m);
+        buf[m] = 0;
+    }
+    return n;
+}
+
+long mto_get_text(mto_doc *d, char *buf, long cap) {
+    sb s;
+    sb_init(&s);
+    build_text(d, &s);
+    long n = copy_out(&s, buf, cap);
+    sb_free(&s);
+    return n;
+}
+
+static void seg_props_json(const Seg *s, sb *out) {
+    if (!s->props) sb_puts(out, "null");
+    else {
+        sb t;
+        sb_init(&t);
+        jv_stringify(s->props, &t);
+        /* re-quote the JSON text as a JSON string (UTF-8 bytes pass through as-is below) */
+        sb_putc(out, '"');
+        for (size_t i = 0; i < t.n; i++) {
+            char ch = t.p[i];
+            if (ch == '"' || ch == '\\') sb_putc(out, '\\');
+            sb_putc(out, ch);
+        }
+        sb_putc(out, '"');
+        sb_free(&t);
+    }
+}
+
+typedef struct {
+    sb *out;
+    int pos;
+    int run_start, run_len;
+    sb run_props;
+    int first;
+} RunCtx;
+
+static void flush_run(RunCtx *c) {
+    if (c->run_len <= 0) return;
+    if (!c->first) sb_putc(c->out, ',');
+    c->first = 0;
+    char t[64];
+    snprintf(t, sizeof t, "[%d,%d,", c->run_start, c->run_len);
+    sb_puts(c->out, t);
+    sb_putn(c->out, c->run_props.p, c->run_props.n);
+    sb_putc(c->out, ']');
+}
+
+static int gather_runs(mto_doc *d, Seg *s, int pos, int r, int cl, int start, int end, void *vctx) {
+    (void)d; (void)pos; (void)r; (void)cl; (void)start; (void)end;
+    RunCtx *c = (RunCtx *)vctx;
+    int len = s->n.cached_length;
+    sb pj;
+    sb_init(&pj);
+    seg_props_json(s, &pj);
+    if (c->run_len > 0 && pj.n == c->run_props.n && !memcmp(pj.p, c->run_props.p, pj.n)) {
+        c->run_len += len;
+    } else {
+        flush_run(c);
+        sb_free(&c->run_props);
+        c->run_props = pj;
+        c->run_start = c->pos;
+        c->run_len = len;
+        pj.p = NULL;
+    }
+    sb_free(&pj);
+    c->pos += len;
+    return 1;
+}
+
+long mto_props_runs(mto_doc *d, char *buf, long cap) {
+    sb out;
+    sb_init(&out);
+    sb_putc(&out, '[');
+    RunCtx c;
+    memset(&c, 0, sizeof c);
+    c.out = &out;
+    c.first = 1;
+    sb_init(&c.run_props);
+    MapActions a = {gather_runs, NULL, &c};
+    int len = block_length(d, d->root, d->cw.current_seq, d->cw.client_id);
+    node_map(d, d->root, &a, 0, d->cw.current_seq, d->cw.client_id, 0, len, 1);
+    flush_run(&c);
+    sb_free(&c.run_props);
+    sb_putc(&out, ']');
+    long n = copy_out(&out, buf, cap);
+    sb_free(&out);
+    return n;
+}
+
+/* UTF-8 -> UTF-16 code units (invalid sequences -> U+FFFD) */
+static u16 *utf8_to_u16(const char *s, int *n) {
+    size_t L = strlen(s);
+    u16 *out = (u16 *)malloc(sizeof(u16) * (L * 2 + 1));
+    int k = 0;
+    const unsigned char *q = (const unsigned char *)s;
+    size_t i = 0;
+    while (i < L) {
+        uint32_t c = q[i];
+        int len = 1;
+        if (c < 0x80) len = 1;
+        else if ((c & 0xE0) == 0xC0) { len = 2; c &= 0x1F; }
+        else if ((c & 0xF0) == 0xE0) { len = 3; c &= 0x0F; }
+        else if ((c & 0xF8) == 0xF0) { len = 4; c &= 0x07; }
+        else { out[k++] = 0xFFFD; i++; continue; }
+        if (i + (size_t)len > L) { out[k++] = 0xFFFD; break; }
+        int bad = 0;
+        for (int m = 1; m < len; m++) {
+            if ((q[i + m] & 0xC0) != 0x80) { bad = 1; break; }
+            c = (c << 6) | (q[i + m] & 0x3F);
+        }
+        if (bad) { out[k++] = 0xFFFD; i++; continue; }
+        i += (size_t)len;
+        if (c >= 0x10000) {
+            c -= 0x10000;
+            out[k++] = (u16)(0xD800 + (c >> 10));
+            out[k++] = (u16)(0xDC00 + (c & 0x3FF));
+        } else {
+            out[k++] = (u16)c;
+        }
+    }
+    *n = k;
+    return out;
+}
+
+static void put_json_string_utf8(sb *out, const char *s) {
+    int n;
+    u16 *u = utf8_to_u16(s, &n);
+    js_quote(out, u, n);
+    free(u);
+}
+
+/* ------------------------------------------------------------------ SnapshotV1 (snapshotV1.ts) */
+typedef struct {
+    sb json; /* serialized JsonSegmentSpecs */
+    int len;
+} SnapSeg;
+
+typedef struct {
+    SnapSeg *p;
+    int n, cap;
+} SnapVec;
+
+static void snap_push(SnapVec *v, sb json, int len) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 64;
+        v->p = (SnapSeg *)realloc(v->p, sizeof(SnapSeg) * (size_t)v->cap);
+    }
+    v->p[v->n].json = json;
+    v->p[v->n].len = len;
+    v->n++;
+}
+
+/* segment.toJSONObject(): TextSegment (textSegment.ts:48-54), Marker (mergeTree.ts:652-656) */
+static void seg_json(sb *out, int kind, const u16 *text, int len, int ref_type, const jv *props) {
+    if (kind == SEG_TEXT) {
+        if (props) {
+            sb_puts(out, "{\"text\":");
+            js_quote(out, text, len);
+            sb_puts(out, ",\"props\":");
+            jv_stringify(props, out);
+            sb_putc(out, '}');
+        } else {
+            js_quote(out, text, len);
+        }
+    } else {
+        char t[64];
+        snprintf(t, sizeof t, "{\"marker\":{\"refType\":%d}", ref_type);
+        sb_puts(out, t);
+        if (props) {
+            sb_puts(out, ",\"props\":");
+            jv_stringify(props, out);
+        }
+        sb_putc(out, '}');
+    }
+}
+
+/* coalescing candidate `prev` (a clone when coalesced: snapshotV1.ts:191-210) */
+typedef struct {
+    int active;
+    int kind, ref_type;
+    u16 *text;
+    int len, cap;
+    const jv *props;
+} Prev;
+
+static void prev_push(SnapVec *v, Prev *p) {
+    if (!p->active) return;
+    sb j;
+    sb_init(&j);
+    seg_json(&j, p->kind, p->text, p->len, p->ref_type, p->props);
+    snap_push(v, j, p->len);
+    p->active = 0;
+}
+
+static void prev_set(Prev *p, const Seg *s) {
+    p->active = 1;
+    p->kind = s->kind;
+    p->ref_type = s->ref_type;
+    p->len = 0;
+    if (s->kind == SEG_TEXT) {
+        if (p->cap < s->n.cached_length) {
+            p->cap = s->n.cached_length + 64;
+            p->text = (u16 *)realloc(p->text, sizeof(u16) * (size_t)p->cap);
+        }
+        memcpy(p->text, s->text, sizeof(u16) * (size_t)s->n.cached_length);
+    }
+    p->len = s->n.cached_length;
+    p->props = s->props;
+}
+
+typedef struct {
+    mto_doc *d;
+    SnapVec *segs;
+    Prev prev;
+    int min_seq;
+} ExtractCtx;
+
+static void extract_segment(ExtractCtx *c, const Seg *s) { /* snapshotV1.ts:175-240 */
+    int min_seq = c->min_seq;
+    if (s->seq == UNASSIGNED_SEQ || (s->removed && s->removed_seq <= min_seq)) return;
+    if (s->seq <= min_seq && (!s->removed || s->removed_seq == UNASSIGNED_SEQ)) {
+        if (!c->prev.active) {
+            prev_set(&c->prev, s);
+        } else {
+            /* prev.canAppend(segment) && matchProperties(prev.properties, segment.properties) */
+            int can = c->prev.kind == SEG_TEXT && s->kind == SEG_TEXT &&
+                      !(c->prev.len > 0 && c->prev.text[c->prev.len - 1] == '\n') &&
+                      (c->prev.len <= TEXT_GRANULARITY || s->n.cached_length <= TEXT_GRANULARITY);
+            if (can && jv_match_properties(c->prev.props, s->props)) {
+                int need = c->prev.len + s->n.cached_length;
+                if (need > c->prev.cap) {
+                    c->prev.cap = need * 2;
+                    c->prev.text = (u16 *)realloc(c->prev.text, sizeof(u16) * (size_t)c->prev.cap);
+                }
+                memcpy(c->prev.text + c->prev.len, s->text, sizeof(u16) * (size_t)s->n.cached_length);
+                c->prev.len = need;
+            } else {
+                prev_push(c->segs, &c->prev);
+                prev_set(&c->prev, s);
+            }
+        }
+    } else {
+        prev_push(c->segs, &c->prev);
+        sb j;
+        sb_init(&j);
+        sb_puts(&j, "{\"json\":");
+        seg_json(&j, s->kind, s->text, s->n.cached_length, s->ref_type, s->props);
+        char t[64];
+        if (s->seq > min_seq) {
+            snprintf(t, sizeof t, ",\"seq\":%d,\"client\":", s->seq);
+            sb_puts(&j, t);
+            put_json_string_utf8(&j, get_long_client_id(c->d, s->client_id));
+        }
+        if (s->removed) {
+            snprintf(t, sizeof t, ",\"removedSeq\":%d,\"removedClient\":", s->removed_seq);
+            sb_puts(&j, t);
+            put_json_string_utf8(&j, get_long_client_id(c->d, s->removed_client));
+        }
+        sb_putc(&j, '}');
+        snap_push(c->segs, j, s->n.cached_length);
+    }
+}
+
+static void walk_all_segments(Block *b, ExtractCtx *c) { /* mergeTree.ts:2969-2983 */
+    for (int i = 0; i < b->child_count; i++) {
+        Node *n = b->children[i];
+        if (n->is_leaf) extract_segment(c, (Seg *)n);
+        else walk_all_segments((Block *)n, c);
+    }
+}
+
+static void add_blob(mto_doc *d, const char *name, sb content) {
+    d->blob_names = (char **)realloc(d->blob_names, sizeof(char *) * (size_t)(d->n_blobs + 1));
+    d->blobs = (sb *)realloc(d->blobs, sizeof(sb) * (size_t)(d->n_blobs + 1));
+    d->blob_names[d->n_blobs] = strdup(name);
+    d->blobs[d->n_blobs] = content;
+    d->n_blobs++;
+}
+
+int mto_snapshot_v1(mto_doc *d, int chunk_size) {
+    if (chunk_size <= 0) chunk_size = 10000; /* SnapshotV1.chunkSize, snapshotV1.ts:40 */
+    free_blobs(d);
+    SnapVec segs = {0, 0, 0};
+    ExtractCtx c;
+    memset(&c, 0, sizeof c);
+    c.d = d;
+    c.segs = &segs;
+    c.min_seq = d->cw.min_seq;
+    walk_all_segments(d->root, &c);
+    prev_push(&segs, &c.prev);
+    free(c.prev.text);
+
+    /* emit (snapshotV1.ts:85-149) + getSeqLengthSegs (57-79) */
+    typedef struct { int start, count, length; } Chunk;
+    Chunk *chunks = NULL;
+    int nch = 0;
+    int total_count = 0, total_length = 0;
+    do {
+        int length = 0, count = 0;
+        while (length < chunk_size && total_count + count < segs.n) {
+            length += segs.p[total_count + count].len;
+            count++;
+        }
+        chunks = (Chunk *)realloc(chunks, sizeof(Chunk) * (size_t)(nch + 1));
+        chunks[nch].start = total_count;
+        chunks[nch].count = count;
+        chunks[nch].length = length;
+        nch++;
+        total_count += count;
+        total_length += length;
+    } while (total_count < segs.n);
+
+    for (int ci = 0; ci < nch; ci++) {
+        sb j;
+        sb_init(&j);
+        char t[128];
+        snprintf(t, sizeof t, "{\"version\":\"1\",\"segmentCount\":%d,\"length\":%d,\"segments\":[", chunks[ci].count,
+                 chunks[ci].length);
+        sb_puts(&j, t);
+        for (int k = 0; k < chunks[ci].count; k++) {
+            if (k) sb_putc(&j, ',');
+            SnapSeg *s = &segs.p[chunks[ci].start + k];
+            sb_putn(&j, s->json.p, s->json.n);
+        }
+        snprintf(t, sizeof t, "],\"startIndex\":%d", chunks[ci].start);
+        sb_puts(&j, t);
+        if (ci == 0) {
+            snprintf(t, sizeof t, ",\"headerMetadata\":{\"minSequenceNumber\":%d,\"sequenceNumber\":%d,"
+                                  "\"orderedChunkMetadata\":[{\"id\":\"header\"}",
+                     d->cw.min_seq, d->cw.current_seq);
+            sb_puts(&j, t);
+            for (int b = 1; b < nch; b++) {
+                snprintf(t, sizeof t, ",{\"id\":\"body_%d\"}", b - 1);
+                sb_puts(&j, t);
+            }
+            snprintf(t, sizeof t, "],\"totalLength\":%d,\"totalSegmentCount\":%d}", total_length, total_count);
+            sb_puts(&j, t);
+        }
+        sb_putc(&j, '}');
+        if (ci == 0) add_blob(d, "header", j);
+        else {
+            snprintf(t, sizeof t, "body_%d", ci - 1);
+            add_blob(d, t, j);
+        }
+    }
+    free(chunks);
+    for (int i = 0; i < segs.n; i++) sb_free(&segs.p[i].json);
+    free(segs.p);
+    return d->n_blobs;
+}
+
+long mto_snapshot_blob(mto_doc *d, int i, char *name, long name_cap, char *buf, long cap) {
+    if (i < 0 || i >= d->n_blobs) return -1;
+    if (name && name_cap > 0) {
+        snprintf(name, (size_t)name_cap, "%s", d->blob_names[i]);
+    }
+    return copy_out(&d->blobs[i], buf, cap);
+}
+
+/* ------------------------------------------------------------------ shape / dump / digest */
+static int tree_depth(const Block *b) {
+    int depth = 1;
+    while (b->child_count > 0 && !b->children[0]->is_leaf) {
+        b = (const Block *)b->children[0];
+        depth++;
+    }
+    return depth;
+}
+
+typedef struct {
+    sb *out;
+    int first;
+} ShapeCtx;
+static void shape_walk(const Block *b, int level, int leaf_level, ShapeCtx *c) {
+    if (level == leaf_level) {
+        char t[16];
+        snprintf(t, sizeof t, "%s%d", c->first ? "" : ",", b->child_count);
+        sb_puts(c->out, t);
+        c->first = 0;
+        return;
+    }
+    for (int i = 0; i < b->child_count; i++) shape_walk((const Block *)b->children[i], level + 1, leaf_level, c);
+}
+
+long mto_shape(mto_doc *d, char *buf, long cap) {
+    sb out;
+    sb_init(&out);
+    int depth = tree_depth(d->root);
+    char t[32];
+    snprintf(t, sizeof t, "D%d:", depth);
+    sb_puts(&out, t);
+    ShapeCtx c = {&out, 1};
+    shape_walk(d->root, 1, depth, &c);
+    long n = copy_out(&out, buf, cap);
+    sb_free(&out);
+    return n;
+}
+
+typedef struct {
+    uint64_t h;
+} Fnv;
+static void fnv_bytes(Fnv *f, const void *p, size_t n) {
+    const unsigned char *q = (const unsigned char *)p;
+    for (size_t i = 0; i < n; i++) {
+        f->h ^= q[i];
+        f->h *= 0x100000001b3ull;
+    }
+}
+static void fnv_u32(Fnv *f, uint32_t x) {
+    unsigned char b[4] = {(unsigned char)x, (unsigned char)(x >> 8), (unsigned char)(x >> 16), (unsigned char)(x >> 24)};
+    fnv_bytes(f, b, 4);
+}
+
+static uint64_t fnv_name(const char *name) {
+    Fnv f = {0xcbf29ce484222325ull};
+    fnv_bytes(&f, name, strlen(name));
+    return f.h;
+}
+static void fnv_u64(Fnv *f, uint64_t x) {
+    fnv_u32(f, (uint32_t)x);
+    fnv_u32(f, (uint32_t)(x >> 32));
+}
+
+/* State digest (DESIGN.md "State digest"): client ids enter by long name, so the digest does
+   not depend on how short ids were numbered. */
+static void digest_walk(mto_doc *d, const Block *b, int level, int leaf_level, Fnv *f) {
+    if (level == leaf_level) {
+        fnv_u32(f, 0xB10CB10Cu);
+        fnv_u32(f, (uint32_t)b->child_count);
+        for (int i = 0; i < b->child_count; i++) {
+            const Seg *s = (const Seg *)b->children[i];
+            uint64_t ovl = 0;
+            for (int k = 0; k < s->novl; k++) ovl += fnv_name(get_long_client_id(d, s->ovl[k]));
+            fnv_u32(f, (uint32_t)s->kind);
+            fnv_u32(f, (uint32_t)s->n.cached_length);
+            fnv_u32(f, (uint32_t)s->seq);
+            fnv_u64(f, fnv_name(get_long_client_id(d, s->client_id)));
+            fnv_u32(f, s->removed ? (uint32_t)s->removed_seq : 0xFFFFFFFFu);
+            fnv_u64(f, s->removed ? fnv_name(get_long_client_id(d, s->removed_client)) : 0ull);
+            fnv_u64(f, ovl);
+            if (!s->props) {
+                fnv_u32(f, 0xFFFFFFFFu);
+            } else {
+                sb t;
+                sb_init(&t);
+                jv_stringify(s->props, &t);
+                fnv_u32(f, (uint32_t)t.n);
+                fnv_bytes(f, t.p, t.n);
+                sb_free(&t);
+            }
+            if (s->kind == SEG_TEXT) {
+                for (int k = 0; k < s->n.cached_length; k++) {
+                    unsigned char b2[2] = {(unsigned char)s->text[k], (unsigned char)(s->text[k] >> 8)};
+                    fnv_bytes(f, b2, 2);
+                }
+            } else {
+                fnv_u32(f, (uint32_t)s->ref_type);
+            }
+        }
+        return;
+    }
+    for (int i = 0; i < b->child_count; i++) digest_walk(d, (const Block *)b->children[i], level + 1, leaf_level, f);
+}
+
+uint64_t mto_state_digest(mto_doc *d) {
+    Fnv f = {0xcbf29ce484222325ull};
+    int depth = tree_depth(d->root);
+    fnv_u32(&f, (uint32_t)depth);
+    digest_walk(d, d->root, 1, depth, &f);
+    fnv_u32(&f, (uint32_t)d->cw.min_seq);
+    fnv_u32(&f, (uint32_t)d->cw.current_seq);
+    fnv_u32(&f, (uint32_t)d->status);
+    return f.h;
+}
+
+static void dump_walk(mto_doc *d, const Block *b, sb *out, int depth) {
+    for (int i = 0; i < b->child_count; i++) {
+        const Node *n = b->children[i];
+        if (!n->is_leaf) {
+            char t[64];
+            snprintf(t, sizeof t, "%*sB(%d)\n", depth * 2, "", ((const Block *)n)->child_count);
+            sb_puts(out, t);
+            dump_walk(d, (const Block *)n, out, depth + 1);
+        } else {
+            const Seg *s = (const Seg *)n;
+            char t[160];
+            snprintf(t, sizeof t, "%*sS len=%d seq=%d cli=%d rseq=%d rcli=%d novl=%d '", depth * 2, "",
+                     s->n.cached_length, s->seq, s->client_id, s->removed ? s->removed_seq : -1,
+                     s->removed ? s->removed_client : -1, s->novl);
+            sb_puts(out, t);
+            if (s->kind == SEG_TEXT) sb_put_u16_utf8(out, s->text, s->n.cached_length);
+            sb_puts(out, "'");
+            if (s->props) {
+                sb_putc(out, ' ');
+                jv_stringify(s->props, out);
+            }
+            sb_putc(out, '\n');
+        }
+    }
+}
+
+long mto_dump(mto_doc *d, char *buf, long cap) {
+    sb out;
+    sb_init(&out);
+    char t[96];
+    snprintf(t, sizeof t, "root(%d) min=%d cur=%d heap=%d\n", d->root->child_count, d->cw.min_seq, d->cw.current_seq,
+             heap_count(d));
+    sb_puts(&out, t);
+    dump_walk(d, d->root, &out, 1);
+    long n = copy_out(&out, buf, cap);
+    sb_free(&out);
+    return n;
+}
+
+/* ------------------------------------------------------------------ packed logs */
+mto_tables *mto_tables_new(const char *const *key_names, int n_keys, const char *const *value_json, int n_values) {
+    mto_tables *t = (mto_tables *)calloc(1, sizeof(mto_tables));
+    t->n_keys = n_keys;
+    t->keys = (char **)calloc((size_t)n_keys + 1, sizeof(char *));
+    t->keys16 = (u16 **)calloc((size_t)n_keys + 1, sizeof(u16 *));
+    t->keylen16 = (int *)calloc((size_t)n_keys + 1, sizeof(int));
+    for (int i = 0; i < n_keys; i++) {
+        t->keys[i] = strdup(key_names[i]);
+        t->keys16[i] = utf8_to_u16(key_names[i], &t->keylen16[i]);
+    }
+    t->n_values = n_values;
+    t->values = (jv **)calloc((size_t)n_values + 1, sizeof(jv *));
+    for (int i = 0; i < n_values; i++) {
+        if (i == 0 || !value_json[i]) t->values[i] = jv_new(JV_NULL);
+        else {
+            t->values[i] = jv_parse(value_json[i], strlen(value_json[i]));
+            if (!t->values[i]) t->values[i] = jv_new(JV_NULL);
+        }
+    }
+    return t;
+}
+
+void mto_tables_free(mto_tables *t) {
+    if (!t) return;
+    for (int i = 0; i < t->n_keys; i++) {
+        free(t->keys[i]);
+        free(t->keys16[i]);
+    }
+    for (int i = 0; i < t->n_values; i++) jv_unref(t->values[i]);
+    free(t->keys);
+    free(t->keys16);
+    free(t->keylen16);
+    free(t->values);
+    free(t);
+}
+
+static jv *props_from_records(mto_doc *d, const mt_prop *p, uint32_t n, const mto_tables *t) {
+    jv *o = jv_new(JV_OBJ);
+    for (uint32_t i = 0; i < n; i++) {
+        if ((int)p[i].key >= t->n_keys || (int)p[i].value >= t->n_values) {
+            jv_unref(o);
+            fail(d, MTO_BAD_INPUT, "prop id out of range");
+        }
+        jv_obj_set(o, t->keys16[p[i].key], t->keylen16[p[i].key], jv_ref(t->values[p[i].value]));
+    }
+    return o;
+}
+
+static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, const mt_prop *props,
+                             const mto_tables *t, const char *const *client_names, int n_clients) {
+    if ((int)op->client >= n_clients) fail(d, MTO_BAD_INPUT, "client index out of range");
+    int sid = d->pk_map[op->client];
+    if (sid < 0) {
+        sid = get_or_add_short_client_id(d, client_names[op->client]); /* applyMsg registration */
+        d->pk_map[op->client] = sid;
+    }
+    if (op->type != MT_OP_NOOP && d->long_client_id && sid == d->cw.client_id)
+        fail(d, MTO_UNSUPPORTED, "ack of a local op (observer path only)");
+    uint32_t bits = MT_OPF_BITS(op->flags);
+    switch (op->type) {
+        case MT_OP_INSERT: {
+            Seg *s;
+            if (bits & MT_OPF_MARKER) s = new_marker(d, (int)op->payload);
+            else s = new_text_seg(d, text + op->payload, (int)op->payload_len);
+            if (bits & MT_OPF_HAS_PROPS) {
+                jv *pr = props_from_records(d, props + op->pos2, MT_OPF_NPROPS(op->flags), t);
+                seg_add_properties(d, s, pr, 0);
+                jv_unref(pr);
+            }
+            insert_segment(d, op->pos1, s, op->ref_seq, sid, op->seq);
+            complete_remote_op(d, op->seq, op->msn);
+            break;
+        }
+        case MT_OP_REMOVE:
+            mark_range_removed(d, op->pos1, op->pos2, op->ref_seq, sid, op->seq);
+            complete_remote_op(d, op->seq, op->msn);
+            break;
+        case MT_OP_ANNOTATE: {
+            jv *pr = props_from_records(d, props + op->payload, op->payload_len, t);
+            annotate_range(d, op->pos1, op->pos2, pr, (bits & MT_OPF_REWRITE) ? 1 : 0, op->ref_seq, sid, op->seq);
+            jv_unref(pr);
+            complete_remote_op(d, op->seq, op->msn);
+            break;
+        }
+        case MT_OP_NOOP: break;
+        default: fail(d, MTO_BAD_INPUT, "op type %d", op->type);
+    }
+    if (!(bits & MT_OPF_GROUP_CONT)) update_seq_numbers(d, op->msn, op->seq);
+}
+
+int mto_apply_packed(mto_doc *d, const mt_op *ops, long n_ops, const uint16_t *text, const mt_prop *props,
+                     const mto_tables *t, const char *const *client_names, int n_clients) {
+    if (d->status != MTO_OK) return d->status;
+    if (!d->cw.collaborating) {
+        mto_start_collab(d, client_names[0], 0, 0);
+        d->pk_map[0] = d->cw.client_id;
+    }
+    GUARD(d);
+    for (long i = 0; i < n_ops; i++) apply_packed_one(d, &ops[i], text, props, t, client_names, n_clients);
+    UNGUARD(d);
+    return d->status;
+}
+
+/* ------------------------------------------------------------------ generator */
+static const char *GEN_KEYS[MT_GEN_N_KEYS] = {"bold", "italic", "color", "size"};
+static const char *GEN_COLORS[3] = {"\"red\"", "\"green\"", "\"blue\""};
+static const char *GEN_CLIENTS[] = {"readonly", "A", "B", "C", "D", "E", "F", "G", "H", "I", "J", "K", "L", "M",
+                                    "N", "O", "P", "Q", "R", "S", "T", "U", "V", "W", "X", "Y", "Z"};
+static char GEN_SIZES[17][4];
+
+const char *mto_gen_key_name(int k) { return (k >= 0 && k < MT_GEN_N_KEYS) ? GEN_KEYS[k] : NULL; }
+const char *mto_gen_value_json(int v) {
+    if (v == 0) return "null";
+    if (v == 1) return "true";
+    if (v >= 2 && v <= 4) return GEN_COLORS[v - 2];
+    if (v >= 5 && v < MT_GEN_N_VALUES) {
+        snprintf(GEN_SIZES[v - 5], sizeof GEN_SIZES[0], "%d", v - 5 + 8);
+        return GEN_SIZES[v - 5];
+    }
+    return NULL;
+}
+const char *mto_gen_client_name(int i) {
+    return (i >= 0 && i < (int)(sizeof GEN_CLIENTS / sizeof GEN_CLIENTS[0])) ? GEN_CLIENTS[i] : NULL;
+}
+
+static const char GEN_ALPHABET[] = "abcdefghijklmnopqrstuvwxyz ";
+
+int mto_gen_doc(const mt_gen_params *p, long doc, mt_op *ops_out, uint16_t *text_out, long text_cap, long *text_len,
+                mt_prop *props_out, long props_cap, long *n_props) {
+    if (p->n_clients < 1 || p->n_clients > 26) return MTO_BAD_INPUT;
+    static mto_tables *tables = NULL;
+    static pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+    pthread_mutex_lock(&mu);
+    if (!tables) {
+        const char *vals[MT_GEN_N_VALUES];
+        for (int v = 0; v < MT_GEN_N_VALUES; v++) vals[v] = mto_gen_value_json(v);
+        tables = mto_tables_new(GEN_KEYS, MT_GEN_N_KEYS, vals, MT_GEN_N_VALUES);
+    }
+    pthread_mutex_unlock(&mu);
+
+    mto_doc *d = mto_new();
+    mto_start_collab(d, GEN_CLIENTS[0], 0, 0);
+    d->pk_map[0] = d->cw.client_id;
+    uint64_t x = mt_rng_seed(p->seed, (uint64_t)doc);
+    int last_ref[64];
+    for (int c = 0; c <= p->n_clients; c++) last_ref[c] = 0;
+    long tl = 0, np = 0;
+    int st = MTO_OK;
+    for (int k = 1; k <= p->n_ops; k++) {
+        mt_op op;
+        memset(&op, 0, sizeof op);
+        int seq = k;
+        int c = 1 + (int)mt_rng_below(&x, (uint32_t)p->n_clients);
+        int lag = (int)mt_rng_below(&x, (uint32_t)p->max_lag + 1);
+        int ref = seq - 1 - lag;
+        if (ref < last_ref[c]) ref = last_ref[c];
+        last_ref[c] = ref;
+        int msn = last_ref[1];
+        for (int i = 2; i <= p->n_clients; i++)
+            if (last_ref[i] < msn) msn = last_ref[i];
+        /* view length of the issuer: MergeTree.getLength(refSeq, clientId) */
+        int sid = d->pk_map[c];
+        int len;
+        if (sid < 0) {
+            /* not yet registered: nodeLength compares ids only; an unknown id sees no own segments */
+            len = block_length(d, d->root, ref, 1000 + c);
+        } else {
+            len = block_length(d, d->root, ref, sid);
+        }
+        uint32_t u = mt_rng_below(&x, 100);
+        int type;
+        if (len < p->min_len || (int)u < p->pct_insert) type = MT_OP_INSERT;
+        else if ((int)u < p->pct_insert + p->pct_remove) type = MT_OP_REMOVE;
+        else type = MT_OP_ANNOTATE;
+        op.type = (uint8_t)type;
+        op.client = (uint8_t)c;
+        op.seq = seq;
+        op.ref_seq = ref;
+        op.msn = msn;
+        if (type == MT_OP_INSERT) {
+            int pos = (int)mt_rng_below(&x, (uint32_t)len + 1);
+            int n = 1 + (int)mt_rng_below(&x, (uint32_t)p->max_insert);
+            if (tl + n > text_cap) { st = MTO_BAD_INPUT; break; }
+            op.pos1 = pos;
+            op.pos2 = 0;
+            op.payload = (uint32_t)tl;
+            op.payload_len = (uint32_t)n;
+            for (int i = 0; i < n; i++) {
+                uint32_t r = mt_rng_below(&x, 100);
+                u16 ch = (int)r < p->pct_newline ? (u16)'\n' : (u16)GEN_ALPHABET[mt_rng_below(&x, 27)];
+                text_out[tl++] = ch;
+            }
+        } else {
+            int rl = 1;
+            while (rl < len && mt_rng_below(&x, 4) != 0) rl++;
+            int start = (int)mt_rng_below(&x, (uint32_t)(len - rl + 1));
+            op.pos1 = start;
+            op.pos2 = start + rl;
+            if (type == MT_OP_ANNOTATE) {
+                int nk = 1 + (int)mt_rng_below(&x, 2);
+                int k0 = (int)mt_rng_below(&x, 4);
+                int keys[2] = {k0, (k0 + 1 + (int)mt_rng_below(&x, 3)) % 4};
+                if (np + nk > props_cap) { st = MTO_BAD_INPUT; break; }
+                op.payload = (uint32_t)np;
+                op.payload_len = (uint32_t)nk;
+                for (int i = 0; i < nk; i++) {
+                    uint32_t v;
+                    if (mt_rng_below(&x, 10) == 0) v = 0;
+                    else if (keys[i] <= 1) v = 1;
+                    else if (keys[i] == 2) v = 2 + mt_rng_below(&x, 3);
+                    else v = 5 + mt_rng_below(&x, 17);
+                    props_out[np].key = (uint32_t)keys[i];
+                    props_out[np].value = v;
+                    np++;
+                }
+            }
+        }
+        ops_out[k - 1] = op;
+        /* replay as the observer (text/props arrays are the doc-relative buffers) */
+        const char *const *names = GEN_CLIENTS;
+        mto_apply_packed(d, &op, 1, text_out, props_out, tables, names, p->n_clients + 1);
+        if (d->status != MTO_OK) { st = d->status; break; }
+    }
+    *text_len = tl;
+    *n_props = np;
+    mto_free(d);
+    return st;
+}
+
+/* ------------------------------------------------------------------ batch replay (CPU baseline) */
+typedef struct {
+    const mt_op *ops;
+    const int64_t *off;
+    long n_docs;
+    const uint16_t *text;
+    const mt_prop *props;
+    const mto_tables *t;
+    const char *const *names;
+    int n_clients;
+    uint64_t *digests;
+    int32_t *status;
+    long next;
+    pthread_mutex_t mu;
+} BatchJob;
+
+static void *batch_worker(void *arg) {
+    BatchJob *j = (BatchJob *)arg;
+    for (;;) {
+        long dd = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (dd >= j->n_docs) break;
+        mto_doc *d = mto_new();
+        mto_apply_packed(d, j->ops + j->off[dd], (long)(j->off[dd + 1] - j->off[dd]), j->text, j->props, j->t, j->names,
+                         j->n_clients);
+        if (j->digests) j->digests[dd] = mto_state_digest(d);
+        if (j->status) j->status[dd] = d->status;
+        mto_free(d);
+    }
+    return NULL;
+}
+
+double mto_replay_batch(const mt_op *ops, const int64_t *doc_op_off, long n_docs, const uint16_t *text,
+                        const mt_prop *props, const mto_tables *t, const char *const *client_names, int n_clients,
+                        int n_threads, uint64_t *digests_out, int32_t *status_out) {
+    BatchJob j;
+    memset(&j, 0, sizeof j);
+    j.ops = ops;
+    j.off = doc_op_off;
+    j.n_docs = n_docs;
+    j.text = text;
+    j.props = props;
+    j.t = t;
+    j.names = client_names;
+    j.n_clients = n_clients;
+    j.digests = digests_out;
+    j.status = status_out;
+    if (n_threads < 1) n_threads = 1;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)n_threads);
+    for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, batch_worker, &j);
+    for (int i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(th);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

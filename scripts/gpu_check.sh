@@ -1,0 +1,23 @@
+#!/bin/bash
+# Run GPU steps on the gpurun box; stop at the first crash-type exit (fault/abort/timeout).
+set -u
+mkdir -p gpurun_out
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "fatal exit in $name; stopping"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case "$step" in
+    tests) run tests 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    smoke) run smoke 300 python -u __graft_entry__.py smoke ;;
+    bench) run bench 600 python -u bench.py --steps 3 --warmup 1 ;;
+    bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
+    *) echo "unknown step $step" ;;
+  esac
+done

@@ -1,0 +1,104 @@
+"""Build tests/golden/kats.json: observer-replay known-answer scenarios.
+
+Each scenario is a list of ISequencedDocumentMessage JSON objects (protocol.ts:132-172)
+applied by a passive observer ("readonly", MT/test/mergeTreeOperationRunner.ts:107-108)
+plus the expected final text / properties.  `source` names where the expectation comes
+from:
+  * "reference:<file>:<lines>" — a literal expectation asserted by the reference's own
+    merge-tree test suite for the same message sequence (every client converges on it,
+    so the observer must produce it too);
+  * "derived:<file>:<lines>" — the reference test checks convergence only; the expected
+    observer value was derived by hand from the cited rules and is NOT reference-pinned.
+
+Run from the repo root:  python tests/golden/make_kats.py
+"""
+import json
+from pathlib import Path
+
+OUT = Path(__file__).with_name("kats.json")
+
+
+def msg(client, seq, ref, contents, msn=0):
+    return {"clientId": client, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+            "minimumSequenceNumber": msn, "type": "op", "contents": contents}
+
+
+def ins(pos, seg):
+    return {"type": 0, "pos1": pos, "seg": seg}
+
+
+def rem(a, b):
+    return {"type": 1, "pos1": a, "pos2": b}
+
+
+def ann(a, b, props, combining=None):
+    op = {"type": 2, "pos1": a, "pos2": b, "props": props}
+    if combining:
+        op["combiningOp"] = combining
+    return op
+
+
+def hello_world():
+    # MT/test/mergeTree.markRangeRemoved.spec.ts:13-22: client "local" inserts each char of
+    # "hello world" at the end, each op sequenced as currentSeq + 1 with refSeq currentSeq.
+    return [msg("local", i + 1, i, ins(i, ch)) for i, ch in enumerate("hello world")]
+
+
+def main():
+    kats = []
+    base = hello_world()
+    kats.append({"name": "hello_world", "source": "reference:MT/test/mergeTree.markRangeRemoved.spec.ts:21",
+                 "messages": base, "text": "hello world"})
+    kats.append({"name": "remote_remove_then_remote_insert",
+                 "source": "reference:MT/test/mergeTree.markRangeRemoved.spec.ts:69-89",
+                 "messages": base + [msg("remote2", 12, 11, rem(0, 11)), msg("remote", 13, 11, ins(0, "text"))],
+                 "text": "text"})
+    kats.append({"name": "remote_insert_then_remote_remove",
+                 "source": "reference:MT/test/mergeTree.markRangeRemoved.spec.ts:91-107",
+                 "messages": base + [msg("remote", 12, 11, ins(0, "text")), msg("remote2", 13, 11, rem(0, 11))],
+                 "text": "text"})
+    # issue #1213 observer run (MT/test/mergeTree.markRangeRemoved.spec.ts:111-135): the test only
+    # compares observer and writer; "cX" follows from breakTie (mergeTree.ts:2248-2277).
+    kats.append({"name": "issue1213_observer", "source": "derived:MT/test/mergeTree.markRangeRemoved.spec.ts:111-135",
+                 "messages": [msg("1", 1, 0, ins(0, "a")), msg("1", 2, 0, rem(0, 1)), msg("2", 3, 0, ins(0, "X")),
+                              msg("1", 4, 2, ins(0, "c"))],
+                 "text": "cX"})
+    # MT/test/snapshot.spec.ts:160-167 "can insert segments relative to removed segment"
+    w = "writer"
+    kats.append({"name": "insert_relative_to_removed", "source": "reference:MT/test/snapshot.spec.ts:160-167",
+                 "messages": [msg(w, 1, 0, ins(0, "0x")), msg(w, 2, 1, ins(2, "2")), msg(w, 3, 2, rem(1, 2)),
+                              msg(w, 4, 3, ins(1, "1")), msg(w, 5, 4, ins(3, "3"))],
+                 "text": "0123"})
+    # MT/test/snapshot.spec.ts:146-151 with MSN advancing (zamboni unlinks the tombstone)
+    kats.append({"name": "removal_above_msn_of_segment_below_msn", "source": "reference:MT/test/snapshot.spec.ts:146-151",
+                 "messages": [msg(w, 1, 0, ins(0, "0x"), msn=1), msg(w, 2, 1, rem(1, 2), msn=1),
+                              msg(w, 3, 2, ins(1, "1"), msn=3)],
+                 "text": "01"})
+    # MT/test/mergeTree.annotate.spec.ts:485-509 "remote first" / "remote only" / "split remote"
+    kats.append({"name": "remote_annotate", "source": "reference:MT/test/mergeTree.annotate.spec.ts:485-519",
+                 "messages": [msg("remote", 1, 0, ins(0, "hello world")),
+                              msg("remote", 2, 1, ann(3, 7, {"propertySource": "remote", "remoteProperty": 1}))],
+                 "text": "hello world",
+                 "props_runs": [[0, 3, None], [3, 4, '{"propertySource":"remote","remoteProperty":1}'],
+                                [7, 4, None]]})
+    # JS key order: integer-like keys first, delete + re-add moves a string key last
+    # (MT/properties.ts:95-116 via Object.keys order); null deletes.
+    kats.append({"name": "annotate_key_order", "source": "derived:MT/properties.ts:95-116",
+                 "messages": [msg("A", 1, 0, ins(0, "abcdef")),
+                              msg("A", 2, 1, ann(0, 6, {"b": 1, "a": 2, "2": 3})),
+                              msg("B", 3, 2, ann(2, 4, {"b": None, "1": 4})),
+                              msg("A", 4, 3, ann(3, 6, {"b": 5}))],
+                 "text": "abcdef",
+                 "props_runs": [[0, 2, '{"2":3,"b":1,"a":2}'], [2, 1, '{"1":4,"2":3,"a":2}'],
+                                [3, 1, '{"1":4,"2":3,"a":2,"b":5}'], [4, 2, '{"2":3,"b":5,"a":2}']]})
+    # overlapping removes (MT/test/client.applyMsg.spec.ts:201-231): both clients remove [0,5)
+    kats.append({"name": "overlapping_removes", "source": "reference:MT/test/client.applyMsg.spec.ts:201-231",
+                 "messages": [msg("A", 1, 0, ins(0, "0123456789")), msg("B", 2, 1, rem(0, 5)),
+                              msg("A", 3, 1, rem(0, 5))],
+                 "text": "56789"})
+    OUT.write_text(json.dumps(kats, indent=1))
+    print(f"wrote {OUT} ({len(kats)} scenarios)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,195 @@
+"""GPU parity: the HIP replay (through the C ABI) vs the oracle on the same inputs.
+
+Bit-exact on everything the path produces: final text, property runs, SnapshotV1 blobs
+and the state digest (full segment table incl. tombstones, leaf-block membership, tree
+depth, collab window).  Sizes are chosen so the oracle finishes in seconds.
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import fluidframework_amd as fa
+from fluidframework_amd import oplog
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+KATS = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+GEN_KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
+GEN_VALUES = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
+
+
+def oracle_docs_from_messages(docs):
+    out = []
+    for msgs in docs:
+        d = O.Doc()
+        d.start_collab("readonly")
+        for m in msgs:
+            if d.apply_msg(json.dumps(m)) != 0:
+                break
+        out.append(d)
+    return out
+
+
+def assert_doc_parity(dv, od, full=True):
+    assert dv.status == od.status, (fa.status_string(dv.status), od.error)
+    if od.status != 0:
+        return
+    assert dv.digest() == od.digest(), f"state digest differs\nGPU shape {dv.shape()}\nCPU shape {od.shape()}"
+    if full:
+        assert dv.shape() == od.shape()
+        assert dv.get_text() == od.text()
+        assert dv.props_runs() == json.loads(od.props_runs())
+        assert dv.snapshot_v1() == od.snapshot_v1()
+
+
+def test_kats_on_gpu():
+    docs = [k["messages"] for k in KATS]
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        for i, k in enumerate(KATS):
+            dv = b.doc(i)
+            assert dv.get_text() == k["text"], k["name"]
+            if "props_runs" in k:
+                assert dv.props_runs() == k["props_runs"], k["name"]
+            assert_doc_parity(dv, oracle[i])
+
+
+def _gen_batch_parity(p, n_docs, full_every=8, **opts):
+    ops, text, props, off = O.gen_batch(p, n_docs)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(n_docs, **opts) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        b.set_clients(names)
+        b.ingest(ops, off, text, props)
+        b.run()
+        stats = b.stats()
+        assert stats["docs_failed"] == int((st != 0).sum())
+        for d in range(n_docs):
+            dv = b.doc(d)
+            assert dv.status == st[d]
+            assert dv.digest() == int(dig[d]), f"doc {d} digest differs"
+            if d % full_every == 0:
+                a, e = off[d], off[d + 1]
+                od = O.replay_doc(ops[a:e].copy(), text, props, t, names)
+                assert_doc_parity(dv, od)
+        return stats
+
+
+def test_text_only_config2_shape():
+    """BASELINE configs[1] shape (8 clients, refSeq lag <= 32, insert 60 / remove 40), 2k ops."""
+    _gen_batch_parity(O.gen_params(2000, seed=0xC0FFEE), 48)
+
+
+def test_annotate_and_zamboni_config3_shape():
+    """BASELINE configs[2] op mix (insert 55 / remove 35 / annotate 10) at 1.5k ops."""
+    _gen_batch_parity(O.gen_params(1500, pct_insert=55, pct_remove=35, seed=0xBADC0DE), 32)
+
+
+def test_high_concurrency_tie_breaks():
+    """Wide collab windows stress breakTie / overlapping removes / pack."""
+    _gen_batch_parity(O.gen_params(1200, n_clients=24, max_lag=200, pct_insert=50, pct_remove=40,
+                                   min_len=0, max_insert=3, seed=77), 32)
+
+
+def test_small_capacity_escalation():
+    """Force a tiny LDS class so documents overflow and are re-run in larger classes."""
+    stats = _gen_batch_parity(O.gen_params(800, seed=3), 16, full_every=4, seg_cap=16, oe_cap=32, blk_cap=16,
+                              heap_cap=16)
+    assert stats["launches"] >= 2
+
+
+def test_gpu_generator_matches_oracle_generator():
+    p = O.gen_params(700, pct_insert=55, pct_remove=35, seed=12345)
+    n = 12
+    with fa.ReplayBatch(n) as b:
+        b.generate(fa.gen_params(700, pct_insert=55, pct_remove=35, seed=12345))
+        ops, off, text, props = b.download_log()
+        b.run()
+        for d in range(n):
+            o_ops, o_text, o_props = O.gen_doc(p, d)
+            g_ops = ops[off[d]:off[d + 1]]
+            for f in ("type", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len"):
+                assert (g_ops[f] == o_ops[f]).all(), (d, f)
+            ins = g_ops["type"] == 0
+            g_txt = np.concatenate([text[o["payload"]:o["payload"] + o["payload_len"]] for o in g_ops[ins]])
+            assert (g_txt == o_text).all()
+            od = O.replay_doc(o_ops, o_text, o_props, O.gen_tables(), O.gen_client_names(8))
+            assert b.doc(d).digest() == od.digest()
+
+
+def _msg(c, s, r, contents, msn=0):
+    return {"clientId": c, "sequenceNumber": s, "referenceSequenceNumber": r, "minimumSequenceNumber": msn,
+            "type": "op", "contents": contents}
+
+
+def test_markers_props_groups_rewrite():
+    docs = [
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "hello", "props": {"b": 1, "3": "x"}}}),
+         _msg("B", 2, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1}, "props": {"id": "m1"}}}),
+         _msg("A", 3, 1, {"type": 3, "ops": [{"type": 0, "pos1": 2, "seg": "XY"},
+                                             {"type": 2, "pos1": 0, "pos2": 4, "props": {"c": True}}]}),
+         _msg("B", 4, 3, {"type": 2, "pos1": 1, "pos2": 6, "props": {"c": None, "b": 2},
+                          "combiningOp": {"name": "rewrite"}}, msn=1),
+         _msg("A", 5, 4, {"type": 0, "pos1": 3, "seg": {"text": "e", "props": {}}}, msn=3),
+         _msg("B", 6, 5, {"type": 1, "pos1": 0, "pos2": 2}, msn=5)],
+        # removes racing an insert at the same position (issue #1213 family)
+        [_msg("1", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"}),
+         _msg("2", 2, 0, {"type": 0, "pos1": 0, "seg": "XYZ"}),
+         _msg("1", 3, 1, {"type": 1, "pos1": 1, "pos2": 3}),
+         _msg("3", 4, 1, {"type": 1, "pos1": 0, "pos2": 3}),
+         _msg("2", 5, 2, {"type": 0, "pos1": 3, "seg": "q"}),
+         _msg("3", 6, 4, {"type": 0, "pos1": 0, "seg": "r"}, msn=1)],
+        # a no-op message advances the MSN (zamboni on setMinSeq)
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "aaaa"}),
+         _msg("A", 2, 1, {"type": 0, "pos1": 4, "seg": "bbbb"}),
+         {"clientId": "A", "sequenceNumber": 3, "referenceSequenceNumber": 2, "minimumSequenceNumber": 2,
+          "type": "noop", "contents": None}],
+    ]
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        for i in range(len(docs)):
+            assert_doc_parity(b.doc(i), oracle[i])
+
+
+def test_error_statuses_match_oracle():
+    docs = [
+        [_msg("A", 1, 0, {"type": 0, "pos1": 3, "seg": "x"})],  # insert beyond the end
+        [_msg("A", 2, 0, {"type": 0, "pos1": 0, "seg": "x"}), _msg("A", 2, 0, {"type": 0, "pos1": 0, "seg": "y"})],
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "x"}), _msg("A", 2, 1, {"type": 0, "pos1": 0, "seg": "y"}, 1),
+         _msg("A", 3, 2, {"type": 0, "pos1": 0, "seg": "z"}, 0)],
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "fine"})],
+    ]
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        got = [b.doc(i).status for i in range(len(docs))]
+        assert got == [od.status for od in oracle] == [fa.MT_INVALID_POS, fa.MT_SEQ_ORDER, fa.MT_MSN_ORDER, 0]
+        assert b.doc(3).get_text() == "fine"
+
+
+def test_too_many_clients_is_flagged_not_wrong():
+    msgs = [_msg(f"c{i}", i + 1, i, {"type": 0, "pos1": 0, "seg": "x"}) for i in range(40)]
+    with fa.ReplayBatch(1) as b:
+        b.ingest_messages([msgs])
+        b.run()
+        assert b.doc(0).status == fa.MT_UNSUPPORTED
+
+
+def test_empty_documents_and_empty_inserts():
+    docs = [[], [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": ""}), _msg("A", 2, 1, {"type": 0, "pos1": 0, "seg": "k"})]]
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(2) as b:
+        b.ingest_messages(docs)
+        b.run()
+        assert b.doc(0).get_text() == "" and b.doc(0).snapshot_v1() == oracle[0].snapshot_v1()
+        assert_doc_parity(b.doc(1), oracle[1])

@@ -1,0 +1,126 @@
+"""CPU-side checks: C-ABI exports, op-log packing, generator invariants (no GPU needed)."""
+import json
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import fluidframework_amd as fa
+from fluidframework_amd import oplog
+
+ROOT = Path(__file__).resolve().parents[1]
+KATS = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+
+
+def test_library_exports_every_declared_symbol():
+    header = (ROOT / "include" / "mtreplay.h").read_text()
+    declared = set(re.findall(r"MT_API\s+[\w\s\*]+?\b(mt_\w+)\s*\(", header))
+    assert declared == set(fa.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", str(fa.mtreplay.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\sT\s(mt_\w+)$", out, re.M))
+    assert declared <= exported, f"missing: {declared - exported}"
+    # nothing else leaks out of the C ABI
+    assert exported == declared
+
+
+def test_library_fails_loudly_without_device():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(fa.MtError) as e:
+        fa.ReplayBatch(2)
+    assert e.value.code == fa.MT_ERR_NO_DEVICE
+
+
+def _oracle_from_packed(pb, d):
+    t = O.Tables(pb.keys or ["_"], pb.values)
+    a, b = pb.doc_op_off[d], pb.doc_op_off[d + 1]
+    doc = O.replay_doc(pb.ops[a:b].copy(), pb.text, pb.props, t, pb.clients[d])
+    doc._t = t
+    return doc
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_packer_roundtrip_matches_json_replay(kat):
+    """ISequencedDocumentMessage -> packed record -> oracle replay == oracle applyMsg replay."""
+    pb = oplog.pack_documents([kat["messages"]])
+    packed = _oracle_from_packed(pb, 0)
+    assert packed.status == 0, packed.error
+    ref = O.Doc()
+    ref.start_collab("readonly")
+    for m in kat["messages"]:
+        ref.apply_msg(json.dumps(m))
+    assert packed.text() == ref.text() == kat["text"]
+    assert packed.props_runs() == ref.props_runs()
+    assert packed.snapshot_v1() == ref.snapshot_v1()
+    assert packed.digest() == ref.digest()
+
+
+def unpack_messages(ops, text, props, keys, values, names):
+    """packed records -> ISequencedDocumentMessage dicts (inverse of oplog.Packer)."""
+    msgs = []
+    for o in ops:
+        t = int(o["type"])
+        m = {"clientId": names[o["client"]], "sequenceNumber": int(o["seq"]),
+             "referenceSequenceNumber": int(o["ref_seq"]), "minimumSequenceNumber": int(o["msn"]), "type": "op"}
+        if t == 0:
+            s = text[o["payload"]: o["payload"] + o["payload_len"]].tobytes().decode("utf-16-le")
+            m["contents"] = {"type": 0, "pos1": int(o["pos1"]), "seg": s}
+        elif t == 1:
+            m["contents"] = {"type": 1, "pos1": int(o["pos1"]), "pos2": int(o["pos2"])}
+        else:
+            pr = props[o["payload"]: o["payload"] + o["payload_len"]]
+            m["contents"] = {"type": 2, "pos1": int(o["pos1"]), "pos2": int(o["pos2"]),
+                             "props": {keys[p["key"]]: json.loads(values[p["value"]]) for p in pr}}
+        msgs.append(m)
+    return msgs
+
+
+def test_generator_invariants_and_message_roundtrip():
+    p = O.gen_params(600, pct_insert=55, pct_remove=35, seed=11)
+    tables, names = O.gen_tables(), O.gen_client_names(8)
+    keys = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
+    values = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
+    for dd in range(3):
+        ops, text, props = O.gen_doc(p, dd)
+        seq, ref, msn = ops["seq"], ops["ref_seq"], ops["msn"]
+        assert (seq == np.arange(1, len(ops) + 1)).all()
+        assert (np.diff(msn) >= 0).all() and (msn <= ref).all() and (ref < seq).all()
+        assert (seq - ref <= 1 + 32 + 600).all()
+        assert set(np.unique(ops["type"])) <= {0, 1, 2}
+        # replaying the packed log and the equivalent JSON messages agree bit for bit
+        d1 = O.replay_doc(ops, text, props, tables, names)
+        assert d1.status == 0, d1.error
+        d2 = O.Doc()
+        d2.start_collab("readonly")
+        for m in unpack_messages(ops, text, props, keys, values, names):
+            assert d2.apply_msg(json.dumps(m)) == 0, d2.error
+        assert d1.digest() == d2.digest()
+        assert d1.snapshot_v1() == d2.snapshot_v1()
+        # and the oplog packer reproduces the generator's records exactly
+        pb = oplog.pack_documents([unpack_messages(ops, text, props, keys, values, names)])
+        for f in ("type", "seq", "ref_seq", "msn", "pos1"):
+            assert (pb.ops[f] == ops[f]).all()
+
+
+def test_generator_is_deterministic():
+    p = O.gen_params(300, seed=5)
+    a = O.gen_doc(p, 3)
+    b = O.gen_doc(p, 3)
+    assert all((x == y).all() for x, y in zip(a, b))
+    c = O.gen_doc(p, 4)
+    assert not (a[0] == c[0]).all()
+
+
+def test_batch_replay_threads_agree():
+    p = O.gen_params(400, seed=9)
+    ops, text, props, off = O.gen_batch(p, 12)
+    t, names = O.gen_tables(), O.gen_client_names(8)
+    _, d1, s1 = O.replay_batch(ops, off, text, props, t, names, n_threads=1)
+    _, d4, s4 = O.replay_batch(ops, off, text, props, t, names, n_threads=4)
+    assert (s1 == 0).all() and (d1 == d4).all()

@@ -1,0 +1,119 @@
+"""Pin the oracle (CPU restatement) against the reference's own fixtures.
+
+* SnapshotV1 golden files (sequence/src/test/snapshots/v1/*.json, byte-checked by the
+  reference in snapshotVersion.spec.ts:86-105), regenerated with the recipe of
+  generateSharedStrings.ts:24-97 through the non-collaborating local edit path.
+* Known-answer observer scenarios (tests/golden/kats.json, see make_kats.py for sources).
+"""
+import json
+from pathlib import Path
+
+import pytest
+
+import oracle_ffi as O
+
+GOLDEN = Path(__file__).with_name("golden")
+SNAP = json.loads((GOLDEN / "snapshot_v1.json").read_text())
+KATS = json.loads((GOLDEN / "kats.json").read_text())
+
+
+def build_recipe(r) -> O.Doc:
+    d = O.Doc()
+    for i in range(r["inserts"]):
+        assert d.insert_local(0, json.dumps(r["fmt"] % i)) == 0, d.error
+    if "markers_every" in r:
+        i = 0
+        while i < d.length():
+            seg = '{"marker":{"refType":%d},"props":%s}' % (r["marker_ref_type"], r["marker_props"] % i)
+            assert d.insert_local(i, seg) == 0, d.error
+            i += r["markers_every"]
+    if "annotate_every" in r:
+        i = 0
+        while i < d.length():
+            assert d.annotate_local(i, i + r["annotate_len"], r["annotate_props"]) == 0, d.error
+            i += r["annotate_every"]
+    return d
+
+
+@pytest.mark.parametrize("name", sorted(SNAP))
+def test_snapshot_v1_golden_bytes(name):
+    fx = SNAP[name]
+    d = build_recipe(fx["recipe"])
+    blobs = d.snapshot_v1()
+    assert list(blobs) == [p for p, _ in fx["blobs"]]
+    for path, contents in fx["blobs"]:
+        assert blobs[path] == contents, f"{name}/{path} differs from the reference golden file"
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_observer_kats(kat):
+    d = O.Doc()
+    d.start_collab("readonly")
+    for m in kat["messages"]:
+        assert d.apply_msg(json.dumps(m)) == 0, d.error
+    assert d.text() == kat["text"]
+    if "props_runs" in kat:
+        assert json.loads(d.props_runs()) == kat["props_runs"]
+
+
+def test_snapshot_chunking_and_merge_info():
+    """SnapshotV1 with a collaborating tree: merge info for segments above the MSN,
+    elision of removals at/below it, 10000-char chunking (snapshotV1.ts:57-79,151-247)."""
+    d = O.Doc()
+    d.start_collab("readonly")
+    seq = 0
+    for i in range(1200):
+        seq += 1
+        m = {"clientId": "A" if i % 2 else "B", "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
+             "minimumSequenceNumber": max(0, seq - 30), "type": "op",
+             "contents": {"type": 0, "pos1": 0, "seg": "abcdefghij"}}
+        assert d.apply_msg(json.dumps(m)) == 0, d.error
+    seq += 1
+    rm = {"clientId": "B", "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
+          "minimumSequenceNumber": seq - 30, "type": "op", "contents": {"type": 1, "pos1": 5, "pos2": 25}}
+    assert d.apply_msg(json.dumps(rm)) == 0
+    blobs = d.snapshot_v1()
+    hdr = json.loads(blobs["header"])
+    assert hdr["headerMetadata"]["minSequenceNumber"] == seq - 30
+    assert hdr["headerMetadata"]["sequenceNumber"] == seq
+    assert hdr["headerMetadata"]["totalLength"] == 12000
+    assert [c["id"] for c in hdr["headerMetadata"]["orderedChunkMetadata"]] == list(blobs)
+    seg0 = hdr["segments"][0]
+    assert seg0["json"] == "abcde" and seg0["seq"] == seq - 1 and seg0["client"] == "A"
+    assert hdr["segments"][1]["removedSeq"] == seq and hdr["segments"][1]["removedClient"] == "B"
+    total = 0
+    for name, blob in blobs.items():
+        c = json.loads(blob)
+        assert c["length"] == sum(len(s["json"] if isinstance(s, dict) else s) for s in c["segments"])
+        total += c["length"]
+    assert total == hdr["headerMetadata"]["totalLength"]
+
+
+def test_invalid_insert_position_status():
+    d = O.Doc()
+    d.start_collab("readonly")
+    m = {"clientId": "A", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+         "type": "op", "contents": {"type": 0, "pos1": 5, "seg": "x"}}
+    assert d.apply_msg(json.dumps(m)) == 1  # MergeTree insert failed
+    assert "MergeTree insert failed" in d.error
+
+
+def test_sequence_order_violation_status():
+    d = O.Doc()
+    d.start_collab("readonly")
+    mk = lambda s, ms=0: json.dumps({"clientId": "A", "sequenceNumber": s, "referenceSequenceNumber": 0,
+                                     "minimumSequenceNumber": ms, "type": "op",
+                                     "contents": {"type": 0, "pos1": 0, "seg": "x"}})
+    assert d.apply_msg(mk(2)) == 0
+    assert d.apply_msg(mk(2)) == 2
+
+
+def test_msn_backwards_status():
+    d = O.Doc()
+    d.start_collab("readonly")
+    mk = lambda s, ms: json.dumps({"clientId": "A", "sequenceNumber": s, "referenceSequenceNumber": s - 1,
+                                   "minimumSequenceNumber": ms, "type": "op",
+                                   "contents": {"type": 0, "pos1": 0, "seg": "x"}})
+    assert d.apply_msg(mk(1, 0)) == 0
+    assert d.apply_msg(mk(2, 1)) == 0
+    assert d.apply_msg(mk(3, 0)) == 3
