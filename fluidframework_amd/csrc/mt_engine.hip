@@ -83,6 +83,9 @@ struct Engine {
     int32_t n_oe, slot_top, n_free, blk_top, n_bfree, root, depth, hn;
     int32_t min_seq, cur_seq, status;
     uint32_t arena_top, pool_top;
+    uint32_t pay_end, arena_base, arena_end, semi_t;  // text: payload | semispace A | semispace B
+    uint32_t pool_base, pool_end, semi_p;             // prop pool: [0] reserved | A | B
+    int32_t pool_gcs;
     int32_t max_oe, max_heap;
     // ---- global
     uint16_t *text;
@@ -379,15 +382,97 @@ struct Engine {
     __device__ void text_copy(uint32_t dst, uint32_t src, uint32_t n) {
         for (uint32_t i = lane; i < n; i += kWave) text[dst + i] = text[src + i];
     }
+    // Bump allocation in the active text semispace; when it is full, live text moves to the
+    // other semispace (text_gc) and the garbage left by reallocating merges is dropped.
     __device__ uint32_t arena_alloc(uint32_t n) {
         uint32_t n16 = (n + 15u) & ~15u;
-        if (arena_top + n16 > text_cap) {
-            cap_fail(2);
-            return 0;
+        if (arena_top + n16 > arena_end) {
+            text_gc();
+            if (arena_top + n16 > arena_end) {
+                cap_fail(2);
+                return 0;
+            }
         }
         uint32_t o = arena_top;
         arena_top += n16;
         return o;
+    }
+
+    // copy every linked segment's arena text into the other semispace (document order)
+    __device__ void text_gc() {
+        uint32_t nb = arena_base == pay_end ? pay_end + semi_t : pay_end;
+        uint32_t top = nb;
+        wsync();
+        for (int32_t base = 0; base < n_oe; base += kWave) {
+            int32_t j = base + lane;
+            uint32_t slot = j < n_oe ? (oe[j] & 0xFFFFu) : kMarkerSlot;
+            bool mv = false;
+            if (slot != kMarkerSlot) {
+                uint32_t t = s_toff[slot];
+                mv = !(s_meta[slot] & kMetaMarker) && t >= arena_base && t < arena_end;
+            }
+            uint64_t m = ballot(mv);
+            while (m) {
+                int f = first_lane(m);
+                m &= m - 1;
+                uint32_t sl = rdl(slot, f);
+                uint32_t len = s_len[sl];
+                uint32_t cap16 = (len + 15u) & ~15u;
+                if (cap16 == 0) cap16 = 16;
+                if (top + cap16 > nb + semi_t) {
+                    cap_fail(2);
+                    return;
+                }
+                text_copy(top, s_toff[sl], len);
+                s_toff[sl] = top;
+                s_tcap[sl] = cap16;
+                top += cap16;
+            }
+            wsync();
+        }
+        arena_base = nb;
+        arena_end = nb + semi_t;
+        arena_top = top;
+        wsync();
+    }
+
+    // make room for `words` in the prop pool (semispace copy of the live sets when full)
+    __device__ void pool_reserve(uint32_t words) {
+        if (pool_top + words <= pool_end) return;
+        uint32_t nb = pool_base == 1u ? 1u + semi_p : 1u;
+        uint32_t top = nb, last_old = 0, last_new = 0;
+        wsync();
+        for (int32_t base = 0; base < n_oe; base += kWave) {
+            int32_t j = base + lane;
+            uint32_t slot = j < n_oe ? (oe[j] & 0xFFFFu) : kMarkerSlot;
+            bool mv = slot != kMarkerSlot && s_props[slot] != 0u;
+            uint64_t m = ballot(mv);
+            while (m) {
+                int f = first_lane(m);
+                m &= m - 1;
+                uint32_t sl = rdl(slot, f);
+                uint32_t old = s_props[sl];
+                if (old != last_old) {
+                    uint32_t w = 2u + 2u * pool[old];
+                    if (top + w > nb + semi_p) {
+                        cap_fail(3);
+                        return;
+                    }
+                    for (uint32_t i = lane; i < w; i += kWave) pool[top + i] = pool[old + i];
+                    last_old = old;
+                    last_new = top;
+                    top += w;
+                }
+                s_props[sl] = last_new;
+            }
+            wsync();
+        }
+        pool_base = nb;
+        pool_end = nb + semi_p;
+        pool_top = top;
+        pool_gcs++;
+        wsync();
+        if (pool_top + words > pool_end) cap_fail(3);
     }
 
     // ------------------------------------------------------------------ block tree
@@ -679,7 +764,7 @@ struct Engine {
             }
         }
         uint32_t words = 2 + 2 * n;
-        if (pool_top + words > pool_cap) {
+        if (pool_top + words > pool_end) {
             cap_fail(3);
             return 0;
         }
@@ -730,11 +815,22 @@ struct Engine {
                     // TextSegment.append: prev.text += segment.text
                     uint32_t pl = s_len[prev], sl = s_len[slot];
                     uint32_t need = pl + sl;
-                    if (s_tcap[prev] >= need) {
-                        text_copy(s_toff[prev] + pl, s_toff[slot], sl);
+                    uint32_t ptoff = s_toff[prev], stoff = s_toff[slot], pcap = s_tcap[prev];
+                    if (pcap == pl && ptoff + pl == stoff) {
+                        // texts already adjacent (split halves, consecutive payloads): take over the region
+                        s_tcap[prev] = pl + s_tcap[slot];
+                    } else if (pcap >= need) {
+                        text_copy(ptoff + pl, stoff, sl);
+                    } else if (ptoff >= arena_base && ptoff < arena_end && ptoff + pcap == arena_top &&
+                               ptoff + ((2u * need + 15u) & ~15u) <= arena_end) {
+                        // last allocation of the arena: grow in place
+                        uint32_t ncap = (2u * need + 15u) & ~15u;
+                        arena_top = ptoff + ncap;
+                        s_tcap[prev] = ncap;
+                        text_copy(ptoff + pl, stoff, sl);
                     } else {
                         uint32_t ncap = 2 * need;
-                        uint32_t dst = arena_alloc(ncap);
+                        uint32_t dst = arena_alloc(ncap);  // may compact: offsets re-read below
                         if (status) return nh;
                         text_copy(dst, s_toff[prev], pl);
                         text_copy(dst + pl, s_toff[slot], sl);
@@ -932,6 +1028,8 @@ struct Engine {
             if (slot < 0) return;
             uint32_t props = 0, ph = 0;
             if (op.flags & MT_OPF_HAS_PROPS) {
+                pool_reserve(2u + 2u * MT_OPF_NPROPS(op.flags));
+                if (status) return;
                 props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
                 if (status) return;
             }
@@ -1003,6 +1101,10 @@ struct Engine {
                 uint32_t slot = e2 & 0xFFFFu;
                 int32_t blk = (int32_t)(e2 >> 16);
                 if (!is_remove) {
+                    int32_t g0 = pool_gcs;
+                    pool_reserve(2u + 2u * (64u + op.payload_len));
+                    if (status) return;
+                    if (pool_gcs != g0) memo_n = 0;  // ids moved
                     uint32_t old = s_props[slot];
                     uint64_t mb = ballot((uint32_t)lane < memo_n && memo_old == old);
                     uint32_t nid, nh;
@@ -1142,10 +1244,18 @@ __device__ void engine_setup(Engine &E, const ReplayParams &P, int64_t d, uint8_
     E.carve(smem, P.caps);
     E.text = P.text + P.doc_text_base[d];
     E.text_cap = P.doc_text_cap[d];
-    E.arena_top = (P.doc_text_len[d] + 15u) & ~15u;
+    E.pay_end = (P.doc_text_len[d] + 15u) & ~15u;
+    E.semi_t = E.text_cap > E.pay_end ? ((E.text_cap - E.pay_end) / 2u) & ~15u : 0u;
+    E.arena_base = E.pay_end;
+    E.arena_end = E.pay_end + E.semi_t;
+    E.arena_top = E.pay_end;
     E.pool = P.pool + P.doc_pool_base[d];
     E.pool_cap = P.doc_pool_cap[d];
-    E.pool_top = 1;  // id 0 = undefined
+    E.semi_p = E.pool_cap > 1u ? (E.pool_cap - 1u) / 2u : 0u;
+    E.pool_base = 1;  // id 0 = undefined
+    E.pool_end = 1 + E.semi_p;
+    E.pool_top = 1;
+    E.pool_gcs = 0;
     E.props_in = (const mt_prop *)P.props_in;
     E.value_flags = P.value_flags;
     E.n_values = P.n_values;

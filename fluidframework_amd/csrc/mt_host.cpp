@@ -1061,6 +1061,37 @@ MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out) {
     return MT_OK;
 }
 
+// debugging aid: one line per oe entry (segment fields or end-of-block marker)
+MT_API int mt_doc_dump(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len) {
+    if (!b) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    std::string o = "status=" + std::to_string(b->c_out.status) + " min=" + std::to_string(b->c_out.min_seq) +
+                    " cur=" + std::to_string(b->c_out.cur_seq) + " depth=" + std::to_string(b->c_out.depth) +
+                    " ops_done=" + std::to_string(b->c_out.ops_done) + " fail_op=" + std::to_string(b->c_out.fail_op) +
+                    " cap_kind=" + std::to_string(b->c_out.cap_kind) + "\n";
+    std::string tmp;
+    for (const OutRec &r : b->c_recs) {
+        if (rec_is_marker(r)) {
+            o += "  M blk=" + std::to_string(r.blk >> 16) + "\n";
+            continue;
+        }
+        o += "  S blk=" + std::to_string(r.blk >> 16) + " len=" + std::to_string(r.len) + " seq=" + std::to_string(r.seq) +
+             " cli=" + client_name(b, doc, r.meta & 63u, tmp) +
+             " rseq=" + std::to_string(rec_removed(r) ? r.rseq : -1) + " rcli=" +
+             (rec_removed(r) ? client_name(b, doc, (r.meta >> 6) & 63u, tmp) : std::string("-")) +
+             " ovl=" + std::to_string(r.ovl) + " '";
+        if (rec_is_text(r)) utf16_to_utf8(o, b->c_text.data() + r.toff, r.len);
+        o += "'";
+        if (r.props) {
+            o += " ";
+            props_json(b, r.props, o);
+        }
+        o += "\n";
+    }
+    return out_str(o, buf, cap, len);
+}
+
 // ---------------------------------------------------------------- logs
 MT_API int mt_batch_log_sizes(mt_batch *b, int64_t *n_ops, int64_t *n_text, int64_t *n_props) {
     if (!b || !b->have_log) return MT_ERR_STATE;

@@ -34,7 +34,7 @@ EXPORTS = [
     "mt_status_string", "mt_batch_create", "mt_batch_destroy", "mt_batch_set_tables", "mt_batch_set_clients",
     "mt_batch_ingest", "mt_batch_generate", "mt_batch_run", "mt_batch_launch", "mt_batch_sync",
     "mt_batch_get_stats", "mt_batch_algorithmic_bytes", "mt_doc_status", "mt_doc_text", "mt_doc_props_runs",
-    "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_batch_log_sizes",
+    "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
     "mt_batch_download_log",
 ]
 
@@ -103,7 +103,7 @@ def lib():
     L.mt_batch_algorithmic_bytes.argtypes = [vp, P(C.c_double)]
     L.mt_doc_status.argtypes = [vp, i64]
     L.mt_doc_status.restype = i32
-    for fn in ("mt_doc_text", "mt_doc_props_runs", "mt_doc_shape"):
+    for fn in ("mt_doc_text", "mt_doc_props_runs", "mt_doc_shape", "mt_doc_dump"):
         getattr(L, fn).argtypes = [vp, i64, C.c_char_p, i64, P(i64)]
     L.mt_doc_snapshot_v1.argtypes = [vp, i64, P(i32)]
     L.mt_doc_snapshot_blob.argtypes = [vp, i64, i32, C.c_char_p, i64, C.c_char_p, i64, P(i64)]
@@ -161,6 +161,9 @@ class DocView:
 
     def shape(self) -> str:
         return self._string(lib().mt_doc_shape)
+
+    def dump(self) -> str:
+        return self._string(lib().mt_doc_dump)
 
     def digest(self) -> int:
         out = C.c_uint64(0)

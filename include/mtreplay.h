@@ -117,6 +117,8 @@ MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name,
                                 int64_t cap, int64_t *len);
 MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out);
 MT_API int mt_doc_shape(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
+/* debugging aid: the final segment table, one line per entry */
+MT_API int mt_doc_dump(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
 
 /* the (ingested or generated) log in host memory, batch-global offsets (CPU baseline / parity) */
 MT_API int mt_batch_log_sizes(mt_batch *b, int64_t *n_ops, int64_t *n_text, int64_t *n_props);

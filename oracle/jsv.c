@@ -83,10 +83,15 @@ jv *jv_new_str_ascii(const char *s) {
     v->slen = n;
     return v;
 }
-jv *jv_ref(jv *v) { if (v) v->rc++; return v; }
+/* refcounts are atomic: property values from mto_tables are shared by the worker threads
+   of mto_replay_batch */
+jv *jv_ref(jv *v) {
+    if (v) __atomic_add_fetch(&v->rc, 1, __ATOMIC_RELAXED);
+    return v;
+}
 void jv_unref(jv *v) {
     if (!v) return;
-    if (--v->rc > 0) return;
+    if (__atomic_sub_fetch(&v->rc, 1, __ATOMIC_ACQ_REL) > 0) return;
     free(v->s);
     for (int i = 0; i < v->n; i++) {
         jv_unref(v->vals[i]);

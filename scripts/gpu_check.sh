@@ -14,10 +14,12 @@ run() {
 }
 for step in "$@"; do
   case "$step" in
-    tests) run tests 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    tests) run tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 300 python -u __graft_entry__.py smoke ;;
     bench) run bench 600 python -u bench.py --steps 3 --warmup 1 ;;
     bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
+    bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
+    bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
     *) echo "unknown step $step" ;;
   esac
 done
