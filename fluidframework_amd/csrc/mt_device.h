@@ -108,6 +108,8 @@ struct ReplayParams {
     const void *gen;              // mt_gen_params*
     void *gen_ops;                // mt_op[n_docs * n_ops]
     void *gen_props;              // mt_prop[n_docs * 2 * n_ops] (doc-local offsets rebased by host)
+    uint64_t *prof;               // MT_PROF builds: kProfSlots cycle counters per workgroup
 };
+constexpr int kProfSlots = 8;
 
 }  // namespace mt

@@ -30,26 +30,35 @@
 
 namespace mt {
 
+#define MT_FI __device__ __attribute__((always_inline)) inline
+
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int32_t rfl(int32_t x) { return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)x); }
 __device__ __forceinline__ uint32_t rdl(uint32_t x, int l) { return __builtin_amdgcn_readlane(x, l); }
 __device__ __forceinline__ int32_t rdl(int32_t x, int l) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)x, l); }
 
+// wave64 inclusive prefix sum on DPP (GFX9 row_shr + row_bcast): no LDS round trips
 __device__ __forceinline__ uint32_t scan_incl(uint32_t v) {
-    const int l = threadIdx.x;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        uint32_t t = __shfl_up(v, o, kWave);
-        if (l >= o) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int first_lane(uint64_t b) { return __builtin_ctzll(b); }
 
-// single-wave workgroup: orders LDS traffic between lanes
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// Lane-to-lane ordering inside the single wave that owns a document.  A wavefront's LDS and
+// vector-memory instructions execute and complete in program order (AMDGPU memory model:
+// wavefront scope needs no waits), so only the compiler must be kept from reordering
+// accesses across the point: no s_waitcnt, no s_barrier.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ uint32_t hash_pair(uint32_t k, uint32_t v) {
     uint32_t h = k * 0x9E3779B1u ^ (v + 0x7F4A7C15u) * 0x85EBCA77u;
@@ -58,6 +67,20 @@ __device__ __forceinline__ uint32_t hash_pair(uint32_t k, uint32_t v) {
     h ^= h >> 12;
     return h | 1u;
 }
+
+// Phase cycle counters (MT_PROF builds only; tools/prof_phases.py): 0 kernel, 1 scans,
+// 2 split, 3 insert, 4 range walk, 5 zamboni, 6 oe shifts, 7 scour
+#ifdef MT_PROF
+struct PfScope {
+    uint64_t &acc;
+    uint64_t t0;
+    __device__ explicit PfScope(uint64_t &a) : acc(a), t0(clock64()) {}
+    __device__ ~PfScope() { acc += clock64() - t0; }
+};
+#define PF_SCOPE(k) PfScope _pf_scope(pf[k])
+#else
+#define PF_SCOPE(k) (void)0
+#endif
 
 struct Loc {
     int32_t idx;    // oe index
@@ -86,7 +109,12 @@ struct Engine {
     uint32_t pay_end, arena_base, arena_end, semi_t;  // text: payload | semispace A | semispace B
     uint32_t pool_base, pool_end, semi_p;             // prop pool: [0] reserved | A | B
     int32_t pool_gcs;
+    // ends-with-'\n' of a split's left half, resolved after the op's LDS work so the text load
+    // latency overlaps it (at most two splits per op)
+    int32_t pend_n;
+    uint32_t pend_slot0, pend_slot1, pend_ch0, pend_ch1;
     int32_t max_oe, max_heap;
+    int32_t split_mark;  // oe index of the end marker the last leaf split inserted, -1: none
     // ---- global
     uint16_t *text;
     uint32_t text_cap;
@@ -96,6 +124,9 @@ struct Engine {
     const uint8_t *value_flags;
     uint32_t n_values;
     int lane;
+#ifdef MT_PROF
+    uint64_t pf[kProfSlots];
+#endif
 
     // ------------------------------------------------------------------ layout
     __device__ static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -116,7 +147,7 @@ struct Engine {
         take(4u * 256);
         return o;
     }
-    __device__ void carve(uint8_t *base, const Caps &c) {
+    MT_FI void carve(uint8_t *base, const Caps &c) {
         size_t o = 0;
         auto take = [&](size_t n) {
             uint8_t *p = base + o;
@@ -147,10 +178,10 @@ struct Engine {
     }
 
     int32_t cap_kind;
-    __device__ void set_fail(int32_t st) {
+    MT_FI void set_fail(int32_t st) {
         if (status == ST_OK) status = st;
     }
-    __device__ void cap_fail(int32_t kind) {
+    MT_FI void cap_fail(int32_t kind) {
         if (status == ST_OK) {
             status = ST_CAPACITY;
             cap_kind = kind;
@@ -158,7 +189,7 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ init
-    __device__ void init() {
+    MT_FI void init() {
         n_oe = 0;
         slot_top = 0;
         n_free = 0;
@@ -169,6 +200,8 @@ struct Engine {
         cur_seq = 0;
         status = ST_OK;
         cap_kind = 0;
+        pend_n = 0;
+        split_mark = -1;
         max_oe = 0;
         max_heap = 0;
         // initialNode (mergeTree.ts:1125): an empty root leaf block
@@ -183,7 +216,7 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ allocation
-    __device__ int32_t alloc_slot() {
+    MT_FI int32_t alloc_slot() {
         int32_t s;
         if (n_free > 0) {
             s = rfl((int32_t)s_free[n_free - 1]);
@@ -198,14 +231,14 @@ struct Engine {
         }
         return s;
     }
-    __device__ void free_slot(int32_t s) {
+    MT_FI void free_slot(int32_t s) {
         uint32_t m = s_meta[s];
         uint32_t gen = (m >> 16) + 1;
         s_meta[s] = (gen << 16);  // unlinked, next generation
         s_free[n_free] = (uint16_t)s;
         n_free++;
     }
-    __device__ int32_t alloc_block(int leaf) {
+    MT_FI int32_t alloc_block(int leaf) {
         int32_t b;
         if (n_bfree > 0) {
             b = rfl((int32_t)b_free[n_bfree - 1]);
@@ -223,14 +256,15 @@ struct Engine {
         b_parent[b] = 0xFFFF;
         return b;
     }
-    __device__ void free_block(int32_t b) {
+    MT_FI void free_block(int32_t b) {
         b_free[n_bfree] = (uint16_t)b;
         n_bfree++;
     }
 
     // ------------------------------------------------------------------ oe shifting
     // insert entry e before index p (lane-parallel shift right by one)
-    __device__ void oe_insert(int32_t p, uint32_t e) {
+    MT_FI void oe_insert(int32_t p, uint32_t e) {
+        PF_SCOPE(6);
         if (n_oe + 1 > cap.oe) {
             cap_fail(1);
             return;
@@ -251,7 +285,8 @@ struct Engine {
         wsync();
     }
     // move oe[from, n_oe) to start at `to` (to < from: left shift; to > from: right shift)
-    __device__ void oe_move_tail(int32_t from, int32_t to) {
+    MT_FI void oe_move_tail(int32_t from, int32_t to) {
+        PF_SCOPE(6);
         int32_t cnt = n_oe - from;
         int32_t new_n = to + cnt;
         if (new_n > cap.oe) {
@@ -308,14 +343,16 @@ struct Engine {
     }
 
     // insertingWalk target for pos under (ref, c): see header comment
-    __device__ Loc locate(uint32_t pos, int32_t ref, uint32_t c) {
+    // Scanning may start at any index `from` whose view position `carry` is known and before
+    // which no entry satisfies the walk's stop condition.
+    MT_FI Loc locate(uint32_t pos, int32_t ref, uint32_t c, int32_t from = 0, uint32_t carry = 0) {
+        PF_SCOPE(1);
         Loc L;
         L.found = 0;
         L.idx = -1;
         L.excl = 0;
         L.marker = 0;
-        uint32_t carry = 0;
-        for (int32_t base = 0; base < n_oe; base += kWave) {
+        for (int32_t base = from; base < n_oe; base += kWave) {
             int32_t j = base + lane;
             bool valid = j < n_oe;
             uint32_t vlen = 0;
@@ -339,8 +376,41 @@ struct Engine {
         return L;
     }
 
+    // the visible segment strictly containing pos (excl < pos < excl + vlen) at or after `from`:
+    // the one ensureIntervalBoundary splits.  found = 0 when pos is already a boundary.
+    MT_FI Loc containing(uint32_t pos, int32_t ref, uint32_t c, int32_t from, uint32_t carry) {
+        PF_SCOPE(1);
+        Loc L;
+        L.found = 0;
+        L.idx = -1;
+        L.excl = 0;
+        L.marker = 0;
+        for (int32_t base = from; base < n_oe; base += kWave) {
+            int32_t j = base + lane;
+            bool valid = j < n_oe;
+            uint32_t vlen = 0;
+            bool tie = false, mk = false;
+            if (valid) view_of(oe[j], ref, c, vlen, tie, mk);
+            uint32_t incl = scan_incl(vlen) + carry;
+            uint32_t excl = incl - vlen;
+            uint64_t b = ballot(valid && incl > pos);
+            if (b) {
+                int f = first_lane(b);
+                uint32_t e = rdl(excl, f);
+                if (e < pos) {
+                    L.found = 1;
+                    L.idx = base + f;
+                    L.excl = e;
+                }
+                return L;
+            }
+            carry = rdl(incl, 63);
+        }
+        return L;
+    }
+
     // MergeTree.getLength(refSeq, clientId) (generator)
-    __device__ uint32_t view_length(int32_t ref, uint32_t c) {
+    MT_FI uint32_t view_length(int32_t ref, uint32_t c) {
         uint32_t carry = 0;
         for (int32_t base = 0; base < n_oe; base += kWave) {
             int32_t j = base + lane;
@@ -353,7 +423,7 @@ struct Engine {
     }
 
     // first oe index with entry predicate; kind 0: slot == key, kind 1: block == key
-    __device__ int32_t find_entry(uint32_t key, int kind, int32_t from = 0) {
+    MT_FI int32_t find_entry(uint32_t key, int kind, int32_t from = 0) {
         for (int32_t base = from; base < n_oe; base += kWave) {
             int32_t j = base + lane;
             bool hit = false;
@@ -367,7 +437,7 @@ struct Engine {
         return -1;
     }
     // first index of block `blk`'s range, given an index inside it (ranges are <= 9 entries)
-    __device__ int32_t block_start_near(uint32_t blk, int32_t inside) {
+    MT_FI int32_t block_start_near(uint32_t blk, int32_t inside) {
         int32_t j = inside - 8 + lane;
         bool hit = lane < 17 && j >= 0 && j < n_oe && (oe[j] >> 16) == blk;
         uint64_t b = ballot(hit);
@@ -375,16 +445,16 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ text helpers
-    __device__ bool text_ends_nl(uint32_t toff, uint32_t len) const {
+    MT_FI bool text_ends_nl(uint32_t toff, uint32_t len) const {
         return len > 0 && text[toff + len - 1] == (uint16_t)'\n';
     }
     // lane-parallel copy of n code units inside the doc's text region
-    __device__ void text_copy(uint32_t dst, uint32_t src, uint32_t n) {
+    MT_FI void text_copy(uint32_t dst, uint32_t src, uint32_t n) {
         for (uint32_t i = lane; i < n; i += kWave) text[dst + i] = text[src + i];
     }
     // Bump allocation in the active text semispace; when it is full, live text moves to the
     // other semispace (text_gc) and the garbage left by reallocating merges is dropped.
-    __device__ uint32_t arena_alloc(uint32_t n) {
+    MT_FI uint32_t arena_alloc(uint32_t n) {
         uint32_t n16 = (n + 15u) & ~15u;
         if (arena_top + n16 > arena_end) {
             text_gc();
@@ -399,7 +469,7 @@ struct Engine {
     }
 
     // copy every linked segment's arena text into the other semispace (document order)
-    __device__ void text_gc() {
+    MT_FI void text_gc() {
         uint32_t nb = arena_base == pay_end ? pay_end + semi_t : pay_end;
         uint32_t top = nb;
         wsync();
@@ -437,7 +507,7 @@ struct Engine {
     }
 
     // make room for `words` in the prop pool (semispace copy of the live sets when full)
-    __device__ void pool_reserve(uint32_t words) {
+    MT_FI void pool_reserve(uint32_t words) {
         if (pool_top + words <= pool_end) return;
         uint32_t nb = pool_base == 1u ? 1u + semi_p : 1u;
         uint32_t top = nb, last_old = 0, last_new = 0;
@@ -476,7 +546,7 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ block tree
-    __device__ int32_t child_index(int32_t p, int32_t c) {
+    MT_FI int32_t child_index(int32_t p, int32_t c) {
         int32_t n = b_count[p];
         bool hit = lane < n && b_child[p * 8 + lane] == (uint16_t)c;
         uint64_t b = ballot(hit);
@@ -484,7 +554,7 @@ struct Engine {
     }
 
     // updateRoot (mergeTree.ts:1876-1887)
-    __device__ void update_root(int32_t split_node) {
+    MT_FI void update_root(int32_t split_node) {
         int32_t nr = alloc_block(0);
         if (status) return;
         b_child[nr * 8 + 0] = (uint16_t)root;
@@ -498,7 +568,7 @@ struct Engine {
 
     // insertingWalk's "insert the split-off node after its source" (mergeTree.ts:2446-2453),
     // cascading MergeTree.split (2476-2489) up the interior levels and updateRoot at the top.
-    __device__ void insert_child_after(int32_t p, int32_t after, int32_t nc) {
+    MT_FI void insert_child_after(int32_t p, int32_t after, int32_t nc) {
         for (;;) {
             int32_t i = child_index(p, after);
             int32_t n = b_count[p];
@@ -538,7 +608,7 @@ struct Engine {
 
     // MergeTree.split on a leaf block whose range starts at s and now holds 8 children.
     // Returns the new right block.
-    __device__ int32_t split_leaf(int32_t blk, int32_t s) {
+    MT_FI int32_t split_leaf(int32_t blk, int32_t s) {
         int32_t nb = alloc_block(1);
         if (status) return blk;
         wsync();
@@ -550,6 +620,7 @@ struct Engine {
         wsync();
         b_count[nb] = 4;
         b_count[blk] = 4;
+        split_mark = s + 4;
         oe_insert(s + 4, ((uint32_t)blk << 16) | kMarkerSlot);
         if (status) return nb;
         if (blk == root) update_root(nb);
@@ -560,7 +631,7 @@ struct Engine {
     // ------------------------------------------------------------------ split / insert leaves
     // insert a leaf before oe index idx into the leaf block owning oe[idx]; returns the
     // block the new leaf ends up in (after a possible split)
-    __device__ int32_t insert_leaf(int32_t idx, uint32_t slot) {
+    MT_FI int32_t insert_leaf(int32_t idx, uint32_t slot) {
         uint32_t blk = rfl(oe[idx] >> 16);
         oe_insert(idx, (blk << 16) | slot);
         if (status) return (int32_t)blk;
@@ -577,14 +648,25 @@ struct Engine {
 
     // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568,
     // textSegment.ts:103-111): the right part becomes a new leaf right after the left one
-    __device__ void split_at(int32_t idx, uint32_t r) {
+    // Returns the left half's oe index afterwards (a leaf split may insert an end marker before it).
+    MT_FI int32_t split_at(int32_t idx, uint32_t r) {
+        PF_SCOPE(2);
+        split_mark = -1;
         uint32_t slot = rfl(oe[idx] & 0xFFFFu);
         uint32_t meta = s_meta[slot];
-        if (meta & kMetaMarker) return;  // Marker.createSplitSegmentAt returns undefined
+        if (meta & kMetaMarker) return idx;  // Marker.createSplitSegmentAt returns undefined
         int32_t ns = alloc_slot();
-        if (ns < 0) return;
+        if (ns < 0) return idx;
         uint32_t len = s_len[slot], toff = s_toff[slot], tcap = s_tcap[slot];
-        bool left_nl = text_ends_nl(toff, r);
+        uint32_t last = text[toff + r - 1];  // consumed in resolve_splits()
+        if (pend_n == 0) {
+            pend_slot0 = slot;
+            pend_ch0 = last;
+        } else {
+            pend_slot1 = slot;
+            pend_ch1 = last;
+        }
+        pend_n++;
         s_len[ns] = len - r;
         s_seq[ns] = s_seq[slot];
         s_rseq[ns] = s_rseq[slot];
@@ -597,19 +679,29 @@ struct Engine {
         s_meta[ns] = (meta & 0x0000FFFFu) | gen;  // inherits ends-NL of the original tail
         s_len[slot] = r;
         s_tcap[slot] = r;
-        s_meta[slot] = left_nl ? (meta | kMetaEndsNL) : (meta & ~kMetaEndsNL);
         wsync();
         insert_leaf(idx + 1, (uint32_t)ns);
+        return shifted(idx);
+    }
+    // index of a pre-split entry at or before the split point after the last split_at
+    MT_FI int32_t shifted(int32_t i) const { return (split_mark >= 0 && split_mark <= i) ? i + 1 : i; }
+
+    MT_FI void resolve_splits() {
+        if (pend_n > 0) {
+            uint32_t m = s_meta[pend_slot0];
+            s_meta[pend_slot0] = pend_ch0 == (uint32_t)'\n' ? (m | kMetaEndsNL) : (m & ~kMetaEndsNL);
+        }
+        if (pend_n > 1) {
+            uint32_t m = s_meta[pend_slot1];
+            s_meta[pend_slot1] = pend_ch1 == (uint32_t)'\n' ? (m | kMetaEndsNL) : (m & ~kMetaEndsNL);
+        }
+        pend_n = 0;
+        wsync();
     }
 
-    // ensureIntervalBoundary (mergeTree.ts:2241-2245)
-    __device__ void ensure_boundary(uint32_t pos, int32_t ref, uint32_t c) {
-        Loc L = locate(pos, ref, c);
-        if (L.found && !L.marker && L.excl < pos) split_at(L.idx, pos - L.excl);
-    }
 
     // addToLRUSet (mergeTree.ts:1273-1283); seq > currentSeq holds for sequenced remote ops
-    __device__ void add_to_lru(int32_t blk, uint32_t slot, int32_t seq) {
+    MT_FI void add_to_lru(int32_t blk, uint32_t slot, int32_t seq) {
         if (b_scour[blk] != kScourTrue && seq > cur_seq) {
             b_scour[blk] = kScourTrue;
             heap_add(slot | (s_meta[slot] & 0xFFFF0000u), seq);
@@ -617,7 +709,7 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ heap (collections.ts:213-265)
-    __device__ void heap_add(uint32_t key, int32_t seq) {
+    MT_FI void heap_add(uint32_t key, int32_t seq) {
         if (hn + 1 > cap.heap) {
             cap_fail(1);
             return;
@@ -637,7 +729,7 @@ struct Engine {
         }
         if (hn > max_heap) max_heap = hn;
     }
-    __device__ void heap_get(uint32_t &key, int32_t &seq) {
+    MT_FI void heap_get(uint32_t &key, int32_t &seq) {
         key = h_key[1];
         seq = h_seq[1];
         h_key[1] = h_key[hn];
@@ -660,7 +752,7 @@ struct Engine {
 
     // ------------------------------------------------------------------ properties
     // prop-set record in the doc pool: [n, hash, (key, value) x n] in insertion order
-    __device__ bool props_match(uint32_t a, uint32_t ha, uint32_t b, uint32_t hb) {
+    MT_FI bool props_match(uint32_t a, uint32_t ha, uint32_t b, uint32_t hb) {
         if (a == b) return true;
         if (a == 0 || b == 0) return false;
         if (ha != hb) return false;
@@ -680,7 +772,7 @@ struct Engine {
     // SegmentPropertiesManager.addProperties for a sequenced remote op (or insert-time props):
     // start from `old` (0 = undefined -> new empty map), apply rewrite then the op's pairs in
     // order (null deletes: properties.ts:95-116).  Returns the new set id (hash in hout).
-    __device__ uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout) {
+    MT_FI uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout) {
         uint32_t *keys = scratch;
         uint32_t *vals = scratch + 128;
         uint32_t n = old ? pool[old] : 0u;
@@ -792,7 +884,8 @@ struct Engine {
     // ------------------------------------------------------------------ scour / pack / zamboni
     // scourNode (mergeTree.ts:1289-1365) over leaf block entries oe[s, s+cnt): appends the kept
     // slots to hold[nh..], unlinks removed-below-minSeq leaves and appends mergeable neighbours.
-    __device__ int32_t scour_leaves(int32_t s, int32_t cnt, uint32_t *hold, int32_t nh) {
+    MT_FI int32_t scour_leaves(int32_t s, int32_t cnt, uint32_t *hold, int32_t nh) {
+        PF_SCOPE(7);
         int32_t prev = -1;
         for (int32_t k = 0; k < cnt; k++) {
             uint32_t slot = rfl(oe[s + k] & 0xFFFFu);
@@ -855,7 +948,7 @@ struct Engine {
 
     // pack for an interior block `blk` (its parent's children are interior blocks);
     // repeats upward while the parent underflows (mergeTree.ts:1414-1419)
-    __device__ void pack_interior(int32_t blk) {
+    MT_FI void pack_interior(int32_t blk) {
         for (;;) {
             int32_t parent = b_parent[blk];
             int32_t pn = b_count[parent];
@@ -873,23 +966,22 @@ struct Engine {
             if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
             if (child_count < 1) child_count = 1;
             int32_t base = total / child_count, extra = total % child_count;
-            int32_t nb[kMaxNodes];
             for (int32_t i = 0; i < pn; i++) free_block(b_child[parent * 8 + i]);
-            for (int32_t i = 0; i < child_count; i++) nb[i] = alloc_block(0);
-            if (status) return;
             int32_t read = 0;
             for (int32_t i = 0; i < child_count; i++) {
+                int32_t nbi = alloc_block(0);
+                if (status) return;
                 int32_t cnt = base + (i < extra ? 1 : 0);
                 wsync();
                 if (lane < cnt) {
                     uint16_t g = (uint16_t)hold[read + lane];
-                    b_child[nb[i] * 8 + lane] = g;
-                    b_parent[g] = (uint16_t)nb[i];
+                    b_child[nbi * 8 + lane] = g;
+                    b_parent[g] = (uint16_t)nbi;
                 }
                 wsync();
-                b_count[nb[i]] = (uint8_t)cnt;
-                b_parent[nb[i]] = (uint16_t)parent;
-                b_child[parent * 8 + i] = (uint16_t)nb[i];
+                b_count[nbi] = (uint8_t)cnt;
+                b_parent[nbi] = (uint16_t)parent;
+                b_child[parent * 8 + i] = (uint16_t)nbi;
                 read += cnt;
             }
             b_count[parent] = (uint8_t)child_count;
@@ -900,7 +992,7 @@ struct Engine {
     }
 
     // pack for a leaf block (mergeTree.ts:1368-1420)
-    __device__ void pack_leaf(int32_t blk, int32_t hint) {
+    MT_FI void pack_leaf(int32_t blk, int32_t hint) {
         int32_t parent = b_parent[blk];
         int32_t pn = b_count[parent];
         int32_t first = b_child[parent * 8 + 0];
@@ -925,24 +1017,23 @@ struct Engine {
         if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
         if (child_count < 1) child_count = 1;
         int32_t base = total / child_count, extra = total % child_count;
-        int32_t nb[kMaxNodes];
         for (int32_t i = 0; i < pn; i++) free_block(b_child[parent * 8 + i]);
-        for (int32_t i = 0; i < child_count; i++) nb[i] = alloc_block(1);
-        if (status) return;
         int32_t new_len = total + child_count;
         oe_move_tail(old_end, s0 + new_len);
         if (status) return;
-        // write the regrouped range
+        // write the regrouped range, one new leaf block at a time
         int32_t read = 0, w = s0;
         for (int32_t i = 0; i < child_count; i++) {
+            int32_t nbi = alloc_block(1);
+            if (status) return;
             int32_t cnt = base + (i < extra ? 1 : 0);
             wsync();
-            if (lane < cnt) oe[w + lane] = ((uint32_t)nb[i] << 16) | hold[read + lane];
-            if (lane == cnt) oe[w + lane] = ((uint32_t)nb[i] << 16) | kMarkerSlot;
+            if (lane < cnt) oe[w + lane] = ((uint32_t)nbi << 16) | hold[read + lane];
+            if (lane == cnt) oe[w + lane] = ((uint32_t)nbi << 16) | kMarkerSlot;
             wsync();
-            b_count[nb[i]] = (uint8_t)cnt;
-            b_parent[nb[i]] = (uint16_t)parent;
-            b_child[parent * 8 + i] = (uint16_t)nb[i];
+            b_count[nbi] = (uint8_t)cnt;
+            b_parent[nbi] = (uint16_t)parent;
+            b_child[parent * 8 + i] = (uint16_t)nbi;
             read += cnt;
             w += cnt + 1;
         }
@@ -952,7 +1043,8 @@ struct Engine {
     }
 
     // zamboniSegments (mergeTree.ts:1422-1478)
-    __device__ void zamboni() {
+    MT_FI void zamboni() {
+        PF_SCOPE(5);
         for (int it = 0; it < kZamboniMax; it++) {
             if (hn < 1 || h_seq[1] > min_seq) break;
             uint32_t key;
@@ -989,7 +1081,7 @@ struct Engine {
     }
 
     // setMinSeq (mergeTree.ts:1718-1736) via Client.updateSeqNumbers (client.ts:821-828)
-    __device__ void update_seq_numbers(int32_t msn, int32_t seq) {
+    MT_FI void update_seq_numbers(int32_t msn, int32_t seq) {
         if (!(cur_seq <= seq)) {
             set_fail(ST_SEQ_ORDER);
             return;
@@ -1011,15 +1103,22 @@ struct Engine {
 
     // ------------------------------------------------------------------ ops
     // insertSegments + blockInsert for one remote segment (mergeTree.ts:1968-1998, 2141-2224)
-    __device__ void op_insert(const mt_op &op) {
+    MT_FI void op_insert(const mt_op &op) {
         uint32_t c = op.client;
         uint32_t pos = (uint32_t)op.pos1;
-        ensure_boundary(pos, op.ref_seq, c);
-        if (status) return;
+        // ensureIntervalBoundary (mergeTree.ts:2241-2245) and the insertingWalk share one scan:
+        // the walk's target is the segment the boundary split cuts, whose left half keeps every
+        // entry before it, so the walk resumes at that half with the same view position.
+        Loc L = locate(pos, op.ref_seq, c);
+        if (L.found && !L.marker && L.excl < pos) {
+            int32_t li = split_at(L.idx, pos - L.excl);
+            if (status) return;
+            L = locate(pos, op.ref_seq, c, li, L.excl);
+        }
         bool marker = (op.flags & MT_OPF_MARKER) != 0;
         uint32_t len = marker ? 1u : op.payload_len;
         if (len > 0) {
-            Loc L = locate(pos, op.ref_seq, c);
+            PF_SCOPE(3);
             if (!L.found) {
                 set_fail(ST_INVALID_POS);
                 return;
@@ -1052,25 +1151,55 @@ struct Engine {
             // saveIfLocal (mergeTree.ts:2164-2179)
             if (op.seq > min_seq) add_to_lru(blk, (uint32_t)slot, op.seq);
         }
+        resolve_splits();
         zamboni();
     }
 
     // markRangeRemoved / annotateRange range walk (nodeMap, mergeTree.ts:2903-2965)
-    __device__ void op_range(const mt_op &op) {
+    MT_FI void op_range(const mt_op &op) {
         uint32_t c = op.client;
         int32_t ref = op.ref_seq;
         uint32_t start = (uint32_t)op.pos1, end = (uint32_t)op.pos2;
-        ensure_boundary(start, ref, c);
-        if (status) return;
-        ensure_boundary(end, ref, c);
-        if (status) return;
+        // ensureIntervalBoundary(start), ensureIntervalBoundary(end) (mergeTree.ts:2241-2245,
+        // 2903-2904): every entry before the start walk's target ends at or before `start`, so
+        // the end search and the range walk resume there with its view position.
+        Loc A = locate(start, ref, c);
+        if (!A.found) {
+            resolve_splits();
+            zamboni();
+            return;
+        }
+        int32_t from = A.idx;
+        uint32_t carry = A.excl;
+        if (!A.marker && A.excl < start) {
+            from = split_at(A.idx, start - A.excl);
+            if (status) return;
+        }
+        if (end > start) {
+            Loc B = containing(end, ref, c, from, carry);
+            if (B.found) {
+                split_at(B.idx, end - B.excl);
+                if (status) return;
+                from = shifted(from);
+            }
+        } else if (end < start) {
+            // inverted range: nothing is marked, but the end boundary is still cut
+            Loc B = containing(end, ref, c, 0, 0);
+            if (B.found) {
+                split_at(B.idx, end - B.excl);
+                if (status) return;
+            }
+            from = 0;
+            carry = 0;
+        }
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = (op.flags & MT_OPF_REWRITE) != 0;
         // per-op memo old prop-set -> new prop-set (annotate)
         uint32_t memo_n = 0;
         uint32_t memo_old = 0, memo_new = 0, memo_h = 0;  // lane i holds entry i
-        uint32_t carry = 0;
-        for (int32_t base = 0; base < n_oe; base += kWave) {
+        {
+        PF_SCOPE(4);
+        for (int32_t base = from; base < n_oe; base += kWave) {
             int32_t j = base + lane;
             bool valid = j < n_oe;
             uint32_t e = valid ? oe[j] : 0u;
@@ -1134,10 +1263,13 @@ struct Engine {
             if (pb) break;
             carry = rdl(incl, 63);
         }
+        }
+        resolve_splits();
         zamboni();
     }
 
-    __device__ void apply(const mt_op &op) {
+    MT_FI void apply(const mt_op &op) {
+        pend_n = 0;
         if (op.client >= kMaxClients || (op.client == 0 && op.type != MT_OP_NOOP)) {
             set_fail(ST_UNSUPPORTED);
             return;
@@ -1149,6 +1281,7 @@ struct Engine {
             case MT_OP_NOOP: break;
             default: set_fail(ST_BAD_INPUT); return;
         }
+        resolve_splits();  // on early exits (capacity) keep the table consistent
         if (status) return;
         if (op.type != MT_OP_NOOP) {
             // completeAndLogOp (client.ts:461-464)
@@ -1165,7 +1298,7 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ output
-    __device__ void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op) {
+    MT_FI void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op) {
         wsync();
         int32_t n = n_oe <= out_cap ? n_oe : out_cap;
         for (int32_t j = lane; j < n; j += kWave) {
@@ -1239,7 +1372,7 @@ __device__ __forceinline__ mt_op bcast_op(const mt_op &o, int l) {
     return r;
 }
 
-__device__ void engine_setup(Engine &E, const ReplayParams &P, int64_t d, uint8_t *smem) {
+MT_FI void engine_setup(Engine &E, const ReplayParams &P, int64_t d, uint8_t *smem) {
     E.lane = threadIdx.x;
     E.carve(smem, P.caps);
     E.text = P.text + P.doc_text_base[d];
@@ -1268,6 +1401,10 @@ extern "C" __global__ __launch_bounds__(64) void mt_replay_kernel(ReplayParams P
     if (w >= P.n_docs) return;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
     Engine E;
+#ifdef MT_PROF
+    for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
+    const uint64_t t_kernel = clock64();
+#endif
     engine_setup(E, P, d, smem);
     const mt_op *ops = (const mt_op *)P.ops;
     const int64_t b0 = P.doc_op_off[d], b1 = P.doc_op_off[d + 1];
@@ -1289,6 +1426,15 @@ extern "C" __global__ __launch_bounds__(64) void mt_replay_kernel(ReplayParams P
         cur = nxt;
     }
     E.write_out(P.out + w * (int64_t)P.out_cap, P.out_cap, P.doc_out + w, done, fail_op);
+#ifdef MT_PROF
+    E.pf[0] = clock64() - t_kernel;
+    if (P.prof && E.lane < kProfSlots) {
+        uint64_t v = E.pf[0];
+        for (int k = 1; k < kProfSlots; k++)
+            if (E.lane == k) v = E.pf[k];
+        P.prof[w * kProfSlots + E.lane] = v;
+    }
+#endif
 }
 
 // Generator: draws each op from the issuer's view (include/mt_gen.h, DESIGN.md
@@ -1371,17 +1517,17 @@ extern "C" __global__ __launch_bounds__(64) void mt_generate_kernel(ReplayParams
             if (type == MT_OP_ANNOTATE) {
                 uint32_t nk = 1u + mt_rng_below(&x, 2);
                 uint32_t k0 = mt_rng_below(&x, 4);
-                uint32_t keys[2] = {k0, (k0 + 1u + mt_rng_below(&x, 3)) % 4u};
+                uint32_t k1 = (k0 + 1u + mt_rng_below(&x, 3)) % 4u;
                 op.payload = (uint32_t)(prop_base + np);
                 op.payload_len = nk;
                 for (uint32_t i = 0; i < nk; i++) {
                     uint32_t v;
                     if (mt_rng_below(&x, 10) == 0) v = 0;
-                    else if (keys[i] <= 1) v = 1;
-                    else if (keys[i] == 2) v = 2 + mt_rng_below(&x, 3);
+                    else if ((i ? k1 : k0) <= 1) v = 1;
+                    else if ((i ? k1 : k0) == 2) v = 2 + mt_rng_below(&x, 3);
                     else v = 5 + mt_rng_below(&x, 17);
                     if (E.lane == 0) {
-                        props_out[prop_base + np].key = keys[i];
+                        props_out[prop_base + np].key = i ? k1 : k0;
                         props_out[prop_base + np].value = v;
                     }
                     np++;
@@ -1389,7 +1535,6 @@ extern "C" __global__ __launch_bounds__(64) void mt_generate_kernel(ReplayParams
             }
         }
         if (E.lane == 0) ops_out[k - 1] = op;
-        __threadfence_block();
         wsync();
         E.apply(op);
         if (E.status != ST_OK) {

@@ -53,6 +53,7 @@ struct Launch {
     OutRec *d_out = nullptr;
     DocOut *d_docout = nullptr;
     int32_t *d_list = nullptr;
+    uint64_t *d_prof = nullptr;  // MT_PROF builds
     size_t lds = 0;
 };
 
@@ -279,6 +280,7 @@ static void free_launches(mt_batch *b) {
         (void)hipFree(L.d_out);
         (void)hipFree(L.d_docout);
         (void)hipFree(L.d_list);
+        (void)hipFree(L.d_prof);
     }
     b->launches.clear();
 }
@@ -582,6 +584,10 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.doc_list = L.d_list;
     P.out_cap = L.out_cap;
     P.caps = L.caps;
+#ifdef MT_PROF
+    HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
+    P.prof = L.d_prof;
+#endif
     if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)mt::mt_replay_kernel,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
     hipLaunchKernelGGL(mt::mt_replay_kernel, dim3((unsigned)n), dim3(64), L.lds, s, P);
@@ -617,6 +623,22 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
 static int gather_launch(mt_batch *b, int li) {
     Launch &L = b->launches[li];
     int64_t n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+#ifdef MT_PROF
+    {
+        std::vector<uint64_t> pf((size_t)n * mt::kProfSlots);
+        HIPCHK(hipMemcpy(pf.data(), L.d_prof, 8 * pf.size(), hipMemcpyDeviceToHost));
+        double sum[mt::kProfSlots] = {0}, mx = 0;
+        for (int64_t i = 0; i < n; i++)
+            for (int k = 0; k < mt::kProfSlots; k++) {
+                sum[k] += (double)pf[(size_t)i * mt::kProfSlots + k];
+                if (k == 0 && (double)pf[(size_t)i * mt::kProfSlots] > mx) mx = (double)pf[(size_t)i * mt::kProfSlots];
+            }
+        fprintf(stderr, "MT_PROF launch %d docs %lld lds %zu: mean cycles/doc", li, (long long)n, L.lds);
+        static const char *nm[mt::kProfSlots] = {"kernel", "scans", "split", "insert", "range", "zamboni", "shift", "scour"};
+        for (int k = 0; k < mt::kProfSlots; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (double)n);
+        fprintf(stderr, " max_kernel=%.0f\n", mx);
+    }
+#endif
     std::vector<DocOut> tmp((size_t)n);
     HIPCHK(hipMemcpy(tmp.data(), L.d_docout, sizeof(DocOut) * (size_t)n, hipMemcpyDeviceToHost));
     if (b->docout.size() != (size_t)b->n_docs) {

@@ -17,6 +17,7 @@ when the compiled library is missing or no GPU is present (there is no CPU fallb
 from __future__ import annotations
 
 import ctypes as C
+import os
 import json
 from pathlib import Path
 
@@ -24,7 +25,7 @@ import numpy as np
 
 from .oplog import OP_DTYPE, PROP_DTYPE, PackedBatch, Packer
 
-LIB_PATH = Path(__file__).resolve().parent / "libmtreplay.so"
+LIB_PATH = Path(os.environ.get("FLUIDFRAMEWORK_AMD_LIB") or Path(__file__).resolve().parent / "libmtreplay.so")
 
 MT_OK, MT_INVALID_POS, MT_SEQ_ORDER, MT_MSN_ORDER, MT_UNSUPPORTED, MT_BAD_INPUT, MT_CAPACITY, MT_INTERNAL = range(8)
 MT_ERR_HIP, MT_ERR_ARG, MT_ERR_STATE, MT_ERR_NO_DEVICE = 100, 101, 102, 103

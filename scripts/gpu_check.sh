@@ -20,6 +20,11 @@ for step in "$@"; do
     bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
+    phases) run phases 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --steps 1 --warmup 0 --no-cpu ;;
+    phases3) run phases3 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --config 3 --docs 2048 --steps 1 --warmup 0 --no-cpu ;;
+    docs256) run docs256 600 python -u bench.py --docs 256 --steps 2 --warmup 1 --no-cpu ;;
+    docs1024) run docs1024 600 python -u bench.py --docs 1024 --steps 2 --warmup 1 --no-cpu ;;
     *) echo "unknown step $step" ;;
   esac
 done
