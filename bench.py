@@ -104,6 +104,11 @@ def main():
 
     st = b.stats()
     statuses = b.statuses()
+    import numpy as np
+
+    cnt = b.counters()
+    capacity = {f: [int(np.percentile(cnt[f], q)) for q in (50, 99, 100)]
+                for f in ("max_slots", "max_entries", "max_blocks", "max_heap")}
     ops_done = st["ops_applied"]
     # gather per-document results to rank 0 over RCCL (status, ops applied)
     gather_ms = 0.0
@@ -162,6 +167,7 @@ def main():
             "ops_applied_per_step": int(ops_done),
             "lds_bytes_per_doc": st["lds_bytes"],
             "launches_per_step": st["launches"],
+            "capacity_p50_p99_max": capacity,
             "gen_s": round(gen_s, 2),
             "gather_ms": round(gather_ms, 3),
         }

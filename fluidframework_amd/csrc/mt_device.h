@@ -25,6 +25,7 @@ constexpr int kMaxNodes = 8;            // MaxNodesInBlock, mergeTree.ts:334
 constexpr uint32_t kGranularity = 256;  // TextSegmentGranularity, mergeTree.ts:1059
 constexpr int kZamboniMax = 2;          // zamboniSegmentsMaxCount, mergeTree.ts:1061
 constexpr int kMaxClients = 32;         // overlap mask width
+constexpr int kHeapRegs = 4;            // LRU heap in VGPRs: 64 * kHeapRegs - 1 entries
 constexpr int32_t kNoneSeq = 0x7FFFFFFF;  // removedSeq === undefined
 constexpr uint32_t kMarkerSlot = 0xFFFFu; // oe entry that ends a leaf block
 constexpr uint32_t kNoClient = 63u;
@@ -110,6 +111,6 @@ struct ReplayParams {
     void *gen_props;              // mt_prop[n_docs * 2 * n_ops] (doc-local offsets rebased by host)
     uint64_t *prof;               // MT_PROF builds: kProfSlots cycle counters per workgroup
 };
-constexpr int kProfSlots = 8;
+constexpr int kProfSlots = 12;
 
 }  // namespace mt

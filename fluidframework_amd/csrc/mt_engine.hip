@@ -98,8 +98,6 @@ struct Engine {
     uint16_t *b_parent, *b_free, *b_child;
     uint8_t *b_count, *b_leaf;
     int8_t *b_scour;
-    uint32_t *h_key;
-    int32_t *h_seq;
     uint32_t *scratch;  // 256 words
     Caps cap;
     // ---- uniform scalars
@@ -108,12 +106,14 @@ struct Engine {
     uint32_t arena_top, pool_top;
     uint32_t pay_end, arena_base, arena_end, semi_t;  // text: payload | semispace A | semispace B
     uint32_t pool_base, pool_end, semi_p;             // prop pool: [0] reserved | A | B
-    int32_t pool_gcs;
+    int32_t pool_gcs, text_gcs;
     // ends-with-'\n' of a split's left half, resolved after the op's LDS work so the text load
     // latency overlaps it (at most two splits per op)
     int32_t pend_n;
     uint32_t pend_slot0, pend_slot1, pend_ch0, pend_ch1;
     int32_t max_oe, max_heap;
+    uint32_t hk[kHeapRegs];
+    int32_t hs[kHeapRegs];
     int32_t split_mark;  // oe index of the end marker the last leaf split inserted, -1: none
     // ---- global
     uint16_t *text;
@@ -142,8 +142,6 @@ struct Engine {
         take(c.blk);
         take(c.blk);
         take(c.blk);
-        take(4u * (c.heap + 1));
-        take(4u * (c.heap + 1));
         take(4u * 256);
         return o;
     }
@@ -172,8 +170,6 @@ struct Engine {
         b_count = (uint8_t *)take(c.blk);
         b_leaf = (uint8_t *)take(c.blk);
         b_scour = (int8_t *)take(c.blk);
-        h_key = (uint32_t *)take(4u * (c.heap + 1));
-        h_seq = (int32_t *)take(4u * (c.heap + 1));
         scratch = (uint32_t *)take(4u * 256);
     }
 
@@ -209,9 +205,11 @@ struct Engine {
         depth = 1;
         b_parent[root] = 0xFFFF;  // lane-uniform writes (every lane stores the same value)
         oe_insert(0, (uint32_t)root << 16 | kMarkerSlot);
-        // heap sentinel LRUSegmentComparer.min = { maxSeq: -2 }
-        h_key[0] = 0;
-        h_seq[0] = -2;
+        // heap entry 0 is the sentinel LRUSegmentComparer.min = { maxSeq: -2 } (never compared)
+        for (int i = 0; i < kHeapRegs; i++) {
+            hk[i] = 0;
+            hs[i] = -2;
+        }
         wsync();
     }
 
@@ -503,6 +501,7 @@ struct Engine {
         arena_base = nb;
         arena_end = nb + semi_t;
         arena_top = top;
+        text_gcs++;
         wsync();
     }
 
@@ -709,45 +708,72 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ heap (collections.ts:213-265)
+    // The LRU heap lives in VGPRs: entry k is lane k & 63 of register k >> 6, so sifting is
+    // readlane / writelane arithmetic with no memory round trips.  Same array layout and sift
+    // order as Heap.add / Heap.get, hence the same pop order on seq ties.
+    MT_FI int32_t hseq(int32_t k) const {
+        int32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < kHeapRegs; i++)
+            if ((k >> 6) == i) v = rdl(hs[i], k & 63);
+        return v;
+    }
+    MT_FI uint32_t hkey(int32_t k) const {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < kHeapRegs; i++)
+            if ((k >> 6) == i) v = rdl(hk[i], k & 63);
+        return v;
+    }
+    MT_FI void hset(int32_t k, uint32_t key, int32_t seq) {
+#pragma unroll
+        for (int i = 0; i < kHeapRegs; i++)
+            if ((k >> 6) == i && lane == (k & 63)) {
+                hk[i] = key;
+                hs[i] = seq;
+            }
+    }
     MT_FI void heap_add(uint32_t key, int32_t seq) {
-        if (hn + 1 > cap.heap) {
-            cap_fail(1);
+        PF_SCOPE(9);
+        if (hn + 1 > cap.heap || hn + 1 >= 64 * kHeapRegs) {
+            cap_fail(hn + 1 >= 64 * kHeapRegs ? 5 : 1);
             return;
         }
         hn++;
         int32_t k = hn;
-        h_key[k] = key;
-        h_seq[k] = seq;
-        while (k > 1 && h_seq[k >> 1] - h_seq[k] > 0) {
-            uint32_t tk = h_key[k >> 1];
-            int32_t ts = h_seq[k >> 1];
-            h_key[k >> 1] = h_key[k];
-            h_seq[k >> 1] = h_seq[k];
-            h_key[k] = tk;
-            h_seq[k] = ts;
+        // sift up: parents larger than the new entry move down into the hole
+        while (k > 1) {
+            int32_t ps = hseq(k >> 1);
+            if (!(ps - seq > 0)) break;
+            hset(k, hkey(k >> 1), ps);
             k >>= 1;
         }
+        hset(k, key, seq);
         if (hn > max_heap) max_heap = hn;
     }
     MT_FI void heap_get(uint32_t &key, int32_t &seq) {
-        key = h_key[1];
-        seq = h_seq[1];
-        h_key[1] = h_key[hn];
-        h_seq[1] = h_seq[hn];
+        PF_SCOPE(9);
+        key = hkey(1);
+        seq = hseq(1);
+        uint32_t lk = hkey(hn);
+        int32_t ls = hseq(hn);
         hn--;
         int32_t k = 1;
         while ((k << 1) <= hn) {
             int32_t j = k << 1;
-            if (j < hn && h_seq[j] - h_seq[j + 1] > 0) j++;
-            if (h_seq[k] - h_seq[j] <= 0) break;
-            uint32_t tk = h_key[k];
-            int32_t ts = h_seq[k];
-            h_key[k] = h_key[j];
-            h_seq[k] = h_seq[j];
-            h_key[j] = tk;
-            h_seq[j] = ts;
+            int32_t sj = hseq(j);
+            if (j < hn) {
+                int32_t sj1 = hseq(j + 1);
+                if (sj - sj1 > 0) {
+                    j++;
+                    sj = sj1;
+                }
+            }
+            if (ls - sj <= 0) break;
+            hset(k, hkey(j), sj);
             k = j;
         }
+        if (hn >= 1) hset(k, lk, ls);
     }
 
     // ------------------------------------------------------------------ properties
@@ -882,68 +908,146 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ scour / pack / zamboni
-    // scourNode (mergeTree.ts:1289-1365) over leaf block entries oe[s, s+cnt): appends the kept
-    // slots to hold[nh..], unlinks removed-below-minSeq leaves and appends mergeable neighbours.
-    MT_FI int32_t scour_leaves(int32_t s, int32_t cnt, uint32_t *hold, int32_t nh) {
+    // scourNode (mergeTree.ts:1289-1365) over the leaf entries oe[s, s+n), n <= 64, which may
+    // span several blocks (their end markers reset the append chain, as each scourNode call
+    // starts afresh).  Kept slots are appended to hold[nh..] in order; returns the new count.
+    // The leaves are gathered one per lane; only the TextSegment.canAppend chain (textSegment.ts:
+    // 63-68, whose length test depends on earlier appends) runs serially, on scalars.
+    MT_FI int32_t scour_range(int32_t s, int32_t n, uint32_t *hold, int32_t nh) {
         PF_SCOPE(7);
-        int32_t prev = -1;
-        for (int32_t k = 0; k < cnt; k++) {
-            uint32_t slot = rfl(oe[s + k] & 0xFFFFu);
-            int32_t rseq = s_rseq[slot];
-            if (rseq != kNoneSeq) {
-                if (rseq > min_seq) hold[nh++] = slot;
-                else free_slot((int32_t)slot);
-                prev = -1;
-            } else if (s_seq[slot] <= min_seq) {
+        const bool in = lane < n;
+        const uint32_t e = in ? oe[s + lane] : (uint32_t)kMarkerSlot;
+        const uint32_t slot = e & 0xFFFFu;
+        const bool mk = slot == kMarkerSlot;
+        int32_t rseq = kNoneSeq, seq = 0;
+        uint32_t meta = 0, len = 0, props = 0, ph = 0, toff = 0, tcap = 0;
+        if (!mk) {
+            rseq = s_rseq[slot];
+            seq = s_seq[slot];
+            meta = s_meta[slot];
+            len = s_len[slot];
+            props = s_props[slot];
+            ph = s_phash[slot];
+            toff = s_toff[slot];
+            tcap = s_tcap[slot];
+        }
+        const bool rem = !mk && rseq != kNoneSeq;
+        const bool cand = !mk && !rem && seq <= min_seq;
+        const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
+        const bool peq = lane > 0 && pprev == props;
+        const bool pmaybe = lane > 0 && !peq && props != 0u && pprev != 0u && hprev == ph;
+        const uint64_t candM = ballot(cand), peqM = ballot(peq), maybeM = ballot(pmaybe);
+        const uint64_t freeR = ballot(rem && rseq <= min_seq);
+        const uint64_t liveM = ballot(in && !mk);
+        uint64_t mergeM = 0;
+        uint32_t head = 0;  // lane f (merged): lane of its chain head
+        {
+            int32_t prev = -1;
+            uint32_t acc = 0;
+            bool pnl = false, pmk = false;
+            for (int32_t k = 0; k < n; k++) {
+                if (!((candM >> k) & 1ull)) {
+                    prev = -1;
+                    continue;
+                }
+                const uint32_t lk = rdl(len, k), mk_ = rdl(meta, k);
                 bool can = false;
-                if (prev >= 0) {
-                    uint32_t pm = s_meta[prev], sm = s_meta[slot];
-                    uint32_t pl = s_len[prev], sl = s_len[slot];
-                    // TextSegment.canAppend (textSegment.ts:63-68)
-                    can = !(pm & kMetaMarker) && !(sm & kMetaMarker) && !(pm & kMetaEndsNL) &&
-                          (pl <= kGranularity || sl <= kGranularity);
-                    if (can) can = props_match(s_props[prev], s_phash[prev], s_props[slot], s_phash[slot]);
+                if (prev >= 0 && !pmk && !(mk_ & kMetaMarker) && !pnl && (acc <= kGranularity || lk <= kGranularity)) {
+                    if ((peqM >> k) & 1ull) can = true;
+                    else if ((maybeM >> k) & 1ull)
+                        can = props_match(rdl(props, k - 1), rdl(ph, k - 1), rdl(props, k), rdl(ph, k));
                 }
                 if (can) {
-                    // TextSegment.append: prev.text += segment.text
-                    uint32_t pl = s_len[prev], sl = s_len[slot];
-                    uint32_t need = pl + sl;
-                    uint32_t ptoff = s_toff[prev], stoff = s_toff[slot], pcap = s_tcap[prev];
-                    if (pcap == pl && ptoff + pl == stoff) {
-                        // texts already adjacent (split halves, consecutive payloads): take over the region
-                        s_tcap[prev] = pl + s_tcap[slot];
-                    } else if (pcap >= need) {
-                        text_copy(ptoff + pl, stoff, sl);
-                    } else if (ptoff >= arena_base && ptoff < arena_end && ptoff + pcap == arena_top &&
-                               ptoff + ((2u * need + 15u) & ~15u) <= arena_end) {
-                        // last allocation of the arena: grow in place
-                        uint32_t ncap = (2u * need + 15u) & ~15u;
-                        arena_top = ptoff + ncap;
-                        s_tcap[prev] = ncap;
-                        text_copy(ptoff + pl, stoff, sl);
-                    } else {
-                        uint32_t ncap = 2 * need;
-                        uint32_t dst = arena_alloc(ncap);  // may compact: offsets re-read below
-                        if (status) return nh;
-                        text_copy(dst, s_toff[prev], pl);
-                        text_copy(dst + pl, s_toff[slot], sl);
-                        s_toff[prev] = dst;
-                        s_tcap[prev] = (ncap + 15u) & ~15u;
-                    }
-                    s_len[prev] = need;
-                    s_meta[prev] = (s_meta[prev] & ~kMetaEndsNL) | (s_meta[slot] & kMetaEndsNL);
-                    free_slot((int32_t)slot);
+                    mergeM |= 1ull << k;
+                    if (lane == k) head = (uint32_t)prev;
+                    acc += lk;
                 } else {
-                    hold[nh++] = slot;
-                    prev = (int32_t)slot;
+                    prev = k;
+                    acc = lk;
+                    pmk = (mk_ & kMetaMarker) != 0;
                 }
-            } else {
-                hold[nh++] = slot;
-                prev = -1;
+                pnl = (mk_ & kMetaEndsNL) != 0;
             }
         }
+        // TextSegment.append for every merge, head by head in document order
+        if (mergeM) {
+            PF_SCOPE(8);
+            uint64_t m = mergeM;
+            int32_t h = -1;
+            uint32_t hslot = 0, pl = 0, ptoff = 0, pcap = 0, hmeta = 0;
+            int32_t gcs0 = text_gcs;
+            while (m) {
+                const int k = first_lane(m);
+                m &= m - 1;
+                const int32_t hk_ = (int32_t)rdl(head, k);
+                if (hk_ != h) {
+                    h = hk_;
+                    hslot = rdl(slot, h);
+                    pl = rdl(len, h);
+                    ptoff = rdl(toff, h);
+                    pcap = rdl(tcap, h);
+                    hmeta = rdl(meta, h);
+                }
+                const uint32_t fslot = rdl(slot, k), sl = rdl(len, k);
+                uint32_t stoff = rdl(toff, k), stcap = rdl(tcap, k);
+                if (text_gcs != gcs0) {  // a compaction moved texts: offsets live in LDS again
+                    ptoff = s_toff[hslot];
+                    pcap = s_tcap[hslot];
+                    stoff = s_toff[fslot];
+                    stcap = s_tcap[fslot];
+                }
+                const uint32_t need = pl + sl;
+                if (pcap == pl && ptoff + pl == stoff) {
+                    // texts already adjacent (split halves, consecutive payloads): take over the region
+                    pcap = pl + stcap;
+                } else if (pcap >= need) {
+                    text_copy(ptoff + pl, stoff, sl);
+                } else if (ptoff >= arena_base && ptoff < arena_end && ptoff + pcap == arena_top &&
+                           ptoff + ((2u * need + 15u) & ~15u) <= arena_end) {
+                    // last allocation of the arena: grow in place
+                    pcap = (2u * need + 15u) & ~15u;
+                    arena_top = ptoff + pcap;
+                    text_copy(ptoff + pl, stoff, sl);
+                } else {
+                    // reallocate; a compaction inside arena_alloc moves every text, so the head
+                    // is written back first and both offsets re-read afterwards
+                    s_len[hslot] = pl;
+                    s_toff[hslot] = ptoff;
+                    s_tcap[hslot] = pcap;
+                    wsync();
+                    const uint32_t ncap = 2u * need;
+                    const uint32_t dst = arena_alloc(ncap);
+                    if (status) return nh;
+                    if (text_gcs != gcs0) {
+                        ptoff = s_toff[hslot];
+                        stoff = s_toff[fslot];
+                    }
+                    text_copy(dst, ptoff, pl);
+                    text_copy(dst + pl, stoff, sl);
+                    ptoff = dst;
+                    pcap = (ncap + 15u) & ~15u;
+                }
+                pl = need;
+                hmeta = (hmeta & ~kMetaEndsNL) | (rdl(meta, k) & kMetaEndsNL);
+                s_len[hslot] = pl;
+                s_toff[hslot] = ptoff;
+                s_tcap[hslot] = pcap;
+                s_meta[hslot] = hmeta;
+                wsync();
+            }
+        }
+        // unlink removed-below-minSeq leaves and appended ones; keep the rest in order
+        const uint64_t freeM = freeR | mergeM;
+        const uint64_t holdM = liveM & ~freeM;
+        const uint64_t below = (1ull << lane) - 1ull;
+        if ((freeM >> lane) & 1ull) {
+            s_meta[slot] = ((meta >> 16) + 1u) << 16;  // unlinked, next generation
+            s_free[n_free + __popcll(freeM & below)] = (uint16_t)slot;
+        }
+        if ((holdM >> lane) & 1ull) hold[nh + __popcll(holdM & below)] = slot;
+        n_free += __popcll(freeM);
         wsync();
-        return nh;
+        return nh + __popcll(holdM);
     }
 
     // pack for an interior block `blk` (its parent's children are interior blocks);
@@ -1003,15 +1107,18 @@ struct Engine {
         }
         (void)hint;
         uint32_t *hold = scratch + 128;
-        int32_t total = 0;
         int32_t s = s0;
-        for (int32_t ci = 0; ci < pn; ci++) {
-            int32_t cb = b_child[parent * 8 + ci];
-            int32_t cn = b_count[cb];
-            total = scour_leaves(s, cn, hold, total);
-            if (status) return;
-            s += cn + 1;  // skip its marker
+        for (int32_t ci = 0; ci < pn; ci++) s += b_count[b_child[parent * 8 + ci]] + 1;  // leaves + marker
+        if (s - s0 > kWave) {
+            set_fail(ST_INTERNAL);
+            return;
         }
+        int32_t total;
+        {
+            PF_SCOPE(10);
+            total = scour_range(s0, s - s0, hold, 0);
+        }
+        if (status) return;
         int32_t old_end = s;  // one past the last marker
         int32_t child_count = total / (kMaxNodes / 2);
         if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
@@ -1046,7 +1153,7 @@ struct Engine {
     MT_FI void zamboni() {
         PF_SCOPE(5);
         for (int it = 0; it < kZamboniMax; it++) {
-            if (hn < 1 || h_seq[1] > min_seq) break;
+            if (hn < 1 || hseq(1) > min_seq) break;
             uint32_t key;
             int32_t mseq;
             heap_get(key, mseq);
@@ -1063,7 +1170,7 @@ struct Engine {
             int32_t s = block_start_near((uint32_t)blk, idx);
             int32_t cnt = b_count[blk];
             uint32_t *hold = scratch;
-            int32_t nk = scour_leaves(s, cnt, hold, 0);
+            int32_t nk = scour_range(s, cnt, hold, 0);
             if (status) return;
             b_scour[blk] = kScourFalse;
             if (nk < cnt) {
@@ -1389,6 +1496,7 @@ MT_FI void engine_setup(Engine &E, const ReplayParams &P, int64_t d, uint8_t *sm
     E.pool_end = 1 + E.semi_p;
     E.pool_top = 1;
     E.pool_gcs = 0;
+    E.text_gcs = 0;
     E.props_in = (const mt_prop *)P.props_in;
     E.value_flags = P.value_flags;
     E.n_values = P.n_values;

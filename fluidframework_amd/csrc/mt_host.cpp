@@ -529,6 +529,7 @@ static Caps caps_for(const mt_batch *b, int32_t ops_per_doc, int level) {
     c.oe = b->opt.oe_cap > 0 ? (b->opt.oe_cap << level) : seg + seg / 2 + 16;
     c.blk = b->opt.blk_cap > 0 ? (b->opt.blk_cap << level) : seg / 2 + 16;
     c.heap = b->opt.heap_cap > 0 ? (b->opt.heap_cap << level) : seg / 2 + 64;
+    c.heap = std::min(c.heap, 64 * mt::kHeapRegs - 1);  // the heap lives in VGPRs
     return c;
 }
 
@@ -609,7 +610,7 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
         L.caps.seg /= 2;
         L.caps.oe = L.caps.seg + L.caps.seg / 2 + 16;
         L.caps.blk = L.caps.seg / 2 + 16;
-        L.caps.heap = L.caps.seg / 2 + 64;
+        L.caps.heap = std::min(L.caps.seg / 2 + 64, 64 * mt::kHeapRegs - 1);
     }
     b->launches.push_back(L);
     HIPCHK(hipEventRecord(b->ev0, s));
@@ -634,7 +635,7 @@ static int gather_launch(mt_batch *b, int li) {
                 if (k == 0 && (double)pf[(size_t)i * mt::kProfSlots] > mx) mx = (double)pf[(size_t)i * mt::kProfSlots];
             }
         fprintf(stderr, "MT_PROF launch %d docs %lld lds %zu: mean cycles/doc", li, (long long)n, L.lds);
-        static const char *nm[mt::kProfSlots] = {"kernel", "scans", "split", "insert", "range", "zamboni", "shift", "scour"};
+        static const char *nm[mt::kProfSlots] = {"kernel", "scans", "split", "insert", "range", "zamboni", "shift", "scour", "text", "heap", "pack", "-"};
         for (int k = 0; k < mt::kProfSlots; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (double)n);
         fprintf(stderr, " max_kernel=%.0f\n", mx);
     }
@@ -731,6 +732,19 @@ MT_API int mt_batch_algorithmic_bytes(mt_batch *b, double *bytes) {
 MT_API int32_t mt_doc_status(mt_batch *b, int64_t doc) {
     if (!b || !b->ran || doc < 0 || doc >= b->n_docs) return -MT_ERR_ARG;
     return b->docout[doc].status;
+}
+
+MT_API int mt_batch_doc_counters(mt_batch *b, int32_t *out) {
+    if (!b || !out) return MT_ERR_ARG;
+    if (!b->ran) return MT_ERR_STATE;
+    static_assert(sizeof(DocOut) == 4 * MT_DOC_COUNTERS, "DocOut layout");
+    for (int64_t d = 0; d < b->n_docs; d++) {
+        int32_t *o = out + d * MT_DOC_COUNTERS;
+        memcpy(o, &b->docout[(size_t)d], sizeof(DocOut));
+        o[14] = b->where[(size_t)d].launch;
+        o[15] = 0;
+    }
+    return MT_OK;
 }
 
 // ---------------------------------------------------------------- per-document results

@@ -36,8 +36,10 @@ EXPORTS = [
     "mt_batch_ingest", "mt_batch_generate", "mt_batch_run", "mt_batch_launch", "mt_batch_sync",
     "mt_batch_get_stats", "mt_batch_algorithmic_bytes", "mt_doc_status", "mt_doc_text", "mt_doc_props_runs",
     "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
-    "mt_batch_download_log",
+    "mt_batch_download_log", "mt_batch_doc_counters",
 ]
+DOC_COUNTERS = ("status", "min_seq", "cur_seq", "depth", "n_entries", "text_top", "pool_top", "ops_done",
+                "max_entries", "max_slots", "max_blocks", "max_heap", "fail_op", "cap_kind", "launch", "reserved")
 
 
 class MtError(RuntimeError):
@@ -111,6 +113,7 @@ def lib():
     L.mt_doc_digest.argtypes = [vp, i64, P(C.c_uint64)]
     L.mt_batch_log_sizes.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.mt_batch_download_log.argtypes = [vp, vp, vp, vp, vp]
+    L.mt_batch_doc_counters.argtypes = [vp, vp]
     _lib = L
     return L
 
@@ -280,6 +283,12 @@ class ReplayBatch:
         if not 0 <= i < self.n_docs:
             raise IndexError(i)
         return DocView(self, i)
+
+    def counters(self) -> np.ndarray:
+        """Per-document run counters (mt_batch_doc_counters) as a structured array."""
+        a = np.zeros((self.n_docs, len(DOC_COUNTERS)), np.int32)
+        _chk(lib().mt_batch_doc_counters(self.h, a.ctypes.data), "doc counters")
+        return np.rec.fromarrays(a.T, names=list(DOC_COUNTERS))
 
     def statuses(self) -> np.ndarray:
         L = lib()

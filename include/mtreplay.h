@@ -110,6 +110,11 @@ MT_API int mt_batch_get_stats(mt_batch *b, mt_batch_stats *out);
 MT_API int mt_batch_algorithmic_bytes(mt_batch *b, double *bytes);
 
 MT_API int32_t mt_doc_status(mt_batch *b, int64_t doc);
+/* per-document run counters, MT_DOC_COUNTERS int32 per document (capacity planning / stats):
+   status, min_seq, cur_seq, depth, n_entries, text_top, pool_top, ops_done, max_entries,
+   max_slots, max_blocks, max_heap, fail_op, cap_kind, launch, reserved */
+#define MT_DOC_COUNTERS 16
+MT_API int mt_batch_doc_counters(mt_batch *b, int32_t *out);
 MT_API int mt_doc_text(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
 MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
 MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs);
