@@ -159,7 +159,7 @@ def main():
                        "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": None,
-                         "kernel": "mt_replay_kernel", "avg_kernel_ms": round(avg_kernel_ms, 3),
+                         "kernel": f"mt_replay_kernel_{st['lds_class']}", "avg_kernel_ms": round(avg_kernel_ms, 3),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
             "cpu_baseline": cpu,
             "parity": parity,

@@ -83,6 +83,48 @@ struct Caps {
     int32_t heap;  // zamboni heap entries
 };
 
+// Capacity classes are compile-time: each class is its own kernel instantiation
+// (mt_kernels.hip), so every LDS array base is an immediate offset and no SGPRs hold
+// table pointers or bounds.
+constexpr int kClassSegs[] = {64, 128, 256, 512, 1024, 2048};
+constexpr int kNumClasses = 6;
+constexpr Caps class_caps(int seg) {
+    return Caps{seg, seg + seg / 2 + 16, seg / 2 + 16, (seg / 2 + 64) < (64 * kHeapRegs - 1) ? (seg / 2 + 64)
+                                                                                           : (64 * kHeapRegs - 1)};
+}
+
+// LDS layout of one document (byte offsets; every array 16-byte aligned)
+struct Layout {
+    uint32_t oe, len, seq, rseq, meta, ovl, props, toff, tcap, phash, sfree;
+    uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, scratch, bytes;
+};
+constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
+constexpr Layout make_layout(int seg) {
+    const Caps c = class_caps(seg);
+    Layout L{};
+    uint32_t o = 0;
+    L.oe = o;      o = lds_align(o + 4u * c.oe);
+    L.len = o;     o = lds_align(o + 4u * c.seg);
+    L.seq = o;     o = lds_align(o + 4u * c.seg);
+    L.rseq = o;    o = lds_align(o + 4u * c.seg);
+    L.meta = o;    o = lds_align(o + 4u * c.seg);
+    L.ovl = o;     o = lds_align(o + 4u * c.seg);
+    L.props = o;   o = lds_align(o + 4u * c.seg);
+    L.toff = o;    o = lds_align(o + 4u * c.seg);
+    L.tcap = o;    o = lds_align(o + 4u * c.seg);
+    L.phash = o;   o = lds_align(o + 4u * c.seg);
+    L.sfree = o;   o = lds_align(o + 2u * c.seg);
+    L.bparent = o; o = lds_align(o + 2u * c.blk);
+    L.bfree = o;   o = lds_align(o + 2u * c.blk);
+    L.bchild = o;  o = lds_align(o + 16u * c.blk);
+    L.bcount = o;  o = lds_align(o + 1u * c.blk);
+    L.bleaf = o;   o = lds_align(o + 1u * c.blk);
+    L.bscour = o;  o = lds_align(o + 1u * c.blk);
+    L.scratch = o; o = lds_align(o + 4u * 256);
+    L.bytes = o;
+    return L;
+}
+
 // kernel parameters
 struct ReplayParams {
     const void *ops;              // mt_op[]
@@ -104,7 +146,6 @@ struct ReplayParams {
     const int32_t *doc_list;      // non-null: blockIdx.x replays doc doc_list[blockIdx.x]
                                   // (capacity escalation); out/doc_out stay indexed by blockIdx.x
     int32_t out_cap;
-    Caps caps;
     // generator mode (non-null gen): ops/text/props are written, not read
     const void *gen;              // mt_gen_params*
     void *gen_ops;                // mt_op[n_docs * n_ops]

@@ -89,7 +89,10 @@ struct Loc {
     int32_t marker;
 };
 
+template <int SEG>
 struct Engine {
+    static constexpr Caps cap = class_caps(SEG);
+    static constexpr Layout lay = make_layout(SEG);
     // ---- LDS state
     uint32_t *oe;
     uint32_t *s_len, *s_meta, *s_ovl, *s_props, *s_toff, *s_tcap, *s_phash;
@@ -99,7 +102,6 @@ struct Engine {
     uint8_t *b_count, *b_leaf;
     int8_t *b_scour;
     uint32_t *scratch;  // 256 words
-    Caps cap;
     // ---- uniform scalars
     int32_t n_oe, slot_top, n_free, blk_top, n_bfree, root, depth, hn;
     int32_t min_seq, cur_seq, status;
@@ -129,48 +131,25 @@ struct Engine {
 #endif
 
     // ------------------------------------------------------------------ layout
-    __device__ static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-    __host__ __device__ static size_t lds_bytes(const Caps &c) {
-        size_t o = 0;
-        auto take = [&](size_t n) { o = (o + n + 15) & ~(size_t)15; };
-        take(4u * c.oe);
-        for (int i = 0; i < 9; i++) take(4u * c.seg);
-        take(2u * c.seg);
-        take(2u * c.blk);
-        take(2u * c.blk);
-        take(2u * 8 * c.blk);
-        take(c.blk);
-        take(c.blk);
-        take(c.blk);
-        take(4u * 256);
-        return o;
-    }
-    MT_FI void carve(uint8_t *base, const Caps &c) {
-        size_t o = 0;
-        auto take = [&](size_t n) {
-            uint8_t *p = base + o;
-            o = (o + n + 15) & ~(size_t)15;
-            return p;
-        };
-        cap = c;
-        oe = (uint32_t *)take(4u * c.oe);
-        s_len = (uint32_t *)take(4u * c.seg);
-        s_seq = (int32_t *)take(4u * c.seg);
-        s_rseq = (int32_t *)take(4u * c.seg);
-        s_meta = (uint32_t *)take(4u * c.seg);
-        s_ovl = (uint32_t *)take(4u * c.seg);
-        s_props = (uint32_t *)take(4u * c.seg);
-        s_toff = (uint32_t *)take(4u * c.seg);
-        s_tcap = (uint32_t *)take(4u * c.seg);
-        s_phash = (uint32_t *)take(4u * c.seg);
-        s_free = (uint16_t *)take(2u * c.seg);
-        b_parent = (uint16_t *)take(2u * c.blk);
-        b_free = (uint16_t *)take(2u * c.blk);
-        b_child = (uint16_t *)take(2u * 8 * c.blk);
-        b_count = (uint8_t *)take(c.blk);
-        b_leaf = (uint8_t *)take(c.blk);
-        b_scour = (int8_t *)take(c.blk);
-        scratch = (uint32_t *)take(4u * 256);
+    MT_FI void carve(uint8_t *base) {
+        oe = (uint32_t *)(base + lay.oe);
+        s_len = (uint32_t *)(base + lay.len);
+        s_seq = (int32_t *)(base + lay.seq);
+        s_rseq = (int32_t *)(base + lay.rseq);
+        s_meta = (uint32_t *)(base + lay.meta);
+        s_ovl = (uint32_t *)(base + lay.ovl);
+        s_props = (uint32_t *)(base + lay.props);
+        s_toff = (uint32_t *)(base + lay.toff);
+        s_tcap = (uint32_t *)(base + lay.tcap);
+        s_phash = (uint32_t *)(base + lay.phash);
+        s_free = (uint16_t *)(base + lay.sfree);
+        b_parent = (uint16_t *)(base + lay.bparent);
+        b_free = (uint16_t *)(base + lay.bfree);
+        b_child = (uint16_t *)(base + lay.bchild);
+        b_count = (uint8_t *)(base + lay.bcount);
+        b_leaf = (uint8_t *)(base + lay.bleaf);
+        b_scour = (int8_t *)(base + lay.bscour);
+        scratch = (uint32_t *)(base + lay.scratch);
     }
 
     int32_t cap_kind;
@@ -1479,9 +1458,10 @@ __device__ __forceinline__ mt_op bcast_op(const mt_op &o, int l) {
     return r;
 }
 
-MT_FI void engine_setup(Engine &E, const ReplayParams &P, int64_t d, uint8_t *smem) {
+template <int SEG>
+MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t d, uint8_t *smem) {
     E.lane = threadIdx.x;
-    E.carve(smem, P.caps);
+    E.carve(smem);
     E.text = P.text + P.doc_text_base[d];
     E.text_cap = P.doc_text_cap[d];
     E.pay_end = (P.doc_text_len[d] + 15u) & ~15u;
@@ -1503,12 +1483,13 @@ MT_FI void engine_setup(Engine &E, const ReplayParams &P, int64_t d, uint8_t *sm
     E.init();
 }
 
-extern "C" __global__ __launch_bounds__(64) void mt_replay_kernel(ReplayParams P) {
+template <int SEG>
+MT_FI void replay_body(const ReplayParams &P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
-    Engine E;
+    Engine<SEG> E;
 #ifdef MT_PROF
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
     const uint64_t t_kernel = clock64();
@@ -1547,12 +1528,14 @@ extern "C" __global__ __launch_bounds__(64) void mt_replay_kernel(ReplayParams P
 
 // Generator: draws each op from the issuer's view (include/mt_gen.h, DESIGN.md
 // "Synthetic op logs"), writes the record + payload, then applies it as the observer.
-extern "C" __global__ __launch_bounds__(64) void mt_generate_kernel(ReplayParams P) {
+template <int SEG>
+MT_FI void generate_body(const ReplayParams &P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int64_t d = (int64_t)blockIdx.x;
-    if (d >= P.n_docs) return;
+    const int64_t w = (int64_t)blockIdx.x;
+    if (w >= P.n_docs) return;
+    const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;  // re-generation of overflowed docs
     const mt_gen_params g = *(const mt_gen_params *)P.gen;
-    Engine E;
+    Engine<SEG> E;
     engine_setup(E, P, d, smem);
     mt_op *ops_out = (mt_op *)P.gen_ops + d * (int64_t)g.n_ops;
     mt_prop *props_out = (mt_prop *)P.gen_props;
@@ -1651,10 +1634,10 @@ extern "C" __global__ __launch_bounds__(64) void mt_generate_kernel(ReplayParams
         }
         done++;
     }
-    E.write_out(P.out + d * (int64_t)P.out_cap, P.out_cap, P.doc_out + d, done, fail_op);
+    E.write_out(P.out + w * (int64_t)P.out_cap, P.out_cap, P.doc_out + w, done, fail_op);
     if (E.lane == 0) {
-        P.doc_out[d].gen_text = (int32_t)pay_top;
-        P.doc_out[d].gen_props = (int32_t)np;
+        P.doc_out[w].gen_text = (int32_t)pay_top;
+        P.doc_out[w].gen_props = (int32_t)np;
     }
 }
 

@@ -1,7 +1,7 @@
 // mt_host.cpp — host side of libmtreplay.so: the C ABI declared in include/mtreplay.h.
 //
 // Owns a batch of documents on one HIP device: stages packed op logs into per-document
-// HBM regions, launches the replay kernels (mt_engine.hip, compiled into this TU), escalates
+// HBM regions, launches the replay kernels (mt_kernels.hip, one object per capacity class), escalates
 // documents that overflow their LDS capacity class, and serializes per-document results
 // (text, properties, SnapshotV1 blobs, digest) from the device's final segment tables.
 //
@@ -21,7 +21,18 @@
 #include <vector>
 
 #include "../../include/mtreplay.h"
-#include "mt_engine.hip"
+#include "mt_device.h"
+
+// kernels of each capacity class (mt_kernels.hip compiled with -DMT_SEG=<seg>)
+#define MT_DECLARE_CLASS(S)                                                   \
+    extern "C" __global__ void mt_replay_kernel_##S(mt::ReplayParams P);      \
+    extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);
+MT_DECLARE_CLASS(64)
+MT_DECLARE_CLASS(128)
+MT_DECLARE_CLASS(256)
+MT_DECLARE_CLASS(512)
+MT_DECLARE_CLASS(1024)
+MT_DECLARE_CLASS(2048)
 
 using mt::Caps;
 using mt::DocOut;
@@ -46,8 +57,24 @@ static hipError_t dalloc(T **p, size_t n) {
     return hipMalloc((void **)p, n * sizeof(T));
 }
 
+struct KernelClass {
+    int seg;
+    const void *replay;
+    const void *generate;
+};
+static const KernelClass kKernels[mt::kNumClasses] = {
+    {64, (const void *)mt_replay_kernel_64, (const void *)mt_generate_kernel_64},
+    {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128},
+    {256, (const void *)mt_replay_kernel_256, (const void *)mt_generate_kernel_256},
+    {512, (const void *)mt_replay_kernel_512, (const void *)mt_generate_kernel_512},
+    {1024, (const void *)mt_replay_kernel_1024, (const void *)mt_generate_kernel_1024},
+    {2048, (const void *)mt_replay_kernel_2048, (const void *)mt_generate_kernel_2048},
+};
+constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
+
 struct Launch {
     std::vector<int32_t> docs;  // empty: identity over all docs
+    int cls = 0;                // index into kKernels
     Caps caps;
     int32_t out_cap = 0;
     OutRec *d_out = nullptr;
@@ -515,23 +542,16 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     return MT_OK;
 }
 
-// capacity classes: derived from ops per document unless given
-static Caps caps_for(const mt_batch *b, int32_t ops_per_doc, int level) {
-    Caps c;
-    int32_t seg = b->opt.seg_cap;
-    if (seg <= 0) {
-        seg = 64;
-        while (seg < ops_per_doc / 16 + 64 && seg < 2048) seg *= 2;
-    }
-    seg <<= level;
-    if (seg > 4096) seg = 4096;
-    c.seg = seg;
-    c.oe = b->opt.oe_cap > 0 ? (b->opt.oe_cap << level) : seg + seg / 2 + 16;
-    c.blk = b->opt.blk_cap > 0 ? (b->opt.blk_cap << level) : seg / 2 + 16;
-    c.heap = b->opt.heap_cap > 0 ? (b->opt.heap_cap << level) : seg / 2 + 64;
-    c.heap = std::min(c.heap, 64 * mt::kHeapRegs - 1);  // the heap lives in VGPRs
-    return c;
+// capacity class index: derived from ops per document unless seg_cap is given; `level`
+// escalates by whole classes
+static int class_for(const mt_batch *b, int32_t ops_per_doc, int level) {
+    int32_t want = b->opt.seg_cap > 0 ? b->opt.seg_cap : ops_per_doc / 16 + 64;
+    int c = 0;
+    while (c + 1 < mt::kNumClasses && mt::kClassSegs[c] < want) c++;
+    c += level;
+    return c < mt::kNumClasses ? c : mt::kNumClasses;  // kNumClasses: nothing larger
 }
+static size_t class_lds(int c) { return mt::make_layout(mt::kClassSegs[c]).bytes; }
 
 static int max_lds_bytes() {
     static int v = -1;
@@ -546,7 +566,7 @@ static int max_lds_bytes() {
             v = (int)m;
         }
         if (v > 160 * 1024) v = 160 * 1024;
-        v -= 1024;  // static LDS of the generator kernel + margin
+        v -= (int)kGenStaticLds;  // static LDS of the generator kernel
     }
     return v;
 }
@@ -570,8 +590,9 @@ static mt::ReplayParams base_params(mt_batch *b) {
 
 static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     int64_t n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+    L.caps = mt::class_caps(mt::kClassSegs[L.cls]);
     L.out_cap = L.caps.oe;
-    L.lds = mt::Engine::lds_bytes(L.caps);
+    L.lds = class_lds(L.cls);
     HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
     HIPCHK(dalloc(&L.d_docout, (size_t)n));
     if (!L.docs.empty()) {
@@ -584,15 +605,14 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.n_docs = n;
     P.doc_list = L.d_list;
     P.out_cap = L.out_cap;
-    P.caps = L.caps;
 #ifdef MT_PROF
     HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
     P.prof = L.d_prof;
 #endif
-    if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)mt::mt_replay_kernel,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
-    hipLaunchKernelGGL(mt::mt_replay_kernel, dim3((unsigned)n), dim3(64), L.lds, s, P);
-    HIPCHK(hipGetLastError());
+    const void *fn = kKernels[L.cls].replay;
+    if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
+    void *args[] = {&P};
+    HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, s));
     return MT_OK;
 }
 
@@ -605,13 +625,8 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
     b->c_blob_doc = -1;
     b->t_launch = std::chrono::steady_clock::now();
     Launch L;
-    L.caps = caps_for(b, b->max_ops_per_doc, 0);
-    while (mt::Engine::lds_bytes(L.caps) > (size_t)max_lds_bytes() && L.caps.seg > 64) {
-        L.caps.seg /= 2;
-        L.caps.oe = L.caps.seg + L.caps.seg / 2 + 16;
-        L.caps.blk = L.caps.seg / 2 + 16;
-        L.caps.heap = std::min(L.caps.seg / 2 + 64, 64 * mt::kHeapRegs - 1);
-    }
+    L.cls = std::min(class_for(b, b->max_ops_per_doc, 0), mt::kNumClasses - 1);
+    while (L.cls > 0 && class_lds(L.cls) > (size_t)max_lds_bytes()) L.cls--;
     b->launches.push_back(L);
     HIPCHK(hipEventRecord(b->ev0, s));
     int rc = launch_replay(b, s, b->launches.back());
@@ -670,8 +685,8 @@ MT_API int mt_batch_sync(mt_batch *b) {
             if (b->docout[d].status == MT_CAPACITY && (b->docout[d].cap_kind == 1 || b->docout[d].cap_kind == 4))
                 L.docs.push_back((int32_t)d);
         if (L.docs.empty()) break;
-        L.caps = caps_for(b, b->max_ops_per_doc, level);
-        if (mt::Engine::lds_bytes(L.caps) > (size_t)max_lds_bytes()) break;  // largest LDS class reached
+        L.cls = b->launches.back().cls + 1;
+        if (L.cls >= mt::kNumClasses || class_lds(L.cls) > (size_t)max_lds_bytes()) break;  // largest class reached
         b->launches.push_back(L);
         HIPCHK(hipEventRecord(b->ev0, b->run_stream));
         rc = launch_replay(b, b->run_stream, b->launches.back());
@@ -702,7 +717,10 @@ MT_API int mt_batch_get_stats(mt_batch *b, mt_batch_stats *o) {
     o->launches = (int32_t)b->launches.size();
     o->kernel_ms = b->kernel_ms;
     o->total_ms = b->total_ms;
-    if (!b->launches.empty()) o->lds_bytes = (int32_t)b->launches[0].lds;
+    if (!b->launches.empty()) {
+        o->lds_bytes = (int32_t)b->launches[0].lds;
+        o->lds_class = mt::kClassSegs[b->launches[0].cls];
+    }
     if (!b->ran) return MT_OK;
     for (int64_t d = 0; d < b->n_docs; d++) {
         const DocOut &x = b->docout[d];
@@ -1235,37 +1253,55 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
     mt_gen_params *d_gen = nullptr;
     HIPCHK(dalloc(&d_gen, 1));
     HIPCHK(hipMemcpy(d_gen, p, sizeof(mt_gen_params), hipMemcpyHostToDevice));
-    // generation runs in the largest LDS class so no document overflows during synthesis
-    Launch L;
-    L.caps = caps_for(b, p->n_ops, 0);
-    for (int lvl = 1; lvl <= 3; lvl++) {
-        Caps c2 = caps_for(b, p->n_ops, lvl);
-        if (mt::Engine::lds_bytes(c2) <= (size_t)max_lds_bytes()) L.caps = c2;
-    }
-    L.out_cap = L.caps.oe;
-    L.lds = mt::Engine::lds_bytes(L.caps);
-    HIPCHK(dalloc(&L.d_out, (size_t)D * (size_t)L.out_cap));
-    HIPCHK(dalloc(&L.d_docout, (size_t)D));
-    mt::ReplayParams P = base_params(b);
-    P.out = L.d_out;
-    P.doc_out = L.d_docout;
-    P.n_docs = D;
-    P.doc_first = doc_first;
-    P.out_cap = L.out_cap;
-    P.caps = L.caps;
-    P.gen = d_gen;
-    P.gen_ops = b->d_ops;
-    P.gen_props = b->d_props;
-    if (L.lds > 64 * 1024)
-        HIPCHK(hipFuncSetAttribute((const void *)mt::mt_generate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)L.lds));
-    hipLaunchKernelGGL(mt::mt_generate_kernel, dim3((unsigned)D), dim3(64), L.lds, b->stream, P);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(b->stream));
+    // generation runs in the replay's capacity class; documents that overflow it are
+    // generated again (deterministically, from their own seed) in the next larger class
     std::vector<DocOut> outs((size_t)D);
-    HIPCHK(hipMemcpy(outs.data(), L.d_docout, sizeof(DocOut) * (size_t)D, hipMemcpyDeviceToHost));
-    (void)hipFree(L.d_out);
-    (void)hipFree(L.d_docout);
+    std::vector<int32_t> todo;
+    int cls = std::min(class_for(b, p->n_ops, 0), mt::kNumClasses - 1);
+    while (cls > 0 && class_lds(cls) > (size_t)max_lds_bytes()) cls--;
+    for (;; cls++) {
+        const int64_t n = todo.empty() ? D : (int64_t)todo.size();
+        Launch L;
+        L.cls = cls;
+        L.caps = mt::class_caps(mt::kClassSegs[cls]);
+        L.out_cap = L.caps.oe;
+        L.lds = class_lds(cls);
+        HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
+        HIPCHK(dalloc(&L.d_docout, (size_t)n));
+        if (!todo.empty()) {
+            HIPCHK(dalloc(&L.d_list, todo.size()));
+            HIPCHK(hipMemcpy(L.d_list, todo.data(), 4 * todo.size(), hipMemcpyHostToDevice));
+        }
+        mt::ReplayParams P = base_params(b);
+        P.out = L.d_out;
+        P.doc_out = L.d_docout;
+        P.n_docs = n;
+        P.doc_first = doc_first;
+        P.doc_list = L.d_list;
+        P.out_cap = L.out_cap;
+        P.gen = d_gen;
+        P.gen_ops = b->d_ops;
+        P.gen_props = b->d_props;
+        const void *fn = kKernels[cls].generate;
+        if (L.lds > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
+        void *args[] = {&P};
+        HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        std::vector<DocOut> part((size_t)n);
+        HIPCHK(hipMemcpy(part.data(), L.d_docout, sizeof(DocOut) * (size_t)n, hipMemcpyDeviceToHost));
+        (void)hipFree(L.d_out);
+        (void)hipFree(L.d_docout);
+        (void)hipFree(L.d_list);
+        std::vector<int32_t> again;
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t d = todo.empty() ? i : todo[(size_t)i];
+            outs[(size_t)d] = part[(size_t)i];
+            if (part[(size_t)i].status == MT_CAPACITY && part[(size_t)i].cap_kind == 1) again.push_back((int32_t)d);
+        }
+        if (again.empty() || cls + 1 >= mt::kNumClasses || class_lds(cls + 1) > (size_t)max_lds_bytes()) break;
+        todo.swap(again);
+    }
     (void)hipFree(d_gen);
     b->payload_units = 0;
     b->prop_records = 0;

@@ -66,7 +66,8 @@ class BatchStats(C.Structure):
     _fields_ = [("n_docs", C.c_int64), ("n_ops", C.c_int64), ("ops_applied", C.c_int64),
                 ("docs_failed", C.c_int64), ("max_oe", C.c_int32), ("max_slots", C.c_int32),
                 ("max_blocks", C.c_int32), ("max_heap", C.c_int32), ("lds_bytes", C.c_int32),
-                ("launches", C.c_int32), ("kernel_ms", C.c_float), ("total_ms", C.c_float)]
+                ("launches", C.c_int32), ("kernel_ms", C.c_float), ("total_ms", C.c_float),
+                ("lds_class", C.c_int32), ("reserved", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

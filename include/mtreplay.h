@@ -62,10 +62,11 @@ typedef struct mt_batch mt_batch;
 
 typedef struct mt_batch_options {
     int32_t chunk_size;      /* SnapshotV1 chunk size; 0 -> 10000 (snapshotV1.ts:40)              */
-    int32_t seg_cap;         /* per-doc LDS capacities; 0 -> derived from the ops per document     */
-    int32_t oe_cap;
-    int32_t blk_cap;
-    int32_t heap_cap;
+    int32_t seg_cap;         /* segment slots of the first LDS capacity class (rounded up to a
+                                class: 64 .. 2048); 0 -> derived from the ops per document        */
+    int32_t oe_cap;          /* reserved (entries / blocks / heap follow from the class)           */
+    int32_t blk_cap;         /* reserved                                                           */
+    int32_t heap_cap;        /* reserved                                                           */
     int32_t arena_factor;    /* text arena = factor * payload + 4096 code units; 0 -> 4            */
     int32_t pool_per_op;     /* prop pool words per annotate / props insert; 0 -> 96               */
     int32_t max_retries;     /* capacity-class escalations for docs that overflow; 0 -> 3          */
@@ -81,6 +82,8 @@ typedef struct mt_batch_stats {
     int32_t launches;       /* replay launches incl. capacity escalations                       */
     float kernel_ms;        /* device time of the replay launch(es) (hipEvents, batch stream)    */
     float total_ms;         /* mt_batch_run wall time incl. escalations                         */
+    int32_t lds_class;      /* segment slots of the first launch's capacity class               */
+    int32_t reserved;
 } mt_batch_stats;
 
 MT_API const char *mt_status_string(int code);

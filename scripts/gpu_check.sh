@@ -25,6 +25,10 @@ for step in "$@"; do
     phases3) run phases3 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --config 3 --docs 2048 --steps 1 --warmup 0 --no-cpu ;;
     docs256) run docs256 600 python -u bench.py --docs 256 --steps 2 --warmup 1 --no-cpu ;;
     docs1024) run docs1024 600 python -u bench.py --docs 1024 --steps 2 --warmup 1 --no-cpu ;;
+    pmc1) run pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc1 -o run -- python3 -u bench.py --docs 1024 --steps 1 --warmup 0 --no-cpu ;;
+    pmc2) run pmc2 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc2 -o run -- python3 -u bench.py --docs 1024 --steps 1 --warmup 0 --no-cpu ;;
+    pmcf) run pmcf 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf -o run -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu ;;
+    pmcw) run pmcw 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o run -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu ;;
     *) echo "unknown step $step" ;;
   esac
 done

@@ -99,9 +99,8 @@ def test_high_concurrency_tie_breaks():
 
 
 def test_small_capacity_escalation():
-    """Force a tiny LDS class so documents overflow and are re-run in larger classes."""
-    stats = _gen_batch_parity(O.gen_params(800, seed=3), 16, full_every=4, seg_cap=32, oe_cap=48, blk_cap=24,
-                              heap_cap=32, max_retries=6)
+    """Force the smallest LDS class so documents overflow and are re-run in larger classes."""
+    stats = _gen_batch_parity(O.gen_params(800, seed=3), 16, full_every=4, seg_cap=64, max_retries=6)
     assert stats["launches"] >= 2
 
 
