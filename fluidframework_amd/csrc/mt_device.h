@@ -36,12 +36,15 @@ constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
 // segment meta word
 //   [0,6)  clientId (short id)         [6,12) removedClientId (63 = none)
 //   [12]   Marker                       [13]   text ends with '\n'
-//   [14]   linked (in the tree)         [16,32) slot generation (heap entry validity)
+//   [14]   linked (in the tree)         [15]   unsettled (in the overlay list, see below)
+//   [16,32) slot generation (heap / overlay entry validity)
 constexpr uint32_t kMetaMarker = 1u << 12;
 constexpr uint32_t kMetaEndsNL = 1u << 13;
 constexpr uint32_t kMetaLinked = 1u << 14;
+constexpr uint32_t kMetaUnsettled = 1u << 15;
+constexpr uint16_t kNoBlock = 0xFFFFu;
 
-// one output record per oe entry (doc order), 8 x u32
+// one output record per leaf or end-of-leaf-block entry (doc order), 8 x u32
 struct OutRec {
     uint32_t len;    // cachedLength (0 for a block marker)
     int32_t seq;
@@ -64,7 +67,7 @@ struct DocOut {
     uint32_t text_top;  // text region high-water mark (code units)
     uint32_t pool_top;  // prop pool high-water mark (words)
     int32_t ops_done;   // ops applied before status != OK
-    int32_t max_oe;     // high-water marks (capacity planning)
+    int32_t max_oe;     // output entries (leaves + leaf blocks); then high-water marks
     int32_t max_slots;
     int32_t max_blocks;
     int32_t max_heap;
@@ -78,9 +81,10 @@ static_assert(sizeof(DocOut) == 64, "DocOut");
 // per-document capacities of the LDS-resident state
 struct Caps {
     int32_t seg;   // segment slots
-    int32_t oe;    // ordered entries (segments + one end marker per leaf block)
+    int32_t oe;    // output entries (segments + one end marker per leaf block)
     int32_t blk;   // blocks
     int32_t heap;  // zamboni heap entries
+    int32_t ulist; // unsettled-overlay list entries
 };
 
 // Capacity classes are compile-time: each class is its own kernel instantiation
@@ -89,21 +93,20 @@ struct Caps {
 constexpr int kClassSegs[] = {64, 128, 256, 512, 1024, 2048};
 constexpr int kNumClasses = 6;
 constexpr Caps class_caps(int seg) {
-    return Caps{seg, seg + seg / 2 + 16, seg / 2 + 16, (seg / 2 + 64) < (64 * kHeapRegs - 1) ? (seg / 2 + 64)
-                                                                                           : (64 * kHeapRegs - 1)};
+    return Caps{seg, seg + seg / 2 + 16, seg / 2 + 16,
+                (seg / 2 + 64) < (64 * kHeapRegs - 1) ? (seg / 2 + 64) : (64 * kHeapRegs - 1), seg + 64};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
-    uint32_t oe, len, seq, rseq, meta, ovl, props, toff, tcap, phash, sfree;
-    uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, scratch, bytes;
+    uint32_t len, seq, rseq, meta, ovl, props, toff, tcap, phash, sfree, sblk, ulist;
+    uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, bslen, bacc, scratch, bytes;
 };
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
 constexpr Layout make_layout(int seg) {
     const Caps c = class_caps(seg);
     Layout L{};
     uint32_t o = 0;
-    L.oe = o;      o = lds_align(o + 4u * c.oe);
     L.len = o;     o = lds_align(o + 4u * c.seg);
     L.seq = o;     o = lds_align(o + 4u * c.seg);
     L.rseq = o;    o = lds_align(o + 4u * c.seg);
@@ -114,12 +117,16 @@ constexpr Layout make_layout(int seg) {
     L.tcap = o;    o = lds_align(o + 4u * c.seg);
     L.phash = o;   o = lds_align(o + 4u * c.seg);
     L.sfree = o;   o = lds_align(o + 2u * c.seg);
+    L.sblk = o;    o = lds_align(o + 2u * c.seg);
+    L.ulist = o;   o = lds_align(o + 4u * c.ulist);
     L.bparent = o; o = lds_align(o + 2u * c.blk);
     L.bfree = o;   o = lds_align(o + 2u * c.blk);
     L.bchild = o;  o = lds_align(o + 16u * c.blk);
     L.bcount = o;  o = lds_align(o + 1u * c.blk);
     L.bleaf = o;   o = lds_align(o + 1u * c.blk);
     L.bscour = o;  o = lds_align(o + 1u * c.blk);
+    L.bslen = o;   o = lds_align(o + 4u * c.blk);
+    L.bacc = o;    o = lds_align(o + 4u * c.blk);
     L.scratch = o; o = lds_align(o + 4u * 256);
     L.bytes = o;
     return L;

@@ -1,26 +1,34 @@
 // mt_engine.hip — MI355X (gfx950) batch replay of sequenced merge-tree ops.
 //
-// One 64-lane wavefront (= one workgroup) owns one document for the whole op log; the
-// document's merge-tree lives in LDS as a flat, wave-scannable structure:
+// One 64-lane wavefront (= one workgroup) owns one document for the whole op log.  The
+// document's merge-tree lives in LDS as the reference's own B-tree (MaxNodesInBlock = 8,
+// mergeTree.ts:334): leaf blocks list segment slots, interior blocks list blocks, every
+// child list is one 16-byte row that a wave reads with one lane per child.
 //
-//   oe[]        document order of the tree's leaves: each entry is (leaf block id << 16 | slot);
-//               every leaf block ends with a marker entry (slot 0xFFFF), so empty leaf blocks
-//               (pack can create them, mergeTree.ts:1383-1386) stay addressable.
 //   s_*[slot]   segment fields (SoA): length, seq, removedSeq, client ids, overlap mask,
-//               prop-set id, text offset/capacity.
-//   b_*[block]  B-tree blocks (MaxNodesInBlock = 8): parent, child count, needsScour,
-//               interior child lists.  Leaf membership is implicit in oe.
-//   h_*         the zamboni heap (collections.ts:213-265), same algorithm, same tie order.
+//               prop-set id, text offset/capacity, leaf block.
+//   b_*[block]  children[8], count, parent, needsScour, and the block's SETTLED length.
+//   u_list      the unsettled segments (the collab window's "hot" set).
+//   heap        the zamboni heap (collections.ts:213-265), in VGPRs.
 //
-// Position resolution replaces PartialSequenceLengths (partialLengths.ts) by a per-op,
-// lane-parallel visibility test of every leaf (nodeLength, mergeTree.ts:1659-1699) and a
-// wave prefix scan; the B-tree walk of insertingWalk (mergeTree.ts:2345-2474) reduces to
-// "first entry that satisfies the leaf tie rule, else the end of the first leaf block whose
-// cumulative length reaches pos" (DESIGN.md "Flat insertingWalk").  Block splits, pack and
-// zamboni follow mergeTree.ts:1289-1478, 2476-2489 exactly, so leaf-block membership — and
-// hence SnapshotV1 bytes — match the reference.
+// Position resolution (PartialSequenceLengths, partialLengths.ts, in the reference) is a
+// settled/unsettled split.  A segment is *settled* once seq <= minSeq and it is either not
+// removed or removed at or below minSeq: every valid op view (refSeq >= minSeq) then sees
+// exactly `len` (not removed) or 0 (removed) of it, so the block sums b_slen are view
+// independent and maintained incrementally.  The few unsettled segments (inserted or
+// removed inside the collab window) form the overlay: per op, every lane takes one of
+// them, evaluates nodeLength (mergeTree.ts:1659-1699) for the op's (refSeq, clientId) and
+// adds it into b_acc along its ancestor chain (LDS atomics).  A block's view length is then
+// b_slen + b_acc, and insertingWalk (mergeTree.ts:2345-2474) / nodeMap (2903-2965) descend
+// the tree level by level, one lane per child, with an 8-lane prefix scan per level —
+// O(depth) LDS round trips per op instead of the O(segments) scans of a flat table.
+// refSeq < minSeq (outside valid logs) falls back to an overlay over every segment with
+// b_slen ignored, so block lengths stay the exact leaf sums either way.
 //
-// No MFMA: the path is integer scan / compaction work bound by LDS latency and HBM.
+// Block splits, pack and zamboni follow mergeTree.ts:1289-1478, 2476-2489 exactly, so
+// leaf-block membership — and hence SnapshotV1 bytes — match the reference.
+//
+// No MFMA: the path is integer scan / tree work bound by LDS latency.
 
 #include <hip/hip_runtime.h>
 
@@ -47,6 +55,20 @@ __device__ __forceinline__ uint32_t scan_incl(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
 }
+// inclusive prefix sum over lanes 0..7 (one child row); other lanes hold garbage
+__device__ __forceinline__ uint32_t scan8(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    return v;
+}
+// sum over each aligned group of 8 lanes (every lane of the group gets it)
+__device__ __forceinline__ uint32_t sum8(uint32_t v) {
+    v += (uint32_t)__shfl_xor((int)v, 1, 64);
+    v += (uint32_t)__shfl_xor((int)v, 2, 64);
+    v += (uint32_t)__shfl_xor((int)v, 4, 64);
+    return v;
+}
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int first_lane(uint64_t b) { return __builtin_ctzll(b); }
@@ -60,6 +82,10 @@ __device__ __forceinline__ void wsync() {
     asm volatile("" ::: "memory");
 }
 
+__device__ __forceinline__ void lds_add(uint32_t *p, uint32_t v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 __device__ __forceinline__ uint32_t hash_pair(uint32_t k, uint32_t v) {
     uint32_t h = k * 0x9E3779B1u ^ (v + 0x7F4A7C15u) * 0x85EBCA77u;
     h ^= h >> 15;
@@ -68,8 +94,8 @@ __device__ __forceinline__ uint32_t hash_pair(uint32_t k, uint32_t v) {
     return h | 1u;
 }
 
-// Phase cycle counters (MT_PROF builds only; tools/prof_phases.py): 0 kernel, 1 scans,
-// 2 split, 3 insert, 4 range walk, 5 zamboni, 6 oe shifts, 7 scour
+// Phase cycle counters (MT_PROF builds only): 0 kernel, 1 descents, 2 split, 3 insert,
+// 4 range walk, 5 zamboni, 6 overlay, 7 scour, 8 text, 9 heap, 10 pack, 11 settle
 #ifdef MT_PROF
 struct PfScope {
     uint64_t &acc;
@@ -82,11 +108,14 @@ struct PfScope {
 #define PF_SCOPE(k) (void)0
 #endif
 
-struct Loc {
-    int32_t idx;    // oe index
-    uint32_t excl;  // view position before entry idx
-    int32_t found;
-    int32_t marker;
+// result of a descent: leaf block, child index, view positions
+struct Walk {
+    int32_t blk;    // leaf block (-1: the walk found nothing)
+    int32_t k;      // insert mode: insert before child k (k == n: at the block end)
+    int32_t n;      // child count of blk
+    uint32_t base;  // view position of the block start
+    uint32_t excl;  // insert mode: view position before child k
+    int32_t ok;     // insert mode: the walk found an insertion point
 };
 
 template <int SEG>
@@ -94,17 +123,20 @@ struct Engine {
     static constexpr Caps cap = class_caps(SEG);
     static constexpr Layout lay = make_layout(SEG);
     // ---- LDS state
-    uint32_t *oe;
     uint32_t *s_len, *s_meta, *s_ovl, *s_props, *s_toff, *s_tcap, *s_phash;
     int32_t *s_seq, *s_rseq;
-    uint16_t *s_free;
+    uint16_t *s_free, *s_blk;
+    uint32_t *u_list;  // slot | generation << 16
     uint16_t *b_parent, *b_free, *b_child;
     uint8_t *b_count, *b_leaf;
     int8_t *b_scour;
+    uint32_t *b_slen, *b_acc;
     uint32_t *scratch;  // 256 words
     // ---- uniform scalars
-    int32_t n_oe, slot_top, n_free, blk_top, n_bfree, root, depth, hn;
-    int32_t min_seq, cur_seq, status;
+    int32_t slot_top, n_free, blk_top, n_bfree, root, depth, hn, nu;
+    int32_t min_seq, cur_seq, status, settled_min;
+    int32_t splits;                 // leaf/interior block splits so far (overlay staleness)
+    int32_t ov_splits, ov_full;     // overlay computed at `ov_splits`; full (refSeq < minSeq) mode
     uint32_t arena_top, pool_top;
     uint32_t pay_end, arena_base, arena_end, semi_t;  // text: payload | semispace A | semispace B
     uint32_t pool_base, pool_end, semi_p;             // prop pool: [0] reserved | A | B
@@ -113,10 +145,9 @@ struct Engine {
     // latency overlaps it (at most two splits per op)
     int32_t pend_n;
     uint32_t pend_slot0, pend_slot1, pend_ch0, pend_ch1;
-    int32_t max_oe, max_heap;
+    int32_t max_heap, max_u;
     uint32_t hk[kHeapRegs];
     int32_t hs[kHeapRegs];
-    int32_t split_mark;  // oe index of the end marker the last leaf split inserted, -1: none
     // ---- global
     uint16_t *text;
     uint32_t text_cap;
@@ -126,13 +157,13 @@ struct Engine {
     const uint8_t *value_flags;
     uint32_t n_values;
     int lane;
+    int32_t cap_kind;
 #ifdef MT_PROF
     uint64_t pf[kProfSlots];
 #endif
 
     // ------------------------------------------------------------------ layout
     MT_FI void carve(uint8_t *base) {
-        oe = (uint32_t *)(base + lay.oe);
         s_len = (uint32_t *)(base + lay.len);
         s_seq = (int32_t *)(base + lay.seq);
         s_rseq = (int32_t *)(base + lay.rseq);
@@ -143,16 +174,19 @@ struct Engine {
         s_tcap = (uint32_t *)(base + lay.tcap);
         s_phash = (uint32_t *)(base + lay.phash);
         s_free = (uint16_t *)(base + lay.sfree);
+        s_blk = (uint16_t *)(base + lay.sblk);
+        u_list = (uint32_t *)(base + lay.ulist);
         b_parent = (uint16_t *)(base + lay.bparent);
         b_free = (uint16_t *)(base + lay.bfree);
         b_child = (uint16_t *)(base + lay.bchild);
         b_count = (uint8_t *)(base + lay.bcount);
         b_leaf = (uint8_t *)(base + lay.bleaf);
         b_scour = (int8_t *)(base + lay.bscour);
+        b_slen = (uint32_t *)(base + lay.bslen);
+        b_acc = (uint32_t *)(base + lay.bacc);
         scratch = (uint32_t *)(base + lay.scratch);
     }
 
-    int32_t cap_kind;
     MT_FI void set_fail(int32_t st) {
         if (status == ST_OK) status = st;
     }
@@ -165,25 +199,26 @@ struct Engine {
 
     // ------------------------------------------------------------------ init
     MT_FI void init() {
-        n_oe = 0;
         slot_top = 0;
         n_free = 0;
         blk_top = 0;
         n_bfree = 0;
         hn = 0;
+        nu = 0;
         min_seq = 0;
         cur_seq = 0;
+        settled_min = 0;
         status = ST_OK;
         cap_kind = 0;
         pend_n = 0;
-        split_mark = -1;
-        max_oe = 0;
+        splits = 0;
+        ov_splits = -1;
+        ov_full = 0;
         max_heap = 0;
+        max_u = 0;
         // initialNode (mergeTree.ts:1125): an empty root leaf block
         root = alloc_block(1);
         depth = 1;
-        b_parent[root] = 0xFFFF;  // lane-uniform writes (every lane stores the same value)
-        oe_insert(0, (uint32_t)root << 16 | kMarkerSlot);
         // heap entry 0 is the sentinel LRUSegmentComparer.min = { maxSeq: -2 } (never compared)
         for (int i = 0; i < kHeapRegs; i++) {
             hk[i] = 0;
@@ -208,13 +243,6 @@ struct Engine {
         }
         return s;
     }
-    MT_FI void free_slot(int32_t s) {
-        uint32_t m = s_meta[s];
-        uint32_t gen = (m >> 16) + 1;
-        s_meta[s] = (gen << 16);  // unlinked, next generation
-        s_free[n_free] = (uint16_t)s;
-        n_free++;
-    }
     MT_FI int32_t alloc_block(int leaf) {
         int32_t b;
         if (n_bfree > 0) {
@@ -230,7 +258,8 @@ struct Engine {
         b_leaf[b] = (uint8_t)leaf;
         b_count[b] = 0;
         b_scour[b] = kScourUndef;
-        b_parent[b] = 0xFFFF;
+        b_parent[b] = kNoBlock;
+        b_slen[b] = 0;
         return b;
     }
     MT_FI void free_block(int32_t b) {
@@ -238,75 +267,9 @@ struct Engine {
         n_bfree++;
     }
 
-    // ------------------------------------------------------------------ oe shifting
-    // insert entry e before index p (lane-parallel shift right by one)
-    MT_FI void oe_insert(int32_t p, uint32_t e) {
-        PF_SCOPE(6);
-        if (n_oe + 1 > cap.oe) {
-            cap_fail(1);
-            return;
-        }
-        wsync();
-        for (int32_t base = ((n_oe - 1 - p) / kWave) * kWave + p; base >= p; base -= kWave) {
-            int32_t j = base + lane;
-            uint32_t v = 0;
-            bool ok = j < n_oe;
-            if (ok) v = oe[j];
-            wsync();
-            if (ok) oe[j + 1] = v;
-            wsync();
-        }
-        if (lane == 0) oe[p] = e;
-        n_oe++;
-        if (n_oe > max_oe) max_oe = n_oe;
-        wsync();
-    }
-    // move oe[from, n_oe) to start at `to` (to < from: left shift; to > from: right shift)
-    MT_FI void oe_move_tail(int32_t from, int32_t to) {
-        PF_SCOPE(6);
-        int32_t cnt = n_oe - from;
-        int32_t new_n = to + cnt;
-        if (new_n > cap.oe) {
-            cap_fail(1);
-            return;
-        }
-        wsync();
-        if (to < from) {
-            for (int32_t base = 0; base < cnt; base += kWave) {
-                int32_t j = base + lane;
-                uint32_t v = 0;
-                if (j < cnt) v = oe[from + j];
-                wsync();
-                if (j < cnt) oe[to + j] = v;
-                wsync();
-            }
-        } else if (to > from) {
-            for (int32_t base = ((cnt - 1) / kWave) * kWave; base >= 0; base -= kWave) {
-                int32_t j = base + lane;
-                uint32_t v = 0;
-                if (j < cnt) v = oe[from + j];
-                wsync();
-                if (j < cnt) oe[to + j] = v;
-                wsync();
-            }
-        }
-        n_oe = new_n;
-        if (n_oe > max_oe) max_oe = n_oe;
-        wsync();
-    }
-
     // ------------------------------------------------------------------ visibility
     // nodeLength of one leaf for (refSeq, clientId) + breakTie's leaf rule (mergeTree.ts:2248-2277)
-    __device__ __forceinline__ void view_of(uint32_t e, int32_t ref, uint32_t c, uint32_t &vlen, bool &tie,
-                                            bool &mk) const {
-        uint32_t slot = e & 0xFFFFu;
-        if (slot == kMarkerSlot) {
-            vlen = 0;
-            tie = false;
-            mk = true;
-            return;
-        }
-        mk = false;
+    __device__ __forceinline__ void view_of(uint32_t slot, int32_t ref, uint32_t c, uint32_t &vlen, bool &tie) const {
         uint32_t meta = s_meta[slot];
         int32_t seq = s_seq[slot];
         int32_t rseq = s_rseq[slot];
@@ -318,113 +281,192 @@ struct Engine {
         vlen = (vis && !rem) ? len : 0u;
         tie = !(rseq <= ref);
     }
-
-    // insertingWalk target for pos under (ref, c): see header comment
-    // Scanning may start at any index `from` whose view position `carry` is known and before
-    // which no entry satisfies the walk's stop condition.
-    MT_FI Loc locate(uint32_t pos, int32_t ref, uint32_t c, int32_t from = 0, uint32_t carry = 0) {
-        PF_SCOPE(1);
-        Loc L;
-        L.found = 0;
-        L.idx = -1;
-        L.excl = 0;
-        L.marker = 0;
-        for (int32_t base = from; base < n_oe; base += kWave) {
-            int32_t j = base + lane;
-            bool valid = j < n_oe;
-            uint32_t vlen = 0;
-            bool tie = false, mk = false;
-            if (valid) view_of(oe[j], ref, c, vlen, tie, mk);
-            uint32_t incl = scan_incl(vlen) + carry;
-            uint32_t excl = incl - vlen;
-            bool cond = valid && !mk && (incl > pos || (excl == pos && vlen == 0 && tie));
-            bool mhit = valid && mk && incl >= pos;
-            uint64_t b = ballot(cond || mhit);
-            if (b) {
-                int f = first_lane(b);
-                L.found = 1;
-                L.idx = base + f;
-                L.excl = rdl(excl, f);
-                L.marker = (int32_t)((ballot(mhit) >> f) & 1ull);
-                return L;
-            }
-            carry = rdl(incl, 63);
-        }
-        return L;
+    // a leaf's contribution to the settled block sums
+    __device__ __forceinline__ uint32_t settled_len(uint32_t slot) const {
+        uint32_t meta = s_meta[slot];
+        return (!(meta & kMetaUnsettled) && s_rseq[slot] == kNoneSeq) ? s_len[slot] : 0u;
     }
 
-    // the visible segment strictly containing pos (excl < pos < excl + vlen) at or after `from`:
-    // the one ensureIntervalBoundary splits.  found = 0 when pos is already a boundary.
-    MT_FI Loc containing(uint32_t pos, int32_t ref, uint32_t c, int32_t from, uint32_t carry) {
-        PF_SCOPE(1);
-        Loc L;
-        L.found = 0;
-        L.idx = -1;
-        L.excl = 0;
-        L.marker = 0;
-        for (int32_t base = from; base < n_oe; base += kWave) {
-            int32_t j = base + lane;
-            bool valid = j < n_oe;
-            uint32_t vlen = 0;
-            bool tie = false, mk = false;
-            if (valid) view_of(oe[j], ref, c, vlen, tie, mk);
-            uint32_t incl = scan_incl(vlen) + carry;
-            uint32_t excl = incl - vlen;
-            uint64_t b = ballot(valid && incl > pos);
-            if (b) {
-                int f = first_lane(b);
-                uint32_t e = rdl(excl, f);
-                if (e < pos) {
-                    L.found = 1;
-                    L.idx = base + f;
-                    L.excl = e;
+    // ------------------------------------------------------------------ ancestor chains
+    // every active lane adds v into arr[] on the chain leaf block b -> root (all leaves sit at
+    // depth - 1, so the walk is `depth` uniform steps)
+    MT_FI void chain_add(uint32_t *arr, bool act, uint32_t b, uint32_t v) {
+        for (int32_t l = 0; l < depth; l++) {
+            if (act && b != kNoBlock) {
+                lds_add(&arr[b], v);
+                b = b_parent[b];
+            }
+        }
+    }
+    // uniform: b_slen += v on the chain b -> root
+    MT_FI void chain_add_uniform(int32_t b, uint32_t v) {
+        wsync();
+        while (b != (int32_t)kNoBlock) {
+            uint32_t x = b_slen[b];
+            int32_t p = b_parent[b];
+            b_slen[b] = x + v;
+            b = p;
+        }
+        wsync();
+    }
+
+    MT_FI void u_push(uint32_t slot) {
+        if (nu >= cap.ulist) {
+            cap_fail(1);
+            return;
+        }
+        u_list[nu] = slot | (s_meta[slot] & 0xFFFF0000u);
+        nu++;
+        if (nu > max_u) max_u = nu;
+    }
+
+    // Per-op overlay: b_acc[B] = sum of nodeLength(refSeq, c) over the unsettled segments under
+    // B (or over all segments in full mode).  Also drops stale list entries.
+    MT_FI void overlay(int32_t ref, uint32_t c) {
+        PF_SCOPE(6);
+        wsync();
+        for (int32_t i = lane; i < blk_top; i += kWave) b_acc[i] = 0u;
+        wsync();
+        ov_full = ref < min_seq;
+        if (!ov_full) {
+            int32_t w = 0;
+            for (int32_t base = 0; base < nu; base += kWave) {
+                const int32_t j = base + lane;
+                const bool in = j < nu;
+                const uint32_t e = in ? u_list[j] : 0u;
+                const uint32_t slot = e & 0xFFFFu;
+                bool valid = false;
+                if (in) {
+                    uint32_t meta = s_meta[slot];
+                    valid = (meta & kMetaUnsettled) && (meta & kMetaLinked) && ((meta ^ e) & 0xFFFF0000u) == 0u;
                 }
-                return L;
+                const uint64_t vm = ballot(valid);
+                wsync();
+                if (valid) u_list[w + __popcll(vm & ((1ull << lane) - 1ull))] = e;
+                w += __popcll(vm);
+                uint32_t vlen = 0, b = 0;
+                bool tie;
+                if (valid) {
+                    view_of(slot, ref, c, vlen, tie);
+                    b = s_blk[slot];
+                }
+                chain_add(b_acc, valid && vlen > 0u, b, vlen);
             }
-            carry = rdl(incl, 63);
+            nu = w;
+        } else {
+            for (int32_t base = 0; base < slot_top; base += kWave) {
+                const int32_t slot = base + lane;
+                bool live = slot < slot_top && (s_meta[slot] & kMetaLinked);
+                uint32_t vlen = 0, b = 0;
+                bool tie;
+                if (live) {
+                    view_of((uint32_t)slot, ref, c, vlen, tie);
+                    b = s_blk[slot];
+                }
+                chain_add(b_acc, live && vlen > 0u, b, vlen);
+            }
         }
-        return L;
+        ov_splits = splits;
+        wsync();
+    }
+    MT_FI void ensure_overlay(int32_t ref, uint32_t c) {
+        if (ov_splits != splits) overlay(ref, c);
     }
 
-    // MergeTree.getLength(refSeq, clientId) (generator)
-    MT_FI uint32_t view_length(int32_t ref, uint32_t c) {
-        uint32_t carry = 0;
-        for (int32_t base = 0; base < n_oe; base += kWave) {
-            int32_t j = base + lane;
-            uint32_t vlen = 0;
-            bool tie, mk;
-            if (j < n_oe) view_of(oe[j], ref, c, vlen, tie, mk);
-            carry = rdl(scan_incl(vlen) + carry, 63);
+    // settle every overlay entry that minSeq has caught up with (before zamboni scours)
+    MT_FI void settle_all() {
+        PF_SCOPE(11);
+        int32_t w = 0;
+        wsync();
+        for (int32_t base = 0; base < nu; base += kWave) {
+            const int32_t j = base + lane;
+            const bool in = j < nu;
+            const uint32_t e = in ? u_list[j] : 0u;
+            const uint32_t slot = e & 0xFFFFu;
+            bool valid = false, elig = false;
+            uint32_t meta = 0, add = 0, b = 0;
+            if (in) {
+                meta = s_meta[slot];
+                valid = (meta & kMetaUnsettled) && (meta & kMetaLinked) && ((meta ^ e) & 0xFFFF0000u) == 0u;
+                if (valid) {
+                    int32_t seq = s_seq[slot], rseq = s_rseq[slot];
+                    elig = seq <= min_seq && (rseq == kNoneSeq || rseq <= min_seq);
+                    if (elig && rseq == kNoneSeq) add = s_len[slot];
+                    b = s_blk[slot];
+                }
+            }
+            const bool keep = valid && !elig;
+            const uint64_t km = ballot(keep);
+            wsync();
+            if (keep) u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = e;
+            if (elig) s_meta[slot] = meta & ~kMetaUnsettled;
+            w += __popcll(km);
+            chain_add(b_slen, elig && add > 0u, b, add);
         }
-        return carry;
+        nu = w;
+        settled_min = min_seq;
+        ov_splits = -1;  // b_slen moved under the overlay
+        wsync();
     }
 
-    // first oe index with entry predicate; kind 0: slot == key, kind 1: block == key
-    MT_FI int32_t find_entry(uint32_t key, int kind, int32_t from = 0) {
-        for (int32_t base = from; base < n_oe; base += kWave) {
-            int32_t j = base + lane;
-            bool hit = false;
-            if (j < n_oe) {
-                uint32_t e = oe[j];
-                hit = kind == 0 ? ((e & 0xFFFFu) == key) : ((e >> 16) == key);
+    // ------------------------------------------------------------------ descent
+    // insertingWalk (mergeTree.ts:2345-2474) in insert mode: at every interior level the first
+    // child whose cumulative view length reaches pos (breakTie is true for blocks); in the leaf
+    // block the first leaf with pos < len or the leaf tie rule, else the block end.
+    // strict mode (nodeMap's start < len, mergeTree.ts:2903-2965): first child whose cumulative
+    // length exceeds pos; returns only the leaf block and its start position.
+    MT_FI Walk descend(uint32_t pos, int32_t ref, uint32_t c, bool strict) {
+        PF_SCOPE(1);
+        Walk W;
+        W.blk = -1;
+        W.k = 0;
+        W.n = 0;
+        W.base = 0;
+        W.excl = 0;
+        W.ok = 0;
+        int32_t N = root;
+        uint32_t base = 0;
+        const bool lanes8 = lane < kMaxNodes;
+        for (int32_t l = 0; l + 1 < depth; l++) {
+            const int32_t n = b_count[N];
+            uint32_t ch = 0, v = 0;
+            if (lane < n) {
+                ch = b_child[N * 8 + lane];
+                v = b_acc[ch] + (ov_full ? 0u : b_slen[ch]);
             }
-            uint64_t b = ballot(hit);
-            if (b) return base + first_lane(b);
+            const uint32_t incl = scan8(v) + base;
+            const uint64_t hb = ballot(lanes8 && lane < n && (strict ? incl > pos : incl >= pos));
+            if (!hb) return W;
+            const int f = first_lane(hb);
+            base = rdl(incl - v, f);
+            N = (int32_t)rdl(ch, f);
         }
-        return -1;
-    }
-    // first index of block `blk`'s range, given an index inside it (ranges are <= 9 entries)
-    MT_FI int32_t block_start_near(uint32_t blk, int32_t inside) {
-        int32_t j = inside - 8 + lane;
-        bool hit = lane < 17 && j >= 0 && j < n_oe && (oe[j] >> 16) == blk;
-        uint64_t b = ballot(hit);
-        return inside - 8 + first_lane(b);
+        const int32_t n = b_count[N];
+        W.blk = N;
+        W.n = n;
+        W.base = base;
+        if (strict) return W;
+        uint32_t vlen = 0;
+        bool tie = false;
+        if (lane < n) view_of(b_child[N * 8 + lane], ref, c, vlen, tie);
+        const uint32_t incl = scan8(vlen) + base;
+        const uint32_t excl = incl - vlen;
+        const uint64_t cb = ballot(lanes8 && lane < n && (incl > pos || (excl == pos && vlen == 0u && tie)));
+        if (cb) {
+            const int f = first_lane(cb);
+            W.k = f;
+            W.excl = rdl(excl, f);
+            W.ok = 1;
+        } else {
+            const uint32_t end = n > 0 ? rdl(incl, n - 1) : base;
+            W.k = n;
+            W.excl = end;
+            W.ok = end == pos;
+        }
+        return W;
     }
 
     // ------------------------------------------------------------------ text helpers
-    MT_FI bool text_ends_nl(uint32_t toff, uint32_t len) const {
-        return len > 0 && text[toff + len - 1] == (uint16_t)'\n';
-    }
     // lane-parallel copy of n code units inside the doc's text region
     MT_FI void text_copy(uint32_t dst, uint32_t src, uint32_t n) {
         for (uint32_t i = lane; i < n; i += kWave) text[dst + i] = text[src + i];
@@ -445,24 +487,24 @@ struct Engine {
         return o;
     }
 
-    // copy every linked segment's arena text into the other semispace (document order)
+    // copy every linked segment's arena text into the other semispace
     MT_FI void text_gc() {
         uint32_t nb = arena_base == pay_end ? pay_end + semi_t : pay_end;
         uint32_t top = nb;
         wsync();
-        for (int32_t base = 0; base < n_oe; base += kWave) {
-            int32_t j = base + lane;
-            uint32_t slot = j < n_oe ? (oe[j] & 0xFFFFu) : kMarkerSlot;
+        for (int32_t base = 0; base < slot_top; base += kWave) {
+            const int32_t slot = base + lane;
             bool mv = false;
-            if (slot != kMarkerSlot) {
+            if (slot < slot_top) {
+                uint32_t m = s_meta[slot];
                 uint32_t t = s_toff[slot];
-                mv = !(s_meta[slot] & kMetaMarker) && t >= arena_base && t < arena_end;
+                mv = (m & kMetaLinked) && !(m & kMetaMarker) && t >= arena_base && t < arena_end;
             }
-            uint64_t m = ballot(mv);
-            while (m) {
-                int f = first_lane(m);
-                m &= m - 1;
-                uint32_t sl = rdl(slot, f);
+            uint64_t msk = ballot(mv);
+            while (msk) {
+                int f = first_lane(msk);
+                msk &= msk - 1;
+                uint32_t sl = (uint32_t)(base + f);
                 uint32_t len = s_len[sl];
                 uint32_t cap16 = (len + 15u) & ~15u;
                 if (cap16 == 0) cap16 = 16;
@@ -484,36 +526,43 @@ struct Engine {
         wsync();
     }
 
-    // make room for `words` in the prop pool (semispace copy of the live sets when full)
+    // make room for `words` in the prop pool: semispace copy of the live sets when full
+    // (Cheney-style: a copied record's header becomes a forwarding pointer, so sets shared by
+    // several segments are copied once)
     MT_FI void pool_reserve(uint32_t words) {
         if (pool_top + words <= pool_end) return;
         uint32_t nb = pool_base == 1u ? 1u + semi_p : 1u;
-        uint32_t top = nb, last_old = 0, last_new = 0;
+        uint32_t top = nb;
         wsync();
-        for (int32_t base = 0; base < n_oe; base += kWave) {
-            int32_t j = base + lane;
-            uint32_t slot = j < n_oe ? (oe[j] & 0xFFFFu) : kMarkerSlot;
-            bool mv = slot != kMarkerSlot && s_props[slot] != 0u;
+        for (int32_t base = 0; base < slot_top; base += kWave) {
+            const int32_t slot = base + lane;
+            bool mv = slot < slot_top && (s_meta[slot] & kMetaLinked) && s_props[slot] != 0u;
             uint64_t m = ballot(mv);
             while (m) {
                 int f = first_lane(m);
                 m &= m - 1;
-                uint32_t sl = rdl(slot, f);
+                uint32_t sl = (uint32_t)(base + f);
                 uint32_t old = s_props[sl];
-                if (old != last_old) {
-                    uint32_t w = 2u + 2u * pool[old];
+                uint32_t hdr = pool[old];
+                uint32_t nid;
+                if (hdr == 0xFFFFFFFFu) {
+                    nid = pool[old + 1];
+                } else {
+                    uint32_t w = 2u + 2u * hdr;
                     if (top + w > nb + semi_p) {
                         cap_fail(3);
                         return;
                     }
                     for (uint32_t i = lane; i < w; i += kWave) pool[top + i] = pool[old + i];
-                    last_old = old;
-                    last_new = top;
+                    wsync();
+                    nid = top;
                     top += w;
+                    pool[old] = 0xFFFFFFFFu;
+                    pool[old + 1] = nid;
                 }
-                s_props[sl] = last_new;
+                s_props[sl] = nid;
+                wsync();
             }
-            wsync();
         }
         pool_base = nb;
         pool_end = nb + semi_p;
@@ -538,10 +587,12 @@ struct Engine {
         b_child[nr * 8 + 0] = (uint16_t)root;
         b_child[nr * 8 + 1] = (uint16_t)split_node;
         b_count[nr] = 2;
+        b_slen[nr] = b_slen[root] + b_slen[split_node];
         b_parent[root] = (uint16_t)nr;
         b_parent[split_node] = (uint16_t)nr;
         root = nr;
         depth++;
+        wsync();
     }
 
     // insertingWalk's "insert the split-off node after its source" (mergeTree.ts:2446-2453),
@@ -564,15 +615,21 @@ struct Engine {
             // split the interior block p: children 4..7 move to m
             int32_t m = alloc_block(0);
             if (status) return;
+            splits++;
             wsync();
-            if (lane < 4) {
-                uint16_t c = b_child[p * 8 + 4 + lane];
-                b_child[m * 8 + lane] = c;
+            uint32_t sl = 0;
+            if (lane >= 4 && lane < 8) {
+                uint16_t c = b_child[p * 8 + lane];
+                b_child[m * 8 + lane - 4] = c;
                 b_parent[c] = (uint16_t)m;
+                sl = b_slen[c];
             }
+            const uint32_t moved = rdl(sum8(lane >= 4 && lane < 8 ? sl : 0u), 0);
             wsync();
             b_count[m] = 4;
             b_count[p] = 4;
+            b_slen[m] = moved;
+            b_slen[p] = b_slen[p] - moved;
             wsync();
             if (p == root) {
                 update_root(m);
@@ -584,57 +641,63 @@ struct Engine {
         }
     }
 
-    // MergeTree.split on a leaf block whose range starts at s and now holds 8 children.
-    // Returns the new right block.
-    MT_FI int32_t split_leaf(int32_t blk, int32_t s) {
+    // MergeTree.split on a leaf block that now holds 8 children; returns the new right block.
+    MT_FI int32_t split_leaf(int32_t blk) {
         int32_t nb = alloc_block(1);
         if (status) return blk;
+        splits++;
         wsync();
-        // children 4..7 and the block's end marker move to the new block
-        if (lane >= 4 && lane <= 8) {
-            uint32_t e = oe[s + lane];
-            oe[s + lane] = ((uint32_t)nb << 16) | (e & 0xFFFFu);
+        uint32_t sl = 0;
+        if (lane >= 4 && lane < 8) {
+            uint16_t c = b_child[blk * 8 + lane];
+            b_child[nb * 8 + lane - 4] = c;
+            s_blk[c] = (uint16_t)nb;
+            sl = settled_len(c);
         }
+        const uint32_t moved = rdl(sum8(lane >= 4 && lane < 8 ? sl : 0u), 0);
         wsync();
         b_count[nb] = 4;
         b_count[blk] = 4;
-        split_mark = s + 4;
-        oe_insert(s + 4, ((uint32_t)blk << 16) | kMarkerSlot);
-        if (status) return nb;
+        b_slen[nb] = moved;
+        b_slen[blk] = b_slen[blk] - moved;
+        wsync();
         if (blk == root) update_root(nb);
         else insert_child_after(b_parent[blk], blk, nb);
         return nb;
     }
 
     // ------------------------------------------------------------------ split / insert leaves
-    // insert a leaf before oe index idx into the leaf block owning oe[idx]; returns the
-    // block the new leaf ends up in (after a possible split)
-    MT_FI int32_t insert_leaf(int32_t idx, uint32_t slot) {
-        uint32_t blk = rfl(oe[idx] >> 16);
-        oe_insert(idx, (blk << 16) | slot);
-        if (status) return (int32_t)blk;
-        int32_t cnt = b_count[blk] + 1;
-        b_count[blk] = (uint8_t)cnt;
+    // insert slot before child k of leaf block blk; returns the block the new leaf ends up in
+    MT_FI int32_t insert_leaf(int32_t blk, int32_t k, uint32_t slot) {
+        const int32_t n = b_count[blk];
         wsync();
-        if (cnt >= kMaxNodes) {
-            int32_t s = block_start_near(blk, idx);
-            int32_t nb = split_leaf((int32_t)blk, s);
-            if (idx - s >= 4) return nb;
+        uint16_t v = 0;
+        const bool mv = lane >= k && lane < n;
+        if (mv) v = b_child[blk * 8 + lane];
+        wsync();
+        if (mv) b_child[blk * 8 + lane + 1] = v;
+        wsync();
+        b_child[blk * 8 + k] = (uint16_t)slot;
+        s_blk[slot] = (uint16_t)blk;
+        b_count[blk] = (uint8_t)(n + 1);
+        wsync();
+        if (n + 1 >= kMaxNodes) {
+            int32_t nb = split_leaf(blk);
+            if (k >= kMaxNodes / 2) return nb;
         }
-        return (int32_t)blk;
+        return blk;
     }
 
     // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568,
-    // textSegment.ts:103-111): the right part becomes a new leaf right after the left one
-    // Returns the left half's oe index afterwards (a leaf split may insert an end marker before it).
-    MT_FI int32_t split_at(int32_t idx, uint32_t r) {
+    // textSegment.ts:103-111): the right part becomes a new leaf right after child k of blk.
+    // The settled sums do not change (both halves inherit the segment's state).
+    MT_FI void split_at(int32_t blk, int32_t k, uint32_t r) {
         PF_SCOPE(2);
-        split_mark = -1;
-        uint32_t slot = rfl(oe[idx] & 0xFFFFu);
+        uint32_t slot = rfl((uint32_t)b_child[blk * 8 + k]);
         uint32_t meta = s_meta[slot];
-        if (meta & kMetaMarker) return idx;  // Marker.createSplitSegmentAt returns undefined
+        if (meta & kMetaMarker) return;  // Marker.createSplitSegmentAt returns undefined
         int32_t ns = alloc_slot();
-        if (ns < 0) return idx;
+        if (ns < 0) return;
         uint32_t len = s_len[slot], toff = s_toff[slot], tcap = s_tcap[slot];
         uint32_t last = text[toff + r - 1];  // consumed in resolve_splits()
         if (pend_n == 0) {
@@ -654,15 +717,13 @@ struct Engine {
         s_toff[ns] = toff + r;
         s_tcap[ns] = tcap - r;
         uint32_t gen = s_meta[ns] & 0xFFFF0000u;
-        s_meta[ns] = (meta & 0x0000FFFFu) | gen;  // inherits ends-NL of the original tail
+        s_meta[ns] = (meta & 0x0000FFFFu) | gen;  // inherits ends-NL of the tail, linked, unsettled
         s_len[slot] = r;
         s_tcap[slot] = r;
         wsync();
-        insert_leaf(idx + 1, (uint32_t)ns);
-        return shifted(idx);
+        if (meta & kMetaUnsettled) u_push((uint32_t)ns);
+        insert_leaf(blk, k + 1, (uint32_t)ns);
     }
-    // index of a pre-split entry at or before the split point after the last split_at
-    MT_FI int32_t shifted(int32_t i) const { return (split_mark >= 0 && split_mark <= i) ? i + 1 : i; }
 
     MT_FI void resolve_splits() {
         if (pend_n > 0) {
@@ -677,6 +738,27 @@ struct Engine {
         wsync();
     }
 
+    // ensureIntervalBoundary (mergeTree.ts:2241-2245): split the leaf that strictly contains pos
+    // in the op's view.  Returns the insert-mode walk for pos *after* the split.
+    MT_FI Walk boundary(uint32_t pos, int32_t ref, uint32_t c) {
+        ensure_overlay(ref, c);
+        Walk W = descend(pos, ref, c, false);
+        if (W.blk >= 0 && W.ok && W.k < W.n && W.excl < pos) {
+            const int32_t s0 = splits;
+            split_at(W.blk, W.k, pos - W.excl);
+            if (status) return W;
+            if (splits == s0) {
+                // no block split: the left half ends at pos, the right half (k + 1) starts there
+                W.k += 1;
+                W.n += 1;
+                W.excl = pos;
+            } else {
+                ensure_overlay(ref, c);
+                W = descend(pos, ref, c, false);
+            }
+        }
+        return W;
+    }
 
     // addToLRUSet (mergeTree.ts:1273-1283); seq > currentSeq holds for sequenced remote ops
     MT_FI void add_to_lru(int32_t blk, uint32_t slot, int32_t seq) {
@@ -887,20 +969,19 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ scour / pack / zamboni
-    // scourNode (mergeTree.ts:1289-1365) over the leaf entries oe[s, s+n), n <= 64, which may
-    // span several blocks (their end markers reset the append chain, as each scourNode call
-    // starts afresh).  Kept slots are appended to hold[nh..] in order; returns the new count.
-    // The leaves are gathered one per lane; only the TextSegment.canAppend chain (textSegment.ts:
-    // 63-68, whose length test depends on earlier appends) runs serially, on scalars.
-    MT_FI int32_t scour_range(int32_t s, int32_t n, uint32_t *hold, int32_t nh) {
+    // scourNode (mergeTree.ts:1289-1365) over up to 64 leaves, one per lane (`slot`, valid for
+    // lane < n), which may come from several blocks: `startM` marks each block's first leaf,
+    // where the append chain restarts (each scourNode call starts afresh).  Kept slots are
+    // written to hold[0..] in order; returns their count.  Only settled leaves are merged or
+    // unlinked (settle_all ran at this minSeq), so the settled block sums are unchanged.
+    // The TextSegment.canAppend chain (textSegment.ts:63-68, whose length test depends on
+    // earlier appends) runs serially on scalars.
+    MT_FI int32_t scour(uint32_t slot, int32_t n, uint64_t startM, uint32_t *hold) {
         PF_SCOPE(7);
         const bool in = lane < n;
-        const uint32_t e = in ? oe[s + lane] : (uint32_t)kMarkerSlot;
-        const uint32_t slot = e & 0xFFFFu;
-        const bool mk = slot == kMarkerSlot;
         int32_t rseq = kNoneSeq, seq = 0;
         uint32_t meta = 0, len = 0, props = 0, ph = 0, toff = 0, tcap = 0;
-        if (!mk) {
+        if (in) {
             rseq = s_rseq[slot];
             seq = s_seq[slot];
             meta = s_meta[slot];
@@ -910,14 +991,14 @@ struct Engine {
             toff = s_toff[slot];
             tcap = s_tcap[slot];
         }
-        const bool rem = !mk && rseq != kNoneSeq;
-        const bool cand = !mk && !rem && seq <= min_seq;
+        const bool rem = in && rseq != kNoneSeq;
+        const bool cand = in && !rem && seq <= min_seq;
         const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
         const bool peq = lane > 0 && pprev == props;
         const bool pmaybe = lane > 0 && !peq && props != 0u && pprev != 0u && hprev == ph;
         const uint64_t candM = ballot(cand), peqM = ballot(peq), maybeM = ballot(pmaybe);
         const uint64_t freeR = ballot(rem && rseq <= min_seq);
-        const uint64_t liveM = ballot(in && !mk);
+        const uint64_t liveM = ballot(in);
         uint64_t mergeM = 0;
         uint32_t head = 0;  // lane f (merged): lane of its chain head
         {
@@ -925,6 +1006,7 @@ struct Engine {
             uint32_t acc = 0;
             bool pnl = false, pmk = false;
             for (int32_t k = 0; k < n; k++) {
+                if ((startM >> k) & 1ull) prev = -1;
                 if (!((candM >> k) & 1ull)) {
                     prev = -1;
                     continue;
@@ -996,7 +1078,7 @@ struct Engine {
                     wsync();
                     const uint32_t ncap = 2u * need;
                     const uint32_t dst = arena_alloc(ncap);
-                    if (status) return nh;
+                    if (status) return 0;
                     if (text_gcs != gcs0) {
                         ptoff = s_toff[hslot];
                         stoff = s_toff[fslot];
@@ -1019,14 +1101,15 @@ struct Engine {
         const uint64_t freeM = freeR | mergeM;
         const uint64_t holdM = liveM & ~freeM;
         const uint64_t below = (1ull << lane) - 1ull;
+        wsync();
         if ((freeM >> lane) & 1ull) {
             s_meta[slot] = ((meta >> 16) + 1u) << 16;  // unlinked, next generation
             s_free[n_free + __popcll(freeM & below)] = (uint16_t)slot;
         }
-        if ((holdM >> lane) & 1ull) hold[nh + __popcll(holdM & below)] = slot;
+        if ((holdM >> lane) & 1ull) hold[__popcll(holdM & below)] = slot;
         n_free += __popcll(freeM);
         wsync();
-        return nh + __popcll(holdM);
+        return __popcll(holdM);
     }
 
     // pack for an interior block `blk` (its parent's children are interior blocks);
@@ -1056,14 +1139,18 @@ struct Engine {
                 if (status) return;
                 int32_t cnt = base + (i < extra ? 1 : 0);
                 wsync();
+                uint32_t sl = 0;
                 if (lane < cnt) {
                     uint16_t g = (uint16_t)hold[read + lane];
                     b_child[nbi * 8 + lane] = g;
                     b_parent[g] = (uint16_t)nbi;
+                    sl = b_slen[g];
                 }
+                const uint32_t tot = rdl(sum8(lane < 8 ? sl : 0u), 0);
                 wsync();
                 b_count[nbi] = (uint8_t)cnt;
                 b_parent[nbi] = (uint16_t)parent;
+                b_slen[nbi] = tot;
                 b_child[parent * 8 + i] = (uint16_t)nbi;
                 read += cnt;
             }
@@ -1074,56 +1161,60 @@ struct Engine {
         }
     }
 
-    // pack for a leaf block (mergeTree.ts:1368-1420)
-    MT_FI void pack_leaf(int32_t blk, int32_t hint) {
-        int32_t parent = b_parent[blk];
-        int32_t pn = b_count[parent];
-        int32_t first = b_child[parent * 8 + 0];
-        int32_t s0 = find_entry((uint32_t)first, 1, 0);
-        if (s0 < 0) {
-            set_fail(ST_INTERNAL);
-            return;
-        }
-        (void)hint;
+    // pack for a leaf block (mergeTree.ts:1368-1420): every sibling leaf block is scoured and
+    // the surviving leaves are regrouped into floor(total / 4) (1..7) new leaf blocks
+    MT_FI void pack_leaf(int32_t blk) {
+        PF_SCOPE(10);
+        const int32_t parent = b_parent[blk];
+        const int32_t pn = b_count[parent];
+        uint32_t *gat = scratch;
         uint32_t *hold = scratch + 128;
-        int32_t s = s0;
-        for (int32_t ci = 0; ci < pn; ci++) s += b_count[b_child[parent * 8 + ci]] + 1;  // leaves + marker
-        if (s - s0 > kWave) {
+        int32_t total = 0;
+        uint64_t startM = 0;
+        for (int32_t ci = 0; ci < pn; ci++) {
+            int32_t cb = b_child[parent * 8 + ci];
+            int32_t cn = b_count[cb];
+            wsync();
+            if (lane < cn) gat[total + lane] = b_child[cb * 8 + lane];
+            if (cn > 0) startM |= 1ull << total;
+            total += cn;
+            wsync();
+        }
+        if (total > kWave) {
             set_fail(ST_INTERNAL);
             return;
         }
-        int32_t total;
-        {
-            PF_SCOPE(10);
-            total = scour_range(s0, s - s0, hold, 0);
-        }
+        const uint32_t slot = lane < total ? gat[lane] : 0u;
+        const int32_t nk = scour(slot, total, startM, hold);
         if (status) return;
-        int32_t old_end = s;  // one past the last marker
-        int32_t child_count = total / (kMaxNodes / 2);
+        int32_t child_count = nk / (kMaxNodes / 2);
         if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
         if (child_count < 1) child_count = 1;
-        int32_t base = total / child_count, extra = total % child_count;
+        const int32_t base = nk / child_count, extra = nk % child_count;
         for (int32_t i = 0; i < pn; i++) free_block(b_child[parent * 8 + i]);
-        int32_t new_len = total + child_count;
-        oe_move_tail(old_end, s0 + new_len);
-        if (status) return;
-        // write the regrouped range, one new leaf block at a time
-        int32_t read = 0, w = s0;
+        int32_t read = 0;
         for (int32_t i = 0; i < child_count; i++) {
             int32_t nbi = alloc_block(1);
             if (status) return;
             int32_t cnt = base + (i < extra ? 1 : 0);
             wsync();
-            if (lane < cnt) oe[w + lane] = ((uint32_t)nbi << 16) | hold[read + lane];
-            if (lane == cnt) oe[w + lane] = ((uint32_t)nbi << 16) | kMarkerSlot;
+            uint32_t sl = 0;
+            if (lane < cnt) {
+                uint32_t c = hold[read + lane];
+                b_child[nbi * 8 + lane] = (uint16_t)c;
+                s_blk[c] = (uint16_t)nbi;
+                sl = settled_len(c);
+            }
+            const uint32_t tot = rdl(sum8(lane < 8 ? sl : 0u), 0);
             wsync();
             b_count[nbi] = (uint8_t)cnt;
             b_parent[nbi] = (uint16_t)parent;
+            b_slen[nbi] = tot;
             b_child[parent * 8 + i] = (uint16_t)nbi;
             read += cnt;
-            w += cnt + 1;
         }
         b_count[parent] = (uint8_t)child_count;
+        splits++;  // structure changed under the overlay
         wsync();
         if (child_count < kMaxNodes / 2 && parent != root) pack_interior(parent);
     }
@@ -1133,34 +1224,28 @@ struct Engine {
         PF_SCOPE(5);
         for (int it = 0; it < kZamboniMax; it++) {
             if (hn < 1 || hseq(1) > min_seq) break;
+            if (settled_min != min_seq) settle_all();
             uint32_t key;
             int32_t mseq;
             heap_get(key, mseq);
-            uint32_t slot = key & 0xFFFFu;
-            uint32_t meta = s_meta[slot];
+            const uint32_t slot = key & 0xFFFFu;
+            const uint32_t meta = s_meta[slot];
             if ((meta & 0xFFFF0000u) != (key & 0xFFFF0000u) || !(meta & kMetaLinked)) continue;  // parent undefined
-            int32_t idx = find_entry(slot, 0, 0);
-            if (idx < 0) {
-                set_fail(ST_INTERNAL);
-                return;
-            }
-            int32_t blk = rfl((int32_t)(oe[idx] >> 16));
+            const int32_t blk = s_blk[slot];
             if (b_scour[blk] == kScourFalse) continue;
-            int32_t s = block_start_near((uint32_t)blk, idx);
-            int32_t cnt = b_count[blk];
+            const int32_t cnt = b_count[blk];
+            const uint32_t cs = lane < cnt ? (uint32_t)b_child[blk * 8 + lane] : 0u;
             uint32_t *hold = scratch;
-            int32_t nk = scour_range(s, cnt, hold, 0);
+            const int32_t nk = scour(cs, cnt, 1ull, hold);
             if (status) return;
             b_scour[blk] = kScourFalse;
             if (nk < cnt) {
                 wsync();
-                if (lane < nk) oe[s + lane] = ((uint32_t)blk << 16) | hold[lane];
-                if (lane == nk) oe[s + lane] = ((uint32_t)blk << 16) | kMarkerSlot;
-                wsync();
-                oe_move_tail(s + cnt + 1, s + nk + 1);
+                if (lane < nk) b_child[blk * 8 + lane] = (uint16_t)hold[lane];
                 b_count[blk] = (uint8_t)nk;
+                splits++;
                 wsync();
-                if (nk < kMaxNodes / 2 && blk != root) pack_leaf(blk, s);
+                if (nk < kMaxNodes / 2 && blk != root) pack_leaf(blk);
                 if (status) return;
             }
         }
@@ -1188,24 +1273,20 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ ops
-    // insertSegments + blockInsert for one remote segment (mergeTree.ts:1968-1998, 2141-2224)
+    // insertSegments + blockInsert for one remote segment (mergeTree.ts:1968-1998, 2141-2224):
+    // ensureIntervalBoundary(pos) then the inserting walk, which after the split resolves to
+    // the split's right half (unless the split restructured the tree: then it walks again)
     MT_FI void op_insert(const mt_op &op) {
-        uint32_t c = op.client;
-        uint32_t pos = (uint32_t)op.pos1;
-        // ensureIntervalBoundary (mergeTree.ts:2241-2245) and the insertingWalk share one scan:
-        // the walk's target is the segment the boundary split cuts, whose left half keeps every
-        // entry before it, so the walk resumes at that half with the same view position.
-        Loc L = locate(pos, op.ref_seq, c);
-        if (L.found && !L.marker && L.excl < pos) {
-            int32_t li = split_at(L.idx, pos - L.excl);
-            if (status) return;
-            L = locate(pos, op.ref_seq, c, li, L.excl);
-        }
-        bool marker = (op.flags & MT_OPF_MARKER) != 0;
-        uint32_t len = marker ? 1u : op.payload_len;
+        const uint32_t c = op.client;
+        const uint32_t pos = (uint32_t)op.pos1;
+        ov_splits = -1;
+        Walk W = boundary(pos, op.ref_seq, c);
+        if (status) return;
+        const bool marker = (op.flags & MT_OPF_MARKER) != 0;
+        const uint32_t len = marker ? 1u : op.payload_len;
         if (len > 0) {
             PF_SCOPE(3);
-            if (!L.found) {
+            if (W.blk < 0 || !W.ok) {
                 set_fail(ST_INVALID_POS);
                 return;
             }
@@ -1219,7 +1300,7 @@ struct Engine {
                 if (status) return;
             }
             uint32_t gen = s_meta[slot] & 0xFFFF0000u;
-            uint32_t meta = gen | kMetaLinked | (c & 63u) | (kNoClient << 6);
+            uint32_t meta = gen | kMetaLinked | kMetaUnsettled | (c & 63u) | (kNoClient << 6);
             if (marker) meta |= kMetaMarker;
             if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
             s_len[slot] = len;
@@ -1228,11 +1309,12 @@ struct Engine {
             s_ovl[slot] = 0;
             s_props[slot] = props;
             s_phash[slot] = ph;
-            s_toff[slot] = marker ? op.payload : op.payload;
+            s_toff[slot] = op.payload;
             s_tcap[slot] = marker ? 0u : len;
             s_meta[slot] = meta;
             wsync();
-            int32_t blk = insert_leaf(L.idx, (uint32_t)slot);
+            u_push((uint32_t)slot);
+            int32_t blk = insert_leaf(W.blk, W.k, (uint32_t)slot);
             if (status) return;
             // saveIfLocal (mergeTree.ts:2164-2179)
             if (op.seq > min_seq) add_to_lru(blk, (uint32_t)slot, op.seq);
@@ -1241,65 +1323,65 @@ struct Engine {
         zamboni();
     }
 
-    // markRangeRemoved / annotateRange range walk (nodeMap, mergeTree.ts:2903-2965)
+    // markRangeRemoved / annotateRange (mergeTree.ts:2565-2719): both boundaries, then the
+    // nodeMap range walk leaf block by leaf block
     MT_FI void op_range(const mt_op &op) {
-        uint32_t c = op.client;
-        int32_t ref = op.ref_seq;
-        uint32_t start = (uint32_t)op.pos1, end = (uint32_t)op.pos2;
-        // ensureIntervalBoundary(start), ensureIntervalBoundary(end) (mergeTree.ts:2241-2245,
-        // 2903-2904): every entry before the start walk's target ends at or before `start`, so
-        // the end search and the range walk resume there with its view position.
-        Loc A = locate(start, ref, c);
-        if (!A.found) {
-            resolve_splits();
-            zamboni();
-            return;
-        }
-        int32_t from = A.idx;
-        uint32_t carry = A.excl;
-        if (!A.marker && A.excl < start) {
-            from = split_at(A.idx, start - A.excl);
-            if (status) return;
-        }
-        if (end > start) {
-            Loc B = containing(end, ref, c, from, carry);
-            if (B.found) {
-                split_at(B.idx, end - B.excl);
-                if (status) return;
-                from = shifted(from);
+        const uint32_t c = op.client;
+        const int32_t ref = op.ref_seq;
+        const uint32_t start = (uint32_t)op.pos1, end = (uint32_t)op.pos2;
+        ov_splits = -1;
+        boundary(start, ref, c);
+        if (status) return;
+        boundary(end, ref, c);
+        if (status) return;
+        // nodeMap visits leaves with vlen > 0 and E < end and P > start: none when end <= start
+        // (both boundaries were cut, so no leaf can straddle them)
+        if (end > start) range_walk(op, start, end);
+        resolve_splits();
+        zamboni();
+    }
+
+    MT_FI int32_t next_leaf_block(int32_t b) {
+        for (;;) {
+            int32_t p = b_parent[b];
+            if (p == (int32_t)kNoBlock) return -1;
+            int32_t i = child_index(p, b);
+            if (i + 1 < (int32_t)b_count[p]) {
+                b = b_child[p * 8 + i + 1];
+                while (!b_leaf[b]) b = b_child[b * 8];
+                return b;
             }
-        } else if (end < start) {
-            // inverted range: nothing is marked, but the end boundary is still cut
-            Loc B = containing(end, ref, c, 0, 0);
-            if (B.found) {
-                split_at(B.idx, end - B.excl);
-                if (status) return;
-            }
-            from = 0;
-            carry = 0;
+            b = p;
         }
+    }
+
+    MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end) {
+        const uint32_t c = op.client;
+        const int32_t ref = op.ref_seq;
+        ensure_overlay(ref, c);
+        Walk W = descend(start, ref, c, true);
+        PF_SCOPE(4);
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = (op.flags & MT_OPF_REWRITE) != 0;
         // per-op memo old prop-set -> new prop-set (annotate)
         uint32_t memo_n = 0;
         uint32_t memo_old = 0, memo_new = 0, memo_h = 0;  // lane i holds entry i
-        {
-        PF_SCOPE(4);
-        for (int32_t base = from; base < n_oe; base += kWave) {
-            int32_t j = base + lane;
-            bool valid = j < n_oe;
-            uint32_t e = valid ? oe[j] : 0u;
-            uint32_t vlen = 0;
-            bool tie, mk;
-            if (valid) view_of(e, ref, c, vlen, tie, mk);
-            uint32_t incl = scan_incl(vlen) + carry;
-            uint32_t excl = incl - vlen;
-            bool hit = valid && vlen > 0 && excl < end && incl > start;
+        int32_t blk = W.blk;
+        uint32_t base = W.base;
+        while (blk >= 0) {
+            const int32_t n = b_count[blk];
+            uint32_t slot = 0, vlen = 0;
+            bool tie;
+            if (lane < n) {
+                slot = b_child[blk * 8 + lane];
+                view_of(slot, ref, c, vlen, tie);
+            }
+            const uint32_t incl = scan8(vlen) + base;
+            const uint32_t excl = incl - vlen;
+            const bool hit = lane < n && lane < kMaxNodes && vlen > 0u && excl < end && incl > start;
             uint64_t hb = ballot(hit);
-            bool past = valid && excl >= end;
-            uint64_t pb = ballot(past);
+            const uint32_t bend = n > 0 ? rdl(incl, n - 1) : base;
             if (is_remove && hit) {
-                uint32_t slot = e & 0xFFFFu;
                 if (s_rseq[slot] != kNoneSeq) {
                     s_ovl[slot] |= 1u << c;  // addOverlappingClient (mergeTree.ts:2544-2552)
                 } else {
@@ -1307,20 +1389,40 @@ struct Engine {
                     s_meta[slot] = (s_meta[slot] & ~(63u << 6)) | ((c & 63u) << 6);
                 }
             }
+            if (is_remove) {
+                // a settled leaf removed now leaves the settled sums and joins the overlay
+                // (a visible leaf already removed is concurrent, hence already unsettled)
+                uint32_t meta = hit ? s_meta[slot] : 0u;
+                const bool newu = hit && !(meta & kMetaUnsettled);
+                const uint64_t um = ballot(newu);
+                if (um) {
+                    const uint32_t lost = rdl(sum8(newu ? s_len[slot] : 0u), 0);
+                    wsync();
+                    if (newu) {
+                        s_meta[slot] = meta | kMetaUnsettled;
+                        u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = slot | (meta & 0xFFFF0000u);
+                    }
+                    nu += __popcll(um);
+                    if (nu > cap.ulist) {
+                        cap_fail(1);
+                        return;
+                    }
+                    if (nu > max_u) max_u = nu;
+                    chain_add_uniform(blk, 0u - lost);
+                }
+            }
             wsync();
             // in document order: properties (annotate) and addToLRUSet
             while (hb) {
-                int f = first_lane(hb);
+                const int f = first_lane(hb);
                 hb &= hb - 1;
-                uint32_t e2 = rdl(e, f);
-                uint32_t slot = e2 & 0xFFFFu;
-                int32_t blk = (int32_t)(e2 >> 16);
+                const uint32_t sl = rdl(slot, f);
                 if (!is_remove) {
                     int32_t g0 = pool_gcs;
                     pool_reserve(2u + 2u * (64u + op.payload_len));
                     if (status) return;
                     if (pool_gcs != g0) memo_n = 0;  // ids moved
-                    uint32_t old = s_props[slot];
+                    uint32_t old = s_props[sl];
                     uint64_t mb = ballot((uint32_t)lane < memo_n && memo_old == old);
                     uint32_t nid, nh;
                     if (mb) {
@@ -1339,19 +1441,17 @@ struct Engine {
                             memo_n++;
                         }
                     }
-                    s_props[slot] = nid;
-                    s_phash[slot] = nh;
+                    s_props[sl] = nid;
+                    s_phash[sl] = nh;
                 }
-                add_to_lru(blk, slot, op.seq);
+                add_to_lru(blk, sl, op.seq);
                 if (status) return;
             }
             wsync();
-            if (pb) break;
-            carry = rdl(incl, 63);
+            if (bend >= end) break;
+            blk = next_leaf_block(blk);
+            base = bend;
         }
-        }
-        resolve_splits();
-        zamboni();
     }
 
     MT_FI void apply(const mt_op &op) {
@@ -1383,46 +1483,88 @@ struct Engine {
         if (!(op.flags & MT_OPF_GROUP_CONT)) update_seq_numbers(op.msn, op.seq);
     }
 
+    // MergeTree.getLength(refSeq, clientId) (generator)
+    MT_FI uint32_t view_length(int32_t ref, uint32_t c) {
+        uint32_t sum = 0;
+        if (ref >= min_seq) {
+            sum = b_slen[root];
+            for (int32_t base = 0; base < nu; base += kWave) {
+                const int32_t j = base + lane;
+                uint32_t vlen = 0;
+                if (j < nu) {
+                    const uint32_t e = u_list[j];
+                    const uint32_t slot = e & 0xFFFFu;
+                    const uint32_t meta = s_meta[slot];
+                    if ((meta & kMetaUnsettled) && (meta & kMetaLinked) && ((meta ^ e) & 0xFFFF0000u) == 0u) {
+                        bool tie;
+                        view_of(slot, ref, c, vlen, tie);
+                    }
+                }
+                sum += rdl(scan_incl(vlen), 63);
+            }
+        } else {
+            for (int32_t base = 0; base < slot_top; base += kWave) {
+                const int32_t slot = base + lane;
+                uint32_t vlen = 0;
+                if (slot < slot_top && (s_meta[slot] & kMetaLinked)) {
+                    bool tie;
+                    view_of((uint32_t)slot, ref, c, vlen, tie);
+                }
+                sum += rdl(scan_incl(vlen), 63);
+            }
+        }
+        return sum;
+    }
+
     // ------------------------------------------------------------------ output
+    // the leaves in document order, each leaf block closed by an end-marker record
     MT_FI void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op) {
         wsync();
-        int32_t n = n_oe <= out_cap ? n_oe : out_cap;
-        for (int32_t j = lane; j < n; j += kWave) {
-            uint32_t e = oe[j];
-            uint32_t slot = e & 0xFFFFu;
-            OutRec r;
-            if (slot == kMarkerSlot) {
-                r.len = 0;
-                r.seq = 0;
-                r.rseq = kNoneSeq;
-                r.meta = 0;
-                r.ovl = 0;
-                r.props = 0;
-                r.toff = 0;
-            } else {
-                r.len = s_len[slot];
-                r.seq = s_seq[slot];
-                r.rseq = s_rseq[slot];
-                r.meta = s_meta[slot];
-                r.ovl = s_ovl[slot];
-                r.props = s_props[slot];
-                r.toff = s_toff[slot];
+        int32_t w = 0;
+        int32_t blk = root;
+        while (!b_leaf[blk]) blk = b_child[blk * 8];
+        while (blk >= 0) {
+            const int32_t n = b_count[blk];
+            const int32_t j = w + lane;
+            if (lane <= n && j < out_cap) {
+                OutRec r;
+                if (lane < n) {
+                    const uint32_t slot = b_child[blk * 8 + lane];
+                    r.len = s_len[slot];
+                    r.seq = s_seq[slot];
+                    r.rseq = s_rseq[slot];
+                    r.meta = s_meta[slot] & ~kMetaUnsettled;
+                    r.ovl = s_ovl[slot];
+                    r.props = s_props[slot];
+                    r.toff = s_toff[slot];
+                    r.blk = ((uint32_t)blk << 16) | slot;
+                } else {
+                    r.len = 0;
+                    r.seq = 0;
+                    r.rseq = kNoneSeq;
+                    r.meta = 0;
+                    r.ovl = 0;
+                    r.props = 0;
+                    r.toff = 0;
+                    r.blk = ((uint32_t)blk << 16) | kMarkerSlot;
+                }
+                out[j] = r;
             }
-            r.blk = e;
-            out[j] = r;
+            w += n + 1;
+            blk = next_leaf_block(blk);
         }
         if (lane == 0) {
             DocOut o;
-            o.status = (n_oe > out_cap && status == ST_OK) ? ST_CAPACITY : status;
-            o.cap_kind = (n_oe > out_cap && status == ST_OK) ? 4 : cap_kind;
+            o.status = (w > out_cap && status == ST_OK) ? ST_CAPACITY : status;
+            o.cap_kind = (w > out_cap && status == ST_OK) ? 4 : cap_kind;
             o.min_seq = min_seq;
             o.cur_seq = cur_seq;
             o.depth = depth;
-            o.n_out = n;
+            o.n_out = w <= out_cap ? w : out_cap;
             o.text_top = arena_top;
             o.pool_top = pool_top;
             o.ops_done = ops_done;
-            o.max_oe = max_oe;
+            o.max_oe = max_u;
             o.max_slots = slot_top;
             o.max_blocks = blk_top;
             o.max_heap = max_heap;
@@ -1536,6 +1678,9 @@ MT_FI void generate_body(const ReplayParams &P) {
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;  // re-generation of overflowed docs
     const mt_gen_params g = *(const mt_gen_params *)P.gen;
     Engine<SEG> E;
+#ifdef MT_PROF
+    for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
+#endif
     engine_setup(E, P, d, smem);
     mt_op *ops_out = (mt_op *)P.gen_ops + d * (int64_t)g.n_ops;
     mt_prop *props_out = (mt_prop *)P.gen_props;
