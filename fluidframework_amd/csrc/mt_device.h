@@ -25,7 +25,6 @@ constexpr int kMaxNodes = 8;            // MaxNodesInBlock, mergeTree.ts:334
 constexpr uint32_t kGranularity = 256;  // TextSegmentGranularity, mergeTree.ts:1059
 constexpr int kZamboniMax = 2;          // zamboniSegmentsMaxCount, mergeTree.ts:1061
 constexpr int kMaxClients = 32;         // overlap mask width
-constexpr int kHeapRegs = 4;            // LRU heap in VGPRs: 64 * kHeapRegs - 1 entries
 constexpr int32_t kNoneSeq = 0x7FFFFFFF;  // removedSeq === undefined
 constexpr uint32_t kMarkerSlot = 0xFFFFu; // oe entry that ends a leaf block
 constexpr uint32_t kNoClient = 63u;
@@ -93,14 +92,13 @@ struct Caps {
 constexpr int kClassSegs[] = {64, 128, 256, 512, 1024, 2048};
 constexpr int kNumClasses = 6;
 constexpr Caps class_caps(int seg) {
-    return Caps{seg, seg + seg / 2 + 16, seg / 2 + 16,
-                (seg / 2 + 64) < (64 * kHeapRegs - 1) ? (seg / 2 + 64) : (64 * kHeapRegs - 1), seg + 64};
+    return Caps{seg, seg + seg / 2 + 16, seg / 2 + 16, seg / 2 + 64, seg + 64};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
     uint32_t len, seq, rseq, meta, ovl, props, toff, tcap, phash, sfree, sblk, ulist;
-    uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, bslen, bacc, scratch, bytes;
+    uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, bytes;
 };
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
 constexpr Layout make_layout(int seg) {
@@ -127,6 +125,7 @@ constexpr Layout make_layout(int seg) {
     L.bscour = o;  o = lds_align(o + 1u * c.blk);
     L.bslen = o;   o = lds_align(o + 4u * c.blk);
     L.bacc = o;    o = lds_align(o + 4u * c.blk);
+    L.heap = o;    o = lds_align(o + 8u * (c.heap + 2));
     L.scratch = o; o = lds_align(o + 4u * 256);
     L.bytes = o;
     return L;

@@ -145,9 +145,8 @@ struct Engine {
     // latency overlaps it (at most two splits per op)
     int32_t pend_n;
     uint32_t pend_slot0, pend_slot1, pend_ch0, pend_ch1;
-    int32_t max_heap, max_u;
-    uint32_t hk[kHeapRegs];
-    int32_t hs[kHeapRegs];
+    int32_t max_heap, max_u, htop;
+    uint2 *h_ent;
     // ---- global
     uint16_t *text;
     uint32_t text_cap;
@@ -184,6 +183,7 @@ struct Engine {
         b_scour = (int8_t *)(base + lay.bscour);
         b_slen = (uint32_t *)(base + lay.bslen);
         b_acc = (uint32_t *)(base + lay.bacc);
+        h_ent = (uint2 *)(base + lay.heap);
         scratch = (uint32_t *)(base + lay.scratch);
     }
 
@@ -220,10 +220,7 @@ struct Engine {
         root = alloc_block(1);
         depth = 1;
         // heap entry 0 is the sentinel LRUSegmentComparer.min = { maxSeq: -2 } (never compared)
-        for (int i = 0; i < kHeapRegs; i++) {
-            hk[i] = 0;
-            hs[i] = -2;
-        }
+        htop = kNoneSeq;
         wsync();
     }
 
@@ -429,9 +426,10 @@ struct Engine {
         const bool lanes8 = lane < kMaxNodes;
         for (int32_t l = 0; l + 1 < depth; l++) {
             const int32_t n = b_count[N];
+            const uint32_t row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;  // issued with the count
             uint32_t ch = 0, v = 0;
             if (lane < n) {
-                ch = b_child[N * 8 + lane];
+                ch = row;
                 v = b_acc[ch] + (ov_full ? 0u : b_slen[ch]);
             }
             const uint32_t incl = scan8(v) + base;
@@ -446,9 +444,10 @@ struct Engine {
         W.n = n;
         W.base = base;
         if (strict) return W;
+        const uint32_t row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;
         uint32_t vlen = 0;
         bool tie = false;
-        if (lane < n) view_of(b_child[N * 8 + lane], ref, c, vlen, tie);
+        if (lane < n) view_of(row, ref, c, vlen, tie);
         const uint32_t incl = scan8(vlen) + base;
         const uint32_t excl = incl - vlen;
         const uint64_t cb = ballot(lanes8 && lane < n && (incl > pos || (excl == pos && vlen == 0u && tie)));
@@ -769,72 +768,62 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ heap (collections.ts:213-265)
-    // The LRU heap lives in VGPRs: entry k is lane k & 63 of register k >> 6, so sifting is
-    // readlane / writelane arithmetic with no memory round trips.  Same array layout and sift
-    // order as Heap.add / Heap.get, hence the same pop order on seq ties.
-    MT_FI int32_t hseq(int32_t k) const {
-        int32_t v = 0;
-#pragma unroll
-        for (int i = 0; i < kHeapRegs; i++)
-            if ((k >> 6) == i) v = rdl(hs[i], k & 63);
-        return v;
-    }
-    MT_FI uint32_t hkey(int32_t k) const {
-        uint32_t v = 0;
-#pragma unroll
-        for (int i = 0; i < kHeapRegs; i++)
-            if ((k >> 6) == i) v = rdl(hk[i], k & 63);
-        return v;
-    }
-    MT_FI void hset(int32_t k, uint32_t key, int32_t seq) {
-#pragma unroll
-        for (int i = 0; i < kHeapRegs; i++)
-            if ((k >> 6) == i && lane == (k & 63)) {
-                hk[i] = key;
-                hs[i] = seq;
-            }
-    }
+    // The LRU heap lives in LDS as 8-byte {key, seq} entries, 1-based; a sift-down level reads
+    // both children with one 16-byte load.  Same array layout and sift order as Heap.add /
+    // Heap.get, hence the same pop order on seq ties.  `htop` caches heap[1].seq.
     MT_FI void heap_add(uint32_t key, int32_t seq) {
         PF_SCOPE(9);
-        if (hn + 1 > cap.heap || hn + 1 >= 64 * kHeapRegs) {
-            cap_fail(hn + 1 >= 64 * kHeapRegs ? 5 : 1);
+        if (hn + 1 > cap.heap) {
+            cap_fail(1);
             return;
         }
         hn++;
         int32_t k = hn;
         // sift up: parents larger than the new entry move down into the hole
         while (k > 1) {
-            int32_t ps = hseq(k >> 1);
+            const uint2 pe = h_ent[k >> 1];
+            const int32_t ps = (int32_t)rfl(pe.y);
             if (!(ps - seq > 0)) break;
-            hset(k, hkey(k >> 1), ps);
+            h_ent[k] = pe;
             k >>= 1;
         }
-        hset(k, key, seq);
+        h_ent[k] = make_uint2(key, (uint32_t)seq);
+        if (k == 1) htop = seq;
         if (hn > max_heap) max_heap = hn;
+        wsync();
     }
     MT_FI void heap_get(uint32_t &key, int32_t &seq) {
         PF_SCOPE(9);
-        key = hkey(1);
-        seq = hseq(1);
-        uint32_t lk = hkey(hn);
-        int32_t ls = hseq(hn);
+        const uint2 top = h_ent[1];
+        const uint2 last = h_ent[hn];
+        key = rfl(top.x);
+        seq = (int32_t)rfl(top.y);
+        const int32_t ls = (int32_t)rfl(last.y);
         hn--;
         int32_t k = 1;
+        int32_t newtop = ls;
         while ((k << 1) <= hn) {
-            int32_t j = k << 1;
-            int32_t sj = hseq(j);
-            if (j < hn) {
-                int32_t sj1 = hseq(j + 1);
+            const int32_t j0 = k << 1;
+            const uint4 pr = *(const uint4 *)&h_ent[j0];
+            int32_t j = j0;
+            uint32_t jk = pr.x;
+            int32_t sj = (int32_t)rfl(pr.y);
+            if (j0 < hn) {
+                const int32_t sj1 = (int32_t)rfl(pr.w);
                 if (sj - sj1 > 0) {
-                    j++;
+                    j = j0 + 1;
                     sj = sj1;
+                    jk = pr.z;
                 }
             }
             if (ls - sj <= 0) break;
-            hset(k, hkey(j), sj);
+            h_ent[k] = make_uint2(jk, (uint32_t)sj);
+            if (k == 1) newtop = sj;
             k = j;
         }
-        if (hn >= 1) hset(k, lk, ls);
+        if (hn >= 1) h_ent[k] = last;
+        htop = hn >= 1 ? newtop : kNoneSeq;
+        wsync();
     }
 
     // ------------------------------------------------------------------ properties
@@ -994,42 +983,45 @@ struct Engine {
         const bool rem = in && rseq != kNoneSeq;
         const bool cand = in && !rem && seq <= min_seq;
         const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
-        const bool peq = lane > 0 && pprev == props;
-        const bool pmaybe = lane > 0 && !peq && props != 0u && pprev != 0u && hprev == ph;
-        const uint64_t candM = ballot(cand), peqM = ballot(peq), maybeM = ballot(pmaybe);
+        const uint32_t mprev = __shfl_up(meta, 1, kWave);
+        const uint64_t candM = ballot(cand);
         const uint64_t freeR = ballot(rem && rseq <= min_seq);
         const uint64_t liveM = ballot(in);
-        uint64_t mergeM = 0;
-        uint32_t head = 0;  // lane f (merged): lane of its chain head
-        {
-            int32_t prev = -1;
+        // lane k may append to the chain ending at lane k - 1 (TextSegment.canAppend without its
+        // length rule, plus matchProperties): both candidates, same block, neither a Marker, the
+        // tail not ending in '\n'
+        const bool pair = lane > 0 && cand && ((candM >> (lane - 1)) & 1ull) && !((startM >> lane) & 1ull) &&
+                          !(meta & kMetaMarker) && !(mprev & kMetaMarker) && !(mprev & kMetaEndsNL);
+        const bool peq = pprev == props;
+        const bool pmaybe = !peq && props != 0u && pprev != 0u && hprev == ph;
+        uint64_t pairM = ballot(pair && peq);
+        uint64_t maybeM = ballot(pair && pmaybe);
+        while (maybeM) {  // equal hashes, different sets: compare contents (rare)
+            const int k = first_lane(maybeM);
+            maybeM &= maybeM - 1;
+            if (props_match(rdl(props, k - 1), rdl(ph, k - 1), rdl(props, k), rdl(ph, k))) pairM |= 1ull << k;
+        }
+        uint64_t mergeM;
+        const uint64_t longM = ballot(in && len > kGranularity);
+        if (!(pairM & longM)) {
+            // every appended leaf is <= 256 long, so the length rule never fails: all pairs merge
+            mergeM = pairM;
+        } else {
+            // a long leaf appends only while its chain is still <= 256 long: walk the chains
+            mergeM = 0;
             uint32_t acc = 0;
-            bool pnl = false, pmk = false;
             for (int32_t k = 0; k < n; k++) {
-                if ((startM >> k) & 1ull) prev = -1;
-                if (!((candM >> k) & 1ull)) {
-                    prev = -1;
-                    continue;
-                }
-                const uint32_t lk = rdl(len, k), mk_ = rdl(meta, k);
-                bool can = false;
-                if (prev >= 0 && !pmk && !(mk_ & kMetaMarker) && !pnl && (acc <= kGranularity || lk <= kGranularity)) {
-                    if ((peqM >> k) & 1ull) can = true;
-                    else if ((maybeM >> k) & 1ull)
-                        can = props_match(rdl(props, k - 1), rdl(ph, k - 1), rdl(props, k), rdl(ph, k));
-                }
-                if (can) {
+                const uint32_t lk = rdl(len, k);
+                if (((pairM >> k) & 1ull) && (acc <= kGranularity || lk <= kGranularity)) {
                     mergeM |= 1ull << k;
-                    if (lane == k) head = (uint32_t)prev;
                     acc += lk;
                 } else {
-                    prev = k;
                     acc = lk;
-                    pmk = (mk_ & kMetaMarker) != 0;
                 }
-                pnl = (mk_ & kMetaEndsNL) != 0;
             }
         }
+        // chain head of every appended lane: the last non-appended lane before it
+        const uint32_t head = 63u - (uint32_t)__builtin_clzll((~mergeM & ((1ull << lane) - 1ull)) | 1ull);
         // TextSegment.append for every merge, head by head in document order
         if (mergeM) {
             PF_SCOPE(8);
@@ -1112,51 +1104,110 @@ struct Engine {
         return __popcll(holdM);
     }
 
+    // Lane-parallel block allocation: lane q < cnt receives a block id (free-list pops first,
+    // in the order alloc_block would return them) initialised as MergeTree.makeBlock does.
+    MT_FI uint32_t alloc_blocks(int32_t cnt, int leaf, int32_t parent) {
+        const int32_t pop = cnt < n_bfree ? cnt : n_bfree;
+        if (blk_top + (cnt - pop) > cap.blk) {
+            cap_fail(1);
+            return 0;
+        }
+        uint32_t id = 0;
+        if (lane < pop) id = b_free[n_bfree - 1 - lane];
+        else if (lane < cnt) id = (uint32_t)(blk_top + lane - pop);
+        n_bfree -= pop;
+        blk_top += cnt - pop;
+        wsync();
+        if (lane < cnt) {
+            b_leaf[id] = (uint8_t)leaf;
+            b_scour[id] = kScourUndef;
+            b_parent[id] = (uint16_t)parent;
+            b_slen[id] = 0u;
+        }
+        return id;
+    }
+
+    // Regroup `nk` children (hold[0..nk)) of `parent`'s former child blocks into
+    // floor(nk / 4) (1..7) new blocks of near-equal size, first blocks one larger
+    // (pack, mergeTree.ts:1389-1411).  Leaf mode also moves the leaves' s_blk.
+    MT_FI int32_t regroup(int32_t parent, int32_t pn, const uint32_t *hold, int32_t nk, int leaf) {
+        int32_t cc = nk / (kMaxNodes / 2);
+        if (cc > kMaxNodes - 1) cc = kMaxNodes - 1;
+        if (cc < 1) cc = 1;
+        const int32_t base = nk / cc, extra = nk % cc;
+        wsync();
+        // the old child blocks go to the free list, then cc new ones come off it
+        if (lane < pn) b_free[n_bfree + lane] = b_child[parent * 8 + lane];
+        n_bfree += pn;
+        wsync();
+        const uint32_t id = alloc_blocks(cc, leaf, parent);
+        if (status) return cc;
+        if (lane < cc) {
+            b_count[id] = (uint8_t)(base + (lane < extra ? 1 : 0));
+            b_child[parent * 8 + lane] = (uint16_t)id;
+        }
+        // leaf i goes to block q at position p
+        uint32_t c = 0, sl = 0;
+        const bool in = lane < nk;
+        if (in) c = hold[lane];
+        const int32_t big = extra * (base + 1);
+        const int32_t q = lane < big ? lane / (base + 1) : extra + (lane - big) / (base > 0 ? base : 1);
+        const int32_t p = lane < big ? lane % (base + 1) : (lane - big) % (base > 0 ? base : 1);
+        const uint32_t nb = (uint32_t)__shfl((int)id, in ? q : 0, kWave);
+        wsync();
+        if (in) {
+            b_child[nb * 8 + p] = (uint16_t)c;
+            if (leaf) {
+                s_blk[c] = (uint16_t)nb;
+                sl = settled_len(c);
+            } else {
+                b_parent[c] = (uint16_t)nb;
+                sl = b_slen[c];
+            }
+        }
+        wsync();
+        if (in && sl) lds_add(&b_slen[nb], sl);
+        b_count[parent] = (uint8_t)cc;
+        splits++;  // structure changed under the overlay
+        wsync();
+        return cc;
+    }
+
+    // the children of parent's child blocks, in order, gathered one per lane (8 lanes per
+    // child block) and compacted into dst[0..total); returns total, block starts in *startM
+    MT_FI int32_t gather_grandchildren(int32_t parent, int32_t pn, uint32_t *dst, uint64_t *startM) {
+        const int32_t ci = lane >> 3, j = lane & 7;
+        uint32_t cb = 0, cn = 0, g = 0;
+        if (ci < pn) {
+            cb = b_child[parent * 8 + ci];
+            cn = b_count[cb];
+            g = b_child[cb * 8 + j];
+        }
+        const bool valid = ci < pn && (uint32_t)j < cn;
+        const uint64_t vm = ballot(valid);
+        const int32_t total = __popcll(vm);
+        wsync();
+        if (valid) dst[__popcll(vm & ((1ull << lane) - 1ull))] = g | (j == 0 ? 0x80000000u : 0u);
+        wsync();
+        const uint32_t e = lane < total ? dst[lane] : 0u;
+        *startM = ballot(lane < total && (e >> 31));
+        wsync();
+        if (lane < total) dst[lane] = e & 0xFFFFu;
+        wsync();
+        return total;
+    }
+
     // pack for an interior block `blk` (its parent's children are interior blocks);
     // repeats upward while the parent underflows (mergeTree.ts:1414-1419)
     MT_FI void pack_interior(int32_t blk) {
         for (;;) {
-            int32_t parent = b_parent[blk];
-            int32_t pn = b_count[parent];
-            uint32_t *hold = scratch;  // grandchildren block ids
-            int32_t total = 0;
-            for (int32_t ci = 0; ci < pn; ci++) {
-                int32_t cb = b_child[parent * 8 + ci];
-                int32_t cn = b_count[cb];
-                wsync();
-                if (lane < cn) hold[total + lane] = b_child[cb * 8 + lane];
-                total += cn;
-                wsync();
-            }
-            int32_t child_count = total / (kMaxNodes / 2);
-            if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
-            if (child_count < 1) child_count = 1;
-            int32_t base = total / child_count, extra = total % child_count;
-            for (int32_t i = 0; i < pn; i++) free_block(b_child[parent * 8 + i]);
-            int32_t read = 0;
-            for (int32_t i = 0; i < child_count; i++) {
-                int32_t nbi = alloc_block(0);
-                if (status) return;
-                int32_t cnt = base + (i < extra ? 1 : 0);
-                wsync();
-                uint32_t sl = 0;
-                if (lane < cnt) {
-                    uint16_t g = (uint16_t)hold[read + lane];
-                    b_child[nbi * 8 + lane] = g;
-                    b_parent[g] = (uint16_t)nbi;
-                    sl = b_slen[g];
-                }
-                const uint32_t tot = rdl(sum8(lane < 8 ? sl : 0u), 0);
-                wsync();
-                b_count[nbi] = (uint8_t)cnt;
-                b_parent[nbi] = (uint16_t)parent;
-                b_slen[nbi] = tot;
-                b_child[parent * 8 + i] = (uint16_t)nbi;
-                read += cnt;
-            }
-            b_count[parent] = (uint8_t)child_count;
-            wsync();
-            if (child_count < kMaxNodes / 2 && parent != root) blk = parent;
+            const int32_t parent = b_parent[blk];
+            const int32_t pn = b_count[parent];
+            uint64_t sm;
+            const int32_t total = gather_grandchildren(parent, pn, scratch, &sm);
+            const int32_t cc = regroup(parent, pn, scratch, total, 0);
+            if (status) return;
+            if (cc < kMaxNodes / 2 && parent != root) blk = parent;
             else return;
         }
     }
@@ -1169,61 +1220,21 @@ struct Engine {
         const int32_t pn = b_count[parent];
         uint32_t *gat = scratch;
         uint32_t *hold = scratch + 128;
-        int32_t total = 0;
-        uint64_t startM = 0;
-        for (int32_t ci = 0; ci < pn; ci++) {
-            int32_t cb = b_child[parent * 8 + ci];
-            int32_t cn = b_count[cb];
-            wsync();
-            if (lane < cn) gat[total + lane] = b_child[cb * 8 + lane];
-            if (cn > 0) startM |= 1ull << total;
-            total += cn;
-            wsync();
-        }
-        if (total > kWave) {
-            set_fail(ST_INTERNAL);
-            return;
-        }
+        uint64_t startM;
+        const int32_t total = gather_grandchildren(parent, pn, gat, &startM);
         const uint32_t slot = lane < total ? gat[lane] : 0u;
         const int32_t nk = scour(slot, total, startM, hold);
         if (status) return;
-        int32_t child_count = nk / (kMaxNodes / 2);
-        if (child_count > kMaxNodes - 1) child_count = kMaxNodes - 1;
-        if (child_count < 1) child_count = 1;
-        const int32_t base = nk / child_count, extra = nk % child_count;
-        for (int32_t i = 0; i < pn; i++) free_block(b_child[parent * 8 + i]);
-        int32_t read = 0;
-        for (int32_t i = 0; i < child_count; i++) {
-            int32_t nbi = alloc_block(1);
-            if (status) return;
-            int32_t cnt = base + (i < extra ? 1 : 0);
-            wsync();
-            uint32_t sl = 0;
-            if (lane < cnt) {
-                uint32_t c = hold[read + lane];
-                b_child[nbi * 8 + lane] = (uint16_t)c;
-                s_blk[c] = (uint16_t)nbi;
-                sl = settled_len(c);
-            }
-            const uint32_t tot = rdl(sum8(lane < 8 ? sl : 0u), 0);
-            wsync();
-            b_count[nbi] = (uint8_t)cnt;
-            b_parent[nbi] = (uint16_t)parent;
-            b_slen[nbi] = tot;
-            b_child[parent * 8 + i] = (uint16_t)nbi;
-            read += cnt;
-        }
-        b_count[parent] = (uint8_t)child_count;
-        splits++;  // structure changed under the overlay
-        wsync();
-        if (child_count < kMaxNodes / 2 && parent != root) pack_interior(parent);
+        const int32_t cc = regroup(parent, pn, hold, nk, 1);
+        if (status) return;
+        if (cc < kMaxNodes / 2 && parent != root) pack_interior(parent);
     }
 
     // zamboniSegments (mergeTree.ts:1422-1478)
     MT_FI void zamboni() {
         PF_SCOPE(5);
         for (int it = 0; it < kZamboniMax; it++) {
-            if (hn < 1 || hseq(1) > min_seq) break;
+            if (hn < 1 || htop > min_seq) break;
             if (settled_min != min_seq) settle_all();
             uint32_t key;
             int32_t mseq;
