@@ -35,12 +35,17 @@ constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
 // segment meta word
 //   [0,6)  clientId (short id)         [6,12) removedClientId (63 = none)
 //   [12]   Marker                       [13]   text ends with '\n'
-//   [14]   linked (in the tree)         [15]   unsettled (in the overlay list, see below)
-//   [16,32) slot generation (heap / overlay entry validity)
+//   [14]   linked (in the tree)         [15]   unsettled (in the overlay list, see mt_engine.hip)
+//   [16]   has a prop set               [17]   text contains a '\n' somewhere
+//   [18,32) slot generation (heap / overlay entry validity)
 constexpr uint32_t kMetaMarker = 1u << 12;
 constexpr uint32_t kMetaEndsNL = 1u << 13;
 constexpr uint32_t kMetaLinked = 1u << 14;
 constexpr uint32_t kMetaUnsettled = 1u << 15;
+constexpr uint32_t kMetaHasProps = 1u << 16;
+constexpr uint32_t kMetaHasNL = 1u << 17;
+constexpr uint32_t kGenShift = 18;
+constexpr uint32_t kGenMask = 0xFFFFFFFFu << kGenShift;
 constexpr uint16_t kNoBlock = 0xFFFFu;
 
 // one output record per leaf or end-of-leaf-block entry (doc order), 8 x u32
@@ -92,12 +97,12 @@ struct Caps {
 constexpr int kClassSegs[] = {64, 128, 256, 512, 1024, 2048};
 constexpr int kNumClasses = 6;
 constexpr Caps class_caps(int seg) {
-    return Caps{seg, seg + seg / 2 + 16, seg / 2 + 16, seg / 2 + 64, seg + 64};
+    return Caps{seg, seg + seg / 4 + 16, seg / 4 + 16, seg / 8 + 64, seg / 2 + 96};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
-    uint32_t len, seq, rseq, meta, ovl, props, toff, tcap, phash, sfree, sblk, ulist;
+    uint32_t len, seq, rseq, meta, ovl, sblk, ulist;
     uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, bytes;
 };
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
@@ -110,13 +115,8 @@ constexpr Layout make_layout(int seg) {
     L.rseq = o;    o = lds_align(o + 4u * c.seg);
     L.meta = o;    o = lds_align(o + 4u * c.seg);
     L.ovl = o;     o = lds_align(o + 4u * c.seg);
-    L.props = o;   o = lds_align(o + 4u * c.seg);
-    L.toff = o;    o = lds_align(o + 4u * c.seg);
-    L.tcap = o;    o = lds_align(o + 4u * c.seg);
-    L.phash = o;   o = lds_align(o + 4u * c.seg);
-    L.sfree = o;   o = lds_align(o + 2u * c.seg);
     L.sblk = o;    o = lds_align(o + 2u * c.seg);
-    L.ulist = o;   o = lds_align(o + 4u * c.ulist);
+    L.ulist = o;   o = lds_align(o + 2u * c.ulist);
     L.bparent = o; o = lds_align(o + 2u * c.blk);
     L.bfree = o;   o = lds_align(o + 2u * c.blk);
     L.bchild = o;  o = lds_align(o + 16u * c.blk);
@@ -126,7 +126,7 @@ constexpr Layout make_layout(int seg) {
     L.bslen = o;   o = lds_align(o + 4u * c.blk);
     L.bacc = o;    o = lds_align(o + 4u * c.blk);
     L.heap = o;    o = lds_align(o + 8u * (c.heap + 2));
-    L.scratch = o; o = lds_align(o + 4u * 256);
+    L.scratch = o; o = lds_align(o + 4u * 128);
     L.bytes = o;
     return L;
 }
@@ -157,6 +157,7 @@ struct ReplayParams {
     void *gen_ops;                // mt_op[n_docs * n_ops]
     void *gen_props;              // mt_prop[n_docs * 2 * n_ops] (doc-local offsets rebased by host)
     uint64_t *prof;               // MT_PROF builds: kProfSlots cycle counters per workgroup
+    uint4 *cold;                  // [n_docs * cap.seg] cold segment records {props, phash, toff, tcap}
 };
 constexpr int kProfSlots = 12;
 

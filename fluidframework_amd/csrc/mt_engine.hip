@@ -5,8 +5,9 @@
 // mergeTree.ts:334): leaf blocks list segment slots, interior blocks list blocks, every
 // child list is one 16-byte row that a wave reads with one lane per child.
 //
-//   s_*[slot]   segment fields (SoA): length, seq, removedSeq, client ids, overlap mask,
-//               prop-set id, text offset/capacity, leaf block.
+//   s_*[slot]   the fields nodeLength reads (SoA): length, seq, removedSeq, client ids, overlap
+//               mask, flags; and the leaf block.  The cold fields (prop-set id, prop hash, text
+//               offset/capacity) live in a per-document HBM table `cold[slot]` (16 B records).
 //   b_*[block]  children[8], count, parent, needsScour, and the block's SETTLED length.
 //   u_list      the unsettled segments (the collab window's "hot" set).
 //   heap        the zamboni heap (collections.ts:213-265), in VGPRs.
@@ -123,17 +124,17 @@ struct Engine {
     static constexpr Caps cap = class_caps(SEG);
     static constexpr Layout lay = make_layout(SEG);
     // ---- LDS state
-    uint32_t *s_len, *s_meta, *s_ovl, *s_props, *s_toff, *s_tcap, *s_phash;
-    int32_t *s_seq, *s_rseq;
-    uint16_t *s_free, *s_blk;
-    uint32_t *u_list;  // slot | generation << 16
+    uint32_t *s_len, *s_meta, *s_ovl;
+    int32_t *s_seq, *s_rseq;  // s_seq of a free slot links the free list
+    uint16_t *s_blk;
+    uint16_t *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
     uint16_t *b_parent, *b_free, *b_child;
     uint8_t *b_count, *b_leaf;
     int8_t *b_scour;
     uint32_t *b_slen, *b_acc;
-    uint32_t *scratch;  // 256 words
+    uint32_t *scratch;  // 128 words
     // ---- uniform scalars
-    int32_t slot_top, n_free, blk_top, n_bfree, root, depth, hn, nu;
+    int32_t slot_top, free_head, blk_top, n_bfree, root, depth, hn, nu;
     int32_t min_seq, cur_seq, status, settled_min;
     int32_t splits;                 // leaf/interior block splits so far (overlay staleness)
     int32_t ov_splits, ov_full;     // overlay computed at `ov_splits`; full (refSeq < minSeq) mode
@@ -141,13 +142,16 @@ struct Engine {
     uint32_t pay_end, arena_base, arena_end, semi_t;  // text: payload | semispace A | semispace B
     uint32_t pool_base, pool_end, semi_p;             // prop pool: [0] reserved | A | B
     int32_t pool_gcs, text_gcs;
-    // ends-with-'\n' of a split's left half, resolved after the op's LDS work so the text load
-    // latency overlaps it (at most two splits per op)
-    int32_t pend_n;
-    uint32_t pend_slot0, pend_slot1, pend_ch0, pend_ch1;
+    // Splits of the current op (at most two): the cold records of both halves and the left
+    // half's ends-with-'\n' are resolved after the op's LDS work, so the HBM latency of the
+    // cold-record and text loads overlaps it.
+    int32_t pend_n, pend_cold;
+    uint32_t ps0, pn0, pr0, pch0, ps1, pn1, pr1, pch1;
+    uint4 pc0, pc1;
     int32_t max_heap, max_u, htop;
     uint2 *h_ent;
     // ---- global
+    uint4 *cold;  // cold segment records {props, phash, toff, tcap}
     uint16_t *text;
     uint32_t text_cap;
     uint32_t *pool;
@@ -168,13 +172,8 @@ struct Engine {
         s_rseq = (int32_t *)(base + lay.rseq);
         s_meta = (uint32_t *)(base + lay.meta);
         s_ovl = (uint32_t *)(base + lay.ovl);
-        s_props = (uint32_t *)(base + lay.props);
-        s_toff = (uint32_t *)(base + lay.toff);
-        s_tcap = (uint32_t *)(base + lay.tcap);
-        s_phash = (uint32_t *)(base + lay.phash);
-        s_free = (uint16_t *)(base + lay.sfree);
         s_blk = (uint16_t *)(base + lay.sblk);
-        u_list = (uint32_t *)(base + lay.ulist);
+        u_list = (uint16_t *)(base + lay.ulist);
         b_parent = (uint16_t *)(base + lay.bparent);
         b_free = (uint16_t *)(base + lay.bfree);
         b_child = (uint16_t *)(base + lay.bchild);
@@ -200,7 +199,7 @@ struct Engine {
     // ------------------------------------------------------------------ init
     MT_FI void init() {
         slot_top = 0;
-        n_free = 0;
+        free_head = -1;
         blk_top = 0;
         n_bfree = 0;
         hn = 0;
@@ -211,6 +210,7 @@ struct Engine {
         status = ST_OK;
         cap_kind = 0;
         pend_n = 0;
+        pend_cold = 0;
         splits = 0;
         ov_splits = -1;
         ov_full = 0;
@@ -227,9 +227,9 @@ struct Engine {
     // ------------------------------------------------------------------ allocation
     MT_FI int32_t alloc_slot() {
         int32_t s;
-        if (n_free > 0) {
-            s = rfl((int32_t)s_free[n_free - 1]);
-            n_free--;
+        if (free_head >= 0) {
+            s = free_head;
+            free_head = rfl(s_seq[s]);
         } else {
             if (slot_top >= cap.seg) {
                 cap_fail(1);
@@ -312,7 +312,7 @@ struct Engine {
             cap_fail(1);
             return;
         }
-        u_list[nu] = slot | (s_meta[slot] & 0xFFFF0000u);
+        u_list[nu] = (uint16_t)slot;
         nu++;
         if (nu > max_u) max_u = nu;
     }
@@ -330,16 +330,15 @@ struct Engine {
             for (int32_t base = 0; base < nu; base += kWave) {
                 const int32_t j = base + lane;
                 const bool in = j < nu;
-                const uint32_t e = in ? u_list[j] : 0u;
-                const uint32_t slot = e & 0xFFFFu;
+                const uint32_t slot = in ? (uint32_t)u_list[j] : 0u;
                 bool valid = false;
                 if (in) {
                     uint32_t meta = s_meta[slot];
-                    valid = (meta & kMetaUnsettled) && (meta & kMetaLinked) && ((meta ^ e) & 0xFFFF0000u) == 0u;
+                    valid = (meta & kMetaUnsettled) && (meta & kMetaLinked);
                 }
                 const uint64_t vm = ballot(valid);
                 wsync();
-                if (valid) u_list[w + __popcll(vm & ((1ull << lane) - 1ull))] = e;
+                if (valid) u_list[w + __popcll(vm & ((1ull << lane) - 1ull))] = (uint16_t)slot;
                 w += __popcll(vm);
                 uint32_t vlen = 0, b = 0;
                 bool tie;
@@ -378,13 +377,12 @@ struct Engine {
         for (int32_t base = 0; base < nu; base += kWave) {
             const int32_t j = base + lane;
             const bool in = j < nu;
-            const uint32_t e = in ? u_list[j] : 0u;
-            const uint32_t slot = e & 0xFFFFu;
+            const uint32_t slot = in ? (uint32_t)u_list[j] : 0u;
             bool valid = false, elig = false;
             uint32_t meta = 0, add = 0, b = 0;
             if (in) {
                 meta = s_meta[slot];
-                valid = (meta & kMetaUnsettled) && (meta & kMetaLinked) && ((meta ^ e) & 0xFFFF0000u) == 0u;
+                valid = (meta & kMetaUnsettled) && (meta & kMetaLinked);
                 if (valid) {
                     int32_t seq = s_seq[slot], rseq = s_rseq[slot];
                     elig = seq <= min_seq && (rseq == kNoneSeq || rseq <= min_seq);
@@ -395,7 +393,7 @@ struct Engine {
             const bool keep = valid && !elig;
             const uint64_t km = ballot(keep);
             wsync();
-            if (keep) u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = e;
+            if (keep) u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (uint16_t)slot;
             if (elig) s_meta[slot] = meta & ~kMetaUnsettled;
             w += __popcll(km);
             chain_add(b_slen, elig && add > 0u, b, add);
@@ -488,32 +486,39 @@ struct Engine {
 
     // copy every linked segment's arena text into the other semispace
     MT_FI void text_gc() {
-        uint32_t nb = arena_base == pay_end ? pay_end + semi_t : pay_end;
+        resolve_cold();  // pending split records must be in HBM before they are rewritten
+        const uint32_t nb = arena_base == pay_end ? pay_end + semi_t : pay_end;
         uint32_t top = nb;
         wsync();
         for (int32_t base = 0; base < slot_top; base += kWave) {
             const int32_t slot = base + lane;
             bool mv = false;
+            uint4 cr = make_uint4(0, 0, 0, 0);
             if (slot < slot_top) {
-                uint32_t m = s_meta[slot];
-                uint32_t t = s_toff[slot];
-                mv = (m & kMetaLinked) && !(m & kMetaMarker) && t >= arena_base && t < arena_end;
+                const uint32_t m = s_meta[slot];
+                if ((m & kMetaLinked) && !(m & kMetaMarker)) {
+                    cr = cold[slot];
+                    mv = cr.z >= arena_base && cr.z < arena_end;
+                }
             }
             uint64_t msk = ballot(mv);
             while (msk) {
-                int f = first_lane(msk);
+                const int f = first_lane(msk);
                 msk &= msk - 1;
-                uint32_t sl = (uint32_t)(base + f);
-                uint32_t len = s_len[sl];
+                const uint32_t sl = (uint32_t)(base + f);
+                const uint32_t len = s_len[sl];
                 uint32_t cap16 = (len + 15u) & ~15u;
                 if (cap16 == 0) cap16 = 16;
                 if (top + cap16 > nb + semi_t) {
                     cap_fail(2);
                     return;
                 }
-                text_copy(top, s_toff[sl], len);
-                s_toff[sl] = top;
-                s_tcap[sl] = cap16;
+                text_copy(top, rdl(cr.z, f), len);
+                if (lane == f) {
+                    cr.z = top;
+                    cr.w = cap16;
+                    cold[sl] = cr;
+                }
                 top += cap16;
             }
             wsync();
@@ -530,36 +535,43 @@ struct Engine {
     // several segments are copied once)
     MT_FI void pool_reserve(uint32_t words) {
         if (pool_top + words <= pool_end) return;
-        uint32_t nb = pool_base == 1u ? 1u + semi_p : 1u;
+        resolve_cold();
+        const uint32_t nb = pool_base == 1u ? 1u + semi_p : 1u;
         uint32_t top = nb;
         wsync();
         for (int32_t base = 0; base < slot_top; base += kWave) {
             const int32_t slot = base + lane;
-            bool mv = slot < slot_top && (s_meta[slot] & kMetaLinked) && s_props[slot] != 0u;
-            uint64_t m = ballot(mv);
-            while (m) {
-                int f = first_lane(m);
-                m &= m - 1;
-                uint32_t sl = (uint32_t)(base + f);
-                uint32_t old = s_props[sl];
-                uint32_t hdr = pool[old];
+            uint32_t old = 0;
+            if (slot < slot_top) {
+                const uint32_t m = s_meta[slot];
+                if ((m & kMetaLinked) && (m & kMetaHasProps)) old = cold[slot].x;
+            }
+            uint64_t msk = ballot(old != 0u);
+            while (msk) {
+                const int f = first_lane(msk);
+                msk &= msk - 1;
+                const uint32_t sl = (uint32_t)(base + f);
+                const uint32_t o = rdl(old, f);
+                const uint32_t hdr = pool[o];
                 uint32_t nid;
                 if (hdr == 0xFFFFFFFFu) {
-                    nid = pool[old + 1];
+                    nid = pool[o + 1];
                 } else {
-                    uint32_t w = 2u + 2u * hdr;
+                    const uint32_t w = 2u + 2u * hdr;
                     if (top + w > nb + semi_p) {
                         cap_fail(3);
                         return;
                     }
-                    for (uint32_t i = lane; i < w; i += kWave) pool[top + i] = pool[old + i];
+                    for (uint32_t i = lane; i < w; i += kWave) pool[top + i] = pool[o + i];
                     wsync();
                     nid = top;
                     top += w;
-                    pool[old] = 0xFFFFFFFFu;
-                    pool[old + 1] = nid;
+                    if (lane == 0) {
+                        pool[o] = 0xFFFFFFFFu;
+                        pool[o + 1] = nid;
+                    }
                 }
-                s_props[sl] = nid;
+                if (lane == 0) cold[sl].x = nid;
                 wsync();
             }
         }
@@ -689,51 +701,78 @@ struct Engine {
 
     // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568,
     // textSegment.ts:103-111): the right part becomes a new leaf right after child k of blk.
-    // The settled sums do not change (both halves inherit the segment's state).
+    // The settled sums do not change (both halves inherit the segment's state).  The cold
+    // record is read now and written back in resolve_cold(); a second split of the same op
+    // forwards the first one's pending records instead of reading HBM.
     MT_FI void split_at(int32_t blk, int32_t k, uint32_t r) {
         PF_SCOPE(2);
-        uint32_t slot = rfl((uint32_t)b_child[blk * 8 + k]);
-        uint32_t meta = s_meta[slot];
+        const uint32_t slot = rfl((uint32_t)b_child[blk * 8 + k]);
+        const uint32_t meta = s_meta[slot];
         if (meta & kMetaMarker) return;  // Marker.createSplitSegmentAt returns undefined
-        int32_t ns = alloc_slot();
-        if (ns < 0) return;
-        uint32_t len = s_len[slot], toff = s_toff[slot], tcap = s_tcap[slot];
-        uint32_t last = text[toff + r - 1];  // consumed in resolve_splits()
-        if (pend_n == 0) {
-            pend_slot0 = slot;
-            pend_ch0 = last;
+        uint4 cr;
+        if (pend_n > 0 && slot == ps0) {
+            resolve_splits();  // (inverted range) the first split's left half is cut again
+            cr = make_uint4(pc0.x, pc0.y, pc0.z, pr0);
+        } else if (pend_n > 0 && slot == pn0) {
+            cr = make_uint4(pc0.x, pc0.y, pc0.z + pr0, pc0.w - pr0);
         } else {
-            pend_slot1 = slot;
-            pend_ch1 = last;
+            cr = cold[slot];
+        }
+        const int32_t ns = alloc_slot();
+        if (ns < 0) return;
+        const uint32_t len = s_len[slot];
+        if (pend_n == 0) {
+            ps0 = slot;
+            pn0 = (uint32_t)ns;
+            pr0 = r;
+            pc0 = cr;
+        } else {
+            ps1 = slot;
+            pn1 = (uint32_t)ns;
+            pr1 = r;
+            pc1 = cr;
         }
         pend_n++;
         s_len[ns] = len - r;
         s_seq[ns] = s_seq[slot];
         s_rseq[ns] = s_rseq[slot];
         s_ovl[ns] = s_ovl[slot];
-        s_props[ns] = s_props[slot];
-        s_phash[ns] = s_phash[slot];
-        s_toff[ns] = toff + r;
-        s_tcap[ns] = tcap - r;
-        uint32_t gen = s_meta[ns] & 0xFFFF0000u;
-        s_meta[ns] = (meta & 0x0000FFFFu) | gen;  // inherits ends-NL of the tail, linked, unsettled
+        const uint32_t gen = s_meta[ns] & kGenMask;
+        s_meta[ns] = (meta & ~kGenMask) | gen;  // inherits ends-NL of the tail, linked, unsettled
         s_len[slot] = r;
-        s_tcap[slot] = r;
         wsync();
         if (meta & kMetaUnsettled) u_push((uint32_t)ns);
         insert_leaf(blk, k + 1, (uint32_t)ns);
     }
 
-    MT_FI void resolve_splits() {
-        if (pend_n > 0) {
-            uint32_t m = s_meta[pend_slot0];
-            s_meta[pend_slot0] = pend_ch0 == (uint32_t)'\n' ? (m | kMetaEndsNL) : (m & ~kMetaEndsNL);
+    // write the pending splits' cold records and start the text loads for ends-with-'\n'
+    MT_FI void resolve_cold() {
+        for (int32_t i = pend_cold; i < pend_n; i++) {
+            const uint32_t sl = i ? ps1 : ps0, ns = i ? pn1 : pn0, r = i ? pr1 : pr0;
+            const uint4 c = i ? pc1 : pc0;
+            if (lane == 0) {
+                cold[sl] = make_uint4(c.x, c.y, c.z, r);
+                cold[ns] = make_uint4(c.x, c.y, c.z + r, c.w - r);
+            }
+            // a text without any '\n' cannot end in one: no HBM read
+            const uint32_t ch = (s_meta[sl] & kMetaHasNL) ? (uint32_t)text[c.z + r - 1] : 0u;
+            if (i) pch1 = ch;
+            else pch0 = ch;
         }
-        if (pend_n > 1) {
-            uint32_t m = s_meta[pend_slot1];
-            s_meta[pend_slot1] = pend_ch1 == (uint32_t)'\n' ? (m | kMetaEndsNL) : (m & ~kMetaEndsNL);
+        pend_cold = pend_n;
+    }
+
+    MT_FI void resolve_splits() {
+        if (pend_n == 0) return;
+        resolve_cold();
+        for (int32_t i = 0; i < pend_n; i++) {
+            const uint32_t sl = i ? ps1 : ps0;
+            const uint32_t ch = i ? pch1 : pch0;
+            const uint32_t m = s_meta[sl];
+            s_meta[sl] = ch == (uint32_t)'\n' ? (m | kMetaEndsNL) : (m & ~kMetaEndsNL);
         }
         pend_n = 0;
+        pend_cold = 0;
         wsync();
     }
 
@@ -763,7 +802,7 @@ struct Engine {
     MT_FI void add_to_lru(int32_t blk, uint32_t slot, int32_t seq) {
         if (b_scour[blk] != kScourTrue && seq > cur_seq) {
             b_scour[blk] = kScourTrue;
-            heap_add(slot | (s_meta[slot] & 0xFFFF0000u), seq);
+            heap_add(slot | (s_meta[slot] & kGenMask), seq);
         }
     }
 
@@ -850,7 +889,7 @@ struct Engine {
     // order (null deletes: properties.ts:95-116).  Returns the new set id (hash in hout).
     MT_FI uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout) {
         uint32_t *keys = scratch;
-        uint32_t *vals = scratch + 128;
+        uint32_t *vals = scratch + 64;
         uint32_t n = old ? pool[old] : 0u;
         if (n > 64u || nop > 64u) {
             cap_fail(3);
@@ -969,20 +1008,17 @@ struct Engine {
         PF_SCOPE(7);
         const bool in = lane < n;
         int32_t rseq = kNoneSeq, seq = 0;
-        uint32_t meta = 0, len = 0, props = 0, ph = 0, toff = 0, tcap = 0;
+        uint32_t meta = 0, len = 0;
+        uint4 cr = make_uint4(0, 0, 0, 0);
         if (in) {
+            cr = cold[slot];  // HBM: waited on only where props or merges need it
             rseq = s_rseq[slot];
             seq = s_seq[slot];
             meta = s_meta[slot];
             len = s_len[slot];
-            props = s_props[slot];
-            ph = s_phash[slot];
-            toff = s_toff[slot];
-            tcap = s_tcap[slot];
         }
         const bool rem = in && rseq != kNoneSeq;
         const bool cand = in && !rem && seq <= min_seq;
-        const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
         const uint32_t mprev = __shfl_up(meta, 1, kWave);
         const uint64_t candM = ballot(cand);
         const uint64_t freeR = ballot(rem && rseq <= min_seq);
@@ -992,14 +1028,22 @@ struct Engine {
         // tail not ending in '\n'
         const bool pair = lane > 0 && cand && ((candM >> (lane - 1)) & 1ull) && !((startM >> lane) & 1ull) &&
                           !(meta & kMetaMarker) && !(mprev & kMetaMarker) && !(mprev & kMetaEndsNL);
-        const bool peq = pprev == props;
-        const bool pmaybe = !peq && props != 0u && pprev != 0u && hprev == ph;
-        uint64_t pairM = ballot(pair && peq);
-        uint64_t maybeM = ballot(pair && pmaybe);
-        while (maybeM) {  // equal hashes, different sets: compare contents (rare)
-            const int k = first_lane(maybeM);
-            maybeM &= maybeM - 1;
-            if (props_match(rdl(props, k - 1), rdl(ph, k - 1), rdl(props, k), rdl(ph, k))) pairM |= 1ull << k;
+        // matchProperties: two leaves without prop sets match without reading HBM
+        const bool noprops = !((meta | mprev) & kMetaHasProps);
+        uint64_t pairM = ballot(pair && noprops);
+        const uint64_t withM = ballot(pair && !noprops);
+        if (withM) {
+            const uint32_t props = cr.x, ph = cr.y;
+            const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
+            const bool peq = pprev == props;
+            const bool pmaybe = !peq && props != 0u && pprev != 0u && hprev == ph;
+            pairM |= withM & ballot(peq);
+            uint64_t maybeM = withM & ballot(pmaybe);
+            while (maybeM) {  // equal hashes, different sets: compare contents (rare)
+                const int k = first_lane(maybeM);
+                maybeM &= maybeM - 1;
+                if (props_match(rdl(props, k - 1), rdl(ph, k - 1), rdl(props, k), rdl(ph, k))) pairM |= 1ull << k;
+            }
         }
         uint64_t mergeM;
         const uint64_t longM = ballot(in && len > kGranularity);
@@ -1027,7 +1071,7 @@ struct Engine {
             PF_SCOPE(8);
             uint64_t m = mergeM;
             int32_t h = -1;
-            uint32_t hslot = 0, pl = 0, ptoff = 0, pcap = 0, hmeta = 0;
+            uint32_t hslot = 0, pl = 0, ptoff = 0, pcap = 0, hmeta = 0, hprops = 0, hph = 0;
             int32_t gcs0 = text_gcs;
             while (m) {
                 const int k = first_lane(m);
@@ -1037,17 +1081,20 @@ struct Engine {
                     h = hk_;
                     hslot = rdl(slot, h);
                     pl = rdl(len, h);
-                    ptoff = rdl(toff, h);
-                    pcap = rdl(tcap, h);
+                    hprops = rdl(cr.x, h);
+                    hph = rdl(cr.y, h);
+                    ptoff = rdl(cr.z, h);
+                    pcap = rdl(cr.w, h);
                     hmeta = rdl(meta, h);
                 }
                 const uint32_t fslot = rdl(slot, k), sl = rdl(len, k);
-                uint32_t stoff = rdl(toff, k), stcap = rdl(tcap, k);
-                if (text_gcs != gcs0) {  // a compaction moved texts: offsets live in LDS again
-                    ptoff = s_toff[hslot];
-                    pcap = s_tcap[hslot];
-                    stoff = s_toff[fslot];
-                    stcap = s_tcap[fslot];
+                uint32_t stoff = rdl(cr.z, k), stcap = rdl(cr.w, k);
+                if (text_gcs != gcs0) {  // a compaction moved texts: offsets are in HBM again
+                    const uint4 hc = cold[hslot], fc = cold[fslot];
+                    ptoff = hc.z;
+                    pcap = hc.w;
+                    stoff = fc.z;
+                    stcap = fc.w;
                 }
                 const uint32_t need = pl + sl;
                 if (pcap == pl && ptoff + pl == stoff) {
@@ -1065,15 +1112,15 @@ struct Engine {
                     // reallocate; a compaction inside arena_alloc moves every text, so the head
                     // is written back first and both offsets re-read afterwards
                     s_len[hslot] = pl;
-                    s_toff[hslot] = ptoff;
-                    s_tcap[hslot] = pcap;
+                    if (lane == 0) cold[hslot] = make_uint4(hprops, hph, ptoff, pcap);
                     wsync();
                     const uint32_t ncap = 2u * need;
+                    const int32_t g0 = text_gcs;
                     const uint32_t dst = arena_alloc(ncap);
                     if (status) return 0;
-                    if (text_gcs != gcs0) {
-                        ptoff = s_toff[hslot];
-                        stoff = s_toff[fslot];
+                    if (text_gcs != g0) {
+                        ptoff = cold[hslot].z;
+                        stoff = cold[fslot].z;
                     }
                     text_copy(dst, ptoff, pl);
                     text_copy(dst + pl, stoff, sl);
@@ -1081,10 +1128,10 @@ struct Engine {
                     pcap = (ncap + 15u) & ~15u;
                 }
                 pl = need;
-                hmeta = (hmeta & ~kMetaEndsNL) | (rdl(meta, k) & kMetaEndsNL);
+                const uint32_t fm = rdl(meta, k);
+                hmeta = (hmeta & ~kMetaEndsNL) | (fm & (kMetaEndsNL | kMetaHasNL));
                 s_len[hslot] = pl;
-                s_toff[hslot] = ptoff;
-                s_tcap[hslot] = pcap;
+                if (lane == 0) cold[hslot] = make_uint4(hprops, hph, ptoff, pcap);
                 s_meta[hslot] = hmeta;
                 wsync();
             }
@@ -1094,12 +1141,16 @@ struct Engine {
         const uint64_t holdM = liveM & ~freeM;
         const uint64_t below = (1ull << lane) - 1ull;
         wsync();
+        // freed slots are pushed on the free list, linked through s_seq in lane order
+        const uint64_t above = ~((2ull << lane) - 1ull);
+        const uint64_t nxtM = freeM & above;
+        const int32_t nxt = __shfl((int)slot, nxtM ? first_lane(nxtM) : 0, kWave);
         if ((freeM >> lane) & 1ull) {
-            s_meta[slot] = ((meta >> 16) + 1u) << 16;  // unlinked, next generation
-            s_free[n_free + __popcll(freeM & below)] = (uint16_t)slot;
+            s_meta[slot] = ((meta >> kGenShift) + 1u) << kGenShift;  // unlinked, next generation
+            s_seq[slot] = nxtM ? nxt : free_head;
         }
+        if (freeM) free_head = (int32_t)rdl(slot, first_lane(freeM));
         if ((holdM >> lane) & 1ull) hold[__popcll(holdM & below)] = slot;
-        n_free += __popcll(freeM);
         wsync();
         return __popcll(holdM);
     }
@@ -1219,7 +1270,7 @@ struct Engine {
         const int32_t parent = b_parent[blk];
         const int32_t pn = b_count[parent];
         uint32_t *gat = scratch;
-        uint32_t *hold = scratch + 128;
+        uint32_t *hold = scratch + 64;
         uint64_t startM;
         const int32_t total = gather_grandchildren(parent, pn, gat, &startM);
         const uint32_t slot = lane < total ? gat[lane] : 0u;
@@ -1241,7 +1292,7 @@ struct Engine {
             heap_get(key, mseq);
             const uint32_t slot = key & 0xFFFFu;
             const uint32_t meta = s_meta[slot];
-            if ((meta & 0xFFFF0000u) != (key & 0xFFFF0000u) || !(meta & kMetaLinked)) continue;  // parent undefined
+            if ((meta & kGenMask) != (key & kGenMask) || !(meta & kMetaLinked)) continue;  // parent undefined
             const int32_t blk = s_blk[slot];
             if (b_scour[blk] == kScourFalse) continue;
             const int32_t cnt = b_count[blk];
@@ -1310,18 +1361,17 @@ struct Engine {
                 props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
                 if (status) return;
             }
-            uint32_t gen = s_meta[slot] & 0xFFFF0000u;
+            uint32_t gen = s_meta[slot] & kGenMask;
             uint32_t meta = gen | kMetaLinked | kMetaUnsettled | (c & 63u) | (kNoClient << 6);
             if (marker) meta |= kMetaMarker;
             if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
+            if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
+            if (props) meta |= kMetaHasProps;
             s_len[slot] = len;
             s_seq[slot] = op.seq;
             s_rseq[slot] = kNoneSeq;
             s_ovl[slot] = 0;
-            s_props[slot] = props;
-            s_phash[slot] = ph;
-            s_toff[slot] = op.payload;
-            s_tcap[slot] = marker ? 0u : len;
+            if (lane == 0) cold[slot] = make_uint4(props, ph, op.payload, marker ? 0u : len);
             s_meta[slot] = meta;
             wsync();
             u_push((uint32_t)slot);
@@ -1369,6 +1419,7 @@ struct Engine {
     MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end) {
         const uint32_t c = op.client;
         const int32_t ref = op.ref_seq;
+        if (op.type != MT_OP_REMOVE) resolve_cold();  // the walk reads prop ids of split halves
         ensure_overlay(ref, c);
         Walk W = descend(start, ref, c, true);
         PF_SCOPE(4);
@@ -1407,22 +1458,24 @@ struct Engine {
                 const bool newu = hit && !(meta & kMetaUnsettled);
                 const uint64_t um = ballot(newu);
                 if (um) {
+                    if (nu + __popcll(um) > cap.ulist) {
+                        cap_fail(1);
+                        return;
+                    }
                     const uint32_t lost = rdl(sum8(newu ? s_len[slot] : 0u), 0);
                     wsync();
                     if (newu) {
                         s_meta[slot] = meta | kMetaUnsettled;
-                        u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = slot | (meta & 0xFFFF0000u);
+                        u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (uint16_t)slot;
                     }
                     nu += __popcll(um);
-                    if (nu > cap.ulist) {
-                        cap_fail(1);
-                        return;
-                    }
                     if (nu > max_u) max_u = nu;
                     chain_add_uniform(blk, 0u - lost);
                 }
             }
             wsync();
+            uint32_t oldp = 0;
+            if (!is_remove && hit) oldp = cold[slot].x;
             // in document order: properties (annotate) and addToLRUSet
             while (hb) {
                 const int f = first_lane(hb);
@@ -1432,8 +1485,12 @@ struct Engine {
                     int32_t g0 = pool_gcs;
                     pool_reserve(2u + 2u * (64u + op.payload_len));
                     if (status) return;
-                    if (pool_gcs != g0) memo_n = 0;  // ids moved
-                    uint32_t old = s_props[sl];
+                    uint32_t old;
+                    if (pool_gcs != g0) {  // ids moved
+                        memo_n = 0;
+                        oldp = hit ? cold[slot].x : 0u;
+                    }
+                    old = rdl(oldp, f);
                     uint64_t mb = ballot((uint32_t)lane < memo_n && memo_old == old);
                     uint32_t nid, nh;
                     if (mb) {
@@ -1452,8 +1509,12 @@ struct Engine {
                             memo_n++;
                         }
                     }
-                    s_props[sl] = nid;
-                    s_phash[sl] = nh;
+                    if (lane == 0) {
+                        uint4 *cp = &cold[sl];
+                        cp->x = nid;
+                        cp->y = nh;
+                    }
+                    s_meta[sl] = s_meta[sl] | kMetaHasProps;
                 }
                 add_to_lru(blk, sl, op.seq);
                 if (status) return;
@@ -1503,10 +1564,9 @@ struct Engine {
                 const int32_t j = base + lane;
                 uint32_t vlen = 0;
                 if (j < nu) {
-                    const uint32_t e = u_list[j];
-                    const uint32_t slot = e & 0xFFFFu;
+                    const uint32_t slot = u_list[j];
                     const uint32_t meta = s_meta[slot];
-                    if ((meta & kMetaUnsettled) && (meta & kMetaLinked) && ((meta ^ e) & 0xFFFF0000u) == 0u) {
+                    if ((meta & kMetaUnsettled) && (meta & kMetaLinked)) {
                         bool tie;
                         view_of(slot, ref, c, vlen, tie);
                     }
@@ -1530,10 +1590,14 @@ struct Engine {
     // ------------------------------------------------------------------ output
     // the leaves in document order, each leaf block closed by an end-marker record
     MT_FI void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op) {
+        resolve_splits();
         wsync();
         int32_t w = 0;
         int32_t blk = root;
-        while (!b_leaf[blk]) blk = b_child[blk * 8];
+        // a document that ran out of LDS capacity is re-run: its tables may be incomplete
+        if (status == ST_CAPACITY && cap_kind == 1) blk = -1;
+        else
+            while (!b_leaf[blk]) blk = b_child[blk * 8];
         while (blk >= 0) {
             const int32_t n = b_count[blk];
             const int32_t j = w + lane;
@@ -1541,13 +1605,14 @@ struct Engine {
                 OutRec r;
                 if (lane < n) {
                     const uint32_t slot = b_child[blk * 8 + lane];
+                    const uint4 cr = cold[slot < (uint32_t)SEG ? slot : 0u];
                     r.len = s_len[slot];
                     r.seq = s_seq[slot];
                     r.rseq = s_rseq[slot];
-                    r.meta = s_meta[slot] & ~kMetaUnsettled;
+                    r.meta = s_meta[slot] & 0xFFFFu & ~kMetaUnsettled;
                     r.ovl = s_ovl[slot];
-                    r.props = s_props[slot];
-                    r.toff = s_toff[slot];
+                    r.props = cr.x;
+                    r.toff = cr.z;
                     r.blk = ((uint32_t)blk << 16) | slot;
                 } else {
                     r.len = 0;
@@ -1612,9 +1677,10 @@ __device__ __forceinline__ mt_op bcast_op(const mt_op &o, int l) {
 }
 
 template <int SEG>
-MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t d, uint8_t *smem) {
+MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_t d, uint8_t *smem) {
     E.lane = threadIdx.x;
     E.carve(smem);
+    E.cold = P.cold + w * (int64_t)SEG;
     E.text = P.text + P.doc_text_base[d];
     E.text_cap = P.doc_text_cap[d];
     E.pay_end = (P.doc_text_len[d] + 15u) & ~15u;
@@ -1647,7 +1713,7 @@ MT_FI void replay_body(const ReplayParams &P) {
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
     const uint64_t t_kernel = clock64();
 #endif
-    engine_setup(E, P, d, smem);
+    engine_setup(E, P, w, d, smem);
     const mt_op *ops = (const mt_op *)P.ops;
     const int64_t b0 = P.doc_op_off[d], b1 = P.doc_op_off[d + 1];
     int32_t done = 0, fail_op = -1;
@@ -1692,7 +1758,7 @@ MT_FI void generate_body(const ReplayParams &P) {
 #ifdef MT_PROF
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
 #endif
-    engine_setup(E, P, d, smem);
+    engine_setup(E, P, w, d, smem);
     mt_op *ops_out = (mt_op *)P.gen_ops + d * (int64_t)g.n_ops;
     mt_prop *props_out = (mt_prop *)P.gen_props;
     const int64_t prop_base = d * (int64_t)(2 * g.n_ops);
@@ -1743,10 +1809,12 @@ MT_FI void generate_body(const ReplayParams &P) {
             op.payload = pay_top;
             op.payload_len = n;
             uint16_t ch = 0;
+            bool has_nl = false;
             for (uint32_t i = 0; i < n; i++) {
                 uint32_t r = mt_rng_below(&x, 100);
                 if ((int32_t)r < g.pct_newline) {
                     ch = (uint16_t)'\n';
+                    has_nl = true;
                 } else {
                     uint32_t a = mt_rng_below(&x, 27);  // "abcdefghijklmnopqrstuvwxyz "
                     ch = a < 26u ? (uint16_t)('a' + a) : (uint16_t)' ';
@@ -1754,6 +1822,7 @@ MT_FI void generate_body(const ReplayParams &P) {
                 if (E.lane == 0) E.text[pay_top + i] = ch;
             }
             if (ch == (uint16_t)'\n') op.flags |= MT_OPF_INTERNAL_ENDS_NL;
+            if (has_nl) op.flags |= MT_OPF_INTERNAL_HAS_NL;
             pay_top += n;
         } else {
             uint32_t rl = 1;

@@ -81,6 +81,7 @@ struct Launch {
     DocOut *d_docout = nullptr;
     int32_t *d_list = nullptr;
     uint64_t *d_prof = nullptr;  // MT_PROF builds
+    uint4 *d_cold = nullptr;     // per-document cold segment records (class stride)
     size_t lds = 0;
 };
 
@@ -308,6 +309,7 @@ static void free_launches(mt_batch *b) {
         (void)hipFree(L.d_docout);
         (void)hipFree(L.d_list);
         (void)hipFree(L.d_prof);
+        (void)hipFree(L.d_cold);
     }
     b->launches.clear();
 }
@@ -504,9 +506,14 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
             mt_op &o = h_ops[i];
             if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
                 if (o.payload_len) memcpy(&h_text[b->h_text_base[d] + w], text + o.payload, 2ull * o.payload_len);
-                o.flags &= (uint16_t)~MT_OPF_INTERNAL_ENDS_NL;
+                o.flags &= (uint16_t)~MT_OPF_INTERNAL;
                 if (o.payload_len && text[o.payload + o.payload_len - 1] == (uint16_t)'\n')
                     o.flags |= (uint16_t)MT_OPF_INTERNAL_ENDS_NL;
+                for (uint32_t i = 0; i < o.payload_len; i++)
+                    if (text[o.payload + i] == (uint16_t)'\n') {
+                        o.flags |= (uint16_t)MT_OPF_INTERNAL_HAS_NL;
+                        break;
+                    }
                 o.payload = w;
                 w += o.payload_len;
             }
@@ -595,6 +602,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     L.lds = class_lds(L.cls);
     HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
     HIPCHK(dalloc(&L.d_docout, (size_t)n));
+    HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg));
     if (!L.docs.empty()) {
         HIPCHK(dalloc(&L.d_list, L.docs.size()));
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
@@ -605,6 +613,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.n_docs = n;
     P.doc_list = L.d_list;
     P.out_cap = L.out_cap;
+    P.cold = L.d_cold;
 #ifdef MT_PROF
     HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
     P.prof = L.d_prof;
@@ -1168,7 +1177,7 @@ MT_API int mt_batch_download_log(mt_batch *b, mt_op *ops, int64_t *doc_op_off, u
         for (int64_t d = 0; d < b->n_docs; d++) {
             for (int64_t i = b->h_off[d]; i < b->h_off[d + 1]; i++) {
                 mt_op &o = ops[i];
-                o.flags &= (uint16_t)~MT_OPF_INTERNAL_ENDS_NL;
+                o.flags &= (uint16_t)~MT_OPF_INTERNAL;
                 if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) o.payload += (uint32_t)tb;
             }
             tb += b->h_text_len[d];
@@ -1268,6 +1277,7 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
         L.lds = class_lds(cls);
         HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
         HIPCHK(dalloc(&L.d_docout, (size_t)n));
+        HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg));
         if (!todo.empty()) {
             HIPCHK(dalloc(&L.d_list, todo.size()));
             HIPCHK(hipMemcpy(L.d_list, todo.data(), 4 * todo.size(), hipMemcpyHostToDevice));
@@ -1282,6 +1292,7 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
         P.gen = d_gen;
         P.gen_ops = b->d_ops;
         P.gen_props = b->d_props;
+        P.cold = L.d_cold;
         const void *fn = kKernels[cls].generate;
         if (L.lds > 64 * 1024)
             HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
@@ -1293,6 +1304,7 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
         (void)hipFree(L.d_out);
         (void)hipFree(L.d_docout);
         (void)hipFree(L.d_list);
+        (void)hipFree(L.d_cold);
         std::vector<int32_t> again;
         for (int64_t i = 0; i < n; i++) {
             const int64_t d = todo.empty() ? i : todo[(size_t)i];

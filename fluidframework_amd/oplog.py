@@ -32,7 +32,7 @@ assert OP_DTYPE.itemsize == 32
 
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 15
 OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
-MAX_INSERT_PROPS = 2047
+MAX_INSERT_PROPS = 1023
 
 
 class UnsupportedOp(ValueError):

@@ -35,8 +35,9 @@ enum mt_op_type {
     MT_OP_NOOP = 15     /* non-"op" message: only client registration + updateSeqNumbers */
 };
 
-/* mt_op.flags: bits 0-3 public flags, bits 4-14 the prop count of an insert (<= 2047),
-   bit 15 is internal to the library (set at ingest: the insert's last code unit is '\n') */
+/* mt_op.flags: bits 0-3 public flags, bits 4-13 the prop count of an insert (<= 1023),
+   bits 14-15 are internal to the library (set at ingest: the insert's text contains a '\n' /
+   its last code unit is '\n') */
 enum mt_op_flags {
     MT_OPF_GROUP_CONT = 1u, /* more members of the same GROUP message follow          */
     MT_OPF_MARKER = 2u,     /* insert of a Marker: payload = refType, payload_len = 1  */
@@ -44,10 +45,12 @@ enum mt_op_flags {
     MT_OPF_REWRITE = 8u     /* annotate with combiningOp {name:"rewrite"}              */
 };
 #define MT_OPF_BITS(f) ((f) & 0xFu)
-#define MT_OPF_NPROPS(f) (((uint32_t)(f) >> 4) & 0x7FFu)
-#define MT_OPF_MAKE(bits, nprops) ((uint16_t)((((nprops) & 0x7FFu) << 4) | ((bits) & 0xFu)))
-#define MT_OPF_MAX_INSERT_PROPS 2047u
+#define MT_OPF_NPROPS(f) (((uint32_t)(f) >> 4) & 0x3FFu)
+#define MT_OPF_MAKE(bits, nprops) ((uint16_t)((((nprops) & 0x3FFu) << 4) | ((bits) & 0xFu)))
+#define MT_OPF_MAX_INSERT_PROPS 1023u
+#define MT_OPF_INTERNAL_HAS_NL 0x4000u
 #define MT_OPF_INTERNAL_ENDS_NL 0x8000u
+#define MT_OPF_INTERNAL (MT_OPF_INTERNAL_HAS_NL | MT_OPF_INTERNAL_ENDS_NL)
 
 typedef struct mt_op {
     uint8_t type;         /* enum mt_op_type                                             */
