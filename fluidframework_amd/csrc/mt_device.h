@@ -37,14 +37,16 @@ constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
 //   [12]   Marker                       [13]   text ends with '\n'
 //   [14]   linked (in the tree)         [15]   unsettled (in the overlay list, see mt_engine.hip)
 //   [16]   has a prop set               [17]   text contains a '\n' somewhere
-//   [18,32) slot generation (heap / overlay entry validity)
+//   [18]   removedClientOverlap is non-empty (the mask is in the cold record)
+//   [19,32) slot generation (heap entry validity)
 constexpr uint32_t kMetaMarker = 1u << 12;
 constexpr uint32_t kMetaEndsNL = 1u << 13;
 constexpr uint32_t kMetaLinked = 1u << 14;
 constexpr uint32_t kMetaUnsettled = 1u << 15;
 constexpr uint32_t kMetaHasProps = 1u << 16;
 constexpr uint32_t kMetaHasNL = 1u << 17;
-constexpr uint32_t kGenShift = 18;
+constexpr uint32_t kMetaHasOvl = 1u << 18;
+constexpr uint32_t kGenShift = 19;
 constexpr uint32_t kGenMask = 0xFFFFFFFFu << kGenShift;
 constexpr uint16_t kNoBlock = 0xFFFFu;
 
@@ -76,7 +78,8 @@ struct DocOut {
     int32_t max_blocks;
     int32_t max_heap;
     int32_t fail_op;    // index of the op that failed (-1)
-    int32_t cap_kind;   // ST_CAPACITY cause: 1 LDS tables, 2 text arena, 3 prop pool, 4 out records
+    int32_t cap_kind;   // ST_CAPACITY cause: 1 LDS tables, 2 text arena, 3 prop pool, 4 out records,
+                        // 6 LDS headroom: state checkpointed before op ops_done (resumable)
     int32_t gen_text;   // generator: payload code units written
     int32_t gen_props;  // generator: prop records written
 };
@@ -94,15 +97,20 @@ struct Caps {
 // Capacity classes are compile-time: each class is its own kernel instantiation
 // (mt_kernels.hip), so every LDS array base is an immediate offset and no SGPRs hold
 // table pointers or bounds.
-constexpr int kClassSegs[] = {64, 128, 256, 512, 1024, 2048};
-constexpr int kNumClasses = 6;
+constexpr int kClassSegs[] = {64, 128, 192, 256, 320, 384, 512, 768, 1024, 1536, 2048, 3072, 4096};
+constexpr int kNumClasses = 13;
+constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
+
+// checkpoint image of one document (u32 words): header + the used prefix of every LDS table
+constexpr int kCkHdr = 32;
+constexpr int64_t ck_words(int seg) { return 9ll * seg + 1024; }
 constexpr Caps class_caps(int seg) {
-    return Caps{seg, seg + seg / 4 + 16, seg / 4 + 16, seg / 8 + 64, seg / 2 + 96};
+    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 8 + 64, seg / 2 + 96};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
-    uint32_t len, seq, rseq, meta, ovl, sblk, ulist;
+    uint32_t len, seq, rseq, meta, sblk, ulist;
     uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, bytes;
 };
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
@@ -114,7 +122,6 @@ constexpr Layout make_layout(int seg) {
     L.seq = o;     o = lds_align(o + 4u * c.seg);
     L.rseq = o;    o = lds_align(o + 4u * c.seg);
     L.meta = o;    o = lds_align(o + 4u * c.seg);
-    L.ovl = o;     o = lds_align(o + 4u * c.seg);
     L.sblk = o;    o = lds_align(o + 2u * c.seg);
     L.ulist = o;   o = lds_align(o + 2u * c.ulist);
     L.bparent = o; o = lds_align(o + 2u * c.blk);
@@ -157,7 +164,15 @@ struct ReplayParams {
     void *gen_ops;                // mt_op[n_docs * n_ops]
     void *gen_props;              // mt_prop[n_docs * 2 * n_ops] (doc-local offsets rebased by host)
     uint64_t *prof;               // MT_PROF builds: kProfSlots cycle counters per workgroup
-    uint4 *cold;                  // [n_docs * cap.seg] cold segment records {props, phash, toff, tcap}
+    uint4 *cold;                  // [n_docs * cap.seg] cold segment records {props, ovl, toff, tcap}
+    // capacity escalation by checkpoint: a document short of LDS headroom writes its state to
+    // ck_out[w] and stops; a later launch in a larger class resumes it from ck_in[ck_src[w]]
+    uint32_t *ck_out;             // [n_docs * ck_words(SEG)] or null (largest class: no checkpoint)
+    const uint32_t *ck_in;        // previous launch's checkpoints (null: fresh start)
+    const int32_t *ck_src;        // per workgroup: index into ck_in / cold_in, -1: fresh start
+    const uint4 *cold_in;         // previous launch's cold records
+    int64_t ck_in_words;          // stride of ck_in
+    int32_t cold_in_seg;          // stride of cold_in
 };
 constexpr int kProfSlots = 12;
 

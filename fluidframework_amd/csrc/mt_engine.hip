@@ -5,9 +5,10 @@
 // mergeTree.ts:334): leaf blocks list segment slots, interior blocks list blocks, every
 // child list is one 16-byte row that a wave reads with one lane per child.
 //
-//   s_*[slot]   the fields nodeLength reads (SoA): length, seq, removedSeq, client ids, overlap
-//               mask, flags; and the leaf block.  The cold fields (prop-set id, prop hash, text
-//               offset/capacity) live in a per-document HBM table `cold[slot]` (16 B records).
+//   s_*[slot]   the fields nodeLength reads (SoA): length, seq, removedSeq, client ids, flags;
+//               and the leaf block.  The cold fields (prop-set id, removedClientOverlap mask —
+//               flagged in the meta word, read only when set —, text offset/capacity) live in a
+//               per-document HBM table `cold[slot]` (16 B records).
 //   b_*[block]  children[8], count, parent, needsScour, and the block's SETTLED length.
 //   u_list      the unsettled segments (the collab window's "hot" set).
 //   heap        the zamboni heap (collections.ts:213-265), in VGPRs.
@@ -124,7 +125,7 @@ struct Engine {
     static constexpr Caps cap = class_caps(SEG);
     static constexpr Layout lay = make_layout(SEG);
     // ---- LDS state
-    uint32_t *s_len, *s_meta, *s_ovl;
+    uint32_t *s_len, *s_meta;
     int32_t *s_seq, *s_rseq;  // s_seq of a free slot links the free list
     uint16_t *s_blk;
     uint16_t *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
@@ -134,7 +135,7 @@ struct Engine {
     uint32_t *b_slen, *b_acc;
     uint32_t *scratch;  // 128 words
     // ---- uniform scalars
-    int32_t slot_top, free_head, blk_top, n_bfree, root, depth, hn, nu;
+    int32_t slot_top, free_head, free_n, blk_top, n_bfree, root, depth, hn, nu;
     int32_t min_seq, cur_seq, status, settled_min;
     int32_t splits;                 // leaf/interior block splits so far (overlay staleness)
     int32_t ov_splits, ov_full;     // overlay computed at `ov_splits`; full (refSeq < minSeq) mode
@@ -151,7 +152,7 @@ struct Engine {
     int32_t max_heap, max_u, htop;
     uint2 *h_ent;
     // ---- global
-    uint4 *cold;  // cold segment records {props, phash, toff, tcap}
+    uint4 *cold;  // cold segment records {props, ovl, toff, tcap}
     uint16_t *text;
     uint32_t text_cap;
     uint32_t *pool;
@@ -171,7 +172,6 @@ struct Engine {
         s_seq = (int32_t *)(base + lay.seq);
         s_rseq = (int32_t *)(base + lay.rseq);
         s_meta = (uint32_t *)(base + lay.meta);
-        s_ovl = (uint32_t *)(base + lay.ovl);
         s_blk = (uint16_t *)(base + lay.sblk);
         u_list = (uint16_t *)(base + lay.ulist);
         b_parent = (uint16_t *)(base + lay.bparent);
@@ -200,6 +200,7 @@ struct Engine {
     MT_FI void init() {
         slot_top = 0;
         free_head = -1;
+        free_n = 0;
         blk_top = 0;
         n_bfree = 0;
         hn = 0;
@@ -230,6 +231,7 @@ struct Engine {
         if (free_head >= 0) {
             s = free_head;
             free_head = rfl(s_seq[s]);
+            free_n--;
         } else {
             if (slot_top >= cap.seg) {
                 cap_fail(1);
@@ -270,11 +272,11 @@ struct Engine {
         uint32_t meta = s_meta[slot];
         int32_t seq = s_seq[slot];
         int32_t rseq = s_rseq[slot];
-        uint32_t ovl = s_ovl[slot];
         uint32_t len = s_len[slot];
         uint32_t cli = meta & 63u, rcli = (meta >> 6) & 63u;
         bool vis = (cli == c) || (seq <= ref);
-        bool rem = (rcli == c) || ((ovl >> c) & 1u) || (rseq <= ref);
+        bool rem = (rcli == c) || (rseq <= ref);
+        if (!rem && (meta & kMetaHasOvl)) rem = (cold[slot].y >> c) & 1u;  // concurrent removers (rare)
         vlen = (vis && !rem) ? len : 0u;
         tie = !(rseq <= ref);
     }
@@ -736,13 +738,13 @@ struct Engine {
         s_len[ns] = len - r;
         s_seq[ns] = s_seq[slot];
         s_rseq[ns] = s_rseq[slot];
-        s_ovl[ns] = s_ovl[slot];
         const uint32_t gen = s_meta[ns] & kGenMask;
         s_meta[ns] = (meta & ~kGenMask) | gen;  // inherits ends-NL of the tail, linked, unsettled
         s_len[slot] = r;
         wsync();
         if (meta & kMetaUnsettled) u_push((uint32_t)ns);
         insert_leaf(blk, k + 1, (uint32_t)ns);
+        if (meta & kMetaHasOvl) resolve_cold();  // view_of reads the halves' overlap masks from HBM
     }
 
     // write the pending splits' cold records and start the text loads for ends-with-'\n'
@@ -1033,7 +1035,7 @@ struct Engine {
         uint64_t pairM = ballot(pair && noprops);
         const uint64_t withM = ballot(pair && !noprops);
         if (withM) {
-            const uint32_t props = cr.x, ph = cr.y;
+            const uint32_t props = cr.x, ph = props ? pool[props + 1] : 0u;
             const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
             const bool peq = pprev == props;
             const bool pmaybe = !peq && props != 0u && pprev != 0u && hprev == ph;
@@ -1071,7 +1073,7 @@ struct Engine {
             PF_SCOPE(8);
             uint64_t m = mergeM;
             int32_t h = -1;
-            uint32_t hslot = 0, pl = 0, ptoff = 0, pcap = 0, hmeta = 0, hprops = 0, hph = 0;
+            uint32_t hslot = 0, pl = 0, ptoff = 0, pcap = 0, hmeta = 0, hprops = 0, hov = 0;
             int32_t gcs0 = text_gcs;
             while (m) {
                 const int k = first_lane(m);
@@ -1082,7 +1084,7 @@ struct Engine {
                     hslot = rdl(slot, h);
                     pl = rdl(len, h);
                     hprops = rdl(cr.x, h);
-                    hph = rdl(cr.y, h);
+                    hov = rdl(cr.y, h);
                     ptoff = rdl(cr.z, h);
                     pcap = rdl(cr.w, h);
                     hmeta = rdl(meta, h);
@@ -1112,7 +1114,7 @@ struct Engine {
                     // reallocate; a compaction inside arena_alloc moves every text, so the head
                     // is written back first and both offsets re-read afterwards
                     s_len[hslot] = pl;
-                    if (lane == 0) cold[hslot] = make_uint4(hprops, hph, ptoff, pcap);
+                    if (lane == 0) cold[hslot] = make_uint4(hprops, hov, ptoff, pcap);
                     wsync();
                     const uint32_t ncap = 2u * need;
                     const int32_t g0 = text_gcs;
@@ -1131,7 +1133,7 @@ struct Engine {
                 const uint32_t fm = rdl(meta, k);
                 hmeta = (hmeta & ~kMetaEndsNL) | (fm & (kMetaEndsNL | kMetaHasNL));
                 s_len[hslot] = pl;
-                if (lane == 0) cold[hslot] = make_uint4(hprops, hph, ptoff, pcap);
+                if (lane == 0) cold[hslot] = make_uint4(hprops, hov, ptoff, pcap);
                 s_meta[hslot] = hmeta;
                 wsync();
             }
@@ -1150,6 +1152,7 @@ struct Engine {
             s_seq[slot] = nxtM ? nxt : free_head;
         }
         if (freeM) free_head = (int32_t)rdl(slot, first_lane(freeM));
+        free_n += __popcll(freeM);
         if ((holdM >> lane) & 1ull) hold[__popcll(holdM & below)] = slot;
         wsync();
         return __popcll(holdM);
@@ -1370,8 +1373,7 @@ struct Engine {
             s_len[slot] = len;
             s_seq[slot] = op.seq;
             s_rseq[slot] = kNoneSeq;
-            s_ovl[slot] = 0;
-            if (lane == 0) cold[slot] = make_uint4(props, ph, op.payload, marker ? 0u : len);
+            if (lane == 0) cold[slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
             s_meta[slot] = meta;
             wsync();
             u_push((uint32_t)slot);
@@ -1419,7 +1421,7 @@ struct Engine {
     MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end) {
         const uint32_t c = op.client;
         const int32_t ref = op.ref_seq;
-        if (op.type != MT_OP_REMOVE) resolve_cold();  // the walk reads prop ids of split halves
+        resolve_cold();  // the walk reads / updates cold records of split halves
         ensure_overlay(ref, c);
         Walk W = descend(start, ref, c, true);
         PF_SCOPE(4);
@@ -1445,7 +1447,10 @@ struct Engine {
             const uint32_t bend = n > 0 ? rdl(incl, n - 1) : base;
             if (is_remove && hit) {
                 if (s_rseq[slot] != kNoneSeq) {
-                    s_ovl[slot] |= 1u << c;  // addOverlappingClient (mergeTree.ts:2544-2552)
+                    // addOverlappingClient (mergeTree.ts:2544-2552)
+                    uint32_t *ov = &cold[slot].y;
+                    *ov = ((s_meta[slot] & kMetaHasOvl) ? *ov : 0u) | (1u << c);
+                    s_meta[slot] = s_meta[slot] | kMetaHasOvl;
                 } else {
                     s_rseq[slot] = op.seq;
                     s_meta[slot] = (s_meta[slot] & ~(63u << 6)) | ((c & 63u) << 6);
@@ -1509,11 +1514,7 @@ struct Engine {
                             memo_n++;
                         }
                     }
-                    if (lane == 0) {
-                        uint4 *cp = &cold[sl];
-                        cp->x = nid;
-                        cp->y = nh;
-                    }
+                    if (lane == 0) cold[sl].x = nid;
                     s_meta[sl] = s_meta[sl] | kMetaHasProps;
                 }
                 add_to_lru(blk, sl, op.seq);
@@ -1587,6 +1588,119 @@ struct Engine {
         return sum;
     }
 
+    // ------------------------------------------------------------------ checkpoint / resume
+    // LDS headroom for one more op (two splits + an insert, a split cascade per leaf insert,
+    // a range op's heap / overlay pushes, a pack); below it the document is checkpointed and
+    // resumed in a larger capacity class instead of failing mid-op.
+    MT_FI bool low_headroom() const {
+        const int32_t fs = cap.seg - slot_top + free_n;
+        const int32_t fb = cap.blk - blk_top + n_bfree;
+        return fs < 6 || fb < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 24;
+    }
+    template <typename T>
+    MT_FI void dump(uint32_t *&p, const T *src, int32_t n) {
+        for (int32_t i = lane; i < n; i += kWave) p[i] = (uint32_t)src[i];
+        p += n;
+    }
+    template <typename T>
+    MT_FI void load(const uint32_t *&p, T *dst, int32_t n) {
+        for (int32_t i = lane; i < n; i += kWave) dst[i] = (T)p[i];
+        p += n;
+    }
+    MT_FI void checkpoint(uint32_t *ck, int32_t ops_done) {
+        resolve_splits();
+        wsync();
+        if (lane == 0) {
+            ck[0] = 0x4D54434Bu;  // "MTCK"
+            ck[1] = (uint32_t)ops_done;
+            ck[2] = (uint32_t)slot_top;
+            ck[3] = (uint32_t)free_head;
+            ck[4] = (uint32_t)free_n;
+            ck[5] = (uint32_t)blk_top;
+            ck[6] = (uint32_t)n_bfree;
+            ck[7] = (uint32_t)root;
+            ck[8] = (uint32_t)depth;
+            ck[9] = (uint32_t)hn;
+            ck[10] = (uint32_t)nu;
+            ck[11] = (uint32_t)min_seq;
+            ck[12] = (uint32_t)cur_seq;
+            ck[13] = (uint32_t)settled_min;
+            ck[14] = (uint32_t)htop;
+            ck[15] = arena_top;
+            ck[16] = pool_top;
+            ck[17] = arena_base;
+            ck[18] = pool_base;
+            ck[19] = (uint32_t)pool_gcs;
+            ck[20] = (uint32_t)text_gcs;
+            ck[21] = (uint32_t)max_heap;
+            ck[22] = (uint32_t)max_u;
+        }
+        uint32_t *p = ck + kCkHdr;
+        dump(p, s_len, slot_top);
+        dump(p, s_seq, slot_top);
+        dump(p, s_rseq, slot_top);
+        dump(p, s_meta, slot_top);
+        dump(p, s_blk, slot_top);
+        dump(p, u_list, nu);
+        dump(p, b_parent, blk_top);
+        dump(p, b_free, n_bfree);
+        dump(p, (const uint32_t *)b_child, 4 * blk_top);
+        for (int32_t i = lane; i < blk_top; i += kWave)
+            p[i] = (uint32_t)b_count[i] | ((uint32_t)b_leaf[i] << 8) | ((uint32_t)(uint8_t)b_scour[i] << 16);
+        p += blk_top;
+        dump(p, b_slen, blk_top);
+        dump(p, (const uint32_t *)h_ent, 2 * (hn + 1));
+    }
+    // returns the number of ops the checkpoint had applied
+    MT_FI int32_t restore(const uint32_t *ck, const uint4 *cold_src) {
+        const int32_t ops_done = (int32_t)rfl(ck[1]);
+        slot_top = (int32_t)rfl(ck[2]);
+        free_head = (int32_t)rfl(ck[3]);
+        free_n = (int32_t)rfl(ck[4]);
+        blk_top = (int32_t)rfl(ck[5]);
+        n_bfree = (int32_t)rfl(ck[6]);
+        root = (int32_t)rfl(ck[7]);
+        depth = (int32_t)rfl(ck[8]);
+        hn = (int32_t)rfl(ck[9]);
+        nu = (int32_t)rfl(ck[10]);
+        min_seq = (int32_t)rfl(ck[11]);
+        cur_seq = (int32_t)rfl(ck[12]);
+        settled_min = (int32_t)rfl(ck[13]);
+        htop = (int32_t)rfl(ck[14]);
+        arena_top = rfl(ck[15]);
+        pool_top = rfl(ck[16]);
+        arena_base = rfl(ck[17]);
+        pool_base = rfl(ck[18]);
+        pool_gcs = (int32_t)rfl(ck[19]);
+        text_gcs = (int32_t)rfl(ck[20]);
+        max_heap = (int32_t)rfl(ck[21]);
+        max_u = (int32_t)rfl(ck[22]);
+        arena_end = arena_base + semi_t;
+        pool_end = pool_base + semi_p;
+        const uint32_t *p = ck + kCkHdr;
+        load(p, s_len, slot_top);
+        load(p, s_seq, slot_top);
+        load(p, s_rseq, slot_top);
+        load(p, s_meta, slot_top);
+        load(p, s_blk, slot_top);
+        load(p, u_list, nu);
+        load(p, b_parent, blk_top);
+        load(p, b_free, n_bfree);
+        load(p, (uint32_t *)b_child, 4 * blk_top);
+        for (int32_t i = lane; i < blk_top; i += kWave) {
+            const uint32_t v = p[i];
+            b_count[i] = (uint8_t)v;
+            b_leaf[i] = (uint8_t)(v >> 8);
+            b_scour[i] = (int8_t)(uint8_t)(v >> 16);
+        }
+        p += blk_top;
+        load(p, b_slen, blk_top);
+        load(p, (uint32_t *)h_ent, 2 * (hn + 1));
+        for (int32_t i = lane; i < slot_top; i += kWave) cold[i] = cold_src[i];
+        wsync();
+        return ops_done;
+    }
+
     // ------------------------------------------------------------------ output
     // the leaves in document order, each leaf block closed by an end-marker record
     MT_FI void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op) {
@@ -1594,8 +1708,8 @@ struct Engine {
         wsync();
         int32_t w = 0;
         int32_t blk = root;
-        // a document that ran out of LDS capacity is re-run: its tables may be incomplete
-        if (status == ST_CAPACITY && cap_kind == 1) blk = -1;
+        // a document that ran out of LDS capacity is re-run or resumed: no records
+        if (status == ST_CAPACITY && (cap_kind == 1 || cap_kind == kCapCheckpoint)) blk = -1;
         else
             while (!b_leaf[blk]) blk = b_child[blk * 8];
         while (blk >= 0) {
@@ -1610,7 +1724,7 @@ struct Engine {
                     r.seq = s_seq[slot];
                     r.rseq = s_rseq[slot];
                     r.meta = s_meta[slot] & 0xFFFFu & ~kMetaUnsettled;
-                    r.ovl = s_ovl[slot];
+                    r.ovl = (s_meta[slot] & kMetaHasOvl) ? cr.y : 0u;
                     r.props = cr.x;
                     r.toff = cr.z;
                     r.blk = ((uint32_t)blk << 16) | slot;
@@ -1717,12 +1831,23 @@ MT_FI void replay_body(const ReplayParams &P) {
     const mt_op *ops = (const mt_op *)P.ops;
     const int64_t b0 = P.doc_op_off[d], b1 = P.doc_op_off[d + 1];
     int32_t done = 0, fail_op = -1;
+    if (P.ck_in) {
+        const int32_t src = P.ck_src[w];
+        if (src >= 0) done = E.restore(P.ck_in + src * P.ck_in_words, P.cold_in + (int64_t)src * P.cold_in_seg);
+    }
     // ops stream through registers 64 at a time (coalesced 2 KiB loads), broadcast by readlane
-    mt_op cur = load_op_lane(ops, b0 + E.lane, b1);
-    for (int64_t base = b0; base < b1 && E.status == ST_OK; base += kWave) {
+    mt_op cur = load_op_lane(ops, b0 + done + E.lane, b1);
+    for (int64_t base = b0 + done; base < b1 && E.status == ST_OK; base += kWave) {
         mt_op nxt = load_op_lane(ops, base + kWave + E.lane, b1);
         int64_t n = b1 - base < kWave ? b1 - base : kWave;
         for (int i = 0; i < n; i++) {
+            if (P.ck_out && E.low_headroom()) {
+                E.checkpoint(P.ck_out + w * ck_words(SEG), done);
+                E.status = ST_CAPACITY;
+                E.cap_kind = kCapCheckpoint;
+                fail_op = (int32_t)(base - b0 + i);
+                break;
+            }
             mt_op op = bcast_op(cur, i);
             E.apply(op);
             if (E.status != ST_OK) {

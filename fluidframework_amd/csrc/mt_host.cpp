@@ -29,10 +29,17 @@
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);
 MT_DECLARE_CLASS(64)
 MT_DECLARE_CLASS(128)
+MT_DECLARE_CLASS(192)
 MT_DECLARE_CLASS(256)
+MT_DECLARE_CLASS(320)
+MT_DECLARE_CLASS(384)
 MT_DECLARE_CLASS(512)
+MT_DECLARE_CLASS(768)
 MT_DECLARE_CLASS(1024)
+MT_DECLARE_CLASS(1536)
 MT_DECLARE_CLASS(2048)
+MT_DECLARE_CLASS(3072)
+MT_DECLARE_CLASS(4096)
 
 using mt::Caps;
 using mt::DocOut;
@@ -65,10 +72,17 @@ struct KernelClass {
 static const KernelClass kKernels[mt::kNumClasses] = {
     {64, (const void *)mt_replay_kernel_64, (const void *)mt_generate_kernel_64},
     {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128},
+    {192, (const void *)mt_replay_kernel_192, (const void *)mt_generate_kernel_192},
     {256, (const void *)mt_replay_kernel_256, (const void *)mt_generate_kernel_256},
+    {320, (const void *)mt_replay_kernel_320, (const void *)mt_generate_kernel_320},
+    {384, (const void *)mt_replay_kernel_384, (const void *)mt_generate_kernel_384},
     {512, (const void *)mt_replay_kernel_512, (const void *)mt_generate_kernel_512},
+    {768, (const void *)mt_replay_kernel_768, (const void *)mt_generate_kernel_768},
     {1024, (const void *)mt_replay_kernel_1024, (const void *)mt_generate_kernel_1024},
+    {1536, (const void *)mt_replay_kernel_1536, (const void *)mt_generate_kernel_1536},
     {2048, (const void *)mt_replay_kernel_2048, (const void *)mt_generate_kernel_2048},
+    {3072, (const void *)mt_replay_kernel_3072, (const void *)mt_generate_kernel_3072},
+    {4096, (const void *)mt_replay_kernel_4096, (const void *)mt_generate_kernel_4096},
 };
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
 
@@ -82,6 +96,9 @@ struct Launch {
     int32_t *d_list = nullptr;
     uint64_t *d_prof = nullptr;  // MT_PROF builds
     uint4 *d_cold = nullptr;     // per-document cold segment records (class stride)
+    uint32_t *d_ck = nullptr;    // checkpoints of documents short of LDS headroom
+    int32_t *d_cksrc = nullptr;  // resume: per workgroup index into the previous launch (-1 fresh)
+    std::vector<int32_t> cksrc;
     size_t lds = 0;
 };
 
@@ -310,6 +327,8 @@ static void free_launches(mt_batch *b) {
         (void)hipFree(L.d_list);
         (void)hipFree(L.d_prof);
         (void)hipFree(L.d_cold);
+        (void)hipFree(L.d_ck);
+        (void)hipFree(L.d_cksrc);
     }
     b->launches.clear();
 }
@@ -367,7 +386,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
     if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
     if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
     if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
-    if (b->opt.max_retries <= 0) b->opt.max_retries = 3;
+    if (b->opt.max_retries <= 0) b->opt.max_retries = 6;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
@@ -552,13 +571,23 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
 // capacity class index: derived from ops per document unless seg_cap is given; `level`
 // escalates by whole classes
 static int class_for(const mt_batch *b, int32_t ops_per_doc, int level) {
-    int32_t want = b->opt.seg_cap > 0 ? b->opt.seg_cap : ops_per_doc / 16 + 64;
+    int32_t want = b->opt.seg_cap > 0 ? b->opt.seg_cap : ops_per_doc / 12 + 64;
     int c = 0;
     while (c + 1 < mt::kNumClasses && mt::kClassSegs[c] < want) c++;
     c += level;
     return c < mt::kNumClasses ? c : mt::kNumClasses;  // kNumClasses: nothing larger
 }
 static size_t class_lds(int c) { return mt::make_layout(mt::kClassSegs[c]).bytes; }
+static int max_lds_bytes();
+// the class a checkpointed document resumes in: at least 1.5x the slots
+static int resume_class(int c) {
+    int n = c + 1;
+    while (n < mt::kNumClasses && 2 * mt::kClassSegs[n] < 3 * mt::kClassSegs[c]) n++;
+    if (n >= mt::kNumClasses) n = mt::kNumClasses - 1;
+    while (n > c + 1 && class_lds(n) > (size_t)max_lds_bytes()) n--;
+    return n;
+}
+static bool class_usable(int c) { return c < mt::kNumClasses && class_lds(c) <= (size_t)max_lds_bytes(); }
 
 static int max_lds_bytes() {
     static int v = -1;
@@ -607,6 +636,14 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
         HIPCHK(dalloc(&L.d_list, L.docs.size()));
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
     }
+    // documents short of headroom checkpoint here unless this is the largest usable class
+    const bool can_grow = class_usable(L.cls + 1) && b->opt.max_retries > (int)b->launches.size() - 1;
+    if (can_grow) HIPCHK(dalloc(&L.d_ck, (size_t)n * (size_t)mt::ck_words(L.caps.seg)));
+    const Launch *prev = b->launches.size() >= 2 ? &b->launches[b->launches.size() - 2] : nullptr;
+    if (!L.cksrc.empty()) {
+        HIPCHK(dalloc(&L.d_cksrc, L.cksrc.size()));
+        HIPCHK(hipMemcpyAsync(L.d_cksrc, L.cksrc.data(), 4 * L.cksrc.size(), hipMemcpyHostToDevice, s));
+    }
     mt::ReplayParams P = base_params(b);
     P.out = L.d_out;
     P.doc_out = L.d_docout;
@@ -614,6 +651,14 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.doc_list = L.d_list;
     P.out_cap = L.out_cap;
     P.cold = L.d_cold;
+    P.ck_out = L.d_ck;
+    if (!L.cksrc.empty() && prev) {
+        P.ck_in = prev->d_ck;
+        P.ck_src = L.d_cksrc;
+        P.cold_in = prev->d_cold;
+        P.ck_in_words = mt::ck_words(prev->caps.seg);
+        P.cold_in_seg = prev->caps.seg;
+    }
 #ifdef MT_PROF
     HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
     P.prof = L.d_prof;
@@ -687,15 +732,28 @@ MT_API int mt_batch_sync(mt_batch *b) {
     b->kernel_ms = ms;
     int rc = gather_launch(b, 0);
     if (rc) return rc;
-    // capacity escalation: documents whose LDS tables overflowed re-run in a larger class
+    // capacity escalation: checkpointed documents resume in a class with >= 1.5x the slots;
+    // documents whose tables overflowed mid-op re-run from scratch in the next class
     for (int level = 1; level <= b->opt.max_retries; level++) {
+        const Launch &P0 = b->launches.back();
         Launch L;
-        for (int64_t d = 0; d < b->n_docs; d++)
-            if (b->docout[d].status == MT_CAPACITY && (b->docout[d].cap_kind == 1 || b->docout[d].cap_kind == 4))
+        bool any_ck = false;
+        for (int64_t d = 0; d < b->n_docs; d++) {
+            const DocOut &o = b->docout[d];
+            if (o.status != MT_CAPACITY || b->where[d].launch != (int32_t)b->launches.size() - 1) continue;
+            if (o.cap_kind == mt::kCapCheckpoint && P0.d_ck) {
                 L.docs.push_back((int32_t)d);
+                L.cksrc.push_back(b->where[d].idx);
+                any_ck = true;
+            } else if (o.cap_kind == 1 || o.cap_kind == 4) {
+                L.docs.push_back((int32_t)d);
+                L.cksrc.push_back(-1);
+            }
+        }
         if (L.docs.empty()) break;
-        L.cls = b->launches.back().cls + 1;
-        if (L.cls >= mt::kNumClasses || class_lds(L.cls) > (size_t)max_lds_bytes()) break;  // largest class reached
+        L.cls = any_ck ? resume_class(P0.cls) : P0.cls + 1;
+        if (!class_usable(L.cls)) break;  // largest class reached
+        if (!any_ck) L.cksrc.clear();
         b->launches.push_back(L);
         HIPCHK(hipEventRecord(b->ev0, b->run_stream));
         rc = launch_replay(b, b->run_stream, b->launches.back());
