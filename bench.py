@@ -80,18 +80,21 @@ def main():
     t0 = time.time()
     b.generate(p, doc_first)  # synthesize this rank's logs on the GPU (untimed)
     gen_s = time.time() - t0
+    log(rank, f"generated {n_docs} docs x {n_ops} ops in {gen_s:.1f} s")
     stream = torch.cuda.current_stream().cuda_stream
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         b.run(stream)
+        log(rank, f"warmup {i}: {b.stats()['kernel_ms']:.1f} ms kernel")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms = []
-    for _ in range(args.steps):
+    for i in range(args.steps):
         b.run(stream)
         kernel_ms.append(b.stats()["kernel_ms"])
+        log(rank, f"step {i}: {kernel_ms[-1]:.1f} ms kernel")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -175,6 +178,11 @@ def main():
     b.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def log(rank, msg):
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def cpu_baseline(b, fa, n_docs, n_ops, args):

@@ -29,6 +29,8 @@ for step in "$@"; do
     pmc2) run pmc2 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc2 -o run -- python3 -u bench.py --docs 1024 --steps 1 --warmup 0 --no-cpu ;;
     pmcf) run pmcf 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf -o run -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu ;;
     pmcw) run pmcw 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o run -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu ;;
+    full3) run full3 900 python -u bench.py --config 3 --docs 65536 --steps 1 --warmup 0 --no-cpu ;;
+    full3p) run full3p 900 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     *) echo "unknown step $step" ;;
   esac
 done
