@@ -74,7 +74,9 @@ def main():
     n_ops = args.ops or cfg["ops"]
     p = fa.gen_params(n_ops, n_clients=cfg["n_clients"], max_lag=cfg["max_lag"], pct_insert=cfg["pct_insert"],
                       pct_remove=cfg["pct_remove"], seed=args.seed)
-    doc_first = rank * n_docs  # disjoint shard of the global document space
+    from fluidframework_amd import shard
+
+    doc_first = shard.shard(rank, n_docs)  # disjoint shard of the global document space
 
     b = fa.ReplayBatch(n_docs)
     t0 = time.time()
@@ -111,26 +113,22 @@ def main():
 
     cnt = b.counters()
     capacity = {f: [int(np.percentile(cnt[f], q)) for q in (50, 99, 100)]
-                for f in ("max_slots", "max_entries", "max_blocks", "max_heap")}
+                for f in ("max_slots", "max_unsettled", "max_blocks", "max_heap")}
     ops_done = st["ops_applied"]
-    # gather per-document results to rank 0 over RCCL (status, ops applied)
-    gather_ms = 0.0
-    all_ok = int((statuses == 0).all())
-    if world > 1:
-        import numpy as np
-
-        res = torch.from_numpy(np.stack([statuses.astype("int64"),
-                                         np.full(n_docs, rank, "int64")], 1)).cuda()
-        outs = [torch.empty_like(res) for _ in range(world)] if rank == 0 else None
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        dist.gather(res, outs, dst=0)
-        torch.cuda.synchronize()
-        gather_ms = 1e3 * (time.perf_counter() - tg)
-        okt = torch.tensor([all_ok], device="cuda")
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        all_ok = int(okt.item())
-
+    # gather the per-document device digests and statuses to rank 0 over RCCL (untimed)
+    dig_t = torch.empty(n_docs, dtype=torch.int64, device="cuda")
+    b.device_digests(dig_t)
+    st_t = torch.from_numpy(statuses.astype("int64")).cuda()
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    gathered = shard.gather_results(dig_t, st_t, world, rank)
+    torch.cuda.synchronize()
+    gather_ms = 1e3 * (time.perf_counter() - tg)
+    all_ok, digest_xor = 0, None
+    if rank == 0:
+        all_dig, all_st = gathered
+        all_ok = int((all_st == 0).all())
+        digest_xor = f"{int(np.bitwise_xor.reduce(all_dig)):016x}"
     total_ops = n_ops * n_docs * world * args.steps
     value = total_ops / t_max
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
@@ -167,6 +165,8 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "docs_ok": all_ok,
+            "digests_gathered": world * n_docs,
+            "digest_xor": digest_xor,
             "ops_applied_per_step": int(ops_done),
             "lds_bytes_per_doc": st["lds_bytes"],
             "launches_per_step": st["launches"],

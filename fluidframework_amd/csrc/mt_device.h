@@ -176,4 +176,19 @@ struct ReplayParams {
 };
 constexpr int kProfSlots = 12;
 
+// mt_digest.hip: per-document device digest of one launch's results
+struct DigestParams {
+    const OutRec *out;         // this launch's records [n * out_cap]
+    const DocOut *doc_out;     // this launch's per-document results
+    const int32_t *doc_list;   // workgroup -> document (null: identity)
+    int64_t n;                 // workgroups of the launch
+    int32_t out_cap;
+    const uint16_t *text;
+    const uint64_t *doc_text_base;
+    const uint32_t *pool;
+    const uint64_t *doc_pool_base;
+    uint64_t *dst;             // [n_docs]
+};
+
+
 }  // namespace mt

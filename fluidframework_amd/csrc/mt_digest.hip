@@ -1,0 +1,80 @@
+// mt_digest.hip — per-document digest of the final device state, computed on the GPU.
+//
+// One wavefront per document hashes the document's final segment table (mt::OutRec records
+// in document order, leaf-block end markers included), each record together with its text
+// code units and its prop-set contents, and the collab-window scalars.  It is the 8-byte
+// per-document fingerprint that bench.py gathers to rank 0 over RCCL: it needs
+// no host serialization, depends only on the op log (slot and block ids do not enter), and so
+// is identical for a document whichever rank / launch / capacity class replayed it.
+#include <hip/hip_runtime.h>
+
+#include "mt_device.h"
+
+namespace mt {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finalizer
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+__device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
+    h ^= w;
+    return h * 0x100000001B3ull;
+}
+
+
+extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P) {
+    const int64_t w = blockIdx.x;
+    if (w >= P.n) return;
+    const DocOut o = P.doc_out[w];
+    // documents checkpointed or re-run in a later launch get their digest from that launch
+    if (o.status == ST_CAPACITY && (o.cap_kind == 1 || o.cap_kind == kCapCheckpoint || o.cap_kind == 4)) return;
+    const int64_t d = P.doc_list ? P.doc_list[w] : w;
+    const OutRec *rec = P.out + w * (int64_t)P.out_cap;
+    const uint16_t *text = P.text + P.doc_text_base[d];
+    const uint32_t *pool = P.pool + P.doc_pool_base[d];
+    uint64_t acc = 0;
+    for (int32_t i = threadIdx.x; i < o.n_out; i += 64) {
+        const OutRec r = rec[i];
+        uint64_t h = 0xCBF29CE484222325ull;
+        if ((r.blk & 0xFFFFu) == kMarkerSlot) {
+            h = fnv(h, 0xB10CB10Cu);
+        } else {
+            h = fnv(h, r.len);
+            h = fnv(h, (uint32_t)r.seq);
+            h = fnv(h, (uint32_t)r.rseq);
+            h = fnv(h, r.meta & 0x1FFFu);  // client ids, Marker
+            h = fnv(h, r.ovl);
+            if (r.meta & kMetaMarker) {
+                h = fnv(h, r.toff);  // refType
+            } else {
+                for (uint32_t k = 0; k < r.len; k++) h = fnv(h, text[r.toff + k]);
+            }
+            if (r.props) {
+                const uint32_t np = pool[r.props];
+                h = fnv(h, np);
+                uint64_t ps = 0;  // key order does not matter to matchProperties
+                for (uint32_t k = 0; k < np; k++)
+                    ps += mix64(((uint64_t)pool[r.props + 2 + 2 * k] << 32) | pool[r.props + 3 + 2 * k]);
+                h = fnv(h, (uint32_t)ps);
+                h = fnv(h, (uint32_t)(ps >> 32));
+            } else {
+                h = fnv(h, 0xFFFFFFFFu);
+            }
+        }
+        acc += mix64(h + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1));
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (threadIdx.x == 0) {
+        uint64_t h = mix64(acc ^ 0x6D74646967657374ull);
+        h = mix64(h + ((uint64_t)(uint32_t)o.depth << 32 | (uint32_t)o.n_out));
+        h = mix64(h + ((uint64_t)(uint32_t)o.min_seq << 32 | (uint32_t)o.cur_seq));
+        h = mix64(h + (uint64_t)(uint32_t)o.status);
+        P.dst[d] = h;
+    }
+}
+
+}  // namespace mt

@@ -40,6 +40,7 @@ MT_DECLARE_CLASS(1536)
 MT_DECLARE_CLASS(2048)
 MT_DECLARE_CLASS(3072)
 MT_DECLARE_CLASS(4096)
+extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 
 using mt::Caps;
 using mt::DocOut;
@@ -306,6 +307,7 @@ struct mt_batch {
     std::vector<DocRes> where;
     std::vector<DocOut> docout;  // gathered per doc
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint64_t *d_digest = nullptr;  // mt_batch_device_digests
     float kernel_ms = 0, total_ms = 0;
     bool ran = false;
     hipStream_t run_stream = nullptr;
@@ -402,6 +404,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
 MT_API void mt_batch_destroy(mt_batch *b) {
     if (!b) return;
     free_launches(b);
+    (void)hipFree(b->d_digest);
     free_log(b);
     (void)hipFree(b->d_vflags);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
@@ -774,6 +777,33 @@ MT_API int mt_batch_run(mt_batch *b, void *hip_stream) {
     int rc = mt_batch_launch(b, hip_stream);
     if (rc) return rc;
     return mt_batch_sync(b);
+}
+
+MT_API int mt_batch_device_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_device) {
+    if (!b || !dst) return MT_ERR_ARG;
+    if (!b->ran) return MT_ERR_STATE;
+    if (!b->d_digest) HIPCHK(dalloc(&b->d_digest, (size_t)b->n_docs));
+    hipStream_t s = b->run_stream ? b->run_stream : b->stream;
+    // launches in order: a document escalated to a later launch gets its digest from there
+    for (const Launch &L : b->launches) {
+        mt::DigestParams P{};
+        P.out = L.d_out;
+        P.doc_out = L.d_docout;
+        P.doc_list = L.d_list;
+        P.n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+        P.out_cap = L.out_cap;
+        P.text = b->d_text;
+        P.doc_text_base = b->d_text_base;
+        P.pool = b->d_pool;
+        P.doc_pool_base = b->d_pool_base;
+        P.dst = b->d_digest;
+        void *args[] = {&P};
+        HIPCHK(hipLaunchKernel((const void *)mt_digest_kernel, dim3((unsigned)P.n), dim3(64), args, 0, s));
+    }
+    HIPCHK(hipMemcpyAsync(dst, b->d_digest, 8 * (size_t)b->n_docs,
+                          dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MT_OK;
 }
 
 MT_API int mt_batch_get_stats(mt_batch *b, mt_batch_stats *o) {

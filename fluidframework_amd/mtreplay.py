@@ -36,10 +36,10 @@ EXPORTS = [
     "mt_batch_ingest", "mt_batch_generate", "mt_batch_run", "mt_batch_launch", "mt_batch_sync",
     "mt_batch_get_stats", "mt_batch_algorithmic_bytes", "mt_doc_status", "mt_doc_text", "mt_doc_props_runs",
     "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
-    "mt_batch_download_log", "mt_batch_doc_counters",
+    "mt_batch_download_log", "mt_batch_doc_counters", "mt_batch_device_digests",
 ]
 DOC_COUNTERS = ("status", "min_seq", "cur_seq", "depth", "n_entries", "text_top", "pool_top", "ops_done",
-                "max_entries", "max_slots", "max_blocks", "max_heap", "fail_op", "cap_kind", "launch", "reserved")
+                "max_unsettled", "max_slots", "max_blocks", "max_heap", "fail_op", "cap_kind", "launch", "reserved")
 
 
 class MtError(RuntimeError):
@@ -115,6 +115,7 @@ def lib():
     L.mt_batch_log_sizes.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.mt_batch_download_log.argtypes = [vp, vp, vp, vp, vp]
     L.mt_batch_doc_counters.argtypes = [vp, vp]
+    L.mt_batch_device_digests.argtypes = [vp, vp, i32]
     _lib = L
     return L
 
@@ -290,6 +291,18 @@ class ReplayBatch:
         a = np.zeros((self.n_docs, len(DOC_COUNTERS)), np.int32)
         _chk(lib().mt_batch_doc_counters(self.h, a.ctypes.data), "doc counters")
         return np.rec.fromarrays(a.T, names=list(DOC_COUNTERS))
+
+    def device_digests(self, out=None):
+        """Per-document 8-byte device digests of the last run (mt_batch_device_digests).
+        out: None -> numpy uint64 array; a torch int64 CUDA tensor of n_docs -> filled in place."""
+        if out is None:
+            a = np.zeros(self.n_docs, np.uint64)
+            _chk(lib().mt_batch_device_digests(self.h, a.ctypes.data, 0), "mt_batch_device_digests")
+            return a
+        if out.numel() != self.n_docs or out.element_size() != 8 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous 8-byte tensor of n_docs elements")
+        _chk(lib().mt_batch_device_digests(self.h, out.data_ptr(), 1 if out.is_cuda else 0), "mt_batch_device_digests")
+        return out
 
     def statuses(self) -> np.ndarray:
         L = lib()

@@ -23,6 +23,8 @@
  *   mt_doc_snapshot_v1/_blob    new SnapshotV1(mergeTree, logger).extractSync(); emit()
  *                               (merge-tree/src/snapshotV1.ts:85-247): blob path + contents
  *   mt_doc_digest               FNV-1a-64 over the final segment table (DESIGN.md "State digest")
+ *   mt_batch_device_digests     8-byte per-document fingerprint of the final state computed on the
+ *                               GPU (what rank 0 gathers over RCCL; no reference counterpart)
  *
  * Conventions: every call returns an int status (MT_OK = 0); output buffers are caller
  * owned and sized by calling with cap = 0 (the required length is returned in *len).
@@ -124,6 +126,9 @@ MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs);
 MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name, int64_t name_cap, char *buf,
                                 int64_t cap, int64_t *len);
 MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out);
+/* per-document device digests of the last run into dst[n_docs] (a device pointer when
+   dst_is_device, else host memory) */
+MT_API int mt_batch_device_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_device);
 MT_API int mt_doc_shape(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
 /* debugging aid: the final segment table, one line per entry */
 MT_API int mt_doc_dump(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);

@@ -192,3 +192,26 @@ def test_empty_documents_and_empty_inserts():
         b.run()
         assert b.doc(0).get_text() == "" and b.doc(0).snapshot_v1() == oracle[0].snapshot_v1()
         assert_doc_parity(b.doc(1), oracle[1])
+
+
+def test_device_digests_are_placement_independent():
+    """The 8-byte device digest (gathered to rank 0 by bench.py) depends only on a document's
+    log: the same global document replayed in another batch, shard or capacity class (with
+    checkpoint/resume) gets the same digest; different documents get different ones."""
+    p = fa.gen_params(600, pct_insert=55, pct_remove=35, seed=99)
+    with fa.ReplayBatch(12) as a:
+        a.generate(p, 0)
+        a.run()
+        da = a.device_digests()
+    with fa.ReplayBatch(6) as b:
+        b.generate(p, 6)
+        b.run()
+        db = b.device_digests()
+    with fa.ReplayBatch(12, seg_cap=64, max_retries=8) as c:
+        c.generate(p, 0)
+        c.run()
+        assert c.stats()["launches"] >= 2
+        dc = c.device_digests()
+    assert (da[6:] == db).all()
+    assert (da == dc).all()
+    assert len(set(da.tolist())) == 12

@@ -1,0 +1,58 @@
+"""world_size-2 rehearsal of the multi-GPU path on CPU (gloo): each rank replays its shard of
+the global document space and rank 0 gathers the per-document digests; the union must equal
+one process replaying every document.  The per-rank engine here is the oracle (the test
+checker) since there is no GPU; the sharding and gather code is the product's
+(fluidframework_amd/shard.py, also used by bench.py over RCCL)."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+import oracle_ffi as O
+from fluidframework_amd import shard
+
+WORLD, DOCS, OPS = 2, 6, 300
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _replay(first, n):
+    p = O.gen_params(OPS, pct_insert=55, pct_remove=35, seed=0x5EED)
+    ops, text, props, off = O.gen_batch(p, n, first_doc=first)
+    _, dig, st = O.replay_batch(ops, off, text, props, O.gen_tables(), O.gen_client_names(8), n_threads=1)
+    return dig, st
+
+
+def _rank(rank, port, out_path):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dig, st = _replay(shard.shard(rank, DOCS), DOCS)
+    res = shard.gather_results(torch.from_numpy(dig.view(np.int64)), torch.from_numpy(st), WORLD, rank)
+    if rank == 0:
+        np.savez(out_path, dig=res[0], st=res[1])
+    else:
+        assert res is None
+    dist.destroy_process_group()
+
+
+def test_gather_over_gloo_equals_single_process(tmp_path):
+    out = tmp_path / "gathered.npz"
+    mp.spawn(_rank, args=(_free_port(), str(out)), nprocs=WORLD, join=True)
+    got = np.load(out)
+    dig, st = _replay(0, WORLD * DOCS)
+    assert (got["st"] == st).all() and (st == 0).all()
+    assert (got["dig"] == dig).all()
+    assert len(set(got["dig"].tolist())) == WORLD * DOCS  # documents differ: the shards are disjoint
+
+
+def test_shard_ranges_partition_the_document_space():
+    firsts = [shard.shard(r, 1000) for r in range(8)]
+    assert firsts == [r * 1000 for r in range(8)]
