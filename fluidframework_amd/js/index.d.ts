@@ -1,0 +1,53 @@
+// index.d.ts — TypeScript declarations of the Node host layer (index.js) over libmtreplay.so.
+// Method names follow the reference Client (packages/dds/merge-tree/src/client.ts).
+
+/** ISequencedDocumentMessage fields the observer replay reads (protocol.ts:132-172). */
+export interface ISequencedDocumentMessage {
+    clientId: string;
+    sequenceNumber: number;
+    referenceSequenceNumber: number;
+    minimumSequenceNumber: number;
+    type: string;
+    contents: any;  // IMergeTreeOp (ops.ts:29-110) when type === "op"
+}
+
+export interface BatchOptions { segCap?: number; maxRetries?: number; }
+
+export interface GenParams {
+    nOps: number; nClients?: number; maxLag?: number; pctInsert?: number; pctRemove?: number;
+    minLen?: number; maxInsert?: number; pctNewline?: number; seed?: number;
+}
+
+export declare const STATUS: string[];
+export declare class UnsupportedOp extends Error {}
+
+export declare class ReplayClient {
+    readonly index: number;
+    /** Client.startOrUpdateCollaboration(longClientId) (client.ts:1051): the observer's id. */
+    startOrUpdateCollaboration(longClientId: string): void;
+    /** Client.applyMsg(msg) (client.ts:797): queued; applied on the GPU by ReplayBatch.run(). */
+    applyMsg(msg: ISequencedDocumentMessage | string): void;
+    /** 0 = OK, else the MT_* status of the Error applyMsg would have thrown. */
+    readonly status: number;
+    readonly error: string | undefined;
+    getText(): string;
+    getLength(): number;
+    getPropertiesAtPosition(pos: number): Record<string, any> | undefined;
+    propertyRuns(): Array<[number, number, string | null]>;
+    /** new SnapshotV1(mergeTree, logger).extractSync(); emit(): blob name -> utf-8 JSON. */
+    snapshotV1(): Record<string, string>;
+    digest(): bigint;
+}
+
+export declare class ReplayBatch {
+    constructor(nDocs: number, options?: BatchOptions);
+    readonly nDocs: number;
+    client(i: number): ReplayClient;
+    ingestMessages(docs: Array<Array<ISequencedDocumentMessage | string>>): void;
+    generate(params: GenParams, docFirst?: number): void;
+    run(): void;
+    runAsync(): Promise<void>;
+    stats(): { nDocs: number; nOps: number; opsApplied: number; docsFailed: number; launches: number;
+               kernelMs: number; totalMs: number; ldsBytes: number };
+    deviceDigests(): BigUint64Array;
+}

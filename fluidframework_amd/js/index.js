@@ -1,0 +1,248 @@
+// index.js — Node host layer over libmtreplay.so (through the N-API addon mtreplay.node).
+//
+// Mirrors the reference's per-document merge-tree surface so a FluidFramework host can drop
+// it in for the observer replay path:
+//
+//   reference (packages/dds/merge-tree/src, sequence/src)       here
+//   -------------------------------------------------------      ---------------------------------------
+//   new Client(specToSegment, logger)                            batch.client(i)  (a ReplayClient)
+//   client.startOrUpdateCollaboration(longId)  (client.ts:1051)  client.startOrUpdateCollaboration(longId)
+//   client.applyMsg(msg)                       (client.ts:797)   client.applyMsg(msg)   (queued), then
+//                                                                batch.run() / await batch.runAsync()
+//   client.getLength()                         (client.ts:1049)  client.getLength()
+//   sharedString.getText()                     (sharedString.ts:211) client.getText()
+//   client.getPropertiesAtPosition(pos)        (client.ts:1009)  client.getPropertiesAtPosition(pos)
+//   new SnapshotV1(mt, logger).extractSync(); emit()             client.snapshotV1()  ({header, body_0..})
+//   the Error applyMsg would throw                               client.status / client.error
+//
+// Every op is applied by the HIP kernel; this file only packs messages into the C ABI's
+// records (include/mt_oplog.h).  Loading throws when the addon or the GPU is missing: there
+// is no CPU fallback.
+'use strict';
+
+const path = require('path');
+
+let addon = null;
+function native() {
+    if (!addon) addon = require(path.join(__dirname, 'mtreplay.node'));
+    return addon;
+}
+
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 15;
+const OPF_GROUP_CONT = 1, OPF_MARKER = 2, OPF_HAS_PROPS = 4, OPF_REWRITE = 8;
+const MAX_INSERT_PROPS = 1023;
+const STATUS = ['OK', 'INVALID_POS', 'SEQ_ORDER', 'MSN_ORDER', 'UNSUPPORTED', 'BAD_INPUT', 'CAPACITY', 'INTERNAL'];
+
+class UnsupportedOp extends Error {}
+
+// Packs ISequencedDocumentMessage streams (protocol.ts:132-172; ops.ts:29-110) into the
+// 32-byte mt_op records, a UTF-16 text arena and interned property keys / values.  Short
+// client ids follow Client.getOrAddShortClientId (client.ts:636-660): observer first, then
+// first appearance.  Value ids intern JSON.stringify text; 0 is JSON null (delete).
+class Packer {
+    constructor(observer = 'readonly') {
+        this.observer = observer;
+        this.keys = [];
+        this.values = ['null'];
+        this.keyIds = new Map();
+        this.valueIds = new Map([['null', 0]]);
+        this.recs = [];
+        this.textParts = [];
+        this.textLen = 0;
+        this.props = [];
+        this.off = [0];
+        this.clients = [];
+    }
+    key(k) {
+        let i = this.keyIds.get(k);
+        if (i === undefined) {
+            i = this.keys.length;
+            this.keyIds.set(k, i);
+            this.keys.push(k);
+        }
+        return i;
+    }
+    value(v) {
+        if (v === null || v === undefined) return 0;
+        const s = JSON.stringify(v);
+        let i = this.valueIds.get(s);
+        if (i === undefined) {
+            i = this.values.length;
+            this.valueIds.set(s, i);
+            this.values.push(s);
+        }
+        return i;
+    }
+    propRecords(props) {
+        if (typeof props !== 'object' || props === null || Array.isArray(props)) throw new UnsupportedOp('props must be an object');
+        const off = this.props.length / 2;
+        for (const k of Object.keys(props)) this.props.push(this.key(k), this.value(props[k]));
+        return [off, this.props.length / 2 - off];
+    }
+    static flatten(op) {
+        if (op.type === 3) return (op.ops || []).reduce((a, m) => a.concat(Packer.flatten(m)), []);
+        return [op];
+    }
+    packOp(op, base) {
+        const t = op.type;
+        if (op.pos1 === undefined || op.relativePos1 !== undefined || op.register !== undefined)
+            throw new UnsupportedOp('relative positions / registers are not on the observer fast path');
+        const r = Object.assign({}, base, { type: t, flags: 0, pos1: op.pos1 | 0, pos2: 0, payload: 0, payloadLen: 0 });
+        if (t === OP_INSERT) {
+            const seg = op.seg;
+            let text = null, props;
+            if (typeof seg === 'string') text = seg;
+            else if (seg && typeof seg.text === 'string') { text = seg.text; props = seg.props; }
+            else if (seg && seg.marker) {
+                r.flags |= OPF_MARKER;
+                r.payload = seg.marker.refType | 0;
+                r.payloadLen = 1;
+                props = seg.props;
+            } else throw new UnsupportedOp('unknown segment spec');
+            if (text !== null) {
+                r.payload = this.textLen;
+                r.payloadLen = text.length;  // UTF-16 code units, as TextSegment.cachedLength
+                this.textParts.push(text);
+                this.textLen += text.length;
+            }
+            if (props && Object.keys(props).length) {  // TextSegment.make: `if (props) addProperties`
+                const [off, n] = this.propRecords(props);
+                if (n > MAX_INSERT_PROPS) throw new UnsupportedOp('too many insert props');
+                r.flags |= OPF_HAS_PROPS | (n << 4);
+                r.pos2 = off;
+            } else if (props && typeof props === 'object') {  // {} is truthy: an empty map
+                r.flags |= OPF_HAS_PROPS;
+                r.pos2 = this.props.length / 2;
+            }
+        } else if (t === OP_REMOVE || t === OP_ANNOTATE) {
+            r.pos2 = (op.pos2 || 0) | 0;
+            if (t === OP_ANNOTATE) {
+                if (op.combiningOp) {
+                    if (op.combiningOp.name !== 'rewrite') throw new UnsupportedOp('combiningOp other than rewrite');
+                    r.flags |= OPF_REWRITE;
+                }
+                [r.payload, r.payloadLen] = this.propRecords(op.props || {});
+            }
+        } else throw new UnsupportedOp(`op type ${t}`);
+        return r;
+    }
+    addDocument(messages, observer = this.observer) {
+        const names = [observer];
+        const short = new Map([[observer, 0]]);
+        const recs = [];
+        for (let msg of messages) {
+            if (typeof msg === 'string') msg = JSON.parse(msg);
+            let c = short.get(msg.clientId);
+            if (c === undefined) {
+                c = names.length;
+                short.set(msg.clientId, c);
+                names.push(msg.clientId);
+            }
+            const base = { client: c, seq: msg.sequenceNumber, refSeq: msg.referenceSequenceNumber, msn: msg.minimumSequenceNumber };
+            const noop = Object.assign({}, base, { type: OP_NOOP, flags: 0, pos1: 0, pos2: 0, payload: 0, payloadLen: 0 });
+            if (msg.type !== 'op') { recs.push(noop); continue; }
+            if (c === 0) throw new UnsupportedOp("ack of the observer's own op (local path)");
+            const members = Packer.flatten(msg.contents);
+            members.forEach((op, j) => {
+                const r = this.packOp(op, base);
+                if (j + 1 < members.length) r.flags |= OPF_GROUP_CONT;
+                recs.push(r);
+            });
+            if (!members.length) recs.push(noop);  // empty group: updateSeqNumbers only
+        }
+        for (const r of recs) this.recs.push(r);
+        this.off.push(this.off[this.off.length - 1] + recs.length);
+        this.clients.push(names);
+    }
+    finish() {
+        const ops = Buffer.alloc(32 * Math.max(1, this.recs.length));
+        this.recs.forEach((r, i) => {
+            const o = 32 * i;
+            ops.writeUInt8(r.type, o);
+            ops.writeUInt8(r.client, o + 1);
+            ops.writeUInt16LE(r.flags, o + 2);
+            ops.writeInt32LE(r.seq, o + 4);
+            ops.writeInt32LE(r.refSeq, o + 8);
+            ops.writeInt32LE(r.msn, o + 12);
+            ops.writeInt32LE(r.pos1, o + 16);
+            ops.writeInt32LE(r.pos2, o + 20);
+            ops.writeUInt32LE(r.payload >>> 0, o + 24);
+            ops.writeUInt32LE(r.payloadLen >>> 0, o + 28);
+        });
+        const text = new Uint16Array(Math.max(1, this.textLen));
+        let w = 0;
+        for (const s of this.textParts) for (let i = 0; i < s.length; i++) text[w++] = s.charCodeAt(i);
+        return {
+            ops, docOpOff: BigInt64Array.from(this.off.map(BigInt)), text, nText: this.textLen,
+            props: Uint32Array.from(this.props.length ? this.props : [0, 0]),
+            keys: this.keys, values: this.values, clients: this.clients,
+        };
+    }
+}
+
+// One document of a batch: the merge-tree Client of an observer replica.
+class ReplayClient {
+    constructor(batch, index) {
+        this.batch = batch;
+        this.index = index;
+        this.longClientId = 'readonly';
+        this.messages = [];
+    }
+    startOrUpdateCollaboration(longClientId) { this.longClientId = longClientId; }
+    applyMsg(msg) { this.batch.queued = true; this.messages.push(msg); }
+    get status() { return native().docStatus(this.batch.h, this.index); }
+    get error() { const s = this.status; return s === 0 ? undefined : STATUS[s] || String(s); }
+    getText() { return native().docText(this.batch.h, this.index); }
+    getLength() { return this.getText().length; }
+    // [start, length, JSON.stringify(props) | null] per run of equal properties over the text
+    propertyRuns() { return JSON.parse(native().docPropsRuns(this.batch.h, this.index)); }
+    getPropertiesAtPosition(pos) {
+        for (const [start, len, props] of this.propertyRuns())
+            if (start <= pos && pos < start + len) return props === null ? undefined : JSON.parse(props);
+        return undefined;
+    }
+    snapshotV1() { return native().docSnapshotV1(this.batch.h, this.index); }
+    digest() { return native().docDigest(this.batch.h, this.index); }
+}
+
+// A batch of SharedString documents replayed on the current MI355X.
+class ReplayBatch {
+    constructor(nDocs, options = {}) {
+        this.nDocs = nDocs;
+        this.h = native().createBatch(nDocs, options);
+        this.clients = Array.from({ length: nDocs }, (_, i) => new ReplayClient(this, i));
+        this.queued = false;
+    }
+    client(i) { return this.clients[i]; }
+    // messages queued through client(i).applyMsg -> one packed upload
+    flush() {
+        if (!this.queued) return;
+        const p = new Packer();
+        for (const c of this.clients) p.addDocument(c.messages, c.longClientId);
+        this.ingestPacked(p.finish());
+        this.queued = false;
+    }
+    ingestPacked(pb) {
+        const n = native();
+        n.setTables(this.h, pb.keys.length ? pb.keys : ['_'], pb.values);
+        const shared = pb.clients.every((c) => JSON.stringify(c) === JSON.stringify(pb.clients[0]));
+        if (shared && pb.clients.length) n.setClients(this.h, -1, pb.clients[0]);
+        else pb.clients.forEach((c, i) => n.setClients(this.h, i, c));
+        n.ingest(this.h, pb.ops, pb.docOpOff, pb.text.subarray(0, Math.max(1, pb.nText)), pb.props);
+    }
+    ingestMessages(docs) {
+        docs.forEach((msgs, i) => { for (const m of msgs) this.clients[i].applyMsg(m); });
+        this.flush();
+    }
+    generate(params, docFirst = 0) { native().generate(this.h, params, docFirst); }
+    run() { this.flush(); native().run(this.h); }
+    runAsync() { this.flush(); return native().runAsync(this.h); }
+    stats() { return native().stats(this.h); }
+    deviceDigests() {
+        const out = new BigUint64Array(this.nDocs);
+        native().deviceDigests(this.h, out);
+        return out;
+    }
+}
+
+module.exports = { ReplayBatch, ReplayClient, Packer, UnsupportedOp, STATUS, native };

@@ -65,7 +65,7 @@ typedef struct mt_batch mt_batch;
 typedef struct mt_batch_options {
     int32_t chunk_size;      /* SnapshotV1 chunk size; 0 -> 10000 (snapshotV1.ts:40)              */
     int32_t seg_cap;         /* segment slots of the first LDS capacity class (rounded up to a
-                                class: 64 .. 2048); 0 -> derived from the ops per document        */
+                                class: 64 .. 4096); 0 -> derived from the ops per document        */
     int32_t oe_cap;          /* reserved (entries / blocks / heap follow from the class)           */
     int32_t blk_cap;         /* reserved                                                           */
     int32_t heap_cap;        /* reserved                                                           */
@@ -116,7 +116,7 @@ MT_API int mt_batch_algorithmic_bytes(mt_batch *b, double *bytes);
 
 MT_API int32_t mt_doc_status(mt_batch *b, int64_t doc);
 /* per-document run counters, MT_DOC_COUNTERS int32 per document (capacity planning / stats):
-   status, min_seq, cur_seq, depth, n_entries, text_top, pool_top, ops_done, max_entries,
+   status, min_seq, cur_seq, depth, n_entries, text_top, pool_top, ops_done, max_unsettled,
    max_slots, max_blocks, max_heap, fail_op, cap_kind, launch, reserved */
 #define MT_DOC_COUNTERS 16
 MT_API int mt_batch_doc_counters(mt_batch *b, int32_t *out);

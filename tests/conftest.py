@@ -17,5 +17,6 @@ def _built():
     import __graft_entry__ as g
 
     g.build_lib()
+    g.build_napi()
     g.build_oracle()
     yield

@@ -1,0 +1,80 @@
+"""The Node host layer (fluidframework_amd/js: N-API addon + index.js) over the C ABI.
+
+CPU: the addon builds, loads and exports its functions; without a GPU it fails loudly.
+GPU: replaying the KATs and mixed-op logs through Node gives the oracle's text, property
+runs, SnapshotV1 blobs and digests (the JS packer is an independent restatement of
+fluidframework_amd/oplog.py, so this also cross-checks the two packers)."""
+import json
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+import oracle_ffi as O
+
+ROOT = Path(__file__).resolve().parents[1]
+NODE = shutil.which("node")
+ADDON = ROOT / "fluidframework_amd" / "js" / "mtreplay.node"
+pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node / N-API addon not available")
+
+FUNCS = {"createBatch", "setTables", "setClients", "ingest", "generate", "run", "runAsync", "docStatus", "docText",
+         "docPropsRuns", "docSnapshotV1", "docDigest", "deviceDigests", "stats", "statusString"}
+
+
+def _node(code):
+    return subprocess.run([NODE, "-e", code], capture_output=True, text=True, cwd=ROOT, timeout=60)
+
+
+def test_addon_loads_and_exports():
+    r = _node("const m=require('./fluidframework_amd/js/mtreplay.node');console.log(JSON.stringify(Object.keys(m)))")
+    assert r.returncode == 0, r.stderr
+    assert set(json.loads(r.stdout)) == FUNCS
+
+
+def test_addon_fails_loudly_without_device():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    r = _node("const {ReplayBatch}=require('./fluidframework_amd/js');"
+              "try{new ReplayBatch(2);console.log('created')}catch(e){console.log(e.code)}")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "103"  # MT_ERR_NO_DEVICE
+
+
+def _msg(c, s, r, contents, msn=0):
+    return {"clientId": c, "sequenceNumber": s, "referenceSequenceNumber": r, "minimumSequenceNumber": msn,
+            "type": "op", "contents": contents}
+
+
+@pytest.mark.gpu
+def test_node_replay_matches_oracle(tmp_path):
+    kats = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+    docs = [k["messages"] for k in kats]
+    docs.append([_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "héllo wörld", "props": {"b": 1, "10": "x", "2": None}}}),
+                 _msg("B", 2, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1}, "props": {"id": "m1"}}}),
+                 _msg("A", 3, 1, {"type": 3, "ops": [{"type": 0, "pos1": 2, "seg": "XY"},
+                                                     {"type": 2, "pos1": 0, "pos2": 4, "props": {"c": {"n": [1, 2]}}}]}),
+                 _msg("B", 4, 3, {"type": 2, "pos1": 1, "pos2": 6, "props": {"c": None, "b": 2},
+                                  "combiningOp": {"name": "rewrite"}}, msn=1),
+                 _msg("A", 5, 4, {"type": 1, "pos1": 0, "pos2": 2}, msn=3)])
+    path = tmp_path / "logs.json"
+    path.write_text(json.dumps(docs))
+    r = subprocess.run([NODE, str(ROOT / "tests" / "node_replay.js"), str(path)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    for msgs, g in zip(docs, got):
+        od = O.Doc()
+        od.start_collab("readonly")
+        for m in msgs:
+            if od.apply_msg(json.dumps(m)) != 0:
+                break
+        assert g["status"] == od.status
+        if od.status:
+            continue
+        assert g["text"] == od.text()
+        assert g["runs"] == json.loads(od.props_runs())
+        assert g["snapshot"] == od.snapshot_v1()
+        assert int(g["digest"]) == od.digest()
