@@ -97,8 +97,8 @@ struct Caps {
 // Capacity classes are compile-time: each class is its own kernel instantiation
 // (mt_kernels.hip), so every LDS array base is an immediate offset and no SGPRs hold
 // table pointers or bounds.
-constexpr int kClassSegs[] = {64, 128, 192, 256, 320, 384, 512, 768, 1024, 1536, 2048, 3072, 4096};
-constexpr int kNumClasses = 13;
+constexpr int kClassSegs[] = {64, 128, 192, 256, 320, 384, 512, 640, 768, 1024, 1280, 1664, 2048, 3072, 4096};
+constexpr int kNumClasses = 15;
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table

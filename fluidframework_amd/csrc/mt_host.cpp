@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -34,9 +35,11 @@ MT_DECLARE_CLASS(256)
 MT_DECLARE_CLASS(320)
 MT_DECLARE_CLASS(384)
 MT_DECLARE_CLASS(512)
+MT_DECLARE_CLASS(640)
 MT_DECLARE_CLASS(768)
 MT_DECLARE_CLASS(1024)
-MT_DECLARE_CLASS(1536)
+MT_DECLARE_CLASS(1280)
+MT_DECLARE_CLASS(1664)
 MT_DECLARE_CLASS(2048)
 MT_DECLARE_CLASS(3072)
 MT_DECLARE_CLASS(4096)
@@ -78,9 +81,11 @@ static const KernelClass kKernels[mt::kNumClasses] = {
     {320, (const void *)mt_replay_kernel_320, (const void *)mt_generate_kernel_320},
     {384, (const void *)mt_replay_kernel_384, (const void *)mt_generate_kernel_384},
     {512, (const void *)mt_replay_kernel_512, (const void *)mt_generate_kernel_512},
+    {640, (const void *)mt_replay_kernel_640, (const void *)mt_generate_kernel_640},
     {768, (const void *)mt_replay_kernel_768, (const void *)mt_generate_kernel_768},
     {1024, (const void *)mt_replay_kernel_1024, (const void *)mt_generate_kernel_1024},
-    {1536, (const void *)mt_replay_kernel_1536, (const void *)mt_generate_kernel_1536},
+    {1280, (const void *)mt_replay_kernel_1280, (const void *)mt_generate_kernel_1280},
+    {1664, (const void *)mt_replay_kernel_1664, (const void *)mt_generate_kernel_1664},
     {2048, (const void *)mt_replay_kernel_2048, (const void *)mt_generate_kernel_2048},
     {3072, (const void *)mt_replay_kernel_3072, (const void *)mt_generate_kernel_3072},
     {4096, (const void *)mt_replay_kernel_4096, (const void *)mt_generate_kernel_4096},
@@ -100,6 +105,7 @@ struct Launch {
     uint32_t *d_ck = nullptr;    // checkpoints of documents short of LDS headroom
     int32_t *d_cksrc = nullptr;  // resume: per workgroup index into the previous launch (-1 fresh)
     std::vector<int32_t> cksrc;
+    int src = -1;               // launch whose checkpoints / cold records cksrc indexes
     size_t lds = 0;
 };
 
@@ -582,10 +588,10 @@ static int class_for(const mt_batch *b, int32_t ops_per_doc, int level) {
 }
 static size_t class_lds(int c) { return mt::make_layout(mt::kClassSegs[c]).bytes; }
 static int max_lds_bytes();
-// the class a checkpointed document resumes in: at least 1.5x the slots
+// the class an escalated document continues in: at least 1.2x the slots
 static int resume_class(int c) {
     int n = c + 1;
-    while (n < mt::kNumClasses && 2 * mt::kClassSegs[n] < 3 * mt::kClassSegs[c]) n++;
+    while (n < mt::kNumClasses && 5 * mt::kClassSegs[n] < 6 * mt::kClassSegs[c]) n++;
     if (n >= mt::kNumClasses) n = mt::kNumClasses - 1;
     while (n > c + 1 && class_lds(n) > (size_t)max_lds_bytes()) n--;
     return n;
@@ -640,9 +646,9 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
     }
     // documents short of headroom checkpoint here unless this is the largest usable class
-    const bool can_grow = class_usable(L.cls + 1) && b->opt.max_retries > (int)b->launches.size() - 1;
+    const bool can_grow = class_usable(L.cls + 1) && b->opt.max_retries > 0;
     if (can_grow) HIPCHK(dalloc(&L.d_ck, (size_t)n * (size_t)mt::ck_words(L.caps.seg)));
-    const Launch *prev = b->launches.size() >= 2 ? &b->launches[b->launches.size() - 2] : nullptr;
+    const Launch *prev = L.src >= 0 ? &b->launches[(size_t)L.src] : nullptr;
     if (!L.cksrc.empty()) {
         HIPCHK(dalloc(&L.d_cksrc, L.cksrc.size()));
         HIPCHK(hipMemcpyAsync(L.d_cksrc, L.cksrc.data(), 4 * L.cksrc.size(), hipMemcpyHostToDevice, s));
@@ -735,38 +741,54 @@ MT_API int mt_batch_sync(mt_batch *b) {
     b->kernel_ms = ms;
     int rc = gather_launch(b, 0);
     if (rc) return rc;
-    // capacity escalation: checkpointed documents resume in a class with >= 1.5x the slots;
-    // documents whose tables overflowed mid-op re-run from scratch in the next class
-    for (int level = 1; level <= b->opt.max_retries; level++) {
-        const Launch &P0 = b->launches.back();
-        Launch L;
-        bool any_ck = false;
+    // capacity escalation: a checkpointed document resumes, a document that overflowed mid-op
+    // re-runs from scratch, both in the next class with >= 1.2x the slots (docs per CU matter
+    // more than the number of resumes: each resume costs one LDS image round trip to HBM).
+    // One launch per (source launch, target class).
+    std::vector<int> frontier{0};
+    for (int level = 1; level <= b->opt.max_retries && !frontier.empty(); level++) {
+        std::map<std::pair<int, int>, Launch> groups;
         for (int64_t d = 0; d < b->n_docs; d++) {
             const DocOut &o = b->docout[d];
-            if (o.status != MT_CAPACITY || b->where[d].launch != (int32_t)b->launches.size() - 1) continue;
-            if (o.cap_kind == mt::kCapCheckpoint && P0.d_ck) {
-                L.docs.push_back((int32_t)d);
-                L.cksrc.push_back(b->where[d].idx);
-                any_ck = true;
+            const int li = b->where[d].launch;
+            if (o.status != MT_CAPACITY || std::find(frontier.begin(), frontier.end(), li) == frontier.end()) continue;
+            const Launch &S = b->launches[(size_t)li];
+            int cls;
+            int32_t src;
+            if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) {
+                cls = resume_class(S.cls);
+                src = b->where[d].idx;
             } else if (o.cap_kind == 1 || o.cap_kind == 4) {
-                L.docs.push_back((int32_t)d);
-                L.cksrc.push_back(-1);
+                cls = resume_class(S.cls);
+                src = -1;
+            } else {
+                continue;
             }
+            while (cls > S.cls + 1 && !class_usable(cls)) cls--;
+            if (!class_usable(cls)) continue;  // largest class reached: the document keeps MT_CAPACITY
+            Launch &L = groups[{li, cls}];
+            L.cls = cls;
+            L.src = li;
+            L.docs.push_back((int32_t)d);
+            L.cksrc.push_back(src);
         }
-        if (L.docs.empty()) break;
-        L.cls = any_ck ? resume_class(P0.cls) : P0.cls + 1;
-        if (!class_usable(L.cls)) break;  // largest class reached
-        if (!any_ck) L.cksrc.clear();
-        b->launches.push_back(L);
-        HIPCHK(hipEventRecord(b->ev0, b->run_stream));
-        rc = launch_replay(b, b->run_stream, b->launches.back());
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(b->ev1, b->run_stream));
-        HIPCHK(hipEventSynchronize(b->ev1));
-        HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-        b->kernel_ms += ms;
-        rc = gather_launch(b, (int)b->launches.size() - 1);
-        if (rc) return rc;
+        frontier.clear();
+        for (auto &kv : groups) {
+            Launch L = std::move(kv.second);
+            if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) L.cksrc.clear();
+            b->launches.push_back(std::move(L));
+            const int li = (int)b->launches.size() - 1;
+            HIPCHK(hipEventRecord(b->ev0, b->run_stream));
+            rc = launch_replay(b, b->run_stream, b->launches.back());
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(b->ev1, b->run_stream));
+            HIPCHK(hipEventSynchronize(b->ev1));
+            HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+            b->kernel_ms += ms;
+            rc = gather_launch(b, li);
+            if (rc) return rc;
+            frontier.push_back(li);
+        }
     }
     b->total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count();
     b->ran = true;
