@@ -135,6 +135,7 @@ def main():
     alg_bytes = b.algorithmic_bytes()
     achieved_gbs = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
 
+    traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, f"mt_replay_kernel_{st['lds_class']}")
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
@@ -159,7 +160,8 @@ def main():
                        "op_mix": [cfg["pct_insert"], cfg["pct_remove"], 100 - cfg["pct_insert"] - cfg["pct_remove"]],
                        "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": None,
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": f"mt_replay_kernel_{st['lds_class']}", "avg_kernel_ms": round(avg_kernel_ms, 3),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
             "cpu_baseline": cpu,
@@ -178,6 +180,21 @@ def main():
     b.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(config, n_docs, n_ops, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes of this same configuration (tools/pmc_traffic.py; scripts/gpu_check.sh pmcf pmcw).
+    The counters cannot be read from inside this process, so the profile of the current kernel
+    build is committed under profiles/ and quoted here; None when no matching profile exists."""
+    path = ROOT / "profiles" / f"pmc_traffic_config{config}.json"
+    try:
+        prof = json.loads(path.read_text())
+    except (OSError, ValueError):
+        return None, None
+    if prof.get("docs") != n_docs or prof.get("ops") != n_ops or kernel not in prof.get("kernels", {}):
+        return None, None
+    return int(prof["kernels"][kernel]["traffic_bytes"]), str(path.relative_to(ROOT))
 
 
 def log(rank, msg):
