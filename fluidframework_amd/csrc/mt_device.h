@@ -97,8 +97,12 @@ struct Caps {
 // Capacity classes are compile-time: each class is its own kernel instantiation
 // (mt_kernels.hip), so every LDS array base is an immediate offset and no SGPRs hold
 // table pointers or bounds.
-constexpr int kClassSegs[] = {64, 128, 192, 256, 320, 384, 512, 640, 768, 1024, 1280, 1664, 2048, 3072, 4096};
-constexpr int kNumClasses = 15;
+// The last class keeps its tables in HBM instead of LDS (the spill path for documents beyond
+// the largest LDS class; slot and block ids stay 16-bit, so it tops out below 65,535 slots).
+constexpr int kClassSegs[] = {64, 128, 192, 256, 320, 384, 512, 640, 768, 1024, 1280, 1664, 2048, 3072, 4096, 60000};
+constexpr int kNumClasses = 16;
+constexpr int kHbmClass = kNumClasses - 1;
+constexpr int kHbmSeg = 60000;
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table
@@ -173,6 +177,7 @@ struct ReplayParams {
     const uint4 *cold_in;         // previous launch's cold records
     int64_t ck_in_words;          // stride of ck_in
     int32_t cold_in_seg;          // stride of cold_in
+    uint8_t *hbm_state;           // HBM class: per-workgroup table images (make_layout(kHbmSeg).bytes each)
 };
 constexpr int kProfSlots = 12;
 

@@ -473,7 +473,7 @@ struct Engine {
     // Bump allocation in the active text semispace; when it is full, live text moves to the
     // other semispace (text_gc) and the garbage left by reallocating merges is dropped.
     MT_FI uint32_t arena_alloc(uint32_t n) {
-        uint32_t n16 = (n + 15u) & ~15u;
+        const uint32_t n16 = (n + 1u) & ~1u;  // 4-byte granules
         if (arena_top + n16 > arena_end) {
             text_gc();
             if (arena_top + n16 > arena_end) {
@@ -509,8 +509,8 @@ struct Engine {
                 msk &= msk - 1;
                 const uint32_t sl = (uint32_t)(base + f);
                 const uint32_t len = s_len[sl];
-                uint32_t cap16 = (len + 15u) & ~15u;
-                if (cap16 == 0) cap16 = 16;
+                // packed tightly: short segments would otherwise waste most of a semispace
+                const uint32_t cap16 = (len + 1u) & ~1u;
                 if (top + cap16 > nb + semi_t) {
                     cap_fail(2);
                     return;
@@ -1105,9 +1105,9 @@ struct Engine {
                 } else if (pcap >= need) {
                     text_copy(ptoff + pl, stoff, sl);
                 } else if (ptoff >= arena_base && ptoff < arena_end && ptoff + pcap == arena_top &&
-                           ptoff + ((2u * need + 15u) & ~15u) <= arena_end) {
+                           ptoff + 2u * need <= arena_end) {
                     // last allocation of the arena: grow in place
-                    pcap = (2u * need + 15u) & ~15u;
+                    pcap = 2u * need;
                     arena_top = ptoff + pcap;
                     text_copy(ptoff + pl, stoff, sl);
                 } else {
@@ -1127,7 +1127,7 @@ struct Engine {
                     text_copy(dst, ptoff, pl);
                     text_copy(dst + pl, stoff, sl);
                     ptoff = dst;
-                    pcap = (ncap + 15u) & ~15u;
+                    pcap = (ncap + 1u) & ~1u;
                 }
                 pl = need;
                 const uint32_t fm = rdl(meta, k);
@@ -1816,12 +1816,24 @@ MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_
     E.init();
 }
 
+// Base of the document's tables: the workgroup's LDS, or for the HBM class its image in
+// global memory (same layout, same engine code; every table access becomes a global one).
+template <int SEG>
+MT_FI uint8_t *tables(const ReplayParams &P, int64_t w) {
+    if constexpr (SEG == kHbmSeg) {
+        return P.hbm_state + w * (int64_t)make_layout(SEG).bytes;
+    } else {
+        extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+        return smem;
+    }
+}
+
 template <int SEG>
 MT_FI void replay_body(const ReplayParams &P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
+    uint8_t *smem = tables<SEG>(P, w);
     Engine<SEG> E;
 #ifdef MT_PROF
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
@@ -1874,10 +1886,10 @@ MT_FI void replay_body(const ReplayParams &P) {
 // "Synthetic op logs"), writes the record + payload, then applies it as the observer.
 template <int SEG>
 MT_FI void generate_body(const ReplayParams &P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;  // re-generation of overflowed docs
+    uint8_t *smem = tables<SEG>(P, w);
     const mt_gen_params g = *(const mt_gen_params *)P.gen;
     Engine<SEG> E;
 #ifdef MT_PROF

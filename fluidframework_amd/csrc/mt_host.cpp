@@ -43,6 +43,7 @@ MT_DECLARE_CLASS(1664)
 MT_DECLARE_CLASS(2048)
 MT_DECLARE_CLASS(3072)
 MT_DECLARE_CLASS(4096)
+MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 
 using mt::Caps;
@@ -89,6 +90,7 @@ static const KernelClass kKernels[mt::kNumClasses] = {
     {2048, (const void *)mt_replay_kernel_2048, (const void *)mt_generate_kernel_2048},
     {3072, (const void *)mt_replay_kernel_3072, (const void *)mt_generate_kernel_3072},
     {4096, (const void *)mt_replay_kernel_4096, (const void *)mt_generate_kernel_4096},
+    {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000},
 };
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
 
@@ -104,6 +106,7 @@ struct Launch {
     uint4 *d_cold = nullptr;     // per-document cold segment records (class stride)
     uint32_t *d_ck = nullptr;    // checkpoints of documents short of LDS headroom
     int32_t *d_cksrc = nullptr;  // resume: per workgroup index into the previous launch (-1 fresh)
+    uint8_t *d_state = nullptr;  // HBM class: per-workgroup table images
     std::vector<int32_t> cksrc;
     int src = -1;               // launch whose checkpoints / cold records cksrc indexes
     size_t lds = 0;
@@ -337,6 +340,7 @@ static void free_launches(mt_batch *b) {
         (void)hipFree(L.d_cold);
         (void)hipFree(L.d_ck);
         (void)hipFree(L.d_cksrc);
+        (void)hipFree(L.d_state);
     }
     b->launches.clear();
 }
@@ -586,7 +590,9 @@ static int class_for(const mt_batch *b, int32_t ops_per_doc, int level) {
     c += level;
     return c < mt::kNumClasses ? c : mt::kNumClasses;  // kNumClasses: nothing larger
 }
-static size_t class_lds(int c) { return mt::make_layout(mt::kClassSegs[c]).bytes; }
+// dynamic LDS of a class's launch (the HBM class keeps its tables in global memory)
+static size_t class_lds(int c) { return c == mt::kHbmClass ? 0 : mt::make_layout(mt::kClassSegs[c]).bytes; }
+static size_t class_state_bytes(int c) { return c == mt::kHbmClass ? mt::make_layout(mt::kHbmSeg).bytes : 0; }
 static int max_lds_bytes();
 // the class an escalated document continues in: at least 1.2x the slots
 static int resume_class(int c) {
@@ -596,6 +602,7 @@ static int resume_class(int c) {
     while (n > c + 1 && class_lds(n) > (size_t)max_lds_bytes()) n--;
     return n;
 }
+constexpr size_t kMaxHbmDocs = 4096;  // documents per HBM-class launch (~6 MB of tables each)
 static bool class_usable(int c) { return c < mt::kNumClasses && class_lds(c) <= (size_t)max_lds_bytes(); }
 
 static int max_lds_bytes() {
@@ -641,6 +648,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
     HIPCHK(dalloc(&L.d_docout, (size_t)n));
     HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg));
+    if (class_state_bytes(L.cls)) HIPCHK(dalloc(&L.d_state, (size_t)n * class_state_bytes(L.cls)));
     if (!L.docs.empty()) {
         HIPCHK(dalloc(&L.d_list, L.docs.size()));
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
@@ -660,6 +668,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.doc_list = L.d_list;
     P.out_cap = L.out_cap;
     P.cold = L.d_cold;
+    P.hbm_state = L.d_state;
     P.ck_out = L.d_ck;
     if (!L.cksrc.empty() && prev) {
         P.ck_in = prev->d_ck;
@@ -766,6 +775,8 @@ MT_API int mt_batch_sync(mt_batch *b) {
             }
             while (cls > S.cls + 1 && !class_usable(cls)) cls--;
             if (!class_usable(cls)) continue;  // largest class reached: the document keeps MT_CAPACITY
+            if (cls == mt::kHbmClass && (groups.count({li, cls}) ? groups[{li, cls}].docs.size() : 0) >= kMaxHbmDocs)
+                continue;  // the HBM class holds ~6 MB per document: bounded
             Launch &L = groups[{li, cls}];
             L.cls = cls;
             L.src = li;
@@ -1388,6 +1399,7 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
         HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
         HIPCHK(dalloc(&L.d_docout, (size_t)n));
         HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg));
+        if (class_state_bytes(cls)) HIPCHK(dalloc(&L.d_state, (size_t)n * class_state_bytes(cls)));
         if (!todo.empty()) {
             HIPCHK(dalloc(&L.d_list, todo.size()));
             HIPCHK(hipMemcpy(L.d_list, todo.data(), 4 * todo.size(), hipMemcpyHostToDevice));
@@ -1403,6 +1415,7 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
         P.gen_ops = b->d_ops;
         P.gen_props = b->d_props;
         P.cold = L.d_cold;
+        P.hbm_state = L.d_state;
         const void *fn = kKernels[cls].generate;
         if (L.lds > 64 * 1024)
             HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
@@ -1415,6 +1428,7 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
         (void)hipFree(L.d_docout);
         (void)hipFree(L.d_list);
         (void)hipFree(L.d_cold);
+        (void)hipFree(L.d_state);
         std::vector<int32_t> again;
         for (int64_t i = 0; i < n; i++) {
             const int64_t d = todo.empty() ? i : todo[(size_t)i];

@@ -215,3 +215,25 @@ def test_device_digests_are_placement_independent():
     assert (da[6:] == db).all()
     assert (da == dc).all()
     assert len(set(da.tolist())) == 12
+
+
+def test_hbm_class_spills_documents_beyond_lds():
+    """A document that outgrows the largest LDS class (4,096 slots) is checkpointed and resumed
+    in the HBM class (tables in global memory, same engine code) and stays bit-exact."""
+    p = O.gen_params(12000, pct_insert=50, pct_remove=15, seed=2024)  # 35% annotate: props keep segments apart
+    n = 1
+    ops, text, props, off = O.gen_batch(p, n)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(n) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        b.set_clients(names)
+        b.ingest(ops, off, text, props)
+        b.run()
+        c = b.counters()
+        assert (c["max_slots"] > 4096).any(), c["max_slots"]
+        for d in range(n):
+            assert b.doc(d).status == st[d] == 0, {k: int(c[k][d]) for k in c.dtype.names}
+            assert b.doc(d).digest() == int(dig[d])
+        od = O.replay_doc(ops[off[0]:off[1]].copy(), text, props, t, names)
+        assert b.doc(0).snapshot_v1() == od.snapshot_v1()
