@@ -196,4 +196,34 @@ struct DigestParams {
 };
 
 
+// mt_snapshot.hip: SnapshotV1 (extractSync + emit) of one launch's documents on the GPU
+constexpr int kSnapMaxChunks = 32;  // blobs per document (320k code units at chunk_size 10000)
+constexpr int kSnapMeta = 1 + 3 * kSnapMaxChunks;  // per doc: n_chunks, then (count, length, bytes) per chunk
+struct SnapParams {
+    const OutRec *out;
+    const DocOut *doc_out;
+    const int32_t *doc_list;
+    int64_t n;
+    int32_t out_cap;
+    const uint16_t *text;
+    const uint64_t *doc_text_base;
+    const uint32_t *pool;
+    const uint64_t *doc_pool_base;
+    const uint8_t *strs;        // UTF-8 bytes of the string tables below
+    const uint32_t *key_str;    // per key: (offset, length) of JSON.stringify(key)
+    const uint32_t *key_rank;   // per key: its array index, 0xFFFFFFFF for an ordinary key
+    const uint32_t *val_str;    // per value: (offset, length) of its JSON text
+    const uint32_t *cli_str;    // client table entries: (offset, length) of JSON.stringify(long id)
+    const int32_t *doc_cli;     // per document: (first entry, count) in cli_str; null: the shared table
+    int32_t cli_first, cli_n;   // the shared client table (entry 0 of cli_str is "undefined")
+    const uint8_t *final_mask;  // per workgroup: 1 when this launch holds the document's final table
+    int32_t n_keys, n_values;   // key_str has n_keys + 1 entries (the last is "?")
+    int32_t chunk_size;
+    int32_t pass;               // 0: sizes into meta / bytes, 1: write into dst
+    int32_t *meta;              // [n_docs * kSnapMeta]
+    int64_t *bytes;             // [n_docs] total bytes of the document's blobs (-1: not on the GPU)
+    uint8_t *dst;
+    const int64_t *dst_off;     // [n_docs]
+};
+
 }  // namespace mt

@@ -45,6 +45,7 @@ MT_DECLARE_CLASS(3072)
 MT_DECLARE_CLASS(4096)
 MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
+extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
 
 using mt::Caps;
 using mt::DocOut;
@@ -329,7 +330,24 @@ struct mt_batch {
     DocOut c_out{};
     std::vector<std::string> c_blob_names, c_blobs;
     int64_t c_blob_doc = -1;
+    // GPU SnapshotV1 of every document (mt_batch_snapshots)
+    bool snap_ready = false;
+    int32_t *d_snap_meta = nullptr;
+    int64_t *d_snap_bytes = nullptr, *d_snap_off = nullptr;
+    uint8_t *d_snap = nullptr;
+    std::vector<int64_t> h_snap_bytes, h_snap_off;
 };
+
+static void free_snap(mt_batch *b) {
+    (void)hipFree(b->d_snap_meta);
+    (void)hipFree(b->d_snap_bytes);
+    (void)hipFree(b->d_snap_off);
+    (void)hipFree(b->d_snap);
+    b->d_snap_meta = nullptr;
+    b->d_snap_bytes = b->d_snap_off = nullptr;
+    b->d_snap = nullptr;
+    b->snap_ready = false;
+}
 
 static void free_launches(mt_batch *b) {
     for (auto &L : b->launches) {
@@ -414,6 +432,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
 MT_API void mt_batch_destroy(mt_batch *b) {
     if (!b) return;
     free_launches(b);
+    free_snap(b);
     (void)hipFree(b->d_digest);
     free_log(b);
     (void)hipFree(b->d_vflags);
@@ -692,6 +711,7 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
     if (!b || !b->have_log) return MT_ERR_STATE;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->stream;
     free_launches(b);
+    free_snap(b);
     b->ran = false;
     b->cached_doc = -1;
     b->c_blob_doc = -1;
@@ -886,6 +906,7 @@ MT_API int mt_batch_doc_counters(mt_batch *b, int32_t *out) {
     if (!b || !out) return MT_ERR_ARG;
     if (!b->ran) return MT_ERR_STATE;
     static_assert(sizeof(DocOut) == 4 * MT_DOC_COUNTERS, "DocOut layout");
+    static_assert(MT_SNAP_META == mt::kSnapMeta, "snapshot meta row");
     for (int64_t d = 0; d < b->n_docs; d++) {
         int32_t *o = out + d * MT_DOC_COUNTERS;
         memcpy(o, &b->docout[(size_t)d], sizeof(DocOut));
@@ -1169,6 +1190,218 @@ MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name,
     if (i < 0 || i >= (int32_t)b->c_blobs.size()) return MT_ERR_ARG;
     if (name && name_cap > 0) snprintf(name, (size_t)name_cap, "%s", b->c_blob_names[i].c_str());
     return out_str(b->c_blobs[i], buf, cap, len);
+}
+
+// ---------------------------------------------------------------- SnapshotV1 on the GPU
+// mt_snapshot.hip: pass 0 sizes every document's chunks, the host prefix-sums the bytes, pass 1
+// writes all blobs into one device buffer.  Same bytes as mt_doc_snapshot_v1 above.
+MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_ms) {
+    if (!b) return MT_ERR_ARG;
+    if (!b->ran) return MT_ERR_STATE;
+    free_snap(b);
+    hipStream_t s = b->run_stream ? b->run_stream : b->stream;
+    // string tables: JSON.stringify(key), value JSON texts, JSON.stringify(long client id)
+    std::string strs;
+    std::vector<uint32_t> key_str, key_rank, val_str, cli_str;
+    auto add = [&](std::vector<uint32_t> &tab, const std::string &js) {
+        tab.push_back((uint32_t)strs.size());
+        tab.push_back((uint32_t)js.size());
+        strs += js;
+    };
+    auto add_quoted = [&](std::vector<uint32_t> &tab, const std::string &raw) {
+        std::string q;
+        json_quote8(q, raw);
+        add(tab, q);
+    };
+    for (size_t k = 0; k < b->keys.size(); k++) {
+        add_quoted(key_str, b->keys[k]);
+        key_rank.push_back(b->key_is_index[k] ? b->key_index[k] : 0xFFFFFFFFu);
+    }
+    add_quoted(key_str, "?");
+    key_rank.push_back(0xFFFFFFFFu);
+    for (const std::string &v : b->values) add(val_str, v);
+    add_quoted(cli_str, "undefined");
+    const int32_t cli_first = 1, cli_n = (int32_t)b->clients.size();
+    for (const std::string &c : b->clients) add_quoted(cli_str, c);
+    std::vector<int32_t> doc_cli;
+    if (!b->doc_clients.empty()) {
+        doc_cli.resize(2 * (size_t)b->n_docs);
+        for (int64_t d = 0; d < b->n_docs; d++) {
+            auto it = b->doc_clients.find(d);
+            if (it == b->doc_clients.end()) {
+                doc_cli[2 * d] = cli_first;
+                doc_cli[2 * d + 1] = cli_n;
+            } else {
+                doc_cli[2 * d] = (int32_t)(cli_str.size() / 2);
+                doc_cli[2 * d + 1] = (int32_t)it->second.size();
+                for (const std::string &c : it->second) add_quoted(cli_str, c);
+            }
+        }
+    }
+    if (strs.empty()) strs.push_back(0);
+    uint8_t *d_strs = nullptr;
+    uint32_t *d_key_str = nullptr, *d_key_rank = nullptr, *d_val_str = nullptr, *d_cli_str = nullptr;
+    int32_t *d_doc_cli = nullptr;
+    std::vector<uint8_t *> d_final(b->launches.size(), nullptr);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = MT_OK;
+    auto fail = [&](int code) {
+        rc = code;
+        return code;
+    };
+    auto up = [&](auto **dp, const auto &v) -> bool {
+        if (dalloc(dp, v.size()) != hipSuccess) return false;
+        return hipMemcpyAsync(*dp, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+    };
+    do {
+        if (!up(&d_strs, strs) || !up(&d_key_str, key_str) || !up(&d_key_rank, key_rank) || !up(&d_val_str, val_str) ||
+            !up(&d_cli_str, cli_str) || (!doc_cli.empty() && !up(&d_doc_cli, doc_cli))) {
+            fail(MT_ERR_HIP);
+            break;
+        }
+        if (dalloc(&b->d_snap_meta, (size_t)b->n_docs * mt::kSnapMeta) != hipSuccess ||
+            dalloc(&b->d_snap_bytes, (size_t)b->n_docs) != hipSuccess ||
+            hipMemsetAsync(b->d_snap_bytes, 0xFF, 8 * (size_t)b->n_docs, s) != hipSuccess) {
+            fail(MT_ERR_HIP);
+            break;
+        }
+        for (size_t li = 0; li < b->launches.size() && !rc; li++) {
+            const Launch &L = b->launches[li];
+            const int64_t n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+            std::vector<uint8_t> fm((size_t)n);
+            for (int64_t i = 0; i < n; i++) fm[i] = b->where[L.docs.empty() ? i : L.docs[i]].launch == (int32_t)li;
+            if (!up(&d_final[li], fm)) fail(MT_ERR_HIP);
+        }
+        if (rc) break;
+        if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
+            hipEventRecord(e0, s) != hipSuccess) {
+            fail(MT_ERR_HIP);
+            break;
+        }
+        for (int pass = 0; pass < 2 && !rc; pass++) {
+            if (pass == 1) {
+                // per-document offsets of the blobs
+                b->h_snap_bytes.resize((size_t)b->n_docs);
+                if (hipMemcpyAsync(b->h_snap_bytes.data(), b->d_snap_bytes, 8 * (size_t)b->n_docs,
+                                   hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess) {
+                    fail(MT_ERR_HIP);
+                    break;
+                }
+                b->h_snap_off.assign((size_t)b->n_docs + 1, 0);
+                for (int64_t d = 0; d < b->n_docs; d++)
+                    b->h_snap_off[d + 1] = b->h_snap_off[d] + std::max<int64_t>(0, b->h_snap_bytes[d]);
+                if (dalloc(&b->d_snap, (size_t)std::max<int64_t>(1, b->h_snap_off.back())) != hipSuccess ||
+                    !up(&b->d_snap_off, b->h_snap_off)) {
+                    fail(MT_ERR_HIP);
+                    break;
+                }
+            }
+            for (size_t li = 0; li < b->launches.size(); li++) {
+                const Launch &L = b->launches[li];
+                mt::SnapParams P{};
+                P.out = L.d_out;
+                P.doc_out = L.d_docout;
+                P.doc_list = L.d_list;
+                P.n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+                P.out_cap = L.out_cap;
+                P.text = b->d_text;
+                P.doc_text_base = b->d_text_base;
+                P.pool = b->d_pool;
+                P.doc_pool_base = b->d_pool_base;
+                P.strs = d_strs;
+                P.key_str = d_key_str;
+                P.key_rank = d_key_rank;
+                P.val_str = d_val_str;
+                P.cli_str = d_cli_str;
+                P.doc_cli = d_doc_cli;
+                P.cli_first = cli_first;
+                P.cli_n = cli_n;
+                P.final_mask = d_final[li];
+                P.n_keys = (int32_t)b->keys.size();
+                P.n_values = (int32_t)b->values.size();
+                P.chunk_size = b->opt.chunk_size;
+                P.pass = pass;
+                P.meta = b->d_snap_meta;
+                P.bytes = b->d_snap_bytes;
+                P.dst = b->d_snap;
+                P.dst_off = b->d_snap_off;
+                void *args[] = {&P};
+                if (hipLaunchKernel((const void *)mt_snapshot_kernel, dim3((unsigned)P.n), dim3(64), args, 0, s) !=
+                    hipSuccess) {
+                    fail(MT_ERR_HIP);
+                    break;
+                }
+            }
+        }
+        if (rc) break;
+        float ms = 0;
+        if (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+            hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+            fail(MT_ERR_HIP);
+            break;
+        }
+        if (device_ms) *device_ms = ms;
+        if (total_bytes) *total_bytes = b->h_snap_off.back();
+        b->snap_ready = true;
+    } while (0);
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(d_strs);
+    (void)hipFree(d_key_str);
+    (void)hipFree(d_key_rank);
+    (void)hipFree(d_val_str);
+    (void)hipFree(d_cli_str);
+    (void)hipFree(d_doc_cli);
+    for (uint8_t *p : d_final) (void)hipFree(p);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (rc) free_snap(b);
+    return rc;
+}
+
+MT_API int mt_doc_snapshot_v1_device(mt_batch *b, int64_t doc, int32_t *n_blobs) {
+    if (!b) return MT_ERR_ARG;
+    if (!b->snap_ready) return MT_ERR_STATE;
+    if (doc < 0 || doc >= b->n_docs) return MT_ERR_ARG;
+    // documents beyond MT_SNAP_MAX_BLOBS blobs are serialized by the host path above
+    if (b->h_snap_bytes[doc] < 0) return mt_doc_snapshot_v1(b, doc, n_blobs);
+    int32_t meta[mt::kSnapMeta];
+    HIPCHK(hipMemcpy(meta, b->d_snap_meta + doc * (int64_t)mt::kSnapMeta, sizeof meta, hipMemcpyDeviceToHost));
+    std::string all((size_t)b->h_snap_bytes[doc], '\0');
+    if (!all.empty())
+        HIPCHK(hipMemcpy(&all[0], b->d_snap + b->h_snap_off[doc], all.size(), hipMemcpyDeviceToHost));
+    b->c_blob_names.clear();
+    b->c_blobs.clear();
+    size_t at = 0;
+    for (int32_t c = 0; c < meta[0]; c++) {
+        const size_t n = (size_t)meta[3 + 3 * c];
+        if (at + n > all.size()) return MT_INTERNAL;
+        b->c_blob_names.push_back(c == 0 ? std::string("header") : "body_" + std::to_string(c - 1));
+        b->c_blobs.push_back(all.substr(at, n));
+        at += n;
+    }
+    if (at != all.size()) return MT_INTERNAL;
+    b->c_blob_doc = doc;
+    if (n_blobs) *n_blobs = meta[0];
+    return MT_OK;
+}
+
+MT_API int mt_batch_snapshot_index(mt_batch *b, int64_t *doc_off, int32_t *blob_meta) {
+    if (!b) return MT_ERR_ARG;
+    if (!b->snap_ready) return MT_ERR_STATE;
+    if (doc_off) memcpy(doc_off, b->h_snap_off.data(), 8 * b->h_snap_off.size());
+    if (blob_meta)
+        HIPCHK(hipMemcpy(blob_meta, b->d_snap_meta, 4 * (size_t)b->n_docs * mt::kSnapMeta, hipMemcpyDeviceToHost));
+    return MT_OK;
+}
+
+MT_API int mt_batch_snapshot_copy(mt_batch *b, void *dst, int32_t dst_is_device) {
+    if (!b || !dst) return MT_ERR_ARG;
+    if (!b->snap_ready) return MT_ERR_STATE;
+    if (b->h_snap_off.back())
+        HIPCHK(hipMemcpy(dst, b->d_snap, (size_t)b->h_snap_off.back(),
+                         dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+    return MT_OK;
 }
 
 MT_API int mt_doc_shape(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len) {

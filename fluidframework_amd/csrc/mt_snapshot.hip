@@ -1,0 +1,558 @@
+// mt_snapshot.hip — SnapshotV1 serialization of final segment tables on the GPU.
+//
+// Reference: SnapshotV1.extractSync + emit (packages/dds/merge-tree/src/snapshotV1.ts:85-247)
+// with the chunk format of snapshotChunks.ts:122-131 and segment.toJSONObject()
+// (textSegment.ts:48-54, mergeTree.ts:652-656).  Output is byte-identical to the host
+// serializer mt_doc_snapshot_v1 (mt_host.cpp), which the parity tests compare it against.
+//
+// One wavefront per document walks the document's mt::OutRec records in order:
+//   * records removed at or below minSeq are dropped (snapshotV1.ts:178-186);
+//   * records at or below minSeq that are not removed coalesce into runs — text after text,
+//     the run not ending in '\n', either side <= TextSegmentGranularity, equal properties
+//     (snapshotV1.ts:191-210: canAppend + matchProperties);
+//   * everything else is written standalone with seq / client / removedSeq / removedClient.
+// Segments close a chunk once its length reaches chunk_size (snapshotV1.ts:132-160), so chunk
+// boundaries are known on the fly.  Two launches per batch: pass 0 sizes every chunk (count,
+// length, bytes) into P.meta; the host prefix-sums the per-document bytes; pass 1 writes the
+// blobs back to back at P.dst + P.dst_off[doc] (header blob first, then body_0 ..).
+//
+// JSON strings are escaped lane-parallel, 64 UTF-16 code units per step: per-unit byte counts
+// (JSON.stringify escapes, UTF-8 widths, surrogate pairs -> 4 bytes, lone surrogates -> \udxxx),
+// a wave exclusive scan for offsets, then every lane stores its bytes.  A high surrogate at
+// the end of a record is carried into the next record of the same run, so pairs split across
+// coalesced records join exactly as in the reference's concatenated string.
+#include <hip/hip_runtime.h>
+
+#include "mt_device.h"
+
+namespace mt {
+namespace {
+
+constexpr uint32_t kNoRank = 0xFFFFFFFFu;
+
+__device__ __constant__ uint64_t kPow10[20] = {1ull,
+                                               10ull,
+                                               100ull,
+                                               1000ull,
+                                               10000ull,
+                                               100000ull,
+                                               1000000ull,
+                                               10000000ull,
+                                               100000000ull,
+                                               1000000000ull,
+                                               10000000000ull,
+                                               100000000000ull,
+                                               1000000000000ull,
+                                               10000000000000ull,
+                                               100000000000000ull,
+                                               1000000000000000ull,
+                                               10000000000000000ull,
+                                               100000000000000000ull,
+                                               1000000000000000000ull,
+                                               10000000000000000000ull};
+
+__device__ __forceinline__ uint32_t lane() { return threadIdx.x; }
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane() >= (uint32_t)d) x += y;
+    }
+    *total = rl(x, 63);
+    return x - v;
+}
+
+__device__ __forceinline__ bool is_hi(uint32_t c) { return c >= 0xD800u && c <= 0xDBFFu; }
+__device__ __forceinline__ bool is_lo(uint32_t c) { return c >= 0xDC00u && c <= 0xDFFFu; }
+
+// Uniform writer: every lane tracks `pos`; kWrite=false only counts bytes.
+template <bool kWrite>
+struct Writer {
+    uint8_t *dst;
+    int64_t pos;
+
+    __device__ __forceinline__ void byte(uint32_t c) {
+        if (kWrite && lane() == 0) dst[pos] = (uint8_t)c;
+        pos++;
+    }
+    template <int N>
+    __device__ __forceinline__ void lit(const char (&s)[N]) {
+        static_assert(N - 1 <= 64, "literal longer than a wave");
+        if (kWrite && lane() < (uint32_t)(N - 1)) dst[pos + lane()] = (uint8_t)s[lane()];
+        pos += N - 1;
+    }
+    __device__ __forceinline__ void copy(const uint8_t *src, uint32_t n) {
+        if (kWrite)
+            for (uint32_t i = lane(); i < n; i += 64) dst[pos + i] = src[i];
+        pos += n;
+    }
+    // std::to_string of a signed 64-bit value
+    __device__ __forceinline__ void num(int64_t v) {
+        if (v < 0) {
+            byte('-');
+            v = -v;
+        }
+        const uint64_t u = (uint64_t)v;
+        int nd = 1;
+        while (nd < 20 && u >= kPow10[nd]) nd++;
+        if (kWrite && lane() < (uint32_t)nd) dst[pos + lane()] = (uint8_t)('0' + (u / kPow10[nd - 1 - lane()]) % 10);
+        pos += nd;
+    }
+    // JSON string body of the virtual array v[0..m): v[0] = carry (when has_carry) followed by
+    // t[0..n).  Unless `last`, a trailing high surrogate is held back in *carry_out.
+    __device__ void text(const uint16_t *t, uint32_t n, int32_t carry, bool last, int32_t *carry_out) {
+        const uint32_t hc = carry >= 0 ? 1u : 0u, m = n + hc;
+        uint32_t me = m;
+        *carry_out = -1;
+        if (!last && m > 0) {
+            const uint32_t c = (m - 1 >= hc) ? t[m - 1 - hc] : (uint32_t)carry;
+            if (is_hi(c)) {
+                me = m - 1;
+                *carry_out = (int32_t)c;
+            }
+        }
+        for (uint32_t base = 0; base < me; base += 64) {
+            const uint32_t k = base + lane();
+            auto at = [&](uint32_t i) -> uint32_t { return i < hc ? (uint32_t)carry : (uint32_t)t[i - hc]; };
+            uint32_t c = 0, p = 0, nx = 0, nb = 0;
+            if (k < me) {
+                c = at(k);
+                p = k > 0 ? at(k - 1) : 0u;
+                nx = k + 1 < m ? at(k + 1) : 0u;
+                if (c == 0x22 || c == 0x5C || c == 0x08 || c == 0x0C || c == 0x0A || c == 0x0D || c == 0x09) nb = 2;
+                else if (c < 0x20) nb = 6;
+                else if (is_hi(c)) nb = is_lo(nx) ? 4 : 6;
+                else if (is_lo(c)) nb = is_hi(p) ? 0 : 6;
+                else nb = c < 0x80 ? 1 : c < 0x800 ? 2 : 3;
+            }
+            uint32_t tot;
+            const uint32_t off = wave_excl_scan(nb, &tot);
+            if (kWrite && nb) {
+                uint8_t *o = dst + pos + off;
+                const char *hex = "0123456789abcdef";
+                if (nb == 2 && c < 0x80) {
+                    o[0] = '\\';
+                    o[1] = c == 0x22 ? '"' : c == 0x5C ? '\\' : c == 0x08 ? 'b' : c == 0x0C ? 'f' : c == 0x0A ? 'n'
+                                                                                    : c == 0x0D ? 'r' : 't';
+                } else if (nb == 6) {
+                    o[0] = '\\';
+                    o[1] = 'u';
+                    o[2] = hex[(c >> 12) & 15];
+                    o[3] = hex[(c >> 8) & 15];
+                    o[4] = hex[(c >> 4) & 15];
+                    o[5] = hex[c & 15];
+                } else if (nb == 4) {
+                    const uint32_t cp = 0x10000u + ((c - 0xD800u) << 10) + (nx - 0xDC00u);
+                    o[0] = (uint8_t)(0xF0 | (cp >> 18));
+                    o[1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+                    o[2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+                    o[3] = (uint8_t)(0x80 | (cp & 0x3F));
+                } else if (nb == 1) {
+                    o[0] = (uint8_t)c;
+                } else if (nb == 2) {
+                    o[0] = (uint8_t)(0xC0 | (c >> 6));
+                    o[1] = (uint8_t)(0x80 | (c & 0x3F));
+                } else {
+                    o[0] = (uint8_t)(0xE0 | (c >> 12));
+                    o[1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+                    o[2] = (uint8_t)(0x80 | (c & 0x3F));
+                }
+            }
+            pos += tot;
+        }
+    }
+};
+
+struct Rec {  // one OutRec, wave-uniform
+    uint32_t len, meta, props, toff, blk;
+    int32_t seq, rseq;
+    uint32_t lastc;  // last code unit of a text record with len > 0
+};
+
+// lane l of the tile holds record base + l
+struct Tile {
+    uint32_t len, meta, props, toff, blk, lastc;
+    int32_t seq, rseq;
+    __device__ __forceinline__ void load(const OutRec *rec, int32_t i, int32_t n, const uint16_t *text) {
+        if (i < n) {
+            const uint4 a = reinterpret_cast<const uint4 *>(rec + i)[0];
+            const uint4 b = reinterpret_cast<const uint4 *>(rec + i)[1];
+            len = a.x;
+            seq = (int32_t)a.y;
+            rseq = (int32_t)a.z;
+            meta = a.w;
+            props = b.y;
+            toff = b.z;
+            blk = b.w;
+            const bool txt = (blk & 0xFFFFu) != kMarkerSlot && !(meta & kMetaMarker) && len > 0;
+            lastc = txt ? text[toff + len - 1] : 0u;
+        } else {
+            len = meta = props = toff = lastc = 0;
+            blk = kMarkerSlot;
+            seq = rseq = 0;
+        }
+    }
+    __device__ __forceinline__ Rec get(uint32_t l) const {
+        Rec r;
+        r.len = rl(len, l);
+        r.meta = rl(meta, l);
+        r.props = rl(props, l);
+        r.toff = rl(toff, l);
+        r.blk = rl(blk, l);
+        r.seq = (int32_t)rl((uint32_t)seq, l);
+        r.rseq = (int32_t)rl((uint32_t)rseq, l);
+        r.lastc = rl(lastc, l);
+        return r;
+    }
+};
+
+template <bool kWrite>
+struct Doc {
+    const SnapParams &P;
+    const OutRec *rec;
+    const uint16_t *text;
+    const uint32_t *pool;
+    int32_t n_out, min_seq, cur_seq;
+    int32_t cli_first, cli_n;
+    Writer<kWrite> W;
+    int32_t *mrow;
+    // chunking
+    int32_t nch = 0;       // chunks closed
+    bool open = false;
+    int64_t ccount = 0, clen = 0, total_count = 0, total_len = 0;
+    int64_t seg_bytes_at_open = 0;
+    bool overflow = false;
+    int64_t all_len = 0, all_count = 0;  // pass 1: the document's totals from pass 0
+    // coalescing run (snapshotV1.ts:191-210)
+    bool have_prev = false, run_text = false, run_ends_nl = false;
+    int32_t run_first = 0, run_last = 0;
+    int64_t run_len = 0;
+    uint32_t run_props = 0, run_ref = 0;
+
+    __device__ Doc(const SnapParams &p, const OutRec *r, const uint16_t *t, const uint32_t *pl, const DocOut &o,
+                   int32_t cf, int32_t cn, uint8_t *dst, int32_t *mr)
+        : P(p), rec(r), text(t), pool(pl), n_out(o.n_out), min_seq(o.min_seq), cur_seq(o.cur_seq), cli_first(cf),
+          cli_n(cn), W{dst, 0}, mrow(mr) {}
+
+    __device__ __forceinline__ static bool skipped(const Rec &r, int32_t min_seq) {
+        if ((r.blk & 0xFFFFu) == kMarkerSlot) return true;
+        return r.rseq != kNoneSeq && r.rseq <= min_seq;
+    }
+
+    __device__ void str(const uint32_t *tab, uint32_t i) { W.copy(P.strs + tab[2 * i], tab[2 * i + 1]); }
+    __device__ void client(uint32_t id) {
+        if (id < (uint32_t)cli_n) str(P.cli_str, (uint32_t)cli_first + id);
+        else str(P.cli_str, 0);  // "undefined"
+    }
+    __device__ __forceinline__ uint32_t key_rank(uint32_t k) const {
+        return k < (uint32_t)P.n_keys ? P.key_rank[k] : kNoRank;
+    }
+    __device__ void prop_entry(uint32_t id, uint32_t i, bool &first) {
+        const uint32_t k = pool[id + 2 + 2 * i], v = pool[id + 3 + 2 * i];
+        if (!first) W.byte(',');
+        first = false;
+        str(P.key_str, k < (uint32_t)P.n_keys ? k : (uint32_t)P.n_keys);
+        W.byte(':');
+        str(P.val_str, v < (uint32_t)P.n_values ? v : 0u);
+    }
+    // JSON.stringify(properties): array-index keys ascending, then insertion order
+    __device__ void props_json(uint32_t id) {
+        const uint32_t n = pool[id];
+        W.byte('{');
+        bool first = true;
+        bool any_index = false;
+        for (uint32_t base = 0; base < n; base += 64) {
+            const uint32_t i = base + lane();
+            const bool ix = i < n && key_rank(pool[id + 2 + 2 * i]) != kNoRank;
+            any_index |= __ballot(ix) != 0;
+        }
+        if (any_index) {
+            int64_t last = -1;
+            for (;;) {
+                uint32_t best = kNoRank, best_i = 0;
+                for (uint32_t base = 0; base < n; base += 64) {
+                    const uint32_t i = base + lane();
+                    uint32_t r = i < n ? key_rank(pool[id + 2 + 2 * i]) : kNoRank;
+                    if ((int64_t)r <= last) r = kNoRank;
+                    uint32_t m = r;
+                    for (int off = 32; off > 0; off >>= 1) m = min(m, (uint32_t)__shfl_xor(m, off, 64));
+                    if (m < best) {
+                        best = m;
+                        best_i = base + (uint32_t)__builtin_ctzll(__ballot(r == m));
+                    }
+                }
+                if (best == kNoRank) break;
+                prop_entry(id, best_i, first);
+                last = best;
+            }
+        }
+        for (uint32_t i = 0; i < n; i++)
+            if (key_rank(pool[id + 2 + 2 * i]) == kNoRank) prop_entry(id, i, first);
+        W.byte('}');
+    }
+    // matchProperties over the pool's (key, value) lists
+    __device__ bool props_match(uint32_t a, uint32_t c) {
+        if (a == c) return true;
+        if (!a || !c) return false;
+        const uint32_t na = pool[a], nc = pool[c];
+        if (na != nc) return false;
+        for (uint32_t base = 0; base < na; base += 64) {
+            const uint32_t i = base + lane();
+            bool found = i >= na;
+            const uint32_t ka = found ? 0u : pool[a + 2 + 2 * i], va = found ? 0u : pool[a + 3 + 2 * i];
+            for (uint32_t j = 0; j < nc; j++) found |= ka == pool[c + 2 + 2 * j] && va == pool[c + 3 + 2 * j];
+            if (__ballot(!found)) return false;
+        }
+        return true;
+    }
+
+    // ---- chunks
+    template <class Wr>
+    __device__ void header(Wr &w, int64_t count, int64_t length) {
+        w.lit("{\"version\":\"1\",\"segmentCount\":");
+        w.num(count);
+        w.lit(",\"length\":");
+        w.num(length);
+        w.lit(",\"segments\":[");
+    }
+    template <class Wr>
+    __device__ void trailer(Wr &w, int32_t c, int64_t start, int32_t n_chunks, int64_t tlen,
+                            int64_t tcount) {
+        w.lit("],\"startIndex\":");
+        w.num(start);
+        if (c == 0) {
+            w.lit(",\"headerMetadata\":{\"minSequenceNumber\":");
+            w.num(min_seq);
+            w.lit(",\"sequenceNumber\":");
+            w.num(cur_seq);
+            w.lit(",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+            for (int32_t bi = 1; bi < n_chunks; bi++) {
+                w.lit(",{\"id\":\"body_");
+                w.num(bi - 1);
+                w.lit("\"}");
+            }
+            w.lit("],\"totalLength\":");
+            w.num(tlen);
+            w.lit(",\"totalSegmentCount\":");
+            w.num(tcount);
+            w.byte('}');
+        }
+        w.byte('}');
+    }
+    __device__ void open_chunk() {
+        open = true;
+        ccount = clen = 0;
+        if (kWrite) header(W, mrow[1 + 3 * nch], mrow[2 + 3 * nch]);
+        seg_bytes_at_open = W.pos;
+    }
+    __device__ void close_chunk() {
+        if (nch >= kSnapMaxChunks) {
+            overflow = true;
+        } else if (kWrite) {
+            trailer(W, nch, total_count, mrow[0], all_len, all_count);
+        } else if (lane() == 0) {
+            mrow[1 + 3 * nch] = (int32_t)ccount;
+            mrow[2 + 3 * nch] = (int32_t)clen;
+            mrow[3 + 3 * nch] = (int32_t)(W.pos - seg_bytes_at_open);  // segments + commas; framing added at the end
+        }
+        total_count += ccount;
+        total_len += clen;
+        nch++;
+        open = false;
+    }
+    __device__ void begin_seg() {
+        if (!open) open_chunk();
+        else W.byte(',');
+    }
+    __device__ void end_seg(int64_t len) {
+        ccount++;
+        clen += len;
+        if (clen >= P.chunk_size) close_chunk();
+    }
+
+    // ---- segments
+    __device__ void text_run() {
+        W.byte('"');
+        int32_t carry = -1;
+        Tile T;
+        for (int32_t base = run_first & ~63; base <= run_last; base += 64) {
+            T.load(rec, base + (int32_t)lane(), n_out, text);
+            const int32_t lo = max(base, run_first), hi = min(base + 63, run_last);
+            for (int32_t i = lo; i <= hi; i++) {
+                const Rec r = T.get((uint32_t)(i - base));
+                if (skipped(r, min_seq)) continue;
+                int32_t co;
+                W.text(text + r.toff, r.len, carry, i == run_last, &co);
+                carry = co;
+            }
+        }
+        W.byte('"');
+    }
+    __device__ void push_prev() {
+        if (!have_prev) return;
+        have_prev = false;
+        begin_seg();
+        if (run_text) {
+            if (run_props) {
+                W.lit("{\"text\":");
+                text_run();
+                W.lit(",\"props\":");
+                props_json(run_props);
+                W.byte('}');
+            } else {
+                text_run();
+            }
+        } else {
+            W.lit("{\"marker\":{\"refType\":");
+            W.num(run_ref);
+            W.byte('}');
+            if (run_props) {
+                W.lit(",\"props\":");
+                props_json(run_props);
+            }
+            W.byte('}');
+        }
+        end_seg(run_text ? run_len : 1);
+    }
+    __device__ void set_prev(const Rec &r, int32_t i) {
+        have_prev = true;
+        run_text = !(r.meta & kMetaMarker);
+        run_first = run_last = i;
+        run_len = run_text ? r.len : 0;
+        run_props = r.props;
+        run_ref = r.toff;
+        run_ends_nl = run_text && r.len > 0 && r.lastc == 0x0Au;
+    }
+    __device__ void standalone(const Rec &r) {
+        begin_seg();
+        W.lit("{\"json\":");
+        const bool txt = !(r.meta & kMetaMarker);
+        if (txt) {
+            if (r.props) W.lit("{\"text\":");
+            int32_t co;
+            W.byte('"');
+            W.text(text + r.toff, r.len, -1, true, &co);
+            W.byte('"');
+            if (r.props) {
+                W.lit(",\"props\":");
+                props_json(r.props);
+                W.byte('}');
+            }
+        } else {
+            W.lit("{\"marker\":{\"refType\":");
+            W.num(r.toff);
+            W.byte('}');
+            if (r.props) {
+                W.lit(",\"props\":");
+                props_json(r.props);
+            }
+            W.byte('}');
+        }
+        if (r.seq > min_seq) {
+            W.lit(",\"seq\":");
+            W.num(r.seq);
+            W.lit(",\"client\":");
+            client(r.meta & 63u);
+        }
+        if (r.rseq != kNoneSeq) {
+            W.lit(",\"removedSeq\":");
+            W.num(r.rseq);
+            W.lit(",\"removedClient\":");
+            client((r.meta >> 6) & 63u);
+        }
+        W.byte('}');
+        end_seg(r.len);
+    }
+
+    __device__ void walk() {
+        Tile T;
+        for (int32_t base = 0; base < n_out && !overflow; base += 64) {
+            T.load(rec, base + (int32_t)lane(), n_out, text);
+            const int32_t hi = min(64, n_out - base);
+            for (int32_t j = 0; j < hi && !overflow; j++) {
+                const Rec r = T.get((uint32_t)j);
+                if (skipped(r, min_seq)) continue;
+                const bool removed = r.rseq != kNoneSeq;
+                if (r.seq <= min_seq && !removed) {
+                    if (!have_prev) {
+                        set_prev(r, base + j);
+                        continue;
+                    }
+                    const bool txt = !(r.meta & kMetaMarker);
+                    const bool can = run_text && txt && !run_ends_nl && (run_len <= kGranularity || r.len <= kGranularity);
+                    if (can && props_match(run_props, r.props)) {
+                        run_last = base + j;
+                        run_len += r.len;
+                        if (r.len > 0) run_ends_nl = r.lastc == 0x0Au;
+                    } else {
+                        push_prev();
+                        set_prev(r, base + j);
+                    }
+                } else {
+                    push_prev();
+                    standalone(r);
+                }
+            }
+        }
+        if (!overflow) push_prev();
+        if (!overflow && (open || nch == 0)) {
+            if (!open) open_chunk();
+            close_chunk();
+        }
+    }
+};
+
+template <bool kWrite>
+__device__ void snapshot_doc(const SnapParams &P, int64_t w) {
+    const int64_t d = P.doc_list ? P.doc_list[w] : w;
+    if (kWrite && P.bytes[d] < 0) return;
+    const DocOut o = P.doc_out[w];
+    int32_t cf = P.cli_first, cn = P.cli_n;
+    if (P.doc_cli) {
+        cf = P.doc_cli[2 * d];
+        cn = P.doc_cli[2 * d + 1];
+    }
+    int32_t *mrow = P.meta + d * (int64_t)kSnapMeta;
+    Doc<kWrite> D(P, P.out + w * (int64_t)P.out_cap, P.text + P.doc_text_base[d], P.pool + P.doc_pool_base[d], o, cf,
+                  cn, kWrite ? P.dst + P.dst_off[d] : nullptr, mrow);
+    if (kWrite)
+        for (int32_t c = 0; c < mrow[0]; c++) {
+            D.all_count += mrow[1 + 3 * c];
+            D.all_len += mrow[2 + 3 * c];
+        }
+    D.walk();
+    if (kWrite) return;
+    // framing of each chunk, now that counts and totals are known
+    int64_t total = 0;
+    if (!D.overflow) {
+        Writer<false> f{nullptr, 0};
+        int64_t start = 0;
+        for (int32_t c = 0; c < D.nch; c++) {
+            const int64_t cnt = mrow[1 + 3 * c], len = mrow[2 + 3 * c];
+            f.pos = mrow[3 + 3 * c];
+            D.header(f, cnt, len);
+            D.trailer(f, c, start, D.nch, D.total_len, D.total_count);
+            if (lane() == 0) mrow[3 + 3 * c] = (int32_t)f.pos;
+            total += f.pos;
+            start += cnt;
+        }
+    }
+    if (lane() == 0) {
+        mrow[0] = D.overflow ? 0 : D.nch;
+        P.bytes[d] = D.overflow ? -1 : total;
+    }
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64) void mt_snapshot_kernel(SnapParams P) {
+    const int64_t w = blockIdx.x;
+    if (w >= P.n || !P.final_mask[w]) return;
+    if (P.pass) snapshot_doc<true>(P, w);
+    else snapshot_doc<false>(P, w);
+}
+
+}  // namespace mt

@@ -36,8 +36,11 @@ EXPORTS = [
     "mt_batch_ingest", "mt_batch_generate", "mt_batch_run", "mt_batch_launch", "mt_batch_sync",
     "mt_batch_get_stats", "mt_batch_algorithmic_bytes", "mt_doc_status", "mt_doc_text", "mt_doc_props_runs",
     "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
-    "mt_batch_download_log", "mt_batch_doc_counters", "mt_batch_device_digests",
+    "mt_batch_download_log", "mt_batch_doc_counters", "mt_batch_device_digests", "mt_batch_snapshots",
+    "mt_doc_snapshot_v1_device", "mt_batch_snapshot_index", "mt_batch_snapshot_copy",
 ]
+SNAP_MAX_BLOBS = 32
+SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
 DOC_COUNTERS = ("status", "min_seq", "cur_seq", "depth", "n_entries", "text_top", "pool_top", "ops_done",
                 "max_unsettled", "max_slots", "max_blocks", "max_heap", "fail_op", "cap_kind", "launch", "reserved")
 
@@ -116,6 +119,10 @@ def lib():
     L.mt_batch_download_log.argtypes = [vp, vp, vp, vp, vp]
     L.mt_batch_doc_counters.argtypes = [vp, vp]
     L.mt_batch_device_digests.argtypes = [vp, vp, i32]
+    L.mt_batch_snapshots.argtypes = [vp, P(i64), P(C.c_float)]
+    L.mt_doc_snapshot_v1_device.argtypes = [vp, i64, P(i32)]
+    L.mt_batch_snapshot_index.argtypes = [vp, vp, vp]
+    L.mt_batch_snapshot_copy.argtypes = [vp, vp, i32]
     _lib = L
     return L
 
@@ -176,10 +183,15 @@ class DocView:
         _chk(lib().mt_doc_digest(self.batch.h, self.index, C.byref(out)), "mt_doc_digest")
         return int(out.value)
 
-    def snapshot_v1(self) -> dict:
+    def snapshot_v1(self, device: bool = False) -> dict:
+        """{blob path: JSON} of SnapshotV1.  device=True: the blobs ReplayBatch.snapshots()
+        serialized on the GPU; False: the host serializer over the same final table."""
         L = lib()
         n = C.c_int32(0)
-        _chk(L.mt_doc_snapshot_v1(self.batch.h, self.index, C.byref(n)), "mt_doc_snapshot_v1")
+        if device:
+            _chk(L.mt_doc_snapshot_v1_device(self.batch.h, self.index, C.byref(n)), "mt_doc_snapshot_v1_device")
+        else:
+            _chk(L.mt_doc_snapshot_v1(self.batch.h, self.index, C.byref(n)), "mt_doc_snapshot_v1")
         out = {}
         for i in range(n.value):
             name = C.create_string_buffer(64)
@@ -303,6 +315,23 @@ class ReplayBatch:
             raise ValueError("out must be a contiguous 8-byte tensor of n_docs elements")
         _chk(lib().mt_batch_device_digests(self.h, out.data_ptr(), 1 if out.is_cuda else 0), "mt_batch_device_digests")
         return out
+
+    def snapshots(self) -> dict:
+        """SnapshotV1 of every document serialized on the GPU (mt_batch_snapshots).  Returns
+        {"bytes": total, "device_ms": both passes}; read back with doc(i).snapshot_v1(device=True)
+        or snapshot_buffer()."""
+        total, ms = C.c_int64(0), C.c_float(0)
+        _chk(lib().mt_batch_snapshots(self.h, C.byref(total), C.byref(ms)), "mt_batch_snapshots")
+        return {"bytes": int(total.value), "device_ms": float(ms.value)}
+
+    def snapshot_buffer(self):
+        """(bytes, doc_off[n_docs+1], meta[n_docs, SNAP_META]) of the last snapshots() call."""
+        off = np.zeros(self.n_docs + 1, np.int64)
+        meta = np.zeros((self.n_docs, SNAP_META), np.int32)
+        _chk(lib().mt_batch_snapshot_index(self.h, off.ctypes.data, meta.ctypes.data), "mt_batch_snapshot_index")
+        buf = np.zeros(max(1, int(off[-1])), np.uint8)
+        _chk(lib().mt_batch_snapshot_copy(self.h, buf.ctypes.data, 0), "mt_batch_snapshot_copy")
+        return buf[: int(off[-1])].tobytes(), off, meta
 
     def statuses(self) -> np.ndarray:
         L = lib()

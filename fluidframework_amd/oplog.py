@@ -72,7 +72,7 @@ def _is_array_index(k: str) -> bool:
 
 
 def _utf16(s: str) -> np.ndarray:
-    return np.frombuffer(s.encode("utf-16-le"), dtype="<u2")
+    return np.frombuffer(s.encode("utf-16-le", "surrogatepass"), dtype="<u2")
 
 
 def _js_keys(obj: dict) -> list:

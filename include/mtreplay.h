@@ -22,6 +22,9 @@
  *                               run-length encoded
  *   mt_doc_snapshot_v1/_blob    new SnapshotV1(mergeTree, logger).extractSync(); emit()
  *                               (merge-tree/src/snapshotV1.ts:85-247): blob path + contents
+ *   mt_batch_snapshots + mt_doc_snapshot_v1_device / mt_batch_snapshot_index / _copy
+ *                               the same SnapshotV1 blobs for every document, serialized on the GPU
+ *                               (snapshotV1.ts:85-247 for a whole batch of documents at once)
  *   mt_doc_digest               FNV-1a-64 over the final segment table (DESIGN.md "State digest")
  *   mt_batch_device_digests     8-byte per-document fingerprint of the final state computed on the
  *                               GPU (what rank 0 gathers over RCCL; no reference counterpart)
@@ -125,6 +128,19 @@ MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, i
 MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs);
 MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name, int64_t name_cap, char *buf,
                                 int64_t cap, int64_t *len);
+/* SnapshotV1 of every document on the GPU (mt_snapshot.hip: a sizing pass, a host prefix sum of
+   the bytes, a writing pass) into one device buffer of *total_bytes; *device_ms = both passes.
+   Blobs of a document lie back to back (header, body_0, ..) at doc_off[doc]; a document with more
+   than MT_SNAP_MAX_BLOBS blobs gets size 0 there and n_blobs 0 in its meta row. */
+#define MT_SNAP_MAX_BLOBS 32
+#define MT_SNAP_META (1 + 3 * MT_SNAP_MAX_BLOBS) /* n_blobs, then (segmentCount, length, bytes) */
+MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_ms);
+/* after mt_batch_snapshots: the GPU blobs of `doc` become what mt_doc_snapshot_blob returns
+   (documents over MT_SNAP_MAX_BLOBS blobs: the host serializer, as mt_doc_snapshot_v1) */
+MT_API int mt_doc_snapshot_v1_device(mt_batch *b, int64_t doc, int32_t *n_blobs);
+/* doc_off[n_docs + 1] byte offsets; blob_meta[n_docs * MT_SNAP_META] (either may be NULL) */
+MT_API int mt_batch_snapshot_index(mt_batch *b, int64_t *doc_off, int32_t *blob_meta);
+MT_API int mt_batch_snapshot_copy(mt_batch *b, void *dst, int32_t dst_is_device);
 MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out);
 /* per-document device digests of the last run into dst[n_docs] (a device pointer when
    dst_is_device, else host memory) */
