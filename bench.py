@@ -30,6 +30,9 @@ CONFIGS = {
             workload="configs[1]: 4,096 docs x 2k text-only insert/removeRange ops, 8 clients, refSeq lag<=32"),
     3: dict(docs=8192, ops=10000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35,
             workload="configs[2] mix: docs x 10k ops, 10% annotate, minSeq advance/zamboni, 8 clients"),
+    5: dict(docs=131072, ops=2000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35, snapshot=True,
+            workload="configs[4]: 1M docs over 8 GPUs (131,072 per GPU) x 2k ops (10% annotate), full replay + "
+                     "SnapshotV1 of every doc on the GPU in each step, digests gathered to rank 0"),
 }
 
 
@@ -45,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="oracle baseline sample (default: auto)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--snapshot", action="store_true", help="serialize SnapshotV1 of every doc in each step")
     return ap.parse_args()
 
 
@@ -85,18 +89,28 @@ def main():
     log(rank, f"generated {n_docs} docs x {n_ops} ops in {gen_s:.1f} s")
     stream = torch.cuda.current_stream().cuda_stream
 
+    with_snap = args.snapshot or cfg.get("snapshot", False)
     for i in range(args.warmup):
         b.run(stream)
+        if with_snap:
+            b.snapshots()
         log(rank, f"warmup {i}: {b.stats()['kernel_ms']:.1f} ms kernel")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kernel_ms = []
+    kernel_ms, first_ms, first_ops, snap_ms, snap_bytes = [], [], [], [], 0
     for i in range(args.steps):
         b.run(stream)
         kernel_ms.append(b.stats()["kernel_ms"])
-        log(rank, f"step {i}: {kernel_ms[-1]:.1f} ms kernel")
+        l0 = b.launches()[0]  # the dominant kernel: the launch that holds every document
+        first_ms.append(l0["ms"])
+        first_ops.append(l0["ops"])
+        if with_snap:  # SnapshotV1 of every document, part of the step
+            sn = b.snapshots()
+            snap_ms.append(sn["device_ms"])
+            snap_bytes = sn["bytes"]
+        log(rank, f"step {i}: {kernel_ms[-1]:.1f} ms kernel" + (f", {snap_ms[-1]:.1f} ms snapshot" if with_snap else ""))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -133,13 +147,27 @@ def main():
     value = total_ops / t_max
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     alg_bytes = b.algorithmic_bytes()
-    achieved_gbs = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+    # roofline of the dominant kernel (launch 0, mt_replay_kernel_<class>): the algorithmic bytes
+    # of the ops it applied (DESIGN.md "Roofline": per-op share of the batch's algorithmic bytes)
+    # over its average launch duration (hipEvents on the run stream)
+    avg_first_ms = sum(first_ms) / len(first_ms)
+    first_bytes = alg_bytes * (sum(first_ops) / len(first_ops)) / max(1, ops_done)
+    achieved_gbs = first_bytes / (avg_first_ms * 1e-3) / 1e9
 
     traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, f"mt_replay_kernel_{st['lds_class']}")
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
         cpu, parity = cpu_baseline(b, fa, n_docs, n_ops, args)
+    snapshot = None
+    if with_snap:
+        avg_snap = sum(snap_ms) / len(snap_ms)
+        snapshot = {"bytes_per_step": int(snap_bytes), "avg_device_ms": round(avg_snap, 3),
+                    "GB_per_s": round(snap_bytes / (avg_snap * 1e-3) / 1e9, 3), "kernel": "mt_snapshot_kernel"}
+        if rank == 0:  # spot check: GPU blobs == host serializer on a sample
+            sample = range(0, n_docs, max(1, n_docs // 64))
+            snapshot["host_match"] = sum(b.doc(d).snapshot_v1(device=True) == b.doc(d).snapshot_v1() for d in sample)
+            snapshot["checked"] = len(sample)
 
     if rank == 0:
         line = {
@@ -162,10 +190,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": f"mt_replay_kernel_{st['lds_class']}", "avg_kernel_ms": round(avg_kernel_ms, 3),
-                         "algorithmic_bytes_per_launch": int(alg_bytes)},
+                         "kernel": f"mt_replay_kernel_{st['lds_class']}", "avg_launch_ms": round(avg_first_ms, 3),
+                         "algorithmic_bytes_per_launch": int(first_bytes),
+                         "ops_per_launch": int(sum(first_ops) / len(first_ops))},
+            "replay_ms_per_step": round(avg_kernel_ms, 3),
+            "launches": b.launches(),
             "cpu_baseline": cpu,
             "parity": parity,
+            "snapshot": snapshot,
             "docs_ok": all_ok,
             "digests_gathered": world * n_docs,
             "digest_xor": digest_xor,

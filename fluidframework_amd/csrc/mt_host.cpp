@@ -111,6 +111,8 @@ struct Launch {
     std::vector<int32_t> cksrc;
     int src = -1;               // launch whose checkpoints / cold records cksrc indexes
     size_t lds = 0;
+    float ms = 0;               // device time (hipEvents)
+    int64_t ops = 0;            // ops applied by this launch (resumed documents: after their checkpoint)
 };
 
 struct DocRes {  // per-document result location
@@ -335,6 +337,7 @@ struct mt_batch {
     int32_t *d_snap_meta = nullptr;
     int64_t *d_snap_bytes = nullptr, *d_snap_off = nullptr;
     uint8_t *d_snap = nullptr;
+    size_t snap_cap = 0;
     std::vector<int64_t> h_snap_bytes, h_snap_off;
 };
 
@@ -346,6 +349,7 @@ static void free_snap(mt_batch *b) {
     b->d_snap_meta = nullptr;
     b->d_snap_bytes = b->d_snap_off = nullptr;
     b->d_snap = nullptr;
+    b->snap_cap = 0;
     b->snap_ready = false;
 }
 
@@ -416,7 +420,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
     if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
     if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
     if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
-    if (b->opt.max_retries <= 0) b->opt.max_retries = 6;
+    if (b->opt.max_retries == 0) b->opt.max_retries = 6;  // < 0: checkpoint, but stop after the first launch
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
@@ -673,7 +677,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
     }
     // documents short of headroom checkpoint here unless this is the largest usable class
-    const bool can_grow = class_usable(L.cls + 1) && b->opt.max_retries > 0;
+    const bool can_grow = class_usable(L.cls + 1) && b->opt.max_retries != 0;
     if (can_grow) HIPCHK(dalloc(&L.d_ck, (size_t)n * (size_t)mt::ck_words(L.caps.seg)));
     const Launch *prev = L.src >= 0 ? &b->launches[(size_t)L.src] : nullptr;
     if (!L.cksrc.empty()) {
@@ -711,7 +715,7 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
     if (!b || !b->have_log) return MT_ERR_STATE;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->stream;
     free_launches(b);
-    free_snap(b);
+    b->snap_ready = false;  // buffers are kept for the next mt_batch_snapshots
     b->ran = false;
     b->cached_doc = -1;
     b->c_blob_doc = -1;
@@ -753,8 +757,11 @@ static int gather_launch(mt_batch *b, int li) {
         b->docout.assign((size_t)b->n_docs, DocOut{});
         b->where.assign((size_t)b->n_docs, DocRes{});
     }
+    L.ops = 0;
     for (int64_t i = 0; i < n; i++) {
         int64_t d = L.docs.empty() ? i : L.docs[i];
+        const bool resumed = !L.cksrc.empty() && L.cksrc[(size_t)i] >= 0;
+        L.ops += tmp[i].ops_done - (resumed ? b->docout[d].ops_done : 0);
         b->docout[d] = tmp[i];
         b->where[d].launch = li;
         b->where[d].idx = (int32_t)i;
@@ -768,6 +775,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
     b->kernel_ms = ms;
+    b->launches[0].ms = ms;
     int rc = gather_launch(b, 0);
     if (rc) return rc;
     // capacity escalation: a checkpointed document resumes, a document that overflowed mid-op
@@ -816,6 +824,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
             HIPCHK(hipEventSynchronize(b->ev1));
             HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
             b->kernel_ms += ms;
+            b->launches[(size_t)li].ms = ms;
             rc = gather_launch(b, li);
             if (rc) return rc;
             frontier.push_back(li);
@@ -886,6 +895,21 @@ MT_API int mt_batch_get_stats(mt_batch *b, mt_batch_stats *o) {
 
 // DESIGN.md "Roofline": per document 32 B per op record + 2 B per inserted code unit + 8 B per
 // prop record (read) + 32 B per final table entry + 2 B per final text code unit (written).
+MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *o) {
+    if (!b || !o) return MT_ERR_ARG;
+    if (!b->ran) return MT_ERR_STATE;
+    if (i < 0 || i >= (int32_t)b->launches.size()) return MT_ERR_ARG;
+    const Launch &L = b->launches[(size_t)i];
+    memset(o, 0, sizeof *o);
+    o->seg_class = mt::kClassSegs[L.cls];
+    o->n_docs = L.docs.empty() ? (int32_t)b->n_docs : (int32_t)L.docs.size();
+    o->resumed = (int32_t)std::count_if(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x >= 0; });
+    o->lds_bytes = (int32_t)L.lds;
+    o->ms = L.ms;
+    o->ops = L.ops;
+    return MT_OK;
+}
+
 MT_API int mt_batch_algorithmic_bytes(mt_batch *b, double *bytes) {
     if (!b || !bytes || !b->ran) return MT_ERR_STATE;
     double t = 32.0 * (double)b->total_ops + 2.0 * b->payload_units + 8.0 * b->prop_records;
@@ -1198,7 +1222,7 @@ MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name,
 MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_ms) {
     if (!b) return MT_ERR_ARG;
     if (!b->ran) return MT_ERR_STATE;
-    free_snap(b);
+    b->snap_ready = false;
     hipStream_t s = b->run_stream ? b->run_stream : b->stream;
     // string tables: JSON.stringify(key), value JSON texts, JSON.stringify(long client id)
     std::string strs;
@@ -1259,8 +1283,9 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
             fail(MT_ERR_HIP);
             break;
         }
-        if (dalloc(&b->d_snap_meta, (size_t)b->n_docs * mt::kSnapMeta) != hipSuccess ||
-            dalloc(&b->d_snap_bytes, (size_t)b->n_docs) != hipSuccess ||
+        if ((!b->d_snap_meta && dalloc(&b->d_snap_meta, (size_t)b->n_docs * mt::kSnapMeta) != hipSuccess) ||
+            (!b->d_snap_bytes && dalloc(&b->d_snap_bytes, (size_t)b->n_docs) != hipSuccess) ||
+            (!b->d_snap_off && dalloc(&b->d_snap_off, (size_t)b->n_docs + 1) != hipSuccess) ||
             hipMemsetAsync(b->d_snap_bytes, 0xFF, 8 * (size_t)b->n_docs, s) != hipSuccess) {
             fail(MT_ERR_HIP);
             break;
@@ -1291,8 +1316,19 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                 b->h_snap_off.assign((size_t)b->n_docs + 1, 0);
                 for (int64_t d = 0; d < b->n_docs; d++)
                     b->h_snap_off[d + 1] = b->h_snap_off[d] + std::max<int64_t>(0, b->h_snap_bytes[d]);
-                if (dalloc(&b->d_snap, (size_t)std::max<int64_t>(1, b->h_snap_off.back())) != hipSuccess ||
-                    !up(&b->d_snap_off, b->h_snap_off)) {
+                const size_t need = (size_t)std::max<int64_t>(1, b->h_snap_off.back());
+                if (need > b->snap_cap) {
+                    (void)hipFree(b->d_snap);
+                    b->d_snap = nullptr;
+                    b->snap_cap = 0;
+                    if (dalloc(&b->d_snap, need + need / 8) != hipSuccess) {
+                        fail(MT_ERR_HIP);
+                        break;
+                    }
+                    b->snap_cap = need + need / 8;
+                }
+                if (hipMemcpyAsync(b->d_snap_off, b->h_snap_off.data(), 8 * b->h_snap_off.size(),
+                                   hipMemcpyHostToDevice, s) != hipSuccess) {
                     fail(MT_ERR_HIP);
                     break;
                 }
@@ -1355,7 +1391,6 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
     for (uint8_t *p : d_final) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
-    if (rc) free_snap(b);
     return rc;
 }
 

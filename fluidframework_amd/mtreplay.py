@@ -37,7 +37,7 @@ EXPORTS = [
     "mt_batch_get_stats", "mt_batch_algorithmic_bytes", "mt_doc_status", "mt_doc_text", "mt_doc_props_runs",
     "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
     "mt_batch_download_log", "mt_batch_doc_counters", "mt_batch_device_digests", "mt_batch_snapshots",
-    "mt_doc_snapshot_v1_device", "mt_batch_snapshot_index", "mt_batch_snapshot_copy",
+    "mt_doc_snapshot_v1_device", "mt_batch_snapshot_index", "mt_batch_snapshot_copy", "mt_batch_launch_info",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -63,6 +63,14 @@ class BatchOptions(C.Structure):
     _fields_ = [("chunk_size", C.c_int32), ("seg_cap", C.c_int32), ("oe_cap", C.c_int32), ("blk_cap", C.c_int32),
                 ("heap_cap", C.c_int32), ("arena_factor", C.c_int32), ("pool_per_op", C.c_int32),
                 ("max_retries", C.c_int32)]
+
+
+class LaunchInfo(C.Structure):
+    _fields_ = [("seg_class", C.c_int32), ("n_docs", C.c_int32), ("resumed", C.c_int32), ("lds_bytes", C.c_int32),
+                ("ms", C.c_float), ("reserved", C.c_int32), ("ops", C.c_int64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
 class BatchStats(C.Structure):
@@ -119,6 +127,7 @@ def lib():
     L.mt_batch_download_log.argtypes = [vp, vp, vp, vp, vp]
     L.mt_batch_doc_counters.argtypes = [vp, vp]
     L.mt_batch_device_digests.argtypes = [vp, vp, i32]
+    L.mt_batch_launch_info.argtypes = [vp, i32, P(LaunchInfo)]
     L.mt_batch_snapshots.argtypes = [vp, P(i64), P(C.c_float)]
     L.mt_doc_snapshot_v1_device.argtypes = [vp, i64, P(i32)]
     L.mt_batch_snapshot_index.argtypes = [vp, vp, vp]
@@ -314,6 +323,15 @@ class ReplayBatch:
         if out.numel() != self.n_docs or out.element_size() != 8 or not out.is_contiguous():
             raise ValueError("out must be a contiguous 8-byte tensor of n_docs elements")
         _chk(lib().mt_batch_device_digests(self.h, out.data_ptr(), 1 if out.is_cuda else 0), "mt_batch_device_digests")
+        return out
+
+    def launches(self) -> list:
+        """Per-launch info of the last run (mt_batch_launch_info): class, docs, resumed, ms, ops."""
+        out = []
+        for i in range(self.stats()["launches"]):
+            li = LaunchInfo()
+            _chk(lib().mt_batch_launch_info(self.h, i, C.byref(li)), "mt_batch_launch_info")
+            out.append(li.as_dict())
         return out
 
     def snapshots(self) -> dict:

@@ -74,7 +74,8 @@ typedef struct mt_batch_options {
     int32_t heap_cap;        /* reserved                                                           */
     int32_t arena_factor;    /* text arena = factor * payload + 4096 code units; 0 -> 4            */
     int32_t pool_per_op;     /* prop pool words per annotate / props insert; 0 -> 96               */
-    int32_t max_retries;     /* capacity-class escalations for docs that overflow; 0 -> 6          */
+    int32_t max_retries;     /* capacity-class escalations for docs that overflow; 0 -> 6; < 0: none
+                                (documents short of headroom still checkpoint: capacity planning)  */
 } mt_batch_options;
 
 typedef struct mt_batch_stats {
@@ -114,6 +115,18 @@ MT_API int mt_batch_run(mt_batch *b, void *hip_stream);
 MT_API int mt_batch_launch(mt_batch *b, void *hip_stream);
 MT_API int mt_batch_sync(mt_batch *b);
 MT_API int mt_batch_get_stats(mt_batch *b, mt_batch_stats *out);
+/* one replay launch of the last run: launch 0 holds every document, later ones the documents
+   escalated to a larger capacity class (mt_batch_stats.launches of them) */
+typedef struct mt_launch_info {
+    int32_t seg_class;      /* segment slots of the launch's capacity class                  */
+    int32_t n_docs;         /* documents (workgroups) in the launch                           */
+    int32_t resumed;        /* of them resumed from a checkpoint (the rest start from op 0)   */
+    int32_t lds_bytes;      /* dynamic LDS per document (0: HBM class)                        */
+    float ms;               /* device time (hipEvents on the run stream)                      */
+    int32_t reserved;
+    int64_t ops;            /* ops applied by this launch                                     */
+} mt_launch_info;
+MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *out);
 /* algorithmic HBM bytes of one replay (DESIGN.md "Roofline"): ops, payloads, final table, text */
 MT_API int mt_batch_algorithmic_bytes(mt_batch *b, double *bytes);
 

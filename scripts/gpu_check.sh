@@ -31,6 +31,10 @@ for step in "$@"; do
     pmcw) run pmcw 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o run -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu ;;
     full3) run full3 900 python -u bench.py --config 3 --docs 65536 --steps 1 --warmup 0 --no-cpu ;;
     full3p) run full3p 900 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
+    snaptests) run snaptests 300 python -u -m pytest tests/test_gpu_snapshot.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    benchsnap) run benchsnap 600 python -u bench.py --snapshot --steps 3 --warmup 1 --no-cpu ;;
+    bench5) run bench5 900 python -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
+    profsnap) run profsnap 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profsnap -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 2 --warmup 1 --no-cpu ;;
     *) echo "unknown step $step" ;;
   esac
 done
