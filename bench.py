@@ -135,14 +135,22 @@ def main():
     st_t = torch.from_numpy(statuses.astype("int64")).cuda()
     torch.cuda.synchronize()
     tg = time.perf_counter()
-    gathered = shard.gather_results(dig_t, st_t, world, rank)
+    snap_t = None
+    if with_snap:  # per-document digest of the GPU SnapshotV1 bytes, gathered with the rest
+        snap_t = torch.empty(n_docs, dtype=torch.int64, device="cuda")
+        b.snapshot_digests(snap_t)
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+    gathered = shard.gather_results(dig_t, st_t, world, rank, snap_t)
     torch.cuda.synchronize()
     gather_ms = 1e3 * (time.perf_counter() - tg)
-    all_ok, digest_xor = 0, None
+    all_ok, digest_xor, snap_xor = 0, None, None
     if rank == 0:
-        all_dig, all_st = gathered
+        all_dig, all_st = gathered[:2]
         all_ok = int((all_st == 0).all())
         digest_xor = f"{int(np.bitwise_xor.reduce(all_dig)):016x}"
+        if with_snap:
+            snap_xor = f"{int(np.bitwise_xor.reduce(gathered[2])):016x}"
     total_ops = n_ops * n_docs * world * args.steps
     value = total_ops / t_max
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
@@ -201,6 +209,7 @@ def main():
             "docs_ok": all_ok,
             "digests_gathered": world * n_docs,
             "digest_xor": digest_xor,
+            "snapshot_digest_xor": snap_xor,
             "ops_applied_per_step": int(ops_done),
             "lds_bytes_per_doc": st["lds_bytes"],
             "launches_per_step": st["launches"],

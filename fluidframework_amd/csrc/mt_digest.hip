@@ -78,3 +78,39 @@ extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P
 }
 
 }  // namespace mt
+
+namespace mt {
+
+// 64-bit digest of each document's byte range [off, off + len) of a buffer (the GPU SnapshotV1
+// blobs): mix64(len-seeded state ^ sum over 8-byte little-endian words k of
+// mix64(word_k + (k + 1) * golden)), the last word zero-padded.  Order-dependent through k,
+// lane-parallel.  Documents with len < 0 (not serialized on the GPU) get 0.  The buffer must
+// be readable 8 bytes past its last range (the host pads the allocation).
+extern "C" __global__ __launch_bounds__(64) void mt_bytes_digest_kernel(const uint8_t *buf, const int64_t *off,
+                                                                      const int64_t *len, int64_t n, uint64_t *dst) {
+    const int64_t d = blockIdx.x;
+    if (d >= n) return;
+    const int64_t L = len[d];
+    if (L < 0) {
+        if (threadIdx.x == 0) dst[d] = 0;
+        return;
+    }
+    const int64_t o = off[d];
+    const uint64_t *w64 = reinterpret_cast<const uint64_t *>(buf);
+    uint64_t acc = 0;
+    const int64_t nw = (L + 7) / 8;
+    for (int64_t k = threadIdx.x; k < nw; k += 64) {
+        const int64_t b = o + 8 * k;
+        const int64_t q = b >> 3;
+        const uint32_t sh = (uint32_t)(b & 7) * 8;
+        uint64_t w = w64[q];
+        if (sh) w = (w >> sh) | (w64[q + 1] << (64 - sh));
+        const int64_t rem = L - 8 * k;
+        if (rem < 8) w &= (1ull << (8 * rem)) - 1;
+        acc += mix64(w + 0x9E3779B97F4A7C15ull * (uint64_t)(k + 1));
+    }
+    for (int s = 32; s > 0; s >>= 1) acc += __shfl_xor(acc, s, 64);
+    if (threadIdx.x == 0) dst[d] = mix64(mix64((uint64_t)L ^ 0x736E617073686F74ull) ^ acc);
+}
+
+}  // namespace mt

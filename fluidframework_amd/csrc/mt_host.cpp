@@ -46,6 +46,8 @@ MT_DECLARE_CLASS(4096)
 MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
+extern "C" __global__ void mt_bytes_digest_kernel(const uint8_t *buf, const int64_t *off, const int64_t *len, int64_t n,
+                                                  uint64_t *dst);
 
 using mt::Caps;
 using mt::DocOut;
@@ -1321,7 +1323,8 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                     (void)hipFree(b->d_snap);
                     b->d_snap = nullptr;
                     b->snap_cap = 0;
-                    if (dalloc(&b->d_snap, need + need / 8) != hipSuccess) {
+                    // +64: mt_bytes_digest_kernel reads up to 8 bytes past the last range
+                    if (dalloc(&b->d_snap, need + need / 8 + 64) != hipSuccess) {
                         fail(MT_ERR_HIP);
                         break;
                     }
@@ -1427,6 +1430,21 @@ MT_API int mt_batch_snapshot_index(mt_batch *b, int64_t *doc_off, int32_t *blob_
     if (doc_off) memcpy(doc_off, b->h_snap_off.data(), 8 * b->h_snap_off.size());
     if (blob_meta)
         HIPCHK(hipMemcpy(blob_meta, b->d_snap_meta, 4 * (size_t)b->n_docs * mt::kSnapMeta, hipMemcpyDeviceToHost));
+    return MT_OK;
+}
+
+MT_API int mt_batch_snapshot_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_device) {
+    if (!b || !dst) return MT_ERR_ARG;
+    if (!b->snap_ready) return MT_ERR_STATE;
+    hipStream_t s = b->run_stream ? b->run_stream : b->stream;
+    if (!b->d_digest) HIPCHK(dalloc(&b->d_digest, (size_t)b->n_docs));
+    // d_snap_off holds the per-document starts, d_snap_bytes the sizes (-1: host serializer)
+    HIPCHK(hipMemcpyAsync(b->d_snap_off, b->h_snap_off.data(), 8 * b->h_snap_off.size(), hipMemcpyHostToDevice, s));
+    void *args[] = {&b->d_snap, &b->d_snap_off, &b->d_snap_bytes, &b->n_docs, &b->d_digest};
+    HIPCHK(hipLaunchKernel((const void *)mt_bytes_digest_kernel, dim3((unsigned)b->n_docs), dim3(64), args, 0, s));
+    HIPCHK(hipMemcpyAsync(dst, b->d_digest, 8 * (size_t)b->n_docs,
+                          dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     return MT_OK;
 }
 

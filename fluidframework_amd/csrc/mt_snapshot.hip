@@ -78,10 +78,12 @@ struct Writer {
         if (kWrite && lane() == 0) dst[pos] = (uint8_t)c;
         pos++;
     }
+    // a string literal (read-only data in global memory, one byte per lane)
     template <int N>
     __device__ __forceinline__ void lit(const char (&s)[N]) {
         static_assert(N - 1 <= 64, "literal longer than a wave");
-        if (kWrite && lane() < (uint32_t)(N - 1)) dst[pos + lane()] = (uint8_t)s[lane()];
+        const char *p = s;
+        if (kWrite && lane() < (uint32_t)(N - 1)) dst[pos + lane()] = (uint8_t)p[lane()];
         pos += N - 1;
     }
     __device__ __forceinline__ void copy(const uint8_t *src, uint32_t n) {
@@ -103,7 +105,7 @@ struct Writer {
     }
     // JSON string body of the virtual array v[0..m): v[0] = carry (when has_carry) followed by
     // t[0..n).  Unless `last`, a trailing high surrogate is held back in *carry_out.
-    __device__ void text(const uint16_t *t, uint32_t n, int32_t carry, bool last, int32_t *carry_out) {
+    __device__ __forceinline__ void text(const uint16_t *t, uint32_t n, int32_t carry, bool last, int32_t *carry_out) {
         const uint32_t hc = carry >= 0 ? 1u : 0u, m = n + hc;
         uint32_t me = m;
         *carry_out = -1;
@@ -177,23 +179,21 @@ struct Tile {
     uint32_t len, meta, props, toff, blk, lastc;
     int32_t seq, rseq;
     __device__ __forceinline__ void load(const OutRec *rec, int32_t i, int32_t n, const uint16_t *text) {
+        uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, kMarkerSlot);
         if (i < n) {
-            const uint4 a = reinterpret_cast<const uint4 *>(rec + i)[0];
-            const uint4 b = reinterpret_cast<const uint4 *>(rec + i)[1];
-            len = a.x;
-            seq = (int32_t)a.y;
-            rseq = (int32_t)a.z;
-            meta = a.w;
-            props = b.y;
-            toff = b.z;
-            blk = b.w;
-            const bool txt = (blk & 0xFFFFu) != kMarkerSlot && !(meta & kMetaMarker) && len > 0;
-            lastc = txt ? text[toff + len - 1] : 0u;
-        } else {
-            len = meta = props = toff = lastc = 0;
-            blk = kMarkerSlot;
-            seq = rseq = 0;
+            a = reinterpret_cast<const uint4 *>(rec + i)[0];
+            b = reinterpret_cast<const uint4 *>(rec + i)[1];
         }
+        len = a.x;
+        seq = (int32_t)a.y;
+        rseq = (int32_t)a.z;
+        meta = a.w;
+        props = b.y;
+        toff = b.z;
+        blk = b.w;
+        uint32_t lc = 0;
+        if ((blk & 0xFFFFu) != kMarkerSlot && !(meta & kMetaMarker) && len > 0) lc = text[toff + len - 1];
+        lastc = lc;
     }
     __device__ __forceinline__ Rec get(uint32_t l) const {
         Rec r;
@@ -242,15 +242,15 @@ struct Doc {
         return r.rseq != kNoneSeq && r.rseq <= min_seq;
     }
 
-    __device__ void str(const uint32_t *tab, uint32_t i) { W.copy(P.strs + tab[2 * i], tab[2 * i + 1]); }
-    __device__ void client(uint32_t id) {
+    __device__ __forceinline__ void str(const uint32_t *tab, uint32_t i) { W.copy(P.strs + tab[2 * i], tab[2 * i + 1]); }
+    __device__ __forceinline__ void client(uint32_t id) {
         if (id < (uint32_t)cli_n) str(P.cli_str, (uint32_t)cli_first + id);
         else str(P.cli_str, 0);  // "undefined"
     }
     __device__ __forceinline__ uint32_t key_rank(uint32_t k) const {
         return k < (uint32_t)P.n_keys ? P.key_rank[k] : kNoRank;
     }
-    __device__ void prop_entry(uint32_t id, uint32_t i, bool &first) {
+    __device__ __forceinline__ void prop_entry(uint32_t id, uint32_t i, bool &first) {
         const uint32_t k = pool[id + 2 + 2 * i], v = pool[id + 3 + 2 * i];
         if (!first) W.byte(',');
         first = false;
@@ -259,7 +259,7 @@ struct Doc {
         str(P.val_str, v < (uint32_t)P.n_values ? v : 0u);
     }
     // JSON.stringify(properties): array-index keys ascending, then insertion order
-    __device__ void props_json(uint32_t id) {
+    __device__ __forceinline__ void props_json(uint32_t id) {
         const uint32_t n = pool[id];
         W.byte('{');
         bool first = true;
@@ -294,7 +294,7 @@ struct Doc {
         W.byte('}');
     }
     // matchProperties over the pool's (key, value) lists
-    __device__ bool props_match(uint32_t a, uint32_t c) {
+    __device__ __forceinline__ bool props_match(uint32_t a, uint32_t c) {
         if (a == c) return true;
         if (!a || !c) return false;
         const uint32_t na = pool[a], nc = pool[c];
@@ -311,7 +311,7 @@ struct Doc {
 
     // ---- chunks
     template <class Wr>
-    __device__ void header(Wr &w, int64_t count, int64_t length) {
+    __device__ __forceinline__ void header(Wr &w, int64_t count, int64_t length) {
         w.lit("{\"version\":\"1\",\"segmentCount\":");
         w.num(count);
         w.lit(",\"length\":");
@@ -319,7 +319,7 @@ struct Doc {
         w.lit(",\"segments\":[");
     }
     template <class Wr>
-    __device__ void trailer(Wr &w, int32_t c, int64_t start, int32_t n_chunks, int64_t tlen,
+    __device__ __forceinline__ void trailer(Wr &w, int32_t c, int64_t start, int32_t n_chunks, int64_t tlen,
                             int64_t tcount) {
         w.lit("],\"startIndex\":");
         w.num(start);
@@ -342,13 +342,13 @@ struct Doc {
         }
         w.byte('}');
     }
-    __device__ void open_chunk() {
+    __device__ __forceinline__ void open_chunk() {
         open = true;
         ccount = clen = 0;
         if (kWrite) header(W, mrow[1 + 3 * nch], mrow[2 + 3 * nch]);
         seg_bytes_at_open = W.pos;
     }
-    __device__ void close_chunk() {
+    __device__ __forceinline__ void close_chunk() {
         if (nch >= kSnapMaxChunks) {
             overflow = true;
         } else if (kWrite) {
@@ -363,18 +363,18 @@ struct Doc {
         nch++;
         open = false;
     }
-    __device__ void begin_seg() {
+    __device__ __forceinline__ void begin_seg() {
         if (!open) open_chunk();
         else W.byte(',');
     }
-    __device__ void end_seg(int64_t len) {
+    __device__ __forceinline__ void end_seg(int64_t len) {
         ccount++;
         clen += len;
         if (clen >= P.chunk_size) close_chunk();
     }
 
     // ---- segments
-    __device__ void text_run() {
+    __device__ __forceinline__ void text_run() {
         W.byte('"');
         int32_t carry = -1;
         Tile T;
@@ -391,7 +391,7 @@ struct Doc {
         }
         W.byte('"');
     }
-    __device__ void push_prev() {
+    __device__ __forceinline__ void push_prev() {
         if (!have_prev) return;
         have_prev = false;
         begin_seg();
@@ -417,7 +417,7 @@ struct Doc {
         }
         end_seg(run_text ? run_len : 1);
     }
-    __device__ void set_prev(const Rec &r, int32_t i) {
+    __device__ __forceinline__ void set_prev(const Rec &r, int32_t i) {
         have_prev = true;
         run_text = !(r.meta & kMetaMarker);
         run_first = run_last = i;
@@ -426,7 +426,7 @@ struct Doc {
         run_ref = r.toff;
         run_ends_nl = run_text && r.len > 0 && r.lastc == 0x0Au;
     }
-    __device__ void standalone(const Rec &r) {
+    __device__ __forceinline__ void standalone(const Rec &r) {
         begin_seg();
         W.lit("{\"json\":");
         const bool txt = !(r.meta & kMetaMarker);
@@ -467,7 +467,7 @@ struct Doc {
         end_seg(r.len);
     }
 
-    __device__ void walk() {
+    __device__ __forceinline__ void walk() {
         Tile T;
         for (int32_t base = 0; base < n_out && !overflow; base += 64) {
             T.load(rec, base + (int32_t)lane(), n_out, text);
@@ -506,7 +506,7 @@ struct Doc {
 };
 
 template <bool kWrite>
-__device__ void snapshot_doc(const SnapParams &P, int64_t w) {
+__device__ __forceinline__ void snapshot_doc(const SnapParams &P, int64_t w) {
     const int64_t d = P.doc_list ? P.doc_list[w] : w;
     if (kWrite && P.bytes[d] < 0) return;
     const DocOut o = P.doc_out[w];
@@ -548,7 +548,7 @@ __device__ void snapshot_doc(const SnapParams &P, int64_t w) {
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(64) void mt_snapshot_kernel(SnapParams P) {
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mt_snapshot_kernel(SnapParams P) {
     const int64_t w = blockIdx.x;
     if (w >= P.n || !P.final_mask[w]) return;
     if (P.pass) snapshot_doc<true>(P, w);

@@ -38,6 +38,7 @@ EXPORTS = [
     "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
     "mt_batch_download_log", "mt_batch_doc_counters", "mt_batch_device_digests", "mt_batch_snapshots",
     "mt_doc_snapshot_v1_device", "mt_batch_snapshot_index", "mt_batch_snapshot_copy", "mt_batch_launch_info",
+    "mt_batch_snapshot_digests",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -132,6 +133,7 @@ def lib():
     L.mt_doc_snapshot_v1_device.argtypes = [vp, i64, P(i32)]
     L.mt_batch_snapshot_index.argtypes = [vp, vp, vp]
     L.mt_batch_snapshot_copy.argtypes = [vp, vp, i32]
+    L.mt_batch_snapshot_digests.argtypes = [vp, vp, i32]
     _lib = L
     return L
 
@@ -341,6 +343,19 @@ class ReplayBatch:
         total, ms = C.c_int64(0), C.c_float(0)
         _chk(lib().mt_batch_snapshots(self.h, C.byref(total), C.byref(ms)), "mt_batch_snapshots")
         return {"bytes": int(total.value), "device_ms": float(ms.value)}
+
+    def snapshot_digests(self, out=None):
+        """Per-document 64-bit digests of the GPU SnapshotV1 bytes (mt_batch_snapshot_digests);
+        out: None -> numpy uint64, or a contiguous 8-byte torch tensor of n_docs (filled)."""
+        if out is None:
+            a = np.zeros(self.n_docs, np.uint64)
+            _chk(lib().mt_batch_snapshot_digests(self.h, a.ctypes.data, 0), "mt_batch_snapshot_digests")
+            return a
+        if out.numel() != self.n_docs or out.element_size() != 8 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous 8-byte tensor of n_docs elements")
+        _chk(lib().mt_batch_snapshot_digests(self.h, out.data_ptr(), 1 if out.is_cuda else 0),
+             "mt_batch_snapshot_digests")
+        return out
 
     def snapshot_buffer(self):
         """(bytes, doc_off[n_docs+1], meta[n_docs, SNAP_META]) of the last snapshots() call."""

@@ -17,16 +17,20 @@ def shard(rank: int, docs_per_rank: int) -> int:
     return rank * docs_per_rank
 
 
-def gather_results(digests, statuses, world: int, rank: int):
-    """Gather per-document (digest, status) to rank 0.
+def gather_results(digests, statuses, world: int, rank: int, snapshot_digests=None):
+    """Gather per-document (digest, status[, SnapshotV1 digest]) to rank 0.
 
-    digests: int64 tensor [D] (uint64 digests viewed as int64), statuses: int tensor [D], both
-    on the backend's device.  Returns (digests uint64 [W*D], statuses int32 [W*D]) in global
-    document order on rank 0, None on the other ranks."""
+    digests: int64 tensor [D] (uint64 digests viewed as int64), statuses: int tensor [D],
+    snapshot_digests: optional int64 tensor [D] (mt_batch_snapshot_digests), all on the
+    backend's device.  Returns (digests uint64 [W*D], statuses int32 [W*D][, snapshot digests
+    uint64 [W*D]]) in global document order on rank 0, None on the other ranks."""
     import torch
     import torch.distributed as dist
 
-    rec = torch.stack([digests.to(torch.int64), statuses.to(torch.int64)], 1).contiguous()
+    cols = [digests.to(torch.int64), statuses.to(torch.int64)]
+    if snapshot_digests is not None:
+        cols.append(snapshot_digests.to(torch.int64))
+    rec = torch.stack(cols, 1).contiguous()
     if world == 1:
         parts = [rec]
     else:
@@ -35,4 +39,7 @@ def gather_results(digests, statuses, world: int, rank: int):
     if rank != 0:
         return None
     allr = torch.cat(parts, 0).cpu().numpy()
-    return allr[:, 0].view(np.uint64).copy(), allr[:, 1].astype(np.int32)
+    out = (allr[:, 0].copy().view(np.uint64), allr[:, 1].astype(np.int32))
+    if snapshot_digests is not None:
+        out += (allr[:, 2].copy().view(np.uint64),)
+    return out

@@ -154,6 +154,10 @@ MT_API int mt_doc_snapshot_v1_device(mt_batch *b, int64_t doc, int32_t *n_blobs)
 /* doc_off[n_docs + 1] byte offsets; blob_meta[n_docs * MT_SNAP_META] (either may be NULL) */
 MT_API int mt_batch_snapshot_index(mt_batch *b, int64_t *doc_off, int32_t *blob_meta);
 MT_API int mt_batch_snapshot_copy(mt_batch *b, void *dst, int32_t dst_is_device);
+/* per-document 64-bit digest of the GPU SnapshotV1 bytes (all blobs in order; 0 for a document
+   left to the host serializer), into dst[n_docs] (device pointer when dst_is_device) — with
+   mt_batch_device_digests, the per-document summary rank 0 gathers (config 5) */
+MT_API int mt_batch_snapshot_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_device);
 MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out);
 /* per-document device digests of the last run into dst[n_docs] (a device pointer when
    dst_is_device, else host memory) */

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+from snapdigest import bytes_digest
 import fluidframework_amd as fa
 
 pytestmark = pytest.mark.gpu
@@ -145,3 +146,14 @@ def test_snapshot_after_capacity_escalation():
     with b:
         assert b.stats()["launches"] > 1
         _check_batch(b)
+
+
+def test_snapshot_digests_cover_all_blobs():
+    b, _ = _gen(O.gen_params(1500, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35, seed=15), 96)
+    with b:
+        b.snapshots()
+        dig = b.snapshot_digests()
+        for i in range(b.n_docs):
+            blobs = b.doc(i).snapshot_v1()
+            assert int(dig[i]) == bytes_digest("".join(blobs.values()).encode("utf-8")), i
+        assert len(set(dig.tolist())) == b.n_docs

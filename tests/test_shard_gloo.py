@@ -11,6 +11,7 @@ import torch.multiprocessing as mp
 
 import oracle_ffi as O
 from fluidframework_amd import shard
+from snapdigest import bytes_digest
 
 WORLD, DOCS, OPS = 2, 6, 300
 
@@ -24,8 +25,11 @@ def _free_port():
 def _replay(first, n):
     p = O.gen_params(OPS, pct_insert=55, pct_remove=35, seed=0x5EED)
     ops, text, props, off = O.gen_batch(p, n, first_doc=first)
-    _, dig, st = O.replay_batch(ops, off, text, props, O.gen_tables(), O.gen_client_names(8), n_threads=1)
-    return dig, st
+    t, names = O.gen_tables(), O.gen_client_names(8)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names, n_threads=1)
+    snap = np.array([bytes_digest("".join(O.replay_doc(ops[off[d]:off[d + 1]].copy(), text, props, t, names)
+                                          .snapshot_v1().values()).encode("utf-8")) for d in range(n)], np.uint64)
+    return dig, st, snap
 
 
 def _rank(rank, port, out_path):
@@ -34,10 +38,11 @@ def _rank(rank, port, out_path):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-    dig, st = _replay(shard.shard(rank, DOCS), DOCS)
-    res = shard.gather_results(torch.from_numpy(dig.view(np.int64)), torch.from_numpy(st), WORLD, rank)
+    dig, st, snap = _replay(shard.shard(rank, DOCS), DOCS)
+    res = shard.gather_results(torch.from_numpy(dig.view(np.int64)), torch.from_numpy(st), WORLD, rank,
+                               torch.from_numpy(snap.view(np.int64)))
     if rank == 0:
-        np.savez(out_path, dig=res[0], st=res[1])
+        np.savez(out_path, dig=res[0], st=res[1], snap=res[2])
     else:
         assert res is None
     dist.destroy_process_group()
@@ -47,9 +52,10 @@ def test_gather_over_gloo_equals_single_process(tmp_path):
     out = tmp_path / "gathered.npz"
     mp.spawn(_rank, args=(_free_port(), str(out)), nprocs=WORLD, join=True)
     got = np.load(out)
-    dig, st = _replay(0, WORLD * DOCS)
+    dig, st, snap = _replay(0, WORLD * DOCS)
     assert (got["st"] == st).all() and (st == 0).all()
     assert (got["dig"] == dig).all()
+    assert (got["snap"] == snap).all()
     assert len(set(got["dig"].tolist())) == WORLD * DOCS  # documents differ: the shards are disjoint
 
 
