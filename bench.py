@@ -30,6 +30,10 @@ CONFIGS = {
             workload="configs[1]: 4,096 docs x 2k text-only insert/removeRange ops, 8 clients, refSeq lag<=32"),
     3: dict(docs=8192, ops=10000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35,
             workload="configs[2] mix: docs x 10k ops, 10% annotate, minSeq advance/zamboni, 8 clients"),
+    4: dict(docs=16384, ops=200000, ops_min=1000, zipf_s=1.1, n_clients=8, max_lag=32, pct_insert=70, pct_remove=20,
+            workload="configs[3]: Zipf(s=1.1) document sizes by rank over [1k, 200k] ops (70/20/10 mix), "
+                     "16,384 docs per GPU, LPT-balanced across GPUs, largest documents through the LDS ladder "
+                     "and the HBM spill class"),
     5: dict(docs=131072, ops=2000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35, snapshot=True,
             workload="configs[4]: 1M docs over 8 GPUs (131,072 per GPU) x 2k ops (10% annotate), full replay + "
                      "SnapshotV1 of every doc on the GPU in each step, digests gathered to rank 0"),
@@ -80,13 +84,28 @@ def main():
                       pct_remove=cfg["pct_remove"], seed=args.seed)
     from fluidframework_amd import shard
 
-    doc_first = shard.shard(rank, n_docs)  # disjoint shard of the global document space
+    sizes = None
+    if "zipf_s" in cfg:  # config 4: Zipf sizes over the global documents, LPT across ranks
+        all_sizes = shard.zipf_sizes(n_docs * world, cfg["ops_min"], n_ops, cfg["zipf_s"])
+        parts, loads = shard.lpt(all_sizes, world)
+        my_docs = parts[rank]
+        sizes = all_sizes[my_docs]
+        counts = [len(q) for q in parts]
+        total_ops_step = int(all_sizes.sum())
+        n_docs = len(my_docs)
+    else:
+        doc_first = shard.shard(rank, n_docs)  # disjoint shard of the global document space
+        counts = None
+        total_ops_step = n_ops * n_docs * world
 
     b = fa.ReplayBatch(n_docs)
     t0 = time.time()
-    b.generate(p, doc_first)  # synthesize this rank's logs on the GPU (untimed)
+    if sizes is not None:
+        b.generate_docs(p, my_docs, sizes)
+    else:
+        b.generate(p, doc_first)  # synthesize this rank's logs on the GPU (untimed)
     gen_s = time.time() - t0
-    log(rank, f"generated {n_docs} docs x {n_ops} ops in {gen_s:.1f} s")
+    log(rank, f"generated {n_docs} docs, {int(b.stats()['n_ops'])} ops in {gen_s:.1f} s")
     stream = torch.cuda.current_stream().cuda_stream
 
     with_snap = args.snapshot or cfg.get("snapshot", False)
@@ -103,9 +122,11 @@ def main():
     for i in range(args.steps):
         b.run(stream)
         kernel_ms.append(b.stats()["kernel_ms"])
-        l0 = b.launches()[0]  # the dominant kernel: the launch that holds every document
+        # the dominant kernel: the launch that applied the most ops (launch 0 in uniform batches)
+        l0 = max(b.launches(), key=lambda li: li["ops"])
         first_ms.append(l0["ms"])
         first_ops.append(l0["ops"])
+        dom_class = l0["seg_class"]
         if with_snap:  # SnapshotV1 of every document, part of the step
             sn = b.snapshots()
             snap_ms.append(sn["device_ms"])
@@ -141,7 +162,7 @@ def main():
         b.snapshot_digests(snap_t)
         torch.cuda.synchronize()
         tg = time.perf_counter()
-    gathered = shard.gather_results(dig_t, st_t, world, rank, snap_t)
+    gathered = shard.gather_results(dig_t, st_t, world, rank, snap_t, counts)
     torch.cuda.synchronize()
     gather_ms = 1e3 * (time.perf_counter() - tg)
     all_ok, digest_xor, snap_xor = 0, None, None
@@ -151,7 +172,7 @@ def main():
         digest_xor = f"{int(np.bitwise_xor.reduce(all_dig)):016x}"
         if with_snap:
             snap_xor = f"{int(np.bitwise_xor.reduce(gathered[2])):016x}"
-    total_ops = n_ops * n_docs * world * args.steps
+    total_ops = total_ops_step * args.steps
     value = total_ops / t_max
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     alg_bytes = b.algorithmic_bytes()
@@ -162,11 +183,11 @@ def main():
     first_bytes = alg_bytes * (sum(first_ops) / len(first_ops)) / max(1, ops_done)
     achieved_gbs = first_bytes / (avg_first_ms * 1e-3) / 1e9
 
-    traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, f"mt_replay_kernel_{st['lds_class']}")
+    traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, f"mt_replay_kernel_{dom_class}")
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
-        cpu, parity = cpu_baseline(b, fa, n_docs, n_ops, args)
+        cpu, parity = cpu_baseline(b, fa, n_docs, args)
     snapshot = None
     if with_snap:
         avg_snap = sum(snap_ms) / len(snap_ms)
@@ -191,14 +212,16 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (GPU-generated conflict-farm logs, include/mt_gen.h)",
-            "config": {"workload": cfg["workload"], "docs_per_gpu": n_docs, "ops_per_doc": n_ops,
+            "config": {"workload": cfg["workload"], "docs_per_gpu": n_docs,
+                       "ops_per_doc": n_ops if sizes is None else {"min": int(sizes.min()), "max": int(sizes.max()),
+                                                                  "lpt_loads": loads},
                        "clients": cfg["n_clients"], "max_lag": cfg["max_lag"],
                        "op_mix": [cfg["pct_insert"], cfg["pct_remove"], 100 - cfg["pct_insert"] - cfg["pct_remove"]],
                        "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": f"mt_replay_kernel_{st['lds_class']}", "avg_launch_ms": round(avg_first_ms, 3),
+                         "kernel": f"mt_replay_kernel_{dom_class}", "avg_launch_ms": round(avg_first_ms, 3),
                          "algorithmic_bytes_per_launch": int(first_bytes),
                          "ops_per_launch": int(sum(first_ops) / len(first_ops))},
             "replay_ms_per_step": round(avg_kernel_ms, 3),
@@ -207,7 +230,7 @@ def main():
             "parity": parity,
             "snapshot": snapshot,
             "docs_ok": all_ok,
-            "digests_gathered": world * n_docs,
+            "digests_gathered": len(gathered[0]) if rank == 0 else None,
             "digest_xor": digest_xor,
             "snapshot_digest_xor": snap_xor,
             "ops_applied_per_step": int(ops_done),
@@ -243,17 +266,21 @@ def log(rank, msg):
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(b, fa, n_docs, n_ops, args):
+def cpu_baseline(b, fa, n_docs, args):
     """Oracle (CPU restatement, tests-only code) on a bounded sample of the same logs,
-    timed on this host's cores; its per-doc digests double as a parity spot check."""
+    timed on this host's cores; its per-doc digests double as a parity spot check.
+    Sample: the first documents of this rank's batch up to ~8.2M ops (config 2's size)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import numpy as np
 
     import oracle_ffi as O
 
-    sample = args.cpu_sample_docs or max(16, min(n_docs, int(4096 * 2000 / max(1, n_ops))))
-    sample = min(sample, n_docs)
     ops, off, text, props = b.download_log()
+    if args.cpu_sample_docs:
+        sample = min(args.cpu_sample_docs, n_docs)
+    else:
+        sample = int(np.searchsorted(off, 4096 * 2000, side="left"))
+        sample = min(n_docs, max(16, sample))
     end = off[sample]
     sops = ops[:end].copy()
     soff = off[: sample + 1].copy()
@@ -262,8 +289,8 @@ def cpu_baseline(b, fa, n_docs, n_ops, args):
     secs, dig, st = O.replay_batch(sops, soff, text, props, tables, names, n_threads=threads)
     gpu_dig = np.array([b.doc(d).digest() for d in range(sample)], np.uint64)
     match = int((gpu_dig == dig).sum())
-    cpu = {"value": round(sample * n_ops / secs, 1), "unit": "ops/s", "cores": threads, "kind": "port",
-           "sample": f"first {sample} docs x {n_ops} ops of the same log, oracle/ C restatement, {threads} threads",
+    cpu = {"value": round(int(end) / secs, 1), "unit": "ops/s", "cores": threads, "kind": "port",
+           "sample": f"first {sample} docs ({int(end)} ops) of the same log, oracle/ C restatement, {threads} threads",
            "seconds": round(secs, 3)}
     parity = {"docs_checked": sample, "digest_match": match, "oracle_status_ok": int((st == 0).sum())}
     return cpu, parity

@@ -165,8 +165,10 @@ struct ReplayParams {
     int32_t out_cap;
     // generator mode (non-null gen): ops/text/props are written, not read
     const void *gen;              // mt_gen_params*
-    void *gen_ops;                // mt_op[n_docs * n_ops]
-    void *gen_props;              // mt_prop[n_docs * 2 * n_ops] (doc-local offsets rebased by host)
+    void *gen_ops;                // mt_op[], document d's ops at doc_op_off[d]
+    void *gen_props;              // mt_prop[], document d's records at 2 * doc_op_off[d]
+    const int64_t *gen_doc_ids;   // per document: global index seeding its stream (null: doc_first + d)
+    const int32_t *gen_doc_ops;   // per document: ops to generate (null: gen->n_ops)
     uint64_t *prof;               // MT_PROF builds: kProfSlots cycle counters per workgroup
     uint4 *cold;                  // [n_docs * cap.seg] cold segment records {props, ovl, toff, tcap}
     // capacity escalation by checkpoint: a document short of LDS headroom writes its state to

@@ -1896,17 +1896,19 @@ MT_FI void generate_body(const ReplayParams &P) {
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
 #endif
     engine_setup(E, P, w, d, smem);
-    mt_op *ops_out = (mt_op *)P.gen_ops + d * (int64_t)g.n_ops;
+    const int64_t op_base = P.doc_op_off[d];
+    const int32_t n_ops = P.gen_doc_ops ? P.gen_doc_ops[d] : g.n_ops;
+    mt_op *ops_out = (mt_op *)P.gen_ops + op_base;
     mt_prop *props_out = (mt_prop *)P.gen_props;
-    const int64_t prop_base = d * (int64_t)(2 * g.n_ops);
+    const int64_t prop_base = 2 * op_base;
     E.props_in = props_out;
-    uint64_t x = mt_rng_seed(g.seed, (uint64_t)(P.doc_first + d));
+    uint64_t x = mt_rng_seed(g.seed, (uint64_t)(P.gen_doc_ids ? P.gen_doc_ids[d] : P.doc_first + d));
     __shared__ int32_t lref[64];  // last refSeq per client (160 B static + 16-aligned dynamic base)
     lref[E.lane] = 0;
     wsync();
     uint32_t pay_top = 0, np = 0;
     int32_t done = 0, fail_op = -1;
-    for (int32_t k = 1; k <= g.n_ops; k++) {
+    for (int32_t k = 1; k <= n_ops; k++) {
         mt_op op;
         op.seq = k;
         int32_t c = 1 + (int32_t)mt_rng_below(&x, (uint32_t)g.n_clients);

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -115,6 +116,8 @@ struct Launch {
     size_t lds = 0;
     float ms = 0;               // device time (hipEvents)
     int64_t ops = 0;            // ops applied by this launch (resumed documents: after their checkpoint)
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int level = 0;              // escalation depth (0: a first launch)
 };
 
 struct DocRes {  // per-document result location
@@ -321,9 +324,13 @@ struct mt_batch {
     std::vector<DocRes> where;
     std::vector<DocOut> docout;  // gathered per doc
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent first launches of mixed-size batches
+    hipStream_t cstream = nullptr;  // result gathers (never queued behind a running launch)
+    hipEvent_t ev_user = nullptr;
     uint64_t *d_digest = nullptr;  // mt_batch_device_digests
     float kernel_ms = 0, total_ms = 0;
     bool ran = false;
+    int n_first = 0;  // launches of mt_batch_launch (the rest are escalations)
     hipStream_t run_stream = nullptr;
     std::chrono::steady_clock::time_point t_launch;
     // single-document result cache
@@ -365,6 +372,8 @@ static void free_launches(mt_batch *b) {
         (void)hipFree(L.d_ck);
         (void)hipFree(L.d_cksrc);
         (void)hipFree(L.d_state);
+        if (L.e0) (void)hipEventDestroy(L.e0);
+        if (L.e1) (void)hipEventDestroy(L.e1);
     }
     b->launches.clear();
 }
@@ -444,6 +453,10 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     (void)hipFree(b->d_vflags);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
     if (b->ev1) (void)hipEventDestroy(b->ev1);
+    for (hipStream_t a : b->aux)
+        if (a) (void)hipStreamDestroy(a);
+    if (b->cstream) (void)hipStreamDestroy(b->cstream);
+    if (b->ev_user) (void)hipEventDestroy(b->ev_user);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }
@@ -713,22 +726,72 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     return MT_OK;
 }
 
+// initial capacity class of every document from its own op count; documents of one class
+// form one launch (the HBM class in chunks of kMaxHbmDocs), largest documents first within a
+// launch (blocks dispatch roughly in index order: the longest serial replays start first).
+// Launches of different classes run concurrently on the run stream and up to 3 aux streams.
 MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
     if (!b || !b->have_log) return MT_ERR_STATE;
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->stream;
+    // launches go to the batch's own non-blocking streams, ordered after the caller's stream
+    hipStream_t s = b->stream;
+    if (hip_stream && (hipStream_t)hip_stream != s) {
+        if (!b->ev_user) HIPCHK(hipEventCreateWithFlags(&b->ev_user, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(b->ev_user, (hipStream_t)hip_stream));
+        HIPCHK(hipStreamWaitEvent(s, b->ev_user, 0));
+    }
     free_launches(b);
     b->snap_ready = false;  // buffers are kept for the next mt_batch_snapshots
     b->ran = false;
     b->cached_doc = -1;
     b->c_blob_doc = -1;
     b->t_launch = std::chrono::steady_clock::now();
-    Launch L;
-    L.cls = std::min(class_for(b, b->max_ops_per_doc, 0), mt::kNumClasses - 1);
-    while (L.cls > 0 && class_lds(L.cls) > (size_t)max_lds_bytes()) L.cls--;
-    b->launches.push_back(L);
+    std::map<int, std::vector<int32_t>, std::greater<int>> groups;
+    for (int64_t d = 0; d < b->n_docs; d++) {
+        // documents start in LDS (the largest LDS class at most: a document reaches the HBM
+        // class only through a checkpoint, after its first ops ran at LDS speed)
+        int c = std::min(class_for(b, (int32_t)(b->h_off[d + 1] - b->h_off[d]), 0), mt::kHbmClass - 1);
+        while (c > 0 && !class_usable(c)) c--;
+        groups[c].push_back((int32_t)d);
+    }
+    for (auto &g : groups) {
+        const int cls = g.first;
+        std::vector<int32_t> &docs = g.second;
+        if (groups.size() == 1 && cls != mt::kHbmClass) {
+            Launch L;
+            L.cls = cls;
+            b->launches.push_back(L);  // every document, in index order
+            break;
+        }
+        std::stable_sort(docs.begin(), docs.end(), [&](int32_t x, int32_t y) {
+            return b->h_off[x + 1] - b->h_off[x] > b->h_off[y + 1] - b->h_off[y];
+        });
+        const size_t chunk = cls == mt::kHbmClass ? kMaxHbmDocs : docs.size();
+        for (size_t at = 0; at < docs.size(); at += chunk) {
+            Launch L;
+            L.cls = cls;
+            L.docs.assign(docs.begin() + at, docs.begin() + std::min(docs.size(), at + chunk));
+            b->launches.push_back(std::move(L));
+        }
+    }
     HIPCHK(hipEventRecord(b->ev0, s));
-    int rc = launch_replay(b, s, b->launches.back());
-    if (rc) return rc;
+    for (size_t i = 0; i < b->launches.size(); i++) {
+        Launch &L = b->launches[i];
+        hipStream_t ls = s;
+        if (i > 0) {
+            hipStream_t &a = b->aux[(i - 1) % 3];
+            if (!a) HIPCHK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+            HIPCHK(hipStreamWaitEvent(a, b->ev0, 0));
+            ls = a;
+        }
+        HIPCHK(hipEventCreate(&L.e0));
+        HIPCHK(hipEventCreate(&L.e1));
+        HIPCHK(hipEventRecord(L.e0, ls));
+        int rc = launch_replay(b, ls, L);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(L.e1, ls));
+        if (ls != s) HIPCHK(hipStreamWaitEvent(s, L.e1, 0));
+    }
+    b->n_first = (int)b->launches.size();
     HIPCHK(hipEventRecord(b->ev1, s));
     b->run_stream = s;
     return MT_OK;
@@ -754,7 +817,9 @@ static int gather_launch(mt_batch *b, int li) {
     }
 #endif
     std::vector<DocOut> tmp((size_t)n);
-    HIPCHK(hipMemcpy(tmp.data(), L.d_docout, sizeof(DocOut) * (size_t)n, hipMemcpyDeviceToHost));
+    if (!b->cstream) HIPCHK(hipStreamCreateWithFlags(&b->cstream, hipStreamNonBlocking));
+    HIPCHK(hipMemcpyAsync(tmp.data(), L.d_docout, sizeof(DocOut) * (size_t)n, hipMemcpyDeviceToHost, b->cstream));
+    HIPCHK(hipStreamSynchronize(b->cstream));
     if (b->docout.size() != (size_t)b->n_docs) {
         b->docout.assign((size_t)b->n_docs, DocOut{});
         b->where.assign((size_t)b->n_docs, DocRes{});
@@ -771,67 +836,103 @@ static int gather_launch(mt_batch *b, int li) {
     return MT_OK;
 }
 
+// Capacity escalation, scheduled as launches complete: a checkpointed document resumes, a
+// document that overflowed mid-op re-runs from scratch, both in the next class with >= 1.2x the
+// slots (docs per CU matter more than the number of resumes: each resume costs one LDS image
+// round trip to HBM).  When a launch finishes, its escalated documents are grouped by target
+// class and launched at once on the next of the run / aux streams, so a large document's chain
+// of classes never waits for unrelated launches (mixed-size batches, config 4).
+static int launch_on(mt_batch *b, Launch &&L, int *next_stream, std::vector<int> &pending) {
+    if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) L.cksrc.clear();
+    b->launches.push_back(std::move(L));
+    const int li = (int)b->launches.size() - 1;
+    Launch &N = b->launches.back();
+    const int k = (*next_stream)++ % 4;
+    hipStream_t s = b->run_stream;
+    if (k > 0) {
+        hipStream_t &a = b->aux[k - 1];
+        if (!a) HIPCHK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+        s = a;
+    }
+    HIPCHK(hipEventCreate(&N.e0));
+    HIPCHK(hipEventCreate(&N.e1));
+    HIPCHK(hipEventRecord(N.e0, s));
+    int rc = launch_replay(b, s, N);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(N.e1, s));
+    pending.push_back(li);
+    return MT_OK;
+}
+
 MT_API int mt_batch_sync(mt_batch *b) {
     if (!b || b->launches.empty()) return MT_ERR_STATE;
-    HIPCHK(hipEventSynchronize(b->ev1));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-    b->kernel_ms = ms;
-    b->launches[0].ms = ms;
-    int rc = gather_launch(b, 0);
-    if (rc) return rc;
-    // capacity escalation: a checkpointed document resumes, a document that overflowed mid-op
-    // re-runs from scratch, both in the next class with >= 1.2x the slots (docs per CU matter
-    // more than the number of resumes: each resume costs one LDS image round trip to HBM).
-    // One launch per (source launch, target class).
-    std::vector<int> frontier{0};
-    for (int level = 1; level <= b->opt.max_retries && !frontier.empty(); level++) {
-        std::map<std::pair<int, int>, Launch> groups;
-        for (int64_t d = 0; d < b->n_docs; d++) {
-            const DocOut &o = b->docout[d];
-            const int li = b->where[d].launch;
-            if (o.status != MT_CAPACITY || std::find(frontier.begin(), frontier.end(), li) == frontier.end()) continue;
-            const Launch &S = b->launches[(size_t)li];
-            int cls;
-            int32_t src;
-            if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) {
-                cls = resume_class(S.cls);
-                src = b->where[d].idx;
-            } else if (o.cap_kind == 1 || o.cap_kind == 4) {
-                cls = resume_class(S.cls);
-                src = -1;
-            } else {
-                continue;
+    std::vector<int> pending;
+    for (int li = 0; li < b->n_first; li++) pending.push_back(li);
+    int next_stream = 1, rc = MT_OK;
+    while (!pending.empty()) {
+        size_t k = 0;
+        for (;; std::this_thread::sleep_for(std::chrono::microseconds(20))) {
+            for (k = 0; k < pending.size(); k++) {
+                hipError_t q = hipEventQuery(b->launches[(size_t)pending[k]].e1);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) HIPCHK(q);
             }
+            if (k < pending.size()) break;
+        }
+        const int li = pending[k];
+        pending.erase(pending.begin() + (long)k);
+        {
+            Launch &L = b->launches[(size_t)li];
+            HIPCHK(hipEventElapsedTime(&L.ms, L.e0, L.e1));
+        }
+        rc = gather_launch(b, li);
+        if (rc) return rc;
+        const Launch &S = b->launches[(size_t)li];
+        if (S.level >= b->opt.max_retries) continue;
+        const int64_t n = S.docs.empty() ? b->n_docs : (int64_t)S.docs.size();
+        std::map<int, Launch> groups;
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
+            const DocOut &o = b->docout[d];
+            if (o.status != MT_CAPACITY || b->where[d].launch != li) continue;
+            int32_t src;
+            if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) src = (int32_t)i;
+            else if (o.cap_kind == 1 || o.cap_kind == 4) src = -1;
+            else continue;
+            int cls = resume_class(S.cls);
             while (cls > S.cls + 1 && !class_usable(cls)) cls--;
             if (!class_usable(cls)) continue;  // largest class reached: the document keeps MT_CAPACITY
-            if (cls == mt::kHbmClass && (groups.count({li, cls}) ? groups[{li, cls}].docs.size() : 0) >= kMaxHbmDocs)
-                continue;  // the HBM class holds ~6 MB per document: bounded
-            Launch &L = groups[{li, cls}];
+            Launch &L = groups[cls];
             L.cls = cls;
             L.src = li;
+            L.level = S.level + 1;
             L.docs.push_back((int32_t)d);
             L.cksrc.push_back(src);
         }
-        frontier.clear();
         for (auto &kv : groups) {
-            Launch L = std::move(kv.second);
-            if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) L.cksrc.clear();
-            b->launches.push_back(std::move(L));
-            const int li = (int)b->launches.size() - 1;
-            HIPCHK(hipEventRecord(b->ev0, b->run_stream));
-            rc = launch_replay(b, b->run_stream, b->launches.back());
-            if (rc) return rc;
-            HIPCHK(hipEventRecord(b->ev1, b->run_stream));
-            HIPCHK(hipEventSynchronize(b->ev1));
-            HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-            b->kernel_ms += ms;
-            b->launches[(size_t)li].ms = ms;
-            rc = gather_launch(b, li);
-            if (rc) return rc;
-            frontier.push_back(li);
+            Launch &G = kv.second;
+            // the HBM class holds ~6 MB of tables per document: bounded launches
+            const size_t chunk = G.cls == mt::kHbmClass ? kMaxHbmDocs : G.docs.size();
+            for (size_t at = 0; at < G.docs.size(); at += chunk) {
+                Launch L;
+                L.cls = G.cls;
+                L.src = G.src;
+                L.level = G.level;
+                const size_t e = std::min(G.docs.size(), at + chunk);
+                L.docs.assign(G.docs.begin() + (long)at, G.docs.begin() + (long)e);
+                L.cksrc.assign(G.cksrc.begin() + (long)at, G.cksrc.begin() + (long)e);
+                rc = launch_on(b, std::move(L), &next_stream, pending);
+                if (rc) return rc;
+            }
         }
     }
+    // device wall time: from the first launch to the last completion
+    float ms = 0, mx = 0;
+    for (const Launch &L : b->launches) {
+        HIPCHK(hipEventElapsedTime(&ms, b->ev0, L.e1));
+        mx = std::max(mx, ms);
+    }
+    b->kernel_ms = mx;
     b->total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count();
     b->ran = true;
     return MT_OK;
@@ -1609,8 +1710,11 @@ static const char *GEN_KEYS[MT_GEN_N_KEYS] = {"bold", "italic", "color", "size"}
 static const char *GEN_CLIENTS[] = {"readonly", "A", "B", "C", "D", "E", "F", "G", "H", "I", "J", "K", "L", "M",
                                     "N", "O", "P", "Q", "R", "S", "T", "U", "V", "W", "X", "Y", "Z"};
 
-MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_first) {
-    if (!b || !p || p->n_ops < 1 || p->n_clients < 1 || p->n_clients > 26 || p->max_insert < 1) return MT_ERR_ARG;
+// generation of D documents: document d has global index doc_ids[d] (its stream's seed) and
+// doc_ops[d] ops; logs are laid out back to back (doc_op_off = prefix sums of doc_ops)
+static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<int64_t> &doc_ids,
+                         const std::vector<int32_t> &doc_ops) {
+    if (!b || !p || p->n_clients < 1 || p->n_clients > 26 || p->max_insert < 1) return MT_ERR_ARG;
     // fixed generator tables (include/mt_gen.h)
     std::vector<std::string> vals = {"null", "true", "\"red\"", "\"green\"", "\"blue\""};
     for (int s = 8; s <= 24; s++) vals.push_back(std::to_string(s));
@@ -1621,33 +1725,44 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
     rc = mt_batch_set_clients(b, -1, GEN_CLIENTS, p->n_clients + 1);
     if (rc) return rc;
     const int64_t D = b->n_docs;
-    const int64_t N = (int64_t)p->n_ops * D;
+    if ((int64_t)doc_ids.size() != D || (int64_t)doc_ops.size() != D) return MT_ERR_ARG;
     free_launches(b);
     free_log(b);
     b->h_off.resize(D + 1);
-    for (int64_t d = 0; d <= D; d++) b->h_off[d] = d * p->n_ops;
+    b->h_off[0] = 0;
+    int32_t max_ops = 0;
+    for (int64_t d = 0; d < D; d++) {
+        if (doc_ops[d] < 1) return MT_ERR_ARG;
+        b->h_off[d + 1] = b->h_off[d] + doc_ops[d];
+        max_ops = std::max(max_ops, doc_ops[d]);
+    }
+    const int64_t N = b->h_off[D];
     b->h_text_base.assign(D, 0);
     b->h_text_len.assign(D, 0);
     b->h_text_cap.assign(D, 0);
     b->h_pool_base.assign(D, 0);
     b->h_pool_cap.assign(D, 0);
-    const uint64_t pay_cap = (uint64_t)p->n_ops * (uint64_t)p->max_insert;
-    const uint64_t cap = align16u(pay_cap) + (uint64_t)b->opt.arena_factor * pay_cap / 2 + 4096;
-    const int64_t ann = (int64_t)p->n_ops * std::max(0, 100 - p->pct_insert - p->pct_remove) / 100;
-    const uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * (uint64_t)(ann + ann / 2 + 16);
-    if (cap > 0xFFFFFFF0ull || pc > 0xFFFFFFF0ull) return MT_ERR_ARG;
+    uint64_t tbase = 0, pbase = 0;
+    const int32_t pct_ann = std::max(0, 100 - p->pct_insert - p->pct_remove);
     for (int64_t d = 0; d < D; d++) {
-        b->h_text_base[d] = (uint64_t)d * align16u(cap);
+        const uint64_t pay_cap = (uint64_t)doc_ops[d] * (uint64_t)p->max_insert;
+        const uint64_t cap = align16u(pay_cap) + (uint64_t)b->opt.arena_factor * pay_cap / 2 + 4096;
+        const int64_t ann = (int64_t)doc_ops[d] * pct_ann / 100;
+        const uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * (uint64_t)(ann + ann / 2 + 16);
+        if (cap > 0xFFFFFFF0ull || pc > 0xFFFFFFF0ull) return MT_ERR_ARG;
+        b->h_text_base[d] = tbase;
         b->h_text_len[d] = (uint32_t)pay_cap;  // payload capacity: the arena starts after it
         b->h_text_cap[d] = (uint32_t)cap;
-        b->h_pool_base[d] = (uint64_t)d * align16u(pc);
+        b->h_pool_base[d] = pbase;
         b->h_pool_cap[d] = (uint32_t)pc;
+        tbase += align16u(cap);
+        pbase += align16u(pc);
     }
-    b->text_words = (uint64_t)D * align16u(cap);
-    b->pool_words = (uint64_t)D * align16u(pc);
+    b->text_words = tbase;
+    b->pool_words = pbase;
     b->total_ops = N;
     b->total_props = 2 * N;
-    b->max_ops_per_doc = p->n_ops;
+    b->max_ops_per_doc = max_ops;
     int rc2 = ensure_tables(b);
     if (rc2) return rc2;
     HIPCHK(dalloc(&b->d_ops, (size_t)N));
@@ -1666,65 +1781,84 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
     HIPCHK(hipMemcpy(b->d_text_cap, b->h_text_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_pool_base, b->h_pool_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_pool_cap, b->h_pool_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    int64_t *d_ids = nullptr;
+    int32_t *d_nops = nullptr;
+    HIPCHK(dalloc(&d_ids, (size_t)D));
+    HIPCHK(dalloc(&d_nops, (size_t)D));
+    HIPCHK(hipMemcpy(d_ids, doc_ids.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_nops, doc_ops.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
     mt_gen_params *d_gen = nullptr;
     HIPCHK(dalloc(&d_gen, 1));
     HIPCHK(hipMemcpy(d_gen, p, sizeof(mt_gen_params), hipMemcpyHostToDevice));
-    // generation runs in the replay's capacity class; documents that overflow it are
+    // generation runs in each document's initial replay class; documents that overflow it are
     // generated again (deterministically, from their own seed) in the next larger class
     std::vector<DocOut> outs((size_t)D);
-    std::vector<int32_t> todo;
-    int cls = std::min(class_for(b, p->n_ops, 0), mt::kNumClasses - 1);
-    while (cls > 0 && class_lds(cls) > (size_t)max_lds_bytes()) cls--;
-    for (;; cls++) {
-        const int64_t n = todo.empty() ? D : (int64_t)todo.size();
-        Launch L;
-        L.cls = cls;
-        L.caps = mt::class_caps(mt::kClassSegs[cls]);
-        L.out_cap = L.caps.oe;
-        L.lds = class_lds(cls);
-        HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
-        HIPCHK(dalloc(&L.d_docout, (size_t)n));
-        HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg));
-        if (class_state_bytes(cls)) HIPCHK(dalloc(&L.d_state, (size_t)n * class_state_bytes(cls)));
-        if (!todo.empty()) {
-            HIPCHK(dalloc(&L.d_list, todo.size()));
-            HIPCHK(hipMemcpy(L.d_list, todo.data(), 4 * todo.size(), hipMemcpyHostToDevice));
+    std::map<int, std::vector<int32_t>> work;  // class -> documents
+    for (int64_t d = 0; d < D; d++) {
+        int c = std::min(class_for(b, doc_ops[d], 0), mt::kNumClasses - 1);
+        while (c > 0 && !class_usable(c)) c--;
+        work[c].push_back((int32_t)d);
+    }
+    while (!work.empty()) {
+        const int cls = work.begin()->first;
+        std::vector<int32_t> todo = std::move(work.begin()->second);
+        work.erase(work.begin());
+        const bool all = (int64_t)todo.size() == D;
+        for (size_t at = 0; at < todo.size();) {
+            // the HBM class holds ~6 MB of tables per document: bounded launches
+            const size_t n = cls == mt::kHbmClass ? std::min(todo.size() - at, kMaxHbmDocs) : todo.size() - at;
+            Launch L;
+            L.cls = cls;
+            L.caps = mt::class_caps(mt::kClassSegs[cls]);
+            L.out_cap = L.caps.oe;
+            L.lds = class_lds(cls);
+            HIPCHK(dalloc(&L.d_out, n * (size_t)L.out_cap));
+            HIPCHK(dalloc(&L.d_docout, n));
+            HIPCHK(dalloc(&L.d_cold, n * (size_t)L.caps.seg));
+            if (class_state_bytes(cls)) HIPCHK(dalloc(&L.d_state, n * class_state_bytes(cls)));
+            if (!all) {
+                HIPCHK(dalloc(&L.d_list, n));
+                HIPCHK(hipMemcpy(L.d_list, todo.data() + at, 4 * n, hipMemcpyHostToDevice));
+            }
+            mt::ReplayParams P = base_params(b);
+            P.out = L.d_out;
+            P.doc_out = L.d_docout;
+            P.n_docs = (int64_t)n;
+            P.doc_first = 0;
+            P.doc_list = L.d_list;
+            P.out_cap = L.out_cap;
+            P.gen = d_gen;
+            P.gen_ops = b->d_ops;
+            P.gen_props = b->d_props;
+            P.gen_doc_ids = d_ids;
+            P.gen_doc_ops = d_nops;
+            P.cold = L.d_cold;
+            P.hbm_state = L.d_state;
+            const void *fn = kKernels[cls].generate;
+            if (L.lds > 64 * 1024)
+                HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
+            void *args[] = {&P};
+            HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, b->stream));
+            HIPCHK(hipStreamSynchronize(b->stream));
+            std::vector<DocOut> part(n);
+            HIPCHK(hipMemcpy(part.data(), L.d_docout, sizeof(DocOut) * n, hipMemcpyDeviceToHost));
+            (void)hipFree(L.d_out);
+            (void)hipFree(L.d_docout);
+            (void)hipFree(L.d_list);
+            (void)hipFree(L.d_cold);
+            (void)hipFree(L.d_state);
+            for (size_t i = 0; i < n; i++) {
+                const int32_t d = todo[at + i];
+                outs[(size_t)d] = part[i];
+                if (part[i].status == MT_CAPACITY && part[i].cap_kind == 1 && class_usable(cls + 1))
+                    work[cls + 1].push_back(d);
+            }
+            at += n;
         }
-        mt::ReplayParams P = base_params(b);
-        P.out = L.d_out;
-        P.doc_out = L.d_docout;
-        P.n_docs = n;
-        P.doc_first = doc_first;
-        P.doc_list = L.d_list;
-        P.out_cap = L.out_cap;
-        P.gen = d_gen;
-        P.gen_ops = b->d_ops;
-        P.gen_props = b->d_props;
-        P.cold = L.d_cold;
-        P.hbm_state = L.d_state;
-        const void *fn = kKernels[cls].generate;
-        if (L.lds > 64 * 1024)
-            HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
-        void *args[] = {&P};
-        HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, b->stream));
-        HIPCHK(hipStreamSynchronize(b->stream));
-        std::vector<DocOut> part((size_t)n);
-        HIPCHK(hipMemcpy(part.data(), L.d_docout, sizeof(DocOut) * (size_t)n, hipMemcpyDeviceToHost));
-        (void)hipFree(L.d_out);
-        (void)hipFree(L.d_docout);
-        (void)hipFree(L.d_list);
-        (void)hipFree(L.d_cold);
-        (void)hipFree(L.d_state);
-        std::vector<int32_t> again;
-        for (int64_t i = 0; i < n; i++) {
-            const int64_t d = todo.empty() ? i : todo[(size_t)i];
-            outs[(size_t)d] = part[(size_t)i];
-            if (part[(size_t)i].status == MT_CAPACITY && part[(size_t)i].cap_kind == 1) again.push_back((int32_t)d);
-        }
-        if (again.empty() || cls + 1 >= mt::kNumClasses || class_lds(cls + 1) > (size_t)max_lds_bytes()) break;
-        todo.swap(again);
     }
     (void)hipFree(d_gen);
+    (void)hipFree(d_ids);
+    (void)hipFree(d_nops);
     b->payload_units = 0;
     b->prop_records = 0;
     int bad = 0;
@@ -1741,6 +1875,20 @@ MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_fi
         return MT_INTERNAL;
     }
     return MT_OK;
+}
+
+MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_first) {
+    if (!b || !p || p->n_ops < 1) return MT_ERR_ARG;
+    std::vector<int64_t> ids((size_t)b->n_docs);
+    for (int64_t d = 0; d < b->n_docs; d++) ids[(size_t)d] = doc_first + d;
+    return generate_docs(b, p, ids, std::vector<int32_t>((size_t)b->n_docs, p->n_ops));
+}
+
+MT_API int mt_batch_generate_docs(mt_batch *b, const mt_gen_params *p, const int64_t *doc_ids,
+                                  const int32_t *doc_ops) {
+    if (!b || !p || !doc_ids || !doc_ops) return MT_ERR_ARG;
+    return generate_docs(b, p, std::vector<int64_t>(doc_ids, doc_ids + b->n_docs),
+                         std::vector<int32_t>(doc_ops, doc_ops + b->n_docs));
 }
 
 }  // extern "C"

@@ -38,7 +38,7 @@ EXPORTS = [
     "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
     "mt_batch_download_log", "mt_batch_doc_counters", "mt_batch_device_digests", "mt_batch_snapshots",
     "mt_doc_snapshot_v1_device", "mt_batch_snapshot_index", "mt_batch_snapshot_copy", "mt_batch_launch_info",
-    "mt_batch_snapshot_digests",
+    "mt_batch_snapshot_digests", "mt_batch_generate_docs",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -112,6 +112,7 @@ def lib():
     L.mt_batch_set_clients.argtypes = [vp, i64, P(cp), i32]
     L.mt_batch_ingest.argtypes = [vp, vp, vp, vp, i64, vp, i64]
     L.mt_batch_generate.argtypes = [vp, P(GenParams), i64]
+    L.mt_batch_generate_docs.argtypes = [vp, P(GenParams), vp, vp]
     L.mt_batch_run.argtypes = [vp, vp]
     L.mt_batch_launch.argtypes = [vp, vp]
     L.mt_batch_sync.argtypes = [vp]
@@ -283,6 +284,15 @@ class ReplayBatch:
 
     def generate(self, params: GenParams, doc_first: int = 0):
         _chk(lib().mt_batch_generate(self.h, C.byref(params), doc_first), "mt_batch_generate")
+
+    def generate_docs(self, params: GenParams, doc_ids, doc_ops):
+        """Generate documents with the given global indices and op counts (params.n_ops unused)."""
+        ids = np.ascontiguousarray(doc_ids, np.int64)
+        ops = np.ascontiguousarray(doc_ops, np.int32)
+        if len(ids) != self.n_docs or len(ops) != self.n_docs:
+            raise ValueError("doc_ids / doc_ops must have n_docs entries")
+        _chk(lib().mt_batch_generate_docs(self.h, C.byref(params), ids.ctypes.data, ops.ctypes.data),
+             "mt_batch_generate_docs")
 
     # -- run
     def run(self, stream=None):

@@ -108,6 +108,10 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
                            int64_t n_text, const mt_prop *props, int64_t n_props);
 /* synthesize logs on the device (include/mt_gen.h); doc_first = global index of doc 0 */
 MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_first);
+/* the same with per-document global indices (stream seeds) and op counts (p->n_ops ignored):
+   mixed-size batches, e.g. config 4's Zipf sizes after LPT assignment to this GPU */
+MT_API int mt_batch_generate_docs(mt_batch *b, const mt_gen_params *p, const int64_t *doc_ids,
+                                  const int32_t *doc_ops);
 
 /* launch the replay on `hip_stream` (NULL = the batch's own stream) and wait for it */
 MT_API int mt_batch_run(mt_batch *b, void *hip_stream);

@@ -237,3 +237,38 @@ def test_hbm_class_spills_documents_beyond_lds():
             assert b.doc(d).digest() == int(dig[d])
         od = O.replay_doc(ops[off[0]:off[1]].copy(), text, props, t, names)
         assert b.doc(0).snapshot_v1() == od.snapshot_v1()
+
+
+def test_mixed_size_batch_generate_docs_and_concurrent_classes():
+    """Config 4 machinery on a small scale: per-document sizes and global ids
+    (mt_batch_generate_docs == the oracle generator), first launches grouped by capacity class
+    and run concurrently (largest documents first), LPT order, parity of every document."""
+    from fluidframework_amd import shard
+
+    sizes = shard.zipf_sizes(64, 200, 12000, 1.1)
+    parts, _ = shard.lpt(sizes, 2)
+    ids = parts[1]  # rank 1's documents, in decreasing size
+    ops_n = sizes[ids]
+    p = O.gen_params(0, pct_insert=70, pct_remove=20, seed=0x21BF)
+    ops, text, props, off = O.gen_batch(p, len(ids), doc_ids=ids, doc_ops=ops_n)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(len(ids)) as b:
+        b.generate_docs(fa.gen_params(0, pct_insert=70, pct_remove=20, seed=0x21BF), ids, ops_n)
+        gops, goff, gtext, gprops = b.download_log()
+        assert (goff == off).all()
+        for f in ("type", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len"):
+            assert (gops[f] == ops[f]).all(), f
+        ins = gops["type"] == 0
+        g_txt = np.concatenate([gtext[o["payload"]:o["payload"] + o["payload_len"]] for o in gops[ins]])
+        o_txt = np.concatenate([text[o["payload"]:o["payload"] + o["payload_len"]] for o in ops[ins]])
+        assert (g_txt == o_txt).all()
+        b.run()
+        launches = b.launches()
+        assert len({li["seg_class"] for li in launches}) >= 3
+        for d in range(len(ids)):
+            assert b.doc(d).status == st[d]
+            assert b.doc(d).digest() == int(dig[d]), f"doc {d} ({ops_n[d]} ops) digest differs"
+        b.snapshots()
+        for d in range(0, len(ids), 5):
+            assert b.doc(d).snapshot_v1(device=True) == b.doc(d).snapshot_v1()

@@ -62,3 +62,49 @@ def test_gather_over_gloo_equals_single_process(tmp_path):
 def test_shard_ranges_partition_the_document_space():
     firsts = [shard.shard(r, 1000) for r in range(8)]
     assert firsts == [r * 1000 for r in range(8)]
+
+
+def test_zipf_sizes_are_deterministic_and_bounded():
+    z = shard.zipf_sizes(5000, 1000, 200000, 1.1)
+    assert (z == shard.zipf_sizes(5000, 1000, 200000, 1.1)).all()
+    assert z.max() == 200000 and z.min() == 1000
+    top = np.sort(z)[::-1]
+    assert top[1] == int(200000 * 2 ** -1.1) and top[9] == int(200000 * 10 ** -1.1)
+    assert np.argmax(z) != 0  # ranks are permuted over the document ids
+
+
+def test_lpt_assigns_every_document_once_and_balances():
+    costs = shard.zipf_sizes(4000, 100, 50000, 1.1)
+    parts, loads = shard.lpt(costs, 8)
+    allp = np.concatenate(parts)
+    assert sorted(allp.tolist()) == list(range(4000))
+    assert loads == [int(costs[q].sum()) for q in parts]
+    assert max(loads) - min(loads) <= costs.max()  # greedy LPT bound
+    for q in parts:
+        assert (np.diff(costs[q]) <= 0).all()  # each rank launches its largest documents first
+
+
+def _rank_uneven(rank, port, out_path):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    sizes = shard.zipf_sizes(11, 50, 900, 1.1)
+    parts, _ = shard.lpt(sizes, WORLD)
+    mine = parts[rank]
+    dig = (mine.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)).view(np.int64)
+    res = shard.gather_results(torch.from_numpy(dig), torch.from_numpy(np.zeros(len(mine), np.int32)), WORLD, rank,
+                               counts=[len(q) for q in parts])
+    if rank == 0:
+        np.savez(out_path, dig=res[0], ids=np.concatenate(parts))
+    dist.destroy_process_group()
+
+
+def test_gather_with_uneven_lpt_shards(tmp_path):
+    out = tmp_path / "uneven.npz"
+    mp.spawn(_rank_uneven, args=(_free_port(), str(out)), nprocs=WORLD, join=True)
+    got = np.load(out)
+    assert len(got["dig"]) == 11
+    with np.errstate(over="ignore"):
+        assert (got["dig"] == got["ids"].astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)).all()
