@@ -1,0 +1,831 @@
+// mt_json.cpp — native ingest of ISequencedDocumentMessage JSON logs.
+//
+// Real op logs are JSON: the file driver reads `messages*.json`, one JSON array of sequenced
+// messages (packages/drivers/file-driver/src/fileDeltaStorageService.ts:23-31), and the
+// replay tool feeds each message to Client.applyMsg (packages/tools/replay-tool/src/
+// clientReplayTool.ts:194-252; merge-tree/src/client.ts:797-819).  This file parses such logs
+// on host threads (one document per task) and packs them into the records of mt_oplog.h with
+// exactly the rules of the Python / JS packers (fluidframework_amd/oplog.py Packer,
+// fluidframework_amd/js/index.js Packer):
+//
+//   * short client ids per document in first-appearance order, the observer first
+//     (Client.getOrAddShortClientId, client.ts:636-660);
+//   * a non-"op" message -> an MT_OP_NOOP record (updateSeqNumbers only);
+//   * GROUP ops (type 3) flattened recursively, members chained with MT_OPF_GROUP_CONT;
+//   * insert seg: a string, {text, props?} or {marker: {refType}, props?}; a props object
+//     with keys -> prop records (JS key order: array indices ascending, then insertion order),
+//     {} -> an empty map; annotate props -> prop records, combiningOp only "rewrite";
+//   * values interned as JSON.stringify texts (JS number formatting, JS key order, lone
+//     surrogates escaped), JSON null -> value 0 (delete);
+//   * keys and values interned batch-wide in first-appearance order (document order, then
+//     op order), text and prop records laid out back to back in document order.
+//
+// Relative positions, registers and the observer's own ops are outside the observer replay
+// path and fail the document with MT_UNSUPPORTED (the packers raise UnsupportedOp).
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mtreplay.h"
+
+namespace {
+
+// ---------------------------------------------------------------- a compact JSON DOM
+enum JType : uint8_t { J_NULL, J_FALSE, J_TRUE, J_NUM, J_STR, J_ARR, J_OBJ };
+
+struct JNode {
+    JType type = J_NULL;
+    double num = 0;
+    uint32_t str = 0, slen = 0;  // J_STR: code units in Dom::u16
+    uint32_t key = 0, klen = 0;  // member of an object: its key in Dom::u16
+    int32_t first = -1, next = -1;
+};
+
+struct Dom {
+    std::vector<JNode> nodes;
+    std::u16string u16;
+    const char *p = nullptr, *end = nullptr;
+    std::string err;
+
+    bool fail(const char *m) {
+        if (err.empty()) err = m;
+        return false;
+    }
+    void ws() {
+        while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++;
+    }
+    static int hexv(char c) {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        return -1;
+    }
+    // a JSON string into u16 (UTF-8 input -> UTF-16 code units; \u escapes kept as code units)
+    bool string(uint32_t *off, uint32_t *len) {
+        if (p >= end || *p != '"') return fail("expected a string");
+        p++;
+        *off = (uint32_t)u16.size();
+        while (p < end && *p != '"') {
+            unsigned char c = (unsigned char)*p;
+            if (c == '\\') {
+                if (++p >= end) return fail("bad escape");
+                switch (*p) {
+                    case '"': u16.push_back(u'"'); break;
+                    case '\\': u16.push_back(u'\\'); break;
+                    case '/': u16.push_back(u'/'); break;
+                    case 'b': u16.push_back(u'\b'); break;
+                    case 'f': u16.push_back(u'\f'); break;
+                    case 'n': u16.push_back(u'\n'); break;
+                    case 'r': u16.push_back(u'\r'); break;
+                    case 't': u16.push_back(u'\t'); break;
+                    case 'u': {
+                        if (end - p < 5) return fail("bad \\u escape");
+                        uint32_t v = 0;
+                        for (int i = 1; i <= 4; i++) {
+                            int h = hexv(p[i]);
+                            if (h < 0) return fail("bad \\u escape");
+                            v = v * 16 + (uint32_t)h;
+                        }
+                        u16.push_back((char16_t)v);
+                        p += 4;
+                        break;
+                    }
+                    default: return fail("bad escape");
+                }
+                p++;
+            } else if (c < 0x20) {
+                return fail("control character in string");
+            } else if (c < 0x80) {
+                u16.push_back((char16_t)c);
+                p++;
+            } else {
+                int n = (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : (c & 0xF8) == 0xF0 ? 4 : 0;
+                if (!n || end - p < n) return fail("bad UTF-8");
+                uint32_t cp = c & (n == 2 ? 0x1F : n == 3 ? 0x0F : 0x07);
+                for (int i = 1; i < n; i++) {
+                    if (((unsigned char)p[i] & 0xC0) != 0x80) return fail("bad UTF-8");
+                    cp = (cp << 6) | ((unsigned char)p[i] & 0x3F);
+                }
+                p += n;
+                if (cp >= 0x10000) {
+                    cp -= 0x10000;
+                    u16.push_back((char16_t)(0xD800 + (cp >> 10)));
+                    u16.push_back((char16_t)(0xDC00 + (cp & 0x3FF)));
+                } else {
+                    u16.push_back((char16_t)cp);  // WTF-8 surrogates pass through as code units
+                }
+            }
+        }
+        if (p >= end) return fail("unterminated string");
+        p++;
+        *len = (uint32_t)u16.size() - *off;
+        return true;
+    }
+    bool number(double *v) {
+        const char *s = p;
+        if (p < end && *p == '-') p++;
+        if (p >= end || !(*p >= '0' && *p <= '9')) return fail("bad number");
+        while (p < end && ((*p >= '0' && *p <= '9') || *p == '.' || *p == 'e' || *p == 'E' || *p == '+' || *p == '-'))
+            p++;
+        std::string t(s, p);
+        char *e = nullptr;
+        *v = strtod(t.c_str(), &e);
+        if (!e || *e) return fail("bad number");
+        return true;
+    }
+    int32_t value(int depth) {
+        if (depth > 256) return fail("nesting too deep"), -1;
+        ws();
+        if (p >= end) return fail("unexpected end"), -1;
+        const int32_t id = (int32_t)nodes.size();
+        nodes.emplace_back();
+        char c = *p;
+        if (c == '{' || c == '[') {
+            const bool obj = c == '{';
+            nodes[id].type = obj ? J_OBJ : J_ARR;
+            p++;
+            ws();
+            int32_t last = -1;
+            if (p < end && *p == (obj ? '}' : ']')) {
+                p++;
+                return id;
+            }
+            for (;;) {
+                uint32_t ko = 0, kl = 0;
+                if (obj) {
+                    ws();
+                    if (!string(&ko, &kl)) return -1;
+                    ws();
+                    if (p >= end || *p != ':') return fail("expected ':'"), -1;
+                    p++;
+                }
+                const int32_t ch = value(depth + 1);
+                if (ch < 0) return -1;
+                nodes[ch].key = ko;
+                nodes[ch].klen = kl;
+                bool dup = false;
+                if (obj)  // JSON.parse: a repeated key keeps its first position, the last value
+                    for (int32_t m = nodes[id].first; m >= 0; m = nodes[m].next)
+                        if (nodes[m].klen == kl && !u16.compare(nodes[m].key, kl, u16, ko, kl)) {
+                            const int32_t nx = nodes[m].next;
+                            const uint32_t mk = nodes[m].key;
+                            nodes[m] = nodes[ch];
+                            nodes[m].next = nx;
+                            nodes[m].key = mk;
+                            dup = true;
+                            break;
+                        }
+                if (!dup) {
+                    if (last < 0) nodes[id].first = ch;
+                    else nodes[last].next = ch;
+                    last = ch;
+                }
+                ws();
+                if (p < end && *p == ',') {
+                    p++;
+                    continue;
+                }
+                if (p < end && *p == (obj ? '}' : ']')) {
+                    p++;
+                    return id;
+                }
+                return fail("expected ',' or a closing bracket"), -1;
+            }
+        }
+        if (c == '"') {
+            nodes[id].type = J_STR;
+            uint32_t o = 0, l = 0;
+            if (!string(&o, &l)) return -1;
+            nodes[id].str = o;
+            nodes[id].slen = l;
+            return id;
+        }
+        auto word = [&](const char *w, JType t) -> int32_t {
+            size_t n = strlen(w);
+            if ((size_t)(end - p) < n || memcmp(p, w, n)) return fail("bad literal"), -1;
+            p += n;
+            nodes[id].type = t;
+            return id;
+        };
+        if (c == 't') return word("true", J_TRUE);
+        if (c == 'f') return word("false", J_FALSE);
+        if (c == 'n') return word("null", J_NULL);
+        nodes[id].type = J_NUM;
+        double v = 0;
+        if (!number(&v)) return -1;
+        nodes[id].num = v;
+        return id;
+    }
+    std::u16string str_of(int32_t n) const { return u16.substr(nodes[n].str, nodes[n].slen); }
+    std::u16string key_of(int32_t n) const { return u16.substr(nodes[n].key, nodes[n].klen); }
+    bool key_is(int32_t n, const char *k) const {
+        const size_t kl = strlen(k);
+        if (nodes[n].klen != kl) return false;
+        for (size_t i = 0; i < kl; i++)
+            if (u16[nodes[n].key + i] != (char16_t)(unsigned char)k[i]) return false;
+        return true;
+    }
+    int32_t member(int32_t obj, const char *k) const {  // -1: absent
+        if (obj < 0 || nodes[obj].type != J_OBJ) return -1;
+        for (int32_t m = nodes[obj].first; m >= 0; m = nodes[m].next)
+            if (key_is(m, k)) return m;
+        return -1;
+    }
+    bool is_null_or_absent(int32_t n) const { return n < 0 || nodes[n].type == J_NULL; }
+};
+
+// ---------------------------------------------------------------- JS semantics
+bool array_index16(const std::u16string &k, uint32_t *idx) {
+    if (k.empty() || k.size() > 10) return false;
+    if (k[0] == u'0') {
+        if (k.size() != 1) return false;
+        *idx = 0;
+        return true;
+    }
+    uint64_t v = 0;
+    for (char16_t ch : k) {
+        if (ch < u'0' || ch > u'9') return false;
+        v = v * 10 + (uint64_t)(ch - u'0');
+    }
+    if (v > 4294967294ull) return false;
+    *idx = (uint32_t)v;
+    return true;
+}
+
+// Object.keys order: array indices ascending, then the rest in insertion order
+std::vector<int32_t> js_members(const Dom &D, int32_t obj) {
+    std::vector<std::pair<uint32_t, int32_t>> idx;
+    std::vector<int32_t> rest;
+    for (int32_t m = D.nodes[obj].first; m >= 0; m = D.nodes[m].next) {
+        uint32_t i = 0;
+        if (array_index16(D.key_of(m), &i)) idx.push_back({i, m});
+        else rest.push_back(m);
+    }
+    std::stable_sort(idx.begin(), idx.end());
+    std::vector<int32_t> out;
+    for (auto &x : idx) out.push_back(x.second);
+    out.insert(out.end(), rest.begin(), rest.end());
+    return out;
+}
+
+void put_utf8(std::string &o, uint32_t cp) {
+    if (cp < 0x80) {
+        o.push_back((char)cp);
+    } else if (cp < 0x800) {
+        o.push_back((char)(0xC0 | (cp >> 6)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+        o.push_back((char)(0xE0 | (cp >> 12)));
+        o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+        o.push_back((char)(0xF0 | (cp >> 18)));
+        o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+        o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+}
+
+// UTF-16 -> WTF-8 (lone surrogates as 3-byte sequences, so every code unit survives)
+std::string wtf8(const std::u16string &s) {
+    std::string o;
+    for (size_t i = 0; i < s.size(); i++) {
+        uint32_t c = s[i];
+        if (c >= 0xD800 && c <= 0xDBFF && i + 1 < s.size() && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+            put_utf8(o, 0x10000 + ((c - 0xD800) << 10) + (uint32_t)(s[i + 1] - 0xDC00));
+            i++;
+        } else {
+            put_utf8(o, c);
+        }
+    }
+    return o;
+}
+
+// JSON.stringify(string): escapes, lone surrogates as \udxxx (well-formed JSON.stringify)
+void quote(std::string &o, const char16_t *s, size_t n) {
+    static const char *hex = "0123456789abcdef";
+    o.push_back('"');
+    for (size_t i = 0; i < n; i++) {
+        uint32_t c = s[i];
+        switch (c) {
+            case 0x22: o += "\\\""; continue;
+            case 0x5C: o += "\\\\"; continue;
+            case 0x08: o += "\\b"; continue;
+            case 0x0C: o += "\\f"; continue;
+            case 0x0A: o += "\\n"; continue;
+            case 0x0D: o += "\\r"; continue;
+            case 0x09: o += "\\t"; continue;
+            default: break;
+        }
+        if (c < 0x20) {
+            o += "\\u00";
+            o.push_back(hex[c >> 4]);
+            o.push_back(hex[c & 15]);
+        } else if (c >= 0xD800 && c <= 0xDBFF && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+            put_utf8(o, 0x10000 + ((c - 0xD800) << 10) + (uint32_t)(s[i + 1] - 0xDC00));
+            i++;
+        } else if (c >= 0xD800 && c <= 0xDFFF) {
+            o += "\\u";
+            o.push_back(hex[c >> 12]);
+            o.push_back(hex[(c >> 8) & 15]);
+            o.push_back(hex[(c >> 4) & 15]);
+            o.push_back(hex[c & 15]);
+        } else {
+            put_utf8(o, c);
+        }
+    }
+    o.push_back('"');
+}
+
+// Number.prototype.toString (ECMA-262 Number::toString, radix 10): shortest round-trip digits
+void js_number(std::string &o, double v) {
+    if (std::isnan(v) || std::isinf(v)) {
+        o += "null";  // JSON.stringify
+        return;
+    }
+    if (v == 0) {
+        o += "0";
+        return;
+    }
+    if (v < 0) {
+        o.push_back('-');
+        v = -v;
+    }
+    char buf[40];
+    int prec = 1;
+    for (; prec <= 17; prec++) {
+        snprintf(buf, sizeof buf, "%.*e", prec - 1, v);
+        if (strtod(buf, nullptr) == v) break;
+    }
+    // buf = d[.ddd]e±x
+    std::string digits;
+    const char *q = buf;
+    for (; *q && *q != 'e'; q++)
+        if (*q >= '0' && *q <= '9') digits.push_back(*q);
+    const int e10 = atoi(q + 1);
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+    const int k = (int)digits.size(), n = e10 + 1;  // v = 0.d1..dk x 10^n
+    if (k <= n && n <= 21) {
+        o += digits;
+        o.append((size_t)(n - k), '0');
+    } else if (0 < n && n <= 21) {
+        o += digits.substr(0, (size_t)n);
+        o.push_back('.');
+        o += digits.substr((size_t)n);
+    } else if (-6 < n && n <= 0) {
+        o += "0.";
+        o.append((size_t)(-n), '0');
+        o += digits;
+    } else {
+        const int e = n - 1;
+        o.push_back(digits[0]);
+        if (k > 1) {
+            o.push_back('.');
+            o += digits.substr(1);
+        }
+        o.push_back('e');
+        o.push_back(e >= 0 ? '+' : '-');
+        o += std::to_string(e >= 0 ? e : -e);
+    }
+}
+
+void js_stringify(const Dom &D, int32_t n, std::string &o) {
+    const JNode &x = D.nodes[n];
+    switch (x.type) {
+        case J_NULL: o += "null"; return;
+        case J_FALSE: o += "false"; return;
+        case J_TRUE: o += "true"; return;
+        case J_NUM: js_number(o, x.num); return;
+        case J_STR: quote(o, D.u16.data() + x.str, x.slen); return;
+        case J_ARR: {
+            o.push_back('[');
+            bool first = true;
+            for (int32_t m = x.first; m >= 0; m = D.nodes[m].next) {
+                if (!first) o.push_back(',');
+                first = false;
+                js_stringify(D, m, o);
+            }
+            o.push_back(']');
+            return;
+        }
+        case J_OBJ: {
+            o.push_back('{');
+            bool first = true;
+            for (int32_t m : js_members(D, n)) {
+                if (!first) o.push_back(',');
+                first = false;
+                quote(o, D.u16.data() + D.nodes[m].key, D.nodes[m].klen);
+                o.push_back(':');
+                js_stringify(D, m, o);
+            }
+            o.push_back('}');
+            return;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- per-document packing
+struct LocalDoc {
+    std::vector<mt_op> ops;        // text / prop offsets local to this document
+    std::u16string text;
+    std::vector<mt_prop> props;    // local key / value ids
+    std::vector<std::u16string> keys;
+    std::vector<std::string> values;  // JSON texts; local id 0 = "null"
+    std::unordered_map<std::u16string, uint32_t> key_ids;
+    std::unordered_map<std::string, uint32_t> value_ids;
+    std::vector<std::u16string> names;
+    int status = MT_OK;
+    std::string err;
+};
+
+struct Packer1 {
+    const Dom &D;
+    LocalDoc &L;
+
+    bool fail(int code, const std::string &m) {
+        L.status = code;
+        L.err = m;
+        return false;
+    }
+    uint32_t key(const std::u16string &k) {
+        auto it = L.key_ids.find(k);
+        if (it != L.key_ids.end()) return it->second;
+        const uint32_t i = (uint32_t)L.keys.size();
+        L.key_ids.emplace(k, i);
+        L.keys.push_back(k);
+        return i;
+    }
+    uint32_t value(int32_t n) {
+        if (D.nodes[n].type == J_NULL) return 0;
+        std::string s;
+        js_stringify(D, n, s);
+        auto it = L.value_ids.find(s);
+        if (it != L.value_ids.end()) return it->second;
+        const uint32_t i = (uint32_t)L.values.size();
+        L.value_ids.emplace(s, i);
+        L.values.push_back(s);
+        return i;
+    }
+    bool prop_records(int32_t obj, uint32_t *off, uint32_t *cnt) {
+        if (D.nodes[obj].type != J_OBJ) return fail(MT_UNSUPPORTED, "props must be an object");
+        *off = (uint32_t)L.props.size();
+        for (int32_t m : js_members(D, obj)) L.props.push_back(mt_prop{key(D.key_of(m)), value(m)});
+        *cnt = (uint32_t)L.props.size() - *off;
+        return true;
+    }
+    void flatten(int32_t op, std::vector<int32_t> &out) {
+        const int32_t t = D.member(op, "type");
+        if (t >= 0 && D.nodes[t].type == J_NUM && D.nodes[t].num == 3) {
+            const int32_t ops = D.member(op, "ops");
+            if (ops >= 0 && D.nodes[ops].type == J_ARR)
+                for (int32_t m = D.nodes[ops].first; m >= 0; m = D.nodes[m].next) flatten(m, out);
+            return;
+        }
+        out.push_back(op);
+    }
+    static int32_t as_int(const JNode &n) { return n.type == J_NUM ? (int32_t)(int64_t)n.num : 0; }
+    bool pack_op(int32_t op, const mt_op &base, mt_op &r) {
+        r = base;
+        if (D.nodes[op].type != J_OBJ) return fail(MT_UNSUPPORTED, "op must be an object");
+        const int32_t t = D.member(op, "type"), p1 = D.member(op, "pos1");
+        if (p1 < 0 || !D.is_null_or_absent(D.member(op, "relativePos1")) ||
+            !D.is_null_or_absent(D.member(op, "register")))
+            return fail(MT_UNSUPPORTED, "relative positions / registers are not on the observer fast path");
+        const double tv = t >= 0 && D.nodes[t].type == J_NUM ? D.nodes[t].num : -1;
+        r.flags = 0;
+        r.pos1 = as_int(D.nodes[p1]);
+        r.pos2 = 0;
+        r.payload = r.payload_len = 0;
+        if (tv == 0) {
+            r.type = MT_OP_INSERT;
+            const int32_t seg = D.member(op, "seg");
+            int32_t props = -1;
+            bool has_text = false;
+            int32_t txt = -1;
+            if (seg >= 0 && D.nodes[seg].type == J_STR) {
+                has_text = true;
+                txt = seg;
+            } else if (seg >= 0 && D.nodes[seg].type == J_OBJ && D.member(seg, "text") >= 0) {
+                txt = D.member(seg, "text");
+                if (D.nodes[txt].type != J_STR) return fail(MT_UNSUPPORTED, "text must be a string");
+                has_text = true;
+                props = D.member(seg, "props");
+            } else if (seg >= 0 && D.nodes[seg].type == J_OBJ && D.member(seg, "marker") >= 0) {
+                const int32_t mk = D.member(seg, "marker");
+                const int32_t rt = D.member(mk, "refType");
+                r.flags |= MT_OPF_MARKER;
+                r.payload = rt >= 0 ? (uint32_t)as_int(D.nodes[rt]) : 0u;
+                r.payload_len = 1;
+                props = D.member(seg, "props");
+            } else {
+                return fail(MT_UNSUPPORTED, "unknown segment spec");
+            }
+            if (has_text) {
+                r.payload = (uint32_t)L.text.size();
+                r.payload_len = D.nodes[txt].slen;
+                L.text.append(D.u16, D.nodes[txt].str, D.nodes[txt].slen);
+            }
+            // TextSegment.make: `if (props) addProperties(props)` — the Python packer's rules
+            if (props >= 0 && D.nodes[props].type == J_ARR) return fail(MT_UNSUPPORTED, "array props");
+            const bool obj = props >= 0 && D.nodes[props].type == J_OBJ;
+            const bool nonempty = obj && D.nodes[props].first >= 0;
+            const bool truthy_other = props >= 0 && !obj && D.nodes[props].type != J_NULL &&
+                                      D.nodes[props].type != J_FALSE &&
+                                      !(D.nodes[props].type == J_NUM && D.nodes[props].num == 0) &&
+                                      !(D.nodes[props].type == J_STR && D.nodes[props].slen == 0) &&
+                                      !(D.nodes[props].type == J_ARR && D.nodes[props].first < 0);
+            if (truthy_other) return fail(MT_UNSUPPORTED, "props must be an object");
+            if (nonempty) {
+                uint32_t off = 0, n = 0;
+                if (!prop_records(props, &off, &n)) return false;
+                if (n > MT_OPF_MAX_INSERT_PROPS) return fail(MT_UNSUPPORTED, "too many insert props");
+                r.flags |= (uint16_t)(MT_OPF_HAS_PROPS | (n << 4));
+                r.pos2 = (int32_t)off;
+            } else if (obj) {  // {}: an empty map is created
+                r.flags |= MT_OPF_HAS_PROPS;
+                r.pos2 = (int32_t)L.props.size();
+            }
+        } else if (tv == 1 || tv == 2) {
+            r.type = tv == 1 ? MT_OP_REMOVE : MT_OP_ANNOTATE;
+            const int32_t p2 = D.member(op, "pos2");
+            r.pos2 = p2 >= 0 ? as_int(D.nodes[p2]) : 0;
+            if (tv == 2) {
+                const int32_t cop = D.member(op, "combiningOp");
+                if (!D.is_null_or_absent(cop)) {
+                    const int32_t nm = D.member(cop, "name");
+                    if (nm < 0 || D.nodes[nm].type != J_STR || D.str_of(nm) != u"rewrite")
+                        return fail(MT_UNSUPPORTED, "combiningOp other than rewrite");
+                    r.flags |= MT_OPF_REWRITE;
+                }
+                // annotateRange -> addProperties(op.props) iterates its keys: an object is required
+                const int32_t pr = D.member(op, "props");
+                uint32_t off = 0, n = 0;
+                if (pr < 0) return fail(MT_UNSUPPORTED, "props must be an object");
+                if (!prop_records(pr, &off, &n)) return false;
+                r.payload = off;
+                r.payload_len = n;
+            }
+        } else {
+            return fail(MT_UNSUPPORTED, "op type");
+        }
+        return true;
+    }
+    bool run(int32_t root, const std::u16string &observer) {
+        if (root < 0 || D.nodes[root].type != J_ARR) return fail(MT_BAD_INPUT, "a document log must be a JSON array");
+        L.names.assign(1, observer);
+        std::unordered_map<std::u16string, uint8_t> shortid{{observer, 0}};
+        for (int32_t m = D.nodes[root].first; m >= 0; m = D.nodes[m].next) {
+            if (D.nodes[m].type != J_OBJ) return fail(MT_BAD_INPUT, "a message must be an object");
+            const int32_t cid = D.member(m, "clientId");
+            std::u16string name = cid >= 0 && D.nodes[cid].type == J_STR ? D.str_of(cid) : u"null";
+            auto it = shortid.find(name);
+            uint8_t c;
+            if (it == shortid.end()) {  // getOrAddShortClientId (client.ts:636-641)
+                if (L.names.size() >= 64) return fail(MT_UNSUPPORTED, "more than 64 clients");
+                c = (uint8_t)L.names.size();
+                shortid.emplace(name, c);
+                L.names.push_back(name);
+            } else {
+                c = it->second;
+            }
+            mt_op base{};
+            base.client = c;
+            const int32_t sq = D.member(m, "sequenceNumber"), rs = D.member(m, "referenceSequenceNumber"),
+                          ms = D.member(m, "minimumSequenceNumber");
+            if (sq < 0 || rs < 0 || ms < 0) return fail(MT_BAD_INPUT, "message without sequence numbers");
+            base.seq = as_int(D.nodes[sq]);
+            base.ref_seq = as_int(D.nodes[rs]);
+            base.msn = as_int(D.nodes[ms]);
+            base.type = MT_OP_NOOP;
+            const int32_t ty = D.member(m, "type");
+            const bool is_op = ty >= 0 && D.nodes[ty].type == J_STR && D.str_of(ty) == u"op";
+            if (!is_op) {
+                L.ops.push_back(base);
+                continue;
+            }
+            if (c == 0) return fail(MT_UNSUPPORTED, "ack of the observer's own op (local path)");
+            std::vector<int32_t> members;
+            const int32_t contents = D.member(m, "contents");
+            if (contents >= 0) flatten(contents, members);
+            for (size_t j = 0; j < members.size(); j++) {
+                mt_op r{};
+                if (!pack_op(members[j], base, r)) return false;
+                if (j + 1 < members.size()) r.flags |= MT_OPF_GROUP_CONT;
+                L.ops.push_back(r);
+            }
+            if (members.empty()) L.ops.push_back(base);  // empty group: updateSeqNumbers only
+        }
+        return true;
+    }
+};
+
+std::u16string from_utf8(const char *s) {
+    std::u16string out;
+    for (const unsigned char *p = (const unsigned char *)s; *p;) {
+        uint32_t c = *p;
+        int n = c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4;
+        uint32_t cp = n == 1 ? c : c & (n == 2 ? 0x1F : n == 3 ? 0x0F : 0x07);
+        for (int i = 1; i < n && p[i]; i++) cp = (cp << 6) | (p[i] & 0x3F);
+        p += n;
+        if (cp >= 0x10000) {
+            cp -= 0x10000;
+            out.push_back((char16_t)(0xD800 + (cp >> 10)));
+            out.push_back((char16_t)(0xDC00 + (cp & 0x3FF)));
+        } else {
+            out.push_back((char16_t)cp);
+        }
+    }
+    return out;
+}
+
+}  // namespace
+
+struct mt_packed {
+    std::vector<mt_op> ops;
+    std::vector<int64_t> off;
+    std::vector<uint16_t> text;
+    std::vector<mt_prop> props;
+    std::vector<std::string> keys, values;          // keys WTF-8, values JSON (UTF-8)
+    std::vector<std::vector<std::string>> clients;  // per document, WTF-8
+    std::string err;
+};
+
+extern "C" {
+
+MT_API int mt_pack_json(mt_packed **out, int64_t n_docs, const char *const *doc_json, const int64_t *doc_len,
+                        const char *observer, int32_t n_threads, int64_t *bad_doc) {
+    if (!out || n_docs < 0 || (n_docs && (!doc_json || !doc_len))) return MT_ERR_ARG;
+    *out = nullptr;
+    if (bad_doc) *bad_doc = -1;
+    const std::u16string obs = from_utf8(observer ? observer : "readonly");
+    std::vector<LocalDoc> docs((size_t)n_docs);
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const int64_t d = next.fetch_add(1);
+            if (d >= n_docs) return;
+            Dom D;
+            D.p = doc_json[d];
+            D.end = doc_json[d] + doc_len[d];
+            D.nodes.reserve((size_t)(doc_len[d] / 16 + 16));
+            LocalDoc &L = docs[(size_t)d];
+            L.values.push_back("null");
+            L.value_ids.emplace("null", 0);
+            const int32_t root = D.value(0);
+            D.ws();
+            if (root < 0 || D.p != D.end) {
+                L.status = MT_BAD_INPUT;
+                L.err = D.err.empty() ? "trailing characters after the log" : D.err;
+                continue;
+            }
+            Packer1 P{D, L};
+            P.run(root, obs);
+        }
+    };
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min<int>(nt, (int)std::max<int64_t>(1, n_docs)));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    mt_packed *P = new mt_packed();
+    for (int64_t d = 0; d < n_docs; d++)
+        if (docs[(size_t)d].status != MT_OK) {
+            if (bad_doc) *bad_doc = d;
+            P->err = "document " + std::to_string(d) + ": " + docs[(size_t)d].err;
+            const int rc = docs[(size_t)d].status;
+            *out = P;
+            return rc;
+        }
+    // batch-wide interning in first-appearance order (document order, then op order)
+    std::unordered_map<std::u16string, uint32_t> kid;
+    std::unordered_map<std::string, uint32_t> vid{{"null", 0}};
+    std::vector<std::u16string> keys16;
+    P->values.push_back("null");
+    P->off.push_back(0);
+    for (int64_t d = 0; d < n_docs; d++) {
+        LocalDoc &L = docs[(size_t)d];
+        std::vector<uint32_t> kmap(L.keys.size()), vmap(L.values.size());
+        for (size_t i = 0; i < L.keys.size(); i++) {
+            auto it = kid.find(L.keys[i]);
+            if (it == kid.end()) {
+                it = kid.emplace(L.keys[i], (uint32_t)keys16.size()).first;
+                keys16.push_back(L.keys[i]);
+            }
+            kmap[i] = it->second;
+        }
+        for (size_t i = 0; i < L.values.size(); i++) {
+            auto it = vid.find(L.values[i]);
+            if (it == vid.end()) {
+                it = vid.emplace(L.values[i], (uint32_t)P->values.size()).first;
+                P->values.push_back(L.values[i]);
+            }
+            vmap[i] = it->second;
+        }
+        const uint32_t tbase = (uint32_t)P->text.size(), pbase = (uint32_t)P->props.size();
+        for (mt_op o : L.ops) {
+            if (o.type == MT_OP_INSERT) {
+                if (!(o.flags & MT_OPF_MARKER)) o.payload += tbase;
+                if (o.flags & MT_OPF_HAS_PROPS) o.pos2 += (int32_t)pbase;
+            } else if (o.type == MT_OP_ANNOTATE) {
+                o.payload += pbase;
+            }
+            P->ops.push_back(o);
+        }
+        P->text.insert(P->text.end(), L.text.begin(), L.text.end());
+        for (const mt_prop &q : L.props) P->props.push_back(mt_prop{kmap[q.key], vmap[q.value]});
+        P->off.push_back((int64_t)P->ops.size());
+        std::vector<std::string> names;
+        for (const auto &n : L.names) names.push_back(wtf8(n));
+        P->clients.push_back(std::move(names));
+    }
+    for (const auto &k : keys16) P->keys.push_back(wtf8(k));
+    *out = P;
+    return MT_OK;
+}
+
+MT_API void mt_packed_destroy(mt_packed *p) { delete p; }
+
+MT_API const char *mt_packed_error(const mt_packed *p) { return p ? p->err.c_str() : ""; }
+
+MT_API int mt_packed_sizes(const mt_packed *p, int64_t *n_ops, int64_t *n_text, int64_t *n_props, int32_t *n_keys,
+                           int32_t *n_values) {
+    if (!p) return MT_ERR_ARG;
+    if (n_ops) *n_ops = (int64_t)p->ops.size();
+    if (n_text) *n_text = (int64_t)p->text.size();
+    if (n_props) *n_props = (int64_t)p->props.size();
+    if (n_keys) *n_keys = (int32_t)p->keys.size();
+    if (n_values) *n_values = (int32_t)p->values.size();
+    return MT_OK;
+}
+
+MT_API int mt_packed_arrays(const mt_packed *p, mt_op *ops, int64_t *doc_op_off, uint16_t *text, mt_prop *props) {
+    if (!p) return MT_ERR_ARG;
+    if (ops && !p->ops.empty()) memcpy(ops, p->ops.data(), sizeof(mt_op) * p->ops.size());
+    if (doc_op_off) memcpy(doc_op_off, p->off.data(), sizeof(int64_t) * p->off.size());
+    if (text && !p->text.empty()) memcpy(text, p->text.data(), 2 * p->text.size());
+    if (props && !p->props.empty()) memcpy(props, p->props.data(), sizeof(mt_prop) * p->props.size());
+    return MT_OK;
+}
+
+MT_API const char *mt_packed_key(const mt_packed *p, int32_t i) {
+    return p && i >= 0 && i < (int32_t)p->keys.size() ? p->keys[(size_t)i].c_str() : nullptr;
+}
+MT_API const char *mt_packed_value(const mt_packed *p, int32_t i) {
+    return p && i >= 0 && i < (int32_t)p->values.size() ? p->values[(size_t)i].c_str() : nullptr;
+}
+MT_API int32_t mt_packed_doc_clients(const mt_packed *p, int64_t doc) {
+    return p && doc >= 0 && doc < (int64_t)p->clients.size() ? (int32_t)p->clients[(size_t)doc].size() : -1;
+}
+MT_API const char *mt_packed_client(const mt_packed *p, int64_t doc, int32_t i) {
+    if (!p || doc < 0 || doc >= (int64_t)p->clients.size()) return nullptr;
+    const auto &c = p->clients[(size_t)doc];
+    return i >= 0 && i < (int32_t)c.size() ? c[(size_t)i].c_str() : nullptr;
+}
+
+MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p) {
+    if (!b || !p || !p->err.empty()) return MT_ERR_ARG;
+    const int64_t D = (int64_t)p->clients.size();
+    mt_batch_stats st;
+    int rc0 = mt_batch_get_stats(b, &st);
+    if (rc0) return rc0;
+    if (st.n_docs != D) return MT_ERR_ARG;
+    std::vector<const char *> kp, vp;
+    for (const auto &k : p->keys) kp.push_back(k.c_str());
+    for (const auto &v : p->values) vp.push_back(v.c_str());
+    static const char *none = "_";
+    int rc = mt_batch_set_tables(b, kp.empty() ? &none : kp.data(), kp.empty() ? 1 : (int32_t)kp.size(), vp.data(),
+                                 (int32_t)vp.size());
+    if (rc) return rc;
+    bool shared = true;
+    for (int64_t d = 1; d < D && shared; d++) shared = p->clients[(size_t)d] == p->clients[0];
+    auto set = [&](int64_t doc, const std::vector<std::string> &names) {
+        std::vector<const char *> np;
+        for (const auto &n : names) np.push_back(n.c_str());
+        return mt_batch_set_clients(b, doc, np.data(), (int32_t)np.size());
+    };
+    if (D && shared) {
+        rc = set(-1, p->clients[0]);
+        if (rc) return rc;
+    } else {
+        for (int64_t d = 0; d < D; d++) {
+            rc = set(d, p->clients[(size_t)d]);
+            if (rc) return rc;
+        }
+    }
+    static const uint16_t zero_text = 0;
+    static const mt_prop zero_prop{0, 0};
+    static const mt_op zero_op{};
+    return mt_batch_ingest(b, p->ops.empty() ? &zero_op : p->ops.data(), p->off.data(),
+                           p->text.empty() ? &zero_text : p->text.data(), (int64_t)p->text.size(),
+                           p->props.empty() ? &zero_prop : p->props.data(), (int64_t)p->props.size());
+}
+
+}  // extern "C"

@@ -44,6 +44,9 @@ export declare class ReplayBatch {
     readonly nDocs: number;
     client(i: number): ReplayClient;
     ingestMessages(docs: Array<Array<ISequencedDocumentMessage | string>>): void;
+    /** Native parse + pack (mt_pack_json on nThreads host threads, 0 = all cores) of each
+     *  document's message array, given as its JSON text (messages.json) or as the array. */
+    ingestJson(docs: Array<string | ISequencedDocumentMessage[]>, nThreads?: number): void;
     generate(params: GenParams, docFirst?: number): void;
     run(): void;
     runAsync(): Promise<void>;

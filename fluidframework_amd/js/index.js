@@ -105,6 +105,7 @@ class Packer {
                 this.textParts.push(text);
                 this.textLen += text.length;
             }
+            if (Array.isArray(props)) throw new UnsupportedOp('array props');
             if (props && Object.keys(props).length) {  // TextSegment.make: `if (props) addProperties`
                 const [off, n] = this.propRecords(props);
                 if (n > MAX_INSERT_PROPS) throw new UnsupportedOp('too many insert props');
@@ -121,7 +122,8 @@ class Packer {
                     if (op.combiningOp.name !== 'rewrite') throw new UnsupportedOp('combiningOp other than rewrite');
                     r.flags |= OPF_REWRITE;
                 }
-                [r.payload, r.payloadLen] = this.propRecords(op.props || {});
+                // annotateRange -> addProperties(op.props) iterates its keys: an object is required
+                [r.payload, r.payloadLen] = this.propRecords(op.props);
             }
         } else throw new UnsupportedOp(`op type ${t}`);
         return r;
@@ -229,6 +231,14 @@ class ReplayBatch {
         if (shared && pb.clients.length) n.setClients(this.h, -1, pb.clients[0]);
         else pb.clients.forEach((c, i) => n.setClients(this.h, i, c));
         n.ingest(this.h, pb.ops, pb.docOpOff, pb.text.subarray(0, Math.max(1, pb.nText)), pb.props);
+    }
+    // native ingest (mt_pack_json on host threads): per document the JSON text of its message
+    // array (the file driver's messages.json) or the array itself
+    ingestJson(docs, nThreads = 0) {
+        const texts = docs.map((d) => (typeof d === 'string' ? d : JSON.stringify(d)));
+        native().ingestJson(this.h, texts, this.clients.length ? this.clients[0].longClientId : 'readonly', nThreads);
+        this.queued = false;
+        for (const c of this.clients) c.messages = [];
     }
     ingestMessages(docs) {
         docs.forEach((msgs, i) => { for (const m of msgs) this.clients[i].applyMsg(m); });

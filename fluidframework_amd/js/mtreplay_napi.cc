@@ -100,6 +100,35 @@ void *typed(napi_env env, napi_value v, size_t *len) {
 
 void finalize_batch(napi_env, void *data, void *) { mt_batch_destroy(static_cast<mt_batch *>(data)); }
 
+// ingestJson(h, [jsonText per document], observer, nThreads): native parse + pack of
+// ISequencedDocumentMessage logs on host threads (mt_pack_json), then mt_batch_ingest_packed
+napi_value ingest_json(napi_env env, napi_callback_info info) {
+    auto a = args(env, info, 4);
+    mt_batch *b = batch_of(env, a[0]);
+    std::vector<std::string> docs = strs(env, a[1]);
+    std::string observer = str(env, a[2]);
+    int32_t threads = (int32_t)i64(env, a[3]);
+    std::vector<const char *> ptrs;
+    std::vector<int64_t> lens;
+    for (const auto &d : docs) {
+        ptrs.push_back(d.c_str());
+        lens.push_back((int64_t)d.size());
+    }
+    mt_packed *p = nullptr;
+    int64_t bad = -1;
+    int rc = mt_pack_json(&p, (int64_t)docs.size(), ptrs.data(), lens.data(), observer.empty() ? "readonly" : observer.c_str(),
+                          threads, &bad);
+    if (rc != MT_OK) {
+        std::string why = p ? mt_packed_error(p) : "";
+        mt_packed_destroy(p);
+        return throw_mt(env, rc, ("mt_pack_json: " + why).c_str());
+    }
+    rc = mt_batch_ingest_packed(b, p);
+    mt_packed_destroy(p);
+    MT_OK_OR_THROW(rc, "mt_batch_ingest_packed");
+    return nullptr;
+}
+
 // createBatch(nDocs, {segCap, maxRetries}) -> external handle (mt_batch_create)
 napi_value create_batch(napi_env env, napi_callback_info info) {
     auto a = args(env, info, 2);
@@ -345,6 +374,7 @@ napi_value init(napi_env env, napi_value exports) {
         {"setTables", nullptr, set_tables, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"setClients", nullptr, set_clients, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"ingest", nullptr, ingest, nullptr, nullptr, nullptr, kMethod, nullptr},
+        {"ingestJson", nullptr, ingest_json, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"generate", nullptr, generate, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"run", nullptr, run, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"runAsync", nullptr, run_async, nullptr, nullptr, nullptr, kMethod, nullptr},

@@ -17,8 +17,8 @@ when the compiled library is missing or no GPU is present (there is no CPU fallb
 from __future__ import annotations
 
 import ctypes as C
-import os
 import json
+import os
 from pathlib import Path
 
 import numpy as np
@@ -38,7 +38,9 @@ EXPORTS = [
     "mt_doc_snapshot_v1", "mt_doc_snapshot_blob", "mt_doc_digest", "mt_doc_shape", "mt_doc_dump", "mt_batch_log_sizes",
     "mt_batch_download_log", "mt_batch_doc_counters", "mt_batch_device_digests", "mt_batch_snapshots",
     "mt_doc_snapshot_v1_device", "mt_batch_snapshot_index", "mt_batch_snapshot_copy", "mt_batch_launch_info",
-    "mt_batch_snapshot_digests", "mt_batch_generate_docs",
+    "mt_batch_snapshot_digests", "mt_batch_generate_docs", "mt_pack_json", "mt_packed_destroy", "mt_packed_error",
+    "mt_packed_sizes", "mt_packed_arrays", "mt_packed_key", "mt_packed_value", "mt_packed_doc_clients",
+    "mt_packed_client", "mt_batch_ingest_packed",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -113,6 +115,21 @@ def lib():
     L.mt_batch_ingest.argtypes = [vp, vp, vp, vp, i64, vp, i64]
     L.mt_batch_generate.argtypes = [vp, P(GenParams), i64]
     L.mt_batch_generate_docs.argtypes = [vp, P(GenParams), vp, vp]
+    L.mt_pack_json.argtypes = [P(vp), i64, vp, vp, cp, i32, P(i64)]
+    L.mt_packed_destroy.argtypes = [vp]
+    L.mt_packed_destroy.restype = None
+    L.mt_packed_error.argtypes = [vp]
+    L.mt_packed_error.restype = cp
+    L.mt_packed_sizes.argtypes = [vp, P(i64), P(i64), P(i64), P(i32), P(i32)]
+    L.mt_packed_arrays.argtypes = [vp, vp, vp, vp, vp]
+    for fn in ("mt_packed_key", "mt_packed_value"):
+        getattr(L, fn).argtypes = [vp, i32]
+        getattr(L, fn).restype = cp
+    L.mt_packed_doc_clients.argtypes = [vp, i64]
+    L.mt_packed_doc_clients.restype = i32
+    L.mt_packed_client.argtypes = [vp, i64, i32]
+    L.mt_packed_client.restype = cp
+    L.mt_batch_ingest_packed.argtypes = [vp, vp]
     L.mt_batch_run.argtypes = [vp, vp]
     L.mt_batch_launch.argtypes = [vp, vp]
     L.mt_batch_sync.argtypes = [vp]
@@ -151,8 +168,57 @@ def _chk(rc: int, what: str):
 def _cstrs(strs):
     arr = (C.c_char_p * max(1, len(strs)))()
     for k, s in enumerate(strs):
-        arr[k] = s.encode("utf-8")
+        arr[k] = s.encode("utf-8", "surrogatepass")  # WTF-8: lone surrogates survive
     return arr
+
+
+class PackedJson:
+    """Native JSON ingest result (mt_pack_json): ISequencedDocumentMessage logs parsed and packed
+    on host threads, with the packing rules of oplog.Packer."""
+
+    def __init__(self, docs, observer: str = "readonly", n_threads: int = 0):
+        bufs = [d if isinstance(d, bytes) else (d if isinstance(d, str) else json.dumps(d)).encode("utf-8",
+                                                                                              "surrogatepass")
+                for d in docs]
+        n = len(bufs)
+        ptrs = (C.c_char_p * max(1, n))(*bufs)
+        lens = np.array([len(x) for x in bufs] or [0], np.int64)
+        h, bad = C.c_void_p(), C.c_int64(-1)
+        rc = lib().mt_pack_json(C.byref(h), n, ptrs, lens.ctypes.data, observer.encode("utf-8"), n_threads,
+                                C.byref(bad))
+        self.h = h
+        self.n_docs = n
+        if rc != MT_OK:
+            err = lib().mt_packed_error(h).decode("utf-8", "replace") if h else ""
+            self.close()
+            raise MtError(rc, f"mt_pack_json: {err}")
+
+    def close(self):
+        if self.h:
+            lib().mt_packed_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def arrays(self):
+        """PackedBatch (oplog.py) view: ops, doc_op_off, text, props, keys, values, clients."""
+        L = lib()
+        no, nt, npr, nk, nv = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32()
+        _chk(L.mt_packed_sizes(self.h, C.byref(no), C.byref(nt), C.byref(npr), C.byref(nk), C.byref(nv)), "sizes")
+        ops = np.zeros(no.value, OP_DTYPE)
+        off = np.zeros(self.n_docs + 1, np.int64)
+        text = np.zeros(max(1, nt.value), np.uint16)
+        props = np.zeros(max(1, npr.value), PROP_DTYPE)
+        _chk(L.mt_packed_arrays(self.h, ops.ctypes.data, off.ctypes.data, text.ctypes.data, props.ctypes.data),
+             "arrays")
+        dec = lambda b: b.decode("utf-8", "surrogatepass")  # noqa: E731  (WTF-8)
+        keys = [dec(L.mt_packed_key(self.h, i)) for i in range(nk.value)]
+        values = [dec(L.mt_packed_value(self.h, i)) for i in range(nv.value)]
+        clients = [[dec(L.mt_packed_client(self.h, d, i)) for i in range(L.mt_packed_doc_clients(self.h, d))]
+                   for d in range(self.n_docs)]
+        return PackedBatch(ops=ops, doc_op_off=off, text=text[: nt.value], props=props[: npr.value], keys=keys,
+                           values=values, clients=clients)
 
 
 class DocView:
@@ -281,6 +347,15 @@ class ReplayBatch:
             raise ValueError("expected one message list per document")
         self.ingest_packed(pb)
         return pb
+
+    def ingest_json(self, docs, observer: str = "readonly", n_threads: int = 0):
+        """Parse + pack JSON message logs natively (mt_pack_json, host threads) and ingest them.
+        docs: per document a JSON array text (str/bytes) or a list of message dicts."""
+        pj = PackedJson(docs, observer, n_threads)
+        try:
+            _chk(lib().mt_batch_ingest_packed(self.h, pj.h), "mt_batch_ingest_packed")
+        finally:
+            pj.close()
 
     def generate(self, params: GenParams, doc_first: int = 0):
         _chk(lib().mt_batch_generate(self.h, C.byref(params), doc_first), "mt_batch_generate")

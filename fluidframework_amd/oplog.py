@@ -19,6 +19,7 @@ observer first, exactly as ``Client.getOrAddShortClientId`` does (client.ts:636-
 from __future__ import annotations
 
 import json
+import re
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -49,20 +50,60 @@ def js_stringify(value) -> str:
         idx = [(int(k), k, v) for k, v in items if _is_array_index(k)]
         rest = [(k, v) for k, v in items if not _is_array_index(k)]
         ordered = [(k, v) for _, k, v in sorted(idx)] + rest
-        return "{" + ",".join(json.dumps(k, ensure_ascii=False) + ":" + js_stringify(v) for k, v in ordered) + "}"
+        return "{" + ",".join(_js_quote(k) + ":" + js_stringify(v) for k, v in ordered) + "}"
     if isinstance(value, list):
         return "[" + ",".join(js_stringify(v) for v in value) + "]"
     if isinstance(value, bool) or value is None:
         return json.dumps(value)
-    if isinstance(value, float):
-        if value != value or value in (float("inf"), float("-inf")):
-            return "null"
-        if value == int(value) and abs(value) < 1e21:
-            return str(int(value))
-        return repr(value)
-    if isinstance(value, int):
-        return str(value)
-    return json.dumps(value, ensure_ascii=False)
+    if isinstance(value, (int, float)):
+        return js_number(value)
+    return _js_quote(value)
+
+
+_LONE = re.compile("[\ud800-\udfff]")
+
+
+def _js_quote(s: str) -> str:
+    """JSON.stringify(string): like json.dumps(ensure_ascii=False), lone surrogates escaped
+    (well-formed JSON.stringify); paired surrogates arrive as one code point from json.loads."""
+    return _LONE.sub(lambda m: "\\u%04x" % ord(m.group()), json.dumps(s, ensure_ascii=False))
+
+
+def js_number(v) -> str:
+    """Number.prototype.toString (ECMA-262 Number::toString, radix 10) as JSON.stringify writes
+    it: shortest round-trip digits, fixed notation for 1e-7 < |v| < 1e21, else d.ddde±x;
+    NaN / Infinity -> null; integers beyond 2**53 are doubles first, as in JS."""
+    from decimal import Decimal
+
+    v = float(v) if not isinstance(v, int) or abs(v) >= 2 ** 53 else v
+    if isinstance(v, int):
+        return str(v)
+    if v != v or v in (float("inf"), float("-inf")):
+        return "null"
+    if v == 0:
+        return "0"
+    sign = "-" if v < 0 else ""
+    v = abs(v)
+    if v < 2 ** 53 and v == int(v):
+        return sign + str(int(v))
+    t = Decimal(repr(v)).as_tuple()
+    digits = "".join(map(str, t.digits))
+    exp = t.exponent
+    stripped = digits.rstrip("0")
+    exp += len(digits) - len(stripped)
+    digits = stripped or "0"
+    k = len(digits)
+    n = k + exp  # v = 0.d1..dk x 10**n
+    if k <= n <= 21:
+        out = digits + "0" * (n - k)
+    elif 0 < n <= 21:
+        out = digits[:n] + "." + digits[n:]
+    elif -6 < n <= 0:
+        out = "0." + "0" * (-n) + digits
+    else:
+        e = n - 1
+        out = digits[0] + ("." + digits[1:] if k > 1 else "") + "e" + ("+" if e >= 0 else "-") + str(abs(e))
+    return sign + out
 
 
 def _is_array_index(k: str) -> bool:
@@ -144,6 +185,8 @@ class Packer:
             if isinstance(msg, str):
                 msg = json.loads(msg)
             cid = msg["clientId"]
+            if cid is None:  # system messages: one short id for all of them (mt_json.cpp does the same)
+                cid = "null"
             if cid not in short:  # getOrAddShortClientId (client.ts:636-641)
                 short[cid] = len(names)
                 names.append(cid)
@@ -203,6 +246,8 @@ class Packer:
                 r["payload_len"] = len(u)
                 self._text.append(u)
                 self._text_len += len(u)
+            if isinstance(props, list):
+                raise UnsupportedOp("array props")
             if props:  # TextSegment.make: `if (props) addProperties(props)`
                 off, n = self._prop_records(props)
                 if n > MAX_INSERT_PROPS:
@@ -220,7 +265,8 @@ class Packer:
                     if cop.get("name") != "rewrite":
                         raise UnsupportedOp("combiningOp other than rewrite")
                     r["flags"] |= OPF_REWRITE
-                r["payload"], r["payload_len"] = self._prop_records(op.get("props") or {})
+                # annotateRange -> addProperties(op.props) iterates its keys: an object is required
+                r["payload"], r["payload_len"] = self._prop_records(op.get("props"))
         else:
             raise UnsupportedOp(f"op type {t}")
         return r

@@ -1,6 +1,7 @@
 // Replays message logs through the Node host layer (fluidframework_amd/js) on the GPU and
 // prints each document's text, property runs, SnapshotV1 blobs, status and digest as JSON.
-// usage: node tests/node_replay.js <logs.json: [[msg, ...], ...]>   (run by test_node_host.py)
+// usage: node tests/node_replay.js <logs.json: [[msg, ...], ...]> [applyMsg|json]   (run by test_node_host.py)
+// mode json: the native ingest (ReplayBatch.ingestJson -> mt_pack_json) instead of applyMsg
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -9,11 +10,15 @@ const { ReplayBatch } = require(path.join(__dirname, '..', 'fluidframework_amd',
 async function main() {
     const docs = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
     const batch = new ReplayBatch(docs.length);
-    docs.forEach((msgs, i) => {
-        const c = batch.client(i);
-        c.startOrUpdateCollaboration('readonly');
-        for (const m of msgs) c.applyMsg(m);
-    });
+    if (process.argv[3] === 'json') {
+        batch.ingestJson(docs.map((msgs) => JSON.stringify(msgs)), 4);
+    } else {
+        docs.forEach((msgs, i) => {
+            const c = batch.client(i);
+            c.startOrUpdateCollaboration('readonly');
+            for (const m of msgs) c.applyMsg(m);
+        });
+    }
     await batch.runAsync();
     const out = docs.map((_, i) => {
         const c = batch.client(i);

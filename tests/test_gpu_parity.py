@@ -272,3 +272,25 @@ def test_mixed_size_batch_generate_docs_and_concurrent_classes():
         b.snapshots()
         for d in range(0, len(ids), 5):
             assert b.doc(d).snapshot_v1(device=True) == b.doc(d).snapshot_v1()
+
+
+def test_native_json_ingest_replays_like_the_packer():
+    """mt_pack_json + mt_batch_ingest_packed (host threads) replays every document exactly like
+    the Python packer's ingest; both equal the oracle's applyMsg(JSON) replay."""
+    import sys as _sys
+    _sys.path.insert(0, str(ROOT / "tests"))
+    from test_json_ingest import EDGE_DOCS, _farm_messages
+
+    # the oracle's JSON entry point takes string client ids only: the system message gets one
+    edge = [[dict(m, clientId=m["clientId"] or "A") for m in d] for d in EDGE_DOCS[:2]]
+    docs = [k["messages"] for k in KATS] + edge + [_farm_messages()]
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs)) as a, fa.ReplayBatch(len(docs)) as b:
+        a.ingest_messages(docs)
+        b.ingest_json([json.dumps(d) for d in docs], n_threads=4)
+        a.run()
+        b.run()
+        for i in range(len(docs)):
+            assert b.doc(i).status == a.doc(i).status == oracle[i].status
+            assert b.doc(i).digest() == a.doc(i).digest()
+            assert_doc_parity(b.doc(i), oracle[i])

@@ -19,7 +19,7 @@ ADDON = ROOT / "fluidframework_amd" / "js" / "mtreplay.node"
 pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node / N-API addon not available")
 
 FUNCS = {"createBatch", "setTables", "setClients", "ingest", "generate", "run", "runAsync", "docStatus", "docText",
-         "docPropsRuns", "docSnapshotV1", "docDigest", "deviceDigests", "stats", "statusString"}
+         "docPropsRuns", "docSnapshotV1", "docDigest", "deviceDigests", "stats", "statusString", "ingestJson"}
 
 
 def _node(code):
@@ -49,7 +49,8 @@ def _msg(c, s, r, contents, msn=0):
 
 
 @pytest.mark.gpu
-def test_node_replay_matches_oracle(tmp_path):
+@pytest.mark.parametrize("mode", ["applyMsg", "json"])
+def test_node_replay_matches_oracle(tmp_path, mode):
     kats = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
     docs = [k["messages"] for k in kats]
     docs.append([_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "héllo wörld", "props": {"b": 1, "10": "x", "2": None}}}),
@@ -61,8 +62,8 @@ def test_node_replay_matches_oracle(tmp_path):
                  _msg("A", 5, 4, {"type": 1, "pos1": 0, "pos2": 2}, msn=3)])
     path = tmp_path / "logs.json"
     path.write_text(json.dumps(docs))
-    r = subprocess.run([NODE, str(ROOT / "tests" / "node_replay.js"), str(path)], capture_output=True, text=True,
-                       timeout=120)
+    r = subprocess.run([NODE, str(ROOT / "tests" / "node_replay.js"), str(path), mode], capture_output=True,
+                       text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     got = json.loads(r.stdout)
     for msgs, g in zip(docs, got):
