@@ -702,14 +702,19 @@ static void set_min_seq(mto_doc *d, int min_seq) {
 }
 
 /* ------------------------------------------------------------------ edits */
-/* insertSegments (mergeTree.ts:1968-1998) + blockInsert (2141-2224), one segment */
-static void insert_segment(mto_doc *d, int pos, Seg *seg, int ref_seq, int client_id, int seq) {
+/* insertSegments (mergeTree.ts:1968-1998) + blockInsert (2141-2224): ensureIntervalBoundary at
+   pos, then each segment with cachedLength > 0 inserted at insertPos (advancing by its length),
+   then one zamboni */
+static void insert_segments(mto_doc *d, int pos, Seg **segs, int n, int ref_seq, int client_id, int seq) {
     ensure_interval_boundary(d, pos, ref_seq, client_id);
-    if (seg && seg->n.cached_length > 0) {
+    int insert_pos = pos;
+    for (int i = 0; i < n; i++) {
+        Seg *seg = segs[i];
+        if (!seg || seg->n.cached_length <= 0) continue;
         seg->seq = seq;
         seg->client_id = client_id;
         ICtx ctx = {LEAF_INSERT, seg, 1};
-        Block *sn = inserting_walk(d, d->root, pos, ref_seq, client_id, seq, &ctx);
+        Block *sn = inserting_walk(d, d->root, insert_pos, ref_seq, client_id, seq, &ctx);
         if (seg->n.parent == NULL)
             fail(d, MTO_INVALID_POS, "MergeTree insert failed: {\"currentSeq\":%d,\"minSeq\":%d,\"segSeq\":%d}",
                  d->cw.current_seq, d->cw.min_seq, seg->seq);
@@ -722,8 +727,13 @@ static void insert_segment(mto_doc *d, int pos, Seg *seg, int ref_seq, int clien
                 add_to_lru_set(d, seg, seg->seq);
             }
         }
+        insert_pos += seg->n.cached_length;
     }
     if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
+}
+
+static void insert_segment(mto_doc *d, int pos, Seg *seg, int ref_seq, int client_id, int seq) {
+    insert_segments(d, pos, &seg, 1, ref_seq, client_id, seq);
 }
 
 typedef struct {
@@ -1028,6 +1038,157 @@ int mto_apply_msg_json(mto_doc *d, const char *msg_json) {
     sb_free(&name);
     update_seq_numbers(d, msn, seq);
     jv_unref(msg);
+    UNGUARD(d);
+    return d->status;
+}
+
+/* ------------------------------------------------------------------ SnapshotLoader */
+/* SnapshotLoader.specToSegment (snapshotLoader.ts:94-125): merge info when the spec has "json" */
+static Seg *spec_to_loaded_segment(mto_doc *d, const jv *spec) {
+    const jv *json = (spec && spec->kind == JV_OBJ) ? jv_obj_get_ascii(spec, "json") : NULL;
+    Seg *s;
+    if (json) {
+        s = spec_to_segment(d, json);
+        const jv *cl = jv_obj_get_ascii(spec, "client");
+        const jv *sq = jv_obj_get_ascii(spec, "seq");
+        const jv *rs = jv_obj_get_ascii(spec, "removedSeq");
+        const jv *rc = jv_obj_get_ascii(spec, "removedClient");
+        sb name;
+        if (cl && cl->kind != JV_UNDEF) {
+            if (cl->kind != JV_STR) fail(d, MTO_BAD_INPUT, "client is not a string");
+            sb_init(&name);
+            sb_put_u16_utf8(&name, cl->s, cl->slen);
+            s->client_id = get_or_add_short_client_id(d, name.p ? name.p : "");
+            sb_free(&name);
+        } else {
+            s->client_id = NONCOLLAB_CLIENT;
+        }
+        s->seq = UNIVERSAL_SEQ;
+        if (sq && sq->kind != JV_UNDEF && !jv_int(sq, &s->seq)) fail(d, MTO_BAD_INPUT, "seq");
+        if (rs && rs->kind != JV_UNDEF) {
+            if (!jv_int(rs, &s->removed_seq)) fail(d, MTO_BAD_INPUT, "removedSeq");
+            s->removed = 1;
+        }
+        if (rc && rc->kind != JV_UNDEF) {
+            if (rc->kind != JV_STR) fail(d, MTO_BAD_INPUT, "removedClient is not a string");
+            sb_init(&name);
+            sb_put_u16_utf8(&name, rc->s, rc->slen);
+            s->removed_client = get_or_add_short_client_id(d, name.p ? name.p : "");
+            sb_free(&name);
+        }
+    } else {
+        s = spec_to_segment(d, spec);
+        s->seq = UNIVERSAL_SEQ;
+        s->client_id = NONCOLLAB_CLIENT;
+    }
+    return s;
+}
+
+/* MergeTree.reloadFromSegments (mergeTree.ts:1195-1251): bottom-up, MaxNodesInBlock - 1 children */
+static Block *build_merge_block(mto_doc *d, Node **nodes, int n) {
+    const int max_children = MAX_NODES - 1;
+    const int nb = (n + max_children - 1) / max_children;
+    Node **blocks = (Node **)malloc(sizeof(Node *) * (size_t)nb);
+    for (int bi = 0, ni = 0; bi < nb; bi++) {
+        Block *b = make_block(d, 0);
+        for (int c = 0; c < max_children && ni < n; c++, ni++) {
+            const int idx = b->child_count++; /* addNode, mergeTree.ts:1189-1193 */
+            assign_child(b, nodes[ni], idx);
+        }
+        block_update(b);
+        blocks[bi] = &b->n;
+    }
+    Block *r = nb == 1 ? (Block *)blocks[0] : build_merge_block(d, blocks, nb);
+    free(blocks);
+    return r;
+}
+
+static const jv *chunk_segments(mto_doc *d, const jv *chunk) {
+    const jv *segs = (chunk && chunk->kind == JV_OBJ) ? jv_obj_get_ascii(chunk, "segments") : NULL;
+    if (!segs || segs->kind != JV_ARR) fail(d, MTO_BAD_INPUT, "chunk without segments");
+    const jv *ver = jv_obj_get_ascii(chunk, "version");
+    static const u16 V1[1] = {'1'};
+    if (!ver || ver->kind != JV_STR || !u16_eq(ver->s, ver->slen, V1, 1)) fail(d, MTO_UNSUPPORTED, "chunk version");
+    return segs;
+}
+
+/* SnapshotLoader.initialize (snapshotLoader.ts:36-205): loadHeader -> reloadFromSegments +
+   startOrUpdateCollaboration(long_id, minSeq, seq), then loadBody: body segments appended at
+   the end with insertSegments, consecutive NonCollab/Universal ones in one batch */
+int mto_load_snapshot_v1(mto_doc *d, const char *const *blobs, const long *blob_len, int n_blobs,
+                         const char *long_id) {
+    GUARD(d);
+    jv *parsed[256] = {0};
+    Seg **body = NULL;
+    int nbody = 0;
+    if (n_blobs < 1 || n_blobs > 256) fail(d, MTO_BAD_INPUT, "blob count");
+    for (int i = 0; i < n_blobs; i++) {
+        parsed[i] = jv_parse(blobs[i], (size_t)blob_len[i]);
+        if (!parsed[i]) fail(d, MTO_BAD_INPUT, "blob %d is not JSON", i);
+    }
+    const jv *h = parsed[0];
+    const jv *hsegs = chunk_segments(d, h);
+    const jv *meta = jv_obj_get_ascii(h, "headerMetadata");
+    if (!meta || meta->kind != JV_OBJ) fail(d, MTO_BAD_INPUT, "header metadata not available");
+    int seq = 0, min_seq = 0, seg_count = 0, total_count = 0;
+    if (!jv_int(jv_obj_get_ascii(meta, "sequenceNumber"), &seq)) fail(d, MTO_BAD_INPUT, "sequenceNumber");
+    if (!jv_int(jv_obj_get_ascii(meta, "minSequenceNumber"), &min_seq)) min_seq = seq;
+    jv_int(jv_obj_get_ascii(h, "segmentCount"), &seg_count);
+    jv_int(jv_obj_get_ascii(meta, "totalSegmentCount"), &total_count);
+    const jv *order = jv_obj_get_ascii(meta, "orderedChunkMetadata");
+    const int n_chunks = (order && order->kind == JV_ARR) ? order->n : 1;
+    /* loadHeader */
+    Node **hn = (Node **)malloc(sizeof(Node *) * (size_t)(hsegs->n + 1));
+    for (int i = 0; i < hsegs->n; i++) hn[i] = &spec_to_loaded_segment(d, hsegs->vals[i])->n;
+    if (hsegs->n > 0) {
+        d->root = build_merge_block(d, hn, hsegs->n);
+    } else {
+        d->root = make_block(d, 0);
+        d->root->n.cached_length = 0;
+    }
+    free(hn);
+    d->root->n.parent = NULL;
+    d->root->n.index = 0;
+    /* startOrUpdateCollaboration (client.ts:1051-1071) -> startCollaboration (1254-1271) */
+    if (d->long_client_id == NULL) {
+        d->long_client_id = strdup(long_id);
+        d->cw.client_id = get_or_add_short_client_id(d, long_id);
+        d->cw.min_seq = min_seq;
+        d->cw.collaborating = 1;
+        d->cw.current_seq = seq;
+        heap_init(d);
+    }
+    /* loadBody */
+    if (seg_count < total_count) {
+        if (n_blobs < n_chunks) fail(d, MTO_BAD_INPUT, "missing body chunks");
+        int cap = 64;
+        body = (Seg **)malloc(sizeof(Seg *) * (size_t)cap);
+        for (int ci = 1; ci < n_chunks; ci++) {
+            const jv *segs = chunk_segments(d, parsed[ci]);
+            for (int i = 0; i < segs->n; i++) {
+                if (nbody == cap) {
+                    cap *= 2;
+                    body = (Seg **)realloc(body, sizeof(Seg *) * (size_t)cap);
+                }
+                body[nbody++] = spec_to_loaded_segment(d, segs->vals[i]);
+            }
+        }
+        int bstart = 0;
+        for (int i = 0; i <= nbody; i++) {
+            const int batchable = i < nbody && body[i]->client_id == NONCOLLAB_CLIENT && body[i]->seq == UNIVERSAL_SEQ;
+            if (batchable) continue;
+            if (i > bstart)  /* flushBatch */
+                insert_segments(d, d->root->n.cached_length, body + bstart, i - bstart, UNIVERSAL_SEQ,
+                                NONCOLLAB_CLIENT, UNIVERSAL_SEQ);
+            if (i < nbody) {
+                Seg *sg = body[i];
+                insert_segments(d, d->root->n.cached_length, &sg, 1, UNIVERSAL_SEQ, sg->client_id, sg->seq);
+            }
+            bstart = i + 1;
+        }
+    }
+    free(body);
+    for (int i = 0; i < n_blobs; i++) jv_unref(parsed[i]);
     UNGUARD(d);
     return d->status;
 }

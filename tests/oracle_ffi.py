@@ -71,6 +71,7 @@ def lib():
     L.mto_error.restype = cp
     L.mto_start_collab.argtypes = [vp, cp, i, i]
     L.mto_apply_msg_json.argtypes = [vp, cp]
+    L.mto_load_snapshot_v1.argtypes = [vp, C.POINTER(cp), vp, i, cp]
     L.mto_insert_local_json.argtypes = [vp, i, cp]
     L.mto_annotate_local_json.argtypes = [vp, i, i, cp]
     L.mto_remove_local.argtypes = [vp, i, i]
@@ -135,6 +136,17 @@ class Doc:
 
     def start_collab(self, long_id: str, min_seq=0, cur_seq=0) -> int:
         return self.L.mto_start_collab(self.h, long_id.encode(), min_seq, cur_seq)
+
+    def load_snapshot(self, blobs, long_id: str = "readonly") -> int:
+        """SnapshotLoader: blobs = {"header": .., "body_0": ..} (emit order) or a list."""
+        import numpy as np
+
+        vals = list(blobs.values()) if isinstance(blobs, dict) else list(blobs)
+        bufs = [v.encode("utf-8", "surrogatepass") if isinstance(v, str) else v for v in vals]
+        arr = (C.c_char_p * len(bufs))(*bufs)
+        lens = np.array([len(b) for b in bufs], np.int64)
+        self._keep = (arr, lens, bufs)
+        return self.L.mto_load_snapshot_v1(self.h, arr, lens.ctypes.data, len(bufs), long_id.encode())
 
     def apply_msg(self, msg_json: str) -> int:
         return self.L.mto_apply_msg_json(self.h, msg_json.encode())
