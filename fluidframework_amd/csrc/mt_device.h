@@ -217,7 +217,7 @@ struct SnapParams {
     const uint32_t *val_str;    // per value: (offset, length) of its JSON text
     const uint32_t *cli_str;    // client table entries: (offset, length) of JSON.stringify(long id)
     const int32_t *doc_cli;     // per document: (first entry, count) in cli_str; null: the shared table
-    int32_t cli_first, cli_n;   // the shared client table (entry 0 of cli_str is "undefined")
+    int32_t cli_first, cli_n;   // the shared client table (entries 0, 1 of cli_str: "undefined", "original")
     const uint8_t *final_mask;  // per workgroup: 1 when this launch holds the document's final table
     int32_t n_keys, n_values;   // key_str has n_keys + 1 entries (the last is "?")
     int32_t chunk_size;

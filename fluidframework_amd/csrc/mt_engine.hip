@@ -220,8 +220,11 @@ struct Engine {
         // initialNode (mergeTree.ts:1125): an empty root leaf block
         root = alloc_block(1);
         depth = 1;
-        // heap entry 0 is the sentinel LRUSegmentComparer.min = { maxSeq: -2 } (never compared)
+        // heap entry 0 is the sentinel LRUSegmentComparer.min = { maxSeq: -2 } (never compared);
+        // its 8 bytes hold the SnapshotLoader's batch state (insert position, batch open), so
+        // checkpoints carry it and the replay kernel keeps no registers for it
         htop = kNoneSeq;
+        if (lane == 0) h_ent[0] = make_uint2(0u, 0u);
         wsync();
     }
 
@@ -1340,12 +1343,13 @@ struct Engine {
     // ------------------------------------------------------------------ ops
     // insertSegments + blockInsert for one remote segment (mergeTree.ts:1968-1998, 2141-2224):
     // ensureIntervalBoundary(pos) then the inserting walk, which after the split resolves to
-    // the split's right half (unless the split restructured the tree: then it walks again)
-    MT_FI void op_insert(const mt_op &op) {
-        const uint32_t c = op.client;
-        const uint32_t pos = (uint32_t)op.pos1;
+    // the split's right half (unless the split restructured the tree: then it walks again).
+    // `loaded`: a SnapshotLoader body segment (refSeq UniversalSequenceNumber) carrying its own
+    // removal info (op.ref_seq / op.msn) and its settled state.
+    template <bool loaded>
+    MT_FI void insert_one(const mt_op &op, uint32_t c, uint32_t pos, int32_t ref) {
         ov_splits = -1;
-        Walk W = boundary(pos, op.ref_seq, c);
+        Walk W = boundary(pos, ref, c);
         if (status) return;
         const bool marker = (op.flags & MT_OPF_MARKER) != 0;
         const uint32_t len = marker ? 1u : op.payload_len;
@@ -1364,26 +1368,186 @@ struct Engine {
                 props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
                 if (status) return;
             }
+            const int32_t rseq = loaded ? op.ref_seq : kNoneSeq;
+            const uint32_t rcli = loaded && rseq != kNoneSeq ? ((uint32_t)op.msn & 63u) : kNoClient;
+            // a loaded segment below the collab window is settled: it joins the settled sums
+            // after the leaf insert (while it moves through block splits it counts as unsettled)
+            const bool settled = loaded && op.seq <= min_seq && (rseq == kNoneSeq || rseq <= min_seq);
             uint32_t gen = s_meta[slot] & kGenMask;
-            uint32_t meta = gen | kMetaLinked | kMetaUnsettled | (c & 63u) | (kNoClient << 6);
+            uint32_t meta = gen | kMetaLinked | kMetaUnsettled | (c & 63u) | (rcli << 6);
             if (marker) meta |= kMetaMarker;
             if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
             if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
             if (props) meta |= kMetaHasProps;
             s_len[slot] = len;
             s_seq[slot] = op.seq;
-            s_rseq[slot] = kNoneSeq;
+            s_rseq[slot] = rseq;
             if (lane == 0) cold[slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
             s_meta[slot] = meta;
             wsync();
-            u_push((uint32_t)slot);
+            if (!settled) u_push((uint32_t)slot);
             int32_t blk = insert_leaf(W.blk, W.k, (uint32_t)slot);
             if (status) return;
+            if (settled) {
+                s_meta[slot] = meta & ~kMetaUnsettled;
+                if (rseq == kNoneSeq) chain_add_uniform(rfl((int32_t)s_blk[slot]), len);
+            }
             // saveIfLocal (mergeTree.ts:2164-2179)
             if (op.seq > min_seq) add_to_lru(blk, (uint32_t)slot, op.seq);
         }
         resolve_splits();
-        zamboni();
+        if (!loaded || !(op.flags & MT_OPF_GROUP_CONT)) zamboni();
+    }
+    MT_FI void op_insert(const mt_op &op) { insert_one<false>(op, op.client, (uint32_t)op.pos1, op.ref_seq); }
+
+    // ------------------------------------------------------------------ SnapshotLoader
+    // (snapshotLoader.ts:36-205) — the header chunk's segments, MergeTree.reloadFromSegments
+    // (mergeTree.ts:1195-1251): blocks of MaxNodesInBlock - 1 children built bottom up.  Appending
+    // leaf by leaf to the rightmost path (a new block at a level once the last is full, a new
+    // root once the top level has two blocks) gives exactly those blocks.  Lengths and the
+    // overlay are set up by op_collab, once minSeq is known.
+    MT_FI void op_load_header(const mt_op &op) {
+        ov_splits = -1;
+        const bool marker = (op.flags & MT_OPF_MARKER) != 0;
+        const uint32_t len = marker ? 1u : op.payload_len;
+        int32_t slot = alloc_slot();
+        if (slot < 0) return;
+        uint32_t props = 0, ph = 0;
+        if (op.flags & MT_OPF_HAS_PROPS) {
+            pool_reserve(2u + 2u * MT_OPF_NPROPS(op.flags));
+            if (status) return;
+            props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
+            if (status) return;
+        }
+        const int32_t rseq = op.ref_seq;
+        const uint32_t rcli = rseq != kNoneSeq ? ((uint32_t)op.msn & 63u) : kNoClient;
+        uint32_t meta = (s_meta[slot] & kGenMask) | kMetaLinked | (op.client & 63u) | (rcli << 6);
+        if (marker) meta |= kMetaMarker;
+        if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
+        if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
+        if (props) meta |= kMetaHasProps;
+        s_len[slot] = len;
+        s_seq[slot] = op.seq;
+        s_rseq[slot] = rseq;
+        if (lane == 0) cold[slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
+        s_meta[slot] = meta;
+        wsync();
+        // the rightmost leaf block
+        int32_t b = root;
+        for (int32_t l = 0; l + 1 < depth; l++) b = rfl((int32_t)b_child[b * 8 + b_count[b] - 1]);
+        int32_t n = b_count[b];
+        if (n < kMaxNodes - 1) {
+            b_child[b * 8 + n] = (uint16_t)slot;
+            b_count[b] = (uint8_t)(n + 1);
+            s_blk[slot] = (uint16_t)b;
+            wsync();
+            return;
+        }
+        int32_t child = alloc_block(1);
+        if (status) return;
+        b_child[child * 8] = (uint16_t)slot;
+        b_count[child] = 1;
+        s_blk[slot] = (uint16_t)child;
+        wsync();
+        int32_t left = b;
+        for (;;) {
+            const int32_t p = b_parent[left];
+            if (p == (int32_t)kNoBlock) {  // left is the root: the top level now has two blocks
+                const int32_t r = alloc_block(0);
+                if (status) return;
+                b_child[r * 8] = (uint16_t)left;
+                b_child[r * 8 + 1] = (uint16_t)child;
+                b_count[r] = 2;
+                b_parent[left] = (uint16_t)r;
+                b_parent[child] = (uint16_t)r;
+                root = r;
+                depth++;
+                break;
+            }
+            const int32_t pn = b_count[p];
+            if (pn < kMaxNodes - 1) {
+                b_child[p * 8 + pn] = (uint16_t)child;
+                b_count[p] = (uint8_t)(pn + 1);
+                b_parent[child] = (uint16_t)p;
+                break;
+            }
+            const int32_t np = alloc_block(0);
+            if (status) return;
+            b_child[np * 8] = (uint16_t)child;
+            b_count[np] = 1;
+            b_parent[child] = (uint16_t)np;
+            child = np;
+            left = p;
+        }
+        splits++;
+        wsync();
+    }
+
+    // startOrUpdateCollaboration(observer, minSeq, currentSeq) after loadHeader
+    // (snapshotLoader.ts:147-160; client.ts:1051-1071): the settled sums and the overlay list
+    // of the loaded tree (MergeTree.startCollaboration recomputes the partial lengths)
+    MT_FI void op_collab(const mt_op &op) {
+        min_seq = op.msn;
+        cur_seq = op.seq;
+        settled_min = min_seq;
+        ov_splits = -1;
+        wsync();
+        for (int32_t i = lane; i < blk_top; i += kWave) b_slen[i] = 0u;
+        wsync();
+        for (int32_t base = 0; base < slot_top; base += kWave) {
+            const int32_t slot = base + lane;
+            uint32_t meta = 0;
+            bool live = false, sett = false;
+            uint32_t add = 0, b = 0;
+            if (slot < slot_top) {
+                meta = s_meta[slot];
+                live = (meta & kMetaLinked) != 0;
+                if (live) {
+                    const int32_t sq = s_seq[slot], rs = s_rseq[slot];
+                    sett = sq <= min_seq && (rs == kNoneSeq || rs <= min_seq);
+                    if (sett && rs == kNoneSeq) add = s_len[slot];
+                    b = s_blk[slot];
+                }
+            }
+            const bool un = live && !sett;
+            const uint64_t um = ballot(un);
+            if (nu + __popcll(um) > cap.ulist) {
+                cap_fail(1);
+                return;
+            }
+            if (un) {
+                s_meta[slot] = meta | kMetaUnsettled;
+                u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+            }
+            nu += __popcll(um);
+            if (nu > max_u) max_u = nu;
+            chain_add(b_slen, add > 0u, b, add);
+        }
+        wsync();
+    }
+
+    // MergeTree.length of the local view (root.cachedLength: localNetLength, mergeTree.ts:1161)
+    MT_FI uint32_t local_length() {
+        uint32_t sum = 0;
+        for (int32_t base = 0; base < slot_top; base += kWave) {
+            const int32_t slot = base + lane;
+            uint32_t v = 0;
+            if (slot < slot_top && (s_meta[slot] & kMetaLinked) && s_rseq[slot] == kNoneSeq) v = s_len[slot];
+            sum += rdl(scan_incl(v), 63);
+        }
+        return sum;
+    }
+
+    // loadBody (snapshotLoader.ts:166-205): insertSegments(root.cachedLength, batch,
+    // UniversalSequenceNumber, client, seq); members of a batch go in at advancing positions
+    MT_FI void op_load_body(const mt_op &op) {
+        const uint2 st = h_ent[0];  // {insert position, batch open}
+        const uint32_t pos = rfl(st.y) ? rfl(st.x) : local_length();
+        const uint32_t len = (op.flags & MT_OPF_MARKER) ? 1u : op.payload_len;
+        insert_one<true>(op, op.client, pos, 0);
+        wsync();
+        if (lane == 0) h_ent[0] = make_uint2(pos + len, (op.flags & MT_OPF_GROUP_CONT) ? 1u : 0u);
+        wsync();
     }
 
     // markRangeRemoved / annotateRange (mergeTree.ts:2565-2719): both boundaries, then the
@@ -1525,6 +1689,20 @@ struct Engine {
             blk = next_leaf_block(blk);
             base = bend;
         }
+    }
+
+    // SnapshotLoader records (mt_load_kernel only): no sequence checks, no updateSeqNumbers
+    MT_FI void apply_load(const mt_op &op) {
+        pend_n = 0;
+        const bool noncollab = op.client == MT_CLIENT_NONCOLLAB;
+        if (op.type != MT_OP_COLLAB && (op.client == 0 || (op.client >= kMaxClients && !noncollab))) {
+            set_fail(ST_UNSUPPORTED);
+            return;
+        }
+        if (op.type == MT_OP_LOAD_HEADER) op_load_header(op);
+        else if (op.type == MT_OP_COLLAB) op_collab(op);
+        else op_load_body(op);
+        resolve_splits();
     }
 
     MT_FI void apply(const mt_op &op) {
@@ -1828,7 +2006,9 @@ MT_FI uint8_t *tables(const ReplayParams &P, int64_t w) {
     }
 }
 
-template <int SEG>
+// kLoad: apply only the document's leading SnapshotLoader records, then checkpoint at the
+// first other record (cap_kind kCapCheckpoint); the replay launch resumes there.
+template <int SEG, bool kLoad>
 MT_FI void replay_body(const ReplayParams &P) {
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
@@ -1853,15 +2033,27 @@ MT_FI void replay_body(const ReplayParams &P) {
         mt_op nxt = load_op_lane(ops, base + kWave + E.lane, b1);
         int64_t n = b1 - base < kWave ? b1 - base : kWave;
         for (int i = 0; i < n; i++) {
-            if (P.ck_out && E.low_headroom()) {
-                E.checkpoint(P.ck_out + w * ck_words(SEG), done);
-                E.status = ST_CAPACITY;
-                E.cap_kind = kCapCheckpoint;
-                fail_op = (int32_t)(base - b0 + i);
-                break;
+            if constexpr (kLoad) {  // the loader stops at the first record that is not a LOAD one
+                const uint32_t t = rdl((uint32_t)cur.type, i);
+                if (P.ck_out && (E.low_headroom() || !(t == MT_OP_LOAD_HEADER || t == MT_OP_LOAD_BODY || t == MT_OP_COLLAB))) {
+                    E.checkpoint(P.ck_out + w * ck_words(SEG), done);
+                    E.status = ST_CAPACITY;
+                    E.cap_kind = kCapCheckpoint;
+                    fail_op = (int32_t)(base - b0 + i);
+                    break;
+                }
+                E.apply_load(bcast_op(cur, i));
+            } else {
+                if (P.ck_out && E.low_headroom()) {
+                    E.checkpoint(P.ck_out + w * ck_words(SEG), done);
+                    E.status = ST_CAPACITY;
+                    E.cap_kind = kCapCheckpoint;
+                    fail_op = (int32_t)(base - b0 + i);
+                    break;
+                }
+                mt_op op = bcast_op(cur, i);
+                E.apply(op);
             }
-            mt_op op = bcast_op(cur, i);
-            E.apply(op);
             if (E.status != ST_OK) {
                 fail_op = (int32_t)(base - b0 + i);
                 break;

@@ -28,6 +28,7 @@
 // kernels of each capacity class (mt_kernels.hip compiled with -DMT_SEG=<seg>)
 #define MT_DECLARE_CLASS(S)                                                   \
     extern "C" __global__ void mt_replay_kernel_##S(mt::ReplayParams P);      \
+    extern "C" __global__ void mt_load_kernel_##S(mt::ReplayParams P);        \
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);
 MT_DECLARE_CLASS(64)
 MT_DECLARE_CLASS(128)
@@ -77,24 +78,25 @@ struct KernelClass {
     int seg;
     const void *replay;
     const void *generate;
+    const void *load;
 };
 static const KernelClass kKernels[mt::kNumClasses] = {
-    {64, (const void *)mt_replay_kernel_64, (const void *)mt_generate_kernel_64},
-    {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128},
-    {192, (const void *)mt_replay_kernel_192, (const void *)mt_generate_kernel_192},
-    {256, (const void *)mt_replay_kernel_256, (const void *)mt_generate_kernel_256},
-    {320, (const void *)mt_replay_kernel_320, (const void *)mt_generate_kernel_320},
-    {384, (const void *)mt_replay_kernel_384, (const void *)mt_generate_kernel_384},
-    {512, (const void *)mt_replay_kernel_512, (const void *)mt_generate_kernel_512},
-    {640, (const void *)mt_replay_kernel_640, (const void *)mt_generate_kernel_640},
-    {768, (const void *)mt_replay_kernel_768, (const void *)mt_generate_kernel_768},
-    {1024, (const void *)mt_replay_kernel_1024, (const void *)mt_generate_kernel_1024},
-    {1280, (const void *)mt_replay_kernel_1280, (const void *)mt_generate_kernel_1280},
-    {1664, (const void *)mt_replay_kernel_1664, (const void *)mt_generate_kernel_1664},
-    {2048, (const void *)mt_replay_kernel_2048, (const void *)mt_generate_kernel_2048},
-    {3072, (const void *)mt_replay_kernel_3072, (const void *)mt_generate_kernel_3072},
-    {4096, (const void *)mt_replay_kernel_4096, (const void *)mt_generate_kernel_4096},
-    {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000},
+    {64, (const void *)mt_replay_kernel_64, (const void *)mt_generate_kernel_64, (const void *)mt_load_kernel_64},
+    {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128},
+    {192, (const void *)mt_replay_kernel_192, (const void *)mt_generate_kernel_192, (const void *)mt_load_kernel_192},
+    {256, (const void *)mt_replay_kernel_256, (const void *)mt_generate_kernel_256, (const void *)mt_load_kernel_256},
+    {320, (const void *)mt_replay_kernel_320, (const void *)mt_generate_kernel_320, (const void *)mt_load_kernel_320},
+    {384, (const void *)mt_replay_kernel_384, (const void *)mt_generate_kernel_384, (const void *)mt_load_kernel_384},
+    {512, (const void *)mt_replay_kernel_512, (const void *)mt_generate_kernel_512, (const void *)mt_load_kernel_512},
+    {640, (const void *)mt_replay_kernel_640, (const void *)mt_generate_kernel_640, (const void *)mt_load_kernel_640},
+    {768, (const void *)mt_replay_kernel_768, (const void *)mt_generate_kernel_768, (const void *)mt_load_kernel_768},
+    {1024, (const void *)mt_replay_kernel_1024, (const void *)mt_generate_kernel_1024, (const void *)mt_load_kernel_1024},
+    {1280, (const void *)mt_replay_kernel_1280, (const void *)mt_generate_kernel_1280, (const void *)mt_load_kernel_1280},
+    {1664, (const void *)mt_replay_kernel_1664, (const void *)mt_generate_kernel_1664, (const void *)mt_load_kernel_1664},
+    {2048, (const void *)mt_replay_kernel_2048, (const void *)mt_generate_kernel_2048, (const void *)mt_load_kernel_2048},
+    {3072, (const void *)mt_replay_kernel_3072, (const void *)mt_generate_kernel_3072, (const void *)mt_load_kernel_3072},
+    {4096, (const void *)mt_replay_kernel_4096, (const void *)mt_generate_kernel_4096, (const void *)mt_load_kernel_4096},
+    {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000},
 };
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
 
@@ -118,6 +120,7 @@ struct Launch {
     int64_t ops = 0;            // ops applied by this launch (resumed documents: after their checkpoint)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int level = 0;              // escalation depth (0: a first launch)
+    bool load = false;          // SnapshotLoader launch (mt_load_kernel): LOAD records, then a checkpoint
 };
 
 struct DocRes {  // per-document result location
@@ -307,6 +310,7 @@ struct mt_batch {
     int64_t total_ops = 0, total_props = 0;
     int32_t max_ops_per_doc = 0;
     std::vector<int64_t> h_off;
+    std::vector<int32_t> h_nload, h_nload_segs;  // leading SnapshotLoader records / segments per doc
     std::vector<uint64_t> h_text_base, h_pool_base;
     std::vector<uint32_t> h_text_len, h_text_cap, h_pool_cap;
     uint64_t text_words = 0, pool_words = 0;
@@ -330,7 +334,8 @@ struct mt_batch {
     uint64_t *d_digest = nullptr;  // mt_batch_device_digests
     float kernel_ms = 0, total_ms = 0;
     bool ran = false;
-    int n_first = 0;  // launches of mt_batch_launch (the rest are escalations)
+    int first0 = 0, n_first = 0;  // replay launches [first0, n_first) of mt_batch_launch; before them
+                                  // the SnapshotLoader launches, after them the escalations
     hipStream_t run_stream = nullptr;
     std::chrono::steady_clock::time_point t_launch;
     // single-document result cache
@@ -533,14 +538,25 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     int32_t max_ops = 0;
     b->payload_units = 0;
     b->prop_records = 0;
+    b->h_nload.assign(D, 0);
+    b->h_nload_segs.assign(D, 0);
     for (int64_t d = 0; d < D; d++) {
         int64_t a = doc_op_off[d], e = doc_op_off[d + 1];
         if (e < a) return MT_ERR_ARG;
         max_ops = std::max<int32_t>(max_ops, (int32_t)(e - a));
+        for (int64_t i = a; i < e; i++) {  // leading SnapshotLoader records
+            const uint8_t t = ops[i].type;
+            if (t != MT_OP_LOAD_HEADER && t != MT_OP_LOAD_BODY && t != MT_OP_COLLAB) break;
+            b->h_nload[d]++;
+            if (t != MT_OP_COLLAB) b->h_nload_segs[d]++;
+        }
+        for (int64_t i = a + b->h_nload[d]; i < e; i++)  // LOAD records only lead a log
+            if (ops[i].type == MT_OP_LOAD_HEADER || ops[i].type == MT_OP_LOAD_BODY || ops[i].type == MT_OP_COLLAB)
+                return MT_ERR_ARG;
         uint64_t pay = 0, nprop_ops = 0;
         for (int64_t i = a; i < e; i++) {
             const mt_op &o = ops[i];
-            if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
+            if (MT_OP_IS_INSERT_LIKE(o.type) && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
                 if ((int64_t)o.payload + (int64_t)o.payload_len > n_text) return MT_ERR_ARG;
                 pay += o.payload_len;
             }
@@ -549,7 +565,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
                 nprop_ops++;
                 b->prop_records += o.payload_len;
             }
-            if (o.type == MT_OP_INSERT && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
+            if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
                 if ((int64_t)o.pos2 + (int64_t)MT_OPF_NPROPS(o.flags) > n_props) return MT_ERR_ARG;
                 nprop_ops++;
                 b->prop_records += MT_OPF_NPROPS(o.flags);
@@ -574,7 +590,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         uint32_t w = 0;
         for (int64_t i = doc_op_off[d]; i < doc_op_off[d + 1]; i++) {
             mt_op &o = h_ops[i];
-            if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
+            if (MT_OP_IS_INSERT_LIKE(o.type) && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
                 if (o.payload_len) memcpy(&h_text[b->h_text_base[d] + w], text + o.payload, 2ull * o.payload_len);
                 o.flags &= (uint16_t)~MT_OPF_INTERNAL;
                 if (o.payload_len && text[o.payload + o.payload_len - 1] == (uint16_t)'\n')
@@ -692,7 +708,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
     }
     // documents short of headroom checkpoint here unless this is the largest usable class
-    const bool can_grow = class_usable(L.cls + 1) && b->opt.max_retries != 0;
+    const bool can_grow = (class_usable(L.cls + 1) && b->opt.max_retries != 0) || L.load;
     if (can_grow) HIPCHK(dalloc(&L.d_ck, (size_t)n * (size_t)mt::ck_words(L.caps.seg)));
     const Launch *prev = L.src >= 0 ? &b->launches[(size_t)L.src] : nullptr;
     if (!L.cksrc.empty()) {
@@ -719,7 +735,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
     P.prof = L.d_prof;
 #endif
-    const void *fn = kKernels[L.cls].replay;
+    const void *fn = L.load ? kKernels[L.cls].load : kKernels[L.cls].replay;
     if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
     void *args[] = {&P};
     HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, s));
@@ -730,6 +746,8 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
 // form one launch (the HBM class in chunks of kMaxHbmDocs), largest documents first within a
 // launch (blocks dispatch roughly in index order: the longest serial replays start first).
 // Launches of different classes run concurrently on the run stream and up to 3 aux streams.
+static int gather_launch(mt_batch *b, int li);
+
 MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
     if (!b || !b->have_log) return MT_ERR_STATE;
     // launches go to the batch's own non-blocking streams, ordered after the caller's stream
@@ -745,18 +763,107 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
     b->cached_doc = -1;
     b->c_blob_doc = -1;
     b->t_launch = std::chrono::steady_clock::now();
-    std::map<int, std::vector<int32_t>, std::greater<int>> groups;
-    for (int64_t d = 0; d < b->n_docs; d++) {
-        // documents start in LDS (the largest LDS class at most: a document reaches the HBM
-        // class only through a checkpoint, after its first ops ran at LDS speed)
-        int c = std::min(class_for(b, (int32_t)(b->h_off[d + 1] - b->h_off[d]), 0), mt::kHbmClass - 1);
+    HIPCHK(hipEventRecord(b->ev0, s));
+    // initial class: from the op count, and for a document that starts from a snapshot from its
+    // loaded segments too (documents start in LDS: the largest LDS class at most, a document
+    // reaches the HBM class only through a checkpoint, after its first ops ran at LDS speed)
+    auto first_class = [&](int64_t d) {
+        int32_t ops = (int32_t)(b->h_off[d + 1] - b->h_off[d]);
+        int c = class_for(b, ops, 0);
+        if (b->opt.seg_cap <= 0 && b->h_nload[d] > 0)
+            while (c + 1 < mt::kNumClasses && mt::kClassSegs[c] < b->h_nload_segs[d] + b->h_nload_segs[d] / 4 + 64) c++;
+        c = std::min(c, mt::kHbmClass - 1);
         while (c > 0 && !class_usable(c)) c--;
-        groups[c].push_back((int32_t)d);
+        return c;
+    };
+    if (b->docout.size() != (size_t)b->n_docs) {
+        b->docout.assign((size_t)b->n_docs, DocOut{});
+        b->where.assign((size_t)b->n_docs, DocRes{});
+    }
+    // SnapshotLoader phase (snapshotLoader.ts:36-205): the leading LOAD records of every document
+    // that has them run in mt_load_kernel, which checkpoints at the first catch-up op; a document
+    // whose loaded tree outgrows its class is loaded again (or resumed) in the next one.
+    std::vector<int32_t> resume_li((size_t)b->n_docs, -1), resume_idx((size_t)b->n_docs, -1);
+    std::vector<uint8_t> loaded_final((size_t)b->n_docs, 0);
+    {
+        std::map<int, std::pair<std::vector<int32_t>, std::vector<int32_t>>> work;  // cls -> (docs, cksrc)
+        std::map<int, int> work_src;
+        for (int64_t d = 0; d < b->n_docs; d++)
+            if (b->h_nload[d] > 0) work[first_class(d)].first.push_back((int32_t)d), work[first_class(d)].second.push_back(-1);
+        while (!work.empty()) {
+            const int cls = work.begin()->first;
+            auto item = std::move(work.begin()->second);
+            const int src = work_src.count(cls) ? work_src[cls] : -1;
+            work.erase(work.begin());
+            work_src.erase(cls);
+            const size_t chunk = cls == mt::kHbmClass ? kMaxHbmDocs : item.first.size();
+            for (size_t at = 0; at < item.first.size(); at += chunk) {
+                Launch L;
+                L.cls = cls;
+                L.load = true;
+                const size_t e = std::min(item.first.size(), at + chunk);
+                L.docs.assign(item.first.begin() + (long)at, item.first.begin() + (long)e);
+                L.cksrc.assign(item.second.begin() + (long)at, item.second.begin() + (long)e);
+                L.src = src;
+                if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) {
+                    L.cksrc.clear();
+                    L.src = -1;
+                }
+                b->launches.push_back(std::move(L));
+                const int li = (int)b->launches.size() - 1;
+                Launch &N = b->launches.back();
+                HIPCHK(hipEventCreate(&N.e0));
+                HIPCHK(hipEventCreate(&N.e1));
+                HIPCHK(hipEventRecord(N.e0, s));
+                int rc = launch_replay(b, s, N);
+                if (rc) return rc;
+                HIPCHK(hipEventRecord(N.e1, s));
+                HIPCHK(hipEventSynchronize(N.e1));
+                HIPCHK(hipEventElapsedTime(&N.ms, N.e0, N.e1));
+                rc = gather_launch(b, li);
+                if (rc) return rc;
+                const Launch &S = b->launches[(size_t)li];
+                for (size_t i = 0; i < S.docs.size(); i++) {
+                    const int32_t d = S.docs[i];
+                    const DocOut &o = b->docout[(size_t)d];
+                    const int nxt = std::min(resume_class(cls), mt::kNumClasses - 1);
+                    if (o.status == MT_CAPACITY && o.cap_kind == mt::kCapCheckpoint && o.ops_done >= b->h_nload[d]) {
+                        resume_li[(size_t)d] = li;  // loaded: the replay resumes from this checkpoint
+                        resume_idx[(size_t)d] = (int32_t)i;
+                    } else if (o.status == MT_CAPACITY && (o.cap_kind == mt::kCapCheckpoint || o.cap_kind == 1) &&
+                               class_usable(nxt) && nxt > cls) {
+                        // short of room while loading: resume (checkpoint) or load again (overflow)
+                        auto &w = work[nxt];
+                        if (w.first.empty() || !work_src.count(nxt) || work_src[nxt] == li) {
+                            w.first.push_back(d);
+                            w.second.push_back(o.cap_kind == mt::kCapCheckpoint ? (int32_t)i : -1);
+                            if (o.cap_kind == mt::kCapCheckpoint) work_src[nxt] = li;
+                        } else {
+                            w.first.push_back(d);
+                            w.second.push_back(-1);  // a different source launch: load from scratch
+                        }
+                    } else {
+                        loaded_final[(size_t)d] = 1;  // loaded with no catch-up ops, or failed
+                    }
+                }
+            }
+        }
+    }
+    b->first0 = (int)b->launches.size();
+    // replay launches: one per (initial class, source load launch), largest documents first
+    std::map<std::pair<int, int>, std::vector<int32_t>, std::greater<std::pair<int, int>>> groups;
+    int64_t n_replay = 0;
+    for (int64_t d = 0; d < b->n_docs; d++) {
+        if (loaded_final[(size_t)d]) continue;
+        const int src = resume_li[(size_t)d];
+        const int c = src >= 0 ? b->launches[(size_t)src].cls : first_class(d);
+        groups[{c, src}].push_back((int32_t)d);
+        n_replay++;
     }
     for (auto &g : groups) {
-        const int cls = g.first;
+        const int cls = g.first.first, src = g.first.second;
         std::vector<int32_t> &docs = g.second;
-        if (groups.size() == 1 && cls != mt::kHbmClass) {
+        if (groups.size() == 1 && cls != mt::kHbmClass && src < 0 && n_replay == b->n_docs) {
             Launch L;
             L.cls = cls;
             b->launches.push_back(L);  // every document, in index order
@@ -770,15 +877,18 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
             Launch L;
             L.cls = cls;
             L.docs.assign(docs.begin() + at, docs.begin() + std::min(docs.size(), at + chunk));
+            if (src >= 0) {
+                L.src = src;
+                for (int32_t d : L.docs) L.cksrc.push_back(resume_idx[(size_t)d]);
+            }
             b->launches.push_back(std::move(L));
         }
     }
-    HIPCHK(hipEventRecord(b->ev0, s));
-    for (size_t i = 0; i < b->launches.size(); i++) {
+    for (size_t i = (size_t)b->first0; i < b->launches.size(); i++) {
         Launch &L = b->launches[i];
         hipStream_t ls = s;
-        if (i > 0) {
-            hipStream_t &a = b->aux[(i - 1) % 3];
+        if (i > (size_t)b->first0) {
+            hipStream_t &a = b->aux[(i - (size_t)b->first0 - 1) % 3];
             if (!a) HIPCHK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
             HIPCHK(hipStreamWaitEvent(a, b->ev0, 0));
             ls = a;
@@ -867,7 +977,7 @@ static int launch_on(mt_batch *b, Launch &&L, int *next_stream, std::vector<int>
 MT_API int mt_batch_sync(mt_batch *b) {
     if (!b || b->launches.empty()) return MT_ERR_STATE;
     std::vector<int> pending;
-    for (int li = 0; li < b->n_first; li++) pending.push_back(li);
+    for (int li = b->first0; li < b->n_first; li++) pending.push_back(li);
     int next_stream = 1, rc = MT_OK;
     while (!pending.empty()) {
         size_t k = 0;
@@ -1072,7 +1182,8 @@ static bool rec_is_text(const OutRec &r) { return !(r.meta & mt::kMetaMarker); }
 static const std::string &client_name(mt_batch *b, int64_t d, uint32_t id, std::string &tmp) {
     const auto &t = clients_of(b, d);
     if (id < t.size()) return t[id];
-    tmp = "undefined";
+    // NonCollabClient segments of a loaded snapshot: Client.getLongClientId(-2) is "original"
+    tmp = id == MT_CLIENT_NONCOLLAB ? "original" : "undefined";
     return tmp;
 }
 
@@ -1348,7 +1459,8 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
     key_rank.push_back(0xFFFFFFFFu);
     for (const std::string &v : b->values) add(val_str, v);
     add_quoted(cli_str, "undefined");
-    const int32_t cli_first = 1, cli_n = (int32_t)b->clients.size();
+    add_quoted(cli_str, "original");  // MT_CLIENT_NONCOLLAB
+    const int32_t cli_first = 2, cli_n = (int32_t)b->clients.size();
     for (const std::string &c : b->clients) add_quoted(cli_str, c);
     std::vector<int32_t> doc_cli;
     if (!b->doc_clients.empty()) {
@@ -1686,7 +1798,7 @@ MT_API int mt_batch_download_log(mt_batch *b, mt_op *ops, int64_t *doc_op_off, u
             for (int64_t i = b->h_off[d]; i < b->h_off[d + 1]; i++) {
                 mt_op &o = ops[i];
                 o.flags &= (uint16_t)~MT_OPF_INTERNAL;
-                if (o.type == MT_OP_INSERT && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) o.payload += (uint32_t)tb;
+                if (MT_OP_IS_INSERT_LIKE(o.type) && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) o.payload += (uint32_t)tb;
             }
             tb += b->h_text_len[d];
         }
@@ -1730,6 +1842,8 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
     free_log(b);
     b->h_off.resize(D + 1);
     b->h_off[0] = 0;
+    b->h_nload.assign(D, 0);
+    b->h_nload_segs.assign(D, 0);
     int32_t max_ops = 0;
     for (int64_t d = 0; d < D; d++) {
         if (doc_ops[d] < 1) return MT_ERR_ARG;

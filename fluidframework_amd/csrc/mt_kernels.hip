@@ -1,9 +1,9 @@
-// mt_kernels.hip — one capacity class of the replay and generator kernels.
+// mt_kernels.hip — one capacity class of the replay, snapshot-load and generator kernels.
 //
 // Compiled once per class with -DMT_SEG=<segment slots> (kClassSegs in mt_device.h); each
-// object exports mt_replay_kernel_<SEG> and mt_generate_kernel_<SEG>, which mt_host.cpp
-// selects per launch.  Keeping the class a template argument makes every LDS table base an
-// immediate offset (mt::make_layout) instead of a runtime pointer.
+// object exports mt_replay_kernel_<SEG>, mt_load_kernel_<SEG> and mt_generate_kernel_<SEG>,
+// which mt_host.cpp selects per launch.  Keeping the class a template argument makes every LDS
+// table base an immediate offset (mt::make_layout) instead of a runtime pointer.
 
 #include "mt_engine.hip"
 
@@ -15,7 +15,13 @@
 #define MT_CAT(a, b) MT_CAT2(a, b)
 
 extern "C" __global__ __launch_bounds__(64) void MT_CAT(mt_replay_kernel_, MT_SEG)(mt::ReplayParams P) {
-    mt::replay_body<MT_SEG>(P);
+    mt::replay_body<MT_SEG, false>(P);
+}
+
+// SnapshotLoader: the leading LOAD_HEADER / COLLAB / LOAD_BODY records of each document, then a
+// checkpoint that the document's first replay launch resumes from
+extern "C" __global__ __launch_bounds__(64) void MT_CAT(mt_load_kernel_, MT_SEG)(mt::ReplayParams P) {
+    mt::replay_body<MT_SEG, true>(P);
 }
 
 extern "C" __global__ __launch_bounds__(64) void MT_CAT(mt_generate_kernel_, MT_SEG)(mt::ReplayParams P) {

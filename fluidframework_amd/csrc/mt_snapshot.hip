@@ -23,6 +23,7 @@
 // coalesced records join exactly as in the reference's concatenated string.
 #include <hip/hip_runtime.h>
 
+#include "../../include/mt_oplog.h"
 #include "mt_device.h"
 
 namespace mt {
@@ -245,7 +246,7 @@ struct Doc {
     __device__ __forceinline__ void str(const uint32_t *tab, uint32_t i) { W.copy(P.strs + tab[2 * i], tab[2 * i + 1]); }
     __device__ __forceinline__ void client(uint32_t id) {
         if (id < (uint32_t)cli_n) str(P.cli_str, (uint32_t)cli_first + id);
-        else str(P.cli_str, 0);  // "undefined"
+        else str(P.cli_str, id == MT_CLIENT_NONCOLLAB ? 1u : 0u);  // "original" / "undefined"
     }
     __device__ __forceinline__ uint32_t key_rank(uint32_t k) const {
         return k < (uint32_t)P.n_keys ? P.key_rank[k] : kNoRank;

@@ -32,8 +32,26 @@ enum mt_op_type {
     MT_OP_INSERT = 0,   /* MergeTreeDeltaType.INSERT   */
     MT_OP_REMOVE = 1,   /* MergeTreeDeltaType.REMOVE   */
     MT_OP_ANNOTATE = 2, /* MergeTreeDeltaType.ANNOTATE */
+    /* SnapshotLoader (merge-tree/src/snapshotLoader.ts:36-205), a document's first records:
+       LOAD_HEADER  one segment of the "header" chunk; the run of them is built bottom-up as
+                    MergeTree.reloadFromSegments does (mergeTree.ts:1195-1251)
+       COLLAB       startOrUpdateCollaboration(observer, minSeq = msn, currentSeq = seq)
+       LOAD_BODY    one segment of a body chunk, appended at the end with insertSegments
+                    (refSeq UniversalSequenceNumber); MT_OPF_GROUP_CONT chains the members of
+                    one batch (consecutive NonCollabClient / UniversalSequenceNumber segments)
+       A LOAD record is an insert record (payload / flags / pos2 as for MT_OP_INSERT) with
+       client = the segment's clientId (MT_CLIENT_NONCOLLAB for NonCollabClient), seq = its
+       seq (0 = UniversalSequenceNumber), ref_seq = its removedSeq (MT_SEQ_NONE if not
+       removed) and msn = its removedClientId (MT_CLIENT_NONE if not removed). */
+    MT_OP_LOAD_HEADER = 3,
+    MT_OP_LOAD_BODY = 4,
+    MT_OP_COLLAB = 5,
     MT_OP_NOOP = 15     /* non-"op" message: only client registration + updateSeqNumbers */
 };
+#define MT_CLIENT_NONCOLLAB 62u /* NonCollabClient (constants.ts:15); long id "original" */
+#define MT_CLIENT_NONE 63u
+#define MT_SEQ_NONE 0x7FFFFFFF
+#define MT_OP_IS_INSERT_LIKE(t) ((t) == MT_OP_INSERT || (t) == MT_OP_LOAD_HEADER || (t) == MT_OP_LOAD_BODY)
 
 /* mt_op.flags: bits 0-3 public flags, bits 4-13 the prop count of an insert (<= 1023),
    bits 14-15 are internal to the library (set at ingest: the insert's text contains a '\n' /

@@ -1,0 +1,152 @@
+"""SnapshotLoader on the GPU: documents start from a SnapshotV1 summary
+(header + body chunks) and replay their catch-up ops, as the replay tool does
+(clientReplayTool.ts:194-252 via snapshotLoader.ts:36-205).
+
+Input per document is {"snapshot": {blob path: JSON}, "messages": [...]} through the native
+JSON ingest; the packer turns the blobs into LOAD records (mt_oplog.h), mt_load_kernel builds the
+tree and checkpoints, the replay resumes.  Every result must equal the oracle's own loader
+(oracle/mergetree.c mto_load_snapshot_v1, pinned by the reference's golden files in
+test_oracle_golden.py) followed by the same messages: state digest (incl. tree shape), text,
+property runs and SnapshotV1 bytes (host and GPU serializers)."""
+import json
+from pathlib import Path
+
+import pytest
+
+import oracle_ffi as O
+import fluidframework_amd as fa
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+SNAP = json.loads((ROOT / "tests" / "golden" / "snapshot_v1.json").read_text())
+NAMES = O.gen_client_names(8)
+KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
+VALS = [json.loads(O.lib().mto_gen_value_json(v).decode()) for v in range(22)]
+
+
+def _messages(p, doc):
+    ops, text, props = O.gen_doc(p, doc)
+    out = []
+    for o in ops:
+        t = int(o["type"])
+        if t == 0:
+            c = {"type": 0, "pos1": int(o["pos1"]),
+                 "seg": text[o["payload"]:o["payload"] + o["payload_len"]].tobytes().decode("utf-16-le")}
+        elif t == 1:
+            c = {"type": 1, "pos1": int(o["pos1"]), "pos2": int(o["pos2"])}
+        else:
+            pr = props[o["payload"]:o["payload"] + o["payload_len"]]
+            c = {"type": 2, "pos1": int(o["pos1"]), "pos2": int(o["pos2"]),
+                 "props": {KEYS[int(q["key"])]: VALS[int(q["value"])] for q in pr}}
+        out.append({"clientId": NAMES[int(o["client"])], "sequenceNumber": int(o["seq"]),
+                    "referenceSequenceNumber": int(o["ref_seq"]), "minimumSequenceNumber": int(o["msn"]),
+                    "type": "op", "contents": c})
+    return out
+
+
+def _oracle_loaded(blobs, msgs):
+    """The oracle's loader + catch-up.  A failing load is a result too: with a body chunk, the
+    reference appends body segments at root.cachedLength (the local view, which counts header
+    segments above seq 0) in the view of refSeq UniversalSequenceNumber (which does not), so a
+    header holding collab-window segments makes insertSegments throw "MergeTree insert failed"
+    (snapshotLoader.ts:166-205, mergeTree.ts:2210-2216); the GPU must report the same status."""
+    d = O.Doc()
+    if d.load_snapshot(blobs, "readonly") != 0:
+        return d
+    for m in msgs:
+        if d.apply_msg(json.dumps(m)) != 0:
+            break
+    return d
+
+
+def _mid_log_case(p, doc, cut, chunk):
+    """(snapshot blobs of the first `cut` messages, the remaining messages)"""
+    msgs = _messages(p, doc)
+    a = O.Doc()
+    a.start_collab("readonly")
+    for m in msgs[:cut]:
+        assert a.apply_msg(json.dumps(m)) == 0, a.error
+    return a.snapshot_v1(chunk), msgs[cut:]
+
+
+def _check(b, i, od):
+    dv = b.doc(i)
+    assert dv.status == od.status, (i, fa.status_string(dv.status), od.error)
+    if od.status:
+        return
+    assert dv.digest() == od.digest(), f"doc {i}: state digest differs\nGPU {dv.shape()}\nCPU {od.shape()}"
+    assert dv.get_text() == od.text()
+    assert dv.props_runs() == json.loads(od.props_runs())
+    assert dv.snapshot_v1() == od.snapshot_v1()
+    assert dv.snapshot_v1(device=True) == od.snapshot_v1()
+
+
+def test_golden_snapshots_load_on_gpu():
+    names = sorted(SNAP)
+    docs = [{"snapshot": {p: c for p, c in SNAP[n]["blobs"]}, "messages": []} for n in names]
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_json([json.dumps(d) for d in docs])
+        b.run()
+        b.snapshots()
+        for i, n in enumerate(names):
+            od = _oracle_loaded(docs[i]["snapshot"], [])
+            _check(b, i, od)
+            assert b.doc(i).snapshot_v1() == docs[i]["snapshot"]  # the golden bytes again
+
+
+@pytest.mark.parametrize("chunk", [10000, 400])
+def test_mid_log_snapshot_then_catch_up(chunk):
+    """Snapshots taken inside the collab window (merge info, tombstones above the MSN, body
+    chunks at small chunk sizes), loaded on the GPU, then the rest of the log."""
+    p = O.gen_params(2500, n_clients=6, max_lag=24, pct_insert=60, pct_remove=30, seed=0x5A4D)
+    docs, oracle = [], []
+    for doc, cut in enumerate([1, 300, 1200, 1900, 2499, 2500, 700, 1500]):
+        blobs, rest = _mid_log_case(p, doc, cut, chunk)
+        docs.append({"snapshot": blobs, "messages": rest})
+        oracle.append(_oracle_loaded(blobs, rest))
+    # documents without a snapshot in the same batch
+    plain = [_messages(p, 100 + k) for k in range(3)]
+    if chunk == 10000:
+        assert sum(od.status == 0 for od in oracle) >= 6
+    with fa.ReplayBatch(len(docs) + len(plain)) as b:
+        b.ingest_json([json.dumps(d) for d in docs] + [json.dumps(m) for m in plain])
+        b.run()
+        b.snapshots()
+        for i, od in enumerate(oracle):
+            _check(b, i, od)
+        for k, msgs in enumerate(plain):
+            od = O.Doc()
+            od.start_collab("readonly")
+            for m in msgs:
+                assert od.apply_msg(json.dumps(m)) == 0
+            _check(b, len(docs) + k, od)
+
+
+def test_snapshot_load_escalates_capacity():
+    """A loaded tree larger than the first class: the load re-runs / resumes in larger classes."""
+    p = O.gen_params(6000, n_clients=4, max_lag=8, pct_insert=75, pct_remove=15, seed=0x10AD)
+    blobs, rest = _mid_log_case(p, 0, 5000, 1 << 30)  # header only
+    docs = [{"snapshot": blobs, "messages": rest}]
+    assert _oracle_loaded(blobs, rest).status == 0
+    with fa.ReplayBatch(1, seg_cap=64) as b:
+        b.ingest_json([json.dumps(d) for d in docs])
+        b.run()
+        assert b.stats()["launches"] > 2
+        b.snapshots()
+        _check(b, 0, _oracle_loaded(blobs, rest))
+
+
+def test_snapshot_blobs_as_objects_or_arrays():
+    """Blobs may be given parsed (objects) or as an ordered array, not only as JSON text."""
+    name = "withAnnotations"
+    blobs = {p: c for p, c in SNAP[name]["blobs"]}
+    forms = [{"snapshot": {k: json.loads(v) for k, v in blobs.items()}, "messages": []},
+             {"snapshot": list(blobs.values()), "messages": []}]
+    od = _oracle_loaded(blobs, [])
+    with fa.ReplayBatch(len(forms)) as b:
+        b.ingest_json([json.dumps(f) for f in forms])
+        b.run()
+        b.snapshots()
+        for i in range(len(forms)):
+            _check(b, i, od)
