@@ -64,17 +64,29 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # MT_BENCH_BACKEND=gloo rehearses the multi-rank path with ranks sharing GPUs (RCCL needs
+    # one rank per device); the real runs use "nccl" (= RCCL) with one process per GPU
+    backend = os.environ.get("MT_BENCH_BACKEND", "nccl")
+    dev = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     torch.cuda.init()
 
     import __graft_entry__ as g
 
-    g.build_lib()
+    # the library is built in-tree beforehand (build()); ranks never compile concurrently
+    if not g.LIB.exists():
+        if rank == 0:
+            g.build_lib()
+        if world > 1:
+            dist.barrier()
     import fluidframework_amd as fa
 
     cfg = dict(CONFIGS[args.config])
@@ -138,7 +150,7 @@ def main():
     elapsed = time.perf_counter() - t0
     t_max = elapsed
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
 

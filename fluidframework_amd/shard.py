@@ -72,6 +72,8 @@ def gather_results(digests, statuses, world: int, rank: int, snapshot_digests=No
     if snapshot_digests is not None:
         cols.append(snapshot_digests.to(torch.int64))
     rec = torch.stack(cols, 1).contiguous()
+    if world > 1 and dist.get_backend() == "gloo":
+        rec = rec.cpu()  # gloo gathers host tensors
     if counts is not None and max(counts) > rec.shape[0]:
         rec = torch.cat([rec, rec.new_zeros((max(counts) - rec.shape[0], rec.shape[1]))], 0)
     if world == 1:
