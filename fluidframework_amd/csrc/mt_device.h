@@ -99,11 +99,22 @@ struct Caps {
 // table pointers or bounds.
 // The last class keeps its tables in HBM instead of LDS (the spill path for documents beyond
 // the largest LDS class; slot and block ids stay 16-bit, so it tops out below 65,535 slots).
-constexpr int kClassSegs[] = {64, 128, 192, 256, 320, 384, 512, 640, 768, 1024, 1280, 1664, 2048, 3072, 4096, 60000};
+// The LDS classes are sized to the residency they buy: LDS is allocated in 1,280-byte granules
+// (128 per CU; measured with tools/probe/lds_residency.hip, profiles/r01_lds_residency.json) and
+// the replay kernel's 128 VGPRs cap a CU at 16 workgroups, so each class is the largest slot
+// count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 6, 5, 4, 3, 2
+// and 1 documents per CU (64 and 128 keep small documents' buffers small).
+constexpr int kClassSegs[] = {64, 128, 280, 323, 368, 408, 456, 540, 628, 848, 1023, 1328, 1764, 2724, 4999, 60000};
 constexpr int kNumClasses = 16;
 constexpr int kHbmClass = kNumClasses - 1;
 constexpr int kHbmSeg = 60000;
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
+constexpr int kCapQueued = 7;      // checkpointed and taken by the launch's follow-on workers
+
+// follow-on queue (one per producer launch, hipMalloc'd, zeroed): word 0 = documents enqueued,
+// 1 = items claimed by workers, 2 = producer workgroups finished, 3 = producer workgroups started,
+// items from word kFqItems: producer workgroup index + 1 (0 = not yet published)
+constexpr int kFqItems = 16;
 
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table
 constexpr int kCkHdr = 32;
@@ -180,6 +191,16 @@ struct ReplayParams {
     int64_t ck_in_words;          // stride of ck_in
     int32_t cold_in_seg;          // stride of cold_in
     uint8_t *hbm_state;           // HBM class: per-workgroup table images (make_layout(kHbmSeg).bytes each)
+    // follow-on workers: a single-round launch (fq_role 1) pushes each document it checkpoints
+    // into fq; a concurrent launch of the next class (fq_role 2, a few workgroups) pops and
+    // resumes them while the producer is still running, so the escalation tail overlaps it
+    uint32_t *fq;
+    int32_t fq_cap;               // items
+    int32_t fq_role;              // 0 none, 1 producer, 2 consumer
+    int64_t fq_producers;         // consumer: workgroups of the producer launch
+    const int32_t *fq_doc_list;   // consumer: the producer's doc_list (null: identity)
+    uint32_t *fq_started;         // producer: host-mapped word set to 1 by the last workgroup to
+                                  // start (the host launches the consumer only then)
 };
 constexpr int kProfSlots = 12;
 

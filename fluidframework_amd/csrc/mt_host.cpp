@@ -29,22 +29,23 @@
 #define MT_DECLARE_CLASS(S)                                                   \
     extern "C" __global__ void mt_replay_kernel_##S(mt::ReplayParams P);      \
     extern "C" __global__ void mt_load_kernel_##S(mt::ReplayParams P);        \
-    extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);
+    extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);    \
+    extern "C" __global__ void mt_follow_kernel_##S(mt::ReplayParams P);
 MT_DECLARE_CLASS(64)
 MT_DECLARE_CLASS(128)
-MT_DECLARE_CLASS(192)
-MT_DECLARE_CLASS(256)
-MT_DECLARE_CLASS(320)
-MT_DECLARE_CLASS(384)
-MT_DECLARE_CLASS(512)
-MT_DECLARE_CLASS(640)
-MT_DECLARE_CLASS(768)
-MT_DECLARE_CLASS(1024)
-MT_DECLARE_CLASS(1280)
-MT_DECLARE_CLASS(1664)
-MT_DECLARE_CLASS(2048)
-MT_DECLARE_CLASS(3072)
-MT_DECLARE_CLASS(4096)
+MT_DECLARE_CLASS(280)
+MT_DECLARE_CLASS(323)
+MT_DECLARE_CLASS(368)
+MT_DECLARE_CLASS(408)
+MT_DECLARE_CLASS(456)
+MT_DECLARE_CLASS(540)
+MT_DECLARE_CLASS(628)
+MT_DECLARE_CLASS(848)
+MT_DECLARE_CLASS(1023)
+MT_DECLARE_CLASS(1328)
+MT_DECLARE_CLASS(1764)
+MT_DECLARE_CLASS(2724)
+MT_DECLARE_CLASS(4999)
 MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
@@ -79,24 +80,41 @@ struct KernelClass {
     const void *replay;
     const void *generate;
     const void *load;
+    const void *follow;
 };
 static const KernelClass kKernels[mt::kNumClasses] = {
-    {64, (const void *)mt_replay_kernel_64, (const void *)mt_generate_kernel_64, (const void *)mt_load_kernel_64},
-    {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128},
-    {192, (const void *)mt_replay_kernel_192, (const void *)mt_generate_kernel_192, (const void *)mt_load_kernel_192},
-    {256, (const void *)mt_replay_kernel_256, (const void *)mt_generate_kernel_256, (const void *)mt_load_kernel_256},
-    {320, (const void *)mt_replay_kernel_320, (const void *)mt_generate_kernel_320, (const void *)mt_load_kernel_320},
-    {384, (const void *)mt_replay_kernel_384, (const void *)mt_generate_kernel_384, (const void *)mt_load_kernel_384},
-    {512, (const void *)mt_replay_kernel_512, (const void *)mt_generate_kernel_512, (const void *)mt_load_kernel_512},
-    {640, (const void *)mt_replay_kernel_640, (const void *)mt_generate_kernel_640, (const void *)mt_load_kernel_640},
-    {768, (const void *)mt_replay_kernel_768, (const void *)mt_generate_kernel_768, (const void *)mt_load_kernel_768},
-    {1024, (const void *)mt_replay_kernel_1024, (const void *)mt_generate_kernel_1024, (const void *)mt_load_kernel_1024},
-    {1280, (const void *)mt_replay_kernel_1280, (const void *)mt_generate_kernel_1280, (const void *)mt_load_kernel_1280},
-    {1664, (const void *)mt_replay_kernel_1664, (const void *)mt_generate_kernel_1664, (const void *)mt_load_kernel_1664},
-    {2048, (const void *)mt_replay_kernel_2048, (const void *)mt_generate_kernel_2048, (const void *)mt_load_kernel_2048},
-    {3072, (const void *)mt_replay_kernel_3072, (const void *)mt_generate_kernel_3072, (const void *)mt_load_kernel_3072},
-    {4096, (const void *)mt_replay_kernel_4096, (const void *)mt_generate_kernel_4096, (const void *)mt_load_kernel_4096},
-    {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000},
+    {64, (const void *)mt_replay_kernel_64, (const void *)mt_generate_kernel_64, (const void *)mt_load_kernel_64,
+     (const void *)mt_follow_kernel_64},
+    {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
+     (const void *)mt_follow_kernel_128},
+    {280, (const void *)mt_replay_kernel_280, (const void *)mt_generate_kernel_280, (const void *)mt_load_kernel_280,
+     (const void *)mt_follow_kernel_280},
+    {323, (const void *)mt_replay_kernel_323, (const void *)mt_generate_kernel_323, (const void *)mt_load_kernel_323,
+     (const void *)mt_follow_kernel_323},
+    {368, (const void *)mt_replay_kernel_368, (const void *)mt_generate_kernel_368, (const void *)mt_load_kernel_368,
+     (const void *)mt_follow_kernel_368},
+    {408, (const void *)mt_replay_kernel_408, (const void *)mt_generate_kernel_408, (const void *)mt_load_kernel_408,
+     (const void *)mt_follow_kernel_408},
+    {456, (const void *)mt_replay_kernel_456, (const void *)mt_generate_kernel_456, (const void *)mt_load_kernel_456,
+     (const void *)mt_follow_kernel_456},
+    {540, (const void *)mt_replay_kernel_540, (const void *)mt_generate_kernel_540, (const void *)mt_load_kernel_540,
+     (const void *)mt_follow_kernel_540},
+    {628, (const void *)mt_replay_kernel_628, (const void *)mt_generate_kernel_628, (const void *)mt_load_kernel_628,
+     (const void *)mt_follow_kernel_628},
+    {848, (const void *)mt_replay_kernel_848, (const void *)mt_generate_kernel_848, (const void *)mt_load_kernel_848,
+     (const void *)mt_follow_kernel_848},
+    {1023, (const void *)mt_replay_kernel_1023, (const void *)mt_generate_kernel_1023, (const void *)mt_load_kernel_1023,
+     (const void *)mt_follow_kernel_1023},
+    {1328, (const void *)mt_replay_kernel_1328, (const void *)mt_generate_kernel_1328, (const void *)mt_load_kernel_1328,
+     (const void *)mt_follow_kernel_1328},
+    {1764, (const void *)mt_replay_kernel_1764, (const void *)mt_generate_kernel_1764, (const void *)mt_load_kernel_1764,
+     (const void *)mt_follow_kernel_1764},
+    {2724, (const void *)mt_replay_kernel_2724, (const void *)mt_generate_kernel_2724, (const void *)mt_load_kernel_2724,
+     (const void *)mt_follow_kernel_2724},
+    {4999, (const void *)mt_replay_kernel_4999, (const void *)mt_generate_kernel_4999, (const void *)mt_load_kernel_4999,
+     (const void *)mt_follow_kernel_4999},
+    {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000,
+     (const void *)mt_follow_kernel_60000},
 };
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
 
@@ -121,7 +139,28 @@ struct Launch {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int level = 0;              // escalation depth (0: a first launch)
     bool load = false;          // SnapshotLoader launch (mt_load_kernel): LOAD records, then a checkpoint
+    // follow-on workers: a producer launch pushes its checkpointed documents to
+    // the consumer launch `follow`, which runs concurrently in the next class; the consumer's
+    // docs / cksrc are read back from the queue when it completes
+    int follow = -1;            // -2: consumer not launched yet
+    bool consumer = false;
+    uint32_t *d_fq = nullptr;   // producer: queue header + items (the consumer reads the same one)
+    uint32_t *h_started = nullptr;  // producer: host-mapped "every workgroup started" word
+    int32_t fq_cap = 0;
+    int32_t workers = 0;
+    // producer: the consumer's buffers, allocated and initialised before the producer runs (a
+    // memset issued while the producer fills every CU would wait for a free slot)
+    int f_cls = -1;
+    OutRec *f_out = nullptr;
+    DocOut *f_docout = nullptr;
+    uint4 *f_cold = nullptr;
+    uint32_t *f_ck = nullptr;
 };
+
+// workgroups (documents) of a launch
+static int64_t launch_n(int64_t n_docs, const Launch &L) {
+    return L.consumer ? (int64_t)L.docs.size() : (L.docs.empty() ? n_docs : (int64_t)L.docs.size());
+}
 
 struct DocRes {  // per-document result location
     int32_t launch = -1;
@@ -330,6 +369,8 @@ struct mt_batch {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent first launches of mixed-size batches
     hipStream_t cstream = nullptr;  // result gathers (never queued behind a running launch)
+    hipStream_t fstream = nullptr;  // follow-on consumer launches
+    uint32_t *h_started = nullptr;  // host-mapped: per first launch, 1 once all its workgroups started
     hipEvent_t ev_user = nullptr;
     uint64_t *d_digest = nullptr;  // mt_batch_device_digests
     float kernel_ms = 0, total_ms = 0;
@@ -377,6 +418,11 @@ static void free_launches(mt_batch *b) {
         (void)hipFree(L.d_ck);
         (void)hipFree(L.d_cksrc);
         (void)hipFree(L.d_state);
+        (void)hipFree(L.d_fq);
+        (void)hipFree(L.f_out);
+        (void)hipFree(L.f_docout);
+        (void)hipFree(L.f_cold);
+        (void)hipFree(L.f_ck);
         if (L.e0) (void)hipEventDestroy(L.e0);
         if (L.e1) (void)hipEventDestroy(L.e1);
     }
@@ -461,6 +507,8 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     for (hipStream_t a : b->aux)
         if (a) (void)hipStreamDestroy(a);
     if (b->cstream) (void)hipStreamDestroy(b->cstream);
+    if (b->fstream) (void)hipStreamDestroy(b->fstream);
+    if (b->h_started) (void)hipHostFree(b->h_started);
     if (b->ev_user) (void)hipEventDestroy(b->ev_user);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -724,6 +772,18 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.cold = L.d_cold;
     P.hbm_state = L.d_state;
     P.ck_out = L.d_ck;
+    if (L.fq_cap > 0 && L.d_ck) {
+        // header, items, then a trace: per item the publish time and the consumer's
+        // (started, item seen, done) times on the 100 MHz clock (MT_DEBUG_FOLLOW prints them)
+        HIPCHK(dalloc(&L.d_fq, (size_t)mt::kFqItems + 5 * (size_t)L.fq_cap));
+        HIPCHK(hipMemsetAsync(L.d_fq, 0, 4 * ((size_t)mt::kFqItems + 5 * (size_t)L.fq_cap), s));
+        P.fq = L.d_fq;
+        P.fq_cap = L.fq_cap;
+        P.fq_role = 1;
+        P.fq_started = L.h_started;
+    } else {
+        L.fq_cap = 0;
+    }
     if (!L.cksrc.empty() && prev) {
         P.ck_in = prev->d_ck;
         P.ck_src = L.d_cksrc;
@@ -739,6 +799,152 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
     void *args[] = {&P};
     HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, s));
+    return MT_OK;
+}
+
+// Follow-on workers for a first launch whose escalation tail would otherwise run after it (a
+// launch that fits the GPU in about one round: its last documents finish together, and a document
+// that checkpoints would resume only then, replaying its remaining ops at one-wave latency as a
+// second serial phase).  Off for SnapshotLoader launches, the HBM class and batches that cannot
+// escalate.  MT_FOLLOW_WORKERS overrides the worker count (0: off).
+static int follow_workers(mt_batch *b, const Launch &L, int64_t n) {
+    static int env = -2;
+    if (env == -2) {
+        const char *e = getenv("MT_FOLLOW_WORKERS");
+        env = e && *e ? atoi(e) : -1;
+    }
+    if (env == 0 || L.load || L.level != 0 || L.cls == mt::kHbmClass || b->opt.max_retries <= 0) return 0;
+    int nxt = resume_class(L.cls);
+    while (nxt > L.cls + 1 && !class_usable(nxt)) nxt--;
+    if (!class_usable(L.cls + 1) || !class_usable(nxt) || nxt == mt::kHbmClass) return 0;
+    static int n_cu = -1;
+    if (n_cu < 0) {
+        int dev = 0;
+        hipDeviceProp_t p;
+        n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 256;
+    }
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)(160 * 1024) / (int64_t)std::max<size_t>(1, class_lds(L.cls))));
+    if (n > 2 * (int64_t)n_cu * per_cu) return 0;
+    const int64_t g = env > 0 ? env : 64;
+    return (int)std::min<int64_t>(g, n);
+}
+
+// the consumer's class and buffers, before the producer is launched on stream s
+static int prep_follow(Launch &L, hipStream_t s) {
+    int cls = resume_class(L.cls);
+    while (cls > L.cls + 1 && !class_usable(cls)) cls--;
+    L.f_cls = cls;
+    const Caps c = mt::class_caps(mt::kClassSegs[cls]);
+    const size_t n = (size_t)L.fq_cap;
+    HIPCHK(dalloc(&L.f_out, n * (size_t)c.oe));
+    HIPCHK(dalloc(&L.f_docout, n));
+    HIPCHK(hipMemsetAsync(L.f_docout, 0xFF, sizeof(DocOut) * n, s));  // status -1: not replayed
+    HIPCHK(dalloc(&L.f_cold, n * (size_t)c.seg));
+    if (class_usable(cls + 1)) HIPCHK(dalloc(&L.f_ck, n * (size_t)mt::ck_words(c.seg)));
+    return MT_OK;
+}
+
+// the consumer of producer launch `pi`: `workers` workgroups of the next class popping the
+// producer's queue (results at the queue index; docs / cksrc read back in gather_follow)
+static int launch_follow(mt_batch *b, int pi) {
+    if (!b->fstream) HIPCHK(hipStreamCreateWithFlags(&b->fstream, hipStreamNonBlocking));
+    hipStream_t s = b->fstream;
+    Launch C;
+    {
+        const Launch &Pr = b->launches[(size_t)pi];
+        C.cls = Pr.f_cls;
+        C.consumer = true;
+        C.src = pi;
+        C.level = 1;
+        C.fq_cap = Pr.fq_cap;
+        C.workers = Pr.workers;
+    }
+    b->launches.push_back(std::move(C));
+    const int li = (int)b->launches.size() - 1;
+    Launch &L = b->launches.back();
+    const Launch &Pr = b->launches[(size_t)pi];
+    const int64_t n = L.fq_cap;
+    L.caps = mt::class_caps(mt::kClassSegs[L.cls]);
+    L.out_cap = L.caps.oe;
+    L.lds = class_lds(L.cls);
+    {
+        Launch &Pm = b->launches[(size_t)pi];
+        L.d_out = Pm.f_out;
+        L.d_docout = Pm.f_docout;
+        L.d_cold = Pm.f_cold;
+        L.d_ck = Pm.f_ck;
+        Pm.f_out = nullptr;
+        Pm.f_docout = nullptr;
+        Pm.f_cold = nullptr;
+        Pm.f_ck = nullptr;
+    }
+    mt::ReplayParams P = base_params(b);
+    P.out = L.d_out;
+    P.doc_out = L.d_docout;
+    P.n_docs = n;
+    P.out_cap = L.out_cap;
+    P.cold = L.d_cold;
+    P.ck_out = L.d_ck;
+    P.ck_in = Pr.d_ck;
+    P.cold_in = Pr.d_cold;
+    P.ck_in_words = mt::ck_words(Pr.caps.seg);
+    P.cold_in_seg = Pr.caps.seg;
+    P.fq = Pr.d_fq;
+    P.fq_cap = L.fq_cap;
+    P.fq_role = 2;
+    P.fq_producers = launch_n(b->n_docs, Pr);
+    P.fq_doc_list = Pr.d_list;
+#ifdef MT_PROF
+    HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
+    P.prof = L.d_prof;
+#endif
+    const void *fn = kKernels[L.cls].follow;
+    if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
+    HIPCHK(hipEventCreate(&L.e0));
+    HIPCHK(hipEventCreate(&L.e1));
+    HIPCHK(hipEventRecord(L.e0, s));
+    void *args[] = {&P};
+    HIPCHK(hipLaunchKernel(fn, dim3((unsigned)L.workers), dim3(64), args, L.lds, s));
+    HIPCHK(hipEventRecord(L.e1, s));
+    b->launches[(size_t)pi].follow = li;
+    if (getenv("MT_DEBUG_FOLLOW"))
+        fprintf(stderr, "mtreplay: follow-on consumer of launch %d (class %d, %d workers) at %.3f ms\n", pi,
+                mt::kClassSegs[L.cls], L.workers,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count());
+    return MT_OK;
+}
+
+// a completed consumer: its documents are the queue's items, in queue order
+static int gather_follow(mt_batch *b, int li) {
+    Launch &L = b->launches[(size_t)li];
+    const Launch &Pr = b->launches[(size_t)L.src];
+    std::vector<uint32_t> q((size_t)mt::kFqItems + 5 * (size_t)L.fq_cap);
+    if (!b->cstream) HIPCHK(hipStreamCreateWithFlags(&b->cstream, hipStreamNonBlocking));
+    HIPCHK(hipMemcpyAsync(q.data(), Pr.d_fq, 4 * q.size(), hipMemcpyDeviceToHost, b->cstream));
+    HIPCHK(hipStreamSynchronize(b->cstream));
+    const uint32_t n = std::min<uint32_t>(q[0], (uint32_t)L.fq_cap);
+    L.docs.clear();
+    L.cksrc.clear();
+    for (uint32_t i = 0; i < n; i++) {
+        const int32_t w = (int32_t)q[(size_t)mt::kFqItems + i] - 1;
+        if (w < 0 || w >= launch_n(b->n_docs, Pr)) return MT_INTERNAL;
+        L.docs.push_back(Pr.docs.empty() ? w : Pr.docs[(size_t)w]);
+        L.cksrc.push_back(w);
+    }
+    if (getenv("MT_DEBUG_FOLLOW") && n > 0) {
+        const uint32_t *pub = q.data() + mt::kFqItems + L.fq_cap, *tr = pub + L.fq_cap;
+        uint32_t t0 = pub[0];
+        for (uint32_t i = 0; i < n; i++) t0 = std::min(t0, std::min(pub[i], tr[3 * i]));
+        for (uint32_t i = 0; i < n; i++)
+            fprintf(stderr, "mtreplay: follow item %u doc %d: published %+.3f ms, worker started %+.3f, took it %+.3f, done %+.3f\n",
+                    i, L.docs[i], (pub[i] - t0) * 1e-5, (tr[3 * i] - t0) * 1e-5, (tr[3 * i + 1] - t0) * 1e-5,
+                    (tr[3 * i + 2] - t0) * 1e-5);
+    }
+    if (n > 0) {
+        HIPCHK(dalloc(&L.d_list, (size_t)n));
+        HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * (size_t)n, hipMemcpyHostToDevice, b->cstream));
+        HIPCHK(hipStreamSynchronize(b->cstream));
+    }
     return MT_OK;
 }
 
@@ -896,11 +1102,30 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
         HIPCHK(hipEventCreate(&L.e0));
         HIPCHK(hipEventCreate(&L.e1));
         HIPCHK(hipEventRecord(L.e0, ls));
+        L.workers = follow_workers(b, L, launch_n(b->n_docs, L));
+        L.fq_cap = L.workers;  // one queue slot per consumer workgroup
+        if (L.fq_cap > 0) {
+            const size_t k = i - (size_t)b->first0;
+            if (!b->h_started) HIPCHK(hipHostMalloc((void **)&b->h_started, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent));
+            if (k < 64) {
+                ((volatile uint32_t *)b->h_started)[k] = 0;
+                L.h_started = b->h_started + k;
+                L.follow = -2;
+            } else {
+                L.workers = L.fq_cap = 0;
+            }
+        }
+        if (L.fq_cap > 0) {
+            int rc = prep_follow(L, ls);
+            if (rc) return rc;
+        }
         int rc = launch_replay(b, ls, L);
         if (rc) return rc;
         HIPCHK(hipEventRecord(L.e1, ls));
         if (ls != s) HIPCHK(hipStreamWaitEvent(s, L.e1, 0));
     }
+    // the consumers are launched by mt_batch_sync once every producer workgroup is resident
+    // (a worker dispatched ahead of a producer's workgroups would hold LDS they need)
     b->n_first = (int)b->launches.size();
     HIPCHK(hipEventRecord(b->ev1, s));
     b->run_stream = s;
@@ -909,7 +1134,8 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
 
 static int gather_launch(mt_batch *b, int li) {
     Launch &L = b->launches[li];
-    int64_t n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+    int64_t n = launch_n(b->n_docs, L);
+    if (n == 0) return MT_OK;
 #ifdef MT_PROF
     {
         std::vector<uint64_t> pf((size_t)n * mt::kProfSlots);
@@ -977,11 +1203,25 @@ static int launch_on(mt_batch *b, Launch &&L, int *next_stream, std::vector<int>
 MT_API int mt_batch_sync(mt_batch *b) {
     if (!b || b->launches.empty()) return MT_ERR_STATE;
     std::vector<int> pending;
-    for (int li = b->first0; li < b->n_first; li++) pending.push_back(li);
+    for (int li = b->first0; li < b->n_first; li++)
+        if (!b->launches[(size_t)li].consumer) pending.push_back(li);
     int next_stream = 1, rc = MT_OK;
+    // follow-on consumers: launched as soon as their producer is resident (or has finished)
+    auto launch_ready_follows = [&](int only) -> int {
+        for (int li = b->first0; li < b->n_first; li++) {
+            if (b->launches[(size_t)li].follow != -2) continue;
+            const Launch &Pr = b->launches[(size_t)li];
+            if (li != only && !((volatile uint32_t *)Pr.h_started)[0]) continue;
+            int r = launch_follow(b, li);
+            if (r) return r;
+        }
+        return MT_OK;
+    };
     while (!pending.empty()) {
         size_t k = 0;
         for (;; std::this_thread::sleep_for(std::chrono::microseconds(20))) {
+            rc = launch_ready_follows(-1);
+            if (rc) return rc;
             for (k = 0; k < pending.size(); k++) {
                 hipError_t q = hipEventQuery(b->launches[(size_t)pending[k]].e1);
                 if (q == hipSuccess) break;
@@ -995,11 +1235,24 @@ MT_API int mt_batch_sync(mt_batch *b) {
             Launch &L = b->launches[(size_t)li];
             HIPCHK(hipEventElapsedTime(&L.ms, L.e0, L.e1));
         }
+        if (b->launches[(size_t)li].consumer) {
+            rc = gather_follow(b, li);
+            if (rc) return rc;
+        }
         rc = gather_launch(b, li);
         if (rc) return rc;
+        // a producer's consumer is gathered after it (it overrides the queued documents' results)
+        if (b->launches[(size_t)li].follow == -2) {
+            rc = launch_ready_follows(li);
+            if (rc) return rc;
+        }
+        if (b->launches[(size_t)li].follow >= 0) pending.push_back(b->launches[(size_t)li].follow);
         const Launch &S = b->launches[(size_t)li];
+        if (S.consumer)
+            for (size_t i = 0; i < S.docs.size(); i++)
+                if (b->docout[(size_t)S.docs[i]].status < 0) return MT_INTERNAL;  // an item no worker replayed
         if (S.level >= b->opt.max_retries) continue;
-        const int64_t n = S.docs.empty() ? b->n_docs : (int64_t)S.docs.size();
+        const int64_t n = launch_n(b->n_docs, S);
         std::map<int, Launch> groups;
         for (int64_t i = 0; i < n; i++) {
             const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
@@ -1065,7 +1318,8 @@ MT_API int mt_batch_device_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_de
         P.out = L.d_out;
         P.doc_out = L.d_docout;
         P.doc_list = L.d_list;
-        P.n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+        P.n = launch_n(b->n_docs, L);
+        if (P.n == 0) continue;
         P.out_cap = L.out_cap;
         P.text = b->d_text;
         P.doc_text_base = b->d_text_base;
@@ -1115,10 +1369,11 @@ MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *o) {
     const Launch &L = b->launches[(size_t)i];
     memset(o, 0, sizeof *o);
     o->seg_class = mt::kClassSegs[L.cls];
-    o->n_docs = L.docs.empty() ? (int32_t)b->n_docs : (int32_t)L.docs.size();
+    o->n_docs = (int32_t)launch_n(b->n_docs, L);
     o->resumed = (int32_t)std::count_if(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x >= 0; });
     o->lds_bytes = (int32_t)L.lds;
     o->ms = L.ms;
+    o->workers = L.consumer ? L.workers : 0;
     o->ops = L.ops;
     return MT_OK;
 }
@@ -1507,7 +1762,7 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
         }
         for (size_t li = 0; li < b->launches.size() && !rc; li++) {
             const Launch &L = b->launches[li];
-            const int64_t n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+            const int64_t n = launch_n(b->n_docs, L);
             std::vector<uint8_t> fm((size_t)n);
             for (int64_t i = 0; i < n; i++) fm[i] = b->where[L.docs.empty() ? i : L.docs[i]].launch == (int32_t)li;
             if (!up(&d_final[li], fm)) fail(MT_ERR_HIP);
@@ -1555,7 +1810,8 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                 P.out = L.d_out;
                 P.doc_out = L.d_docout;
                 P.doc_list = L.d_list;
-                P.n = L.docs.empty() ? b->n_docs : (int64_t)L.docs.size();
+                P.n = launch_n(b->n_docs, L);
+                if (P.n == 0) continue;
                 P.out_cap = L.out_cap;
                 P.text = b->d_text;
                 P.doc_text_base = b->d_text_base;

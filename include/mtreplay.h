@@ -147,7 +147,9 @@ typedef struct mt_launch_info {
     int32_t resumed;        /* of them resumed from a checkpoint (the rest start from op 0)   */
     int32_t lds_bytes;      /* dynamic LDS per document (0: HBM class)                        */
     float ms;               /* device time (hipEvents on the run stream)                      */
-    int32_t reserved;
+    int32_t workers;        /* follow-on consumer launch: its worker workgroups (0: a launch of
+                               one workgroup per document); it runs concurrently with the launch
+                               that queued its documents                      */
     int64_t ops;            /* ops applied by this launch                                     */
 } mt_launch_info;
 MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *out);

@@ -104,6 +104,37 @@ def test_small_capacity_escalation():
     assert stats["launches"] >= 2
 
 
+def test_follow_on_workers_resume_checkpointed_documents():
+    """A one-round first launch queues the documents it checkpoints to a concurrent consumer
+    launch of the next class; the queued documents' results come from there,
+    further escalations continue from the consumer's checkpoints, all bit-exact."""
+    n = 384
+    p = O.gen_params(900, pct_insert=55, pct_remove=35, seed=0xF0110)
+    ops, text, props, off = O.gen_batch(p, n)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(n, seg_cap=64, max_retries=8) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        b.set_clients(names)
+        b.ingest(ops, off, text, props)
+        for _ in range(2):  # a second run reuses the batch (fresh queues)
+            b.run()
+            launches = b.launches()
+            cons = [li for li in launches if li["workers"] > 0]
+            assert cons and cons[0]["n_docs"] > 0 and cons[0]["resumed"] == cons[0]["n_docs"], launches
+            assert launches[0]["n_docs"] == n
+            for d in range(n):
+                dv = b.doc(d)
+                assert dv.status == st[d]
+                assert dv.digest() == int(dig[d]), f"doc {d} digest differs"
+            for d in range(0, n, 37):
+                a, e = off[d], off[d + 1]
+                assert_doc_parity(b.doc(d), O.replay_doc(ops[a:e].copy(), text, props, t, names))
+        b.snapshots()
+        for d in range(0, n, 53):
+            assert b.doc(d).snapshot_v1(device=True) == b.doc(d).snapshot_v1()
+
+
 def test_gpu_generator_matches_oracle_generator():
     p = O.gen_params(700, pct_insert=55, pct_remove=35, seed=12345)
     n = 12

@@ -1,0 +1,51 @@
+"""Register / scratch budget of the replay kernels (CPU: reads the gfx950 code objects built
+by __graft_entry__.build()).
+
+The replay engine keeps every document's per-op control in registers; the class kernels run
+one wavefront per document and rely on 4 waves per SIMD (16 documents per CU, the config-2
+residency) — i.e. at most 128 VGPRs (512-entry register file / 4) — and must not spill to
+scratch.  A change that pushes a replay kernel past that silently halves residency (measured:
+22.3 ms -> 35 ms per config-2 launch), so it is pinned here."""
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+OBJ = ROOT / "fluidframework_amd" / "build" / "release"
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+
+
+def _notes(obj: Path, tmp: Path) -> str:
+    fat, co = tmp / (obj.stem + ".fatbin"), tmp / (obj.stem + ".co")
+    subprocess.run([str(LLVM / "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", str(obj), str(tmp / "x.o")],
+                   check=True, capture_output=True)
+    subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+    return subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(co)], check=True, capture_output=True,
+                          text=True).stdout
+
+
+def _kernels(notes: str) -> dict:
+    out = {}
+    for block in notes.split("  - .")[1:]:
+        m = re.search(r"\.name:\s+(\S+)", block)
+        if not m:
+            continue
+        out[m.group(1)] = {k: int(v) for k, v in re.findall(r"\.(vgpr_count|private_segment_fixed_size):\s+(\d+)", block)}
+    return out
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-readelf").exists() or not OBJ.exists(), reason="no build / ROCm llvm tools")
+@pytest.mark.parametrize("seg", [280, 323, 1023, 1328])
+def test_replay_kernel_fits_four_waves_per_simd(seg, tmp_path):
+    obj = OBJ / f"k{seg}.o"
+    if not obj.exists():
+        pytest.skip("class object not built")
+    k = _kernels(_notes(obj, tmp_path))
+    r = k[f"mt_replay_kernel_{seg}"]
+    assert r["vgpr_count"] <= 128, r
+    assert r["private_segment_fixed_size"] == 0, r
+    assert f"mt_follow_kernel_{seg}" in k
