@@ -709,11 +709,12 @@ struct Engine {
     // The settled sums do not change (both halves inherit the segment's state).  The cold
     // record is read now and written back in resolve_cold(); a second split of the same op
     // forwards the first one's pending records instead of reading HBM.
-    MT_FI void split_at(int32_t blk, int32_t k, uint32_t r) {
+    // Returns the leaf block the right half landed in (-1: no split).
+    MT_FI int32_t split_at(int32_t blk, int32_t k, uint32_t r) {
         PF_SCOPE(2);
         const uint32_t slot = rfl((uint32_t)b_child[blk * 8 + k]);
         const uint32_t meta = s_meta[slot];
-        if (meta & kMetaMarker) return;  // Marker.createSplitSegmentAt returns undefined
+        if (meta & kMetaMarker) return -1;  // Marker.createSplitSegmentAt returns undefined
         uint4 cr;
         if (pend_n > 0 && slot == ps0) {
             resolve_splits();  // (inverted range) the first split's left half is cut again
@@ -724,7 +725,7 @@ struct Engine {
             cr = cold[slot];
         }
         const int32_t ns = alloc_slot();
-        if (ns < 0) return;
+        if (ns < 0) return -1;
         const uint32_t len = s_len[slot];
         if (pend_n == 0) {
             ps0 = slot;
@@ -746,8 +747,9 @@ struct Engine {
         s_len[slot] = r;
         wsync();
         if (meta & kMetaUnsettled) u_push((uint32_t)ns);
-        insert_leaf(blk, k + 1, (uint32_t)ns);
+        const int32_t nb = insert_leaf(blk, k + 1, (uint32_t)ns);
         if (meta & kMetaHasOvl) resolve_cold();  // view_of reads the halves' overlap masks from HBM
+        return nb;
     }
 
     // write the pending splits' cold records and start the text loads for ends-with-'\n'
@@ -788,17 +790,33 @@ struct Engine {
         Walk W = descend(pos, ref, c, false);
         if (W.blk >= 0 && W.ok && W.k < W.n && W.excl < pos) {
             const int32_t s0 = splits;
-            split_at(W.blk, W.k, pos - W.excl);
+            const int32_t nb = split_at(W.blk, W.k, pos - W.excl);
             if (status) return W;
             if (splits == s0) {
                 // no block split: the left half ends at pos, the right half (k + 1) starts there
                 W.k += 1;
                 W.n += 1;
-                W.excl = pos;
             } else {
-                ensure_overlay(ref, c);
-                W = descend(pos, ref, c, false);
+                // The leaf block (7 children + the right half) split 4 + 4 (split_leaf).  The
+                // walk the reference repeats lands here without a new descent: every block left
+                // of the left half's block ends before pos, and the first one reaching pos is
+                //  - blk itself when both halves stayed in it (right half at k + 1 <= 3),
+                //  - blk at its end when the left half is blk's last child (k + 1 == 4: blk ends
+                //    exactly at pos, and no leaf after it in blk can tie),
+                //  - the new block otherwise, right half at k + 1 - 4 (blk ends before pos).
+                // W.base is left stale: boundary's callers read only blk / k / n / ok.
+                const int32_t kr = W.k + 1;
+                if (kr < kMaxNodes / 2) {
+                    W.k = kr;
+                } else if (kr == kMaxNodes / 2) {
+                    W.k = kMaxNodes / 2;
+                } else {
+                    W.blk = nb;
+                    W.k = kr - kMaxNodes / 2;
+                }
+                W.n = kMaxNodes / 2;
             }
+            W.excl = pos;
         }
         return W;
     }
