@@ -1,15 +1,19 @@
 #!/usr/bin/env python3
 """Benchmark: sequenced merge-tree ops/sec of the MI355X batch replay engine.
 
-One step = one replay (mt_replay_kernel) of every document of this rank's batch, starting
-from empty documents, with the synthetic op logs already resident in HBM.  Workload
-(BASELINE.json configs[1]): 4,096 docs x 2,000 text-only insert/removeRange ops per GPU,
-8 writer clients, refSeq lag <= 32; `--config 3` selects configs[2]'s op mix
-(65,536 docs x 10k ops, 10% annotate) scaled per GPU with --docs/--ops.
+One step = one replay (mt_replay_kernel, every capacity-class launch) of every document of this
+rank's batch from empty documents, with the synthetic op logs already resident in HBM, then the
+per-document device digests (mt_digest_kernel) and their gather to rank 0 — SURVEY.md §8(d):
+"wall-clock from ingested logs in HBM to final state plus digests on rank 0".
+
+Default workload = the north-star headline, BASELINE.json configs[2]: 65,536 documents x 10,000
+ops per GPU (insert 55 / remove 35 / annotate 10, 8 writer clients, refSeq lag <= 32, minSeq
+advancing with zamboni).  `--config 2` = configs[1] (4,096 docs x 2k text-only ops),
+`--config 4` = configs[3] (Zipf sizes), `--config 5` = configs[4] (+ SnapshotV1 of every document).
 
 Multi-GPU: one process per GPU (torchrun); documents shard across ranks with no data-path
-collective (weak scaling); after the timed steps rank 0 gathers per-document results with
-RCCL (torch.distributed "nccl").  rank 0 prints ONE JSON line.
+collective (weak scaling); rank 0 gathers per-document results with RCCL (torch.distributed
+"nccl").  rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -24,12 +28,14 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md: 8.0 TB/s spec)
+LDS_PEAK_GBS = 150000.0  # MI355X_MICROARCH.md §LDS: ~150 TB/s aggregate (256 B/clk/CU, 256 CUs, ~2.4 GHz)
 
 CONFIGS = {
     2: dict(docs=4096, ops=2000, n_clients=8, max_lag=32, pct_insert=60, pct_remove=40,
             workload="configs[1]: 4,096 docs x 2k text-only insert/removeRange ops, 8 clients, refSeq lag<=32"),
-    3: dict(docs=8192, ops=10000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35,
-            workload="configs[2] mix: docs x 10k ops, 10% annotate, minSeq advance/zamboni, 8 clients"),
+    3: dict(docs=65536, ops=10000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35,
+            workload="configs[2]: 65,536 docs x 10k ops per GPU, insert 55 / remove 35 / annotate 10, "
+                     "minSeq advance + zamboni, 8 clients, refSeq lag<=32"),
     4: dict(docs=16384, ops=200000, ops_min=1000, zipf_s=1.1, n_clients=8, max_lag=32, pct_insert=70, pct_remove=20,
             workload="configs[3]: Zipf(s=1.1) document sizes by rank over [1k, 200k] ops (70/20/10 mix), "
                      "16,384 docs per GPU, LPT-balanced across GPUs, largest documents through the LDS ladder "
@@ -45,12 +51,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: config)")
     ap.add_argument("--ops", type=int, default=0, help="ops per document (default: config)")
     ap.add_argument("--seed", type=int, default=0xDEADBEEF)
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="oracle baseline sample (default: auto)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (default: every usable core)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--snapshot", action="store_true", help="serialize SnapshotV1 of every doc in each step")
     return ap.parse_args()
@@ -121,26 +127,39 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     with_snap = args.snapshot or cfg.get("snapshot", False)
-    for i in range(args.warmup):
+    import numpy as np
+
+    dig_t = torch.empty(n_docs, dtype=torch.int64, device="cuda")
+    snap_t = torch.empty(n_docs, dtype=torch.int64, device="cuda") if with_snap else None
+
+    def step():
+        """replay + digests (+ SnapshotV1) of this rank's documents, gathered to rank 0"""
         b.run(stream)
+        sn = b.snapshots() if with_snap else None
+        b.device_digests(dig_t)
         if with_snap:
-            b.snapshots()
+            b.snapshot_digests(snap_t)
+        st_t = torch.from_numpy(b.counters()["status"].astype(np.int64)).to(dig_t.device)
+        return sn, shard.gather_results(dig_t, st_t, world, rank, snap_t, counts)
+
+    for i in range(args.warmup):
+        step()
         log(rank, f"warmup {i}: {b.stats()['kernel_ms']:.1f} ms kernel")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms, first_ms, first_ops, snap_ms, snap_bytes = [], [], [], [], 0
+    gathered = None
     for i in range(args.steps):
-        b.run(stream)
+        sn, gathered = step()
         kernel_ms.append(b.stats()["kernel_ms"])
         # the dominant kernel: the launch that applied the most ops (launch 0 in uniform batches)
         l0 = max(b.launches(), key=lambda li: li["ops"])
         first_ms.append(l0["ms"])
         first_ops.append(l0["ops"])
         dom_class = l0["seg_class"]
-        if with_snap:  # SnapshotV1 of every document, part of the step
-            sn = b.snapshots()
+        if with_snap:
             snap_ms.append(sn["device_ms"])
             snap_bytes = sn["bytes"]
         log(rank, f"step {i}: {kernel_ms[-1]:.1f} ms kernel" + (f", {snap_ms[-1]:.1f} ms snapshot" if with_snap else ""))
@@ -149,34 +168,24 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     t_max = elapsed
+    st = b.stats()
+    ops_done = int(st["ops_applied"])  # ops applied per step on this rank (same every step)
+    ops_all = ops_done
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
+        dev = "cuda" if backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
-
-    st = b.stats()
-    statuses = b.statuses()
-    import numpy as np
+        o = torch.tensor([ops_done], device=dev, dtype=torch.int64)
+        dist.all_reduce(o, op=dist.ReduceOp.SUM)
+        ops_all = int(o.item())
+    summaries = None
+    if with_snap:  # the SnapshotV1 bytes themselves to rank 0 (after the timed steps)
+        summaries = gather_summaries(b, torch, dist, world, rank, backend)
 
     cnt = b.counters()
     capacity = {f: [int(np.percentile(cnt[f], q)) for q in (50, 99, 100)]
                 for f in ("max_slots", "max_unsettled", "max_blocks", "max_heap")}
-    ops_done = st["ops_applied"]
-    # gather the per-document device digests and statuses to rank 0 over RCCL (untimed)
-    dig_t = torch.empty(n_docs, dtype=torch.int64, device="cuda")
-    b.device_digests(dig_t)
-    st_t = torch.from_numpy(statuses.astype("int64")).cuda()
-    torch.cuda.synchronize()
-    tg = time.perf_counter()
-    snap_t = None
-    if with_snap:  # per-document digest of the GPU SnapshotV1 bytes, gathered with the rest
-        snap_t = torch.empty(n_docs, dtype=torch.int64, device="cuda")
-        b.snapshot_digests(snap_t)
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-    gathered = shard.gather_results(dig_t, st_t, world, rank, snap_t, counts)
-    torch.cuda.synchronize()
-    gather_ms = 1e3 * (time.perf_counter() - tg)
     all_ok, digest_xor, snap_xor = 0, None, None
     if rank == 0:
         all_dig, all_st = gathered[:2]
@@ -184,8 +193,9 @@ def main():
         digest_xor = f"{int(np.bitwise_xor.reduce(all_dig)):016x}"
         if with_snap:
             snap_xor = f"{int(np.bitwise_xor.reduce(gathered[2])):016x}"
-    total_ops = total_ops_step * args.steps
-    value = total_ops / t_max
+    # throughput counts the ops actually applied (a document that stopped early counts only its
+    # applied ops); requested_ops_per_step is reported beside it
+    value = ops_all * args.steps / t_max
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     alg_bytes = b.algorithmic_bytes()
     # roofline of the dominant kernel (launch 0, mt_replay_kernel_<class>): the algorithmic bytes
@@ -194,8 +204,9 @@ def main():
     avg_first_ms = sum(first_ms) / len(first_ms)
     first_bytes = alg_bytes * (sum(first_ops) / len(first_ops)) / max(1, ops_done)
     achieved_gbs = first_bytes / (avg_first_ms * 1e-3) / 1e9
-
-    traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, f"mt_replay_kernel_{dom_class}")
+    kname = f"mt_replay_kernel_{dom_class}"
+    traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, kname)
+    lds = lds_roofline(args.config, n_docs, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
@@ -204,7 +215,8 @@ def main():
     if with_snap:
         avg_snap = sum(snap_ms) / len(snap_ms)
         snapshot = {"bytes_per_step": int(snap_bytes), "avg_device_ms": round(avg_snap, 3),
-                    "GB_per_s": round(snap_bytes / (avg_snap * 1e-3) / 1e9, 3), "kernel": "mt_snapshot_kernel"}
+                    "GB_per_s": round(snap_bytes / (avg_snap * 1e-3) / 1e9, 3), "kernel": "mt_snapshot_kernel",
+                    "summaries_gathered": summaries}
         if rank == 0:  # spot check: GPU blobs == host serializer on a sample
             sample = range(0, n_docs, max(1, n_docs // 64))
             snapshot["host_match"] = sum(b.doc(d).snapshot_v1(device=True) == b.doc(d).snapshot_v1() for d in sample)
@@ -229,13 +241,18 @@ def main():
                                                                   "lpt_loads": loads},
                        "clients": cfg["n_clients"], "max_lag": cfg["max_lag"],
                        "op_mix": [cfg["pct_insert"], cfg["pct_remove"], 100 - cfg["pct_insert"] - cfg["pct_remove"]],
-                       "parallelism": f"doc-sharded x{world}"},
+                       "parallelism": f"doc-sharded x{world}",
+                       "step": "replay + device digests" + (" + GPU SnapshotV1" if with_snap else "") +
+                               " + gather to rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": f"mt_replay_kernel_{dom_class}", "avg_launch_ms": round(avg_first_ms, 3),
+                         "kernel": kname, "avg_launch_ms": round(avg_first_ms, 3),
                          "algorithmic_bytes_per_launch": int(first_bytes),
-                         "ops_per_launch": int(sum(first_ops) / len(first_ops))},
+                         "algorithmic_bytes_formula": "32 B/op record + 2 B/inserted code unit + 8 B/prop record "
+                                                      "+ 32 B/final table entry (DESIGN.md §5)",
+                         "ops_per_launch": int(sum(first_ops) / len(first_ops)),
+                         "lds": lds},
             "replay_ms_per_step": round(avg_kernel_ms, 3),
             "launches": b.launches(),
             "cpu_baseline": cpu,
@@ -245,12 +262,12 @@ def main():
             "digests_gathered": len(gathered[0]) if rank == 0 else None,
             "digest_xor": digest_xor,
             "snapshot_digest_xor": snap_xor,
-            "ops_applied_per_step": int(ops_done),
+            "ops_applied_per_step": ops_all,
+            "requested_ops_per_step": int(total_ops_step),
             "lds_bytes_per_doc": st["lds_bytes"],
             "launches_per_step": st["launches"],
             "capacity_p50_p99_max": capacity,
             "gen_s": round(gen_s, 2),
-            "gather_ms": round(gather_ms, 3),
         }
         print(json.dumps(line), flush=True)
     b.close()
@@ -278,34 +295,101 @@ def log(rank, msg):
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def usable_cores():
+    """Cores this process may run on: the affinity set, capped by a cgroup CPU quota (the GPU
+    box gives each job a share of a larger machine; os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(float(quota) / float(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(b, fa, n_docs, args):
-    """Oracle (CPU restatement, tests-only code) on a bounded sample of the same logs,
-    timed on this host's cores; its per-doc digests double as a parity spot check.
-    Sample: the first documents of this rank's batch up to ~8.2M ops (config 2's size)."""
+    """Oracle (CPU restatement, tests-only code) on a bounded sample of the same logs, timed on
+    every usable host core (one pthread per core); its per-doc digests double as a parity check
+    of every sampled document.  Sample: the first documents of this rank's batch up to ~8.2M ops."""
     sys.path.insert(0, str(ROOT / "tests"))
     import numpy as np
 
     import oracle_ffi as O
 
-    ops, off, text, props = b.download_log()
     if args.cpu_sample_docs:
         sample = min(args.cpu_sample_docs, n_docs)
     else:
-        sample = int(np.searchsorted(off, 4096 * 2000, side="left"))
+        csum = np.cumsum(b.counters()["ops_done"].astype(np.int64))
+        sample = int(np.searchsorted(csum, 4096 * 2000, side="left")) + 1
         sample = min(n_docs, max(16, sample))
-    end = off[sample]
-    sops = ops[:end].copy()
-    soff = off[: sample + 1].copy()
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    sops, soff, text, props = b.download_log(0, sample)
+    threads = args.cpu_threads or usable_cores()
     tables, names = O.gen_tables(), O.gen_client_names(8)
     secs, dig, st = O.replay_batch(sops, soff, text, props, tables, names, n_threads=threads)
     gpu_dig = np.array([b.doc(d).digest() for d in range(sample)], np.uint64)
     match = int((gpu_dig == dig).sum())
-    cpu = {"value": round(int(end) / secs, 1), "unit": "ops/s", "cores": threads, "kind": "port",
-           "sample": f"first {sample} docs ({int(end)} ops) of the same log, oracle/ C restatement, {threads} threads",
+    n_ops = int(soff[-1])
+    cpu = {"value": round(n_ops / secs, 1), "unit": "ops/s", "cores": threads, "kind": "port",
+           "sample": f"first {sample} docs ({n_ops} ops) of the same log, oracle/ C restatement, {threads} threads "
+                     f"(usable cores; os.cpu_count()={os.cpu_count()}), CPU: {cpu_model()}",
            "seconds": round(secs, 3)}
     parity = {"docs_checked": sample, "digest_match": match, "oracle_status_ok": int((st == 0).sum())}
     return cpu, parity
+
+
+def gather_summaries(b, torch, dist, world, rank, backend):
+    """SnapshotV1 summaries of every document to rank 0 (digests *and summaries*):
+    each rank's GPU SnapshotV1 buffer (mt_batch_snapshot_copy, device to device) is padded to the
+    largest and gathered with one dist.gather over RCCL; rank 0 re-checks the received bytes of
+    its own shard against the local buffer.  Returns {bytes, ranks} on rank 0."""
+    import numpy as np
+
+    from fluidframework_amd import shard
+
+    off, meta = b.snapshot_index()
+    n = int(off[-1])
+    dev = "cuda" if backend == "nccl" or world == 1 else "cpu"
+    buf = torch.empty(max(1, n), dtype=torch.uint8, device="cuda")
+    b.snapshot_copy(buf)
+    recv = shard.gather_bytes(buf[:n] if dev == "cuda" else buf[:n].cpu(), world, rank)
+    if rank != 0:
+        return None
+    ok = bool(torch.equal(recv[0].to(buf.device), buf[:n]))
+    return {"bytes": int(sum(int(r.numel()) for r in recv)), "ranks": len(recv), "rank0_roundtrip_equal": ok}
+
+
+def lds_roofline(config, n_docs, n_ops, kernel, avg_ms, ops_per_launch):
+    """LDS roofline of the dominant kernel from the committed rocprofv3 counter passes of this same
+    configuration (tools/pmc_counters.py -> profiles/pmc_counters_config<N>.json): LDS bytes moved
+    per op (SQ_INSTS_LDS wave-instructions x 256 B, the LDS width per array cycle, over the
+    LDS-array cycles actually used) over the launch time measured live here, against ~150 TB/s
+    (MI355X_MICROARCH.md §LDS: 256 B/clk/CU x 256 CUs x ~2.4 GHz).  None without a matching profile."""
+    path = ROOT / "profiles" / f"pmc_counters_config{config}.json"
+    try:
+        prof = json.loads(path.read_text())
+    except (OSError, ValueError):
+        return None
+    k = prof.get("kernels", {}).get(kernel)
+    if not k or prof.get("ops") != n_ops:
+        return None
+    per_op = k.get("lds_bytes_per_op")
+    if not per_op:
+        return None
+    ach = per_op * ops_per_launch / (avg_ms * 1e-3) / 1e9
+    return {"achieved": round(ach, 3), "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": round(ach / LDS_PEAK_GBS, 6),
+            "bytes_per_op": per_op, "source": str(path.relative_to(ROOT)),
+            "counters_per_op": k.get("per_op")}
 
 
 if __name__ == "__main__":

@@ -29,6 +29,29 @@ constexpr int32_t kNoneSeq = 0x7FFFFFFF;  // removedSeq === undefined
 constexpr uint32_t kMarkerSlot = 0xFFFFu; // oe entry that ends a leaf block
 constexpr uint32_t kNoClient = 63u;
 
+// value flags (mt_values.h kVal*): matchProperties of two interned values is class equality,
+// else membership of the pair in the exception list (both kValIrregular); kValUnknown: undecided
+constexpr uint8_t kVFalsy = 1u, kVIrregular = 2u, kVUnknown = 4u;
+
+// device matchProperties of two values (R(a, b), mt_values.cpp): 1 match, 0 no, -1 undecided
+__device__ __forceinline__ int value_rel(uint32_t va, uint32_t vb, const uint32_t *vclass, const uint8_t *vflags,
+                                         uint32_t n_values, const uint64_t *exc, uint32_t n_exc) {
+    if (va == vb) return 1;
+    if (va >= n_values || vb >= n_values) return 0;
+    if (vclass[va] == vclass[vb]) return 1;
+    const uint32_t fa = vflags[va], fb = vflags[vb];
+    if ((fa | fb) & kVUnknown) return -1;
+    if (!(fa & fb & kVIrregular)) return 0;
+    const uint64_t key = (uint64_t)va << 32 | vb;
+    uint32_t lo = 0, hi = n_exc;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (exc[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n_exc && exc[lo] == key ? 1 : 0;
+}
+
 // needsScour tri-state (mergeTree.ts:63, 1279, 1438)
 constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
 
@@ -165,8 +188,12 @@ struct ReplayParams {
     const uint64_t *doc_pool_base;
     const uint32_t *doc_pool_cap;
     const void *props_in;         // mt_prop[] (op prop records, batch-global offsets)
-    const uint8_t *value_flags;   // per value id: bit0 = JS-falsy (rewrite semantics)
+    const uint8_t *value_flags;   // per value id: bit0 = JS-falsy (rewrite semantics), bit1 irregular,
+                                  // bit2 unknown (mt_values.h)
     uint32_t n_values;
+    const uint32_t *value_class;  // per value id: structural matchProperties class (mt_values.cpp)
+    const uint64_t *exc;          // sorted (u << 32 | v): values matching across classes
+    uint32_t n_exc;
     OutRec *out;                  // [n_docs * out_cap]
     DocOut *doc_out;
     int64_t n_docs;               // workgroups in this launch
@@ -215,6 +242,7 @@ struct DigestParams {
     const uint64_t *doc_text_base;
     const uint32_t *pool;
     const uint64_t *doc_pool_base;
+    const uint8_t *final_mask; // per workgroup: 1 when this launch holds the document's final result
     uint64_t *dst;             // [n_docs]
 };
 
@@ -241,6 +269,10 @@ struct SnapParams {
     int32_t cli_first, cli_n;   // the shared client table (entries 0, 1 of cli_str: "undefined", "original")
     const uint8_t *final_mask;  // per workgroup: 1 when this launch holds the document's final table
     int32_t n_keys, n_values;   // key_str has n_keys + 1 entries (the last is "?")
+    const uint8_t *value_flags; // matchProperties of values (as ReplayParams)
+    const uint32_t *value_class;
+    const uint64_t *exc;
+    uint32_t n_exc;
     int32_t chunk_size;
     int32_t pass;               // 0: sizes into meta / bytes, 1: write into dst
     int32_t *meta;              // [n_docs * kSnapMeta]

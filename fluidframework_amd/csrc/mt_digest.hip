@@ -29,9 +29,11 @@ __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
 extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P) {
     const int64_t w = blockIdx.x;
     if (w >= P.n) return;
+    // a document checkpointed or re-run in a later launch gets its digest from that launch; the
+    // launch holding its final result always writes one (also for a terminal MT_CAPACITY: no
+    // records, the status enters the hash)
+    if (!P.final_mask[w]) return;
     const DocOut o = P.doc_out[w];
-    // documents checkpointed or re-run in a later launch get their digest from that launch
-    if (o.status == ST_CAPACITY && (o.cap_kind == 1 || o.cap_kind == kCapCheckpoint || o.cap_kind == 4)) return;
     const int64_t d = P.doc_list ? P.doc_list[w] : w;
     const OutRec *rec = P.out + w * (int64_t)P.out_cap;
     const uint16_t *text = P.text + P.doc_text_base[d];

@@ -160,6 +160,9 @@ struct Engine {
     const mt_prop *props_in;
     const uint8_t *value_flags;
     uint32_t n_values;
+    const uint32_t *value_class;
+    const uint64_t *exc;
+    uint32_t n_exc;
     int lane;
     int32_t cap_kind;
 #ifdef MT_PROF
@@ -889,21 +892,28 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ properties
-    // prop-set record in the doc pool: [n, hash, (key, value) x n] in insertion order
+    // prop-set record in the doc pool: [n, hash, (key, value) x n] in insertion order.  The hash is
+    // order-insensitive over (key, structural value class); its bit 0 is set when no value of the
+    // set is irregular (mt_values.cpp), so equal classes decide matchProperties and unequal hashes
+    // reject without reading the records.
+    // matchProperties(a, b) (properties.ts:62-93) of two sets, a the earlier segment's
     MT_FI bool props_match(uint32_t a, uint32_t ha, uint32_t b, uint32_t hb) {
         if (a == b) return true;
         if (a == 0 || b == 0) return false;
-        if (ha != hb) return false;
-        uint32_t na = pool[a], nb = pool[b];
+        if ((ha & hb & 1u) && ha != hb) return false;
+        const uint32_t na = pool[a], nb = pool[b];
         if (na != nb) return false;
-        bool ok = true;
+        bool ok = true, unk = false;
         if ((uint32_t)lane < na) {
-            uint32_t k = pool[a + 2 + 2 * lane], v = pool[a + 3 + 2 * lane];
-            bool f = false;
+            const uint32_t k = pool[a + 2 + 2 * lane], va = pool[a + 3 + 2 * lane];
+            int rel = 0;
             for (uint32_t i = 0; i < nb; i++)
-                if (pool[b + 2 + 2 * i] == k && pool[b + 3 + 2 * i] == v) f = true;
-            ok = f;
+                if (pool[b + 2 + 2 * i] == k)
+                    rel = value_rel(va, pool[b + 3 + 2 * i], value_class, value_flags, n_values, exc, n_exc);
+            ok = rel == 1;
+            unk = rel < 0;
         }
+        if (ballot(unk)) set_fail(ST_UNSUPPORTED);  // an undecided structural compare (kVUnknown)
         return ballot(!ok) == 0;
     }
 
@@ -1001,15 +1011,18 @@ struct Engine {
         uint32_t id = pool_top;
         pool_top += words;
         uint32_t h = 0;
+        bool irr = false;
         if ((uint32_t)lane < n) {
             uint32_t k = keys[lane], v = vals[lane];
-            h = hash_pair(k, v);
+            const bool known = v < n_values;
+            h = hash_pair(k, known ? value_class[v] : 0xFFFFFFFFu - v);
+            irr = !known || (value_flags[v] & (kVIrregular | kVUnknown));
             pool[id + 2 + 2 * lane] = k;
             pool[id + 3 + 2 * lane] = v;
         }
-        // order-insensitive content hash (matchProperties ignores key order)
+        // order-insensitive content hash (matchProperties ignores key order), bit 0 = regular
         for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, kWave);
-        h = rfl(h);
+        h = (rfl(h) & ~1u) | (ballot(irr) ? 0u : 1u);
         if (lane == 0) {
             pool[id] = n;
             pool[id + 1] = h;
@@ -1055,22 +1068,49 @@ struct Engine {
         const bool noprops = !((meta | mprev) & kMetaHasProps);
         uint64_t pairM = ballot(pair && noprops);
         const uint64_t withM = ballot(pair && !noprops);
+        const uint64_t longM = ballot(in && len > kGranularity);
+        bool serial = false;
         if (withM) {
             const uint32_t props = cr.x, ph = props ? pool[props + 1] : 0u;
-            const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
-            const bool peq = pprev == props;
-            const bool pmaybe = !peq && props != 0u && pprev != 0u && hprev == ph;
-            pairM |= withM & ballot(peq);
-            uint64_t maybeM = withM & ballot(pmaybe);
-            while (maybeM) {  // equal hashes, different sets: compare contents (rare)
-                const int k = first_lane(maybeM);
-                maybeM &= maybeM - 1;
-                if (props_match(rdl(props, k - 1), rdl(ph, k - 1), rdl(props, k), rdl(ph, k))) pairM |= 1ull << k;
+            // an irregular set (a value matching across structural classes) makes matchProperties
+            // intransitive: decide the chains serially against their heads, as scourNode does
+            serial = ballot(cand && props != 0u && !(ph & 1u)) != 0;
+            if (!serial) {
+                const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
+                const bool peq = pprev == props;
+                const bool pmaybe = !peq && props != 0u && pprev != 0u && hprev == ph;
+                pairM |= withM & ballot(peq);
+                uint64_t maybeM = withM & ballot(pmaybe);
+                while (maybeM) {  // equal hashes, different sets: compare contents (rare)
+                    const int k = first_lane(maybeM);
+                    maybeM &= maybeM - 1;
+                    if (props_match(rdl(props, k - 1), rdl(ph, k - 1), rdl(props, k), rdl(ph, k))) pairM |= 1ull << k;
+                }
             }
         }
         uint64_t mergeM;
-        const uint64_t longM = ballot(in && len > kGranularity);
-        if (!(pairM & longM)) {
+        if (serial) {
+            // scourNode's loop (mergeTree.ts:1300-1345): prev = the chain head; canAppend's
+            // structural part is lane-pairwise (pair), its length rule and matchProperties use the head
+            const uint64_t structM = ballot(pair);
+            mergeM = 0;
+            int32_t h = 0;
+            uint32_t acc = 0;
+            for (int32_t k = 0; k < n; k++) {
+                const uint32_t lk = rdl(len, k);
+                if ((structM >> k) & 1ull) {
+                    const uint32_t pa = rdl(cr.x, h), pb = rdl(cr.x, k);
+                    if ((acc <= kGranularity || lk <= kGranularity) &&
+                        (pa == pb || (pa && pb && props_match(pa, rfl(pool[pa + 1]), pb, rfl(pool[pb + 1]))))) {
+                        mergeM |= 1ull << k;
+                        acc += lk;
+                        continue;
+                    }
+                }
+                h = k;
+                acc = lk;
+            }
+        } else if (!(pairM & longM)) {
             // every appended leaf is <= 256 long, so the length rule never fails: all pairs merge
             mergeM = pairM;
         } else {
@@ -1087,6 +1127,7 @@ struct Engine {
                 }
             }
         }
+        if (status) return 0;
         // chain head of every appended lane: the last non-appended lane before it
         const uint32_t head = 63u - (uint32_t)__builtin_clzll((~mergeM & ((1ull << lane) - 1ull)) | 1ull);
         // TextSegment.append for every merge, head by head in document order
@@ -2008,6 +2049,9 @@ MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_
     E.text_gcs = 0;
     E.props_in = (const mt_prop *)P.props_in;
     E.value_flags = P.value_flags;
+    E.value_class = P.value_class;
+    E.exc = P.exc;
+    E.n_exc = P.n_exc;
     E.n_values = P.n_values;
     E.init();
 }

@@ -24,6 +24,7 @@
 
 #include "../../include/mtreplay.h"
 #include "mt_device.h"
+#include "mt_values.h"
 
 // kernels of each capacity class (mt_kernels.hip compiled with -DMT_SEG=<seg>)
 #define MT_DECLARE_CLASS(S)                                                   \
@@ -342,6 +343,8 @@ struct mt_batch {
     std::vector<uint8_t> key_is_index;
     std::vector<uint32_t> key_index;
     std::vector<uint8_t> value_flags;
+    std::vector<uint32_t> value_class;  // structural matchProperties classes (mt_values.cpp)
+    std::vector<uint64_t> value_exc;    // sorted cross-class matches (u << 32 | v)
     std::vector<std::string> clients;  // shared table
     std::unordered_map<int64_t, std::vector<std::string>> doc_clients;
     // log (device) + host mirror of the layout
@@ -361,6 +364,8 @@ struct mt_batch {
     uint32_t *d_pool = nullptr;
     mt_prop *d_props = nullptr;
     uint8_t *d_vflags = nullptr;
+    uint32_t *d_vclass = nullptr;
+    uint64_t *d_vexc = nullptr;
     double payload_units = 0, prop_records = 0;
     // launches / results
     std::vector<Launch> launches;
@@ -450,7 +455,14 @@ static void free_log(mt_batch *b) {
     b->have_log = false;
 }
 
+#ifndef MT_BUILD_ID
+#define MT_BUILD_ID "MTBUILDID:unstamped000000"
+#endif
+static const char kBuildId[] = MT_BUILD_ID;  // "MTBUILDID:" + 16 hex digits (buildinfo.py)
+
 extern "C" {
+
+MT_API const char *mt_build_id(void) { return kBuildId + 10; }
 
 MT_API const char *mt_status_string(int code) {
     switch (code) {
@@ -502,6 +514,8 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     (void)hipFree(b->d_digest);
     free_log(b);
     (void)hipFree(b->d_vflags);
+    (void)hipFree(b->d_vclass);
+    (void)hipFree(b->d_vexc);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
     if (b->ev1) (void)hipEventDestroy(b->ev1);
     for (hipStream_t a : b->aux)
@@ -513,6 +527,8 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }
+
+static int ensure_tables(mt_batch *b);
 
 MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_keys, const char *const *values_json,
                                int32_t n_values) {
@@ -531,13 +547,17 @@ MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_k
     b->value_flags.resize(n_values);
     for (int i = 0; i < n_values; i++) {
         b->values[i] = (i == 0 || !values_json[i]) ? std::string("null") : std::string(values_json[i]);
-        b->value_flags[i] = json_falsy(b->values[i]) ? 1 : 0;
+        b->value_flags[i] = json_falsy(b->values[i]) ? mt::kValFalsy : 0;
     }
+    // matchProperties classes of the values (nested objects compare structurally)
+    mt::value_relations(b->values, b->value_class, b->value_flags, b->value_exc);
     (void)hipFree(b->d_vflags);
+    (void)hipFree(b->d_vclass);
+    (void)hipFree(b->d_vexc);
     b->d_vflags = nullptr;
-    HIPCHK(dalloc(&b->d_vflags, b->value_flags.size()));
-    HIPCHK(hipMemcpy(b->d_vflags, b->value_flags.data(), b->value_flags.size(), hipMemcpyHostToDevice));
-    return MT_OK;
+    b->d_vclass = nullptr;
+    b->d_vexc = nullptr;
+    return ensure_tables(b);
 }
 
 MT_API int mt_batch_set_clients(mt_batch *b, int64_t doc, const char *const *names, int32_t n) {
@@ -558,47 +578,68 @@ static const std::vector<std::string> &clients_of(mt_batch *b, int64_t doc) {
 }
 
 static int ensure_tables(mt_batch *b) {
+    if (b->value_class.size() != b->values.size())
+        mt::value_relations(b->values, b->value_class, b->value_flags, b->value_exc);
     if (!b->d_vflags) {
         HIPCHK(dalloc(&b->d_vflags, b->value_flags.size()));
         HIPCHK(hipMemcpy(b->d_vflags, b->value_flags.data(), b->value_flags.size(), hipMemcpyHostToDevice));
     }
+    if (!b->d_vclass) {
+        HIPCHK(dalloc(&b->d_vclass, b->value_class.size()));
+        HIPCHK(hipMemcpy(b->d_vclass, b->value_class.data(), 4 * b->value_class.size(), hipMemcpyHostToDevice));
+    }
+    if (!b->d_vexc) {
+        HIPCHK(dalloc(&b->d_vexc, b->value_exc.size()));
+        if (!b->value_exc.empty())
+            HIPCHK(hipMemcpy(b->d_vexc, b->value_exc.data(), 8 * b->value_exc.size(), hipMemcpyHostToDevice));
+    }
     return MT_OK;
+}
+
+// matchProperties of two interned values, host side (same rule as value_rel on the device)
+static int host_value_rel(const mt_batch *b, uint32_t va, uint32_t vb) {
+    if (va == vb) return 1;
+    const size_t n = b->value_class.size();
+    if (va >= n || vb >= n) return 0;
+    if (b->value_class[va] == b->value_class[vb]) return 1;
+    const uint8_t fa = b->value_flags[va], fb = b->value_flags[vb];
+    if ((fa | fb) & mt::kValUnknown) return -1;
+    if (!(fa & fb & mt::kValIrregular)) return 0;
+    return std::binary_search(b->value_exc.begin(), b->value_exc.end(), (uint64_t)va << 32 | vb) ? 1 : 0;
 }
 
 static uint32_t align16u(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
 
 MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_off, const uint16_t *text,
                            int64_t n_text, const mt_prop *props, int64_t n_props) {
-    if (!b || !ops || !doc_op_off || doc_op_off[0] != 0) return MT_ERR_ARG;
-    int rc = ensure_tables(b);
-    if (rc) return rc;
+    if (!b || !ops || !doc_op_off || doc_op_off[0] != 0 || n_text < 0 || n_props < 0) return MT_ERR_ARG;
+    if (n_text > 0 && !text) return MT_ERR_ARG;
+    if (n_props > 0 && !props) return MT_ERR_ARG;
     const int64_t D = b->n_docs;
+    // every check runs on locals before the batch is touched: a failed (re-)ingest leaves the
+    // previous log, its device buffers and its results intact
+    for (int64_t d = 0; d < D; d++)
+        if (doc_op_off[d + 1] < doc_op_off[d]) return MT_ERR_ARG;
     const int64_t N = doc_op_off[D];
-    // stage: per-doc text regions (payload in op order, then the merge arena), prop pools
-    std::vector<mt_op> h_ops(ops, ops + N);
-    b->h_off.assign(doc_op_off, doc_op_off + D + 1);
-    b->h_text_base.assign(D, 0);
-    b->h_text_len.assign(D, 0);
-    b->h_text_cap.assign(D, 0);
-    b->h_pool_base.assign(D, 0);
-    b->h_pool_cap.assign(D, 0);
+    if (N < 0 || N > ((int64_t)1 << 40)) return MT_ERR_ARG;
+    std::vector<int64_t> h_off(doc_op_off, doc_op_off + D + 1);
+    std::vector<uint64_t> text_base((size_t)D, 0), pool_base((size_t)D, 0);
+    std::vector<uint32_t> text_len((size_t)D, 0), text_cap((size_t)D, 0), pool_cap((size_t)D, 0);
+    std::vector<int32_t> nload((size_t)D, 0), nload_segs((size_t)D, 0);
     uint64_t tbase = 0, pbase = 0;
     int32_t max_ops = 0;
-    b->payload_units = 0;
-    b->prop_records = 0;
-    b->h_nload.assign(D, 0);
-    b->h_nload_segs.assign(D, 0);
+    double payload_units = 0, prop_records = 0;
     for (int64_t d = 0; d < D; d++) {
-        int64_t a = doc_op_off[d], e = doc_op_off[d + 1];
-        if (e < a) return MT_ERR_ARG;
+        const int64_t a = h_off[d], e = h_off[d + 1];
+        if (e - a > 0x7FFFFFFF) return MT_ERR_ARG;
         max_ops = std::max<int32_t>(max_ops, (int32_t)(e - a));
         for (int64_t i = a; i < e; i++) {  // leading SnapshotLoader records
             const uint8_t t = ops[i].type;
             if (t != MT_OP_LOAD_HEADER && t != MT_OP_LOAD_BODY && t != MT_OP_COLLAB) break;
-            b->h_nload[d]++;
-            if (t != MT_OP_COLLAB) b->h_nload_segs[d]++;
+            nload[d]++;
+            if (t != MT_OP_COLLAB) nload_segs[d]++;
         }
-        for (int64_t i = a + b->h_nload[d]; i < e; i++)  // LOAD records only lead a log
+        for (int64_t i = a + nload[d]; i < e; i++)  // LOAD records only lead a log
             if (ops[i].type == MT_OP_LOAD_HEADER || ops[i].type == MT_OP_LOAD_BODY || ops[i].type == MT_OP_COLLAB)
                 return MT_ERR_ARG;
         uint64_t pay = 0, nprop_ops = 0;
@@ -611,35 +652,36 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
             if (o.type == MT_OP_ANNOTATE) {
                 if ((int64_t)o.payload + (int64_t)o.payload_len > n_props) return MT_ERR_ARG;
                 nprop_ops++;
-                b->prop_records += o.payload_len;
+                prop_records += o.payload_len;
             }
             if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
-                if ((int64_t)o.pos2 + (int64_t)MT_OPF_NPROPS(o.flags) > n_props) return MT_ERR_ARG;
+                if (o.pos2 < 0 || (int64_t)o.pos2 + (int64_t)MT_OPF_NPROPS(o.flags) > n_props) return MT_ERR_ARG;
                 nprop_ops++;
-                b->prop_records += MT_OPF_NPROPS(o.flags);
+                prop_records += MT_OPF_NPROPS(o.flags);
             }
         }
-        b->payload_units += (double)pay;
+        payload_units += (double)pay;
         uint64_t cap = (uint64_t)align16u(pay) + (uint64_t)b->opt.arena_factor * pay + 4096;
         if (cap > 0xFFFFFFF0ull) return MT_ERR_ARG;
-        b->h_text_base[d] = tbase;
-        b->h_text_len[d] = (uint32_t)pay;
-        b->h_text_cap[d] = (uint32_t)cap;
+        text_base[d] = tbase;
+        text_len[d] = (uint32_t)pay;
+        text_cap[d] = (uint32_t)cap;
         tbase += align16u(cap);
         uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * nprop_ops;
-        b->h_pool_base[d] = pbase;
-        b->h_pool_cap[d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
+        pool_base[d] = pbase;
+        pool_cap[d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
         pbase += align16u(pc);
     }
-    b->text_words = tbase;
-    b->pool_words = pbase;
+    int rc = ensure_tables(b);
+    if (rc) return rc;
+    std::vector<mt_op> h_ops(ops, ops + N);
     std::vector<uint16_t> h_text(tbase ? tbase : 1, 0);
     for (int64_t d = 0; d < D; d++) {
         uint32_t w = 0;
-        for (int64_t i = doc_op_off[d]; i < doc_op_off[d + 1]; i++) {
+        for (int64_t i = h_off[d]; i < h_off[d + 1]; i++) {
             mt_op &o = h_ops[i];
             if (MT_OP_IS_INSERT_LIKE(o.type) && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
-                if (o.payload_len) memcpy(&h_text[b->h_text_base[d] + w], text + o.payload, 2ull * o.payload_len);
+                if (o.payload_len) memcpy(&h_text[text_base[d] + w], text + o.payload, 2ull * o.payload_len);
                 o.flags &= (uint16_t)~MT_OPF_INTERNAL;
                 if (o.payload_len && text[o.payload + o.payload_len - 1] == (uint16_t)'\n')
                     o.flags |= (uint16_t)MT_OPF_INTERNAL_ENDS_NL;
@@ -653,8 +695,24 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
             }
         }
     }
+    // the validated log replaces the previous one
     free_launches(b);
     free_log(b);
+    b->ran = false;
+    b->cached_doc = -1;
+    b->c_blob_doc = -1;
+    b->h_off = std::move(h_off);
+    b->h_text_base = std::move(text_base);
+    b->h_text_len = std::move(text_len);
+    b->h_text_cap = std::move(text_cap);
+    b->h_pool_base = std::move(pool_base);
+    b->h_pool_cap = std::move(pool_cap);
+    b->h_nload = std::move(nload);
+    b->h_nload_segs = std::move(nload_segs);
+    b->payload_units = payload_units;
+    b->prop_records = prop_records;
+    b->text_words = tbase;
+    b->pool_words = pbase;
     b->total_ops = N;
     b->total_props = n_props;
     b->max_ops_per_doc = max_ops;
@@ -669,7 +727,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     HIPCHK(dalloc(&b->d_pool_cap, (size_t)D));
     HIPCHK(dalloc(&b->d_props, (size_t)std::max<int64_t>(n_props, 1)));
     HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(b->d_off, doc_op_off, sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_off, b->h_off.data(), sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_text, h_text.data(), 2 * h_text.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_text_base, b->h_text_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_text_len, b->h_text_len.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
@@ -679,7 +737,6 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     if (n_props > 0) HIPCHK(hipMemcpy(b->d_props, props, sizeof(mt_prop) * (size_t)n_props, hipMemcpyHostToDevice));
     b->have_log = true;
     b->generated = false;
-    b->ran = false;
     return MT_OK;
 }
 
@@ -739,6 +796,9 @@ static mt::ReplayParams base_params(mt_batch *b) {
     P.props_in = b->d_props;
     P.value_flags = b->d_vflags;
     P.n_values = (uint32_t)b->value_flags.size();
+    P.value_class = b->d_vclass;
+    P.exc = b->d_vexc;
+    P.n_exc = (uint32_t)b->value_exc.size();
     return P;
 }
 
@@ -1312,8 +1372,21 @@ MT_API int mt_batch_device_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_de
     if (!b->ran) return MT_ERR_STATE;
     if (!b->d_digest) HIPCHK(dalloc(&b->d_digest, (size_t)b->n_docs));
     hipStream_t s = b->run_stream ? b->run_stream : b->stream;
-    // launches in order: a document escalated to a later launch gets its digest from there
-    for (const Launch &L : b->launches) {
+    // every document is hashed by exactly the launch that holds its final result (where[]), so
+    // each entry of dst is written by this call, whatever the document's status
+    size_t max_n = 0;
+    for (const Launch &L : b->launches) max_n = std::max(max_n, (size_t)launch_n(b->n_docs, L));
+    std::vector<uint8_t> mask(max_n * b->launches.size(), 0);
+    for (int64_t d = 0; d < b->n_docs; d++) {
+        const DocRes &w = b->where[(size_t)d];
+        if (w.launch < 0 || w.idx < 0) return MT_INTERNAL;
+        mask[(size_t)w.launch * max_n + (size_t)w.idx] = 1;
+    }
+    uint8_t *d_mask = nullptr;
+    HIPCHK(dalloc(&d_mask, mask.size()));
+    HIPCHK(hipMemcpyAsync(d_mask, mask.data(), mask.size(), hipMemcpyHostToDevice, s));
+    for (size_t li = 0; li < b->launches.size(); li++) {
+        const Launch &L = b->launches[li];
         mt::DigestParams P{};
         P.out = L.d_out;
         P.doc_out = L.d_docout;
@@ -1325,6 +1398,7 @@ MT_API int mt_batch_device_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_de
         P.doc_text_base = b->d_text_base;
         P.pool = b->d_pool;
         P.doc_pool_base = b->d_pool_base;
+        P.final_mask = d_mask + li * max_n;
         P.dst = b->d_digest;
         void *args[] = {&P};
         HIPCHK(hipLaunchKernel((const void *)mt_digest_kernel, dim3((unsigned)P.n), dim3(64), args, 0, s));
@@ -1332,6 +1406,7 @@ MT_API int mt_batch_device_digests(mt_batch *b, uint64_t *dst, int32_t dst_is_de
     HIPCHK(hipMemcpyAsync(dst, b->d_digest, 8 * (size_t)b->n_docs,
                           dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    (void)hipFree(d_mask);
     return MT_OK;
 }
 
@@ -1468,16 +1543,19 @@ static void props_json(mt_batch *b, uint32_t id, std::string &o) {
     o.push_back('}');
 }
 
-static bool props_match_host(mt_batch *b, uint32_t a, uint32_t c) {
+// matchProperties(a, c) of two prop sets of the cached document (a the earlier segment's);
+// *undecided is set when a structural comparison could not be decided (kValUnknown)
+static bool props_match_host(mt_batch *b, uint32_t a, uint32_t c, bool *undecided) {
     if (a == c) return true;
     if (!a || !c) return false;
     const uint32_t *pa = b->c_pool.data() + a, *pc = b->c_pool.data() + c;
     if (pa[0] != pc[0]) return false;
     for (uint32_t i = 0; i < pa[0]; i++) {
-        bool f = false;
+        int rel = 0;
         for (uint32_t j = 0; j < pc[0]; j++)
-            if (pa[2 + 2 * i] == pc[2 + 2 * j] && pa[3 + 2 * i] == pc[3 + 2 * j]) f = true;
-        if (!f) return false;
+            if (pa[2 + 2 * i] == pc[2 + 2 * j]) rel = host_value_rel(b, pa[3 + 2 * i], pc[3 + 2 * j]);
+        if (rel < 0) *undecided = true;
+        if (rel != 1) return false;
     }
     return true;
 }
@@ -1595,6 +1673,7 @@ MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs) {
         if (prev_text) ptext.assign(b->c_text.begin() + r.toff, b->c_text.begin() + r.toff + r.len);
     };
     std::string tmp;
+    bool undecided = false;
     for (const OutRec &r : b->c_recs) {
         if (rec_is_marker(r)) continue;
         bool removed = rec_removed(r);
@@ -1605,7 +1684,7 @@ MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs) {
             } else {
                 bool can = prev_text && rec_is_text(r) && !(!ptext.empty() && ptext.back() == (uint16_t)'\n') &&
                            (ptext.size() <= mt::kGranularity || r.len <= mt::kGranularity);
-                if (can && props_match_host(b, pprops, r.props)) {
+                if (can && props_match_host(b, pprops, r.props, &undecided)) {
                     ptext.insert(ptext.end(), b->c_text.begin() + r.toff, b->c_text.begin() + r.toff + r.len);
                 } else {
                     push_prev();
@@ -1631,6 +1710,7 @@ MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs) {
         }
     }
     push_prev();
+    if (undecided) return MT_UNSUPPORTED;  // a structural matchProperties the tables could not decide
     // emit: chunks of >= chunk_size code units (each chunk includes the segment that crosses)
     struct Chunk {
         int64_t start, count, length;
@@ -1828,6 +1908,10 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                 P.final_mask = d_final[li];
                 P.n_keys = (int32_t)b->keys.size();
                 P.n_values = (int32_t)b->values.size();
+                P.value_flags = b->d_vflags;
+                P.value_class = b->d_vclass;
+                P.exc = b->d_vexc;
+                P.n_exc = (uint32_t)b->value_exc.size();
                 P.chunk_size = b->opt.chunk_size;
                 P.pass = pass;
                 P.meta = b->d_snap_meta;
@@ -2032,45 +2116,93 @@ MT_API int mt_doc_dump(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t
 }
 
 // ---------------------------------------------------------------- logs
-MT_API int mt_batch_log_sizes(mt_batch *b, int64_t *n_ops, int64_t *n_text, int64_t *n_props) {
-    if (!b || !b->have_log) return MT_ERR_STATE;
-    if (n_ops) *n_ops = b->total_ops;
-    if (n_text) {
-        int64_t t = 0;
-        for (int64_t d = 0; d < b->n_docs; d++) t += b->h_text_len[d];
-        *n_text = t;
+// prop records referenced by the ops of documents [d0, d1): [0, end)
+static int64_t props_end(mt_batch *b, int64_t d0, int64_t d1, const mt_op *ops) {
+    if (d0 == 0 && d1 == b->n_docs) return b->total_props;
+    int64_t end = 0;
+    const int64_t base = b->h_off[d0];
+    for (int64_t i = b->h_off[d0]; i < b->h_off[d1]; i++) {
+        const mt_op &o = ops[i - base];
+        if (o.type == MT_OP_ANNOTATE) end = std::max<int64_t>(end, (int64_t)o.payload + o.payload_len);
+        if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS))
+            end = std::max<int64_t>(end, (int64_t)o.pos2 + MT_OPF_NPROPS(o.flags));
     }
-    if (n_props) *n_props = b->total_props;
+    return std::min(end, b->total_props);
+}
+
+static int download_ops(mt_batch *b, int64_t d0, int64_t d1, std::vector<mt_op> &ops) {
+    ops.resize((size_t)(b->h_off[d1] - b->h_off[d0]));
+    if (!ops.empty())
+        HIPCHK(hipMemcpy(ops.data(), b->d_ops + b->h_off[d0], sizeof(mt_op) * ops.size(), hipMemcpyDeviceToHost));
     return MT_OK;
 }
 
-// batch-global layout: text of doc d follows doc d-1; prop offsets unchanged
-MT_API int mt_batch_download_log(mt_batch *b, mt_op *ops, int64_t *doc_op_off, uint16_t *text, mt_prop *props) {
+MT_API int mt_batch_log_sizes_docs(mt_batch *b, int64_t d0, int64_t d1, int64_t *n_ops, int64_t *n_text,
+                                   int64_t *n_props) {
     if (!b || !b->have_log) return MT_ERR_STATE;
+    if (d0 < 0 || d1 < d0 || d1 > b->n_docs) return MT_ERR_ARG;
+    if (n_ops) *n_ops = b->h_off[d1] - b->h_off[d0];
+    if (n_text) {
+        int64_t t = 0;
+        for (int64_t d = d0; d < d1; d++) t += b->h_text_len[d];
+        *n_text = t;
+    }
+    if (n_props) {
+        std::vector<mt_op> ops;
+        if (!(d0 == 0 && d1 == b->n_docs)) {
+            int rc = download_ops(b, d0, d1, ops);
+            if (rc) return rc;
+        }
+        *n_props = props_end(b, d0, d1, ops.data());
+    }
+    return MT_OK;
+}
+
+// documents [d0, d1) as a standalone log: offsets from 0, the text of doc d follows doc d-1's,
+// prop offsets unchanged (records [0, n_props) of the batch, n_props from the sizes call)
+MT_API int mt_batch_download_log_docs(mt_batch *b, int64_t d0, int64_t d1, mt_op *ops, int64_t *doc_op_off,
+                                      uint16_t *text, mt_prop *props) {
+    if (!b || !b->have_log) return MT_ERR_STATE;
+    if (d0 < 0 || d1 < d0 || d1 > b->n_docs) return MT_ERR_ARG;
+    std::vector<mt_op> h;
+    int rc = download_ops(b, d0, d1, h);
+    if (rc) return rc;
+    const int64_t base = b->h_off[d0];
     if (ops) {
-        HIPCHK(hipMemcpy(ops, b->d_ops, sizeof(mt_op) * (size_t)b->total_ops, hipMemcpyDeviceToHost));
         int64_t tb = 0;
-        for (int64_t d = 0; d < b->n_docs; d++) {
+        for (int64_t d = d0; d < d1; d++) {
             for (int64_t i = b->h_off[d]; i < b->h_off[d + 1]; i++) {
-                mt_op &o = ops[i];
+                mt_op &o = h[(size_t)(i - base)];
                 o.flags &= (uint16_t)~MT_OPF_INTERNAL;
                 if (MT_OP_IS_INSERT_LIKE(o.type) && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) o.payload += (uint32_t)tb;
             }
             tb += b->h_text_len[d];
         }
+        if (!h.empty()) memcpy(ops, h.data(), sizeof(mt_op) * h.size());
     }
-    if (doc_op_off) memcpy(doc_op_off, b->h_off.data(), sizeof(int64_t) * (size_t)(b->n_docs + 1));
+    if (doc_op_off)
+        for (int64_t d = d0; d <= d1; d++) doc_op_off[d - d0] = b->h_off[d] - base;
     if (text) {
         int64_t tb = 0;
-        for (int64_t d = 0; d < b->n_docs; d++) {
+        for (int64_t d = d0; d < d1; d++) {
             if (b->h_text_len[d])
                 HIPCHK(hipMemcpy(text + tb, b->d_text + b->h_text_base[d], 2ull * b->h_text_len[d], hipMemcpyDeviceToHost));
             tb += b->h_text_len[d];
         }
     }
-    if (props && b->total_props > 0)
-        HIPCHK(hipMemcpy(props, b->d_props, sizeof(mt_prop) * (size_t)b->total_props, hipMemcpyDeviceToHost));
+    const int64_t np = props_end(b, d0, d1, h.data());
+    if (props && np > 0) HIPCHK(hipMemcpy(props, b->d_props, sizeof(mt_prop) * (size_t)np, hipMemcpyDeviceToHost));
     return MT_OK;
+}
+
+MT_API int mt_batch_log_sizes(mt_batch *b, int64_t *n_ops, int64_t *n_text, int64_t *n_props) {
+    if (!b || !b->have_log) return MT_ERR_STATE;
+    return mt_batch_log_sizes_docs(b, 0, b->n_docs, n_ops, n_text, n_props);
+}
+
+MT_API int mt_batch_download_log(mt_batch *b, mt_op *ops, int64_t *doc_op_off, uint16_t *text, mt_prop *props) {
+    if (!b || !b->have_log) return MT_ERR_STATE;
+    return mt_batch_download_log_docs(b, 0, b->n_docs, ops, doc_op_off, text, props);
 }
 
 // ---------------------------------------------------------------- generator

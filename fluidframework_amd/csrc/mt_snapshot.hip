@@ -294,18 +294,32 @@ struct Doc {
             if (key_rank(pool[id + 2 + 2 * i]) == kNoRank) prop_entry(id, i, first);
         W.byte('}');
     }
-    // matchProperties over the pool's (key, value) lists
+    // matchProperties(a, c) over the pool's (key, value) lists (properties.ts:62-93): same key
+    // set, values compared structurally (value_rel: class equality or a listed exception); an
+    // undecided comparison leaves the document to the host serializer
     __device__ __forceinline__ bool props_match(uint32_t a, uint32_t c) {
         if (a == c) return true;
         if (!a || !c) return false;
         const uint32_t na = pool[a], nc = pool[c];
         if (na != nc) return false;
+        const uint32_t ha = pool[a + 1], hc = pool[c + 1];
+        if ((ha & hc & 1u) && ha != hc) return false;
         for (uint32_t base = 0; base < na; base += 64) {
             const uint32_t i = base + lane();
-            bool found = i >= na;
-            const uint32_t ka = found ? 0u : pool[a + 2 + 2 * i], va = found ? 0u : pool[a + 3 + 2 * i];
-            for (uint32_t j = 0; j < nc; j++) found |= ka == pool[c + 2 + 2 * j] && va == pool[c + 3 + 2 * j];
-            if (__ballot(!found)) return false;
+            int rel = 1;
+            if (i < na) {
+                const uint32_t ka = pool[a + 2 + 2 * i], va = pool[a + 3 + 2 * i];
+                rel = 0;
+                for (uint32_t j = 0; j < nc; j++)
+                    if (pool[c + 2 + 2 * j] == ka)
+                        rel = value_rel(va, pool[c + 3 + 2 * j], P.value_class, P.value_flags, (uint32_t)P.n_values,
+                                        P.exc, P.n_exc);
+            }
+            if (__ballot(rel < 0)) {
+                overflow = true;
+                return false;
+            }
+            if (__ballot(rel != 1)) return false;
         }
         return true;
     }

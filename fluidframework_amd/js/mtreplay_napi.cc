@@ -190,6 +190,21 @@ napi_value ingest(napi_env env, napi_callback_info info) {
         napi_throw_type_error(env, nullptr, "ingest(h, opsBuffer, BigInt64Array, Uint16Array, Uint32Array)");
         return nullptr;
     }
+    // the C ABI takes the op count from docOpOff: check it against the buffers first
+    mt_batch_stats st{};
+    if (mt_batch_get_stats(batch_of(env, a[0]), &st) != MT_OK || n_off != (size_t)st.n_docs + 1 || off[0] != 0) {
+        napi_throw_range_error(env, nullptr, "ingest: docOpOff must hold nDocs + 1 offsets starting at 0");
+        return nullptr;
+    }
+    for (size_t i = 1; i < n_off; i++)
+        if (off[i] < off[i - 1]) {
+            napi_throw_range_error(env, nullptr, "ingest: docOpOff must be non-decreasing");
+            return nullptr;
+        }
+    if ((uint64_t)off[n_off - 1] > n_ops_b / sizeof(mt_op)) {
+        napi_throw_range_error(env, nullptr, "ingest: docOpOff ends beyond the ops buffer");
+        return nullptr;
+    }
     static const uint16_t z16 = 0;
     static const mt_prop zp{0, 0};
     MT_OK_OR_THROW(mt_batch_ingest(batch_of(env, a[0]), ops, off, text ? text : &z16, (int64_t)n_text,

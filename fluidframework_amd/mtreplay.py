@@ -40,7 +40,8 @@ EXPORTS = [
     "mt_doc_snapshot_v1_device", "mt_batch_snapshot_index", "mt_batch_snapshot_copy", "mt_batch_launch_info",
     "mt_batch_snapshot_digests", "mt_batch_generate_docs", "mt_pack_json", "mt_packed_destroy", "mt_packed_error",
     "mt_packed_sizes", "mt_packed_arrays", "mt_packed_key", "mt_packed_value", "mt_packed_doc_clients",
-    "mt_packed_client", "mt_batch_ingest_packed",
+    "mt_packed_client", "mt_batch_ingest_packed", "mt_batch_log_sizes_docs", "mt_batch_download_log_docs",
+    "mt_build_id",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -105,6 +106,16 @@ def lib():
     L = C.CDLL(str(LIB_PATH))
     vp, i32, i64, cp = C.c_void_p, C.c_int32, C.c_int64, C.c_char_p
     P = C.POINTER
+    L.mt_build_id.argtypes = []
+    L.mt_build_id.restype = cp
+    # the in-tree library must have been built from the sources next to it (buildinfo.py); a stale
+    # binary is refused rather than tested (FLUIDFRAMEWORK_AMD_LIB overrides skip the check)
+    from . import buildinfo
+    if not os.environ.get("FLUIDFRAMEWORK_AMD_LIB") and buildinfo.sources_present():
+        want, got = buildinfo.src_hash(), L.mt_build_id().decode()
+        if got != want:
+            raise RuntimeError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
+                               "rebuild with __graft_entry__.build()")
     L.mt_status_string.argtypes = [C.c_int]
     L.mt_status_string.restype = cp
     L.mt_batch_create.argtypes = [P(vp), i64, P(BatchOptions)]
@@ -144,6 +155,8 @@ def lib():
     L.mt_doc_digest.argtypes = [vp, i64, P(C.c_uint64)]
     L.mt_batch_log_sizes.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.mt_batch_download_log.argtypes = [vp, vp, vp, vp, vp]
+    L.mt_batch_log_sizes_docs.argtypes = [vp, i64, i64, P(i64), P(i64), P(i64)]
+    L.mt_batch_download_log_docs.argtypes = [vp, i64, i64, vp, vp, vp, vp]
     L.mt_batch_doc_counters.argtypes = [vp, vp]
     L.mt_batch_device_digests.argtypes = [vp, vp, i32]
     L.mt_batch_launch_info.argtypes = [vp, i32, P(LaunchInfo)]
@@ -324,6 +337,8 @@ class ReplayBatch:
         props = np.ascontiguousarray(props if len(props) else np.zeros(1, PROP_DTYPE), PROP_DTYPE)
         if len(off) != self.n_docs + 1:
             raise ValueError("doc_op_off must have n_docs + 1 entries")
+        if off[0] != 0 or (len(off) > 1 and (np.diff(off) < 0).any()) or int(off[-1]) > len(ops):
+            raise ValueError("doc_op_off must start at 0, be non-decreasing and end within ops")
         _chk(lib().mt_batch_ingest(self.h, ops.ctypes.data, off.ctypes.data, text.ctypes.data, len(text),
                                    props.ctypes.data, len(props)), "mt_batch_ingest")
 
@@ -442,6 +457,25 @@ class ReplayBatch:
              "mt_batch_snapshot_digests")
         return out
 
+    def snapshot_index(self):
+        """(doc_off[n_docs+1], meta[n_docs, SNAP_META]) of the last snapshots() call."""
+        off = np.zeros(self.n_docs + 1, np.int64)
+        meta = np.zeros((self.n_docs, SNAP_META), np.int32)
+        _chk(lib().mt_batch_snapshot_index(self.h, off.ctypes.data, meta.ctypes.data), "mt_batch_snapshot_index")
+        return off, meta
+
+    def snapshot_copy(self, out):
+        """Copy the last snapshots() buffer into `out`: a contiguous uint8 torch tensor (CUDA: device
+        to device) or numpy array of at least doc_off[-1] bytes."""
+        if hasattr(out, "data_ptr"):
+            if out.element_size() != 1 or not out.is_contiguous():
+                raise ValueError("out must be a contiguous uint8 tensor")
+            _chk(lib().mt_batch_snapshot_copy(self.h, out.data_ptr(), 1 if out.is_cuda else 0),
+                 "mt_batch_snapshot_copy")
+        else:
+            _chk(lib().mt_batch_snapshot_copy(self.h, out.ctypes.data, 0), "mt_batch_snapshot_copy")
+        return out
+
     def snapshot_buffer(self):
         """(bytes, doc_off[n_docs+1], meta[n_docs, SNAP_META]) of the last snapshots() call."""
         off = np.zeros(self.n_docs + 1, np.int64)
@@ -455,15 +489,18 @@ class ReplayBatch:
         L = lib()
         return np.array([L.mt_doc_status(self.h, i) for i in range(self.n_docs)], np.int32)
 
-    def download_log(self):
-        """(ops, doc_op_off, text, props) with batch-global offsets."""
+    def download_log(self, d0: int = 0, d1: int | None = None):
+        """(ops, doc_op_off, text, props) of documents [d0, d1) (default: all) as a standalone log:
+        offsets from 0, their texts back to back, prop records with batch-global offsets."""
         L = lib()
+        d1 = self.n_docs if d1 is None else d1
         n_ops, n_text, n_props = C.c_int64(), C.c_int64(), C.c_int64()
-        _chk(L.mt_batch_log_sizes(self.h, C.byref(n_ops), C.byref(n_text), C.byref(n_props)), "log sizes")
+        _chk(L.mt_batch_log_sizes_docs(self.h, d0, d1, C.byref(n_ops), C.byref(n_text), C.byref(n_props)),
+             "log sizes")
         ops = np.zeros(n_ops.value, OP_DTYPE)
-        off = np.zeros(self.n_docs + 1, np.int64)
+        off = np.zeros(d1 - d0 + 1, np.int64)
         text = np.zeros(max(1, n_text.value), np.uint16)
         props = np.zeros(max(1, n_props.value), PROP_DTYPE)
-        _chk(L.mt_batch_download_log(self.h, ops.ctypes.data, off.ctypes.data, text.ctypes.data, props.ctypes.data),
-             "mt_batch_download_log")
+        _chk(L.mt_batch_download_log_docs(self.h, d0, d1, ops.ctypes.data, off.ctypes.data, text.ctypes.data,
+                                          props.ctypes.data), "mt_batch_download_log_docs")
         return ops, off, text[: n_text.value], props[: n_props.value]

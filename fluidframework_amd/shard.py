@@ -90,3 +90,27 @@ def gather_results(digests, statuses, world: int, rank: int, snapshot_digests=No
     if snapshot_digests is not None:
         out += (allr[:, 2].copy().view(np.uint64),)
     return out
+
+
+def gather_bytes(buf, world: int, rank: int):
+    """Gather each rank's byte buffer (a 1-D uint8 tensor of any length; SnapshotV1 summaries) to
+    rank 0: one all_gather of the lengths, then one dist.gather of the buffers padded to the
+    longest (RCCL on the GPU box, gloo on CPU).  Returns the per-rank buffers (trimmed) on rank 0,
+    None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return [buf]
+    n = torch.tensor([buf.numel()], dtype=torch.int64, device=buf.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(x.item()) for x in sizes]
+    m = max(1, max(sizes))
+    pad = torch.zeros(m, dtype=torch.uint8, device=buf.device)
+    pad[: buf.numel()] = buf
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+    dist.gather(pad, parts, dst=0)
+    if rank != 0:
+        return None
+    return [q[: sizes[r]] for r, q in enumerate(parts)]

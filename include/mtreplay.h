@@ -195,6 +195,14 @@ MT_API int mt_doc_dump(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t
 /* the (ingested or generated) log in host memory, batch-global offsets (CPU baseline / parity) */
 MT_API int mt_batch_log_sizes(mt_batch *b, int64_t *n_ops, int64_t *n_text, int64_t *n_props);
 MT_API int mt_batch_download_log(mt_batch *b, mt_op *ops, int64_t *doc_op_off, uint16_t *text, mt_prop *props);
+/* the same for documents [d0, d1) only (a bounded sample of a large batch): offsets from 0, text of
+   those documents back to back, prop records [0, *n_props) of the batch */
+MT_API int mt_batch_log_sizes_docs(mt_batch *b, int64_t d0, int64_t d1, int64_t *n_ops, int64_t *n_text,
+                                   int64_t *n_props);
+MT_API int mt_batch_download_log_docs(mt_batch *b, int64_t d0, int64_t d1, mt_op *ops, int64_t *doc_op_off,
+                                      uint16_t *text, mt_prop *props);
+/* hash of the sources this library was built from (__graft_entry__.py SRC, sha256 hex prefix) */
+MT_API const char *mt_build_id(void);
 
 #ifdef __cplusplus
 }

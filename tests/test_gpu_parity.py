@@ -325,3 +325,98 @@ def test_native_json_ingest_replays_like_the_packer():
             assert b.doc(i).status == a.doc(i).status == oracle[i].status
             assert b.doc(i).digest() == a.doc(i).digest()
             assert_doc_parity(b.doc(i), oracle[i])
+
+
+def test_config3_documents_at_full_size():
+    """The north-star workload's documents at their own size: config-3 mix (55/35/10), 10k ops,
+    no seg_cap forcing, so documents run the natural capacity chain (class 1,023 -> 1,328 ->
+    1,764 -> ...) through checkpoint / resume.  Every digest equals the oracle's; every 8th
+    document also text, property runs and SnapshotV1 (host and GPU serializers)."""
+    n = 32
+    p = O.gen_params(10000, pct_insert=55, pct_remove=35, seed=0xDEADBEEF)
+    ops, text, props, off = O.gen_batch(p, n)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(n) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        b.set_clients(names)
+        b.ingest(ops, off, text, props)
+        b.run()
+        launches = b.launches()
+        assert len({li["seg_class"] for li in launches}) >= 3, launches  # the escalation chain ran
+        assert int(b.counters()["max_slots"].max()) > 1328
+        for d in range(n):
+            assert b.doc(d).status == st[d] == 0
+            assert b.doc(d).digest() == int(dig[d]), f"doc {d} digest differs"
+        b.snapshots()
+        for d in range(0, n, 8):
+            od = O.replay_doc(ops[off[d]:off[d + 1]].copy(), text, props, t, names)
+            assert_doc_parity(b.doc(d), od)
+            assert b.doc(d).snapshot_v1(device=True) == od.snapshot_v1()
+
+
+def _settle(msgs, seq):
+    """a no-op message moving the MSN to `seq` (zamboni scours the settled segments)"""
+    return msgs + [{"clientId": "A", "sequenceNumber": seq + 1, "referenceSequenceNumber": seq,
+                    "minimumSequenceNumber": seq, "type": "noop", "contents": None}]
+
+
+def _props_run(values, key="k"):
+    """adjacent inserts carrying {key: value} for each value, then the MSN passes them all"""
+    msgs, pos = [], 0
+    for i, v in enumerate(values):
+        msgs.append(_msg("A", i + 1, i, {"type": 0, "pos1": pos, "seg": {"text": "ab", "props": {key: v}}}))
+        pos += 2
+    return _settle(msgs, len(values))
+
+
+NESTED_PROPS_DOCS = [
+    _props_run([{"x": 1, "y": 2}, {"y": 2, "x": 1}]),              # nested key order: match
+    _props_run([[1, 2], {"0": 1, "1": 2}]),                        # array == index-keyed object
+    _props_run([5, {}]),                                           # for-in over a number: no keys
+    _props_run([{}, 5]),                                           # ... but not the other way round
+    _props_run([{"a": 0}, {"a": None}]),                           # falsy vs nested null: match
+    _props_run([{"a": None}, {"a": 0}]),                           # ... not reversed
+    _props_run(["ab", ["a", "b"]]),                                # for-in over a string: its indices
+    _props_run([5, {}, 5]),                                        # intransitive: the chain head decides
+    _props_run([{"p": [1, {"q": "r"}]}, {"p": {"1": {"q": "r"}, "0": 1}}, {"p": [1, {"q": "s"}]}]),
+    _props_run([{"x": 1}, {"x": 1, "y": 2}]),                      # different key sets
+    _props_run([0, False]),                                        # strict equality of primitives
+]
+
+
+def test_nested_property_values_match_structurally():
+    """matchProperties (properties.ts:62-93) decides zamboni merges and SnapshotV1 coalescing: nested
+    values compare structurally and key-order-free, arrays equal index-keyed objects, and the
+    asymmetric / intransitive cases follow the reference's loop order.  GPU == oracle on the
+    segment table, text, property runs and SnapshotV1 (host and GPU serializers)."""
+    docs = NESTED_PROPS_DOCS
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        b.snapshots()
+        for i in range(len(docs)):
+            assert b.doc(i).status == 0, i
+            assert_doc_parity(b.doc(i), oracle[i])
+            assert b.doc(i).snapshot_v1(device=True) == oracle[i].snapshot_v1(), i
+        merged = [json.loads(b.doc(i).snapshot_v1()["header"])["segmentCount"] for i in range(len(docs))]
+        # the reference's answers (one coalesced segment where matchProperties holds along the chain)
+        assert merged == [1, 1, 1, 2, 1, 2, 1, 1, 2, 2, 2], merged
+
+
+def test_terminal_capacity_digests_are_defined():
+    """A document that stops for good with MT_CAPACITY (no larger class allowed) still gets a
+    device digest from its final launch: deterministic across runs and batches."""
+    p = fa.gen_params(3000, pct_insert=55, pct_remove=35, seed=4242)
+    got = []
+    for _ in range(2):
+        with fa.ReplayBatch(8, seg_cap=64, max_retries=-1) as b:
+            b.generate(p, 0)
+            b.run()
+            st = b.statuses()
+            assert (st == fa.MT_CAPACITY).any(), st
+            got.append(b.device_digests())
+            assert (b.device_digests() == got[-1]).all()
+    assert (got[0] == got[1]).all()
+    assert len(set(got[0].tolist())) == 8

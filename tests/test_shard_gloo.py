@@ -108,3 +108,40 @@ def test_gather_with_uneven_lpt_shards(tmp_path):
     assert len(got["dig"]) == 11
     with np.errstate(over="ignore"):
         assert (got["dig"] == got["ids"].astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)).all()
+
+
+def _rank_summaries(rank, port, out_path):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    p = O.gen_params(OPS, pct_insert=55, pct_remove=35, seed=0x5EED)
+    first = shard.shard(rank, DOCS)
+    ops, text, props, off = O.gen_batch(p, DOCS, first_doc=first)
+    t, names = O.gen_tables(), O.gen_client_names(8)
+    # this rank's SnapshotV1 summaries, back to back (the layout of the GPU snapshot buffer)
+    blob = "".join("".join(O.replay_doc(ops[off[d]:off[d + 1]].copy(), text, props, t, names).snapshot_v1().values())
+                   for d in range(DOCS)).encode("utf-8")
+    blob = blob[: len(blob) - 37 * rank]  # uneven sizes across ranks
+    got = shard.gather_bytes(torch.frombuffer(bytearray(blob), dtype=torch.uint8), WORLD, rank)
+    if rank == 0:
+        np.savez(out_path, *[g.numpy() for g in got])
+    else:
+        assert got is None
+    dist.destroy_process_group()
+
+
+def test_summaries_gather_over_gloo(tmp_path):
+    """SnapshotV1 summaries (variable-size byte buffers) reach rank 0 intact, in rank order."""
+    out = tmp_path / "summaries.npz"
+    mp.spawn(_rank_summaries, args=(_free_port(), str(out)), nprocs=WORLD, join=True)
+    got = np.load(out)
+    p = O.gen_params(OPS, pct_insert=55, pct_remove=35, seed=0x5EED)
+    t, names = O.gen_tables(), O.gen_client_names(8)
+    for r in range(WORLD):
+        ops, text, props, off = O.gen_batch(p, DOCS, first_doc=shard.shard(r, DOCS))
+        want = "".join("".join(O.replay_doc(ops[off[d]:off[d + 1]].copy(), text, props, t, names).snapshot_v1()
+                               .values()) for d in range(DOCS)).encode("utf-8")
+        want = want[: len(want) - 37 * r]
+        assert got[f"arr_{r}"].tobytes() == want
