@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="oracle baseline sample (default: auto)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (default: every usable core)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seg-cap", type=int, default=0, help="first capacity class (default: from the op count)")
     ap.add_argument("--snapshot", action="store_true", help="serialize SnapshotV1 of every doc in each step")
     return ap.parse_args()
 
@@ -116,7 +117,7 @@ def main():
         counts = None
         total_ops_step = n_ops * n_docs * world
 
-    b = fa.ReplayBatch(n_docs)
+    b = fa.ReplayBatch(n_docs, seg_cap=args.seg_cap)
     t0 = time.time()
     if sizes is not None:
         b.generate_docs(p, my_docs, sizes)
@@ -276,18 +277,21 @@ def main():
 
 
 def pmc_traffic(config, n_docs, n_ops, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
-    passes of this same configuration (tools/pmc_traffic.py; scripts/gpu_check.sh pmcf pmcw).
-    The counters cannot be read from inside this process, so the profile of the current kernel
-    build is committed under profiles/ and quoted here; None when no matching profile exists."""
-    path = ROOT / "profiles" / f"pmc_traffic_config{config}.json"
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    of this same configuration (tools/pmc_counters.py -> profiles/pmc_counters_config<N>.json,
+    scripts/gpu_check.sh pmcf<N> / pmcw<N>): (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per the guide's
+    gfx950 correction.  The counters cannot be read from inside this process, so the profile of the
+    current kernel build is committed under profiles/ and quoted here; None when no profile of
+    this configuration and kernel exists."""
+    path = ROOT / "profiles" / f"pmc_counters_config{config}.json"
     try:
         prof = json.loads(path.read_text())
     except (OSError, ValueError):
         return None, None
-    if prof.get("docs") != n_docs or prof.get("ops") != n_ops or kernel not in prof.get("kernels", {}):
+    k = prof.get("kernels", {}).get(kernel)
+    if prof.get("docs") != n_docs or prof.get("ops") != n_ops or not k or "hbm_bytes" not in k:
         return None, None
-    return int(prof["kernels"][kernel]["traffic_bytes"]), str(path.relative_to(ROOT))
+    return int(k["hbm_bytes"]), str(path.relative_to(ROOT))
 
 
 def log(rank, msg):

@@ -494,7 +494,9 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
     if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
     if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
     if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
-    if (b->opt.max_retries == 0) b->opt.max_retries = 6;  // < 0: checkpoint, but stop after the first launch
+    // the whole class ladder (280 -> 368 -> 456 -> 628 -> ... -> HBM class) by default; < 0: checkpoint,
+    // but stop after the first launch
+    if (b->opt.max_retries == 0) b->opt.max_retries = 2 * mt::kNumClasses;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
@@ -741,9 +743,15 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
 }
 
 // capacity class index: derived from ops per document unless seg_cap is given; `level`
-// escalates by whole classes
-static int class_for(const mt_batch *b, int32_t ops_per_doc, int level) {
+// escalates by whole classes.  Replay starts a document in at most the 16-documents-per-CU class
+// (280 slots): the replay kernel is latency bound, so a launch's rate grows with the documents
+// resident per CU (config 3, 65,536 docs: 203k ops/ms at 8 per CU, 113k at 5, 65k at 3), and a
+// document escalates by checkpoint (an image round trip to HBM, ~1 ms per class for 65,536 docs)
+// only when it needs the room.  The generator re-runs a document from scratch on overflow, so it
+// starts in the class of the expected final size (`replay` false).
+static int class_for(const mt_batch *b, int32_t ops_per_doc, int level, bool replay = true) {
     int32_t want = b->opt.seg_cap > 0 ? b->opt.seg_cap : ops_per_doc / 12 + 64;
+    if (replay && b->opt.seg_cap <= 0) want = std::min<int32_t>(want, 280);
     int c = 0;
     while (c + 1 < mt::kNumClasses && mt::kClassSegs[c] < want) c++;
     c += level;
@@ -2297,7 +2305,7 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
     std::vector<DocOut> outs((size_t)D);
     std::map<int, std::vector<int32_t>> work;  // class -> documents
     for (int64_t d = 0; d < D; d++) {
-        int c = std::min(class_for(b, doc_ops[d], 0), mt::kNumClasses - 1);
+        int c = std::min(class_for(b, doc_ops[d], 0, false), mt::kNumClasses - 1);
         while (c > 0 && !class_usable(c)) c--;
         work[c].push_back((int32_t)d);
     }

@@ -74,7 +74,7 @@ typedef struct mt_batch_options {
     int32_t heap_cap;        /* reserved                                                           */
     int32_t arena_factor;    /* text arena = factor * payload + 4096 code units; 0 -> 4            */
     int32_t pool_per_op;     /* prop pool words per annotate / props insert; 0 -> 96               */
-    int32_t max_retries;     /* capacity-class escalations for docs that overflow; 0 -> 6; < 0: none
+    int32_t max_retries;     /* capacity-class escalations for docs that overflow; 0 -> the whole ladder; < 0: none
                                 (documents short of headroom still checkpoint: capacity planning)  */
 } mt_batch_options;
 

@@ -16,13 +16,14 @@ for step in "$@"; do
   case "$step" in
     tests) run tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 300 python -u __graft_entry__.py smoke ;;
-    bench) run bench 600 python -u bench.py --steps 3 --warmup 1 ;;
+    bench) run bench 900 python -u bench.py --steps 3 --warmup 1 ;;
+    bench2) run bench2 600 python -u bench.py --config 2 --steps 3 --warmup 1 ;;
     bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     phases) run phases 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --steps 1 --warmup 0 --no-cpu ;;
-    phases3) run phases3 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --config 3 --docs 2048 --steps 1 --warmup 0 --no-cpu ;;
+    phases3) run phases3 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     docs256) run docs256 600 python -u bench.py --docs 256 --steps 2 --warmup 1 --no-cpu ;;
     docs1024) run docs1024 600 python -u bench.py --docs 1024 --steps 2 --warmup 1 --no-cpu ;;
     pmc1) run pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc1 -o run -- python3 -u bench.py --docs 1024 --steps 1 --warmup 0 --no-cpu ;;
@@ -38,6 +39,22 @@ for step in "$@"; do
     bench4s) run bench4s 600 python -u bench.py --config 4 --docs 4096 --ops 20000 --steps 1 --warmup 0 --no-cpu ;;
     bench4) run bench4 900 python -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu ;;
     loadtests) run loadtests 300 python -u -m pytest tests/test_gpu_snapshot_load.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    cap848) run cap848 600 python -u bench.py --steps 1 --warmup 0 --no-cpu --seg-cap 848 ;;
+    cap456) run cap456 600 python -u bench.py --steps 1 --warmup 0 --no-cpu --seg-cap 456 ;;
+    cap280) run cap280 600 python -u bench.py --steps 1 --warmup 0 --no-cpu --seg-cap 280 ;;
+    cap628) run cap628 600 python -u bench.py --steps 1 --warmup 0 --no-cpu --seg-cap 628 ;;
+    listpmc) run listpmc 120 rocprofv3 -L ;;
+    pmcA3) run pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
+    pmcB3) run pmcB3 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
+    pmcC3) run pmcC3 300 rocprofv3 --pmc SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_VMEM SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_INSTS_LDS_STORE_BANDWIDTH SQ_INSTS_LDS_ATOMIC_BANDWIDTH --output-format csv -d gpurun_out/pmcC3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
+    pmcC2) run pmcC2 200 rocprofv3 --pmc SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_VMEM SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_INSTS_LDS_STORE_BANDWIDTH SQ_INSTS_LDS_ATOMIC_BANDWIDTH --output-format csv -d gpurun_out/pmcC2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
+    pmcf3) run pmcf3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
+    pmcw3) run pmcw3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
+    pmcA2) run pmcA2 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
+    pmcB2) run pmcB2 200 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
+    pmcf2) run pmcf2 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
+    pmcw2) run pmcw2 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
+    prof3) run prof3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     *) echo "unknown step $step" ;;
   esac
 done
