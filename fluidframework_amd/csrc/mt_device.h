@@ -14,7 +14,7 @@ enum : int32_t {
     ST_INVALID_POS = 1,  // "MergeTree insert failed" (merge-tree/src/mergeTree.ts:2210-2216)
     ST_SEQ_ORDER = 2,    // client.ts:461-462, 824
     ST_MSN_ORDER = 3,    // client.ts:463-464, mergeTree.ts:1719-1722
-    ST_UNSUPPORTED = 4,  // outside the observer path / device limits (e.g. > 32 clients)
+    ST_UNSUPPORTED = 4,  // outside the observer path / device limits (e.g. > 253 clients)
     ST_BAD_INPUT = 5,
     ST_CAPACITY = 6,     // per-document LDS/HBM capacity exceeded: re-run with larger caps
     ST_INTERNAL = 7
@@ -24,10 +24,13 @@ constexpr int kWave = 64;
 constexpr int kMaxNodes = 8;            // MaxNodesInBlock, mergeTree.ts:334
 constexpr uint32_t kGranularity = 256;  // TextSegmentGranularity, mergeTree.ts:1059
 constexpr int kZamboniMax = 2;          // zamboniSegmentsMaxCount, mergeTree.ts:1061
-constexpr int kMaxClients = 32;         // overlap mask width
+constexpr int kMaxClients = 254;        // short client ids 0..253 (254 = NonCollabClient, 255 = none)
 constexpr int32_t kNoneSeq = 0x7FFFFFFF;  // removedSeq === undefined
 constexpr uint32_t kMarkerSlot = 0xFFFFu; // oe entry that ends a leaf block
-constexpr uint32_t kNoClient = 63u;
+constexpr uint32_t kNoClient = 255u;
+constexpr uint32_t kOvlMaskClients = 31u; // overlap sets of clients < 31 are a bit mask (see kOvlList)
+constexpr uint32_t kOvlList = 0x80000000u;  // cold.y with this bit: pool offset of an overlap-client list
+constexpr uint32_t kPoolOvlTag = 0x40000000u;  // header word of an overlap-list pool record: n | tag
 
 // value flags (mt_values.h kVal*): matchProperties of two interned values is class equality,
 // else membership of the pair in the exception list (both kValIrregular); kValUnknown: undecided
@@ -56,21 +59,26 @@ __device__ __forceinline__ int value_rel(uint32_t va, uint32_t vb, const uint32_
 constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
 
 // segment meta word
-//   [0,6)  clientId (short id)         [6,12) removedClientId (63 = none)
-//   [12]   Marker                       [13]   text ends with '\n'
-//   [14]   linked (in the tree)         [15]   unsettled (in the overlay list, see mt_engine.hip)
-//   [16]   has a prop set               [17]   text contains a '\n' somewhere
-//   [18]   removedClientOverlap is non-empty (the mask is in the cold record)
-//   [19,32) slot generation (heap entry validity)
-constexpr uint32_t kMetaMarker = 1u << 12;
-constexpr uint32_t kMetaEndsNL = 1u << 13;
-constexpr uint32_t kMetaLinked = 1u << 14;
-constexpr uint32_t kMetaUnsettled = 1u << 15;
-constexpr uint32_t kMetaHasProps = 1u << 16;
-constexpr uint32_t kMetaHasNL = 1u << 17;
-constexpr uint32_t kMetaHasOvl = 1u << 18;
-constexpr uint32_t kGenShift = 19;
-constexpr uint32_t kGenMask = 0xFFFFFFFFu << kGenShift;
+//   [0,8)  clientId (short id)         [8,16) removedClientId (255 = none)
+//   [16]   Marker                       [17]   text ends with '\n'
+//   [18]   linked (in the tree)         [19]   unsettled (in the overlay list, see mt_engine.hip)
+//   [20]   has a prop set               [21]   text contains a '\n' somewhere
+//   [22]   removedClientOverlap is non-empty (mask or list via the cold record)
+constexpr uint32_t kMetaCli = 0xFFu;
+constexpr uint32_t kMetaRcliShift = 8;
+constexpr uint32_t kMetaMarker = 1u << 16;
+constexpr uint32_t kMetaEndsNL = 1u << 17;
+constexpr uint32_t kMetaLinked = 1u << 18;
+constexpr uint32_t kMetaUnsettled = 1u << 19;
+constexpr uint32_t kMetaHasProps = 1u << 20;
+constexpr uint32_t kMetaHasNL = 1u << 21;
+constexpr uint32_t kMetaHasOvl = 1u << 22;
+__host__ __device__ constexpr uint32_t meta_cli(uint32_t m) { return m & kMetaCli; }
+__host__ __device__ constexpr uint32_t meta_rcli(uint32_t m) { return (m >> kMetaRcliShift) & kMetaCli; }
+// 16-bit window-relative sequence numbers in LDS (s_sr[slot] = seq16 | rseq16 << 16, see mt_engine.hip)
+constexpr uint32_t kSeq16None = 0xFFFFu;  // rseq16 of a segment that is not removed
+constexpr int32_t kSeq16Span = 0xFFF0;    // cur_seq - base must stay below (else MT_CAPACITY, cap_kind 5)
+constexpr uint32_t kHeapInvalid = 0xFFFFFFFFu;  // heap entry whose segment was merged away / unlinked
 constexpr uint16_t kNoBlock = 0xFFFFu;
 
 // one output record per leaf or end-of-leaf-block entry (doc order), 8 x u32
@@ -78,8 +86,9 @@ struct OutRec {
     uint32_t len;    // cachedLength (0 for a block marker)
     int32_t seq;
     int32_t rseq;    // kNoneSeq when not removed
-    uint32_t meta;
-    uint32_t ovl;    // removedClientOverlap as a bit mask
+    uint32_t meta;   // segment meta word bits [0,23): client ids and flags
+    uint32_t ovl;    // removedClientOverlap: bit mask of clients < 31, or kOvlList | pool offset of
+                     // a [n | kPoolOvlTag, 0, client x n] list
     uint32_t props;  // prop-set id in the doc's pool (0 = undefined)
     uint32_t toff;   // text offset in the doc's text region (Marker: refType)
     uint32_t blk;    // leaf block id << 16 | slot (slot 0xFFFF: end-of-block marker)
@@ -102,6 +111,7 @@ struct DocOut {
     int32_t max_heap;
     int32_t fail_op;    // index of the op that failed (-1)
     int32_t cap_kind;   // ST_CAPACITY cause: 1 LDS tables, 2 text arena, 3 prop pool, 4 out records,
+                        // 5 collab window wider than kSeq16Span ops (16-bit relative seqs),
                         // 6 LDS headroom: state checkpointed before op ops_done (resumable)
     int32_t gen_text;   // generator: payload code units written
     int32_t gen_props;  // generator: prop records written
@@ -125,12 +135,15 @@ struct Caps {
 // The LDS classes are sized to the residency they buy: LDS is allocated in 1,280-byte granules
 // (128 per CU; measured with tools/probe/lds_residency.hip, profiles/r01_lds_residency.json) and
 // the replay kernel's 128 VGPRs cap a CU at 16 workgroups, so each class is the largest slot
-// count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 6, 5, 4, 3, 2
-// and 1 documents per CU (64 and 128 keep small documents' buffers small).
-constexpr int kClassSegs[] = {64, 128, 280, 323, 368, 408, 456, 540, 628, 848, 1023, 1328, 1764, 2724, 4999, 60000};
+// count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3
+// and 2 documents per CU (tools/class_sizes.cpp); 128 keeps small documents' buffers small and
+// 6,806 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
+// The replay kernel is latency bound, so a launch's rate grows with the documents per CU.
+constexpr int kClassSegs[] = {128, 349, 403, 456, 509, 563, 672, 779, 888, 1048, 1264, 1644, 2184, 3373, 6806, 60000};
 constexpr int kNumClasses = 16;
 constexpr int kHbmClass = kNumClasses - 1;
 constexpr int kHbmSeg = 60000;
+constexpr int kReplayStartClass = 1;  // replay starts documents in at most the 16-per-CU class
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapQueued = 7;      // checkpointed and taken by the launch's follow-on workers
 
@@ -141,15 +154,17 @@ constexpr int kFqItems = 16;
 
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table
 constexpr int kCkHdr = 32;
-constexpr int64_t ck_words(int seg) { return 9ll * seg + 1024; }
+constexpr int64_t ck_words(int seg) { return 8ll * seg + 1024; }
+// cold records per slot in HBM: {props, ovl, toff, tcap} and {seq, rseq, 0, 0} (real seqs)
+constexpr int kColdPerSlot = 2;
 constexpr Caps class_caps(int seg) {
-    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 8 + 64, seg / 2 + 96};
+    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 64, seg / 4 + 96};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
-    uint32_t len, seq, rseq, meta, sblk, ulist;
-    uint32_t bparent, bfree, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, bytes;
+    uint32_t len, sr, meta, sblk, ulist;
+    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, bytes;
 };
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
 constexpr Layout make_layout(int seg) {
@@ -157,13 +172,11 @@ constexpr Layout make_layout(int seg) {
     Layout L{};
     uint32_t o = 0;
     L.len = o;     o = lds_align(o + 4u * c.seg);
-    L.seq = o;     o = lds_align(o + 4u * c.seg);
-    L.rseq = o;    o = lds_align(o + 4u * c.seg);
+    L.sr = o;      o = lds_align(o + 4u * c.seg);
     L.meta = o;    o = lds_align(o + 4u * c.seg);
     L.sblk = o;    o = lds_align(o + 2u * c.seg);
     L.ulist = o;   o = lds_align(o + 2u * c.ulist);
-    L.bparent = o; o = lds_align(o + 2u * c.blk);
-    L.bfree = o;   o = lds_align(o + 2u * c.blk);
+    L.bparent = o; o = lds_align(o + 2u * c.blk);  // a free block's b_parent links the free list
     L.bchild = o;  o = lds_align(o + 16u * c.blk);
     L.bcount = o;  o = lds_align(o + 1u * c.blk);
     L.bleaf = o;   o = lds_align(o + 1u * c.blk);
@@ -208,7 +221,7 @@ struct ReplayParams {
     const int64_t *gen_doc_ids;   // per document: global index seeding its stream (null: doc_first + d)
     const int32_t *gen_doc_ops;   // per document: ops to generate (null: gen->n_ops)
     uint64_t *prof;               // MT_PROF builds: kProfSlots cycle counters per workgroup
-    uint4 *cold;                  // [n_docs * cap.seg] cold segment records {props, ovl, toff, tcap}
+    uint4 *cold;                  // [n_docs * cap.seg * kColdPerSlot] cold segment records
     // capacity escalation by checkpoint: a document short of LDS headroom writes its state to
     // ck_out[w] and stops; a later launch in a larger class resumes it from ck_in[ck_src[w]]
     uint32_t *ck_out;             // [n_docs * ck_words(SEG)] or null (largest class: no checkpoint)

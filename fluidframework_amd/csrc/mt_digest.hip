@@ -48,8 +48,17 @@ extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P
             h = fnv(h, r.len);
             h = fnv(h, (uint32_t)r.seq);
             h = fnv(h, (uint32_t)r.rseq);
-            h = fnv(h, r.meta & 0x1FFFu);  // client ids, Marker
-            h = fnv(h, r.ovl);
+            h = fnv(h, r.meta & (kMetaCli | (kMetaCli << kMetaRcliShift) | kMetaMarker));  // client ids, Marker
+            // removedClientOverlap as a set (mask of clients < 31, or a pool list)
+            uint64_t ov = 0;
+            if (r.ovl & kOvlList) {
+                const uint32_t *l = pool + (r.ovl & ~kOvlList);
+                const uint32_t n = l[0] & ~kPoolOvlTag;
+                for (uint32_t k = 0; k < n; k++) ov += mix64(l[2 + k] + 1ull);
+            } else {
+                for (uint32_t m = r.ovl; m; m &= m - 1) ov += mix64((uint32_t)__builtin_ctz(m) + 1ull);
+            }
+            h = fnv(h, (uint32_t)ov);
             if (r.meta & kMetaMarker) {
                 h = fnv(h, r.toff);  // refType
             } else {

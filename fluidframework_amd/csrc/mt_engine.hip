@@ -5,10 +5,13 @@
 // mergeTree.ts:334): leaf blocks list segment slots, interior blocks list blocks, every
 // child list is one 16-byte row that a wave reads with one lane per child.
 //
-//   s_*[slot]   the fields nodeLength reads (SoA): length, seq, removedSeq, client ids, flags;
-//               and the leaf block.  The cold fields (prop-set id, removedClientOverlap mask —
-//               flagged in the meta word, read only when set —, text offset/capacity) live in a
-//               per-document HBM table `cold[slot]` (16 B records).
+//   s_*[slot]   the fields nodeLength reads (SoA): length, sequence numbers, client ids, flags;
+//               and the leaf block.  Sequence numbers are 16-bit, relative to a per-document base
+//               that follows minSeq (s_sr = seq16 | rseq16 << 16; a settled segment needs none:
+//               seq16 = 0, rseq16 = 0 if removed else kSeq16None), so a slot costs 14 B of LDS.
+//               The cold fields (prop-set id, removedClientOverlap — flagged in the meta word,
+//               read only when set —, text offset/capacity, and the real seq / removedSeq for
+//               output) live in a per-document HBM table `cold[2 * slot + {0,1}]` (2 x 16 B).
 //   b_*[block]  children[8], count, parent, needsScour, and the block's SETTLED length.
 //   u_list      the unsettled segments (the collab window's "hot" set).
 //   heap        the zamboni heap (collections.ts:213-265), in VGPRs.
@@ -126,17 +129,18 @@ struct Engine {
     static constexpr Layout lay = make_layout(SEG);
     // ---- LDS state
     uint32_t *s_len, *s_meta;
-    int32_t *s_seq, *s_rseq;  // s_seq of a free slot links the free list
+    uint32_t *s_sr;  // seq16 | rseq16 << 16 (window-relative); of a free slot: the next free slot
     uint16_t *s_blk;
     uint16_t *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
-    uint16_t *b_parent, *b_free, *b_child;
+    uint16_t *b_parent, *b_child;  // b_parent of a free block links the free block list
     uint8_t *b_count, *b_leaf;
     int8_t *b_scour;
     uint32_t *b_slen, *b_acc;
     uint32_t *scratch;  // 128 words
     // ---- uniform scalars
-    int32_t slot_top, free_head, free_n, blk_top, n_bfree, root, depth, hn, nu;
+    int32_t slot_top, free_head, free_n, blk_top, n_bfree, bfree_head, root, depth, hn, nu;
     int32_t min_seq, cur_seq, status, settled_min;
+    int32_t sbase;  // sequence numbers in s_sr are relative to sbase (<= minSeq)
     int32_t splits;                 // leaf/interior block splits so far (overlay staleness)
     int32_t ov_splits, ov_full;     // overlay computed at `ov_splits`; full (refSeq < minSeq) mode
     uint32_t arena_top, pool_top;
@@ -145,10 +149,11 @@ struct Engine {
     int32_t pool_gcs, text_gcs;
     // Splits of the current op (at most two): the cold records of both halves and the left
     // half's ends-with-'\n' are resolved after the op's LDS work, so the HBM latency of the
-    // cold-record and text loads overlaps it.
+    // cold-record and text loads overlaps it.  A pending split's two cold records are held
+    // lane-distributed (lane i < 8: word i) in one VGPR, so they cost no scalar registers.
     int32_t pend_n, pend_cold;
     uint32_t ps0, pn0, pr0, pch0, ps1, pn1, pr1, pch1;
-    uint4 pc0, pc1;
+    uint32_t pv0, pv1;
     int32_t max_heap, max_u, htop;
     uint2 *h_ent;
     // ---- global
@@ -170,23 +175,21 @@ struct Engine {
 #endif
 
     // ------------------------------------------------------------------ layout
-    MT_FI void carve(uint8_t *base) {
-        s_len = (uint32_t *)(base + lay.len);
-        s_seq = (int32_t *)(base + lay.seq);
-        s_rseq = (int32_t *)(base + lay.rseq);
-        s_meta = (uint32_t *)(base + lay.meta);
-        s_blk = (uint16_t *)(base + lay.sblk);
-        u_list = (uint16_t *)(base + lay.ulist);
-        b_parent = (uint16_t *)(base + lay.bparent);
-        b_free = (uint16_t *)(base + lay.bfree);
-        b_child = (uint16_t *)(base + lay.bchild);
-        b_count = (uint8_t *)(base + lay.bcount);
-        b_leaf = (uint8_t *)(base + lay.bleaf);
-        b_scour = (int8_t *)(base + lay.bscour);
-        b_slen = (uint32_t *)(base + lay.bslen);
-        b_acc = (uint32_t *)(base + lay.bacc);
-        h_ent = (uint2 *)(base + lay.heap);
-        scratch = (uint32_t *)(base + lay.scratch);
+    MT_FI void carve(uint8_t *tb) {
+        s_len = (uint32_t *)(tb + lay.len);
+        s_sr = (uint32_t *)(tb + lay.sr);
+        s_meta = (uint32_t *)(tb + lay.meta);
+        s_blk = (uint16_t *)(tb + lay.sblk);
+        u_list = (uint16_t *)(tb + lay.ulist);
+        b_parent = (uint16_t *)(tb + lay.bparent);
+        b_child = (uint16_t *)(tb + lay.bchild);
+        b_count = (uint8_t *)(tb + lay.bcount);
+        b_leaf = (uint8_t *)(tb + lay.bleaf);
+        b_scour = (int8_t *)(tb + lay.bscour);
+        b_slen = (uint32_t *)(tb + lay.bslen);
+        b_acc = (uint32_t *)(tb + lay.bacc);
+        h_ent = (uint2 *)(tb + lay.heap);
+        scratch = (uint32_t *)(tb + lay.scratch);
     }
 
     MT_FI void set_fail(int32_t st) {
@@ -206,6 +209,8 @@ struct Engine {
         free_n = 0;
         blk_top = 0;
         n_bfree = 0;
+        bfree_head = -1;
+        sbase = 0;
         hn = 0;
         nu = 0;
         min_seq = 0;
@@ -236,7 +241,7 @@ struct Engine {
         int32_t s;
         if (free_head >= 0) {
             s = free_head;
-            free_head = rfl(s_seq[s]);
+            free_head = (int32_t)rfl(s_sr[s]);
             free_n--;
         } else {
             if (slot_top >= cap.seg) {
@@ -244,14 +249,15 @@ struct Engine {
                 return -1;
             }
             s = slot_top++;
-            s_meta[s] = 0;  // generation 0
         }
         return s;
     }
     MT_FI int32_t alloc_block(int leaf) {
         int32_t b;
         if (n_bfree > 0) {
-            b = rfl((int32_t)b_free[n_bfree - 1]);
+            b = bfree_head;
+            bfree_head = (int32_t)rfl((uint32_t)b_parent[b]);
+            if (bfree_head == (int32_t)kNoBlock) bfree_head = -1;
             n_bfree--;
         } else {
             if (blk_top >= cap.blk || blk_top >= 0xFFFF) {
@@ -268,28 +274,56 @@ struct Engine {
         return b;
     }
     MT_FI void free_block(int32_t b) {
-        b_free[n_bfree] = (uint16_t)b;
+        b_parent[b] = (uint16_t)(bfree_head < 0 ? kNoBlock : bfree_head);
+        bfree_head = b;
         n_bfree++;
     }
 
     // ------------------------------------------------------------------ visibility
-    // nodeLength of one leaf for (refSeq, clientId) + breakTie's leaf rule (mergeTree.ts:2248-2277)
-    __device__ __forceinline__ void view_of(uint32_t slot, int32_t ref, uint32_t c, uint32_t &vlen, bool &tie) const {
-        uint32_t meta = s_meta[slot];
-        int32_t seq = s_seq[slot];
-        int32_t rseq = s_rseq[slot];
-        uint32_t len = s_len[slot];
-        uint32_t cli = meta & 63u, rcli = (meta >> 6) & 63u;
-        bool vis = (cli == c) || (seq <= ref);
-        bool rem = (rcli == c) || (rseq <= ref);
-        if (!rem && (meta & kMetaHasOvl)) rem = (cold[slot].y >> c) & 1u;  // concurrent removers (rare)
-        vlen = (vis && !rem) ? len : 0u;
-        tie = !(rseq <= ref);
+    // seq relative to sbase, clamped at 0 (a value below the base is <= every valid refSeq)
+    MT_FI uint32_t rel16(int32_t q) const {
+        const int32_t d = q - sbase;
+        return d <= 0 ? 0u : (uint32_t)d;
     }
+    // removedClientOverlap membership (addOverlappingClient, mergeTree.ts:2544-2552): a bit mask
+    // of clients < 31 in cold.y, else a client list in the pool
+    __device__ __forceinline__ bool ovl_has(uint32_t slot, uint32_t c) const {
+        const uint32_t o = cold[2 * slot].y;
+        if (!(o & kOvlList)) return c < kOvlMaskClients && ((o >> c) & 1u);
+        const uint32_t *r = pool + (o & ~kOvlList);
+        const uint32_t n = r[0] & ~kPoolOvlTag;
+        bool hit = false;
+        for (uint32_t i = 0; i < n; i++) hit |= r[2 + i] == c;
+        return hit;
+    }
+    // nodeLength of one leaf for (refSeq, clientId) + breakTie's leaf rule (mergeTree.ts:2248-2277).
+    // Valid views (refSeq >= minSeq >= sbase) compare the 16-bit relative seqs in LDS, where a
+    // settled leaf has seq16 = 0 and rseq16 = 0 (removed) / kSeq16None; a view below minSeq
+    // (outside valid logs) reads the real seqs from the cold records.
+    __device__ __forceinline__ void view_of(uint32_t slot, int32_t ref, uint32_t c, uint32_t &vlen, bool &tie) const {
+        const uint32_t meta = s_meta[slot];
+        const uint32_t len = s_len[slot];
+        bool vis, rle;
+        if (ref >= min_seq) {
+            const uint32_t sr = s_sr[slot];
+            const uint32_t r16 = (uint32_t)(ref - sbase);
+            vis = (meta_cli(meta) == c) || ((sr & 0xFFFFu) <= r16);
+            rle = (sr >> 16) <= r16;
+        } else {
+            const uint4 q = cold[2 * slot + 1];
+            vis = (meta_cli(meta) == c) || ((int32_t)q.x <= ref);
+            rle = (int32_t)q.y <= ref;
+        }
+        bool rem = (meta_rcli(meta) == c) || rle;
+        if (!rem && (meta & kMetaHasOvl)) rem = ovl_has(slot, c);
+        vlen = (vis && !rem) ? len : 0u;
+        tie = !rle;
+    }
+    MT_FI static bool sr_removed(uint32_t sr) { return (sr >> 16) != kSeq16None; }
     // a leaf's contribution to the settled block sums
     __device__ __forceinline__ uint32_t settled_len(uint32_t slot) const {
         uint32_t meta = s_meta[slot];
-        return (!(meta & kMetaUnsettled) && s_rseq[slot] == kNoneSeq) ? s_len[slot] : 0u;
+        return (!(meta & kMetaUnsettled) && !sr_removed(s_sr[slot])) ? s_len[slot] : 0u;
     }
 
     // ------------------------------------------------------------------ ancestor chains
@@ -377,36 +411,49 @@ struct Engine {
         if (ov_splits != splits) overlay(ref, c);
     }
 
-    // settle every overlay entry that minSeq has caught up with (before zamboni scours)
+    // settle every overlay entry that minSeq has caught up with (before zamboni scours), and
+    // rebase the 16-bit seqs of the rest on minSeq (a settled leaf's s_sr is base independent)
     MT_FI void settle_all() {
         PF_SCOPE(11);
         int32_t w = 0;
+        const uint32_t m16 = (uint32_t)(min_seq - sbase);
         wsync();
-        for (int32_t base = 0; base < nu; base += kWave) {
-            const int32_t j = base + lane;
+        for (int32_t b0 = 0; b0 < nu; b0 += kWave) {
+            const int32_t j = b0 + lane;
             const bool in = j < nu;
             const uint32_t slot = in ? (uint32_t)u_list[j] : 0u;
             bool valid = false, elig = false;
-            uint32_t meta = 0, add = 0, b = 0;
+            uint32_t meta = 0, add = 0, b = 0, sr = 0;
             if (in) {
                 meta = s_meta[slot];
                 valid = (meta & kMetaUnsettled) && (meta & kMetaLinked);
                 if (valid) {
-                    int32_t seq = s_seq[slot], rseq = s_rseq[slot];
-                    elig = seq <= min_seq && (rseq == kNoneSeq || rseq <= min_seq);
-                    if (elig && rseq == kNoneSeq) add = s_len[slot];
+                    sr = s_sr[slot];
+                    const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
+                    elig = q16 <= m16 && (r16 == kSeq16None || r16 <= m16);
+                    if (elig && r16 == kSeq16None) add = s_len[slot];
                     b = s_blk[slot];
                 }
             }
             const bool keep = valid && !elig;
             const uint64_t km = ballot(keep);
             wsync();
-            if (keep) u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (uint16_t)slot;
-            if (elig) s_meta[slot] = meta & ~kMetaUnsettled;
+            if (keep) {
+                u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+                const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
+                const uint32_t nq = q16 > m16 ? q16 - m16 : 0u;
+                const uint32_t nr = r16 == kSeq16None ? kSeq16None : (r16 > m16 ? r16 - m16 : 0u);
+                s_sr[slot] = nq | (nr << 16);
+            }
+            if (elig) {
+                s_meta[slot] = meta & ~kMetaUnsettled;
+                s_sr[slot] = ((sr >> 16) == kSeq16None ? kSeq16None : 0u) << 16;
+            }
             w += __popcll(km);
             chain_add(b_slen, elig && add > 0u, b, add);
         }
         nu = w;
+        sbase = min_seq;
         settled_min = min_seq;
         ov_splits = -1;  // b_slen moved under the overlay
         wsync();
@@ -505,7 +552,7 @@ struct Engine {
             if (slot < slot_top) {
                 const uint32_t m = s_meta[slot];
                 if ((m & kMetaLinked) && !(m & kMetaMarker)) {
-                    cr = cold[slot];
+                    cr = cold[2 * slot];
                     mv = cr.z >= arena_base && cr.z < arena_end;
                 }
             }
@@ -525,7 +572,7 @@ struct Engine {
                 if (lane == f) {
                     cr.z = top;
                     cr.w = cap16;
-                    cold[sl] = cr;
+                    cold[2 * sl] = cr;
                 }
                 top += cap16;
             }
@@ -538,48 +585,62 @@ struct Engine {
         wsync();
     }
 
-    // make room for `words` in the prop pool: semispace copy of the live sets when full
+    // make room for `words` in the prop pool: semispace copy of the live records when full
     // (Cheney-style: a copied record's header becomes a forwarding pointer, so sets shared by
-    // several segments are copied once)
+    // several segments are copied once).  Live records: the prop sets of linked segments
+    // (cold.x) and their overlap-client lists (cold.y with kOvlList).
+    MT_FI uint32_t pool_forward(uint32_t o, uint32_t nb, uint32_t &top) {
+        const uint32_t hdr = pool[o];
+        if (hdr == 0xFFFFFFFFu) return pool[o + 1];
+        const uint32_t w = (hdr & kPoolOvlTag) ? 2u + (hdr & ~kPoolOvlTag) : 2u + 2u * hdr;
+        if (top + w > nb + semi_p) {
+            cap_fail(3);
+            return 0;
+        }
+        for (uint32_t i = lane; i < w; i += kWave) pool[top + i] = pool[o + i];
+        wsync();
+        const uint32_t nid = top;
+        top += w;
+        if (lane == 0) {
+            pool[o] = 0xFFFFFFFFu;
+            pool[o + 1] = nid;
+        }
+        wsync();
+        return nid;
+    }
     MT_FI void pool_reserve(uint32_t words) {
         if (pool_top + words <= pool_end) return;
         resolve_cold();
         const uint32_t nb = pool_base == 1u ? 1u + semi_p : 1u;
         uint32_t top = nb;
         wsync();
-        for (int32_t base = 0; base < slot_top; base += kWave) {
-            const int32_t slot = base + lane;
-            uint32_t old = 0;
+        for (int32_t b0 = 0; b0 < slot_top; b0 += kWave) {
+            const int32_t slot = b0 + lane;
+            uint32_t old = 0, ovl = 0;
             if (slot < slot_top) {
                 const uint32_t m = s_meta[slot];
-                if ((m & kMetaLinked) && (m & kMetaHasProps)) old = cold[slot].x;
+                if (m & kMetaLinked) {
+                    const uint4 cr = cold[2 * slot];
+                    if (m & kMetaHasProps) old = cr.x;
+                    if ((m & kMetaHasOvl) && (cr.y & kOvlList)) ovl = cr.y & ~kOvlList;
+                }
             }
             uint64_t msk = ballot(old != 0u);
             while (msk) {
                 const int f = first_lane(msk);
                 msk &= msk - 1;
-                const uint32_t sl = (uint32_t)(base + f);
-                const uint32_t o = rdl(old, f);
-                const uint32_t hdr = pool[o];
-                uint32_t nid;
-                if (hdr == 0xFFFFFFFFu) {
-                    nid = pool[o + 1];
-                } else {
-                    const uint32_t w = 2u + 2u * hdr;
-                    if (top + w > nb + semi_p) {
-                        cap_fail(3);
-                        return;
-                    }
-                    for (uint32_t i = lane; i < w; i += kWave) pool[top + i] = pool[o + i];
-                    wsync();
-                    nid = top;
-                    top += w;
-                    if (lane == 0) {
-                        pool[o] = 0xFFFFFFFFu;
-                        pool[o + 1] = nid;
-                    }
-                }
-                if (lane == 0) cold[sl].x = nid;
+                const uint32_t nid = pool_forward(rdl(old, f), nb, top);
+                if (status) return;
+                if (lane == 0) cold[2 * (uint32_t)(b0 + f)].x = nid;
+                wsync();
+            }
+            msk = ballot(ovl != 0u);
+            while (msk) {
+                const int f = first_lane(msk);
+                msk &= msk - 1;
+                const uint32_t nid = pool_forward(rdl(ovl, f), nb, top);
+                if (status) return;
+                if (lane == 0) cold[2 * (uint32_t)(b0 + f)].y = nid | kOvlList;
                 wsync();
             }
         }
@@ -718,14 +779,15 @@ struct Engine {
         const uint32_t slot = rfl((uint32_t)b_child[blk * 8 + k]);
         const uint32_t meta = s_meta[slot];
         if (meta & kMetaMarker) return -1;  // Marker.createSplitSegmentAt returns undefined
-        uint4 cr;
+        // the slot's two cold records, lane-distributed (lane i < 8: word i)
+        uint32_t pv;
         if (pend_n > 0 && slot == ps0) {
             resolve_splits();  // (inverted range) the first split's left half is cut again
-            cr = make_uint4(pc0.x, pc0.y, pc0.z, pr0);
+            pv = lane == 3 ? pr0 : pv0;
         } else if (pend_n > 0 && slot == pn0) {
-            cr = make_uint4(pc0.x, pc0.y, pc0.z + pr0, pc0.w - pr0);
+            pv = pv0 + (lane == 2 ? pr0 : 0u) - (lane == 3 ? pr0 : 0u);
         } else {
-            cr = cold[slot];
+            pv = lane < 8 ? reinterpret_cast<const uint32_t *>(cold + 2 * slot)[lane] : 0u;
         }
         const int32_t ns = alloc_slot();
         if (ns < 0) return -1;
@@ -734,19 +796,17 @@ struct Engine {
             ps0 = slot;
             pn0 = (uint32_t)ns;
             pr0 = r;
-            pc0 = cr;
+            pv0 = pv;
         } else {
             ps1 = slot;
             pn1 = (uint32_t)ns;
             pr1 = r;
-            pc1 = cr;
+            pv1 = pv;
         }
         pend_n++;
         s_len[ns] = len - r;
-        s_seq[ns] = s_seq[slot];
-        s_rseq[ns] = s_rseq[slot];
-        const uint32_t gen = s_meta[ns] & kGenMask;
-        s_meta[ns] = (meta & ~kGenMask) | gen;  // inherits ends-NL of the tail, linked, unsettled
+        s_sr[ns] = s_sr[slot];
+        s_meta[ns] = meta;  // inherits ends-NL of the tail, linked, unsettled
         s_len[slot] = r;
         wsync();
         if (meta & kMetaUnsettled) u_push((uint32_t)ns);
@@ -755,17 +815,18 @@ struct Engine {
         return nb;
     }
 
-    // write the pending splits' cold records and start the text loads for ends-with-'\n'
+    // write the pending splits' cold records and start the text loads for ends-with-'\n': the
+    // left half keeps its records with tcap = r, the right half gets (toff + r, tcap - r) and a
+    // copy of the seq record
     MT_FI void resolve_cold() {
         for (int32_t i = pend_cold; i < pend_n; i++) {
             const uint32_t sl = i ? ps1 : ps0, ns = i ? pn1 : pn0, r = i ? pr1 : pr0;
-            const uint4 c = i ? pc1 : pc0;
-            if (lane == 0) {
-                cold[sl] = make_uint4(c.x, c.y, c.z, r);
-                cold[ns] = make_uint4(c.x, c.y, c.z + r, c.w - r);
-            }
+            const uint32_t pv = i ? pv1 : pv0;
+            if (lane == 3) reinterpret_cast<uint32_t *>(cold + 2 * sl)[3] = r;
+            if (lane < 8)
+                reinterpret_cast<uint32_t *>(cold + 2 * ns)[lane] = pv + (lane == 2 ? r : 0u) - (lane == 3 ? r : 0u);
             // a text without any '\n' cannot end in one: no HBM read
-            const uint32_t ch = (s_meta[sl] & kMetaHasNL) ? (uint32_t)text[c.z + r - 1] : 0u;
+            const uint32_t ch = (s_meta[sl] & kMetaHasNL) ? (uint32_t)text[rdl(pv, 2) + r - 1] : 0u;
             if (i) pch1 = ch;
             else pch0 = ch;
         }
@@ -828,7 +889,7 @@ struct Engine {
     MT_FI void add_to_lru(int32_t blk, uint32_t slot, int32_t seq) {
         if (b_scour[blk] != kScourTrue && seq > cur_seq) {
             b_scour[blk] = kScourTrue;
-            heap_add(slot | (s_meta[slot] & kGenMask), seq);
+            heap_add(slot, seq);
         }
     }
 
@@ -888,6 +949,22 @@ struct Engine {
         }
         if (hn >= 1) h_ent[k] = last;
         htop = hn >= 1 ? newtop : kNoneSeq;
+        wsync();
+    }
+
+    // Heap entries hold segment identity (the reference's Heap of {node, maxSeq}): when scour frees
+    // slots (merged away / unlinked: parent = undefined, mergeTree.ts:1317, 1341, 1438), the
+    // entries naming them are invalidated, so a slot reused later is never scoured by an old
+    // entry.  `slot` holds the lanes' slots, `freeM` the freed lanes.
+    MT_FI void heap_forget(uint32_t slot, uint64_t freeM) {
+
+        for (int32_t j0 = 1; j0 <= hn; j0 += kWave) {
+            const int32_t j = j0 + lane;
+            const uint32_t key = j <= hn ? h_ent[j].x : kHeapInvalid;
+            bool hit = false;
+            for (uint64_t m = freeM; m; m &= m - 1) hit |= key == rdl(slot, first_lane(m));
+            if (hit && key != kHeapInvalid) h_ent[j].x = kHeapInvalid;
+        }
         wsync();
     }
 
@@ -1043,21 +1120,21 @@ struct Engine {
     MT_FI int32_t scour(uint32_t slot, int32_t n, uint64_t startM, uint32_t *hold) {
         PF_SCOPE(7);
         const bool in = lane < n;
-        int32_t rseq = kNoneSeq, seq = 0;
-        uint32_t meta = 0, len = 0;
+        uint32_t meta = 0, len = 0, sr = 0;
         uint4 cr = make_uint4(0, 0, 0, 0);
         if (in) {
-            cr = cold[slot];  // HBM: waited on only where props or merges need it
-            rseq = s_rseq[slot];
-            seq = s_seq[slot];
+            cr = cold[2 * slot];  // HBM: waited on only where props or merges need it
+            sr = s_sr[slot];
             meta = s_meta[slot];
             len = s_len[slot];
         }
-        const bool rem = in && rseq != kNoneSeq;
-        const bool cand = in && !rem && seq <= min_seq;
+        // settle_all ran at this minSeq (sbase == minSeq): seq <= minSeq is seq16 == 0, a settled
+        // removal has rseq16 == 0
+        const bool rem = in && sr_removed(sr);
+        const bool cand = in && !rem && (sr & 0xFFFFu) == 0u;
         const uint32_t mprev = __shfl_up(meta, 1, kWave);
         const uint64_t candM = ballot(cand);
-        const uint64_t freeR = ballot(rem && rseq <= min_seq);
+        const uint64_t freeR = ballot(rem && (sr >> 16) == 0u);
         const uint64_t liveM = ballot(in);
         // lane k may append to the chain ending at lane k - 1 (TextSegment.canAppend without its
         // length rule, plus matchProperties): both candidates, same block, neither a Marker, the
@@ -1154,7 +1231,7 @@ struct Engine {
                 const uint32_t fslot = rdl(slot, k), sl = rdl(len, k);
                 uint32_t stoff = rdl(cr.z, k), stcap = rdl(cr.w, k);
                 if (text_gcs != gcs0) {  // a compaction moved texts: offsets are in HBM again
-                    const uint4 hc = cold[hslot], fc = cold[fslot];
+                    const uint4 hc = cold[2 * hslot], fc = cold[2 * fslot];
                     ptoff = hc.z;
                     pcap = hc.w;
                     stoff = fc.z;
@@ -1176,15 +1253,15 @@ struct Engine {
                     // reallocate; a compaction inside arena_alloc moves every text, so the head
                     // is written back first and both offsets re-read afterwards
                     s_len[hslot] = pl;
-                    if (lane == 0) cold[hslot] = make_uint4(hprops, hov, ptoff, pcap);
+                    if (lane == 0) cold[2 * hslot] = make_uint4(hprops, hov, ptoff, pcap);
                     wsync();
                     const uint32_t ncap = 2u * need;
                     const int32_t g0 = text_gcs;
                     const uint32_t dst = arena_alloc(ncap);
                     if (status) return 0;
                     if (text_gcs != g0) {
-                        ptoff = cold[hslot].z;
-                        stoff = cold[fslot].z;
+                        ptoff = cold[2 * hslot].z;
+                        stoff = cold[2 * fslot].z;
                     }
                     text_copy(dst, ptoff, pl);
                     text_copy(dst + pl, stoff, sl);
@@ -1195,7 +1272,7 @@ struct Engine {
                 const uint32_t fm = rdl(meta, k);
                 hmeta = (hmeta & ~kMetaEndsNL) | (fm & (kMetaEndsNL | kMetaHasNL));
                 s_len[hslot] = pl;
-                if (lane == 0) cold[hslot] = make_uint4(hprops, hov, ptoff, pcap);
+                if (lane == 0) cold[2 * hslot] = make_uint4(hprops, hov, ptoff, pcap);
                 s_meta[hslot] = hmeta;
                 wsync();
             }
@@ -1205,42 +1282,22 @@ struct Engine {
         const uint64_t holdM = liveM & ~freeM;
         const uint64_t below = (1ull << lane) - 1ull;
         wsync();
-        // freed slots are pushed on the free list, linked through s_seq in lane order
+        // freed slots are pushed on the free list, linked through s_sr in lane order
         const uint64_t above = ~((2ull << lane) - 1ull);
         const uint64_t nxtM = freeM & above;
         const int32_t nxt = __shfl((int)slot, nxtM ? first_lane(nxtM) : 0, kWave);
         if ((freeM >> lane) & 1ull) {
-            s_meta[slot] = ((meta >> kGenShift) + 1u) << kGenShift;  // unlinked, next generation
-            s_seq[slot] = nxtM ? nxt : free_head;
+            s_meta[slot] = 0u;  // unlinked
+            s_sr[slot] = (uint32_t)(nxtM ? nxt : free_head);
         }
-        if (freeM) free_head = (int32_t)rdl(slot, first_lane(freeM));
+        if (freeM) {
+            free_head = (int32_t)rdl(slot, first_lane(freeM));
+            heap_forget(slot, freeM);
+        }
         free_n += __popcll(freeM);
         if ((holdM >> lane) & 1ull) hold[__popcll(holdM & below)] = slot;
         wsync();
         return __popcll(holdM);
-    }
-
-    // Lane-parallel block allocation: lane q < cnt receives a block id (free-list pops first,
-    // in the order alloc_block would return them) initialised as MergeTree.makeBlock does.
-    MT_FI uint32_t alloc_blocks(int32_t cnt, int leaf, int32_t parent) {
-        const int32_t pop = cnt < n_bfree ? cnt : n_bfree;
-        if (blk_top + (cnt - pop) > cap.blk) {
-            cap_fail(1);
-            return 0;
-        }
-        uint32_t id = 0;
-        if (lane < pop) id = b_free[n_bfree - 1 - lane];
-        else if (lane < cnt) id = (uint32_t)(blk_top + lane - pop);
-        n_bfree -= pop;
-        blk_top += cnt - pop;
-        wsync();
-        if (lane < cnt) {
-            b_leaf[id] = (uint8_t)leaf;
-            b_scour[id] = kScourUndef;
-            b_parent[id] = (uint16_t)parent;
-            b_slen[id] = 0u;
-        }
-        return id;
     }
 
     // Regroup `nk` children (hold[0..nk)) of `parent`'s former child blocks into
@@ -1252,13 +1309,22 @@ struct Engine {
         if (cc < 1) cc = 1;
         const int32_t base = nk / cc, extra = nk % cc;
         wsync();
-        // the old child blocks go to the free list, then cc new ones come off it
-        if (lane < pn) b_free[n_bfree + lane] = b_child[parent * 8 + lane];
-        n_bfree += pn;
+        // the cc new blocks (MergeTree.makeBlock) reuse the ids of the old child blocks; surplus old
+        // blocks go to the free list, missing ones come off it
+        uint32_t id = lane < pn ? (uint32_t)b_child[parent * 8 + lane] : 0u;
         wsync();
-        const uint32_t id = alloc_blocks(cc, leaf, parent);
-        if (status) return cc;
+        for (int32_t q = cc; q < pn; q++) free_block((int32_t)rdl(id, q));
+        for (int32_t q = pn; q < cc; q++) {
+            const int32_t nb = alloc_block(leaf);
+            if (status) return cc;
+            if (lane == q) id = (uint32_t)nb;
+        }
+        wsync();
         if (lane < cc) {
+            b_leaf[id] = (uint8_t)leaf;
+            b_scour[id] = kScourUndef;
+            b_parent[id] = (uint16_t)parent;
+            b_slen[id] = 0u;
             b_count[id] = (uint8_t)(base + (lane < extra ? 1 : 0));
             b_child[parent * 8 + lane] = (uint16_t)id;
         }
@@ -1355,9 +1421,8 @@ struct Engine {
             uint32_t key;
             int32_t mseq;
             heap_get(key, mseq);
-            const uint32_t slot = key & 0xFFFFu;
-            const uint32_t meta = s_meta[slot];
-            if ((meta & kGenMask) != (key & kGenMask) || !(meta & kMetaLinked)) continue;  // parent undefined
+            if (key == kHeapInvalid) continue;  // the segment was merged away / unlinked: parent undefined
+            const uint32_t slot = key;
             const int32_t blk = s_blk[slot];
             if (b_scour[blk] == kScourFalse) continue;
             const int32_t cnt = b_count[blk];
@@ -1428,20 +1493,22 @@ struct Engine {
                 if (status) return;
             }
             const int32_t rseq = loaded ? op.ref_seq : kNoneSeq;
-            const uint32_t rcli = loaded && rseq != kNoneSeq ? ((uint32_t)op.msn & 63u) : kNoClient;
+            const uint32_t rcli = loaded && rseq != kNoneSeq ? ((uint32_t)op.msn & kMetaCli) : kNoClient;
             // a loaded segment below the collab window is settled: it joins the settled sums
             // after the leaf insert (while it moves through block splits it counts as unsettled)
             const bool settled = loaded && op.seq <= min_seq && (rseq == kNoneSeq || rseq <= min_seq);
-            uint32_t gen = s_meta[slot] & kGenMask;
-            uint32_t meta = gen | kMetaLinked | kMetaUnsettled | (c & 63u) | (rcli << 6);
+            uint32_t meta = kMetaLinked | kMetaUnsettled | (c & kMetaCli) | (rcli << kMetaRcliShift);
             if (marker) meta |= kMetaMarker;
             if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
             if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
             if (props) meta |= kMetaHasProps;
             s_len[slot] = len;
-            s_seq[slot] = op.seq;
-            s_rseq[slot] = rseq;
-            if (lane == 0) cold[slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
+            s_sr[slot] = settled ? (rseq == kNoneSeq ? kSeq16None : 0u) << 16
+                                 : rel16(op.seq) | ((rseq == kNoneSeq ? kSeq16None : rel16(rseq)) << 16);
+            if (lane == 0) {
+                cold[2 * slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
+                cold[2 * slot + 1] = make_uint4((uint32_t)op.seq, (uint32_t)rseq, 0u, 0u);
+            }
             s_meta[slot] = meta;
             wsync();
             if (!settled) u_push((uint32_t)slot);
@@ -1479,16 +1546,18 @@ struct Engine {
             if (status) return;
         }
         const int32_t rseq = op.ref_seq;
-        const uint32_t rcli = rseq != kNoneSeq ? ((uint32_t)op.msn & 63u) : kNoClient;
-        uint32_t meta = (s_meta[slot] & kGenMask) | kMetaLinked | (op.client & 63u) | (rcli << 6);
+        const uint32_t rcli = rseq != kNoneSeq ? ((uint32_t)op.msn & kMetaCli) : kNoClient;
+        uint32_t meta = kMetaLinked | (op.client & kMetaCli) | (rcli << kMetaRcliShift);
         if (marker) meta |= kMetaMarker;
         if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
         if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
         if (props) meta |= kMetaHasProps;
         s_len[slot] = len;
-        s_seq[slot] = op.seq;
-        s_rseq[slot] = rseq;
-        if (lane == 0) cold[slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
+        s_sr[slot] = 0u;  // set by op_collab from the real seqs in the cold record
+        if (lane == 0) {
+            cold[2 * slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
+            cold[2 * slot + 1] = make_uint4((uint32_t)op.seq, (uint32_t)rseq, 0u, 0u);
+        }
         s_meta[slot] = meta;
         wsync();
         // the rightmost leaf block
@@ -1549,7 +1618,12 @@ struct Engine {
         min_seq = op.msn;
         cur_seq = op.seq;
         settled_min = min_seq;
+        sbase = min_seq;
         ov_splits = -1;
+        if (cur_seq - sbase >= kSeq16Span) {
+            cap_fail(5);
+            return;
+        }
         wsync();
         for (int32_t i = lane; i < blk_top; i += kWave) b_slen[i] = 0u;
         wsync();
@@ -1562,10 +1636,13 @@ struct Engine {
                 meta = s_meta[slot];
                 live = (meta & kMetaLinked) != 0;
                 if (live) {
-                    const int32_t sq = s_seq[slot], rs = s_rseq[slot];
+                    const uint4 q = cold[2 * slot + 1];  // the loaded segment's real seqs
+                    const int32_t sq = (int32_t)q.x, rs = (int32_t)q.y;
                     sett = sq <= min_seq && (rs == kNoneSeq || rs <= min_seq);
                     if (sett && rs == kNoneSeq) add = s_len[slot];
                     b = s_blk[slot];
+                    s_sr[slot] = sett ? (rs == kNoneSeq ? kSeq16None : 0u) << 16
+                                      : rel16(sq) | ((rs == kNoneSeq ? kSeq16None : rel16(rs)) << 16);
                 }
             }
             const bool un = live && !sett;
@@ -1591,7 +1668,7 @@ struct Engine {
         for (int32_t base = 0; base < slot_top; base += kWave) {
             const int32_t slot = base + lane;
             uint32_t v = 0;
-            if (slot < slot_top && (s_meta[slot] & kMetaLinked) && s_rseq[slot] == kNoneSeq) v = s_len[slot];
+            if (slot < slot_top && (s_meta[slot] & kMetaLinked) && !sr_removed(s_sr[slot])) v = s_len[slot];
             sum += rdl(scan_incl(v), 63);
         }
         return sum;
@@ -1625,6 +1702,47 @@ struct Engine {
         if (end > start) range_walk(op, start, end);
         resolve_splits();
         zamboni();
+    }
+
+    // addOverlappingClient (mergeTree.ts:2544-2552) for the lanes of `m`: client c joins each
+    // segment's removedClientOverlap.  Clients < 31 set a bit of the mask in cold.y; a larger
+    // client turns the set into a pool list [n | kPoolOvlTag, 0, clients...] (rare: concurrent
+    // removes by a client beyond the 31st).
+    MT_FI void ovl_add(uint32_t slot, uint64_t m, uint32_t c) {
+        for (; m; m &= m - 1) {
+            const uint32_t sl = rdl(slot, first_lane(m));
+            const bool had = (s_meta[sl] & kMetaHasOvl) != 0;
+            const uint32_t o = had ? rfl(cold[2 * sl].y) : 0u;
+            if (!(o & kOvlList) && c < kOvlMaskClients) {
+                if (lane == 0) cold[2 * sl].y = o | (1u << c);
+            } else {
+                // members of the old set, then c (no compaction here: a full pool stops the
+                // document with MT_CAPACITY, cap_kind 3)
+                const uint32_t n_old = (o & kOvlList) ? (pool[o & ~kOvlList] & ~kPoolOvlTag) : (uint32_t)__popc(o);
+                if (pool_top + 3u + n_old > pool_end) {
+                    cap_fail(3);
+                    return;
+                }
+                const uint32_t ol = o & ~kOvlList;
+                const uint32_t id = pool_top;
+                pool_top += 3u + n_old;
+                if (o & kOvlList) {
+                    for (uint32_t i = lane; i < n_old; i += kWave) pool[id + 2 + i] = pool[ol + 2 + i];
+                } else {
+                    const bool bit = lane < (int)kOvlMaskClients && ((o >> lane) & 1u);
+                    const uint64_t bm = ballot(bit);
+                    if (bit) pool[id + 2 + __popcll(bm & ((1ull << lane) - 1ull))] = (uint32_t)lane;
+                }
+                if (lane == 0) {
+                    pool[id] = (n_old + 1u) | kPoolOvlTag;
+                    pool[id + 1] = 0u;
+                    pool[id + 2 + n_old] = c;
+                    cold[2 * sl].y = id | kOvlList;
+                }
+            }
+            s_meta[sl] = s_meta[sl] | kMetaHasOvl;
+            wsync();
+        }
     }
 
     MT_FI int32_t next_leaf_block(int32_t b) {
@@ -1668,16 +1786,21 @@ struct Engine {
             const bool hit = lane < n && lane < kMaxNodes && vlen > 0u && excl < end && incl > start;
             uint64_t hb = ballot(hit);
             const uint32_t bend = n > 0 ? rdl(incl, n - 1) : base;
+            bool again = false;
             if (is_remove && hit) {
-                if (s_rseq[slot] != kNoneSeq) {
-                    // addOverlappingClient (mergeTree.ts:2544-2552)
-                    uint32_t *ov = &cold[slot].y;
-                    *ov = ((s_meta[slot] & kMetaHasOvl) ? *ov : 0u) | (1u << c);
-                    s_meta[slot] = s_meta[slot] | kMetaHasOvl;
+                const uint32_t sr = s_sr[slot];
+                if (sr_removed(sr)) {
+                    again = true;  // a concurrent remover: addOverlappingClient below
                 } else {
-                    s_rseq[slot] = op.seq;
-                    s_meta[slot] = (s_meta[slot] & ~(63u << 6)) | ((c & 63u) << 6);
+                    s_sr[slot] = (sr & 0xFFFFu) | (rel16(op.seq) << 16);
+                    s_meta[slot] = (s_meta[slot] & ~(kMetaCli << kMetaRcliShift)) | ((c & kMetaCli) << kMetaRcliShift);
+                    cold[2 * slot + 1].y = (uint32_t)op.seq;
                 }
+            }
+            const uint64_t againM = ballot(again);
+            if (againM) {
+                ovl_add(slot, againM, c);
+                if (status) return;
             }
             if (is_remove) {
                 // a settled leaf removed now leaves the settled sums and joins the overlay
@@ -1703,7 +1826,7 @@ struct Engine {
             }
             wsync();
             uint32_t oldp = 0;
-            if (!is_remove && hit) oldp = cold[slot].x;
+            if (!is_remove && hit) oldp = cold[2 * slot].x;
             // in document order: properties (annotate) and addToLRUSet
             while (hb) {
                 const int f = first_lane(hb);
@@ -1716,7 +1839,7 @@ struct Engine {
                     uint32_t old;
                     if (pool_gcs != g0) {  // ids moved
                         memo_n = 0;
-                        oldp = hit ? cold[slot].x : 0u;
+                        oldp = hit ? cold[2 * slot].x : 0u;
                     }
                     old = rdl(oldp, f);
                     uint64_t mb = ballot((uint32_t)lane < memo_n && memo_old == old);
@@ -1737,7 +1860,7 @@ struct Engine {
                             memo_n++;
                         }
                     }
-                    if (lane == 0) cold[sl].x = nid;
+                    if (lane == 0) cold[2 * sl].x = nid;
                     s_meta[sl] = s_meta[sl] | kMetaHasProps;
                 }
                 add_to_lru(blk, sl, op.seq);
@@ -1754,7 +1877,7 @@ struct Engine {
     MT_FI void apply_load(const mt_op &op) {
         pend_n = 0;
         const bool noncollab = op.client == MT_CLIENT_NONCOLLAB;
-        if (op.type != MT_OP_COLLAB && (op.client == 0 || (op.client >= kMaxClients && !noncollab))) {
+        if (op.type != MT_OP_COLLAB && (op.client == 0 || (op.client >= (uint32_t)kMaxClients && !noncollab))) {
             set_fail(ST_UNSUPPORTED);
             return;
         }
@@ -1766,8 +1889,15 @@ struct Engine {
 
     MT_FI void apply(const mt_op &op) {
         pend_n = 0;
-        if (op.client >= kMaxClients || (op.client == 0 && op.type != MT_OP_NOOP)) {
+        if (op.client >= (uint32_t)kMaxClients || (op.client == 0 && op.type != MT_OP_NOOP)) {
             set_fail(ST_UNSUPPORTED);
+            return;
+        }
+        // the 16-bit relative seqs in LDS need seq - sbase < kSeq16Span: rebase on minSeq, and a
+        // collab window wider than that stops the document (MT_CAPACITY, cap_kind 5)
+        if (op.seq - sbase >= kSeq16Span / 2 && min_seq > sbase) settle_all();
+        if (op.seq - sbase >= kSeq16Span) {
+            cap_fail(5);
             return;
         }
         switch (op.type) {
@@ -1871,16 +2001,16 @@ struct Engine {
             ck[20] = (uint32_t)text_gcs;
             ck[21] = (uint32_t)max_heap;
             ck[22] = (uint32_t)max_u;
+            ck[23] = (uint32_t)sbase;
+            ck[24] = (uint32_t)bfree_head;
         }
         uint32_t *p = ck + kCkHdr;
         dump(p, s_len, slot_top);
-        dump(p, s_seq, slot_top);
-        dump(p, s_rseq, slot_top);
+        dump(p, s_sr, slot_top);
         dump(p, s_meta, slot_top);
         dump(p, s_blk, slot_top);
         dump(p, u_list, nu);
         dump(p, b_parent, blk_top);
-        dump(p, b_free, n_bfree);
         dump(p, (const uint32_t *)b_child, 4 * blk_top);
         for (int32_t i = lane; i < blk_top; i += kWave)
             p[i] = (uint32_t)b_count[i] | ((uint32_t)b_leaf[i] << 8) | ((uint32_t)(uint8_t)b_scour[i] << 16);
@@ -1912,17 +2042,17 @@ struct Engine {
         text_gcs = (int32_t)rfl(ck[20]);
         max_heap = (int32_t)rfl(ck[21]);
         max_u = (int32_t)rfl(ck[22]);
+        sbase = (int32_t)rfl(ck[23]);
+        bfree_head = (int32_t)rfl(ck[24]);
         arena_end = arena_base + semi_t;
         pool_end = pool_base + semi_p;
         const uint32_t *p = ck + kCkHdr;
         load(p, s_len, slot_top);
-        load(p, s_seq, slot_top);
-        load(p, s_rseq, slot_top);
+        load(p, s_sr, slot_top);
         load(p, s_meta, slot_top);
         load(p, s_blk, slot_top);
         load(p, u_list, nu);
         load(p, b_parent, blk_top);
-        load(p, b_free, n_bfree);
         load(p, (uint32_t *)b_child, 4 * blk_top);
         for (int32_t i = lane; i < blk_top; i += kWave) {
             const uint32_t v = p[i];
@@ -1933,7 +2063,7 @@ struct Engine {
         p += blk_top;
         load(p, b_slen, blk_top);
         load(p, (uint32_t *)h_ent, 2 * (hn + 1));
-        for (int32_t i = lane; i < slot_top; i += kWave) cold[i] = cold_src[i];
+        for (int32_t i = lane; i < kColdPerSlot * slot_top; i += kWave) cold[i] = cold_src[i];
         wsync();
         return ops_done;
     }
@@ -1956,11 +2086,12 @@ struct Engine {
                 OutRec r;
                 if (lane < n) {
                     const uint32_t slot = b_child[blk * 8 + lane];
-                    const uint4 cr = cold[slot < (uint32_t)SEG ? slot : 0u];
+                    const uint32_t cs = slot < (uint32_t)SEG ? slot : 0u;
+                    const uint4 cr = cold[2 * cs], sq = cold[2 * cs + 1];
                     r.len = s_len[slot];
-                    r.seq = s_seq[slot];
-                    r.rseq = s_rseq[slot];
-                    r.meta = s_meta[slot] & 0xFFFFu & ~kMetaUnsettled;
+                    r.seq = (int32_t)sq.x;
+                    r.rseq = (int32_t)sq.y;
+                    r.meta = s_meta[slot] & (kMetaHasOvl * 2u - 1u) & ~kMetaUnsettled;
                     r.ovl = (s_meta[slot] & kMetaHasOvl) ? cr.y : 0u;
                     r.props = cr.x;
                     r.toff = cr.z;
@@ -2031,7 +2162,7 @@ template <int SEG>
 MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_t d, uint8_t *smem) {
     E.lane = threadIdx.x;
     E.carve(smem);
-    E.cold = P.cold + w * (int64_t)SEG;
+    E.cold = P.cold + w * (int64_t)SEG * kColdPerSlot;
     E.text = P.text + P.doc_text_base[d];
     E.text_cap = P.doc_text_cap[d];
     E.pay_end = (P.doc_text_len[d] + 15u) & ~15u;
@@ -2158,7 +2289,8 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
     int32_t done = 0, fail_op = -1;
     if (P.ck_in) {
         if (src == kSrcList) src = P.ck_src[w];
-        if (src >= 0) done = E.restore(P.ck_in + src * P.ck_in_words, P.cold_in + (int64_t)src * P.cold_in_seg);
+        if (src >= 0)
+            done = E.restore(P.ck_in + src * P.ck_in_words, P.cold_in + (int64_t)src * P.cold_in_seg * kColdPerSlot);
     }
     // follow-on producer: workgroups are dispatched in index order, so the last one starting
     // means all are resident and the host may launch the consumer

@@ -32,21 +32,21 @@
     extern "C" __global__ void mt_load_kernel_##S(mt::ReplayParams P);        \
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);    \
     extern "C" __global__ void mt_follow_kernel_##S(mt::ReplayParams P);
-MT_DECLARE_CLASS(64)
 MT_DECLARE_CLASS(128)
-MT_DECLARE_CLASS(280)
-MT_DECLARE_CLASS(323)
-MT_DECLARE_CLASS(368)
-MT_DECLARE_CLASS(408)
+MT_DECLARE_CLASS(349)
+MT_DECLARE_CLASS(403)
 MT_DECLARE_CLASS(456)
-MT_DECLARE_CLASS(540)
-MT_DECLARE_CLASS(628)
-MT_DECLARE_CLASS(848)
-MT_DECLARE_CLASS(1023)
-MT_DECLARE_CLASS(1328)
-MT_DECLARE_CLASS(1764)
-MT_DECLARE_CLASS(2724)
-MT_DECLARE_CLASS(4999)
+MT_DECLARE_CLASS(509)
+MT_DECLARE_CLASS(563)
+MT_DECLARE_CLASS(672)
+MT_DECLARE_CLASS(779)
+MT_DECLARE_CLASS(888)
+MT_DECLARE_CLASS(1048)
+MT_DECLARE_CLASS(1264)
+MT_DECLARE_CLASS(1644)
+MT_DECLARE_CLASS(2184)
+MT_DECLARE_CLASS(3373)
+MT_DECLARE_CLASS(6806)
 MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
@@ -84,36 +84,36 @@ struct KernelClass {
     const void *follow;
 };
 static const KernelClass kKernels[mt::kNumClasses] = {
-    {64, (const void *)mt_replay_kernel_64, (const void *)mt_generate_kernel_64, (const void *)mt_load_kernel_64,
-     (const void *)mt_follow_kernel_64},
     {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
      (const void *)mt_follow_kernel_128},
-    {280, (const void *)mt_replay_kernel_280, (const void *)mt_generate_kernel_280, (const void *)mt_load_kernel_280,
-     (const void *)mt_follow_kernel_280},
-    {323, (const void *)mt_replay_kernel_323, (const void *)mt_generate_kernel_323, (const void *)mt_load_kernel_323,
-     (const void *)mt_follow_kernel_323},
-    {368, (const void *)mt_replay_kernel_368, (const void *)mt_generate_kernel_368, (const void *)mt_load_kernel_368,
-     (const void *)mt_follow_kernel_368},
-    {408, (const void *)mt_replay_kernel_408, (const void *)mt_generate_kernel_408, (const void *)mt_load_kernel_408,
-     (const void *)mt_follow_kernel_408},
+    {349, (const void *)mt_replay_kernel_349, (const void *)mt_generate_kernel_349, (const void *)mt_load_kernel_349,
+     (const void *)mt_follow_kernel_349},
+    {403, (const void *)mt_replay_kernel_403, (const void *)mt_generate_kernel_403, (const void *)mt_load_kernel_403,
+     (const void *)mt_follow_kernel_403},
     {456, (const void *)mt_replay_kernel_456, (const void *)mt_generate_kernel_456, (const void *)mt_load_kernel_456,
      (const void *)mt_follow_kernel_456},
-    {540, (const void *)mt_replay_kernel_540, (const void *)mt_generate_kernel_540, (const void *)mt_load_kernel_540,
-     (const void *)mt_follow_kernel_540},
-    {628, (const void *)mt_replay_kernel_628, (const void *)mt_generate_kernel_628, (const void *)mt_load_kernel_628,
-     (const void *)mt_follow_kernel_628},
-    {848, (const void *)mt_replay_kernel_848, (const void *)mt_generate_kernel_848, (const void *)mt_load_kernel_848,
-     (const void *)mt_follow_kernel_848},
-    {1023, (const void *)mt_replay_kernel_1023, (const void *)mt_generate_kernel_1023, (const void *)mt_load_kernel_1023,
-     (const void *)mt_follow_kernel_1023},
-    {1328, (const void *)mt_replay_kernel_1328, (const void *)mt_generate_kernel_1328, (const void *)mt_load_kernel_1328,
-     (const void *)mt_follow_kernel_1328},
-    {1764, (const void *)mt_replay_kernel_1764, (const void *)mt_generate_kernel_1764, (const void *)mt_load_kernel_1764,
-     (const void *)mt_follow_kernel_1764},
-    {2724, (const void *)mt_replay_kernel_2724, (const void *)mt_generate_kernel_2724, (const void *)mt_load_kernel_2724,
-     (const void *)mt_follow_kernel_2724},
-    {4999, (const void *)mt_replay_kernel_4999, (const void *)mt_generate_kernel_4999, (const void *)mt_load_kernel_4999,
-     (const void *)mt_follow_kernel_4999},
+    {509, (const void *)mt_replay_kernel_509, (const void *)mt_generate_kernel_509, (const void *)mt_load_kernel_509,
+     (const void *)mt_follow_kernel_509},
+    {563, (const void *)mt_replay_kernel_563, (const void *)mt_generate_kernel_563, (const void *)mt_load_kernel_563,
+     (const void *)mt_follow_kernel_563},
+    {672, (const void *)mt_replay_kernel_672, (const void *)mt_generate_kernel_672, (const void *)mt_load_kernel_672,
+     (const void *)mt_follow_kernel_672},
+    {779, (const void *)mt_replay_kernel_779, (const void *)mt_generate_kernel_779, (const void *)mt_load_kernel_779,
+     (const void *)mt_follow_kernel_779},
+    {888, (const void *)mt_replay_kernel_888, (const void *)mt_generate_kernel_888, (const void *)mt_load_kernel_888,
+     (const void *)mt_follow_kernel_888},
+    {1048, (const void *)mt_replay_kernel_1048, (const void *)mt_generate_kernel_1048, (const void *)mt_load_kernel_1048,
+     (const void *)mt_follow_kernel_1048},
+    {1264, (const void *)mt_replay_kernel_1264, (const void *)mt_generate_kernel_1264, (const void *)mt_load_kernel_1264,
+     (const void *)mt_follow_kernel_1264},
+    {1644, (const void *)mt_replay_kernel_1644, (const void *)mt_generate_kernel_1644, (const void *)mt_load_kernel_1644,
+     (const void *)mt_follow_kernel_1644},
+    {2184, (const void *)mt_replay_kernel_2184, (const void *)mt_generate_kernel_2184, (const void *)mt_load_kernel_2184,
+     (const void *)mt_follow_kernel_2184},
+    {3373, (const void *)mt_replay_kernel_3373, (const void *)mt_generate_kernel_3373, (const void *)mt_load_kernel_3373,
+     (const void *)mt_follow_kernel_3373},
+    {6806, (const void *)mt_replay_kernel_6806, (const void *)mt_generate_kernel_6806, (const void *)mt_load_kernel_6806,
+     (const void *)mt_follow_kernel_6806},
     {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000,
      (const void *)mt_follow_kernel_60000},
 };
@@ -494,7 +494,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
     if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
     if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
     if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
-    // the whole class ladder (280 -> 368 -> 456 -> 628 -> ... -> HBM class) by default; < 0: checkpoint,
+    // the whole class ladder (349 -> 456 -> 563 -> 779 -> ... -> HBM class) by default; < 0: checkpoint,
     // but stop after the first launch
     if (b->opt.max_retries == 0) b->opt.max_retries = 2 * mt::kNumClasses;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -563,7 +563,7 @@ MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_k
 }
 
 MT_API int mt_batch_set_clients(mt_batch *b, int64_t doc, const char *const *names, int32_t n) {
-    if (!b || n < 1 || n > 64 || doc >= b->n_docs) return MT_ERR_ARG;
+    if (!b || n < 1 || n > MT_MAX_CLIENTS || doc >= b->n_docs) return MT_ERR_ARG;
     std::vector<std::string> v(names, names + n);
     if (doc < 0) {
         b->clients = v;
@@ -744,14 +744,14 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
 
 // capacity class index: derived from ops per document unless seg_cap is given; `level`
 // escalates by whole classes.  Replay starts a document in at most the 16-documents-per-CU class
-// (280 slots): the replay kernel is latency bound, so a launch's rate grows with the documents
+// (kReplayStartClass): the replay kernel is latency bound, so a launch's rate grows with the documents
 // resident per CU (config 3, 65,536 docs: 203k ops/ms at 8 per CU, 113k at 5, 65k at 3), and a
 // document escalates by checkpoint (an image round trip to HBM, ~1 ms per class for 65,536 docs)
 // only when it needs the room.  The generator re-runs a document from scratch on overflow, so it
 // starts in the class of the expected final size (`replay` false).
 static int class_for(const mt_batch *b, int32_t ops_per_doc, int level, bool replay = true) {
     int32_t want = b->opt.seg_cap > 0 ? b->opt.seg_cap : ops_per_doc / 12 + 64;
-    if (replay && b->opt.seg_cap <= 0) want = std::min<int32_t>(want, 280);
+    if (replay && b->opt.seg_cap <= 0) want = std::min<int32_t>(want, mt::kClassSegs[mt::kReplayStartClass]);
     int c = 0;
     while (c + 1 < mt::kNumClasses && mt::kClassSegs[c] < want) c++;
     c += level;
@@ -817,7 +817,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     L.lds = class_lds(L.cls);
     HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
     HIPCHK(dalloc(&L.d_docout, (size_t)n));
-    HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg));
+    HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg * mt::kColdPerSlot));
     if (class_state_bytes(L.cls)) HIPCHK(dalloc(&L.d_state, (size_t)n * class_state_bytes(L.cls)));
     if (!L.docs.empty()) {
         HIPCHK(dalloc(&L.d_list, L.docs.size()));
@@ -907,7 +907,7 @@ static int prep_follow(Launch &L, hipStream_t s) {
     HIPCHK(dalloc(&L.f_out, n * (size_t)c.oe));
     HIPCHK(dalloc(&L.f_docout, n));
     HIPCHK(hipMemsetAsync(L.f_docout, 0xFF, sizeof(DocOut) * n, s));  // status -1: not replayed
-    HIPCHK(dalloc(&L.f_cold, n * (size_t)c.seg));
+    HIPCHK(dalloc(&L.f_cold, n * (size_t)c.seg * mt::kColdPerSlot));
     if (class_usable(cls + 1)) HIPCHK(dalloc(&L.f_ck, n * (size_t)mt::ck_words(c.seg)));
     return MT_OK;
 }
@@ -1568,6 +1568,21 @@ static bool props_match_host(mt_batch *b, uint32_t a, uint32_t c, bool *undecide
     return true;
 }
 
+// removedClientOverlap of a record of the cached document: a mask of clients < 31, or a pool list
+static std::vector<uint32_t> ovl_clients(const mt_batch *b, uint32_t ovl) {
+    std::vector<uint32_t> out;
+    if (!(ovl & mt::kOvlList)) {
+        for (uint32_t c = 0; c < mt::kOvlMaskClients; c++)
+            if (ovl & (1u << c)) out.push_back(c);
+        return out;
+    }
+    const uint32_t o = ovl & ~mt::kOvlList;
+    if (o >= b->c_pool.size()) return out;
+    const uint32_t n = b->c_pool[o] & ~mt::kPoolOvlTag;
+    for (uint32_t i = 0; i < n && o + 2 + i < b->c_pool.size(); i++) out.push_back(b->c_pool[o + 2 + i]);
+    return out;
+}
+
 static int out_str(const std::string &s, char *buf, int64_t cap, int64_t *len) {
     if (len) *len = (int64_t)s.size();
     if (buf && cap > 0) {
@@ -1706,11 +1721,11 @@ MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs) {
                      r.toff, r.props, j);
             if (r.seq > min_seq) {
                 j += ",\"seq\":" + std::to_string(r.seq) + ",\"client\":";
-                json_quote8(j, client_name(b, doc, r.meta & 63u, tmp));
+                json_quote8(j, client_name(b, doc, mt::meta_cli(r.meta), tmp));
             }
             if (removed) {
                 j += ",\"removedSeq\":" + std::to_string(r.rseq) + ",\"removedClient\":";
-                json_quote8(j, client_name(b, doc, (r.meta >> 6) & 63u, tmp));
+                json_quote8(j, client_name(b, doc, mt::meta_rcli(r.meta), tmp));
             }
             j.push_back('}');
             segs.push_back(j);
@@ -2056,14 +2071,13 @@ MT_API int mt_doc_digest(mt_batch *b, int64_t doc, uint64_t *out) {
             const OutRec &r = b->c_recs[k];
             bool text = rec_is_text(r), removed = rec_removed(r);
             uint64_t ovl = 0;
-            for (uint32_t c = 0; c < 32; c++)
-                if (r.ovl & (1u << c)) ovl += fnv_name(client_name(b, doc, c, tmp));
+            for (uint32_t c : ovl_clients(b, r.ovl)) ovl += fnv_name(client_name(b, doc, c, tmp));
             f.u32(text ? 0u : 1u);
             f.u32(r.len);
             f.u32((uint32_t)r.seq);
-            f.u64(fnv_name(client_name(b, doc, r.meta & 63u, tmp)));
+            f.u64(fnv_name(client_name(b, doc, mt::meta_cli(r.meta), tmp)));
             f.u32(removed ? (uint32_t)r.rseq : 0xFFFFFFFFu);
-            f.u64(removed ? fnv_name(client_name(b, doc, (r.meta >> 6) & 63u, tmp)) : 0ull);
+            f.u64(removed ? fnv_name(client_name(b, doc, mt::meta_rcli(r.meta), tmp)) : 0ull);
             f.u64(ovl);
             if (!r.props) {
                 f.u32(0xFFFFFFFFu);
@@ -2108,9 +2122,9 @@ MT_API int mt_doc_dump(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t
             continue;
         }
         o += "  S blk=" + std::to_string(r.blk >> 16) + " len=" + std::to_string(r.len) + " seq=" + std::to_string(r.seq) +
-             " cli=" + client_name(b, doc, r.meta & 63u, tmp) +
+             " cli=" + client_name(b, doc, mt::meta_cli(r.meta), tmp) +
              " rseq=" + std::to_string(rec_removed(r) ? r.rseq : -1) + " rcli=" +
-             (rec_removed(r) ? client_name(b, doc, (r.meta >> 6) & 63u, tmp) : std::string("-")) +
+             (rec_removed(r) ? client_name(b, doc, mt::meta_rcli(r.meta), tmp) : std::string("-")) +
              " ovl=" + std::to_string(r.ovl) + " '";
         if (rec_is_text(r)) utf16_to_utf8(o, b->c_text.data() + r.toff, r.len);
         o += "'";
@@ -2324,7 +2338,7 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
             L.lds = class_lds(cls);
             HIPCHK(dalloc(&L.d_out, n * (size_t)L.out_cap));
             HIPCHK(dalloc(&L.d_docout, n));
-            HIPCHK(dalloc(&L.d_cold, n * (size_t)L.caps.seg));
+            HIPCHK(dalloc(&L.d_cold, n * (size_t)L.caps.seg * mt::kColdPerSlot));
             if (class_state_bytes(cls)) HIPCHK(dalloc(&L.d_state, n * class_state_bytes(cls)));
             if (!all) {
                 HIPCHK(dalloc(&L.d_list, n));

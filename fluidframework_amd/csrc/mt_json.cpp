@@ -583,11 +583,11 @@ struct Packer1 {
         }
         return true;
     }
-    // getOrAddShortClientId (client.ts:636-641); -1 past 64 clients
+    // getOrAddShortClientId (client.ts:636-641); -1 past MT_MAX_CLIENTS clients
     int client_id(const std::u16string &name) {
         auto it = L.shortid.find(name);
         if (it != L.shortid.end()) return it->second;
-        if (L.names.size() >= 62) return -1;  // 62, 63 are MT_CLIENT_NONCOLLAB / MT_CLIENT_NONE
+        if (L.names.size() >= MT_MAX_CLIENTS) return -1;  // 254, 255 are MT_CLIENT_NONCOLLAB / MT_CLIENT_NONE
         const uint8_t c = (uint8_t)L.names.size();
         L.shortid.emplace(name, c);
         L.names.push_back(name);
@@ -610,7 +610,7 @@ struct Packer1 {
             if (cl >= 0) {
                 if (D.nodes[cl].type != J_STR) return fail(MT_BAD_INPUT, "client is not a string");
                 const int c = client_id(D.str_of(cl));
-                if (c < 0) return fail(MT_UNSUPPORTED, "more than 62 clients");
+                if (c < 0) return fail(MT_UNSUPPORTED, "more than 253 clients");
                 r.client = (uint8_t)c;
             }
             if (sq >= 0) r.seq = as_int(D.nodes[sq]);
@@ -618,7 +618,7 @@ struct Packer1 {
             if (rc >= 0) {
                 if (D.nodes[rc].type != J_STR) return fail(MT_BAD_INPUT, "removedClient is not a string");
                 const int c = client_id(D.str_of(rc));
-                if (c < 0) return fail(MT_UNSUPPORTED, "more than 62 clients");
+                if (c < 0) return fail(MT_UNSUPPORTED, "more than 253 clients");
                 r.msn = c;
             }
         }
@@ -747,7 +747,7 @@ struct Packer1 {
             const int32_t cid = D.member(m, "clientId");
             std::u16string name = cid >= 0 && D.nodes[cid].type == J_STR ? D.str_of(cid) : u"null";
             const int ci = client_id(name);
-            if (ci < 0) return fail(MT_UNSUPPORTED, "more than 62 clients");
+            if (ci < 0) return fail(MT_UNSUPPORTED, "more than 253 clients");
             const uint8_t c = (uint8_t)ci;
             mt_op base{};
             base.client = c;

@@ -470,13 +470,13 @@ struct Doc {
             W.lit(",\"seq\":");
             W.num(r.seq);
             W.lit(",\"client\":");
-            client(r.meta & 63u);
+            client(meta_cli(r.meta));
         }
         if (r.rseq != kNoneSeq) {
             W.lit(",\"removedSeq\":");
             W.num(r.rseq);
             W.lit(",\"removedClient\":");
-            client((r.meta >> 6) & 63u);
+            client(meta_rcli(r.meta));
         }
         W.byte('}');
         end_seg(r.len);

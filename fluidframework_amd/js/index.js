@@ -136,6 +136,8 @@ class Packer {
             if (typeof msg === 'string') msg = JSON.parse(msg);
             let c = short.get(msg.clientId);
             if (c === undefined) {
+                // short ids 0..253 (include/mt_oplog.h MT_MAX_CLIENTS; 254 / 255 are sentinels)
+                if (names.length >= 254) throw new UnsupportedOp('more than 253 clients (short ids are 8-bit)');
                 c = names.length;
                 short.set(msg.clientId, c);
                 names.push(msg.clientId);

@@ -36,6 +36,9 @@ OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
 MAX_INSERT_PROPS = 1023
 
 
+MAX_CLIENTS = 254  # short ids 0..253 (include/mt_oplog.h MT_MAX_CLIENTS; 254 / 255 are sentinels)
+
+
 class UnsupportedOp(ValueError):
     """An op shape outside the observer replay path (relative positions, registers,
     combining ops other than "rewrite")."""
@@ -188,6 +191,8 @@ class Packer:
             if cid is None:  # system messages: one short id for all of them (mt_json.cpp does the same)
                 cid = "null"
             if cid not in short:  # getOrAddShortClientId (client.ts:636-641)
+                if len(names) >= MAX_CLIENTS:
+                    raise UnsupportedOp(f"more than {MAX_CLIENTS - 1} clients (short ids are 8-bit)")
                 short[cid] = len(names)
                 names.append(cid)
             c = short[cid]

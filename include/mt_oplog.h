@@ -48,8 +48,9 @@ enum mt_op_type {
     MT_OP_COLLAB = 5,
     MT_OP_NOOP = 15     /* non-"op" message: only client registration + updateSeqNumbers */
 };
-#define MT_CLIENT_NONCOLLAB 62u /* NonCollabClient (constants.ts:15); long id "original" */
-#define MT_CLIENT_NONE 63u
+#define MT_CLIENT_NONCOLLAB 254u /* NonCollabClient (constants.ts:15); long id "original" */
+#define MT_CLIENT_NONE 255u
+#define MT_MAX_CLIENTS 254      /* short ids 0 .. 253 per document (0 = the observer)          */
 #define MT_SEQ_NONE 0x7FFFFFFF
 #define MT_OP_IS_INSERT_LIKE(t) ((t) == MT_OP_INSERT || (t) == MT_OP_LOAD_HEADER || (t) == MT_OP_LOAD_BODY)
 
@@ -72,7 +73,7 @@ enum mt_op_flags {
 
 typedef struct mt_op {
     uint8_t type;         /* enum mt_op_type                                             */
-    uint8_t client;       /* short client id (index in the doc's client table, 1..63; 0 is
+    uint8_t client;       /* short client id (index in the doc's client table, 1..253; 0 is
                              the observer itself, as Client.startOrUpdateCollaboration
                              assigns it first: client.ts:1051-1062)                       */
     uint16_t flags;       /* enum mt_op_flags | nprops<<4                                  */
