@@ -112,7 +112,9 @@ struct DocOut {
     int32_t fail_op;    // index of the op that failed (-1)
     int32_t cap_kind;   // ST_CAPACITY cause: 1 LDS tables, 2 text arena, 3 prop pool, 4 out records,
                         // 5 collab window wider than kSeq16Span ops (16-bit relative seqs),
-                        // 6 LDS headroom: state checkpointed before op ops_done (resumable)
+                        // 6 LDS headroom: state checkpointed before op ops_done (resumable),
+                        // 8 a segment longer than an LDS class's 16-bit lengths: re-run from
+                        //   scratch in the HBM class
     int32_t gen_text;   // generator: payload code units written
     int32_t gen_props;  // generator: prop records written
 };
@@ -137,14 +139,15 @@ struct Caps {
 // the replay kernel's 128 VGPRs cap a CU at 16 workgroups, so each class is the largest slot
 // count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3
 // and 2 documents per CU (tools/class_sizes.cpp); 128 keeps small documents' buffers small and
-// 6,806 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
+// 7,436 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
 // The replay kernel is latency bound, so a launch's rate grows with the documents per CU.
-constexpr int kClassSegs[] = {128, 349, 403, 456, 509, 563, 672, 779, 888, 1048, 1264, 1644, 2184, 3373, 6806, 60000};
+constexpr int kClassSegs[] = {128, 380, 440, 496, 559, 616, 736, 852, 969, 1149, 1384, 1795, 2384, 3683, 7436, 60000};
 constexpr int kNumClasses = 16;
 constexpr int kHbmClass = kNumClasses - 1;
 constexpr int kHbmSeg = 60000;
 constexpr int kReplayStartClass = 1;  // replay starts documents in at most the 16-per-CU class
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
+constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS class (16-bit lengths)
 constexpr int kCapQueued = 7;      // checkpointed and taken by the launch's follow-on workers
 
 // follow-on queue (one per producer launch, hipMalloc'd, zeroed): word 0 = documents enqueued,
@@ -167,11 +170,14 @@ struct Layout {
     uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, bytes;
 };
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
+// segment lengths are 16-bit in the LDS classes (a longer segment moves the document to the HBM
+// class, cap_kind 8), 32-bit in the HBM class
+constexpr uint32_t len_bytes(int seg) { return seg == 60000 ? 4u : 2u; }
 constexpr Layout make_layout(int seg) {
     const Caps c = class_caps(seg);
     Layout L{};
     uint32_t o = 0;
-    L.len = o;     o = lds_align(o + 4u * c.seg);
+    L.len = o;     o = lds_align(o + len_bytes(seg) * c.seg);
     L.sr = o;      o = lds_align(o + 4u * c.seg);
     L.meta = o;    o = lds_align(o + 4u * c.seg);
     L.sblk = o;    o = lds_align(o + 2u * c.seg);

@@ -37,6 +37,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/mt_gen.h"
 #include "../../include/mt_oplog.h"
 #include "mt_device.h"
@@ -127,8 +129,11 @@ template <int SEG>
 struct Engine {
     static constexpr Caps cap = class_caps(SEG);
     static constexpr Layout lay = make_layout(SEG);
+    using Len = std::conditional_t<len_bytes(SEG) == 2u, uint16_t, uint32_t>;
+    static constexpr uint32_t kMaxLen = len_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
     // ---- LDS state
-    uint32_t *s_len, *s_meta;
+    Len *s_len;
+    uint32_t *s_meta;
     uint32_t *s_sr;  // seq16 | rseq16 << 16 (window-relative); of a free slot: the next free slot
     uint16_t *s_blk;
     uint16_t *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
@@ -176,7 +181,7 @@ struct Engine {
 
     // ------------------------------------------------------------------ layout
     MT_FI void carve(uint8_t *tb) {
-        s_len = (uint32_t *)(tb + lay.len);
+        s_len = (Len *)(tb + lay.len);
         s_sr = (uint32_t *)(tb + lay.sr);
         s_meta = (uint32_t *)(tb + lay.meta);
         s_blk = (uint16_t *)(tb + lay.sblk);
@@ -804,10 +809,10 @@ struct Engine {
             pv1 = pv;
         }
         pend_n++;
-        s_len[ns] = len - r;
+        s_len[ns] = (Len)(len - r);
         s_sr[ns] = s_sr[slot];
         s_meta[ns] = meta;  // inherits ends-NL of the tail, linked, unsettled
-        s_len[slot] = r;
+        s_len[slot] = (Len)r;
         wsync();
         if (meta & kMetaUnsettled) u_push((uint32_t)ns);
         const int32_t nb = insert_leaf(blk, k + 1, (uint32_t)ns);
@@ -1238,6 +1243,10 @@ struct Engine {
                     stcap = fc.w;
                 }
                 const uint32_t need = pl + sl;
+                if (need > kMaxLen) {  // beyond 16-bit lengths: the document continues in the HBM class
+                    cap_fail(kCapLongSeg);
+                    return 0;
+                }
                 if (pcap == pl && ptoff + pl == stoff) {
                     // texts already adjacent (split halves, consecutive payloads): take over the region
                     pcap = pl + stcap;
@@ -1252,7 +1261,7 @@ struct Engine {
                 } else {
                     // reallocate; a compaction inside arena_alloc moves every text, so the head
                     // is written back first and both offsets re-read afterwards
-                    s_len[hslot] = pl;
+                    s_len[hslot] = (Len)pl;
                     if (lane == 0) cold[2 * hslot] = make_uint4(hprops, hov, ptoff, pcap);
                     wsync();
                     const uint32_t ncap = 2u * need;
@@ -1271,7 +1280,7 @@ struct Engine {
                 pl = need;
                 const uint32_t fm = rdl(meta, k);
                 hmeta = (hmeta & ~kMetaEndsNL) | (fm & (kMetaEndsNL | kMetaHasNL));
-                s_len[hslot] = pl;
+                s_len[hslot] = (Len)pl;
                 if (lane == 0) cold[2 * hslot] = make_uint4(hprops, hov, ptoff, pcap);
                 s_meta[hslot] = hmeta;
                 wsync();
@@ -1483,6 +1492,10 @@ struct Engine {
                 set_fail(ST_INVALID_POS);
                 return;
             }
+            if (len > kMaxLen) {
+                cap_fail(kCapLongSeg);
+                return;
+            }
             int32_t slot = alloc_slot();
             if (slot < 0) return;
             uint32_t props = 0, ph = 0;
@@ -1502,7 +1515,7 @@ struct Engine {
             if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
             if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
             if (props) meta |= kMetaHasProps;
-            s_len[slot] = len;
+            s_len[slot] = (Len)len;
             s_sr[slot] = settled ? (rseq == kNoneSeq ? kSeq16None : 0u) << 16
                                  : rel16(op.seq) | ((rseq == kNoneSeq ? kSeq16None : rel16(rseq)) << 16);
             if (lane == 0) {
@@ -1536,6 +1549,10 @@ struct Engine {
         ov_splits = -1;
         const bool marker = (op.flags & MT_OPF_MARKER) != 0;
         const uint32_t len = marker ? 1u : op.payload_len;
+        if (len > kMaxLen) {
+            cap_fail(kCapLongSeg);
+            return;
+        }
         int32_t slot = alloc_slot();
         if (slot < 0) return;
         uint32_t props = 0, ph = 0;
@@ -1552,7 +1569,7 @@ struct Engine {
         if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
         if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
         if (props) meta |= kMetaHasProps;
-        s_len[slot] = len;
+        s_len[slot] = (Len)len;
         s_sr[slot] = 0u;  // set by op_collab from the real seqs in the cold record
         if (lane == 0) {
             cold[2 * slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
@@ -2076,7 +2093,7 @@ struct Engine {
         int32_t w = 0;
         int32_t blk = root;
         // a document that ran out of LDS capacity is re-run or resumed: no records
-        if (status == ST_CAPACITY && (cap_kind == 1 || cap_kind == kCapCheckpoint)) blk = -1;
+        if (status == ST_CAPACITY && (cap_kind == 1 || cap_kind == kCapCheckpoint || cap_kind == kCapLongSeg)) blk = -1;
         else
             while (!b_leaf[blk]) blk = b_child[blk * 8];
         while (blk >= 0) {

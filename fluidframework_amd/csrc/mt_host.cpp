@@ -33,20 +33,20 @@
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);    \
     extern "C" __global__ void mt_follow_kernel_##S(mt::ReplayParams P);
 MT_DECLARE_CLASS(128)
-MT_DECLARE_CLASS(349)
-MT_DECLARE_CLASS(403)
-MT_DECLARE_CLASS(456)
-MT_DECLARE_CLASS(509)
-MT_DECLARE_CLASS(563)
-MT_DECLARE_CLASS(672)
-MT_DECLARE_CLASS(779)
-MT_DECLARE_CLASS(888)
-MT_DECLARE_CLASS(1048)
-MT_DECLARE_CLASS(1264)
-MT_DECLARE_CLASS(1644)
-MT_DECLARE_CLASS(2184)
-MT_DECLARE_CLASS(3373)
-MT_DECLARE_CLASS(6806)
+MT_DECLARE_CLASS(380)
+MT_DECLARE_CLASS(440)
+MT_DECLARE_CLASS(496)
+MT_DECLARE_CLASS(559)
+MT_DECLARE_CLASS(616)
+MT_DECLARE_CLASS(736)
+MT_DECLARE_CLASS(852)
+MT_DECLARE_CLASS(969)
+MT_DECLARE_CLASS(1149)
+MT_DECLARE_CLASS(1384)
+MT_DECLARE_CLASS(1795)
+MT_DECLARE_CLASS(2384)
+MT_DECLARE_CLASS(3683)
+MT_DECLARE_CLASS(7436)
 MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
@@ -86,34 +86,34 @@ struct KernelClass {
 static const KernelClass kKernels[mt::kNumClasses] = {
     {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
      (const void *)mt_follow_kernel_128},
-    {349, (const void *)mt_replay_kernel_349, (const void *)mt_generate_kernel_349, (const void *)mt_load_kernel_349,
-     (const void *)mt_follow_kernel_349},
-    {403, (const void *)mt_replay_kernel_403, (const void *)mt_generate_kernel_403, (const void *)mt_load_kernel_403,
-     (const void *)mt_follow_kernel_403},
-    {456, (const void *)mt_replay_kernel_456, (const void *)mt_generate_kernel_456, (const void *)mt_load_kernel_456,
-     (const void *)mt_follow_kernel_456},
-    {509, (const void *)mt_replay_kernel_509, (const void *)mt_generate_kernel_509, (const void *)mt_load_kernel_509,
-     (const void *)mt_follow_kernel_509},
-    {563, (const void *)mt_replay_kernel_563, (const void *)mt_generate_kernel_563, (const void *)mt_load_kernel_563,
-     (const void *)mt_follow_kernel_563},
-    {672, (const void *)mt_replay_kernel_672, (const void *)mt_generate_kernel_672, (const void *)mt_load_kernel_672,
-     (const void *)mt_follow_kernel_672},
-    {779, (const void *)mt_replay_kernel_779, (const void *)mt_generate_kernel_779, (const void *)mt_load_kernel_779,
-     (const void *)mt_follow_kernel_779},
-    {888, (const void *)mt_replay_kernel_888, (const void *)mt_generate_kernel_888, (const void *)mt_load_kernel_888,
-     (const void *)mt_follow_kernel_888},
-    {1048, (const void *)mt_replay_kernel_1048, (const void *)mt_generate_kernel_1048, (const void *)mt_load_kernel_1048,
-     (const void *)mt_follow_kernel_1048},
-    {1264, (const void *)mt_replay_kernel_1264, (const void *)mt_generate_kernel_1264, (const void *)mt_load_kernel_1264,
-     (const void *)mt_follow_kernel_1264},
-    {1644, (const void *)mt_replay_kernel_1644, (const void *)mt_generate_kernel_1644, (const void *)mt_load_kernel_1644,
-     (const void *)mt_follow_kernel_1644},
-    {2184, (const void *)mt_replay_kernel_2184, (const void *)mt_generate_kernel_2184, (const void *)mt_load_kernel_2184,
-     (const void *)mt_follow_kernel_2184},
-    {3373, (const void *)mt_replay_kernel_3373, (const void *)mt_generate_kernel_3373, (const void *)mt_load_kernel_3373,
-     (const void *)mt_follow_kernel_3373},
-    {6806, (const void *)mt_replay_kernel_6806, (const void *)mt_generate_kernel_6806, (const void *)mt_load_kernel_6806,
-     (const void *)mt_follow_kernel_6806},
+    {380, (const void *)mt_replay_kernel_380, (const void *)mt_generate_kernel_380, (const void *)mt_load_kernel_380,
+     (const void *)mt_follow_kernel_380},
+    {440, (const void *)mt_replay_kernel_440, (const void *)mt_generate_kernel_440, (const void *)mt_load_kernel_440,
+     (const void *)mt_follow_kernel_440},
+    {496, (const void *)mt_replay_kernel_496, (const void *)mt_generate_kernel_496, (const void *)mt_load_kernel_496,
+     (const void *)mt_follow_kernel_496},
+    {559, (const void *)mt_replay_kernel_559, (const void *)mt_generate_kernel_559, (const void *)mt_load_kernel_559,
+     (const void *)mt_follow_kernel_559},
+    {616, (const void *)mt_replay_kernel_616, (const void *)mt_generate_kernel_616, (const void *)mt_load_kernel_616,
+     (const void *)mt_follow_kernel_616},
+    {736, (const void *)mt_replay_kernel_736, (const void *)mt_generate_kernel_736, (const void *)mt_load_kernel_736,
+     (const void *)mt_follow_kernel_736},
+    {852, (const void *)mt_replay_kernel_852, (const void *)mt_generate_kernel_852, (const void *)mt_load_kernel_852,
+     (const void *)mt_follow_kernel_852},
+    {969, (const void *)mt_replay_kernel_969, (const void *)mt_generate_kernel_969, (const void *)mt_load_kernel_969,
+     (const void *)mt_follow_kernel_969},
+    {1149, (const void *)mt_replay_kernel_1149, (const void *)mt_generate_kernel_1149, (const void *)mt_load_kernel_1149,
+     (const void *)mt_follow_kernel_1149},
+    {1384, (const void *)mt_replay_kernel_1384, (const void *)mt_generate_kernel_1384, (const void *)mt_load_kernel_1384,
+     (const void *)mt_follow_kernel_1384},
+    {1795, (const void *)mt_replay_kernel_1795, (const void *)mt_generate_kernel_1795, (const void *)mt_load_kernel_1795,
+     (const void *)mt_follow_kernel_1795},
+    {2384, (const void *)mt_replay_kernel_2384, (const void *)mt_generate_kernel_2384, (const void *)mt_load_kernel_2384,
+     (const void *)mt_follow_kernel_2384},
+    {3683, (const void *)mt_replay_kernel_3683, (const void *)mt_generate_kernel_3683, (const void *)mt_load_kernel_3683,
+     (const void *)mt_follow_kernel_3683},
+    {7436, (const void *)mt_replay_kernel_7436, (const void *)mt_generate_kernel_7436, (const void *)mt_load_kernel_7436,
+     (const void *)mt_follow_kernel_7436},
     {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000,
      (const void *)mt_follow_kernel_60000},
 };
@@ -494,7 +494,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
     if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
     if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
     if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
-    // the whole class ladder (349 -> 456 -> 563 -> 779 -> ... -> HBM class) by default; < 0: checkpoint,
+    // the whole class ladder (380 -> 496 -> 616 -> 852 -> ... -> HBM class) by default; < 0: checkpoint,
     // but stop after the first launch
     if (b->opt.max_retries == 0) b->opt.max_retries = 2 * mt::kNumClasses;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1100,11 +1100,12 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
                 for (size_t i = 0; i < S.docs.size(); i++) {
                     const int32_t d = S.docs[i];
                     const DocOut &o = b->docout[(size_t)d];
-                    const int nxt = std::min(resume_class(cls), mt::kNumClasses - 1);
+                    const bool long_seg = o.status == MT_CAPACITY && o.cap_kind == mt::kCapLongSeg;
+                    const int nxt = long_seg ? mt::kHbmClass : std::min(resume_class(cls), mt::kNumClasses - 1);
                     if (o.status == MT_CAPACITY && o.cap_kind == mt::kCapCheckpoint && o.ops_done >= b->h_nload[d]) {
                         resume_li[(size_t)d] = li;  // loaded: the replay resumes from this checkpoint
                         resume_idx[(size_t)d] = (int32_t)i;
-                    } else if (o.status == MT_CAPACITY && (o.cap_kind == mt::kCapCheckpoint || o.cap_kind == 1) &&
+                    } else if (o.status == MT_CAPACITY && (o.cap_kind == mt::kCapCheckpoint || o.cap_kind == 1 || long_seg) &&
                                class_usable(nxt) && nxt > cls) {
                         // short of room while loading: resume (checkpoint) or load again (overflow)
                         auto &w = work[nxt];
@@ -1328,10 +1329,12 @@ MT_API int mt_batch_sync(mt_batch *b) {
             if (o.status != MT_CAPACITY || b->where[d].launch != li) continue;
             int32_t src;
             if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) src = (int32_t)i;
-            else if (o.cap_kind == 1 || o.cap_kind == 4) src = -1;
+            else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg) src = -1;
             else continue;
             int cls = resume_class(S.cls);
             while (cls > S.cls + 1 && !class_usable(cls)) cls--;
+            // a segment beyond 16-bit lengths: re-run from scratch in the HBM class (32-bit lengths)
+            if (o.cap_kind == mt::kCapLongSeg) cls = S.cls == mt::kHbmClass ? mt::kNumClasses : mt::kHbmClass;
             if (!class_usable(cls)) continue;  // largest class reached: the document keeps MT_CAPACITY
             Launch &L = groups[cls];
             L.cls = cls;
@@ -2376,6 +2379,8 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
                 outs[(size_t)d] = part[i];
                 if (part[i].status == MT_CAPACITY && part[i].cap_kind == 1 && class_usable(cls + 1))
                     work[cls + 1].push_back(d);
+                else if (part[i].status == MT_CAPACITY && part[i].cap_kind == mt::kCapLongSeg && cls != mt::kHbmClass)
+                    work[mt::kHbmClass].push_back(d);
             }
             at += n;
         }

@@ -383,8 +383,8 @@ def test_native_json_ingest_replays_like_the_packer():
 
 def test_config3_documents_at_full_size():
     """The north-star workload's documents at their own size: config-3 mix (55/35/10), 10k ops,
-    no seg_cap forcing, so documents run the natural capacity chain (class 349 -> 456 -> ... ->
-    1,644 -> 2,184) through checkpoint / resume.  Every digest equals the oracle's; every 8th
+    no seg_cap forcing, so documents run the natural capacity chain (class 380 -> 496 -> ... ->
+    1,384 -> 1,795) through checkpoint / resume.  Every digest equals the oracle's; every 8th
     document also text, property runs and SnapshotV1 (host and GPU serializers)."""
     n = 32
     p = O.gen_params(10000, pct_insert=55, pct_remove=35, seed=0xDEADBEEF)
@@ -398,7 +398,7 @@ def test_config3_documents_at_full_size():
         b.run()
         launches = b.launches()
         assert len({li["seg_class"] for li in launches}) >= 3, launches  # the escalation chain ran
-        assert int(b.counters()["max_slots"].max()) > 1264
+        assert int(b.counters()["max_slots"].max()) > 1384
         for d in range(n):
             assert b.doc(d).status == st[d] == 0
             assert b.doc(d).digest() == int(dig[d]), f"doc {d} digest differs"
@@ -474,3 +474,26 @@ def test_terminal_capacity_digests_are_defined():
             assert (b.device_digests() == got[-1]).all()
     assert (got[0] == got[1]).all()
     assert len(set(got[0].tolist())) == 8
+
+
+def test_segments_beyond_16_bit_lengths_move_to_the_hbm_class():
+    """LDS classes keep segment lengths in 16 bits; a longer segment (one large insert, or zamboni
+    appending short inserts to a 65,530-unit run) re-runs the document from scratch in the HBM
+    class with 32-bit lengths, bit-exact with the oracle."""
+    big = "x" * 70000
+    near = "y" * 65530
+    docs = [
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": big}), _msg("B", 2, 1, {"type": 1, "pos1": 10, "pos2": 20}, 1)],
+        _settle([_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": near})] +
+                [_msg("B", k, k - 1, {"type": 0, "pos1": 65530 + 2 * (k - 2), "seg": "ab"}) for k in range(2, 12)], 11),
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "short"})],
+    ]
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        classes = {li["seg_class"] for li in b.launches()}
+        assert 60000 in classes, b.launches()
+        for i in range(len(docs)):
+            assert_doc_parity(b.doc(i), oracle[i])
+        assert len(json.loads(b.doc(1).snapshot_v1()["header"])["segments"]) == 1  # merged past 65,535
