@@ -139,9 +139,9 @@ struct Caps {
 // the replay kernel's 128 VGPRs cap a CU at 16 workgroups, so each class is the largest slot
 // count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3
 // and 2 documents per CU (tools/class_sizes.cpp); 128 keeps small documents' buffers small and
-// 7,436 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
+// 7,432 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
 // The replay kernel is latency bound, so a launch's rate grows with the documents per CU.
-constexpr int kClassSegs[] = {128, 380, 440, 496, 559, 616, 736, 852, 969, 1149, 1384, 1795, 2384, 3683, 7436, 60000};
+constexpr int kClassSegs[] = {128, 376, 433, 496, 552, 613, 728, 848, 964, 1144, 1376, 1789, 2380, 3680, 7432, 60000};
 constexpr int kNumClasses = 16;
 constexpr int kHbmClass = kNumClasses - 1;
 constexpr int kHbmSeg = 60000;
@@ -167,8 +167,9 @@ constexpr Caps class_caps(int seg) {
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
     uint32_t len, sr, meta, sblk, ulist;
-    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, bytes;
+    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, hdr, bytes;
 };
+constexpr int kHdrWords = 24;  // per-document scalars kept in LDS (mt_engine.hip LWord)
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
 // segment lengths are 16-bit in the LDS classes (a longer segment moves the document to the HBM
 // class, cap_kind 8), 32-bit in the HBM class
@@ -191,9 +192,18 @@ constexpr Layout make_layout(int seg) {
     L.bacc = o;    o = lds_align(o + 4u * c.blk);
     L.heap = o;    o = lds_align(o + 8u * (c.heap + 2));
     L.scratch = o; o = lds_align(o + 4u * 128);
+    L.hdr = o;     o = lds_align(o + 4u * kHdrWords);
     L.bytes = o;
     return L;
 }
+
+// matchProperties / rewrite tables of the interned property values (device memory, one per batch)
+struct ValueTables {
+    const uint8_t *flags;  // per value id: bit0 = JS-falsy (rewrite semantics), bit1 irregular, bit2 unknown
+    const uint32_t *cls;   // per value id: structural matchProperties class (mt_values.cpp)
+    const uint64_t *exc;   // sorted (u << 32 | v): values matching across classes
+    uint32_t n_values, n_exc;
+};
 
 // kernel parameters
 struct ReplayParams {
@@ -207,12 +217,7 @@ struct ReplayParams {
     const uint64_t *doc_pool_base;
     const uint32_t *doc_pool_cap;
     const void *props_in;         // mt_prop[] (op prop records, batch-global offsets)
-    const uint8_t *value_flags;   // per value id: bit0 = JS-falsy (rewrite semantics), bit1 irregular,
-                                  // bit2 unknown (mt_values.h)
-    uint32_t n_values;
-    const uint32_t *value_class;  // per value id: structural matchProperties class (mt_values.cpp)
-    const uint64_t *exc;          // sorted (u << 32 | v): values matching across classes
-    uint32_t n_exc;
+    const ValueTables *vt;        // property value tables (device memory)
     OutRec *out;                  // [n_docs * out_cap]
     DocOut *doc_out;
     int64_t n_docs;               // workgroups in this launch

@@ -125,6 +125,23 @@ struct Walk {
     int32_t ok;     // insert mode: the walk found an insertion point
 };
 
+// A per-document scalar kept in LDS instead of a scalar register: the engine's rarely used state
+// (text / pool semispaces, GC counters, high-water marks) would otherwise be live in SGPRs across
+// the whole op loop and spill.  Every lane reads / writes the same word.
+template <typename T>
+struct LWord {
+    T *p;
+    MT_FI operator T() const { return (T)rfl((uint32_t)*p); }
+    MT_FI LWord &operator=(T v) {
+        *p = v;
+        return *this;
+    }
+    // assignment between words copies the value, never the address
+    MT_FI LWord &operator=(const LWord &o) { return *this = T(o); }
+    MT_FI LWord &operator+=(T v) { return *this = (T)(T(*this) + v); }
+    MT_FI LWord &operator++(int) { return *this = (T)(T(*this) + 1); }
+};
+
 template <int SEG>
 struct Engine {
     static constexpr Caps cap = class_caps(SEG);
@@ -149,17 +166,18 @@ struct Engine {
     int32_t splits;                 // leaf/interior block splits so far (overlay staleness)
     int32_t ov_splits, ov_full;     // overlay computed at `ov_splits`; full (refSeq < minSeq) mode
     uint32_t arena_top, pool_top;
-    uint32_t pay_end, arena_base, arena_end, semi_t;  // text: payload | semispace A | semispace B
-    uint32_t pool_base, pool_end, semi_p;             // prop pool: [0] reserved | A | B
-    int32_t pool_gcs, text_gcs;
+    // text: payload | semispace A | semispace B; prop pool: [0] reserved | A | B (LDS words)
+    LWord<uint32_t> pay_end, arena_base, arena_end, semi_t, pool_base, pool_end, semi_p;
+    LWord<int32_t> pool_gcs, text_gcs;
     // Splits of the current op (at most two): the cold records of both halves and the left
     // half's ends-with-'\n' are resolved after the op's LDS work, so the HBM latency of the
     // cold-record and text loads overlaps it.  A pending split's two cold records are held
     // lane-distributed (lane i < 8: word i) in one VGPR, so they cost no scalar registers.
     int32_t pend_n, pend_cold;
-    uint32_t ps0, pn0, pr0, pch0, ps1, pn1, pr1, pch1;
+    LWord<uint32_t> ps0, pn0, pr0, pch0, ps1, pn1, pr1, pch1;
     uint32_t pv0, pv1;
-    int32_t max_heap, max_u, htop;
+    LWord<int32_t> max_heap, max_u;
+    int32_t htop;
     uint2 *h_ent;
     // ---- global
     uint4 *cold;  // cold segment records {props, ovl, toff, tcap}
@@ -168,13 +186,9 @@ struct Engine {
     uint32_t *pool;
     uint32_t pool_cap;
     const mt_prop *props_in;
-    const uint8_t *value_flags;
-    uint32_t n_values;
-    const uint32_t *value_class;
-    const uint64_t *exc;
-    uint32_t n_exc;
+    const ValueTables *vt;  // value flags / classes / exceptions (scalar loads where used)
     int lane;
-    int32_t cap_kind;
+    LWord<int32_t> cap_kind;
 #ifdef MT_PROF
     uint64_t pf[kProfSlots];
 #endif
@@ -195,6 +209,27 @@ struct Engine {
         b_acc = (uint32_t *)(tb + lay.bacc);
         h_ent = (uint2 *)(tb + lay.heap);
         scratch = (uint32_t *)(tb + lay.scratch);
+        uint32_t *hw = (uint32_t *)(tb + lay.hdr);
+        pay_end.p = hw + 0;
+        arena_base.p = hw + 1;
+        arena_end.p = hw + 2;
+        semi_t.p = hw + 3;
+        pool_base.p = hw + 4;
+        pool_end.p = hw + 5;
+        semi_p.p = hw + 6;
+        pool_gcs.p = (int32_t *)hw + 7;
+        text_gcs.p = (int32_t *)hw + 8;
+        max_heap.p = (int32_t *)hw + 9;
+        max_u.p = (int32_t *)hw + 10;
+        cap_kind.p = (int32_t *)hw + 11;
+        ps0.p = hw + 12;
+        pn0.p = hw + 13;
+        pr0.p = hw + 14;
+        pch0.p = hw + 15;
+        ps1.p = hw + 16;
+        pn1.p = hw + 17;
+        pr1.p = hw + 18;
+        pch1.p = hw + 19;
     }
 
     MT_FI void set_fail(int32_t st) {
@@ -991,7 +1026,7 @@ struct Engine {
             int rel = 0;
             for (uint32_t i = 0; i < nb; i++)
                 if (pool[b + 2 + 2 * i] == k)
-                    rel = value_rel(va, pool[b + 3 + 2 * i], value_class, value_flags, n_values, exc, n_exc);
+                    rel = value_rel(va, pool[b + 3 + 2 * i], vt->cls, vt->flags, vt->n_values, vt->exc, vt->n_exc);
             ok = rel == 1;
             unk = rel < 0;
         }
@@ -1028,7 +1063,7 @@ struct Engine {
                 uint32_t k = keys[lane];
                 for (uint32_t i = 0; i < nop; i++) {
                     uint32_t kk = rdl(ok_k, (int)i), vv = rdl(ok_v, (int)i);
-                    if (kk == k && vv < n_values && !(value_flags[vv] & 1u)) keep = true;
+                    if (kk == k && vv < vt->n_values && !(vt->flags[vv] & 1u)) keep = true;
                 }
             }
             uint64_t kb = ballot(keep && (uint32_t)lane < n);
@@ -1096,9 +1131,9 @@ struct Engine {
         bool irr = false;
         if ((uint32_t)lane < n) {
             uint32_t k = keys[lane], v = vals[lane];
-            const bool known = v < n_values;
-            h = hash_pair(k, known ? value_class[v] : 0xFFFFFFFFu - v);
-            irr = !known || (value_flags[v] & (kVIrregular | kVUnknown));
+            const bool known = v < vt->n_values;
+            h = hash_pair(k, known ? vt->cls[v] : 0xFFFFFFFFu - v);
+            irr = !known || (vt->flags[v] & (kVIrregular | kVUnknown));
             pool[id + 2 + 2 * lane] = k;
             pool[id + 3 + 2 * lane] = v;
         }
@@ -2196,11 +2231,7 @@ MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_
     E.pool_gcs = 0;
     E.text_gcs = 0;
     E.props_in = (const mt_prop *)P.props_in;
-    E.value_flags = P.value_flags;
-    E.value_class = P.value_class;
-    E.exc = P.exc;
-    E.n_exc = P.n_exc;
-    E.n_values = P.n_values;
+    E.vt = P.vt;
     E.init();
 }
 

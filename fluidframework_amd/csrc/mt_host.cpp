@@ -33,20 +33,20 @@
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);    \
     extern "C" __global__ void mt_follow_kernel_##S(mt::ReplayParams P);
 MT_DECLARE_CLASS(128)
-MT_DECLARE_CLASS(380)
-MT_DECLARE_CLASS(440)
+MT_DECLARE_CLASS(376)
+MT_DECLARE_CLASS(433)
 MT_DECLARE_CLASS(496)
-MT_DECLARE_CLASS(559)
-MT_DECLARE_CLASS(616)
-MT_DECLARE_CLASS(736)
-MT_DECLARE_CLASS(852)
-MT_DECLARE_CLASS(969)
-MT_DECLARE_CLASS(1149)
-MT_DECLARE_CLASS(1384)
-MT_DECLARE_CLASS(1795)
-MT_DECLARE_CLASS(2384)
-MT_DECLARE_CLASS(3683)
-MT_DECLARE_CLASS(7436)
+MT_DECLARE_CLASS(552)
+MT_DECLARE_CLASS(613)
+MT_DECLARE_CLASS(728)
+MT_DECLARE_CLASS(848)
+MT_DECLARE_CLASS(964)
+MT_DECLARE_CLASS(1144)
+MT_DECLARE_CLASS(1376)
+MT_DECLARE_CLASS(1789)
+MT_DECLARE_CLASS(2380)
+MT_DECLARE_CLASS(3680)
+MT_DECLARE_CLASS(7432)
 MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
@@ -86,34 +86,34 @@ struct KernelClass {
 static const KernelClass kKernels[mt::kNumClasses] = {
     {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
      (const void *)mt_follow_kernel_128},
-    {380, (const void *)mt_replay_kernel_380, (const void *)mt_generate_kernel_380, (const void *)mt_load_kernel_380,
-     (const void *)mt_follow_kernel_380},
-    {440, (const void *)mt_replay_kernel_440, (const void *)mt_generate_kernel_440, (const void *)mt_load_kernel_440,
-     (const void *)mt_follow_kernel_440},
+    {376, (const void *)mt_replay_kernel_376, (const void *)mt_generate_kernel_376, (const void *)mt_load_kernel_376,
+     (const void *)mt_follow_kernel_376},
+    {433, (const void *)mt_replay_kernel_433, (const void *)mt_generate_kernel_433, (const void *)mt_load_kernel_433,
+     (const void *)mt_follow_kernel_433},
     {496, (const void *)mt_replay_kernel_496, (const void *)mt_generate_kernel_496, (const void *)mt_load_kernel_496,
      (const void *)mt_follow_kernel_496},
-    {559, (const void *)mt_replay_kernel_559, (const void *)mt_generate_kernel_559, (const void *)mt_load_kernel_559,
-     (const void *)mt_follow_kernel_559},
-    {616, (const void *)mt_replay_kernel_616, (const void *)mt_generate_kernel_616, (const void *)mt_load_kernel_616,
-     (const void *)mt_follow_kernel_616},
-    {736, (const void *)mt_replay_kernel_736, (const void *)mt_generate_kernel_736, (const void *)mt_load_kernel_736,
-     (const void *)mt_follow_kernel_736},
-    {852, (const void *)mt_replay_kernel_852, (const void *)mt_generate_kernel_852, (const void *)mt_load_kernel_852,
-     (const void *)mt_follow_kernel_852},
-    {969, (const void *)mt_replay_kernel_969, (const void *)mt_generate_kernel_969, (const void *)mt_load_kernel_969,
-     (const void *)mt_follow_kernel_969},
-    {1149, (const void *)mt_replay_kernel_1149, (const void *)mt_generate_kernel_1149, (const void *)mt_load_kernel_1149,
-     (const void *)mt_follow_kernel_1149},
-    {1384, (const void *)mt_replay_kernel_1384, (const void *)mt_generate_kernel_1384, (const void *)mt_load_kernel_1384,
-     (const void *)mt_follow_kernel_1384},
-    {1795, (const void *)mt_replay_kernel_1795, (const void *)mt_generate_kernel_1795, (const void *)mt_load_kernel_1795,
-     (const void *)mt_follow_kernel_1795},
-    {2384, (const void *)mt_replay_kernel_2384, (const void *)mt_generate_kernel_2384, (const void *)mt_load_kernel_2384,
-     (const void *)mt_follow_kernel_2384},
-    {3683, (const void *)mt_replay_kernel_3683, (const void *)mt_generate_kernel_3683, (const void *)mt_load_kernel_3683,
-     (const void *)mt_follow_kernel_3683},
-    {7436, (const void *)mt_replay_kernel_7436, (const void *)mt_generate_kernel_7436, (const void *)mt_load_kernel_7436,
-     (const void *)mt_follow_kernel_7436},
+    {552, (const void *)mt_replay_kernel_552, (const void *)mt_generate_kernel_552, (const void *)mt_load_kernel_552,
+     (const void *)mt_follow_kernel_552},
+    {613, (const void *)mt_replay_kernel_613, (const void *)mt_generate_kernel_613, (const void *)mt_load_kernel_613,
+     (const void *)mt_follow_kernel_613},
+    {728, (const void *)mt_replay_kernel_728, (const void *)mt_generate_kernel_728, (const void *)mt_load_kernel_728,
+     (const void *)mt_follow_kernel_728},
+    {848, (const void *)mt_replay_kernel_848, (const void *)mt_generate_kernel_848, (const void *)mt_load_kernel_848,
+     (const void *)mt_follow_kernel_848},
+    {964, (const void *)mt_replay_kernel_964, (const void *)mt_generate_kernel_964, (const void *)mt_load_kernel_964,
+     (const void *)mt_follow_kernel_964},
+    {1144, (const void *)mt_replay_kernel_1144, (const void *)mt_generate_kernel_1144, (const void *)mt_load_kernel_1144,
+     (const void *)mt_follow_kernel_1144},
+    {1376, (const void *)mt_replay_kernel_1376, (const void *)mt_generate_kernel_1376, (const void *)mt_load_kernel_1376,
+     (const void *)mt_follow_kernel_1376},
+    {1789, (const void *)mt_replay_kernel_1789, (const void *)mt_generate_kernel_1789, (const void *)mt_load_kernel_1789,
+     (const void *)mt_follow_kernel_1789},
+    {2380, (const void *)mt_replay_kernel_2380, (const void *)mt_generate_kernel_2380, (const void *)mt_load_kernel_2380,
+     (const void *)mt_follow_kernel_2380},
+    {3680, (const void *)mt_replay_kernel_3680, (const void *)mt_generate_kernel_3680, (const void *)mt_load_kernel_3680,
+     (const void *)mt_follow_kernel_3680},
+    {7432, (const void *)mt_replay_kernel_7432, (const void *)mt_generate_kernel_7432, (const void *)mt_load_kernel_7432,
+     (const void *)mt_follow_kernel_7432},
     {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000,
      (const void *)mt_follow_kernel_60000},
 };
@@ -366,6 +366,7 @@ struct mt_batch {
     uint8_t *d_vflags = nullptr;
     uint32_t *d_vclass = nullptr;
     uint64_t *d_vexc = nullptr;
+    mt::ValueTables *d_vt = nullptr;  // {d_vflags, d_vclass, d_vexc, counts} for the kernels
     double payload_units = 0, prop_records = 0;
     // launches / results
     std::vector<Launch> launches;
@@ -494,7 +495,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
     if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
     if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
     if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
-    // the whole class ladder (380 -> 496 -> 616 -> 852 -> ... -> HBM class) by default; < 0: checkpoint,
+    // the whole class ladder (376 -> 496 -> 613 -> 848 -> ... -> HBM class) by default; < 0: checkpoint,
     // but stop after the first launch
     if (b->opt.max_retries == 0) b->opt.max_retries = 2 * mt::kNumClasses;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -518,6 +519,7 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     (void)hipFree(b->d_vflags);
     (void)hipFree(b->d_vclass);
     (void)hipFree(b->d_vexc);
+    (void)hipFree(b->d_vt);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
     if (b->ev1) (void)hipEventDestroy(b->ev1);
     for (hipStream_t a : b->aux)
@@ -556,9 +558,11 @@ MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_k
     (void)hipFree(b->d_vflags);
     (void)hipFree(b->d_vclass);
     (void)hipFree(b->d_vexc);
+    (void)hipFree(b->d_vt);
     b->d_vflags = nullptr;
     b->d_vclass = nullptr;
     b->d_vexc = nullptr;
+    b->d_vt = nullptr;
     return ensure_tables(b);
 }
 
@@ -594,6 +598,12 @@ static int ensure_tables(mt_batch *b) {
         HIPCHK(dalloc(&b->d_vexc, b->value_exc.size()));
         if (!b->value_exc.empty())
             HIPCHK(hipMemcpy(b->d_vexc, b->value_exc.data(), 8 * b->value_exc.size(), hipMemcpyHostToDevice));
+    }
+    if (!b->d_vt) {
+        mt::ValueTables vt{b->d_vflags, b->d_vclass, b->d_vexc, (uint32_t)b->value_flags.size(),
+                           (uint32_t)b->value_exc.size()};
+        HIPCHK(dalloc(&b->d_vt, 1));
+        HIPCHK(hipMemcpy(b->d_vt, &vt, sizeof vt, hipMemcpyHostToDevice));
     }
     return MT_OK;
 }
@@ -802,11 +812,7 @@ static mt::ReplayParams base_params(mt_batch *b) {
     P.doc_pool_base = b->d_pool_base;
     P.doc_pool_cap = b->d_pool_cap;
     P.props_in = b->d_props;
-    P.value_flags = b->d_vflags;
-    P.n_values = (uint32_t)b->value_flags.size();
-    P.value_class = b->d_vclass;
-    P.exc = b->d_vexc;
-    P.n_exc = (uint32_t)b->value_exc.size();
+    P.vt = b->d_vt;
     return P;
 }
 

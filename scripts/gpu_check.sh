@@ -48,6 +48,7 @@ for step in "$@"; do
     pmcB3) run pmcB3 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
     pmcC3) run pmcC3 300 rocprofv3 --pmc SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_VMEM SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_INSTS_LDS_STORE_BANDWIDTH SQ_INSTS_LDS_ATOMIC_BANDWIDTH --output-format csv -d gpurun_out/pmcC3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
     pmcC2) run pmcC2 200 rocprofv3 --pmc SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_VMEM SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_INSTS_LDS_STORE_BANDWIDTH SQ_INSTS_LDS_ATOMIC_BANDWIDTH --output-format csv -d gpurun_out/pmcC2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
+    pmcD3) run pmcD3 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_TRANSLATION_HIT TCP_TCC_READ_REQ_LATENCY TCP_TCP_LATENCY TCC_HIT TCC_MISS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d gpurun_out/pmcD3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
     pmcf3) run pmcf3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
     pmcw3) run pmcw3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw3 -o run -- python3 -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
     pmcA2) run pmcA2 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;

@@ -398,7 +398,7 @@ def test_config3_documents_at_full_size():
         b.run()
         launches = b.launches()
         assert len({li["seg_class"] for li in launches}) >= 3, launches  # the escalation chain ran
-        assert int(b.counters()["max_slots"].max()) > 1384
+        assert int(b.counters()["max_slots"].max()) > 1376
         for d in range(n):
             assert b.doc(d).status == st[d] == 0
             assert b.doc(d).digest() == int(dig[d]), f"doc {d} digest differs"
