@@ -139,9 +139,9 @@ struct Caps {
 // the replay kernel's 128 VGPRs cap a CU at 16 workgroups, so each class is the largest slot
 // count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3
 // and 2 documents per CU (tools/class_sizes.cpp); 128 keeps small documents' buffers small and
-// 7,432 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
+// 7,496 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
 // The replay kernel is latency bound, so a launch's rate grows with the documents per CU.
-constexpr int kClassSegs[] = {128, 376, 433, 496, 552, 613, 728, 848, 964, 1144, 1376, 1789, 2380, 3680, 7432, 60000};
+constexpr int kClassSegs[] = {128, 363, 423, 483, 540, 600, 720, 840, 960, 1136, 1376, 1792, 2389, 3704, 7496, 60000};
 constexpr int kNumClasses = 16;
 constexpr int kHbmClass = kNumClasses - 1;
 constexpr int kHbmSeg = 60000;
@@ -151,7 +151,8 @@ constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS c
 constexpr int kCapQueued = 7;      // checkpointed and taken by the launch's follow-on workers
 
 // follow-on queue (one per producer launch, hipMalloc'd, zeroed): word 0 = documents enqueued,
-// 1 = items claimed by workers, 2 = producer workgroups finished, 3 = producer workgroups started,
+// 1 = items claimed by workers, 2 = producer workgroups finished, 3 = unused, 4 = a consumer's
+// bounded wait timed out,
 // items from word kFqItems: producer workgroup index + 1 (0 = not yet published)
 constexpr int kFqItems = 16;
 
@@ -161,7 +162,7 @@ constexpr int64_t ck_words(int seg) { return 8ll * seg + 1024; }
 // cold records per slot in HBM: {props, ovl, toff, tcap} and {seq, rseq, 0, 0} (real seqs)
 constexpr int kColdPerSlot = 2;
 constexpr Caps class_caps(int seg) {
-    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 64, seg / 4 + 96};
+    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg / 8 + 224};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
@@ -250,8 +251,8 @@ struct ReplayParams {
     int32_t fq_role;              // 0 none, 1 producer, 2 consumer
     int64_t fq_producers;         // consumer: workgroups of the producer launch
     const int32_t *fq_doc_list;   // consumer: the producer's doc_list (null: identity)
-    uint32_t *fq_started;         // producer: host-mapped word set to 1 by the last workgroup to
-                                  // start (the host launches the consumer only then)
+    uint32_t *fq_started;         // producer: host-mapped count of started workgroups (the host
+                                  // launches the consumer once all are resident)
 };
 constexpr int kProfSlots = 12;
 

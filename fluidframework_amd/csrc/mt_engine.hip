@@ -2288,7 +2288,13 @@ MT_FI int32_t fq_claim(const ReplayParams &P, int32_t *src) {
         {
             const uint32_t i = __hip_atomic_fetch_add(&q[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (i < (uint32_t)P.fq_cap) {
-                for (;;) {
+                // bounded: a hand-off that never completes ends as an error (q[4], MT_INTERNAL on
+                // the host), never as a hung launch (~1 us per poll, ~8 s in all)
+                for (uint32_t polls = 0;; polls++) {
+                    if (polls >= (1u << 23)) {
+                        __hip_atomic_store(&q[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
                     uint32_t it = fq_load(&q[kFqItems + i]);
                     if (it) {
                         r = (int32_t)i;
@@ -2342,8 +2348,11 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
     }
     // follow-on producer: workgroups are dispatched in index order, so the last one starting
     // means all are resident and the host may launch the consumer
-    if (P.fq_started && w + 1 == P.n_docs && E.lane == 0)
-        __hip_atomic_store(P.fq_started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // follow-on producer: every workgroup counts itself in once resident (host-mapped, system
+    // scope); the host launches the consumer when the count reaches the launch's workgroups, so
+    // no dispatch order is assumed
+    if (P.fq_started && E.lane == 0)
+        __hip_atomic_fetch_add(P.fq_started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // ops stream through registers 64 at a time (coalesced 2 KiB loads), broadcast by readlane
     mt_op cur = load_op_lane(ops, b0 + done + E.lane, b1);
     for (int64_t base = b0 + done; base < b1 && E.status == ST_OK; base += kWave) {

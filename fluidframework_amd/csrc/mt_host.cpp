@@ -33,20 +33,20 @@
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);    \
     extern "C" __global__ void mt_follow_kernel_##S(mt::ReplayParams P);
 MT_DECLARE_CLASS(128)
-MT_DECLARE_CLASS(376)
-MT_DECLARE_CLASS(433)
-MT_DECLARE_CLASS(496)
-MT_DECLARE_CLASS(552)
-MT_DECLARE_CLASS(613)
-MT_DECLARE_CLASS(728)
-MT_DECLARE_CLASS(848)
-MT_DECLARE_CLASS(964)
-MT_DECLARE_CLASS(1144)
+MT_DECLARE_CLASS(363)
+MT_DECLARE_CLASS(423)
+MT_DECLARE_CLASS(483)
+MT_DECLARE_CLASS(540)
+MT_DECLARE_CLASS(600)
+MT_DECLARE_CLASS(720)
+MT_DECLARE_CLASS(840)
+MT_DECLARE_CLASS(960)
+MT_DECLARE_CLASS(1136)
 MT_DECLARE_CLASS(1376)
-MT_DECLARE_CLASS(1789)
-MT_DECLARE_CLASS(2380)
-MT_DECLARE_CLASS(3680)
-MT_DECLARE_CLASS(7432)
+MT_DECLARE_CLASS(1792)
+MT_DECLARE_CLASS(2389)
+MT_DECLARE_CLASS(3704)
+MT_DECLARE_CLASS(7496)
 MT_DECLARE_CLASS(60000)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
@@ -86,34 +86,34 @@ struct KernelClass {
 static const KernelClass kKernels[mt::kNumClasses] = {
     {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
      (const void *)mt_follow_kernel_128},
-    {376, (const void *)mt_replay_kernel_376, (const void *)mt_generate_kernel_376, (const void *)mt_load_kernel_376,
-     (const void *)mt_follow_kernel_376},
-    {433, (const void *)mt_replay_kernel_433, (const void *)mt_generate_kernel_433, (const void *)mt_load_kernel_433,
-     (const void *)mt_follow_kernel_433},
-    {496, (const void *)mt_replay_kernel_496, (const void *)mt_generate_kernel_496, (const void *)mt_load_kernel_496,
-     (const void *)mt_follow_kernel_496},
-    {552, (const void *)mt_replay_kernel_552, (const void *)mt_generate_kernel_552, (const void *)mt_load_kernel_552,
-     (const void *)mt_follow_kernel_552},
-    {613, (const void *)mt_replay_kernel_613, (const void *)mt_generate_kernel_613, (const void *)mt_load_kernel_613,
-     (const void *)mt_follow_kernel_613},
-    {728, (const void *)mt_replay_kernel_728, (const void *)mt_generate_kernel_728, (const void *)mt_load_kernel_728,
-     (const void *)mt_follow_kernel_728},
-    {848, (const void *)mt_replay_kernel_848, (const void *)mt_generate_kernel_848, (const void *)mt_load_kernel_848,
-     (const void *)mt_follow_kernel_848},
-    {964, (const void *)mt_replay_kernel_964, (const void *)mt_generate_kernel_964, (const void *)mt_load_kernel_964,
-     (const void *)mt_follow_kernel_964},
-    {1144, (const void *)mt_replay_kernel_1144, (const void *)mt_generate_kernel_1144, (const void *)mt_load_kernel_1144,
-     (const void *)mt_follow_kernel_1144},
+    {363, (const void *)mt_replay_kernel_363, (const void *)mt_generate_kernel_363, (const void *)mt_load_kernel_363,
+     (const void *)mt_follow_kernel_363},
+    {423, (const void *)mt_replay_kernel_423, (const void *)mt_generate_kernel_423, (const void *)mt_load_kernel_423,
+     (const void *)mt_follow_kernel_423},
+    {483, (const void *)mt_replay_kernel_483, (const void *)mt_generate_kernel_483, (const void *)mt_load_kernel_483,
+     (const void *)mt_follow_kernel_483},
+    {540, (const void *)mt_replay_kernel_540, (const void *)mt_generate_kernel_540, (const void *)mt_load_kernel_540,
+     (const void *)mt_follow_kernel_540},
+    {600, (const void *)mt_replay_kernel_600, (const void *)mt_generate_kernel_600, (const void *)mt_load_kernel_600,
+     (const void *)mt_follow_kernel_600},
+    {720, (const void *)mt_replay_kernel_720, (const void *)mt_generate_kernel_720, (const void *)mt_load_kernel_720,
+     (const void *)mt_follow_kernel_720},
+    {840, (const void *)mt_replay_kernel_840, (const void *)mt_generate_kernel_840, (const void *)mt_load_kernel_840,
+     (const void *)mt_follow_kernel_840},
+    {960, (const void *)mt_replay_kernel_960, (const void *)mt_generate_kernel_960, (const void *)mt_load_kernel_960,
+     (const void *)mt_follow_kernel_960},
+    {1136, (const void *)mt_replay_kernel_1136, (const void *)mt_generate_kernel_1136, (const void *)mt_load_kernel_1136,
+     (const void *)mt_follow_kernel_1136},
     {1376, (const void *)mt_replay_kernel_1376, (const void *)mt_generate_kernel_1376, (const void *)mt_load_kernel_1376,
      (const void *)mt_follow_kernel_1376},
-    {1789, (const void *)mt_replay_kernel_1789, (const void *)mt_generate_kernel_1789, (const void *)mt_load_kernel_1789,
-     (const void *)mt_follow_kernel_1789},
-    {2380, (const void *)mt_replay_kernel_2380, (const void *)mt_generate_kernel_2380, (const void *)mt_load_kernel_2380,
-     (const void *)mt_follow_kernel_2380},
-    {3680, (const void *)mt_replay_kernel_3680, (const void *)mt_generate_kernel_3680, (const void *)mt_load_kernel_3680,
-     (const void *)mt_follow_kernel_3680},
-    {7432, (const void *)mt_replay_kernel_7432, (const void *)mt_generate_kernel_7432, (const void *)mt_load_kernel_7432,
-     (const void *)mt_follow_kernel_7432},
+    {1792, (const void *)mt_replay_kernel_1792, (const void *)mt_generate_kernel_1792, (const void *)mt_load_kernel_1792,
+     (const void *)mt_follow_kernel_1792},
+    {2389, (const void *)mt_replay_kernel_2389, (const void *)mt_generate_kernel_2389, (const void *)mt_load_kernel_2389,
+     (const void *)mt_follow_kernel_2389},
+    {3704, (const void *)mt_replay_kernel_3704, (const void *)mt_generate_kernel_3704, (const void *)mt_load_kernel_3704,
+     (const void *)mt_follow_kernel_3704},
+    {7496, (const void *)mt_replay_kernel_7496, (const void *)mt_generate_kernel_7496, (const void *)mt_load_kernel_7496,
+     (const void *)mt_follow_kernel_7496},
     {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000,
      (const void *)mt_follow_kernel_60000},
 };
@@ -146,7 +146,7 @@ struct Launch {
     int follow = -1;            // -2: consumer not launched yet
     bool consumer = false;
     uint32_t *d_fq = nullptr;   // producer: queue header + items (the consumer reads the same one)
-    uint32_t *h_started = nullptr;  // producer: host-mapped "every workgroup started" word
+    uint32_t *h_started = nullptr;  // producer: host-mapped count of its workgroups that have started
     int32_t fq_cap = 0;
     int32_t workers = 0;
     // producer: the consumer's buffers, allocated and initialised before the producer runs (a
@@ -376,7 +376,7 @@ struct mt_batch {
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent first launches of mixed-size batches
     hipStream_t cstream = nullptr;  // result gathers (never queued behind a running launch)
     hipStream_t fstream = nullptr;  // follow-on consumer launches
-    uint32_t *h_started = nullptr;  // host-mapped: per first launch, 1 once all its workgroups started
+    uint32_t *h_started = nullptr;  // host-mapped: per first launch, the count of its started workgroups
     hipEvent_t ev_user = nullptr;
     uint64_t *d_digest = nullptr;  // mt_batch_device_digests
     float kernel_ms = 0, total_ms = 0;
@@ -495,7 +495,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
     if (b->opt.chunk_size <= 0) b->opt.chunk_size = 10000;
     if (b->opt.arena_factor <= 0) b->opt.arena_factor = 4;
     if (b->opt.pool_per_op <= 0) b->opt.pool_per_op = 96;
-    // the whole class ladder (376 -> 496 -> 613 -> 848 -> ... -> HBM class) by default; < 0: checkpoint,
+    // the whole class ladder (363 -> 483 -> 600 -> 840 -> ... -> HBM class) by default; < 0: checkpoint,
     // but stop after the first launch
     if (b->opt.max_retries == 0) b->opt.max_retries = 2 * mt::kNumClasses;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -771,10 +771,11 @@ static int class_for(const mt_batch *b, int32_t ops_per_doc, int level, bool rep
 static size_t class_lds(int c) { return c == mt::kHbmClass ? 0 : mt::make_layout(mt::kClassSegs[c]).bytes; }
 static size_t class_state_bytes(int c) { return c == mt::kHbmClass ? mt::make_layout(mt::kHbmSeg).bytes : 0; }
 static int max_lds_bytes();
-// the class an escalated document continues in: at least 1.2x the slots
+// the class an escalated document continues in: at least 1.1x the slots (every class of the
+// ladder is a residency tier; skipping one costs more than the extra checkpoint)
 static int resume_class(int c) {
     int n = c + 1;
-    while (n < mt::kNumClasses && 5 * mt::kClassSegs[n] < 6 * mt::kClassSegs[c]) n++;
+    while (n < mt::kNumClasses && 10 * mt::kClassSegs[n] < 11 * mt::kClassSegs[c]) n++;
     if (n >= mt::kNumClasses) n = mt::kNumClasses - 1;
     while (n > c + 1 && class_lds(n) > (size_t)max_lds_bytes()) n--;
     return n;
@@ -880,13 +881,12 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
 // launch that fits the GPU in about one round: its last documents finish together, and a document
 // that checkpoints would resume only then, replaying its remaining ops at one-wave latency as a
 // second serial phase).  Off for SnapshotLoader launches, the HBM class and batches that cannot
-// escalate.  MT_FOLLOW_WORKERS overrides the worker count (0: off).
+// escalate.  Off by default since the capacity ladder was re-derived (config 2's documents fit
+// the first class, and idle consumers polling beside the producer cost it 15 %); MT_FOLLOW_WORKERS
+// sets the worker count (read per launch).
 static int follow_workers(mt_batch *b, const Launch &L, int64_t n) {
-    static int env = -2;
-    if (env == -2) {
-        const char *e = getenv("MT_FOLLOW_WORKERS");
-        env = e && *e ? atoi(e) : -1;
-    }
+    const char *e = getenv("MT_FOLLOW_WORKERS");
+    const int env = e && *e ? atoi(e) : 0;
     if (env == 0 || L.load || L.level != 0 || L.cls == mt::kHbmClass || b->opt.max_retries <= 0) return 0;
     int nxt = resume_class(L.cls);
     while (nxt > L.cls + 1 && !class_usable(nxt)) nxt--;
@@ -996,6 +996,10 @@ static int gather_follow(mt_batch *b, int li) {
     if (!b->cstream) HIPCHK(hipStreamCreateWithFlags(&b->cstream, hipStreamNonBlocking));
     HIPCHK(hipMemcpyAsync(q.data(), Pr.d_fq, 4 * q.size(), hipMemcpyDeviceToHost, b->cstream));
     HIPCHK(hipStreamSynchronize(b->cstream));
+    if (q[4]) {  // a consumer's bounded wait for its item ran out (fq_claim)
+        fprintf(stderr, "mtreplay: follow-on hand-off of launch %d timed out\n", L.src);
+        return MT_INTERNAL;
+    }
     const uint32_t n = std::min<uint32_t>(q[0], (uint32_t)L.fq_cap);
     L.docs.clear();
     L.cksrc.clear();
@@ -1286,7 +1290,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
         for (int li = b->first0; li < b->n_first; li++) {
             if (b->launches[(size_t)li].follow != -2) continue;
             const Launch &Pr = b->launches[(size_t)li];
-            if (li != only && !((volatile uint32_t *)Pr.h_started)[0]) continue;
+            if (li != only && ((volatile uint32_t *)Pr.h_started)[0] < (uint32_t)launch_n(b->n_docs, Pr)) continue;
             int r = launch_follow(b, li);
             if (r) return r;
         }

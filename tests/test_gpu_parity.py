@@ -108,6 +108,9 @@ def test_follow_on_workers_resume_checkpointed_documents():
     """A one-round first launch queues the documents it checkpoints to a concurrent consumer
     launch of the next class; the queued documents' results come from there,
     further escalations continue from the consumer's checkpoints, all bit-exact."""
+    import os
+
+    os.environ["MT_FOLLOW_WORKERS"] = "64"  # off by default (DESIGN.md §4a)
     n = 384
     p = O.gen_params(900, pct_insert=55, pct_remove=35, seed=0xF0110)
     ops, text, props, off = O.gen_batch(p, n)
@@ -133,6 +136,7 @@ def test_follow_on_workers_resume_checkpointed_documents():
         b.snapshots()
         for d in range(0, n, 53):
             assert b.doc(d).snapshot_v1(device=True) == b.doc(d).snapshot_v1()
+    del os.environ["MT_FOLLOW_WORKERS"]
 
 
 def test_gpu_generator_matches_oracle_generator():

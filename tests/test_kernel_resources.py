@@ -39,7 +39,7 @@ def _kernels(notes: str) -> dict:
 
 
 @pytest.mark.skipif(not (LLVM / "llvm-readelf").exists() or not OBJ.exists(), reason="no build / ROCm llvm tools")
-@pytest.mark.parametrize("seg", [376, 433, 1144, 1376, 1789])
+@pytest.mark.parametrize("seg", [363, 423, 1136, 1376, 1792])
 def test_replay_kernel_fits_four_waves_per_simd(seg, tmp_path):
     obj = OBJ / f"k{seg}.o"
     if not obj.exists():
