@@ -26,7 +26,8 @@ constexpr uint32_t kGranularity = 256;  // TextSegmentGranularity, mergeTree.ts:
 constexpr int kZamboniMax = 2;          // zamboniSegmentsMaxCount, mergeTree.ts:1061
 constexpr int kMaxClients = 254;        // short client ids 0..253 (254 = NonCollabClient, 255 = none)
 constexpr int32_t kNoneSeq = 0x7FFFFFFF;  // removedSeq === undefined
-constexpr uint32_t kMarkerSlot = 0xFFFFu; // oe entry that ends a leaf block
+constexpr uint32_t kOutBlockEnd = 0x80000000u;  // OutRec.blk of the entry that ends a leaf block
+__host__ __device__ constexpr bool out_is_end(uint32_t blk) { return (blk & kOutBlockEnd) != 0; }
 constexpr uint32_t kNoClient = 255u;
 constexpr uint32_t kOvlMaskClients = 31u; // overlap sets of clients < 31 are a bit mask (see kOvlList)
 constexpr uint32_t kOvlList = 0x80000000u;  // cold.y with this bit: pool offset of an overlap-client list
@@ -91,7 +92,7 @@ struct OutRec {
                      // a [n | kPoolOvlTag, 0, client x n] list
     uint32_t props;  // prop-set id in the doc's pool (0 = undefined)
     uint32_t toff;   // text offset in the doc's text region (Marker: refType)
-    uint32_t blk;    // leaf block id << 16 | slot (slot 0xFFFF: end-of-block marker)
+    uint32_t blk;    // leaf block id; | kOutBlockEnd for the entry that ends the block
 };
 static_assert(sizeof(OutRec) == 32, "OutRec");
 
@@ -139,12 +140,13 @@ struct Caps {
 // the replay kernel's 128 VGPRs cap a CU at 16 workgroups, so each class is the largest slot
 // count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3
 // and 2 documents per CU (tools/class_sizes.cpp); 128 keeps small documents' buffers small and
-// 7,496 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
+// 7,266 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
+// The last class keeps its tables in HBM (2,097,152 slots, 32-bit ids: the spill path).
 // The replay kernel is latency bound, so a launch's rate grows with the documents per CU.
-constexpr int kClassSegs[] = {128, 363, 423, 483, 540, 600, 720, 840, 960, 1136, 1376, 1792, 2389, 3704, 7496, 60000};
+constexpr int kClassSegs[] = {128, 363, 423, 483, 540, 600, 720, 840, 960, 1136, 1376, 1792, 2389, 3600, 7266, 2097152};
 constexpr int kNumClasses = 16;
 constexpr int kHbmClass = kNumClasses - 1;
-constexpr int kHbmSeg = 60000;
+constexpr int kHbmSeg = 2097152;  // giant documents (config 4: ~10^6 segments)
 constexpr int kReplayStartClass = 1;  // replay starts documents in at most the 16-per-CU class
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS class (16-bit lengths)
@@ -162,19 +164,24 @@ constexpr int64_t ck_words(int seg) { return 8ll * seg + 1024; }
 // cold records per slot in HBM: {props, ovl, toff, tcap} and {seq, rseq, 0, 0} (real seqs)
 constexpr int kColdPerSlot = 2;
 constexpr Caps class_caps(int seg) {
-    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg / 8 + 224};
+    // the overlay list (unsettled segments, ~100-200 at a lag <= 32) is sized to the collab window;
+    // the largest classes, where a document with a wide window ends up, can hold half their slots
+    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg >= 3000 ? seg / 2 : seg / 8 + 224};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
     uint32_t len, sr, meta, sblk, ulist;
-    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, heap, scratch, hdr, bytes;
+    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, bep, heap, scratch, hdr, bytes;
 };
 constexpr int kHdrWords = 24;  // per-document scalars kept in LDS (mt_engine.hip LWord)
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
-// segment lengths are 16-bit in the LDS classes (a longer segment moves the document to the HBM
-// class, cap_kind 8), 32-bit in the HBM class
-constexpr uint32_t len_bytes(int seg) { return seg == 60000 ? 4u : 2u; }
+// The HBM class (tables in global memory) holds giant documents: 32-bit slot / block ids and
+// segment lengths.  The LDS classes use 16-bit ones (a longer segment moves the document to the
+// HBM class, cap_kind 8).
+constexpr bool is_hbm_seg(int seg) { return seg > 65000; }
+constexpr uint32_t len_bytes(int seg) { return is_hbm_seg(seg) ? 4u : 2u; }
+constexpr uint32_t idx_bytes(int seg) { return is_hbm_seg(seg) ? 4u : 2u; }
 constexpr Layout make_layout(int seg) {
     const Caps c = class_caps(seg);
     Layout L{};
@@ -182,15 +189,16 @@ constexpr Layout make_layout(int seg) {
     L.len = o;     o = lds_align(o + len_bytes(seg) * c.seg);
     L.sr = o;      o = lds_align(o + 4u * c.seg);
     L.meta = o;    o = lds_align(o + 4u * c.seg);
-    L.sblk = o;    o = lds_align(o + 2u * c.seg);
-    L.ulist = o;   o = lds_align(o + 2u * c.ulist);
-    L.bparent = o; o = lds_align(o + 2u * c.blk);  // a free block's b_parent links the free list
-    L.bchild = o;  o = lds_align(o + 16u * c.blk);
+    L.sblk = o;    o = lds_align(o + idx_bytes(seg) * c.seg);
+    L.ulist = o;   o = lds_align(o + idx_bytes(seg) * c.ulist);
+    L.bparent = o; o = lds_align(o + idx_bytes(seg) * c.blk);  // a free block's b_parent links the free list
+    L.bchild = o;  o = lds_align(o + 8u * idx_bytes(seg) * c.blk);
     L.bcount = o;  o = lds_align(o + 1u * c.blk);
     L.bleaf = o;   o = lds_align(o + 1u * c.blk);
     L.bscour = o;  o = lds_align(o + 1u * c.blk);
     L.bslen = o;   o = lds_align(o + 4u * c.blk);
     L.bacc = o;    o = lds_align(o + 4u * c.blk);
+    L.bep = o;     o = lds_align(o + (is_hbm_seg(seg) ? 4u * c.blk : 0u));
     L.heap = o;    o = lds_align(o + 8u * (c.heap + 2));
     L.scratch = o; o = lds_align(o + 4u * 128);
     L.hdr = o;     o = lds_align(o + 4u * kHdrWords);

@@ -42,7 +42,7 @@ extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P
     for (int32_t i = threadIdx.x; i < o.n_out; i += 64) {
         const OutRec r = rec[i];
         uint64_t h = 0xCBF29CE484222325ull;
-        if ((r.blk & 0xFFFFu) == kMarkerSlot) {
+        if (out_is_end(r.blk)) {
             h = fnv(h, 0xB10CB10Cu);
         } else {
             h = fnv(h, r.len);

@@ -147,17 +147,23 @@ struct Engine {
     static constexpr Caps cap = class_caps(SEG);
     static constexpr Layout lay = make_layout(SEG);
     using Len = std::conditional_t<len_bytes(SEG) == 2u, uint16_t, uint32_t>;
+    // slot and block ids: 16-bit in the LDS classes, 32-bit in the HBM class (giant documents)
+    using Idx = std::conditional_t<idx_bytes(SEG) == 2u, uint16_t, uint32_t>;
+    static constexpr uint32_t kNoBlk = idx_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
+    static constexpr bool kHbm = is_hbm_seg(SEG);
     static constexpr uint32_t kMaxLen = len_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
     // ---- LDS state
     Len *s_len;
     uint32_t *s_meta;
     uint32_t *s_sr;  // seq16 | rseq16 << 16 (window-relative); of a free slot: the next free slot
-    uint16_t *s_blk;
-    uint16_t *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
-    uint16_t *b_parent, *b_child;  // b_parent of a free block links the free block list
+    Idx *s_blk;
+    Idx *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
+    Idx *b_parent, *b_child;  // b_parent of a free block links the free block list
     uint8_t *b_count, *b_leaf;
     int8_t *b_scour;
     uint32_t *b_slen, *b_acc;
+    uint32_t *b_ep;      // HBM class: the overlay epoch that last wrote b_acc[B] (no O(blocks) clear)
+    uint32_t ov_epoch;
     uint32_t *scratch;  // 128 words
     // ---- uniform scalars
     int32_t slot_top, free_head, free_n, blk_top, n_bfree, bfree_head, root, depth, hn, nu;
@@ -198,15 +204,16 @@ struct Engine {
         s_len = (Len *)(tb + lay.len);
         s_sr = (uint32_t *)(tb + lay.sr);
         s_meta = (uint32_t *)(tb + lay.meta);
-        s_blk = (uint16_t *)(tb + lay.sblk);
-        u_list = (uint16_t *)(tb + lay.ulist);
-        b_parent = (uint16_t *)(tb + lay.bparent);
-        b_child = (uint16_t *)(tb + lay.bchild);
+        s_blk = (Idx *)(tb + lay.sblk);
+        u_list = (Idx *)(tb + lay.ulist);
+        b_parent = (Idx *)(tb + lay.bparent);
+        b_child = (Idx *)(tb + lay.bchild);
         b_count = (uint8_t *)(tb + lay.bcount);
         b_leaf = (uint8_t *)(tb + lay.bleaf);
         b_scour = (int8_t *)(tb + lay.bscour);
         b_slen = (uint32_t *)(tb + lay.bslen);
         b_acc = (uint32_t *)(tb + lay.bacc);
+        b_ep = (uint32_t *)(tb + lay.bep);
         h_ent = (uint2 *)(tb + lay.heap);
         scratch = (uint32_t *)(tb + lay.scratch);
         uint32_t *hw = (uint32_t *)(tb + lay.hdr);
@@ -251,6 +258,7 @@ struct Engine {
         n_bfree = 0;
         bfree_head = -1;
         sbase = 0;
+        clear_epochs();
         hn = 0;
         nu = 0;
         min_seq = 0;
@@ -297,10 +305,10 @@ struct Engine {
         if (n_bfree > 0) {
             b = bfree_head;
             bfree_head = (int32_t)rfl((uint32_t)b_parent[b]);
-            if (bfree_head == (int32_t)kNoBlock) bfree_head = -1;
+            if (bfree_head == (int32_t)kNoBlk) bfree_head = -1;
             n_bfree--;
         } else {
-            if (blk_top >= cap.blk || blk_top >= 0xFFFF) {
+            if (blk_top >= cap.blk || (uint32_t)blk_top >= kNoBlk) {
                 cap_fail(1);
                 return 0;
             }
@@ -309,12 +317,12 @@ struct Engine {
         b_leaf[b] = (uint8_t)leaf;
         b_count[b] = 0;
         b_scour[b] = kScourUndef;
-        b_parent[b] = kNoBlock;
+        b_parent[b] = (Idx)kNoBlk;
         b_slen[b] = 0;
         return b;
     }
     MT_FI void free_block(int32_t b) {
-        b_parent[b] = (uint16_t)(bfree_head < 0 ? kNoBlock : bfree_head);
+        b_parent[b] = (Idx)(bfree_head < 0 ? (int32_t)kNoBlk : (int32_t)bfree_head);
         bfree_head = b;
         n_bfree++;
     }
@@ -371,7 +379,7 @@ struct Engine {
     // depth - 1, so the walk is `depth` uniform steps)
     MT_FI void chain_add(uint32_t *arr, bool act, uint32_t b, uint32_t v) {
         for (int32_t l = 0; l < depth; l++) {
-            if (act && b != kNoBlock) {
+            if (act && b != kNoBlk) {
                 lds_add(&arr[b], v);
                 b = b_parent[b];
             }
@@ -380,7 +388,7 @@ struct Engine {
     // uniform: b_slen += v on the chain b -> root
     MT_FI void chain_add_uniform(int32_t b, uint32_t v) {
         wsync();
-        while (b != (int32_t)kNoBlock) {
+        while (b != (int32_t)kNoBlk) {
             uint32_t x = b_slen[b];
             int32_t p = b_parent[b];
             b_slen[b] = x + v;
@@ -389,12 +397,42 @@ struct Engine {
         wsync();
     }
 
+    // the overlay's b_acc: in the HBM class a block first touched in this epoch is reset before
+    // the adds (every lane of a shared block writes the same reset)
+    MT_FI void ov_chain_add(bool act, uint32_t b, uint32_t v) {
+        if constexpr (kHbm) {
+            uint32_t c = b;
+            for (int32_t l = 0; l < depth; l++) {
+                if (act && c != kNoBlk) {
+                    if (b_ep[c] != ov_epoch) {
+                        b_acc[c] = 0u;
+                        b_ep[c] = ov_epoch;
+                    }
+                    c = b_parent[c];
+                }
+            }
+            wsync();
+        }
+        chain_add(b_acc, act, b, v);
+    }
+    MT_FI void clear_epochs() {
+        ov_epoch = 0;
+        if constexpr (kHbm) {  // once per launch: the tables are uninitialised device memory
+            for (int32_t i = lane; i < cap.blk; i += kWave) b_ep[i] = 0xFFFFFFFFu;
+            wsync();
+        }
+    }
+    MT_FI uint32_t ov_acc(uint32_t b) const {
+        if constexpr (kHbm) return b_ep[b] == ov_epoch ? b_acc[b] : 0u;
+        return b_acc[b];
+    }
+
     MT_FI void u_push(uint32_t slot) {
         if (nu >= cap.ulist) {
             cap_fail(1);
             return;
         }
-        u_list[nu] = (uint16_t)slot;
+        u_list[nu] = (Idx)slot;
         nu++;
         if (nu > max_u) max_u = nu;
     }
@@ -404,7 +442,11 @@ struct Engine {
     MT_FI void overlay(int32_t ref, uint32_t c) {
         PF_SCOPE(6);
         wsync();
-        for (int32_t i = lane; i < blk_top; i += kWave) b_acc[i] = 0u;
+        if constexpr (kHbm) {
+            ov_epoch++;  // blocks of other epochs read as 0 (giant documents: ~10^5 blocks)
+        } else {
+            for (int32_t i = lane; i < blk_top; i += kWave) b_acc[i] = 0u;
+        }
         wsync();
         ov_full = ref < min_seq;
         if (!ov_full) {
@@ -420,7 +462,7 @@ struct Engine {
                 }
                 const uint64_t vm = ballot(valid);
                 wsync();
-                if (valid) u_list[w + __popcll(vm & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+                if (valid) u_list[w + __popcll(vm & ((1ull << lane) - 1ull))] = (Idx)slot;
                 w += __popcll(vm);
                 uint32_t vlen = 0, b = 0;
                 bool tie;
@@ -428,7 +470,7 @@ struct Engine {
                     view_of(slot, ref, c, vlen, tie);
                     b = s_blk[slot];
                 }
-                chain_add(b_acc, valid && vlen > 0u, b, vlen);
+                ov_chain_add(valid && vlen > 0u, b, vlen);
             }
             nu = w;
         } else {
@@ -441,7 +483,7 @@ struct Engine {
                     view_of((uint32_t)slot, ref, c, vlen, tie);
                     b = s_blk[slot];
                 }
-                chain_add(b_acc, live && vlen > 0u, b, vlen);
+                ov_chain_add(live && vlen > 0u, b, vlen);
             }
         }
         ov_splits = splits;
@@ -479,7 +521,7 @@ struct Engine {
             const uint64_t km = ballot(keep);
             wsync();
             if (keep) {
-                u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+                u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (Idx)slot;
                 const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
                 const uint32_t nq = q16 > m16 ? q16 - m16 : 0u;
                 const uint32_t nr = r16 == kSeq16None ? kSeq16None : (r16 > m16 ? r16 - m16 : 0u);
@@ -523,7 +565,7 @@ struct Engine {
             uint32_t ch = 0, v = 0;
             if (lane < n) {
                 ch = row;
-                v = b_acc[ch] + (ov_full ? 0u : b_slen[ch]);
+                v = ov_acc(ch) + (ov_full ? 0u : b_slen[ch]);
             }
             const uint32_t incl = scan8(v) + base;
             const uint64_t hb = ballot(lanes8 && lane < n && (strict ? incl > pos : incl >= pos));
@@ -695,7 +737,7 @@ struct Engine {
     // ------------------------------------------------------------------ block tree
     MT_FI int32_t child_index(int32_t p, int32_t c) {
         int32_t n = b_count[p];
-        bool hit = lane < n && b_child[p * 8 + lane] == (uint16_t)c;
+        bool hit = lane < n && b_child[p * 8 + lane] == (Idx)c;
         uint64_t b = ballot(hit);
         return b ? first_lane(b) : -1;
     }
@@ -704,12 +746,12 @@ struct Engine {
     MT_FI void update_root(int32_t split_node) {
         int32_t nr = alloc_block(0);
         if (status) return;
-        b_child[nr * 8 + 0] = (uint16_t)root;
-        b_child[nr * 8 + 1] = (uint16_t)split_node;
+        b_child[nr * 8 + 0] = (Idx)root;
+        b_child[nr * 8 + 1] = (Idx)split_node;
         b_count[nr] = 2;
         b_slen[nr] = b_slen[root] + b_slen[split_node];
-        b_parent[root] = (uint16_t)nr;
-        b_parent[split_node] = (uint16_t)nr;
+        b_parent[root] = (Idx)nr;
+        b_parent[split_node] = (Idx)nr;
         root = nr;
         depth++;
         wsync();
@@ -722,13 +764,13 @@ struct Engine {
             int32_t i = child_index(p, after);
             int32_t n = b_count[p];
             wsync();
-            uint16_t v = 0;
+            Idx v = 0;
             if (lane > i && lane < n) v = b_child[p * 8 + lane];
             wsync();
             if (lane > i && lane < n) b_child[p * 8 + lane + 1] = v;
             wsync();
-            b_child[p * 8 + i + 1] = (uint16_t)nc;
-            b_parent[nc] = (uint16_t)p;
+            b_child[p * 8 + i + 1] = (Idx)nc;
+            b_parent[nc] = (Idx)p;
             b_count[p] = (uint8_t)(n + 1);
             wsync();
             if (n + 1 < kMaxNodes) return;
@@ -739,9 +781,9 @@ struct Engine {
             wsync();
             uint32_t sl = 0;
             if (lane >= 4 && lane < 8) {
-                uint16_t c = b_child[p * 8 + lane];
+                Idx c = b_child[p * 8 + lane];
                 b_child[m * 8 + lane - 4] = c;
-                b_parent[c] = (uint16_t)m;
+                b_parent[c] = (Idx)m;
                 sl = b_slen[c];
             }
             const uint32_t moved = rdl(sum8(lane >= 4 && lane < 8 ? sl : 0u), 0);
@@ -769,9 +811,9 @@ struct Engine {
         wsync();
         uint32_t sl = 0;
         if (lane >= 4 && lane < 8) {
-            uint16_t c = b_child[blk * 8 + lane];
+            Idx c = b_child[blk * 8 + lane];
             b_child[nb * 8 + lane - 4] = c;
-            s_blk[c] = (uint16_t)nb;
+            s_blk[c] = (Idx)nb;
             sl = settled_len(c);
         }
         const uint32_t moved = rdl(sum8(lane >= 4 && lane < 8 ? sl : 0u), 0);
@@ -791,14 +833,14 @@ struct Engine {
     MT_FI int32_t insert_leaf(int32_t blk, int32_t k, uint32_t slot) {
         const int32_t n = b_count[blk];
         wsync();
-        uint16_t v = 0;
+        Idx v = 0;
         const bool mv = lane >= k && lane < n;
         if (mv) v = b_child[blk * 8 + lane];
         wsync();
         if (mv) b_child[blk * 8 + lane + 1] = v;
         wsync();
-        b_child[blk * 8 + k] = (uint16_t)slot;
-        s_blk[slot] = (uint16_t)blk;
+        b_child[blk * 8 + k] = (Idx)slot;
+        s_blk[slot] = (Idx)blk;
         b_count[blk] = (uint8_t)(n + 1);
         wsync();
         if (n + 1 >= kMaxNodes) {
@@ -1367,10 +1409,10 @@ struct Engine {
         if (lane < cc) {
             b_leaf[id] = (uint8_t)leaf;
             b_scour[id] = kScourUndef;
-            b_parent[id] = (uint16_t)parent;
+            b_parent[id] = (Idx)parent;
             b_slen[id] = 0u;
             b_count[id] = (uint8_t)(base + (lane < extra ? 1 : 0));
-            b_child[parent * 8 + lane] = (uint16_t)id;
+            b_child[parent * 8 + lane] = (Idx)id;
         }
         // leaf i goes to block q at position p
         uint32_t c = 0, sl = 0;
@@ -1382,12 +1424,12 @@ struct Engine {
         const uint32_t nb = (uint32_t)__shfl((int)id, in ? q : 0, kWave);
         wsync();
         if (in) {
-            b_child[nb * 8 + p] = (uint16_t)c;
+            b_child[nb * 8 + p] = (Idx)c;
             if (leaf) {
-                s_blk[c] = (uint16_t)nb;
+                s_blk[c] = (Idx)nb;
                 sl = settled_len(c);
             } else {
-                b_parent[c] = (uint16_t)nb;
+                b_parent[c] = (Idx)nb;
                 sl = b_slen[c];
             }
         }
@@ -1418,7 +1460,7 @@ struct Engine {
         const uint32_t e = lane < total ? dst[lane] : 0u;
         *startM = ballot(lane < total && (e >> 31));
         wsync();
-        if (lane < total) dst[lane] = e & 0xFFFFu;
+        if (lane < total) dst[lane] = e & 0x7FFFFFFFu;
         wsync();
         return total;
     }
@@ -1477,7 +1519,7 @@ struct Engine {
             b_scour[blk] = kScourFalse;
             if (nk < cnt) {
                 wsync();
-                if (lane < nk) b_child[blk * 8 + lane] = (uint16_t)hold[lane];
+                if (lane < nk) b_child[blk * 8 + lane] = (Idx)hold[lane];
                 b_count[blk] = (uint8_t)nk;
                 splits++;
                 wsync();
@@ -1617,45 +1659,45 @@ struct Engine {
         for (int32_t l = 0; l + 1 < depth; l++) b = rfl((int32_t)b_child[b * 8 + b_count[b] - 1]);
         int32_t n = b_count[b];
         if (n < kMaxNodes - 1) {
-            b_child[b * 8 + n] = (uint16_t)slot;
+            b_child[b * 8 + n] = (Idx)slot;
             b_count[b] = (uint8_t)(n + 1);
-            s_blk[slot] = (uint16_t)b;
+            s_blk[slot] = (Idx)b;
             wsync();
             return;
         }
         int32_t child = alloc_block(1);
         if (status) return;
-        b_child[child * 8] = (uint16_t)slot;
+        b_child[child * 8] = (Idx)slot;
         b_count[child] = 1;
-        s_blk[slot] = (uint16_t)child;
+        s_blk[slot] = (Idx)child;
         wsync();
         int32_t left = b;
         for (;;) {
             const int32_t p = b_parent[left];
-            if (p == (int32_t)kNoBlock) {  // left is the root: the top level now has two blocks
+            if (p == (int32_t)kNoBlk) {  // left is the root: the top level now has two blocks
                 const int32_t r = alloc_block(0);
                 if (status) return;
-                b_child[r * 8] = (uint16_t)left;
-                b_child[r * 8 + 1] = (uint16_t)child;
+                b_child[r * 8] = (Idx)left;
+                b_child[r * 8 + 1] = (Idx)child;
                 b_count[r] = 2;
-                b_parent[left] = (uint16_t)r;
-                b_parent[child] = (uint16_t)r;
+                b_parent[left] = (Idx)r;
+                b_parent[child] = (Idx)r;
                 root = r;
                 depth++;
                 break;
             }
             const int32_t pn = b_count[p];
             if (pn < kMaxNodes - 1) {
-                b_child[p * 8 + pn] = (uint16_t)child;
+                b_child[p * 8 + pn] = (Idx)child;
                 b_count[p] = (uint8_t)(pn + 1);
-                b_parent[child] = (uint16_t)p;
+                b_parent[child] = (Idx)p;
                 break;
             }
             const int32_t np = alloc_block(0);
             if (status) return;
-            b_child[np * 8] = (uint16_t)child;
+            b_child[np * 8] = (Idx)child;
             b_count[np] = 1;
-            b_parent[child] = (uint16_t)np;
+            b_parent[child] = (Idx)np;
             child = np;
             left = p;
         }
@@ -1705,7 +1747,7 @@ struct Engine {
             }
             if (un) {
                 s_meta[slot] = meta | kMetaUnsettled;
-                u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+                u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (Idx)slot;
             }
             nu += __popcll(um);
             if (nu > max_u) max_u = nu;
@@ -1800,7 +1842,7 @@ struct Engine {
     MT_FI int32_t next_leaf_block(int32_t b) {
         for (;;) {
             int32_t p = b_parent[b];
-            if (p == (int32_t)kNoBlock) return -1;
+            if (p == (int32_t)kNoBlk) return -1;
             int32_t i = child_index(p, b);
             if (i + 1 < (int32_t)b_count[p]) {
                 b = b_child[p * 8 + i + 1];
@@ -1869,7 +1911,7 @@ struct Engine {
                     wsync();
                     if (newu) {
                         s_meta[slot] = meta | kMetaUnsettled;
-                        u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (uint16_t)slot;
+                        u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (Idx)slot;
                     }
                     nu += __popcll(um);
                     if (nu > max_u) max_u = nu;
@@ -2026,6 +2068,16 @@ struct Engine {
         for (int32_t i = lane; i < n; i += kWave) dst[i] = (T)p[i];
         p += n;
     }
+    // block ids in the image are index-width independent: kNoBlk (0xFFFF in the LDS classes,
+    // 0xFFFFFFFF in the HBM class) is stored as 0xFFFFFFFF
+    MT_FI void dump_blk(uint32_t *&p, const Idx *src, int32_t n) {
+        for (int32_t i = lane; i < n; i += kWave) p[i] = src[i] == (Idx)kNoBlk ? 0xFFFFFFFFu : (uint32_t)src[i];
+        p += n;
+    }
+    MT_FI void load_blk(const uint32_t *&p, Idx *dst, int32_t n) {
+        for (int32_t i = lane; i < n; i += kWave) dst[i] = p[i] == 0xFFFFFFFFu ? (Idx)kNoBlk : (Idx)p[i];
+        p += n;
+    }
     MT_FI void checkpoint(uint32_t *ck, int32_t ops_done) {
         resolve_splits();
         wsync();
@@ -2062,8 +2114,8 @@ struct Engine {
         dump(p, s_meta, slot_top);
         dump(p, s_blk, slot_top);
         dump(p, u_list, nu);
-        dump(p, b_parent, blk_top);
-        dump(p, (const uint32_t *)b_child, 4 * blk_top);
+        dump_blk(p, b_parent, blk_top);
+        dump(p, b_child, 8 * blk_top);  // one word per child entry: the image is index-width independent
         for (int32_t i = lane; i < blk_top; i += kWave)
             p[i] = (uint32_t)b_count[i] | ((uint32_t)b_leaf[i] << 8) | ((uint32_t)(uint8_t)b_scour[i] << 16);
         p += blk_top;
@@ -2072,6 +2124,7 @@ struct Engine {
     }
     // returns the number of ops the checkpoint had applied
     MT_FI int32_t restore(const uint32_t *ck, const uint4 *cold_src) {
+        clear_epochs();
         const int32_t ops_done = (int32_t)rfl(ck[1]);
         slot_top = (int32_t)rfl(ck[2]);
         free_head = (int32_t)rfl(ck[3]);
@@ -2104,8 +2157,8 @@ struct Engine {
         load(p, s_meta, slot_top);
         load(p, s_blk, slot_top);
         load(p, u_list, nu);
-        load(p, b_parent, blk_top);
-        load(p, (uint32_t *)b_child, 4 * blk_top);
+        load_blk(p, b_parent, blk_top);
+        load(p, b_child, 8 * blk_top);
         for (int32_t i = lane; i < blk_top; i += kWave) {
             const uint32_t v = p[i];
             b_count[i] = (uint8_t)v;
@@ -2147,7 +2200,7 @@ struct Engine {
                     r.ovl = (s_meta[slot] & kMetaHasOvl) ? cr.y : 0u;
                     r.props = cr.x;
                     r.toff = cr.z;
-                    r.blk = ((uint32_t)blk << 16) | slot;
+                    r.blk = (uint32_t)blk;
                 } else {
                     r.len = 0;
                     r.seq = 0;
@@ -2156,7 +2209,7 @@ struct Engine {
                     r.ovl = 0;
                     r.props = 0;
                     r.toff = 0;
-                    r.blk = ((uint32_t)blk << 16) | kMarkerSlot;
+                    r.blk = (uint32_t)blk | kOutBlockEnd;
                 }
                 out[j] = r;
             }

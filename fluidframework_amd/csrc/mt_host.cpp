@@ -45,9 +45,9 @@ MT_DECLARE_CLASS(1136)
 MT_DECLARE_CLASS(1376)
 MT_DECLARE_CLASS(1792)
 MT_DECLARE_CLASS(2389)
-MT_DECLARE_CLASS(3704)
-MT_DECLARE_CLASS(7496)
-MT_DECLARE_CLASS(60000)
+MT_DECLARE_CLASS(3600)
+MT_DECLARE_CLASS(7266)
+MT_DECLARE_CLASS(2097152)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
 extern "C" __global__ void mt_bytes_digest_kernel(const uint8_t *buf, const int64_t *off, const int64_t *len, int64_t n,
@@ -110,12 +110,12 @@ static const KernelClass kKernels[mt::kNumClasses] = {
      (const void *)mt_follow_kernel_1792},
     {2389, (const void *)mt_replay_kernel_2389, (const void *)mt_generate_kernel_2389, (const void *)mt_load_kernel_2389,
      (const void *)mt_follow_kernel_2389},
-    {3704, (const void *)mt_replay_kernel_3704, (const void *)mt_generate_kernel_3704, (const void *)mt_load_kernel_3704,
-     (const void *)mt_follow_kernel_3704},
-    {7496, (const void *)mt_replay_kernel_7496, (const void *)mt_generate_kernel_7496, (const void *)mt_load_kernel_7496,
-     (const void *)mt_follow_kernel_7496},
-    {60000, (const void *)mt_replay_kernel_60000, (const void *)mt_generate_kernel_60000, (const void *)mt_load_kernel_60000,
-     (const void *)mt_follow_kernel_60000},
+    {3600, (const void *)mt_replay_kernel_3600, (const void *)mt_generate_kernel_3600, (const void *)mt_load_kernel_3600,
+     (const void *)mt_follow_kernel_3600},
+    {7266, (const void *)mt_replay_kernel_7266, (const void *)mt_generate_kernel_7266, (const void *)mt_load_kernel_7266,
+     (const void *)mt_follow_kernel_7266},
+    {2097152, (const void *)mt_replay_kernel_2097152, (const void *)mt_generate_kernel_2097152, (const void *)mt_load_kernel_2097152,
+     (const void *)mt_follow_kernel_2097152},
 };
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
 
@@ -780,7 +780,13 @@ static int resume_class(int c) {
     while (n > c + 1 && class_lds(n) > (size_t)max_lds_bytes()) n--;
     return n;
 }
-constexpr size_t kMaxHbmDocs = 4096;  // documents per HBM-class launch (~6 MB of tables each)
+// documents per HBM-class launch: each holds its 2M-slot tables, cold records and output records
+// in device memory (~220 MB), so a launch is bounded to ~24 GB
+static size_t hbm_doc_bytes() {
+    const mt::Caps c = mt::class_caps(mt::kHbmSeg);
+    return (size_t)mt::make_layout(mt::kHbmSeg).bytes + (size_t)c.seg * mt::kColdPerSlot * 16 + (size_t)c.oe * sizeof(OutRec);
+}
+static const size_t kMaxHbmDocs = std::max<size_t>(1, ((size_t)24 << 30) / hbm_doc_bytes());
 static bool class_usable(int c) { return c < mt::kNumClasses && class_lds(c) <= (size_t)max_lds_bytes(); }
 
 static int max_lds_bytes() {
@@ -871,6 +877,9 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.prof = L.d_prof;
 #endif
     const void *fn = L.load ? kKernels[L.cls].load : kKernels[L.cls].replay;
+    if (getenv("MT_DEBUG_LAUNCHES"))
+        fprintf(stderr, "mtreplay: launch class %d docs %lld resumed %d level %d lds %zu load %d\n", mt::kClassSegs[L.cls],
+                (long long)n, (int)L.cksrc.size(), L.level, L.lds, (int)L.load);
     if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
     void *args[] = {&P};
     HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, s));
@@ -1355,7 +1364,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
         }
         for (auto &kv : groups) {
             Launch &G = kv.second;
-            // the HBM class holds ~6 MB of tables per document: bounded launches
+            // the HBM class holds ~220 MB per document: bounded launches
             const size_t chunk = G.cls == mt::kHbmClass ? kMaxHbmDocs : G.docs.size();
             for (size_t at = 0; at < G.docs.size(); at += chunk) {
                 Launch L;
@@ -1526,7 +1535,7 @@ static int load_doc(mt_batch *b, int64_t d) {
     return MT_OK;
 }
 
-static bool rec_is_marker(const OutRec &r) { return (r.blk & 0xFFFFu) == mt::kMarkerSlot; }
+static bool rec_is_marker(const OutRec &r) { return mt::out_is_end(r.blk); }
 static bool rec_removed(const OutRec &r) { return r.rseq != mt::kNoneSeq; }
 static bool rec_is_text(const OutRec &r) { return !(r.meta & mt::kMetaMarker); }
 
@@ -2131,10 +2140,10 @@ MT_API int mt_doc_dump(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t
     std::string tmp;
     for (const OutRec &r : b->c_recs) {
         if (rec_is_marker(r)) {
-            o += "  M blk=" + std::to_string(r.blk >> 16) + "\n";
+            o += "  M blk=" + std::to_string(r.blk & ~mt::kOutBlockEnd) + "\n";
             continue;
         }
-        o += "  S blk=" + std::to_string(r.blk >> 16) + " len=" + std::to_string(r.len) + " seq=" + std::to_string(r.seq) +
+        o += "  S blk=" + std::to_string(r.blk) + " len=" + std::to_string(r.len) + " seq=" + std::to_string(r.seq) +
              " cli=" + client_name(b, doc, mt::meta_cli(r.meta), tmp) +
              " rseq=" + std::to_string(rec_removed(r) ? r.rseq : -1) + " rcli=" +
              (rec_removed(r) ? client_name(b, doc, mt::meta_rcli(r.meta), tmp) : std::string("-")) +
@@ -2342,7 +2351,7 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
         work.erase(work.begin());
         const bool all = (int64_t)todo.size() == D;
         for (size_t at = 0; at < todo.size();) {
-            // the HBM class holds ~6 MB of tables per document: bounded launches
+            // the HBM class holds ~220 MB per document: bounded launches
             const size_t n = cls == mt::kHbmClass ? std::min(todo.size() - at, kMaxHbmDocs) : todo.size() - at;
             Launch L;
             L.cls = cls;

@@ -180,7 +180,7 @@ struct Tile {
     uint32_t len, meta, props, toff, blk, lastc;
     int32_t seq, rseq;
     __device__ __forceinline__ void load(const OutRec *rec, int32_t i, int32_t n, const uint16_t *text) {
-        uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, kMarkerSlot);
+        uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, kOutBlockEnd);
         if (i < n) {
             a = reinterpret_cast<const uint4 *>(rec + i)[0];
             b = reinterpret_cast<const uint4 *>(rec + i)[1];
@@ -193,7 +193,7 @@ struct Tile {
         toff = b.z;
         blk = b.w;
         uint32_t lc = 0;
-        if ((blk & 0xFFFFu) != kMarkerSlot && !(meta & kMetaMarker) && len > 0) lc = text[toff + len - 1];
+        if (!out_is_end(blk) && !(meta & kMetaMarker) && len > 0) lc = text[toff + len - 1];
         lastc = lc;
     }
     __device__ __forceinline__ Rec get(uint32_t l) const {
@@ -239,7 +239,7 @@ struct Doc {
           cli_n(cn), W{dst, 0}, mrow(mr) {}
 
     __device__ __forceinline__ static bool skipped(const Rec &r, int32_t min_seq) {
-        if ((r.blk & 0xFFFFu) == kMarkerSlot) return true;
+        if (out_is_end(r.blk)) return true;
         return r.rseq != kNoneSeq && r.rseq <= min_seq;
     }
 

@@ -12,6 +12,7 @@
  * non-collaborating local edit path that the reference's golden SnapshotV1 files
  * were generated with (sequence/src/test/generateSharedStrings.ts:24-97).
  */
+#include <limits.h>
 #include <pthread.h>
 #include <setjmp.h>
 #include <stdarg.h>
@@ -54,6 +55,9 @@ struct Block { /* MergeBlock / HierMergeBlock, mergeTree.ts:336-420 */
     int child_count;
     Node *children[MAX_NODES];
     int needs_scour; /* undefined / true / false (mergeTree.ts:63, 1279, 1438) */
+    /* upper bounds of the seq / removedSeq of every leaf below (UnassignedSequenceNumber counts as
+       +inf): a view with refSeq at or above both sees exactly cachedLength (block_partial_length) */
+    int max_seq, max_rseq;
     Block *all_next;
 };
 
@@ -130,6 +134,7 @@ static Block *make_block(mto_doc *d, int child_count) { /* MergeTree.makeBlock, 
     b->n.is_leaf = 0;
     b->child_count = child_count;
     b->needs_scour = SCOUR_UNDEF;
+    b->max_seq = b->max_rseq = INT_MAX; /* unknown until block_update */
     b->all_next = d->all_blocks;
     d->all_blocks = b;
     return b;
@@ -189,10 +194,33 @@ static int node_total_length(const Node *n) { /* mergeTree.ts:422-427 */
     return n->is_leaf ? local_net_length((const Seg *)n) : n->cached_length;
 }
 
+static int seq_bound(int seq) { return seq == UNASSIGNED_SEQ ? INT_MAX : seq; }
 static void block_update(Block *b) { /* mergeTree.ts:2748-2768 (cachedLength part) */
-    int len = 0;
-    for (int i = 0; i < b->child_count; i++) len += node_total_length(b->children[i]);
+    int len = 0, ms = INT_MIN, mr = INT_MIN;
+    for (int i = 0; i < b->child_count; i++) {
+        Node *c = b->children[i];
+        len += node_total_length(c);
+        if (c->is_leaf) {
+            const Seg *sg = (const Seg *)c;
+            if (seq_bound(sg->seq) > ms) ms = seq_bound(sg->seq);
+            if (sg->removed && seq_bound(sg->removed_seq) > mr) mr = seq_bound(sg->removed_seq);
+        } else {
+            const Block *cb = (const Block *)c;
+            if (cb->max_seq > ms) ms = cb->max_seq;
+            if (cb->max_rseq > mr) mr = cb->max_rseq;
+        }
+    }
     b->n.cached_length = len;
+    b->max_seq = ms;
+    b->max_rseq = mr;
+}
+/* raise the bounds on the path above a leaf whose seq / removedSeq was just set */
+static void bump_bounds(Seg *s) {
+    const int q = seq_bound(s->seq), r = s->removed ? seq_bound(s->removed_seq) : INT_MIN;
+    for (Block *b = s->n.parent; b; b = b->n.parent) {
+        if (q > b->max_seq) b->max_seq = q;
+        if (r > b->max_rseq) b->max_rseq = r;
+    }
 }
 
 static int seg_has_overlap(const Seg *s, int client) {
@@ -203,8 +231,14 @@ static int seg_has_overlap(const Seg *s, int client) {
 
 static int node_length(mto_doc *d, Node *node, int ref_seq, int client_id);
 
-/* PartialSequenceLengths.getPartialLength substitute: exact leaf sum of nodeLength */
+/* PartialSequenceLengths.getPartialLength substitute: exact leaf sum of nodeLength.  A subtree
+   whose every seq and removedSeq is at or below refSeq is seen exactly as the local view sees it
+   (visible, or removed), so its cachedLength is that sum (MTO_SLOW_LENGTHS=1 always recurses:
+   tests/test_oracle_golden.py checks both agree). */
+static int slow_lengths = -1;
 static int block_partial_length(mto_doc *d, Block *b, int ref_seq, int client_id) {
+    if (slow_lengths < 0) slow_lengths = getenv("MTO_SLOW_LENGTHS") != NULL;
+    if (!slow_lengths && b->max_seq <= ref_seq && b->max_rseq <= ref_seq) return b->n.cached_length;
     int len = 0;
     for (int i = 0; i < b->child_count; i++) len += node_length(d, b->children[i], ref_seq, client_id);
     return len;
@@ -715,6 +749,7 @@ static void insert_segments(mto_doc *d, int pos, Seg **segs, int n, int ref_seq,
         seg->client_id = client_id;
         ICtx ctx = {LEAF_INSERT, seg, 1};
         Block *sn = inserting_walk(d, d->root, insert_pos, ref_seq, client_id, seq, &ctx);
+        if (seg->n.parent) bump_bounds(seg);
         if (seg->n.parent == NULL)
             fail(d, MTO_INVALID_POS, "MergeTree insert failed: {\"currentSeq\":%d,\"minSeq\":%d,\"segSeq\":%d}",
                  d->cw.current_seq, d->cw.min_seq, seg->seq);
@@ -761,6 +796,7 @@ static int mark_removed(mto_doc *d, Seg *s, int pos, int r, int c, int st, int e
         s->removed_client = ctx->client_id;
         s->removed_seq = ctx->seq;
         s->removed = 1;
+        bump_bounds(s);
     }
     if (d->cw.collaborating) {
         if (s->removed_seq == UNASSIGNED_SEQ && ctx->client_id == d->cw.client_id) {

@@ -14,7 +14,7 @@ run() {
 }
 for step in "$@"; do
   case "$step" in
-    tests) run tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 300 python -u __graft_entry__.py smoke ;;
     bench) run bench 900 python -u bench.py --steps 3 --warmup 1 ;;
     bench2) run bench2 600 python -u bench.py --config 2 --steps 3 --warmup 1 ;;

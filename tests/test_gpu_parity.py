@@ -497,7 +497,33 @@ def test_segments_beyond_16_bit_lengths_move_to_the_hbm_class():
         b.ingest_messages(docs)
         b.run()
         classes = {li["seg_class"] for li in b.launches()}
-        assert 60000 in classes, b.launches()
+        assert 2097152 in classes, b.launches()
         for i in range(len(docs)):
             assert_doc_parity(b.doc(i), oracle[i])
         assert len(json.loads(b.doc(1).snapshot_v1()["header"])["segments"]) == 1  # merged past 65,535
+
+
+def test_giant_document_beyond_65k_segments():
+    """A document far beyond the LDS classes and 16-bit ids (>= 100k live segments; SURVEY §8d
+    config 4's tail) escalates through the ladder into the HBM class (2M slots, 32-bit slot and
+    block ids, epoch-tagged overlay) and stays bit-exact with the oracle."""
+    p = O.gen_params(360000, pct_insert=50, pct_remove=15, seed=4096)  # 35% annotate: props keep segments apart
+    ops, text, props, off = O.gen_batch(p, 1)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(1) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        b.set_clients(names)
+        b.ingest(ops, off, text, props)
+        b.run()
+        c = b.counters()
+        hbm = [li for li in b.launches() if li["seg_class"] == 2097152]
+        print(f"max slots {int(c['max_slots'][0])}; HBM class: {hbm[0]['ops']} ops in {hbm[0]['ms']:.1f} ms = "
+              f"{1e3 * hbm[0]['ms'] / max(1, hbm[0]['ops']):.2f} us/op")
+        assert b.doc(0).status == st[0] == 0
+        assert b.doc(0).digest() == int(dig[0])
+        assert hbm and hbm[0]["ops"] > 0
+        assert int(c["max_slots"][0]) >= 100000, int(c["max_slots"][0])
+        od = O.replay_doc(ops.copy(), text, props, t, names)
+        assert b.doc(0).get_text() == od.text()
+        assert b.doc(0).snapshot_v1() == od.snapshot_v1()

@@ -133,3 +133,38 @@ def test_snapshot_loader_rebuilds_golden_files(name):
     assert d.text() == want.text()
     assert json.loads(d.props_runs()) == json.loads(want.props_runs())
     assert d.snapshot_v1() == blobs
+
+
+_FARMS = [  # (n_ops, docs, kwargs) — text-only, config-3 mix, wide collab windows, markers-free farms
+    (1500, 6, dict(seed=0xC0FFEE)),
+    (1500, 6, dict(pct_insert=55, pct_remove=35, seed=0xBADC0DE)),
+    (1200, 6, dict(n_clients=24, max_lag=200, pct_insert=50, pct_remove=40, min_len=0, max_insert=3, seed=77)),
+    (3000, 3, dict(pct_insert=50, pct_remove=15, seed=2024)),
+]
+
+
+def _farm_digests():
+    out = []
+    for n, docs, kw in _FARMS:
+        p = O.gen_params(n, **kw)
+        ops, text, props, off = O.gen_batch(p, docs)
+        _, dig, st = O.replay_batch(ops, off, text, props, O.gen_tables(), O.gen_client_names(p.n_clients), n_threads=2)
+        out += [int(x) for x in dig] + [int(x) for x in st]
+    return out
+
+
+def test_oracle_subtree_shortcut_is_exact():
+    """The oracle's block lengths skip subtrees whose seqs are all at or below refSeq (their view
+    length is cachedLength); with MTO_SLOW_LENGTHS=1 every block length is the full recursive leaf
+    sum.  Both give identical final states on conflict farms, including wide collab windows."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    code = ("import json, sys; sys.path.insert(0, %r); import test_oracle_golden as T; "
+            "print(json.dumps(T._farm_digests()))") % str(Path(__file__).resolve().parent)
+    env = dict(os.environ, MTO_SLOW_LENGTHS="1")
+    slow = json.loads(subprocess.run([sys.executable, "-c", code], env=env, check=True, capture_output=True,
+                                     text=True, cwd=str(Path(__file__).resolve().parents[1])).stdout)
+    assert slow == _farm_digests()
