@@ -36,10 +36,11 @@ CONFIGS = {
     3: dict(docs=65536, ops=10000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35,
             workload="configs[2]: 65,536 docs x 10k ops per GPU, insert 55 / remove 35 / annotate 10, "
                      "minSeq advance + zamboni, 8 clients, refSeq lag<=32"),
-    4: dict(docs=16384, ops=200000, ops_min=1000, zipf_s=1.1, n_clients=8, max_lag=32, pct_insert=70, pct_remove=20,
-            workload="configs[3]: Zipf(s=1.1) document sizes by rank over [1k, 200k] ops (70/20/10 mix), "
-                     "16,384 docs per GPU, LPT-balanced across GPUs, largest documents through the LDS ladder "
-                     "and the HBM spill class"),
+    4: dict(docs=16384, ops=2000000, ops_min=1000, zipf_s=1.1, n_clients=8, max_lag=32, pct_insert=50, pct_remove=15,
+            workload="configs[3]: Zipf(s=1.1) document sizes by rank over [1k, 2M] ops (insert 50 / remove 15 / "
+                     "annotate 35: props keep segments apart, so the largest documents reach ~10^6 segments), "
+                     "16,384 docs per GPU, LPT-balanced across GPUs; the largest documents run the LDS ladder, "
+                     "then the HBM class (2M slots)"),
     5: dict(docs=131072, ops=2000, n_clients=8, max_lag=32, pct_insert=55, pct_remove=35, snapshot=True,
             workload="configs[4]: 1M docs over 8 GPUs (131,072 per GPU) x 2k ops (10% annotate), full replay + "
                      "SnapshotV1 of every doc on the GPU in each step, digests gathered to rank 0"),

@@ -38,7 +38,7 @@ for step in "$@"; do
     bench5) run bench5 900 python -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
     profsnap) run profsnap 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profsnap -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 2 --warmup 1 --no-cpu ;;
     bench4s) run bench4s 600 python -u bench.py --config 4 --docs 4096 --ops 20000 --steps 1 --warmup 0 --no-cpu ;;
-    bench4) run bench4 900 python -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu ;;
+    bench4) run bench4 1100 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     loadtests) run loadtests 300 python -u -m pytest tests/test_gpu_snapshot_load.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     cap848) run cap848 600 python -u bench.py --steps 1 --warmup 0 --no-cpu --seg-cap 848 ;;
     cap456) run cap456 600 python -u bench.py --steps 1 --warmup 0 --no-cpu --seg-cap 456 ;;
