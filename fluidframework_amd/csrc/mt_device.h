@@ -35,15 +35,19 @@ constexpr uint32_t kPoolOvlTag = 0x40000000u;  // header word of an overlap-list
 
 // value flags (mt_values.h kVal*): matchProperties of two interned values is class equality,
 // else membership of the pair in the exception list (both kValIrregular); kValUnknown: undecided
-constexpr uint8_t kVFalsy = 1u, kVIrregular = 2u, kVUnknown = 4u;
+// kVNum: `v += undefined` is NaN; kVNever: matches nothing (NaN, a consensus {value: undefined});
+// kVSeqM1: an object with own seq === -1 (consensus would update it in place)
+constexpr uint8_t kVFalsy = 1u, kVIrregular = 2u, kVUnknown = 4u, kVNum = 8u, kVNever = 16u, kVSeqM1 = 32u;
+// prop-set hash bits (mt_engine.hip props_extend): bit 0 every value regular, bit 1 a value matches nothing
+constexpr uint32_t kSetRegular = 1u, kSetNever = 2u;
 
 // device matchProperties of two values (R(a, b), mt_values.cpp): 1 match, 0 no, -1 undecided
 __device__ __forceinline__ int value_rel(uint32_t va, uint32_t vb, const uint32_t *vclass, const uint8_t *vflags,
                                          uint32_t n_values, const uint64_t *exc, uint32_t n_exc) {
-    if (va == vb) return 1;
-    if (va >= n_values || vb >= n_values) return 0;
-    if (vclass[va] == vclass[vb]) return 1;
+    if (va >= n_values || vb >= n_values) return va == vb ? 1 : 0;
     const uint32_t fa = vflags[va], fb = vflags[vb];
+    if ((fa | fb) & kVNever) return 0;  // NaN !== NaN
+    if (va == vb || vclass[va] == vclass[vb]) return 1;
     if ((fa | fb) & kVUnknown) return -1;
     if (!(fa & fb & kVIrregular)) return 0;
     const uint64_t key = (uint64_t)va << 32 | vb;
@@ -208,10 +212,11 @@ constexpr Layout make_layout(int seg) {
 
 // matchProperties / rewrite tables of the interned property values (device memory, one per batch)
 struct ValueTables {
-    const uint8_t *flags;  // per value id: bit0 = JS-falsy (rewrite semantics), bit1 irregular, bit2 unknown
+    const uint8_t *flags;  // per value id: kVFalsy (rewrite semantics), kVIrregular, kVUnknown, kVNum, kVNever, kVSeqM1
     const uint32_t *cls;   // per value id: structural matchProperties class (mt_values.cpp)
     const uint64_t *exc;   // sorted (u << 32 | v): values matching across classes
     uint32_t n_values, n_exc;
+    uint32_t nan_id;       // the NaN value (combine "incr"); 0xFFFFFFFF when the log has none
 };
 
 // kernel parameters

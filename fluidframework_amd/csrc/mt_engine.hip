@@ -1057,9 +1057,10 @@ struct Engine {
     // reject without reading the records.
     // matchProperties(a, b) (properties.ts:62-93) of two sets, a the earlier segment's
     MT_FI bool props_match(uint32_t a, uint32_t ha, uint32_t b, uint32_t hb) {
+        if (a == 0 || b == 0) return a == b;
+        if ((ha | hb) & kSetNever) return false;  // a value that matches nothing (NaN !== NaN)
         if (a == b) return true;
-        if (a == 0 || b == 0) return false;
-        if ((ha & hb & 1u) && ha != hb) return false;
+        if ((ha & hb & kSetRegular) && ha != hb) return false;
         const uint32_t na = pool[a], nb = pool[b];
         if (na != nb) return false;
         bool ok = true, unk = false;
@@ -1076,10 +1077,52 @@ struct Engine {
         return ballot(!ok) == 0;
     }
 
+    // combiningOp (segmentPropertiesManager.ts:96-101, properties.ts:26-60) per key, lane-parallel
+    // (an op's keys are distinct, so its keys do not see each other): the value to assign — a
+    // present key keeps its value (assigning it is the identity) except that "incr" makes a number
+    // / boolean / NaN NaN; an absent key gets the host's result (0: stays absent).  Lane i < nop
+    // holds key ok_k; keys / vals (scratch) hold the set's n pairs.  Returns true when the device
+    // cannot reproduce it (incr of a string / object, consensus updating a shared object in place,
+    // an undefined result): the document is MT_UNSUPPORTED.
+    MT_FI bool combine_values(uint32_t ckind, const mt_prop *op, uint32_t nop, uint32_t n, uint32_t ok_k,
+                              uint32_t &ok_v) {
+        // the result slot: value = an absent key's result, key = the NaN value for "incr"
+        // (mt_host.cpp rc_resolve_combine)
+        const mt_prop res = op[nop + 2];
+        const uint32_t nv = vt->n_values;
+        // lane j < n: the set's pair j; lane i < nop finds its key among them
+        const uint32_t kj = (uint32_t)lane < n ? scratch[lane] : MT_KEY_COMBINE;
+        const uint32_t vj = (uint32_t)lane < n ? scratch[64 + lane] : MT_VALUE_NULL;
+        uint32_t ev = MT_VALUE_NULL;
+        for (uint32_t j = 0; j < n; j++)
+            if (rdl(kj, (int)j) == ok_k) ev = rdl(vj, (int)j);
+        bool bad = false;
+        if ((uint32_t)lane < nop) {
+            if (ev != MT_VALUE_NULL) {
+                const uint32_t f = ev < nv ? vt->flags[ev] : 0u;
+                // incr: `v += undefined` is NaN for a number / boolean; a string or object would
+                // concatenate "undefined" (not modelled on the device).  consensus of an object
+                // with seq === -1 would update a shared object in place.
+                bad = ckind == MT_COMBINE_INCR ? (!(f & kVNum) || res.key >= nv)
+                                               : (ckind == MT_COMBINE_CONSENSUS && (f & kVSeqM1));
+                ok_v = ckind == MT_COMBINE_INCR ? res.key : ev;
+            } else {
+                ok_v = res.value;
+                bad = res.value != MT_VALUE_NULL && res.value >= nv;
+            }
+        }
+        return ballot(bad) != 0;
+    }
+
     // SegmentPropertiesManager.addProperties for a sequenced remote op (or insert-time props):
     // start from `old` (0 = undefined -> new empty map), apply rewrite then the op's pairs in
     // order (null deletes: properties.ts:95-116).  Returns the new set id (hash in hout).
-    MT_FI uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout) {
+    // ckind != 0: a combiningOp (segmentPropertiesManager.ts:96-101, properties.ts:26-60) — only
+    // the op's keys count; a key the set lacks gets `cres` (the host's combine of an undefined
+    // current value, mt_host.cpp rc_resolve_combine; 0 = stays absent), a key it has keeps its
+    // value, except that "incr" turns a number / boolean / NaN into NaN.
+    MT_FI uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout,
+                                uint32_t ckind = 0u) {
         uint32_t *keys = scratch;
         uint32_t *vals = scratch + 64;
         uint32_t n = old ? pool[old] : 0u;
@@ -1098,6 +1141,10 @@ struct Engine {
             ok_v = op[lane].value;
         }
         wsync();
+        if (ckind != MT_COMBINE_NONE && combine_values(ckind, op, nop, n, ok_k, ok_v)) {
+            set_fail(ST_UNSUPPORTED);
+            return 0;
+        }
         if (rewrite) {
             // delete existing keys whose new value is absent or falsy (segmentPropertiesManager.ts:70-80)
             bool keep = false;
@@ -1170,18 +1217,21 @@ struct Engine {
         uint32_t id = pool_top;
         pool_top += words;
         uint32_t h = 0;
-        bool irr = false;
+        bool irr = false, never = false;
         if ((uint32_t)lane < n) {
             uint32_t k = keys[lane], v = vals[lane];
             const bool known = v < vt->n_values;
+            const uint32_t f = known ? vt->flags[v] : 0u;
             h = hash_pair(k, known ? vt->cls[v] : 0xFFFFFFFFu - v);
-            irr = !known || (vt->flags[v] & (kVIrregular | kVUnknown));
+            never = (f & kVNever) != 0;
+            irr = !known || (f & (kVIrregular | kVUnknown | kVNever));
             pool[id + 2 + 2 * lane] = k;
             pool[id + 3 + 2 * lane] = v;
         }
-        // order-insensitive content hash (matchProperties ignores key order), bit 0 = regular
+        // order-insensitive content hash (matchProperties ignores key order), bit 0 = regular,
+        // bit 1 = a value that matches nothing (such a set does not even match itself)
         for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, kWave);
-        h = (rfl(h) & ~1u) | (ballot(irr) ? 0u : 1u);
+        h = (rfl(h) & ~(kSetRegular | kSetNever)) | (ballot(irr) ? 0u : kSetRegular) | (ballot(never) ? kSetNever : 0u);
         if (lane == 0) {
             pool[id] = n;
             pool[id + 1] = h;
@@ -1260,7 +1310,7 @@ struct Engine {
                 if ((structM >> k) & 1ull) {
                     const uint32_t pa = rdl(cr.x, h), pb = rdl(cr.x, k);
                     if ((acc <= kGranularity || lk <= kGranularity) &&
-                        (pa == pb || (pa && pb && props_match(pa, rfl(pool[pa + 1]), pb, rfl(pool[pb + 1]))))) {
+                        props_match(pa, pa ? rfl(pool[pa + 1]) : 0u, pb, pb ? rfl(pool[pb + 1]) : 0u)) {
                         mergeM |= 1ull << k;
                         acc += lk;
                         continue;
@@ -1943,7 +1993,8 @@ struct Engine {
                         nid = rdl(memo_new, m);
                         nh = rdl(memo_h, m);
                     } else {
-                        nid = props_extend(old, props_in + op.payload, op.payload_len, rewrite, nh);
+                        nid = props_extend(old, props_in + op.payload, op.payload_len, rewrite, nh,
+                                           MT_OPF_COMBINE(op.flags));
                         if (status) return;
                         if (memo_n < 64u) {
                             if ((uint32_t)lane == memo_n) {

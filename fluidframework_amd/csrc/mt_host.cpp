@@ -345,6 +345,10 @@ struct mt_batch {
     std::vector<uint8_t> value_flags;
     std::vector<uint32_t> value_class;  // structural matchProperties classes (mt_values.cpp)
     std::vector<uint64_t> value_exc;    // sorted cross-class matches (u << 32 | v)
+    // values [0, n_user_values) are the caller's table (mt_batch_set_tables); the ingest appends
+    // the results of combiningOps (combine_absent: NaN, consensus values, ...) after them
+    size_t n_user_values = 1;
+    uint32_t nan_id = 0xFFFFFFFFu;  // the derived NaN value (kValNever | kValNum), if any
     std::vector<std::string> clients;  // shared table
     std::unordered_map<int64_t, std::vector<std::string>> doc_clients;
     // log (device) + host mirror of the layout
@@ -549,6 +553,8 @@ MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_k
     }
     b->values.resize(n_values);
     b->value_flags.resize(n_values);
+    b->n_user_values = (size_t)n_values;
+    b->nan_id = 0xFFFFFFFFu;
     for (int i = 0; i < n_values; i++) {
         b->values[i] = (i == 0 || !values_json[i]) ? std::string("null") : std::string(values_json[i]);
         b->value_flags[i] = json_falsy(b->values[i]) ? mt::kValFalsy : 0;
@@ -601,7 +607,7 @@ static int ensure_tables(mt_batch *b) {
     }
     if (!b->d_vt) {
         mt::ValueTables vt{b->d_vflags, b->d_vclass, b->d_vexc, (uint32_t)b->value_flags.size(),
-                           (uint32_t)b->value_exc.size()};
+                           (uint32_t)b->value_exc.size(), b->nan_id};
         HIPCHK(dalloc(&b->d_vt, 1));
         HIPCHK(hipMemcpy(b->d_vt, &vt, sizeof vt, hipMemcpyHostToDevice));
     }
@@ -610,9 +616,10 @@ static int ensure_tables(mt_batch *b) {
 
 // matchProperties of two interned values, host side (same rule as value_rel on the device)
 static int host_value_rel(const mt_batch *b, uint32_t va, uint32_t vb) {
-    if (va == vb) return 1;
     const size_t n = b->value_class.size();
-    if (va >= n || vb >= n) return 0;
+    if (va >= n || vb >= n) return va == vb ? 1 : 0;
+    if ((b->value_flags[va] | b->value_flags[vb]) & mt::kValNever) return 0;  // NaN !== NaN
+    if (va == vb) return 1;
     if (b->value_class[va] == b->value_class[vb]) return 1;
     const uint8_t fa = b->value_flags[va], fb = b->value_flags[vb];
     if ((fa | fb) & mt::kValUnknown) return -1;
@@ -621,6 +628,94 @@ static int host_value_rel(const mt_batch *b, uint32_t va, uint32_t vb) {
 }
 
 static uint32_t align16u(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
+
+// The result slot of every combining annotate (mt_oplog.h): the value Properties.combine gives a
+// key that the segment does not have (segmentPropertiesManager.ts:93-98 with previousValue and
+// newValue undefined: mt::combine_absent).  Results that are not values of the caller's table
+// are appended to it (NaN and consensus objects match nothing: kValNever).  Keys the segment
+// does have are combined on the device (incr of a number / boolean / NaN is NaN — the slot's key
+// holds the NaN value's id for "incr" ops; consensus and other kinds keep the value).  h_props
+// stays empty when the log has no combining op.
+static void rc_resolve_combine(mt_batch *b, const mt_op *ops, int64_t N, const mt_prop *props, int64_t n_props,
+                               std::vector<mt_prop> &h_props) {
+    const size_t nu = b->n_user_values;
+    const bool had_derived = b->values.size() != nu;
+    bool any = false;
+    for (int64_t i = 0; i < N && !any; i++) any = ops[i].type == MT_OP_ANNOTATE && MT_OPF_COMBINE(ops[i].flags);
+    if (!any && !had_derived) return;
+    b->values.resize(nu);
+    b->value_flags.resize(nu);
+    for (uint8_t &f : b->value_flags) f &= mt::kValFalsy;  // value_relations derives the rest again
+    b->nan_id = 0xFFFFFFFFu;
+    if (any) {
+        h_props.assign(props, props + n_props);
+        std::unordered_map<std::string, uint32_t> ids;  // text -> id of the ordinary values
+        for (size_t v = 1; v < nu; v++) ids.emplace(b->values[v], (uint32_t)v);
+        auto text_of = [&](uint32_t v) -> const std::string * {
+            return v == MT_VALUE_UNDEFINED || v >= nu ? nullptr : &b->values[v];
+        };
+        auto append = [&](const std::string &t, uint8_t flags) {
+            b->values.push_back(t);
+            b->value_flags.push_back(flags);
+            return (uint32_t)(b->values.size() - 1);
+        };
+        // NaN (JSON text "null"): `v += undefined` of a number / boolean, also on the device
+        auto nan = [&]() {
+            if (b->nan_id == 0xFFFFFFFFu) b->nan_id = append("null", mt::kValFalsy | mt::kValNum | mt::kValNever);
+            return b->nan_id;
+        };
+        std::unordered_map<std::string, uint32_t> cons_ids;
+        for (int64_t i = 0; i < N; i++) {
+            const mt_op &o = ops[i];
+            const uint32_t kind = o.type == MT_OP_ANNOTATE ? MT_OPF_COMBINE(o.flags) : 0u;
+            if (!kind) continue;
+            mt_prop *x = h_props.data() + o.payload + o.payload_len;
+            if (kind == MT_COMBINE_INCR) x[2].key = nan();  // a present number / boolean becomes NaN
+            if (x[0].value != MT_VALUE_UNDEFINED && x[0].value >= nu) {
+                x[2].value = mt::kValueCombineFail;
+                continue;
+            }
+            std::string out;
+            const std::string nul = "null";
+            const std::string *def = x[0].value == 0 ? &nul : text_of(x[0].value);
+            const std::string *mn = x[1].value == 0 ? &nul : text_of(x[1].value);
+            uint32_t u = mt::kValueCombineFail;
+            switch (mt::combine_absent((int)kind, def, mn, o.seq, out)) {
+                case mt::kCombineValue: {
+                    if (out == "null") {
+                        u = 0;
+                        break;
+                    }
+                    auto it = ids.find(out);
+                    if (it == ids.end()) it = ids.emplace(out, append(out, json_falsy(out) ? mt::kValFalsy : 0)).first;
+                    u = it->second;
+                    break;
+                }
+                case mt::kCombineMin: u = x[1].value; break;
+                case mt::kCombineNaN: u = nan(); break;
+                case mt::kCombineConsensus: {
+                    auto it = cons_ids.find(out);
+                    if (it == cons_ids.end()) it = cons_ids.emplace(out, append(out, mt::kValNever)).first;
+                    u = it->second;
+                    break;
+                }
+                case mt::kCombineDelete: u = 0; break;
+                default: break;
+            }
+            x[2].value = u;
+        }
+    }
+    // the value tables are rebuilt (classes, flags) and uploaded again
+    b->value_class.clear();
+    (void)hipFree(b->d_vflags);
+    (void)hipFree(b->d_vclass);
+    (void)hipFree(b->d_vexc);
+    (void)hipFree(b->d_vt);
+    b->d_vflags = nullptr;
+    b->d_vclass = nullptr;
+    b->d_vexc = nullptr;
+    b->d_vt = nullptr;
+}
 
 MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_off, const uint16_t *text,
                            int64_t n_text, const mt_prop *props, int64_t n_props) {
@@ -662,7 +757,10 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
                 pay += o.payload_len;
             }
             if (o.type == MT_OP_ANNOTATE) {
-                if ((int64_t)o.payload + (int64_t)o.payload_len > n_props) return MT_ERR_ARG;
+                const int64_t extra = MT_OPF_COMBINE(o.flags) ? MT_COMBINE_RECORDS : 0;
+                if ((int64_t)o.payload + (int64_t)o.payload_len + extra > n_props) return MT_ERR_ARG;
+                for (int64_t x = 0; x < extra; x++)
+                    if (props[o.payload + o.payload_len + x].key != MT_KEY_COMBINE) return MT_ERR_ARG;
                 nprop_ops++;
                 prop_records += o.payload_len;
             }
@@ -684,6 +782,9 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         pool_cap[d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
         pbase += align16u(pc);
     }
+    // combiningOps: the value each one gives a key the segment does not have yet
+    std::vector<mt_prop> h_props;
+    rc_resolve_combine(b, ops, N, props, n_props, h_props);
     int rc = ensure_tables(b);
     if (rc) return rc;
     std::vector<mt_op> h_ops(ops, ops + N);
@@ -746,7 +847,9 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     HIPCHK(hipMemcpy(b->d_text_cap, b->h_text_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_pool_base, b->h_pool_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_pool_cap, b->h_pool_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
-    if (n_props > 0) HIPCHK(hipMemcpy(b->d_props, props, sizeof(mt_prop) * (size_t)n_props, hipMemcpyHostToDevice));
+    if (n_props > 0)
+        HIPCHK(hipMemcpy(b->d_props, h_props.empty() ? props : h_props.data(), sizeof(mt_prop) * (size_t)n_props,
+                         hipMemcpyHostToDevice));
     b->have_log = true;
     b->generated = false;
     return MT_OK;
@@ -1576,8 +1679,7 @@ static void props_json(mt_batch *b, uint32_t id, std::string &o) {
 // matchProperties(a, c) of two prop sets of the cached document (a the earlier segment's);
 // *undecided is set when a structural comparison could not be decided (kValUnknown)
 static bool props_match_host(mt_batch *b, uint32_t a, uint32_t c, bool *undecided) {
-    if (a == c) return true;
-    if (!a || !c) return false;
+    if (!a || !c) return a == c;
     const uint32_t *pa = b->c_pool.data() + a, *pc = b->c_pool.data() + c;
     if (pa[0] != pc[0]) return false;
     for (uint32_t i = 0; i < pa[0]; i++) {

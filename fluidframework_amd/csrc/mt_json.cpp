@@ -14,7 +14,8 @@
 //   * GROUP ops (type 3) flattened recursively, members chained with MT_OPF_GROUP_CONT;
 //   * insert seg: a string, {text, props?} or {marker: {refType}, props?}; a props object
 //     with keys -> prop records (JS key order: array indices ascending, then insertion order),
-//     {} -> an empty map; annotate props -> prop records, combiningOp only "rewrite";
+//     {} -> an empty map; annotate props -> prop records; combiningOp "rewrite" -> a flag, any
+//     other truthy combiningOp -> its kind + defaultValue / minValue records (mt_oplog.h);
 //   * values interned as JSON.stringify texts (JS number formatting, JS key order, lone
 //     surrogates escaped), JSON null -> value 0 (delete);
 //   * keys and values interned batch-wide in first-appearance order (document order, then
@@ -34,6 +35,7 @@
 #include <vector>
 
 #include "../../include/mtreplay.h"
+#include "mt_values.h"
 
 namespace {
 
@@ -431,6 +433,16 @@ void js_stringify(const Dom &D, int32_t n, std::string &o) {
     }
 }
 
+// JS ToBoolean of a parsed value
+bool truthy(const JNode &n) {
+    switch (n.type) {
+        case J_NULL: case J_FALSE: return false;
+        case J_NUM: return !(n.num == 0 || std::isnan(n.num));
+        case J_STR: return n.slen > 0;
+        default: return true;
+    }
+}
+
 // ---------------------------------------------------------------- per-document packing
 struct LocalDoc {
     std::vector<mt_op> ops;        // text / prop offsets local to this document
@@ -563,12 +575,17 @@ struct Packer1 {
             const int32_t p2 = D.member(op, "pos2");
             r.pos2 = p2 >= 0 ? as_int(D.nodes[p2]) : 0;
             if (tv == 2) {
+                // addProperties (segmentPropertiesManager.ts:53-54): "rewrite" when op.name is
+                // "rewrite", else any truthy combiningOp goes through Properties.combine
                 const int32_t cop = D.member(op, "combiningOp");
-                if (!D.is_null_or_absent(cop)) {
-                    const int32_t nm = D.member(cop, "name");
-                    if (nm < 0 || D.nodes[nm].type != J_STR || D.str_of(nm) != u"rewrite")
-                        return fail(MT_UNSUPPORTED, "combiningOp other than rewrite");
-                    r.flags |= MT_OPF_REWRITE;
+                uint32_t kind = MT_COMBINE_NONE;
+                if (cop >= 0 && truthy(D.nodes[cop])) {
+                    const int32_t nm = D.nodes[cop].type == J_OBJ ? D.member(cop, "name") : -1;
+                    const bool is_str = nm >= 0 && D.nodes[nm].type == J_STR;
+                    if (is_str && D.str_of(nm) == u"rewrite") r.flags |= MT_OPF_REWRITE;
+                    else if (is_str && D.str_of(nm) == u"incr") kind = MT_COMBINE_INCR;
+                    else if (is_str && D.str_of(nm) == u"consensus") kind = MT_COMBINE_CONSENSUS;
+                    else kind = MT_COMBINE_OTHER;
                 }
                 // annotateRange -> addProperties(op.props) iterates its keys: an object is required
                 const int32_t pr = D.member(op, "props");
@@ -577,6 +594,14 @@ struct Packer1 {
                 if (!prop_records(pr, &off, &n)) return false;
                 r.payload = off;
                 r.payload_len = n;
+                if (kind != MT_COMBINE_NONE) {  // mt_oplog.h: defaultValue, minValue, result slot
+                    r.flags |= MT_OPF_MAKE_COMBINE(kind);
+                    for (const char *f : {"defaultValue", "minValue"}) {
+                        const int32_t m = D.nodes[cop].type == J_OBJ ? D.member(cop, f) : -1;
+                        L.props.push_back(mt_prop{MT_KEY_COMBINE, m >= 0 ? value(m) : MT_VALUE_UNDEFINED});
+                    }
+                    L.props.push_back(mt_prop{MT_KEY_COMBINE, MT_VALUE_UNDEFINED});
+                }
             }
         } else {
             return fail(MT_UNSUPPORTED, "op type");
@@ -801,6 +826,11 @@ std::u16string from_utf8(const char *s) {
 
 }  // namespace
 
+namespace mt {
+void json_quote(std::string &o, const char16_t *s, size_t n) { quote(o, s, n); }
+void json_number(std::string &o, double v) { js_number(o, v); }
+}  // namespace mt
+
 struct mt_packed {
     std::vector<mt_op> ops;
     std::vector<int64_t> off;
@@ -894,7 +924,9 @@ MT_API int mt_pack_json(mt_packed **out, int64_t n_docs, const char *const *doc_
             P->ops.push_back(o);
         }
         P->text.insert(P->text.end(), L.text.begin(), L.text.end());
-        for (const mt_prop &q : L.props) P->props.push_back(mt_prop{kmap[q.key], vmap[q.value]});
+        for (const mt_prop &q : L.props)  // combiningOp records keep their sentinel key / undefined
+            P->props.push_back(mt_prop{q.key == MT_KEY_COMBINE ? q.key : kmap[q.key],
+                                       q.value == MT_VALUE_UNDEFINED ? q.value : vmap[q.value]});
         P->off.push_back((int64_t)P->ops.size());
         std::vector<std::string> names;
         for (const auto &n : L.names) names.push_back(wtf8(n));

@@ -298,12 +298,13 @@ struct Doc {
     // set, values compared structurally (value_rel: class equality or a listed exception); an
     // undecided comparison leaves the document to the host serializer
     __device__ __forceinline__ bool props_match(uint32_t a, uint32_t c) {
+        if (!a || !c) return a == c;
+        const uint32_t ha = pool[a + 1], hc = pool[c + 1];
+        if ((ha | hc) & kSetNever) return false;  // a value that matches nothing (NaN !== NaN)
         if (a == c) return true;
-        if (!a || !c) return false;
         const uint32_t na = pool[a], nc = pool[c];
         if (na != nc) return false;
-        const uint32_t ha = pool[a + 1], hc = pool[c + 1];
-        if ((ha & hc & 1u) && ha != hc) return false;
+        if ((ha & hc & kSetRegular) && ha != hc) return false;
         for (uint32_t base = 0; base < na; base += 64) {
             const uint32_t i = base + lane();
             int rel = 1;

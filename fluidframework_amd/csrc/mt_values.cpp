@@ -361,10 +361,14 @@ int value_relations(const std::vector<std::string> &values, std::vector<uint32_t
     std::vector<JV> jv(V);
     std::vector<uint8_t> parsed(V, 0);
     cls.assign(V, 0);
-    if (flags.size() != V) flags.assign(V, 0);
+    if (flags.size() != V) flags.resize(V, 0);
     exc.clear();
     Canon canon;
     for (size_t i = 0; i < V; i++) {
+        if (flags[i] & kValNever) {  // derived values that match nothing: a class of their own
+            cls[i] = canon.id_of("!" + std::to_string(i));
+            continue;
+        }
         Parser P{values[i].data(), values[i].data() + values[i].size()};
         JV v;
         if (P.value(v, 0)) {
@@ -376,6 +380,12 @@ int value_relations(const std::vector<std::string> &values, std::vector<uint32_t
         }
         // an unparsable text only ever equals itself (its own class)
         cls[i] = parsed[i] ? canon.of(jv[i]) : canon.id_of("?" + values[i]);
+        if (!parsed[i]) continue;
+        const JV &x = jv[i];
+        if (x.kind == JV::NUM || x.kind == JV::TRUE || x.kind == JV::FALSE) flags[i] |= kValNum;
+        if (x.kind == JV::OBJ)
+            for (size_t k = 0; k < x.keys.size(); k++)
+                if (x.keys[k] == u"seq" && x.vals[k].kind == JV::NUM && x.vals[k].num == -1) flags[i] |= kValSeqM1;
     }
     // exceptions: R(u, v) with v an object / array (a top-level null means "delete": never stored)
     std::vector<size_t> objs;
@@ -398,6 +408,125 @@ int value_relations(const std::vector<std::string> &values, std::vector<uint32_t
     }
     std::sort(exc.begin(), exc.end());
     return 0;
+}
+
+namespace {
+// JSON.stringify of a parsed value (key order: array indices ascending, then insertion order)
+void stringify(const JV &v, std::string &o) {
+    switch (v.kind) {
+        case JV::NUL: o += "null"; return;
+        case JV::TRUE: o += "true"; return;
+        case JV::FALSE: o += "false"; return;
+        case JV::NUM: json_number(o, v.num); return;
+        case JV::STR: json_quote(o, v.str.data(), v.str.size()); return;
+        case JV::ARR:
+            o.push_back('[');
+            for (size_t i = 0; i < v.vals.size(); i++) {
+                if (i) o.push_back(',');
+                stringify(v.vals[i], o);
+            }
+            o.push_back(']');
+            return;
+        case JV::OBJ: {
+            std::vector<std::pair<uint32_t, size_t>> idx;
+            std::vector<size_t> rest;
+            for (size_t i = 0; i < v.keys.size(); i++) {
+                uint32_t a;
+                if (array_index(v.keys[i], &a)) idx.emplace_back(a, i);
+                else rest.push_back(i);
+            }
+            std::sort(idx.begin(), idx.end());
+            std::vector<size_t> order;
+            for (auto &x : idx) order.push_back(x.second);
+            order.insert(order.end(), rest.begin(), rest.end());
+            o.push_back('{');
+            for (size_t j = 0; j < order.size(); j++) {
+                if (j) o.push_back(',');
+                json_quote(o, v.keys[order[j]].data(), v.keys[order[j]].size());
+                o.push_back(':');
+                stringify(v.vals[order[j]], o);
+            }
+            o.push_back('}');
+            return;
+        }
+    }
+}
+// String(v): "[object Object]" for a plain object, Array.prototype.join(",") for an array
+void to_string(const JV &v, u16s &o) {
+    switch (v.kind) {
+        case JV::NUL: o += u"null"; return;
+        case JV::TRUE: o += u"true"; return;
+        case JV::FALSE: o += u"false"; return;
+        case JV::NUM: {
+            std::string t;
+            json_number(t, v.num);
+            o.append(t.begin(), t.end());
+            return;
+        }
+        case JV::STR: o += v.str; return;
+        case JV::OBJ: o += u"[object Object]"; return;
+        case JV::ARR:
+            for (size_t i = 0; i < v.vals.size(); i++) {
+                if (i) o.push_back(u',');
+                if (v.vals[i].kind != JV::NUL) to_string(v.vals[i], o);
+            }
+            return;
+    }
+}
+bool parse(const std::string &t, JV &v) {
+    Parser P{t.data(), t.data() + t.size()};
+    if (!P.value(v, 0)) return false;
+    P.ws();
+    return P.p == P.e;
+}
+}  // namespace
+
+// combine kinds: include/mt_oplog.h mt_combine_kind (1 incr, 2 consensus, 3 other)
+CombineResult combine_absent(int kind, const std::string *def, const std::string *min, int32_t seq, std::string &out) {
+    JV d;
+    if (def && !parse(*def, d)) return kCombineUnsupported;
+    if (kind == 1) {  // incr: currentValue = defaultValue; currentValue += undefined
+        if (!def || d.kind == JV::NUL || d.kind == JV::TRUE || d.kind == JV::FALSE || d.kind == JV::NUM)
+            return kCombineNaN;  // NaN < minValue is false: no clamp
+        u16s r;
+        to_string(d, r);
+        r += u"undefined";
+        // `r < minValue`: r's ToNumber is NaN, so only a string comparison (minValue a string, or an
+        // object / array compared through its String()) can hold: UTF-16 code-unit order
+        JV m;
+        if (min && parse(*min, m) && truthy(&m) && (m.kind == JV::STR || m.kind == JV::OBJ || m.kind == JV::ARR)) {
+            u16s ms;
+            to_string(m, ms);
+            if (r < ms) return kCombineMin;
+        }
+        out.clear();
+        json_quote(out, r.data(), r.size());
+        return kCombineValue;
+    }
+    if (kind == 2) {  // consensus
+        if (!def) {
+            out = "{\"seq\":";
+            json_number(out, (double)seq);
+            out += "}";
+            return kCombineConsensus;
+        }
+        if (d.kind == JV::NUL) return kCombineUnsupported;  // TypeError: reading seq of null
+        if (d.kind == JV::OBJ)
+            for (size_t k = 0; k < d.keys.size(); k++)
+                if (d.keys[k] == u"seq" && d.vals[k].kind == JV::NUM && d.vals[k].num == -1) {
+                    d.vals[k].num = (double)seq;  // cv.seq = seq on the op's defaultValue object
+                    out.clear();
+                    stringify(d, out);
+                    return kCombineValue;
+                }
+        out = *def;
+        return kCombineValue;
+    }
+    // any other combiningOp: combine returns currentValue (= defaultValue)
+    if (!def) return kCombineUnsupported;  // properties[key] = undefined
+    if (d.kind == JV::NUL) return kCombineDelete;
+    out = *def;
+    return kCombineValue;
 }
 
 }  // namespace mt

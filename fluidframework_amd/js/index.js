@@ -30,6 +30,7 @@ function native() {
 
 const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 15;
 const OPF_GROUP_CONT = 1, OPF_MARKER = 2, OPF_HAS_PROPS = 4, OPF_REWRITE = 8;
+const COMBINE_INCR = 1, COMBINE_CONSENSUS = 2, COMBINE_OTHER = 3, KEY_COMBINE = 0xFFFFFFFF, VALUE_UNDEFINED = 0xFFFFFFFF;
 const MAX_INSERT_PROPS = 1023;
 const STATUS = ['OK', 'INVALID_POS', 'SEQ_ORDER', 'MSN_ORDER', 'UNSUPPORTED', 'BAD_INPUT', 'CAPACITY', 'INTERNAL'];
 
@@ -118,12 +119,23 @@ class Packer {
         } else if (t === OP_REMOVE || t === OP_ANNOTATE) {
             r.pos2 = (op.pos2 || 0) | 0;
             if (t === OP_ANNOTATE) {
-                if (op.combiningOp) {
-                    if (op.combiningOp.name !== 'rewrite') throw new UnsupportedOp('combiningOp other than rewrite');
-                    r.flags |= OPF_REWRITE;
+                // addProperties (segmentPropertiesManager.ts:53-54): "rewrite", or Properties.combine
+                // for any other truthy combiningOp (include/mt_oplog.h mt_combine_kind)
+                const cop = op.combiningOp;
+                let kind = 0;
+                if (cop) {
+                    if (cop.name === 'rewrite') r.flags |= OPF_REWRITE;
+                    else kind = cop.name === 'incr' ? COMBINE_INCR : cop.name === 'consensus' ? COMBINE_CONSENSUS : COMBINE_OTHER;
                 }
                 // annotateRange -> addProperties(op.props) iterates its keys: an object is required
                 [r.payload, r.payloadLen] = this.propRecords(op.props);
+                if (kind) {
+                    r.flags |= kind << 4;
+                    const c = (typeof cop === 'object' && !Array.isArray(cop)) ? cop : {};
+                    for (const f of ['defaultValue', 'minValue'])
+                        this.props.push(KEY_COMBINE, Object.prototype.hasOwnProperty.call(c, f) ? this.value(c[f]) : VALUE_UNDEFINED);
+                    this.props.push(KEY_COMBINE, VALUE_UNDEFINED);  // result slot (filled by the library)
+                }
             }
         } else throw new UnsupportedOp(`op type ${t}`);
         return r;

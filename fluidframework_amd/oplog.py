@@ -34,14 +34,29 @@ assert OP_DTYPE.itemsize == 32
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 15
 OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
 MAX_INSERT_PROPS = 1023
+# combiningOp other than "rewrite" (include/mt_oplog.h mt_combine_kind): annotate flags bits 4-5,
+# then three records {KEY_COMBINE, defaultValue}, {KEY_COMBINE, minValue}, {KEY_COMBINE, result slot}
+COMBINE_INCR, COMBINE_CONSENSUS, COMBINE_OTHER = 1, 2, 3
+KEY_COMBINE = VALUE_UNDEFINED = 0xFFFFFFFF
 
 
 MAX_CLIENTS = 254  # short ids 0..253 (include/mt_oplog.h MT_MAX_CLIENTS; 254 / 255 are sentinels)
 
 
 class UnsupportedOp(ValueError):
-    """An op shape outside the observer replay path (relative positions, registers,
-    combining ops other than "rewrite")."""
+    """An op shape outside the observer replay path (relative positions, registers, the
+    observer's own ops)."""
+
+
+def js_truthy(v) -> bool:
+    """JS ToBoolean of a JSON-parsed value."""
+    if v is None or isinstance(v, bool):
+        return bool(v)
+    if isinstance(v, (int, float)):
+        return v == v and v != 0
+    if isinstance(v, str):
+        return len(v) > 0
+    return True
 
 
 def js_stringify(value) -> str:
@@ -265,13 +280,25 @@ class Packer:
         elif t in (1, 2):
             r["pos2"] = int(op.get("pos2", 0))
             if t == 2:
+                # addProperties (segmentPropertiesManager.ts:53-54): "rewrite" when op.name is
+                # "rewrite", else any truthy combiningOp goes through Properties.combine
                 cop = op.get("combiningOp")
-                if cop is not None:
-                    if cop.get("name") != "rewrite":
-                        raise UnsupportedOp("combiningOp other than rewrite")
-                    r["flags"] |= OPF_REWRITE
+                kind = 0
+                if js_truthy(cop):
+                    name = cop.get("name") if isinstance(cop, dict) else None
+                    if isinstance(name, str) and name == "rewrite":
+                        r["flags"] |= OPF_REWRITE
+                    else:
+                        kind = {"incr": COMBINE_INCR, "consensus": COMBINE_CONSENSUS}.get(
+                            name if isinstance(name, str) else None, COMBINE_OTHER)
                 # annotateRange -> addProperties(op.props) iterates its keys: an object is required
                 r["payload"], r["payload_len"] = self._prop_records(op.get("props"))
+                if kind:
+                    r["flags"] |= kind << 4
+                    c = cop if isinstance(cop, dict) else {}
+                    for f in ("defaultValue", "minValue"):
+                        self._props.append((KEY_COMBINE, self._value(c[f]) if f in c else VALUE_UNDEFINED))
+                    self._props.append((KEY_COMBINE, VALUE_UNDEFINED))  # result slot (library)
         else:
             raise UnsupportedOp(f"op type {t}")
         return r

@@ -63,6 +63,25 @@ enum mt_op_flags {
     MT_OPF_HAS_PROPS = 4u,  /* insert seg carries a props object (may be empty {})     */
     MT_OPF_REWRITE = 8u     /* annotate with combiningOp {name:"rewrite"}              */
 };
+/* An annotate's combiningOp other than "rewrite" (properties.ts:26-60 combine, called by
+   SegmentPropertiesManager.addProperties, segmentPropertiesManager.ts:96-101): flags bits 4-5 of
+   an ANNOTATE record (insert records use bits 4-13 for their prop count).  The op's props keys
+   select the keys to combine; their values are ignored — the reference passes the local
+   `newValue` (still undefined) to combine at segmentPropertiesManager.ts:98, not newProps[key].
+   Three records follow the op's payload_len prop records, all with key MT_KEY_COMBINE:
+   defaultValue, minValue (value ids; MT_VALUE_UNDEFINED when absent) and a result slot that the
+   packers leave MT_VALUE_UNDEFINED and the library fills at ingest. */
+enum mt_combine_kind {
+    MT_COMBINE_NONE = 0,      /* no combiningOp (or "rewrite": MT_OPF_REWRITE)               */
+    MT_COMBINE_INCR = 1,      /* {name:"incr"}                                                */
+    MT_COMBINE_CONSENSUS = 2, /* {name:"consensus"}                                           */
+    MT_COMBINE_OTHER = 3      /* any other truthy combiningOp: combine keeps the current value */
+};
+#define MT_OPF_COMBINE(f) (((uint32_t)(f) >> 4) & 0x3u)
+#define MT_OPF_MAKE_COMBINE(kind) ((uint16_t)(((kind) & 0x3u) << 4))
+#define MT_COMBINE_RECORDS 3u
+#define MT_KEY_COMBINE 0xFFFFFFFFu
+#define MT_VALUE_UNDEFINED 0xFFFFFFFFu
 #define MT_OPF_BITS(f) ((f) & 0xFu)
 #define MT_OPF_NPROPS(f) (((uint32_t)(f) >> 4) & 0x3FFu)
 #define MT_OPF_MAKE(bits, nprops) ((uint16_t)((((nprops) & 0x3FFu) << 4) | ((bits) & 0xFu)))

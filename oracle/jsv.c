@@ -543,6 +543,27 @@ static int js_truthy(const jv *v) {
     }
 }
 
+int jv_truthy(const jv *v) { return js_truthy(v); }
+
+/* a fresh copy of a parsed value (what JSON.parse of the same text returns): objects and arrays
+   are new objects, primitives are immutable and shared */
+jv *jv_deep_clone(const jv *v) {
+    if (!v) return NULL;
+    if (v->kind == JV_ARR) {
+        jv *a = jv_new(JV_ARR);
+        jv_reserve(a, v->n);
+        for (int i = 0; i < v->n; i++) a->vals[i] = jv_deep_clone(v->vals[i]);
+        a->n = v->n;
+        return a;
+    }
+    if (v->kind == JV_OBJ) {
+        jv *o = jv_new(JV_OBJ);
+        for (int i = 0; i < v->n; i++) jv_obj_set(o, v->keys[i], v->klens[i], jv_deep_clone(v->vals[i]));
+        return o;
+    }
+    return jv_ref((jv *)v);
+}
+
 static int js_typeof_object(const jv *v) {
     return v && (v->kind == JV_OBJ || v->kind == JV_ARR || v->kind == JV_NULL);
 }

@@ -74,6 +74,11 @@ jv *jv_obj_clone(const jv *o);
 /* 1 if key is a canonical array index (0 .. 2^32-2) */
 int js_is_array_index(const u16 *k, int kl, uint32_t *idx);
 
+/* JS ToBoolean; NULL stands for undefined */
+int jv_truthy(const jv *v);
+/* JSON.parse(JSON text of v) for parsed values: new objects / arrays, primitives shared */
+jv *jv_deep_clone(const jv *v);
+
 /* Properties.matchProperties(a, b); NULL stands for undefined */
 int jv_match_properties(const jv *a, const jv *b);
 

@@ -13,6 +13,7 @@
  * were generated with (sequence/src/test/generateSharedStrings.ts:24-97).
  */
 #include <limits.h>
+#include <math.h>
 #include <pthread.h>
 #include <setjmp.h>
 #include <stdarg.h>
@@ -329,10 +330,125 @@ static HeapEnt heap_get(mto_doc *d) {
 }
 
 /* ------------------------------------------------------------------ properties */
+/* A combiningOp other than "rewrite" (include/mt_oplog.h mt_combine_kind) */
+typedef struct {
+    int kind;      /* MT_COMBINE_INCR / _CONSENSUS / _OTHER */
+    jv *def, *min; /* combiningOp.defaultValue / .minValue (the op's own objects); NULL = undefined */
+} CombineOp;
+
+/* growable UTF-16 buffer */
+typedef struct {
+    u16 *p;
+    int n, cap;
+} u16buf;
+static void ub_put(u16buf *b, const u16 *s, int n) {
+    if (b->n + n > b->cap) {
+        b->cap = (b->n + n) * 2 + 16;
+        b->p = (u16 *)realloc(b->p, sizeof(u16) * (size_t)b->cap);
+    }
+    if (n) memcpy(b->p + b->n, s, sizeof(u16) * (size_t)n);
+    b->n += n;
+}
+static void ub_ascii(u16buf *b, const char *s) {
+    while (*s) {
+        u16 c = (u16)(unsigned char)*s++;
+        ub_put(b, &c, 1);
+    }
+}
+/* String(v) of a JSON-parsed value: Number::toString, "[object Object]" for a plain object,
+   Array.prototype.join(",") for an array (null / undefined elements -> "") */
+static void js_to_string(const jv *v, u16buf *b) {
+    if (!v || v->kind == JV_UNDEF) { ub_ascii(b, "undefined"); return; }
+    switch (v->kind) {
+        case JV_NULL: ub_ascii(b, "null"); return;
+        case JV_TRUE: ub_ascii(b, "true"); return;
+        case JV_FALSE: ub_ascii(b, "false"); return;
+        case JV_NUM: {
+            sb t;
+            sb_init(&t);
+            js_number(&t, v->num);
+            sb_putc(&t, 0);
+            ub_ascii(b, t.p);
+            sb_free(&t);
+            return;
+        }
+        case JV_STR: ub_put(b, v->s, v->slen); return;
+        case JV_OBJ: ub_ascii(b, "[object Object]"); return;
+        default:
+            for (int i = 0; i < v->n; i++) {
+                if (i) ub_ascii(b, ",");
+                const jv *e = v->vals[i];
+                if (e && e->kind != JV_UNDEF && e->kind != JV_NULL) js_to_string(e, b);
+            }
+    }
+}
+/* `v += undefined` (properties.ts:34): ToPrimitive(v) is a string for strings, objects and
+   arrays (string concatenation), else both sides go through ToNumber and undefined is NaN */
+static jv *js_plus_undefined(const jv *v) {
+    if (!v || v->kind == JV_UNDEF || v->kind == JV_NULL || v->kind == JV_TRUE || v->kind == JV_FALSE ||
+        v->kind == JV_NUM)
+        return jv_new_num(NAN);
+    u16buf b = {NULL, 0, 0};
+    js_to_string(v, &b);
+    ub_ascii(&b, "undefined");
+    jv *r = jv_new_str(b.p, b.n);
+    free(b.p);
+    return r;
+}
+/* `a < b` with a = js_plus_undefined's result (properties.ts:36): a is NaN or a string ending in
+   "undefined", whose ToNumber is NaN, so only a string-to-string comparison (b a string, or an
+   object / array whose ToPrimitive is its String()) can hold: UTF-16 code-unit order */
+static int js_less_combined(const jv *a, const jv *b) {
+    if (a->kind != JV_STR || !b || (b->kind != JV_STR && b->kind != JV_OBJ && b->kind != JV_ARR)) return 0;
+    u16buf t = {NULL, 0, 0};
+    js_to_string(b, &t);
+    int n = a->slen < t.n ? a->slen : t.n, lt = a->slen < t.n;
+    for (int i = 0; i < n; i++)
+        if (a->s[i] != t.p[i]) {
+            lt = a->s[i] < t.p[i];
+            break;
+        }
+    free(t.p);
+    return lt;
+}
+/* Properties.combine(combiningInfo, currentValue, newValue, seq) (properties.ts:26-60) with
+   newValue undefined: segmentPropertiesManager.ts:98 passes its local `newValue`, not
+   newProps[key].  Returns a new reference, NULL for undefined.  A consensus value object with
+   seq === -1 is updated in place, so every segment sharing that object sees the new seq. */
+static jv *js_combine(mto_doc *d, const CombineOp *co, jv *cur, int seq) {
+    jv *cv = (cur && cur->kind != JV_UNDEF) ? cur : co->def;
+    if (cv && cv->kind == JV_UNDEF) cv = NULL;
+    switch (co->kind) {
+        case MT_COMBINE_INCR: {
+            jv *r = js_plus_undefined(cv);
+            if (co->min && jv_truthy(co->min) && js_less_combined(r, co->min)) {
+                jv_unref(r);
+                r = jv_ref(co->min);
+            }
+            return r;
+        }
+        case MT_COMBINE_CONSENSUS:
+            if (!cv) {
+                jv *o = jv_new(JV_OBJ); /* { value: newValue, seq } */
+                jv_obj_set_ascii(o, "value", jv_new(JV_UNDEF));
+                jv_obj_set_ascii(o, "seq", jv_new_num(seq));
+                return o;
+            }
+            if (cv->kind == JV_NULL) fail(d, MTO_UNSUPPORTED, "combine: TypeError reading seq of null");
+            if (cv->kind == JV_OBJ) {
+                const jv *sq = jv_obj_get_ascii(cv, "seq");
+                if (sq && sq->kind == JV_NUM && sq->num == -1) jv_obj_set_ascii(cv, "seq", jv_new_num(seq));
+            }
+            return jv_ref(cv);
+        default: return cv ? jv_ref(cv) : NULL;
+    }
+}
+
 /* SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111) for
-   seq !== UnassignedSequenceNumber and no pending local state; combiningOp limited to
-   undefined / {name:"rewrite"} (other combining ops: MTO_UNSUPPORTED). */
-static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewrite) {
+   seq !== UnassignedSequenceNumber and no pending local state.  `rewrite`: combiningOp
+   {name:"rewrite"}; `co`: any other combiningOp (NULL: none). */
+static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewrite, const CombineOp *co,
+                               int seq) {
     if (!s->props) s->props = jv_new(JV_OBJ);
     if (!new_props || new_props->kind != JV_OBJ) fail(d, MTO_BAD_INPUT, "props is not an object");
     if (rewrite) {
@@ -367,7 +483,15 @@ static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewr
         const u16 *k = new_props->keys[ord[i]];
         int kl = new_props->klens[ord[i]];
         jv *v = new_props->vals[ord[i]];
-        if (v->kind == JV_NULL) jv_obj_del(s->props, k, kl);
+        if (co && co->kind) { /* newValue = combine(op, previousValue, newValue, seq) */
+            jv *nv = js_combine(d, co, jv_obj_get(s->props, k, kl), seq);
+            if (nv && nv->kind == JV_NULL) {
+                jv_unref(nv);
+                jv_obj_del(s->props, k, kl);
+            } else {
+                jv_obj_set(s->props, k, kl, nv ? nv : jv_new(JV_UNDEF)); /* properties[key] = undefined */
+            }
+        } else if (v->kind == JV_NULL) jv_obj_del(s->props, k, kl);
         else jv_obj_set(s->props, k, kl, jv_ref(v));
     }
     free(ord);
@@ -379,7 +503,7 @@ static void seg_init_props(mto_doc *d, Seg *s, const jv *props) {
     if (props->kind == JV_FALSE || (props->kind == JV_NUM && props->num == 0) ||
         (props->kind == JV_STR && props->slen == 0))
         return;
-    seg_add_properties(d, s, props, 0);
+    seg_add_properties(d, s, props, 0, NULL, 0);
 }
 
 /* ------------------------------------------------------------------ split / append */
@@ -826,12 +950,13 @@ typedef struct {
     const jv *props;
     int rewrite;
     int seq;
+    const CombineOp *co;
 } AnnotateCtx;
 
 static int annotate_segment(mto_doc *d, Seg *s, int pos, int r, int c, int st, int en, void *vctx) {
     (void)pos; (void)r; (void)c; (void)st; (void)en;
     AnnotateCtx *ctx = (AnnotateCtx *)vctx;
-    seg_add_properties(d, s, ctx->props, ctx->rewrite);
+    seg_add_properties(d, s, ctx->props, ctx->rewrite, ctx->co, ctx->seq);
     if (d->cw.collaborating) {
         if (ctx->seq == UNASSIGNED_SEQ) fail(d, MTO_UNSUPPORTED, "pending local annotate");
         else add_to_lru_set(d, s, ctx->seq);
@@ -840,11 +965,11 @@ static int annotate_segment(mto_doc *d, Seg *s, int pos, int r, int c, int st, i
 }
 
 /* annotateRange, mergeTree.ts:2565-2605 */
-static void annotate_range(mto_doc *d, int start, int end, const jv *props, int rewrite, int ref_seq, int client_id,
-                           int seq) {
+static void annotate_range(mto_doc *d, int start, int end, const jv *props, int rewrite, const CombineOp *co,
+                           int ref_seq, int client_id, int seq) {
     ensure_interval_boundary(d, start, ref_seq, client_id);
     ensure_interval_boundary(d, end, ref_seq, client_id);
-    AnnotateCtx ctx = {props, rewrite, seq};
+    AnnotateCtx ctx = {props, rewrite, seq, co};
     MapActions a = {annotate_segment, NULL, &ctx};
     node_map(d, d->root, &a, 0, ref_seq, client_id, start, end, 1);
     if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
@@ -1024,14 +1149,26 @@ static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int
             const jv *props = jv_obj_get_ascii(op, "props");
             const jv *cop = jv_obj_get_ascii(op, "combiningOp");
             int rewrite = 0;
-            if (cop && cop->kind == JV_OBJ) {
-                const jv *nm = jv_obj_get_ascii(cop, "name");
+            CombineOp co = {MT_COMBINE_NONE, NULL, NULL};
+            if (jv_truthy(cop)) { /* segmentPropertiesManager.ts:53-54 */
+                const jv *nm = cop->kind == JV_OBJ ? jv_obj_get_ascii(cop, "name") : NULL;
                 static const u16 RW[7] = {'r', 'e', 'w', 'r', 'i', 't', 'e'};
-                if (nm && nm->kind == JV_STR && u16_eq(nm->s, nm->slen, RW, 7)) rewrite = 1;
-                else fail(d, MTO_UNSUPPORTED, "combiningOp other than rewrite");
+                static const u16 INCR[4] = {'i', 'n', 'c', 'r'};
+                static const u16 CONS[9] = {'c', 'o', 'n', 's', 'e', 'n', 's', 'u', 's'};
+                const int str = nm && nm->kind == JV_STR;
+                if (str && u16_eq(nm->s, nm->slen, RW, 7)) rewrite = 1;
+                else {
+                    co.kind = str && u16_eq(nm->s, nm->slen, INCR, 4)   ? MT_COMBINE_INCR
+                              : str && u16_eq(nm->s, nm->slen, CONS, 9) ? MT_COMBINE_CONSENSUS
+                                                                        : MT_COMBINE_OTHER;
+                    if (cop->kind == JV_OBJ) {
+                        co.def = jv_obj_get_ascii(cop, "defaultValue");
+                        co.min = jv_obj_get_ascii(cop, "minValue");
+                    }
+                }
             }
             if (!has2) pos2 = 0;
-            annotate_range(d, pos1, pos2, props, rewrite, ref_seq, short_id, seq);
+            annotate_range(d, pos1, pos2, props, rewrite, co.kind ? &co : NULL, ref_seq, short_id, seq);
             complete_remote_op(d, seq, msn);
             break;
         }
@@ -1255,7 +1392,7 @@ int mto_annotate_local_json(mto_doc *d, int start, int end, const char *props_js
     if (start < 0 || start >= len || end <= start) fail(d, MTO_INVALID_POS, "InvalidOpRange");
     jv *props = jv_parse(props_json, strlen(props_json));
     if (!props) fail(d, MTO_BAD_INPUT, "props");
-    annotate_range(d, start, end, props, 0, d->cw.current_seq, d->cw.client_id, UNIVERSAL_SEQ);
+    annotate_range(d, start, end, props, 0, NULL, d->cw.current_seq, d->cw.client_id, UNIVERSAL_SEQ);
     jv_unref(props);
     UNGUARD(d);
     return d->status;
@@ -1862,6 +1999,13 @@ void mto_tables_free(mto_tables *t) {
     free(t);
 }
 
+/* a value of a packed record as the message's JSON.parse would give it: objects are per-op objects
+   (consensus may update one in place), so they are copied, not shared through the table */
+static jv *value_from_record(mto_doc *d, uint32_t v, const mto_tables *t) {
+    if (v == MT_VALUE_UNDEFINED) return NULL;
+    if ((int)v >= t->n_values) fail(d, MTO_BAD_INPUT, "prop id out of range");
+    return jv_deep_clone(t->values[v]);
+}
 static jv *props_from_records(mto_doc *d, const mt_prop *p, uint32_t n, const mto_tables *t) {
     jv *o = jv_new(JV_OBJ);
     for (uint32_t i = 0; i < n; i++) {
@@ -1869,7 +2013,7 @@ static jv *props_from_records(mto_doc *d, const mt_prop *p, uint32_t n, const mt
             jv_unref(o);
             fail(d, MTO_BAD_INPUT, "prop id out of range");
         }
-        jv_obj_set(o, t->keys16[p[i].key], t->keylen16[p[i].key], jv_ref(t->values[p[i].value]));
+        jv_obj_set(o, t->keys16[p[i].key], t->keylen16[p[i].key], value_from_record(d, p[i].value, t));
     }
     return o;
 }
@@ -1892,7 +2036,7 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
             else s = new_text_seg(d, text + op->payload, (int)op->payload_len);
             if (bits & MT_OPF_HAS_PROPS) {
                 jv *pr = props_from_records(d, props + op->pos2, MT_OPF_NPROPS(op->flags), t);
-                seg_add_properties(d, s, pr, 0);
+                seg_add_properties(d, s, pr, 0, NULL, 0);
                 jv_unref(pr);
             }
             insert_segment(d, op->pos1, s, op->ref_seq, sid, op->seq);
@@ -1905,8 +2049,21 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
             break;
         case MT_OP_ANNOTATE: {
             jv *pr = props_from_records(d, props + op->payload, op->payload_len, t);
-            annotate_range(d, op->pos1, op->pos2, pr, (bits & MT_OPF_REWRITE) ? 1 : 0, op->ref_seq, sid, op->seq);
+            CombineOp co = {(int)MT_OPF_COMBINE(op->flags), NULL, NULL};
+            if (co.kind) { /* defaultValue, minValue records after the props (mt_oplog.h) */
+                const mt_prop *x = props + op->payload + op->payload_len;
+                if (x[0].key != MT_KEY_COMBINE || x[1].key != MT_KEY_COMBINE) {
+                    jv_unref(pr);
+                    fail(d, MTO_BAD_INPUT, "combiningOp records");
+                }
+                co.def = value_from_record(d, x[0].value, t);
+                co.min = value_from_record(d, x[1].value, t);
+            }
+            annotate_range(d, op->pos1, op->pos2, pr, (bits & MT_OPF_REWRITE) ? 1 : 0, co.kind ? &co : NULL,
+                           op->ref_seq, sid, op->seq);
             jv_unref(pr);
+            jv_unref(co.def);
+            jv_unref(co.min);
             complete_remote_op(d, op->seq, op->msn);
             break;
         }

@@ -1,0 +1,99 @@
+"""Op logs with combiningOp annotates (properties.ts:26-60, segmentPropertiesManager.ts:96-101),
+shared by the CPU packer / oracle tests and the GPU parity tests."""
+import json
+import random
+
+import oracle_ffi as O
+
+
+def _msg(c, s, r, contents, msn=0):
+    return {"clientId": c, "sequenceNumber": s, "referenceSequenceNumber": r, "minimumSequenceNumber": msn,
+            "type": "op", "contents": contents}
+
+
+def combine_farm(n_ops, seed, n_clients=6, lag=16):
+    """A valid conflict-farm log whose annotates use combiningOps (properties.ts:26-60) next to plain
+    and "rewrite" annotates: "incr" (numeric defaults, keys holding numbers -> NaN), "consensus"
+    (absent keys -> {value: undefined, seq} or the defaultValue with seq -1 updated), any other
+    name (keeps the value, absent -> defaultValue).  Keys are typed so that every combine stays on
+    the device's path (incr never meets a string)."""
+    rnd = random.Random(seed)
+    names = [f"w{i}" for i in range(n_clients)]
+    model = O.Doc()
+    model.start_collab("readonly")
+    short, last_ref, msgs = {}, {}, []
+    for k in range(1, n_ops + 1):
+        c = names[rnd.randrange(n_clients)]
+        ref = max(last_ref.get(c, 0), k - 1 - rnd.randrange(lag + 1))
+        last_ref[c] = ref
+        msn = min(last_ref.values()) if len(last_ref) == n_clients else 0
+        sid = short.get(c, len(short) + 1)
+        n = model.view_length(ref, sid)
+        u = rnd.randrange(100)
+        if n < 4 or u < 45:
+            seg = "".join(rnd.choice("abcdef\n") for _ in range(rnd.randint(1, 5)))
+            if rnd.random() < 0.2:
+                seg = {"text": seg, "props": {"n": rnd.randrange(3)}}
+            contents = {"type": 0, "pos1": rnd.randrange(n + 1), "seg": seg}
+        else:
+            a = rnd.randrange(n)
+            b = min(n, a + 1 + rnd.randrange(6))
+            if u < 70:
+                contents = {"type": 1, "pos1": a, "pos2": b}
+            else:
+                v = rnd.randrange(8)
+                if v == 0:
+                    contents = {"type": 2, "pos1": a, "pos2": b, "props": {"n": rnd.randrange(3), "k": "x"}}
+                elif v == 1:
+                    cop = {"name": "incr"}
+                    if rnd.random() < 0.5:
+                        cop["defaultValue"] = rnd.randrange(-2, 3)
+                    if rnd.random() < 0.3:
+                        cop["minValue"] = 1
+                    contents = {"type": 2, "pos1": a, "pos2": b, "props": {"n": 1}, "combiningOp": cop}
+                elif v == 2:
+                    cop = {"name": "consensus"}
+                    r = rnd.random()
+                    if r < 0.3:
+                        cop["defaultValue"] = {"value": rnd.randrange(3), "seq": -1}
+                    elif r < 0.5:
+                        cop["defaultValue"] = rnd.choice(["d", 7, True])
+                    contents = {"type": 2, "pos1": a, "pos2": b, "props": {"c": 0}, "combiningOp": cop}
+                elif v == 3:
+                    contents = {"type": 2, "pos1": a, "pos2": b, "props": {"o": None},
+                                "combiningOp": {"name": "keep", "defaultValue": rnd.choice(["p", 2, None])}}
+                elif v == 4:
+                    contents = {"type": 2, "pos1": a, "pos2": b, "props": {"k": rnd.choice(["x", "y"])},
+                                "combiningOp": {"name": "rewrite"}}
+                else:
+                    contents = {"type": 2, "pos1": a, "pos2": b, "props": {"k": rnd.choice(["x", "y", None])}}
+        m = _msg(c, k, ref, contents, msn)
+        assert model.apply_msg(json.dumps(m)) == 0, model.error()
+        short.setdefault(c, len(short) + 1)
+        msgs.append(m)
+    return msgs
+
+
+COMBINE_DOCS = [
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "hello world", "props": {"n": 5, "s": "ab"}}}),
+     _msg("B", 2, 1, {"type": 2, "pos1": 0, "pos2": 5, "props": {"n": 1, "z": None},
+                      "combiningOp": {"name": "incr", "defaultValue": 2, "minValue": 3}}),
+     _msg("A", 3, 2, {"type": 2, "pos1": 3, "pos2": 8, "props": {"c": 1, "d": 1},
+                      "combiningOp": {"name": "consensus", "defaultValue": {"value": 7, "seq": -1}}}, 1),
+     _msg("B", 4, 3, {"type": 2, "pos1": 6, "pos2": 11, "props": {"e": 1}, "combiningOp": {"name": "consensus"}}, 2),
+     _msg("A", 5, 4, {"type": 2, "pos1": 0, "pos2": 11, "props": {"q": 1}, "combiningOp": {"name": "zzz", "defaultValue": "dv"}}, 3),
+     _msg("A", 6, 5, {"type": 0, "pos1": 11, "seg": "!"}, 5)],
+    # incr of an absent key with a string default: "<default>undefined", clamped to a larger string minValue
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abcdef"}),
+     _msg("A", 2, 1, {"type": 2, "pos1": 0, "pos2": 3, "props": {"s": 0},
+                      "combiningOp": {"name": "incr", "defaultValue": "a", "minValue": "b"}}),
+     _msg("A", 3, 2, {"type": 2, "pos1": 3, "pos2": 6, "props": {"s": 0},
+                      "combiningOp": {"name": "incr", "defaultValue": "c", "minValue": "b"}}, 2)],
+    # NaN never matches, not even itself: the halves of a split stay apart after zamboni
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "abcdefgh", "props": {"n": 1}}}),
+     _msg("A", 2, 1, {"type": 2, "pos1": 2, "pos2": 5, "props": {"n": 0}, "combiningOp": {"name": "incr"}}),
+     _msg("A", 3, 2, {"type": 2, "pos1": 0, "pos2": 8, "props": {"n": 0}, "combiningOp": {"name": "incr"}}, 2),
+     _msg("A", 4, 3, {"type": 0, "pos1": 8, "seg": "z"}, 3),
+     _msg("A", 5, 4, {"type": 0, "pos1": 9, "seg": "y"}, 4)],
+]
+

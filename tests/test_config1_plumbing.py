@@ -95,3 +95,26 @@ def test_config1_node_packer_is_byte_identical(farm, tmp_path):
     assert meta["off"] == pb.doc_op_off.tolist()
     node = _replay_packed(pb)
     assert node.digest() == ref.digest()
+
+
+@pytest.mark.skipif(NODE is None, reason="node not available")
+def test_node_packer_combining_ops_byte_identical(tmp_path):
+    """The Node packer's combiningOp records equal the Python packer's (include/mt_oplog.h)."""
+    from combine_logs import COMBINE_DOCS, combine_farm
+
+    docs = COMBINE_DOCS + [combine_farm(300, seed=3)]
+    src = tmp_path / "msgs.json"
+    src.write_text(json.dumps(docs))
+    code = ("const {Packer}=require('./fluidframework_amd/js');const fs=require('fs');"
+            f"const docs=JSON.parse(fs.readFileSync({json.dumps(str(src))},'utf8'));const p=new Packer();"
+            "for(const d of docs)p.addDocument(d);const r=p.finish();"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'ops.bin'))},r.ops);"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'props.bin'))},Buffer.from(r.props.buffer));"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'meta.json'))},JSON.stringify({{values:r.values}}));")
+    r = subprocess.run([NODE, "-e", code], capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    pb = oplog.pack_documents(docs)
+    assert np.frombuffer((tmp_path / "ops.bin").read_bytes(), oplog.OP_DTYPE).tobytes() == pb.ops.tobytes()
+    assert np.frombuffer((tmp_path / "props.bin").read_bytes(), oplog.PROP_DTYPE).tobytes() == pb.props.tobytes()
+    assert json.loads((tmp_path / "meta.json").read_text())["values"] == pb.values
+

@@ -13,6 +13,7 @@ import pytest
 import oracle_ffi as O
 import fluidframework_amd as fa
 from fluidframework_amd import oplog
+from combine_logs import COMBINE_DOCS, combine_farm
 
 pytestmark = pytest.mark.gpu
 
@@ -527,3 +528,53 @@ def test_giant_document_beyond_65k_segments():
         od = O.replay_doc(ops.copy(), text, props, t, names)
         assert b.doc(0).get_text() == od.text()
         assert b.doc(0).snapshot_v1() == od.snapshot_v1()
+
+
+def test_combining_ops_match_oracle():
+    """combiningOp "incr" / "consensus" / other names with the reference's quirk (segmentPropertiesManager.ts:98
+    passes the still-undefined local `newValue` to combine, so the op's values are ignored; incr of a
+    number is NaN, serialized as null and matching nothing).  GPU == oracle on text, property runs, the
+    segment table (zamboni merges) and SnapshotV1 (host and GPU serializers)."""
+    docs = COMBINE_DOCS + [combine_farm(1500, seed=s) for s in (1, 2, 3)]
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        b.snapshots()
+        for i in range(len(docs)):
+            assert b.doc(i).status == 0, (i, fa.status_string(b.doc(i).status))
+            assert_doc_parity(b.doc(i), oracle[i])
+            assert b.doc(i).snapshot_v1(device=True) == oracle[i].snapshot_v1(), i
+        nan_doc = json.loads(b.doc(2).snapshot_v1()["header"])
+        assert nan_doc["segmentCount"] >= 3, nan_doc  # NaN-valued halves are never coalesced
+    with fa.ReplayBatch(len(docs), seg_cap=64) as b:  # through checkpoint / resume
+        b.ingest_messages(docs)
+        b.run()
+        for i in range(len(docs)):
+            assert_doc_parity(b.doc(i), oracle[i], full=False)
+
+
+def test_combining_ops_outside_the_device_path_are_flagged():
+    """Combines the device does not model are MT_UNSUPPORTED, never silently different: incr of a key
+    holding a string (string concatenation), consensus over an object with seq -1 set by a plain
+    annotate (the reference updates that shared object in place), an "other" combiningOp without a
+    defaultValue on an absent key (a key holding undefined).  consensus of an absent key with a null
+    defaultValue throws in the reference (the oracle fails too)."""
+    docs = [
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "abc", "props": {"n": "s"}}}),
+         _msg("A", 2, 1, {"type": 2, "pos1": 0, "pos2": 3, "props": {"n": 1}, "combiningOp": {"name": "incr"}})],
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"}),
+         _msg("A", 2, 1, {"type": 2, "pos1": 0, "pos2": 3, "props": {"c": {"seq": -1}}}),
+         _msg("A", 3, 2, {"type": 2, "pos1": 1, "pos2": 2, "props": {"c": 0}, "combiningOp": {"name": "consensus"}})],
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"}),
+         _msg("A", 2, 1, {"type": 2, "pos1": 0, "pos2": 3, "props": {"c": 0}, "combiningOp": {"name": "other"}})],
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"}),
+         _msg("A", 2, 1, {"type": 2, "pos1": 0, "pos2": 3, "props": {"c": 0},
+                          "combiningOp": {"name": "consensus", "defaultValue": None}})],
+    ]
+    oracle = oracle_docs_from_messages(docs)
+    assert [od.status for od in oracle] == [0, 0, 0, fa.MT_UNSUPPORTED]
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        assert [b.doc(i).status for i in range(len(docs))] == [fa.MT_UNSUPPORTED] * len(docs)

@@ -124,3 +124,29 @@ def test_unsupported_and_malformed_logs_fail_with_the_document_index():
     with pytest.raises(MtError) as e:
         PackedJson([json.dumps(own)])
     assert e.value.code == MT_UNSUPPORTED
+
+
+def test_combining_ops_pack_identically():
+    """combiningOp kinds + defaultValue / minValue records (include/mt_oplog.h mt_combine_kind)."""
+    from combine_logs import COMBINE_DOCS, combine_farm
+
+    _assert_same(COMBINE_DOCS + [combine_farm(400, seed=5)], n_threads=2)
+
+
+def test_oracle_packed_combine_matches_json_replay():
+    """The oracle's packed path (defaultValue / minValue from the records, values re-created per op
+    as JSON.parse would) replays combining ops exactly like its JSON path."""
+    from combine_logs import COMBINE_DOCS, combine_farm
+
+    docs = COMBINE_DOCS + [combine_farm(600, seed=9)]
+    pb = oplog.pack_documents(docs)
+    t = O.Tables(pb.keys, pb.values)
+    for i, msgs in enumerate(docs):
+        ref = O.Doc()
+        ref.start_collab("readonly")
+        for m in msgs:
+            assert ref.apply_msg(json.dumps(m)) == 0, ref.error
+        a, e = pb.doc_op_off[i], pb.doc_op_off[i + 1]
+        got = O.replay_doc(pb.ops[a:e].copy(), pb.text, pb.props, t, pb.clients[i])
+        assert got.status == 0, got.error
+        assert got.digest() == ref.digest() and got.props_runs() == ref.props_runs()

@@ -47,7 +47,16 @@ def test_replay_kernel_fits_four_waves_per_simd(seg, tmp_path):
     k = _kernels(_notes(obj, tmp_path))
     r = k[f"mt_replay_kernel_{seg}"]
     assert r["vgpr_count"] <= 128, r
-    # at most a couple of dwords of scratch (a spill outside the per-op loop); a real VGPR
-    # overflow spills hundreds of bytes
-    assert r["private_segment_fixed_size"] <= 16, r
+    # no spill traffic: a real VGPR overflow spills hundreds of bytes and shows up as scratch
+    # instructions; a few dwords of reserved (unused) private segment are tolerated
+    assert r["private_segment_fixed_size"] <= 64, r
+    assert _scratch_insts(tmp_path / (obj.stem + ".co"), f"mt_replay_kernel_{seg}") == 0
     assert f"mt_follow_kernel_{seg}" in k
+
+
+def _scratch_insts(co: Path, kernel: str) -> int:
+    """scratch loads / stores in `kernel`'s code (llvm-objdump of the code object _notes unbundled)"""
+    dis = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], check=True, capture_output=True,
+                         text=True).stdout
+    body = dis.split(f"<{kernel}>:", 1)[1].split("\n\n", 1)[0]
+    return len(re.findall(r"\bscratch_(?:load|store)", body))
