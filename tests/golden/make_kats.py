@@ -44,6 +44,91 @@ def hello_world():
     return [msg("local", i + 1, i, ins(i, ch)) for i, ch in enumerate("hello world")]
 
 
+def inserting_walk_kats():
+    """MT/test/mergeTree.insertingWalk.spec.ts:26-257: three tree shapes — one segment "hello world";
+    a full single layer (MaxNodesInBlock - 1 = 7 leaves "0".."6"); 32 leaves "0".."31" with the first
+    and last quarter of the text removed — and an insert of "a" at the beginning, the end and
+    Math.round(...) "middle" of each; expected text `a${t}`, `${t}a`, t[:m] + "a" + t[m:]
+    (:206, :225, :244-248).  The spec builds the trees with local edits at
+    UniversalSequenceNumber; here the same edits arrive as sequenced ops of a "builder" client (MSN
+    0: no zamboni, every segment stays a leaf) and the insert is a remote op of a "writer" that has
+    seen them all.  tests/test_oracle_golden.py also rebuilds the spec's exact trees through the
+    oracle's local path and checks the same answers."""
+    out = []
+    shapes = []
+    # single segment tree (:27-50)
+    t = "hello world"
+    shapes.append(("single_segment", [ins(0, t)], t, int(len(t) / 2 + 0.5)))
+    # full single layer tree (:51-102): "0" then appends "1".."6"
+    edits, t = [], ""
+    for i in range(7):
+        edits.append(ins(len(t), str(i)))
+        t += str(i)
+    shapes.append(("full_single_layer", edits, t, 4))  # Math.round(MaxNodesInBlock / 2)
+    # tree with remove segments (:103-156): "0".."31" appended, remove = Math.round(len / 4) from the
+    # start, then the same count from the end of what is left
+    edits, t = [], ""
+    for i in range(32):
+        edits.append(ins(len(t), str(i)))
+        t += str(i)
+    r = int(len(t) / 4 + 0.5)
+    edits.append(rem(0, r))
+    t = t[r:]
+    edits.append(rem(len(t) - r, len(t)))
+    t = t[:len(t) - r]
+    shapes.append(("with_removes", edits, t, int(len(t) / 2 + 0.5)))
+    for name, edits, t, mid in shapes:
+        base = [msg("builder", i + 1, i, e) for i, e in enumerate(edits)]
+        n = len(base)
+        for where, pos, want in (("beginning", 0, "a" + t), ("end", len(t), t + "a"),
+                                 ("middle", mid, t[:mid] + "a" + t[mid:])):
+            out.append({"name": f"inserting_walk_{name}_{where}",
+                        "source": "reference:MT/test/mergeTree.insertingWalk.spec.ts:26-257",
+                        "messages": base + [msg("writer", n + 1, n, ins(pos, "a"))], "text": want})
+    return out
+
+
+def snapshot_kats():
+    """MT/test/snapshot.spec.ts:136-202 through a passive observer: TestString.queue (:96-106) sends
+    each op with refSeq = the previous seq and minSeq = seq when increaseMsn, else the last minSeq.
+    `reload_after` = messages applied before TestString.expect / checkSnapshot round-trips the
+    replica through SnapshotV1 (:59-79): the rest is applied to the client loaded from the
+    snapshot.  `append_digits` expands to that many appends of `${i % 10}` (:188-202)."""
+    w = "fakeId"
+    out = []
+
+    def seq_msgs(edits):
+        res, msn = [], 0
+        for i, (e, inc) in enumerate(edits):
+            if inc:
+                msn = i + 1
+            res.append(msg(w, i + 1, i, e, msn=msn))
+        return res
+
+    src = "reference:MT/test/snapshot.spec.ts"
+    out.append({"name": "snapshot_segments_below_msn", "source": f"{src}:136-139",
+                "messages": seq_msgs([(ins(0, "0"), True)]), "reload_after": 1, "text": "0"})
+    out.append({"name": "snapshot_acked_segments_above_msn", "source": f"{src}:141-144",
+                "messages": seq_msgs([(ins(0, "0"), False)]), "reload_after": 1, "text": "0"})
+    out.append({"name": "snapshot_removal_above_msn", "source": f"{src}:146-150",
+                "messages": seq_msgs([(ins(0, "0x"), False), (rem(1, 2), False)]), "reload_after": 2, "text": "0"})
+    out.append({"name": "snapshot_removal_above_msn_of_segment_below_msn", "source": f"{src}:152-156",
+                "messages": seq_msgs([(ins(0, "0x"), True), (rem(1, 2), False)]), "reload_after": 2, "text": "0"})
+    out.append({"name": "snapshot_insert_after_loading_removed_segment", "source": f"{src}:158-164",
+                "messages": seq_msgs([(ins(0, "0x"), True), (rem(1, 2), False), (ins(1, "1"), False)]),
+                "reload_after": 2, "text": "01"})
+    out.append({"name": "snapshot_insert_relative_to_removed_segment_loaded", "source": f"{src}:175-186",
+                "messages": seq_msgs([(ins(0, "0x"), False), (ins(2, "2"), False), (rem(1, 2), False),
+                                      (ins(1, "1"), False), (ins(3, "3"), False)]),
+                "reload_after": 3, "text": "0123"})
+    n = 10000 + 10  # SnapshotV1.chunkSize + 10
+    for inc, lines in ((True, "188-194"), (False, "196-202")):
+        out.append({"name": f"snapshot_body_chunk_{'below' if inc else 'above'}_msn", "source": f"{src}:{lines}",
+                    "append_digits": {"client": w, "n": n, "increase_msn": inc}, "reload_after": n,
+                    "text": "".join(str(i % 10) for i in range(n))})
+    return out
+
+
 def main():
     kats = []
     base = hello_world()
@@ -96,6 +181,19 @@ def main():
                  "messages": [msg("A", 1, 0, ins(0, "0123456789")), msg("B", 2, 1, rem(0, 5)),
                               msg("A", 3, 1, rem(0, 5))],
                  "text": "56789"})
+    # MT/test/mergeTree.annotate.spec.ts:504-521 "remote first": "remote only" reads the annotated
+    # segment's props, "split remote" splits it (splitAt(1)) and the right part carries the same
+    # props; here a concurrent remote insert splits it
+    kats.append({"name": "split_remote_annotate", "source": "reference:MT/test/mergeTree.annotate.spec.ts:504-521",
+                 "messages": [msg("remote", 1, 0, ins(0, "hello world")),
+                              msg("remote", 2, 1, ann(3, 7, {"propertySource": "remote", "remoteProperty": 1})),
+                              msg("other", 3, 2, ins(4, "X"))],
+                 "text": "hellXo world",
+                 "props_runs": [[0, 3, None], [3, 1, '{"propertySource":"remote","remoteProperty":1}'],
+                                [4, 1, None], [5, 3, '{"propertySource":"remote","remoteProperty":1}'],
+                                [8, 4, None]]})
+    kats.extend(inserting_walk_kats())
+    kats.extend(snapshot_kats())
     OUT.write_text(json.dumps(kats, indent=1))
     print(f"wrote {OUT} ({len(kats)} scenarios)")
 

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+from kat_util import load_kats
 import fluidframework_amd as fa
 from fluidframework_amd import oplog
 from combine_logs import COMBINE_DOCS, combine_farm
@@ -18,7 +19,7 @@ from combine_logs import COMBINE_DOCS, combine_farm
 pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parents[1]
-KATS = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+KATS = load_kats()
 GEN_KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
 GEN_VALUES = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
 

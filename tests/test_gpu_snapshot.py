@@ -14,13 +14,14 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+from kat_util import load_kats
 from snapdigest import bytes_digest
 import fluidframework_amd as fa
 
 pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parents[1]
-KATS = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+KATS = load_kats()
 GEN_KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
 GEN_VALUES = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
 

@@ -150,3 +150,32 @@ def test_snapshot_blobs_as_objects_or_arrays():
         b.snapshots()
         for i in range(len(forms)):
             _check(b, i, od)
+
+
+def test_snapshot_roundtrip_kats():
+    """MT/test/snapshot.spec.ts:136-202 (tests/golden/kats.json `reload_after`): the observer's own
+    GPU SnapshotV1 after the first ops, loaded on the GPU, then the remaining ops — the reference's
+    expected text, and GPU == oracle (same round trip) on digest, text, props and SnapshotV1."""
+    from kat_util import load_kats
+
+    kats = [k for k in load_kats() if "reload_after" in k]
+    heads = [k["messages"][:k["reload_after"]] for k in kats]
+    with fa.ReplayBatch(len(kats)) as a:
+        a.ingest_messages(heads)
+        a.run()
+        a.snapshots()
+        blobs = [a.doc(i).snapshot_v1(device=True) for i in range(len(kats))]
+    docs = [{"snapshot": blobs[i], "messages": k["messages"][k["reload_after"]:]} for i, k in enumerate(kats)]
+    with fa.ReplayBatch(len(kats)) as b:
+        b.ingest_json([json.dumps(d) for d in docs])
+        b.run()
+        b.snapshots()
+        for i, k in enumerate(kats):
+            od = O.Doc()
+            od.start_collab("readonly")
+            for m in heads[i]:
+                assert od.apply_msg(json.dumps(m)) == 0
+            assert od.snapshot_v1() == blobs[i], k["name"]
+            od = _oracle_loaded(od.snapshot_v1(), docs[i]["messages"])
+            assert b.doc(i).get_text() == k["text"], k["name"]
+            _check(b, i, od)

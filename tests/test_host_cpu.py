@@ -8,11 +8,12 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+from kat_util import load_kats
 import fluidframework_amd as fa
 from fluidframework_amd import oplog
 
 ROOT = Path(__file__).resolve().parents[1]
-KATS = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+KATS = load_kats()
 
 
 def test_library_exports_every_declared_symbol():

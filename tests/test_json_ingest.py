@@ -13,11 +13,12 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+from kat_util import load_kats
 from fluidframework_amd import oplog
 from fluidframework_amd.mtreplay import MtError, PackedJson, MT_BAD_INPUT, MT_UNSUPPORTED
 
 ROOT = Path(__file__).resolve().parents[1]
-KATS = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+KATS = load_kats()
 
 
 def _msg(c, s, r, contents, msn=0, type_="op"):

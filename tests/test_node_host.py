@@ -12,6 +12,7 @@ from pathlib import Path
 import pytest
 
 import oracle_ffi as O
+from kat_util import load_kats
 
 ROOT = Path(__file__).resolve().parents[1]
 NODE = shutil.which("node")
@@ -51,7 +52,7 @@ def _msg(c, s, r, contents, msn=0):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["applyMsg", "json"])
 def test_node_replay_matches_oracle(tmp_path, mode):
-    kats = json.loads((ROOT / "tests" / "golden" / "kats.json").read_text())
+    kats = load_kats()
     docs = [k["messages"] for k in kats]
     docs.append([_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "héllo wörld", "props": {"b": 1, "10": "x", "2": None}}}),
                  _msg("B", 2, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1}, "props": {"id": "m1"}}}),

@@ -11,10 +11,11 @@ from pathlib import Path
 import pytest
 
 import oracle_ffi as O
+from kat_util import load_kats
 
 GOLDEN = Path(__file__).with_name("golden")
 SNAP = json.loads((GOLDEN / "snapshot_v1.json").read_text())
-KATS = json.loads((GOLDEN / "kats.json").read_text())
+KATS = load_kats()
 
 
 def build_recipe(r) -> O.Doc:
@@ -49,11 +50,55 @@ def test_snapshot_v1_golden_bytes(name):
 def test_observer_kats(kat):
     d = O.Doc()
     d.start_collab("readonly")
-    for m in kat["messages"]:
+    msgs = kat["messages"]
+    cut = kat.get("reload_after", len(msgs))
+    for m in msgs[:cut]:
+        assert d.apply_msg(json.dumps(m)) == 0, d.error
+    if "reload_after" in kat:
+        # TestString.checkSnapshot (MT/test/snapshot.spec.ts:59-79): SnapshotV1 round trip into a
+        # new client with the same text and length, which then takes the remaining ops
+        d2 = O.Doc()
+        assert d2.load_snapshot(d.snapshot_v1(), "readonly") == 0, d2.error
+        assert d2.text() == d.text() and d2.length() == d.length()
+        d = d2
+    for m in msgs[cut:]:
         assert d.apply_msg(json.dumps(m)) == 0, d.error
     assert d.text() == kat["text"]
     if "props_runs" in kat:
         assert json.loads(d.props_runs()) == kat["props_runs"]
+
+
+def _inserting_walk_tree(shape):
+    """The spec's trees built exactly as MT/test/mergeTree.insertingWalk.spec.ts:26-157 does: local
+    edits of a non-collaborating tree (UniversalSequenceNumber segments), then collaboration."""
+    d = O.Doc()
+    if shape == "single_segment":
+        assert d.insert_local(0, json.dumps("hello world")) == 0
+    else:
+        n = 7 if shape == "full_single_layer" else 32
+        for i in range(n):
+            assert d.insert_local(d.length(), json.dumps(str(i))) == 0
+        if shape == "with_removes":
+            r = int(d.length() / 4 + 0.5)
+            assert d.remove_local(0, r) == 0
+            assert d.remove_local(d.length() - r, d.length()) == 0
+    return d
+
+
+@pytest.mark.parametrize("shape", ["single_segment", "full_single_layer", "with_removes"])
+def test_inserting_walk_spec_trees(shape):
+    """The insertingWalk KATs on the spec's own tree shapes: the full single layer is one block of
+    MaxNodesInBlock - 1 leaves (:80-91), and an insert at the beginning / end / middle gives the
+    spec's text (:187-253) — here as a remote insert of a client that has seen the whole tree."""
+    for where in ("beginning", "end", "middle"):
+        kat = next(k for k in KATS if k["name"] == f"inserting_walk_{shape}_{where}")
+        d = _inserting_walk_tree(shape)
+        if shape == "full_single_layer":
+            assert d.shape() == "D1:7", d.shape()
+        assert d.start_collab("readonly") == 0
+        ins = dict(kat["messages"][-1], sequenceNumber=1, referenceSequenceNumber=0)
+        assert d.apply_msg(json.dumps(ins)) == 0, d.error
+        assert d.text() == kat["text"], (shape, where)
 
 
 def test_snapshot_chunking_and_merge_info():
