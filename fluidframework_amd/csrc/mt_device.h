@@ -266,7 +266,13 @@ struct ReplayParams {
     const int32_t *fq_doc_list;   // consumer: the producer's doc_list (null: identity)
     uint32_t *fq_started;         // producer: host-mapped count of started workgroups (the host
                                   // launches the consumer once all are resident)
+    // MergeTree.idToSegment (mergeTree.ts:1098) per document, persistent across launches:
+    // {marker-id key, slot} entries in mapping order (kIdUnlinked: the marker was unlinked)
+    uint2 *idmap;
+    const uint64_t *doc_idmap_base;
 };
+constexpr uint32_t kIdUnlinked = 0xFFFFFFFFu;
+constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // RELPOS key the host cannot resolve safely
 constexpr int kProfSlots = 12;
 
 // mt_digest.hip: per-document device digest of one launch's results

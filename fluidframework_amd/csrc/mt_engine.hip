@@ -183,6 +183,9 @@ struct Engine {
     LWord<uint32_t> ps0, pn0, pr0, pch0, ps1, pn1, pr1, pch1;
     uint32_t pv0, pv1;
     LWord<int32_t> max_heap, max_u;
+    // marker ids (idToSegment) and the positions an MT_OP_RELPOS record resolved for the next op
+    LWord<int32_t> idmap_n, rel_pend, rel_p1, rel_p2;
+    uint2 *idmap;
     int32_t htop;
     uint2 *h_ent;
     // ---- global
@@ -237,6 +240,10 @@ struct Engine {
         pn1.p = hw + 17;
         pr1.p = hw + 18;
         pch1.p = hw + 19;
+        idmap_n.p = (int32_t *)hw + 20;
+        rel_pend.p = (int32_t *)hw + 21;
+        rel_p1.p = (int32_t *)hw + 22;
+        rel_p2.p = (int32_t *)hw + 23;
     }
 
     MT_FI void set_fail(int32_t st) {
@@ -273,6 +280,8 @@ struct Engine {
         ov_full = 0;
         max_heap = 0;
         max_u = 0;
+        idmap_n = 0;
+        rel_pend = 0;
         // initialNode (mergeTree.ts:1125): an empty root leaf block
         root = alloc_block(1);
         depth = 1;
@@ -1050,6 +1059,98 @@ struct Engine {
         wsync();
     }
 
+    // ------------------------------------------------------------------ marker ids, relative positions
+    // mapIdToSegment (mergeTree.ts:1185-1187): entries in mapping order; a lookup takes the only
+    // entry of its key (a key mapped twice is left to the host: the reference re-maps ids on every
+    // blockUpdate of a block, so which marker it names depends on which block was updated last)
+    MT_FI void idmap_add(uint32_t key, uint32_t slot) {
+        const int32_t n = idmap_n;
+        if (lane == 0) idmap[n] = make_uint2(key, slot);
+        idmap_n = n + 1;
+        wsync();
+    }
+    // zamboni unlinked these markers (lanes in m): the reference's map keeps the detached segment,
+    // whose getPosition is 0 (no parent)
+    MT_FI void idmap_forget(uint32_t slot, uint64_t m) {
+        const int32_t n = idmap_n;
+        for (int32_t j0 = 0; j0 < n; j0 += kWave) {
+            const int32_t j = j0 + lane;
+            const uint32_t s = j < n ? idmap[j].y : kIdUnlinked;
+            bool hit = false;
+            for (uint64_t mm = m; mm; mm &= mm - 1) hit |= s == rdl(slot, first_lane(mm));
+            if (hit) idmap[j].y = kIdUnlinked;
+        }
+        wsync();
+    }
+    // getPosition (mergeTree.ts:1586-1603): the view length of everything before `slot` on its
+    // path to the root (block lengths from the settled sums + this op's overlay)
+    MT_FI uint32_t get_position(uint32_t slot, int32_t ref, uint32_t c) {
+        int32_t B = (int32_t)rfl((uint32_t)s_blk[slot]);
+        uint32_t pos = 0, child = slot;
+        bool leaf = true;
+        while (B != (int32_t)kNoBlk) {
+            const int32_t n = b_count[B];
+            const uint32_t row = lane < n ? (uint32_t)b_child[B * 8 + lane] : kNoBlk;
+            const uint64_t at = ballot(lane < n && row == child);
+            const int32_t k = at ? first_lane(at) : n;
+            uint32_t v = 0;
+            if (lane < k) {
+                if (leaf) {
+                    bool tie;
+                    view_of(row, ref, c, v, tie);
+                } else {
+                    v = ov_acc(row) + (ov_full ? 0u : b_slen[row]);
+                }
+            }
+            pos += rdl(sum8(v), 0);
+            child = (uint32_t)B;
+            B = (int32_t)rfl((uint32_t)b_parent[B]);
+            leaf = false;
+        }
+        return pos;
+    }
+    // MT_OP_RELPOS: posFromRelativePos (mergeTree.ts:1942-1966) for the next record's pos1 / pos2
+    // (client.ts:485-502).  An id with no marker gives -1 in the reference and a position below 0
+    // is passed on; both, and keys the host flagged, end the document as MT_UNSUPPORTED.
+    MT_FI void op_relpos(const mt_op &op) {
+        ov_splits = -1;
+        ensure_overlay(op.ref_seq, op.client);
+        int32_t pend = 0;
+        for (int k = 0; k < 2; k++) {
+            if (!(op.flags & (k ? MT_RELF_POS2 : MT_RELF_POS1))) continue;
+            const uint32_t key = (uint32_t)(k ? op.pos2 : op.pos1);
+            const int32_t n = idmap_n;
+            uint32_t found = 0, slot = kIdUnlinked;
+            for (int32_t j0 = 0; j0 < n; j0 += kWave) {
+                const int32_t j = j0 + lane;
+                const uint2 e = j < n ? idmap[j] : make_uint2(0u, 0u);
+                const uint64_t hm = ballot(j < n && e.x == key);
+                if (hm) slot = rdl(e.y, first_lane(hm));
+                found += __popcll(hm);
+            }
+            if (key == 0u || key == kIdKeyUnsupported || found != 1u) {
+                set_fail(ST_UNSUPPORTED);
+                return;
+            }
+            int64_t pos = slot == kIdUnlinked ? 0 : (int64_t)get_position(slot, op.ref_seq, op.client);
+            const int32_t off = (int32_t)(k ? op.payload_len : op.payload);
+            if (!(op.flags & (k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1))) {
+                pos += 1;  // marker.cachedLength
+                if (op.flags & (k ? MT_RELF_OFF2 : MT_RELF_OFF1)) pos += off;
+            } else if (op.flags & (k ? MT_RELF_OFF2 : MT_RELF_OFF1)) {
+                pos -= off;
+            }
+            if (pos < 0 || pos > 0x7FFFFFFF) {
+                set_fail(ST_UNSUPPORTED);
+                return;
+            }
+            if (k) rel_p2 = (int32_t)pos;
+            else rel_p1 = (int32_t)pos;
+            pend |= 1 << k;
+        }
+        rel_pend = pend;
+    }
+
     // ------------------------------------------------------------------ properties
     // prop-set record in the doc pool: [n, hash, (key, value) x n] in insertion order.  The hash is
     // order-insensitive over (key, structural value class); its bit 0 is set when no value of the
@@ -1429,6 +1530,8 @@ struct Engine {
         if (freeM) {
             free_head = (int32_t)rdl(slot, first_lane(freeM));
             heap_forget(slot, freeM);
+            const uint64_t mkM = freeR & ballot((meta & kMetaMarker) != 0u);
+            if (mkM) idmap_forget(slot, mkM);
         }
         free_n += __popcll(freeM);
         if ((holdM >> lane) & 1ull) hold[__popcll(holdM & below)] = slot;
@@ -1660,6 +1763,9 @@ struct Engine {
             }
             // saveIfLocal (mergeTree.ts:2164-2179)
             if (op.seq > min_seq) add_to_lru(blk, (uint32_t)slot, op.seq);
+            // blockInsert maps a marker's id (mergeTree.ts:2200-2205); the host put the id's key
+            // in payload_len (0: no id)
+            if (marker && op.payload_len) idmap_add(op.payload_len, (uint32_t)slot);
         }
         resolve_splits();
         if (!loaded || !(op.flags & MT_OPF_GROUP_CONT)) zamboni();
@@ -1704,6 +1810,9 @@ struct Engine {
         }
         s_meta[slot] = meta;
         wsync();
+        // reloadFromSegments' blockUpdate maps the ids of markers with localNetLength > 0
+        // (addNodeReferences, mergeTree.ts:270-285): not removed ones
+        if (marker && op.payload_len && rseq == kNoneSeq) idmap_add(op.payload_len, (uint32_t)slot);
         // the rightmost leaf block
         int32_t b = root;
         for (int32_t l = 0; l + 1 < depth; l++) b = rfl((int32_t)b_child[b * 8 + b_count[b] - 1]);
@@ -2032,8 +2141,14 @@ struct Engine {
         resolve_splits();
     }
 
-    MT_FI void apply(const mt_op &op) {
+    MT_FI void apply(mt_op op) {
         pend_n = 0;
+        if (rel_pend) {  // the positions the MT_OP_RELPOS record before this one resolved
+            const int32_t rp = rel_pend;
+            if (rp & 1) op.pos1 = rel_p1;
+            if (rp & 2) op.pos2 = rel_p2;
+            rel_pend = 0;
+        }
         if (op.client >= (uint32_t)kMaxClients || (op.client == 0 && op.type != MT_OP_NOOP)) {
             set_fail(ST_UNSUPPORTED);
             return;
@@ -2049,6 +2164,7 @@ struct Engine {
             case MT_OP_INSERT: op_insert(op); break;
             case MT_OP_REMOVE:
             case MT_OP_ANNOTATE: op_range(op); break;
+            case MT_OP_RELPOS: op_relpos(op); break;
             case MT_OP_NOOP: break;
             default: set_fail(ST_BAD_INPUT); return;
         }
@@ -2158,6 +2274,10 @@ struct Engine {
             ck[22] = (uint32_t)max_u;
             ck[23] = (uint32_t)sbase;
             ck[24] = (uint32_t)bfree_head;
+            ck[25] = (uint32_t)(int32_t)idmap_n;
+            ck[26] = (uint32_t)(int32_t)rel_pend;
+            ck[27] = (uint32_t)(int32_t)rel_p1;
+            ck[28] = (uint32_t)(int32_t)rel_p2;
         }
         uint32_t *p = ck + kCkHdr;
         dump(p, s_len, slot_top);
@@ -2200,6 +2320,10 @@ struct Engine {
         max_u = (int32_t)rfl(ck[22]);
         sbase = (int32_t)rfl(ck[23]);
         bfree_head = (int32_t)rfl(ck[24]);
+        idmap_n = (int32_t)rfl(ck[25]);
+        rel_pend = (int32_t)rfl(ck[26]);
+        rel_p1 = (int32_t)rfl(ck[27]);
+        rel_p2 = (int32_t)rfl(ck[28]);
         arena_end = arena_base + semi_t;
         pool_end = pool_base + semi_p;
         const uint32_t *p = ck + kCkHdr;
@@ -2336,6 +2460,7 @@ MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_
     E.text_gcs = 0;
     E.props_in = (const mt_prop *)P.props_in;
     E.vt = P.vt;
+    E.idmap = P.idmap ? P.idmap + P.doc_idmap_base[d] : nullptr;
     E.init();
 }
 

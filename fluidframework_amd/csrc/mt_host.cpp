@@ -364,6 +364,8 @@ struct mt_batch {
     int64_t *d_off = nullptr;
     uint16_t *d_text = nullptr;
     uint64_t *d_text_base = nullptr, *d_pool_base = nullptr;
+    uint2 *d_idmap = nullptr;          // per-document marker-id maps (mt_device.h ReplayParams.idmap)
+    uint64_t *d_idmap_base = nullptr;
     uint32_t *d_text_len = nullptr, *d_text_cap = nullptr, *d_pool_cap = nullptr;
     uint32_t *d_pool = nullptr;
     mt_prop *d_props = nullptr;
@@ -450,6 +452,10 @@ static void free_log(mt_batch *b) {
     (void)hipFree(b->d_pool_base);
     (void)hipFree(b->d_pool_cap);
     (void)hipFree(b->d_props);
+    (void)hipFree(b->d_idmap);
+    (void)hipFree(b->d_idmap_base);
+    b->d_idmap = nullptr;
+    b->d_idmap_base = nullptr;
     b->d_ops = nullptr;
     b->d_off = nullptr;
     b->d_text = nullptr;
@@ -629,6 +635,63 @@ static int host_value_rel(const mt_batch *b, uint32_t va, uint32_t vb) {
 
 static uint32_t align16u(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
 
+// Marker ids and relative positions (idToSegment, posFromRelativePos: mergeTree.ts:1185,
+// 1942-1966).  Ids are object keys, so both sides are compared as String(value): every marker
+// insert / load record whose props give a truthy markerId gets that key's id (>= 1) in
+// payload_len (0: no id; a marker's payload_len is otherwise unused), every MT_OP_RELPOS record
+// its ids' keys in pos1 / pos2 (0: no id).  A document whose annotates touch markerId gets
+// kIdKeyUnsupported instead: the reference re-maps a re-annotated id only at a later blockUpdate.
+// idmap_base[d]: the first entry of document d's map (one per marker with an id).
+static void resolve_marker_ids(mt_batch *b, std::vector<mt_op> &h_ops, const std::vector<int64_t> &off,
+                               const mt_prop *props, int64_t n_props, std::vector<uint64_t> &idmap_base) {
+    uint32_t mk = 0xFFFFFFFFu;
+    for (size_t k = 0; k < b->keys.size(); k++)
+        if (b->keys[k] == "markerId") mk = (uint32_t)k;
+    std::unordered_map<std::u16string, uint32_t> keys;
+    std::unordered_map<uint32_t, uint32_t> of_value;
+    auto key_of = [&](uint32_t v) -> uint32_t {  // 0: no id (null / falsy / not a value)
+        if (v == 0 || v >= b->values.size() || (b->value_flags[v] & mt::kValFalsy)) return 0;
+        auto it = of_value.find(v);
+        if (it != of_value.end()) return it->second;
+        std::u16string s;
+        uint32_t k = 0;
+        if (mt::js_string_of(b->values[v], s)) {
+            auto kt = keys.find(s);
+            if (kt == keys.end()) kt = keys.emplace(s, (uint32_t)keys.size() + 1).first;
+            k = kt->second;
+        }
+        of_value.emplace(v, k);
+        return k;
+    };
+    const size_t D = off.size() - 1;
+    uint64_t total = 0;
+    for (size_t d = 0; d < D; d++) {
+        idmap_base[d] = total;
+        bool annot_mk = false;
+        for (int64_t i = off[d]; i < off[d + 1]; i++) {
+            mt_op &o = h_ops[(size_t)i];
+            if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
+                uint32_t id = 0;
+                if (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)
+                    for (uint32_t q = 0; q < MT_OPF_NPROPS(o.flags); q++)
+                        if ((int64_t)o.pos2 + q < n_props && props[o.pos2 + q].key == mk) id = key_of(props[o.pos2 + q].value);
+                o.payload_len = id;
+                if (id) total++;
+            } else if (o.type == MT_OP_ANNOTATE) {
+                for (uint32_t q = 0; q < o.payload_len; q++)
+                    if (props[o.payload + q].key == mk) annot_mk = true;
+            }
+        }
+        for (int64_t i = off[d]; i < off[d + 1]; i++) {
+            mt_op &o = h_ops[(size_t)i];
+            if (o.type != MT_OP_RELPOS) continue;
+            o.pos1 = (int32_t)(annot_mk ? mt::kIdKeyUnsupported : key_of((uint32_t)o.pos1));
+            o.pos2 = (int32_t)(annot_mk ? mt::kIdKeyUnsupported : key_of((uint32_t)o.pos2));
+        }
+    }
+    idmap_base[D] = total;
+}
+
 // The result slot of every combining annotate (mt_oplog.h): the value Properties.combine gives a
 // key that the segment does not have (segmentPropertiesManager.ts:93-98 with previousValue and
 // newValue undefined: mt::combine_absent).  Results that are not values of the caller's table
@@ -788,6 +851,8 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     int rc = ensure_tables(b);
     if (rc) return rc;
     std::vector<mt_op> h_ops(ops, ops + N);
+    std::vector<uint64_t> idmap_base((size_t)D + 1, 0);
+    resolve_marker_ids(b, h_ops, h_off, props, n_props, idmap_base);
     std::vector<uint16_t> h_text(tbase ? tbase : 1, 0);
     for (int64_t d = 0; d < D; d++) {
         uint32_t w = 0;
@@ -839,6 +904,9 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     HIPCHK(dalloc(&b->d_pool_base, (size_t)D));
     HIPCHK(dalloc(&b->d_pool_cap, (size_t)D));
     HIPCHK(dalloc(&b->d_props, (size_t)std::max<int64_t>(n_props, 1)));
+    HIPCHK(dalloc(&b->d_idmap, (size_t)std::max<uint64_t>(idmap_base[(size_t)D], 1)));
+    HIPCHK(dalloc(&b->d_idmap_base, (size_t)D + 1));
+    HIPCHK(hipMemcpy(b->d_idmap_base, idmap_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_off, b->h_off.data(), sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_text, h_text.data(), 2 * h_text.size(), hipMemcpyHostToDevice));
@@ -923,6 +991,8 @@ static mt::ReplayParams base_params(mt_batch *b) {
     P.doc_pool_cap = b->d_pool_cap;
     P.props_in = b->d_props;
     P.vt = b->d_vt;
+    P.idmap = b->d_idmap;
+    P.doc_idmap_base = b->d_idmap_base;
     return P;
 }
 

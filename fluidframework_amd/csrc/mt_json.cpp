@@ -555,16 +555,53 @@ struct Packer1 {
         return true;
     }
 
+    // the MT_OP_RELPOS record of an op whose pos1 (pos2) is undefined and relativePos1
+    // (relativePos2) truthy (Client.getValidOpRange, client.ts:485-502); r.type stays base's otherwise
+    bool relpos(int32_t op, const mt_op &base, mt_op &r) {
+        r = base;
+        if (D.nodes[op].type != J_OBJ) return true;
+        const int32_t t = D.member(op, "type");
+        const double tv = t >= 0 && D.nodes[t].type == J_NUM ? D.nodes[t].num : -1;
+        uint32_t flags = MT_OPF_GROUP_CONT;
+        for (int k = 1; k <= 2; k++) {
+            const int32_t rp = D.member(op, k == 1 ? "relativePos1" : "relativePos2");
+            if (D.member(op, k == 1 ? "pos1" : "pos2") >= 0 || rp < 0 || !truthy(D.nodes[rp]) ||
+                (k == 2 && tv != 1 && tv != 2))
+                continue;
+            flags |= k == 1 ? MT_RELF_POS1 : MT_RELF_POS2;
+            const bool obj = D.nodes[rp].type == J_OBJ;
+            const int32_t id = obj ? D.member(rp, "id") : -1, bf = obj ? D.member(rp, "before") : -1;
+            const int32_t off = obj ? D.member(rp, "offset") : -1;
+            if (id >= 0 && truthy(D.nodes[id])) (k == 1 ? r.pos1 : r.pos2) = (int32_t)value(id);
+            if (bf >= 0 && truthy(D.nodes[bf])) flags |= k == 1 ? MT_RELF_BEFORE1 : MT_RELF_BEFORE2;
+            if (off >= 0) {  // `offset !== undefined`; null adds 0
+                double o = 0;
+                if (D.nodes[off].type == J_NUM) o = D.nodes[off].num;
+                else if (D.nodes[off].type != J_NULL) return fail(MT_UNSUPPORTED, "relative position offset must be an integer");
+                if (o != std::floor(o) || std::fabs(o) > 2147483647.0)
+                    return fail(MT_UNSUPPORTED, "relative position offset must be an integer");
+                flags |= k == 1 ? MT_RELF_OFF1 : MT_RELF_OFF2;
+                (k == 1 ? r.payload : r.payload_len) = (uint32_t)(int32_t)o;
+            }
+        }
+        if (flags & (MT_RELF_POS1 | MT_RELF_POS2)) {
+            r.type = MT_OP_RELPOS;
+            r.flags = (uint16_t)flags;
+        }
+        return true;
+    }
+
     bool pack_op(int32_t op, const mt_op &base, mt_op &r) {
         r = base;
         if (D.nodes[op].type != J_OBJ) return fail(MT_UNSUPPORTED, "op must be an object");
         const int32_t t = D.member(op, "type"), p1 = D.member(op, "pos1");
-        if (p1 < 0 || !D.is_null_or_absent(D.member(op, "relativePos1")) ||
-            !D.is_null_or_absent(D.member(op, "register")))
-            return fail(MT_UNSUPPORTED, "relative positions / registers are not on the observer fast path");
+        const int32_t rp1 = D.member(op, "relativePos1");
+        if (p1 < 0 && (rp1 < 0 || !truthy(D.nodes[rp1]))) return fail(MT_UNSUPPORTED, "op without a position");
+        if (!D.is_null_or_absent(D.member(op, "register")))
+            return fail(MT_UNSUPPORTED, "registers are not on the observer fast path");
         const double tv = t >= 0 && D.nodes[t].type == J_NUM ? D.nodes[t].num : -1;
         r.flags = 0;
-        r.pos1 = as_int(D.nodes[p1]);
+        r.pos1 = p1 >= 0 ? as_int(D.nodes[p1]) : 0;
         r.pos2 = 0;
         r.payload = r.payload_len = 0;
         if (tv == 0) {
@@ -795,6 +832,9 @@ struct Packer1 {
             if (contents >= 0) flatten(contents, members);
             for (size_t j = 0; j < members.size(); j++) {
                 mt_op r{};
+                if (!relpos(members[j], base, r)) return false;
+                if (r.type == MT_OP_RELPOS) L.ops.push_back(r);
+                r = mt_op{};
                 if (!pack_op(members[j], base, r)) return false;
                 if (j + 1 < members.size()) r.flags |= MT_OPF_GROUP_CONT;
                 L.ops.push_back(r);
@@ -920,6 +960,9 @@ MT_API int mt_pack_json(mt_packed **out, int64_t n_docs, const char *const *doc_
                 if (o.flags & MT_OPF_HAS_PROPS) o.pos2 += (int32_t)pbase;
             } else if (o.type == MT_OP_ANNOTATE) {
                 o.payload += pbase;
+            } else if (o.type == MT_OP_RELPOS) {  // relativePosN.id value ids
+                o.pos1 = (int32_t)vmap[(uint32_t)o.pos1];
+                o.pos2 = (int32_t)vmap[(uint32_t)o.pos2];
             }
             P->ops.push_back(o);
         }

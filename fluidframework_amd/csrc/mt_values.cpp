@@ -481,6 +481,14 @@ bool parse(const std::string &t, JV &v) {
 }
 }  // namespace
 
+bool js_string_of(const std::string &json, std::u16string &out) {
+    JV v;
+    if (!parse(json, v)) return false;
+    out.clear();
+    to_string(v, out);
+    return true;
+}
+
 // combine kinds: include/mt_oplog.h mt_combine_kind (1 incr, 2 consensus, 3 other)
 CombineResult combine_absent(int kind, const std::string *def, const std::string *min, int32_t seq, std::string &out) {
     JV d;

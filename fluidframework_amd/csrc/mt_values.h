@@ -40,6 +40,10 @@ enum CombineResult {
 };
 CombineResult combine_absent(int kind, const std::string *def, const std::string *min, int32_t seq, std::string &out);
 
+// String(v) of a value given as JSON text (an object key: idToSegment[id], mergeTree.ts:1185);
+// false when the text does not parse
+bool js_string_of(const std::string &json, std::u16string &out);
+
 // JSON.stringify helpers shared with mt_json.cpp
 void json_quote(std::string &o, const char16_t *s, size_t n);
 void json_number(std::string &o, double v);

@@ -30,6 +30,7 @@ function native() {
 
 const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 15;
 const OPF_GROUP_CONT = 1, OPF_MARKER = 2, OPF_HAS_PROPS = 4, OPF_REWRITE = 8;
+const OP_RELPOS = 6, RELF_POS1 = 0x10, RELF_POS2 = 0x20, RELF_BEFORE1 = 0x40, RELF_BEFORE2 = 0x80, RELF_OFF1 = 0x100, RELF_OFF2 = 0x200;
 const COMBINE_INCR = 1, COMBINE_CONSENSUS = 2, COMBINE_OTHER = 3, KEY_COMBINE = 0xFFFFFFFF, VALUE_UNDEFINED = 0xFFFFFFFF;
 const MAX_INSERT_PROPS = 1023;
 const STATUS = ['OK', 'INVALID_POS', 'SEQ_ORDER', 'MSN_ORDER', 'UNSUPPORTED', 'BAD_INPUT', 'CAPACITY', 'INTERNAL'];
@@ -84,11 +85,31 @@ class Packer {
         if (op.type === 3) return (op.ops || []).reduce((a, m) => a.concat(Packer.flatten(m)), []);
         return [op];
     }
+    // the MT_OP_RELPOS record of an op whose pos1 (pos2) is undefined and relativePos1 (relativePos2)
+    // truthy (Client.getValidOpRange, client.ts:485-502), else null
+    relPos(op, base) {
+        const r = Object.assign({}, base, { type: OP_RELPOS, flags: OPF_GROUP_CONT, pos1: 0, pos2: 0, payload: 0, payloadLen: 0 });
+        for (const k of [1, 2]) {
+            let rp = op[`relativePos${k}`];
+            if (op[`pos${k}`] !== undefined || !rp || (k === 2 && op.type !== OP_REMOVE && op.type !== OP_ANNOTATE)) continue;
+            r.flags |= k === 1 ? RELF_POS1 : RELF_POS2;
+            if (typeof rp !== 'object' || Array.isArray(rp)) rp = {};
+            if (rp.id) r[`pos${k}`] = this.value(rp.id);
+            if (rp.before) r.flags |= k === 1 ? RELF_BEFORE1 : RELF_BEFORE2;
+            if (Object.prototype.hasOwnProperty.call(rp, 'offset')) {  // `offset !== undefined`; null adds 0
+                const off = rp.offset === null ? 0 : rp.offset;
+                if (!Number.isInteger(off)) throw new UnsupportedOp('relative position offset must be an integer');
+                r.flags |= k === 1 ? RELF_OFF1 : RELF_OFF2;
+                r[k === 1 ? 'payload' : 'payloadLen'] = off >>> 0;
+            }
+        }
+        return (r.flags & (RELF_POS1 | RELF_POS2)) ? r : null;
+    }
     packOp(op, base) {
         const t = op.type;
-        if (op.pos1 === undefined || op.relativePos1 !== undefined || op.register !== undefined)
-            throw new UnsupportedOp('relative positions / registers are not on the observer fast path');
-        const r = Object.assign({}, base, { type: t, flags: 0, pos1: op.pos1 | 0, pos2: 0, payload: 0, payloadLen: 0 });
+        if (op.pos1 === undefined && !op.relativePos1) throw new UnsupportedOp('op without a position');
+        if (op.register !== undefined) throw new UnsupportedOp('registers are not on the observer fast path');
+        const r = Object.assign({}, base, { type: t, flags: 0, pos1: op.pos1 === undefined ? 0 : op.pos1 | 0, pos2: 0, payload: 0, payloadLen: 0 });
         if (t === OP_INSERT) {
             const seg = op.seg;
             let text = null, props;
@@ -160,6 +181,8 @@ class Packer {
             if (c === 0) throw new UnsupportedOp("ack of the observer's own op (local path)");
             const members = Packer.flatten(msg.contents);
             members.forEach((op, j) => {
+                const rel = this.relPos(op, base);
+                if (rel) recs.push(rel);
                 const r = this.packOp(op, base);
                 if (j + 1 < members.length) r.flags |= OPF_GROUP_CONT;
                 recs.push(r);

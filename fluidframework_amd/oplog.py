@@ -31,7 +31,9 @@ OP_DTYPE = np.dtype(
 PROP_DTYPE = np.dtype([("key", "<u4"), ("value", "<u4")])
 assert OP_DTYPE.itemsize == 32
 
-OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 15
+OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_RELPOS, OP_NOOP = 0, 1, 2, 6, 15
+# MT_OP_RELPOS flags (include/mt_oplog.h mt_relpos_flags)
+RELF_POS1, RELF_POS2, RELF_BEFORE1, RELF_BEFORE2, RELF_OFF1, RELF_OFF2 = 0x10, 0x20, 0x40, 0x80, 0x100, 0x200
 OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
 MAX_INSERT_PROPS = 1023
 # combiningOp other than "rewrite" (include/mt_oplog.h mt_combine_kind): annotate flags bits 4-5,
@@ -220,6 +222,9 @@ class Packer:
                 raise UnsupportedOp("ack of the observer's own op (local path)")
             members = self._flatten(msg["contents"])
             for j, op in enumerate(members):
+                rel = self._relpos(op, base)
+                if rel is not None:
+                    recs.append(rel)
                 r = self._pack_op(op, base)
                 if j + 1 < len(members):
                     r["flags"] |= OPF_GROUP_CONT
@@ -240,11 +245,37 @@ class Packer:
             return out
         return [op]
 
+    def _relpos(self, op: dict, base: dict):
+        """The MT_OP_RELPOS record of an op whose pos1 (pos2) is undefined and relativePos1
+        (relativePos2) truthy (Client.getValidOpRange, client.ts:485-502), else None."""
+        t = op.get("type")
+        r = dict(base, type=OP_RELPOS, flags=OPF_GROUP_CONT, pos1=0, pos2=0, payload=0, payload_len=0)
+        for k in (1, 2):
+            rp = op.get(f"relativePos{k}")
+            if f"pos{k}" in op or not js_truthy(rp) or (k == 2 and t not in (1, 2)):
+                continue
+            r["flags"] |= RELF_POS1 if k == 1 else RELF_POS2
+            rp = rp if isinstance(rp, dict) else {}
+            if js_truthy(rp.get("id")):
+                r[f"pos{k}"] = self._value(rp["id"])
+            if js_truthy(rp.get("before")):
+                r["flags"] |= RELF_BEFORE1 if k == 1 else RELF_BEFORE2
+            if "offset" in rp:  # `offset !== undefined`; null adds 0
+                off = rp["offset"] if rp["offset"] is not None else 0
+                if isinstance(off, bool) or not isinstance(off, int):
+                    raise UnsupportedOp("relative position offset must be an integer")
+                r["flags"] |= RELF_OFF1 if k == 1 else RELF_OFF2
+                r["payload" if k == 1 else "payload_len"] = off & 0xFFFFFFFF
+        return r if r["flags"] & (RELF_POS1 | RELF_POS2) else None
+
     def _pack_op(self, op: dict, base: dict) -> dict:
         t = op.get("type")
-        if "pos1" not in op or op.get("relativePos1") is not None or op.get("register") is not None:
-            raise UnsupportedOp("relative positions / registers are not on the observer fast path")
-        r = dict(base, type=t, flags=0, pos1=int(op["pos1"]), pos2=0, payload=0, payload_len=0)
+        if "pos1" not in op and not js_truthy(op.get("relativePos1")):
+            raise UnsupportedOp("op without a position")
+        if op.get("register") is not None:
+            raise UnsupportedOp("registers are not on the observer fast path")
+        r = dict(base, type=t, flags=0, pos1=int(op["pos1"]) if "pos1" in op else 0, pos2=0, payload=0,
+                 payload_len=0)
         if t == 0:
             seg = op.get("seg")
             props = None
@@ -278,7 +309,7 @@ class Packer:
                 r["flags"] |= OPF_HAS_PROPS
                 r["pos2"] = len(self._props)
         elif t in (1, 2):
-            r["pos2"] = int(op.get("pos2", 0))
+            r["pos2"] = int(op["pos2"]) if op.get("pos2") is not None else 0
             if t == 2:
                 # addProperties (segmentPropertiesManager.ts:53-54): "rewrite" when op.name is
                 # "rewrite", else any truthy combiningOp goes through Properties.combine

@@ -46,7 +46,21 @@ enum mt_op_type {
     MT_OP_LOAD_HEADER = 3,
     MT_OP_LOAD_BODY = 4,
     MT_OP_COLLAB = 5,
+    /* RELPOS  the relative positions of the record that follows it (same client / seq / refSeq /
+               msn, always MT_OPF_GROUP_CONT): an op with pos1 (pos2) undefined and relativePos1
+               (relativePos2) given takes posFromRelativePos (client.ts:485-502, mergeTree.ts:
+               1942-1966).  pos1 / pos2 = value id of relativePosN.id (0: none), payload /
+               payload_len = offsetN (int32), flags = MT_RELF_*. */
+    MT_OP_RELPOS = 6,
     MT_OP_NOOP = 15     /* non-"op" message: only client registration + updateSeqNumbers */
+};
+enum mt_relpos_flags {
+    MT_RELF_POS1 = 0x10u,    /* pos1 of the next record is relativePos1            */
+    MT_RELF_POS2 = 0x20u,    /* pos2 of the next record is relativePos2            */
+    MT_RELF_BEFORE1 = 0x40u, /* relativePos1.before is truthy                      */
+    MT_RELF_BEFORE2 = 0x80u,
+    MT_RELF_OFF1 = 0x100u,   /* relativePos1.offset is defined (payload)           */
+    MT_RELF_OFF2 = 0x200u    /* relativePos2.offset is defined (payload_len)       */
 };
 #define MT_CLIENT_NONCOLLAB 254u /* NonCollabClient (constants.ts:15); long id "original" */
 #define MT_CLIENT_NONE 255u

@@ -60,6 +60,7 @@ struct Block { /* MergeBlock / HierMergeBlock, mergeTree.ts:336-420 */
        +inf): a view with refSeq at or above both sees exactly cachedLength (block_partial_length) */
     int max_seq, max_rseq;
     Block *all_next;
+    struct mto_doc *doc; /* for blockUpdate's marker-id bookkeeping (addNodeReferences) */
 };
 
 typedef struct Seg { /* BaseSegment, mergeTree.ts:429-573 */
@@ -77,6 +78,8 @@ typedef struct Seg { /* BaseSegment, mergeTree.ts:429-573 */
     int novl, covl;
     jv *props; /* properties (NULL = undefined) */
     struct Seg *all_next;
+    const jv *id_jv; /* marker id value last mapped (id_idx: its idToSegment entry) */
+    int id_idx;
 } Seg;
 
 typedef struct { /* LRUSegment, mergeTree.ts:918-926 */
@@ -115,6 +118,15 @@ struct mto_doc {
     int n_blobs;
     /* packed-op client index -> short id cache */
     int pk_map[256];
+    /* MergeTree.idToSegment (mergeTree.ts:1098): String(markerId) -> marker */
+    u16 **id_keys;
+    int *id_klens;
+    Seg **id_segs;
+    int n_ids_map, cap_ids_map;
+    int *id_hash; /* open addressing over id_keys (index + 1, 0 empty), id_hcap slots */
+    int id_hcap;
+    /* packed MT_OP_RELPOS: resolved positions for the next record (bit 0 pos1, bit 1 pos2) */
+    int rel_pending, rel_pos1, rel_pos2;
 };
 
 /* ------------------------------------------------------------------ errors */
@@ -136,6 +148,7 @@ static Block *make_block(mto_doc *d, int child_count) { /* MergeTree.makeBlock, 
     b->child_count = child_count;
     b->needs_scour = SCOUR_UNDEF;
     b->max_seq = b->max_rseq = INT_MAX; /* unknown until block_update */
+    b->doc = d;
     b->all_next = d->all_blocks;
     d->all_blocks = b;
     return b;
@@ -196,11 +209,14 @@ static int node_total_length(const Node *n) { /* mergeTree.ts:422-427 */
 }
 
 static int seq_bound(int seq) { return seq == UNASSIGNED_SEQ ? INT_MAX : seq; }
+static void map_marker_id(mto_doc *d, Seg *s);
 static void block_update(Block *b) { /* mergeTree.ts:2748-2768 (cachedLength part) */
     int len = 0, ms = INT_MIN, mr = INT_MIN;
     for (int i = 0; i < b->child_count; i++) {
         Node *c = b->children[i];
         len += node_total_length(c);
+        /* addNodeReferences (mergeTree.ts:270-285): a marker with localNetLength > 0 re-maps its id */
+        if (c->is_leaf && local_net_length((const Seg *)c) > 0 && b->doc) map_marker_id(b->doc, (Seg *)c);
         if (c->is_leaf) {
             const Seg *sg = (const Seg *)c;
             if (seq_bound(sg->seq) > ms) ms = seq_bound(sg->seq);
@@ -871,6 +887,7 @@ static void insert_segments(mto_doc *d, int pos, Seg **segs, int n, int ref_seq,
         if (!seg || seg->n.cached_length <= 0) continue;
         seg->seq = seq;
         seg->client_id = client_id;
+        map_marker_id(d, seg); /* blockInsert: Marker.is(newSegment) && getId() (mergeTree.ts:2200-2205) */
         ICtx ctx = {LEAF_INSERT, seg, 1};
         Block *sn = inserting_walk(d, d->root, insert_pos, ref_seq, client_id, seq, &ctx);
         if (seg->n.parent) bump_bounds(seg);
@@ -893,6 +910,125 @@ static void insert_segments(mto_doc *d, int pos, Seg **segs, int n, int ref_seq,
 
 static void insert_segment(mto_doc *d, int pos, Seg *seg, int ref_seq, int client_id, int seq) {
     insert_segments(d, pos, &seg, 1, ref_seq, client_id, seq);
+}
+
+/* ------------------------------------------------------------------ marker ids, relative positions */
+static int jv_int(const jv *v, int *out);
+/* String(v) of a JSON value as an object key (idToSegment[id]) */
+static u16 *js_key_of(const jv *v, int *n) {
+    u16buf b = {NULL, 0, 0};
+    js_to_string(v, &b);
+    if (!b.p) b.p = (u16 *)malloc(sizeof(u16));
+    *n = b.n;
+    return b.p;
+}
+/* Marker.getId (mergeTree.ts:690-695): properties.markerId when truthy */
+static const jv *marker_id(const Seg *s) {
+    if (s->kind != SEG_MARKER || !s->props) return NULL;
+    static const u16 MID[8] = {'m', 'a', 'r', 'k', 'e', 'r', 'I', 'd'};
+    const jv *v = jv_obj_get(s->props, MID, 8);
+    return jv_truthy(v) ? v : NULL;
+}
+static uint32_t key_hash(const u16 *k, int kl) {
+    uint32_t h = 2166136261u;
+    for (int i = 0; i < kl; i++) h = (h ^ k[i]) * 16777619u;
+    return h;
+}
+/* index of key k in the id map, or -1 */
+static int id_find(mto_doc *d, const u16 *k, int kl) {
+    if (!d->id_hcap) return -1;
+    for (uint32_t h = key_hash(k, kl) & (uint32_t)(d->id_hcap - 1);; h = (h + 1) & (uint32_t)(d->id_hcap - 1)) {
+        const int e = d->id_hash[h];
+        if (!e) return -1;
+        if (u16_eq(d->id_keys[e - 1], d->id_klens[e - 1], k, kl)) return e - 1;
+    }
+}
+static Seg *id_lookup(mto_doc *d, const u16 *k, int kl) {
+    const int i = id_find(d, k, kl);
+    return i < 0 ? NULL : d->id_segs[i];
+}
+static void id_rehash(mto_doc *d) {
+    d->id_hcap = d->id_hcap ? 2 * d->id_hcap : 16;
+    free(d->id_hash);
+    d->id_hash = (int *)calloc((size_t)d->id_hcap, sizeof(int));
+    for (int i = 0; i < d->n_ids_map; i++) {
+        uint32_t h = key_hash(d->id_keys[i], d->id_klens[i]) & (uint32_t)(d->id_hcap - 1);
+        while (d->id_hash[h]) h = (h + 1) & (uint32_t)(d->id_hcap - 1);
+        d->id_hash[h] = i + 1;
+    }
+}
+/* mapIdToSegment (mergeTree.ts:1185-1187) */
+static void map_marker_id(mto_doc *d, Seg *s) {
+    const jv *id = marker_id(s);
+    if (!id) return;
+    if (s->id_jv == id) { /* same id object as last time: same entry */
+        d->id_segs[s->id_idx] = s;
+        return;
+    }
+    int kl;
+    u16 *k = js_key_of(id, &kl);
+    int i = id_find(d, k, kl);
+    if (i >= 0) {
+        free(k);
+    } else {
+        if (d->n_ids_map == d->cap_ids_map) {
+            d->cap_ids_map = d->cap_ids_map ? 2 * d->cap_ids_map : 8;
+            d->id_keys = (u16 **)realloc(d->id_keys, sizeof(u16 *) * (size_t)d->cap_ids_map);
+            d->id_klens = (int *)realloc(d->id_klens, sizeof(int) * (size_t)d->cap_ids_map);
+            d->id_segs = (Seg **)realloc(d->id_segs, sizeof(Seg *) * (size_t)d->cap_ids_map);
+        }
+        i = d->n_ids_map++;
+        d->id_keys[i] = k;
+        d->id_klens[i] = kl;
+        if (2 * d->n_ids_map > d->id_hcap) id_rehash(d);
+        else {
+            uint32_t h = key_hash(k, kl) & (uint32_t)(d->id_hcap - 1);
+            while (d->id_hash[h]) h = (h + 1) & (uint32_t)(d->id_hcap - 1);
+            d->id_hash[h] = i + 1;
+        }
+    }
+    d->id_segs[i] = s;
+    jv_unref((jv *)s->id_jv);
+    s->id_jv = jv_ref((jv *)id); /* held: the cached address cannot be reused by another value */
+    s->id_idx = i;
+}
+/* getPosition (mergeTree.ts:1586-1603): view lengths of everything before `node` on its path to the
+   root (an unlinked node has no parent: 0) */
+static int get_position(mto_doc *d, Node *node, int ref_seq, int client_id) {
+    int total = 0;
+    Block *prev = NULL;
+    for (Block *p = node->parent; p; prev = p, p = p->n.parent)
+        for (int i = 0; i < p->child_count; i++) {
+            Node *c = p->children[i];
+            if ((prev && c == &prev->n) || c == node) break;
+            total += node_length(d, c, ref_seq, client_id);
+        }
+    return total;
+}
+/* posFromRelativePos (mergeTree.ts:1942-1966): -1 when the id names no marker */
+static int pos_from_relative_pos(mto_doc *d, const jv *rel, int ref_seq, int client_id) {
+    int pos = -1;
+    const jv *id = rel && rel->kind == JV_OBJ ? jv_obj_get_ascii(rel, "id") : NULL;
+    Seg *m = NULL;
+    if (jv_truthy(id)) {
+        int kl;
+        u16 *k = js_key_of(id, &kl);
+        m = id_lookup(d, k, kl);
+        free(k);
+    }
+    if (m) {
+        pos = get_position(d, &m->n, ref_seq, client_id);
+        const jv *before = jv_obj_get_ascii(rel, "before"), *off = jv_obj_get_ascii(rel, "offset");
+        int o = 0;
+        if (off && off->kind != JV_UNDEF && !jv_int(off, &o)) fail(d, MTO_UNSUPPORTED, "non-integer offset");
+        if (!jv_truthy(before)) {
+            pos += m->n.cached_length;
+            if (off) pos += o;
+        } else if (off) {
+            pos -= o;
+        }
+    }
+    return pos;
 }
 
 typedef struct {
@@ -1027,6 +1163,7 @@ void mto_free(mto_doc *d) {
         free(s->text);
         free(s->ovl);
         jv_unref(s->props);
+        jv_unref((jv *)s->id_jv);
         free(s);
         s = n;
     }
@@ -1037,6 +1174,11 @@ void mto_free(mto_doc *d) {
     }
     for (int i = 0; i < d->n_ids; i++) free(d->long_ids[i]);
     free(d->long_ids);
+    for (int i = 0; i < d->n_ids_map; i++) free(d->id_keys[i]);
+    free(d->id_keys);
+    free(d->id_klens);
+    free(d->id_segs);
+    free(d->id_hash);
     free(d->long_client_id);
     free(d->heap);
     free_blobs(d);
@@ -1129,7 +1271,16 @@ static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int
     int pos1 = 0, pos2 = 0;
     int has1 = jv_int(jv_obj_get_ascii(op, "pos1"), &pos1);
     int has2 = jv_int(jv_obj_get_ascii(op, "pos2"), &pos2);
-    if (type != 3 && !has1) fail(d, MTO_UNSUPPORTED, "relative positions are not supported");
+    /* getValidOpRange (client.ts:485-502): pos undefined and relativePos given -> posFromRelativePos */
+    if (type != 3 && !jv_obj_get_ascii(op, "pos1") && jv_truthy(jv_obj_get_ascii(op, "relativePos1"))) {
+        pos1 = pos_from_relative_pos(d, jv_obj_get_ascii(op, "relativePos1"), ref_seq, short_id);
+        has1 = 1;
+    }
+    if ((type == 1 || type == 2) && !jv_obj_get_ascii(op, "pos2") && jv_truthy(jv_obj_get_ascii(op, "relativePos2"))) {
+        pos2 = pos_from_relative_pos(d, jv_obj_get_ascii(op, "relativePos2"), ref_seq, short_id);
+        has2 = 1;
+    }
+    if (type != 3 && !has1) fail(d, MTO_UNSUPPORTED, "op without a position");
     switch (type) {
         case 0: { /* applyInsertOp, client.ts:393-441 */
             const jv *segspec = jv_obj_get_ascii(op, "seg");
@@ -2029,6 +2180,14 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
     if (op->type != MT_OP_NOOP && d->long_client_id && sid == d->cw.client_id)
         fail(d, MTO_UNSUPPORTED, "ack of a local op (observer path only)");
     uint32_t bits = MT_OPF_BITS(op->flags);
+    mt_op rop;
+    if (d->rel_pending && op->type != MT_OP_RELPOS) { /* positions resolved by the RELPOS record */
+        rop = *op;
+        if (d->rel_pending & 1) rop.pos1 = d->rel_pos1;
+        if (d->rel_pending & 2) rop.pos2 = d->rel_pos2;
+        d->rel_pending = 0;
+        op = &rop;
+    }
     switch (op->type) {
         case MT_OP_INSERT: {
             Seg *s;
@@ -2065,6 +2224,25 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
             jv_unref(co.def);
             jv_unref(co.min);
             complete_remote_op(d, op->seq, op->msn);
+            break;
+        }
+        case MT_OP_RELPOS: { /* getValidOpRange of the next record (client.ts:485-502) */
+            d->rel_pending = 0;
+            for (int k = 0; k < 2; k++) {
+                const uint32_t f = op->flags;
+                if (!(f & (k ? MT_RELF_POS2 : MT_RELF_POS1))) continue;
+                const uint32_t idv = (uint32_t)(k ? op->pos2 : op->pos1);
+                jv *rel = jv_new(JV_OBJ);
+                if (idv) jv_obj_set_ascii(rel, "id", value_from_record(d, idv, t));
+                if (f & (k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1)) jv_obj_set_ascii(rel, "before", jv_new(JV_TRUE));
+                if (f & (k ? MT_RELF_OFF2 : MT_RELF_OFF1))
+                    jv_obj_set_ascii(rel, "offset", jv_new_num((double)(int32_t)(k ? op->payload_len : op->payload)));
+                const int pos = pos_from_relative_pos(d, rel, op->ref_seq, sid);
+                jv_unref(rel);
+                if (k) d->rel_pos2 = pos;
+                else d->rel_pos1 = pos;
+                d->rel_pending |= 1 << k;
+            }
             break;
         }
         case MT_OP_NOOP: break;

@@ -97,3 +97,93 @@ COMBINE_DOCS = [
      _msg("A", 5, 4, {"type": 0, "pos1": 9, "seg": "y"}, 4)],
 ]
 
+
+
+def _probe_ok(msgs):
+    """True when the oracle replays `msgs` without an error status."""
+    d = O.Doc()
+    d.start_collab("readonly")
+    for m in msgs:
+        if d.apply_msg(json.dumps(m)) != 0:
+            return False
+    return True
+
+
+def relpos_farm(n_ops, seed, n_clients=5, lag=12, rel_pct=20):
+    """A valid conflict-farm log with markers carrying ids (props.markerId) and ops addressed by
+    relative positions (relativePos1 / relativePos2: a marker id, before, offset — client.ts:485-502,
+    mergeTree.ts:1942-1966).  Every relative op is checked by replaying the log with the oracle;
+    one that would fail is replaced by a positional insert."""
+    rnd = random.Random(seed)
+    names = [f"r{i}" for i in range(n_clients)]
+    model = O.Doc()
+    model.start_collab("readonly")
+    short, last_ref, msgs, ids = {}, {}, [], []
+    for k in range(1, n_ops + 1):
+        c = names[rnd.randrange(n_clients)]
+        ref = max(last_ref.get(c, 0), k - 1 - rnd.randrange(lag + 1))
+        last_ref[c] = ref
+        msn = min(last_ref.values()) if len(last_ref) == n_clients else 0
+        sid = short.get(c, len(short) + 1)
+        n = model.view_length(ref, sid)
+        u = rnd.randrange(100)
+        contents = None
+        if ids and u < rel_pct:
+            rel = {"id": rnd.choice(ids)}
+            if rnd.random() < 0.5:
+                rel["before"] = True
+            if rnd.random() < 0.4:
+                rel["offset"] = rnd.randrange(0, 3)
+            kind = rnd.randrange(3)
+            if kind == 0:
+                contents = {"type": 0, "relativePos1": rel, "seg": rnd.choice(["x", "yz", "\n"])}
+            elif kind == 1 and n > 0:
+                contents = {"type": 1, "pos1": rnd.randrange(n), "relativePos2": rel}
+            else:
+                contents = {"type": 2, "relativePos1": rel, "pos2": n, "props": {"r": rnd.randrange(3)}}
+            if not _probe_ok(msgs + [_msg(c, k, ref, contents, msn)]):
+                contents = None
+        if contents is None:
+            if n < 4 or u < 60:
+                if rnd.random() < 0.25:
+                    mid = f"m{k}"
+                    ids.append(mid)
+                    seg = {"marker": {"refType": 1}, "props": {"markerId": mid}}
+                else:
+                    seg = "".join(rnd.choice("abcde") for _ in range(rnd.randint(1, 4)))
+                contents = {"type": 0, "pos1": rnd.randrange(n + 1), "seg": seg}
+            else:
+                a = rnd.randrange(n)
+                b = min(n, a + 1 + rnd.randrange(4))
+                contents = {"type": 1, "pos1": a, "pos2": b} if u < 85 else \
+                    {"type": 2, "pos1": a, "pos2": b, "props": {"k": rnd.randrange(3)}}
+        m = _msg(c, k, ref, contents, msn)
+        assert model.apply_msg(json.dumps(m)) == 0, model.error
+        short.setdefault(c, len(short) + 1)
+        msgs.append(m)
+    return msgs
+
+
+RELPOS_DOCS = [
+    # insert before / after a marker, with offsets; a range ending at a marker
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "hello world"}),
+     _msg("A", 2, 1, {"type": 0, "pos1": 5, "seg": {"marker": {"refType": 1}, "props": {"markerId": "p1"}}}),
+     _msg("B", 3, 2, {"type": 0, "relativePos1": {"id": "p1"}, "seg": "A"}),
+     _msg("B", 4, 3, {"type": 0, "relativePos1": {"id": "p1", "before": True}, "seg": "B"}),
+     _msg("A", 5, 3, {"type": 0, "relativePos1": {"id": "p1", "offset": 2}, "seg": "C"}),
+     _msg("B", 6, 5, {"type": 1, "pos1": 0, "relativePos2": {"id": "p1", "before": True, "offset": 1}}),
+     _msg("A", 7, 6, {"type": 2, "relativePos1": {"id": "p1"}, "pos2": 9, "props": {"x": 1}})],
+    # numeric id (idToSegment keys are strings: 7 and "7" are the same key), ids in a group
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abcdef"}),
+     _msg("A", 2, 1, {"type": 3, "ops": [
+         {"type": 0, "pos1": 3, "seg": {"marker": {"refType": 2}, "props": {"markerId": 7}}},
+         {"type": 0, "relativePos1": {"id": "7", "before": True}, "seg": "Q"}]}),
+     _msg("B", 3, 1, {"type": 0, "relativePos1": {"id": 7}, "seg": "R"})],
+    # a removed marker unlinked by zamboni: the reference's map keeps the detached marker
+    # (getPosition 0), so "after" it is position 1
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abcdef"}),
+     _msg("A", 2, 1, {"type": 0, "pos1": 2, "seg": {"marker": {"refType": 1}, "props": {"markerId": "gone"}}}, 1),
+     _msg("A", 3, 2, {"type": 1, "pos1": 2, "pos2": 3}, 2),
+     _msg("A", 4, 3, {"type": 0, "pos1": 0, "seg": "zz"}, 4),
+     _msg("A", 5, 4, {"type": 0, "relativePos1": {"id": "gone"}, "seg": "!"}, 5)],
+]

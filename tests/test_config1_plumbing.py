@@ -99,10 +99,10 @@ def test_config1_node_packer_is_byte_identical(farm, tmp_path):
 
 @pytest.mark.skipif(NODE is None, reason="node not available")
 def test_node_packer_combining_ops_byte_identical(tmp_path):
-    """The Node packer's combiningOp records equal the Python packer's (include/mt_oplog.h)."""
-    from combine_logs import COMBINE_DOCS, combine_farm
+    """The Node packer's combiningOp and MT_OP_RELPOS records equal the Python packer's (include/mt_oplog.h)."""
+    from combine_logs import COMBINE_DOCS, RELPOS_DOCS, combine_farm, relpos_farm
 
-    docs = COMBINE_DOCS + [combine_farm(300, seed=3)]
+    docs = COMBINE_DOCS + [combine_farm(300, seed=3)] + RELPOS_DOCS + [relpos_farm(150, seed=3)]
     src = tmp_path / "msgs.json"
     src.write_text(json.dumps(docs))
     code = ("const {Packer}=require('./fluidframework_amd/js');const fs=require('fs');"

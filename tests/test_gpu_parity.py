@@ -14,7 +14,7 @@ import oracle_ffi as O
 from kat_util import load_kats
 import fluidframework_amd as fa
 from fluidframework_amd import oplog
-from combine_logs import COMBINE_DOCS, combine_farm
+from combine_logs import COMBINE_DOCS, RELPOS_DOCS, combine_farm, relpos_farm
 
 pytestmark = pytest.mark.gpu
 
@@ -575,6 +575,53 @@ def test_combining_ops_outside_the_device_path_are_flagged():
     ]
     oracle = oracle_docs_from_messages(docs)
     assert [od.status for od in oracle] == [0, 0, 0, fa.MT_UNSUPPORTED]
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs)
+        b.run()
+        assert [b.doc(i).status for i in range(len(docs))] == [fa.MT_UNSUPPORTED] * len(docs)
+
+
+def test_relative_positions_match_oracle():
+    """Ops addressed by marker ids (relativePos1 / relativePos2 with before / offset:
+    Client.getValidOpRange client.ts:485-502, MergeTree.posFromRelativePos mergeTree.ts:1942-1966,
+    getPosition :1586-1603): numeric and string ids, ids inside a GROUP, a marker unlinked by
+    zamboni (the reference's map keeps the detached marker: position 0), random farms.  GPU == oracle
+    on digest / text / props / SnapshotV1, also through checkpoint / resume."""
+    docs = RELPOS_DOCS + [relpos_farm(400, seed=s) for s in (1, 2, 3, 4)]
+    oracle = oracle_docs_from_messages(docs)
+    for od in oracle:
+        assert od.status == 0, od.error
+    for opts in ({}, {"seg_cap": 64}):
+        with fa.ReplayBatch(len(docs), **opts) as b:
+            b.ingest_messages(docs)
+            b.run()
+            for i in range(len(docs)):
+                assert b.doc(i).status == 0, (i, fa.status_string(b.doc(i).status))
+                assert_doc_parity(b.doc(i), oracle[i], full=not opts)
+    with fa.ReplayBatch(len(docs)) as b:  # the native JSON ingest packs them the same way
+        b.ingest_json([json.dumps(d) for d in docs])
+        b.run()
+        for i in range(len(docs)):
+            assert_doc_parity(b.doc(i), oracle[i], full=False)
+
+
+def test_relative_positions_outside_the_device_path_are_flagged():
+    """An id that names no marker (the reference passes position -1 on), an id two markers carry
+    (the reference's map follows its blockUpdate order) and ids re-annotated on markers are
+    MT_UNSUPPORTED on the device, never silently different."""
+    mk = lambda i: {"marker": {"refType": 1}, "props": {"markerId": i}}
+    docs = [
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"}),
+         _msg("A", 2, 1, {"type": 0, "relativePos1": {"id": "nope"}, "seg": "x"})],
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"}),
+         _msg("A", 2, 1, {"type": 0, "pos1": 1, "seg": mk("d")}),
+         _msg("A", 3, 2, {"type": 0, "pos1": 3, "seg": mk("d")}),
+         _msg("A", 4, 3, {"type": 0, "relativePos1": {"id": "d"}, "seg": "x"})],
+        [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"}),
+         _msg("A", 2, 1, {"type": 0, "pos1": 1, "seg": mk("e")}),
+         _msg("A", 3, 2, {"type": 2, "pos1": 1, "pos2": 2, "props": {"markerId": "f"}}),
+         _msg("A", 4, 3, {"type": 0, "relativePos1": {"id": "e"}, "seg": "x"})],
+    ]
     with fa.ReplayBatch(len(docs)) as b:
         b.ingest_messages(docs)
         b.run()

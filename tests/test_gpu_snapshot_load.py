@@ -179,3 +179,27 @@ def test_snapshot_roundtrip_kats():
             od = _oracle_loaded(od.snapshot_v1(), docs[i]["messages"])
             assert b.doc(i).get_text() == k["text"], k["name"]
             _check(b, i, od)
+
+
+def test_snapshot_markers_with_ids_then_relative_ops():
+    """Markers with ids in a loaded SnapshotV1 (header: reloadFromSegments maps the ids of markers
+    that are not removed; body: insertSegments maps every one), then catch-up ops addressed by those
+    ids: GPU == oracle (the oracle's own loader)."""
+    from combine_logs import relpos_farm
+
+    docs, oracle = [], []
+    for seed, cut, chunk in ((11, 150, 10000), (12, 250, 40), (13, 300, 10000)):
+        msgs = relpos_farm(350, seed=seed)
+        a = O.Doc()
+        a.start_collab("readonly")
+        for m in msgs[:cut]:
+            assert a.apply_msg(json.dumps(m)) == 0, a.error
+        blobs = a.snapshot_v1(chunk)
+        docs.append({"snapshot": blobs, "messages": msgs[cut:]})
+        oracle.append(_oracle_loaded(blobs, msgs[cut:]))
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_json([json.dumps(d) for d in docs])
+        b.run()
+        b.snapshots()
+        for i, od in enumerate(oracle):
+            _check(b, i, od)

@@ -107,9 +107,9 @@ def test_raw_bytes_and_whitespace():
 
 
 def test_unsupported_and_malformed_logs_fail_with_the_document_index():
-    rel = [_msg("A", 1, 0, {"type": 0, "relativePos1": {"id": "x"}, "pos1": 0, "seg": "a"})]
+    reg = [_msg("A", 1, 0, {"type": 0, "register": "r", "pos1": 0, "seg": "a"})]  # registers: not on the path
     with pytest.raises(MtError) as e:
-        PackedJson([json.dumps(EDGE_DOCS[0]), json.dumps(rel)])
+        PackedJson([json.dumps(EDGE_DOCS[0]), json.dumps(reg)])
     assert e.value.code == MT_UNSUPPORTED and "document 1" in str(e.value)
     with pytest.raises(MtError) as e:
         PackedJson(["[]", '[{"clientId": "A", "sequenceNumber": 1,'])
@@ -134,12 +134,19 @@ def test_combining_ops_pack_identically():
     _assert_same(COMBINE_DOCS + [combine_farm(400, seed=5)], n_threads=2)
 
 
+def test_relative_positions_pack_identically():
+    """MT_OP_RELPOS records (include/mt_oplog.h) for ops addressed by marker ids."""
+    from combine_logs import RELPOS_DOCS, relpos_farm
+
+    _assert_same(RELPOS_DOCS + [relpos_farm(200, seed=4)], n_threads=2)
+
+
 def test_oracle_packed_combine_matches_json_replay():
     """The oracle's packed path (defaultValue / minValue from the records, values re-created per op
     as JSON.parse would) replays combining ops exactly like its JSON path."""
-    from combine_logs import COMBINE_DOCS, combine_farm
+    from combine_logs import COMBINE_DOCS, RELPOS_DOCS, combine_farm, relpos_farm
 
-    docs = COMBINE_DOCS + [combine_farm(600, seed=9)]
+    docs = COMBINE_DOCS + [combine_farm(600, seed=9)] + RELPOS_DOCS + [relpos_farm(250, seed=8)]
     pb = oplog.pack_documents(docs)
     t = O.Tables(pb.keys, pb.values)
     for i, msgs in enumerate(docs):
