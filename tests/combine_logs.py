@@ -109,11 +109,23 @@ def _probe_ok(msgs):
     return True
 
 
-def relpos_farm(n_ops, seed, n_clients=5, lag=12, rel_pct=20):
+def _live_ids(doc):
+    """ids of the markers the oracle's segment table holds and has not removed (mto_dump lines;
+    a marker zamboni unlinked is gone from the table)"""
+    out = set()
+    for ln in doc.dump().splitlines():
+        if '"markerId"' in ln and " rseq=-1 " in ln:
+            out.add(json.loads(ln[ln.index("{"):])["markerId"])
+    return out
+
+
+def relpos_farm(n_ops, seed, n_clients=5, lag=12, rel_pct=20, live_ids_only=False):
     """A valid conflict-farm log with markers carrying ids (props.markerId) and ops addressed by
     relative positions (relativePos1 / relativePos2: a marker id, before, offset — client.ts:485-502,
     mergeTree.ts:1942-1966).  Every relative op is checked by replaying the log with the oracle;
-    one that would fail is replaced by a positional insert."""
+    one that would fail is replaced by a positional insert.  live_ids_only: relative ops name only
+    markers not removed so far (a SnapshotV1 reload maps only those: snapshotLoader via
+    reloadFromSegments' addNodeReferences, mergeTree.ts:270-285)."""
     rnd = random.Random(seed)
     names = [f"r{i}" for i in range(n_clients)]
     model = O.Doc()
@@ -128,11 +140,15 @@ def relpos_farm(n_ops, seed, n_clients=5, lag=12, rel_pct=20):
         n = model.view_length(ref, sid)
         u = rnd.randrange(100)
         contents = None
-        if ids and u < rel_pct:
-            rel = {"id": rnd.choice(ids)}
+        cands = ids
+        if live_ids_only and ids and u < rel_pct:
+            live = _live_ids(model)
+            cands = [i for i in ids if i in live]
+        if cands and u < rel_pct:
+            rel = {"id": rnd.choice(cands)}
             if rnd.random() < 0.5:
-                rel["before"] = True
-            if rnd.random() < 0.4:
+                rel["before"] = True  # (an offset before a marker can reach below 0: not on the device)
+            elif rnd.random() < 0.4:
                 rel["offset"] = rnd.randrange(0, 3)
             kind = rnd.randrange(3)
             if kind == 0:

@@ -189,7 +189,7 @@ def test_snapshot_markers_with_ids_then_relative_ops():
 
     docs, oracle = [], []
     for seed, cut, chunk in ((11, 150, 10000), (12, 250, 40), (13, 300, 10000)):
-        msgs = relpos_farm(350, seed=seed)
+        msgs = relpos_farm(350, seed=seed, live_ids_only=True)
         a = O.Doc()
         a.start_collab("readonly")
         for m in msgs[:cut]:
