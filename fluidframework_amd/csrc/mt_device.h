@@ -78,10 +78,15 @@ constexpr uint32_t kMetaUnsettled = 1u << 19;
 constexpr uint32_t kMetaHasProps = 1u << 20;
 constexpr uint32_t kMetaHasNL = 1u << 21;
 constexpr uint32_t kMetaHasOvl = 1u << 22;
+//   [23]   in a pending (unacked) local segment group of a writer replica: its groups are the bits
+//          of the cold record's pending mask (cold[2 slot + 1].z / .w, bit G & 63 of group G)
+constexpr uint32_t kMetaPending = 1u << 23;
 __host__ __device__ constexpr uint32_t meta_cli(uint32_t m) { return m & kMetaCli; }
 __host__ __device__ constexpr uint32_t meta_rcli(uint32_t m) { return (m >> kMetaRcliShift) & kMetaCli; }
 // 16-bit window-relative sequence numbers in LDS (s_sr[slot] = seq16 | rseq16 << 16, see mt_engine.hip)
 constexpr uint32_t kSeq16None = 0xFFFFu;  // rseq16 of a segment that is not removed
+constexpr uint32_t kSeq16Unassigned = 0xFFFEu;  // seq16 / rseq16 of a pending local insert / remove
+constexpr int32_t kUnassignedSeq = -1;  // UnassignedSequenceNumber (constants.ts:11): real seqs of pending ops
 constexpr int32_t kSeq16Span = 0xFFF0;    // cur_seq - base must stay below (else MT_CAPACITY, cap_kind 5)
 constexpr uint32_t kHeapInvalid = 0xFFFFFFFFu;  // heap entry whose segment was merged away / unlinked
 constexpr uint16_t kNoBlock = 0xFFFFu;
@@ -155,6 +160,19 @@ constexpr int kReplayStartClass = 1;  // replay starts documents in at most the 
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS class (16-bit lengths)
 constexpr int kCapQueued = 7;      // checkpointed and taken by the launch's follow-on workers
+
+// Writer replicas (the local-client path, mergeTree.ts:1893-1929, client.ts:588-625): per document
+// a pending-group region in HBM, persistent across launches (u32 words):
+//   [0] pending groups n   [1] id G of the oldest (groups are numbered in creation order)
+//   [2] first entry that may be live   [3] entries used
+//   [kPendDesc ..) per group G & 63: {type | flags << 16, prop-record offset, prop count, 0}
+//   [kPendEntries ..) entries {G, slot} in append order (the group's `segments` array order:
+//   members as the op reached them, split-off halves appended when the split happens)
+constexpr int kPendMaxGroups = 64;  // unacked local ops at once (more: MT_UNSUPPORTED)
+constexpr int kPendDesc = 8;
+constexpr int kPendEntries = kPendDesc + 4 * kPendMaxGroups;
+constexpr int kCapPending = 9;  // DocOut.cap_kind: the pending-entry region is full (terminal)
+constexpr int64_t pend_words(int32_t cap) { return kPendEntries + 2ll * cap; }
 
 // follow-on queue (one per producer launch, hipMalloc'd, zeroed): word 0 = documents enqueued,
 // 1 = items claimed by workers, 2 = producer workgroups finished, 3 = unused, 4 = a consumer's
@@ -270,6 +288,10 @@ struct ReplayParams {
     // {marker-id key, slot} entries in mapping order (kIdUnlinked: the marker was unlinked)
     uint2 *idmap;
     const uint64_t *doc_idmap_base;
+    // writer replicas (mt_writer_kernel_<SEG>): per-document pending-group regions (pend_words)
+    uint32_t *pend;
+    const uint64_t *doc_pend_base;
+    int32_t pend_cap;             // entries per document
 };
 constexpr uint32_t kIdUnlinked = 0xFFFFFFFFu;
 constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // RELPOS key the host cannot resolve safely

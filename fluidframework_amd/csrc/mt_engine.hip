@@ -142,7 +142,10 @@ struct LWord {
     MT_FI LWord &operator++(int) { return *this = (T)(T(*this) + 1); }
 };
 
-template <int SEG>
+// kW: a writer replica (the local-client path: local ops with UnassignedSequenceNumber, pending
+// segment groups acked by the replica's own sequenced messages); compiled as mt_writer_kernel_<SEG>
+// so the observer kernels carry none of it
+template <int SEG, bool kW = false>
 struct Engine {
     static constexpr Caps cap = class_caps(SEG);
     static constexpr Layout lay = make_layout(SEG);
@@ -186,6 +189,10 @@ struct Engine {
     // marker ids (idToSegment) and the positions an MT_OP_RELPOS record resolved for the next op
     LWord<int32_t> idmap_n, rel_pend, rel_p1, rel_p2;
     uint2 *idmap;
+    // writer replicas: the document's pending-group region (mt_device.h kPendDesc / kPendEntries)
+    // and its group count (kept in HBM word 0 as well, so checkpoints carry it)
+    uint32_t *pend;
+    int32_t pend_cap_e, n_pend;
     int32_t htop;
     uint2 *h_ent;
     // ---- global
@@ -361,20 +368,30 @@ struct Engine {
         const uint32_t meta = s_meta[slot];
         const uint32_t len = s_len[slot];
         bool vis, rle;
+        bool pending = false;  // writer: an unacked local insert (seq === UnassignedSequenceNumber)
         if (ref >= min_seq) {
             const uint32_t sr = s_sr[slot];
             const uint32_t r16 = (uint32_t)(ref - sbase);
             vis = (meta_cli(meta) == c) || ((sr & 0xFFFFu) <= r16);
             rle = (sr >> 16) <= r16;
+            if constexpr (kW) pending = (sr & 0xFFFFu) == kSeq16Unassigned;
         } else {
             const uint4 q = cold[2 * slot + 1];
-            vis = (meta_cli(meta) == c) || ((int32_t)q.x <= ref);
-            rle = (int32_t)q.y <= ref;
+            if constexpr (kW) {
+                pending = (int32_t)q.x == kUnassignedSeq;
+                vis = (meta_cli(meta) == c) || (!pending && (int32_t)q.x <= ref);
+                rle = (int32_t)q.y != kUnassignedSeq && (int32_t)q.y <= ref;
+            } else {
+                vis = (meta_cli(meta) == c) || ((int32_t)q.x <= ref);
+                rle = (int32_t)q.y <= ref;
+            }
         }
         bool rem = (meta_rcli(meta) == c) || rle;
         if (!rem && (meta & kMetaHasOvl)) rem = ovl_has(slot, c);
         vlen = (vis && !rem) ? len : 0u;
-        tie = !rle;
+        // breakTie's leaf rule: a remote op does not insert before a pending local segment; the
+        // local client breaks every tie it reaches (mergeTree.ts:2263-2271)
+        tie = !rle && (!kW || c == 0u || !pending);
     }
     MT_FI static bool sr_removed(uint32_t sr) { return (sr >> 16) != kSeq16None; }
     // a leaf's contribution to the settled block sums
@@ -532,8 +549,12 @@ struct Engine {
             if (keep) {
                 u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (Idx)slot;
                 const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
-                const uint32_t nq = q16 > m16 ? q16 - m16 : 0u;
-                const uint32_t nr = r16 == kSeq16None ? kSeq16None : (r16 > m16 ? r16 - m16 : 0u);
+                uint32_t nq = q16 > m16 ? q16 - m16 : 0u;
+                uint32_t nr = r16 == kSeq16None ? kSeq16None : (r16 > m16 ? r16 - m16 : 0u);
+                if constexpr (kW) {  // pending local ops keep their sentinel
+                    if (q16 == kSeq16Unassigned) nq = kSeq16Unassigned;
+                    if (r16 == kSeq16Unassigned) nr = kSeq16Unassigned;
+                }
                 s_sr[slot] = nq | (nr << 16);
             }
             if (elig) {
@@ -901,6 +922,18 @@ struct Engine {
         s_len[slot] = (Len)r;
         wsync();
         if (meta & kMetaUnsettled) u_push((uint32_t)ns);
+        if constexpr (kW) {
+            // segmentGroups.copyTo (mergeTree.ts:560): the right half joins every group of the
+            // segment, oldest first, at the end of each group's segments; its cold record (written
+            // by resolve_cold) carries the same pending mask
+            if (meta & kMetaPending) {
+                const uint64_t m = (uint64_t)rdl(pv, 6) | ((uint64_t)rdl(pv, 7) << 32);
+                const uint32_t head = pend_word(1);
+                for (int32_t i = 0; i < n_pend && !status; i++)
+                    if ((m >> ((head + (uint32_t)i) & 63u)) & 1ull) entry_append(head + (uint32_t)i, (uint32_t)ns);
+                if (status) return -1;
+            }
+        }
         const int32_t nb = insert_leaf(blk, k + 1, (uint32_t)ns);
         if (meta & kMetaHasOvl) resolve_cold();  // view_of reads the halves' overlap masks from HBM
         return nb;
@@ -974,6 +1007,215 @@ struct Engine {
             W.excl = pos;
         }
         return W;
+    }
+
+    // ------------------------------------------------------------------ writer: pending segment groups
+    // MergeTree.pendingSegments / SegmentGroup (mergeTree.ts:1093, 1922-1929) in the document's HBM
+    // region (mt_device.h kPendDesc / kPendEntries); lane 0 writes, every lane reads back.
+    MT_FI uint32_t pend_word(int i) const { return rfl(pend[i]); }
+    MT_FI uint64_t pend_mask(uint32_t slot) const {
+        const uint4 q = cold[2 * slot + 1];
+        return (uint64_t)rfl(q.z) | ((uint64_t)rfl(q.w) << 32);
+    }
+    MT_FI void pend_set_mask(uint32_t slot, uint64_t m) {
+        if (lane == 0) {
+            cold[2 * slot + 1].z = (uint32_t)m;
+            cold[2 * slot + 1].w = (uint32_t)(m >> 32);
+        }
+        const uint32_t meta = s_meta[slot];
+        s_meta[slot] = m ? (meta | kMetaPending) : (meta & ~kMetaPending);
+        wsync();
+    }
+    // live entries (of pending groups) move to the front, in order
+    MT_FI void pend_compact() {
+        const uint32_t head = pend_word(1), start = pend_word(2), n = pend_word(3);
+        uint2 *E = (uint2 *)(pend + kPendEntries);
+        uint32_t w = 0;
+        for (uint32_t b0 = start; b0 < n; b0 += kWave) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            const uint2 e = j < n ? E[j] : make_uint2(0u, 0u);
+            const bool live = j < n && e.x - head < (uint32_t)n_pend;
+            const uint64_t m = ballot(live);
+            if (live) E[w + __popcll(m & ((1ull << lane) - 1ull))] = e;
+            w += __popcll(m);
+        }
+        if (lane == 0) {
+            pend[2] = 0u;
+            pend[3] = w;
+        }
+    }
+    // SegmentGroupCollection.enqueue (segmentGroupCollection.ts:24-27): group G gets `slot` last
+    MT_FI void entry_append(uint32_t G, uint32_t slot) {
+        uint32_t n = pend_word(3);
+        if (n >= (uint32_t)pend_cap_e) {
+            pend_compact();
+            n = pend_word(3);
+            if (n >= (uint32_t)pend_cap_e) {
+                cap_fail(kCapPending);
+                return;
+            }
+        }
+        if (lane == 0) {
+            ((uint2 *)(pend + kPendEntries))[n] = make_uint2(G, slot);
+            pend[3] = n + 1u;
+        }
+    }
+    // addToPendingList (mergeTree.ts:1922-1929) for the current local op: its group is created with
+    // its first segment (cur_g < 0 until then)
+    int32_t cur_g;
+    MT_FI void pend_add(uint32_t slot, const mt_op &op) {
+        resolve_cold();  // the split halves' cold records (pending masks) are in HBM
+        if (cur_g < 0) {
+            if (n_pend >= kPendMaxGroups) {
+                set_fail(ST_UNSUPPORTED);
+                return;
+            }
+            cur_g = (int32_t)(pend_word(1) + (uint32_t)n_pend);
+            if (lane == 0) {
+                *(uint4 *)(pend + kPendDesc + 4 * (cur_g & 63)) =
+                    make_uint4((uint32_t)op.type | ((uint32_t)op.flags << 16), op.payload, op.payload_len, 0u);
+                pend[0] = (uint32_t)(n_pend + 1);
+            }
+            n_pend++;
+        }
+        entry_append((uint32_t)cur_g, slot);
+        if (status) return;
+        pend_set_mask(slot, pend_mask(slot) | (1ull << (cur_g & 63)));
+    }
+    // the keys of the pending local annotates holding `slot` (lane j < npk: key j) and whether one of
+    // them is a rewrite: SegmentPropertiesManager.pendingKeyUpdateCount / pendingRewriteCount
+    // (segmentPropertiesManager.ts:12-14, 49-51, 56-63)
+    MT_FI void pending_keys(uint32_t slot, uint32_t &pk, uint32_t &npk, bool &prw) {
+        const uint64_t m = pend_mask(slot);
+        const uint32_t head = pend_word(1);
+        npk = 0;
+        pk = 0;
+        prw = false;
+        for (int32_t i = 0; i < n_pend; i++) {
+            const uint32_t b = (head + (uint32_t)i) & 63u;
+            if (!((m >> b) & 1ull)) continue;
+            const uint32_t *dp = pend + kPendDesc + 4 * b;
+            const uint32_t tf = rfl(dp[0]), off = rfl(dp[1]), cnt = rfl(dp[2]);
+            if ((tf & 0xFFu) != MT_OP_ANNOTATE) continue;
+            if ((tf >> 16) & MT_OPF_REWRITE) prw = true;
+            for (uint32_t k = 0; k < cnt; k++) {
+                const uint32_t key = rfl(props_in[off + k].key);
+                if (ballot((uint32_t)lane < npk && pk == key)) continue;
+                if (npk >= 64u) {
+                    set_fail(ST_UNSUPPORTED);
+                    return;
+                }
+                if ((uint32_t)lane == npk) pk = key;
+                npk++;
+            }
+        }
+    }
+    // Client.ackPendingSegment -> MergeTree.ackPendingSegment (client.ts:588-625, mergeTree.ts:
+    // 1893-1920) with BaseSegment.ack (487-522): the oldest group's segments, in group order, get
+    // the op's sequence number (insert: seq; remove: removedSeq unless a sequenced remove replaced
+    // the local one; annotate: its keys stop being pending), each then addToLRUSet; then zamboni
+    MT_FI void op_ack(const mt_op &op) {
+        if (n_pend > 0) {
+            const uint32_t head = pend_word(1);
+            const uint32_t b = head & 63u;
+            const uint32_t tf = rfl(pend[kPendDesc + 4 * b]);
+            if ((tf & 0xFFu) != op.type) {  // not the op this group was made by: the stream is corrupt
+                set_fail(ST_BAD_INPUT);
+                return;
+            }
+            const uint32_t start = pend_word(2), n = pend_word(3);
+            const uint2 *E = (const uint2 *)(pend + kPendEntries);
+            for (uint32_t b0 = start; b0 < n; b0 += kWave) {
+                const uint32_t j = b0 + (uint32_t)lane;
+                const uint2 e = j < n ? E[j] : make_uint2(head + 1u, 0u);
+                uint64_t hm = ballot(j < n && e.x == head);
+                while (hm) {
+                    const uint32_t slot = rdl(e.y, first_lane(hm));
+                    hm &= hm - 1;
+                    const uint32_t sr = s_sr[slot];
+                    if (op.type == MT_OP_INSERT) {
+                        if ((sr & 0xFFFFu) != kSeq16Unassigned) {
+                            set_fail(ST_BAD_INPUT);
+                            return;
+                        }
+                        s_sr[slot] = (sr & 0xFFFF0000u) | rel16(op.seq);
+                        if (lane == 0) cold[2 * slot + 1].x = (uint32_t)op.seq;
+                    } else if (op.type == MT_OP_REMOVE) {
+                        if (!sr_removed(sr)) {
+                            set_fail(ST_BAD_INPUT);
+                            return;
+                        }
+                        if ((sr >> 16) == kSeq16Unassigned) {
+                            s_sr[slot] = (sr & 0xFFFFu) | (rel16(op.seq) << 16);
+                            if (lane == 0) cold[2 * slot + 1].y = (uint32_t)op.seq;
+                        }
+                    }
+                    pend_set_mask(slot, pend_mask(slot) & ~(1ull << b));
+                    add_to_lru(rfl((int32_t)s_blk[slot]), slot, op.seq);
+                    if (status) return;
+                }
+            }
+            // the next live entry (later groups' entries may sit behind this group's)
+            uint32_t ns = n;
+            for (uint32_t b0 = start; b0 < n; b0 += kWave) {
+                const uint32_t j = b0 + (uint32_t)lane;
+                const uint64_t lm = ballot(j < n && E[j].x - (head + 1u) < (uint32_t)(n_pend - 1));
+                if (lm) {
+                    ns = b0 + (uint32_t)first_lane(lm);
+                    break;
+                }
+            }
+            if (lane == 0) {
+                pend[0] = (uint32_t)(n_pend - 1);
+                pend[1] = head + 1u;
+                pend[2] = ns;
+            }
+            n_pend--;
+        }
+        zamboni();
+    }
+
+    // insertingWalk's continuePredicate for a remote insert (blockInsert.continueFrom, mergeTree.ts:
+    // 2154-2161, 2431-2436): a walk that finishes at the end of a leaf block continues into the next
+    // one while the first segment after the block that the local view holds (rightExcursion ->
+    // nodeMap: not removed) is a pending local insert; it goes on at that block's start (pos 0 there)
+    MT_FI Walk continue_walk(Walk W, int32_t ref, uint32_t c) {
+        for (;;) {
+            const int32_t nb = next_leaf_block(W.blk);
+            bool cont = false;
+            for (int32_t b = nb; b >= 0; b = next_leaf_block(b)) {
+                const int32_t n = b_count[b];
+                uint32_t sr = 0;
+                bool live = false;
+                if (lane < n) {
+                    sr = s_sr[b_child[b * 8 + lane]];
+                    live = !sr_removed(sr);
+                }
+                const uint64_t lm = ballot(live);
+                if (lm) {
+                    cont = (rdl(sr, first_lane(lm)) & 0xFFFFu) == kSeq16Unassigned;
+                    break;
+                }
+            }
+            if (!cont) return W;
+            const int32_t n = b_count[nb];
+            const uint32_t pos = W.excl;
+            uint32_t vlen = 0;
+            bool tie = false;
+            if (lane < n) view_of((uint32_t)b_child[nb * 8 + lane], ref, c, vlen, tie);
+            const uint32_t incl = scan8(vlen) + pos;
+            const uint32_t excl = incl - vlen;
+            const uint64_t cb = ballot(lane < n && lane < kMaxNodes && (incl > pos || (excl == pos && vlen == 0u && tie)));
+            W.blk = nb;
+            W.n = n;
+            W.ok = 1;
+            W.base = pos;
+            if (cb) {
+                W.k = first_lane(cb);
+                return W;
+            }
+            W.k = n;  // every leaf of the block is invisible to the op: its end is still pos
+        }
     }
 
     // addToLRUSet (mergeTree.ts:1273-1283); seq > currentSeq holds for sequenced remote ops
@@ -1222,8 +1464,10 @@ struct Engine {
     // the op's keys count; a key the set lacks gets `cres` (the host's combine of an undefined
     // current value, mt_host.cpp rc_resolve_combine; 0 = stays absent), a key it has keeps its
     // value, except that "incr" turns a number / boolean / NaN into NaN.
+    // Writer: pk / npk (lane j < npk: key j) are the keys of pending local annotates on the segment,
+    // which a remote op leaves alone (shouldModifyKey, segmentPropertiesManager.ts:56-63).
     MT_FI uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout,
-                                uint32_t ckind = 0u) {
+                                uint32_t ckind = 0u, uint32_t pk = 0u, uint32_t npk = 0u) {
         uint32_t *keys = scratch;
         uint32_t *vals = scratch + 64;
         uint32_t n = old ? pool[old] : 0u;
@@ -1255,6 +1499,7 @@ struct Engine {
                     uint32_t kk = rdl(ok_k, (int)i), vv = rdl(ok_v, (int)i);
                     if (kk == k && vv < vt->n_values && !(vt->flags[vv] & 1u)) keep = true;
                 }
+                for (uint32_t i = 0; i < npk; i++) keep |= rdl(pk, (int)i) == k;
             }
             uint64_t kb = ballot(keep && (uint32_t)lane < n);
             uint32_t nk = 0, kv = 0, vv2 = 0;
@@ -1274,6 +1519,7 @@ struct Engine {
         }
         for (uint32_t i = 0; i < nop; i++) {
             uint32_t k = rdl(ok_k, (int)i), v = rdl(ok_v, (int)i);
+            if (npk && ballot((uint32_t)lane < npk && pk == k)) continue;  // a pending local key
             bool hit = (uint32_t)lane < n && keys[lane] == k;
             uint64_t b = ballot(hit);
             if (v == MT_VALUE_NULL) {
@@ -1364,10 +1610,13 @@ struct Engine {
         // settle_all ran at this minSeq (sbase == minSeq): seq <= minSeq is seq16 == 0, a settled
         // removal has rseq16 == 0
         const bool rem = in && sr_removed(sr);
-        const bool cand = in && !rem && (sr & 0xFFFFu) == 0u;
+        // writer: a segment in a pending group is held as is and breaks the append chain
+        // (scourNode: segmentGroups not empty, mergeTree.ts:1295, 1353-1356)
+        const bool pend = kW && (meta & kMetaPending) != 0u;
+        const bool cand = in && !rem && !pend && (sr & 0xFFFFu) == 0u;
         const uint32_t mprev = __shfl_up(meta, 1, kWave);
         const uint64_t candM = ballot(cand);
-        const uint64_t freeR = ballot(rem && (sr >> 16) == 0u);
+        const uint64_t freeR = ballot(rem && !pend && (sr >> 16) == 0u);
         const uint64_t liveM = ballot(in);
         // lane k may append to the chain ending at lane k - 1 (TextSegment.canAppend without its
         // length rule, plus matchProperties): both candidates, same block, neither a Marker, the
@@ -1716,6 +1965,10 @@ struct Engine {
         if (status) return;
         const bool marker = (op.flags & MT_OPF_MARKER) != 0;
         const uint32_t len = marker ? 1u : op.payload_len;
+        const bool local = kW && op.seq == kUnassignedSeq;  // a writer's own unacked insert
+        if constexpr (kW) {
+            if (!local && n_pend > 0 && len > 0 && W.blk >= 0 && W.ok && W.k == W.n) W = continue_walk(W, ref, c);
+        }
         if (len > 0) {
             PF_SCOPE(3);
             if (W.blk < 0 || !W.ok) {
@@ -1747,7 +2000,8 @@ struct Engine {
             if (props) meta |= kMetaHasProps;
             s_len[slot] = (Len)len;
             s_sr[slot] = settled ? (rseq == kNoneSeq ? kSeq16None : 0u) << 16
-                                 : rel16(op.seq) | ((rseq == kNoneSeq ? kSeq16None : rel16(rseq)) << 16);
+                                 : (local ? kSeq16Unassigned : rel16(op.seq)) |
+                                       ((rseq == kNoneSeq ? kSeq16None : rel16(rseq)) << 16);
             if (lane == 0) {
                 cold[2 * slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
                 cold[2 * slot + 1] = make_uint4((uint32_t)op.seq, (uint32_t)rseq, 0u, 0u);
@@ -1762,12 +2016,14 @@ struct Engine {
                 if (rseq == kNoneSeq) chain_add_uniform(rfl((int32_t)s_blk[slot]), len);
             }
             // saveIfLocal (mergeTree.ts:2164-2179)
-            if (op.seq > min_seq) add_to_lru(blk, (uint32_t)slot, op.seq);
+            if (local) pend_add((uint32_t)slot, op);
+            else if (op.seq > min_seq) add_to_lru(blk, (uint32_t)slot, op.seq);
             // blockInsert maps a marker's id (mergeTree.ts:2200-2205); the host put the id's key
             // in payload_len (0: no id)
             if (marker && op.payload_len) idmap_add(op.payload_len, (uint32_t)slot);
         }
         resolve_splits();
+        if (local) return;  // no zamboni after a local op (mergeTree.ts:1994-1997)
         if (!loaded || !(op.flags & MT_OPF_GROUP_CONT)) zamboni();
     }
     MT_FI void op_insert(const mt_op &op) { insert_one<false>(op, op.client, (uint32_t)op.pos1, op.ref_seq); }
@@ -1954,6 +2210,7 @@ struct Engine {
         // (both boundaries were cut, so no leaf can straddle them)
         if (end > start) range_walk(op, start, end);
         resolve_splits();
+        if (kW && op.seq == kUnassignedSeq) return;  // a local op: no zamboni (mergeTree.ts:2600, 2713)
         zamboni();
     }
 
@@ -2021,6 +2278,7 @@ struct Engine {
         PF_SCOPE(4);
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = (op.flags & MT_OPF_REWRITE) != 0;
+        const bool local = kW && op.seq == kUnassignedSeq;  // a writer's own unacked op
         // per-op memo old prop-set -> new prop-set (annotate)
         uint32_t memo_n = 0;
         uint32_t memo_old = 0, memo_new = 0, memo_h = 0;  // lane i holds entry i
@@ -2042,10 +2300,12 @@ struct Engine {
             bool again = false;
             if (is_remove && hit) {
                 const uint32_t sr = s_sr[slot];
-                if (sr_removed(sr)) {
+                if (sr_removed(sr) && !(kW && (sr >> 16) == kSeq16Unassigned)) {
                     again = true;  // a concurrent remover: addOverlappingClient below
                 } else {
-                    s_sr[slot] = (sr & 0xFFFFu) | (rel16(op.seq) << 16);
+                    // first remover; or (writer) a sequenced remove replacing a pending local one
+                    // (mergeTree.ts:2624-2630: its client and seq, no overlap entry)
+                    s_sr[slot] = (sr & 0xFFFFu) | ((local ? kSeq16Unassigned : rel16(op.seq)) << 16);
                     s_meta[slot] = (s_meta[slot] & ~(kMetaCli << kMetaRcliShift)) | ((c & kMetaCli) << kMetaRcliShift);
                     cold[2 * slot + 1].y = (uint32_t)op.seq;
                 }
@@ -2097,7 +2357,22 @@ struct Engine {
                     old = rdl(oldp, f);
                     uint64_t mb = ballot((uint32_t)lane < memo_n && memo_old == old);
                     uint32_t nid, nh;
-                    if (mb) {
+                    bool pseg = false;
+                    if constexpr (kW) pseg = !local && (s_meta[sl] & kMetaPending);
+                    if (pseg) {
+                        // a remote annotate of a segment with pending local annotates
+                        // (segmentPropertiesManager.ts:48-92): nothing while a local rewrite is
+                        // pending, else the pending keys are left alone unless the op combines
+                        uint32_t pk, npk;
+                        bool prw;
+                        pending_keys(sl, pk, npk, prw);
+                        if (status) return;
+                        const uint32_t ck = MT_OPF_COMBINE(op.flags);
+                        nid = prw ? old
+                                  : props_extend(old, props_in + op.payload, op.payload_len, rewrite, nh, ck, pk,
+                                                 ck ? 0u : npk);
+                        if (status) return;
+                    } else if (mb) {
                         int m = first_lane(mb);
                         nid = rdl(memo_new, m);
                         nh = rdl(memo_h, m);
@@ -2115,9 +2390,10 @@ struct Engine {
                         }
                     }
                     if (lane == 0) cold[2 * sl].x = nid;
-                    s_meta[sl] = s_meta[sl] | kMetaHasProps;
+                    if (nid) s_meta[sl] = s_meta[sl] | kMetaHasProps;
                 }
-                add_to_lru(blk, sl, op.seq);
+                if (local) pend_add(sl, op);
+                else add_to_lru(blk, sl, op.seq);
                 if (status) return;
             }
             wsync();
@@ -2141,6 +2417,35 @@ struct Engine {
         resolve_splits();
     }
 
+    // a local op of a writer replica: Client.insertSegmentLocal / removeRangeLocal /
+    // annotateRangeLocal (client.ts:201-291) -> applyXOp with the local args (currentSeq, own
+    // client, UnassignedSequenceNumber; 553-563).  getValidOpRange's local check (504-543): an
+    // invalid range is logged (InvalidOpRange) and the op is not applied.
+    MT_FI void op_local(mt_op op) {
+        if (op.client != 0u) {
+            set_fail(ST_BAD_INPUT);
+            return;
+        }
+        if (op.type == MT_OP_RELPOS || rel_pend ||
+            (op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) != MT_COMBINE_NONE)) {
+            set_fail(ST_UNSUPPORTED);  // relative positions / combiningOps in local ops: not modelled
+            return;
+        }
+        if (op.type != MT_OP_INSERT && op.type != MT_OP_REMOVE && op.type != MT_OP_ANNOTATE) {
+            if (op.type != MT_OP_NOOP) set_fail(ST_BAD_INPUT);
+            return;
+        }
+        const int32_t len = (int32_t)view_length(cur_seq, 0u);  // getLength(): the local view
+        const int32_t st = op.pos1;
+        if (st < 0 || st > len || (st == len && op.type != MT_OP_INSERT)) return;
+        if (op.type != MT_OP_INSERT && op.pos2 <= st) return;
+        op.ref_seq = cur_seq;
+        cur_g = -1;
+        ov_splits = -1;
+        if (op.type == MT_OP_INSERT) insert_one<false>(op, 0u, (uint32_t)st, cur_seq);
+        else op_range(op);
+    }
+
     MT_FI void apply(mt_op op) {
         pend_n = 0;
         if (rel_pend) {  // the positions the MT_OP_RELPOS record before this one resolved
@@ -2149,7 +2454,14 @@ struct Engine {
             if (rp & 2) op.pos2 = rel_p2;
             rel_pend = 0;
         }
-        if (op.client >= (uint32_t)kMaxClients || (op.client == 0 && op.type != MT_OP_NOOP)) {
+        if constexpr (kW) {
+            if (op.seq == kUnassignedSeq) {  // a local op of this replica (mt_oplog.h)
+                op_local(op);
+                resolve_splits();
+                return;
+            }
+        }
+        if (op.client >= (uint32_t)kMaxClients || (!kW && op.client == 0 && op.type != MT_OP_NOOP)) {
             set_fail(ST_UNSUPPORTED);
             return;
         }
@@ -2159,6 +2471,21 @@ struct Engine {
         if (op.seq - sbase >= kSeq16Span) {
             cap_fail(5);
             return;
+        }
+        if constexpr (kW) {
+            if (op.client == 0 && op.type != MT_OP_NOOP) {
+                // the replica's own sequenced message acks its oldest pending group (client.ts:
+                // 810-812; a GROUP acks one group per member); positions are not read
+                if (op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) == MT_COMBINE_CONSENSUS) {
+                    set_fail(ST_UNSUPPORTED);  // updateConsensusProperty (client.ts:596-600)
+                    return;
+                }
+                if (op.type != MT_OP_RELPOS) op_ack(op);
+                resolve_splits();
+                if (status) return;
+                if (!(op.flags & MT_OPF_GROUP_CONT)) update_seq_numbers(op.msn, op.seq);
+                return;
+            }
         }
         switch (op.type) {
             case MT_OP_INSERT: op_insert(op); break;
@@ -2438,8 +2765,8 @@ __device__ __forceinline__ mt_op bcast_op(const mt_op &o, int l) {
     return r;
 }
 
-template <int SEG>
-MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_t d, uint8_t *smem) {
+template <int SEG, bool kW>
+MT_FI void engine_setup(Engine<SEG, kW> &E, const ReplayParams &P, int64_t w, int64_t d, uint8_t *smem) {
     E.lane = threadIdx.x;
     E.carve(smem);
     E.cold = P.cold + w * (int64_t)SEG * kColdPerSlot;
@@ -2461,6 +2788,12 @@ MT_FI void engine_setup(Engine<SEG> &E, const ReplayParams &P, int64_t w, int64_
     E.props_in = (const mt_prop *)P.props_in;
     E.vt = P.vt;
     E.idmap = P.idmap ? P.idmap + P.doc_idmap_base[d] : nullptr;
+    if constexpr (kW) {
+        E.pend = P.pend + P.doc_pend_base[d];
+        E.pend_cap_e = P.pend_cap;
+        E.n_pend = 0;
+        E.cur_g = -1;
+    }
     E.init();
 }
 
@@ -2558,10 +2891,10 @@ MT_FI int32_t fq_claim(const ReplayParams &P, int32_t *src) {
 // Workgroup index w writes its results at w; document d; src >= 0: resume from the checkpoint
 // ck_in[src] (kSrcList: src = ck_src[w]).  Returns true if the document stopped at a checkpoint.
 constexpr int32_t kSrcList = -2;
-template <int SEG, bool kLoad>
+template <int SEG, bool kLoad, bool kW = false>
 MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) {
     uint8_t *smem = tables<SEG>(P, w);
-    Engine<SEG> E;
+    Engine<SEG, kW> E;
 #ifdef MT_PROF
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
     const uint64_t t_kernel = clock64();
@@ -2575,6 +2908,18 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
         if (src >= 0)
             done = E.restore(P.ck_in + src * P.ck_in_words, P.cold_in + (int64_t)src * P.cold_in_seg * kColdPerSlot);
     }
+    // writer batches: the pending-group region persists across launches.  A fresh start (first run,
+    // a re-run from scratch, or the SnapshotLoader's run before the replay) clears it; a resumed
+    // writer document reads its group count back.
+    const bool resumed = P.ck_in && src >= 0;
+    if (P.pend && !resumed && E.lane == 0) {
+        uint32_t *pr = P.pend + P.doc_pend_base[d];
+        pr[0] = 0u;
+        pr[1] = 0u;
+        pr[2] = 0u;
+        pr[3] = 0u;
+    }
+    if constexpr (kW) E.n_pend = resumed ? (int32_t)E.pend_word(0) : 0;
     // follow-on producer: workgroups are dispatched in index order, so the last one starting
     // means all are resident and the host may launch the consumer
     // follow-on producer: every workgroup counts itself in once resident (host-mapped, system
@@ -2632,13 +2977,13 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
 
 // one workgroup per document (blockIdx.x); a producer (fq_role 1) hands its checkpointed
 // documents to the follow-on consumer
-template <int SEG, bool kLoad>
+template <int SEG, bool kLoad, bool kW = false>
 MT_FI void replay_body(const ReplayParams &P) {
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
     const bool producer = !kLoad && P.fq_role == 1;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
-    const bool ck = replay_one<SEG, kLoad>(P, w, d, kSrcList);
+    const bool ck = replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
     if (producer) fq_push(P, w, ck);
 }
 

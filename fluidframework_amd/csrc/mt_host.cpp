@@ -29,6 +29,7 @@
 // kernels of each capacity class (mt_kernels.hip compiled with -DMT_SEG=<seg>)
 #define MT_DECLARE_CLASS(S)                                                   \
     extern "C" __global__ void mt_replay_kernel_##S(mt::ReplayParams P);      \
+    extern "C" __global__ void mt_writer_kernel_##S(mt::ReplayParams P);      \
     extern "C" __global__ void mt_load_kernel_##S(mt::ReplayParams P);        \
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);    \
     extern "C" __global__ void mt_follow_kernel_##S(mt::ReplayParams P);
@@ -82,40 +83,57 @@ struct KernelClass {
     const void *generate;
     const void *load;
     const void *follow;
+    const void *writer;  // replay + the local-client path (writer replicas)
 };
 static const KernelClass kKernels[mt::kNumClasses] = {
     {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
-     (const void *)mt_follow_kernel_128},
+     (const void *)mt_follow_kernel_128,
+     (const void *)mt_writer_kernel_128},
     {363, (const void *)mt_replay_kernel_363, (const void *)mt_generate_kernel_363, (const void *)mt_load_kernel_363,
-     (const void *)mt_follow_kernel_363},
+     (const void *)mt_follow_kernel_363,
+     (const void *)mt_writer_kernel_363},
     {423, (const void *)mt_replay_kernel_423, (const void *)mt_generate_kernel_423, (const void *)mt_load_kernel_423,
-     (const void *)mt_follow_kernel_423},
+     (const void *)mt_follow_kernel_423,
+     (const void *)mt_writer_kernel_423},
     {483, (const void *)mt_replay_kernel_483, (const void *)mt_generate_kernel_483, (const void *)mt_load_kernel_483,
-     (const void *)mt_follow_kernel_483},
+     (const void *)mt_follow_kernel_483,
+     (const void *)mt_writer_kernel_483},
     {540, (const void *)mt_replay_kernel_540, (const void *)mt_generate_kernel_540, (const void *)mt_load_kernel_540,
-     (const void *)mt_follow_kernel_540},
+     (const void *)mt_follow_kernel_540,
+     (const void *)mt_writer_kernel_540},
     {600, (const void *)mt_replay_kernel_600, (const void *)mt_generate_kernel_600, (const void *)mt_load_kernel_600,
-     (const void *)mt_follow_kernel_600},
+     (const void *)mt_follow_kernel_600,
+     (const void *)mt_writer_kernel_600},
     {720, (const void *)mt_replay_kernel_720, (const void *)mt_generate_kernel_720, (const void *)mt_load_kernel_720,
-     (const void *)mt_follow_kernel_720},
+     (const void *)mt_follow_kernel_720,
+     (const void *)mt_writer_kernel_720},
     {840, (const void *)mt_replay_kernel_840, (const void *)mt_generate_kernel_840, (const void *)mt_load_kernel_840,
-     (const void *)mt_follow_kernel_840},
+     (const void *)mt_follow_kernel_840,
+     (const void *)mt_writer_kernel_840},
     {960, (const void *)mt_replay_kernel_960, (const void *)mt_generate_kernel_960, (const void *)mt_load_kernel_960,
-     (const void *)mt_follow_kernel_960},
+     (const void *)mt_follow_kernel_960,
+     (const void *)mt_writer_kernel_960},
     {1136, (const void *)mt_replay_kernel_1136, (const void *)mt_generate_kernel_1136, (const void *)mt_load_kernel_1136,
-     (const void *)mt_follow_kernel_1136},
+     (const void *)mt_follow_kernel_1136,
+     (const void *)mt_writer_kernel_1136},
     {1376, (const void *)mt_replay_kernel_1376, (const void *)mt_generate_kernel_1376, (const void *)mt_load_kernel_1376,
-     (const void *)mt_follow_kernel_1376},
+     (const void *)mt_follow_kernel_1376,
+     (const void *)mt_writer_kernel_1376},
     {1792, (const void *)mt_replay_kernel_1792, (const void *)mt_generate_kernel_1792, (const void *)mt_load_kernel_1792,
-     (const void *)mt_follow_kernel_1792},
+     (const void *)mt_follow_kernel_1792,
+     (const void *)mt_writer_kernel_1792},
     {2389, (const void *)mt_replay_kernel_2389, (const void *)mt_generate_kernel_2389, (const void *)mt_load_kernel_2389,
-     (const void *)mt_follow_kernel_2389},
+     (const void *)mt_follow_kernel_2389,
+     (const void *)mt_writer_kernel_2389},
     {3600, (const void *)mt_replay_kernel_3600, (const void *)mt_generate_kernel_3600, (const void *)mt_load_kernel_3600,
-     (const void *)mt_follow_kernel_3600},
+     (const void *)mt_follow_kernel_3600,
+     (const void *)mt_writer_kernel_3600},
     {7266, (const void *)mt_replay_kernel_7266, (const void *)mt_generate_kernel_7266, (const void *)mt_load_kernel_7266,
-     (const void *)mt_follow_kernel_7266},
+     (const void *)mt_follow_kernel_7266,
+     (const void *)mt_writer_kernel_7266},
     {2097152, (const void *)mt_replay_kernel_2097152, (const void *)mt_generate_kernel_2097152, (const void *)mt_load_kernel_2097152,
-     (const void *)mt_follow_kernel_2097152},
+     (const void *)mt_follow_kernel_2097152,
+     (const void *)mt_writer_kernel_2097152},
 };
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
 
@@ -353,6 +371,12 @@ struct mt_batch {
     std::unordered_map<int64_t, std::vector<std::string>> doc_clients;
     // log (device) + host mirror of the layout
     bool have_log = false, generated = false;
+    // writer replicas (the log has local ops / own acks): mt_writer_kernel_<SEG> and per-document
+    // pending-group regions (mt_device.h pend_words)
+    bool writer = false;
+    int32_t pend_cap = 0;
+    uint32_t *d_pend = nullptr;
+    uint64_t *d_pend_base = nullptr;
     int64_t total_ops = 0, total_props = 0;
     int32_t max_ops_per_doc = 0;
     std::vector<int64_t> h_off;
@@ -456,6 +480,11 @@ static void free_log(mt_batch *b) {
     (void)hipFree(b->d_idmap_base);
     b->d_idmap = nullptr;
     b->d_idmap_base = nullptr;
+    (void)hipFree(b->d_pend);
+    (void)hipFree(b->d_pend_base);
+    b->d_pend = nullptr;
+    b->d_pend_base = nullptr;
+    b->writer = false;
     b->d_ops = nullptr;
     b->d_off = nullptr;
     b->d_text = nullptr;
@@ -845,6 +874,15 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         pool_cap[d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
         pbase += align16u(pc);
     }
+    // a writer replica's log: local ops (seq == UnassignedSequenceNumber) or sequenced messages of
+    // the replica itself (short id 0) that ack them
+    bool writer = false;
+    for (int64_t d = 0; d < D && !writer; d++)
+        for (int64_t i = h_off[d] + nload[d]; i < h_off[d + 1]; i++)
+            if (ops[i].seq == mt::kUnassignedSeq || (ops[i].client == 0 && ops[i].type != MT_OP_NOOP)) {
+                writer = true;
+                break;
+            }
     // combiningOps: the value each one gives a key the segment does not have yet
     std::vector<mt_prop> h_props;
     rc_resolve_combine(b, ops, N, props, n_props, h_props);
@@ -907,6 +945,20 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     HIPCHK(dalloc(&b->d_idmap, (size_t)std::max<uint64_t>(idmap_base[(size_t)D], 1)));
     HIPCHK(dalloc(&b->d_idmap_base, (size_t)D + 1));
     HIPCHK(hipMemcpy(b->d_idmap_base, idmap_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+    if (writer) {
+        // pending-group regions: MT_PEND_CAP entries per document (default 4096: the live entries
+        // of at most kPendMaxGroups unacked ops, compacted when full)
+        const char *e = getenv("MT_PEND_CAP");
+        b->pend_cap = e && atoi(e) > 0 ? atoi(e) : 4096;
+        const uint64_t words = (uint64_t)mt::pend_words(b->pend_cap);
+        std::vector<uint64_t> pbase_((size_t)D + 1);
+        for (int64_t d = 0; d <= D; d++) pbase_[(size_t)d] = (uint64_t)d * words;
+        HIPCHK(dalloc(&b->d_pend, (size_t)(words * (uint64_t)D)));
+        if (D > 0) HIPCHK(hipMemset(b->d_pend, 0, 4 * words * (uint64_t)D));
+        HIPCHK(dalloc(&b->d_pend_base, (size_t)D + 1));
+        HIPCHK(hipMemcpy(b->d_pend_base, pbase_.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+        b->writer = true;
+    }
     HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_off, b->h_off.data(), sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_text, h_text.data(), 2 * h_text.size(), hipMemcpyHostToDevice));
@@ -993,6 +1045,9 @@ static mt::ReplayParams base_params(mt_batch *b) {
     P.vt = b->d_vt;
     P.idmap = b->d_idmap;
     P.doc_idmap_base = b->d_idmap_base;
+    P.pend = b->d_pend;
+    P.doc_pend_base = b->d_pend_base;
+    P.pend_cap = b->pend_cap;
     return P;
 }
 
@@ -1049,7 +1104,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
     P.prof = L.d_prof;
 #endif
-    const void *fn = L.load ? kKernels[L.cls].load : kKernels[L.cls].replay;
+    const void *fn = L.load ? kKernels[L.cls].load : b->writer ? kKernels[L.cls].writer : kKernels[L.cls].replay;
     if (getenv("MT_DEBUG_LAUNCHES"))
         fprintf(stderr, "mtreplay: launch class %d docs %lld resumed %d level %d lds %zu load %d\n", mt::kClassSegs[L.cls],
                 (long long)n, (int)L.cksrc.size(), L.level, L.lds, (int)L.load);
@@ -1069,7 +1124,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
 static int follow_workers(mt_batch *b, const Launch &L, int64_t n) {
     const char *e = getenv("MT_FOLLOW_WORKERS");
     const int env = e && *e ? atoi(e) : 0;
-    if (env == 0 || L.load || L.level != 0 || L.cls == mt::kHbmClass || b->opt.max_retries <= 0) return 0;
+    if (env == 0 || L.load || L.level != 0 || L.cls == mt::kHbmClass || b->opt.max_retries <= 0 || b->writer) return 0;
     int nxt = resume_class(L.cls);
     while (nxt > L.cls + 1 && !class_usable(nxt)) nxt--;
     if (!class_usable(L.cls + 1) || !class_usable(nxt) || nxt == mt::kHbmClass) return 0;
@@ -1894,7 +1949,9 @@ MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs) {
     for (const OutRec &r : b->c_recs) {
         if (rec_is_marker(r)) continue;
         bool removed = rec_removed(r);
-        if (removed && r.rseq <= min_seq) continue;
+        // unacked inserts and segments removed at or below the MSN (incl. a pending local remove,
+        // removedSeq -1) are elided (snapshotV1.ts:184-186)
+        if (r.seq == mt::kUnassignedSeq || (removed && r.rseq <= min_seq)) continue;
         if (r.seq <= min_seq && !removed) {
             if (!have_prev) {
                 set_prev(r);

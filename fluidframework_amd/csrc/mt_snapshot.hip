@@ -240,7 +240,9 @@ struct Doc {
 
     __device__ __forceinline__ static bool skipped(const Rec &r, int32_t min_seq) {
         if (out_is_end(r.blk)) return true;
-        return r.rseq != kNoneSeq && r.rseq <= min_seq;
+        // unacked inserts and segments removed at or below the MSN (a pending local remove has
+        // removedSeq -1) are elided (snapshotV1.ts:184-186)
+        return r.seq == kUnassignedSeq || (r.rseq != kNoneSeq && r.rseq <= min_seq);
     }
 
     __device__ __forceinline__ void str(const uint32_t *tab, uint32_t i) { W.copy(P.strs + tab[2 * i], tab[2 * i + 1]); }

@@ -6,6 +6,8 @@ Mirrors the reference's per-document surface so tests read like the reference's 
     ------------------------------------------------------      ---------------------------------
     new Client(...); client.startOrUpdateCollaboration(id)      ReplayBatch(n_docs, observer=id)
     client.applyMsg(msg) for msg in log                         batch.ingest_messages(logs); batch.run()
+    client.insertTextLocal / removeRangeLocal / annotateRange-  {"sequenceNumber": -1, ...} entries of a
+      Local, then applyMsg(own sequenced msg) (ack)               writer's log: ingest_messages(logs, observer=[ids])
     sharedString.getText()                                      batch.doc(i).get_text()
     client.getPropertiesAtPosition(pos)                         batch.doc(i).get_properties_at_position(pos)
     new SnapshotV1(mt, logger).extractSync(); emit()            batch.doc(i).snapshot_v1()
@@ -352,11 +354,14 @@ class ReplayBatch:
                 self.set_clients(names, i)
         self.ingest(pb.ops, pb.doc_op_off, pb.text, pb.props)
 
-    def ingest_messages(self, docs, observer: str = "readonly"):
-        """docs: one ISequencedDocumentMessage list (dicts or JSON strings) per document."""
-        p = Packer(observer=observer)
-        for msgs in docs:
-            p.add_document(msgs)
+    def ingest_messages(self, docs, observer="readonly"):
+        """docs: one ISequencedDocumentMessage list (dicts or JSON strings) per document.
+        observer: the replicas' long id, or one per document (writer replicas: their unsequenced
+        messages, sequenceNumber -1, are local ops; their sequenced ones ack them)."""
+        reps = [observer] * len(docs) if isinstance(observer, str) else list(observer)
+        p = Packer(observer=reps[0] if reps else "readonly")
+        for msgs, rep in zip(docs, reps):
+            p.add_document(msgs, rep)
         pb = p.finish()
         if len(pb.doc_op_off) != self.n_docs + 1:
             raise ValueError("expected one message list per document")

@@ -15,6 +15,13 @@ arena, interned property keys/values and per-document client tables.
 
 Short client ids are assigned per document in first-appearance order with the
 observer first, exactly as ``Client.getOrAddShortClientId`` does (client.ts:636-660).
+
+Writer replicas (the local-client path): a document's stream may also hold the replica's own
+*unsequenced* messages — ``{"clientId": <replica>, "sequenceNumber": -1, "contents": op, ...}``,
+what ``TestClient.makeOpMessage(op)`` builds for a local op (testClient.ts:213-234) — which the
+replica applies locally (insertSegmentLocal / removeRangeLocal / annotateRangeLocal) and keeps
+pending until its own *sequenced* message arrives and acks it (client.ts:797-819).  They pack as
+records with seq -1 and client 0; the acks as ordinary records of client 0.
 """
 from __future__ import annotations
 
@@ -32,6 +39,7 @@ PROP_DTYPE = np.dtype([("key", "<u4"), ("value", "<u4")])
 assert OP_DTYPE.itemsize == 32
 
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_RELPOS, OP_NOOP = 0, 1, 2, 6, 15
+UNASSIGNED_SEQ = -1  # UnassignedSequenceNumber (merge-tree/src/constants.ts:11): a local, unacked op
 # MT_OP_RELPOS flags (include/mt_oplog.h mt_relpos_flags)
 RELF_POS1, RELF_POS2, RELF_BEFORE1, RELF_BEFORE2, RELF_OFF1, RELF_OFF2 = 0x10, 0x20, 0x40, 0x80, 0x100, 0x200
 OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
@@ -46,8 +54,8 @@ MAX_CLIENTS = 254  # short ids 0..253 (include/mt_oplog.h MT_MAX_CLIENTS; 254 / 
 
 
 class UnsupportedOp(ValueError):
-    """An op shape outside the observer replay path (relative positions, registers, the
-    observer's own ops)."""
+    """An op shape outside the device's replay path (registers, relative positions or
+    combiningOps in local ops, ...)."""
 
 
 def js_truthy(v) -> bool:
@@ -196,10 +204,13 @@ class Packer:
             self._props.append((self._key(k), self._value(props[k])))
         return off, len(self._props) - off
 
-    def add_document(self, messages) -> int:
-        """Append one document's message stream; returns its index."""
-        names = [self.observer]
-        short = {self.observer: 0}
+    def add_document(self, messages, replica: str | None = None) -> int:
+        """Append one document's message stream; returns its index.  ``replica`` (default: the
+        packer's ``observer``) is the document's own long id: its unsequenced messages
+        (sequenceNumber -1) are local ops, its sequenced ones ack them (a writer replica)."""
+        me = self.observer if replica is None else replica
+        names = [me]
+        short = {me: 0}
         recs = []
         for msg in messages:
             if isinstance(msg, str):
@@ -213,18 +224,35 @@ class Packer:
                 short[cid] = len(names)
                 names.append(cid)
             c = short[cid]
-            base = dict(client=c, seq=msg["sequenceNumber"], ref_seq=msg["referenceSequenceNumber"],
-                        msn=msg["minimumSequenceNumber"])
+            seq = msg["sequenceNumber"]
+            # a local op of this replica: an unsequenced message (TestClient.makeOpMessage's default
+            # seq, UnassignedSequenceNumber = -1), applied with the replica's local view and kept
+            # pending until the replica's own sequenced message (client 0) acks it
+            local = seq == UNASSIGNED_SEQ
+            if local and c != 0:
+                raise UnsupportedOp("an unsequenced message of another client")
+            base = dict(client=c, seq=seq, ref_seq=msg.get("referenceSequenceNumber", 0),
+                        msn=0 if local else msg["minimumSequenceNumber"])
             if msg.get("type") != "op":
+                if local:
+                    raise UnsupportedOp("a local message that is not an op")
                 recs.append(dict(base, type=OP_NOOP, flags=0, pos1=0, pos2=0, payload=0, payload_len=0))
                 continue
-            if c == 0:
-                raise UnsupportedOp("ack of the observer's own op (local path)")
+            ack = c == 0 and not local  # Client.applyMsg -> ackPendingSegment (client.ts:810-812)
             members = self._flatten(msg["contents"])
             for j, op in enumerate(members):
+                if local and (js_truthy(op.get("combiningOp")) and
+                              not (isinstance(op.get("combiningOp"), dict) and op["combiningOp"].get("name") == "rewrite")):
+                    raise UnsupportedOp("local combiningOp other than rewrite")
+                if ack and op.get("type") == 2 and isinstance(op.get("combiningOp"), dict) and \
+                        op["combiningOp"].get("name") == "consensus":
+                    raise UnsupportedOp("ack of a consensus annotate (updateConsensusProperty)")
                 rel = self._relpos(op, base)
                 if rel is not None:
-                    recs.append(rel)
+                    if local:
+                        raise UnsupportedOp("relative positions in a local op")
+                    if not ack:  # an ack reads no positions
+                        recs.append(rel)
                 r = self._pack_op(op, base)
                 if j + 1 < len(members):
                     r["flags"] |= OPF_GROUP_CONT

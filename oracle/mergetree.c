@@ -63,6 +63,8 @@ struct Block { /* MergeBlock / HierMergeBlock, mergeTree.ts:336-420 */
     struct mto_doc *doc; /* for blockUpdate's marker-id bookkeeping (addNodeReferences) */
 };
 
+typedef struct Group Group;
+
 typedef struct Seg { /* BaseSegment, mergeTree.ts:429-573 */
     Node n;
     int kind;
@@ -80,7 +82,23 @@ typedef struct Seg { /* BaseSegment, mergeTree.ts:429-573 */
     struct Seg *all_next;
     const jv *id_jv; /* marker id value last mapped (id_idx: its idToSegment entry) */
     int id_idx;
+    /* local-client state (mergeTree.ts:441-448): localSeq / localRemovedSeq (0 = undefined), the
+       segment's SegmentGroupCollection (a FIFO of the pending groups holding it,
+       segmentGroupCollection.ts:9-40) and SegmentPropertiesManager's pending counts
+       (segmentPropertiesManager.ts:12-14; pend_keys is created with props, NULL = undefined) */
+    int local_seq, local_removed_seq;
+    Group **sg;
+    int sg_head, sg_n, sg_cap;
+    jv *pend_keys;
+    int pend_rewrite;
 } Seg;
+
+struct Group { /* SegmentGroup (mergeTree.ts:198-201): { segments, localSeq } */
+    Seg **segs;
+    int n, cap;
+    int local_seq;
+    Group *all_next;
+};
 
 typedef struct { /* LRUSegment, mergeTree.ts:918-926 */
     Seg *seg;
@@ -127,6 +145,12 @@ struct mto_doc {
     int id_hcap;
     /* packed MT_OP_RELPOS: resolved positions for the next record (bit 0 pos1, bit 1 pos2) */
     int rel_pending, rel_pos1, rel_pos2;
+    /* local-client path: collabWindow.localSeq (mergeTree.ts:831) and MergeTree.pendingSegments,
+       the FIFO of SegmentGroups awaiting their ack (mergeTree.ts:1093, 1261) */
+    int local_seq;
+    Group **pend;
+    int pend_head, pend_n, pend_cap;
+    Group *all_groups;
 };
 
 /* ------------------------------------------------------------------ errors */
@@ -460,14 +484,33 @@ static jv *js_combine(mto_doc *d, const CombineOp *co, jv *cur, int seq) {
     }
 }
 
-/* SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111) for
-   seq !== UnassignedSequenceNumber and no pending local state.  `rewrite`: combiningOp
-   {name:"rewrite"}; `co`: any other combiningOp (NULL: none). */
+static int jv_truthy_value(const jv *v) {
+    return v && !(v->kind == JV_NULL || v->kind == JV_FALSE || v->kind == JV_UNDEF ||
+                  (v->kind == JV_NUM && (v->num == 0 || v->num != v->num)) || (v->kind == JV_STR && v->slen == 0));
+}
+/* pendingKeyUpdateCount[key] (undefined: 0) */
+static int pend_count(const Seg *s, const u16 *k, int kl) {
+    const jv *c = s->pend_keys ? jv_obj_get(s->pend_keys, k, kl) : NULL;
+    return c ? (int)c->num : 0;
+}
+/* SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111).  `rewrite`:
+   combiningOp {name:"rewrite"}; `co`: any other combiningOp (NULL: none); `collab`:
+   collabWindow.collaborating (false for the props a segment is made with).  A local op
+   (seq === UnassignedSequenceNumber) counts its keys as pending; a remote op leaves pending keys
+   alone unless it combines, and changes nothing while a local rewrite is pending. */
 static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewrite, const CombineOp *co,
-                               int seq) {
-    if (!s->props) s->props = jv_new(JV_OBJ);
+                               int seq, int collab) {
+    if (!s->props) {
+        s->props = jv_new(JV_OBJ);
+        s->pend_keys = jv_new(JV_OBJ);
+        s->pend_rewrite = 0;
+    }
+    if (s->pend_rewrite > 0 && seq != UNASSIGNED_SEQ && collab) return;
     if (!new_props || new_props->kind != JV_OBJ) fail(d, MTO_BAD_INPUT, "props is not an object");
+    const int has_co = co && co->kind;
+#define SHOULD_MODIFY(k, kl) (seq == UNASSIGNED_SEQ || !jv_obj_get(s->pend_keys, (k), (kl)) || has_co)
     if (rewrite) {
+        if (collab && seq == UNASSIGNED_SEQ) s->pend_rewrite++;
         int *ord = (int *)malloc(sizeof(int) * (size_t)(s->props->n + 1));
         int n = jv_obj_enum(s->props, ord);
         /* collect keys first: deleting while enumerating */
@@ -475,14 +518,12 @@ static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewr
         int *kl = (int *)malloc(sizeof(int) * (size_t)(n + 1));
         int m = 0;
         for (int i = 0; i < n; i++) {
-            const jv *nv = jv_obj_get(new_props, s->props->keys[ord[i]], s->props->klens[ord[i]]);
-            int truthy = nv && !(nv->kind == JV_NULL || nv->kind == JV_FALSE || nv->kind == JV_UNDEF ||
-                                 (nv->kind == JV_NUM && (nv->num == 0 || nv->num != nv->num)) ||
-                                 (nv->kind == JV_STR && nv->slen == 0));
-            if (!truthy) {
-                ks[m] = (u16 *)malloc(sizeof(u16) * (size_t)(s->props->klens[ord[i]] + 1));
-                memcpy(ks[m], s->props->keys[ord[i]], sizeof(u16) * (size_t)s->props->klens[ord[i]]);
-                kl[m++] = s->props->klens[ord[i]];
+            const u16 *k = s->props->keys[ord[i]];
+            const int klen = s->props->klens[ord[i]];
+            if (!jv_truthy_value(jv_obj_get(new_props, k, klen)) && SHOULD_MODIFY(k, klen)) {
+                ks[m] = (u16 *)malloc(sizeof(u16) * (size_t)(klen + 1));
+                memcpy(ks[m], k, sizeof(u16) * (size_t)klen);
+                kl[m++] = klen;
             }
         }
         for (int i = 0; i < m; i++) {
@@ -499,7 +540,14 @@ static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewr
         const u16 *k = new_props->keys[ord[i]];
         int kl = new_props->klens[ord[i]];
         jv *v = new_props->vals[ord[i]];
-        if (co && co->kind) { /* newValue = combine(op, previousValue, newValue, seq) */
+        if (collab) {
+            if (seq == UNASSIGNED_SEQ) {
+                jv_obj_set(s->pend_keys, k, kl, jv_new_num(pend_count(s, k, kl) + 1));
+            } else if (!SHOULD_MODIFY(k, kl)) {
+                continue;
+            }
+        }
+        if (has_co) { /* newValue = combine(op, previousValue, newValue, seq) */
             jv *nv = js_combine(d, co, jv_obj_get(s->props, k, kl), seq);
             if (nv && nv->kind == JV_NULL) {
                 jv_unref(nv);
@@ -510,6 +558,30 @@ static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewr
         } else if (v->kind == JV_NULL) jv_obj_del(s->props, k, kl);
         else jv_obj_set(s->props, k, kl, jv_ref(v));
     }
+#undef SHOULD_MODIFY
+    free(ord);
+}
+
+/* SegmentPropertiesManager.ackPendingProperties (segmentPropertiesManager.ts:19-33) */
+static void seg_ack_pending_properties(mto_doc *d, Seg *s, const jv *op_props, int rewrite) {
+    if (!s->props) fail(d, MTO_BAD_INPUT, "ack: segment without a property manager");
+    if (rewrite) s->pend_rewrite--;
+    if (!op_props || op_props->kind != JV_OBJ) return;
+    int *ord = (int *)malloc(sizeof(int) * (size_t)(op_props->n + 1));
+    int n = jv_obj_enum(op_props, ord);
+    for (int i = 0; i < n; i++) {
+        const u16 *k = op_props->keys[ord[i]];
+        const int kl = op_props->klens[ord[i]];
+        if (jv_obj_get(s->pend_keys, k, kl)) {
+            const int c = pend_count(s, k, kl);
+            if (!(c > 0)) {
+                free(ord);
+                fail(d, MTO_BAD_INPUT, "ack: pendingKeyUpdateCount");
+            }
+            if (c - 1 == 0) jv_obj_del(s->pend_keys, k, kl);
+            else jv_obj_set(s->pend_keys, k, kl, jv_new_num(c - 1));
+        }
+    }
     free(ord);
 }
 
@@ -519,7 +591,55 @@ static void seg_init_props(mto_doc *d, Seg *s, const jv *props) {
     if (props->kind == JV_FALSE || (props->kind == JV_NUM && props->num == 0) ||
         (props->kind == JV_STR && props->slen == 0))
         return;
-    seg_add_properties(d, s, props, 0, NULL, 0);
+    seg_add_properties(d, s, props, 0, NULL, 0, 0);
+}
+
+/* ------------------------------------------------------------------ pending segment groups */
+/* SegmentGroupCollection.enqueue (segmentGroupCollection.ts:24-27): the segment's queue gets the
+   group, the group's segments array gets the segment (at its end) */
+static void seg_group_enqueue(Seg *s, Group *g) {
+    if (s->sg_head + s->sg_n == s->sg_cap) {
+        if (s->sg_head > 0) {
+            memmove(s->sg, s->sg + s->sg_head, sizeof(Group *) * (size_t)s->sg_n);
+            s->sg_head = 0;
+        } else {
+            s->sg_cap = s->sg_cap ? s->sg_cap * 2 : 4;
+            s->sg = (Group **)realloc(s->sg, sizeof(Group *) * (size_t)s->sg_cap);
+        }
+    }
+    s->sg[s->sg_head + s->sg_n++] = g;
+    if (g->n == g->cap) {
+        g->cap = g->cap ? g->cap * 2 : 4;
+        g->segs = (Seg **)realloc(g->segs, sizeof(Seg *) * (size_t)g->cap);
+    }
+    g->segs[g->n++] = s;
+}
+static Group *seg_group_dequeue(Seg *s) { /* segmentGroupCollection.ts:29-31 */
+    if (s->sg_n == 0) return NULL;
+    s->sg_n--;
+    return s->sg[s->sg_head++];
+}
+/* MergeTree.addToPendingList (mergeTree.ts:1922-1929): the op's group is created (and queued on
+   pendingSegments) with its first segment */
+static Group *add_to_pending_list(mto_doc *d, Seg *s, Group *g, int local_seq) {
+    if (!g) {
+        g = (Group *)calloc(1, sizeof(Group));
+        g->local_seq = local_seq;
+        g->all_next = d->all_groups;
+        d->all_groups = g;
+        if (d->pend_head + d->pend_n == d->pend_cap) {
+            if (d->pend_head > 0) {
+                memmove(d->pend, d->pend + d->pend_head, sizeof(Group *) * (size_t)d->pend_n);
+                d->pend_head = 0;
+            } else {
+                d->pend_cap = d->pend_cap ? d->pend_cap * 2 : 16;
+                d->pend = (Group **)realloc(d->pend, sizeof(Group *) * (size_t)d->pend_cap);
+            }
+        }
+        d->pend[d->pend_head + d->pend_n++] = g;
+    }
+    seg_group_enqueue(s, g);
+    return g;
 }
 
 /* ------------------------------------------------------------------ split / append */
@@ -531,18 +651,25 @@ static Seg *seg_split_at(mto_doc *d, Seg *s, int pos) {
     int len = s->n.cached_length;
     Seg *leaf = new_text_seg(d, s->text + pos, len - pos);
     s->n.cached_length = pos;
-    if (s->props) leaf->props = jv_obj_clone(s->props); /* propertyManager.copyTo */
+    if (s->props) { /* SegmentPropertiesManager.copyTo (segmentPropertiesManager.ts:113-125) */
+        leaf->props = jv_obj_clone(s->props);
+        leaf->pend_keys = jv_obj_clone(s->pend_keys);
+        leaf->pend_rewrite = s->pend_rewrite;
+    }
     leaf->n.parent = s->n.parent;
     leaf->removed_client = s->removed_client;
     leaf->removed_seq = s->removed_seq;
     leaf->removed = s->removed;
+    leaf->local_removed_seq = s->local_removed_seq;
     leaf->seq = s->seq;
+    leaf->local_seq = s->local_seq;
     leaf->client_id = s->client_id;
     if (s->novl) {
         leaf->ovl = (int *)malloc(sizeof(int) * (size_t)s->novl);
         memcpy(leaf->ovl, s->ovl, sizeof(int) * (size_t)s->novl);
         leaf->novl = leaf->covl = s->novl;
     }
+    for (int i = 0; i < s->sg_n; i++) seg_group_enqueue(leaf, s->sg[s->sg_head + i]); /* segmentGroups.copyTo */
     return leaf;
 }
 
@@ -757,14 +884,18 @@ static void nv_push(NodeVec *v, Node *x) {
     v->p[v->n++] = x;
 }
 
-/* scourNode, mergeTree.ts:1289-1365 (segmentGroups / trackingCollection are empty on this path) */
+/* scourNode, mergeTree.ts:1289-1365 (trackingCollection is empty on this path): a segment in a
+   pending group is held as is */
 static void scour_node(mto_doc *d, Block *node, NodeVec *hold) {
     Seg *prev = NULL;
     for (int k = 0; k < node->child_count; k++) {
         Node *child = node->children[k];
         if (child->is_leaf) {
             Seg *s = (Seg *)child;
-            if (s->removed) {
+            if (s->sg_n > 0) {
+                nv_push(hold, child);
+                prev = NULL;
+            } else if (s->removed) {
                 if (s->removed_seq > d->cw.min_seq) {
                     nv_push(hold, child);
                 } else {
@@ -881,11 +1012,14 @@ static void set_min_seq(mto_doc *d, int min_seq) {
    then one zamboni */
 static void insert_segments(mto_doc *d, int pos, Seg **segs, int n, int ref_seq, int client_id, int seq) {
     ensure_interval_boundary(d, pos, ref_seq, client_id);
+    const int local_seq = seq == UNASSIGNED_SEQ ? ++d->local_seq : 0; /* mergeTree.ts:1976 */
+    Group *group = NULL;
     int insert_pos = pos;
     for (int i = 0; i < n; i++) {
         Seg *seg = segs[i];
         if (!seg || seg->n.cached_length <= 0) continue;
         seg->seq = seq;
+        seg->local_seq = local_seq;
         seg->client_id = client_id;
         map_marker_id(d, seg); /* blockInsert: Marker.is(newSegment) && getId() (mergeTree.ts:2200-2205) */
         ICtx ctx = {LEAF_INSERT, seg, 1};
@@ -898,7 +1032,7 @@ static void insert_segments(mto_doc *d, int pos, Seg **segs, int n, int ref_seq,
         /* saveIfLocal (2164-2179) */
         if (d->cw.collaborating) {
             if (seg->seq == UNASSIGNED_SEQ && client_id == d->cw.client_id) {
-                fail(d, MTO_UNSUPPORTED, "pending local segment");
+                group = add_to_pending_list(d, seg, group, local_seq);
             } else if (seg->seq > d->cw.min_seq) {
                 add_to_lru_set(d, seg, seg->seq);
             }
@@ -1035,6 +1169,8 @@ typedef struct {
     int seq;
     int client_id;
     int overwrite;
+    int local_seq;
+    Group *group;
 } RemoveCtx;
 
 /* markRangeRemoved.markRemoved (mergeTree.ts:2614-2660), single branch */
@@ -1043,8 +1179,11 @@ static int mark_removed(mto_doc *d, Seg *s, int pos, int r, int c, int st, int e
     RemoveCtx *ctx = (RemoveCtx *)vctx;
     if (s->removed) {
         ctx->overwrite = 1;
-        if (s->removed_seq == UNASSIGNED_SEQ) {
-            fail(d, MTO_UNSUPPORTED, "pending local remove");
+        if (s->removed_seq == UNASSIGNED_SEQ) { /* a pending local remove: the sequenced one replaces it */
+            s->removed_client = ctx->client_id;
+            s->removed_seq = ctx->seq;
+            s->local_removed_seq = 0;
+            bump_bounds(s);
         } else {
             if (s->novl == s->covl) {
                 s->covl = s->covl ? s->covl * 2 : 4;
@@ -1055,12 +1194,13 @@ static int mark_removed(mto_doc *d, Seg *s, int pos, int r, int c, int st, int e
     } else {
         s->removed_client = ctx->client_id;
         s->removed_seq = ctx->seq;
+        s->local_removed_seq = ctx->local_seq;
         s->removed = 1;
         bump_bounds(s);
     }
     if (d->cw.collaborating) {
         if (s->removed_seq == UNASSIGNED_SEQ && ctx->client_id == d->cw.client_id) {
-            fail(d, MTO_UNSUPPORTED, "pending local remove");
+            ctx->group = add_to_pending_list(d, s, ctx->group, ctx->local_seq);
         } else {
             add_to_lru_set(d, s, ctx->seq);
         }
@@ -1076,7 +1216,7 @@ static int after_mark_removed(mto_doc *d, Block *b, void *ctx) {
 static void mark_range_removed(mto_doc *d, int start, int end, int ref_seq, int client_id, int seq) {
     ensure_interval_boundary(d, start, ref_seq, client_id);
     ensure_interval_boundary(d, end, ref_seq, client_id);
-    RemoveCtx ctx = {seq, client_id, 0};
+    RemoveCtx ctx = {seq, client_id, 0, seq == UNASSIGNED_SEQ ? ++d->local_seq : 0, NULL}; /* mergeTree.ts:2613 */
     MapActions a = {mark_removed, after_mark_removed, &ctx};
     node_map(d, d->root, &a, 0, ref_seq, client_id, start, end, 1);
     if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
@@ -1087,14 +1227,16 @@ typedef struct {
     int rewrite;
     int seq;
     const CombineOp *co;
+    int local_seq;
+    Group *group;
 } AnnotateCtx;
 
 static int annotate_segment(mto_doc *d, Seg *s, int pos, int r, int c, int st, int en, void *vctx) {
     (void)pos; (void)r; (void)c; (void)st; (void)en;
     AnnotateCtx *ctx = (AnnotateCtx *)vctx;
-    seg_add_properties(d, s, ctx->props, ctx->rewrite, ctx->co, ctx->seq);
+    seg_add_properties(d, s, ctx->props, ctx->rewrite, ctx->co, ctx->seq, d->cw.collaborating);
     if (d->cw.collaborating) {
-        if (ctx->seq == UNASSIGNED_SEQ) fail(d, MTO_UNSUPPORTED, "pending local annotate");
+        if (ctx->seq == UNASSIGNED_SEQ) ctx->group = add_to_pending_list(d, s, ctx->group, ctx->local_seq);
         else add_to_lru_set(d, s, ctx->seq);
     }
     return 1;
@@ -1105,7 +1247,7 @@ static void annotate_range(mto_doc *d, int start, int end, const jv *props, int 
                            int ref_seq, int client_id, int seq) {
     ensure_interval_boundary(d, start, ref_seq, client_id);
     ensure_interval_boundary(d, end, ref_seq, client_id);
-    AnnotateCtx ctx = {props, rewrite, seq, co};
+    AnnotateCtx ctx = {props, rewrite, seq, co, seq == UNASSIGNED_SEQ ? ++d->local_seq : 0, NULL}; /* 2571 */
     MapActions a = {annotate_segment, NULL, &ctx};
     node_map(d, d->root, &a, 0, ref_seq, client_id, start, end, 1);
     if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
@@ -1162,6 +1304,8 @@ void mto_free(mto_doc *d) {
         Seg *n = s->all_next;
         free(s->text);
         free(s->ovl);
+        free(s->sg);
+        jv_unref(s->pend_keys);
         jv_unref(s->props);
         jv_unref((jv *)s->id_jv);
         free(s);
@@ -1172,6 +1316,13 @@ void mto_free(mto_doc *d) {
         free(b);
         b = n;
     }
+    for (Group *g = d->all_groups; g;) {
+        Group *n = g->all_next;
+        free(g->segs);
+        free(g);
+        g = n;
+    }
+    free(d->pend);
     for (int i = 0; i < d->n_ids; i++) free(d->long_ids[i]);
     free(d->long_ids);
     for (int i = 0; i < d->n_ids_map; i++) free(d->id_keys[i]);
@@ -1264,6 +1415,55 @@ static Seg *spec_to_segment(mto_doc *d, const jv *spec) {
     return NULL;
 }
 
+/* MergeTree.ackPendingSegment (mergeTree.ts:1893-1920) with BaseSegment.ack (487-522): one op of
+   the replica's own sequenced message (Client.ackPendingSegment, client.ts:588-625) assigns `seq`
+   to the segments of the oldest pending group, in the group's order */
+static void ack_pending_segment(mto_doc *d, int type, const jv *op_props, int rewrite, int seq) {
+    Group *g = NULL;
+    if (d->pend_n > 0) {
+        g = d->pend[d->pend_head++];
+        d->pend_n--;
+    }
+    if (g) {
+        Block *nodes[64];
+        int nn = 0;
+        Block **more = NULL;
+        for (int i = 0; i < g->n; i++) {
+            Seg *s = g->segs[i];
+            if (seg_group_dequeue(s) != g) fail(d, MTO_BAD_INPUT, "ack: segment group not at the head");
+            switch (type) {
+                case MT_OP_ANNOTATE: seg_ack_pending_properties(d, s, op_props, rewrite); break;
+                case MT_OP_INSERT:
+                    if (s->seq != UNASSIGNED_SEQ) fail(d, MTO_BAD_INPUT, "ack: insert of a sequenced segment");
+                    s->seq = seq;
+                    s->local_seq = 0;
+                    break;
+                case MT_OP_REMOVE:
+                    if (!s->removed) fail(d, MTO_BAD_INPUT, "ack: remove of a segment not removed");
+                    s->local_removed_seq = 0;
+                    if (s->removed_seq == UNASSIGNED_SEQ) s->removed_seq = seq;
+                    break;
+                default: fail(d, MTO_BAD_INPUT, "ack: op type %d", type);
+            }
+            add_to_lru_set(d, s, seq);
+            Block *p = s->n.parent; /* nodesToUpdate, first appearance order */
+            int seen = 0;
+            for (int j = 0; j < nn && !seen; j++) seen = (j < 64 ? nodes[j] : more[j - 64]) == p;
+            if (!seen) {
+                if (nn < 64) nodes[nn] = p;
+                else {
+                    more = (Block **)realloc(more, sizeof(Block *) * (size_t)(nn - 63));
+                    more[nn - 64] = p;
+                }
+                nn++;
+            }
+        }
+        for (int j = 0; j < nn; j++) block_update_path_lengths(j < 64 ? nodes[j] : more[j - 64]);
+        free(more);
+    }
+    zamboni_segments(d);
+}
+
 /* Client.applyRemoteOp (client.ts:768-795) */
 static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int ref_seq, int msn) {
     int type = -1;
@@ -1333,6 +1533,94 @@ static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int
     }
 }
 
+static int annotate_rewrite_of(mto_doc *d, const jv *op, int local) {
+    const jv *cop = jv_obj_get_ascii(op, "combiningOp");
+    if (!jv_truthy(cop)) return 0;
+    const jv *nm = cop->kind == JV_OBJ ? jv_obj_get_ascii(cop, "name") : NULL;
+    static const u16 RW[7] = {'r', 'e', 'w', 'r', 'i', 't', 'e'};
+    if (nm && nm->kind == JV_STR && u16_eq(nm->s, nm->slen, RW, 7)) return 1;
+    if (local) fail(d, MTO_UNSUPPORTED, "local combiningOp other than rewrite");
+    return 0;
+}
+/* Client.ackPendingSegment (client.ts:588-625): a GROUP acks each member */
+static void ack_op_json(mto_doc *d, const jv *op, int seq) {
+    int type = -1;
+    if (!op || op->kind != JV_OBJ || !jv_int(jv_obj_get_ascii(op, "type"), &type)) fail(d, MTO_BAD_INPUT, "bad op");
+    if (type == 3) {
+        const jv *ops = jv_obj_get_ascii(op, "ops");
+        if (!ops || ops->kind != JV_ARR) fail(d, MTO_BAD_INPUT, "group without ops");
+        for (int i = 0; i < ops->n; i++) ack_op_json(d, ops->vals[i], seq);
+        return;
+    }
+    if (type == 2 && jv_truthy(jv_obj_get_ascii(op, "combiningOp")) && !annotate_rewrite_of(d, op, 0)) {
+        const jv *cop = jv_obj_get_ascii(op, "combiningOp");
+        const jv *nm = cop->kind == JV_OBJ ? jv_obj_get_ascii(cop, "name") : NULL;
+        static const u16 CONS[9] = {'c', 'o', 'n', 's', 'e', 'n', 's', 'u', 's'};
+        if (nm && nm->kind == JV_STR && u16_eq(nm->s, nm->slen, CONS, 9))
+            fail(d, MTO_UNSUPPORTED, "ack of a consensus annotate (updateConsensusProperty)");
+    }
+    ack_pending_segment(d, type, type == 2 ? jv_obj_get_ascii(op, "props") : NULL,
+                        type == 2 ? annotate_rewrite_of(d, op, 0) : 0, seq);
+}
+
+/* a local op of a collaborating replica: Client.insertSegmentLocal / removeRangeLocal /
+   annotateRangeLocal (client.ts:201-291) -> applyXOp with getClientSequenceArgs' local args
+   (currentSeq, clientId, UnassignedSequenceNumber; 553-563).  getValidOpRange's local check
+   (504-543): an invalid range is logged (InvalidOpRange) and the op is not applied; returns 0 then. */
+static int local_range_valid(mto_doc *d, int type, int start, int has_end, int end) {
+    const int len = d->root->n.cached_length; /* getLength() */
+    if (start < 0 || start > len || (start == len && type != 0)) return 0;
+    if (type != 0 || has_end) {
+        if (!has_end || end <= start) return 0;
+    }
+    return 1;
+}
+static void apply_local_op_json(mto_doc *d, const jv *op) {
+    int type = -1;
+    if (!op || op->kind != JV_OBJ || !jv_int(jv_obj_get_ascii(op, "type"), &type)) fail(d, MTO_BAD_INPUT, "bad op");
+    const int ref = d->cw.current_seq, cid = d->cw.client_id;
+    const int seq = d->cw.collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ; /* getLocalSequenceNumber (client.ts:949-955) */
+    if (type == 3) {
+        const jv *ops = jv_obj_get_ascii(op, "ops");
+        if (!ops || ops->kind != JV_ARR) fail(d, MTO_BAD_INPUT, "group without ops");
+        for (int i = 0; i < ops->n; i++) apply_local_op_json(d, ops->vals[i]);
+        return;
+    }
+    int pos1 = 0, pos2 = 0;
+    const int has1 = jv_int(jv_obj_get_ascii(op, "pos1"), &pos1);
+    const int has2 = jv_int(jv_obj_get_ascii(op, "pos2"), &pos2);
+    if (!has1) fail(d, MTO_UNSUPPORTED, "local op without pos1");
+    if (!local_range_valid(d, type, pos1, has2, pos2)) return;
+    switch (type) {
+        case 0: {
+            const jv *segspec = jv_obj_get_ascii(op, "seg");
+            if (!segspec) fail(d, MTO_UNSUPPORTED, "register insert");
+            Seg *s = spec_to_segment(d, segspec);
+            insert_segment(d, pos1, s, ref, cid, seq);
+            break;
+        }
+        case 1: mark_range_removed(d, pos1, pos2, ref, cid, seq); break;
+        case 2: {
+            const int rewrite = annotate_rewrite_of(d, op, 1);
+            annotate_range(d, pos1, pos2, jv_obj_get_ascii(op, "props"), rewrite, NULL, ref, cid, seq);
+            break;
+        }
+        default: break;
+    }
+}
+
+int mto_local_op_json(mto_doc *d, const char *op_json) {
+    GUARD(d);
+    jv *op = jv_parse(op_json, strlen(op_json));
+    if (!op) fail(d, MTO_BAD_INPUT, "op is not JSON");
+    apply_local_op_json(d, op);
+    jv_unref(op);
+    UNGUARD(d);
+    return d->status;
+}
+
+int mto_pending_groups(const mto_doc *d) { return d->pend_n; }
+
 int mto_apply_msg_json(mto_doc *d, const char *msg_json) {
     GUARD(d);
     jv *msg = jv_parse(msg_json, strlen(msg_json));
@@ -1354,10 +1642,10 @@ int mto_apply_msg_json(mto_doc *d, const char *msg_json) {
     static const u16 OP[2] = {'o', 'p'};
     if (type && type->kind == JV_STR && u16_eq(type->s, type->slen, OP, 2)) {
         if (d->long_client_id && !strcmp(name.p ? name.p : "", d->long_client_id)) {
-            sb_free(&name);
-            fail(d, MTO_UNSUPPORTED, "ack of a local op (observer path only)");
+            ack_op_json(d, jv_obj_get_ascii(msg, "contents"), seq); /* client.ts:810-812 */
+        } else {
+            apply_remote_op(d, jv_obj_get_ascii(msg, "contents"), short_id, seq, ref, msn);
         }
-        apply_remote_op(d, jv_obj_get_ascii(msg, "contents"), short_id, seq, ref, msn);
     }
     sb_free(&name);
     update_seq_numbers(d, msn, seq);
@@ -2085,10 +2373,16 @@ static void dump_walk(mto_doc *d, const Block *b, sb *out, int depth) {
         } else {
             const Seg *s = (const Seg *)n;
             char t[160];
-            snprintf(t, sizeof t, "%*sS len=%d seq=%d cli=%d rseq=%d rcli=%d novl=%d '", depth * 2, "",
-                     s->n.cached_length, s->seq, s->client_id, s->removed ? s->removed_seq : -1,
-                     s->removed ? s->removed_client : -1, s->novl);
+            char rs[16] = "none";
+            if (s->removed) snprintf(rs, sizeof rs, "%d", s->removed_seq);
+            snprintf(t, sizeof t, "%*sS len=%d seq=%d cli=%d rseq=%s rcli=%d novl=%d ", depth * 2, "",
+                     s->n.cached_length, s->seq, s->client_id, rs, s->removed ? s->removed_client : -1, s->novl);
             sb_puts(out, t);
+            if (s->sg_n > 0) {
+                snprintf(t, sizeof t, "grp=%d ", s->sg_n);
+                sb_puts(out, t);
+            }
+            sb_putc(out, '\'');
             if (s->kind == SEG_TEXT) sb_put_u16_utf8(out, s->text, s->n.cached_length);
             sb_puts(out, "'");
             if (s->props) {
@@ -2169,6 +2463,43 @@ static jv *props_from_records(mto_doc *d, const mt_prop *p, uint32_t n, const mt
     return o;
 }
 
+/* a packed local op (seq == -1, client 0): see apply_local_op_json */
+static void apply_local_packed(mto_doc *d, const mt_op *op, const uint16_t *text, const mt_prop *props,
+                               const mto_tables *t) {
+    const uint32_t bits = MT_OPF_BITS(op->flags);
+    const int ref = d->cw.current_seq, cid = d->cw.client_id;
+    if (d->rel_pending) fail(d, MTO_UNSUPPORTED, "relative positions in a local op");
+    switch (op->type) {
+        case MT_OP_INSERT: {
+            if (!local_range_valid(d, 0, op->pos1, 0, 0)) return;
+            Seg *s;
+            if (bits & MT_OPF_MARKER) s = new_marker(d, (int)op->payload);
+            else s = new_text_seg(d, text + op->payload, (int)op->payload_len);
+            if (bits & MT_OPF_HAS_PROPS) {
+                jv *pr = props_from_records(d, props + op->pos2, MT_OPF_NPROPS(op->flags), t);
+                seg_add_properties(d, s, pr, 0, NULL, 0, 0);
+                jv_unref(pr);
+            }
+            insert_segment(d, op->pos1, s, ref, cid, UNASSIGNED_SEQ);
+            break;
+        }
+        case MT_OP_REMOVE:
+            if (!local_range_valid(d, 1, op->pos1, 1, op->pos2)) return;
+            mark_range_removed(d, op->pos1, op->pos2, ref, cid, UNASSIGNED_SEQ);
+            break;
+        case MT_OP_ANNOTATE: {
+            if (MT_OPF_COMBINE(op->flags)) fail(d, MTO_UNSUPPORTED, "local combiningOp other than rewrite");
+            if (!local_range_valid(d, 2, op->pos1, 1, op->pos2)) return;
+            jv *pr = props_from_records(d, props + op->payload, op->payload_len, t);
+            annotate_range(d, op->pos1, op->pos2, pr, (bits & MT_OPF_REWRITE) ? 1 : 0, NULL, ref, cid, UNASSIGNED_SEQ);
+            jv_unref(pr);
+            break;
+        }
+        case MT_OP_RELPOS: fail(d, MTO_UNSUPPORTED, "relative positions in a local op"); break;
+        default: fail(d, MTO_BAD_INPUT, "local op type %d", op->type);
+    }
+}
+
 static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, const mt_prop *props,
                              const mto_tables *t, const char *const *client_names, int n_clients) {
     if ((int)op->client >= n_clients) fail(d, MTO_BAD_INPUT, "client index out of range");
@@ -2177,9 +2508,27 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
         sid = get_or_add_short_client_id(d, client_names[op->client]); /* applyMsg registration */
         d->pk_map[op->client] = sid;
     }
-    if (op->type != MT_OP_NOOP && d->long_client_id && sid == d->cw.client_id)
-        fail(d, MTO_UNSUPPORTED, "ack of a local op (observer path only)");
     uint32_t bits = MT_OPF_BITS(op->flags);
+    if (op->seq == UNASSIGNED_SEQ) { /* a local op of this replica (mt_oplog.h "local ops") */
+        if (sid != d->cw.client_id) fail(d, MTO_BAD_INPUT, "local op of another client");
+        apply_local_packed(d, op, text, props, t);
+        return;
+    }
+    if (op->type != MT_OP_NOOP && d->long_client_id && sid == d->cw.client_id) {
+        /* the replica's own sequenced message: ack (client.ts:810-812); positions are not read */
+        if (op->type != MT_OP_RELPOS) {
+            jv *pr = NULL;
+            if (op->type == MT_OP_ANNOTATE) {
+                if (MT_OPF_COMBINE(op->flags) == MT_COMBINE_CONSENSUS)
+                    fail(d, MTO_UNSUPPORTED, "ack of a consensus annotate (updateConsensusProperty)");
+                pr = props_from_records(d, props + op->payload, op->payload_len, t);
+            }
+            ack_pending_segment(d, op->type, pr, op->type == MT_OP_ANNOTATE && (bits & MT_OPF_REWRITE), op->seq);
+            jv_unref(pr);
+        }
+        if (!(bits & MT_OPF_GROUP_CONT)) update_seq_numbers(d, op->msn, op->seq);
+        return;
+    }
     mt_op rop;
     if (d->rel_pending && op->type != MT_OP_RELPOS) { /* positions resolved by the RELPOS record */
         rop = *op;
@@ -2195,7 +2544,7 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
             else s = new_text_seg(d, text + op->payload, (int)op->payload_len);
             if (bits & MT_OPF_HAS_PROPS) {
                 jv *pr = props_from_records(d, props + op->pos2, MT_OPF_NPROPS(op->flags), t);
-                seg_add_properties(d, s, pr, 0, NULL, 0);
+                seg_add_properties(d, s, pr, 0, NULL, 0, 0);
                 jv_unref(pr);
             }
             insert_segment(d, op->pos1, s, op->ref_seq, sid, op->seq);

@@ -114,7 +114,7 @@ def _live_ids(doc):
     a marker zamboni unlinked is gone from the table)"""
     out = set()
     for ln in doc.dump().splitlines():
-        if '"markerId"' in ln and " rseq=-1 " in ln:
+        if '"markerId"' in ln and " rseq=none " in ln:
             out.add(json.loads(ln[ln.index("{"):])["markerId"])
     return out
 

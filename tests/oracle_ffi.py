@@ -75,6 +75,8 @@ def lib():
     L.mto_insert_local_json.argtypes = [vp, i, cp]
     L.mto_annotate_local_json.argtypes = [vp, i, i, cp]
     L.mto_remove_local.argtypes = [vp, i, i]
+    L.mto_local_op_json.argtypes = [vp, cp]
+    L.mto_pending_groups.argtypes = [vp]
     L.mto_get_length.argtypes = [vp]
     L.mto_view_length.argtypes = [vp, i, i]
     L.mto_current_seq.argtypes = [vp]
@@ -159,6 +161,15 @@ class Doc:
 
     def remove_local(self, start: int, end: int) -> int:
         return self.L.mto_remove_local(self.h, start, end)
+
+    def local_op(self, op) -> int:
+        """A local IMergeTreeOp of a collaborating replica (pending until its own message acks it)."""
+        import json as _json
+
+        return self.L.mto_local_op_json(self.h, (op if isinstance(op, str) else _json.dumps(op)).encode())
+
+    def pending_groups(self) -> int:
+        return self.L.mto_pending_groups(self.h)
 
     def length(self) -> int:
         return self.L.mto_get_length(self.h)

@@ -1,0 +1,167 @@
+"""GPU parity of the local-client path (writer replicas) through the C ABI (mt_writer_kernel_<SEG>).
+
+A writer replica's log interleaves its own local ops (unsequenced, UnassignedSequenceNumber) with
+the sequenced stream, in which its own messages ack them (client.ts:797-819, mergeTree.ts:
+1893-1929).  The HIP replay must equal the oracle's replica bit for bit: state digest (segment table
+incl. pending seqs, tombstones, leaf-block membership), tree shape, text, property runs and
+SnapshotV1 (which elides unacked segments, snapshotV1.ts:184-186).
+"""
+import json
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import fluidframework_amd as fa
+from writer_sim import farm, round_farm, writer_batch
+
+pytestmark = pytest.mark.gpu
+
+GEN_KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
+GEN_VALUES = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
+
+
+def assert_same(dv, od, what=""):
+    assert dv.status == od.status, (what, fa.status_string(dv.status), od.error)
+    if od.status != 0:
+        return
+    assert dv.digest() == od.digest(), f"{what}: digest\nGPU {dv.shape()}\nCPU {od.shape()}"
+    assert dv.shape() == od.shape(), what
+    assert dv.get_text() == od.text(), what
+    assert dv.props_runs() == json.loads(od.props_runs()), what
+    assert dv.snapshot_v1() == od.snapshot_v1(), what
+
+
+def oracle_replica(name, events, initial=""):
+    d = O.Doc()
+    if initial:
+        d.insert_local(0, json.dumps(initial))
+    d.start_collab(name)
+    for m in events:
+        if m["sequenceNumber"] == -1:
+            assert d.local_op(m["contents"]) == 0
+        elif d.apply_msg(json.dumps(m)) != 0:
+            break
+    return d
+
+
+def _farm_parity(f, **opts):
+    names = list(f.names)
+    docs = [f.events[n] for n in names]
+    with fa.ReplayBatch(len(docs), **opts) as b:
+        b.ingest_messages(docs, observer=names)
+        b.run()
+        for i, n in enumerate(names):
+            assert_same(b.doc(i), f.docs[n], n)
+        return b.stats()
+
+
+@pytest.mark.parametrize("seed,n_clients,steps,rewrite", [(1, 3, 400, 0), (2, 6, 900, 10), (3, 8, 1500, 25)])
+def test_free_running_farm_writers(seed, n_clients, steps, rewrite):
+    """Writers at their own pace (deep pending windows, remote ops on pending segments, the #1213
+    race): every writer's replica on the GPU equals the oracle's."""
+    _farm_parity(farm(n_clients, steps, seed, initial="hello world" if seed % 2 else "", rewrite=rewrite))
+
+
+@pytest.mark.parametrize("seed,n_clients,rounds", [(5, 4, 40), (6, 8, 30)])
+def test_conflict_farm_rounds_writers(seed, n_clients, rounds):
+    """The reference's conflict-farm schedule: writers converge (checked on the oracle) and the GPU
+    equals every writer exactly."""
+    f = round_farm(n_clients, rounds, seed, rewrite=15)
+    _farm_parity(f)
+    assert len({f.docs[n].text() for n in f.names}) == 1
+
+
+def test_writer_farm_with_forced_escalation():
+    """Checkpoint / resume through several capacity classes with pending groups in flight (the
+    pending-group region persists across launches)."""
+    f = farm(5, 1500, 9, rewrite=10)
+    stats = _farm_parity(f, seg_cap=64, max_retries=8)
+    assert stats["launches"] >= 2
+
+
+def test_issue_1213_writer_on_gpu():
+    """mergeTree.markRangeRemoved.spec.ts:111-164: the writer ends with "Xc" (its observer "cX")."""
+    m = lambda op, seq, c, ref: {"clientId": c, "sequenceNumber": seq, "referenceSequenceNumber": ref,  # noqa
+                                 "minimumSequenceNumber": 0, "type": "op", "contents": op}
+    op1, op2, op4 = ({"type": 0, "pos1": 0, "seg": "a"}, {"type": 1, "pos1": 0, "pos2": 1},
+                     {"type": 0, "pos1": 0, "seg": "c"})
+    events = [m(op1, -1, "1", 0), m(op2, -1, "1", 0), m(op1, 1, "1", 0), m(op2, 2, "1", 0), m(op4, -1, "1", 2),
+              m({"type": 0, "pos1": 0, "seg": "X"}, 3, "2", 0), m(op4, 4, "1", 2)]
+    with fa.ReplayBatch(1) as b:
+        b.ingest_messages([events], observer=["1"])
+        b.run()
+        assert b.doc(0).get_text() == "Xc"
+        assert_same(b.doc(0), oracle_replica("1", events))
+
+
+def test_pending_segments_in_snapshot_and_text():
+    """A writer stopped with ops still pending: getText holds its unacked inserts, SnapshotV1 elides
+    them and its pending removes (snapshotV1.ts:184-186)."""
+    f = farm(3, 300, 21)
+    names = list(f.names)
+    docs = []
+    for n in names:
+        ev = list(f.events[n])
+        # drop the acks of the last few local ops: they stay pending
+        own = [i for i, e in enumerate(ev) if e["clientId"] == n and e["sequenceNumber"] > 0]
+        cut = own[-3] if len(own) >= 3 else len(ev)
+        docs.append(ev[:cut])
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs, observer=names)
+        b.run()
+        for i, n in enumerate(names):
+            od = oracle_replica(n, docs[i])
+            assert od.pending_groups() > 0
+            assert_same(b.doc(i), od, n)
+
+
+def _gen_writer_parity(p, n_docs, full_every=4, **opts):
+    ops, text, props, off = O.gen_batch(p, n_docs)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    wops, woff, wnames = writer_batch(ops, off, names, lambda d: 1 + d % p.n_clients)
+    with fa.ReplayBatch(n_docs, **opts) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        for d in range(n_docs):
+            b.set_clients(wnames[d], d)
+        b.ingest(wops, woff, text, props)
+        b.run()
+        for d in range(n_docs):
+            od = O.replay_doc(wops[woff[d]:woff[d + 1]].copy(), text, props, t, wnames[d])
+            dv = b.doc(d)
+            assert dv.status == od.status, (d, fa.status_string(dv.status), od.error)
+            assert dv.digest() == od.digest(), f"doc {d}"
+            if d % full_every == 0:
+                assert_same(dv, od, f"doc {d}")
+        return b.stats()
+
+
+def test_generated_writer_logs_config2_shape():
+    """Writers of BASELINE configs[1]-shaped logs (8 clients, lag <= 32, insert 60 / remove 40)."""
+    _gen_writer_parity(O.gen_params(2000, seed=0xC0FFEE), 24)
+
+
+def test_generated_writer_logs_config3_mix():
+    """Writers of configs[2]-mix logs (annotate 10 %: remote annotates meet pending local keys)."""
+    _gen_writer_parity(O.gen_params(1500, pct_insert=55, pct_remove=35, seed=0xBADC0DE), 24)
+
+
+def test_generated_writer_logs_wide_windows():
+    """24 clients, lag 200: up to ~60 pending groups per writer, deep continuation walks."""
+    _gen_writer_parity(O.gen_params(1200, n_clients=24, max_lag=200, pct_insert=50, pct_remove=40, min_len=0,
+                                    max_insert=3, seed=77), 16)
+
+
+def test_observer_logs_still_run_the_observer_kernel():
+    """A log without local ops / own acks is an observer batch (mt_replay_kernel_<SEG>)."""
+    p = O.gen_params(500, seed=4)
+    ops, text, props, off = O.gen_batch(p, 4)
+    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(4) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        b.set_clients(names)
+        b.ingest(ops, off, text, props)
+        b.run()
+        for d in range(4):
+            assert b.doc(d).digest() == int(dig[d])

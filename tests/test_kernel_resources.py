@@ -52,6 +52,11 @@ def test_replay_kernel_fits_four_waves_per_simd(seg, tmp_path):
     assert r["private_segment_fixed_size"] <= 64, r
     assert _scratch_insts(tmp_path / (obj.stem + ".co"), f"mt_replay_kernel_{seg}") == 0
     assert f"mt_follow_kernel_{seg}" in k
+    # the writer replay (local-client path) keeps the 4-waves-per-SIMD residency; its extra state
+    # spills a few dwords (bounded here so growth is noticed)
+    w = k[f"mt_writer_kernel_{seg}"]
+    assert w["vgpr_count"] <= 128, w
+    assert w["private_segment_fixed_size"] <= 512, w
 
 
 def _scratch_insts(co: Path, kernel: str) -> int:

@@ -1,0 +1,216 @@
+"""Writer-replica logs for the local-client path (TEST INFRASTRUCTURE).
+
+A writer replica sees two kinds of events (client.ts:797-819, testClient.ts:213-234):
+  * its own local ops, applied at once with UnassignedSequenceNumber — here an unsequenced message
+    {"clientId": <replica>, "sequenceNumber": -1, "referenceSequenceNumber": <its currentSeq>, ...}
+    (what TestClient.makeOpMessage(op) builds), and
+  * the sequenced stream, in which its own messages ack its pending segment groups.
+
+Two sources:
+  * `farm`: a conflict farm in the oracle (client.conflictFarm.spec.ts's shape): writer replicas
+    issue ops from their own local views, a server sequences them as they arrive (msn = the
+    lowest sequence number every replica has processed, the deli rule), replicas process the
+    stream at their own pace.  Every replica's event stream is recorded.
+  * `writer_log`: the stream a writer `w` of a generated observer log saw.  Its op k (sequenced at
+    s_k with refSeq r_k) was issued right after it processed message r_k; its position is the same
+    in both views (the observer's view (r_k, w) and w's local view hold the same segments), so the
+    log is rearranged, not re-derived.
+"""
+from __future__ import annotations
+
+import json
+import random
+
+import numpy as np
+
+import oracle_ffi as O
+
+UNASSIGNED = -1
+
+
+def local_message(client: str, op: dict, ref: int) -> dict:
+    return {"clientId": client, "sequenceNumber": UNASSIGNED, "referenceSequenceNumber": ref,
+            "minimumSequenceNumber": 0, "type": "op", "contents": op}
+
+
+def random_op(rng: random.Random, length: int, n_keys: int = 4, p_annotate: int = 15, p_remove: int = 30,
+              max_insert: int = 6, rewrite: int = 0) -> dict:
+    """An op drawn from a replica's local view (length = its getLength())."""
+    u = rng.randrange(100)
+    if length == 0 or u >= p_annotate + p_remove:
+        n = 1 + rng.randrange(max_insert)
+        text = "".join(rng.choice("abcdefgh \n" if rng.randrange(10) == 0 else "abcdefgh ") for _ in range(n))
+        seg = text if rng.randrange(4) else {"text": text, "props": {"k0": rng.randrange(3)}}
+        return {"type": 0, "pos1": rng.randrange(length + 1), "seg": seg}
+    start = rng.randrange(length)
+    end = min(length, start + 1 + rng.randrange(8))
+    if u < p_remove:
+        return {"type": 1, "pos1": start, "pos2": end}
+    props = {}
+    for _ in range(1 + rng.randrange(2)):
+        props[f"k{rng.randrange(n_keys)}"] = None if rng.randrange(8) == 0 else rng.randrange(4)
+    op = {"type": 2, "pos1": start, "pos2": end, "props": props}
+    if rewrite and rng.randrange(100) < rewrite:
+        op["combiningOp"] = {"name": "rewrite"}
+    return op
+
+
+class Farm:
+    """Writer replicas + an observer over one sequenced stream (all in the oracle)."""
+
+    def __init__(self, n_clients: int, seed: int, initial: str = ""):
+        self.rng = random.Random(seed)
+        self.names = [chr(ord("A") + i) for i in range(n_clients)]
+        self.docs = {}
+        self.events = {n: [] for n in self.names}
+        for n in self.names:
+            d = O.Doc()
+            if initial:
+                assert d.insert_local(0, json.dumps(initial)) == 0
+            d.start_collab(n)
+            self.docs[n] = d
+        self.observer = O.Doc()
+        if initial:
+            assert self.observer.insert_local(0, json.dumps(initial)) == 0
+        self.observer.start_collab("readonly")
+        self.log = []        # sequenced messages
+        self.cursor = {n: 0 for n in self.names}
+
+    def msn(self) -> int:
+        return min(self.cursor.values())
+
+    def local(self, name: str, op: dict):
+        d = self.docs[name]
+        ref = d.L.mto_current_seq(d.h)
+        before = d.pending_groups()
+        assert d.local_op(op) == 0, d.error
+        msg = local_message(name, op, ref)
+        self.events[name].append(msg)
+        if d.pending_groups() == before:  # not applied (empty): nothing is submitted
+            return
+        seq = len(self.log) + 1
+        self.log.append({"clientId": name, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+                         "minimumSequenceNumber": self.msn(), "type": "op", "contents": op})
+
+    def deliver(self, name: str, k: int = 1):
+        d = self.docs[name]
+        for _ in range(k):
+            c = self.cursor[name]
+            if c >= len(self.log):
+                return
+            m = self.log[c]
+            self.events[name].append(m)
+            assert d.apply_msg(json.dumps(m)) == 0, d.error
+            self.cursor[name] = c + 1
+
+    def step(self, p_op=45, **op_kw):
+        name = self.rng.choice(self.names)
+        if self.rng.randrange(100) < p_op:
+            d = self.docs[name]
+            self.local(name, random_op(self.rng, d.length(), **op_kw))
+        else:
+            self.deliver(name, 1 + self.rng.randrange(4))
+
+    def finish(self):
+        for n in self.names:
+            self.deliver(n, len(self.log))
+        for m in self.log:
+            assert self.observer.apply_msg(json.dumps(m)) == 0, self.observer.error
+
+
+def farm(n_clients: int, n_steps: int, seed: int, initial: str = "", **kw) -> Farm:
+    """Free-running farm: replicas issue ops and process the stream at their own pace, so a
+    replica may have acked its own ops while another's concurrent ops are still unseen — the
+    race of issue #1213 (mergeTree.markRangeRemoved.spec.ts:111-164, a skipped test: the
+    reference's replicas can diverge from the observer there).  For GPU == oracle parity."""
+    f = Farm(n_clients, seed, initial)
+    for _ in range(n_steps):
+        f.step(**kw)
+    f.finish()
+    return f
+
+
+def round_farm(n_clients: int, n_rounds: int, seed: int, initial: str = "", max_ops: int = 24, **kw) -> Farm:
+    """The reference's conflict farm schedule (client.conflictFarm.spec.ts:60-99,
+    mergeTreeOperationRunner.ts:95-176): each round every replica starts caught up at seq S with
+    minSeq S, random replicas issue local ops (refSeq S, each seeing its own pending ops), the
+    round's messages are sequenced in issue order with msn S and every replica applies all of them.
+    The reference asserts convergence for this schedule."""
+    f = Farm(n_clients, seed, initial)
+    for _ in range(n_rounds):
+        s0 = len(f.log)
+        ops = 1 + f.rng.randrange(max_ops)
+        for _ in range(ops):
+            name = f.rng.choice(f.names)
+            f.local(name, random_op(f.rng, f.docs[name].length(), **kw))
+        for m in f.log[s0:]:
+            m["minimumSequenceNumber"] = s0
+        for n in f.names:
+            f.deliver(n, len(f.log))
+    f.finish()
+    return f
+
+
+def writer_messages(msgs: list, w: str) -> list:
+    """The event stream writer `w` saw, rebuilt from a sequenced message list (seq order)."""
+    issued = {}
+    for m in msgs:
+        if m["clientId"] == w and m.get("type") == "op":
+            issued.setdefault(m["referenceSequenceNumber"], []).append(
+                local_message(w, m["contents"], m["referenceSequenceNumber"]))
+    out = list(issued.get(0, []))
+    for m in msgs:
+        out.append(m)
+        out.extend(issued.get(m["sequenceNumber"], []))
+    return out
+
+
+def writer_log(ops: np.ndarray, names: list, w: int):
+    """writer_messages on a packed log (one document, generator / packer records): records of
+    client `w` are issued as local copies (seq -1, client 0) after the last record of the message
+    numbered by their refSeq, and ack as client 0; every other client keeps its name.  Returns
+    (records, client names with w's name first)."""
+    ops = np.asarray(ops)
+    # group the records into messages (a GROUP's members share one message: GROUP_CONT chains)
+    msgs, cur = [], []
+    for i in range(len(ops)):
+        cur.append(i)
+        if not (int(ops[i]["flags"]) & 1):
+            msgs.append(cur)
+            cur = []
+    if cur:
+        msgs.append(cur)
+    issued = {}
+    for m in msgs:
+        r0 = ops[m[0]]
+        if int(r0["client"]) == w and int(r0["type"]) != 15:
+            local = ops[m].copy()
+            local["seq"] = UNASSIGNED
+            local["client"] = 0
+            local["msn"] = 0
+            issued.setdefault(int(r0["ref_seq"]), []).append(local)
+    # short ids: w first, the others keep their order (the packed client field indexes `names`)
+    order = [w] + [c for c in range(len(names)) if c != w]
+    remap = np.zeros(256, np.int64)
+    for new, old in enumerate(order):
+        remap[old] = new
+    out = list(issued.get(0, []))
+    for m in msgs:
+        rec = ops[m].copy()
+        rec["client"] = remap[rec["client"].astype(np.int64)]
+        out.append(rec)
+        out.extend(issued.get(int(ops[m[0]]["seq"]), []))
+    recs = np.concatenate(out) if out else ops[:0].copy()
+    return recs, [names[c] for c in order]
+
+
+def writer_batch(ops: np.ndarray, off: np.ndarray, names: list, writer_of) -> tuple:
+    """writer_log over every document of a packed batch; writer_of(d) picks the writer's short id.
+    Returns (ops, off, per-document client names)."""
+    out, offs, docs_names = [], [0], []
+    for d in range(len(off) - 1):
+        recs, nm = writer_log(ops[off[d]:off[d + 1]], names, writer_of(d))
+        out.append(recs)
+        offs.append(offs[-1] + len(recs))
+        docs_names.append(nm)
+    return np.concatenate(out), np.array(offs, np.int64), docs_names
