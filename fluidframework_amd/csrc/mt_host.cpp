@@ -381,6 +381,7 @@ struct mt_batch {
     int32_t max_ops_per_doc = 0;
     std::vector<int64_t> h_off;
     std::vector<int32_t> h_nload, h_nload_segs;  // leading SnapshotLoader records / segments per doc
+    std::vector<uint8_t> h_tile_annot;  // per doc: an annotate touches referenceTileLabels (findTile)
     std::vector<uint64_t> h_text_base, h_pool_base;
     std::vector<uint32_t> h_text_len, h_text_cap, h_pool_cap;
     uint64_t text_words = 0, pool_words = 0;
@@ -874,6 +875,21 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         pool_cap[d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
         pbase += align16u(pc);
     }
+    // findTile reads the block tile maps that blockUpdate rebuilds (mergeTree.ts:2748-2767); an
+    // annotate of referenceTileLabels changes a marker's labels without one, so such documents'
+    // tile queries are MT_UNSUPPORTED
+    std::vector<uint8_t> tile_annot((size_t)D, 0);
+    {
+        uint32_t tk = 0xFFFFFFFFu;
+        for (size_t k = 0; k < b->keys.size(); k++)
+            if (b->keys[k] == "referenceTileLabels") tk = (uint32_t)k;
+        if (tk != 0xFFFFFFFFu)
+            for (int64_t d = 0; d < D; d++)
+                for (int64_t i = h_off[d]; i < h_off[d + 1] && !tile_annot[(size_t)d]; i++)
+                    if (ops[i].type == MT_OP_ANNOTATE)
+                        for (uint32_t q = 0; q < ops[i].payload_len; q++)
+                            if (props[ops[i].payload + q].key == tk) tile_annot[(size_t)d] = 1;
+    }
     // a writer replica's log: local ops (seq == UnassignedSequenceNumber) or sequenced messages of
     // the replica itself (short id 0) that ack them
     bool writer = false;
@@ -925,6 +941,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     b->h_pool_cap = std::move(pool_cap);
     b->h_nload = std::move(nload);
     b->h_nload_segs = std::move(nload_segs);
+    b->h_tile_annot = std::move(tile_annot);
     b->payload_units = payload_units;
     b->prop_records = prop_records;
     b->text_words = tbase;
@@ -1893,6 +1910,114 @@ MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, i
     return out_str(o, buf, cap, len);
 }
 
+// The labels of a Tile marker (refHasTileLabels / refHasTileLabel, mergeTree.ts:580-597): its
+// referenceTileLabels value parsed as an array of strings.  0: not a tile (no Tile refType or no
+// truthy labels), 1: labels in `out`, -1: a value the device does not model (a string — for-of
+// would visit its code points — or non-string elements, which the block maps key by String(x)
+// while the leaf test compares with ===).
+static int tile_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, std::vector<std::u16string> &out) {
+    out.clear();
+    if (!(r.meta & mt::kMetaMarker) || !(r.toff & 1u) || !r.props || tk == 0xFFFFFFFFu) return 0;
+    const uint32_t *p = b->c_pool.data() + r.props;
+    uint32_t v = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < p[0]; i++)
+        if (p[2 + 2 * i] == tk) v = p[3 + 2 * i];
+    if (v == 0xFFFFFFFFu || v >= b->values.size() || (b->value_flags[v] & mt::kValFalsy)) return 0;
+    const std::string &j = b->values[v];
+    size_t i = 0;
+    auto ws = [&]() { while (i < j.size() && (j[i] == ' ' || j[i] == '\t' || j[i] == '\n' || j[i] == '\r')) i++; };
+    ws();
+    if (i >= j.size() || j[i] != '[') return -1;
+    i++;
+    ws();
+    if (i < j.size() && j[i] == ']') return 1;
+    for (;;) {
+        ws();
+        if (i >= j.size() || j[i] != '"') return -1;
+        size_t e = i + 1;
+        while (e < j.size() && j[e] != '"') e += j[e] == '\\' ? 2 : 1;
+        if (e >= j.size()) return -1;
+        std::u16string s;
+        if (!mt::js_string_of(j.substr(i, e + 1 - i), s)) return -1;
+        out.push_back(s);
+        i = e + 1;
+        ws();
+        if (i < j.size() && j[i] == ',') {
+            i++;
+            continue;
+        }
+        return (i < j.size() && j[i] == ']') ? 1 : -1;
+    }
+}
+
+// Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076 -> MergeTree.findTile,
+// mergeTree.ts:1763-1789) on the document's final table, in the replica's local view
+// (refSeq UniversalSequenceNumber).  With the block tile maps current (every path that changes a
+// marker's presence runs blockUpdate on its ancestors), search / backwardSearch reduce to:
+//   preceding:  the labelled tile marker containing startPos, else the last one (not removed)
+//               before it; past the end, the last one of the document;
+//   following:  startPos > length: none; the labelled tile containing startPos, else the first one
+//               (not removed) after it; startPos == length: the document's last leaf, if it is one.
+MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const char *label_utf8, int32_t preceding,
+                            int64_t *tile_pos, char *props_buf, int64_t props_cap, int64_t *props_len) {
+    if (!b || !label_utf8 || !tile_pos) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    *tile_pos = -1;
+    if (props_len) *props_len = 0;
+    if (b->c_out.status != MT_OK) return b->c_out.status;
+    if (b->h_tile_annot[(size_t)doc]) return MT_UNSUPPORTED;
+    const std::vector<uint16_t> lu = utf8_to_utf16(std::string(label_utf8));
+    const std::u16string label(lu.begin(), lu.end());
+    uint32_t tk = 0xFFFFFFFFu;
+    for (size_t k = 0; k < b->keys.size(); k++)
+        if (b->keys[k] == "referenceTileLabels") tk = (uint32_t)k;
+    std::vector<const OutRec *> leaves;
+    for (const OutRec &r : b->c_recs)
+        if (!rec_is_marker(r)) leaves.push_back(&r);
+    std::vector<std::u16string> labels;
+    bool bad = false;
+    auto labelled = [&](const OutRec &r) {
+        const int t = tile_labels_of(b, r, tk, labels);
+        if (t < 0) bad = true;
+        if (t <= 0) return false;
+        for (const auto &l : labels)
+            if (l == label) return true;
+        return false;
+    };
+    auto local_len = [](const OutRec &r) -> int64_t { return rec_removed(r) ? 0 : (int64_t)r.len; };
+    int64_t total = 0;
+    for (const OutRec *r : leaves) total += local_len(*r);
+    // every tile marker's labels are checked, so an unmodelled value anywhere is reported
+    for (const OutRec *r : leaves) (void)labelled(*r);
+    if (bad) return MT_UNSUPPORTED;
+    int64_t found = -1;  // leaf index
+    int64_t pos = 0, k = 0;
+    const int64_t n = (int64_t)leaves.size();
+    while (k < n && !(start_pos < pos + local_len(*leaves[(size_t)k]))) pos += local_len(*leaves[(size_t)k++]);
+    // k: the containing leaf (n: none)
+    if (preceding) {
+        if (k < n && labelled(*leaves[(size_t)k])) found = k;
+        else
+            for (int64_t i = (k < n ? k : n) - 1; i >= 0 && found < 0; i--)
+                if (local_len(*leaves[(size_t)i]) > 0 && labelled(*leaves[(size_t)i])) found = i;
+    } else if (start_pos < total) {
+        if (labelled(*leaves[(size_t)k])) found = k;
+        else
+            for (int64_t i = k + 1; i < n && found < 0; i++)
+                if (local_len(*leaves[(size_t)i]) > 0 && labelled(*leaves[(size_t)i])) found = i;
+    } else if (start_pos == total && n > 0) {
+        if (labelled(*leaves[(size_t)(n - 1)])) found = n - 1;
+    }
+    if (found < 0) return MT_OK;
+    int64_t tp = 0;
+    for (int64_t i = 0; i < found; i++) tp += local_len(*leaves[(size_t)i]);
+    *tile_pos = tp;
+    std::string pj;
+    if (leaves[(size_t)found]->props) props_json(b, leaves[(size_t)found]->props, pj);
+    return out_str(pj, props_buf, props_cap, props_len);
+}
+
 // segment.toJSONObject() (textSegment.ts:48-54, mergeTree.ts:652-656)
 static void seg_json(mt_batch *b, bool text, const uint16_t *t, size_t n, uint32_t ref_type, uint32_t props,
                      std::string &o) {
@@ -2505,6 +2630,7 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
     b->h_off[0] = 0;
     b->h_nload.assign(D, 0);
     b->h_nload_segs.assign(D, 0);
+    b->h_tile_annot.assign(D, 0);
     int32_t max_ops = 0;
     for (int64_t d = 0; d < D; d++) {
         if (doc_ops[d] < 1) return MT_ERR_ARG;

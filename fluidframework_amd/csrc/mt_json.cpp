@@ -21,8 +21,10 @@
 //   * keys and values interned batch-wide in first-appearance order (document order, then
 //     op order), text and prop records laid out back to back in document order.
 //
-// Relative positions, registers and the observer's own ops are outside the observer replay
-// path and fail the document with MT_UNSUPPORTED (the packers raise UnsupportedOp).
+// A writer replica's unsequenced messages (sequenceNumber -1) pack as local-op records (seq -1,
+// client 0) and its sequenced ones as acks (client 0).  Registers, relative positions and
+// combiningOps other than rewrite in local ops fail the document with MT_UNSUPPORTED (the packers
+// raise UnsupportedOp).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -793,7 +795,12 @@ struct Packer1 {
         return true;
     }
 
-    bool run(int32_t root, const std::u16string &observer) {
+    bool run(int32_t root, std::u16string observer) {
+        // {"replica": id, ...}: the document's own long id (a writer replica), default `observer`
+        if (root >= 0 && D.nodes[root].type == J_OBJ) {
+            const int32_t rep = D.member(root, "replica");
+            if (rep >= 0 && D.nodes[rep].type == J_STR) observer = D.str_of(rep);
+        }
         L.names.assign(1, observer);
         L.shortid.clear();
         L.shortid.emplace(observer, 0);
@@ -820,22 +827,38 @@ struct Packer1 {
             base.ref_seq = as_int(D.nodes[rs]);
             base.msn = as_int(D.nodes[ms]);
             base.type = MT_OP_NOOP;
+            // a writer replica's own unsequenced message (sequenceNumber -1, UnassignedSequenceNumber)
+            // is a local op; its sequenced ones ack them (client.ts:797-819; mt_oplog.h)
+            const bool local = base.seq == -1;
+            const bool ack = c == 0 && !local;
+            if (local) {
+                if (c != 0) return fail(MT_UNSUPPORTED, "an unsequenced message of another client");
+                base.msn = 0;
+            }
             const int32_t ty = D.member(m, "type");
             const bool is_op = ty >= 0 && D.nodes[ty].type == J_STR && D.str_of(ty) == u"op";
             if (!is_op) {
+                if (local) return fail(MT_UNSUPPORTED, "a local message that is not an op");
                 L.ops.push_back(base);
                 continue;
             }
-            if (c == 0) return fail(MT_UNSUPPORTED, "ack of the observer's own op (local path)");
             std::vector<int32_t> members;
             const int32_t contents = D.member(m, "contents");
             if (contents >= 0) flatten(contents, members);
             for (size_t j = 0; j < members.size(); j++) {
                 mt_op r{};
                 if (!relpos(members[j], base, r)) return false;
-                if (r.type == MT_OP_RELPOS) L.ops.push_back(r);
+                if (r.type == MT_OP_RELPOS) {
+                    if (local) return fail(MT_UNSUPPORTED, "relative positions in a local op");
+                    if (!ack) L.ops.push_back(r);  // an ack reads no positions
+                }
                 r = mt_op{};
                 if (!pack_op(members[j], base, r)) return false;
+                if (r.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(r.flags) != MT_COMBINE_NONE) {
+                    if (local) return fail(MT_UNSUPPORTED, "local combiningOp other than rewrite");
+                    if (ack && MT_OPF_COMBINE(r.flags) == MT_COMBINE_CONSENSUS)
+                        return fail(MT_UNSUPPORTED, "ack of a consensus annotate (updateConsensusProperty)");
+                }
                 if (j + 1 < members.size()) r.flags |= MT_OPF_GROUP_CONT;
                 L.ops.push_back(r);
             }

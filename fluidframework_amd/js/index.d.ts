@@ -25,8 +25,17 @@ export declare class ReplayClient {
     readonly index: number;
     /** Client.startOrUpdateCollaboration(longClientId) (client.ts:1051): the observer's id. */
     startOrUpdateCollaboration(longClientId: string): void;
-    /** Client.applyMsg(msg) (client.ts:797): queued; applied on the GPU by ReplayBatch.run(). */
+    /** Client.applyMsg(msg) (client.ts:797): queued; applied on the GPU by ReplayBatch.run().
+     *  The replica's own sequenced messages ack its pending local ops. */
     applyMsg(msg: ISequencedDocumentMessage | string): void;
+    /** Writer replicas: Client.insertSegmentLocal / removeRangeLocal / annotateRangeLocal
+     *  (client.ts:201-291), queued as unsequenced messages (sequenceNumber -1); returns the op. */
+    insertTextLocal(pos: number, text: string, props?: Record<string, any>): object;
+    insertMarkerLocal(pos: number, refType: number, props?: Record<string, any>): object;
+    removeRangeLocal(start: number, end: number): object;
+    annotateRangeLocal(start: number, end: number, props: Record<string, any>, combiningOp?: { name: string }): object;
+    /** Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076) on the final state. */
+    findTile(startPos: number, tileLabel: string, preceding?: boolean): { pos: number; props?: Record<string, any> } | undefined;
     /** 0 = OK, else the MT_* status of the Error applyMsg would have thrown. */
     readonly status: number;
     readonly error: string | undefined;

@@ -175,14 +175,27 @@ class Packer {
                 short.set(msg.clientId, c);
                 names.push(msg.clientId);
             }
-            const base = { client: c, seq: msg.sequenceNumber, refSeq: msg.referenceSequenceNumber, msn: msg.minimumSequenceNumber };
+            // a writer replica's own unsequenced message (sequenceNumber -1 = UnassignedSequenceNumber,
+            // TestClient.makeOpMessage's default) is a local op; its sequenced ones ack them
+            const local = msg.sequenceNumber === -1;
+            const ack = c === 0 && !local;
+            if (local && c !== 0) throw new UnsupportedOp('an unsequenced message of another client');
+            const base = { client: c, seq: msg.sequenceNumber, refSeq: msg.referenceSequenceNumber || 0, msn: local ? 0 : msg.minimumSequenceNumber };
             const noop = Object.assign({}, base, { type: OP_NOOP, flags: 0, pos1: 0, pos2: 0, payload: 0, payloadLen: 0 });
-            if (msg.type !== 'op') { recs.push(noop); continue; }
-            if (c === 0) throw new UnsupportedOp("ack of the observer's own op (local path)");
+            if (msg.type !== 'op') {
+                if (local) throw new UnsupportedOp('a local message that is not an op');
+                recs.push(noop);
+                continue;
+            }
             const members = Packer.flatten(msg.contents);
             members.forEach((op, j) => {
+                const cop = op.combiningOp;
+                if (local && cop && cop.name !== 'rewrite') throw new UnsupportedOp('local combiningOp other than rewrite');
+                if (ack && op.type === OP_ANNOTATE && cop && cop.name === 'consensus')
+                    throw new UnsupportedOp('ack of a consensus annotate (updateConsensusProperty)');
                 const rel = this.relPos(op, base);
-                if (rel) recs.push(rel);
+                if (rel && local) throw new UnsupportedOp('relative positions in a local op');
+                if (rel && !ack) recs.push(rel);  // an ack reads no positions
                 const r = this.packOp(op, base);
                 if (j + 1 < members.length) r.flags |= OPF_GROUP_CONT;
                 recs.push(r);
@@ -229,6 +242,32 @@ class ReplayClient {
     }
     startOrUpdateCollaboration(longClientId) { this.longClientId = longClientId; }
     applyMsg(msg) { this.batch.queued = true; this.messages.push(msg); }
+    // A writer replica's local ops (Client.insertSegmentLocal / removeRangeLocal /
+    // annotateRangeLocal, client.ts:201-291): queued as the replica's unsequenced messages
+    // (sequenceNumber -1, as TestClient.makeOpMessage(op) builds them), applied on the GPU with
+    // UnassignedSequenceNumber and acked when applyMsg later passes the replica's own sequenced
+    // message.  Each returns the op, as the reference does.
+    localOp(op) {
+        this.batch.queued = true;
+        this.messages.push({ clientId: this.longClientId, sequenceNumber: -1, referenceSequenceNumber: 0,
+            minimumSequenceNumber: 0, type: 'op', contents: op });
+        return op;
+    }
+    insertTextLocal(pos, text, props) { return this.localOp({ pos1: pos, seg: props ? { text, props } : text, type: OP_INSERT }); }
+    insertMarkerLocal(pos, refType, props) {
+        return this.localOp({ pos1: pos, seg: props ? { marker: { refType }, props } : { marker: { refType } }, type: OP_INSERT });
+    }
+    removeRangeLocal(start, end) { return this.localOp({ pos1: start, pos2: end, type: OP_REMOVE }); }
+    annotateRangeLocal(start, end, props, combiningOp) {
+        const op = { pos1: start, pos2: end, props, type: OP_ANNOTATE };
+        if (combiningOp) op.combiningOp = combiningOp;
+        return this.localOp(op);
+    }
+    // Client.findTile(startPos, tileLabel, preceding = true) (client.ts:1073-1076) on the final state
+    findTile(startPos, tileLabel, preceding = true) {
+        const r = native().docFindTile(this.batch.h, this.index, startPos, tileLabel, preceding);
+        return r === undefined ? undefined : { pos: r.pos, props: r.props ? JSON.parse(r.props) : undefined };
+    }
     get status() { return native().docStatus(this.batch.h, this.index); }
     get error() { const s = this.status; return s === 0 ? undefined : STATUS[s] || String(s); }
     getText() { return native().docText(this.batch.h, this.index); }

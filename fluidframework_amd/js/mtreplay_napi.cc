@@ -329,6 +329,34 @@ napi_value doc_snapshot(napi_env env, napi_callback_info info) {
     return obj;
 }
 
+// docFindTile(h, doc, startPos, label, preceding) -> { pos, props } | undefined
+// (Client.findTile, client.ts:1073-1076, via mt_doc_find_tile)
+napi_value doc_find_tile(napi_env env, napi_callback_info info) {
+    auto a = args(env, info, 5);
+    mt_batch *b = batch_of(env, a[0]);
+    const int64_t doc = i64(env, a[1]), start = i64(env, a[2]);
+    const std::string label = str(env, a[3]);
+    bool prec = true;
+    NAPI_OK(napi_get_value_bool(env, a[4], &prec));
+    int64_t pos = -1, n = 0;
+    MT_OK_OR_THROW(mt_doc_find_tile(b, doc, start, label.c_str(), prec ? 1 : 0, &pos, nullptr, 0, &n), "mt_doc_find_tile");
+    napi_value r;
+    if (pos < 0) {
+        NAPI_OK(napi_get_undefined(env, &r));
+        return r;
+    }
+    std::string props((size_t)n + 1, '\0');
+    MT_OK_OR_THROW(mt_doc_find_tile(b, doc, start, label.c_str(), prec ? 1 : 0, &pos, &props[0], n + 1, &n),
+                   "mt_doc_find_tile");
+    napi_value vp, vs;
+    NAPI_OK(napi_create_object(env, &r));
+    NAPI_OK(napi_create_int64(env, pos, &vp));
+    NAPI_OK(napi_create_string_utf8(env, props.data(), (size_t)n, &vs));
+    NAPI_OK(napi_set_named_property(env, r, "pos", vp));
+    NAPI_OK(napi_set_named_property(env, r, "props", vs));
+    return r;
+}
+
 napi_value doc_digest(napi_env env, napi_callback_info info) {
     auto a = args(env, info, 2);
     uint64_t d = 0;
@@ -398,6 +426,7 @@ napi_value init(napi_env env, napi_value exports) {
         {"docPropsRuns", nullptr, doc_props_runs, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docSnapshotV1", nullptr, doc_snapshot, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docDigest", nullptr, doc_digest, nullptr, nullptr, nullptr, kMethod, nullptr},
+        {"docFindTile", nullptr, doc_find_tile, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"deviceDigests", nullptr, device_digests, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"stats", nullptr, stats, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"statusString", nullptr, status_string, nullptr, nullptr, nullptr, kMethod, nullptr},

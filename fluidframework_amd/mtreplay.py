@@ -43,7 +43,7 @@ EXPORTS = [
     "mt_batch_snapshot_digests", "mt_batch_generate_docs", "mt_pack_json", "mt_packed_destroy", "mt_packed_error",
     "mt_packed_sizes", "mt_packed_arrays", "mt_packed_key", "mt_packed_value", "mt_packed_doc_clients",
     "mt_packed_client", "mt_batch_ingest_packed", "mt_batch_log_sizes_docs", "mt_batch_download_log_docs",
-    "mt_build_id",
+    "mt_build_id", "mt_doc_find_tile",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -167,6 +167,7 @@ def lib():
     L.mt_batch_snapshot_index.argtypes = [vp, vp, vp]
     L.mt_batch_snapshot_copy.argtypes = [vp, vp, i32]
     L.mt_batch_snapshot_digests.argtypes = [vp, vp, i32]
+    L.mt_doc_find_tile.argtypes = [vp, i64, i64, cp, i32, P(i64), C.c_char_p, i64, P(i64)]
     _lib = L
     return L
 
@@ -264,6 +265,20 @@ class DocView:
             if start <= pos < start + length:
                 return None if props is None else json.loads(props)
         return None
+
+    def find_tile(self, start_pos: int, label: str, preceding: bool = True):
+        """Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076): None when there is
+        no tile, else {"pos": .., "props": marker properties}."""
+        L = lib()
+        pos, n = C.c_int64(-1), C.c_int64(0)
+        args = (self.batch.h, self.index, start_pos, label.encode("utf-8"), 1 if preceding else 0, C.byref(pos))
+        _chk(L.mt_doc_find_tile(*args, None, 0, C.byref(n)), "mt_doc_find_tile")
+        if pos.value < 0:
+            return None
+        buf = C.create_string_buffer(n.value + 1)
+        _chk(L.mt_doc_find_tile(*args, buf, n.value + 1, C.byref(n)), "mt_doc_find_tile")
+        raw = buf.raw[: n.value].decode("utf-8")
+        return {"pos": pos.value, "props": json.loads(raw) if raw else None}
 
     def shape(self) -> str:
         return self._string(lib().mt_doc_shape)

@@ -18,6 +18,7 @@
  *                               client.ts:461-464, 824-826) as a per-document code
  *   mt_doc_text                 SharedString.getText() (sequence/src/sharedString.ts:211-214 ->
  *                               MergeTreeTextHelper.getText, textSegment.ts:154-172)
+ *   mt_doc_find_tile            Client.findTile(startPos, label, preceding) (client.ts:1073-1076)
  *   mt_doc_props_runs           Client.getPropertiesAtPosition(pos) for every pos (client.ts:1009-1023),
  *                               run-length encoded
  *   mt_doc_snapshot_v1/_blob    new SnapshotV1(mergeTree, logger).extractSync(); emit()
@@ -164,6 +165,13 @@ MT_API int32_t mt_doc_status(mt_batch *b, int64_t doc);
 MT_API int mt_batch_doc_counters(mt_batch *b, int32_t *out);
 MT_API int mt_doc_text(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
 MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
+/* Client.findTile(startPos, tileLabel, preceding) (merge-tree/src/client.ts:1073-1076,
+   mergeTree.ts:1763-1789) on the document's final state: *tile_pos = the tile marker's position
+   (-1: no tile); props_buf gets JSON.stringify(marker.properties) (size query with cap 0).
+   MT_UNSUPPORTED: the document annotates referenceTileLabels (the reference's block tile maps
+   would be stale) or holds a label list other than an array of strings. */
+MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const char *label_utf8, int32_t preceding,
+                            int64_t *tile_pos, char *props_buf, int64_t props_cap, int64_t *props_len);
 MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs);
 MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name, int64_t name_cap, char *buf,
                                 int64_t cap, int64_t *len);

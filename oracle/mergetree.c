@@ -61,6 +61,14 @@ struct Block { /* MergeBlock / HierMergeBlock, mergeTree.ts:336-420 */
     int max_seq, max_rseq;
     Block *all_next;
     struct mto_doc *doc; /* for blockUpdate's marker-id bookkeeping (addNodeReferences) */
+    /* HierMergeBlock.rightmostTiles / leftmostTiles (mergeTree.ts:386-399): String(label) -> the
+       marker, rebuilt by every blockUpdate from the children (addNodeReferences, 263-318) */
+    struct TileMap {
+        u16 **keys;
+        int *klens;
+        struct Seg **segs;
+        int n, cap;
+    } rt, lt;
 };
 
 typedef struct Group Group;
@@ -145,6 +153,9 @@ struct mto_doc {
     int id_hcap;
     /* packed MT_OP_RELPOS: resolved positions for the next record (bit 0 pos1, bit 1 pos2) */
     int rel_pending, rel_pos1, rel_pos2;
+    /* a Tile marker whose referenceTileLabels is not an array / string (for-of would throw in
+       blockUpdate): tile queries report MTO_UNSUPPORTED */
+    int tile_bad;
     /* local-client path: collabWindow.localSeq (mergeTree.ts:831) and MergeTree.pendingSegments,
        the FIFO of SegmentGroups awaiting their ack (mergeTree.ts:1093, 1261) */
     int local_seq;
@@ -234,6 +245,7 @@ static int node_total_length(const Node *n) { /* mergeTree.ts:422-427 */
 
 static int seq_bound(int seq) { return seq == UNASSIGNED_SEQ ? INT_MAX : seq; }
 static void map_marker_id(mto_doc *d, Seg *s);
+static void block_update_tiles(Block *b);
 static void block_update(Block *b) { /* mergeTree.ts:2748-2768 (cachedLength part) */
     int len = 0, ms = INT_MIN, mr = INT_MIN;
     for (int i = 0; i < b->child_count; i++) {
@@ -254,6 +266,7 @@ static void block_update(Block *b) { /* mergeTree.ts:2748-2768 (cachedLength par
     b->n.cached_length = len;
     b->max_seq = ms;
     b->max_rseq = mr;
+    block_update_tiles(b);
 }
 /* raise the bounds on the path above a leaf whose seq / removedSeq was just set */
 static void bump_bounds(Seg *s) {
@@ -1253,6 +1266,205 @@ static void annotate_range(mto_doc *d, int start, int end, const jv *props, int 
     if (d->cw.collaborating && seq != UNASSIGNED_SEQ) zamboni_segments(d);
 }
 
+static u16 *utf8_to_u16(const char *s, int *n);
+/* ------------------------------------------------------------------ tiles (findTile) */
+static void tm_clear(struct TileMap *m) {
+    for (int i = 0; i < m->n; i++) free(m->keys[i]);
+    m->n = 0;
+}
+static void tm_free(struct TileMap *m) {
+    tm_clear(m);
+    free(m->keys);
+    free(m->klens);
+    free(m->segs);
+}
+static int tm_find(const struct TileMap *m, const u16 *k, int kl) {
+    for (int i = 0; i < m->n; i++)
+        if (m->klens[i] == kl && !memcmp(m->keys[i], k, sizeof(u16) * (size_t)kl)) return i;
+    return -1;
+}
+/* tiles[label] = seg (overwrite), or only if absent */
+static void tm_set(struct TileMap *m, const u16 *k, int kl, Seg *seg, int only_if_absent) {
+    int i = tm_find(m, k, kl);
+    if (i >= 0) {
+        if (!only_if_absent) m->segs[i] = seg;
+        return;
+    }
+    if (m->n == m->cap) {
+        m->cap = m->cap ? m->cap * 2 : 4;
+        m->keys = (u16 **)realloc(m->keys, sizeof(u16 *) * (size_t)m->cap);
+        m->klens = (int *)realloc(m->klens, sizeof(int) * (size_t)m->cap);
+        m->segs = (Seg **)realloc(m->segs, sizeof(Seg *) * (size_t)m->cap);
+    }
+    m->keys[m->n] = (u16 *)malloc(sizeof(u16) * (size_t)(kl + 1));
+    memcpy(m->keys[m->n], k, sizeof(u16) * (size_t)kl);
+    m->klens[m->n] = kl;
+    m->segs[m->n++] = seg;
+}
+/* refHasTileLabels (mergeTree.ts:580-582): refType & Tile and a truthy properties[referenceTileLabels] */
+static const jv *tile_labels(const Seg *s) {
+    if (s->kind != SEG_MARKER || !(s->ref_type & 1) || !s->props) return NULL;
+    const jv *v = jv_obj_get_ascii(s->props, "referenceTileLabels");
+    return jv_truthy(v) ? v : NULL;
+}
+/* for (const label of labels): array elements (as object keys: String(element)) or the code
+   points of a string; anything else would throw */
+typedef void (*LabelFn)(void *ctx, const u16 *k, int kl, const jv *elem);
+static int each_label(const jv *v, LabelFn fn, void *ctx) {
+    if (v->kind == JV_ARR) {
+        for (int i = 0; i < v->n; i++) {
+            int kl;
+            u16 *k = js_key_of(v->vals[i], &kl);
+            fn(ctx, k, kl, v->vals[i]);
+            free(k);
+        }
+        return 1;
+    }
+    if (v->kind == JV_STR) {
+        for (int i = 0; i < v->slen;) {
+            int w = (v->s[i] >= 0xD800 && v->s[i] < 0xDC00 && i + 1 < v->slen && v->s[i + 1] >= 0xDC00 && v->s[i + 1] < 0xE000) ? 2 : 1;
+            fn(ctx, v->s + i, w, NULL);
+            i += w;
+        }
+        return 1;
+    }
+    return 0;
+}
+typedef struct {
+    Block *b;
+    Seg *seg;
+} AddTileCtx;
+static void add_tile_cb(void *vctx, const u16 *k, int kl, const jv *elem) {
+    (void)elem;
+    AddTileCtx *c = (AddTileCtx *)vctx;
+    tm_set(&c->b->rt, k, kl, c->seg, 0); /* addTile */
+    tm_set(&c->b->lt, k, kl, c->seg, 1); /* addTileIfNotPresent */
+}
+/* blockUpdate's rightmostTiles / leftmostTiles (mergeTree.ts:2751-2762 -> addNodeReferences) */
+static void block_update_tiles(Block *b) {
+    tm_clear(&b->rt);
+    tm_clear(&b->lt);
+    for (int i = 0; i < b->child_count; i++) {
+        Node *c = b->children[i];
+        if (c->is_leaf) {
+            Seg *sg = (Seg *)c;
+            if (local_net_length(sg) > 0 && sg->kind == SEG_MARKER && (sg->ref_type & 1)) {
+                const jv *labels = tile_labels(sg);
+                if (!labels) continue; /* getTileLabels() -> [] */
+                AddTileCtx ctx = {b, sg};
+                if (!each_label(labels, add_tile_cb, &ctx) && b->doc) b->doc->tile_bad = 1;
+            }
+        } else {
+            const Block *cb = (const Block *)c;
+            for (int j = 0; j < cb->rt.n; j++) tm_set(&b->rt, cb->rt.keys[j], cb->rt.klens[j], cb->rt.segs[j], 0);
+            for (int j = 0; j < cb->lt.n; j++) tm_set(&b->lt, cb->lt.keys[j], cb->lt.klens[j], cb->lt.segs[j], 1);
+        }
+    }
+}
+typedef struct {
+    const u16 *label;
+    int llen;
+    int hit;
+} HasLabelCtx;
+static void has_label_cb(void *vctx, const u16 *k, int kl, const jv *elem) {
+    HasLabelCtx *c = (HasLabelCtx *)vctx;
+    /* refHasTileLabel (mergeTree.ts:588-597): label === refLabel (a string element, or a code point) */
+    if (elem && elem->kind != JV_STR) return;
+    if (kl == c->llen && !memcmp(k, c->label, sizeof(u16) * (size_t)kl)) c->hit = 1;
+}
+static int seg_has_tile_label(mto_doc *d, const Seg *s, const u16 *label, int llen) {
+    const jv *labels = tile_labels(s);
+    if (!labels) return 0;
+    HasLabelCtx ctx = {label, llen, 0};
+    if (!each_label(labels, has_label_cb, &ctx)) d->tile_bad = 1;
+    return ctx.hit;
+}
+
+typedef struct {
+    const u16 *label;
+    int llen;
+    int preceding;
+    Seg *tile;
+} TileSearch;
+/* tileShift (mergeTree.ts:1012-1035) */
+static void tile_shift(mto_doc *d, Node *node, TileSearch *ts) {
+    if (node->is_leaf) {
+        Seg *sg = (Seg *)node;
+        if (local_net_length(sg) > 0 && sg->kind == SEG_MARKER && seg_has_tile_label(d, sg, ts->label, ts->llen))
+            ts->tile = sg;
+    } else {
+        const Block *b = (const Block *)node;
+        const struct TileMap *m = ts->preceding ? &b->rt : &b->lt;
+        int i = tm_find(m, ts->label, ts->llen);
+        if (i >= 0) ts->tile = m->segs[i];
+    }
+}
+/* recordTileStart (mergeTree.ts:998-1010) */
+static void record_tile_start(mto_doc *d, Seg *sg, TileSearch *ts) {
+    if (sg->kind == SEG_MARKER && seg_has_tile_label(d, sg, ts->label, ts->llen)) ts->tile = sg;
+}
+/* searchBlock (mergeTree.ts:1797-1829) with the local client's view (refSeq UniversalSequenceNumber) */
+static void search_block(mto_doc *d, Block *block, int pos, TileSearch *ts) {
+    for (int ci = 0; ci < block->child_count; ci++) {
+        Node *child = block->children[ci];
+        const int len = node_length(d, child, UNIVERSAL_SEQ, d->cw.client_id);
+        if (pos < len) {
+            if (!child->is_leaf) search_block(d, (Block *)child, pos, ts);
+            else record_tile_start(d, (Seg *)child, ts);
+            return;
+        }
+        tile_shift(d, child, ts);
+        pos -= len;
+    }
+}
+/* backwardSearchBlock (mergeTree.ts:1841-1874) */
+static void backward_search_block(mto_doc *d, Block *block, int pos, int seg_end, TileSearch *ts) {
+    for (int ci = block->child_count - 1; ci >= 0; ci--) {
+        Node *child = block->children[ci];
+        const int len = node_length(d, child, UNIVERSAL_SEQ, d->cw.client_id);
+        const int segpos = seg_end - len;
+        if (pos >= segpos) {
+            if (!child->is_leaf) backward_search_block(d, (Block *)child, pos, seg_end, ts);
+            else record_tile_start(d, (Seg *)child, ts);
+            return;
+        }
+        tile_shift(d, child, ts);
+        seg_end = segpos;
+    }
+}
+/* MergeTree.findTile (mergeTree.ts:1763-1789) for the local client (Client.findTile, client.ts:
+   1073-1076): the tile's position, or -1 when there is none; -2 when the document holds a tile
+   label list the reference could not iterate.  *props_json: the marker's properties (caller frees). */
+long mto_find_tile(mto_doc *d, int start_pos, const char *label_utf8, int preceding, char **props_json) {
+    if (props_json) *props_json = NULL;
+    int llen;
+    u16 *label = utf8_to_u16(label_utf8, &llen);
+    TileSearch ts = {label, llen, preceding, NULL};
+    if (preceding) {
+        search_block(d, d->root, start_pos, &ts);
+    } else {
+        const int len = d->root->n.cached_length; /* getLength(UniversalSequenceNumber, local client) */
+        if (start_pos <= len) backward_search_block(d, d->root, start_pos, len, &ts);
+    }
+    free(label);
+    if (d->tile_bad) return -2;
+    if (!ts.tile) return -1;
+    /* getPosition(marker, UniversalSequenceNumber, clientId) (mergeTree.ts:1586-1603) */
+    long pos = 0;
+    Node *node = &ts.tile->n;
+    for (Block *p = node->parent; p; node = &p->n, p = p->n.parent)
+        for (int i = 0; i < p->child_count && p->children[i] != node; i++)
+            pos += node_length(d, p->children[i], UNIVERSAL_SEQ, d->cw.client_id);
+    if (props_json && ts.tile->props) {
+        sb o;
+        sb_init(&o);
+        jv_stringify(ts.tile->props, &o);
+        sb_putc(&o, 0);
+        *props_json = o.p;
+    }
+    return pos;
+}
+
 /* ------------------------------------------------------------------ client */
 static int get_short_client_id(mto_doc *d, const char *long_id) {
     for (int i = 0; i < d->n_ids; i++)
@@ -1313,6 +1525,8 @@ void mto_free(mto_doc *d) {
     }
     for (Block *b = d->all_blocks; b;) {
         Block *n = b->all_next;
+        tm_free(&b->rt);
+        tm_free(&b->lt);
         free(b);
         b = n;
     }
@@ -2382,6 +2596,10 @@ static void dump_walk(mto_doc *d, const Block *b, sb *out, int depth) {
                 snprintf(t, sizeof t, "grp=%d ", s->sg_n);
                 sb_puts(out, t);
             }
+            if (s->kind == SEG_MARKER) {
+                snprintf(t, sizeof t, "rt=%d ", s->ref_type);
+                sb_puts(out, t);
+            }
             sb_putc(out, '\'');
             if (s->kind == SEG_TEXT) sb_put_u16_utf8(out, s->text, s->n.cached_length);
             sb_puts(out, "'");
@@ -2795,3 +3013,5 @@ double mto_replay_batch(const mt_op *ops, const int64_t *doc_op_off, long n_docs
     free(th);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+void mto_free_string(char *p) { free(p); }

@@ -77,6 +77,9 @@ def lib():
     L.mto_remove_local.argtypes = [vp, i, i]
     L.mto_local_op_json.argtypes = [vp, cp]
     L.mto_pending_groups.argtypes = [vp]
+    L.mto_find_tile.argtypes = [vp, i, cp, i, C.POINTER(C.c_void_p)]
+    L.mto_find_tile.restype = l
+    L.mto_free_string.argtypes = [vp]
     L.mto_get_length.argtypes = [vp]
     L.mto_view_length.argtypes = [vp, i, i]
     L.mto_current_seq.argtypes = [vp]
@@ -170,6 +173,21 @@ class Doc:
 
     def pending_groups(self) -> int:
         return self.L.mto_pending_groups(self.h)
+
+    def find_tile(self, start_pos: int, label: str, preceding: bool = True):
+        """MergeTree.findTile for the local client: None, or {"pos", "props"}; raises on a label
+        list the reference could not iterate."""
+        import json as _json
+
+        pj = C.c_void_p()
+        pos = self.L.mto_find_tile(self.h, start_pos, label.encode(), 1 if preceding else 0, C.byref(pj))
+        props = None
+        if pj.value:
+            props = _json.loads(C.string_at(pj.value).decode())
+            self.L.mto_free_string(pj)
+        if pos == -2:
+            raise ValueError("unsupported tile labels")
+        return None if pos < 0 else {"pos": pos, "props": props}
 
     def length(self) -> int:
         return self.L.mto_get_length(self.h)

@@ -118,3 +118,30 @@ def test_node_packer_combining_ops_byte_identical(tmp_path):
     assert np.frombuffer((tmp_path / "props.bin").read_bytes(), oplog.PROP_DTYPE).tobytes() == pb.props.tobytes()
     assert json.loads((tmp_path / "meta.json").read_text())["values"] == pb.values
 
+
+
+@pytest.mark.skipif(NODE is None, reason="node not available")
+def test_node_packer_writer_streams_byte_identical(tmp_path):
+    """Writer replicas' streams (local ops, acks): the Node packer == the Python packer."""
+    from writer_sim import farm as writer_farm
+
+    f = writer_farm(4, 400, 8, rewrite=20, markers=10)
+    docs = [[n, f.events[n]] for n in f.names]
+    src = tmp_path / "msgs.json"
+    src.write_text(json.dumps(docs))
+    code = ("const {Packer}=require('./fluidframework_amd/js');const fs=require('fs');"
+            f"const docs=JSON.parse(fs.readFileSync({json.dumps(str(src))},'utf8'));const p=new Packer();"
+            "for(const [n,d] of docs)p.addDocument(d,n);const r=p.finish();"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'ops.bin'))},r.ops);"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'props.bin'))},Buffer.from(r.props.buffer));"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'meta.json'))},JSON.stringify({{values:r.values,clients:r.clients}}));")
+    r = subprocess.run([NODE, "-e", code], capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    p = oplog.Packer()
+    for n, d in docs:
+        p.add_document(d, n)
+    pb = p.finish()
+    assert np.frombuffer((tmp_path / "ops.bin").read_bytes(), oplog.OP_DTYPE).tobytes() == pb.ops.tobytes()
+    assert np.frombuffer((tmp_path / "props.bin").read_bytes(), oplog.PROP_DTYPE).tobytes() == pb.props.tobytes()
+    meta = json.loads((tmp_path / "meta.json").read_text())
+    assert meta["values"] == pb.values and meta["clients"] == pb.clients

@@ -165,3 +165,57 @@ def test_observer_logs_still_run_the_observer_kernel():
         b.run()
         for d in range(4):
             assert b.doc(d).digest() == int(dig[d])
+
+
+def test_find_tile_kats_on_gpu():
+    """client.spec.ts:29-231 (findTile literal positions) on GPU replicas of local-only logs."""
+    def mk(label="EOP"):
+        return {"marker": {"refType": 1}, "props": {"referenceTileLabels": [label], "markerId": "some-id"}}
+
+    def local(ops):
+        return [{"clientId": "localUser", "sequenceNumber": -1, "referenceSequenceNumber": 0,
+                 "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 0, "pos1": p, "seg": s}}
+                for p, s in ops]
+
+    three = [(0, mk()), (0, "abc d"), (0, mk()), (7, "ef"), (8, mk())]
+    cases = [  # (ops, [(startPos, preceding, expected pos or None)])
+        ([(0, mk()), (0, "abc")], [(0, False, 3), (5, True, 3), (5, False, None)]),
+        ([(0, "abc d"), (0, mk())], [(0, False, 0)]),
+        (three, [(5, True, 0), (5, False, 6)]),
+        ([(0, mk())], [(0, True, 0), (0, False, 0)]),
+        ([(0, "abc")], [(1, True, None), (1, False, None)]),
+        ([(0, "x")], []),
+    ]
+    docs = [local(ops) for ops, _ in cases] + [[]]
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_messages(docs, observer="localUser")
+        b.run()
+        for i, (_, queries) in enumerate(cases):
+            for start, prec, want in queries:
+                got = b.doc(i).find_tile(start, "EOP", prec)
+                assert (None if got is None else got["pos"]) == want, (i, start, prec)
+        empty = b.doc(len(docs) - 1)
+        assert empty.find_tile(1, "EOP") is None and empty.find_tile(1, "EOP", False) is None
+
+
+@pytest.mark.parametrize("mk", [lambda: round_farm(4, 30, 31, markers=30), lambda: farm(5, 600, 32, markers=25)])
+def test_find_tile_matches_oracle(mk):
+    """Every replica (writers and observer) of farms with Tile markers: the GPU table's findTile
+    equals the oracle's block-map search at every position, both directions, every label."""
+    from writer_sim import TILE_LABELS
+
+    f = mk()
+    names = list(f.names)
+    docs = [f.events[n] for n in names]
+    obs_msgs = list(f.log)
+    with fa.ReplayBatch(len(docs) + 1) as b:
+        b.ingest_messages(docs + [obs_msgs], observer=names + ["readonly"])
+        b.run()
+        for i, od in enumerate([f.docs[n] for n in names] + [f.observer]):
+            dv = b.doc(i)
+            assert dv.digest() == od.digest()
+            n = od.length()
+            for label in TILE_LABELS:
+                for pos in range(0, n + 2):
+                    for prec in (True, False):
+                        assert dv.find_tile(pos, label, prec) == od.find_tile(pos, label, prec), (i, label, pos, prec)

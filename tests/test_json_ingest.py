@@ -121,10 +121,12 @@ def test_unsupported_and_malformed_logs_fail_with_the_document_index():
         assert e.value.code == MT_UNSUPPORTED
         with pytest.raises(oplog.UnsupportedOp):
             oplog.pack_documents([arr])
-    own = [_msg("readonly", 1, 0, {"type": 0, "pos1": 0, "seg": "a"})]
+    other_local = [_msg("A", -1, 0, {"type": 0, "pos1": 0, "seg": "a"})]  # an unsequenced op of another client
     with pytest.raises(MtError) as e:
-        PackedJson([json.dumps(own)])
+        PackedJson([json.dumps(other_local)])
     assert e.value.code == MT_UNSUPPORTED
+    with pytest.raises(oplog.UnsupportedOp):
+        oplog.pack_documents([other_local])
 
 
 def test_combining_ops_pack_identically():
@@ -158,3 +160,24 @@ def test_oracle_packed_combine_matches_json_replay():
         got = O.replay_doc(pb.ops[a:e].copy(), pb.text, pb.props, t, pb.clients[i])
         assert got.status == 0, got.error
         assert got.digest() == ref.digest() and got.props_runs() == ref.props_runs()
+
+
+def test_writer_streams_pack_identically():
+    """Writer replicas' streams (local ops as sequenceNumber -1, own messages as acks): the native
+    ingest ({"replica": id, "messages": [...]}) == the Python packer (add_document(msgs, id))."""
+    from writer_sim import farm
+
+    f = farm(4, 500, 3, rewrite=20, markers=10)
+    p = oplog.Packer()
+    for n in f.names:
+        p.add_document(f.events[n], n)
+    want = p.finish()
+    pj = PackedJson([json.dumps({"replica": n, "messages": f.events[n]}) for n in f.names], n_threads=2)
+    got = pj.arrays()
+    pj.close()
+    assert (got.doc_op_off == want.doc_op_off).all()
+    assert (got.ops == want.ops).all()
+    assert (got.text == want.text).all()
+    assert len(got.props) == len(want.props) and (got.props == want.props).all()
+    assert got.keys == want.keys and got.values == want.values and got.clients == want.clients
+    assert (got.ops["seq"] == -1).any()

@@ -20,7 +20,8 @@ ADDON = ROOT / "fluidframework_amd" / "js" / "mtreplay.node"
 pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node / N-API addon not available")
 
 FUNCS = {"createBatch", "setTables", "setClients", "ingest", "generate", "run", "runAsync", "docStatus", "docText",
-         "docPropsRuns", "docSnapshotV1", "docDigest", "deviceDigests", "stats", "statusString", "ingestJson"}
+         "docPropsRuns", "docSnapshotV1", "docDigest", "deviceDigests", "stats", "statusString", "ingestJson",
+         "docFindTile"}
 
 
 def _node(code):
@@ -80,3 +81,46 @@ def test_node_replay_matches_oracle(tmp_path, mode):
         assert g["runs"] == json.loads(od.props_runs())
         assert g["snapshot"] == od.snapshot_v1()
         assert int(g["digest"]) == od.digest()
+
+
+@pytest.mark.gpu
+def test_node_writer_replica_and_find_tile():
+    """The JS Client's local methods (insertTextLocal / insertMarkerLocal / removeRangeLocal) +
+    applyMsg acks, and findTile: client.spec.ts:75-151's three-tile document (preceding tile of 5 at
+    0, following at 6) and the issue-1213 writer ("Xc"), equal to the oracle's replicas."""
+    code = r"""
+const { ReplayBatch } = require('./fluidframework_amd/js');
+(async () => {
+  const b = new ReplayBatch(2);
+  const c = b.client(0);
+  c.startOrUpdateCollaboration('localUser');
+  const m = { referenceTileLabels: ['EOP'], markerId: 'some-id' };
+  c.insertMarkerLocal(0, 1, m); c.insertTextLocal(0, 'abc d'); c.insertMarkerLocal(0, 1, m);
+  c.insertTextLocal(7, 'ef'); c.insertMarkerLocal(8, 1, m);
+  const w = b.client(1);
+  w.startOrUpdateCollaboration('1');
+  const msg = (op, seq, cid, ref) => ({ clientId: cid, sequenceNumber: seq, referenceSequenceNumber: ref,
+                                        minimumSequenceNumber: 0, type: 'op', contents: op });
+  const op1 = w.insertTextLocal(0, 'a'), op2 = w.removeRangeLocal(0, 1);
+  w.applyMsg(msg(op1, 1, '1', 0)); w.applyMsg(msg(op2, 2, '1', 0));
+  const op4 = w.insertTextLocal(0, 'c');
+  w.applyMsg(msg({ type: 0, pos1: 0, seg: 'X' }, 3, '2', 0)); w.applyMsg(msg(op4, 4, '1', 2));
+  await b.runAsync();
+  process.stdout.write(JSON.stringify({
+    len: c.getText().length, prec: c.findTile(5, 'EOP'), next: c.findTile(5, 'EOP', false),
+    none: c.findTile(5, 'pg') === undefined, wtext: w.getText(), wdigest: w.digest().toString(),
+    cdigest: c.digest().toString() }));
+})().catch((e) => { console.error(e); process.exit(1); });
+"""
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    assert got["len"] == 10 and got["prec"]["pos"] == 0 and got["next"]["pos"] == 6 and got["none"]
+    assert got["prec"]["props"] == {"referenceTileLabels": ["EOP"], "markerId": "some-id"}
+    assert got["wtext"] == "Xc"
+    od = O.Doc()
+    od.start_collab("localUser")
+    mk = {"marker": {"refType": 1}, "props": {"referenceTileLabels": ["EOP"], "markerId": "some-id"}}
+    for pos, seg in ((0, mk), (0, "abc d"), (0, mk), (7, "ef"), (8, mk)):
+        od.local_op({"type": 0, "pos1": pos, "seg": seg})
+    assert int(got["cdigest"]) == od.digest()
