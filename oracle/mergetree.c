@@ -1835,6 +1835,162 @@ int mto_local_op_json(mto_doc *d, const char *op_json) {
 
 int mto_pending_groups(const mto_doc *d) { return d->pend_n; }
 
+static void seg_json(sb *out, int kind, const u16 *text, int len, int ref_type, const jv *props);
+/* ------------------------------------------------------------------ regeneratePendingOp */
+/* document order of every linked segment (the ordinal order resetPendingDeltaToOps sorts by) */
+typedef struct {
+    Seg **segs;
+    int n, cap;
+} SegList;
+static void collect_segs(Block *b, SegList *l) {
+    for (int i = 0; i < b->child_count; i++) {
+        Node *c = b->children[i];
+        if (!c->is_leaf) collect_segs((Block *)c, l);
+        else {
+            if (l->n == l->cap) {
+                l->cap = l->cap ? 2 * l->cap : 64;
+                l->segs = (Seg **)realloc(l->segs, sizeof(Seg *) * (size_t)l->cap);
+            }
+            l->segs[l->n++] = (Seg *)c;
+        }
+    }
+}
+static int seg_index(const SegList *l, const Seg *s) {
+    for (int i = 0; i < l->n; i++)
+        if (l->segs[i] == s) return i;
+    return -1;
+}
+/* Client.findReconnectionPostition (client.ts:674-706) */
+static int reconnection_position(const SegList *l, const Seg *seg, int local_seq) {
+    int pos = 0;
+    for (int i = 0; i < l->n && l->segs[i] != seg; i++) {
+        const Seg *s = l->segs[i];
+        const int inserted = s->local_seq == 0 || s->local_seq <= local_seq;
+        const int not_removed = !s->removed || (s->local_removed_seq != 0 && s->local_removed_seq > local_seq);
+        if (inserted && not_removed) pos += s->n.cached_length;
+    }
+    return pos;
+}
+/* Client.resetPendingDeltaToOps (client.ts:708-766): the oldest pending group regenerated against
+   the current tree, one op (and one new group, queued last) per segment; ops appended to `out` as
+   JSON (comma separated), returns how many */
+static int reset_pending_delta_to_ops(mto_doc *d, const jv *reset_op, sb *out, int n_prev) {
+    int type = -1;
+    if (!reset_op || reset_op->kind != JV_OBJ || !jv_int(jv_obj_get_ascii(reset_op, "type"), &type))
+        fail(d, MTO_BAD_INPUT, "regeneratePendingOp: bad op");
+    if (d->pend_n == 0) fail(d, MTO_BAD_INPUT, "regeneratePendingOp: no pending segment group");
+    Group *g = d->pend[d->pend_head++];
+    d->pend_n--;
+    SegList all = {NULL, 0, 0};
+    collect_segs(d->root, &all);
+    /* segmentGroup.segments.sort by ordinal (document order) */
+    int *ord = (int *)malloc(sizeof(int) * (size_t)(g->n + 1));
+    for (int i = 0; i < g->n; i++) ord[i] = seg_index(&all, g->segs[i]);
+    for (int i = 1; i < g->n; i++) { /* insertion sort of (index, seg) pairs */
+        int k = ord[i];
+        Seg *sk = g->segs[i];
+        int j = i - 1;
+        while (j >= 0 && ord[j] > k) {
+            ord[j + 1] = ord[j];
+            g->segs[j + 1] = g->segs[j];
+            j--;
+        }
+        ord[j + 1] = k;
+        g->segs[j + 1] = sk;
+    }
+    free(ord);
+    int n = n_prev;
+    for (int i = 0; i < g->n; i++) {
+        Seg *seg = g->segs[i];
+        if (seg_group_dequeue(seg) != g) fail(d, MTO_BAD_INPUT, "Segment group not at head of segment pending queue");
+        const int pos = reconnection_position(&all, seg, g->local_seq);
+        char t[96];
+        int made = 0;
+        switch (type) {
+            case 2: { /* createAnnotateRangeOp(pos, pos + len, props, combiningOp) */
+                if (n++) sb_putc(out, ',');
+                sb_puts(out, "{");
+                const jv *co = jv_obj_get_ascii(reset_op, "combiningOp");
+                if (co && co->kind != JV_UNDEF) {
+                    sb_puts(out, "\"combiningOp\":");
+                    jv_stringify(co, out);
+                    sb_putc(out, ',');
+                }
+                snprintf(t, sizeof t, "\"pos1\":%d,\"pos2\":%d,\"props\":", pos, pos + seg->n.cached_length);
+                sb_puts(out, t);
+                const jv *pr = jv_obj_get_ascii(reset_op, "props");
+                if (pr) jv_stringify(pr, out);
+                else sb_puts(out, "null");
+                sb_puts(out, ",\"type\":2}");
+                made = 1;
+                break;
+            }
+            case 0: /* createInsertSegmentOp(pos, segment) */
+                if (seg->seq != UNASSIGNED_SEQ) fail(d, MTO_BAD_INPUT, "regenerate: insert of a sequenced segment");
+                if (n++) sb_putc(out, ',');
+                snprintf(t, sizeof t, "{\"pos1\":%d,\"seg\":", pos);
+                sb_puts(out, t);
+                seg_json(out, seg->kind, seg->text, seg->n.cached_length, seg->ref_type, seg->props);
+                sb_puts(out, ",\"type\":0}");
+                made = 1;
+                break;
+            case 1: /* createRemoveRangeOp, only while the local remove is still pending */
+                if (seg->local_removed_seq != 0) {
+                    if (n++) sb_putc(out, ',');
+                    snprintf(t, sizeof t, "{\"pos1\":%d,\"pos2\":%d,\"type\":1}", pos, pos + seg->n.cached_length);
+                    sb_puts(out, t);
+                    made = 1;
+                }
+                break;
+            default: fail(d, MTO_BAD_INPUT, "Invalid op type");
+        }
+        if (made) { /* a new group of this segment alone, queued last (same localSeq) */
+            Group *ng = NULL;
+            ng = add_to_pending_list(d, seg, NULL, g->local_seq);
+            (void)ng;
+        }
+    }
+    free(all.segs);
+    return n;
+}
+/* Client.regeneratePendingOp(resetOp, segmentGroup) (client.ts:855-893) with segmentGroup = the
+   oldest pending group(s): the regenerated op as JSON (a GROUP when it is more than one op), in
+   *out_json (malloc'd) */
+int mto_regenerate_pending_op_json(mto_doc *d, const char *reset_op_json, char **out_json) {
+    *out_json = NULL;
+    GUARD(d);
+    jv *op = jv_parse(reset_op_json, strlen(reset_op_json));
+    if (!op) fail(d, MTO_BAD_INPUT, "op is not JSON");
+    sb ops;
+    sb_init(&ops);
+    int n = 0;
+    int type = -1;
+    jv_int(jv_obj_get_ascii(op, "type"), &type);
+    if (type == 3) {
+        const jv *members = jv_obj_get_ascii(op, "ops");
+        if (!members || members->kind != JV_ARR) fail(d, MTO_BAD_INPUT, "group without ops");
+        for (int i = 0; i < members->n; i++) n = reset_pending_delta_to_ops(d, members->vals[i], &ops, n);
+    } else {
+        n = reset_pending_delta_to_ops(d, op, &ops, 0);
+    }
+    sb res;
+    sb_init(&res);
+    if (n == 1) {
+        sb_putn(&res, ops.p, ops.n);
+    } else { /* createGroupOp(...opList) */
+        sb_puts(&res, "{\"ops\":[");
+        if (ops.n) sb_putn(&res, ops.p, ops.n);
+        sb_puts(&res, "],\"type\":3}");
+    }
+    sb_putc(&res, 0);
+    *out_json = res.p;
+    sb_free(&ops);
+    jv_unref(op);
+    UNGUARD(d);
+    return d->status;
+}
+
+
 int mto_apply_msg_json(mto_doc *d, const char *msg_json) {
     GUARD(d);
     jv *msg = jv_parse(msg_json, strlen(msg_json));

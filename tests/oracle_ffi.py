@@ -80,6 +80,7 @@ def lib():
     L.mto_find_tile.argtypes = [vp, i, cp, i, C.POINTER(C.c_void_p)]
     L.mto_find_tile.restype = l
     L.mto_free_string.argtypes = [vp]
+    L.mto_regenerate_pending_op_json.argtypes = [vp, cp, C.POINTER(C.c_void_p)]
     L.mto_get_length.argtypes = [vp]
     L.mto_view_length.argtypes = [vp, i, i]
     L.mto_current_seq.argtypes = [vp]
@@ -173,6 +174,19 @@ class Doc:
 
     def pending_groups(self) -> int:
         return self.L.mto_pending_groups(self.h)
+
+    def regenerate(self, op):
+        """Client.regeneratePendingOp(op, oldest pending group): the regenerated op (a dict)."""
+        import json as _json
+
+        out = C.c_void_p()
+        rc = self.L.mto_regenerate_pending_op_json(self.h, (op if isinstance(op, str) else _json.dumps(op)).encode(),
+                                                   C.byref(out))
+        if rc != 0:
+            raise RuntimeError(self.error)
+        r = _json.loads(C.string_at(out.value).decode())
+        self.L.mto_free_string(out)
+        return r
 
     def find_tile(self, start_pos: int, label: str, preceding: bool = True):
         """MergeTree.findTile for the local client: None, or {"pos", "props"}; raises on a label
