@@ -168,11 +168,19 @@ constexpr int kCapQueued = 7;      // checkpointed and taken by the launch's fol
 //   [kPendDesc ..) per group G & 63: {type | flags << 16, prop-record offset, prop count, 0}
 //   [kPendEntries ..) entries {G, slot} in append order (the group's `segments` array order:
 //   members as the op reached them, split-off halves appended when the split happens)
+//   word 4: collabWindow.localSeq (one per applied local op); a group's desc .w = its localSeq
 constexpr int kPendMaxGroups = 64;  // unacked local ops at once (more: MT_UNSUPPORTED)
 constexpr int kPendDesc = 8;
 constexpr int kPendEntries = kPendDesc + 4 * kPendMaxGroups;
 constexpr int kCapPending = 9;  // DocOut.cap_kind: the pending-entry region is full (terminal)
+constexpr int kCapRegen = 10;   // DocOut.cap_kind: the regenerated-op output region is full (terminal)
 constexpr int64_t pend_words(int32_t cap) { return kPendEntries + 2ll * cap; }
+// regenerated ops of MT_OP_REGENERATE records, per document (u32 words): [0] words used (from 2),
+// [1] records; per record {GROUP_CONT flag, ops} then per op {type, pos1, pos2, a, b, c, nprops, 0}
+// + nprops (key, value) pairs.  insert: a = 1 | refType << 1 for a Marker (else 0), b = text offset
+// in the document's payload, c = length, the pairs = its properties (nprops 0xFFFFFFFF: none);
+// annotate: a = flags, b / c = the reset op's prop records; remove: nothing more
+constexpr int kRegenOpWords = 8;
 
 // follow-on queue (one per producer launch, hipMalloc'd, zeroed): word 0 = documents enqueued,
 // 1 = items claimed by workers, 2 = producer workgroups finished, 3 = unused, 4 = a consumer's
@@ -292,6 +300,9 @@ struct ReplayParams {
     uint32_t *pend;
     const uint64_t *doc_pend_base;
     int32_t pend_cap;             // entries per document
+    uint32_t *regen;              // regenerated ops (kRegenOpWords layout), per document
+    const uint64_t *doc_regen_base;
+    int32_t regen_cap;            // words per document
 };
 constexpr uint32_t kIdUnlinked = 0xFFFFFFFFu;
 constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // RELPOS key the host cannot resolve safely

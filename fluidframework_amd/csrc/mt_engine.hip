@@ -193,6 +193,8 @@ struct Engine {
     // and its group count (kept in HBM word 0 as well, so checkpoints carry it)
     uint32_t *pend;
     int32_t pend_cap_e, n_pend;
+    uint32_t *regen;  // regenerated ops (mt_device.h kRegenOpWords), regen_cap words
+    int32_t regen_cap;
     int32_t htop;
     uint2 *h_ent;
     // ---- global
@@ -1071,9 +1073,10 @@ struct Engine {
                 return;
             }
             cur_g = (int32_t)(pend_word(1) + (uint32_t)n_pend);
+            const uint32_t lseq = pend_word(4);  // collabWindow.localSeq of this op
             if (lane == 0) {
                 *(uint4 *)(pend + kPendDesc + 4 * (cur_g & 63)) =
-                    make_uint4((uint32_t)op.type | ((uint32_t)op.flags << 16), op.payload, op.payload_len, 0u);
+                    make_uint4((uint32_t)op.type | ((uint32_t)op.flags << 16), op.payload, op.payload_len, lseq);
                 pend[0] = (uint32_t)(n_pend + 1);
             }
             n_pend++;
@@ -2426,6 +2429,10 @@ struct Engine {
             set_fail(ST_BAD_INPUT);
             return;
         }
+        if (op.type == MT_OP_REGENERATE) {
+            op_regenerate(op);
+            return;
+        }
         if (op.type == MT_OP_RELPOS || rel_pend ||
             (op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) != MT_COMBINE_NONE)) {
             set_fail(ST_UNSUPPORTED);  // relative positions / combiningOps in local ops: not modelled
@@ -2442,8 +2449,149 @@ struct Engine {
         op.ref_seq = cur_seq;
         cur_g = -1;
         ov_splits = -1;
+        if (lane == 0) pend[4] = pend_word(4) + 1u;  // ++collabWindow.localSeq (mergeTree.ts:1976, 2571, 2613)
         if (op.type == MT_OP_INSERT) insert_one<false>(op, 0u, (uint32_t)st, cur_seq);
         else op_range(op);
+    }
+
+    // Client.regeneratePendingOp(resetOp, oldest pending group) -> resetPendingDeltaToOps
+    // (client.ts:708-766): the group's segments in document order, each at its
+    // findReconnectionPostition (674-706: the length before it of the segments inserted and not
+    // removed as of the group's localSeq), get one op and one new group each (queued last, same
+    // localSeq); the ops are written to the document's regen region (mt_device.h kRegenOpWords).
+    MT_FI void op_regenerate(const mt_op &op) {
+        const uint32_t T = (uint32_t)op.ref_seq;
+        if (n_pend == 0 || T > MT_OP_ANNOTATE) {
+            set_fail(ST_BAD_INPUT);
+            return;
+        }
+        resolve_cold();
+        const uint32_t head = pend_word(1), gb = head & 63u;
+        const uint32_t L = rfl(pend[kPendDesc + 4 * gb + 3]);
+        if ((rfl(pend[kPendDesc + 4 * gb]) & 0xFFu) != T) {
+            set_fail(ST_BAD_INPUT);
+            return;
+        }
+        // the record header: GROUP_CONT of the reset op member, ops (filled in below)
+        uint32_t used = rfl(regen[0]);
+        if (used < 2u) used = 2u;
+        const uint32_t hdr = used;
+        if (used + 2u > (uint32_t)regen_cap) {
+            cap_fail(kCapRegen);
+            return;
+        }
+        used += 2u;
+        uint32_t nops = 0;
+        int32_t blk = root;
+        while (!b_leaf[blk]) blk = b_child[blk * 8];
+        uint32_t base = 0;
+        for (; blk >= 0 && !status; blk = next_leaf_block(blk)) {
+            const int32_t n = b_count[blk];
+            uint32_t slot = 0, meta = 0, len = 0, sr = 0;
+            uint64_t m = 0;
+            bool member = false;
+            uint32_t contrib = 0;
+            if (lane < n) {
+                slot = b_child[blk * 8 + lane];
+                meta = s_meta[slot];
+                len = s_len[slot];
+                sr = s_sr[slot];
+                // seg.localSeq / localRemovedSeq: the localSeq of its pending insert / remove group
+                uint32_t ins_l = 0xFFFFFFFFu, rem_l = 0xFFFFFFFFu;
+                if (meta & kMetaPending) {
+                    const uint4 q = cold[2 * slot + 1];
+                    m = (uint64_t)q.z | ((uint64_t)q.w << 32);
+                    member = (m >> gb) & 1ull;
+                    for (uint64_t mm = m; mm; mm &= mm - 1) {
+                        const uint32_t bi = (uint32_t)__builtin_ctzll(mm);
+                        const uint32_t t = pend[kPendDesc + 4 * bi] & 0xFFu, ls = pend[kPendDesc + 4 * bi + 3];
+                        if (t == MT_OP_INSERT) ins_l = ls;
+                        if (t == MT_OP_REMOVE) rem_l = ls;
+                    }
+                }
+                const bool pins = (sr & 0xFFFFu) == kSeq16Unassigned, prem = (sr >> 16) == kSeq16Unassigned;
+                const bool inserted = !pins || ins_l <= L;
+                const bool not_removed = !sr_removed(sr) || (prem && rem_l != 0xFFFFFFFFu && rem_l > L);
+                contrib = inserted && not_removed ? len : 0u;
+            }
+            const uint32_t incl = scan8(contrib) + base;
+            const uint32_t excl = incl - contrib;
+            base = rdl(incl, kMaxNodes - 1);
+            uint64_t mb = ballot(lane < n && member);
+            while (mb && !status) {
+                const int f = first_lane(mb);
+                mb &= mb - 1;
+                const uint32_t sl = rdl(slot, f), pos = rdl(excl, f), ln = rdl(len, f), sr_f = rdl(sr, f);
+                const uint32_t mt_f = rdl(meta, f);
+                const uint64_t mask = (uint64_t)rdl((uint32_t)m, f) | ((uint64_t)rdl((uint32_t)(m >> 32), f) << 32);
+                bool made = true;
+                uint32_t w[kRegenOpWords] = {T, pos, pos + ln, 0u, 0u, 0u, 0u, 0u};
+                uint32_t props = 0, np = 0;
+                if (T == MT_OP_INSERT) {
+                    if ((sr_f & 0xFFFFu) != kSeq16Unassigned) {  // assert(segment.seq === UnassignedSequenceNumber)
+                        set_fail(ST_BAD_INPUT);
+                        return;
+                    }
+                    const uint4 cr = cold[2 * sl];
+                    w[3] = (mt_f & kMetaMarker) ? (1u | (rfl(cr.z) << 1)) : 0u;
+                    w[4] = (mt_f & kMetaMarker) ? 0u : rfl(cr.z);
+                    w[5] = ln;
+                    props = (mt_f & kMetaHasProps) ? rfl(cr.x) : 0u;
+                    np = props ? pool[props] : 0xFFFFFFFFu;
+                    w[6] = np;
+                } else if (T == MT_OP_REMOVE) {
+                    made = (sr_f >> 16) == kSeq16Unassigned;  // only while the local remove is pending
+                } else {
+                    w[3] = op.flags;
+                    w[4] = op.payload;
+                    w[5] = op.payload_len;
+                }
+                uint64_t nm = mask & ~(1ull << gb);
+                if (made) {
+                    const uint32_t words = kRegenOpWords + (np != 0xFFFFFFFFu ? 2u * np : 0u);
+                    if (used + words > (uint32_t)regen_cap) {
+                        cap_fail(kCapRegen);
+                        return;
+                    }
+                    if (lane < kRegenOpWords) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int i = 0; i < kRegenOpWords; i++)
+                            if (lane == i) v = w[i];
+                        regen[used + lane] = v;
+                    }
+                    for (uint32_t i = lane; props && i < 2u * np; i += kWave) regen[used + kRegenOpWords + i] = pool[props + 2 + i];
+                    used += words;
+                    nops++;
+                    // the new group of this segment alone (same localSeq), queued last
+                    if (n_pend >= kPendMaxGroups) {
+                        set_fail(ST_UNSUPPORTED);
+                        return;
+                    }
+                    const uint32_t ng = head + (uint32_t)n_pend;
+                    if (lane == 0) {
+                        *(uint4 *)(pend + kPendDesc + 4 * (ng & 63u)) =
+                            make_uint4(T | ((uint32_t)op.flags << 16), op.payload, op.payload_len, L);
+                        pend[0] = (uint32_t)(n_pend + 1);
+                    }
+                    n_pend++;
+                    entry_append(ng, sl);
+                    if (status) return;
+                    nm |= 1ull << (ng & 63u);
+                }
+                pend_set_mask(sl, nm);
+            }
+        }
+        if (status) return;
+        if (lane == 0) {
+            regen[hdr] = op.flags & MT_OPF_GROUP_CONT;
+            regen[hdr + 1] = nops;
+            regen[0] = used;
+            regen[1] = regen[1] + 1u;
+            pend[0] = (uint32_t)(n_pend - 1);  // the reset group leaves the queue
+            pend[1] = head + 1u;
+        }
+        n_pend--;
     }
 
     MT_FI void apply(mt_op op) {
@@ -2791,6 +2939,8 @@ MT_FI void engine_setup(Engine<SEG, kW> &E, const ReplayParams &P, int64_t w, in
     if constexpr (kW) {
         E.pend = P.pend + P.doc_pend_base[d];
         E.pend_cap_e = P.pend_cap;
+        E.regen = P.regen + P.doc_regen_base[d];
+        E.regen_cap = P.regen_cap;
         E.n_pend = 0;
         E.cur_g = -1;
     }
@@ -2918,6 +3068,10 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
         pr[1] = 0u;
         pr[2] = 0u;
         pr[3] = 0u;
+        pr[4] = 0u;
+        uint32_t *rg = P.regen + P.doc_regen_base[d];
+        rg[0] = 2u;
+        rg[1] = 0u;
     }
     if constexpr (kW) E.n_pend = resumed ? (int32_t)E.pend_word(0) : 0;
     // follow-on producer: workgroups are dispatched in index order, so the last one starting

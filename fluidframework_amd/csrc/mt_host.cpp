@@ -375,6 +375,11 @@ struct mt_batch {
     // pending-group regions (mt_device.h pend_words)
     bool writer = false;
     int32_t pend_cap = 0;
+    int32_t regen_cap = 0;               // words per document of regenerated-op output
+    uint32_t *d_regen = nullptr;
+    uint64_t *d_regen_base = nullptr;
+    std::vector<mt_prop> h_props_all;    // the ingested prop records (regenerated annotates' props)
+    std::vector<uint64_t> h_regen_base;
     uint32_t *d_pend = nullptr;
     uint64_t *d_pend_base = nullptr;
     int64_t total_ops = 0, total_props = 0;
@@ -485,6 +490,10 @@ static void free_log(mt_batch *b) {
     (void)hipFree(b->d_pend_base);
     b->d_pend = nullptr;
     b->d_pend_base = nullptr;
+    (void)hipFree(b->d_regen);
+    (void)hipFree(b->d_regen_base);
+    b->d_regen = nullptr;
+    b->d_regen_base = nullptr;
     b->writer = false;
     b->d_ops = nullptr;
     b->d_off = nullptr;
@@ -857,6 +866,9 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
                 nprop_ops++;
                 prop_records += o.payload_len;
             }
+            if (o.type == MT_OP_REGENERATE && o.ref_seq == MT_OP_ANNOTATE &&
+                (int64_t)o.payload + (int64_t)o.payload_len > n_props)
+                return MT_ERR_ARG;
             if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
                 if (o.pos2 < 0 || (int64_t)o.pos2 + (int64_t)MT_OPF_NPROPS(o.flags) > n_props) return MT_ERR_ARG;
                 nprop_ops++;
@@ -934,6 +946,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     b->cached_doc = -1;
     b->c_blob_doc = -1;
     b->h_off = std::move(h_off);
+    b->h_props_all.assign(props, props + n_props);
     b->h_text_base = std::move(text_base);
     b->h_text_len = std::move(text_len);
     b->h_text_cap = std::move(text_cap);
@@ -974,6 +987,28 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         if (D > 0) HIPCHK(hipMemset(b->d_pend, 0, 4 * words * (uint64_t)D));
         HIPCHK(dalloc(&b->d_pend_base, (size_t)D + 1));
         HIPCHK(hipMemcpy(b->d_pend_base, pbase_.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+        // regenerated-op output (MT_OP_REGENERATE records): MT_REGEN_CAP words per document that
+        // has such records (default 16384), 2 for the others
+        const char *er = getenv("MT_REGEN_CAP");
+        const uint64_t rcap = er && atoi(er) > 0 ? (uint64_t)atoi(er) : 16384;
+        std::vector<uint64_t> rbase((size_t)D + 1, 0);
+        uint64_t rtot = 0;
+        for (int64_t d = 0; d < D; d++) {
+            rbase[(size_t)d] = rtot;
+            bool has = false;
+            for (int64_t i = b->h_off[(size_t)d]; i < b->h_off[(size_t)d + 1] && !has; i++)
+                has = ops[i].type == MT_OP_REGENERATE;
+            rtot += has ? rcap : 2;
+        }
+        rbase[(size_t)D] = rtot;
+        b->regen_cap = (int32_t)rcap;
+        HIPCHK(dalloc(&b->d_regen, (size_t)std::max<uint64_t>(rtot, 2)));
+        HIPCHK(hipMemset(b->d_regen, 0, 4 * std::max<uint64_t>(rtot, 2)));
+        HIPCHK(dalloc(&b->d_regen_base, (size_t)D + 1));
+        HIPCHK(hipMemcpy(b->d_regen_base, rbase.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+        // per-document caps differ (2 words without REGENERATE records): the device checks
+        // regen_cap only after a REGENERATE record, which only the large regions see
+        b->h_regen_base = std::move(rbase);
         b->writer = true;
     }
     HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));
@@ -1065,6 +1100,9 @@ static mt::ReplayParams base_params(mt_batch *b) {
     P.pend = b->d_pend;
     P.doc_pend_base = b->d_pend_base;
     P.pend_cap = b->pend_cap;
+    P.regen = b->d_regen;
+    P.doc_regen_base = b->d_regen_base;
+    P.regen_cap = b->regen_cap;
     return P;
 }
 
@@ -2016,6 +2054,106 @@ MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const c
     std::string pj;
     if (leaves[(size_t)found]->props) props_json(b, leaves[(size_t)found]->props, pj);
     return out_str(pj, props_buf, props_cap, props_len);
+}
+
+// JSON.stringify of a property object given as (key, value) records in insertion order (JS key
+// order: integer-like keys first, as props_json does for pool sets)
+static void pairs_json(mt_batch *b, const uint32_t *kv, uint32_t n, std::string &o) {
+    std::vector<std::pair<uint64_t, uint32_t>> order;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t k = kv[2 * i];
+        const uint64_t rank = (k < b->key_is_index.size() && b->key_is_index[k]) ? (uint64_t)b->key_index[k]
+                                                                              : (1ull << 32) + i;
+        order.push_back({rank, i});
+    }
+    std::sort(order.begin(), order.end());
+    o.push_back('{');
+    for (size_t j = 0; j < order.size(); j++) {
+        const uint32_t k = kv[2 * order[j].second], v = kv[2 * order[j].second + 1];
+        if (j) o.push_back(',');
+        json_quote8(o, k < b->keys.size() ? b->keys[k] : std::string("?"));
+        o.push_back(':');
+        o += v < b->values.size() ? b->values[v] : std::string("null");
+    }
+    o.push_back('}');
+}
+
+// Client.regeneratePendingOp results of the document's MT_OP_REGENERATE records, in order: a JSON
+// array with one element per regenerated message (records chained by MT_OPF_GROUP_CONT form one):
+// the op, or createGroupOp(...ops) when it is not exactly one (client.ts:885), keys in
+// opBuilder.ts order
+MT_API int mt_doc_regenerated_ops(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len) {
+    if (!b) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    std::string o = "[";
+    if (b->writer && !b->h_regen_base.empty()) {
+        const uint64_t a = b->h_regen_base[(size_t)doc], e = b->h_regen_base[(size_t)doc + 1];
+        std::vector<uint32_t> w((size_t)(e - a));
+        if (!w.empty())
+            HIPCHK(hipMemcpy(w.data(), b->d_regen + a, 4 * w.size(), hipMemcpyDeviceToHost));
+        const uint32_t used = w.size() >= 2 ? std::min<uint32_t>(w[0], (uint32_t)w.size()) : 0;
+        std::vector<std::string> msg_ops;
+        bool first_msg = true;
+        for (uint32_t p = 2; p + 2 <= used;) {
+            const uint32_t cont = w[p], nops = w[p + 1];
+            p += 2;
+            for (uint32_t k = 0; k < nops && p + mt::kRegenOpWords <= used; k++) {
+                const uint32_t *r = &w[p];
+                std::string j;
+                if (r[0] == MT_OP_INSERT) {
+                    j = "{\"pos1\":" + std::to_string(r[1]) + ",\"seg\":";
+                    const bool has_props = r[6] != 0xFFFFFFFFu;
+                    const uint32_t np = has_props ? r[6] : 0;
+                    std::string pj;
+                    if (has_props) pairs_json(b, r + mt::kRegenOpWords, np, pj);
+                    if (r[3] & 1u) {
+                        j += "{\"marker\":{\"refType\":" + std::to_string(r[3] >> 1) + "}";
+                        if (has_props) j += ",\"props\":" + pj;
+                        j += "}";
+                    } else {
+                        std::string t;
+                        if ((size_t)r[4] + r[5] <= b->c_text.size())
+                            json_quote16(t, b->c_text.data() + r[4], r[5]);
+                        j += has_props ? "{\"text\":" + t + ",\"props\":" + pj + "}" : t;
+                    }
+                    j += ",\"type\":0}";
+                    p += mt::kRegenOpWords + 2 * np;
+                } else if (r[0] == MT_OP_REMOVE) {
+                    j = "{\"pos1\":" + std::to_string(r[1]) + ",\"pos2\":" + std::to_string(r[2]) + ",\"type\":1}";
+                    p += mt::kRegenOpWords;
+                } else {
+                    j = "{";
+                    if (r[3] & MT_OPF_REWRITE) j += "\"combiningOp\":{\"name\":\"rewrite\"},";
+                    j += "\"pos1\":" + std::to_string(r[1]) + ",\"pos2\":" + std::to_string(r[2]) + ",\"props\":";
+                    std::vector<uint32_t> kv;
+                    for (uint32_t q = 0; q < r[5] && (size_t)r[4] + q < b->h_props_all.size(); q++) {
+                        kv.push_back(b->h_props_all[r[4] + q].key);
+                        kv.push_back(b->h_props_all[r[4] + q].value);
+                    }
+                    std::string pj;
+                    pairs_json(b, kv.data(), (uint32_t)(kv.size() / 2), pj);
+                    j += pj + ",\"type\":2}";
+                    p += mt::kRegenOpWords;
+                }
+                msg_ops.push_back(j);
+            }
+            if (!cont) {
+                if (!first_msg) o.push_back(',');
+                first_msg = false;
+                if (msg_ops.size() == 1) {
+                    o += msg_ops[0];
+                } else {
+                    o += "{\"ops\":[";
+                    for (size_t i = 0; i < msg_ops.size(); i++) o += (i ? "," : "") + msg_ops[i];
+                    o += "],\"type\":3}";
+                }
+                msg_ops.clear();
+            }
+        }
+    }
+    o.push_back(']');
+    return out_str(o, buf, cap, len);
 }
 
 // segment.toJSONObject() (textSegment.ts:48-54, mergeTree.ts:652-656)

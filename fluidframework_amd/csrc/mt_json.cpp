@@ -822,10 +822,12 @@ struct Packer1 {
             base.client = c;
             const int32_t sq = D.member(m, "sequenceNumber"), rs = D.member(m, "referenceSequenceNumber"),
                           ms = D.member(m, "minimumSequenceNumber");
-            if (sq < 0 || rs < 0 || ms < 0) return fail(MT_BAD_INPUT, "message without sequence numbers");
+            if (sq < 0) return fail(MT_BAD_INPUT, "message without sequence numbers");
             base.seq = as_int(D.nodes[sq]);
-            base.ref_seq = as_int(D.nodes[rs]);
-            base.msn = as_int(D.nodes[ms]);
+            // a local (unsequenced) message needs no refSeq / msn
+            if ((rs < 0 || ms < 0) && base.seq != -1) return fail(MT_BAD_INPUT, "message without sequence numbers");
+            base.ref_seq = rs >= 0 ? as_int(D.nodes[rs]) : 0;
+            base.msn = ms >= 0 ? as_int(D.nodes[ms]) : 0;
             base.type = MT_OP_NOOP;
             // a writer replica's own unsequenced message (sequenceNumber -1, UnassignedSequenceNumber)
             // is a local op; its sequenced ones ack them (client.ts:797-819; mt_oplog.h)
@@ -837,6 +839,44 @@ struct Packer1 {
             }
             const int32_t ty = D.member(m, "type");
             const bool is_op = ty >= 0 && D.nodes[ty].type == J_STR && D.str_of(ty) == u"op";
+            if (local && ty >= 0 && D.nodes[ty].type == J_STR && D.str_of(ty) == u"regenerate") {
+                // Client.regeneratePendingOp(contents, oldest pending group) on reconnect: one
+                // MT_OP_REGENERATE record per member of the reset op (mt_oplog.h)
+                std::vector<int32_t> members;
+                const int32_t contents = D.member(m, "contents");
+                if (contents >= 0) flatten(contents, members);
+                for (size_t j = 0; j < members.size(); j++) {
+                    mt_op r = base;
+                    const int32_t op = members[j];
+                    if (D.nodes[op].type != J_OBJ) return fail(MT_UNSUPPORTED, "op must be an object");
+                    const int32_t t = D.member(op, "type");
+                    const double tv = t >= 0 && D.nodes[t].type == J_NUM ? D.nodes[t].num : -1;
+                    if (tv != 0 && tv != 1 && tv != 2) return fail(MT_UNSUPPORTED, "regenerate of an op type");
+                    r.type = MT_OP_REGENERATE;
+                    r.ref_seq = (int32_t)tv;
+                    r.flags = 0;
+                    r.pos1 = r.pos2 = 0;
+                    r.payload = r.payload_len = 0;
+                    if (tv == 2) {
+                        const int32_t cop = D.member(op, "combiningOp");
+                        if (cop >= 0 && truthy(D.nodes[cop])) {
+                            const int32_t nm = D.nodes[cop].type == J_OBJ ? D.member(cop, "name") : -1;
+                            if (!(nm >= 0 && D.nodes[nm].type == J_STR && D.str_of(nm) == u"rewrite"))
+                                return fail(MT_UNSUPPORTED, "local combiningOp other than rewrite");
+                            r.flags |= MT_OPF_REWRITE;
+                        }
+                        const int32_t pr = D.member(op, "props");
+                        uint32_t off = 0, n = 0;
+                        if (pr < 0) return fail(MT_UNSUPPORTED, "props must be an object");
+                        if (!prop_records(pr, &off, &n)) return false;
+                        r.payload = off;
+                        r.payload_len = n;
+                    }
+                    if (j + 1 < members.size()) r.flags |= MT_OPF_GROUP_CONT;
+                    L.ops.push_back(r);
+                }
+                continue;
+            }
             if (!is_op) {
                 if (local) return fail(MT_UNSUPPORTED, "a local message that is not an op");
                 L.ops.push_back(base);
@@ -981,7 +1021,7 @@ MT_API int mt_pack_json(mt_packed **out, int64_t n_docs, const char *const *doc_
             if (MT_OP_IS_INSERT_LIKE(o.type)) {
                 if (!(o.flags & MT_OPF_MARKER)) o.payload += tbase;
                 if (o.flags & MT_OPF_HAS_PROPS) o.pos2 += (int32_t)pbase;
-            } else if (o.type == MT_OP_ANNOTATE) {
+            } else if (o.type == MT_OP_ANNOTATE || (o.type == MT_OP_REGENERATE && o.ref_seq == MT_OP_ANNOTATE)) {
                 o.payload += pbase;
             } else if (o.type == MT_OP_RELPOS) {  // relativePosN.id value ids
                 o.pos1 = (int32_t)vmap[(uint32_t)o.pos1];

@@ -34,6 +34,10 @@ export declare class ReplayClient {
     insertMarkerLocal(pos: number, refType: number, props?: Record<string, any>): object;
     removeRangeLocal(start: number, end: number): object;
     annotateRangeLocal(start: number, end: number, props: Record<string, any>, combiningOp?: { name: string }): object;
+    /** Client.regeneratePendingOp(resetOp, oldest pending group) on reconnect (client.ts:855-893). */
+    regeneratePendingOp(resetOp: object): void;
+    /** the regenerated ops of every regeneratePendingOp call, in order (after run()). */
+    regeneratedOps(): object[];
     /** Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076) on the final state. */
     findTile(startPos: number, tileLabel: string, preceding?: boolean): { pos: number; props?: Record<string, any> } | undefined;
     /** 0 = OK, else the MT_* status of the Error applyMsg would have thrown. */

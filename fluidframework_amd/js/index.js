@@ -28,7 +28,7 @@ function native() {
     return addon;
 }
 
-const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 15;
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_REGENERATE = 7, OP_NOOP = 15;
 const OPF_GROUP_CONT = 1, OPF_MARKER = 2, OPF_HAS_PROPS = 4, OPF_REWRITE = 8;
 const OP_RELPOS = 6, RELF_POS1 = 0x10, RELF_POS2 = 0x20, RELF_BEFORE1 = 0x40, RELF_BEFORE2 = 0x80, RELF_OFF1 = 0x100, RELF_OFF2 = 0x200;
 const COMBINE_INCR = 1, COMBINE_CONSENSUS = 2, COMBINE_OTHER = 3, KEY_COMBINE = 0xFFFFFFFF, VALUE_UNDEFINED = 0xFFFFFFFF;
@@ -182,6 +182,25 @@ class Packer {
             if (local && c !== 0) throw new UnsupportedOp('an unsequenced message of another client');
             const base = { client: c, seq: msg.sequenceNumber, refSeq: msg.referenceSequenceNumber || 0, msn: local ? 0 : msg.minimumSequenceNumber };
             const noop = Object.assign({}, base, { type: OP_NOOP, flags: 0, pos1: 0, pos2: 0, payload: 0, payloadLen: 0 });
+            if (local && msg.type === 'regenerate') {
+                // Client.regeneratePendingOp(contents, oldest pending group) on reconnect: one
+                // MT_OP_REGENERATE record per member of the reset op (include/mt_oplog.h)
+                const members = Packer.flatten(msg.contents);
+                members.forEach((op, j) => {
+                    const r = Object.assign({}, base, { type: OP_REGENERATE, refSeq: op.type, flags: 0, pos1: 0, pos2: 0, payload: 0, payloadLen: 0 });
+                    if (op.type === OP_ANNOTATE) {
+                        const cop = op.combiningOp;
+                        if (cop) {
+                            if (cop.name !== 'rewrite') throw new UnsupportedOp('local combiningOp other than rewrite');
+                            r.flags |= OPF_REWRITE;
+                        }
+                        [r.payload, r.payloadLen] = this.propRecords(op.props);
+                    } else if (op.type !== OP_INSERT && op.type !== OP_REMOVE) throw new UnsupportedOp(`regenerate of op type ${op.type}`);
+                    if (j + 1 < members.length) r.flags |= OPF_GROUP_CONT;
+                    recs.push(r);
+                });
+                continue;
+            }
             if (msg.type !== 'op') {
                 if (local) throw new UnsupportedOp('a local message that is not an op');
                 recs.push(noop);
@@ -263,6 +282,13 @@ class ReplayClient {
         if (combiningOp) op.combiningOp = combiningOp;
         return this.localOp(op);
     }
+    // Client.regeneratePendingOp(resetOp, ...) on reconnect (client.ts:855-893): queued; the
+    // regenerated ops come back from regeneratedOps() after run()
+    regeneratePendingOp(resetOp) {
+        this.batch.queued = true;
+        this.messages.push({ clientId: this.longClientId, sequenceNumber: -1, type: 'regenerate', contents: resetOp });
+    }
+    regeneratedOps() { return JSON.parse(native().docRegeneratedOps(this.batch.h, this.index)); }
     // Client.findTile(startPos, tileLabel, preceding = true) (client.ts:1073-1076) on the final state
     findTile(startPos, tileLabel, preceding = true) {
         const r = native().docFindTile(this.batch.h, this.index, startPos, tileLabel, preceding);

@@ -303,6 +303,9 @@ napi_value string_out(napi_env env, napi_callback_info info,
     return r;
 }
 napi_value doc_text(napi_env env, napi_callback_info info) { return string_out(env, info, mt_doc_text, "mt_doc_text"); }
+napi_value doc_regenerated_ops(napi_env env, napi_callback_info info) {
+    return string_out(env, info, mt_doc_regenerated_ops, "mt_doc_regenerated_ops");
+}
 napi_value doc_props_runs(napi_env env, napi_callback_info info) {
     return string_out(env, info, mt_doc_props_runs, "mt_doc_props_runs");
 }
@@ -427,6 +430,7 @@ napi_value init(napi_env env, napi_value exports) {
         {"docSnapshotV1", nullptr, doc_snapshot, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docDigest", nullptr, doc_digest, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docFindTile", nullptr, doc_find_tile, nullptr, nullptr, nullptr, kMethod, nullptr},
+        {"docRegeneratedOps", nullptr, doc_regenerated_ops, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"deviceDigests", nullptr, device_digests, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"stats", nullptr, stats, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"statusString", nullptr, status_string, nullptr, nullptr, nullptr, kMethod, nullptr},

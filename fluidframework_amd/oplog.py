@@ -38,7 +38,7 @@ OP_DTYPE = np.dtype(
 PROP_DTYPE = np.dtype([("key", "<u4"), ("value", "<u4")])
 assert OP_DTYPE.itemsize == 32
 
-OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_RELPOS, OP_NOOP = 0, 1, 2, 6, 15
+OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_RELPOS, OP_REGENERATE, OP_NOOP = 0, 1, 2, 6, 7, 15
 UNASSIGNED_SEQ = -1  # UnassignedSequenceNumber (merge-tree/src/constants.ts:11): a local, unacked op
 # MT_OP_RELPOS flags (include/mt_oplog.h mt_relpos_flags)
 RELF_POS1, RELF_POS2, RELF_BEFORE1, RELF_BEFORE2, RELF_OFF1, RELF_OFF2 = 0x10, 0x20, 0x40, 0x80, 0x100, 0x200
@@ -233,6 +233,26 @@ class Packer:
                 raise UnsupportedOp("an unsequenced message of another client")
             base = dict(client=c, seq=seq, ref_seq=msg.get("referenceSequenceNumber", 0),
                         msn=0 if local else msg["minimumSequenceNumber"])
+            if local and msg.get("type") == "regenerate":
+                # Client.regeneratePendingOp(contents, oldest pending group) on reconnect: one
+                # MT_OP_REGENERATE record per member of the reset op (include/mt_oplog.h)
+                members = self._flatten(msg["contents"])
+                for j, op in enumerate(members):
+                    t = op.get("type")
+                    r = dict(base, type=OP_REGENERATE, ref_seq=t, flags=0, pos1=0, pos2=0, payload=0, payload_len=0)
+                    if t == 2:
+                        cop = op.get("combiningOp")
+                        if js_truthy(cop):
+                            if not (isinstance(cop, dict) and cop.get("name") == "rewrite"):
+                                raise UnsupportedOp("local combiningOp other than rewrite")
+                            r["flags"] |= OPF_REWRITE
+                        r["payload"], r["payload_len"] = self._prop_records(op.get("props"))
+                    elif t not in (0, 1):
+                        raise UnsupportedOp(f"regenerate of op type {t}")
+                    if j + 1 < len(members):
+                        r["flags"] |= OPF_GROUP_CONT
+                    recs.append(r)
+                continue
             if msg.get("type") != "op":
                 if local:
                     raise UnsupportedOp("a local message that is not an op")

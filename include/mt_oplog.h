@@ -52,6 +52,13 @@ enum mt_op_type {
                1942-1966).  pos1 / pos2 = value id of relativePosN.id (0: none), payload /
                payload_len = offsetN (int32), flags = MT_RELF_*. */
     MT_OP_RELPOS = 6,
+    /* REGENERATE  a writer replica's Client.regeneratePendingOp(resetOp, oldest pending group)
+                   (client.ts:708-766, 855-893) on reconnect: seq -1, client 0, ref_seq = the reset
+                   op's type (insert / remove / annotate), flags / payload / payload_len = its
+                   flags and prop records (annotate); a GROUP reset op is one record per member,
+                   MT_OPF_GROUP_CONT on all but the last.  The regenerated ops are an output
+                   (mt_doc_regenerated_ops); their sequenced messages later ack the new groups. */
+    MT_OP_REGENERATE = 7,
     MT_OP_NOOP = 15     /* non-"op" message: only client registration + updateSeqNumbers */
 };
 enum mt_relpos_flags {
@@ -67,6 +74,11 @@ enum mt_relpos_flags {
 #define MT_MAX_CLIENTS 254      /* short ids 0 .. 253 per document (0 = the observer)          */
 #define MT_SEQ_NONE 0x7FFFFFFF
 #define MT_OP_IS_INSERT_LIKE(t) ((t) == MT_OP_INSERT || (t) == MT_OP_LOAD_HEADER || (t) == MT_OP_LOAD_BODY)
+
+/* Writer replicas (the local-client path): a record with seq == -1 (UnassignedSequenceNumber) is
+   a local op of the replica (client 0), applied in its local view and kept pending; a sequenced
+   record of client 0 acks the oldest pending group (client.ts:797-819, mergeTree.ts:1893-1929). */
+#define MT_SEQ_LOCAL (-1)
 
 /* mt_op.flags: bits 0-3 public flags, bits 4-13 the prop count of an insert (<= 1023),
    bits 14-15 are internal to the library (set at ingest: the insert's text contains a '\n' /

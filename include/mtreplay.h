@@ -172,6 +172,10 @@ MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, i
    would be stale) or holds a label list other than an array of strings. */
 MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const char *label_utf8, int32_t preceding,
                             int64_t *tile_pos, char *props_buf, int64_t props_cap, int64_t *props_len);
+/* Client.regeneratePendingOp results (client.ts:855-893) of the document's MT_OP_REGENERATE
+   records (a writer replica reconnecting), in order: a JSON array of the regenerated ops, one per
+   reset message (a GROUP op when it regenerates to more or fewer than one op) */
+MT_API int mt_doc_regenerated_ops(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
 MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs);
 MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name, int64_t name_cap, char *buf,
                                 int64_t cap, int64_t *len);

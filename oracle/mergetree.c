@@ -162,6 +162,10 @@ struct mto_doc {
     Group **pend;
     int pend_head, pend_n, pend_cap;
     Group *all_groups;
+    /* regeneratePendingOp outputs (JSON ops): the current reset message's ops, and every finished
+       message's op (or group op), comma separated */
+    sb regen_cur, regen_all;
+    int regen_cur_n, regen_all_n;
 };
 
 /* ------------------------------------------------------------------ errors */
@@ -1537,6 +1541,8 @@ void mto_free(mto_doc *d) {
         g = n;
     }
     free(d->pend);
+    sb_free(&d->regen_cur);
+    sb_free(&d->regen_all);
     for (int i = 0; i < d->n_ids; i++) free(d->long_ids[i]);
     free(d->long_ids);
     for (int i = 0; i < d->n_ids_map; i++) free(d->id_keys[i]);
@@ -1834,6 +1840,17 @@ int mto_local_op_json(mto_doc *d, const char *op_json) {
 }
 
 int mto_pending_groups(const mto_doc *d) { return d->pend_n; }
+static long copy_out(const sb *s, char *buf, long cap);
+long mto_regenerated_ops(mto_doc *d, char *buf, long cap) {
+    sb o;
+    sb_init(&o);
+    sb_putc(&o, '[');
+    if (d->regen_all.n) sb_putn(&o, d->regen_all.p, d->regen_all.n);
+    sb_putc(&o, ']');
+    long n = copy_out(&o, buf, cap);
+    sb_free(&o);
+    return n;
+}
 
 static void seg_json(sb *out, int kind, const u16 *text, int len, int ref_type, const jv *props);
 /* ------------------------------------------------------------------ regeneratePendingOp */
@@ -1953,6 +1970,16 @@ static int reset_pending_delta_to_ops(mto_doc *d, const jv *reset_op, sb *out, i
     free(all.segs);
     return n;
 }
+/* regeneratePendingOp's result: the op, or createGroupOp(...opList) (client.ts:885) */
+static void wrap_regenerated(sb *res, const sb *ops, int n) {
+    if (n == 1) {
+        sb_putn(res, ops->p, ops->n);
+    } else {
+        sb_puts(res, "{\"ops\":[");
+        if (ops->n) sb_putn(res, ops->p, ops->n);
+        sb_puts(res, "],\"type\":3}");
+    }
+}
 /* Client.regeneratePendingOp(resetOp, segmentGroup) (client.ts:855-893) with segmentGroup = the
    oldest pending group(s): the regenerated op as JSON (a GROUP when it is more than one op), in
    *out_json (malloc'd) */
@@ -1975,13 +2002,9 @@ int mto_regenerate_pending_op_json(mto_doc *d, const char *reset_op_json, char *
     }
     sb res;
     sb_init(&res);
-    if (n == 1) {
-        sb_putn(&res, ops.p, ops.n);
-    } else { /* createGroupOp(...opList) */
-        sb_puts(&res, "{\"ops\":[");
-        if (ops.n) sb_putn(&res, ops.p, ops.n);
-        sb_puts(&res, "],\"type\":3}");
-    }
+    wrap_regenerated(&res, &ops, n);
+    if (d->regen_all_n++) sb_putc(&d->regen_all, ',');
+    sb_putn(&d->regen_all, res.p, res.n);
     sb_putc(&res, 0);
     *out_json = res.p;
     sb_free(&ops);
@@ -2870,6 +2893,27 @@ static void apply_local_packed(mto_doc *d, const mt_op *op, const uint16_t *text
             break;
         }
         case MT_OP_RELPOS: fail(d, MTO_UNSUPPORTED, "relative positions in a local op"); break;
+        case MT_OP_REGENERATE: { /* regeneratePendingOp of one reset op (member) */
+            jv *reset = jv_new(JV_OBJ);
+            jv_obj_set_ascii(reset, "type", jv_new_num(op->ref_seq));
+            if (op->ref_seq == MT_OP_ANNOTATE) {
+                if (bits & MT_OPF_REWRITE) {
+                    jv *co = jv_new(JV_OBJ);
+                    jv_obj_set_ascii(co, "name", jv_new_str_ascii("rewrite"));
+                    jv_obj_set_ascii(reset, "combiningOp", co);
+                }
+                jv_obj_set_ascii(reset, "props", props_from_records(d, props + op->payload, op->payload_len, t));
+            }
+            d->regen_cur_n = reset_pending_delta_to_ops(d, reset, &d->regen_cur, d->regen_cur_n);
+            jv_unref(reset);
+            if (!(bits & MT_OPF_GROUP_CONT)) {
+                if (d->regen_all_n++) sb_putc(&d->regen_all, ',');
+                wrap_regenerated(&d->regen_all, &d->regen_cur, d->regen_cur_n);
+                d->regen_cur.n = 0;
+                d->regen_cur_n = 0;
+            }
+            break;
+        }
         default: fail(d, MTO_BAD_INPUT, "local op type %d", op->type);
     }
 }

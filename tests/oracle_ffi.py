@@ -81,6 +81,8 @@ def lib():
     L.mto_find_tile.restype = l
     L.mto_free_string.argtypes = [vp]
     L.mto_regenerate_pending_op_json.argtypes = [vp, cp, C.POINTER(C.c_void_p)]
+    L.mto_regenerated_ops.argtypes = [vp, C.c_char_p, l]
+    L.mto_regenerated_ops.restype = l
     L.mto_get_length.argtypes = [vp]
     L.mto_view_length.argtypes = [vp, i, i]
     L.mto_current_seq.argtypes = [vp]
@@ -187,6 +189,11 @@ class Doc:
         r = _json.loads(C.string_at(out.value).decode())
         self.L.mto_free_string(out)
         return r
+
+    def regenerated_ops(self) -> list:
+        import json as _json
+
+        return _json.loads(_read(self.L.mto_regenerated_ops, self.h))
 
     def find_tile(self, start_pos: int, label: str, preceding: bool = True):
         """MergeTree.findTile for the local client: None, or {"pos", "props"}; raises on a label

@@ -38,7 +38,9 @@ def oracle_replica(name, events, initial=""):
         d.insert_local(0, json.dumps(initial))
     d.start_collab(name)
     for m in events:
-        if m["sequenceNumber"] == -1:
+        if m.get("type") == "regenerate":
+            d.regenerate(m["contents"])
+        elif m["sequenceNumber"] == -1:
             assert d.local_op(m["contents"]) == 0
         elif d.apply_msg(json.dumps(m)) != 0:
             break
@@ -219,3 +221,66 @@ def test_find_tile_matches_oracle(mk):
                 for pos in range(0, n + 2):
                     for prec in (True, False):
                         assert dv.find_tile(pos, label, prec) == od.find_tile(pos, label, prec), (i, label, pos, prec)
+
+
+def test_regenerate_pending_ops_on_gpu():
+    """Reconnecting writers (client.reconnectFarm.spec.ts's schedule): each regeneratePendingOp on
+    the GPU gives the oracle's regenerated ops, and every replica (incl. the one that regenerated
+    and was then acked through its new groups) equals the oracle's."""
+    from test_oracle_regenerate import reconnect_farm
+
+    for n_clients, seed in ((2, 1), (4, 2), (8, 3)):
+        names, docs, _, events = reconnect_farm(n_clients, 3, seed)
+        with fa.ReplayBatch(len(names)) as b:
+            b.ingest_messages([events[n] for n in names], observer=names)
+            b.run()
+            for i, n in enumerate(names):
+                assert_same(b.doc(i), docs[n], n)
+                assert b.doc(i).regenerated_ops() == docs[n].regenerated_ops(), n
+
+
+def test_reset_pending_segments_to_op_kats_on_gpu():
+    """resetPendingSegmentsToOp.spec.ts:46-125 as writer streams: regenerated inserts / removes /
+    annotates, acked through the new groups (pending counts pinned on the oracle)."""
+    def local(op):
+        return {"clientId": "local user", "sequenceNumber": -1, "referenceSequenceNumber": 0,
+                "minimumSequenceNumber": 0, "type": "op", "contents": op}
+
+    def regen(op):
+        return {"clientId": "local user", "sequenceNumber": -1, "type": "regenerate", "contents": op}
+
+    inserts = [{"pos1": i, "seg": "hello", "type": 0} for i in range(5)]
+    streams = []
+    # nacked insertSegment: every insert regenerated, then the regenerated ops acked
+    ev = [local(o) for o in inserts] + [regen(o) for o in inserts]
+    streams.append(ev)
+    # nacked insertSegment and removeRange / annotateRange
+    for extra in ({"pos1": 0, "pos2": 25, "type": 1}, {"pos1": 0, "pos2": 25, "props": {"foo": "bar"}, "type": 2}):
+        streams.append([local(o) for o in inserts] + [local(extra)] + [regen(o) for o in inserts + [extra]])
+    # replay each stream on the oracle to learn the regenerated ops, then ack them in order
+    full = []
+    for ev in streams:
+        od = oracle_replica("local user", ev)
+        seq = 0
+        acks = []
+        for op in od.regenerated_ops():
+            seq += 1
+            acks.append({"clientId": "local user", "sequenceNumber": seq, "referenceSequenceNumber": 0,
+                         "minimumSequenceNumber": 0, "type": "op", "contents": op})
+        full.append(ev + acks)
+    with fa.ReplayBatch(len(full)) as b:
+        b.ingest_messages(full, observer="local user")
+        b.run()
+        for i, ev in enumerate(full):
+            od = O.Doc()
+            od.start_collab("local user")
+            for e in ev:
+                if e.get("type") == "regenerate":
+                    od.regenerate(e["contents"])
+                elif e["sequenceNumber"] == -1:
+                    assert od.local_op(e["contents"]) == 0
+                else:
+                    assert od.apply_msg(json.dumps(e)) == 0, od.error
+            assert od.pending_groups() == 0
+            assert_same(b.doc(i), od, f"stream {i}")
+            assert b.doc(i).regenerated_ops() == od.regenerated_ops()

@@ -181,3 +181,19 @@ def test_writer_streams_pack_identically():
     assert len(got.props) == len(want.props) and (got.props == want.props).all()
     assert got.keys == want.keys and got.values == want.values and got.clients == want.clients
     assert (got.ops["seq"] == -1).any()
+
+
+def test_reconnect_streams_pack_identically():
+    """Regenerate events (a reconnecting writer's regeneratePendingOp calls) pack the same natively."""
+    from test_oracle_regenerate import reconnect_farm
+
+    names, _, _, events = reconnect_farm(4, 3, 7)
+    p = oplog.Packer()
+    for n in names:
+        p.add_document(events[n], n)
+    want = p.finish()
+    pj = PackedJson([json.dumps({"replica": n, "messages": events[n]}) for n in names])
+    got = pj.arrays()
+    pj.close()
+    assert (got.ops == want.ops).all() and (got.props == want.props).all() and got.values == want.values
+    assert (got.ops["type"] == oplog.OP_REGENERATE).any()

@@ -166,3 +166,25 @@ def test_reconnect_farm_converges(n_clients, seed):
     for n in names:
         assert docs[n].pending_groups() == 0
         assert docs[n].text() == obs.text(), n
+
+
+def test_packed_reconnect_streams_replay_like_the_json_ones():
+    """A reconnecting writer's stream packed by oplog (MT_OP_REGENERATE records) rebuilds the same
+    replica and the same regenerated ops on the oracle's packed path."""
+    from fluidframework_amd import oplog
+
+    names, docs, _, events = reconnect_farm(4, 3, 7)
+    r = names[1]
+    assert any(e.get("type") == "regenerate" for e in events[r])
+    p = oplog.Packer()
+    for n in names:
+        p.add_document(events[n], n)
+    pb = p.finish()
+    t = O.Tables(pb.keys or ["_"], pb.values)
+    for i, n in enumerate(names):
+        recs = pb.ops[pb.doc_op_off[i]:pb.doc_op_off[i + 1]].copy()
+        d = O.replay_doc(recs, pb.text, pb.props, t, pb.clients[i])
+        assert d.status == 0, d.error
+        assert d.digest() == docs[n].digest() and d.dump() == docs[n].dump()
+        assert d.regenerated_ops() == docs[n].regenerated_ops()
+    assert len(docs[r].regenerated_ops()) > 0
