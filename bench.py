@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seg-cap", type=int, default=0, help="first capacity class (default: from the op count)")
     ap.add_argument("--snapshot", action="store_true", help="serialize SnapshotV1 of every doc in each step")
+    ap.add_argument("--writers", action="store_true",
+                    help="replay every document as one of its writers (local ops + acks, the local-client path)")
     return ap.parse_args()
 
 
@@ -118,6 +120,8 @@ def main():
         counts = None
         total_ops_step = n_ops * n_docs * world
 
+    import numpy as np
+
     b = fa.ReplayBatch(n_docs, seg_cap=args.seg_cap)
     t0 = time.time()
     if sizes is not None:
@@ -126,10 +130,31 @@ def main():
         b.generate(p, doc_first)  # synthesize this rank's logs on the GPU (untimed)
     gen_s = time.time() - t0
     log(rank, f"generated {n_docs} docs, {int(b.stats()['n_ops'])} ops in {gen_s:.1f} s")
+    if args.writers:
+        # writer replicas of the same logs: document d is replayed as its writer 1 + d % C
+        # (oplog.writer_records: local copies of its ops + its own messages as acks) on
+        # mt_writer_kernel_<SEG>; the metric still counts the sequenced ops of the log
+        from fluidframework_amd import oplog
+        from fluidframework_amd.mtreplay import GEN_KEYS, GEN_VALUES, gen_client_names
+
+        t0 = time.time()
+        ops, off, text, props = b.download_log()
+        b.close()
+        wof = 1 + np.arange(n_docs) % cfg["n_clients"]
+        wops, woff = oplog.writer_records(ops, off, wof)
+        base = gen_client_names(cfg["n_clients"])
+        b = fa.ReplayBatch(n_docs, seg_cap=args.seg_cap)
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        for d in range(n_docs):
+            nm = list(base)
+            nm[0], nm[int(wof[d])] = nm[int(wof[d])], nm[0]
+            b.set_clients(nm, d)
+        b.ingest(wops, woff, text, props)
+        n_local = len(wops) - len(ops)
+        log(rank, f"writer logs: {len(wops)} records ({n_local} local ops) in {time.time() - t0:.1f} s")
     stream = torch.cuda.current_stream().cuda_stream
 
     with_snap = args.snapshot or cfg.get("snapshot", False)
-    import numpy as np
 
     dig_t = torch.empty(n_docs, dtype=torch.int64, device="cuda")
     snap_t = torch.empty(n_docs, dtype=torch.int64, device="cuda") if with_snap else None
@@ -172,6 +197,8 @@ def main():
     t_max = elapsed
     st = b.stats()
     ops_done = int(st["ops_applied"])  # ops applied per step on this rank (same every step)
+    if args.writers:  # the metric counts the log's sequenced messages, not the writers' local copies
+        ops_done -= n_local
     ops_all = ops_done
     if world > 1:
         dev = "cuda" if backend == "nccl" else "cpu"
@@ -206,12 +233,12 @@ def main():
     avg_first_ms = sum(first_ms) / len(first_ms)
     first_bytes = alg_bytes * (sum(first_ops) / len(first_ops)) / max(1, ops_done)
     achieved_gbs = first_bytes / (avg_first_ms * 1e-3) / 1e9
-    kname = f"mt_replay_kernel_{dom_class}"
+    kname = f"mt_{'writer' if args.writers else 'replay'}_kernel_{dom_class}"
     traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, kname)
     lds = lds_roofline(args.config, n_docs, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
     cpu = None
     parity = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu and not args.writers:  # (writer logs: parity is tests/test_gpu_writer.py)
         cpu, parity = cpu_baseline(b, fa, n_docs, args)
     snapshot = None
     if with_snap:
@@ -238,7 +265,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (GPU-generated conflict-farm logs, include/mt_gen.h)",
-            "config": {"workload": cfg["workload"], "docs_per_gpu": n_docs,
+            "config": {"workload": ("writer replicas (local ops + acks) of " if args.writers else "") + cfg["workload"],
+                       "docs_per_gpu": n_docs,
                        "ops_per_doc": n_ops if sizes is None else {"min": int(sizes.min()), "max": int(sizes.max()),
                                                                   "lpt_loads": loads},
                        "clients": cfg["n_clients"], "max_lag": cfg["max_lag"],

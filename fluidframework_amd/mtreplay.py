@@ -90,6 +90,16 @@ class BatchStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+# the generator's key / value / client tables (include/mt_gen.h MT_GEN_N_KEYS, MT_GEN_N_VALUES)
+GEN_KEYS = ["bold", "italic", "color", "size"]
+GEN_VALUES = ["null", "true", '"red"', '"green"', '"blue"'] + [str(v) for v in range(8, 25)]
+
+
+def gen_client_names(n_clients: int) -> list:
+    """short id 0 = the observer "readonly", 1.. = "A", "B", .. (mt_gen.h)"""
+    return ["readonly"] + [chr(ord("A") + i) for i in range(n_clients)]
+
+
 def gen_params(n_ops, n_clients=8, max_lag=32, pct_insert=60, pct_remove=40, min_len=4, max_insert=8,
                pct_newline=2, seed=0xDEADBEEF) -> GenParams:
     return GenParams(n_ops, n_clients, max_lag, pct_insert, pct_remove, min_len, max_insert, pct_newline, seed)

@@ -397,3 +397,41 @@ def pack_documents(docs, observer: str = "readonly") -> PackedBatch:
     for msgs in docs:
         p.add_document(msgs)
     return p.finish()
+
+
+def writer_records(ops: np.ndarray, off: np.ndarray, writer_of: np.ndarray):
+    """Writer replicas of observer logs whose messages are single records with contiguous seqs
+    1..N per document (the generator's, include/mt_gen.h): document d is replayed as its client
+    writer_of[d] (>= 1) saw it.  That writer's op k (seq s_k, refSeq r_k) was issued right after it
+    processed message r_k, in the view (r_k, writer) — the same segments its local view held — so
+    each of its records gets a local copy (seq -1, client 0, the writer's own unsequenced message)
+    placed after record r_k, and the original stays as the ack.  Short ids: the writer becomes 0,
+    the observer (0, which sends nothing) takes the writer's old id.  Vectorized over the batch;
+    returns (ops, off): per-document client tables are the observer's with 0 and writer_of[d]
+    swapped."""
+    ops = np.asarray(ops)
+    off = np.asarray(off, np.int64)
+    D = len(off) - 1
+    counts = np.diff(off)
+    doc = np.repeat(np.arange(D, dtype=np.int64), counts)
+    idx = np.arange(len(ops), dtype=np.int64) - off[doc]
+    w = np.asarray(writer_of, np.int64)[doc]
+    client = ops["client"].astype(np.int64)
+    mine = client == w
+    orig = ops.copy()
+    orig["client"] = np.where(mine, 0, np.where(client == 0, w, client)).astype(np.uint8)
+    loc = ops[mine].copy()
+    loc["seq"] = -1
+    loc["client"] = 0
+    loc["msn"] = 0
+    # order inside a document: original record i at 2i, a local copy with refSeq r at 2r - 1 (right
+    # after the record with seq r, i.e. index r - 1); copies with the same refSeq in issue order
+    key = np.concatenate([2 * idx, 2 * ops["ref_seq"][mine].astype(np.int64) - 1])
+    tie = np.concatenate([idx, idx[mine]])
+    dd = np.concatenate([doc, doc[mine]])
+    allr = np.concatenate([orig, loc])
+    order = np.lexsort((tie, key, dd))
+    new_counts = counts + np.bincount(doc[mine], minlength=D)
+    new_off = np.zeros(D + 1, np.int64)
+    np.cumsum(new_counts, out=new_off[1:])
+    return allr[order], new_off

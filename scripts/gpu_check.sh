@@ -37,6 +37,11 @@ for step in "$@"; do
     benchsnap) run benchsnap 600 python -u bench.py --snapshot --steps 3 --warmup 1 --no-cpu ;;
     bench5) run bench5 900 python -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
     profsnap) run profsnap 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profsnap -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 2 --warmup 1 --no-cpu ;;
+    benchw2) run benchw2 600 python -u bench.py --config 2 --writers --steps 3 --warmup 1 ;;
+    benchw3) run benchw3 900 python -u bench.py --config 3 --docs 8192 --writers --steps 2 --warmup 1 ;;
+    bench2o) run bench2o 600 python -u bench.py --config 2 --steps 3 --warmup 1 --no-cpu ;;
+    bench3s) run bench3s 900 python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
+    writertests) run writertests 600 python -u -m pytest tests/test_gpu_writer.py tests/test_node_host.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     bench4s) run bench4s 600 python -u bench.py --config 4 --docs 4096 --ops 20000 --steps 1 --warmup 0 --no-cpu ;;
     bench4) run bench4 1100 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     loadtests) run loadtests 300 python -u -m pytest tests/test_gpu_snapshot_load.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;

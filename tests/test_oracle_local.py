@@ -361,3 +361,25 @@ def test_packed_writer_streams_replay_like_the_json_ones():
         d = O.replay_doc(recs, pb.text, pb.props, t, pb.clients[i])
         assert d.status == 0, d.error
         assert d.digest() == f.docs[n].digest() and d.dump() == f.docs[n].dump()
+
+
+def test_vectorized_writer_records_equal_writer_log():
+    """oplog.writer_records (the bench's batch transform) == writer_log, record for record."""
+    from fluidframework_amd import oplog
+
+    p = O.gen_params(600, pct_insert=55, pct_remove=35, seed=0xAB)
+    ops, text, props, off = O.gen_batch(p, 6)
+    names = O.gen_client_names(p.n_clients)
+    wof = np.array([1 + d % p.n_clients for d in range(6)])
+    got, goff = oplog.writer_records(ops, off, wof)
+    for d in range(6):
+        recs, _ = writer_log(ops[off[d]:off[d + 1]], names, int(wof[d]))
+        mine = got[goff[d]:goff[d + 1]]
+        # writer_log keeps client names by remapping; writer_records swaps 0 and w
+        w = int(wof[d])
+        exp = recs.copy()
+        order = [w] + [c for c in range(len(names)) if c != w]
+        back = {new: old for new, old in enumerate(order)}
+        exp_client = np.array([0 if back[int(c)] == w else (w if back[int(c)] == 0 else back[int(c)]) for c in exp["client"]])
+        exp["client"] = exp_client
+        assert mine.tobytes() == exp.tobytes(), d
