@@ -130,6 +130,7 @@ def main():
         b.generate(p, doc_first)  # synthesize this rank's logs on the GPU (untimed)
     gen_s = time.time() - t0
     log(rank, f"generated {n_docs} docs, {int(b.stats()['n_ops'])} ops in {gen_s:.1f} s")
+    writer_log = None
     if args.writers:
         # writer replicas of the same logs: document d is replayed as its writer 1 + d % C
         # (oplog.writer_records: local copies of its ops + its own messages as acks) on
@@ -151,6 +152,7 @@ def main():
             b.set_clients(nm, d)
         b.ingest(wops, woff, text, props)
         n_local = len(wops) - len(ops)
+        writer_log = (wops, woff, text, props, wof, base)
         log(rank, f"writer logs: {len(wops)} records ({n_local} local ops) in {time.time() - t0:.1f} s")
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -215,10 +217,11 @@ def main():
     cnt = b.counters()
     capacity = {f: [int(np.percentile(cnt[f], q)) for q in (50, 99, 100)]
                 for f in ("max_slots", "max_unsettled", "max_blocks", "max_heap")}
-    all_ok, digest_xor, snap_xor = 0, None, None
+    all_ok, not_ok, digest_xor, snap_xor = 0, None, None, None
     if rank == 0:
         all_dig, all_st = gathered[:2]
         all_ok = int((all_st == 0).all())
+        not_ok = int((all_st != 0).sum())
         digest_xor = f"{int(np.bitwise_xor.reduce(all_dig)):016x}"
         if with_snap:
             snap_xor = f"{int(np.bitwise_xor.reduce(gathered[2])):016x}"
@@ -238,8 +241,8 @@ def main():
     lds = lds_roofline(args.config, n_docs, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
     cpu = None
     parity = None
-    if rank == 0 and not args.no_cpu and not args.writers:  # (writer logs: parity is tests/test_gpu_writer.py)
-        cpu, parity = cpu_baseline(b, fa, n_docs, args)
+    if rank == 0 and not args.no_cpu:
+        cpu, parity = cpu_baseline(b, fa, n_docs, args, writer_log)
     snapshot = None
     if with_snap:
         avg_snap = sum(snap_ms) / len(snap_ms)
@@ -289,6 +292,10 @@ def main():
             "parity": parity,
             "snapshot": snapshot,
             "docs_ok": all_ok,
+            # writer replicas can stop where the reference's would (a remote insert beside the
+            # replica's own unacked removes: the #1213 family, "MergeTree insert failed");
+            # parity.digest_match compares statuses too
+            "docs_not_ok": not_ok,
             "digests_gathered": len(gathered[0]) if rank == 0 else None,
             "digest_xor": digest_xor,
             "snapshot_digest_xor": snap_xor,
@@ -351,10 +358,12 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(b, fa, n_docs, args):
+def cpu_baseline(b, fa, n_docs, args, writer=None):
     """Oracle (CPU restatement, tests-only code) on a bounded sample of the same logs, timed on
-    every usable host core (one pthread per core); its per-doc digests double as a parity check
-    of every sampled document.  Sample: the first documents of this rank's batch up to ~8.2M ops."""
+    every usable host core (one pthread per core); its per-doc digests and statuses double as a
+    parity check of every sampled document.  Sample: the first documents of this rank's batch up to
+    ~8.2M ops.  writer = (records, offsets, text, props, writer_of, client names) of --writers: the
+    oracle replays the same writer replicas (one sub-batch per writer id, its client table)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import numpy as np
 
@@ -366,18 +375,36 @@ def cpu_baseline(b, fa, n_docs, args):
         csum = np.cumsum(b.counters()["ops_done"].astype(np.int64))
         sample = int(np.searchsorted(csum, 4096 * 2000, side="left")) + 1
         sample = min(n_docs, max(16, sample))
-    sops, soff, text, props = b.download_log(0, sample)
     threads = args.cpu_threads or usable_cores()
-    tables, names = O.gen_tables(), O.gen_client_names(8)
-    secs, dig, st = O.replay_batch(sops, soff, text, props, tables, names, n_threads=threads)
+    tables = O.gen_tables()
+    if writer is None:
+        sops, soff, text, props = b.download_log(0, sample)
+        secs, dig, st = O.replay_batch(sops, soff, text, props, tables, O.gen_client_names(8), n_threads=threads)
+        n_ops = int(soff[-1])
+    else:
+        wops, woff, text, props, wof, base = writer
+        dig, st = np.zeros(sample, np.uint64), np.zeros(sample, np.int32)
+        secs, n_ops = 0.0, 0
+        for w in sorted(set(int(x) for x in wof[:sample])):
+            idx = np.nonzero(wof[:sample] == w)[0]
+            parts = [wops[woff[d]:woff[d + 1]] for d in idx]
+            soff = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+            nm = list(base)
+            nm[0], nm[w] = nm[w], nm[0]
+            s, dg, sg = O.replay_batch(np.concatenate(parts), soff, text, props, tables, nm, n_threads=threads)
+            secs += s
+            dig[idx], st[idx] = dg, sg
+            n_ops += int(soff[-1])
     gpu_dig = np.array([b.doc(d).digest() for d in range(sample)], np.uint64)
-    match = int((gpu_dig == dig).sum())
-    n_ops = int(soff[-1])
+    gpu_st = b.counters()["status"][:sample]
+    match = int(((gpu_dig == dig) & (gpu_st == st)).sum())
     cpu = {"value": round(n_ops / secs, 1), "unit": "ops/s", "cores": threads, "kind": "port",
            "sample": f"first {sample} docs ({n_ops} ops) of the same log, oracle/ C restatement, {threads} threads "
                      f"(usable cores; os.cpu_count()={os.cpu_count()}), CPU: {cpu_model()}",
            "seconds": round(secs, 3)}
     parity = {"docs_checked": sample, "digest_match": match, "oracle_status_ok": int((st == 0).sum())}
+    if writer is not None:  # records: local copies + sequenced messages
+        cpu["sample"] = "writer replicas: " + cpu["sample"].replace(" ops)", " records)")
     return cpu, parity
 
 

@@ -41,7 +41,7 @@ for step in "$@"; do
     benchw3) run benchw3 900 python -u bench.py --config 3 --docs 8192 --writers --steps 2 --warmup 1 ;;
     bench2o) run bench2o 600 python -u bench.py --config 2 --steps 3 --warmup 1 --no-cpu ;;
     bench3s) run bench3s 900 python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
-    writertests) run writertests 600 python -u -m pytest tests/test_gpu_writer.py tests/test_node_host.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    writertests) run writertests 600 python -u -m pytest tests/test_gpu_writer.py tests/test_node_host.py -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     bench4s) run bench4s 600 python -u bench.py --config 4 --docs 4096 --ops 20000 --steps 1 --warmup 0 --no-cpu ;;
     bench4) run bench4 1100 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     loadtests) run loadtests 300 python -u -m pytest tests/test_gpu_snapshot_load.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;

@@ -30,11 +30,10 @@ def oracle_replica(name, events, initial):
 def main():
     a = [int(x) for x in sys.argv[1:]] if len(sys.argv) > 1 else [1, 3, 400, 0, 0]
     seed, n_clients, steps, rewrite, wi = a
-    initial = "hello world" if seed % 2 else ""
+    initial = ""  # a message stream carries no pre-collaboration text
     f = farm(n_clients, steps, seed, initial=initial, rewrite=rewrite)
     name = f.names[wi]
     ev = f.events[name]
-    init = [] if not initial else []
     print(f"writer {name}: {len(ev)} events; oracle status {f.docs[name].status} {f.docs[name].error}")
     docs = [ev[:L] for L in range(1, len(ev) + 1)]
     with fa.ReplayBatch(len(docs)) as b:
