@@ -19,6 +19,10 @@ from .mtreplay import (  # noqa: F401
     DocView,
     GenParams,
     MtError,
+    NotOnGpuPath,
+    PackedJson,
+    PackedJsonGpu,
+    json_concat,
     ReplayBatch,
     gen_params,
     lib,

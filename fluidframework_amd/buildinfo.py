@@ -10,7 +10,8 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 SRC = [PKG / "csrc" / "mt_host.cpp", PKG / "csrc" / "mt_engine.hip", PKG / "csrc" / "mt_kernels.hip",
        PKG / "csrc" / "mt_device.h", PKG / "csrc" / "mt_digest.hip", PKG / "csrc" / "mt_snapshot.hip",
-       PKG / "csrc" / "mt_json.cpp", PKG / "csrc" / "mt_values.cpp", ROOT / "include" / "mtreplay.h",
+       PKG / "csrc" / "mt_json.cpp", PKG / "csrc" / "mt_values.cpp", PKG / "csrc" / "mt_json_gpu.hip",
+       PKG / "csrc" / "mt_json_gpu.h", ROOT / "include" / "mtreplay.h",
        ROOT / "include" / "mt_oplog.h", ROOT / "include" / "mt_gen.h"]
 MARKER = b"MTBUILDID:"
 

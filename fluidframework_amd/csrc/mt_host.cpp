@@ -24,6 +24,7 @@
 
 #include "../../include/mtreplay.h"
 #include "mt_device.h"
+#include "mt_json_gpu.h"
 #include "mt_values.h"
 
 // kernels of each capacity class (mt_kernels.hip compiled with -DMT_SEG=<seg>)
@@ -1024,6 +1025,196 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
                          hipMemcpyHostToDevice));
     b->have_log = true;
     b->generated = false;
+    return MT_OK;
+}
+
+static void json_gpu_stats(const mt::jg::Result &r, double ms_total, mt_json_gpu_stats *st) {
+    if (!st) return;
+    *st = mt_json_gpu_stats{};
+    st->ms_scan = r.ms_scan;
+    st->ms_count = r.ms_count;
+    st->ms_clients = r.ms_clients;
+    st->ms_write = r.ms_write;
+    st->ms_props = r.ms_props;
+    st->ms_host = r.ms_host;
+    st->ms_total = ms_total;
+    st->n_msgs = r.n_msgs;
+    st->n_ops = r.n_ops;
+    st->n_text = r.n_text;
+    st->n_props = r.n_props;
+    st->fail_bits = r.fail_bits;
+}
+
+MT_API int mt_pack_json_gpu(mt_packed **out, int64_t n_docs, const char *json, const int64_t *doc_off,
+                            const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats) {
+    if (!out || n_docs < 0 || !doc_off || (n_docs && !json)) return MT_ERR_ARG;
+    *out = nullptr;
+    if (bad_doc) *bad_doc = -1;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MT_ERR_NO_DEVICE;
+    const auto t0 = std::chrono::steady_clock::now();
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    mt::jg::Result r;
+    mt_op *d_ops = nullptr;
+    uint16_t *d_text = nullptr;
+    mt_prop *d_props = nullptr;
+    uint64_t words = 0;
+    int rc = mt::jg::parse(json, doc_off, n_docs, nullptr, observer, s, nullptr, &d_ops, &d_text, &words, &d_props, r);
+    std::vector<mt_op> ops;
+    std::vector<uint16_t> text;
+    std::vector<mt_prop> props;
+    if (rc == MT_OK) {
+        ops.resize((size_t)r.n_ops);
+        text.resize((size_t)r.n_text);
+        props.resize((size_t)r.n_props);
+        if (hipMemcpy(ops.data(), d_ops, sizeof(mt_op) * ops.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(text.data(), d_text, 2 * text.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(props.data(), d_props, sizeof(mt_prop) * props.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = MT_ERR_HIP;
+    }
+    (void)hipFree(d_ops);
+    (void)hipFree(d_text);
+    (void)hipFree(d_props);
+    (void)hipStreamDestroy(s);
+    if (bad_doc) *bad_doc = r.bad_doc;
+    json_gpu_stats(r, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                   stats);
+    if (rc != MT_OK) return rc;
+    *out = mt_packed_from(std::move(ops), std::move(r.doc_op_off), std::move(text), std::move(props),
+                          std::move(r.keys), std::move(r.values), std::move(r.clients));
+    return MT_OK;
+}
+
+// GPU parse straight into the replay's layout: per-document text arenas (payloads document-
+// relative, the '\n' flags set), the same host metadata as mt_batch_ingest for a log of the
+// observer fast path (no LOAD / RELPOS / REGENERATE records, markers, combiningOps or local ops)
+MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, const void *d_json,
+                                    const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats) {
+    if (!b || !doc_off || (b->n_docs && !json)) return MT_ERR_ARG;
+    if (bad_doc) *bad_doc = -1;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t D = b->n_docs;
+    std::vector<uint32_t> text_len((size_t)D), text_cap((size_t)D);
+    mt::jg::TextLayout layout = [&](const mt::jg::Result &r, std::vector<uint64_t> &base, uint64_t &words) -> int {
+        uint64_t tb = 0;
+        for (int64_t d = 0; d < D; d++) {
+            const uint64_t pay = r.doc_text[(size_t)d];
+            const uint64_t cap = (uint64_t)align16u(pay) + (uint64_t)b->opt.arena_factor * pay + 4096;
+            if (cap > 0xFFFFFFF0ull) return MT_ERR_ARG;
+            base[(size_t)d] = tb;
+            text_len[(size_t)d] = (uint32_t)pay;
+            text_cap[(size_t)d] = (uint32_t)cap;
+            tb += align16u(cap);
+        }
+        words = tb;
+        return MT_OK;
+    };
+    mt::jg::Result r;
+    mt_op *d_ops = nullptr;
+    uint16_t *d_text = nullptr;
+    mt_prop *d_props = nullptr;
+    uint64_t words = 0;
+    int rc = mt::jg::parse(json, doc_off, D, (const uint8_t *)d_json, observer, b->stream, &layout, &d_ops, &d_text,
+                           &words, &d_props, r);
+    auto drop = [&]() {
+        (void)hipFree(d_ops);
+        (void)hipFree(d_text);
+        (void)hipFree(d_props);
+    };
+    if (bad_doc) *bad_doc = r.bad_doc;
+    if (rc != MT_OK) {
+        drop();
+        json_gpu_stats(r, 0, stats);
+        return rc;
+    }
+    std::vector<mt_prop> h_props((size_t)r.n_props);
+    if (!h_props.empty() &&
+        hipMemcpy(h_props.data(), d_props, sizeof(mt_prop) * h_props.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+        drop();
+        return MT_ERR_HIP;
+    }
+    // tables (as mt_batch_ingest_packed)
+    std::vector<const char *> kp, vp;
+    for (const auto &k : r.keys) kp.push_back(k.c_str());
+    for (const auto &v : r.values) vp.push_back(v.c_str());
+    static const char *none = "_";
+    rc = mt_batch_set_tables(b, kp.empty() ? &none : kp.data(), kp.empty() ? 1 : (int32_t)kp.size(), vp.data(),
+                             (int32_t)vp.size());
+    bool shared = true;
+    for (int64_t d = 1; d < D && shared; d++) shared = r.clients[(size_t)d] == r.clients[0];
+    auto set = [&](int64_t doc, const std::vector<std::string> &names) {
+        std::vector<const char *> np;
+        for (const auto &n : names) np.push_back(n.c_str());
+        return mt_batch_set_clients(b, doc, np.data(), (int32_t)np.size());
+    };
+    if (!rc && D && shared) rc = set(-1, r.clients[0]);
+    for (int64_t d = 0; !rc && !shared && d < D; d++) rc = set(d, r.clients[(size_t)d]);
+    if (rc) {
+        drop();
+        return rc;
+    }
+    // the parsed log replaces the previous one (mt_batch_ingest's fields for this log shape)
+    free_launches(b);
+    free_log(b);
+    b->ran = false;
+    b->cached_doc = -1;
+    b->c_blob_doc = -1;
+    std::vector<uint64_t> text_base((size_t)D), pool_base((size_t)D);
+    std::vector<uint32_t> pool_cap((size_t)D);
+    uint64_t tb = 0, pb = 0;
+    int32_t max_ops = 0;
+    for (int64_t d = 0; d < D; d++) {
+        text_base[(size_t)d] = tb;
+        tb += align16u(text_cap[(size_t)d]);
+        const uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * r.doc_nprop_ops[(size_t)d];
+        pool_base[(size_t)d] = pb;
+        pool_cap[(size_t)d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
+        pb += align16u(pc);
+        max_ops = std::max<int32_t>(max_ops, (int32_t)(r.doc_op_off[(size_t)d + 1] - r.doc_op_off[(size_t)d]));
+    }
+    const int64_t N = r.n_ops;
+    b->h_off = r.doc_op_off;
+    b->h_props_all = std::move(h_props);
+    b->h_text_base = text_base;
+    b->h_text_len = text_len;
+    b->h_text_cap = text_cap;
+    b->h_pool_base = pool_base;
+    b->h_pool_cap = pool_cap;
+    b->h_nload.assign((size_t)D, 0);
+    b->h_nload_segs.assign((size_t)D, 0);
+    b->h_tile_annot.assign((size_t)D, 0);
+    b->payload_units = (double)r.n_text;
+    b->prop_records = (double)r.n_props;
+    b->text_words = tb;
+    b->pool_words = pb;
+    b->total_ops = N;
+    b->total_props = r.n_props;
+    b->max_ops_per_doc = max_ops;
+    b->d_ops = d_ops;
+    b->d_text = d_text;
+    b->d_props = d_props;
+    std::vector<uint64_t> idmap_base((size_t)D + 1, 0);
+    HIPCHK(dalloc(&b->d_off, (size_t)D + 1));
+    HIPCHK(dalloc(&b->d_text_base, (size_t)D));
+    HIPCHK(dalloc(&b->d_text_len, (size_t)D));
+    HIPCHK(dalloc(&b->d_text_cap, (size_t)D));
+    HIPCHK(dalloc(&b->d_pool, (size_t)pb));
+    HIPCHK(dalloc(&b->d_pool_base, (size_t)D));
+    HIPCHK(dalloc(&b->d_pool_cap, (size_t)D));
+    HIPCHK(dalloc(&b->d_idmap, 1));
+    HIPCHK(dalloc(&b->d_idmap_base, (size_t)D + 1));
+    HIPCHK(hipMemcpy(b->d_idmap_base, idmap_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_off, b->h_off.data(), sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_base, b->h_text_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_len, b->h_text_len.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_text_cap, b->h_text_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_pool_base, b->h_pool_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->d_pool_cap, b->h_pool_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    b->have_log = true;
+    b->generated = false;
+    json_gpu_stats(r, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                   stats);
     return MT_OK;
 }
 

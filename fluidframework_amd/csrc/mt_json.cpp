@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "../../include/mtreplay.h"
+#include "mt_json_gpu.h"
 #include "mt_values.h"
 
 namespace {
@@ -943,6 +944,20 @@ struct mt_packed {
     std::vector<std::vector<std::string>> clients;  // per document, WTF-8
     std::string err;
 };
+
+mt_packed *mt_packed_from(std::vector<mt_op> &&ops, std::vector<int64_t> &&off, std::vector<uint16_t> &&text,
+                          std::vector<mt_prop> &&props, std::vector<std::string> &&keys,
+                          std::vector<std::string> &&values, std::vector<std::vector<std::string>> &&clients) {
+    mt_packed *P = new mt_packed();
+    P->ops = std::move(ops);
+    P->off = std::move(off);
+    P->text = std::move(text);
+    P->props = std::move(props);
+    P->keys = std::move(keys);
+    P->values = std::move(values);
+    P->clients = std::move(clients);
+    return P;
+}
 
 extern "C" {
 

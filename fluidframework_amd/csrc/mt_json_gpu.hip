@@ -1,0 +1,1404 @@
+// mt_json_gpu.hip — GPU JSON op-log ingest (the GPU half).
+//
+// Real op logs are JSON: one array of ISequencedDocumentMessage per document (the file driver's
+// messages.json, fileDeltaStorageService.ts:23-31; each message goes to Client.applyMsg,
+// client.ts:797-819).  mt_json.cpp parses them on host threads; this file does the same on the
+// GPU for the observer fast path (mt_json_gpu.h) and produces the identical packed records
+// (mt_oplog.h), text and interned key / value / client tables — or reports the first document
+// that needs the host parser.  Stages (one wavefront per document unless noted):
+//
+//   scan     64 bytes per step: backslash runs -> unescaped quotes -> in-string mask (prefix
+//            xor of the quote ballot), brackets outside strings -> depth; depth-1 '{' are the
+//            message starts; the top level is validated (one '[' ... ']', exactly one ','
+//            between messages, nothing else outside them)
+//   count    one lane per message: a validating recursive-descent parse of the message
+//            (Packer1::run's rules) -> records / code units / prop records; wave prefix sums
+//            give each message its offsets in the document
+//   clients  getOrAddShortClientId (client.ts:636-641): the observer is 0, every other long id
+//            gets the next id at its first message; first appearance = the smallest message
+//            index holding the name (hash table per document, CAS + atomicMin), ids = prefix
+//            count of first appearances
+//   write    the same parse again, writing records, UTF-16 text and the raw spans of prop keys
+//            / values
+//   props    the same first-appearance interning for keys and values per document; the host
+//            merges the per-document tables batch-wide in document order (as mt_pack_json
+//            does) and a remap pass writes the final ids
+//
+// Text layout: packed (payload = batch-global code-unit offset, mt_pack_json's format) or
+// install (the replay's per-document arena, payload document-relative with the '\n' flags that
+// mt_batch_ingest sets), so a parsed batch goes to the replay without a host round trip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <unordered_map>
+
+#include "../../include/mtreplay.h"
+#include "mt_json_gpu.h"
+
+namespace mt {
+namespace jg {
+
+constexpr uint32_t kNullSpan = 0xFFFFFFFFu;
+constexpr int kClientSlots = 512;  // per-document client hash table (<= 253 distinct names)
+constexpr int kMaxProps = 16;      // keys per props object on the fast path
+
+// reasons a document leaves the fast path (Result::fail_bits)
+enum : uint32_t {
+    kFSyntax = 1,   // not JSON the host parser accepts as is (it decides: maybe an error)
+    kFShape = 2,    // a message / op shape outside the fast path (markers, escapes, floats ...)
+    kFRange = 4,    // an integer outside int32
+    kFWriter = 8,   // a writer replica's log (local ops / own acks)
+    kFClients = 16, // more than 253 clients
+    kFCap = 32      // more messages than the scan's per-document region holds
+};
+
+// message flags
+enum : uint32_t { kMsgOp = 1 };
+
+struct Params {
+    const uint8_t *J;
+    const int64_t *doc_off;
+    int64_t D;
+    // per message (region of document d starts at doc_off[d] / 64 + 2 d)
+    uint32_t *m_start, *m_flags, *m_nrec, *m_ntext, *m_nprop, *m_recoff, *m_textoff, *m_propoff;
+    uint32_t *m_cloff, *m_cllen, *m_cid;
+    // per document
+    uint32_t *d_nmsg, *d_fail, *d_nrec, *d_ntext, *d_nprop, *d_npropops, *d_nnames, *d_nuk, *d_nuv;
+    uint32_t *cl_ht;                 // kClientSlots per document
+    uint32_t *nm_off, *nm_len;       // per message region: client id k's span at index k - 1
+    const uint8_t *obs;              // observer long id (UTF-8) + "null" at obs + 256
+    uint32_t obs_len;
+    // write
+    const int64_t *op_base;          // per document: first record (batch-global)
+    const uint64_t *text_dst;        // per document: first code unit of its text in `text`
+    const uint32_t *text_pay;        // per document: payload of its first code unit
+    const uint32_t *prop_base;       // per document: first prop record (batch-global)
+    mt_op *ops;
+    uint16_t *text;
+    mt_prop *props;
+    int install;
+    uint32_t *pk_off, *pk_len, *pv_off, *pv_len;  // raw spans per prop record
+    uint32_t *lk, *lv;                            // per-document ids per prop record
+    uint32_t *uk_off, *uk_len, *uv_off, *uv_len;  // per-document unique spans (at prop_base)
+    uint32_t *ht;                                  // prop hash tables (keys then values)
+    const uint64_t *ht_base;                       // per document: its key table; values follow
+    const uint32_t *ht_cap;                        // per document: slots per table (power of 2)
+    const uint32_t *kmap, *vmap;                   // remap: per-document id -> batch id
+};
+
+__device__ __forceinline__ int lane_id() { return (int)threadIdx.x; }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t wave_incl(uint32_t v) {
+    const int l = lane_id();
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t mregion(const int64_t *doc_off, int64_t d) {
+    return (uint64_t)(doc_off[d] / 64 + 2 * d);
+}
+
+// ---------------------------------------------------------------- stage 1: structural scan
+extern "C" __global__ __launch_bounds__(64) void jg_scan_kernel(Params P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D) return;
+    const int lane = lane_id();
+    const int64_t a = P.doc_off[d];
+    const uint32_t len = (uint32_t)(P.doc_off[d + 1] - a);
+    const uint64_t mb = mregion(P.doc_off, d);
+    const uint32_t mcap = (uint32_t)(mregion(P.doc_off, d + 1) - mb);
+    const uint8_t *s = P.J + a;
+    uint32_t depth = 0, nmsg = 0, commas = 0, fail = 0, bs_run = 0;
+    bool started = false, ended = false, in_str = false;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint32_t pos = 0; pos < len && !fail; pos += 64) {
+        const uint32_t i = pos + (uint32_t)lane;
+        const int c = i < len ? s[i] : ' ';
+        const uint64_t bs = ballot(c == '\\');
+        // a quote is escaped by an odd run of backslashes right before it
+        const uint64_t nb = ~bs & below;
+        const uint32_t run = nb ? (uint32_t)(lane - 1 - (63 - __builtin_clzll(nb))) : (uint32_t)lane + bs_run;
+        uint64_t x = ballot(c == '"' && !(run & 1u));
+        x ^= x << 1;
+        x ^= x << 2;
+        x ^= x << 4;
+        x ^= x << 8;
+        x ^= x << 16;
+        x ^= x << 32;
+        const uint64_t S = in_str ? ~x : x;  // 1: inside a string (opening quote included)
+        in_str = (S >> 63) & 1ull;
+        bs_run = bs == ~0ull ? bs_run + 64u : (uint32_t)__builtin_clzll(~bs);
+        const bool ws = c == ' ' || c == '\t' || c == '\n' || c == '\r';
+        const uint64_t nonws = ballot(!ws) & ~S;
+        const uint64_t opn = ballot(c == '{' || c == '[') & ~S;
+        const uint64_t cls = ballot(c == '}' || c == ']') & ~S;
+        const uint64_t brace = ballot(c == '{' || c == '}');
+        const uint64_t comma = ballot(c == ',') & ~S;
+        uint64_t st = opn | cls;
+        uint32_t lo = 0;
+        // the bytes strictly between structural characters are at one depth: at depth 0 only
+        // whitespace, at depth 1 (between messages) whitespace and commas
+        auto segment = [&](uint32_t hi) {
+            if (hi > lo) {
+                const uint64_t m = (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
+                if (depth == 0 && (nonws & m)) fail |= kFSyntax;
+                if (depth == 1) {
+                    if (nonws & ~comma & m) fail |= kFSyntax;
+                    commas += (uint32_t)__builtin_popcountll(comma & m);
+                }
+            }
+        };
+        while (st && !fail) {
+            const uint32_t t = (uint32_t)__builtin_ctzll(st);
+            st &= st - 1;
+            segment(t);
+            lo = t + 1;
+            const bool o = (opn >> t) & 1ull, br = (brace >> t) & 1ull;
+            if (ended) {
+                fail |= kFSyntax;
+                break;
+            }
+            if (o) {
+                if (depth == 0) {
+                    if (started || br) fail |= kFSyntax;  // the log is one array
+                    started = true;
+                } else if (depth == 1) {
+                    if (!br) fail |= kFSyntax;  // a message must be an object
+                    if (commas != (nmsg ? 1u : 0u)) fail |= kFSyntax;
+                    commas = 0;
+                    if (nmsg >= mcap) fail |= kFCap;
+                    else if (lane == 0) P.m_start[mb + nmsg] = pos + t;
+                    nmsg++;
+                }
+                depth++;
+            } else {
+                if (depth == 0) {
+                    fail |= kFSyntax;
+                    break;
+                }
+                depth--;
+                if (depth == 0) {
+                    if (br || commas) fail |= kFSyntax;  // ']' closes the log, no trailing comma
+                    ended = true;
+                }
+            }
+        }
+        if (!fail) segment(64);
+    }
+    if (!started || !ended || in_str) fail |= kFSyntax;
+    if (lane == 0) {
+        P.d_nmsg[d] = fail ? 0u : nmsg;
+        P.d_fail[d] = fail;
+    }
+}
+
+// ---------------------------------------------------------------- lane-serial JSON reading
+struct Rd {
+    const uint8_t *s;
+    uint32_t p, n;
+    __device__ int at() const { return p < n ? (int)s[p] : -1; }
+    __device__ void ws() {
+        while (p < n) {
+            const uint8_t c = s[p];
+            if (c == ' ' || c == '\t' || c == '\n' || c == '\r') p++;
+            else break;
+        }
+    }
+    __device__ bool lit(const char *w, uint32_t k) {
+        if (n - p < k) return false;
+        for (uint32_t i = 0; i < k; i++)
+            if (s[p + i] != (uint8_t)w[i]) return false;
+        p += k;
+        return true;
+    }
+};
+
+__device__ __forceinline__ bool is_digit(int c) { return c >= '0' && c <= '9'; }
+__device__ __forceinline__ int hexv(int c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+}
+
+// a string token: raw span of its contents; plain = no escapes, ASCII only
+__device__ bool str_raw(Rd &r, uint32_t &off, uint32_t &len, bool &plain) {
+    if (r.at() != '"') return false;
+    r.p++;
+    off = r.p;
+    plain = true;
+    for (;;) {
+        if (r.p >= r.n) return false;
+        const uint8_t c = r.s[r.p];
+        if (c == '"') break;
+        if (c < 0x20) return false;
+        if (c == '\\') {
+            plain = false;
+            if (++r.p >= r.n) return false;
+            const uint8_t e = r.s[r.p];
+            if (e == 'u') {
+                if (r.n - r.p < 5) return false;
+                for (int i = 1; i <= 4; i++)
+                    if (hexv(r.s[r.p + i]) < 0) return false;
+                r.p += 4;
+            } else if (!(e == '"' || e == '\\' || e == '/' || e == 'b' || e == 'f' || e == 'n' || e == 'r' ||
+                         e == 't')) {
+                return false;
+            }
+            r.p++;
+            continue;
+        }
+        if (c >= 0x80) plain = false;
+        r.p++;
+    }
+    len = r.p - off;
+    r.p++;
+    return true;
+}
+
+// a text string decoded to UTF-16 code units exactly as mt_json.cpp Dom::string (\u escapes
+// kept as code units, UTF-8 -> UTF-16 with surrogate pairs); dst may be null (count only)
+__device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bool &ends_nl) {
+    if (r.at() != '"') return false;
+    r.p++;
+    units = 0;
+    has_nl = ends_nl = false;
+    uint32_t last = 0xFFFFFFFFu;
+    auto put = [&](uint32_t u) {
+        if (dst) dst[units] = (uint16_t)u;
+        units++;
+        last = u & 0xFFFFu;
+        if (last == '\n') has_nl = true;
+    };
+    for (;;) {
+        if (r.p >= r.n) return false;
+        const uint8_t c = r.s[r.p];
+        if (c == '"') break;
+        if (c == '\\') {
+            if (++r.p >= r.n) return false;
+            const uint8_t e = r.s[r.p];
+            switch (e) {
+                case '"': put('"'); break;
+                case '\\': put('\\'); break;
+                case '/': put('/'); break;
+                case 'b': put('\b'); break;
+                case 'f': put('\f'); break;
+                case 'n': put('\n'); break;
+                case 'r': put('\r'); break;
+                case 't': put('\t'); break;
+                case 'u': {
+                    if (r.n - r.p < 5) return false;
+                    uint32_t v = 0;
+                    for (int i = 1; i <= 4; i++) {
+                        const int h = hexv(r.s[r.p + i]);
+                        if (h < 0) return false;
+                        v = v * 16 + (uint32_t)h;
+                    }
+                    put(v);
+                    r.p += 4;
+                    break;
+                }
+                default: return false;
+            }
+            r.p++;
+        } else if (c < 0x20) {
+            return false;
+        } else if (c < 0x80) {
+            put(c);
+            r.p++;
+        } else {
+            const int k = (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : (c & 0xF8) == 0xF0 ? 4 : 0;
+            if (!k || r.n - r.p < (uint32_t)k) return false;
+            uint32_t cp = c & (k == 2 ? 0x1Fu : k == 3 ? 0x0Fu : 0x07u);
+            for (int i = 1; i < k; i++) {
+                const uint8_t b = r.s[r.p + i];
+                if ((b & 0xC0) != 0x80) return false;
+                cp = (cp << 6) | (b & 0x3Fu);
+            }
+            r.p += (uint32_t)k;
+            if (cp >= 0x10000) {
+                cp -= 0x10000;
+                put(0xD800u + (cp >> 10));
+                put(0xDC00u + (cp & 0x3FFu));
+            } else {
+                put(cp);
+            }
+        }
+    }
+    r.p++;
+    ends_nl = last == '\n';
+    return true;
+}
+
+// a number token: 1 = canonical integer (no fraction / exponent, <= 18 digits) in v,
+// 2 = another JSON number, 0 = not one the fast path reads like the host (strtod) would
+__device__ int num_tok(Rd &r, int64_t &v, uint32_t &ndig) {
+    uint32_t p = r.p;
+    bool neg = false;
+    if (p < r.n && r.s[p] == '-') {
+        neg = true;
+        p++;
+    }
+    if (p >= r.n || !is_digit(r.s[p])) return 0;
+    bool canon = true;
+    int64_t acc = 0;
+    ndig = 0;
+    if (r.s[p] == '0') {
+        p++;
+        ndig = 1;
+        if (p < r.n && is_digit(r.s[p])) return 0;
+    } else {
+        while (p < r.n && is_digit(r.s[p])) {
+            if (ndig < 18) acc = acc * 10 + (r.s[p] - '0');
+            ndig++;
+            p++;
+        }
+    }
+    if (p < r.n && r.s[p] == '.') {
+        canon = false;
+        p++;
+        if (p >= r.n || !is_digit(r.s[p])) return 0;
+        while (p < r.n && is_digit(r.s[p])) p++;
+    }
+    if (p < r.n && (r.s[p] == 'e' || r.s[p] == 'E')) {
+        canon = false;
+        p++;
+        if (p < r.n && (r.s[p] == '+' || r.s[p] == '-')) p++;
+        if (p >= r.n || !is_digit(r.s[p])) return 0;
+        while (p < r.n && is_digit(r.s[p])) p++;
+    }
+    if (p < r.n) {  // the host's number scan is greedy over [0-9.eE+-]
+        const uint8_t c = r.s[p];
+        if (is_digit(c) || c == '.' || c == 'e' || c == 'E' || c == '+' || c == '-') return 0;
+    }
+    if (neg && ndig == 1 && acc == 0 && canon) canon = false;  // -0
+    r.p = p;
+    v = neg ? -acc : acc;
+    if (ndig > 18) canon = false;
+    return canon ? 1 : 2;
+}
+
+// any JSON value, validated (strings, numbers, literals, nesting up to 64 levels)
+__device__ bool skip_value(Rd &r) {
+    uint64_t stack = 0;  // bit k: container k is an object
+    int sd = 0;
+    bool want_key = false;
+    for (;;) {
+        r.ws();
+        if (want_key) {
+            uint32_t o, l;
+            bool pl;
+            if (!str_raw(r, o, l, pl)) return false;
+            r.ws();
+            if (r.at() != ':') return false;
+            r.p++;
+            r.ws();
+            want_key = false;
+        }
+        const int c = r.at();
+        bool done_value = true;
+        if (c == '{' || c == '[') {
+            r.p++;
+            r.ws();
+            if (r.at() == (c == '{' ? '}' : ']')) {
+                r.p++;
+            } else {
+                if (sd >= 63) return false;
+                stack = (stack << 1) | (c == '{' ? 1ull : 0ull);
+                sd++;
+                want_key = c == '{';
+                done_value = false;
+            }
+        } else if (c == '"') {
+            uint32_t o, l;
+            bool pl;
+            if (!str_raw(r, o, l, pl)) return false;
+        } else if (c == 't') {
+            if (!r.lit("true", 4)) return false;
+        } else if (c == 'f') {
+            if (!r.lit("false", 5)) return false;
+        } else if (c == 'n') {
+            if (!r.lit("null", 4)) return false;
+        } else {
+            int64_t v;
+            uint32_t nd;
+            if (!num_tok(r, v, nd)) return false;
+        }
+        if (!done_value) continue;
+        // after a value: close containers / next element
+        for (;;) {
+            if (sd == 0) return true;
+            r.ws();
+            const bool obj = stack & 1ull;
+            const int e = r.at();
+            if (e == ',') {
+                r.p++;
+                want_key = obj;
+                break;
+            }
+            if (e == (obj ? '}' : ']')) {
+                r.p++;
+                stack >>= 1;
+                sd--;
+                continue;
+            }
+            return false;
+        }
+    }
+}
+
+__device__ __forceinline__ bool span_eq(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
+    if (la != lb) return false;
+    for (uint32_t i = 0; i < la; i++)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+__device__ __forceinline__ bool key_is(const uint8_t *k, uint32_t kl, const char *w) {
+    uint32_t i = 0;
+    for (; w[i]; i++)
+        if (i >= kl || k[i] != (uint8_t)w[i]) return false;
+    return i == kl;
+}
+__device__ __forceinline__ uint32_t fnv32(const uint8_t *p, uint32_t n) {
+    uint32_t h = 2166136261u;
+    for (uint32_t i = 0; i < n; i++) h = (h ^ p[i]) * 16777619u;
+    return h ^ (h >> 15);
+}
+
+// ---------------------------------------------------------------- per-message parse
+struct MsgOut {
+    uint32_t nrec = 0, ntext = 0, nprop = 0, npropops = 0;
+    uint32_t cl_off = kNullSpan, cl_len = 4, flags = 0;
+};
+
+struct Ctx {  // write pass
+    mt_op *ops = nullptr;       // this message's first record
+    uint16_t *text = nullptr;   // this message's first code unit
+    uint32_t pay = 0;           // payload of that code unit
+    uint32_t gprop = 0;         // batch-global index of this message's first prop record
+    uint32_t *pk_off, *pk_len, *pv_off, *pv_len;
+    uint8_t cid = 0;
+    bool install = false;
+};
+
+struct OpInfo {
+    int64_t type = -1;
+    int32_t p1 = 0, p2 = 0;
+    uint32_t seg_p = 0, props_p = 0, ops_p = 0;
+    uint32_t seen = 0;
+};
+enum { kOType = 1, kOPos1 = 2, kOPos2 = 4, kOSeg = 8, kOProps = 16, kOOps = 32 };
+
+// an op object's members (pack_op / flatten / relpos / register rules, mt_json.cpp:596-649)
+__device__ uint32_t parse_op(Rd &r, OpInfo &op) {
+    if (r.at() != '{') return kFShape;
+    r.p++;
+    r.ws();
+    if (r.at() == '}') {
+        r.p++;
+        return 0;
+    }
+    uint32_t extra = 0;
+    for (;;) {
+        r.ws();
+        uint32_t ko, kl;
+        bool plain;
+        if (!str_raw(r, ko, kl, plain)) return kFSyntax;
+        if (!plain) return kFShape;
+        r.ws();
+        if (r.at() != ':') return kFSyntax;
+        r.p++;
+        r.ws();
+        const uint8_t *k = r.s + ko;
+        uint32_t bit = 0;
+        if (key_is(k, kl, "type")) bit = kOType;
+        else if (key_is(k, kl, "pos1")) bit = kOPos1;
+        else if (key_is(k, kl, "pos2")) bit = kOPos2;
+        else if (key_is(k, kl, "seg")) bit = kOSeg;
+        else if (key_is(k, kl, "props")) bit = kOProps;
+        else if (key_is(k, kl, "ops")) bit = kOOps;
+        if (bit) {
+            if (op.seen & bit) return kFShape;  // a repeated key: the host keeps the last value
+            op.seen |= bit;
+        }
+        if (bit == kOType || bit == kOPos1 || bit == kOPos2) {
+            int64_t v;
+            uint32_t nd;
+            const int t = num_tok(r, v, nd);
+            if (t != 1) return t ? kFShape : kFSyntax;
+            if (v < -2147483648ll || v > 2147483647ll) return kFRange;
+            if (bit == kOType) op.type = v;
+            else if (bit == kOPos1) op.p1 = (int32_t)v;
+            else op.p2 = (int32_t)v;
+        } else {
+            if (bit == kOSeg) op.seg_p = r.p;
+            if (bit == kOProps) op.props_p = r.p;
+            if (bit == kOOps) op.ops_p = r.p;
+            if (!bit) {
+                // combiningOp (a falsy one is ignored), register (null is absent): anything else
+                // and relative positions leave the fast path
+                const bool cop = key_is(k, kl, "combiningOp"), reg = key_is(k, kl, "register");
+                if (cop || reg) {
+                    if (r.lit("null", 4) || (cop && r.lit("false", 5))) {
+                        if (extra & (cop ? 1u : 2u)) return kFShape;
+                        extra |= cop ? 1u : 2u;
+                        goto next;
+                    }
+                    return kFShape;
+                }
+                if (key_is(k, kl, "relativePos1") || key_is(k, kl, "relativePos2")) return kFShape;
+            }
+            if (!skip_value(r)) return kFSyntax;
+        }
+    next:
+        r.ws();
+        const int c = r.at();
+        if (c == ',') {
+            r.p++;
+            continue;
+        }
+        if (c == '}') {
+            r.p++;
+            return 0;
+        }
+        return kFSyntax;
+    }
+}
+
+// a flat props object -> prop records (JS key order = insertion order: array-index keys leave
+// the fast path; duplicates too)
+template <bool W>
+__device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const Ctx &cx) {
+    if (r.at() != '{') return kFShape;
+    r.p++;
+    r.ws();
+    np = 0;
+    if (r.at() == '}') {
+        r.p++;
+        return 0;
+    }
+    uint32_t koff[kMaxProps], klen[kMaxProps];
+    for (;;) {
+        r.ws();
+        uint32_t ko, kl;
+        bool plain;
+        if (!str_raw(r, ko, kl, plain)) return kFSyntax;
+        if (!plain) return kFShape;
+        bool digits = kl > 0;
+        for (uint32_t i = 0; i < kl && digits; i++) digits = is_digit(r.s[ko + i]);
+        if (digits) return kFShape;
+        for (uint32_t j = 0; j < np; j++)
+            if (span_eq(r.s + koff[j], klen[j], r.s + ko, kl)) return kFShape;
+        if (np >= (uint32_t)kMaxProps) return kFShape;
+        koff[np] = ko;
+        klen[np] = kl;
+        r.ws();
+        if (r.at() != ':') return kFSyntax;
+        r.p++;
+        r.ws();
+        uint32_t vo = r.p, vl = 0;
+        const int c = r.at();
+        if (c == 'n') {
+            if (!r.lit("null", 4)) return kFSyntax;
+            vo = kNullSpan;
+        } else if (c == 't') {
+            if (!r.lit("true", 4)) return kFSyntax;
+            vl = 4;
+        } else if (c == 'f') {
+            if (!r.lit("false", 5)) return kFSyntax;
+            vl = 5;
+        } else if (c == '"') {
+            uint32_t so, sl;
+            bool pl;
+            if (!str_raw(r, so, sl, pl)) return kFSyntax;
+            if (!pl) return kFShape;
+            vl = sl + 2;  // JSON.stringify of a plain ASCII string = its source text
+        } else if (c == '-' || is_digit(c)) {
+            int64_t v;
+            uint32_t nd;
+            const int t = num_tok(r, v, nd);
+            if (t != 1) return t ? kFShape : kFSyntax;
+            if (nd > 15) return kFShape;  // Number::toString keeps <= 15 digits exactly
+            vl = r.p - vo;
+        } else {
+            return kFShape;  // nested values: the host's js_stringify
+        }
+        if (W) {
+            cx.pk_off[gidx + np] = ko;
+            cx.pk_len[gidx + np] = kl;
+            cx.pv_off[gidx + np] = vo;
+            cx.pv_len[gidx + np] = vl;
+        }
+        np++;
+        r.ws();
+        const int e = r.at();
+        if (e == ',') {
+            r.p++;
+            continue;
+        }
+        if (e == '}') {
+            r.p++;
+            return 0;
+        }
+        return kFSyntax;
+    }
+}
+
+// one member op -> one record (Packer1::pack_op / pack_seg)
+template <bool W>
+__device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, const mt_op &base, MsgOut &mo,
+                            const Ctx &cx) {
+    if (!(op.seen & kOType)) return kFShape;
+    if (!(op.seen & kOPos1)) return kFShape;  // a position from relativePos1 only: host path
+    mt_op r = base;
+    r.flags = MT_OPF_GROUP_CONT;  // cleared on the message's last record
+    r.pos1 = op.p1;
+    r.pos2 = 0;
+    r.payload = r.payload_len = 0;
+    if (op.type == 0) {
+        if (!(op.seen & kOSeg)) return kFShape;
+        Rd rs{s, op.seg_p, n};
+        uint32_t text_p = 0, props_p = 0;
+        bool has_text = false, has_props = false;
+        if (rs.at() == '"') {
+            text_p = op.seg_p;
+            has_text = true;
+        } else if (rs.at() == '{') {
+            rs.p++;
+            rs.ws();
+            if (rs.at() == '}') return kFShape;
+            for (;;) {
+                rs.ws();
+                uint32_t ko, kl;
+                bool plain;
+                if (!str_raw(rs, ko, kl, plain)) return kFSyntax;
+                if (!plain) return kFShape;
+                rs.ws();
+                if (rs.at() != ':') return kFSyntax;
+                rs.p++;
+                rs.ws();
+                if (key_is(s + ko, kl, "text")) {
+                    if (has_text || rs.at() != '"') return kFShape;
+                    has_text = true;
+                    text_p = rs.p;
+                } else if (key_is(s + ko, kl, "props")) {
+                    if (has_props) return kFShape;
+                    has_props = true;
+                    props_p = rs.p;
+                } else if (key_is(s + ko, kl, "marker")) {
+                    return kFShape;  // markers: the host path (marker ids, tile labels)
+                }
+                if (!skip_value(rs)) return kFSyntax;
+                rs.ws();
+                const int c = rs.at();
+                if (c == ',') {
+                    rs.p++;
+                    continue;
+                }
+                if (c == '}') break;
+                return kFSyntax;
+            }
+            if (!has_text) return kFShape;
+        } else {
+            return kFShape;
+        }
+        Rd rt{s, text_p, n};
+        uint32_t units = 0;
+        bool has_nl = false, ends_nl = false;
+        if (!str_text(rt, W ? cx.text + mo.ntext : nullptr, units, has_nl, ends_nl)) return kFSyntax;
+        uint32_t np = 0;
+        bool hp = false;
+        if (has_props) {
+            Rd rp{s, props_p, n};
+            const int c = rp.at();
+            if (c == '{') {
+                hp = true;
+                const uint32_t f = props_obj<W>(rp, np, cx.gprop + mo.nprop, cx);
+                if (f) return f;
+            } else if (!(rp.lit("null", 4) || rp.lit("false", 5))) {
+                return kFShape;  // arrays fail, other truthy values fail, 0 / "" are rare: host
+            }
+        }
+        r.type = MT_OP_INSERT;
+        if (hp) {
+            r.flags |= (uint16_t)(MT_OPF_HAS_PROPS | (np << 4));
+            r.pos2 = (int32_t)(cx.gprop + mo.nprop);
+            mo.npropops++;
+        }
+        r.payload = cx.pay + mo.ntext;
+        r.payload_len = units;
+        if (cx.install) {
+            if (has_nl) r.flags |= (uint16_t)MT_OPF_INTERNAL_HAS_NL;
+            if (ends_nl) r.flags |= (uint16_t)MT_OPF_INTERNAL_ENDS_NL;
+        }
+        mo.ntext += units;
+        mo.nprop += np;
+    } else if (op.type == 1 || op.type == 2) {
+        r.type = op.type == 1 ? MT_OP_REMOVE : MT_OP_ANNOTATE;
+        r.pos2 = (op.seen & kOPos2) ? op.p2 : 0;
+        if (op.type == 2) {
+            if (!(op.seen & kOProps)) return kFShape;
+            Rd rp{s, op.props_p, n};
+            uint32_t np = 0;
+            const uint32_t f = props_obj<W>(rp, np, cx.gprop + mo.nprop, cx);
+            if (f) return f;
+            r.payload = cx.gprop + mo.nprop;
+            r.payload_len = np;
+            mo.nprop += np;
+            mo.npropops++;
+        }
+    } else {
+        return kFShape;
+    }
+    if (W) cx.ops[mo.nrec] = r;
+    mo.nrec++;
+    return 0;
+}
+
+// one message (Packer1::run's loop body): returns fail bits
+template <bool W>
+__device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0, MsgOut &mo, const Ctx &cx) {
+    Rd r{s, p0 + 1, n};  // after '{'
+    enum { kCl = 1, kSeq = 2, kRef = 4, kMsn = 8, kTy = 16, kCo = 32 };
+    uint32_t seen = 0, contents_p = 0;
+    int64_t seq = 0, ref = 0, msn = 0;
+    bool is_op = false;
+    r.ws();
+    if (r.at() == '}') return kFShape;
+    for (;;) {
+        r.ws();
+        uint32_t ko, kl;
+        bool plain;
+        if (!str_raw(r, ko, kl, plain)) return kFSyntax;
+        if (!plain) return kFShape;
+        r.ws();
+        if (r.at() != ':') return kFSyntax;
+        r.p++;
+        r.ws();
+        const uint8_t *k = s + ko;
+        uint32_t bit = 0;
+        if (key_is(k, kl, "clientId")) bit = kCl;
+        else if (key_is(k, kl, "sequenceNumber")) bit = kSeq;
+        else if (key_is(k, kl, "referenceSequenceNumber")) bit = kRef;
+        else if (key_is(k, kl, "minimumSequenceNumber")) bit = kMsn;
+        else if (key_is(k, kl, "type")) bit = kTy;
+        else if (key_is(k, kl, "contents")) bit = kCo;
+        if (bit) {
+            if (seen & bit) return kFShape;
+            seen |= bit;
+        }
+        if (bit == kCl && r.at() == '"') {
+            uint32_t o, l;
+            bool pl;
+            if (!str_raw(r, o, l, pl)) return kFSyntax;
+            if (!pl) return kFShape;
+            mo.cl_off = o;
+            mo.cl_len = l;
+        } else if (bit == kSeq || bit == kRef || bit == kMsn) {
+            int64_t v;
+            uint32_t nd;
+            const int t = num_tok(r, v, nd);
+            if (t != 1) return t ? kFShape : kFSyntax;
+            if (v < -2147483648ll || v > 2147483647ll) return kFRange;
+            (bit == kSeq ? seq : bit == kRef ? ref : msn) = v;
+        } else if (bit == kTy && r.at() == '"') {
+            uint32_t o, l;
+            bool pl;
+            if (!str_raw(r, o, l, pl)) return kFSyntax;
+            if (!pl) return kFShape;
+            is_op = l == 2 && s[o] == 'o' && s[o + 1] == 'p';
+        } else {
+            if (bit == kCo) contents_p = r.p;
+            // clientId / type of another JSON type: "null" / not an op (the host's rules)
+            if (!skip_value(r)) return kFSyntax;
+        }
+        r.ws();
+        const int c = r.at();
+        if (c == ',') {
+            r.p++;
+            continue;
+        }
+        if (c == '}') {
+            r.p++;
+            break;
+        }
+        return kFSyntax;
+    }
+    r.ws();
+    if (r.at() != ',' && r.at() != ']') return kFSyntax;
+    if ((seen & (kSeq | kRef | kMsn)) != (kSeq | kRef | kMsn)) return kFShape;
+    if (seq == -1) return kFWriter;  // a local op: the writer path
+    if (is_op) mo.flags |= kMsgOp;
+    mt_op base{};
+    base.type = MT_OP_NOOP;
+    base.client = cx.cid;
+    base.seq = (int32_t)seq;
+    base.ref_seq = (int32_t)ref;
+    base.msn = (int32_t)msn;
+    if (is_op && (seen & kCo)) {
+        OpInfo top;
+        Rd rc{s, contents_p, n};
+        uint32_t f = parse_op(rc, top);
+        if (f) return f;
+        if ((top.seen & kOType) && top.type == 3) {  // GROUP: one level of member ops
+            if (!(top.seen & kOOps)) return kFShape;
+            Rd ro{s, top.ops_p, n};
+            if (ro.at() != '[') return kFShape;
+            ro.p++;
+            ro.ws();
+            if (ro.at() == ']') {
+                ro.p++;
+            } else {
+                for (;;) {
+                    ro.ws();
+                    OpInfo m;
+                    f = parse_op(ro, m);
+                    if (f) return f;
+                    if (!(m.seen & kOType) || m.type == 3) return kFShape;
+                    f = emit_op<W>(s, n, m, base, mo, cx);
+                    if (f) return f;
+                    ro.ws();
+                    const int c = ro.at();
+                    if (c == ',') {
+                        ro.p++;
+                        continue;
+                    }
+                    if (c == ']') break;
+                    return kFSyntax;
+                }
+            }
+        } else {
+            f = emit_op<W>(s, n, top, base, mo, cx);
+            if (f) return f;
+        }
+    }
+    if (mo.nrec == 0) {  // not an op / no member: updateSeqNumbers only
+        if (W) cx.ops[0] = base;
+        mo.nrec = 1;
+    } else if (W) {
+        cx.ops[mo.nrec - 1].flags &= (uint16_t)~MT_OPF_GROUP_CONT;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------- stage 2 / 4: parse passes
+template <bool W>
+__device__ void parse_doc(const Params &P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D || P.d_fail[d]) return;
+    const int lane = lane_id();
+    const int64_t a = P.doc_off[d];
+    const uint32_t len = (uint32_t)(P.doc_off[d + 1] - a);
+    const uint8_t *s = P.J + a;
+    const uint64_t mb = mregion(P.doc_off, d);
+    const uint32_t nmsg = P.d_nmsg[d];
+    uint32_t sr = 0, st = 0, sp = 0, so = 0, fail = 0;
+    for (uint32_t i0 = 0; i0 < nmsg; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        const bool valid = i < nmsg;
+        MsgOut mo;
+        uint32_t f = 0;
+        if (valid) {
+            const uint64_t m = mb + i;
+            Ctx cx;
+            if (W) {
+                cx.ops = P.ops + P.op_base[d] + P.m_recoff[m];
+                cx.text = P.text + P.text_dst[d] + P.m_textoff[m];
+                cx.pay = P.text_pay[d] + P.m_textoff[m];
+                cx.gprop = P.prop_base[d] + P.m_propoff[m];
+                cx.pk_off = P.pk_off;
+                cx.pk_len = P.pk_len;
+                cx.pv_off = P.pv_off;
+                cx.pv_len = P.pv_len;
+                cx.cid = (uint8_t)P.m_cid[m];
+                cx.install = P.install != 0;
+            }
+            f = parse_msg<W>(s, len, P.m_start[m], mo, cx);
+        }
+        if (!W) {
+            const uint32_t ir = wave_incl(mo.nrec), it = wave_incl(mo.ntext), ip = wave_incl(mo.nprop);
+            const uint32_t io = wave_incl(mo.npropops);
+            if (valid) {
+                const uint64_t m = mb + i;
+                P.m_flags[m] = mo.flags;
+                P.m_nrec[m] = mo.nrec;
+                P.m_ntext[m] = mo.ntext;
+                P.m_nprop[m] = mo.nprop;
+                P.m_recoff[m] = sr + ir - mo.nrec;
+                P.m_textoff[m] = st + it - mo.ntext;
+                P.m_propoff[m] = sp + ip - mo.nprop;
+                P.m_cloff[m] = mo.cl_off;
+                P.m_cllen[m] = mo.cl_len;
+            }
+            sr += __shfl(ir, 63, 64);
+            st += __shfl(it, 63, 64);
+            sp += __shfl(ip, 63, 64);
+            so += __shfl(io, 63, 64);
+        }
+        // fail bits of the document (any lane)
+        for (int o = 32; o > 0; o >>= 1) f |= __shfl_xor(f, o, 64);
+        fail |= f;
+        if (fail) break;
+    }
+    if (lane == 0) {
+        if (!W) {
+            P.d_nrec[d] = sr;
+            P.d_ntext[d] = st;
+            P.d_nprop[d] = sp;
+            P.d_npropops[d] = so;
+        }
+        if (fail) P.d_fail[d] = fail;
+    }
+}
+extern "C" __global__ __launch_bounds__(64) void jg_count_kernel(Params P) { parse_doc<false>(P); }
+extern "C" __global__ __launch_bounds__(64) void jg_write_kernel(Params P) { parse_doc<true>(P); }
+
+// ---------------------------------------------------------------- first-appearance interning
+// Entries are indices (+1) into the document's spans; a slot keeps the smallest index holding
+// its string (CAS to claim, atomicMin on a match), so after every earlier index was inserted the
+// slot's value is the string's first appearance.  cap: power of two, > distinct strings.
+struct Spans {
+    const uint8_t *s;          // document bytes
+    const uint32_t *off, *len; // spans (kNullSpan: the text "null")
+    uint64_t base;             // index of entry 0
+    const uint8_t *null4;
+    __device__ const uint8_t *ptr(uint32_t i) const { return off[base + i] == kNullSpan ? null4 : s + off[base + i]; }
+    __device__ uint32_t n(uint32_t i) const { return off[base + i] == kNullSpan ? 4u : len[base + i]; }
+};
+
+// insert entry i; returns false when the table is full
+__device__ bool ht_insert(uint32_t *tab, uint32_t cap, const Spans &S, uint32_t i) {
+    const uint8_t *p = S.ptr(i);
+    const uint32_t l = S.n(i);
+    uint32_t slot = fnv32(p, l) & (cap - 1);
+    for (uint32_t probe = 0; probe < cap; probe++) {
+        const uint32_t v = atomicCAS(tab + slot, 0u, i + 1);
+        if (v == 0) return true;
+        const uint32_t j = v - 1;
+        if (span_eq(S.ptr(j), S.n(j), p, l)) {
+            atomicMin(tab + slot, i + 1);
+            return true;
+        }
+        slot = (slot + 1) & (cap - 1);
+    }
+    return false;
+}
+// first appearance of entry i's string
+__device__ uint32_t ht_first(const uint32_t *tab, uint32_t cap, const Spans &S, uint32_t i) {
+    const uint8_t *p = S.ptr(i);
+    const uint32_t l = S.n(i);
+    uint32_t slot = fnv32(p, l) & (cap - 1);
+    for (uint32_t probe = 0; probe < cap; probe++) {
+        const uint32_t v = __hip_atomic_load(tab + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == 0) break;
+        const uint32_t j = v - 1;
+        if (span_eq(S.ptr(j), S.n(j), p, l)) return j;
+        slot = (slot + 1) & (cap - 1);
+    }
+    return i;
+}
+
+// ids of n entries in first-appearance order: id(i) = first0 + number of first appearances
+// before i's string's; skip(i): entries that take no id (the observer, null values).  ids[] is
+// indexed like the spans; uniq_off / uniq_len receive each id's span.  Returns the id count, or
+// 0xFFFFFFFF when the table overflowed.
+template <class Skip>
+__device__ uint32_t intern(uint32_t *tab, uint32_t cap, const Spans &S, uint32_t n, uint32_t first0, uint32_t *ids,
+                           uint32_t *uniq_off, uint32_t *uniq_len, Skip skip) {
+    const int lane = lane_id();
+    uint32_t count = 0;
+    bool full = false;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        const bool act = i < n && !skip(i);
+        if (act && !ht_insert(tab, cap, S, i)) full = true;
+        if (ballot(full)) return 0xFFFFFFFFu;
+        __syncthreads();
+        const uint32_t rep = act ? ht_first(tab, cap, S, i) : i;
+        const bool fresh = act && rep == i;
+        const uint64_t fm = ballot(fresh);
+        const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        if (fresh) {
+            const uint32_t id = first0 + count + (uint32_t)__builtin_popcountll(fm & below);
+            ids[S.base + i] = id;
+            uniq_off[S.base + id - first0] = S.off[S.base + i];
+            uniq_len[S.base + id - first0] = S.len[S.base + i];
+        }
+        __syncthreads();
+        if (act && !fresh) ids[S.base + i] = ids[S.base + rep];
+        count += (uint32_t)__builtin_popcountll(fm);
+        __syncthreads();
+    }
+    return count;
+}
+
+// stage 3: short client ids
+extern "C" __global__ __launch_bounds__(64) void jg_clients_kernel(Params P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D || P.d_fail[d]) return;
+    const int lane = lane_id();
+    const uint64_t mb = mregion(P.doc_off, d);
+    const uint32_t nmsg = P.d_nmsg[d];
+    Spans S{P.J + P.doc_off[d], P.m_cloff, P.m_cllen, mb, P.obs + 256};
+    uint32_t fail = 0;
+    // the observer's own messages: short id 0 (an op of its own is an ack: the writer path)
+    for (uint32_t i0 = 0; i0 < nmsg; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        if (i < nmsg && span_eq(S.ptr(i), S.n(i), P.obs, P.obs_len)) {
+            P.m_cid[mb + i] = 0;
+            if (P.m_flags[mb + i] & kMsgOp) fail |= kFWriter;
+        } else if (i < nmsg) {
+            P.m_cid[mb + i] = 0xFFFFFFFFu;
+        }
+    }
+    __syncthreads();
+    uint32_t *tab = P.cl_ht + (uint64_t)d * kClientSlots;
+    const uint32_t *cid = P.m_cid;
+    auto is_obs = [&](uint32_t i) { return cid[mb + i] == 0u; };
+    const uint32_t cnt = intern(tab, kClientSlots, S, nmsg, 1u, P.m_cid, P.nm_off, P.nm_len, is_obs);
+    for (int o = 32; o > 0; o >>= 1) fail |= __shfl_xor(fail, o, 64);
+    if (cnt == 0xFFFFFFFFu || cnt + 1 > (uint32_t)MT_MAX_CLIENTS) fail |= kFClients;
+    if (lane == 0) {
+        P.d_nnames[d] = cnt == 0xFFFFFFFFu ? 0u : cnt + 1;
+        if (fail) P.d_fail[d] = fail;
+    }
+}
+
+// stage 5: prop keys and values
+extern "C" __global__ __launch_bounds__(64) void jg_props_kernel(Params P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D) return;
+    const uint32_t n = P.d_nprop[d];
+    const uint64_t pb = P.prop_base[d];
+    const uint32_t cap = P.ht_cap[d];
+    uint32_t *tk = P.ht + P.ht_base[d], *tv = tk + cap;
+    const uint8_t *s = P.J + P.doc_off[d];
+    Spans K{s, P.pk_off, P.pk_len, pb, P.obs + 256};
+    Spans V{s, P.pv_off, P.pv_len, pb, P.obs + 256};
+    const uint32_t nk = intern(tk, cap, K, n, 0u, P.lk, P.uk_off, P.uk_len, [](uint32_t) { return false; });
+    const uint32_t *pvo = P.pv_off;
+    auto is_null = [&](uint32_t i) { return pvo[pb + i] == kNullSpan; };
+    for (uint32_t i = (uint32_t)lane_id(); i < n; i += 64)
+        if (is_null(i)) P.lv[pb + i] = 0;
+    __syncthreads();
+    const uint32_t nv = intern(tv, cap, V, n, 1u, P.lv, P.uv_off, P.uv_len, is_null);
+    if (lane_id() == 0) {
+        P.d_nuk[d] = nk;
+        P.d_nuv[d] = nv;
+    }
+}
+
+// stage 6: batch-wide ids
+extern "C" __global__ __launch_bounds__(64) void jg_remap_kernel(Params P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D) return;
+    const uint32_t n = P.d_nprop[d];
+    const uint64_t pb = P.prop_base[d];
+    for (uint32_t i = (uint32_t)lane_id(); i < n; i += 64) {
+        const uint32_t k = P.lk[pb + i], v = P.lv[pb + i];
+        P.props[pb + i] = mt_prop{P.kmap[pb + k], v ? P.vmap[pb + v - 1] : 0u};
+    }
+}
+
+}  // namespace jg
+}  // namespace mt
+
+// ---------------------------------------------------------------- host driver
+namespace mt {
+namespace jg {
+namespace {
+
+#define JGCHK(x)                                                                                   \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            fprintf(stderr, "mtreplay: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                                     \
+            return MT_ERR_HIP;                                                                     \
+        }                                                                                          \
+    } while (0)
+
+struct DevBufs {
+    std::vector<void *> ptrs;
+    ~DevBufs() {
+        for (void *p : ptrs) (void)hipFree(p);
+    }
+    template <class T>
+    hipError_t get(T **p, size_t n) {
+        *p = nullptr;
+        hipError_t e = hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) ptrs.push_back((void *)*p);
+        return e;
+    }
+};
+
+template <class T>
+hipError_t dl(std::vector<T> &h, const T *d, size_t n, hipStream_t s) {
+    h.resize(n);
+    if (!n) return hipSuccess;
+    hipError_t e = hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s);
+    return e == hipSuccess ? hipStreamSynchronize(s) : e;
+}
+
+uint32_t pow2_at_least(uint64_t x) {
+    uint32_t c = 16;
+    while (c < x) c <<= 1;
+    return c;
+}
+
+}  // namespace
+
+int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *d_json_in, const char *observer,
+          void *stream, const TextLayout *install, mt_op **d_ops_out, uint16_t **d_text_out, uint64_t *text_words,
+          mt_prop **d_props_out, Result &res) {
+    *d_ops_out = nullptr;
+    *d_text_out = nullptr;
+    *d_props_out = nullptr;
+    res = Result{};
+    if (D < 0 || !doc_off || doc_off[0] != 0) return MT_ERR_ARG;
+    for (int64_t d = 0; d < D; d++)
+        if (doc_off[d + 1] < doc_off[d] || doc_off[d + 1] - doc_off[d] > 0xFFFFFFF0ll) return MT_ERR_ARG;
+    const std::string obs = observer ? observer : "readonly";
+    if (obs.size() > 255) return MT_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t total = (uint64_t)doc_off[D];
+    DevBufs B;
+    Params P{};
+    P.D = D;
+    hipEvent_t ev[6];
+    for (auto &e : ev) JGCHK(hipEventCreate(&e));
+    struct EvFree {
+        hipEvent_t *e;
+        ~EvFree() {
+            for (int i = 0; i < 6; i++) (void)hipEventDestroy(e[i]);
+        }
+    } evf{ev};
+    const uint8_t *J = d_json_in;
+    if (!J) {
+        uint8_t *dj = nullptr;
+        JGCHK(B.get(&dj, total + 64));
+        JGCHK(hipMemcpyAsync(dj, h_json, total, hipMemcpyHostToDevice, s));
+        JGCHK(hipMemsetAsync(dj + total, 0, 64, s));
+        J = dj;
+    }
+    P.J = J;
+    int64_t *d_off = nullptr;
+    JGCHK(B.get(&d_off, (size_t)D + 1));
+    JGCHK(hipMemcpyAsync(d_off, doc_off, 8 * ((size_t)D + 1), hipMemcpyHostToDevice, s));
+    P.doc_off = d_off;
+    const size_t M = (size_t)(total / 64 + 2 * (uint64_t)D + 2);
+    uint32_t **marr[] = {&P.m_start, &P.m_flags, &P.m_nrec, &P.m_ntext, &P.m_nprop, &P.m_recoff,
+                         &P.m_textoff, &P.m_propoff, &P.m_cloff, &P.m_cllen, &P.m_cid, &P.nm_off, &P.nm_len};
+    for (uint32_t **a : marr) JGCHK(B.get(a, M));
+    uint32_t **darr[] = {&P.d_nmsg, &P.d_fail, &P.d_nrec, &P.d_ntext, &P.d_nprop, &P.d_npropops,
+                         &P.d_nnames, &P.d_nuk, &P.d_nuv};
+    for (uint32_t **a : darr) JGCHK(B.get(a, (size_t)D));
+    JGCHK(hipMemsetAsync(P.d_nrec, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
+    JGCHK(hipMemsetAsync(P.d_ntext, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
+    JGCHK(hipMemsetAsync(P.d_nprop, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
+    JGCHK(hipMemsetAsync(P.d_npropops, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
+    JGCHK(B.get(&P.cl_ht, (size_t)D * kClientSlots));
+    JGCHK(hipMemsetAsync(P.cl_ht, 0, 4 * (size_t)D * kClientSlots, s));
+    {
+        uint8_t *o = nullptr;
+        JGCHK(B.get(&o, 512));
+        std::vector<uint8_t> ob(512, 0);
+        memcpy(ob.data(), obs.data(), obs.size());
+        memcpy(ob.data() + 256, "null", 4);
+        JGCHK(hipMemcpyAsync(o, ob.data(), 512, hipMemcpyHostToDevice, s));
+        P.obs = o;
+        P.obs_len = (uint32_t)obs.size();
+    }
+    const unsigned grid = (unsigned)std::max<int64_t>(D, 1);
+    void *args[] = {&P};
+    JGCHK(hipEventRecord(ev[0], s));
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_scan_kernel, dim3(grid), dim3(64), args, 0, s));
+    JGCHK(hipEventRecord(ev[1], s));
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_count_kernel, dim3(grid), dim3(64), args, 0, s));
+    JGCHK(hipEventRecord(ev[2], s));
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_clients_kernel, dim3(grid), dim3(64), args, 0, s));
+    JGCHK(hipEventRecord(ev[3], s));
+    std::vector<uint32_t> fail, nrec, ntext, nprop, npops, nmsg;
+    JGCHK(dl(fail, P.d_fail, (size_t)D, s));
+    for (int64_t d = 0; d < D; d++)
+        if (fail[(size_t)d]) {
+            res.status = MT_UNSUPPORTED;
+            res.bad_doc = d;
+            res.fail_bits = fail[(size_t)d];
+            return MT_UNSUPPORTED;
+        }
+    JGCHK(dl(nrec, P.d_nrec, (size_t)D, s));
+    JGCHK(dl(ntext, P.d_ntext, (size_t)D, s));
+    JGCHK(dl(nprop, P.d_nprop, (size_t)D, s));
+    JGCHK(dl(npops, P.d_npropops, (size_t)D, s));
+    JGCHK(dl(nmsg, P.d_nmsg, (size_t)D, s));
+    // batch layout: records and prop records back to back in document order
+    res.doc_op_off.assign((size_t)D + 1, 0);
+    std::vector<int64_t> op_base((size_t)D);
+    std::vector<uint32_t> prop_base((size_t)D), text_pay((size_t)D);
+    std::vector<uint64_t> text_dst((size_t)D);
+    uint64_t tp = 0, pp = 0;
+    for (int64_t d = 0; d < D; d++) {
+        op_base[(size_t)d] = res.doc_op_off[(size_t)d];
+        res.doc_op_off[(size_t)d + 1] = res.doc_op_off[(size_t)d] + nrec[(size_t)d];
+        prop_base[(size_t)d] = (uint32_t)pp;
+        text_pay[(size_t)d] = (uint32_t)tp;
+        text_dst[(size_t)d] = tp;
+        tp += ntext[(size_t)d];
+        pp += nprop[(size_t)d];
+        res.n_msgs += nmsg[(size_t)d];
+    }
+    if (tp > 0xFFFFFFF0ull || pp > 0x7FFFFFF0ull) return MT_ERR_ARG;
+    res.n_ops = res.doc_op_off[(size_t)D];
+    res.n_text = (int64_t)tp;
+    res.n_props = (int64_t)pp;
+    res.doc_text = ntext;
+    res.doc_nprop_ops = npops;
+    res.doc_nprops = nprop;
+    uint64_t words = tp;
+    if (install) {
+        int rc = (*install)(res, text_dst, words);
+        if (rc) return rc;
+        std::fill(text_pay.begin(), text_pay.end(), 0u);
+    }
+    mt_op *d_ops = nullptr;
+    uint16_t *d_text = nullptr;
+    mt_prop *d_props = nullptr;
+    if (hipMalloc((void **)&d_ops, std::max<size_t>((size_t)res.n_ops, 1) * sizeof(mt_op)) != hipSuccess)
+        return MT_ERR_HIP;
+    if (hipMalloc((void **)&d_text, std::max<uint64_t>(words, 1) * 2) != hipSuccess ||
+        hipMalloc((void **)&d_props, std::max<uint64_t>(pp, 1) * sizeof(mt_prop)) != hipSuccess) {
+        (void)hipFree(d_ops);
+        (void)hipFree(d_text);
+        return MT_ERR_HIP;
+    }
+    *d_ops_out = d_ops;
+    *d_text_out = d_text;
+    *d_props_out = d_props;
+    *text_words = words;
+    JGCHK(hipMemsetAsync(d_text, 0, std::max<uint64_t>(words, 1) * 2, s));
+    P.ops = d_ops;
+    P.text = d_text;
+    P.props = d_props;
+    P.install = install != nullptr;
+    int64_t *d_opb = nullptr;
+    uint64_t *d_tdst = nullptr;
+    uint32_t *d_tpay = nullptr, *d_pb = nullptr;
+    JGCHK(B.get(&d_opb, (size_t)D));
+    JGCHK(B.get(&d_tdst, (size_t)D));
+    JGCHK(B.get(&d_tpay, (size_t)D));
+    JGCHK(B.get(&d_pb, (size_t)D));
+    JGCHK(hipMemcpyAsync(d_opb, op_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice, s));
+    JGCHK(hipMemcpyAsync(d_tdst, text_dst.data(), 8 * (size_t)D, hipMemcpyHostToDevice, s));
+    JGCHK(hipMemcpyAsync(d_tpay, text_pay.data(), 4 * (size_t)D, hipMemcpyHostToDevice, s));
+    JGCHK(hipMemcpyAsync(d_pb, prop_base.data(), 4 * (size_t)D, hipMemcpyHostToDevice, s));
+    P.op_base = d_opb;
+    P.text_dst = d_tdst;
+    P.text_pay = d_tpay;
+    P.prop_base = d_pb;
+    uint32_t **parr[] = {&P.pk_off, &P.pk_len, &P.pv_off, &P.pv_len, &P.lk, &P.lv,
+                         &P.uk_off, &P.uk_len, &P.uv_off, &P.uv_len};
+    for (uint32_t **a : parr) JGCHK(B.get(a, (size_t)pp));
+    // prop hash tables: per document two tables of a power of two > 2 x its records
+    std::vector<uint64_t> ht_base((size_t)D);
+    std::vector<uint32_t> ht_cap((size_t)D);
+    uint64_t hsum = 0;
+    for (int64_t d = 0; d < D; d++) {
+        ht_cap[(size_t)d] = pow2_at_least(2ull * nprop[(size_t)d] + 1);
+        ht_base[(size_t)d] = hsum;
+        hsum += 2ull * ht_cap[(size_t)d];
+    }
+    uint64_t *d_htb = nullptr;
+    uint32_t *d_htc = nullptr;
+    JGCHK(B.get(&P.ht, (size_t)hsum));
+    JGCHK(hipMemsetAsync(P.ht, 0, 4 * std::max<uint64_t>(hsum, 1), s));
+    JGCHK(B.get(&d_htb, (size_t)D));
+    JGCHK(B.get(&d_htc, (size_t)D));
+    JGCHK(hipMemcpyAsync(d_htb, ht_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice, s));
+    JGCHK(hipMemcpyAsync(d_htc, ht_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice, s));
+    P.ht_base = d_htb;
+    P.ht_cap = d_htc;
+    void *args2[] = {&P};
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_write_kernel, dim3(grid), dim3(64), args2, 0, s));
+    JGCHK(hipEventRecord(ev[4], s));
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_props_kernel, dim3(grid), dim3(64), args2, 0, s));
+    // host: batch-wide tables in first-appearance order (document order, then record order)
+    std::vector<uint32_t> nuk, nuv, uko, ukl, uvo, uvl, nnames, cl_off, cl_len;
+    JGCHK(dl(nuk, P.d_nuk, (size_t)D, s));
+    JGCHK(dl(nuv, P.d_nuv, (size_t)D, s));
+    JGCHK(dl(uko, P.uk_off, (size_t)pp, s));
+    JGCHK(dl(ukl, P.uk_len, (size_t)pp, s));
+    JGCHK(dl(uvo, P.uv_off, (size_t)pp, s));
+    JGCHK(dl(uvl, P.uv_len, (size_t)pp, s));
+    JGCHK(dl(nnames, P.d_nnames, (size_t)D, s));
+    JGCHK(dl(cl_off, P.nm_off, M, s));  // jg_clients_kernel: names' spans by id - 1
+    JGCHK(dl(cl_len, P.nm_len, M, s));
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint32_t> kmap((size_t)std::max<uint64_t>(pp, 1)), vmap((size_t)std::max<uint64_t>(pp, 1));
+    std::unordered_map<std::string, uint32_t> kid, vid{{"null", 0u}};
+    res.values.assign(1, "null");
+    res.clients.resize((size_t)D);
+    for (int64_t d = 0; d < D; d++) {
+        const char *js = h_json + doc_off[d];
+        const uint32_t pb = prop_base[(size_t)d];
+        for (uint32_t i = 0; i < nuk[(size_t)d]; i++) {
+            std::string k(js + uko[pb + i], ukl[pb + i]);
+            auto it = kid.find(k);
+            if (it == kid.end()) {
+                it = kid.emplace(k, (uint32_t)res.keys.size()).first;
+                res.keys.push_back(k);
+            }
+            kmap[pb + i] = it->second;
+        }
+        for (uint32_t i = 0; i < nuv[(size_t)d]; i++) {
+            std::string v(js + uvo[pb + i], uvl[pb + i]);
+            auto it = vid.find(v);
+            if (it == vid.end()) {
+                it = vid.emplace(v, (uint32_t)res.values.size()).first;
+                res.values.push_back(v);
+            }
+            vmap[pb + i] = it->second;
+        }
+        auto &nm = res.clients[(size_t)d];
+        nm.assign(1, obs);
+        const uint64_t mb = (uint64_t)(doc_off[d] / 64 + 2 * d);
+        for (uint32_t i = 1; i < nnames[(size_t)d]; i++) {
+            const uint32_t o = cl_off[mb + i - 1];
+            nm.push_back(o == kNullSpan ? std::string("null") : std::string(js + o, cl_len[mb + i - 1]));
+        }
+    }
+    for (const auto &k : res.keys)
+        if (k == "referenceTileLabels" || k == "markerId") {  // tile / marker bookkeeping: host path
+            res.status = MT_UNSUPPORTED;
+            res.fail_bits = kFShape;
+            res.bad_doc = 0;
+            return MT_UNSUPPORTED;
+        }
+    res.ms_host = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    uint32_t *d_km = nullptr, *d_vm = nullptr;
+    JGCHK(B.get(&d_km, kmap.size()));
+    JGCHK(B.get(&d_vm, vmap.size()));
+    JGCHK(hipMemcpyAsync(d_km, kmap.data(), 4 * kmap.size(), hipMemcpyHostToDevice, s));
+    JGCHK(hipMemcpyAsync(d_vm, vmap.data(), 4 * vmap.size(), hipMemcpyHostToDevice, s));
+    P.kmap = d_km;
+    P.vmap = d_vm;
+    void *args3[] = {&P};
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_remap_kernel, dim3(grid), dim3(64), args3, 0, s));
+    JGCHK(hipEventRecord(ev[5], s));
+    JGCHK(hipStreamSynchronize(s));
+    JGCHK(hipEventElapsedTime(&res.ms_scan, ev[0], ev[1]));
+    JGCHK(hipEventElapsedTime(&res.ms_count, ev[1], ev[2]));
+    JGCHK(hipEventElapsedTime(&res.ms_clients, ev[2], ev[3]));
+    JGCHK(hipEventElapsedTime(&res.ms_write, ev[3], ev[4]));
+    JGCHK(hipEventElapsedTime(&res.ms_props, ev[4], ev[5]));
+    res.status = MT_OK;
+    return MT_OK;
+}
+
+}  // namespace jg
+}  // namespace mt

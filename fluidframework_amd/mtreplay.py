@@ -43,7 +43,7 @@ EXPORTS = [
     "mt_batch_snapshot_digests", "mt_batch_generate_docs", "mt_pack_json", "mt_packed_destroy", "mt_packed_error",
     "mt_packed_sizes", "mt_packed_arrays", "mt_packed_key", "mt_packed_value", "mt_packed_doc_clients",
     "mt_packed_client", "mt_batch_ingest_packed", "mt_batch_log_sizes_docs", "mt_batch_download_log_docs",
-    "mt_build_id", "mt_doc_find_tile", "mt_doc_regenerated_ops",
+    "mt_build_id", "mt_doc_find_tile", "mt_doc_regenerated_ops", "mt_pack_json_gpu", "mt_batch_ingest_json_gpu",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -55,6 +55,27 @@ class MtError(RuntimeError):
     def __init__(self, code: int, what: str):
         super().__init__(f"{what}: {status_string(code)} ({code})")
         self.code = code
+
+
+class JsonGpuStats(C.Structure):
+    """mt_json_gpu_stats (include/mtreplay.h)"""
+
+    _fields_ = [("ms_scan", C.c_double), ("ms_count", C.c_double), ("ms_clients", C.c_double),
+                ("ms_write", C.c_double), ("ms_props", C.c_double), ("ms_host", C.c_double),
+                ("ms_total", C.c_double), ("n_msgs", C.c_int64), ("n_ops", C.c_int64), ("n_text", C.c_int64),
+                ("n_props", C.c_int64), ("fail_bits", C.c_uint32), ("reserved", C.c_int32)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+class NotOnGpuPath(RuntimeError):
+    """A JSON batch outside the GPU parser's fast path (mt_json_gpu.h): use the host parser."""
+
+    def __init__(self, bad_doc: int, fail_bits: int):
+        super().__init__(f"document {bad_doc} needs the host JSON parser (reasons 0x{fail_bits:x})")
+        self.bad_doc = bad_doc
+        self.fail_bits = fail_bits
 
 
 class GenParams(C.Structure):
@@ -153,6 +174,8 @@ def lib():
     L.mt_packed_client.argtypes = [vp, i64, i32]
     L.mt_packed_client.restype = cp
     L.mt_batch_ingest_packed.argtypes = [vp, vp]
+    L.mt_pack_json_gpu.argtypes = [P(vp), i64, vp, vp, cp, P(i64), P(JsonGpuStats)]
+    L.mt_batch_ingest_json_gpu.argtypes = [vp, vp, vp, vp, cp, P(i64), P(JsonGpuStats)]
     L.mt_batch_run.argtypes = [vp, vp]
     L.mt_batch_launch.argtypes = [vp, vp]
     L.mt_batch_sync.argtypes = [vp]
@@ -196,6 +219,17 @@ def _cstrs(strs):
     for k, s in enumerate(strs):
         arr[k] = s.encode("utf-8", "surrogatepass")  # WTF-8: lone surrogates survive
     return arr
+
+
+def json_concat(docs):
+    """Documents (JSON text / bytes / message lists) back to back: (bytes, doc_off int64[D + 1])."""
+    bufs = [d if isinstance(d, bytes) else (d if isinstance(d, str) else json.dumps(d)).encode("utf-8",
+                                                                                          "surrogatepass")
+            for d in docs]
+    off = np.zeros(len(bufs) + 1, np.int64)
+    if bufs:
+        off[1:] = np.cumsum([len(x) for x in bufs])
+    return b"".join(bufs), off
 
 
 class PackedJson:
@@ -245,6 +279,24 @@ class PackedJson:
                    for d in range(self.n_docs)]
         return PackedBatch(ops=ops, doc_op_off=off, text=text[: nt.value], props=props[: npr.value], keys=keys,
                            values=values, clients=clients)
+
+
+class PackedJsonGpu(PackedJson):
+    """The same packed result from the GPU parser (mt_pack_json_gpu, mt_json_gpu.hip); raises
+    NotOnGpuPath for a batch outside its fast path."""
+
+    def __init__(self, docs, observer: str = "readonly"):
+        buf, off = json_concat(docs)
+        h, bad, st = C.c_void_p(), C.c_int64(-1), JsonGpuStats()
+        rc = lib().mt_pack_json_gpu(C.byref(h), len(off) - 1, buf, off.ctypes.data, observer.encode("utf-8"),
+                                    C.byref(bad), C.byref(st))
+        self.h = h if rc == MT_OK else None
+        self.n_docs = len(off) - 1
+        self.stats = st.as_dict()
+        if rc == MT_UNSUPPORTED:
+            raise NotOnGpuPath(bad.value, st.fail_bits)
+        if rc != MT_OK:
+            raise MtError(rc, "mt_pack_json_gpu")
 
 
 class DocView:
@@ -397,14 +449,46 @@ class ReplayBatch:
         self.ingest_packed(pb)
         return pb
 
-    def ingest_json(self, docs, observer: str = "readonly", n_threads: int = 0):
-        """Parse + pack JSON message logs natively (mt_pack_json, host threads) and ingest them.
-        docs: per document a JSON array text (str/bytes) or a list of message dicts."""
+    def ingest_json(self, docs, observer: str = "readonly", n_threads: int = 0, device: str = "auto"):
+        """Parse + pack JSON message logs natively and ingest them.  docs: per document a JSON
+        array text (str/bytes) or a list of message dicts.  device "gpu": the GPU parser
+        (mt_batch_ingest_json_gpu; NotOnGpuPath outside its fast path), "host": mt_pack_json on
+        host threads, "auto": the GPU parser, the host parser for batches outside its fast path.
+        Returns {"path": "gpu" | "host", ...GPU parser stats}."""
+        if device not in ("auto", "gpu", "host"):
+            raise ValueError("device must be auto, gpu or host")
+        info = {"path": "host"}
+        if device != "host":
+            buf, off = json_concat(docs)
+            try:
+                info.update(self.ingest_json_gpu(buf, off, observer))
+                info["path"] = "gpu"
+                return info
+            except NotOnGpuPath as e:
+                if device == "gpu":
+                    raise
+                info.update(bad_doc=e.bad_doc, fail_bits=e.fail_bits)
         pj = PackedJson(docs, observer, n_threads)
         try:
             _chk(lib().mt_batch_ingest_packed(self.h, pj.h), "mt_batch_ingest_packed")
         finally:
             pj.close()
+        return info
+
+    def ingest_json_gpu(self, buf: bytes, doc_off, observer: str = "readonly", d_json=None) -> dict:
+        """GPU JSON ingest of documents back to back in `buf` (doc_off[D + 1]); d_json: the same
+        bytes already on the device (a pointer, e.g. a torch uint8 tensor's data_ptr(), 64 bytes
+        readable past the end) — the parse then reads HBM only.  Returns the stage timings."""
+        off = np.ascontiguousarray(doc_off, np.int64)
+        if len(off) != self.n_docs + 1:
+            raise ValueError("doc_off must have n_docs + 1 entries")
+        bad, st = C.c_int64(-1), JsonGpuStats()
+        rc = lib().mt_batch_ingest_json_gpu(self.h, buf, off.ctypes.data, d_json, observer.encode("utf-8"),
+                                            C.byref(bad), C.byref(st))
+        if rc == MT_UNSUPPORTED:
+            raise NotOnGpuPath(bad.value, st.fail_bits)
+        _chk(rc, "mt_batch_ingest_json_gpu")
+        return st.as_dict()
 
     def generate(self, params: GenParams, doc_first: int = 0):
         _chk(lib().mt_batch_generate(self.h, C.byref(params), doc_first), "mt_batch_generate")

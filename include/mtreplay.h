@@ -127,6 +127,28 @@ MT_API int32_t mt_packed_doc_clients(const mt_packed *p, int64_t doc);
 MT_API const char *mt_packed_client(const mt_packed *p, int64_t doc, int32_t i);
 MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p);
 
+/* JSON op logs parsed on the GPU (fluidframework_amd/csrc/mt_json_gpu.hip): the same records,
+   text and tables as mt_pack_json for the observer fast path — sequenced messages whose contents
+   are insert (text / {text, props}) / remove / annotate without combiningOp / a one-level group of
+   those, prop values null / booleans / integers / plain ASCII strings.  A batch with any other
+   document returns MT_UNSUPPORTED with *bad_doc set and nothing changed: parse it with
+   mt_pack_json (the bindings' ingest_json does).  json: the documents back to back, document d =
+   json[doc_off[d] .. doc_off[d+1]).  d_json: the same bytes already on the device (NULL: copied
+   here), readable 64 bytes past the end.  Replaces the host parse of Client.applyMsg's input
+   (clientReplayTool.ts:194-252 feeding client.ts:797-819). */
+typedef struct mt_json_gpu_stats {
+    double ms_scan, ms_count, ms_clients, ms_write, ms_props; /* device stages (hipEvents) */
+    double ms_host;                                           /* host merge of the key / value tables */
+    double ms_total;                                          /* wall time of the call */
+    int64_t n_msgs, n_ops, n_text, n_props;
+    uint32_t fail_bits;                                       /* why *bad_doc left the fast path */
+    int32_t reserved;
+} mt_json_gpu_stats;
+MT_API int mt_pack_json_gpu(mt_packed **out, int64_t n_docs, const char *json, const int64_t *doc_off,
+                            const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats);
+MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, const void *d_json,
+                                    const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats);
+
 /* synthesize logs on the device (include/mt_gen.h); doc_first = global index of doc 0 */
 MT_API int mt_batch_generate(mt_batch *b, const mt_gen_params *p, int64_t doc_first);
 /* the same with per-document global indices (stream seeds) and op counts (p->n_ops ignored):

@@ -61,6 +61,7 @@ for step in "$@"; do
     pmcB2) run pmcB2 200 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
     pmcf2) run pmcf2 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
     pmcw2) run pmcw2 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
+    jsontests) run jsontests 300 python -u -m pytest tests/test_gpu_json.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     prof3) run prof3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     *) echo "unknown step $step" ;;
   esac

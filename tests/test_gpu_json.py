@@ -1,0 +1,201 @@
+"""GPU JSON op-log ingest (mt_json_gpu.hip) == the host parser (mt_pack_json), on the MI355X.
+
+The GPU parser must produce the host parser's packed records, text, prop records and interned key /
+value / client tables byte for byte on every log of its fast path (mt_json_gpu.h), report the first
+document outside it (never a silently different result), and a batch ingested through it must
+replay exactly like the host-ingested batch (the host parser is itself pinned to the Python / JS
+packers by tests/test_json_ingest.py)."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+import fluidframework_amd as fa
+from fluidframework_amd.mtreplay import NotOnGpuPath, PackedJson, PackedJsonGpu
+from kat_util import load_kats
+from test_json_ingest import _farm_messages, _msg
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(docs, observer="readonly"):
+    want = PackedJson(docs, observer).arrays()
+    pg = PackedJsonGpu(docs, observer)
+    got = pg.arrays()
+    assert (got.doc_op_off == want.doc_op_off).all()
+    assert len(got.ops) == len(want.ops)
+    for i in np.nonzero(got.ops != want.ops)[0][:3]:
+        raise AssertionError(f"record {i}: GPU {got.ops[i]} host {want.ops[i]}")
+    assert (got.text == want.text).all()
+    assert len(got.props) == len(want.props) and (got.props == want.props).all()
+    assert got.keys == want.keys
+    assert got.values == want.values
+    assert got.clients == want.clients
+    return pg.stats
+
+
+FAST_DOCS = [
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "hello", "props": {"b": 1, "c": "x", "d": None}}}),
+     _msg("B", 2, 0, {"type": 3, "ops": [{"type": 0, "pos1": 2, "seg": "XY"},
+                                         {"type": 2, "pos1": 0, "pos2": 4, "props": {"c": True, "e": False}}]}),
+     _msg("A", 3, 1, {"type": 0, "pos1": 3, "seg": {"text": "e", "props": {}}}, msn=1),
+     _msg(None, 4, 3, None, msn=1, type_="join"),
+     _msg("readonly", 5, 3, {"anything": [1, 2.5, {"x": "y"}]}, msn=1, type_="noop"),
+     _msg("B", 6, 5, {"type": 1, "pos1": 0, "pos2": 2}, msn=3),
+     _msg("C", 7, 6, {"type": 3, "ops": []}, msn=5),
+     _msg("A", 8, 7, {"type": 2, "pos1": 0, "pos2": 1, "props": {}, "combiningOp": None}, msn=5),
+     _msg("null", 9, 8, {"type": 1, "pos1": 0, "pos2": 1}, msn=5),
+     _msg("A", 10, 9, {"type": 0, "pos1": 0, "seg": {"text": "p", "props": None}, "register": None}, msn=5)],
+    [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "a\ud83d"}),
+     _msg("A", 2, 1, {"type": 0, "pos1": 2, "seg": "\ude00b\"\\\n\x01é€😀\t/"}),
+     _msg("B", 3, 2, {"type": 2, "pos1": 0, "pos2": 3, "props": {"k": -12, "n": 0, "s": "a b~", "big": 123456789012345}}),
+     _msg("B", 4, 3, {"type": 0, "pos1": 1, "seg": "x\n"})],
+    [],
+]
+
+
+def _extra_fields(doc, rng):
+    """The same messages with the fields real logs carry around the op (timestamps, traces,
+    metadata) and a shuffled key order."""
+    out = []
+    for m in doc:
+        m = dict(m)
+        m["timestamp"] = 1.6e12 + rng.random()
+        m["traces"] = [{"service": "alfred", "action": "start", "timestamp": 1.5e3}]
+        m["term"] = 1
+        m["metadata"] = {"batch": rng.random() < 0.5}
+        items = list(m.items())
+        rng.shuffle(items)
+        out.append(dict(items))
+    return out
+
+
+def test_fast_path_shapes_parse_identically():
+    _same([json.dumps(d) for d in FAST_DOCS] + [json.dumps(FAST_DOCS[1], ensure_ascii=False)])
+
+
+def test_kats_parse_identically():
+    """Every reference KAT log on the fast path parses identically; the others (markers,
+    rewrite annotates) are reported."""
+    on_path = 0
+    for k in load_kats():
+        try:
+            _same([json.dumps(k["messages"])])
+            on_path += 1
+        except NotOnGpuPath:
+            pass
+    assert on_path >= 3
+
+
+def test_generated_logs_parse_identically():
+    farm = _farm_messages()
+    rng = random.Random(5)
+    docs = [farm, farm[:3000], _extra_fields(farm[:2000], rng), FAST_DOCS[0]] * 3
+    texts = [json.dumps(d) for d in docs]
+    # whitespace and indentation variants
+    texts.append("[\n  " + ",\n  ".join(json.dumps(m, indent=1) for m in farm[:500]) + "\n]\n")
+    texts.append(" \t[ " + " , ".join(json.dumps(m, separators=(",", ":")) for m in farm[:500]) + " ] \r\n")
+    st = _same(texts)
+    assert st["n_msgs"] == sum(len(d) for d in docs) + 1000
+
+
+def test_observer_and_many_clients():
+    docs = [[_msg(f"client-{i % 250}", i + 1, i, {"type": 0, "pos1": 0, "seg": "a"}) for i in range(600)],
+            [_msg("me", 1, 0, None, type_="join"), _msg("X", 2, 0, {"type": 0, "pos1": 0, "seg": "a"})]]
+    _same([json.dumps(d) for d in docs], observer="me")
+
+
+OUTSIDE = [  # (message, reason) — every one must be reported, never parsed differently
+    (_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1}}}), "marker"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1.5}}), "float value"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": [1]}}), "nested value"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": "é"}}), "non-ASCII value"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"1": 1}}), "array-index key"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                      "combiningOp": {"name": "rewrite"}}), "combiningOp"),
+    (_msg("A", 1, 0, {"type": 1, "relativePos1": {"id": "m"}, "pos2": 1}), "relative position"),
+    (_msg("A", -1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "local op"),
+    (_msg("readonly", 1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "own op (ack)"),
+    (_msg("A", 1, 0, {"type": 3, "ops": [{"type": 3, "ops": []}]}), "nested group"),
+    (_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "a", "register": "r"}), "register"),
+    (_msg("A", 2 ** 31, 0, {"type": 1, "pos1": 0, "pos2": 1}), "seq beyond int32"),
+]
+
+
+@pytest.mark.parametrize("msg,why", OUTSIDE, ids=[w for _, w in OUTSIDE])
+def test_outside_the_fast_path_is_reported(msg, why):
+    docs = [json.dumps(FAST_DOCS[0]), json.dumps([msg])]
+    with pytest.raises(NotOnGpuPath) as e:
+        PackedJsonGpu(docs)
+    assert e.value.bad_doc == 1, why
+
+
+@pytest.mark.parametrize("text", ['[{"clientId": "A", "sequenceNumber": 1,', '[{"a":1}', '{"messages": []}',
+                                  '[{"sequenceNumber":1,"referenceSequenceNumber":0,"minimumSequenceNumber":0},]',
+                                  '[,{"sequenceNumber":1,"referenceSequenceNumber":0,"minimumSequenceNumber":0}]',
+                                  '[1]', '[] x', '', '[{"clientId":"A","clientId":"B","sequenceNumber":1,'
+                                  '"referenceSequenceNumber":0,"minimumSequenceNumber":0}]',
+                                  '[{"sequenceNumber":01,"referenceSequenceNumber":0,"minimumSequenceNumber":0}]'])
+def test_malformed_or_unusual_json_is_reported(text):
+    with pytest.raises(NotOnGpuPath) as e:
+        PackedJsonGpu(["[]", text])
+    assert e.value.bad_doc == 1
+
+
+def _replay_equal(b1, b2, n):
+    for d in range(n):
+        x, y = b1.doc(d), b2.doc(d)
+        assert x.status == y.status, d
+        assert x.digest() == y.digest(), d
+        if d % 3 == 0 and x.status == 0:
+            assert x.get_text() == y.get_text()
+            assert x.props_runs() == y.props_runs()
+            assert x.snapshot_v1() == y.snapshot_v1()
+
+
+def test_gpu_ingest_replays_like_host_ingest():
+    farm = _farm_messages()
+    docs = [farm, farm[:4000], FAST_DOCS[0], FAST_DOCS[1], [], farm[:7000]]
+    texts = [json.dumps(d) for d in docs]
+    with fa.ReplayBatch(len(docs)) as g, fa.ReplayBatch(len(docs)) as h:
+        info = g.ingest_json(texts, device="gpu")
+        assert info["path"] == "gpu" and info["n_msgs"] == sum(len(d) for d in docs)
+        h.ingest_json(texts, device="host")
+        g.run()
+        h.run()
+        _replay_equal(g, h, len(docs))
+
+
+def test_gpu_ingest_from_device_resident_json():
+    """The parse reads JSON already in HBM (a buffer of the library's own HIP runtime)."""
+    import ctypes as C
+
+    hip = C.CDLL("libamdhip64.so.7")
+    farm = _farm_messages()
+    docs = [farm[:5000], farm[:3000], FAST_DOCS[0]]
+    buf, off = fa.json_concat(docs)
+    ptr = C.c_void_p()
+    assert hip.hipMalloc(C.byref(ptr), C.c_size_t(len(buf) + 64)) == 0
+    try:
+        assert hip.hipMemset(ptr, 0, C.c_size_t(len(buf) + 64)) == 0
+        assert hip.hipMemcpy(ptr, buf, C.c_size_t(len(buf)), 1) == 0  # hipMemcpyHostToDevice
+        with fa.ReplayBatch(len(docs)) as g, fa.ReplayBatch(len(docs)) as h:
+            g.ingest_json_gpu(buf, off, d_json=ptr)
+            h.ingest_json([json.dumps(d) for d in docs], device="host")
+            g.run()
+            h.run()
+            _replay_equal(g, h, len(docs))
+    finally:
+        hip.hipFree(ptr)
+
+
+def test_auto_falls_back_to_the_host_parser():
+    docs = [json.dumps(FAST_DOCS[0]), json.dumps([OUTSIDE[0][0]])]
+    with fa.ReplayBatch(2) as g, fa.ReplayBatch(2) as h:
+        info = g.ingest_json(docs)
+        assert info["path"] == "host" and info["bad_doc"] == 1
+        h.ingest_json(docs, device="host")
+        g.run()
+        h.run()
+        _replay_equal(g, h, 2)
