@@ -435,3 +435,62 @@ def writer_records(ops: np.ndarray, off: np.ndarray, writer_of: np.ndarray):
     new_off = np.zeros(D + 1, np.int64)
     np.cumsum(new_counts, out=new_off[1:])
     return allr[order], new_off
+
+
+def records_to_json(ops: np.ndarray, off: np.ndarray, text: np.ndarray, props: np.ndarray, keys: list,
+                    values: list, clients) -> list:
+    """The inverse of packing for observer logs: per document the JSON text of its
+    ISequencedDocumentMessage array (single-record insert / remove / annotate messages and noops;
+    text segments, annotate props; GROUP_CONT members become one group message).  clients: the
+    long ids (one list for every document, or one per document).  Used to build JSON workloads
+    from generated logs (tools/bench_json.py)."""
+    ops = np.asarray(ops)
+    off = np.asarray(off, np.int64)
+    t16 = np.asarray(text, np.uint16)
+    kq = [json.dumps(k) for k in keys]
+    out = []
+    shared = clients and isinstance(clients[0], str)
+    typ = ops["type"].tolist()
+    cli = ops["client"].tolist()
+    flg = ops["flags"].tolist()
+    seq = ops["seq"].tolist()
+    ref = ops["ref_seq"].tolist()
+    msn = ops["msn"].tolist()
+    p1 = ops["pos1"].tolist()
+    p2 = ops["pos2"].tolist()
+    pay = ops["payload"].tolist()
+    plen = ops["payload_len"].tolist()
+    pk = props["key"].tolist() if len(props) else []
+    pv = props["value"].tolist() if len(props) else []
+    for d in range(len(off) - 1):
+        names = [json.dumps(c) for c in (clients if shared else clients[d])]
+        msgs, members = [], []
+        for i in range(int(off[d]), int(off[d + 1])):
+            t = typ[i]
+            if t == OP_NOOP:
+                c = None
+            elif t == 0:
+                s = t16[pay[i]:pay[i] + plen[i]].tobytes().decode("utf-16-le", "surrogatepass")
+                c = f'{{"type":0,"pos1":{p1[i]},"seg":{json.dumps(s)}}}'
+            elif t == 1:
+                c = f'{{"type":1,"pos1":{p1[i]},"pos2":{p2[i]}}}'
+            elif t == 2:
+                pr = ",".join(f"{kq[pk[q]]}:{values[pv[q]]}" for q in range(pay[i], pay[i] + plen[i]))
+                c = f'{{"type":2,"pos1":{p1[i]},"pos2":{p2[i]},"props":{{{pr}}}}}'
+            else:
+                raise UnsupportedOp(f"record type {t}")
+            if c is not None:
+                members.append(c)
+            if flg[i] & OPF_GROUP_CONT:
+                continue
+            head = (f'{{"clientId":{names[cli[i]]},"sequenceNumber":{seq[i]},"referenceSequenceNumber":{ref[i]},'
+                    f'"minimumSequenceNumber":{msn[i]},')
+            if not members:
+                msgs.append(head + '"type":"noop","contents":null}')
+            elif len(members) == 1:
+                msgs.append(head + f'"type":"op","contents":{members[0]}}}')
+            else:
+                msgs.append(head + f'"type":"op","contents":{{"type":3,"ops":[{",".join(members)}]}}}}')
+            members = []
+        out.append("[" + ",".join(msgs) + "]")
+    return out

@@ -62,6 +62,8 @@ for step in "$@"; do
     pmcf2) run pmcf2 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
     pmcw2) run pmcw2 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw2 -o run -- python3 -u bench.py --config 2 --steps 1 --warmup 0 --no-cpu ;;
     jsontests) run jsontests 300 python -u -m pytest tests/test_gpu_json.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    benchjson) run benchjson 600 python -u tools/bench_json.py ;;
+    benchjson3) run benchjson3 600 python -u tools/bench_json.py --docs 512 --ops 10000 --mix 55,35 ;;
     prof3) run prof3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     *) echo "unknown step $step" ;;
   esac
