@@ -45,7 +45,8 @@ struct Result {
 using TextLayout = std::function<int(const Result &, std::vector<uint64_t> &, uint64_t &)>;
 
 // Parse D documents: h_json (host copy, needed for the interning tables) with doc_off[D + 1];
-// d_json: the same bytes on the device (nullptr: uploaded here), readable 64 bytes past the end.
+// d_json: the same bytes on the device (nullptr: uploaded here), 4-byte aligned, readable 64 bytes
+// past the end.
 // On MT_OK *d_ops / *d_text / *d_props are device allocations owned by the caller.
 int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *d_json, const char *observer,
           void *stream, const TextLayout *install, mt_op **d_ops, uint16_t **d_text, uint64_t *text_words,

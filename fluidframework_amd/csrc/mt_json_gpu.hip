@@ -64,11 +64,14 @@ struct Params {
     int64_t D;
     // per message (region of document d starts at doc_off[d] / 64 + 2 d)
     uint32_t *m_start, *m_flags, *m_nrec, *m_ntext, *m_nprop, *m_recoff, *m_textoff, *m_propoff;
-    uint32_t *m_cloff, *m_cllen, *m_cid;
+    uint32_t *m_cloff, *m_cllen, *m_cid, *m_npops;
+    const int32_t *chunk_doc;        // count / write passes: one wave per 64 messages of a document
+    const uint32_t *chunk_first;
     // per document
     uint32_t *d_nmsg, *d_fail, *d_nrec, *d_ntext, *d_nprop, *d_npropops, *d_nnames, *d_nuk, *d_nuv;
     uint32_t *cl_ht;                 // kClientSlots per document
     uint32_t *nm_off, *nm_len;       // per message region: client id k's span at index k - 1
+    uint32_t *names;                 // per document 256 x {off, len}: ids 1.. (compact, for the host)
     const uint8_t *obs;              // observer long id (UTF-8) + "null" at obs + 256
     uint32_t obs_len;
     // write
@@ -112,83 +115,101 @@ extern "C" __global__ __launch_bounds__(64) void jg_scan_kernel(Params P) {
     const uint32_t len = (uint32_t)(P.doc_off[d + 1] - a);
     const uint64_t mb = mregion(P.doc_off, d);
     const uint32_t mcap = (uint32_t)(mregion(P.doc_off, d + 1) - mb);
-    const uint8_t *s = P.J + a;
+    // dword loads from the 4-byte-aligned address at or below the document's first byte: a step
+    // covers 1 KB as four coalesced 256-byte loads in flight; 64-byte chunk j of the step is
+    // rebuilt across the lanes with one shuffle (lane i: byte i of the chunk)
+    const uint32_t shift = (uint32_t)(a & 3);
+    const uint32_t *w32 = (const uint32_t *)(P.J + (a - shift));
+    const uint32_t span = len + shift;                 // bytes from the aligned start
+    const uint32_t nwords = (span + 3) >> 2;           // the last word may hold the next bytes (or pad)
     uint32_t depth = 0, nmsg = 0, commas = 0, fail = 0, bs_run = 0;
     bool started = false, ended = false, in_str = false;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (uint32_t pos = 0; pos < len && !fail; pos += 64) {
-        const uint32_t i = pos + (uint32_t)lane;
-        const int c = i < len ? s[i] : ' ';
-        const uint64_t bs = ballot(c == '\\');
-        // a quote is escaped by an odd run of backslashes right before it
-        const uint64_t nb = ~bs & below;
-        const uint32_t run = nb ? (uint32_t)(lane - 1 - (63 - __builtin_clzll(nb))) : (uint32_t)lane + bs_run;
-        uint64_t x = ballot(c == '"' && !(run & 1u));
-        x ^= x << 1;
-        x ^= x << 2;
-        x ^= x << 4;
-        x ^= x << 8;
-        x ^= x << 16;
-        x ^= x << 32;
-        const uint64_t S = in_str ? ~x : x;  // 1: inside a string (opening quote included)
-        in_str = (S >> 63) & 1ull;
-        bs_run = bs == ~0ull ? bs_run + 64u : (uint32_t)__builtin_clzll(~bs);
-        const bool ws = c == ' ' || c == '\t' || c == '\n' || c == '\r';
-        const uint64_t nonws = ballot(!ws) & ~S;
-        const uint64_t opn = ballot(c == '{' || c == '[') & ~S;
-        const uint64_t cls = ballot(c == '}' || c == ']') & ~S;
-        const uint64_t brace = ballot(c == '{' || c == '}');
-        const uint64_t comma = ballot(c == ',') & ~S;
-        uint64_t st = opn | cls;
-        uint32_t lo = 0;
-        // the bytes strictly between structural characters are at one depth: at depth 0 only
-        // whitespace, at depth 1 (between messages) whitespace and commas
-        auto segment = [&](uint32_t hi) {
-            if (hi > lo) {
-                const uint64_t m = (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
-                if (depth == 0 && (nonws & m)) fail |= kFSyntax;
-                if (depth == 1) {
-                    if (nonws & ~comma & m) fail |= kFSyntax;
-                    commas += (uint32_t)__builtin_popcountll(comma & m);
+    for (uint32_t base = 0; base < span && !fail; base += 1024) {
+        uint32_t w[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const uint32_t wi = (base >> 2) + 64u * (uint32_t)m + (uint32_t)lane;
+            w[m] = wi < nwords ? w32[wi] : 0x20202020u;
+        }
+        for (int j = 0; j < 16 && !fail; j++) {
+            const uint32_t pos0 = base + 64u * (uint32_t)j;
+            if (pos0 >= span) break;
+            const uint32_t word = __shfl(w[j >> 2], 16 * (j & 3) + (lane >> 2), 64);
+            const uint32_t at = pos0 + (uint32_t)lane;
+            const int c = (at >= shift && at < span) ? (int)((word >> (8 * (lane & 3))) & 0xFFu) : ' ';
+            const uint32_t pos = pos0 - shift;  // document position of lane 0 (may wrap below 0 in step 0)
+            const uint64_t bs = ballot(c == '\\');
+            // a quote is escaped by an odd run of backslashes right before it
+            const uint64_t nb = ~bs & below;
+            const uint32_t run = nb ? (uint32_t)(lane - 1 - (63 - __builtin_clzll(nb))) : (uint32_t)lane + bs_run;
+            uint64_t x = ballot(c == '"' && !(run & 1u));
+            x ^= x << 1;
+            x ^= x << 2;
+            x ^= x << 4;
+            x ^= x << 8;
+            x ^= x << 16;
+            x ^= x << 32;
+            const uint64_t S = in_str ? ~x : x;  // 1: inside a string (opening quote included)
+            in_str = (S >> 63) & 1ull;
+            bs_run = bs == ~0ull ? bs_run + 64u : (uint32_t)__builtin_clzll(~bs);
+            const bool ws = c == ' ' || c == '\t' || c == '\n' || c == '\r';
+            const uint64_t nonws = ballot(!ws) & ~S;
+            const uint64_t opn = ballot(c == '{' || c == '[') & ~S;
+            const uint64_t cls = ballot(c == '}' || c == ']') & ~S;
+            const uint64_t brace = ballot(c == '{' || c == '}');
+            const uint64_t comma = ballot(c == ',') & ~S;
+            uint64_t st = opn | cls;
+            uint32_t lo = 0;
+            // the bytes strictly between structural characters are at one depth: at depth 0 only
+            // whitespace, at depth 1 (between messages) whitespace and commas
+            auto segment = [&](uint32_t hi) {
+                if (hi > lo) {
+                    const uint64_t m = (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
+                    if (depth == 0 && (nonws & m)) fail |= kFSyntax;
+                    if (depth == 1) {
+                        if (nonws & ~comma & m) fail |= kFSyntax;
+                        commas += (uint32_t)__builtin_popcountll(comma & m);
+                    }
                 }
-            }
-        };
-        while (st && !fail) {
-            const uint32_t t = (uint32_t)__builtin_ctzll(st);
-            st &= st - 1;
-            segment(t);
-            lo = t + 1;
-            const bool o = (opn >> t) & 1ull, br = (brace >> t) & 1ull;
-            if (ended) {
-                fail |= kFSyntax;
-                break;
-            }
-            if (o) {
-                if (depth == 0) {
-                    if (started || br) fail |= kFSyntax;  // the log is one array
-                    started = true;
-                } else if (depth == 1) {
-                    if (!br) fail |= kFSyntax;  // a message must be an object
-                    if (commas != (nmsg ? 1u : 0u)) fail |= kFSyntax;
-                    commas = 0;
-                    if (nmsg >= mcap) fail |= kFCap;
-                    else if (lane == 0) P.m_start[mb + nmsg] = pos + t;
-                    nmsg++;
-                }
-                depth++;
-            } else {
-                if (depth == 0) {
+            };
+            while (st && !fail) {
+                const uint32_t t = (uint32_t)__builtin_ctzll(st);
+                st &= st - 1;
+                segment(t);
+                lo = t + 1;
+                const bool o = (opn >> t) & 1ull, br = (brace >> t) & 1ull;
+                if (ended) {
                     fail |= kFSyntax;
                     break;
                 }
-                depth--;
-                if (depth == 0) {
-                    if (br || commas) fail |= kFSyntax;  // ']' closes the log, no trailing comma
-                    ended = true;
+                if (o) {
+                    if (depth == 0) {
+                        if (started || br) fail |= kFSyntax;  // the log is one array
+                        started = true;
+                    } else if (depth == 1) {
+                        if (!br) fail |= kFSyntax;  // a message must be an object
+                        if (commas != (nmsg ? 1u : 0u)) fail |= kFSyntax;
+                        commas = 0;
+                        if (nmsg >= mcap) fail |= kFCap;
+                        else if (lane == 0) P.m_start[mb + nmsg] = pos + t;
+                        nmsg++;
+                    }
+                    depth++;
+                } else {
+                    if (depth == 0) {
+                        fail |= kFSyntax;
+                        break;
+                    }
+                    depth--;
+                    if (depth == 0) {
+                        if (br || commas) fail |= kFSyntax;  // ']' closes the log, no trailing comma
+                        ended = true;
+                    }
                 }
             }
+            if (!fail) segment(64);
         }
-        if (!fail) segment(64);
     }
     if (!started || !ended || in_str) fail |= kFSyntax;
     if (lane == 0) {
@@ -199,21 +220,50 @@ extern "C" __global__ __launch_bounds__(64) void jg_scan_kernel(Params P) {
 
 // ---------------------------------------------------------------- lane-serial JSON reading
 struct Rd {
+    // a lane's cursor over one document; bytes come through a 16-byte window (one aligned 128-bit
+    // load per 16 bytes instead of a load per byte)
     const uint8_t *s;
     uint32_t p, n;
-    __device__ int at() const { return p < n ? (int)s[p] : -1; }
+    uint32_t sh, wb = 0xFFFFFFFFu;
+    uint4 w;
+    __device__ Rd(const uint8_t *s_, uint32_t p_, uint32_t n_)
+        : s(s_), p(p_), n(n_), sh((uint32_t)((uintptr_t)s_ & 15u)) {}
+    __device__ uint32_t b(uint32_t k) {
+        const uint32_t ak = k + sh, blk = ak & ~15u;
+        if (blk != wb) {
+            wb = blk;
+            w = *(const uint4 *)(s - sh + blk);
+        }
+        const uint32_t o = ak & 15u;
+        const uint32_t word = o < 8 ? (o < 4 ? w.x : w.y) : (o < 12 ? w.z : w.w);
+        return (word >> ((o & 3u) * 8u)) & 0xFFu;
+    }
+    __device__ int at() { return p < n ? (int)b(p) : -1; }
     __device__ void ws() {
         while (p < n) {
-            const uint8_t c = s[p];
+            const uint32_t c = b(p);
             if (c == ' ' || c == '\t' || c == '\n' || c == '\r') p++;
             else break;
         }
     }
-    __device__ bool lit(const char *w, uint32_t k) {
+    __device__ bool lit(const char *wd, uint32_t k) {
         if (n - p < k) return false;
         for (uint32_t i = 0; i < k; i++)
-            if (s[p + i] != (uint8_t)w[i]) return false;
+            if (b(p + i) != (uint8_t)wd[i]) return false;
         p += k;
+        return true;
+    }
+    // the key / string span [o, o + l) equals the C string wd
+    __device__ bool is(uint32_t o, uint32_t l, const char *wd) {
+        uint32_t i = 0;
+        for (; wd[i]; i++)
+            if (i >= l || b(o + i) != (uint8_t)wd[i]) return false;
+        return i == l;
+    }
+    __device__ bool eq(uint32_t o1, uint32_t l1, uint32_t o2, uint32_t l2) {
+        if (l1 != l2) return false;
+        for (uint32_t i = 0; i < l1; i++)
+            if (b(o1 + i) != b(o2 + i)) return false;
         return true;
     }
 };
@@ -234,17 +284,17 @@ __device__ bool str_raw(Rd &r, uint32_t &off, uint32_t &len, bool &plain) {
     plain = true;
     for (;;) {
         if (r.p >= r.n) return false;
-        const uint8_t c = r.s[r.p];
+        const uint8_t c = r.b(r.p);
         if (c == '"') break;
         if (c < 0x20) return false;
         if (c == '\\') {
             plain = false;
             if (++r.p >= r.n) return false;
-            const uint8_t e = r.s[r.p];
+            const uint8_t e = r.b(r.p);
             if (e == 'u') {
                 if (r.n - r.p < 5) return false;
                 for (int i = 1; i <= 4; i++)
-                    if (hexv(r.s[r.p + i]) < 0) return false;
+                    if (hexv(r.b(r.p + i)) < 0) return false;
                 r.p += 4;
             } else if (!(e == '"' || e == '\\' || e == '/' || e == 'b' || e == 'f' || e == 'n' || e == 'r' ||
                          e == 't')) {
@@ -277,11 +327,11 @@ __device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bo
     };
     for (;;) {
         if (r.p >= r.n) return false;
-        const uint8_t c = r.s[r.p];
+        const uint8_t c = r.b(r.p);
         if (c == '"') break;
         if (c == '\\') {
             if (++r.p >= r.n) return false;
-            const uint8_t e = r.s[r.p];
+            const uint8_t e = r.b(r.p);
             switch (e) {
                 case '"': put('"'); break;
                 case '\\': put('\\'); break;
@@ -295,7 +345,7 @@ __device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bo
                     if (r.n - r.p < 5) return false;
                     uint32_t v = 0;
                     for (int i = 1; i <= 4; i++) {
-                        const int h = hexv(r.s[r.p + i]);
+                        const int h = hexv(r.b(r.p + i));
                         if (h < 0) return false;
                         v = v * 16 + (uint32_t)h;
                     }
@@ -316,7 +366,7 @@ __device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bo
             if (!k || r.n - r.p < (uint32_t)k) return false;
             uint32_t cp = c & (k == 2 ? 0x1Fu : k == 3 ? 0x0Fu : 0x07u);
             for (int i = 1; i < k; i++) {
-                const uint8_t b = r.s[r.p + i];
+                const uint8_t b = r.b(r.p + i);
                 if ((b & 0xC0) != 0x80) return false;
                 cp = (cp << 6) | (b & 0x3Fu);
             }
@@ -340,40 +390,40 @@ __device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bo
 __device__ int num_tok(Rd &r, int64_t &v, uint32_t &ndig) {
     uint32_t p = r.p;
     bool neg = false;
-    if (p < r.n && r.s[p] == '-') {
+    if (p < r.n && r.b(p) == '-') {
         neg = true;
         p++;
     }
-    if (p >= r.n || !is_digit(r.s[p])) return 0;
+    if (p >= r.n || !is_digit(r.b(p))) return 0;
     bool canon = true;
     int64_t acc = 0;
     ndig = 0;
-    if (r.s[p] == '0') {
+    if (r.b(p) == '0') {
         p++;
         ndig = 1;
-        if (p < r.n && is_digit(r.s[p])) return 0;
+        if (p < r.n && is_digit(r.b(p))) return 0;
     } else {
-        while (p < r.n && is_digit(r.s[p])) {
-            if (ndig < 18) acc = acc * 10 + (r.s[p] - '0');
+        while (p < r.n && is_digit(r.b(p))) {
+            if (ndig < 18) acc = acc * 10 + (r.b(p) - '0');
             ndig++;
             p++;
         }
     }
-    if (p < r.n && r.s[p] == '.') {
+    if (p < r.n && r.b(p) == '.') {
         canon = false;
         p++;
-        if (p >= r.n || !is_digit(r.s[p])) return 0;
-        while (p < r.n && is_digit(r.s[p])) p++;
+        if (p >= r.n || !is_digit(r.b(p))) return 0;
+        while (p < r.n && is_digit(r.b(p))) p++;
     }
-    if (p < r.n && (r.s[p] == 'e' || r.s[p] == 'E')) {
+    if (p < r.n && (r.b(p) == 'e' || r.b(p) == 'E')) {
         canon = false;
         p++;
-        if (p < r.n && (r.s[p] == '+' || r.s[p] == '-')) p++;
-        if (p >= r.n || !is_digit(r.s[p])) return 0;
-        while (p < r.n && is_digit(r.s[p])) p++;
+        if (p < r.n && (r.b(p) == '+' || r.b(p) == '-')) p++;
+        if (p >= r.n || !is_digit(r.b(p))) return 0;
+        while (p < r.n && is_digit(r.b(p))) p++;
     }
     if (p < r.n) {  // the host's number scan is greedy over [0-9.eE+-]
-        const uint8_t c = r.s[p];
+        const uint8_t c = r.b(p);
         if (is_digit(c) || c == '.' || c == 'e' || c == 'E' || c == '+' || c == '-') return 0;
     }
     if (neg && ndig == 1 && acc == 0 && canon) canon = false;  // -0
@@ -458,12 +508,6 @@ __device__ __forceinline__ bool span_eq(const uint8_t *a, uint32_t la, const uin
         if (a[i] != b[i]) return false;
     return true;
 }
-__device__ __forceinline__ bool key_is(const uint8_t *k, uint32_t kl, const char *w) {
-    uint32_t i = 0;
-    for (; w[i]; i++)
-        if (i >= kl || k[i] != (uint8_t)w[i]) return false;
-    return i == kl;
-}
 __device__ __forceinline__ uint32_t fnv32(const uint8_t *p, uint32_t n) {
     uint32_t h = 2166136261u;
     for (uint32_t i = 0; i < n; i++) h = (h ^ p[i]) * 16777619u;
@@ -514,14 +558,13 @@ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
         if (r.at() != ':') return kFSyntax;
         r.p++;
         r.ws();
-        const uint8_t *k = r.s + ko;
         uint32_t bit = 0;
-        if (key_is(k, kl, "type")) bit = kOType;
-        else if (key_is(k, kl, "pos1")) bit = kOPos1;
-        else if (key_is(k, kl, "pos2")) bit = kOPos2;
-        else if (key_is(k, kl, "seg")) bit = kOSeg;
-        else if (key_is(k, kl, "props")) bit = kOProps;
-        else if (key_is(k, kl, "ops")) bit = kOOps;
+        if (r.is(ko, kl, "type")) bit = kOType;
+        else if (r.is(ko, kl, "pos1")) bit = kOPos1;
+        else if (r.is(ko, kl, "pos2")) bit = kOPos2;
+        else if (r.is(ko, kl, "seg")) bit = kOSeg;
+        else if (r.is(ko, kl, "props")) bit = kOProps;
+        else if (r.is(ko, kl, "ops")) bit = kOOps;
         if (bit) {
             if (op.seen & bit) return kFShape;  // a repeated key: the host keeps the last value
             op.seen |= bit;
@@ -542,7 +585,7 @@ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
             if (!bit) {
                 // combiningOp (a falsy one is ignored), register (null is absent): anything else
                 // and relative positions leave the fast path
-                const bool cop = key_is(k, kl, "combiningOp"), reg = key_is(k, kl, "register");
+                const bool cop = r.is(ko, kl, "combiningOp"), reg = r.is(ko, kl, "register");
                 if (cop || reg) {
                     if (r.lit("null", 4) || (cop && r.lit("false", 5))) {
                         if (extra & (cop ? 1u : 2u)) return kFShape;
@@ -551,7 +594,7 @@ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
                     }
                     return kFShape;
                 }
-                if (key_is(k, kl, "relativePos1") || key_is(k, kl, "relativePos2")) return kFShape;
+                if (r.is(ko, kl, "relativePos1") || r.is(ko, kl, "relativePos2")) return kFShape;
             }
             if (!skip_value(r)) return kFSyntax;
         }
@@ -590,10 +633,10 @@ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const Ctx &cx)
         if (!str_raw(r, ko, kl, plain)) return kFSyntax;
         if (!plain) return kFShape;
         bool digits = kl > 0;
-        for (uint32_t i = 0; i < kl && digits; i++) digits = is_digit(r.s[ko + i]);
+        for (uint32_t i = 0; i < kl && digits; i++) digits = is_digit(r.b(ko + i));
         if (digits) return kFShape;
         for (uint32_t j = 0; j < np; j++)
-            if (span_eq(r.s + koff[j], klen[j], r.s + ko, kl)) return kFShape;
+            if (r.eq(koff[j], klen[j], ko, kl)) return kFShape;
         if (np >= (uint32_t)kMaxProps) return kFShape;
         koff[np] = ko;
         klen[np] = kl;
@@ -682,15 +725,15 @@ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, cons
                 if (rs.at() != ':') return kFSyntax;
                 rs.p++;
                 rs.ws();
-                if (key_is(s + ko, kl, "text")) {
+                if (rs.is(ko, kl, "text")) {
                     if (has_text || rs.at() != '"') return kFShape;
                     has_text = true;
                     text_p = rs.p;
-                } else if (key_is(s + ko, kl, "props")) {
+                } else if (rs.is(ko, kl, "props")) {
                     if (has_props) return kFShape;
                     has_props = true;
                     props_p = rs.p;
-                } else if (key_is(s + ko, kl, "marker")) {
+                } else if (rs.is(ko, kl, "marker")) {
                     return kFShape;  // markers: the host path (marker ids, tile labels)
                 }
                 if (!skip_value(rs)) return kFSyntax;
@@ -780,14 +823,13 @@ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0, MsgOut 
         if (r.at() != ':') return kFSyntax;
         r.p++;
         r.ws();
-        const uint8_t *k = s + ko;
         uint32_t bit = 0;
-        if (key_is(k, kl, "clientId")) bit = kCl;
-        else if (key_is(k, kl, "sequenceNumber")) bit = kSeq;
-        else if (key_is(k, kl, "referenceSequenceNumber")) bit = kRef;
-        else if (key_is(k, kl, "minimumSequenceNumber")) bit = kMsn;
-        else if (key_is(k, kl, "type")) bit = kTy;
-        else if (key_is(k, kl, "contents")) bit = kCo;
+        if (r.is(ko, kl, "clientId")) bit = kCl;
+        else if (r.is(ko, kl, "sequenceNumber")) bit = kSeq;
+        else if (r.is(ko, kl, "referenceSequenceNumber")) bit = kRef;
+        else if (r.is(ko, kl, "minimumSequenceNumber")) bit = kMsn;
+        else if (r.is(ko, kl, "type")) bit = kTy;
+        else if (r.is(ko, kl, "contents")) bit = kCo;
         if (bit) {
             if (seen & bit) return kFShape;
             seen |= bit;
@@ -811,7 +853,7 @@ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0, MsgOut 
             bool pl;
             if (!str_raw(r, o, l, pl)) return kFSyntax;
             if (!pl) return kFShape;
-            is_op = l == 2 && s[o] == 'o' && s[o + 1] == 'p';
+            is_op = l == 2 && r.b(o) == 'o' && r.b(o + 1) == 'p';
         } else {
             if (bit == kCo) contents_p = r.p;
             // clientId / type of another JSON type: "null" / not an op (the host's rules)
@@ -887,76 +929,84 @@ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0, MsgOut 
 }
 
 // ---------------------------------------------------------------- stage 2 / 4: parse passes
+// one wavefront per 64 messages of a document (chunk_doc / chunk_first), so a batch of long
+// documents fills the chip; the count pass stores per-message counts, jg_offsets_kernel turns them
+// into each message's offsets in its document, the write pass writes there
 template <bool W>
-__device__ void parse_doc(const Params &P) {
-    const int64_t d = blockIdx.x;
-    if (d >= P.D || P.d_fail[d]) return;
+__device__ void parse_chunk(const Params &P) {
+    const int64_t c = blockIdx.x;
+    const int64_t d = P.chunk_doc[c];
+    if (P.d_fail[d]) return;
     const int lane = lane_id();
     const int64_t a = P.doc_off[d];
     const uint32_t len = (uint32_t)(P.doc_off[d + 1] - a);
     const uint8_t *s = P.J + a;
     const uint64_t mb = mregion(P.doc_off, d);
     const uint32_t nmsg = P.d_nmsg[d];
-    uint32_t sr = 0, st = 0, sp = 0, so = 0, fail = 0;
+    const uint32_t i = P.chunk_first[c] + (uint32_t)lane;
+    if (i >= nmsg) return;
+    const uint64_t m = mb + i;
+    MsgOut mo;
+    Ctx cx;
+    if (W) {
+        cx.ops = P.ops + P.op_base[d] + P.m_recoff[m];
+        cx.text = P.text + P.text_dst[d] + P.m_textoff[m];
+        cx.pay = P.text_pay[d] + P.m_textoff[m];
+        cx.gprop = P.prop_base[d] + P.m_propoff[m];
+        cx.pk_off = P.pk_off;
+        cx.pk_len = P.pk_len;
+        cx.pv_off = P.pv_off;
+        cx.pv_len = P.pv_len;
+        cx.cid = (uint8_t)P.m_cid[m];
+        cx.install = P.install != 0;
+    }
+    const uint32_t f = parse_msg<W>(s, len, P.m_start[m], mo, cx);
+    if (f) atomicOr(P.d_fail + d, f);
+    if (!W) {
+        P.m_flags[m] = mo.flags;
+        P.m_nrec[m] = mo.nrec;
+        P.m_ntext[m] = mo.ntext;
+        P.m_nprop[m] = mo.nprop;
+        P.m_npops[m] = mo.npropops;
+        P.m_cloff[m] = mo.cl_off;
+        P.m_cllen[m] = mo.cl_len;
+    }
+}
+extern "C" __global__ __launch_bounds__(64) void jg_count_kernel(Params P) { parse_chunk<false>(P); }
+extern "C" __global__ __launch_bounds__(64) void jg_write_kernel(Params P) { parse_chunk<true>(P); }
+
+// per document: message offsets (exclusive prefix sums of the counts) and the totals
+extern "C" __global__ __launch_bounds__(64) void jg_offsets_kernel(Params P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D || P.d_fail[d]) return;
+    const int lane = lane_id();
+    const uint64_t mb = mregion(P.doc_off, d);
+    const uint32_t nmsg = P.d_nmsg[d];
+    uint32_t sr = 0, st = 0, sp = 0, so = 0;
     for (uint32_t i0 = 0; i0 < nmsg; i0 += 64) {
         const uint32_t i = i0 + (uint32_t)lane;
         const bool valid = i < nmsg;
-        MsgOut mo;
-        uint32_t f = 0;
+        const uint64_t m = mb + i;
+        const uint32_t nr = valid ? P.m_nrec[m] : 0u, nt = valid ? P.m_ntext[m] : 0u;
+        const uint32_t np = valid ? P.m_nprop[m] : 0u, no = valid ? P.m_npops[m] : 0u;
+        const uint32_t ir = wave_incl(nr), it = wave_incl(nt), ip = wave_incl(np), io = wave_incl(no);
         if (valid) {
-            const uint64_t m = mb + i;
-            Ctx cx;
-            if (W) {
-                cx.ops = P.ops + P.op_base[d] + P.m_recoff[m];
-                cx.text = P.text + P.text_dst[d] + P.m_textoff[m];
-                cx.pay = P.text_pay[d] + P.m_textoff[m];
-                cx.gprop = P.prop_base[d] + P.m_propoff[m];
-                cx.pk_off = P.pk_off;
-                cx.pk_len = P.pk_len;
-                cx.pv_off = P.pv_off;
-                cx.pv_len = P.pv_len;
-                cx.cid = (uint8_t)P.m_cid[m];
-                cx.install = P.install != 0;
-            }
-            f = parse_msg<W>(s, len, P.m_start[m], mo, cx);
+            P.m_recoff[m] = sr + ir - nr;
+            P.m_textoff[m] = st + it - nt;
+            P.m_propoff[m] = sp + ip - np;
         }
-        if (!W) {
-            const uint32_t ir = wave_incl(mo.nrec), it = wave_incl(mo.ntext), ip = wave_incl(mo.nprop);
-            const uint32_t io = wave_incl(mo.npropops);
-            if (valid) {
-                const uint64_t m = mb + i;
-                P.m_flags[m] = mo.flags;
-                P.m_nrec[m] = mo.nrec;
-                P.m_ntext[m] = mo.ntext;
-                P.m_nprop[m] = mo.nprop;
-                P.m_recoff[m] = sr + ir - mo.nrec;
-                P.m_textoff[m] = st + it - mo.ntext;
-                P.m_propoff[m] = sp + ip - mo.nprop;
-                P.m_cloff[m] = mo.cl_off;
-                P.m_cllen[m] = mo.cl_len;
-            }
-            sr += __shfl(ir, 63, 64);
-            st += __shfl(it, 63, 64);
-            sp += __shfl(ip, 63, 64);
-            so += __shfl(io, 63, 64);
-        }
-        // fail bits of the document (any lane)
-        for (int o = 32; o > 0; o >>= 1) f |= __shfl_xor(f, o, 64);
-        fail |= f;
-        if (fail) break;
+        sr += __shfl(ir, 63, 64);
+        st += __shfl(it, 63, 64);
+        sp += __shfl(ip, 63, 64);
+        so += __shfl(io, 63, 64);
     }
     if (lane == 0) {
-        if (!W) {
-            P.d_nrec[d] = sr;
-            P.d_ntext[d] = st;
-            P.d_nprop[d] = sp;
-            P.d_npropops[d] = so;
-        }
-        if (fail) P.d_fail[d] = fail;
+        P.d_nrec[d] = sr;
+        P.d_ntext[d] = st;
+        P.d_nprop[d] = sp;
+        P.d_npropops[d] = so;
     }
 }
-extern "C" __global__ __launch_bounds__(64) void jg_count_kernel(Params P) { parse_doc<false>(P); }
-extern "C" __global__ __launch_bounds__(64) void jg_write_kernel(Params P) { parse_doc<true>(P); }
 
 // ---------------------------------------------------------------- first-appearance interning
 // Entries are indices (+1) into the document's spans; a slot keeps the smallest index holding
@@ -1063,6 +1113,11 @@ extern "C" __global__ __launch_bounds__(64) void jg_clients_kernel(Params P) {
     const uint32_t cnt = intern(tab, kClientSlots, S, nmsg, 1u, P.m_cid, P.nm_off, P.nm_len, is_obs);
     for (int o = 32; o > 0; o >>= 1) fail |= __shfl_xor(fail, o, 64);
     if (cnt == 0xFFFFFFFFu || cnt + 1 > (uint32_t)MT_MAX_CLIENTS) fail |= kFClients;
+    __syncthreads();
+    for (uint32_t k = (uint32_t)lane; !fail && k < cnt; k += 64) {
+        P.names[(uint64_t)d * 512 + 2 * k] = P.nm_off[mb + k];
+        P.names[(uint64_t)d * 512 + 2 * k + 1] = P.nm_len[mb + k];
+    }
     if (lane == 0) {
         P.d_nnames[d] = cnt == 0xFFFFFFFFu ? 0u : cnt + 1;
         if (fail) P.d_fail[d] = fail;
@@ -1193,7 +1248,8 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     P.doc_off = d_off;
     const size_t M = (size_t)(total / 64 + 2 * (uint64_t)D + 2);
     uint32_t **marr[] = {&P.m_start, &P.m_flags, &P.m_nrec, &P.m_ntext, &P.m_nprop, &P.m_recoff,
-                         &P.m_textoff, &P.m_propoff, &P.m_cloff, &P.m_cllen, &P.m_cid, &P.nm_off, &P.nm_len};
+                         &P.m_textoff, &P.m_propoff, &P.m_cloff, &P.m_cllen, &P.m_cid, &P.nm_off, &P.nm_len,
+                         &P.m_npops};
     for (uint32_t **a : marr) JGCHK(B.get(a, M));
     uint32_t **darr[] = {&P.d_nmsg, &P.d_fail, &P.d_nrec, &P.d_ntext, &P.d_nprop, &P.d_npropops,
                          &P.d_nnames, &P.d_nuk, &P.d_nuv};
@@ -1202,6 +1258,7 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(hipMemsetAsync(P.d_ntext, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_nprop, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_npropops, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
+    JGCHK(B.get(&P.names, (size_t)D * 512));
     JGCHK(B.get(&P.cl_ht, (size_t)D * kClientSlots));
     JGCHK(hipMemsetAsync(P.cl_ht, 0, 4 * (size_t)D * kClientSlots, s));
     {
@@ -1218,12 +1275,34 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     void *args[] = {&P};
     JGCHK(hipEventRecord(ev[0], s));
     if (D) JGCHK(hipLaunchKernel((const void *)jg_scan_kernel, dim3(grid), dim3(64), args, 0, s));
+    std::vector<uint32_t> nmsg;
+    JGCHK(dl(nmsg, P.d_nmsg, (size_t)D, s));
+    std::vector<int32_t> chunk_doc;
+    std::vector<uint32_t> chunk_first;
+    for (int64_t d = 0; d < D; d++)
+        for (uint32_t i = 0; i < nmsg[(size_t)d]; i += 64) {
+            chunk_doc.push_back((int32_t)d);
+            chunk_first.push_back(i);
+        }
+    int32_t *d_cdoc = nullptr;
+    uint32_t *d_cfirst = nullptr;
+    JGCHK(B.get(&d_cdoc, chunk_doc.size()));
+    JGCHK(B.get(&d_cfirst, chunk_doc.size()));
+    if (!chunk_doc.empty()) {
+        JGCHK(hipMemcpyAsync(d_cdoc, chunk_doc.data(), 4 * chunk_doc.size(), hipMemcpyHostToDevice, s));
+        JGCHK(hipMemcpyAsync(d_cfirst, chunk_first.data(), 4 * chunk_first.size(), hipMemcpyHostToDevice, s));
+    }
+    P.chunk_doc = d_cdoc;
+    P.chunk_first = d_cfirst;
+    const unsigned cgrid = (unsigned)chunk_doc.size();
+    void *argc[] = {&P};
     JGCHK(hipEventRecord(ev[1], s));
-    if (D) JGCHK(hipLaunchKernel((const void *)jg_count_kernel, dim3(grid), dim3(64), args, 0, s));
+    if (cgrid) JGCHK(hipLaunchKernel((const void *)jg_count_kernel, dim3(cgrid), dim3(64), argc, 0, s));
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_offsets_kernel, dim3(grid), dim3(64), argc, 0, s));
     JGCHK(hipEventRecord(ev[2], s));
-    if (D) JGCHK(hipLaunchKernel((const void *)jg_clients_kernel, dim3(grid), dim3(64), args, 0, s));
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_clients_kernel, dim3(grid), dim3(64), argc, 0, s));
     JGCHK(hipEventRecord(ev[3], s));
-    std::vector<uint32_t> fail, nrec, ntext, nprop, npops, nmsg;
+    std::vector<uint32_t> fail, nrec, ntext, nprop, npops;
     JGCHK(dl(fail, P.d_fail, (size_t)D, s));
     for (int64_t d = 0; d < D; d++)
         if (fail[(size_t)d]) {
@@ -1236,7 +1315,6 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(dl(ntext, P.d_ntext, (size_t)D, s));
     JGCHK(dl(nprop, P.d_nprop, (size_t)D, s));
     JGCHK(dl(npops, P.d_npropops, (size_t)D, s));
-    JGCHK(dl(nmsg, P.d_nmsg, (size_t)D, s));
     // batch layout: records and prop records back to back in document order
     res.doc_op_off.assign((size_t)D + 1, 0);
     std::vector<int64_t> op_base((size_t)D);
@@ -1324,11 +1402,11 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     P.ht_base = d_htb;
     P.ht_cap = d_htc;
     void *args2[] = {&P};
-    if (D) JGCHK(hipLaunchKernel((const void *)jg_write_kernel, dim3(grid), dim3(64), args2, 0, s));
+    if (cgrid) JGCHK(hipLaunchKernel((const void *)jg_write_kernel, dim3(cgrid), dim3(64), args2, 0, s));
     JGCHK(hipEventRecord(ev[4], s));
     if (D) JGCHK(hipLaunchKernel((const void *)jg_props_kernel, dim3(grid), dim3(64), args2, 0, s));
     // host: batch-wide tables in first-appearance order (document order, then record order)
-    std::vector<uint32_t> nuk, nuv, uko, ukl, uvo, uvl, nnames, cl_off, cl_len;
+    std::vector<uint32_t> nuk, nuv, uko, ukl, uvo, uvl, nnames;
     JGCHK(dl(nuk, P.d_nuk, (size_t)D, s));
     JGCHK(dl(nuv, P.d_nuv, (size_t)D, s));
     JGCHK(dl(uko, P.uk_off, (size_t)pp, s));
@@ -1336,8 +1414,8 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(dl(uvo, P.uv_off, (size_t)pp, s));
     JGCHK(dl(uvl, P.uv_len, (size_t)pp, s));
     JGCHK(dl(nnames, P.d_nnames, (size_t)D, s));
-    JGCHK(dl(cl_off, P.nm_off, M, s));  // jg_clients_kernel: names' spans by id - 1
-    JGCHK(dl(cl_len, P.nm_len, M, s));
+    std::vector<uint32_t> names;
+    JGCHK(dl(names, P.names, (size_t)D * 512, s));  // jg_clients_kernel: names' spans by id - 1
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<uint32_t> kmap((size_t)std::max<uint64_t>(pp, 1)), vmap((size_t)std::max<uint64_t>(pp, 1));
     std::unordered_map<std::string, uint32_t> kid, vid{{"null", 0u}};
@@ -1366,10 +1444,10 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
         }
         auto &nm = res.clients[(size_t)d];
         nm.assign(1, obs);
-        const uint64_t mb = (uint64_t)(doc_off[d] / 64 + 2 * d);
+        const uint32_t *nd = names.data() + (size_t)d * 512;
         for (uint32_t i = 1; i < nnames[(size_t)d]; i++) {
-            const uint32_t o = cl_off[mb + i - 1];
-            nm.push_back(o == kNullSpan ? std::string("null") : std::string(js + o, cl_len[mb + i - 1]));
+            const uint32_t o = nd[2 * (i - 1)];
+            nm.push_back(o == kNullSpan ? std::string("null") : std::string(js + o, nd[2 * (i - 1) + 1]));
         }
     }
     for (const auto &k : res.keys)

@@ -54,7 +54,7 @@ enum mt_status_code {
     MT_INVALID_POS = 1,  /* "MergeTree insert failed" */
     MT_SEQ_ORDER = 2,    /* sequence number went backwards */
     MT_MSN_ORDER = 3,    /* minimumSequenceNumber went backwards / above seq */
-    MT_UNSUPPORTED = 4,  /* op outside the observer path or device limits (> 32 clients) */
+    MT_UNSUPPORTED = 4,  /* op outside the device model or limits (> 253 clients) */
     MT_BAD_INPUT = 5,
     MT_CAPACITY = 6,     /* document exceeded the largest device capacity class */
     MT_INTERNAL = 7,
@@ -134,7 +134,7 @@ MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p);
    document returns MT_UNSUPPORTED with *bad_doc set and nothing changed: parse it with
    mt_pack_json (the bindings' ingest_json does).  json: the documents back to back, document d =
    json[doc_off[d] .. doc_off[d+1]).  d_json: the same bytes already on the device (NULL: copied
-   here), readable 64 bytes past the end.  Replaces the host parse of Client.applyMsg's input
+   here), 4-byte aligned and readable 64 bytes past the end.  Replaces the host parse of Client.applyMsg's input
    (clientReplayTool.ts:194-252 feeding client.ts:797-819). */
 typedef struct mt_json_gpu_stats {
     double ms_scan, ms_count, ms_clients, ms_write, ms_props; /* device stages (hipEvents) */

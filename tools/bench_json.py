@@ -73,7 +73,10 @@ def main():
         dig_g = np.array([bg.doc(d).digest() for d in range(args.docs)], np.uint64)
         st_g = bg.counters()["status"].copy()
     hip.hipFree(ptr)
-    threads = args.threads or len(os.sched_getaffinity(0))
+    sys.path.insert(0, str(ROOT))
+    from bench import usable_cores
+
+    threads = args.threads or usable_cores()
     host = []
     with fa.ReplayBatch(args.docs) as bh:
         for k in range(2):
