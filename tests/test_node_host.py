@@ -115,7 +115,8 @@ const { ReplayBatch } = require('./fluidframework_amd/js');
     r = _node(code)
     assert r.returncode == 0, r.stderr
     got = json.loads(r.stdout)
-    assert got["len"] == 10 and got["prec"]["pos"] == 0 and got["next"]["pos"] == 6 and got["none"]
+    # getText() holds the text segments only; each marker is length 1 in positions
+    assert got["len"] == 7 and got["prec"]["pos"] == 0 and got["next"]["pos"] == 6 and got["none"]
     assert got["prec"]["props"] == {"referenceTileLabels": ["EOP"], "markerId": "some-id"}
     assert got["wtext"] == "Xc"
     od = O.Doc()
