@@ -199,3 +199,72 @@ def test_auto_falls_back_to_the_host_parser():
         g.run()
         h.run()
         _replay_equal(g, h, 2)
+
+
+def _fuzz_doc(rng: random.Random, n: int) -> str:
+    """A random observer log on (and sometimes just off) the fast path, as JSON text with random
+    whitespace, key order, escapes and extra fields."""
+    alphabet = "ab c\n\t\"\\/é€😀 \x01\x1f" + "xyz" * 5
+    names = [f"client-{i}" for i in range(rng.randrange(1, 6))] + [None, "readonly"]
+
+    def ws():
+        return rng.choice(["", "", " ", "\n", "\t ", "\r\n  "])
+
+    def dump(v):
+        if isinstance(v, dict):
+            items = list(v.items())
+            rng.shuffle(items)
+            return "{" + ws() + ("," + ws()).join(f"{json.dumps(k)}{ws()}:{ws()}{dump(x)}" for k, x in items) + ws() + "}"
+        if isinstance(v, list):
+            return "[" + ws() + ("," + ws()).join(dump(x) for x in v) + ws() + "]"
+        return json.dumps(v, ensure_ascii=rng.random() < 0.5)
+
+    def text():
+        return "".join(rng.choice(alphabet) for _ in range(1 + rng.randrange(6)))
+
+    def props():
+        return {f"k{rng.randrange(5)}": rng.choice([None, True, False, 0, -7, 123456789012345, "red", "a b", ""])
+                for _ in range(rng.randrange(4))}
+
+    def op():
+        t = rng.randrange(3)
+        if t == 0:
+            seg = text() if rng.random() < 0.6 else {"text": text(), **({"props": props()} if rng.random() < 0.7 else {})}
+            return {"type": 0, "pos1": rng.randrange(50), "seg": seg}
+        if t == 1:
+            return {"type": 1, "pos1": rng.randrange(50), "pos2": rng.randrange(50)}
+        return {"type": 2, "pos1": rng.randrange(50), "pos2": rng.randrange(50), "props": props()}
+
+    msgs = []
+    for s in range(1, n + 1):
+        cid = rng.choice(names)
+        m = {"clientId": cid, "sequenceNumber": s, "referenceSequenceNumber": rng.randrange(s),
+             "minimumSequenceNumber": 0}
+        if cid == "readonly" or rng.random() < 0.1:
+            m["type"] = rng.choice(["join", "leave", "noop"])
+            m["contents"] = rng.choice([None, {"x": [1.5, {"y": "z"}]}, "s"])
+        else:
+            m["type"] = "op"
+            u = rng.random()
+            m["contents"] = {"type": 3, "ops": [op() for _ in range(rng.randrange(4))]} if u < 0.15 else op()
+        if rng.random() < 0.3:
+            m["timestamp"] = rng.random() * 1e12
+            m["traces"] = [{"a": rng.random(), "b": [None, True]}]
+        msgs.append(m)
+    return "[" + ws() + ("," + ws()).join(dump(m) for m in msgs) + ws() + "]" + ws()
+
+
+def test_fuzzed_logs_parse_identically_or_are_reported():
+    """Random logs (unicode / escapes / whitespace / key order / extra fields / groups / noops): the
+    GPU parser equals the host parser on every batch it accepts, and the batches it reports name a
+    document the host parser also handles or rejects by itself."""
+    rng = random.Random(1234)
+    accepted = 0
+    for trial in range(40):
+        docs = [_fuzz_doc(rng, 1 + rng.randrange(300)) for _ in range(1 + rng.randrange(6))]
+        try:
+            _same(docs)
+            accepted += 1
+        except NotOnGpuPath as e:
+            assert 0 <= e.bad_doc < len(docs)
+    assert accepted >= 20
