@@ -51,6 +51,9 @@ MT_DECLARE_CLASS(3600)
 MT_DECLARE_CLASS(7266)
 MT_DECLARE_CLASS(2097152)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
+extern "C" __global__ void jg_markers_kernel(const mt_op *ops, const int64_t *op_off, mt_op *ops_w, const mt_prop *props,
+                                             int64_t D, uint32_t mk_key, uint32_t tile_key, const uint32_t *vkey,
+                                             uint32_t n_values, uint32_t *n_ids, uint32_t *tile_annot);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
 extern "C" __global__ void mt_bytes_digest_kernel(const uint8_t *buf, const int64_t *off, const int64_t *len, int64_t n,
                                                   uint64_t *dst);
@@ -1154,6 +1157,62 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
         drop();
         return rc;
     }
+    // marker ids and tile-label annotates (resolve_marker_ids / tile_annot of mt_batch_ingest) on
+    // the device: a marker's markerId value -> its key (String(value); any consistent numbering
+    // serves, the ids only key idToSegment for relative positions), per-document id counts
+    uint32_t mk = 0xFFFFFFFFu, tk = 0xFFFFFFFFu;
+    for (size_t k = 0; k < b->keys.size(); k++) {
+        if (b->keys[k] == "markerId") mk = (uint32_t)k;
+        if (b->keys[k] == "referenceTileLabels") tk = (uint32_t)k;
+    }
+    std::vector<uint32_t> vkey(b->values.size(), 0u), n_ids((size_t)D, 0u), tile((size_t)D, 0u);
+    {
+        std::unordered_map<std::u16string, uint32_t> km;
+        for (size_t v = 1; v < b->values.size(); v++) {
+            if (b->value_flags[v] & mt::kValFalsy) continue;
+            std::u16string str;
+            if (!mt::js_string_of(b->values[v], str)) continue;
+            auto it = km.find(str);
+            if (it == km.end()) it = km.emplace(str, (uint32_t)km.size() + 1).first;
+            vkey[v] = it->second;
+        }
+    }
+    if (D > 0) {
+        uint32_t *d_vkey = nullptr, *d_nids = nullptr, *d_tile = nullptr;
+        int64_t *d_oo = nullptr;
+        auto mfree = [&]() {
+            (void)hipFree(d_vkey);
+            (void)hipFree(d_nids);
+            (void)hipFree(d_tile);
+            (void)hipFree(d_oo);
+        };
+        if (dalloc(&d_vkey, vkey.size()) != hipSuccess || dalloc(&d_nids, (size_t)D) != hipSuccess ||
+            dalloc(&d_tile, (size_t)D) != hipSuccess || dalloc(&d_oo, (size_t)D + 1) != hipSuccess ||
+            hipMemcpy(d_vkey, vkey.data(), 4 * vkey.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(d_oo, r.doc_op_off.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice) != hipSuccess) {
+            mfree();
+            drop();
+            return MT_ERR_HIP;
+        }
+        const mt_op *ops_c = d_ops;
+        const int64_t *oo_c = d_oo;
+        const mt_prop *pr_c = d_props;
+        const uint32_t *vk_c = d_vkey;
+        uint32_t nv = (uint32_t)vkey.size();
+        int64_t Dd = D;
+        void *args[] = {&ops_c, &oo_c, &d_ops, &pr_c, &Dd, &mk, &tk, &vk_c, &nv, &d_nids, &d_tile};
+        hipError_t e = hipLaunchKernel((const void *)jg_markers_kernel, dim3((unsigned)D), dim3(64), args, 0, b->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
+        if (e == hipSuccess) e = hipMemcpy(n_ids.data(), d_nids, 4 * (size_t)D, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(tile.data(), d_tile, 4 * (size_t)D, hipMemcpyDeviceToHost);
+        mfree();
+        if (e != hipSuccess) {
+            drop();
+            return MT_ERR_HIP;
+        }
+    }
+    std::vector<uint64_t> idmap_base((size_t)D + 1, 0);
+    for (int64_t d = 0; d < D; d++) idmap_base[(size_t)d + 1] = idmap_base[(size_t)d] + n_ids[(size_t)d];
     // the parsed log replaces the previous one (mt_batch_ingest's fields for this log shape)
     free_launches(b);
     free_log(b);
@@ -1184,6 +1243,7 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     b->h_nload.assign((size_t)D, 0);
     b->h_nload_segs.assign((size_t)D, 0);
     b->h_tile_annot.assign((size_t)D, 0);
+    for (int64_t d = 0; d < D; d++) b->h_tile_annot[(size_t)d] = tile[(size_t)d] ? 1 : 0;
     b->payload_units = (double)r.n_text;
     b->prop_records = (double)r.n_props;
     b->text_words = tb;
@@ -1194,7 +1254,6 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     b->d_ops = d_ops;
     b->d_text = d_text;
     b->d_props = d_props;
-    std::vector<uint64_t> idmap_base((size_t)D + 1, 0);
     HIPCHK(dalloc(&b->d_off, (size_t)D + 1));
     HIPCHK(dalloc(&b->d_text_base, (size_t)D));
     HIPCHK(dalloc(&b->d_text_len, (size_t)D));
@@ -1202,7 +1261,7 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     HIPCHK(dalloc(&b->d_pool, (size_t)pb));
     HIPCHK(dalloc(&b->d_pool_base, (size_t)D));
     HIPCHK(dalloc(&b->d_pool_cap, (size_t)D));
-    HIPCHK(dalloc(&b->d_idmap, 1));
+    HIPCHK(dalloc(&b->d_idmap, (size_t)std::max<uint64_t>(idmap_base[(size_t)D], 1)));
     HIPCHK(dalloc(&b->d_idmap_base, (size_t)D + 1));
     HIPCHK(hipMemcpy(b->d_idmap_base, idmap_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_off, b->h_off.data(), sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));

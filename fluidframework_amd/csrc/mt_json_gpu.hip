@@ -668,8 +668,39 @@ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const Ctx &cx)
             if (t != 1) return t ? kFShape : kFSyntax;
             if (nd > 15) return kFShape;  // Number::toString keeps <= 15 digits exactly
             vl = r.p - vo;
+        } else if (c == '[') {
+            // a flat array already in JSON.stringify form (no whitespace, canonical elements:
+            // what a log written by JSON.stringify holds, e.g. referenceTileLabels ["pg"])
+            r.p++;
+            if (r.at() != ']') {
+                for (;;) {
+                    const int e = r.at();
+                    if (e == '"') {
+                        uint32_t so, sl;
+                        bool pl;
+                        if (!str_raw(r, so, sl, pl)) return kFSyntax;
+                        if (!pl) return kFShape;
+                    } else if (e == '-' || is_digit(e)) {
+                        int64_t v;
+                        uint32_t nd;
+                        const int t = num_tok(r, v, nd);
+                        if (t != 1) return t ? kFShape : kFSyntax;
+                        if (nd > 15) return kFShape;
+                    } else if (!(r.lit("true", 4) || r.lit("false", 5) || r.lit("null", 4))) {
+                        return kFShape;  // nested containers / whitespace: the host's js_stringify
+                    }
+                    if (r.at() == ',') {
+                        r.p++;
+                        continue;
+                    }
+                    if (r.at() == ']') break;
+                    return kFShape;
+                }
+            }
+            r.p++;
+            vl = r.p - vo;
         } else {
-            return kFShape;  // nested values: the host's js_stringify
+            return kFShape;  // objects: the host's js_stringify (JS key order, whitespace)
         }
         if (W) {
             cx.pk_off[gidx + np] = ko;
@@ -706,8 +737,8 @@ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, cons
     if (op.type == 0) {
         if (!(op.seen & kOSeg)) return kFShape;
         Rd rs{s, op.seg_p, n};
-        uint32_t text_p = 0, props_p = 0;
-        bool has_text = false, has_props = false;
+        uint32_t text_p = 0, props_p = 0, marker_p = 0;
+        bool has_text = false, has_props = false, has_marker = false;
         if (rs.at() == '"') {
             text_p = op.seg_p;
             has_text = true;
@@ -734,7 +765,9 @@ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, cons
                     has_props = true;
                     props_p = rs.p;
                 } else if (rs.is(ko, kl, "marker")) {
-                    return kFShape;  // markers: the host path (marker ids, tile labels)
+                    if (has_marker) return kFShape;
+                    has_marker = true;
+                    marker_p = rs.p;
                 }
                 if (!skip_value(rs)) return kFSyntax;
                 rs.ws();
@@ -746,14 +779,54 @@ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, cons
                 if (c == '}') break;
                 return kFSyntax;
             }
-            if (!has_text) return kFShape;
+            if (!has_text && !has_marker) return kFShape;
         } else {
             return kFShape;
         }
-        Rd rt{s, text_p, n};
-        uint32_t units = 0;
+        uint32_t units = 0, ref_type = 0;
         bool has_nl = false, ends_nl = false;
-        if (!str_text(rt, W ? cx.text + mo.ntext : nullptr, units, has_nl, ends_nl)) return kFSyntax;
+        const bool marker = !has_text;  // pack_seg: "text" wins over "marker"
+        if (marker) {
+            // {marker: {refType}} (pack_seg, mt_json.cpp:522-528): payload = refType, length 1
+            Rd rm{s, marker_p, n};
+            if (rm.at() != '{') return kFShape;
+            rm.p++;
+            rm.ws();
+            bool seen_rt = false;
+            if (rm.at() != '}') {
+                for (;;) {
+                    rm.ws();
+                    uint32_t ko, kl;
+                    bool plain;
+                    if (!str_raw(rm, ko, kl, plain)) return kFSyntax;
+                    if (!plain) return kFShape;
+                    rm.ws();
+                    if (rm.at() != ':') return kFSyntax;
+                    rm.p++;
+                    rm.ws();
+                    if (rm.is(ko, kl, "refType")) {
+                        int64_t v;
+                        uint32_t nd;
+                        if (seen_rt || num_tok(rm, v, nd) != 1 || v < 0 || v > 0x7FFFFFFF) return kFShape;
+                        seen_rt = true;
+                        ref_type = (uint32_t)v;
+                    } else if (!skip_value(rm)) {
+                        return kFSyntax;
+                    }
+                    rm.ws();
+                    const int c = rm.at();
+                    if (c == ',') {
+                        rm.p++;
+                        continue;
+                    }
+                    if (c == '}') break;
+                    return kFSyntax;
+                }
+            }
+        } else {
+            Rd rt{s, text_p, n};
+            if (!str_text(rt, W ? cx.text + mo.ntext : nullptr, units, has_nl, ends_nl)) return kFSyntax;
+        }
         uint32_t np = 0;
         bool hp = false;
         if (has_props) {
@@ -773,9 +846,15 @@ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, cons
             r.pos2 = (int32_t)(cx.gprop + mo.nprop);
             mo.npropops++;
         }
-        r.payload = cx.pay + mo.ntext;
-        r.payload_len = units;
-        if (cx.install) {
+        if (marker) {
+            r.flags |= (uint16_t)MT_OPF_MARKER;
+            r.payload = ref_type;
+            r.payload_len = 1;  // the marker id (if any) replaces it at install (jg_markers_kernel)
+        } else {
+            r.payload = cx.pay + mo.ntext;
+            r.payload_len = units;
+        }
+        if (cx.install && !marker) {
             if (has_nl) r.flags |= (uint16_t)MT_OPF_INTERNAL_HAS_NL;
             if (ends_nl) r.flags |= (uint16_t)MT_OPF_INTERNAL_ENDS_NL;
         }
@@ -1160,6 +1239,43 @@ extern "C" __global__ __launch_bounds__(64) void jg_remap_kernel(Params P) {
     }
 }
 
+// install: marker ids (resolve_marker_ids in mt_host.cpp: a marker insert whose props give a truthy
+// markerId gets that id's key in payload_len, 0 otherwise; vkey maps value ids to keys) and the
+// documents whose annotates touch referenceTileLabels (their findTile queries are unsupported)
+extern "C" __global__ __launch_bounds__(64) void jg_markers_kernel(const mt_op *ops, const int64_t *op_off,
+                                                                 mt_op *ops_w, const mt_prop *props, int64_t D,
+                                                                 uint32_t mk_key, uint32_t tile_key,
+                                                                 const uint32_t *vkey, uint32_t n_values,
+                                                                 uint32_t *n_ids, uint32_t *tile_annot) {
+    const int64_t d = blockIdx.x;
+    if (d >= D) return;
+    uint32_t cnt = 0, tile = 0;
+    for (int64_t i = op_off[d] + lane_id(); i < op_off[d + 1]; i += 64) {
+        mt_op o = ops[i];
+        if (o.type == MT_OP_INSERT && (o.flags & MT_OPF_MARKER)) {
+            uint32_t id = 0;
+            if (o.flags & MT_OPF_HAS_PROPS)
+                for (uint32_t q = 0; q < MT_OPF_NPROPS(o.flags); q++) {
+                    const mt_prop pr = props[o.pos2 + q];
+                    if (pr.key == mk_key) id = pr.value < n_values ? vkey[pr.value] : 0u;
+                }
+            ops_w[i].payload_len = id;
+            cnt += id != 0;
+        } else if (o.type == MT_OP_ANNOTATE) {
+            for (uint32_t q = 0; q < o.payload_len; q++)
+                if (props[o.payload + q].key == tile_key) tile = 1;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        cnt += __shfl_xor(cnt, off, 64);
+        tile |= __shfl_xor(tile, off, 64);
+    }
+    if (lane_id() == 0) {
+        n_ids[d] = cnt;
+        tile_annot[d] = tile;
+    }
+}
+
 }  // namespace jg
 }  // namespace mt
 
@@ -1450,13 +1566,6 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
             nm.push_back(o == kNullSpan ? std::string("null") : std::string(js + o, nd[2 * (i - 1) + 1]));
         }
     }
-    for (const auto &k : res.keys)
-        if (k == "referenceTileLabels" || k == "markerId") {  // tile / marker bookkeeping: host path
-            res.status = MT_UNSUPPORTED;
-            res.fail_bits = kFShape;
-            res.bad_doc = 0;
-            return MT_UNSUPPORTED;
-        }
     res.ms_host = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     uint32_t *d_km = nullptr, *d_vm = nullptr;
     JGCHK(B.get(&d_km, kmap.size()));

@@ -107,9 +107,13 @@ def test_observer_and_many_clients():
 
 
 OUTSIDE = [  # (message, reason) — every one must be reported, never parsed differently
-    (_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1}}}), "marker"),
+    (_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1},
+                                                      "props": {"referenceTileLabels": ["a", "b"]}}}),
+     "array value with whitespace"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1.5}}), "float value"),
-    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": [1]}}), "nested value"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": {"b": 1}}}), "object value"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": [[1]]}}), "nested array value"),
+    (_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1.5}}}), "float refType"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": "é"}}), "non-ASCII value"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"1": 1}}), "array-index key"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
@@ -191,7 +195,7 @@ def test_gpu_ingest_from_device_resident_json():
 
 
 def test_auto_falls_back_to_the_host_parser():
-    docs = [json.dumps(FAST_DOCS[0]), json.dumps([OUTSIDE[0][0]])]
+    docs = [json.dumps(FAST_DOCS[0]), json.dumps([OUTSIDE[1][0]])]
     with fa.ReplayBatch(2) as g, fa.ReplayBatch(2) as h:
         info = g.ingest_json(docs)
         assert info["path"] == "host" and info["bad_doc"] == 1
@@ -268,3 +272,49 @@ def test_fuzzed_logs_parse_identically_or_are_reported():
         except NotOnGpuPath as e:
             assert 0 <= e.bad_doc < len(docs)
     assert accepted >= 20
+
+
+def _marker_doc(rng: random.Random, n: int, compact=(",", ":")):
+    """A text + Tile-marker log as JSON.stringify writes it (compact): paragraph markers with
+    referenceTileLabels and markerIds, annotates, removes."""
+    msgs, length = [], 0
+    for s in range(1, n + 1):
+        u = rng.random()
+        if length == 0 or u < 0.25:
+            seg = {"marker": {"refType": rng.choice([0, 1, 2])},
+                   "props": {"referenceTileLabels": rng.sample(["pg", "EOP", "cell"], 1 + rng.randrange(2)),
+                             **({"markerId": f"m{s}"} if rng.random() < 0.5 else {})}}
+            op, dl = {"type": 0, "pos1": rng.randrange(length + 1), "seg": seg}, 1
+        elif u < 0.6:
+            t = "".join(rng.choice("abc de") for _ in range(1 + rng.randrange(5)))
+            op, dl = {"type": 0, "pos1": rng.randrange(length + 1), "seg": t}, len(t)
+        elif u < 0.8:
+            a = rng.randrange(length)
+            b = min(length, a + 1 + rng.randrange(3))
+            op, dl = {"type": 1, "pos1": a, "pos2": b}, a - b
+        else:
+            a = rng.randrange(length)
+            op, dl = {"type": 2, "pos1": a, "pos2": min(length, a + 2), "props": {"bold": rng.random() < 0.5}}, 0
+        length += dl
+        msgs.append(_msg(f"c{rng.randrange(3)}", s, s - 1, op, msn=max(0, s - 4)))
+    return json.dumps(msgs, separators=compact)
+
+
+def test_markers_and_tile_labels_on_the_gpu_path():
+    """Tile markers (refType, referenceTileLabels arrays, markerIds) parse on the GPU exactly as on
+    the host, and the GPU-ingested batch replays to the same state and findTile answers."""
+    rng = random.Random(99)
+    docs = [_marker_doc(rng, 200 + 50 * i) for i in range(6)]
+    _same(docs)
+    with fa.ReplayBatch(len(docs)) as g, fa.ReplayBatch(len(docs)) as h:
+        assert g.ingest_json(docs, device="gpu")["path"] == "gpu"
+        h.ingest_json(docs, device="host")
+        g.run()
+        h.run()
+        _replay_equal(g, h, len(docs))
+        for d in range(len(docs)):
+            n = len(g.doc(d).get_text()) + 8
+            for pos in range(0, n, 3):
+                for label in ("pg", "EOP"):
+                    for prec in (True, False):
+                        assert g.doc(d).find_tile(pos, label, prec) == h.doc(d).find_tile(pos, label, prec)
