@@ -535,6 +535,7 @@ struct OpInfo {
     int32_t p1 = 0, p2 = 0;
     uint32_t seg_p = 0, props_p = 0, ops_p = 0;
     uint32_t seen = 0;
+    bool rewrite = false;
 };
 enum { kOType = 1, kOPos1 = 2, kOPos2 = 4, kOSeg = 8, kOProps = 16, kOOps = 32 };
 
@@ -587,9 +588,48 @@ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
                 // and relative positions leave the fast path
                 const bool cop = r.is(ko, kl, "combiningOp"), reg = r.is(ko, kl, "register");
                 if (cop || reg) {
-                    if (r.lit("null", 4) || (cop && r.lit("false", 5))) {
-                        if (extra & (cop ? 1u : 2u)) return kFShape;
-                        extra |= cop ? 1u : 2u;
+                    if (extra & (cop ? 1u : 2u)) return kFShape;
+                    extra |= cop ? 1u : 2u;
+                    if (r.lit("null", 4) || (cop && r.lit("false", 5))) goto next;
+                    if (cop && r.at() == '{') {
+                        // {name: "rewrite"} (segmentPropertiesManager.ts:53-54): a flag; any other
+                        // combiningOp carries defaultValue / minValue records: the host path
+                        r.p++;
+                        r.ws();
+                        bool named = false;
+                        if (r.at() != '}') {
+                            for (;;) {
+                                r.ws();
+                                uint32_t no, nl;
+                                bool pl;
+                                if (!str_raw(r, no, nl, pl)) return kFSyntax;
+                                if (!pl) return kFShape;
+                                r.ws();
+                                if (r.at() != ':') return kFSyntax;
+                                r.p++;
+                                r.ws();
+                                if (r.is(no, nl, "name")) {
+                                    uint32_t vo, vl;
+                                    bool vp;
+                                    if (named || r.at() != '"' || !str_raw(r, vo, vl, vp) || !vp ||
+                                        !r.is(vo, vl, "rewrite"))
+                                        return kFShape;
+                                    named = true;
+                                } else if (!skip_value(r)) {
+                                    return kFSyntax;
+                                }
+                                r.ws();
+                                if (r.at() == ',') {
+                                    r.p++;
+                                    continue;
+                                }
+                                if (r.at() == '}') break;
+                                return kFSyntax;
+                            }
+                        }
+                        r.p++;
+                        if (!named) return kFShape;  // a truthy combiningOp without a name: "other"
+                        op.rewrite = true;
                         goto next;
                     }
                     return kFShape;
@@ -871,6 +911,7 @@ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, cons
             if (f) return f;
             r.payload = cx.gprop + mo.nprop;
             r.payload_len = np;
+            if (op.rewrite) r.flags |= (uint16_t)MT_OPF_REWRITE;
             mo.nprop += np;
             mo.npropops++;
         }

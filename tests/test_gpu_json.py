@@ -46,7 +46,10 @@ FAST_DOCS = [
      _msg("C", 7, 6, {"type": 3, "ops": []}, msn=5),
      _msg("A", 8, 7, {"type": 2, "pos1": 0, "pos2": 1, "props": {}, "combiningOp": None}, msn=5),
      _msg("null", 9, 8, {"type": 1, "pos1": 0, "pos2": 1}, msn=5),
-     _msg("A", 10, 9, {"type": 0, "pos1": 0, "seg": {"text": "p", "props": None}, "register": None}, msn=5)],
+     _msg("A", 10, 9, {"type": 0, "pos1": 0, "seg": {"text": "p", "props": None}, "register": None}, msn=5),
+     _msg("B", 11, 10, {"type": 2, "pos1": 0, "pos2": 3, "props": {"b": 2, "c": None},
+                        "combiningOp": {"name": "rewrite"}}, msn=5),
+     _msg("B", 12, 11, {"type": 2, "pos1": 0, "pos2": 1, "props": {"e": 1}, "combiningOp": False}, msn=5)],
     [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "a\ud83d"}),
      _msg("A", 2, 1, {"type": 0, "pos1": 2, "seg": "\ude00b\"\\\n\x01é€😀\t/"}),
      _msg("B", 3, 2, {"type": 2, "pos1": 0, "pos2": 3, "props": {"k": -12, "n": 0, "s": "a b~", "big": 123456789012345}}),
@@ -117,7 +120,9 @@ OUTSIDE = [  # (message, reason) — every one must be reported, never parsed di
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": "é"}}), "non-ASCII value"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"1": 1}}), "array-index key"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
-                      "combiningOp": {"name": "rewrite"}}), "combiningOp"),
+                      "combiningOp": {"name": "incr"}}), "combiningOp incr"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                      "combiningOp": {"defaultValue": 1}}), "combiningOp without a name"),
     (_msg("A", 1, 0, {"type": 1, "relativePos1": {"id": "m"}, "pos2": 1}), "relative position"),
     (_msg("A", -1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "local op"),
     (_msg("readonly", 1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "own op (ack)"),
