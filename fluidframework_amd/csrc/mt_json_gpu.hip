@@ -67,6 +67,14 @@ struct Params {
     uint32_t *m_cloff, *m_cllen, *m_cid, *m_npops;
     const int32_t *chunk_doc;        // count / write passes: one wave per 64 messages of a document
     const uint32_t *chunk_first;
+    // structural scan: one wave per kSegBytes of a document (segment g: doc seg_doc[g], bytes from
+    // seg_start[g]); per-document segments seg_first[d] .. seg_first[d + 1]
+    const int32_t *seg_doc;
+    const uint32_t *seg_start;
+    const int64_t *seg_first;
+    int64_t G;
+    uint32_t *sg_q, *sg_pre, *sg_post, *sg_flags, *sg_nmsg, *sg_fail, *sg_starts;
+    int32_t *sg_d0, *sg_d1;
     // per document
     uint32_t *d_nmsg, *d_fail, *d_nrec, *d_ntext, *d_nprop, *d_npropops, *d_nnames, *d_nuk, *d_nuv;
     uint32_t *cl_ht;                 // kClientSlots per document
@@ -107,111 +115,247 @@ __device__ __forceinline__ uint64_t mregion(const int64_t *doc_off, int64_t d) {
 }
 
 // ---------------------------------------------------------------- stage 1: structural scan
-extern "C" __global__ __launch_bounds__(64) void jg_scan_kernel(Params P) {
-    const int64_t d = blockIdx.x;
-    if (d >= P.D) return;
+// A document is scanned in segments of kSegBytes, one wavefront each, so a batch of few long
+// documents still fills the chip (simdjson's two-pass idea on 64-lane ballots):
+//   A  per segment, with the in-string state at its start assumed 0: the parity of its unescaped
+//      quotes and its net bracket depth for either start state (the in-string mask under the other
+//      start state is the complement, so one pass gives both);
+//   B  per segment, with the true start state (the XOR of the earlier segments' parities) and the
+//      true start depth (their deltas for their start states): the message starts (depth-1 '{')
+//      and the checks that need no global state; the commas before its first / after its last
+//      message start go to C;
+//   C  per document: the checks across segments (one '[', exactly one comma between messages, no
+//      trailing comma, nothing after ']') and the message starts gathered in order.
+// A quote's escape parity comes from the run of backslashes right before it; a segment reads
+// the 64 bytes before its start for the run it begins in.
+constexpr uint32_t kSegBytes = 65536;
+constexpr uint32_t kSegStarts = kSegBytes / 64 + 2;  // message starts one segment can hold
+enum : uint32_t { kSgMsg = 1, kSgEnd = 2, kSgOpenShift = 8 };
+
+// bytes [start, end) of document d in 64-byte chunks, one byte per lane (outside [0, len):
+// whitespace); f(pos0, c) per chunk with pos0 = document position of lane 0's byte.  Steps of 1 KB:
+// four coalesced 256-byte dword loads in flight, chunk j rebuilt with one shuffle.
+template <class F>
+__device__ void for_chunks(const Params &P, int64_t d, uint32_t start, uint32_t end, F &&f) {
     const int lane = lane_id();
     const int64_t a = P.doc_off[d];
-    const uint32_t len = (uint32_t)(P.doc_off[d + 1] - a);
-    const uint64_t mb = mregion(P.doc_off, d);
-    const uint32_t mcap = (uint32_t)(mregion(P.doc_off, d + 1) - mb);
-    // dword loads from the 4-byte-aligned address at or below the document's first byte: a step
-    // covers 1 KB as four coalesced 256-byte loads in flight; 64-byte chunk j of the step is
-    // rebuilt across the lanes with one shuffle (lane i: byte i of the chunk)
-    const uint32_t shift = (uint32_t)(a & 3);
-    const uint32_t *w32 = (const uint32_t *)(P.J + (a - shift));
-    const uint32_t span = len + shift;                 // bytes from the aligned start
-    const uint32_t nwords = (span + 3) >> 2;           // the last word may hold the next bytes (or pad)
-    uint32_t depth = 0, nmsg = 0, commas = 0, fail = 0, bs_run = 0;
-    bool started = false, ended = false, in_str = false;
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (uint32_t base = 0; base < span && !fail; base += 1024) {
+    const uint64_t abs0 = (uint64_t)a + start;
+    const uint32_t shift = (uint32_t)(abs0 & 3);
+    const uint32_t *w32 = (const uint32_t *)(P.J + (abs0 - shift));
+    const uint32_t span = end - start + shift;
+    const uint32_t nwords = (span + 3) >> 2;
+    bool stop = false;
+    for (uint32_t base = 0; base < span && !stop; base += 1024) {
         uint32_t w[4];
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             const uint32_t wi = (base >> 2) + 64u * (uint32_t)m + (uint32_t)lane;
             w[m] = wi < nwords ? w32[wi] : 0x20202020u;
         }
-        for (int j = 0; j < 16 && !fail; j++) {
+        for (int j = 0; j < 16 && !stop; j++) {
             const uint32_t pos0 = base + 64u * (uint32_t)j;
             if (pos0 >= span) break;
             const uint32_t word = __shfl(w[j >> 2], 16 * (j & 3) + (lane >> 2), 64);
             const uint32_t at = pos0 + (uint32_t)lane;
             const int c = (at >= shift && at < span) ? (int)((word >> (8 * (lane & 3))) & 0xFFu) : ' ';
-            const uint32_t pos = pos0 - shift;  // document position of lane 0 (may wrap below 0 in step 0)
-            const uint64_t bs = ballot(c == '\\');
-            // a quote is escaped by an odd run of backslashes right before it
-            const uint64_t nb = ~bs & below;
-            const uint32_t run = nb ? (uint32_t)(lane - 1 - (63 - __builtin_clzll(nb))) : (uint32_t)lane + bs_run;
-            uint64_t x = ballot(c == '"' && !(run & 1u));
-            x ^= x << 1;
-            x ^= x << 2;
-            x ^= x << 4;
-            x ^= x << 8;
-            x ^= x << 16;
-            x ^= x << 32;
-            const uint64_t S = in_str ? ~x : x;  // 1: inside a string (opening quote included)
-            in_str = (S >> 63) & 1ull;
-            bs_run = bs == ~0ull ? bs_run + 64u : (uint32_t)__builtin_clzll(~bs);
-            const bool ws = c == ' ' || c == '\t' || c == '\n' || c == '\r';
-            const uint64_t nonws = ballot(!ws) & ~S;
-            const uint64_t opn = ballot(c == '{' || c == '[') & ~S;
-            const uint64_t cls = ballot(c == '}' || c == ']') & ~S;
-            const uint64_t brace = ballot(c == '{' || c == '}');
-            const uint64_t comma = ballot(c == ',') & ~S;
-            uint64_t st = opn | cls;
-            uint32_t lo = 0;
-            // the bytes strictly between structural characters are at one depth: at depth 0 only
-            // whitespace, at depth 1 (between messages) whitespace and commas
-            auto segment = [&](uint32_t hi) {
-                if (hi > lo) {
-                    const uint64_t m = (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
-                    if (depth == 0 && (nonws & m)) fail |= kFSyntax;
-                    if (depth == 1) {
-                        if (nonws & ~comma & m) fail |= kFSyntax;
-                        commas += (uint32_t)__builtin_popcountll(comma & m);
-                    }
+            stop = f(start + pos0 - shift, c);  // (wraps below 0 only for lanes that are masked)
+        }
+    }
+}
+
+// the run of backslashes ending right before document position p (up to 63; 64 = "longer")
+__device__ uint32_t bs_before(const Params &P, int64_t d, uint32_t p) {
+    const int lane = lane_id();
+    const int64_t q = (int64_t)p - 64 + lane;
+    const int c = q >= 0 ? P.J[P.doc_off[d] + q] : ' ';
+    const uint64_t bs = ballot(c == '\\');
+    return bs == ~0ull ? 64u : (uint32_t)__builtin_clzll(~bs);
+}
+
+// unescaped quotes of a chunk, prefix-XORed: bit i = parity of those at or below i
+__device__ __forceinline__ uint64_t quote_prefix(int c, uint32_t bs_run, uint64_t &bs_out) {
+    const int lane = lane_id();
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t bs = ballot(c == '\\');
+    const uint64_t nb = ~bs & below;
+    const uint32_t run = nb ? (uint32_t)(lane - 1 - (63 - __builtin_clzll(nb))) : (uint32_t)lane + bs_run;
+    uint64_t x = ballot(c == '"' && !(run & 1u));
+    x ^= x << 1;
+    x ^= x << 2;
+    x ^= x << 4;
+    x ^= x << 8;
+    x ^= x << 16;
+    x ^= x << 32;
+    bs_out = bs;
+    return x;
+}
+
+extern "C" __global__ __launch_bounds__(64) void jg_seg_a_kernel(Params P) {
+    const int64_t g = blockIdx.x;
+    if (g >= P.G) return;
+    const int64_t d = P.seg_doc[g];
+    const uint32_t len = (uint32_t)(P.doc_off[d + 1] - P.doc_off[d]);
+    const uint32_t start = P.seg_start[g], end = min(len, start + kSegBytes);
+    uint32_t bs_run = bs_before(P, d, start), fail = bs_run >= 64 ? kFShape : 0u;
+    bool in0 = false;
+    int32_t d0 = 0, d1 = 0;
+    uint32_t q = 0;
+    for_chunks(P, d, start, end, [&](uint32_t, int c) {
+        uint64_t bs;
+        const uint64_t x = quote_prefix(c, bs_run, bs);
+        const uint64_t S0 = in0 ? ~x : x;
+        q ^= (uint32_t)__builtin_popcountll(x ^ (x << 1)) & 1u;  // unescaped quotes of the chunk
+        in0 = (S0 >> 63) & 1ull;
+        bs_run = bs == ~0ull ? bs_run + 64u : (uint32_t)__builtin_clzll(~bs);
+        const uint64_t opn = ballot(c == '{' || c == '['), cls = ballot(c == '}' || c == ']');
+        d0 += __builtin_popcountll(opn & ~S0) - __builtin_popcountll(cls & ~S0);
+        d1 += __builtin_popcountll(opn & S0) - __builtin_popcountll(cls & S0);
+        return false;
+    });
+    if (lane_id() == 0) {
+        P.sg_q[g] = q;
+        P.sg_d0[g] = d0;
+        P.sg_d1[g] = d1;
+        P.sg_fail[g] = fail;
+    }
+}
+
+extern "C" __global__ __launch_bounds__(64) void jg_seg_b_kernel(Params P) {
+    const int64_t g = blockIdx.x;
+    if (g >= P.G) return;
+    const int lane = lane_id();
+    const int64_t d = P.seg_doc[g];
+    const uint32_t len = (uint32_t)(P.doc_off[d + 1] - P.doc_off[d]);
+    const uint32_t start = P.seg_start[g], end = min(len, start + kSegBytes);
+    // the start state from the earlier segments of the document
+    bool in_str = false;
+    int32_t depth = 0;
+    for (int64_t k = P.seg_first[d]; k < g; k++) {
+        depth += in_str ? P.sg_d1[k] : P.sg_d0[k];
+        in_str ^= P.sg_q[k] & 1u;
+    }
+    uint32_t fail = P.sg_fail[g];
+    if (depth < 0) fail |= kFSyntax;
+    uint32_t bs_run = bs_before(P, d, start);
+    uint32_t commas = 0, pre = 0, post = 0, flags = 0, n = 0, opens = 0;
+    uint32_t *starts = P.sg_starts + (uint64_t)g * kSegStarts;
+    for_chunks(P, d, start, end, [&](uint32_t pos, int c) {
+        uint64_t bs;
+        const uint64_t x = quote_prefix(c, bs_run, bs);
+        const uint64_t S = in_str ? ~x : x;  // 1: inside a string (opening quote included)
+        in_str = (S >> 63) & 1ull;
+        bs_run = bs == ~0ull ? bs_run + 64u : (uint32_t)__builtin_clzll(~bs);
+        const bool ws = c == ' ' || c == '\t' || c == '\n' || c == '\r';
+        const uint64_t nonws = ballot(!ws) & ~S;
+        const uint64_t opn = ballot(c == '{' || c == '[') & ~S;
+        const uint64_t cls = ballot(c == '}' || c == ']') & ~S;
+        const uint64_t brace = ballot(c == '{' || c == '}');
+        const uint64_t comma = ballot(c == ',') & ~S;
+        uint64_t st = opn | cls;
+        uint32_t lo = 0;
+        // between structural characters one depth: at 0 only whitespace, at 1 whitespace + commas
+        auto segment = [&](uint32_t hi) {
+            if (hi > lo) {
+                const uint64_t m = (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
+                if (depth == 0 && (nonws & m)) fail |= kFSyntax;
+                if (depth == 1) {
+                    if (nonws & ~comma & m) fail |= kFSyntax;
+                    commas += (uint32_t)__builtin_popcountll(comma & m);
                 }
-            };
-            while (st && !fail) {
-                const uint32_t t = (uint32_t)__builtin_ctzll(st);
-                st &= st - 1;
-                segment(t);
-                lo = t + 1;
-                const bool o = (opn >> t) & 1ull, br = (brace >> t) & 1ull;
-                if (ended) {
+            }
+        };
+        while (st && !fail) {
+            const uint32_t t = (uint32_t)__builtin_ctzll(st);
+            st &= st - 1;
+            segment(t);
+            lo = t + 1;
+            const bool o = (opn >> t) & 1ull, br = (brace >> t) & 1ull;
+            if (flags & kSgEnd) {
+                fail |= kFSyntax;
+                break;
+            }
+            if (o) {
+                if (depth == 0) {
+                    if (br) fail |= kFSyntax;  // the log is one array
+                    opens++;
+                } else if (depth == 1) {
+                    if (!br) fail |= kFSyntax;  // a message must be an object
+                    if (flags & kSgMsg) {
+                        if (commas != 1u) fail |= kFSyntax;
+                    } else {
+                        pre = commas;
+                    }
+                    commas = 0;
+                    if (n >= kSegStarts) fail |= kFCap;
+                    else if (lane == 0) starts[n] = pos + t;
+                    n++;
+                    flags |= kSgMsg;
+                }
+                depth++;
+            } else {
+                if (depth <= 0) {
                     fail |= kFSyntax;
                     break;
                 }
-                if (o) {
-                    if (depth == 0) {
-                        if (started || br) fail |= kFSyntax;  // the log is one array
-                        started = true;
-                    } else if (depth == 1) {
-                        if (!br) fail |= kFSyntax;  // a message must be an object
-                        if (commas != (nmsg ? 1u : 0u)) fail |= kFSyntax;
-                        commas = 0;
-                        if (nmsg >= mcap) fail |= kFCap;
-                        else if (lane == 0) P.m_start[mb + nmsg] = pos + t;
-                        nmsg++;
+                depth--;
+                if (depth == 0) {
+                    if (br) fail |= kFSyntax;
+                    if (flags & kSgMsg) {
+                        if (commas) fail |= kFSyntax;  // no trailing comma
+                    } else {
+                        pre = commas;
                     }
-                    depth++;
-                } else {
-                    if (depth == 0) {
-                        fail |= kFSyntax;
-                        break;
-                    }
-                    depth--;
-                    if (depth == 0) {
-                        if (br || commas) fail |= kFSyntax;  // ']' closes the log, no trailing comma
-                        ended = true;
-                    }
+                    commas = 0;
+                    flags |= kSgEnd;
                 }
             }
-            if (!fail) segment(64);
         }
+        if (!fail) segment(64);
+        return fail != 0;
+    });
+    if (flags & kSgMsg) post = commas;
+    else if (!(flags & kSgEnd)) pre = commas;
+    if (lane == 0) {
+        P.sg_pre[g] = pre;
+        P.sg_post[g] = post;
+        P.sg_flags[g] = flags | (min(opens, 255u) << kSgOpenShift);
+        P.sg_nmsg[g] = n;
+        P.sg_fail[g] = fail;
     }
-    if (!started || !ended || in_str) fail |= kFSyntax;
+}
+
+extern "C" __global__ __launch_bounds__(64) void jg_seg_c_kernel(Params P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D) return;
+    const int lane = lane_id();
+    const uint64_t mb = mregion(P.doc_off, d);
+    const uint32_t mcap = (uint32_t)(mregion(P.doc_off, d + 1) - mb);
+    uint32_t fail = 0, cur = 0, nmsg = 0, opens = 0, q = 0;
+    bool seen = false, ended = false;
+    for (int64_t k = P.seg_first[d]; k < P.seg_first[d + 1]; k++) {
+        const uint32_t f = P.sg_flags[k], n = P.sg_nmsg[k];
+        fail |= P.sg_fail[k];
+        q ^= P.sg_q[k] & 1u;
+        opens += f >> kSgOpenShift;
+        if (ended && ((f & (kSgMsg | kSgEnd)) || (f >> kSgOpenShift))) fail |= kFSyntax;
+        if (f & kSgMsg) {
+            if (cur + P.sg_pre[k] != (seen ? 1u : 0u)) fail |= kFSyntax;
+            if (nmsg + n > mcap) fail |= kFCap;
+            for (uint32_t i = (uint32_t)lane; !fail && i < n; i += 64)
+                P.m_start[mb + nmsg + i] = P.sg_starts[(uint64_t)k * kSegStarts + i];
+            nmsg += n;
+            cur = P.sg_post[k];
+            seen = true;
+        } else {
+            cur += P.sg_pre[k];
+        }
+        if (f & kSgEnd) {
+            if (!(f & kSgMsg) && cur != 0) fail |= kFSyntax;  // "[..., ]" across segments
+            ended = true;
+        }
+        if (fail) break;
+    }
+    if (opens != 1 || !ended || q) fail |= kFSyntax;
     if (lane == 0) {
         P.d_nmsg[d] = fail ? 0u : nmsg;
         P.d_fail[d] = fail;
@@ -1429,9 +1573,45 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
         P.obs_len = (uint32_t)obs.size();
     }
     const unsigned grid = (unsigned)std::max<int64_t>(D, 1);
+    // scan segments
+    std::vector<int32_t> seg_doc;
+    std::vector<uint32_t> seg_start;
+    std::vector<int64_t> seg_first((size_t)D + 1, 0);
+    for (int64_t d = 0; d < D; d++) {
+        seg_first[(size_t)d] = (int64_t)seg_doc.size();
+        const uint64_t len = (uint64_t)(doc_off[d + 1] - doc_off[d]);
+        for (uint64_t st = 0; st < len; st += kSegBytes) {
+            seg_doc.push_back((int32_t)d);
+            seg_start.push_back((uint32_t)st);
+        }
+    }
+    seg_first[(size_t)D] = (int64_t)seg_doc.size();
+    const size_t G = seg_doc.size();
+    P.G = (int64_t)G;
+    int32_t *d_sdoc = nullptr;
+    uint32_t *d_sstart = nullptr;
+    int64_t *d_sfirst = nullptr;
+    JGCHK(B.get(&d_sdoc, G));
+    JGCHK(B.get(&d_sstart, G));
+    JGCHK(B.get(&d_sfirst, (size_t)D + 1));
+    if (G) {
+        JGCHK(hipMemcpyAsync(d_sdoc, seg_doc.data(), 4 * G, hipMemcpyHostToDevice, s));
+        JGCHK(hipMemcpyAsync(d_sstart, seg_start.data(), 4 * G, hipMemcpyHostToDevice, s));
+    }
+    JGCHK(hipMemcpyAsync(d_sfirst, seg_first.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice, s));
+    P.seg_doc = d_sdoc;
+    P.seg_start = d_sstart;
+    P.seg_first = d_sfirst;
+    uint32_t **sarr[] = {&P.sg_q, &P.sg_pre, &P.sg_post, &P.sg_flags, &P.sg_nmsg, &P.sg_fail};
+    for (uint32_t **a : sarr) JGCHK(B.get(a, G));
+    JGCHK(B.get(&P.sg_d0, G));
+    JGCHK(B.get(&P.sg_d1, G));
+    JGCHK(B.get(&P.sg_starts, G * kSegStarts));
     void *args[] = {&P};
     JGCHK(hipEventRecord(ev[0], s));
-    if (D) JGCHK(hipLaunchKernel((const void *)jg_scan_kernel, dim3(grid), dim3(64), args, 0, s));
+    if (G) JGCHK(hipLaunchKernel((const void *)jg_seg_a_kernel, dim3((unsigned)G), dim3(64), args, 0, s));
+    if (G) JGCHK(hipLaunchKernel((const void *)jg_seg_b_kernel, dim3((unsigned)G), dim3(64), args, 0, s));
+    if (D) JGCHK(hipLaunchKernel((const void *)jg_seg_c_kernel, dim3(grid), dim3(64), args, 0, s));
     std::vector<uint32_t> nmsg;
     JGCHK(dl(nmsg, P.d_nmsg, (size_t)D, s));
     std::vector<int32_t> chunk_doc;
