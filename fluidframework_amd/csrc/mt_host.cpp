@@ -1094,7 +1094,7 @@ MT_API int mt_pack_json_gpu(mt_packed **out, int64_t n_docs, const char *json, c
 // observer fast path (no LOAD / RELPOS / REGENERATE records, markers, combiningOps or local ops)
 MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, const void *d_json,
                                     const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats) {
-    if (!b || !doc_off || (b->n_docs && !json)) return MT_ERR_ARG;
+    if (!b || !doc_off || (b->n_docs && !json) || ((uintptr_t)d_json & 3u)) return MT_ERR_ARG;
     if (bad_doc) *bad_doc = -1;
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t D = b->n_docs;

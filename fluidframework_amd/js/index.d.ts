@@ -59,7 +59,8 @@ export declare class ReplayBatch {
     ingestMessages(docs: Array<Array<ISequencedDocumentMessage | string>>): void;
     /** Native parse + pack (mt_pack_json on nThreads host threads, 0 = all cores) of each
      *  document's message array, given as its JSON text (messages.json) or as the array. */
-    ingestJson(docs: Array<string | ISequencedDocumentMessage[]>, nThreads?: number): void;
+    ingestJson(docs: Array<string | ISequencedDocumentMessage[]>, nThreads?: number,
+               device?: 'auto' | 'gpu' | 'host'): 'gpu' | 'host';
     generate(params: GenParams, docFirst?: number): void;
     run(): void;
     runAsync(): Promise<void>;

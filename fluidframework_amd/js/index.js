@@ -334,13 +334,17 @@ class ReplayBatch {
         else pb.clients.forEach((c, i) => n.setClients(this.h, i, c));
         n.ingest(this.h, pb.ops, pb.docOpOff, pb.text.subarray(0, Math.max(1, pb.nText)), pb.props);
     }
-    // native ingest (mt_pack_json on host threads): per document the JSON text of its message
-    // array (the file driver's messages.json) or the array itself
-    ingestJson(docs, nThreads = 0) {
+    // native ingest: per document the JSON text of its message array (the file driver's
+    // messages.json) or the array itself; device 'auto' parses on the GPU (mt_json_gpu.hip) and
+    // falls back to the host parser (mt_pack_json) outside its fast path, 'gpu' / 'host' force one.
+    // Returns the parser that ran ('gpu' | 'host').
+    ingestJson(docs, nThreads = 0, device = 'auto') {
         const texts = docs.map((d) => (typeof d === 'string' ? d : JSON.stringify(d)));
-        native().ingestJson(this.h, texts, this.clients.length ? this.clients[0].longClientId : 'readonly', nThreads);
+        const path = native().ingestJson(this.h, texts, this.clients.length ? this.clients[0].longClientId : 'readonly',
+                                         nThreads, device);
         this.queued = false;
         for (const c of this.clients) c.messages = [];
+        return path;
     }
     ingestMessages(docs) {
         docs.forEach((msgs, i) => { for (const m of msgs) this.clients[i].applyMsg(m); });

@@ -100,14 +100,37 @@ void *typed(napi_env env, napi_value v, size_t *len) {
 
 void finalize_batch(napi_env, void *data, void *) { mt_batch_destroy(static_cast<mt_batch *>(data)); }
 
-// ingestJson(h, [jsonText per document], observer, nThreads): native parse + pack of
-// ISequencedDocumentMessage logs on host threads (mt_pack_json), then mt_batch_ingest_packed
+// ingestJson(h, [jsonText per document], observer, nThreads, device) -> "gpu" | "host":
+// device "gpu" / "auto": the GPU parser (mt_batch_ingest_json_gpu); "auto" falls back to the host
+// parser (mt_pack_json on host threads + mt_batch_ingest_packed) for a batch outside its fast path
 napi_value ingest_json(napi_env env, napi_callback_info info) {
-    auto a = args(env, info, 4);
+    auto a = args(env, info, 5);
     mt_batch *b = batch_of(env, a[0]);
     std::vector<std::string> docs = strs(env, a[1]);
     std::string observer = str(env, a[2]);
     int32_t threads = (int32_t)i64(env, a[3]);
+    napi_valuetype t;
+    napi_typeof(env, a[4], &t);
+    const std::string device = t == napi_string ? str(env, a[4]) : std::string("auto");
+    if (observer.empty()) observer = "readonly";
+    napi_value path;
+    if (device != "host") {
+        std::string all;
+        std::vector<int64_t> off(1, 0);
+        for (const auto &d : docs) {
+            all += d;
+            off.push_back((int64_t)all.size());
+        }
+        int64_t bad = -1;
+        mt_json_gpu_stats st{};
+        const int rc = mt_batch_ingest_json_gpu(b, all.data(), off.data(), nullptr, observer.c_str(), &bad, &st);
+        if (rc == MT_OK) {
+            napi_create_string_utf8(env, "gpu", NAPI_AUTO_LENGTH, &path);
+            return path;
+        }
+        if (rc != MT_UNSUPPORTED || device == "gpu")
+            return throw_mt(env, rc, ("mt_batch_ingest_json_gpu: document " + std::to_string(bad)).c_str());
+    }
     std::vector<const char *> ptrs;
     std::vector<int64_t> lens;
     for (const auto &d : docs) {
@@ -116,8 +139,7 @@ napi_value ingest_json(napi_env env, napi_callback_info info) {
     }
     mt_packed *p = nullptr;
     int64_t bad = -1;
-    int rc = mt_pack_json(&p, (int64_t)docs.size(), ptrs.data(), lens.data(), observer.empty() ? "readonly" : observer.c_str(),
-                          threads, &bad);
+    int rc = mt_pack_json(&p, (int64_t)docs.size(), ptrs.data(), lens.data(), observer.c_str(), threads, &bad);
     if (rc != MT_OK) {
         std::string why = p ? mt_packed_error(p) : "";
         mt_packed_destroy(p);
@@ -126,7 +148,8 @@ napi_value ingest_json(napi_env env, napi_callback_info info) {
     rc = mt_batch_ingest_packed(b, p);
     mt_packed_destroy(p);
     MT_OK_OR_THROW(rc, "mt_batch_ingest_packed");
-    return nullptr;
+    napi_create_string_utf8(env, "host", NAPI_AUTO_LENGTH, &path);
+    return path;
 }
 
 // createBatch(nDocs, {segCap, maxRetries}) -> external handle (mt_batch_create)

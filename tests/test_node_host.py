@@ -125,3 +125,29 @@ const { ReplayBatch } = require('./fluidframework_amd/js');
     for pos, seg in ((0, mk), (0, "abc d"), (0, mk), (7, "ef"), (8, mk)):
         od.local_op({"type": 0, "pos1": pos, "seg": seg})
     assert int(got["cdigest"]) == od.digest()
+
+
+@pytest.mark.gpu
+def test_node_ingest_json_on_the_gpu():
+    """ReplayBatch.ingestJson parses on the GPU (mt_batch_ingest_json_gpu) and replays exactly like
+    the host parser's batch; a batch outside the GPU fast path falls back to the host parser."""
+    code = r"""
+const { ReplayBatch } = require('./fluidframework_amd/js');
+const msg = (c, s, r, op) => ({ clientId: c, sequenceNumber: s, referenceSequenceNumber: r,
+                                minimumSequenceNumber: 0, type: 'op', contents: op });
+const docs = [[msg('A', 1, 0, { type: 0, pos1: 0, seg: 'hello world' }),
+               msg('B', 2, 1, { type: 2, pos1: 0, pos2: 5, props: { bold: true } }),
+               msg('A', 3, 2, { type: 1, pos1: 5, pos2: 6 })],
+              [msg('C', 1, 0, { type: 0, pos1: 0, seg: { text: 'xyz', props: { k: 'v' } } })]];
+const g = new ReplayBatch(2), h = new ReplayBatch(2), f = new ReplayBatch(1);
+const pg = g.ingestJson(docs, 0, 'gpu'), ph = h.ingestJson(docs, 0, 'host');
+const pf = f.ingestJson([[msg('A', 1, 0, { type: 0, pos1: 0, seg: { text: 'a', props: { n: 1.5 } } })]]);
+g.run(); h.run(); f.run();
+const dg = g.deviceDigests(), dh = h.deviceDigests();
+process.stdout.write(JSON.stringify({ pg, ph, pf, same: dg[0] === dh[0] && dg[1] === dh[1],
+                                      text: g.client(0).getText() }));
+"""
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    assert got == {"pg": "gpu", "ph": "host", "pf": "host", "same": True, "text": "helloworld"}
