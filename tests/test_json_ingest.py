@@ -197,3 +197,22 @@ def test_reconnect_streams_pack_identically():
     pj.close()
     assert (got.ops == want.ops).all() and (got.props == want.props).all() and got.values == want.values
     assert (got.ops["type"] == oplog.OP_REGENERATE).any()
+
+
+def test_records_to_json_round_trips_generated_logs():
+    """oplog.records_to_json (the JSON workloads of tools/bench_json.py): the exported messages
+    replay on the oracle to the same text and properties as the packed records they came from."""
+    from fluidframework_amd.mtreplay import GEN_KEYS, GEN_VALUES, gen_client_names
+
+    p = O.gen_params(1500, pct_insert=55, pct_remove=35, seed=0x5EED)
+    ops, text, props, off = O.gen_batch(p, 4)
+    texts = oplog.records_to_json(ops, off, text, props, GEN_KEYS, GEN_VALUES, gen_client_names(8))
+    t, names = O.gen_tables(), O.gen_client_names(8)
+    for d, js in enumerate(texts):
+        ref = O.replay_doc(ops[off[d]:off[d + 1]].copy(), text, props, t, names)
+        od = O.Doc()
+        od.start_collab("readonly")
+        for m in json.loads(js):
+            assert od.apply_msg(json.dumps(m)) == 0, od.error
+        assert od.text() == ref.text() and od.props_runs() == ref.props_runs()
+    _assert_same([json.loads(js) for js in texts])
