@@ -363,6 +363,8 @@ extern "C" __global__ __launch_bounds__(64) void jg_seg_c_kernel(Params P) {
 }
 
 // ---------------------------------------------------------------- lane-serial JSON reading
+// (host-callable too: tests/jg_parse_asan.cpp runs the lane parser on the CPU under
+// AddressSanitizer over valid and mutated logs, checking every read and write stays in bounds)
 struct Rd {
     // a lane's cursor over one document; bytes come through a 16-byte window (one aligned 128-bit
     // load per 16 bytes instead of a load per byte)
@@ -370,9 +372,9 @@ struct Rd {
     uint32_t p, n;
     uint32_t sh, wb = 0xFFFFFFFFu;
     uint4 w;
-    __device__ Rd(const uint8_t *s_, uint32_t p_, uint32_t n_)
+    __host__ __device__ Rd(const uint8_t *s_, uint32_t p_, uint32_t n_)
         : s(s_), p(p_), n(n_), sh((uint32_t)((uintptr_t)s_ & 15u)) {}
-    __device__ uint32_t b(uint32_t k) {
+    __host__ __device__ uint32_t b(uint32_t k) {
         const uint32_t ak = k + sh, blk = ak & ~15u;
         if (blk != wb) {
             wb = blk;
@@ -382,15 +384,15 @@ struct Rd {
         const uint32_t word = o < 8 ? (o < 4 ? w.x : w.y) : (o < 12 ? w.z : w.w);
         return (word >> ((o & 3u) * 8u)) & 0xFFu;
     }
-    __device__ int at() { return p < n ? (int)b(p) : -1; }
-    __device__ void ws() {
+    __host__ __device__ int at() { return p < n ? (int)b(p) : -1; }
+    __host__ __device__ void ws() {
         while (p < n) {
             const uint32_t c = b(p);
             if (c == ' ' || c == '\t' || c == '\n' || c == '\r') p++;
             else break;
         }
     }
-    __device__ bool lit(const char *wd, uint32_t k) {
+    __host__ __device__ bool lit(const char *wd, uint32_t k) {
         if (n - p < k) return false;
         for (uint32_t i = 0; i < k; i++)
             if (b(p + i) != (uint8_t)wd[i]) return false;
@@ -398,13 +400,13 @@ struct Rd {
         return true;
     }
     // the key / string span [o, o + l) equals the C string wd
-    __device__ bool is(uint32_t o, uint32_t l, const char *wd) {
+    __host__ __device__ bool is(uint32_t o, uint32_t l, const char *wd) {
         uint32_t i = 0;
         for (; wd[i]; i++)
             if (i >= l || b(o + i) != (uint8_t)wd[i]) return false;
         return i == l;
     }
-    __device__ bool eq(uint32_t o1, uint32_t l1, uint32_t o2, uint32_t l2) {
+    __host__ __device__ bool eq(uint32_t o1, uint32_t l1, uint32_t o2, uint32_t l2) {
         if (l1 != l2) return false;
         for (uint32_t i = 0; i < l1; i++)
             if (b(o1 + i) != b(o2 + i)) return false;
@@ -412,8 +414,8 @@ struct Rd {
     }
 };
 
-__device__ __forceinline__ bool is_digit(int c) { return c >= '0' && c <= '9'; }
-__device__ __forceinline__ int hexv(int c) {
+__host__ __device__ __forceinline__ bool is_digit(int c) { return c >= '0' && c <= '9'; }
+__host__ __device__ __forceinline__ int hexv(int c) {
     if (c >= '0' && c <= '9') return c - '0';
     if (c >= 'a' && c <= 'f') return c - 'a' + 10;
     if (c >= 'A' && c <= 'F') return c - 'A' + 10;
@@ -421,7 +423,7 @@ __device__ __forceinline__ int hexv(int c) {
 }
 
 // a string token: raw span of its contents; plain = no escapes, ASCII only
-__device__ bool str_raw(Rd &r, uint32_t &off, uint32_t &len, bool &plain) {
+__host__ __device__ bool str_raw(Rd &r, uint32_t &off, uint32_t &len, bool &plain) {
     if (r.at() != '"') return false;
     r.p++;
     off = r.p;
@@ -457,7 +459,7 @@ __device__ bool str_raw(Rd &r, uint32_t &off, uint32_t &len, bool &plain) {
 
 // a text string decoded to UTF-16 code units exactly as mt_json.cpp Dom::string (\u escapes
 // kept as code units, UTF-8 -> UTF-16 with surrogate pairs); dst may be null (count only)
-__device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bool &ends_nl) {
+__host__ __device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bool &ends_nl) {
     if (r.at() != '"') return false;
     r.p++;
     units = 0;
@@ -531,7 +533,7 @@ __device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bo
 
 // a number token: 1 = canonical integer (no fraction / exponent, <= 18 digits) in v,
 // 2 = another JSON number, 0 = not one the fast path reads like the host (strtod) would
-__device__ int num_tok(Rd &r, int64_t &v, uint32_t &ndig) {
+__host__ __device__ int num_tok(Rd &r, int64_t &v, uint32_t &ndig) {
     uint32_t p = r.p;
     bool neg = false;
     if (p < r.n && r.b(p) == '-') {
@@ -578,7 +580,7 @@ __device__ int num_tok(Rd &r, int64_t &v, uint32_t &ndig) {
 }
 
 // any JSON value, validated (strings, numbers, literals, nesting up to 64 levels)
-__device__ bool skip_value(Rd &r) {
+__host__ __device__ bool skip_value(Rd &r) {
     uint64_t stack = 0;  // bit k: container k is an object
     int sd = 0;
     bool want_key = false;
@@ -646,7 +648,7 @@ __device__ bool skip_value(Rd &r) {
     }
 }
 
-__device__ __forceinline__ bool span_eq(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
+__host__ __device__ __forceinline__ bool span_eq(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
     if (la != lb) return false;
     for (uint32_t i = 0; i < la; i++)
         if (a[i] != b[i]) return false;
@@ -684,7 +686,7 @@ struct OpInfo {
 enum { kOType = 1, kOPos1 = 2, kOPos2 = 4, kOSeg = 8, kOProps = 16, kOOps = 32 };
 
 // an op object's members (pack_op / flatten / relpos / register rules, mt_json.cpp:596-649)
-__device__ uint32_t parse_op(Rd &r, OpInfo &op) {
+__host__ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
     if (r.at() != '{') return kFShape;
     r.p++;
     r.ws();
@@ -800,7 +802,7 @@ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
 // a flat props object -> prop records (JS key order = insertion order: array-index keys leave
 // the fast path; duplicates too)
 template <bool W>
-__device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const Ctx &cx) {
+__host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const Ctx &cx) {
     if (r.at() != '{') return kFShape;
     r.p++;
     r.ws();
@@ -909,7 +911,7 @@ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const Ctx &cx)
 
 // one member op -> one record (Packer1::pack_op / pack_seg)
 template <bool W>
-__device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, const mt_op &base, MsgOut &mo,
+__host__ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, const mt_op &base, MsgOut &mo,
                             const Ctx &cx) {
     if (!(op.seen & kOType)) return kFShape;
     if (!(op.seen & kOPos1)) return kFShape;  // a position from relativePos1 only: host path
@@ -1069,7 +1071,7 @@ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, cons
 
 // one message (Packer1::run's loop body): returns fail bits
 template <bool W>
-__device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0, MsgOut &mo, const Ctx &cx) {
+__host__ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0, MsgOut &mo, const Ctx &cx) {
     Rd r{s, p0 + 1, n};  // after '{'
     enum { kCl = 1, kSeq = 2, kRef = 4, kMsn = 8, kTy = 16, kCo = 32 };
     uint32_t seen = 0, contents_p = 0;
