@@ -3,11 +3,12 @@
 // The device parses per-document ISequencedDocumentMessage JSON arrays (the file driver's
 // messages.json: fileDeltaStorageService.ts:23-31) into the packed records of mt_oplog.h with
 // exactly the rules of mt_json.cpp's host parser (itself equal to the Python / JS packers), for
-// the observer fast path: sequenced messages whose contents are insert (text or {text, props}),
-// remove, annotate (no combiningOp) or a one-level GROUP of those, property values that are
-// null / true / false / canonical integers / plain ASCII strings.  Anything else (markers,
-// relative positions, writer replicas, snapshots, escapes in keys or values, floats, nested
-// values, duplicate keys, > 253 clients, malformed JSON) is reported as "host parser needed"
+// the observer fast path: sequenced messages whose contents are insert (text, {text, props} or a
+// marker), remove, annotate (no combiningOp or rewrite), relative positions, or a one-level GROUP
+// of those, property values that are null / true / false / canonical integers / plain ASCII
+// strings / flat arrays of those in JSON.stringify form.  Anything else (writer replicas,
+// snapshots, escapes in keys or values, floats, objects as values, duplicate keys, > 253
+// clients, malformed JSON) is reported as "host parser needed"
 // (MT_UNSUPPORTED + the first such document): the caller runs mt_pack_json for that batch.
 #ifndef MT_JSON_GPU_H
 #define MT_JSON_GPU_H

@@ -42,6 +42,7 @@ namespace mt {
 namespace jg {
 
 constexpr uint32_t kNullSpan = 0xFFFFFFFFu;
+constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // mt_device.h: a RELPOS key the host cannot resolve
 constexpr int kClientSlots = 512;  // per-document client hash table (<= 253 distinct names)
 constexpr int kMaxProps = 16;      // keys per props object on the fast path
 
@@ -64,7 +65,7 @@ struct Params {
     int64_t D;
     // per message (region of document d starts at doc_off[d] / 64 + 2 d)
     uint32_t *m_start, *m_flags, *m_nrec, *m_ntext, *m_nprop, *m_recoff, *m_textoff, *m_propoff;
-    uint32_t *m_cloff, *m_cllen, *m_cid, *m_npops;
+    uint32_t *m_cloff, *m_cllen, *m_cid, *m_npops, *m_nval, *m_valoff;
     const int32_t *chunk_doc;        // count / write passes: one wave per 64 messages of a document
     const uint32_t *chunk_first;
     // structural scan: one wave per kSegBytes of a document (segment g: doc seg_doc[g], bytes from
@@ -76,7 +77,7 @@ struct Params {
     uint32_t *sg_q, *sg_pre, *sg_post, *sg_flags, *sg_nmsg, *sg_fail, *sg_starts;
     int32_t *sg_d0, *sg_d1;
     // per document
-    uint32_t *d_nmsg, *d_fail, *d_nrec, *d_ntext, *d_nprop, *d_npropops, *d_nnames, *d_nuk, *d_nuv;
+    uint32_t *d_nmsg, *d_fail, *d_nrec, *d_ntext, *d_nprop, *d_npropops, *d_nnames, *d_nuk, *d_nuv, *d_nval;
     uint32_t *cl_ht;                 // kClientSlots per document
     uint32_t *nm_off, *nm_len;       // per message region: client id k's span at index k - 1
     uint32_t *names;                 // per document 256 x {off, len}: ids 1.. (compact, for the host)
@@ -87,6 +88,10 @@ struct Params {
     const uint64_t *text_dst;        // per document: first code unit of its text in `text`
     const uint32_t *text_pay;        // per document: payload of its first code unit
     const uint32_t *prop_base;       // per document: first prop record (batch-global)
+    // value events: every interned value in the host packer's value() order — a relative
+    // position's id, then the op's prop values; per document from val_base[d]
+    const uint32_t *val_base;
+    uint32_t *pe;                    // per prop record: its value event
     mt_op *ops;
     uint16_t *text;
     mt_prop *props;
@@ -662,7 +667,7 @@ __device__ __forceinline__ uint32_t fnv32(const uint8_t *p, uint32_t n) {
 
 // ---------------------------------------------------------------- per-message parse
 struct MsgOut {
-    uint32_t nrec = 0, ntext = 0, nprop = 0, npropops = 0;
+    uint32_t nrec = 0, ntext = 0, nprop = 0, npropops = 0, nval = 0;
     uint32_t cl_off = kNullSpan, cl_len = 4, flags = 0;
 };
 
@@ -671,7 +676,8 @@ struct Ctx {  // write pass
     uint16_t *text = nullptr;   // this message's first code unit
     uint32_t pay = 0;           // payload of that code unit
     uint32_t gprop = 0;         // batch-global index of this message's first prop record
-    uint32_t *pk_off, *pk_len, *pv_off, *pv_len;
+    uint32_t gval = 0;          // batch-global index of this message's first value event
+    uint32_t *pk_off, *pk_len, *pv_off, *pv_len, *pe;  // keys per prop record, values per event
     uint8_t cid = 0;
     bool install = false;
 };
@@ -679,11 +685,11 @@ struct Ctx {  // write pass
 struct OpInfo {
     int64_t type = -1;
     int32_t p1 = 0, p2 = 0;
-    uint32_t seg_p = 0, props_p = 0, ops_p = 0;
+    uint32_t seg_p = 0, props_p = 0, ops_p = 0, rel1_p = 0, rel2_p = 0;
     uint32_t seen = 0;
     bool rewrite = false;
 };
-enum { kOType = 1, kOPos1 = 2, kOPos2 = 4, kOSeg = 8, kOProps = 16, kOOps = 32 };
+enum { kOType = 1, kOPos1 = 2, kOPos2 = 4, kOSeg = 8, kOProps = 16, kOOps = 32, kORel1 = 64, kORel2 = 128 };
 
 // an op object's members (pack_op / flatten / relpos / register rules, mt_json.cpp:596-649)
 __host__ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
@@ -712,6 +718,8 @@ __host__ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
         else if (r.is(ko, kl, "seg")) bit = kOSeg;
         else if (r.is(ko, kl, "props")) bit = kOProps;
         else if (r.is(ko, kl, "ops")) bit = kOOps;
+        else if (r.is(ko, kl, "relativePos1")) bit = kORel1;
+        else if (r.is(ko, kl, "relativePos2")) bit = kORel2;
         if (bit) {
             if (op.seen & bit) return kFShape;  // a repeated key: the host keeps the last value
             op.seen |= bit;
@@ -729,6 +737,8 @@ __host__ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
             if (bit == kOSeg) op.seg_p = r.p;
             if (bit == kOProps) op.props_p = r.p;
             if (bit == kOOps) op.ops_p = r.p;
+            if (bit == kORel1) op.rel1_p = r.p;
+            if (bit == kORel2) op.rel2_p = r.p;
             if (!bit) {
                 // combiningOp (a falsy one is ignored), register (null is absent): anything else
                 // and relative positions leave the fast path
@@ -780,7 +790,6 @@ __host__ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
                     }
                     return kFShape;
                 }
-                if (r.is(ko, kl, "relativePos1") || r.is(ko, kl, "relativePos2")) return kFShape;
             }
             if (!skip_value(r)) return kFSyntax;
         }
@@ -802,7 +811,7 @@ __host__ __device__ uint32_t parse_op(Rd &r, OpInfo &op) {
 // a flat props object -> prop records (JS key order = insertion order: array-index keys leave
 // the fast path; duplicates too)
 template <bool W>
-__host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const Ctx &cx) {
+__host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, uint32_t gev, const Ctx &cx) {
     if (r.at() != '{') return kFShape;
     r.p++;
     r.ws();
@@ -891,8 +900,9 @@ __host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const
         if (W) {
             cx.pk_off[gidx + np] = ko;
             cx.pk_len[gidx + np] = kl;
-            cx.pv_off[gidx + np] = vo;
-            cx.pv_len[gidx + np] = vl;
+            cx.pe[gidx + np] = gev + np;
+            cx.pv_off[gev + np] = vo;
+            cx.pv_len[gev + np] = vl;
         }
         np++;
         r.ws();
@@ -909,12 +919,113 @@ __host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, const
     }
 }
 
+// Packer1::relpos (mt_json.cpp:560-594): posN undefined and relativePosN truthy (N = 2 only for
+// remove / annotate) -> an MT_OP_RELPOS record before the op (GROUP_CONT); a truthy id is a value
+// event (its JSON text: a plain string, an integer or true), pos1 / pos2 = event + 1 until the remap
+template <bool W>
+__host__ __device__ uint32_t relpos_record(const uint8_t *s, uint32_t n, const OpInfo &op, const mt_op &base,
+                                           MsgOut &mo, const Ctx &cx) {
+    mt_op rr = base;
+    rr.type = MT_OP_RELPOS;
+    uint32_t rflags = MT_OPF_GROUP_CONT;
+    for (int k = 0; k < 2; k++) {
+        if ((op.seen & (k ? kOPos2 : kOPos1)) || !(op.seen & (k ? kORel2 : kORel1))) continue;
+        if (k == 1 && op.type != 1 && op.type != 2) continue;
+        Rd rq{s, k ? op.rel2_p : op.rel1_p, n};
+        if (rq.lit("null", 4) || rq.lit("false", 5)) continue;  // falsy: no relative position
+        if (rq.at() != '{') return kFShape;
+        rflags |= k ? MT_RELF_POS2 : MT_RELF_POS1;
+        rq.p++;
+        rq.ws();
+        uint32_t seen_k = 0;
+        if (rq.at() != '}') {
+            for (;;) {
+                rq.ws();
+                uint32_t ko, kl;
+                bool plain;
+                if (!str_raw(rq, ko, kl, plain)) return kFSyntax;
+                if (!plain) return kFShape;
+                rq.ws();
+                if (rq.at() != ':') return kFSyntax;
+                rq.p++;
+                rq.ws();
+                const uint32_t bit = rq.is(ko, kl, "id") ? 1u : rq.is(ko, kl, "before") ? 2u : rq.is(ko, kl, "offset") ? 4u : 0u;
+                if (bit & seen_k) return kFShape;
+                seen_k |= bit;
+                const uint32_t vo = rq.p;
+                const int c = rq.at();
+                if (bit == 1u || bit == 2u) {
+                    bool truthy = false;
+                    if (c == '"') {
+                        uint32_t so, sl;
+                        bool pl;
+                        if (!str_raw(rq, so, sl, pl)) return kFSyntax;
+                        if (!pl) return kFShape;
+                        truthy = sl > 0;
+                    } else if (c == '-' || is_digit(c)) {
+                        int64_t v;
+                        uint32_t nd;
+                        if (num_tok(rq, v, nd) != 1 || nd > 15) return kFShape;
+                        truthy = v != 0;
+                    } else if (rq.lit("true", 4)) {
+                        truthy = true;
+                    } else if (!(rq.lit("false", 5) || rq.lit("null", 4))) {
+                        return kFShape;
+                    }
+                    if (truthy && bit == 2u) rflags |= k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1;
+                    if (truthy && bit == 1u) {
+                        const uint32_t ev = cx.gval + mo.nval;
+                        if (W) {
+                            cx.pv_off[ev] = vo;
+                            cx.pv_len[ev] = rq.p - vo;
+                        }
+                        if (k) rr.pos2 = (int32_t)(ev + 1);
+                        else rr.pos1 = (int32_t)(ev + 1);
+                        mo.nval++;
+                    }
+                } else if (bit == 4u) {
+                    // offset !== undefined: an integer, or null (adds 0)
+                    int32_t o = 0;
+                    if (!rq.lit("null", 4)) {
+                        int64_t v;
+                        uint32_t nd;
+                        if (num_tok(rq, v, nd) != 1 || v < -2147483647ll || v > 2147483647ll) return kFShape;
+                        o = (int32_t)v;
+                    }
+                    rflags |= k ? MT_RELF_OFF2 : MT_RELF_OFF1;
+                    if (k) rr.payload_len = (uint32_t)o;
+                    else rr.payload = (uint32_t)o;
+                } else if (!skip_value(rq)) {
+                    return kFSyntax;
+                }
+                rq.ws();
+                if (rq.at() == ',') {
+                    rq.p++;
+                    continue;
+                }
+                if (rq.at() == '}') break;
+                return kFSyntax;
+            }
+        }
+    }
+    if (rflags & (MT_RELF_POS1 | MT_RELF_POS2)) {
+        rr.flags = (uint16_t)rflags;
+        if (W) cx.ops[mo.nrec] = rr;
+        mo.nrec++;
+        return 0;
+    }
+    return (op.seen & kOPos1) ? 0u : (uint32_t)kFShape;  // an op without a position
+}
+
 // one member op -> one record (Packer1::pack_op / pack_seg)
 template <bool W>
 __host__ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, const mt_op &base, MsgOut &mo,
                             const Ctx &cx) {
     if (!(op.seen & kOType)) return kFShape;
-    if (!(op.seen & kOPos1)) return kFShape;  // a position from relativePos1 only: host path
+    {
+        const uint32_t f = relpos_record<W>(s, n, op, base, mo, cx);
+        if (f) return f;
+    }
     mt_op r = base;
     r.flags = MT_OPF_GROUP_CONT;  // cleared on the message's last record
     r.pos1 = op.p1;
@@ -1020,7 +1131,7 @@ __host__ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo 
             const int c = rp.at();
             if (c == '{') {
                 hp = true;
-                const uint32_t f = props_obj<W>(rp, np, cx.gprop + mo.nprop, cx);
+                const uint32_t f = props_obj<W>(rp, np, cx.gprop + mo.nprop, cx.gval + mo.nval, cx);
                 if (f) return f;
             } else if (!(rp.lit("null", 4) || rp.lit("false", 5))) {
                 return kFShape;  // arrays fail, other truthy values fail, 0 / "" are rare: host
@@ -1046,6 +1157,7 @@ __host__ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo 
         }
         mo.ntext += units;
         mo.nprop += np;
+        mo.nval += np;
     } else if (op.type == 1 || op.type == 2) {
         r.type = op.type == 1 ? MT_OP_REMOVE : MT_OP_ANNOTATE;
         r.pos2 = (op.seen & kOPos2) ? op.p2 : 0;
@@ -1053,12 +1165,13 @@ __host__ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo 
             if (!(op.seen & kOProps)) return kFShape;
             Rd rp{s, op.props_p, n};
             uint32_t np = 0;
-            const uint32_t f = props_obj<W>(rp, np, cx.gprop + mo.nprop, cx);
+            const uint32_t f = props_obj<W>(rp, np, cx.gprop + mo.nprop, cx.gval + mo.nval, cx);
             if (f) return f;
             r.payload = cx.gprop + mo.nprop;
             r.payload_len = np;
             if (op.rewrite) r.flags |= (uint16_t)MT_OPF_REWRITE;
             mo.nprop += np;
+            mo.nval += np;
             mo.npropops++;
         }
     } else {
@@ -1219,6 +1332,8 @@ __device__ void parse_chunk(const Params &P) {
         cx.text = P.text + P.text_dst[d] + P.m_textoff[m];
         cx.pay = P.text_pay[d] + P.m_textoff[m];
         cx.gprop = P.prop_base[d] + P.m_propoff[m];
+        cx.gval = P.val_base[d] + P.m_valoff[m];
+        cx.pe = P.pe;
         cx.pk_off = P.pk_off;
         cx.pk_len = P.pk_len;
         cx.pv_off = P.pv_off;
@@ -1234,6 +1349,7 @@ __device__ void parse_chunk(const Params &P) {
         P.m_ntext[m] = mo.ntext;
         P.m_nprop[m] = mo.nprop;
         P.m_npops[m] = mo.npropops;
+        P.m_nval[m] = mo.nval;
         P.m_cloff[m] = mo.cl_off;
         P.m_cllen[m] = mo.cl_len;
     }
@@ -1248,29 +1364,34 @@ extern "C" __global__ __launch_bounds__(64) void jg_offsets_kernel(Params P) {
     const int lane = lane_id();
     const uint64_t mb = mregion(P.doc_off, d);
     const uint32_t nmsg = P.d_nmsg[d];
-    uint32_t sr = 0, st = 0, sp = 0, so = 0;
+    uint32_t sr = 0, st = 0, sp = 0, so = 0, sv = 0;
     for (uint32_t i0 = 0; i0 < nmsg; i0 += 64) {
         const uint32_t i = i0 + (uint32_t)lane;
         const bool valid = i < nmsg;
         const uint64_t m = mb + i;
         const uint32_t nr = valid ? P.m_nrec[m] : 0u, nt = valid ? P.m_ntext[m] : 0u;
         const uint32_t np = valid ? P.m_nprop[m] : 0u, no = valid ? P.m_npops[m] : 0u;
+        const uint32_t nv = valid ? P.m_nval[m] : 0u;
         const uint32_t ir = wave_incl(nr), it = wave_incl(nt), ip = wave_incl(np), io = wave_incl(no);
+        const uint32_t iv = wave_incl(nv);
         if (valid) {
             P.m_recoff[m] = sr + ir - nr;
             P.m_textoff[m] = st + it - nt;
             P.m_propoff[m] = sp + ip - np;
+            P.m_valoff[m] = sv + iv - nv;
         }
         sr += __shfl(ir, 63, 64);
         st += __shfl(it, 63, 64);
         sp += __shfl(ip, 63, 64);
         so += __shfl(io, 63, 64);
+        sv += __shfl(iv, 63, 64);
     }
     if (lane == 0) {
         P.d_nrec[d] = sr;
         P.d_ntext[d] = st;
         P.d_nprop[d] = sp;
         P.d_npropops[d] = so;
+        P.d_nval[d] = sv;
     }
 }
 
@@ -1394,20 +1515,20 @@ extern "C" __global__ __launch_bounds__(64) void jg_clients_kernel(Params P) {
 extern "C" __global__ __launch_bounds__(64) void jg_props_kernel(Params P) {
     const int64_t d = blockIdx.x;
     if (d >= P.D) return;
-    const uint32_t n = P.d_nprop[d];
-    const uint64_t pb = P.prop_base[d];
+    const uint32_t n = P.d_nprop[d], ne = P.d_nval[d];
+    const uint64_t pb = P.prop_base[d], vb = P.val_base[d];
     const uint32_t cap = P.ht_cap[d];
     uint32_t *tk = P.ht + P.ht_base[d], *tv = tk + cap;
     const uint8_t *s = P.J + P.doc_off[d];
     Spans K{s, P.pk_off, P.pk_len, pb, P.obs + 256};
-    Spans V{s, P.pv_off, P.pv_len, pb, P.obs + 256};
+    Spans V{s, P.pv_off, P.pv_len, vb, P.obs + 256};
     const uint32_t nk = intern(tk, cap, K, n, 0u, P.lk, P.uk_off, P.uk_len, [](uint32_t) { return false; });
     const uint32_t *pvo = P.pv_off;
-    auto is_null = [&](uint32_t i) { return pvo[pb + i] == kNullSpan; };
-    for (uint32_t i = (uint32_t)lane_id(); i < n; i += 64)
-        if (is_null(i)) P.lv[pb + i] = 0;
+    auto is_null = [&](uint32_t i) { return pvo[vb + i] == kNullSpan; };
+    for (uint32_t i = (uint32_t)lane_id(); i < ne; i += 64)
+        if (is_null(i)) P.lv[vb + i] = 0;
     __syncthreads();
-    const uint32_t nv = intern(tv, cap, V, n, 1u, P.lv, P.uv_off, P.uv_len, is_null);
+    const uint32_t nv = intern(tv, cap, V, ne, 1u, P.lv, P.uv_off, P.uv_len, is_null);
     if (lane_id() == 0) {
         P.d_nuk[d] = nk;
         P.d_nuv[d] = nv;
@@ -1419,10 +1540,19 @@ extern "C" __global__ __launch_bounds__(64) void jg_remap_kernel(Params P) {
     const int64_t d = blockIdx.x;
     if (d >= P.D) return;
     const uint32_t n = P.d_nprop[d];
-    const uint64_t pb = P.prop_base[d];
+    const uint64_t pb = P.prop_base[d], vb = P.val_base[d];
     for (uint32_t i = (uint32_t)lane_id(); i < n; i += 64) {
-        const uint32_t k = P.lk[pb + i], v = P.lv[pb + i];
-        P.props[pb + i] = mt_prop{P.kmap[pb + k], v ? P.vmap[pb + v - 1] : 0u};
+        const uint32_t k = P.lk[pb + i], v = P.lv[P.pe[pb + i]];
+        P.props[pb + i] = mt_prop{P.kmap[pb + k], v ? P.vmap[vb + v - 1] : 0u};
+    }
+    // relative positions: value event + 1 -> the batch value id of the id (0: none)
+    const int64_t o0 = P.op_base[d], o1 = o0 + P.d_nrec[d];
+    for (int64_t i = o0 + lane_id(); i < o1; i += 64) {
+        if (P.ops[i].type != MT_OP_RELPOS) continue;
+        const uint32_t e1 = (uint32_t)P.ops[i].pos1, e2 = (uint32_t)P.ops[i].pos2;
+        const uint32_t v1 = e1 ? P.lv[e1 - 1] : 0u, v2 = e2 ? P.lv[e2 - 1] : 0u;
+        P.ops[i].pos1 = (int32_t)(v1 ? P.vmap[vb + v1 - 1] : 0u);
+        P.ops[i].pos2 = (int32_t)(v2 ? P.vmap[vb + v2 - 1] : 0u);
     }
 }
 
@@ -1436,7 +1566,7 @@ extern "C" __global__ __launch_bounds__(64) void jg_markers_kernel(const mt_op *
                                                                  uint32_t *n_ids, uint32_t *tile_annot) {
     const int64_t d = blockIdx.x;
     if (d >= D) return;
-    uint32_t cnt = 0, tile = 0;
+    uint32_t cnt = 0, tile = 0, annot_mk = 0;
     for (int64_t i = op_off[d] + lane_id(); i < op_off[d + 1]; i += 64) {
         mt_op o = ops[i];
         if (o.type == MT_OP_INSERT && (o.flags & MT_OPF_MARKER)) {
@@ -1449,13 +1579,25 @@ extern "C" __global__ __launch_bounds__(64) void jg_markers_kernel(const mt_op *
             ops_w[i].payload_len = id;
             cnt += id != 0;
         } else if (o.type == MT_OP_ANNOTATE) {
-            for (uint32_t q = 0; q < o.payload_len; q++)
+            for (uint32_t q = 0; q < o.payload_len; q++) {
                 if (props[o.payload + q].key == tile_key) tile = 1;
+                if (props[o.payload + q].key == mk_key) annot_mk = 1;
+            }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
         cnt += __shfl_xor(cnt, off, 64);
         tile |= __shfl_xor(tile, off, 64);
+        annot_mk |= __shfl_xor(annot_mk, off, 64);
+    }
+    // relative positions: an id's value -> its key; a document whose annotates touch markerId gets
+    // kIdKeyUnsupported (resolve_marker_ids: the reference re-maps a re-annotated id only at a
+    // later blockUpdate)
+    for (int64_t i = op_off[d] + lane_id(); i < op_off[d + 1]; i += 64) {
+        if (ops[i].type != MT_OP_RELPOS) continue;
+        const uint32_t v1 = (uint32_t)ops[i].pos1, v2 = (uint32_t)ops[i].pos2;
+        ops_w[i].pos1 = (int32_t)(annot_mk ? kIdKeyUnsupported : (v1 < n_values ? vkey[v1] : 0u));
+        ops_w[i].pos2 = (int32_t)(annot_mk ? kIdKeyUnsupported : (v2 < n_values ? vkey[v2] : 0u));
     }
     if (lane_id() == 0) {
         n_ids[d] = cnt;
@@ -1552,10 +1694,10 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     const size_t M = (size_t)(total / 64 + 2 * (uint64_t)D + 2);
     uint32_t **marr[] = {&P.m_start, &P.m_flags, &P.m_nrec, &P.m_ntext, &P.m_nprop, &P.m_recoff,
                          &P.m_textoff, &P.m_propoff, &P.m_cloff, &P.m_cllen, &P.m_cid, &P.nm_off, &P.nm_len,
-                         &P.m_npops};
+                         &P.m_npops, &P.m_nval, &P.m_valoff};
     for (uint32_t **a : marr) JGCHK(B.get(a, M));
     uint32_t **darr[] = {&P.d_nmsg, &P.d_fail, &P.d_nrec, &P.d_ntext, &P.d_nprop, &P.d_npropops,
-                         &P.d_nnames, &P.d_nuk, &P.d_nuv};
+                         &P.d_nnames, &P.d_nuk, &P.d_nuv, &P.d_nval};
     for (uint32_t **a : darr) JGCHK(B.get(a, (size_t)D));
     JGCHK(hipMemsetAsync(P.d_nrec, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_ntext, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
@@ -1641,7 +1783,7 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(hipEventRecord(ev[2], s));
     if (D) JGCHK(hipLaunchKernel((const void *)jg_clients_kernel, dim3(grid), dim3(64), argc, 0, s));
     JGCHK(hipEventRecord(ev[3], s));
-    std::vector<uint32_t> fail, nrec, ntext, nprop, npops;
+    std::vector<uint32_t> fail, nrec, ntext, nprop, npops, nval;
     JGCHK(dl(fail, P.d_fail, (size_t)D, s));
     for (int64_t d = 0; d < D; d++)
         if (fail[(size_t)d]) {
@@ -1654,23 +1796,26 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(dl(ntext, P.d_ntext, (size_t)D, s));
     JGCHK(dl(nprop, P.d_nprop, (size_t)D, s));
     JGCHK(dl(npops, P.d_npropops, (size_t)D, s));
+    JGCHK(dl(nval, P.d_nval, (size_t)D, s));
     // batch layout: records and prop records back to back in document order
     res.doc_op_off.assign((size_t)D + 1, 0);
     std::vector<int64_t> op_base((size_t)D);
-    std::vector<uint32_t> prop_base((size_t)D), text_pay((size_t)D);
+    std::vector<uint32_t> prop_base((size_t)D), val_base((size_t)D), text_pay((size_t)D);
     std::vector<uint64_t> text_dst((size_t)D);
-    uint64_t tp = 0, pp = 0;
+    uint64_t tp = 0, pp = 0, vp = 0;
     for (int64_t d = 0; d < D; d++) {
         op_base[(size_t)d] = res.doc_op_off[(size_t)d];
         res.doc_op_off[(size_t)d + 1] = res.doc_op_off[(size_t)d] + nrec[(size_t)d];
         prop_base[(size_t)d] = (uint32_t)pp;
+        val_base[(size_t)d] = (uint32_t)vp;
+        vp += nval[(size_t)d];
         text_pay[(size_t)d] = (uint32_t)tp;
         text_dst[(size_t)d] = tp;
         tp += ntext[(size_t)d];
         pp += nprop[(size_t)d];
         res.n_msgs += nmsg[(size_t)d];
     }
-    if (tp > 0xFFFFFFF0ull || pp > 0x7FFFFFF0ull) return MT_ERR_ARG;
+    if (tp > 0xFFFFFFF0ull || pp > 0x7FFFFFF0ull || vp > 0x7FFFFFF0ull) return MT_ERR_ARG;
     res.n_ops = res.doc_op_off[(size_t)D];
     res.n_text = (int64_t)tp;
     res.n_props = (int64_t)pp;
@@ -1705,28 +1850,32 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     P.install = install != nullptr;
     int64_t *d_opb = nullptr;
     uint64_t *d_tdst = nullptr;
-    uint32_t *d_tpay = nullptr, *d_pb = nullptr;
+    uint32_t *d_tpay = nullptr, *d_pb = nullptr, *d_vb = nullptr;
     JGCHK(B.get(&d_opb, (size_t)D));
     JGCHK(B.get(&d_tdst, (size_t)D));
     JGCHK(B.get(&d_tpay, (size_t)D));
     JGCHK(B.get(&d_pb, (size_t)D));
+    JGCHK(B.get(&d_vb, (size_t)D));
     JGCHK(hipMemcpyAsync(d_opb, op_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice, s));
     JGCHK(hipMemcpyAsync(d_tdst, text_dst.data(), 8 * (size_t)D, hipMemcpyHostToDevice, s));
     JGCHK(hipMemcpyAsync(d_tpay, text_pay.data(), 4 * (size_t)D, hipMemcpyHostToDevice, s));
     JGCHK(hipMemcpyAsync(d_pb, prop_base.data(), 4 * (size_t)D, hipMemcpyHostToDevice, s));
+    JGCHK(hipMemcpyAsync(d_vb, val_base.data(), 4 * (size_t)D, hipMemcpyHostToDevice, s));
     P.op_base = d_opb;
     P.text_dst = d_tdst;
     P.text_pay = d_tpay;
     P.prop_base = d_pb;
-    uint32_t **parr[] = {&P.pk_off, &P.pk_len, &P.pv_off, &P.pv_len, &P.lk, &P.lv,
-                         &P.uk_off, &P.uk_len, &P.uv_off, &P.uv_len};
+    P.val_base = d_vb;
+    uint32_t **parr[] = {&P.pk_off, &P.pk_len, &P.lk, &P.uk_off, &P.uk_len, &P.pe};
     for (uint32_t **a : parr) JGCHK(B.get(a, (size_t)pp));
+    uint32_t **varr[] = {&P.pv_off, &P.pv_len, &P.lv, &P.uv_off, &P.uv_len};
+    for (uint32_t **a : varr) JGCHK(B.get(a, (size_t)vp));
     // prop hash tables: per document two tables of a power of two > 2 x its records
     std::vector<uint64_t> ht_base((size_t)D);
     std::vector<uint32_t> ht_cap((size_t)D);
     uint64_t hsum = 0;
     for (int64_t d = 0; d < D; d++) {
-        ht_cap[(size_t)d] = pow2_at_least(2ull * nprop[(size_t)d] + 1);
+        ht_cap[(size_t)d] = pow2_at_least(2ull * std::max(nprop[(size_t)d], nval[(size_t)d]) + 1);
         ht_base[(size_t)d] = hsum;
         hsum += 2ull * ht_cap[(size_t)d];
     }
@@ -1750,13 +1899,13 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(dl(nuv, P.d_nuv, (size_t)D, s));
     JGCHK(dl(uko, P.uk_off, (size_t)pp, s));
     JGCHK(dl(ukl, P.uk_len, (size_t)pp, s));
-    JGCHK(dl(uvo, P.uv_off, (size_t)pp, s));
-    JGCHK(dl(uvl, P.uv_len, (size_t)pp, s));
+    JGCHK(dl(uvo, P.uv_off, (size_t)vp, s));
+    JGCHK(dl(uvl, P.uv_len, (size_t)vp, s));
     JGCHK(dl(nnames, P.d_nnames, (size_t)D, s));
     std::vector<uint32_t> names;
     JGCHK(dl(names, P.names, (size_t)D * 512, s));  // jg_clients_kernel: names' spans by id - 1
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<uint32_t> kmap((size_t)std::max<uint64_t>(pp, 1)), vmap((size_t)std::max<uint64_t>(pp, 1));
+    std::vector<uint32_t> kmap((size_t)std::max<uint64_t>(pp, 1)), vmap((size_t)std::max<uint64_t>(vp, 1));
     std::unordered_map<std::string, uint32_t> kid, vid{{"null", 0u}};
     res.values.assign(1, "null");
     res.clients.resize((size_t)D);
@@ -1772,14 +1921,15 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
             }
             kmap[pb + i] = it->second;
         }
+        const uint32_t vb = val_base[(size_t)d];
         for (uint32_t i = 0; i < nuv[(size_t)d]; i++) {
-            std::string v(js + uvo[pb + i], uvl[pb + i]);
+            std::string v(js + uvo[vb + i], uvl[vb + i]);
             auto it = vid.find(v);
             if (it == vid.end()) {
                 it = vid.emplace(v, (uint32_t)res.values.size()).first;
                 res.values.push_back(v);
             }
-            vmap[pb + i] = it->second;
+            vmap[vb + i] = it->second;
         }
         auto &nm = res.clients[(size_t)d];
         nm.assign(1, obs);

@@ -57,7 +57,8 @@ static void run_doc(const std::string &d, std::mt19937_64 &rng) {
         mt_op *ops = new mt_op[mo.nrec];
         uint16_t *text = new uint16_t[mo.ntext ? mo.ntext : 1];
         uint32_t *pk_off = new uint32_t[mo.nprop + 1], *pk_len = new uint32_t[mo.nprop + 1];
-        uint32_t *pv_off = new uint32_t[mo.nprop + 1], *pv_len = new uint32_t[mo.nprop + 1];
+        uint32_t *pv_off = new uint32_t[mo.nval + 1], *pv_len = new uint32_t[mo.nval + 1];
+        uint32_t *pe = new uint32_t[mo.nprop + 1];
         Ctx w;
         w.ops = ops;
         w.text = text;
@@ -67,17 +68,29 @@ static void run_doc(const std::string &d, std::mt19937_64 &rng) {
         w.pk_len = pk_len;
         w.pv_off = pv_off;
         w.pv_len = pv_len;
+        w.pe = pe;
+        w.gval = 0;
         w.cid = 1;
         w.install = (rng() & 1) != 0;
         MsgOut mw;
         const uint32_t f = parse_msg<true>(s, n, p0, mw, w);
-        if (f || mw.nrec != mo.nrec || mw.ntext != mo.ntext || mw.nprop != mo.nprop) {
+        if (f || mw.nrec != mo.nrec || mw.ntext != mo.ntext || mw.nprop != mo.nprop || mw.nval != mo.nval) {
             fprintf(stderr, "count / write passes differ at %u\n", p0);
             abort();
         }
-        for (uint32_t q = 0; q < mo.nprop; q++)  // spans inside the document
-            if (pk_off[q] + pk_len[q] > n || (pv_off[q] != kNullSpan && pv_off[q] + pv_len[q] > n)) {
-                fprintf(stderr, "span outside the document at %u\n", p0);
+        for (uint32_t q = 0; q < mo.nprop; q++)  // spans inside the document, events in range
+            if (pk_off[q] + pk_len[q] > n || pe[q] >= mo.nval) {
+                fprintf(stderr, "prop record out of range at %u\n", p0);
+                abort();
+            }
+        for (uint32_t q = 0; q < mo.nval; q++)
+            if (pv_off[q] != kNullSpan && pv_off[q] + pv_len[q] > n) {
+                fprintf(stderr, "value span outside the document at %u\n", p0);
+                abort();
+            }
+        for (uint32_t q = 0; q < mo.nrec; q++)
+            if (ops[q].type == MT_OP_RELPOS && ((uint32_t)ops[q].pos1 > mo.nval || (uint32_t)ops[q].pos2 > mo.nval)) {
+                fprintf(stderr, "relative position event out of range at %u\n", p0);
                 abort();
             }
         parsed++;
@@ -87,6 +100,7 @@ static void run_doc(const std::string &d, std::mt19937_64 &rng) {
         delete[] pk_len;
         delete[] pv_off;
         delete[] pv_len;
+        delete[] pe;
     }
 }
 

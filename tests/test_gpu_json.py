@@ -123,7 +123,8 @@ OUTSIDE = [  # (message, reason) — every one must be reported, never parsed di
                       "combiningOp": {"name": "incr"}}), "combiningOp incr"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
                       "combiningOp": {"defaultValue": 1}}), "combiningOp without a name"),
-    (_msg("A", 1, 0, {"type": 1, "relativePos1": {"id": "m"}, "pos2": 1}), "relative position"),
+    (_msg("A", 1, 0, {"type": 1, "relativePos1": {"id": "m", "offset": 1.5}, "pos2": 1}), "float offset"),
+    (_msg("A", 1, 0, {"type": 1, "relativePos1": {"id": {"x": 1}}, "pos2": 1}), "object id"),
     (_msg("A", -1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "local op"),
     (_msg("readonly", 1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "own op (ack)"),
     (_msg("A", 1, 0, {"type": 3, "ops": [{"type": 3, "ops": []}]}), "nested group"),
@@ -323,3 +324,28 @@ def test_markers_and_tile_labels_on_the_gpu_path():
                 for label in ("pg", "EOP"):
                     for prec in (True, False):
                         assert g.doc(d).find_tile(pos, label, prec) == h.doc(d).find_tile(pos, label, prec)
+
+
+def test_relative_positions_on_the_gpu_path():
+    """Ops addressed by marker ids (relativePos1 / relativePos2 with id / before / offset): the GPU
+    packs the same MT_OP_RELPOS records and value table as the host (ids are interned in the host
+    packer's value() order: a relative position's id before the op's props), and the GPU-ingested
+    batch replays like the host-ingested one."""
+    from combine_logs import RELPOS_DOCS, relpos_farm
+
+    docs = [json.dumps(d, separators=(",", ":")) for d in RELPOS_DOCS + [relpos_farm(300, seed=5), relpos_farm(500, seed=6)]]
+    on_path = []
+    for d in docs:
+        try:
+            _same([d])
+            on_path.append(d)
+        except NotOnGpuPath:
+            pass
+    assert len(on_path) >= 2
+    _same(on_path)
+    with fa.ReplayBatch(len(on_path)) as g, fa.ReplayBatch(len(on_path)) as h:
+        assert g.ingest_json(on_path, device="gpu")["path"] == "gpu"
+        h.ingest_json(on_path, device="host")
+        g.run()
+        h.run()
+        _replay_equal(g, h, len(on_path))
