@@ -1137,41 +1137,21 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
         drop();
         return MT_ERR_HIP;
     }
-    // tables (as mt_batch_ingest_packed)
-    std::vector<const char *> kp, vp;
-    for (const auto &k : r.keys) kp.push_back(k.c_str());
-    for (const auto &v : r.values) vp.push_back(v.c_str());
-    static const char *none = "_";
-    rc = mt_batch_set_tables(b, kp.empty() ? &none : kp.data(), kp.empty() ? 1 : (int32_t)kp.size(), vp.data(),
-                             (int32_t)vp.size());
-    bool shared = true;
-    for (int64_t d = 1; d < D && shared; d++) shared = r.clients[(size_t)d] == r.clients[0];
-    auto set = [&](int64_t doc, const std::vector<std::string> &names) {
-        std::vector<const char *> np;
-        for (const auto &n : names) np.push_back(n.c_str());
-        return mt_batch_set_clients(b, doc, np.data(), (int32_t)np.size());
-    };
-    if (!rc && D && shared) rc = set(-1, r.clients[0]);
-    for (int64_t d = 0; !rc && !shared && d < D; d++) rc = set(d, r.clients[(size_t)d]);
-    if (rc) {
-        drop();
-        return rc;
-    }
     // marker ids and tile-label annotates (resolve_marker_ids / tile_annot of mt_batch_ingest) on
     // the device: a marker's markerId value -> its key (String(value); any consistent numbering
     // serves, the ids only key idToSegment for relative positions), per-document id counts
     uint32_t mk = 0xFFFFFFFFu, tk = 0xFFFFFFFFu;
-    for (size_t k = 0; k < b->keys.size(); k++) {
-        if (b->keys[k] == "markerId") mk = (uint32_t)k;
-        if (b->keys[k] == "referenceTileLabels") tk = (uint32_t)k;
+    for (size_t k = 0; k < r.keys.size(); k++) {
+        if (r.keys[k] == "markerId") mk = (uint32_t)k;
+        if (r.keys[k] == "referenceTileLabels") tk = (uint32_t)k;
     }
-    std::vector<uint32_t> vkey(b->values.size(), 0u), n_ids((size_t)D, 0u), tile((size_t)D, 0u);
+    std::vector<uint32_t> vkey(r.values.size(), 0u), n_ids((size_t)D, 0u), tile((size_t)D, 0u);
     {
         std::unordered_map<std::u16string, uint32_t> km;
-        for (size_t v = 1; v < b->values.size(); v++) {
-            if (b->value_flags[v] & mt::kValFalsy) continue;
+        for (size_t v = 1; v < r.values.size(); v++) {
+            if (json_falsy(r.values[v])) continue;
             std::u16string str;
-            if (!mt::js_string_of(b->values[v], str)) continue;
+            if (!mt::js_string_of(r.values[v], str)) continue;
             auto it = km.find(str);
             if (it == km.end()) it = km.emplace(str, (uint32_t)km.size() + 1).first;
             vkey[v] = it->second;
@@ -1210,6 +1190,26 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
             drop();
             return MT_ERR_HIP;
         }
+    }
+    // tables (as mt_batch_ingest_packed): the batch changes only after every device step succeeded
+    std::vector<const char *> kp, vp;
+    for (const auto &k : r.keys) kp.push_back(k.c_str());
+    for (const auto &v : r.values) vp.push_back(v.c_str());
+    static const char *none = "_";
+    rc = mt_batch_set_tables(b, kp.empty() ? &none : kp.data(), kp.empty() ? 1 : (int32_t)kp.size(), vp.data(),
+                             (int32_t)vp.size());
+    bool shared = true;
+    for (int64_t d = 1; d < D && shared; d++) shared = r.clients[(size_t)d] == r.clients[0];
+    auto set = [&](int64_t doc, const std::vector<std::string> &names) {
+        std::vector<const char *> np;
+        for (const auto &n : names) np.push_back(n.c_str());
+        return mt_batch_set_clients(b, doc, np.data(), (int32_t)np.size());
+    };
+    if (!rc && D && shared) rc = set(-1, r.clients[0]);
+    for (int64_t d = 0; !rc && !shared && d < D; d++) rc = set(d, r.clients[(size_t)d]);
+    if (rc) {
+        drop();
+        return rc;
     }
     std::vector<uint64_t> idmap_base((size_t)D + 1, 0);
     for (int64_t d = 0; d < D; d++) idmap_base[(size_t)d + 1] = idmap_base[(size_t)d] + n_ids[(size_t)d];
