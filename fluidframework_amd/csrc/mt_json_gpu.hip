@@ -462,6 +462,53 @@ __host__ __device__ bool str_raw(Rd &r, uint32_t &off, uint32_t &len, bool &plai
     return true;
 }
 
+// the string token whose contents are [o, o + l) is already what JSON.stringify writes for the
+// string it decodes to (so its source text can be interned as the value's JSON text): escapes only
+// \" \\ \b \f \n \r \t and \u00xx (lowercase) for the other control characters; every other
+// character raw, non-ASCII as well-formed shortest UTF-8 outside the surrogates
+__host__ __device__ bool str_canonical(Rd &r, uint32_t o, uint32_t l) {
+    for (uint32_t i = 0; i < l;) {
+        const uint32_t c = r.b(o + i);
+        if (c == '\\') {
+            if (i + 1 >= l) return false;
+            const uint32_t e = r.b(o + i + 1);
+            if (e == '"' || e == '\\' || e == 'b' || e == 'f' || e == 'n' || e == 'r' || e == 't') {
+                i += 2;
+                continue;
+            }
+            if (e != 'u' || i + 6 > l) return false;
+            uint32_t v = 0;
+            for (uint32_t k = 2; k < 6; k++) {
+                const uint32_t h = r.b(o + i + k);
+                const int d = (h >= '0' && h <= '9') ? (int)(h - '0') : (h >= 'a' && h <= 'f') ? (int)(h - 'a' + 10) : -1;
+                if (d < 0) return false;  // JSON.stringify writes lowercase hex
+                v = v * 16 + (uint32_t)d;
+            }
+            if (v >= 0x20 || v == 8 || v == 9 || v == 10 || v == 12 || v == 13) return false;
+            i += 6;
+            continue;
+        }
+        if (c < 0x80) {
+            i++;
+            continue;
+        }
+        // well-formed UTF-8, shortest form, no surrogates
+        const uint32_t k = (c & 0xE0) == 0xC0 ? 2u : (c & 0xF0) == 0xE0 ? 3u : (c & 0xF8) == 0xF0 ? 4u : 0u;
+        if (!k || i + k > l) return false;
+        uint32_t cp = c & (k == 2 ? 0x1Fu : k == 3 ? 0x0Fu : 0x07u);
+        for (uint32_t q = 1; q < k; q++) {
+            const uint32_t b = r.b(o + i + q);
+            if ((b & 0xC0) != 0x80) return false;
+            cp = (cp << 6) | (b & 0x3Fu);
+        }
+        if ((k == 2 && cp < 0x80) || (k == 3 && cp < 0x800) || (k == 4 && (cp < 0x10000 || cp > 0x10FFFF)) ||
+            (cp >= 0xD800 && cp <= 0xDFFF))
+            return false;
+        i += k;
+    }
+    return true;
+}
+
 // a text string decoded to UTF-16 code units exactly as mt_json.cpp Dom::string (\u escapes
 // kept as code units, UTF-8 -> UTF-16 with surrogate pairs); dst may be null (count only)
 __host__ __device__ bool str_text(Rd &r, uint16_t *dst, uint32_t &units, bool &has_nl, bool &ends_nl) {
@@ -854,8 +901,8 @@ __host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, uint3
             uint32_t so, sl;
             bool pl;
             if (!str_raw(r, so, sl, pl)) return kFSyntax;
-            if (!pl) return kFShape;
-            vl = sl + 2;  // JSON.stringify of a plain ASCII string = its source text
+            if (!pl && !str_canonical(r, so, sl)) return kFShape;
+            vl = sl + 2;  // a string already in JSON.stringify form: its source text
         } else if (c == '-' || is_digit(c)) {
             int64_t v;
             uint32_t nd;
@@ -874,7 +921,7 @@ __host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, uint3
                         uint32_t so, sl;
                         bool pl;
                         if (!str_raw(r, so, sl, pl)) return kFSyntax;
-                        if (!pl) return kFShape;
+                        if (!pl && !str_canonical(r, so, sl)) return kFShape;
                     } else if (e == '-' || is_digit(e)) {
                         int64_t v;
                         uint32_t nd;
@@ -960,7 +1007,7 @@ __host__ __device__ uint32_t relpos_record(const uint8_t *s, uint32_t n, const O
                         uint32_t so, sl;
                         bool pl;
                         if (!str_raw(rq, so, sl, pl)) return kFSyntax;
-                        if (!pl) return kFShape;
+                        if (!pl && !str_canonical(rq, so, sl)) return kFShape;
                         truthy = sl > 0;
                     } else if (c == '-' || is_digit(c)) {
                         int64_t v;

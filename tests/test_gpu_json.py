@@ -117,7 +117,7 @@ OUTSIDE = [  # (message, reason) — every one must be reported, never parsed di
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": {"b": 1}}}), "object value"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": [[1]]}}), "nested array value"),
     (_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 1.5}}}), "float refType"),
-    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": "é"}}), "non-ASCII value"),
+    (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": "é"}}), "non-ASCII value escaped as \\u00e9"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"1": 1}}), "array-index key"),
     (_msg("A", 1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
                       "combiningOp": {"name": "incr"}}), "combiningOp incr"),
@@ -349,3 +349,19 @@ def test_relative_positions_on_the_gpu_path():
         g.run()
         h.run()
         _replay_equal(g, h, len(on_path))
+
+
+def test_string_values_with_escapes_and_unicode():
+    """String prop values already in JSON.stringify form (escaped quotes / backslashes / control
+    characters, raw non-ASCII as json.dumps(ensure_ascii=False) writes them) parse on the GPU like
+    on the host; other spellings of the same strings (\\u escapes of printable characters, \\/,
+    uppercase hex) are reported."""
+    vals = ["say \"hi\"", "back\\slash", "tab\tnl\nret\r", "ctl\x01\x1f", "é€😀 café", "ß\u2028x", "a/b", "del\x7f"]
+    msgs = [_msg("A", i + 1, i, {"type": 0, "pos1": 0, "seg": {"text": "x", "props": {"k": v}}}) for i, v in enumerate(vals)]
+    msgs.append(_msg("B", len(vals) + 1, len(vals), {"type": 2, "pos1": 0, "pos2": 2, "props": {"tags": ["ü", "a\"b"]}}))
+    _same([json.dumps(msgs, ensure_ascii=False, separators=(",", ":"))])
+    for raw in ['"\\u0041"', '"a\\/b"', '"\\u001F"', '"\\u00e9"']:
+        doc = ('[{"clientId":"A","sequenceNumber":1,"referenceSequenceNumber":0,"minimumSequenceNumber":0,'
+               '"type":"op","contents":{"type":2,"pos1":0,"pos2":1,"props":{"k":' + raw + '}}}]')
+        with pytest.raises(NotOnGpuPath):
+            PackedJsonGpu(["[]", doc])
