@@ -159,7 +159,6 @@ constexpr int kHbmSeg = 2097152;  // giant documents (config 4: ~10^6 segments)
 constexpr int kReplayStartClass = 1;  // replay starts documents in at most the 16-per-CU class
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS class (16-bit lengths)
-constexpr int kCapQueued = 7;      // checkpointed and taken by the launch's follow-on workers
 
 // Writer replicas (the local-client path, mergeTree.ts:1893-1929, client.ts:588-625): per document
 // a pending-group region in HBM, persistent across launches (u32 words):
@@ -181,12 +180,6 @@ constexpr int64_t pend_words(int32_t cap) { return kPendEntries + 2ll * cap; }
 // in the document's payload, c = length, the pairs = its properties (nprops 0xFFFFFFFF: none);
 // annotate: a = flags, b / c = the reset op's prop records; remove: nothing more
 constexpr int kRegenOpWords = 8;
-
-// follow-on queue (one per producer launch, hipMalloc'd, zeroed): word 0 = documents enqueued,
-// 1 = items claimed by workers, 2 = producer workgroups finished, 3 = unused, 4 = a consumer's
-// bounded wait timed out,
-// items from word kFqItems: producer workgroup index + 1 (0 = not yet published)
-constexpr int kFqItems = 16;
 
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table
 constexpr int kCkHdr = 32;
@@ -282,16 +275,6 @@ struct ReplayParams {
     int64_t ck_in_words;          // stride of ck_in
     int32_t cold_in_seg;          // stride of cold_in
     uint8_t *hbm_state;           // HBM class: per-workgroup table images (make_layout(kHbmSeg).bytes each)
-    // follow-on workers: a single-round launch (fq_role 1) pushes each document it checkpoints
-    // into fq; a concurrent launch of the next class (fq_role 2, a few workgroups) pops and
-    // resumes them while the producer is still running, so the escalation tail overlaps it
-    uint32_t *fq;
-    int32_t fq_cap;               // items
-    int32_t fq_role;              // 0 none, 1 producer, 2 consumer
-    int64_t fq_producers;         // consumer: workgroups of the producer launch
-    const int32_t *fq_doc_list;   // consumer: the producer's doc_list (null: identity)
-    uint32_t *fq_started;         // producer: host-mapped count of started workgroups (the host
-                                  // launches the consumer once all are resident)
     // MergeTree.idToSegment (mergeTree.ts:1098) per document, persistent across launches:
     // {marker-id key, slot} entries in mapping order (kIdUnlinked: the marker was unlinked)
     uint2 *idmap;

@@ -2959,83 +2959,6 @@ MT_FI uint8_t *tables(const ReplayParams &P, int64_t w) {
     }
 }
 
-// ------------------------------------------------------------ follow-on queue
-// Producer (fq_role 1): a checkpointed document is published to the consumer launch after the
-// wave's stores (checkpoint image, cold records, text arena) are written back to HBM: vector
-// stores -> s_waitcnt -> agent release (L2 write-back) -> relaxed agent store of the item.
-// Consumer (fq_role 2): relaxed agent polls, then one agent acquire (L1 invalidate) before the
-// wave reads the image.  All flag traffic is vector-memory atomics issued by lane 0.
-MT_FI uint32_t fq_load(uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-MT_FI void fq_release() {
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_s_waitcnt(0);
-}
-
-MT_FI void fq_push(const ReplayParams &P, int64_t w, bool checkpointed) {
-    fq_release();
-    if (threadIdx.x == 0) {
-        uint32_t *q = P.fq;
-        if (checkpointed) {
-            const uint32_t i = __hip_atomic_fetch_add(&q[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (i < (uint32_t)P.fq_cap) {
-                P.doc_out[w].cap_kind = kCapQueued;  // the host leaves it to the consumer
-                q[kFqItems + P.fq_cap + i] = (uint32_t)__builtin_amdgcn_s_memrealtime();  // trace: published
-                __hip_atomic_store(&q[kFqItems + i], (uint32_t)w + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        __hip_atomic_fetch_add(&q[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// consumer: next item index (-1: none left).  *src = the producer workgroup to resume.  Every
-// item below min(enqueued, fq_cap) is claimed by exactly one worker, and a worker leaves only when
-// no further item can come, so the host finds every queued document replayed.
-MT_FI int32_t fq_claim(const ReplayParams &P, int32_t *src) {
-    int32_t r = -1, s = -1;
-    if (threadIdx.x == 0) {
-        uint32_t *q = P.fq;
-        const uint32_t n_prod = (uint32_t)P.fq_producers;
-        {
-            const uint32_t i = __hip_atomic_fetch_add(&q[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (i < (uint32_t)P.fq_cap) {
-                // bounded: a hand-off that never completes ends as an error (q[4], MT_INTERNAL on
-                // the host), never as a hung launch (~1 us per poll, ~8 s in all)
-                for (uint32_t polls = 0;; polls++) {
-                    if (polls >= (1u << 23)) {
-                        __hip_atomic_store(&q[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    uint32_t it = fq_load(&q[kFqItems + i]);
-                    if (it) {
-                        r = (int32_t)i;
-                        s = (int32_t)it - 1;
-                        break;
-                    }
-                    if (__hip_atomic_load(&q[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= n_prod) {
-                        // every producer has finished: item i is published now or never
-                        it = fq_load(&q[kFqItems + i]);
-                        if (it) {
-                            r = (int32_t)i;
-                            s = (int32_t)it - 1;
-                        }
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(32);
-                }
-            }
-        }
-    }
-    r = rfl(r);
-    *src = rfl(s);
-    if (r >= 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __builtin_amdgcn_s_waitcnt(0);
-    }
-    return r;
-}
-
 // kLoad: apply only the document's leading SnapshotLoader records, then checkpoint at the
 // first other record (cap_kind kCapCheckpoint); the replay launch resumes there.
 // Workgroup index w writes its results at w; document d; src >= 0: resume from the checkpoint
@@ -3074,13 +2997,6 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
         rg[1] = 0u;
     }
     if constexpr (kW) E.n_pend = resumed ? (int32_t)E.pend_word(0) : 0;
-    // follow-on producer: workgroups are dispatched in index order, so the last one starting
-    // means all are resident and the host may launch the consumer
-    // follow-on producer: every workgroup counts itself in once resident (host-mapped, system
-    // scope); the host launches the consumer when the count reaches the launch's workgroups, so
-    // no dispatch order is assumed
-    if (P.fq_started && E.lane == 0)
-        __hip_atomic_fetch_add(P.fq_started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // ops stream through registers 64 at a time (coalesced 2 KiB loads), broadcast by readlane
     mt_op cur = load_op_lane(ops, b0 + done + E.lane, b1);
     for (int64_t base = b0 + done; base < b1 && E.status == ST_OK; base += kWave) {
@@ -3129,37 +3045,13 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
     return E.status == ST_CAPACITY && E.cap_kind == kCapCheckpoint;
 }
 
-// one workgroup per document (blockIdx.x); a producer (fq_role 1) hands its checkpointed
-// documents to the follow-on consumer
+// one workgroup per document (blockIdx.x)
 template <int SEG, bool kLoad, bool kW = false>
 MT_FI void replay_body(const ReplayParams &P) {
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
-    const bool producer = !kLoad && P.fq_role == 1;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
-    const bool ck = replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
-    if (producer) fq_push(P, w, ck);
-}
-
-// follow-on consumer (fq_role 2): one workgroup per queue slot; workgroup i waits for item i
-// (or for every producer to finish without it) and resumes that document, writing its results
-// at index i.  (One item per workgroup: a workgroup that replayed a second document in the same
-// launch hung on the GPU — an unexplained interaction, so the loop was removed.)
-template <int SEG>
-MT_FI void follow_body(const ReplayParams &P) {
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    int32_t src;
-    const int32_t i = fq_claim(P, &src);
-    if (i < 0) return;
-    const uint32_t t1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    const int64_t d = P.fq_doc_list ? (int64_t)P.fq_doc_list[src] : (int64_t)src;
-    replay_one<SEG, false>(P, i, d, src);
-    if (threadIdx.x == 0) {  // trace (100 MHz clock): started, item seen, done
-        uint32_t *tr = P.fq + kFqItems + 2 * P.fq_cap + 3 * i;
-        tr[0] = t0;
-        tr[1] = t1;
-        tr[2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    }
+    replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
 }
 
 // Generator: draws each op from the issuer's view (include/mt_gen.h, DESIGN.md

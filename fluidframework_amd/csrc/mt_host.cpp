@@ -32,8 +32,7 @@
     extern "C" __global__ void mt_replay_kernel_##S(mt::ReplayParams P);      \
     extern "C" __global__ void mt_writer_kernel_##S(mt::ReplayParams P);      \
     extern "C" __global__ void mt_load_kernel_##S(mt::ReplayParams P);        \
-    extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);    \
-    extern "C" __global__ void mt_follow_kernel_##S(mt::ReplayParams P);
+    extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);
 MT_DECLARE_CLASS(128)
 MT_DECLARE_CLASS(363)
 MT_DECLARE_CLASS(423)
@@ -86,57 +85,40 @@ struct KernelClass {
     const void *replay;
     const void *generate;
     const void *load;
-    const void *follow;
     const void *writer;  // replay + the local-client path (writer replicas)
 };
 static const KernelClass kKernels[mt::kNumClasses] = {
     {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
-     (const void *)mt_follow_kernel_128,
      (const void *)mt_writer_kernel_128},
     {363, (const void *)mt_replay_kernel_363, (const void *)mt_generate_kernel_363, (const void *)mt_load_kernel_363,
-     (const void *)mt_follow_kernel_363,
      (const void *)mt_writer_kernel_363},
     {423, (const void *)mt_replay_kernel_423, (const void *)mt_generate_kernel_423, (const void *)mt_load_kernel_423,
-     (const void *)mt_follow_kernel_423,
      (const void *)mt_writer_kernel_423},
     {483, (const void *)mt_replay_kernel_483, (const void *)mt_generate_kernel_483, (const void *)mt_load_kernel_483,
-     (const void *)mt_follow_kernel_483,
      (const void *)mt_writer_kernel_483},
     {540, (const void *)mt_replay_kernel_540, (const void *)mt_generate_kernel_540, (const void *)mt_load_kernel_540,
-     (const void *)mt_follow_kernel_540,
      (const void *)mt_writer_kernel_540},
     {600, (const void *)mt_replay_kernel_600, (const void *)mt_generate_kernel_600, (const void *)mt_load_kernel_600,
-     (const void *)mt_follow_kernel_600,
      (const void *)mt_writer_kernel_600},
     {720, (const void *)mt_replay_kernel_720, (const void *)mt_generate_kernel_720, (const void *)mt_load_kernel_720,
-     (const void *)mt_follow_kernel_720,
      (const void *)mt_writer_kernel_720},
     {840, (const void *)mt_replay_kernel_840, (const void *)mt_generate_kernel_840, (const void *)mt_load_kernel_840,
-     (const void *)mt_follow_kernel_840,
      (const void *)mt_writer_kernel_840},
     {960, (const void *)mt_replay_kernel_960, (const void *)mt_generate_kernel_960, (const void *)mt_load_kernel_960,
-     (const void *)mt_follow_kernel_960,
      (const void *)mt_writer_kernel_960},
     {1136, (const void *)mt_replay_kernel_1136, (const void *)mt_generate_kernel_1136, (const void *)mt_load_kernel_1136,
-     (const void *)mt_follow_kernel_1136,
      (const void *)mt_writer_kernel_1136},
     {1376, (const void *)mt_replay_kernel_1376, (const void *)mt_generate_kernel_1376, (const void *)mt_load_kernel_1376,
-     (const void *)mt_follow_kernel_1376,
      (const void *)mt_writer_kernel_1376},
     {1792, (const void *)mt_replay_kernel_1792, (const void *)mt_generate_kernel_1792, (const void *)mt_load_kernel_1792,
-     (const void *)mt_follow_kernel_1792,
      (const void *)mt_writer_kernel_1792},
     {2389, (const void *)mt_replay_kernel_2389, (const void *)mt_generate_kernel_2389, (const void *)mt_load_kernel_2389,
-     (const void *)mt_follow_kernel_2389,
      (const void *)mt_writer_kernel_2389},
     {3600, (const void *)mt_replay_kernel_3600, (const void *)mt_generate_kernel_3600, (const void *)mt_load_kernel_3600,
-     (const void *)mt_follow_kernel_3600,
      (const void *)mt_writer_kernel_3600},
     {7266, (const void *)mt_replay_kernel_7266, (const void *)mt_generate_kernel_7266, (const void *)mt_load_kernel_7266,
-     (const void *)mt_follow_kernel_7266,
      (const void *)mt_writer_kernel_7266},
     {2097152, (const void *)mt_replay_kernel_2097152, (const void *)mt_generate_kernel_2097152, (const void *)mt_load_kernel_2097152,
-     (const void *)mt_follow_kernel_2097152,
      (const void *)mt_writer_kernel_2097152},
 };
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
@@ -162,27 +144,11 @@ struct Launch {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int level = 0;              // escalation depth (0: a first launch)
     bool load = false;          // SnapshotLoader launch (mt_load_kernel): LOAD records, then a checkpoint
-    // follow-on workers: a producer launch pushes its checkpointed documents to
-    // the consumer launch `follow`, which runs concurrently in the next class; the consumer's
-    // docs / cksrc are read back from the queue when it completes
-    int follow = -1;            // -2: consumer not launched yet
-    bool consumer = false;
-    uint32_t *d_fq = nullptr;   // producer: queue header + items (the consumer reads the same one)
-    uint32_t *h_started = nullptr;  // producer: host-mapped count of its workgroups that have started
-    int32_t fq_cap = 0;
-    int32_t workers = 0;
-    // producer: the consumer's buffers, allocated and initialised before the producer runs (a
-    // memset issued while the producer fills every CU would wait for a free slot)
-    int f_cls = -1;
-    OutRec *f_out = nullptr;
-    DocOut *f_docout = nullptr;
-    uint4 *f_cold = nullptr;
-    uint32_t *f_ck = nullptr;
 };
 
 // workgroups (documents) of a launch
 static int64_t launch_n(int64_t n_docs, const Launch &L) {
-    return L.consumer ? (int64_t)L.docs.size() : (L.docs.empty() ? n_docs : (int64_t)L.docs.size());
+    return L.docs.empty() ? n_docs : (int64_t)L.docs.size();
 }
 
 struct DocRes {  // per-document result location
@@ -393,6 +359,10 @@ struct mt_batch {
     std::vector<uint8_t> h_tile_annot;  // per doc: an annotate touches referenceTileLabels (findTile)
     std::vector<uint64_t> h_text_base, h_pool_base;
     std::vector<uint32_t> h_text_len, h_text_cap, h_pool_cap;
+    // MT_OP_RELPOS records hold marker-id keys on the device (resolve_marker_ids); key_value[k] is a
+    // value id whose String() is key k, so mt_batch_download_log returns value ids again (a log
+    // that re-ingests to the same keys)
+    std::vector<uint32_t> key_value;
     uint64_t text_words = 0, pool_words = 0;
     mt_op *d_ops = nullptr;
     int64_t *d_off = nullptr;
@@ -415,8 +385,6 @@ struct mt_batch {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent first launches of mixed-size batches
     hipStream_t cstream = nullptr;  // result gathers (never queued behind a running launch)
-    hipStream_t fstream = nullptr;  // follow-on consumer launches
-    uint32_t *h_started = nullptr;  // host-mapped: per first launch, the count of its started workgroups
     hipEvent_t ev_user = nullptr;
     uint64_t *d_digest = nullptr;  // mt_batch_device_digests
     float kernel_ms = 0, total_ms = 0;
@@ -464,11 +432,6 @@ static void free_launches(mt_batch *b) {
         (void)hipFree(L.d_ck);
         (void)hipFree(L.d_cksrc);
         (void)hipFree(L.d_state);
-        (void)hipFree(L.d_fq);
-        (void)hipFree(L.f_out);
-        (void)hipFree(L.f_docout);
-        (void)hipFree(L.f_cold);
-        (void)hipFree(L.f_ck);
         if (L.e0) (void)hipEventDestroy(L.e0);
         if (L.e1) (void)hipEventDestroy(L.e1);
     }
@@ -507,6 +470,16 @@ static void free_log(mt_batch *b) {
     b->d_pool = nullptr;
     b->d_props = nullptr;
     b->have_log = false;
+}
+
+// internal (mt_json.cpp's mt_batch_ingest_packed): an ingest that fails after it installed new
+// tables leaves no log behind, so no later run can decode the previous log against the new tables
+void mt_internal_drop_log(mt_batch *b) {
+    free_launches(b);
+    free_log(b);
+    b->ran = false;
+    b->cached_doc = -1;
+    b->c_blob_doc = -1;
 }
 
 #ifndef MT_BUILD_ID
@@ -578,8 +551,6 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     for (hipStream_t a : b->aux)
         if (a) (void)hipStreamDestroy(a);
     if (b->cstream) (void)hipStreamDestroy(b->cstream);
-    if (b->fstream) (void)hipStreamDestroy(b->fstream);
-    if (b->h_started) (void)hipHostFree(b->h_started);
     if (b->ev_user) (void)hipEventDestroy(b->ev_user);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -587,42 +558,98 @@ MT_API void mt_batch_destroy(mt_batch *b) {
 
 static int ensure_tables(mt_batch *b);
 
+// device copies of the value tables (matchProperties classes, flags, exceptions) for the kernels
+struct DeviceValueTables {
+    uint8_t *flags = nullptr;
+    uint32_t *cls = nullptr;
+    uint64_t *exc = nullptr;
+    mt::ValueTables *vt = nullptr;
+    void release() {
+        (void)hipFree(flags);
+        (void)hipFree(cls);
+        (void)hipFree(exc);
+        (void)hipFree(vt);
+        *this = DeviceValueTables{};
+    }
+};
+// uploads into `t` (all or nothing: on failure `t` is released and empty)
+static int upload_value_tables(const std::vector<uint8_t> &flags, const std::vector<uint32_t> &cls,
+                               const std::vector<uint64_t> &exc, uint32_t nan_id, DeviceValueTables &t) {
+    hipError_t e = dalloc(&t.flags, flags.size());
+    if (e == hipSuccess) e = hipMemcpy(t.flags, flags.data(), flags.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = dalloc(&t.cls, cls.size());
+    if (e == hipSuccess) e = hipMemcpy(t.cls, cls.data(), 4 * cls.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = dalloc(&t.exc, exc.size());
+    if (e == hipSuccess && !exc.empty()) e = hipMemcpy(t.exc, exc.data(), 8 * exc.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        mt::ValueTables vt{t.flags, t.cls, t.exc, (uint32_t)flags.size(), (uint32_t)exc.size(), nan_id};
+        e = dalloc(&t.vt, 1);
+        if (e == hipSuccess) e = hipMemcpy(t.vt, &vt, sizeof vt, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        fprintf(stderr, "mtreplay: value table upload failed: %s\n", hipGetErrorString(e));
+        t.release();
+        return MT_ERR_HIP;
+    }
+    return MT_OK;
+}
+
+// Built and uploaded into locals first: the batch's tables change only when every step succeeded,
+// so a failed call leaves the previous keys, values and device tables installed together.
 MT_API int mt_batch_set_tables(mt_batch *b, const char *const *keys, int32_t n_keys, const char *const *values_json,
                                int32_t n_values) {
-    if (!b || n_keys < 0 || n_values < 1) return MT_ERR_ARG;
-    b->keys.assign(keys, keys + n_keys);
-    b->key_is_index.assign(n_keys, 0);
-    b->key_index.assign(n_keys, 0);
+    if (!b || n_keys < 0 || n_values < 1 || (n_keys > 0 && !keys) || !values_json) return MT_ERR_ARG;
+    std::vector<std::string> nk(keys, keys + n_keys);
+    std::vector<uint8_t> is_index((size_t)n_keys, 0);
+    std::vector<uint32_t> index((size_t)n_keys, 0);
     for (int i = 0; i < n_keys; i++) {
+        if (!keys[i]) return MT_ERR_ARG;
         uint32_t idx = 0;
-        if (array_index(b->keys[i], &idx)) {
-            b->key_is_index[i] = 1;
-            b->key_index[i] = idx;
+        if (array_index(nk[(size_t)i], &idx)) {
+            is_index[(size_t)i] = 1;
+            index[(size_t)i] = idx;
         }
     }
-    b->values.resize(n_values);
-    b->value_flags.resize(n_values);
-    b->n_user_values = (size_t)n_values;
-    b->nan_id = 0xFFFFFFFFu;
+    std::vector<std::string> values((size_t)n_values);
+    std::vector<uint8_t> flags((size_t)n_values);
     for (int i = 0; i < n_values; i++) {
-        b->values[i] = (i == 0 || !values_json[i]) ? std::string("null") : std::string(values_json[i]);
-        b->value_flags[i] = json_falsy(b->values[i]) ? mt::kValFalsy : 0;
+        values[(size_t)i] = (i == 0 || !values_json[i]) ? std::string("null") : std::string(values_json[i]);
+        flags[(size_t)i] = json_falsy(values[(size_t)i]) ? mt::kValFalsy : 0;
     }
     // matchProperties classes of the values (nested objects compare structurally)
-    mt::value_relations(b->values, b->value_class, b->value_flags, b->value_exc);
+    std::vector<uint32_t> cls;
+    std::vector<uint64_t> exc;
+    mt::value_relations(values, cls, flags, exc);
+    DeviceValueTables t;
+    const int rc = upload_value_tables(flags, cls, exc, 0xFFFFFFFFu, t);
+    if (rc) return rc;
+    b->keys = std::move(nk);
+    b->key_is_index = std::move(is_index);
+    b->key_index = std::move(index);
+    b->values = std::move(values);
+    b->value_flags = std::move(flags);
+    b->value_class = std::move(cls);
+    b->value_exc = std::move(exc);
+    b->n_user_values = (size_t)n_values;
+    b->nan_id = 0xFFFFFFFFu;
     (void)hipFree(b->d_vflags);
     (void)hipFree(b->d_vclass);
     (void)hipFree(b->d_vexc);
     (void)hipFree(b->d_vt);
-    b->d_vflags = nullptr;
-    b->d_vclass = nullptr;
-    b->d_vexc = nullptr;
-    b->d_vt = nullptr;
-    return ensure_tables(b);
+    b->d_vflags = t.flags;
+    b->d_vclass = t.cls;
+    b->d_vexc = t.exc;
+    b->d_vt = t.vt;
+    return MT_OK;
+}
+
+// the checks mt_batch_set_clients makes, so callers can validate every list before changing anything
+static bool clients_ok(const mt_batch *b, int64_t doc, size_t n) {
+    return n >= 1 && n <= (size_t)MT_MAX_CLIENTS && doc < b->n_docs;
 }
 
 MT_API int mt_batch_set_clients(mt_batch *b, int64_t doc, const char *const *names, int32_t n) {
-    if (!b || n < 1 || n > MT_MAX_CLIENTS || doc >= b->n_docs) return MT_ERR_ARG;
+    if (!b || !names || n < 0 || !clients_ok(b, doc, (size_t)n)) return MT_ERR_ARG;
     std::vector<std::string> v(names, names + n);
     if (doc < 0) {
         b->clients = v;
@@ -641,25 +668,20 @@ static const std::vector<std::string> &clients_of(mt_batch *b, int64_t doc) {
 static int ensure_tables(mt_batch *b) {
     if (b->value_class.size() != b->values.size())
         mt::value_relations(b->values, b->value_class, b->value_flags, b->value_exc);
-    if (!b->d_vflags) {
-        HIPCHK(dalloc(&b->d_vflags, b->value_flags.size()));
-        HIPCHK(hipMemcpy(b->d_vflags, b->value_flags.data(), b->value_flags.size(), hipMemcpyHostToDevice));
-    }
-    if (!b->d_vclass) {
-        HIPCHK(dalloc(&b->d_vclass, b->value_class.size()));
-        HIPCHK(hipMemcpy(b->d_vclass, b->value_class.data(), 4 * b->value_class.size(), hipMemcpyHostToDevice));
-    }
-    if (!b->d_vexc) {
-        HIPCHK(dalloc(&b->d_vexc, b->value_exc.size()));
-        if (!b->value_exc.empty())
-            HIPCHK(hipMemcpy(b->d_vexc, b->value_exc.data(), 8 * b->value_exc.size(), hipMemcpyHostToDevice));
-    }
-    if (!b->d_vt) {
-        mt::ValueTables vt{b->d_vflags, b->d_vclass, b->d_vexc, (uint32_t)b->value_flags.size(),
-                           (uint32_t)b->value_exc.size(), b->nan_id};
-        HIPCHK(dalloc(&b->d_vt, 1));
-        HIPCHK(hipMemcpy(b->d_vt, &vt, sizeof vt, hipMemcpyHostToDevice));
-    }
+    if (b->d_vt) return MT_OK;
+    (void)hipFree(b->d_vflags);
+    (void)hipFree(b->d_vclass);
+    (void)hipFree(b->d_vexc);
+    b->d_vflags = nullptr;
+    b->d_vclass = nullptr;
+    b->d_vexc = nullptr;
+    DeviceValueTables t;
+    const int rc = upload_value_tables(b->value_flags, b->value_class, b->value_exc, b->nan_id, t);
+    if (rc) return rc;
+    b->d_vflags = t.flags;
+    b->d_vclass = t.cls;
+    b->d_vexc = t.exc;
+    b->d_vt = t.vt;
     return MT_OK;
 }
 
@@ -700,7 +722,10 @@ static void resolve_marker_ids(mt_batch *b, std::vector<mt_op> &h_ops, const std
         uint32_t k = 0;
         if (mt::js_string_of(b->values[v], s)) {
             auto kt = keys.find(s);
-            if (kt == keys.end()) kt = keys.emplace(s, (uint32_t)keys.size() + 1).first;
+            if (kt == keys.end()) {
+                kt = keys.emplace(s, (uint32_t)keys.size() + 1).first;
+                b->key_value.push_back(v);  // key kt->second == key_value.size() - 1
+            }
             k = kt->second;
         }
         of_value.emplace(v, k);
@@ -708,6 +733,7 @@ static void resolve_marker_ids(mt_batch *b, std::vector<mt_op> &h_ops, const std
     };
     const size_t D = off.size() - 1;
     uint64_t total = 0;
+    b->key_value.assign(1, 0u);  // key 0: no id
     for (size_t d = 0; d < D; d++) {
         idmap_base[d] = total;
         bool annot_mk = false;
@@ -1092,9 +1118,12 @@ MT_API int mt_pack_json_gpu(mt_packed **out, int64_t n_docs, const char *json, c
 // GPU parse straight into the replay's layout: per-document text arenas (payloads document-
 // relative, the '\n' flags set), the same host metadata as mt_batch_ingest for a log of the
 // observer fast path (no LOAD / RELPOS / REGENERATE records, markers, combiningOps or local ops)
-MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, const void *d_json,
-                                    const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats) {
-    if (!b || !doc_off || (b->n_docs && !json) || ((uintptr_t)d_json & 3u)) return MT_ERR_ARG;
+MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, int64_t n_docs,
+                                    const void *d_json, const char *observer, int64_t *bad_doc,
+                                    mt_json_gpu_stats *stats) {
+    // n_docs: the caller's document count; doc_off[0..n_docs] is read, so a count that differs
+    // from the batch's would read past the caller's arrays
+    if (!b || !doc_off || n_docs != b->n_docs || (b->n_docs && !json) || ((uintptr_t)d_json & 3u)) return MT_ERR_ARG;
     if (bad_doc) *bad_doc = -1;
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t D = b->n_docs;
@@ -1146,6 +1175,7 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
         if (r.keys[k] == "referenceTileLabels") tk = (uint32_t)k;
     }
     std::vector<uint32_t> vkey(r.values.size(), 0u), n_ids((size_t)D, 0u), tile((size_t)D, 0u);
+    std::vector<uint32_t> key_value(1, 0u);
     {
         std::unordered_map<std::u16string, uint32_t> km;
         for (size_t v = 1; v < r.values.size(); v++) {
@@ -1153,7 +1183,10 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
             std::u16string str;
             if (!mt::js_string_of(r.values[v], str)) continue;
             auto it = km.find(str);
-            if (it == km.end()) it = km.emplace(str, (uint32_t)km.size() + 1).first;
+            if (it == km.end()) {
+                it = km.emplace(str, (uint32_t)km.size() + 1).first;
+                key_value.push_back((uint32_t)v);  // key it->second == key_value.size() - 1
+            }
             vkey[v] = it->second;
         }
     }
@@ -1196,10 +1229,16 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     for (const auto &k : r.keys) kp.push_back(k.c_str());
     for (const auto &v : r.values) vp.push_back(v.c_str());
     static const char *none = "_";
-    rc = mt_batch_set_tables(b, kp.empty() ? &none : kp.data(), kp.empty() ? 1 : (int32_t)kp.size(), vp.data(),
-                             (int32_t)vp.size());
     bool shared = true;
     for (int64_t d = 1; d < D && shared; d++) shared = r.clients[(size_t)d] == r.clients[0];
+    // every client list is checked before the tables change (set_clients cannot fail after them)
+    for (int64_t d = 0; d < (shared ? std::min<int64_t>(D, 1) : D); d++)
+        if (!clients_ok(b, shared ? -1 : d, r.clients[(size_t)d].size())) {
+            drop();
+            return MT_ERR_ARG;
+        }
+    rc = mt_batch_set_tables(b, kp.empty() ? &none : kp.data(), kp.empty() ? 1 : (int32_t)kp.size(), vp.data(),
+                             (int32_t)vp.size());
     auto set = [&](int64_t doc, const std::vector<std::string> &names) {
         std::vector<const char *> np;
         for (const auto &n : names) np.push_back(n.c_str());
@@ -1216,6 +1255,7 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     // the parsed log replaces the previous one (mt_batch_ingest's fields for this log shape)
     free_launches(b);
     free_log(b);
+    b->key_value = std::move(key_value);
     b->ran = false;
     b->cached_doc = -1;
     b->c_blob_doc = -1;
@@ -1386,18 +1426,6 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.cold = L.d_cold;
     P.hbm_state = L.d_state;
     P.ck_out = L.d_ck;
-    if (L.fq_cap > 0 && L.d_ck) {
-        // header, items, then a trace: per item the publish time and the consumer's
-        // (started, item seen, done) times on the 100 MHz clock (MT_DEBUG_FOLLOW prints them)
-        HIPCHK(dalloc(&L.d_fq, (size_t)mt::kFqItems + 5 * (size_t)L.fq_cap));
-        HIPCHK(hipMemsetAsync(L.d_fq, 0, 4 * ((size_t)mt::kFqItems + 5 * (size_t)L.fq_cap), s));
-        P.fq = L.d_fq;
-        P.fq_cap = L.fq_cap;
-        P.fq_role = 1;
-        P.fq_started = L.h_started;
-    } else {
-        L.fq_cap = 0;
-    }
     if (!L.cksrc.empty() && prev) {
         P.ck_in = prev->d_ck;
         P.ck_src = L.d_cksrc;
@@ -1416,155 +1444,6 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
     void *args[] = {&P};
     HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, s));
-    return MT_OK;
-}
-
-// Follow-on workers for a first launch whose escalation tail would otherwise run after it (a
-// launch that fits the GPU in about one round: its last documents finish together, and a document
-// that checkpoints would resume only then, replaying its remaining ops at one-wave latency as a
-// second serial phase).  Off for SnapshotLoader launches, the HBM class and batches that cannot
-// escalate.  Off by default since the capacity ladder was re-derived (config 2's documents fit
-// the first class, and idle consumers polling beside the producer cost it 15 %); MT_FOLLOW_WORKERS
-// sets the worker count (read per launch).
-static int follow_workers(mt_batch *b, const Launch &L, int64_t n) {
-    const char *e = getenv("MT_FOLLOW_WORKERS");
-    const int env = e && *e ? atoi(e) : 0;
-    if (env == 0 || L.load || L.level != 0 || L.cls == mt::kHbmClass || b->opt.max_retries <= 0 || b->writer) return 0;
-    int nxt = resume_class(L.cls);
-    while (nxt > L.cls + 1 && !class_usable(nxt)) nxt--;
-    if (!class_usable(L.cls + 1) || !class_usable(nxt) || nxt == mt::kHbmClass) return 0;
-    static int n_cu = -1;
-    if (n_cu < 0) {
-        int dev = 0;
-        hipDeviceProp_t p;
-        n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 256;
-    }
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)(160 * 1024) / (int64_t)std::max<size_t>(1, class_lds(L.cls))));
-    if (n > 2 * (int64_t)n_cu * per_cu) return 0;
-    const int64_t g = env > 0 ? env : 64;
-    return (int)std::min<int64_t>(g, n);
-}
-
-// the consumer's class and buffers, before the producer is launched on stream s
-static int prep_follow(Launch &L, hipStream_t s) {
-    int cls = resume_class(L.cls);
-    while (cls > L.cls + 1 && !class_usable(cls)) cls--;
-    L.f_cls = cls;
-    const Caps c = mt::class_caps(mt::kClassSegs[cls]);
-    const size_t n = (size_t)L.fq_cap;
-    HIPCHK(dalloc(&L.f_out, n * (size_t)c.oe));
-    HIPCHK(dalloc(&L.f_docout, n));
-    HIPCHK(hipMemsetAsync(L.f_docout, 0xFF, sizeof(DocOut) * n, s));  // status -1: not replayed
-    HIPCHK(dalloc(&L.f_cold, n * (size_t)c.seg * mt::kColdPerSlot));
-    if (class_usable(cls + 1)) HIPCHK(dalloc(&L.f_ck, n * (size_t)mt::ck_words(c.seg)));
-    return MT_OK;
-}
-
-// the consumer of producer launch `pi`: `workers` workgroups of the next class popping the
-// producer's queue (results at the queue index; docs / cksrc read back in gather_follow)
-static int launch_follow(mt_batch *b, int pi) {
-    if (!b->fstream) HIPCHK(hipStreamCreateWithFlags(&b->fstream, hipStreamNonBlocking));
-    hipStream_t s = b->fstream;
-    Launch C;
-    {
-        const Launch &Pr = b->launches[(size_t)pi];
-        C.cls = Pr.f_cls;
-        C.consumer = true;
-        C.src = pi;
-        C.level = 1;
-        C.fq_cap = Pr.fq_cap;
-        C.workers = Pr.workers;
-    }
-    b->launches.push_back(std::move(C));
-    const int li = (int)b->launches.size() - 1;
-    Launch &L = b->launches.back();
-    const Launch &Pr = b->launches[(size_t)pi];
-    const int64_t n = L.fq_cap;
-    L.caps = mt::class_caps(mt::kClassSegs[L.cls]);
-    L.out_cap = L.caps.oe;
-    L.lds = class_lds(L.cls);
-    {
-        Launch &Pm = b->launches[(size_t)pi];
-        L.d_out = Pm.f_out;
-        L.d_docout = Pm.f_docout;
-        L.d_cold = Pm.f_cold;
-        L.d_ck = Pm.f_ck;
-        Pm.f_out = nullptr;
-        Pm.f_docout = nullptr;
-        Pm.f_cold = nullptr;
-        Pm.f_ck = nullptr;
-    }
-    mt::ReplayParams P = base_params(b);
-    P.out = L.d_out;
-    P.doc_out = L.d_docout;
-    P.n_docs = n;
-    P.out_cap = L.out_cap;
-    P.cold = L.d_cold;
-    P.ck_out = L.d_ck;
-    P.ck_in = Pr.d_ck;
-    P.cold_in = Pr.d_cold;
-    P.ck_in_words = mt::ck_words(Pr.caps.seg);
-    P.cold_in_seg = Pr.caps.seg;
-    P.fq = Pr.d_fq;
-    P.fq_cap = L.fq_cap;
-    P.fq_role = 2;
-    P.fq_producers = launch_n(b->n_docs, Pr);
-    P.fq_doc_list = Pr.d_list;
-#ifdef MT_PROF
-    HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
-    P.prof = L.d_prof;
-#endif
-    const void *fn = kKernels[L.cls].follow;
-    if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
-    HIPCHK(hipEventCreate(&L.e0));
-    HIPCHK(hipEventCreate(&L.e1));
-    HIPCHK(hipEventRecord(L.e0, s));
-    void *args[] = {&P};
-    HIPCHK(hipLaunchKernel(fn, dim3((unsigned)L.workers), dim3(64), args, L.lds, s));
-    HIPCHK(hipEventRecord(L.e1, s));
-    b->launches[(size_t)pi].follow = li;
-    if (getenv("MT_DEBUG_FOLLOW"))
-        fprintf(stderr, "mtreplay: follow-on consumer of launch %d (class %d, %d workers) at %.3f ms\n", pi,
-                mt::kClassSegs[L.cls], L.workers,
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count());
-    return MT_OK;
-}
-
-// a completed consumer: its documents are the queue's items, in queue order
-static int gather_follow(mt_batch *b, int li) {
-    Launch &L = b->launches[(size_t)li];
-    const Launch &Pr = b->launches[(size_t)L.src];
-    std::vector<uint32_t> q((size_t)mt::kFqItems + 5 * (size_t)L.fq_cap);
-    if (!b->cstream) HIPCHK(hipStreamCreateWithFlags(&b->cstream, hipStreamNonBlocking));
-    HIPCHK(hipMemcpyAsync(q.data(), Pr.d_fq, 4 * q.size(), hipMemcpyDeviceToHost, b->cstream));
-    HIPCHK(hipStreamSynchronize(b->cstream));
-    if (q[4]) {  // a consumer's bounded wait for its item ran out (fq_claim)
-        fprintf(stderr, "mtreplay: follow-on hand-off of launch %d timed out\n", L.src);
-        return MT_INTERNAL;
-    }
-    const uint32_t n = std::min<uint32_t>(q[0], (uint32_t)L.fq_cap);
-    L.docs.clear();
-    L.cksrc.clear();
-    for (uint32_t i = 0; i < n; i++) {
-        const int32_t w = (int32_t)q[(size_t)mt::kFqItems + i] - 1;
-        if (w < 0 || w >= launch_n(b->n_docs, Pr)) return MT_INTERNAL;
-        L.docs.push_back(Pr.docs.empty() ? w : Pr.docs[(size_t)w]);
-        L.cksrc.push_back(w);
-    }
-    if (getenv("MT_DEBUG_FOLLOW") && n > 0) {
-        const uint32_t *pub = q.data() + mt::kFqItems + L.fq_cap, *tr = pub + L.fq_cap;
-        uint32_t t0 = pub[0];
-        for (uint32_t i = 0; i < n; i++) t0 = std::min(t0, std::min(pub[i], tr[3 * i]));
-        for (uint32_t i = 0; i < n; i++)
-            fprintf(stderr, "mtreplay: follow item %u doc %d: published %+.3f ms, worker started %+.3f, took it %+.3f, done %+.3f\n",
-                    i, L.docs[i], (pub[i] - t0) * 1e-5, (tr[3 * i] - t0) * 1e-5, (tr[3 * i + 1] - t0) * 1e-5,
-                    (tr[3 * i + 2] - t0) * 1e-5);
-    }
-    if (n > 0) {
-        HIPCHK(dalloc(&L.d_list, (size_t)n));
-        HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * (size_t)n, hipMemcpyHostToDevice, b->cstream));
-        HIPCHK(hipStreamSynchronize(b->cstream));
-    }
     return MT_OK;
 }
 
@@ -1723,30 +1602,11 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
         HIPCHK(hipEventCreate(&L.e0));
         HIPCHK(hipEventCreate(&L.e1));
         HIPCHK(hipEventRecord(L.e0, ls));
-        L.workers = follow_workers(b, L, launch_n(b->n_docs, L));
-        L.fq_cap = L.workers;  // one queue slot per consumer workgroup
-        if (L.fq_cap > 0) {
-            const size_t k = i - (size_t)b->first0;
-            if (!b->h_started) HIPCHK(hipHostMalloc((void **)&b->h_started, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent));
-            if (k < 64) {
-                ((volatile uint32_t *)b->h_started)[k] = 0;
-                L.h_started = b->h_started + k;
-                L.follow = -2;
-            } else {
-                L.workers = L.fq_cap = 0;
-            }
-        }
-        if (L.fq_cap > 0) {
-            int rc = prep_follow(L, ls);
-            if (rc) return rc;
-        }
         int rc = launch_replay(b, ls, L);
         if (rc) return rc;
         HIPCHK(hipEventRecord(L.e1, ls));
         if (ls != s) HIPCHK(hipStreamWaitEvent(s, L.e1, 0));
     }
-    // the consumers are launched by mt_batch_sync once every producer workgroup is resident
-    // (a worker dispatched ahead of a producer's workgroups would hold LDS they need)
     b->n_first = (int)b->launches.size();
     HIPCHK(hipEventRecord(b->ev1, s));
     b->run_stream = s;
@@ -1824,25 +1684,11 @@ static int launch_on(mt_batch *b, Launch &&L, int *next_stream, std::vector<int>
 MT_API int mt_batch_sync(mt_batch *b) {
     if (!b || b->launches.empty()) return MT_ERR_STATE;
     std::vector<int> pending;
-    for (int li = b->first0; li < b->n_first; li++)
-        if (!b->launches[(size_t)li].consumer) pending.push_back(li);
+    for (int li = b->first0; li < b->n_first; li++) pending.push_back(li);
     int next_stream = 1, rc = MT_OK;
-    // follow-on consumers: launched as soon as their producer is resident (or has finished)
-    auto launch_ready_follows = [&](int only) -> int {
-        for (int li = b->first0; li < b->n_first; li++) {
-            if (b->launches[(size_t)li].follow != -2) continue;
-            const Launch &Pr = b->launches[(size_t)li];
-            if (li != only && ((volatile uint32_t *)Pr.h_started)[0] < (uint32_t)launch_n(b->n_docs, Pr)) continue;
-            int r = launch_follow(b, li);
-            if (r) return r;
-        }
-        return MT_OK;
-    };
     while (!pending.empty()) {
         size_t k = 0;
         for (;; std::this_thread::sleep_for(std::chrono::microseconds(20))) {
-            rc = launch_ready_follows(-1);
-            if (rc) return rc;
             for (k = 0; k < pending.size(); k++) {
                 hipError_t q = hipEventQuery(b->launches[(size_t)pending[k]].e1);
                 if (q == hipSuccess) break;
@@ -1856,22 +1702,9 @@ MT_API int mt_batch_sync(mt_batch *b) {
             Launch &L = b->launches[(size_t)li];
             HIPCHK(hipEventElapsedTime(&L.ms, L.e0, L.e1));
         }
-        if (b->launches[(size_t)li].consumer) {
-            rc = gather_follow(b, li);
-            if (rc) return rc;
-        }
         rc = gather_launch(b, li);
         if (rc) return rc;
-        // a producer's consumer is gathered after it (it overrides the queued documents' results)
-        if (b->launches[(size_t)li].follow == -2) {
-            rc = launch_ready_follows(li);
-            if (rc) return rc;
-        }
-        if (b->launches[(size_t)li].follow >= 0) pending.push_back(b->launches[(size_t)li].follow);
         const Launch &S = b->launches[(size_t)li];
-        if (S.consumer)
-            for (size_t i = 0; i < S.docs.size(); i++)
-                if (b->docout[(size_t)S.docs[i]].status < 0) return MT_INTERNAL;  // an item no worker replayed
         if (S.level >= b->opt.max_retries) continue;
         const int64_t n = launch_n(b->n_docs, S);
         std::map<int, Launch> groups;
@@ -2011,7 +1844,6 @@ MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *o) {
     o->resumed = (int32_t)std::count_if(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x >= 0; });
     o->lds_bytes = (int32_t)L.lds;
     o->ms = L.ms;
-    o->workers = L.consumer ? L.workers : 0;
     o->ops = L.ops;
     return MT_OK;
 }
@@ -2960,6 +2792,13 @@ MT_API int mt_batch_download_log_docs(mt_batch *b, int64_t d0, int64_t d1, mt_op
             for (int64_t i = b->h_off[d]; i < b->h_off[d + 1]; i++) {
                 mt_op &o = h[(size_t)(i - base)];
                 o.flags &= (uint16_t)~MT_OPF_INTERNAL;
+                if (o.type == MT_OP_RELPOS) {  // keys back to value ids (kIdKeyUnsupported: re-derived at ingest)
+                    auto val = [&](int32_t k) {
+                        return (uint32_t)k < b->key_value.size() ? (int32_t)b->key_value[(uint32_t)k] : 0;
+                    };
+                    o.pos1 = val(o.pos1);
+                    o.pos2 = val(o.pos2);
+                }
                 if (MT_OP_IS_INSERT_LIKE(o.type) && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) o.payload += (uint32_t)tb;
             }
             tb += b->h_text_len[d];

@@ -959,6 +959,9 @@ mt_packed *mt_packed_from(std::vector<mt_op> &&ops, std::vector<int64_t> &&off, 
     return P;
 }
 
+void mt_internal_drop_log(mt_batch *b);  // mt_host.cpp
+static int ingest_packed_rest(mt_batch *b, const mt_packed *p, int64_t D);
+
 extern "C" {
 
 MT_API int mt_pack_json(mt_packed **out, int64_t n_docs, const char *const *doc_json, const int64_t *doc_len,
@@ -1104,6 +1107,9 @@ MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p) {
     int rc0 = mt_batch_get_stats(b, &st);
     if (rc0) return rc0;
     if (st.n_docs != D) return MT_ERR_ARG;
+    // the client lists are checked before anything changes (mt_batch_set_clients' own checks)
+    for (const auto &c : p->clients)
+        if (c.empty() || c.size() > (size_t)MT_MAX_CLIENTS) return MT_ERR_ARG;
     std::vector<const char *> kp, vp;
     for (const auto &k : p->keys) kp.push_back(k.c_str());
     for (const auto &v : p->values) vp.push_back(v.c_str());
@@ -1111,6 +1117,16 @@ MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p) {
     int rc = mt_batch_set_tables(b, kp.empty() ? &none : kp.data(), kp.empty() ? 1 : (int32_t)kp.size(), vp.data(),
                                  (int32_t)vp.size());
     if (rc) return rc;
+    // from here on a failure drops the previous log: it must never run against the new tables
+    rc = ingest_packed_rest(b, p, D);
+    if (rc) mt_internal_drop_log(b);
+    return rc;
+}
+
+}  // extern "C"
+
+static int ingest_packed_rest(mt_batch *b, const mt_packed *p, int64_t D) {
+    int rc = MT_OK;
     bool shared = true;
     for (int64_t d = 1; d < D && shared; d++) shared = p->clients[(size_t)d] == p->clients[0];
     auto set = [&](int64_t doc, const std::vector<std::string> &names) {
@@ -1134,5 +1150,3 @@ MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p) {
                            p->text.empty() ? &zero_text : p->text.data(), (int64_t)p->text.size(),
                            p->props.empty() ? &zero_prop : p->props.data(), (int64_t)p->props.size());
 }
-
-}  // extern "C"

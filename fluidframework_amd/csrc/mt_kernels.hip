@@ -1,8 +1,8 @@
 // mt_kernels.hip — one capacity class of the replay, snapshot-load and generator kernels.
 //
 // Compiled once per class with -DMT_SEG=<segment slots> (kClassSegs in mt_device.h); each
-// object exports mt_replay_kernel_<SEG>, mt_writer_kernel_<SEG>, mt_load_kernel_<SEG>,
-// mt_follow_kernel_<SEG> and mt_generate_kernel_<SEG>,
+// object exports mt_replay_kernel_<SEG>, mt_writer_kernel_<SEG>, mt_load_kernel_<SEG> and
+// mt_generate_kernel_<SEG>,
 // which mt_host.cpp selects per launch.  Keeping the class a template argument makes every LDS
 // table base an immediate offset (mt::make_layout) instead of a runtime pointer.
 
@@ -29,11 +29,6 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4
 // checkpoint that the document's first replay launch resumes from
 extern "C" __global__ __launch_bounds__(64) void MT_CAT(mt_load_kernel_, MT_SEG)(mt::ReplayParams P) {
     mt::replay_body<MT_SEG, true>(P);
-}
-
-// follow-on consumer of a replay launch's checkpointed documents
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void MT_CAT(mt_follow_kernel_, MT_SEG)(mt::ReplayParams P) {
-    mt::follow_body<MT_SEG>(P);
 }
 
 extern "C" __global__ __launch_bounds__(64) void MT_CAT(mt_generate_kernel_, MT_SEG)(mt::ReplayParams P) {

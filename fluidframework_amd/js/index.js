@@ -339,6 +339,11 @@ class ReplayBatch {
     // falls back to the host parser (mt_pack_json) outside its fast path, 'gpu' / 'host' force one.
     // Returns the parser that ran ('gpu' | 'host').
     ingestJson(docs, nThreads = 0, device = 'auto') {
+        if (docs.length !== this.nDocs) {  // the native parsers read exactly nDocs documents
+            const e = new RangeError(`ingestJson: ${docs.length} documents for a batch of ${this.nDocs}`);
+            e.code = 101;  // MT_ERR_ARG
+            throw e;
+        }
         const texts = docs.map((d) => (typeof d === 'string' ? d : JSON.stringify(d)));
         const path = native().ingestJson(this.h, texts, this.clients.length ? this.clients[0].longClientId : 'readonly',
                                          nThreads, device);

@@ -123,7 +123,8 @@ napi_value ingest_json(napi_env env, napi_callback_info info) {
         }
         int64_t bad = -1;
         mt_json_gpu_stats st{};
-        const int rc = mt_batch_ingest_json_gpu(b, all.data(), off.data(), nullptr, observer.c_str(), &bad, &st);
+        const int rc = mt_batch_ingest_json_gpu(b, all.data(), off.data(), (int64_t)docs.size(), nullptr,
+                                                observer.c_str(), &bad, &st);
         if (rc == MT_OK) {
             napi_create_string_utf8(env, "gpu", NAPI_AUTO_LENGTH, &path);
             return path;

@@ -87,14 +87,14 @@ class GenParams(C.Structure):
 
 
 class BatchOptions(C.Structure):
-    _fields_ = [("chunk_size", C.c_int32), ("seg_cap", C.c_int32), ("oe_cap", C.c_int32), ("blk_cap", C.c_int32),
-                ("heap_cap", C.c_int32), ("arena_factor", C.c_int32), ("pool_per_op", C.c_int32),
+    _fields_ = [("chunk_size", C.c_int32), ("seg_cap", C.c_int32),
+                ("arena_factor", C.c_int32), ("pool_per_op", C.c_int32),
                 ("max_retries", C.c_int32)]
 
 
 class LaunchInfo(C.Structure):
     _fields_ = [("seg_class", C.c_int32), ("n_docs", C.c_int32), ("resumed", C.c_int32), ("lds_bytes", C.c_int32),
-                ("ms", C.c_float), ("workers", C.c_int32), ("ops", C.c_int64)]
+                ("ms", C.c_float), ("reserved", C.c_int32), ("ops", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
@@ -175,7 +175,7 @@ def lib():
     L.mt_packed_client.restype = cp
     L.mt_batch_ingest_packed.argtypes = [vp, vp]
     L.mt_pack_json_gpu.argtypes = [P(vp), i64, vp, vp, cp, P(i64), P(JsonGpuStats)]
-    L.mt_batch_ingest_json_gpu.argtypes = [vp, vp, vp, vp, cp, P(i64), P(JsonGpuStats)]
+    L.mt_batch_ingest_json_gpu.argtypes = [vp, vp, vp, i64, vp, cp, P(i64), P(JsonGpuStats)]
     L.mt_batch_run.argtypes = [vp, vp]
     L.mt_batch_launch.argtypes = [vp, vp]
     L.mt_batch_sync.argtypes = [vp]
@@ -478,12 +478,14 @@ class ReplayBatch:
     def ingest_json_gpu(self, buf: bytes, doc_off, observer: str = "readonly", d_json=None) -> dict:
         """GPU JSON ingest of documents back to back in `buf` (doc_off[D + 1]); d_json: the same
         bytes already on the device (a pointer, e.g. a torch uint8 tensor's data_ptr(), 64 bytes
-        readable past the end) — the parse then reads HBM only.  Returns the stage timings."""
+        readable past the end) — the scan / parse stages then read HBM; `buf` is still required and
+        must hold the same bytes (key, value and client-name strings are interned from the host
+        copy).  Returns the stage timings."""
         off = np.ascontiguousarray(doc_off, np.int64)
         if len(off) != self.n_docs + 1:
             raise ValueError("doc_off must have n_docs + 1 entries")
         bad, st = C.c_int64(-1), JsonGpuStats()
-        rc = lib().mt_batch_ingest_json_gpu(self.h, buf, off.ctypes.data, d_json, observer.encode("utf-8"),
+        rc = lib().mt_batch_ingest_json_gpu(self.h, buf, off.ctypes.data, self.n_docs, d_json, observer.encode("utf-8"),
                                             C.byref(bad), C.byref(st))
         if rc == MT_UNSUPPORTED:
             raise NotOnGpuPath(bad.value, st.fail_bits)

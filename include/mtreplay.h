@@ -70,9 +70,6 @@ typedef struct mt_batch_options {
     int32_t chunk_size;      /* SnapshotV1 chunk size; 0 -> 10000 (snapshotV1.ts:40)              */
     int32_t seg_cap;         /* segment slots of the first LDS capacity class (rounded up to a
                                 class: 64 .. 4096); 0 -> derived from the ops per document        */
-    int32_t oe_cap;          /* reserved (entries / blocks / heap follow from the class)           */
-    int32_t blk_cap;         /* reserved                                                           */
-    int32_t heap_cap;        /* reserved                                                           */
     int32_t arena_factor;    /* text arena = factor * payload + 4096 code units; 0 -> 4            */
     int32_t pool_per_op;     /* prop pool words per annotate / props insert; 0 -> 96               */
     int32_t max_retries;     /* capacity-class escalations for docs that overflow; 0 -> the whole ladder; < 0: none
@@ -133,8 +130,10 @@ MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p);
    those, prop values null / booleans / integers / plain ASCII strings.  A batch with any other
    document returns MT_UNSUPPORTED with *bad_doc set and nothing changed: parse it with
    mt_pack_json (the bindings' ingest_json does).  json: the documents back to back, document d =
-   json[doc_off[d] .. doc_off[d+1]).  d_json: the same bytes already on the device (NULL: copied
-   here), 4-byte aligned and readable 64 bytes past the end.  Replaces the host parse of Client.applyMsg's input
+   json[doc_off[d] .. doc_off[d+1]), doc_off has n_docs + 1 entries and n_docs must equal the
+   batch's (else MT_ERR_ARG).  d_json: the same bytes already on the device (NULL: copied here),
+   4-byte aligned and readable 64 bytes past the end; the host copy `json` is still read (key,
+   value and client-name strings are interned from it), so both must hold the same bytes.  Replaces the host parse of Client.applyMsg's input
    (clientReplayTool.ts:194-252 feeding client.ts:797-819). */
 typedef struct mt_json_gpu_stats {
     double ms_scan, ms_count, ms_clients, ms_write, ms_props; /* device stages (hipEvents) */
@@ -146,7 +145,7 @@ typedef struct mt_json_gpu_stats {
 } mt_json_gpu_stats;
 MT_API int mt_pack_json_gpu(mt_packed **out, int64_t n_docs, const char *json, const int64_t *doc_off,
                             const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats);
-MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, const void *d_json,
+MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, int64_t n_docs, const void *d_json,
                                     const char *observer, int64_t *bad_doc, mt_json_gpu_stats *stats);
 
 /* synthesize logs on the device (include/mt_gen.h); doc_first = global index of doc 0 */
@@ -170,9 +169,7 @@ typedef struct mt_launch_info {
     int32_t resumed;        /* of them resumed from a checkpoint (the rest start from op 0)   */
     int32_t lds_bytes;      /* dynamic LDS per document (0: HBM class)                        */
     float ms;               /* device time (hipEvents on the run stream)                      */
-    int32_t workers;        /* follow-on consumer launch: its worker workgroups (0: a launch of
-                               one workgroup per document); it runs concurrently with the launch
-                               that queued its documents                      */
+    int32_t reserved;
     int64_t ops;            /* ops applied by this launch                                     */
 } mt_launch_info;
 MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *out);

@@ -18,7 +18,6 @@ for step in "$@"; do
     smoke) run smoke 300 python -u __graft_entry__.py smoke ;;
     bench) run bench 900 python -u bench.py --steps 3 --warmup 1 ;;
     bench2) run bench2 600 python -u bench.py --config 2 --steps 3 --warmup 1 ;;
-    bench2nf) run bench2nf 600 env MT_FOLLOW_WORKERS=0 python -u bench.py --config 2 --steps 3 --warmup 1 --no-cpu ;;
     bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;

@@ -183,8 +183,9 @@ def main():
                  "text": "56789"})
     # MT/test/mergeTree.annotate.spec.ts:504-521 "remote first": "remote only" reads the annotated
     # segment's props, "split remote" splits it (splitAt(1)) and the right part carries the same
-    # props; here a concurrent remote insert splits it
-    kats.append({"name": "split_remote_annotate", "source": "reference:MT/test/mergeTree.annotate.spec.ts:504-521",
+    # props.  DERIVED: the reference asserts only the split-off half's two props (:512-519); here a
+    # concurrent remote insert performs the split, and the text and full props runs are derived.
+    kats.append({"name": "split_remote_annotate", "source": "derived:MT/test/mergeTree.annotate.spec.ts:504-521",
                  "messages": [msg("remote", 1, 0, ins(0, "hello world")),
                               msg("remote", 2, 1, ann(3, 7, {"propertySource": "remote", "remoteProperty": 1})),
                               msg("other", 3, 2, ins(4, "X"))],
@@ -192,6 +193,23 @@ def main():
                  "props_runs": [[0, 3, None], [3, 1, '{"propertySource":"remote","remoteProperty":1}'],
                                 [4, 1, None], [5, 3, '{"propertySource":"remote","remoteProperty":1}'],
                                 [8, 4, None]]})
+    # The spec's own tree (:27-45): "hello world!", a Tile marker at annotateStart + 2 = 3 by the
+    # remote client; "remote first" (:486-502) annotates [1, 5) remotely; the segment at
+    # annotateStart is then "el" and splitAt(1) leaves "l" (here: split by a remote insert at 2).
+    # The literal assertion (:512-519): the split-off half has propertySource "remote" and
+    # remoteProperty 1 — props_runs' entry at position 3 (that "l"; the run also covers the marker at 4
+    # and the "l" at 5).  The other
+    # runs are derived.
+    kats.append({"name": "split_remote_annotate_spec_tree",
+                 "source": "reference:MT/test/mergeTree.annotate.spec.ts:27-45,486-519 (split-off half's props)",
+                 "messages": [msg("remote", 1, 0, ins(0, "hello world!")),
+                              msg("remote", 2, 1, ins(3, {"marker": {"refType": 1}})),
+                              msg("remote", 3, 2, ann(1, 5, {"propertySource": "remote", "remoteProperty": 1})),
+                              msg("other", 4, 3, ins(2, "X"))],
+                 "text": "heXllo world!",
+                 "props_runs": [[0, 1, None], [1, 1, '{"propertySource":"remote","remoteProperty":1}'],
+                                [2, 1, None], [3, 3, '{"propertySource":"remote","remoteProperty":1}'],
+                                [6, 8, None]]})
     kats.extend(inserting_walk_kats())
     kats.extend(snapshot_kats())
     OUT.write_text(json.dumps(kats, indent=1))

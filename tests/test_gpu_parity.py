@@ -4,6 +4,7 @@ Bit-exact on everything the path produces: final text, property runs, SnapshotV1
 and the state digest (full segment table incl. tombstones, leaf-block membership, tree
 depth, collab window).  Sizes are chosen so the oracle finishes in seconds.
 """
+import dataclasses
 import json
 from pathlib import Path
 
@@ -104,41 +105,6 @@ def test_small_capacity_escalation():
     """Force the smallest LDS class so documents overflow and are re-run in larger classes."""
     stats = _gen_batch_parity(O.gen_params(800, seed=3), 16, full_every=4, seg_cap=64, max_retries=6)
     assert stats["launches"] >= 2
-
-
-def test_follow_on_workers_resume_checkpointed_documents():
-    """A one-round first launch queues the documents it checkpoints to a concurrent consumer
-    launch of the next class; the queued documents' results come from there,
-    further escalations continue from the consumer's checkpoints, all bit-exact."""
-    import os
-
-    os.environ["MT_FOLLOW_WORKERS"] = "64"  # off by default (DESIGN.md §4a)
-    n = 384
-    p = O.gen_params(900, pct_insert=55, pct_remove=35, seed=0xF0110)
-    ops, text, props, off = O.gen_batch(p, n)
-    t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
-    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
-    with fa.ReplayBatch(n, seg_cap=64, max_retries=8) as b:
-        b.set_tables(GEN_KEYS, GEN_VALUES)
-        b.set_clients(names)
-        b.ingest(ops, off, text, props)
-        for _ in range(2):  # a second run reuses the batch (fresh queues)
-            b.run()
-            launches = b.launches()
-            cons = [li for li in launches if li["workers"] > 0]
-            assert cons and cons[0]["n_docs"] > 0 and cons[0]["resumed"] == cons[0]["n_docs"], launches
-            assert launches[0]["n_docs"] == n
-            for d in range(n):
-                dv = b.doc(d)
-                assert dv.status == st[d]
-                assert dv.digest() == int(dig[d]), f"doc {d} digest differs"
-            for d in range(0, n, 37):
-                a, e = off[d], off[d + 1]
-                assert_doc_parity(b.doc(d), O.replay_doc(ops[a:e].copy(), text, props, t, names))
-        b.snapshots()
-        for d in range(0, n, 53):
-            assert b.doc(d).snapshot_v1(device=True) == b.doc(d).snapshot_v1()
-    del os.environ["MT_FOLLOW_WORKERS"]
 
 
 def test_gpu_generator_matches_oracle_generator():
@@ -593,16 +559,26 @@ def test_relative_positions_match_oracle():
         assert od.status == 0, od.error
     for opts in ({}, {"seg_cap": 64}):
         with fa.ReplayBatch(len(docs), **opts) as b:
-            b.ingest_messages(docs)
+            pb = b.ingest_messages(docs)
             b.run()
             for i in range(len(docs)):
                 assert b.doc(i).status == 0, (i, fa.status_string(b.doc(i).status))
                 assert_doc_parity(b.doc(i), oracle[i], full=not opts)
-    with fa.ReplayBatch(len(docs)) as b:  # the native JSON ingest packs them the same way
-        b.ingest_json([json.dumps(d) for d in docs])
-        b.run()
-        for i in range(len(docs)):
-            assert_doc_parity(b.doc(i), oracle[i], full=False)
+            if not opts:
+                # the downloaded log holds value ids again (the device's marker keys mapped back),
+                # so it re-ingests to the same replay
+                ops, off, text, props = b.download_log()
+                with fa.ReplayBatch(len(docs)) as b2:
+                    b2.ingest_packed(dataclasses.replace(pb, ops=ops, doc_op_off=off, text=text, props=props))
+                    b2.run()
+                    for i in range(len(docs)):
+                        assert b2.doc(i).digest() == b.doc(i).digest(), i
+    for dev in ("gpu", "host"):  # the native JSON ingests pack them the same way
+        with fa.ReplayBatch(len(docs)) as b:
+            b.ingest_json([json.dumps(d) for d in docs], device=dev)
+            b.run()
+            for i in range(len(docs)):
+                assert_doc_parity(b.doc(i), oracle[i], full=False)
 
 
 def test_relative_positions_outside_the_device_path_are_flagged():

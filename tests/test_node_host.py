@@ -144,10 +144,20 @@ const pg = g.ingestJson(docs, 0, 'gpu'), ph = h.ingestJson(docs, 0, 'host');
 const pf = f.ingestJson([[msg('A', 1, 0, { type: 0, pos1: 0, seg: { text: 'a', props: { n: 1.5 } } })]]);
 g.run(); h.run(); f.run();
 const dg = g.deviceDigests(), dh = h.deviceDigests();
+// a document count that differs from the batch's is refused by the wrapper and by the C ABI
+// (mt_batch_ingest_json_gpu's n_docs), never read past the caller's arrays
+const codes = [];
+for (const dev of ['gpu', 'host']) {
+  try { new ReplayBatch(3).ingestJson(docs, 0, dev); codes.push('ok'); } catch (e) { codes.push(e.code); }
+}
+const raw = new ReplayBatch(3);
+try { require('./fluidframework_amd/js').native().ingestJson(raw.h, docs.map((d) => JSON.stringify(d)), 'readonly', 0, 'gpu');
+      codes.push('ok'); } catch (e) { codes.push(e.code); }
 process.stdout.write(JSON.stringify({ pg, ph, pf, same: dg[0] === dh[0] && dg[1] === dh[1],
-                                      text: g.client(0).getText() }));
+                                      text: g.client(0).getText(), codes }));
 """
     r = _node(code)
     assert r.returncode == 0, r.stderr
     got = json.loads(r.stdout)
-    assert got == {"pg": "gpu", "ph": "host", "pf": "host", "same": True, "text": "helloworld"}
+    assert got == {"pg": "gpu", "ph": "host", "pf": "host", "same": True, "text": "helloworld",
+                   "codes": [101, 101, 101]}

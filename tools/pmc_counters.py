@@ -54,8 +54,7 @@ def main():
     line = bench_line(a.bench_log)
     ops_by_class = collections.defaultdict(int)
     for li in line["launches"]:
-        if li.get("workers", 0) == 0:
-            ops_by_class[li["seg_class"]] += li["ops"]
+        ops_by_class[li["seg_class"]] += li["ops"]
     cnt = read_counters(a.csv)
     res = {"config": a.config, "docs": line["config"]["docs_per_gpu"], "ops": line["config"]["ops_per_doc"],
            "command": "bench.py --config %d --docs %d --steps 1 --warmup 0 --no-cpu" % (a.config, line["config"]["docs_per_gpu"]),
