@@ -100,7 +100,8 @@ struct OutRec {
     uint32_t ovl;    // removedClientOverlap: bit mask of clients < 31, or kOvlList | pool offset of
                      // a [n | kPoolOvlTag, 0, client x n] list
     uint32_t props;  // prop-set id in the doc's pool (0 = undefined)
-    uint32_t toff;   // text offset in the doc's text region (Marker: refType)
+    uint32_t toff;   // text offset in the doc's text region (Marker: refType; the end record of a leaf
+                     // block: the interior blocks that end with it)
     uint32_t blk;    // leaf block id; | kOutBlockEnd for the entry that ends the block
 };
 static_assert(sizeof(OutRec) == 32, "OutRec");
@@ -142,21 +143,37 @@ struct Caps {
 // Capacity classes are compile-time: each class is its own kernel instantiation
 // (mt_kernels.hip), so every LDS array base is an immediate offset and no SGPRs hold
 // table pointers or bounds.
-// The last class keeps its tables in HBM instead of LDS (the spill path for documents beyond
-// the largest LDS class; slot and block ids stay 16-bit, so it tops out below 65,535 slots).
 // The LDS classes are sized to the residency they buy: LDS is allocated in 1,280-byte granules
 // (128 per CU; measured with tools/probe/lds_residency.hip, profiles/r01_lds_residency.json) and
 // the replay kernel's 128 VGPRs cap a CU at 16 workgroups, so each class is the largest slot
 // count whose layout fits floor(128 / n) granules for n = 16, 14, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3
 // and 2 documents per CU (tools/class_sizes.cpp); 128 keeps small documents' buffers small and
 // 7,266 is the largest layout within the 160 KiB of one CU (minus the generator's static LDS).
-// The last class keeps its tables in HBM (2,097,152 slots, 32-bit ids: the spill path).
+// Beyond the LDS ladder (32-bit slot / block ids and lengths):
+//  - the GIANT class (2,000,000 slots): segment and low-level block tables in HBM, everything a
+//    per-op walk touches first in the CU's LDS — the interior blocks of levels >=
+//    kGiantLdsLevel (the top of the tree), the overlay list, the zamboni heap and the scalars; one
+//    document per CU (config 4's Zipf tail, ~10^6 segments);
+//  - the HBM class (2,097,152 slots): every table in HBM, the fallback for a giant document whose
+//    LDS-resident parts outgrow the CU.
 // The replay kernel is latency bound, so a launch's rate grows with the documents per CU.
-constexpr int kClassSegs[] = {128, 363, 423, 483, 540, 600, 720, 840, 960, 1136, 1376, 1792, 2389, 3600, 7266, 2097152};
-constexpr int kNumClasses = 16;
+constexpr int kGiantSeg = 2000000;
+constexpr int kHbmSeg = 2097152;
+constexpr int kClassSegs[] = {128, 363, 423, 483, 540, 600, 720, 840, 960, 1136, 1376, 1792, 2389, 3600, 7266, kGiantSeg, kHbmSeg};
+constexpr int kNumClasses = 17;
+constexpr int kGiantClass = kNumClasses - 2;
 constexpr int kHbmClass = kNumClasses - 1;
-constexpr int kHbmSeg = 2097152;  // giant documents (config 4: ~10^6 segments)
+constexpr int kLastLdsClass = kGiantClass - 1;
 constexpr int kReplayStartClass = 1;  // replay starts documents in at most the 16-per-CU class
+constexpr bool is_giant_seg(int seg) { return seg == kGiantSeg; }
+// giant class: block ids [0, kGiantLdsBlocks) are LDS-resident and given to blocks of level >=
+// kGiantLdsLevel (0 = leaf blocks); lower levels (and high ones once the LDS ids run out) take
+// HBM ids [kGiantLdsBlocks, cap.blk).  The overlay list and the heap have LDS capacities: a
+// document short of them checkpoints into the HBM class.
+constexpr int kGiantLdsBlocks = 2560;
+constexpr int kGiantLdsLevel = 3;
+constexpr int kGiantHeap = 1024;
+constexpr int kGiantUlist = 2048;
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS class (16-bit lengths)
 
@@ -189,6 +206,8 @@ constexpr int kColdPerSlot = 2;
 constexpr Caps class_caps(int seg) {
     // the overlay list (unsettled segments, ~100-200 at a lag <= 32) is sized to the collab window;
     // the largest classes, where a document with a wide window ends up, can hold half their slots
+    if (is_giant_seg(seg))
+        return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24 + kGiantLdsBlocks, kGiantHeap, kGiantUlist};
     return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg >= 3000 ? seg / 2 : seg / 8 + 224};
 }
 
@@ -205,8 +224,29 @@ constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
 constexpr bool is_hbm_seg(int seg) { return seg > 65000; }
 constexpr uint32_t len_bytes(int seg) { return is_hbm_seg(seg) ? 4u : 2u; }
 constexpr uint32_t idx_bytes(int seg) { return is_hbm_seg(seg) ? 4u : 2u; }
+// The giant class: make_layout is its HBM image (slot tables and the blocks of HBM ids; the LDS-
+// resident parts get no room there) and make_glayout its LDS part.
 constexpr Layout make_layout(int seg) {
     const Caps c = class_caps(seg);
+    if (is_giant_seg(seg)) {
+        Layout L{};
+        uint32_t o = 0;
+        L.len = o;     o = lds_align(o + 4u * c.seg);
+        L.sr = o;      o = lds_align(o + 4u * c.seg);
+        L.meta = o;    o = lds_align(o + 4u * c.seg);
+        L.sblk = o;    o = lds_align(o + 4u * c.seg);
+        L.bparent = o; o = lds_align(o + 4u * c.blk);
+        L.bchild = o;  o = lds_align(o + 32u * c.blk);
+        L.bcount = o;  o = lds_align(o + 1u * c.blk);
+        L.bleaf = o;   o = lds_align(o + 1u * c.blk);
+        L.bscour = o;  o = lds_align(o + 1u * c.blk);
+        L.bslen = o;   o = lds_align(o + 4u * c.blk);
+        L.bacc = o;    o = lds_align(o + 4u * c.blk);
+        L.bep = o;     o = lds_align(o + 4u * c.blk);
+        L.ulist = L.heap = L.scratch = L.hdr = o;  // in LDS (make_glayout)
+        L.bytes = o;
+        return L;
+    }
     Layout L{};
     uint32_t o = 0;
     L.len = o;     o = lds_align(o + len_bytes(seg) * c.seg);
@@ -227,6 +267,38 @@ constexpr Layout make_layout(int seg) {
     L.hdr = o;     o = lds_align(o + 4u * kHdrWords);
     L.bytes = o;
     return L;
+}
+
+constexpr Layout make_glayout() {
+    Layout L{};
+    uint32_t o = 0;
+    const uint32_t K = (uint32_t)kGiantLdsBlocks;
+    L.hdr = o;     o = lds_align(o + 4u * kHdrWords);
+    L.scratch = o; o = lds_align(o + 4u * 128);
+    L.heap = o;    o = lds_align(o + 8u * (kGiantHeap + 2));
+    L.ulist = o;   o = lds_align(o + 4u * kGiantUlist);
+    L.bparent = o; o = lds_align(o + 4u * K);
+    L.bchild = o;  o = lds_align(o + 32u * K);
+    L.bcount = o;  o = lds_align(o + 1u * K);
+    L.bleaf = o;   o = lds_align(o + 1u * K);
+    L.bscour = o;  o = lds_align(o + 1u * K);
+    L.bslen = o;   o = lds_align(o + 4u * K);
+    L.bacc = o;    o = lds_align(o + 4u * K);
+    L.bep = o;     o = lds_align(o + 4u * K);
+    L.len = L.sr = L.meta = L.sblk = o;  // in HBM (make_layout)
+    L.bytes = o;
+    return L;
+}
+static_assert(make_glayout().bytes <= 160u * 1024u - 256u, "giant class LDS");
+
+// waves per SIMD a class's replay kernel must allow (its VGPR budget is 512 / this): the documents
+// its LDS layout lets a CU hold, over 4 SIMDs (the HBM class: its launches hold a few documents)
+constexpr int class_waves_per_eu(int seg) {
+    if (is_hbm_seg(seg)) return 1;
+    const uint32_t granules = (make_layout(seg).bytes + 1279u) / 1280u;
+    int docs = (int)(128u / granules);
+    if (docs > 16) docs = 16;
+    return (docs + 3) / 4;
 }
 
 // matchProperties / rewrite tables of the interned property values (device memory, one per batch)

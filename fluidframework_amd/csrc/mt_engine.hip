@@ -142,6 +142,20 @@ struct LWord {
     MT_FI LWord &operator++(int) { return *this = (T)(T(*this) + 1); }
 };
 
+// A block table.  In the giant class block ids [0, kGiantLdsBlocks) live in the CU's LDS (the
+// interior blocks near the root) and the rest in HBM: an access selects the base by id, so the
+// engine code is the same for both (flat loads / stores).  Every other class has one base.
+// kShift: log2 of the entries per block (b_child: 8).
+template <typename T, int kShift, bool kSplit>
+struct BArr {
+    T *lds;  // kSplit: entries of the LDS-resident ids
+    T *p;    // the table (giant class: indexed by the full id, ids below kGiantLdsBlocks unused)
+    MT_FI T &operator[](uint32_t i) const {
+        if constexpr (kSplit) return (i >> kShift) < (uint32_t)kGiantLdsBlocks ? lds[i] : p[i];
+        return p[i];
+    }
+};
+
 // kW: a writer replica (the local-client path: local ops with UnassignedSequenceNumber, pending
 // segment groups acked by the replica's own sequenced messages); compiled as mt_writer_kernel_<SEG>
 // so the observer kernels carry none of it
@@ -154,6 +168,10 @@ struct Engine {
     using Idx = std::conditional_t<idx_bytes(SEG) == 2u, uint16_t, uint32_t>;
     static constexpr uint32_t kNoBlk = idx_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
     static constexpr bool kHbm = is_hbm_seg(SEG);
+    static constexpr bool kGiant = is_giant_seg(SEG);
+    static constexpr Layout glay = make_glayout();
+    template <typename T, int kShift = 0>
+    using BA = BArr<T, kShift, kGiant>;
     static constexpr uint32_t kMaxLen = len_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
     // ---- LDS state
     Len *s_len;
@@ -161,15 +179,19 @@ struct Engine {
     uint32_t *s_sr;  // seq16 | rseq16 << 16 (window-relative); of a free slot: the next free slot
     Idx *s_blk;
     Idx *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
-    Idx *b_parent, *b_child;  // b_parent of a free block links the free block list
-    uint8_t *b_count, *b_leaf;
-    int8_t *b_scour;
-    uint32_t *b_slen, *b_acc;
-    uint32_t *b_ep;      // HBM class: the overlay epoch that last wrote b_acc[B] (no O(blocks) clear)
+    BA<Idx> b_parent;  // b_parent of a free block links the free block list
+    BA<Idx, 3> b_child;
+    BA<uint8_t> b_count, b_leaf;
+    BA<int8_t> b_scour;
+    BA<uint32_t> b_slen, b_acc;
+    BA<uint32_t> b_ep;   // HBM / giant class: the overlay epoch that last wrote b_acc[B] (no O(blocks) clear)
     uint32_t ov_epoch;
     uint32_t *scratch;  // 128 words
     // ---- uniform scalars
     int32_t slot_top, free_head, free_n, blk_top, n_bfree, bfree_head, root, depth, hn, nu;
+    // giant class: the LDS-resident block ids [0, lds_top) and their free list (blk_top / bfree_head
+    // are the HBM ids, from kGiantLdsBlocks)
+    int32_t lds_top, n_lfree, lfree_head;
     int32_t min_seq, cur_seq, status, settled_min;
     int32_t sbase;  // sequence numbers in s_sr are relative to sbase (<= minSeq)
     int32_t splits;                 // leaf/interior block splits so far (overlay staleness)
@@ -212,23 +234,37 @@ struct Engine {
 #endif
 
     // ------------------------------------------------------------------ layout
-    MT_FI void carve(uint8_t *tb) {
+    // tb: the document's tables (LDS, or the HBM image of the HBM / giant class); lb: the giant
+    // class's LDS part (make_glayout)
+    MT_FI void carve(uint8_t *tb, uint8_t *lb) {
         s_len = (Len *)(tb + lay.len);
         s_sr = (uint32_t *)(tb + lay.sr);
         s_meta = (uint32_t *)(tb + lay.meta);
         s_blk = (Idx *)(tb + lay.sblk);
-        u_list = (Idx *)(tb + lay.ulist);
-        b_parent = (Idx *)(tb + lay.bparent);
-        b_child = (Idx *)(tb + lay.bchild);
-        b_count = (uint8_t *)(tb + lay.bcount);
-        b_leaf = (uint8_t *)(tb + lay.bleaf);
-        b_scour = (int8_t *)(tb + lay.bscour);
-        b_slen = (uint32_t *)(tb + lay.bslen);
-        b_acc = (uint32_t *)(tb + lay.bacc);
-        b_ep = (uint32_t *)(tb + lay.bep);
-        h_ent = (uint2 *)(tb + lay.heap);
-        scratch = (uint32_t *)(tb + lay.scratch);
-        uint32_t *hw = (uint32_t *)(tb + lay.hdr);
+        uint8_t *xb = kGiant ? lb : tb;  // the per-op state: in LDS for the giant class
+        const Layout &xl = kGiant ? glay : lay;
+        u_list = (Idx *)(xb + xl.ulist);
+        b_parent.p = (Idx *)(tb + lay.bparent);
+        b_child.p = (Idx *)(tb + lay.bchild);
+        b_count.p = (uint8_t *)(tb + lay.bcount);
+        b_leaf.p = (uint8_t *)(tb + lay.bleaf);
+        b_scour.p = (int8_t *)(tb + lay.bscour);
+        b_slen.p = (uint32_t *)(tb + lay.bslen);
+        b_acc.p = (uint32_t *)(tb + lay.bacc);
+        b_ep.p = (uint32_t *)(tb + lay.bep);
+        if constexpr (kGiant) {
+            b_parent.lds = (Idx *)(lb + glay.bparent);
+            b_child.lds = (Idx *)(lb + glay.bchild);
+            b_count.lds = (uint8_t *)(lb + glay.bcount);
+            b_leaf.lds = (uint8_t *)(lb + glay.bleaf);
+            b_scour.lds = (int8_t *)(lb + glay.bscour);
+            b_slen.lds = (uint32_t *)(lb + glay.bslen);
+            b_acc.lds = (uint32_t *)(lb + glay.bacc);
+            b_ep.lds = (uint32_t *)(lb + glay.bep);
+        }
+        h_ent = (uint2 *)(xb + xl.heap);
+        scratch = (uint32_t *)(xb + xl.scratch);
+        uint32_t *hw = (uint32_t *)(xb + xl.hdr);
         pay_end.p = hw + 0;
         arena_base.p = hw + 1;
         arena_end.p = hw + 2;
@@ -270,9 +306,12 @@ struct Engine {
         slot_top = 0;
         free_head = -1;
         free_n = 0;
-        blk_top = 0;
+        blk_top = kGiant ? kGiantLdsBlocks : 0;
         n_bfree = 0;
         bfree_head = -1;
+        lds_top = 0;
+        n_lfree = 0;
+        lfree_head = -1;
         sbase = 0;
         clear_epochs();
         hn = 0;
@@ -292,7 +331,7 @@ struct Engine {
         idmap_n = 0;
         rel_pend = 0;
         // initialNode (mergeTree.ts:1125): an empty root leaf block
-        root = alloc_block(1);
+        root = alloc_block(1, 0);
         depth = 1;
         // heap entry 0 is the sentinel LRUSegmentComparer.min = { maxSeq: -2 } (never compared);
         // its 8 bytes hold the SnapshotLoader's batch state (insert position, batch open), so
@@ -318,9 +357,19 @@ struct Engine {
         }
         return s;
     }
-    MT_FI int32_t alloc_block(int leaf) {
+    // level: the block's height above the leaf blocks (0: a leaf block; a block's level never changes)
+    MT_FI int32_t alloc_block(int leaf, int32_t level) {
         int32_t b;
-        if (n_bfree > 0) {
+        if (kGiant && level >= kGiantLdsLevel && (n_lfree > 0 || lds_top < kGiantLdsBlocks)) {
+            if (n_lfree > 0) {
+                b = lfree_head;
+                lfree_head = (int32_t)rfl((uint32_t)b_parent[b]);
+                if (lfree_head == (int32_t)kNoBlk) lfree_head = -1;
+                n_lfree--;
+            } else {
+                b = lds_top++;
+            }
+        } else if (n_bfree > 0) {
             b = bfree_head;
             bfree_head = (int32_t)rfl((uint32_t)b_parent[b]);
             if (bfree_head == (int32_t)kNoBlk) bfree_head = -1;
@@ -340,6 +389,12 @@ struct Engine {
         return b;
     }
     MT_FI void free_block(int32_t b) {
+        if (kGiant && b < kGiantLdsBlocks) {
+            b_parent[b] = (Idx)(lfree_head < 0 ? (int32_t)kNoBlk : (int32_t)lfree_head);
+            lfree_head = b;
+            n_lfree++;
+            return;
+        }
         b_parent[b] = (Idx)(bfree_head < 0 ? (int32_t)kNoBlk : (int32_t)bfree_head);
         bfree_head = b;
         n_bfree++;
@@ -405,7 +460,8 @@ struct Engine {
     // ------------------------------------------------------------------ ancestor chains
     // every active lane adds v into arr[] on the chain leaf block b -> root (all leaves sit at
     // depth - 1, so the walk is `depth` uniform steps)
-    MT_FI void chain_add(uint32_t *arr, bool act, uint32_t b, uint32_t v) {
+    template <typename Arr>
+    MT_FI void chain_add(Arr &arr, bool act, uint32_t b, uint32_t v) {
         for (int32_t l = 0; l < depth; l++) {
             if (act && b != kNoBlk) {
                 lds_add(&arr[b], v);
@@ -776,7 +832,7 @@ struct Engine {
 
     // updateRoot (mergeTree.ts:1876-1887)
     MT_FI void update_root(int32_t split_node) {
-        int32_t nr = alloc_block(0);
+        int32_t nr = alloc_block(0, depth);  // the old root is at level depth - 1
         if (status) return;
         b_child[nr * 8 + 0] = (Idx)root;
         b_child[nr * 8 + 1] = (Idx)split_node;
@@ -792,7 +848,7 @@ struct Engine {
     // insertingWalk's "insert the split-off node after its source" (mergeTree.ts:2446-2453),
     // cascading MergeTree.split (2476-2489) up the interior levels and updateRoot at the top.
     MT_FI void insert_child_after(int32_t p, int32_t after, int32_t nc) {
-        for (;;) {
+        for (int32_t level = 1;; level++) {  // p's level
             int32_t i = child_index(p, after);
             int32_t n = b_count[p];
             wsync();
@@ -807,7 +863,7 @@ struct Engine {
             wsync();
             if (n + 1 < kMaxNodes) return;
             // split the interior block p: children 4..7 move to m
-            int32_t m = alloc_block(0);
+            int32_t m = alloc_block(0, level);
             if (status) return;
             splits++;
             wsync();
@@ -837,7 +893,7 @@ struct Engine {
 
     // MergeTree.split on a leaf block that now holds 8 children; returns the new right block.
     MT_FI int32_t split_leaf(int32_t blk) {
-        int32_t nb = alloc_block(1);
+        int32_t nb = alloc_block(1, 0);
         if (status) return blk;
         splits++;
         wsync();
@@ -1794,7 +1850,7 @@ struct Engine {
     // Regroup `nk` children (hold[0..nk)) of `parent`'s former child blocks into
     // floor(nk / 4) (1..7) new blocks of near-equal size, first blocks one larger
     // (pack, mergeTree.ts:1389-1411).  Leaf mode also moves the leaves' s_blk.
-    MT_FI int32_t regroup(int32_t parent, int32_t pn, const uint32_t *hold, int32_t nk, int leaf) {
+    MT_FI int32_t regroup(int32_t parent, int32_t pn, const uint32_t *hold, int32_t nk, int leaf, int32_t level) {
         int32_t cc = nk / (kMaxNodes / 2);
         if (cc > kMaxNodes - 1) cc = kMaxNodes - 1;
         if (cc < 1) cc = 1;
@@ -1806,7 +1862,7 @@ struct Engine {
         wsync();
         for (int32_t q = cc; q < pn; q++) free_block((int32_t)rdl(id, q));
         for (int32_t q = pn; q < cc; q++) {
-            const int32_t nb = alloc_block(leaf);
+            const int32_t nb = alloc_block(leaf, level);
             if (status) return cc;
             if (lane == q) id = (uint32_t)nb;
         }
@@ -1873,12 +1929,12 @@ struct Engine {
     // pack for an interior block `blk` (its parent's children are interior blocks);
     // repeats upward while the parent underflows (mergeTree.ts:1414-1419)
     MT_FI void pack_interior(int32_t blk) {
-        for (;;) {
+        for (int32_t level = 1;; level++) {  // blk's level (its parent's children are regrouped)
             const int32_t parent = b_parent[blk];
             const int32_t pn = b_count[parent];
             uint64_t sm;
             const int32_t total = gather_grandchildren(parent, pn, scratch, &sm);
-            const int32_t cc = regroup(parent, pn, scratch, total, 0);
+            const int32_t cc = regroup(parent, pn, scratch, total, 0, level);
             if (status) return;
             if (cc < kMaxNodes / 2 && parent != root) blk = parent;
             else return;
@@ -1898,7 +1954,7 @@ struct Engine {
         const uint32_t slot = lane < total ? gat[lane] : 0u;
         const int32_t nk = scour(slot, total, startM, hold);
         if (status) return;
-        const int32_t cc = regroup(parent, pn, hold, nk, 1);
+        const int32_t cc = regroup(parent, pn, hold, nk, 1, 0);
         if (status) return;
         if (cc < kMaxNodes / 2 && parent != root) pack_interior(parent);
     }
@@ -2083,17 +2139,17 @@ struct Engine {
             wsync();
             return;
         }
-        int32_t child = alloc_block(1);
+        int32_t child = alloc_block(1, 0);
         if (status) return;
         b_child[child * 8] = (Idx)slot;
         b_count[child] = 1;
         s_blk[slot] = (Idx)child;
         wsync();
         int32_t left = b;
-        for (;;) {
+        for (int32_t level = 1;; level++) {  // the level of left's parent (and of np)
             const int32_t p = b_parent[left];
             if (p == (int32_t)kNoBlk) {  // left is the root: the top level now has two blocks
-                const int32_t r = alloc_block(0);
+                const int32_t r = alloc_block(0, level);
                 if (status) return;
                 b_child[r * 8] = (Idx)left;
                 b_child[r * 8 + 1] = (Idx)child;
@@ -2111,7 +2167,7 @@ struct Engine {
                 b_parent[child] = (Idx)p;
                 break;
             }
-            const int32_t np = alloc_block(0);
+            const int32_t np = alloc_block(0, level);
             if (status) return;
             b_child[np * 8] = (Idx)child;
             b_count[np] = 1;
@@ -2258,12 +2314,17 @@ struct Engine {
         }
     }
 
-    MT_FI int32_t next_leaf_block(int32_t b) {
-        for (;;) {
+    // *closes: the interior blocks that end with b (the levels climbed to the next leaf block)
+    MT_FI int32_t next_leaf_block(int32_t b, int32_t *closes = nullptr) {
+        for (int32_t up = 0;; up++) {
             int32_t p = b_parent[b];
-            if (p == (int32_t)kNoBlk) return -1;
+            if (p == (int32_t)kNoBlk) {
+                if (closes) *closes = up;
+                return -1;
+            }
             int32_t i = child_index(p, b);
             if (i + 1 < (int32_t)b_count[p]) {
+                if (closes) *closes = up;
                 b = b_child[p * 8 + i + 1];
                 while (!b_leaf[b]) b = b_child[b * 8];
                 return b;
@@ -2700,29 +2761,45 @@ struct Engine {
         const int32_t fb = cap.blk - blk_top + n_bfree;
         return fs < 6 || fb < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 24;
     }
-    template <typename T>
-    MT_FI void dump(uint32_t *&p, const T *src, int32_t n) {
+    template <typename A>
+    MT_FI void dump(uint32_t *&p, const A &src, int32_t n) {
         for (int32_t i = lane; i < n; i += kWave) p[i] = (uint32_t)src[i];
         p += n;
     }
-    template <typename T>
-    MT_FI void load(const uint32_t *&p, T *dst, int32_t n) {
-        for (int32_t i = lane; i < n; i += kWave) dst[i] = (T)p[i];
+    template <typename A>
+    MT_FI void load(const uint32_t *&p, A dst, int32_t n) {
+        for (int32_t i = lane; i < n; i += kWave) dst[i] = p[i];
         p += n;
     }
     // block ids in the image are index-width independent: kNoBlk (0xFFFF in the LDS classes,
     // 0xFFFFFFFF in the HBM class) is stored as 0xFFFFFFFF
-    MT_FI void dump_blk(uint32_t *&p, const Idx *src, int32_t n) {
+    template <typename A>
+    MT_FI void dump_blk(uint32_t *&p, const A &src, int32_t n) {
         for (int32_t i = lane; i < n; i += kWave) p[i] = src[i] == (Idx)kNoBlk ? 0xFFFFFFFFu : (uint32_t)src[i];
         p += n;
     }
-    MT_FI void load_blk(const uint32_t *&p, Idx *dst, int32_t n) {
+    template <typename A>
+    MT_FI void load_blk(const uint32_t *&p, A dst, int32_t n) {
         for (int32_t i = lane; i < n; i += kWave) dst[i] = p[i] == 0xFFFFFFFFu ? (Idx)kNoBlk : (Idx)p[i];
         p += n;
     }
     MT_FI void checkpoint(uint32_t *ck, int32_t ops_done) {
         resolve_splits();
         wsync();
+        if constexpr (kGiant) {
+            // the image has one id space (the HBM class restores it): the LDS free list joins the
+            // HBM one; LDS ids never handed out ([lds_top, kGiantLdsBlocks)) stay unreferenced
+            if (n_lfree > 0) {
+                int32_t t = lfree_head;
+                for (int32_t i = 1; i < n_lfree; i++) t = (int32_t)rfl((uint32_t)b_parent[t]);
+                b_parent[t] = (Idx)(bfree_head < 0 ? kNoBlk : (uint32_t)bfree_head);
+                bfree_head = lfree_head;
+                n_bfree += n_lfree;
+                lfree_head = -1;
+                n_lfree = 0;
+                wsync();
+            }
+        }
         if (lane == 0) {
             ck[0] = 0x4D54434Bu;  // "MTCK"
             ck[1] = (uint32_t)ops_done;
@@ -2807,20 +2884,106 @@ struct Engine {
         load(p, s_meta, slot_top);
         load(p, s_blk, slot_top);
         load(p, u_list, nu);
-        load_blk(p, b_parent, blk_top);
-        load(p, b_child, 8 * blk_top);
-        for (int32_t i = lane; i < blk_top; i += kWave) {
-            const uint32_t v = p[i];
-            b_count[i] = (uint8_t)v;
-            b_leaf[i] = (uint8_t)(v >> 8);
-            b_scour[i] = (int8_t)(uint8_t)(v >> 16);
+        if constexpr (kGiant) {
+            restore_giant_blocks(p, blk_top);
+            p += 11 * (int64_t)rfl(ck[5]);
+        } else {
+            load_blk(p, b_parent, blk_top);
+            load(p, b_child, 8 * blk_top);
+            for (int32_t i = lane; i < blk_top; i += kWave) {
+                const uint32_t v = p[i];
+                b_count[i] = (uint8_t)v;
+                b_leaf[i] = (uint8_t)(v >> 8);
+                b_scour[i] = (int8_t)(uint8_t)(v >> 16);
+            }
+            p += blk_top;
+            load(p, b_slen, blk_top);
         }
-        p += blk_top;
-        load(p, b_slen, blk_top);
         load(p, (uint32_t *)h_ent, 2 * (hn + 1));
         for (int32_t i = lane; i < kColdPerSlot * slot_top; i += kWave) cold[i] = cold_src[i];
         wsync();
         return ops_done;
+    }
+
+    // giant class: the checkpoint's blocks (image ids [0, n)) are renumbered as they load — levels
+    // >= kGiantLdsLevel to LDS ids (while they last), the others to HBM ids from kGiantLdsBlocks —
+    // and the image's free blocks are dropped.  Per image block, the HBM b_ep / b_acc entries of
+    // ids kGiantLdsBlocks + i serve as temporaries (level, new id); clear_epochs() resets b_ep.
+    MT_FI void restore_giant_blocks(const uint32_t *img, int32_t n) {
+        const uint32_t *ip = img;           // b_parent (0xFFFFFFFF: none; free blocks: the free list)
+        const uint32_t *ic = img + n;       // b_child rows
+        const uint32_t *ik = img + 9 * n;   // count | leaf << 8 | scour << 16
+        const uint32_t *is = img + 10 * n;  // b_slen (settled lengths)
+        uint32_t *tlev = b_ep.p + kGiantLdsBlocks;
+        uint32_t *tmap = b_acc.p + kGiantLdsBlocks;
+        constexpr uint32_t kFree = 0xFFFFFFFFu;
+        for (int32_t i = lane; i < n; i += kWave) tlev[i] = 0u;
+        wsync();
+        {  // the image's free list (its links are b_parent)
+            int32_t t = bfree_head;
+            for (int32_t k = 0; k < n_bfree && t >= 0 && t < n; k++) {
+                if (lane == 0) tlev[t] = kFree;
+                t = (int32_t)rfl(ip[t]);
+            }
+        }
+        wsync();
+        // level = depth - 1 - (distance to the root); ids in image order, LDS ids first come first
+        int32_t nl = 0, nh = 0;
+        for (int32_t b0 = 0; b0 < n; b0 += kWave) {
+            const int32_t i = b0 + lane;
+            const bool live = i < n && tlev[i] != kFree;
+            int32_t dist = 0;
+            uint32_t c = live ? (uint32_t)i : kFree;
+            for (int32_t l = 0; l + 1 < depth; l++) {
+                const uint32_t q = c != kFree ? ip[c] : kFree;
+                if (q != kFree) dist++;
+                c = q;
+            }
+            const int32_t level = depth - 1 - dist;
+            const bool cand = live && level >= kGiantLdsLevel;
+            const uint64_t below = (1ull << lane) - 1ull;
+            const int32_t rl = nl + __popcll(ballot(cand) & below);
+            const bool inl = cand && rl < kGiantLdsBlocks;
+            const uint64_t hm = ballot(live && !inl);
+            const uint32_t nid = inl ? (uint32_t)rl : (uint32_t)(kGiantLdsBlocks + nh + __popcll(hm & below));
+            if (live) tmap[i] = nid;
+            nl += __popcll(ballot(inl));
+            nh += __popcll(hm);
+        }
+        wsync();
+        for (int32_t b0 = 0; b0 < n; b0 += kWave) {
+            const int32_t i = b0 + lane;
+            if (i < n && tlev[i] != kFree) {
+                const uint32_t nb = tmap[i], par = ip[i], k = ik[i];
+                b_parent[nb] = par == kFree ? (Idx)kNoBlk : (Idx)tmap[par];
+                b_count[nb] = (uint8_t)k;
+                b_leaf[nb] = (uint8_t)(k >> 8);
+                b_scour[nb] = (int8_t)(uint8_t)(k >> 16);
+                b_slen[nb] = is[i];
+            }
+        }
+        // child rows: 8 lanes per block
+        for (int32_t e0 = 0; e0 < 8 * n; e0 += kWave) {
+            const int32_t e = e0 + lane, i = e >> 3, j = e & 7;
+            if (e < 8 * n && tlev[i] != kFree) {
+                const uint32_t k = ik[i], c = ic[e];
+                const bool leaf = ((k >> 8) & 0xFFu) != 0u;
+                b_child[tmap[i] * 8 + j] = (Idx)(!leaf && (uint32_t)j < (k & 0xFFu) ? tmap[c] : c);
+            }
+        }
+        for (int32_t b0 = 0; b0 < slot_top; b0 += kWave) {
+            const int32_t sl = b0 + lane;
+            if (sl < slot_top && (s_meta[sl] & kMetaLinked)) s_blk[sl] = (Idx)tmap[(uint32_t)s_blk[sl]];
+        }
+        wsync();
+        root = (int32_t)rfl(tmap[root]);
+        lds_top = nl;
+        blk_top = kGiantLdsBlocks + nh;
+        bfree_head = -1;
+        n_bfree = 0;
+        lfree_head = -1;
+        n_lfree = 0;
+        clear_epochs();
     }
 
     // ------------------------------------------------------------------ output
@@ -2837,6 +3000,10 @@ struct Engine {
         while (blk >= 0) {
             const int32_t n = b_count[blk];
             const int32_t j = w + lane;
+            // the end record of a leaf block carries the interior blocks that end with it, so the
+            // host can rebuild the whole tree (getStackContext's block deltas)
+            int32_t closes = 0;
+            const int32_t nxt = next_leaf_block(blk, &closes);
             if (lane <= n && j < out_cap) {
                 OutRec r;
                 if (lane < n) {
@@ -2858,13 +3025,13 @@ struct Engine {
                     r.meta = 0;
                     r.ovl = 0;
                     r.props = 0;
-                    r.toff = 0;
+                    r.toff = (uint32_t)closes;
                     r.blk = (uint32_t)blk | kOutBlockEnd;
                 }
                 out[j] = r;
             }
             w += n + 1;
-            blk = next_leaf_block(blk);
+            blk = nxt;
         }
         if (lane == 0) {
             DocOut o;
@@ -2879,7 +3046,7 @@ struct Engine {
             o.ops_done = ops_done;
             o.max_oe = max_u;
             o.max_slots = slot_top;
-            o.max_blocks = blk_top;
+            o.max_blocks = kGiant ? blk_top - kGiantLdsBlocks + lds_top : blk_top;
             o.max_heap = max_heap;
             o.fail_op = fail_op;
             o.gen_text = 0;
@@ -2916,7 +3083,12 @@ __device__ __forceinline__ mt_op bcast_op(const mt_op &o, int l) {
 template <int SEG, bool kW>
 MT_FI void engine_setup(Engine<SEG, kW> &E, const ReplayParams &P, int64_t w, int64_t d, uint8_t *smem) {
     E.lane = threadIdx.x;
-    E.carve(smem);
+    if constexpr (is_giant_seg(SEG)) {
+        extern __shared__ __attribute__((aligned(16))) uint8_t gsmem[];
+        E.carve(smem, gsmem);
+    } else {
+        E.carve(smem, nullptr);
+    }
     E.cold = P.cold + w * (int64_t)SEG * kColdPerSlot;
     E.text = P.text + P.doc_text_base[d];
     E.text_cap = P.doc_text_cap[d];
@@ -2951,7 +3123,7 @@ MT_FI void engine_setup(Engine<SEG, kW> &E, const ReplayParams &P, int64_t w, in
 // global memory (same layout, same engine code; every table access becomes a global one).
 template <int SEG>
 MT_FI uint8_t *tables(const ReplayParams &P, int64_t w) {
-    if constexpr (SEG == kHbmSeg) {
+    if constexpr (is_hbm_seg(SEG)) {  // the HBM and giant classes
         return P.hbm_state + w * (int64_t)make_layout(SEG).bytes;
     } else {
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2978,8 +3150,33 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
     int32_t done = 0, fail_op = -1;
     if (P.ck_in) {
         if (src == kSrcList) src = P.ck_src[w];
-        if (src >= 0)
-            done = E.restore(P.ck_in + src * P.ck_in_words, P.cold_in + (int64_t)src * P.cold_in_seg * kColdPerSlot);
+        if (src >= 0) {
+            const uint32_t *ck = P.ck_in + src * P.ck_in_words;
+            const uint4 *cold_src = P.cold_in + (int64_t)src * P.cold_in_seg * kColdPerSlot;
+            if constexpr (is_giant_seg(SEG)) {
+                // an image whose overlay list or heap exceed the giant class's LDS capacities passes
+                // through unchanged (image and cold records) to the HBM class
+                const int32_t hn = (int32_t)rfl(ck[9]), nu = (int32_t)rfl(ck[10]);
+                if (P.ck_out && (nu + 24 > E.cap.ulist || hn + 16 > E.cap.heap)) {
+                    const int32_t st = (int32_t)rfl(ck[2]), bt = (int32_t)rfl(ck[5]);
+                    const int64_t words = kCkHdr + 4ll * st + nu + 11ll * bt + 2ll * (hn + 1);
+                    uint32_t *out = P.ck_out + w * ck_words(SEG);
+                    for (int64_t i = E.lane; i < words; i += kWave) out[i] = ck[i];
+                    for (int64_t i = E.lane; i < (int64_t)kColdPerSlot * st; i += kWave) E.cold[i] = cold_src[i];
+                    if (E.lane == 0) {
+                        DocOut o{};
+                        o.status = ST_CAPACITY;
+                        o.cap_kind = kCapCheckpoint;
+                        o.ops_done = (int32_t)ck[1];
+                        o.fail_op = (int32_t)ck[1];
+                        o.max_slots = st;
+                        P.doc_out[w] = o;
+                    }
+                    return true;
+                }
+            }
+            done = E.restore(ck, cold_src);
+        }
     }
     // writer batches: the pending-group region persists across launches.  A fresh start (first run,
     // a re-run from scratch, or the SnapshotLoader's run before the replay) clears it; a resumed

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -48,10 +49,12 @@ MT_DECLARE_CLASS(1792)
 MT_DECLARE_CLASS(2389)
 MT_DECLARE_CLASS(3600)
 MT_DECLARE_CLASS(7266)
+MT_DECLARE_CLASS(2000000)
 MT_DECLARE_CLASS(2097152)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void jg_markers_kernel(const mt_op *ops, const int64_t *op_off, mt_op *ops_w, const mt_prop *props,
-                                             int64_t D, uint32_t mk_key, uint32_t tile_key, const uint32_t *vkey,
+                                             int64_t D, uint32_t mk_key, uint32_t tile_key, uint32_t range_key,
+                                             const uint32_t *vkey,
                                              uint32_t n_values, uint32_t *n_ids, uint32_t *tile_annot);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
 extern "C" __global__ void mt_bytes_digest_kernel(const uint8_t *buf, const int64_t *off, const int64_t *len, int64_t n,
@@ -118,6 +121,8 @@ static const KernelClass kKernels[mt::kNumClasses] = {
      (const void *)mt_writer_kernel_3600},
     {7266, (const void *)mt_replay_kernel_7266, (const void *)mt_generate_kernel_7266, (const void *)mt_load_kernel_7266,
      (const void *)mt_writer_kernel_7266},
+    {2000000, (const void *)mt_replay_kernel_2000000, (const void *)mt_generate_kernel_2000000, (const void *)mt_load_kernel_2000000,
+     (const void *)mt_writer_kernel_2000000},
     {2097152, (const void *)mt_replay_kernel_2097152, (const void *)mt_generate_kernel_2097152, (const void *)mt_load_kernel_2097152,
      (const void *)mt_writer_kernel_2097152},
 };
@@ -920,17 +925,22 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     // findTile reads the block tile maps that blockUpdate rebuilds (mergeTree.ts:2748-2767); an
     // annotate of referenceTileLabels changes a marker's labels without one, so such documents'
     // tile queries are MT_UNSUPPORTED
+    // (bit 0; bit 1: the same for referenceRangeLabels and getStackContext's rangeStacks)
     std::vector<uint8_t> tile_annot((size_t)D, 0);
     {
-        uint32_t tk = 0xFFFFFFFFu;
-        for (size_t k = 0; k < b->keys.size(); k++)
+        uint32_t tk = 0xFFFFFFFFu, rk = 0xFFFFFFFFu;
+        for (size_t k = 0; k < b->keys.size(); k++) {
             if (b->keys[k] == "referenceTileLabels") tk = (uint32_t)k;
-        if (tk != 0xFFFFFFFFu)
+            if (b->keys[k] == "referenceRangeLabels") rk = (uint32_t)k;
+        }
+        if (tk != 0xFFFFFFFFu || rk != 0xFFFFFFFFu)
             for (int64_t d = 0; d < D; d++)
-                for (int64_t i = h_off[d]; i < h_off[d + 1] && !tile_annot[(size_t)d]; i++)
+                for (int64_t i = h_off[d]; i < h_off[d + 1] && tile_annot[(size_t)d] != 3; i++)
                     if (ops[i].type == MT_OP_ANNOTATE)
-                        for (uint32_t q = 0; q < ops[i].payload_len; q++)
-                            if (props[ops[i].payload + q].key == tk) tile_annot[(size_t)d] = 1;
+                        for (uint32_t q = 0; q < ops[i].payload_len; q++) {
+                            if (props[ops[i].payload + q].key == tk) tile_annot[(size_t)d] |= 1;
+                            if (props[ops[i].payload + q].key == rk) tile_annot[(size_t)d] |= 2;
+                        }
     }
     // a writer replica's log: local ops (seq == UnassignedSequenceNumber) or sequenced messages of
     // the replica itself (short id 0) that ack them
@@ -1169,10 +1179,11 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     // marker ids and tile-label annotates (resolve_marker_ids / tile_annot of mt_batch_ingest) on
     // the device: a marker's markerId value -> its key (String(value); any consistent numbering
     // serves, the ids only key idToSegment for relative positions), per-document id counts
-    uint32_t mk = 0xFFFFFFFFu, tk = 0xFFFFFFFFu;
+    uint32_t mk = 0xFFFFFFFFu, tk = 0xFFFFFFFFu, rk = 0xFFFFFFFFu;
     for (size_t k = 0; k < r.keys.size(); k++) {
         if (r.keys[k] == "markerId") mk = (uint32_t)k;
         if (r.keys[k] == "referenceTileLabels") tk = (uint32_t)k;
+        if (r.keys[k] == "referenceRangeLabels") rk = (uint32_t)k;
     }
     std::vector<uint32_t> vkey(r.values.size(), 0u), n_ids((size_t)D, 0u), tile((size_t)D, 0u);
     std::vector<uint32_t> key_value(1, 0u);
@@ -1213,7 +1224,7 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
         const uint32_t *vk_c = d_vkey;
         uint32_t nv = (uint32_t)vkey.size();
         int64_t Dd = D;
-        void *args[] = {&ops_c, &oo_c, &d_ops, &pr_c, &Dd, &mk, &tk, &vk_c, &nv, &d_nids, &d_tile};
+        void *args[] = {&ops_c, &oo_c, &d_ops, &pr_c, &Dd, &mk, &tk, &rk, &vk_c, &nv, &d_nids, &d_tile};
         hipError_t e = hipLaunchKernel((const void *)jg_markers_kernel, dim3((unsigned)D), dim3(64), args, 0, b->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
         if (e == hipSuccess) e = hipMemcpy(n_ids.data(), d_nids, 4 * (size_t)D, hipMemcpyDeviceToHost);
@@ -1283,7 +1294,7 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     b->h_nload.assign((size_t)D, 0);
     b->h_nload_segs.assign((size_t)D, 0);
     b->h_tile_annot.assign((size_t)D, 0);
-    for (int64_t d = 0; d < D; d++) b->h_tile_annot[(size_t)d] = tile[(size_t)d] ? 1 : 0;
+    for (int64_t d = 0; d < D; d++) b->h_tile_annot[(size_t)d] = (uint8_t)(tile[(size_t)d] & 3u);
     b->payload_units = (double)r.n_text;
     b->prop_records = (double)r.n_props;
     b->text_words = tb;
@@ -1333,8 +1344,14 @@ static int class_for(const mt_batch *b, int32_t ops_per_doc, int level, bool rep
     return c < mt::kNumClasses ? c : mt::kNumClasses;  // kNumClasses: nothing larger
 }
 // dynamic LDS of a class's launch (the HBM class keeps its tables in global memory)
-static size_t class_lds(int c) { return c == mt::kHbmClass ? 0 : mt::make_layout(mt::kClassSegs[c]).bytes; }
-static size_t class_state_bytes(int c) { return c == mt::kHbmClass ? mt::make_layout(mt::kHbmSeg).bytes : 0; }
+// (the giant class: its LDS part; its tables, like the HBM class's, are a per-document image in HBM)
+static size_t class_lds(int c) {
+    if (c == mt::kHbmClass) return 0;
+    if (c == mt::kGiantClass) return mt::make_glayout().bytes;
+    return mt::make_layout(mt::kClassSegs[c]).bytes;
+}
+static bool class_in_hbm(int c) { return c == mt::kHbmClass || c == mt::kGiantClass; }
+static size_t class_state_bytes(int c) { return class_in_hbm(c) ? mt::make_layout(mt::kClassSegs[c]).bytes : 0; }
 static int max_lds_bytes();
 // the class an escalated document continues in: at least 1.1x the slots (every class of the
 // ladder is a residency tier; skipping one costs more than the extra checkpoint)
@@ -1345,13 +1362,24 @@ static int resume_class(int c) {
     while (n > c + 1 && class_lds(n) > (size_t)max_lds_bytes()) n--;
     return n;
 }
-// documents per HBM-class launch: each holds its 2M-slot tables, cold records and output records
-// in device memory (~220 MB), so a launch is bounded to ~24 GB
+// documents per giant / HBM-class launch: each holds its ~2M-slot tables, cold records, output
+// records and (giant class) its checkpoint buffer in device memory (~220-290 MB), so a launch is
+// bounded to ~24 GB
 static size_t hbm_doc_bytes() {
-    const mt::Caps c = mt::class_caps(mt::kHbmSeg);
-    return (size_t)mt::make_layout(mt::kHbmSeg).bytes + (size_t)c.seg * mt::kColdPerSlot * 16 + (size_t)c.oe * sizeof(OutRec);
+    size_t m = 0;
+    for (int cls : {mt::kGiantClass, mt::kHbmClass}) {
+        const int seg = mt::kClassSegs[cls];
+        const mt::Caps c = mt::class_caps(seg);
+        size_t x = (size_t)mt::make_layout(seg).bytes + (size_t)c.seg * mt::kColdPerSlot * 16 + (size_t)c.oe * sizeof(OutRec);
+        if (cls == mt::kGiantClass) x += 4 * (size_t)mt::ck_words(seg);
+        m = std::max(m, x);
+    }
+    return m;
 }
 static const size_t kMaxHbmDocs = std::max<size_t>(1, ((size_t)24 << 30) / hbm_doc_bytes());
+static size_t launch_chunk(int cls, size_t n) { return class_in_hbm(cls) ? kMaxHbmDocs : n; }
+// where a document with a segment longer than the LDS classes' 16-bit lengths continues (from scratch)
+static int long_seg_class(int cls) { return cls < mt::kGiantClass ? mt::kGiantClass : cls == mt::kGiantClass ? mt::kHbmClass : mt::kNumClasses; }
 static bool class_usable(int c) { return c < mt::kNumClasses && class_lds(c) <= (size_t)max_lds_bytes(); }
 
 static int max_lds_bytes() {
@@ -1477,7 +1505,7 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
         int c = class_for(b, ops, 0);
         if (b->opt.seg_cap <= 0 && b->h_nload[d] > 0)
             while (c + 1 < mt::kNumClasses && mt::kClassSegs[c] < b->h_nload_segs[d] + b->h_nload_segs[d] / 4 + 64) c++;
-        c = std::min(c, mt::kHbmClass - 1);
+        c = std::min(c, mt::kLastLdsClass);
         while (c > 0 && !class_usable(c)) c--;
         return c;
     };
@@ -1501,7 +1529,7 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
             const int src = work_src.count(cls) ? work_src[cls] : -1;
             work.erase(work.begin());
             work_src.erase(cls);
-            const size_t chunk = cls == mt::kHbmClass ? kMaxHbmDocs : item.first.size();
+            const size_t chunk = launch_chunk(cls, item.first.size());
             for (size_t at = 0; at < item.first.size(); at += chunk) {
                 Launch L;
                 L.cls = cls;
@@ -1532,7 +1560,9 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
                     const int32_t d = S.docs[i];
                     const DocOut &o = b->docout[(size_t)d];
                     const bool long_seg = o.status == MT_CAPACITY && o.cap_kind == mt::kCapLongSeg;
-                    const int nxt = long_seg ? mt::kHbmClass : std::min(resume_class(cls), mt::kNumClasses - 1);
+                    // (the SnapshotLoader runs in the LDS classes and the HBM class, not the giant one)
+                    int nxt = long_seg ? mt::kHbmClass : std::min(resume_class(cls), mt::kNumClasses - 1);
+                    if (nxt == mt::kGiantClass) nxt = mt::kHbmClass;
                     if (o.status == MT_CAPACITY && o.cap_kind == mt::kCapCheckpoint && o.ops_done >= b->h_nload[d]) {
                         resume_li[(size_t)d] = li;  // loaded: the replay resumes from this checkpoint
                         resume_idx[(size_t)d] = (int32_t)i;
@@ -1569,7 +1599,7 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
     for (auto &g : groups) {
         const int cls = g.first.first, src = g.first.second;
         std::vector<int32_t> &docs = g.second;
-        if (groups.size() == 1 && cls != mt::kHbmClass && src < 0 && n_replay == b->n_docs) {
+        if (groups.size() == 1 && !class_in_hbm(cls) && src < 0 && n_replay == b->n_docs) {
             Launch L;
             L.cls = cls;
             b->launches.push_back(L);  // every document, in index order
@@ -1578,7 +1608,7 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
         std::stable_sort(docs.begin(), docs.end(), [&](int32_t x, int32_t y) {
             return b->h_off[x + 1] - b->h_off[x] > b->h_off[y + 1] - b->h_off[y];
         });
-        const size_t chunk = cls == mt::kHbmClass ? kMaxHbmDocs : docs.size();
+        const size_t chunk = launch_chunk(cls, docs.size());
         for (size_t at = 0; at < docs.size(); at += chunk) {
             Launch L;
             L.cls = cls;
@@ -1718,8 +1748,8 @@ MT_API int mt_batch_sync(mt_batch *b) {
             else continue;
             int cls = resume_class(S.cls);
             while (cls > S.cls + 1 && !class_usable(cls)) cls--;
-            // a segment beyond 16-bit lengths: re-run from scratch in the HBM class (32-bit lengths)
-            if (o.cap_kind == mt::kCapLongSeg) cls = S.cls == mt::kHbmClass ? mt::kNumClasses : mt::kHbmClass;
+            // a segment beyond 16-bit lengths: re-run from scratch in the giant class (32-bit lengths)
+            if (o.cap_kind == mt::kCapLongSeg) cls = long_seg_class(S.cls);
             if (!class_usable(cls)) continue;  // largest class reached: the document keeps MT_CAPACITY
             Launch &L = groups[cls];
             L.cls = cls;
@@ -1731,7 +1761,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
         for (auto &kv : groups) {
             Launch &G = kv.second;
             // the HBM class holds ~220 MB per document: bounded launches
-            const size_t chunk = G.cls == mt::kHbmClass ? kMaxHbmDocs : G.docs.size();
+            const size_t chunk = launch_chunk(G.cls, G.docs.size());
             for (size_t at = 0; at < G.docs.size(); at += chunk) {
                 Launch L;
                 L.cls = G.cls;
@@ -2035,9 +2065,11 @@ MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, i
 // truthy labels), 1: labels in `out`, -1: a value the device does not model (a string — for-of
 // would visit its code points — or non-string elements, which the block maps key by String(x)
 // while the leaf test compares with ===).
-static int tile_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, std::vector<std::u16string> &out) {
+// (ref_labels_of: the same for the key `tk` of the ref types `type_mask` — Tile: referenceTileLabels;
+// NestBegin | NestEnd: referenceRangeLabels, refHasRangeLabels mergeTree.ts:584-586)
+static int ref_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, uint32_t type_mask, std::vector<std::u16string> &out) {
     out.clear();
-    if (!(r.meta & mt::kMetaMarker) || !(r.toff & 1u) || !r.props || tk == 0xFFFFFFFFu) return 0;
+    if (!(r.meta & mt::kMetaMarker) || !(r.toff & type_mask) || !r.props || tk == 0xFFFFFFFFu) return 0;
     const uint32_t *p = b->c_pool.data() + r.props;
     uint32_t v = 0xFFFFFFFFu;
     for (uint32_t i = 0; i < p[0]; i++)
@@ -2069,6 +2101,9 @@ static int tile_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, std::vector
         return (i < j.size() && j[i] == ']') ? 1 : -1;
     }
 }
+static int tile_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, std::vector<std::u16string> &out) {
+    return ref_labels_of(b, r, tk, 1u, out);
+}
 
 // Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076 -> MergeTree.findTile,
 // mergeTree.ts:1763-1789) on the document's final table, in the replica's local view
@@ -2086,7 +2121,7 @@ MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const c
     *tile_pos = -1;
     if (props_len) *props_len = 0;
     if (b->c_out.status != MT_OK) return b->c_out.status;
-    if (b->h_tile_annot[(size_t)doc]) return MT_UNSUPPORTED;
+    if (b->h_tile_annot[(size_t)doc] & 1u) return MT_UNSUPPORTED;
     const std::vector<uint16_t> lu = utf8_to_utf16(std::string(label_utf8));
     const std::u16string label(lu.begin(), lu.end());
     uint32_t tk = 0xFFFFFFFFu;
@@ -2136,6 +2171,211 @@ MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const c
     std::string pj;
     if (leaves[(size_t)found]->props) props_json(b, leaves[(size_t)found]->props, pj);
     return out_str(pj, props_buf, props_cap, props_len);
+}
+
+// Client.getStackContext(startPos, rangeLabels) (client.ts:946-948 -> MergeTree.getStackContext,
+// mergeTree.ts:1750-1760; SharedSegmentSequence.getStackContext, sequence/src/sequence.ts:377) on the
+// document's final state in the replica's local view.  The final table lists the leaves in
+// document order and, per leaf block, the interior blocks that end with it, so the whole tree is
+// rebuilt here; every block's rangeStacks is the current one (blockUpdate runs on every path that
+// changes a marker's presence; a document annotating referenceRangeLabels is MT_UNSUPPORTED, its
+// maps would be stale).  The search is searchBlock with rangeShift / recordRangeLeaf
+// (mergeTree.ts:953-994, 1797-1829): a preceding block applies its whole delta (every label),
+// preceding leaves of the containing leaf block and the containing leaf only the asked-for labels.
+// Output: {label: [{"pos":P,"refType":T[,"props":{..}]}, ..]} in JS key order, stacks bottom to top.
+namespace {
+struct RangeStacks {  // label -> stack of leaf indices, in key creation order
+    std::vector<std::pair<std::u16string, std::vector<int64_t>>> s;
+    std::vector<int64_t> &get(const std::u16string &k) {
+        for (auto &e : s)
+            if (e.first == k) return e.second;
+        s.push_back({k, {}});
+        return s.back().second;
+    }
+};
+}  // namespace
+
+MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, const char *const *labels_utf8,
+                                int32_t n_labels, char *buf, int64_t cap, int64_t *len) {
+    if (!b || n_labels < 0 || (n_labels > 0 && !labels_utf8)) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    if (len) *len = 0;
+    if (b->c_out.status != MT_OK) return b->c_out.status;
+    if (b->h_tile_annot[(size_t)doc] & 2u) return MT_UNSUPPORTED;
+    std::vector<std::u16string> want;
+    for (int32_t i = 0; i < n_labels; i++) {
+        if (!labels_utf8[i]) return MT_ERR_ARG;
+        const std::vector<uint16_t> lu = utf8_to_utf16(std::string(labels_utf8[i]));
+        want.emplace_back(lu.begin(), lu.end());
+    }
+    uint32_t rk = 0xFFFFFFFFu;
+    for (size_t k = 0; k < b->keys.size(); k++)
+        if (b->keys[k] == "referenceRangeLabels") rk = (uint32_t)k;
+    // the tree: level-0 nodes list leaves (indices into `leaves`), level l > 0 nodes list nodes
+    struct TNode {
+        int level;
+        std::vector<int64_t> kids;
+        int64_t len = 0;
+        RangeStacks rs;
+    };
+    std::vector<TNode> nodes;
+    std::vector<const OutRec *> leaves;
+    const int D = std::max(1, b->c_out.depth);
+    std::vector<int64_t> open((size_t)D + 1, -1);
+    int64_t root = -1;
+    std::function<int64_t(int)> get_open = [&](int l) -> int64_t {
+        if (open[(size_t)l] >= 0) return open[(size_t)l];
+        nodes.push_back(TNode{l, {}, 0, {}});
+        const int64_t n = (int64_t)nodes.size() - 1;
+        open[(size_t)l] = n;
+        if (l + 1 <= D - 1) {
+            const int64_t p = get_open(l + 1);
+            nodes[(size_t)p].kids.push_back(n);
+        } else {
+            root = n;
+        }
+        return n;
+    };
+    {
+        TNode cur{0, {}, 0, {}};
+        for (const OutRec &r : b->c_recs) {
+            if (!rec_is_marker(r)) {
+                cur.kids.push_back((int64_t)leaves.size());
+                leaves.push_back(&r);
+                continue;
+            }
+            nodes.push_back(std::move(cur));
+            cur = TNode{0, {}, 0, {}};
+            const int64_t n = (int64_t)nodes.size() - 1;
+            if (D == 1) root = n;
+            else nodes[(size_t)get_open(1)].kids.push_back(n);
+            for (uint32_t l = 1; l <= r.toff && l < (uint32_t)D; l++) open[l] = -1;
+        }
+    }
+    if (root < 0) return MT_INTERNAL;
+    auto local_len = [](const OutRec &r) -> int64_t { return rec_removed(r) ? 0 : (int64_t)r.len; };
+    std::vector<std::u16string> labels;
+    bool bad = false;
+    auto range_labels = [&](const OutRec &r) -> bool {  // refHasRangeLabels + getRangeLabels
+        const int t = ref_labels_of(b, r, rk, 6u, labels);
+        if (t < 0) bad = true;
+        return t > 0;
+    };
+    // applyRangeReference (mergeTree.ts:246-261): NestBegin pushes; an end pops a NestBegin on top
+    auto apply_ref = [&](std::vector<int64_t> &st, int64_t leaf) {
+        if (leaves[(size_t)leaf]->toff & 2u) {
+            st.push_back(leaf);
+        } else if (!st.empty() && (leaves[(size_t)st.back()]->toff & 2u)) {
+            st.pop_back();
+        } else {
+            st.push_back(leaf);
+        }
+    };
+    auto apply_delta = [&](RangeStacks &cur, const RangeStacks &delta) {  // applyStackDelta (229-244)
+        for (const auto &e : delta.s) {
+            if (e.second.empty()) continue;
+            std::vector<int64_t> &c = cur.get(e.first);
+            for (int64_t x : e.second) apply_ref(c, x);
+        }
+    };
+    // blockUpdate's lengths and rangeStacks, children before parents (nodes were created parents
+    // before their later children, so a post-order walk from the root)
+    std::function<void(int64_t)> update = [&](int64_t n) {
+        TNode &t = nodes[(size_t)n];
+        for (int64_t k : t.kids) {
+            if (t.level == 0) {
+                const OutRec &r = *leaves[(size_t)k];
+                t.len += local_len(r);
+                if (local_len(r) > 0 && (r.meta & mt::kMetaMarker) && (r.toff & 6u) && range_labels(r))
+                    for (const auto &l : labels) apply_ref(t.rs.get(l), k);  // updateRangeInfo
+            } else {
+                update(k);
+                t.len += nodes[(size_t)k].len;
+                apply_delta(t.rs, nodes[(size_t)k].rs);
+            }
+        }
+    };
+    update(root);
+    for (const OutRec *r : leaves) (void)range_labels(*r);  // every list is checked, as the reference's blockUpdate iterates them
+    if (bad) return MT_UNSUPPORTED;
+    RangeStacks out;
+    auto leaf_marker = [&](int64_t k) {  // applyLeafRangeMarker (953-964): the asked-for labels in order
+        const OutRec &r = *leaves[(size_t)k];
+        if (!range_labels(r)) return;
+        for (const auto &w : want)
+            for (const auto &l : labels)
+                if (l == w) {
+                    apply_ref(out.get(w), k);
+                    break;
+                }
+    };
+    int64_t pos = start_pos;
+    for (int64_t n = root;;) {
+        const TNode &t = nodes[(size_t)n];
+        int64_t next = -1;
+        for (int64_t k : t.kids) {
+            const int64_t len = t.level == 0 ? local_len(*leaves[(size_t)k]) : nodes[(size_t)k].len;
+            if (pos < len) {
+                if (t.level == 0) {
+                    const OutRec &r = *leaves[(size_t)k];
+                    if ((r.meta & mt::kMetaMarker) && (r.toff & 6u)) leaf_marker(k);  // recordRangeLeaf
+                } else {
+                    next = k;
+                }
+                break;
+            }
+            if (t.level == 0) {  // rangeShift of a leaf
+                const OutRec &r = *leaves[(size_t)k];
+                if (len > 0 && (r.meta & mt::kMetaMarker) && (r.toff & 6u)) leaf_marker(k);
+            } else {  // rangeShift of a block
+                apply_delta(out, nodes[(size_t)k].rs);
+            }
+            pos -= len;
+        }
+        if (next < 0) break;
+        n = next;
+    }
+    // JSON: integer-like keys ascending first, then creation order
+    std::vector<size_t> order;
+    std::vector<std::pair<uint32_t, size_t>> idx;
+    for (size_t i = 0; i < out.s.size(); i++) {
+        uint32_t v = 0;
+        std::string k8;
+        for (char16_t c : out.s[i].first) k8.push_back(c < 0x80 ? (char)c : '\x01');
+        if (array_index(k8, &v)) idx.push_back({v, i});
+    }
+    std::sort(idx.begin(), idx.end());
+    for (auto &e : idx) order.push_back(e.second);
+    for (size_t i = 0; i < out.s.size(); i++) {
+        uint32_t v = 0;
+        std::string k8;
+        for (char16_t c : out.s[i].first) k8.push_back(c < 0x80 ? (char)c : '\x01');
+        if (!array_index(k8, &v)) order.push_back(i);
+    }
+    std::vector<int64_t> lpos(leaves.size() + 1, 0);
+    for (size_t i = 0; i < leaves.size(); i++) lpos[i + 1] = lpos[i] + local_len(*leaves[i]);
+    std::string o = "{";
+    for (size_t q = 0; q < order.size(); q++) {
+        const auto &e = out.s[order[q]];
+        if (q) o.push_back(',');
+        json_quote16(o, (const uint16_t *)e.first.data(), e.first.size());
+        o += ":[";
+        for (size_t j = 0; j < e.second.size(); j++) {
+            const OutRec &r = *leaves[(size_t)e.second[j]];
+            if (j) o.push_back(',');
+            o += "{\"pos\":" + std::to_string(lpos[(size_t)e.second[j]]) + ",\"refType\":" + std::to_string(r.toff);
+            if (r.props) {
+                std::string pj;
+                props_json(b, r.props, pj);
+                o += ",\"props\":" + pj;
+            }
+            o.push_back('}');
+        }
+        o.push_back(']');
+    }
+    o.push_back('}');
+    return out_str(o, buf, cap, len);
 }
 
 // JSON.stringify of a property object given as (key, value) records in insertion order (JS key
@@ -2934,7 +3174,7 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
         const bool all = (int64_t)todo.size() == D;
         for (size_t at = 0; at < todo.size();) {
             // the HBM class holds ~220 MB per document: bounded launches
-            const size_t n = cls == mt::kHbmClass ? std::min(todo.size() - at, kMaxHbmDocs) : todo.size() - at;
+            const size_t n = std::min(todo.size() - at, launch_chunk(cls, todo.size() - at));
             Launch L;
             L.cls = cls;
             L.caps = mt::class_caps(mt::kClassSegs[cls]);
@@ -2980,8 +3220,8 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
                 outs[(size_t)d] = part[i];
                 if (part[i].status == MT_CAPACITY && part[i].cap_kind == 1 && class_usable(cls + 1))
                     work[cls + 1].push_back(d);
-                else if (part[i].status == MT_CAPACITY && part[i].cap_kind == mt::kCapLongSeg && cls != mt::kHbmClass)
-                    work[mt::kHbmClass].push_back(d);
+                else if (part[i].status == MT_CAPACITY && part[i].cap_kind == mt::kCapLongSeg && long_seg_class(cls) < mt::kNumClasses)
+                    work[long_seg_class(cls)].push_back(d);
             }
             at += n;
         }

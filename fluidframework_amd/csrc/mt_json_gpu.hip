@@ -1605,10 +1605,12 @@ extern "C" __global__ __launch_bounds__(64) void jg_remap_kernel(Params P) {
 
 // install: marker ids (resolve_marker_ids in mt_host.cpp: a marker insert whose props give a truthy
 // markerId gets that id's key in payload_len, 0 otherwise; vkey maps value ids to keys) and the
-// documents whose annotates touch referenceTileLabels (their findTile queries are unsupported)
+// documents whose annotates touch referenceTileLabels (bit 0: their findTile queries are
+// unsupported) or referenceRangeLabels (bit 1: getStackContext)
 extern "C" __global__ __launch_bounds__(64) void jg_markers_kernel(const mt_op *ops, const int64_t *op_off,
                                                                  mt_op *ops_w, const mt_prop *props, int64_t D,
                                                                  uint32_t mk_key, uint32_t tile_key,
+                                                                 uint32_t range_key,
                                                                  const uint32_t *vkey, uint32_t n_values,
                                                                  uint32_t *n_ids, uint32_t *tile_annot) {
     const int64_t d = blockIdx.x;
@@ -1627,7 +1629,8 @@ extern "C" __global__ __launch_bounds__(64) void jg_markers_kernel(const mt_op *
             cnt += id != 0;
         } else if (o.type == MT_OP_ANNOTATE) {
             for (uint32_t q = 0; q < o.payload_len; q++) {
-                if (props[o.payload + q].key == tile_key) tile = 1;
+                if (props[o.payload + q].key == tile_key) tile |= 1u;
+                if (props[o.payload + q].key == range_key) tile |= 2u;
                 if (props[o.payload + q].key == mk_key) annot_mk = 1;
             }
         }

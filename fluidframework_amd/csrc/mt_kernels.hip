@@ -15,13 +15,22 @@
 #define MT_CAT2(a, b) a##b
 #define MT_CAT(a, b) MT_CAT2(a, b)
 
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void MT_CAT(mt_replay_kernel_, MT_SEG)(mt::ReplayParams P) {
+// The replay kernels' register budget: 512 / kWpe VGPRs.  The LDS classes allow the waves their
+// layout lets a CU hold (mt_device.h class_waves_per_eu; -DMT_WPE_UNIFORM=4 gives every LDS class
+// the 4-waves budget, the A/B baseline); the giant and HBM classes run one document per SIMD at most.
+#ifdef MT_WPE_UNIFORM
+constexpr int kWpe = mt::is_hbm_seg(MT_SEG) ? 1 : MT_WPE_UNIFORM;
+#else
+constexpr int kWpe = mt::class_waves_per_eu(MT_SEG);
+#endif
+
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void MT_CAT(mt_replay_kernel_, MT_SEG)(mt::ReplayParams P) {
     mt::replay_body<MT_SEG, false>(P);
 }
 
 // writer replicas: the same replay plus the local-client path (local ops, pending segment groups,
 // acks by the replica's own sequenced messages)
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void MT_CAT(mt_writer_kernel_, MT_SEG)(mt::ReplayParams P) {
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void MT_CAT(mt_writer_kernel_, MT_SEG)(mt::ReplayParams P) {
     mt::replay_body<MT_SEG, false, true>(P);
 }
 

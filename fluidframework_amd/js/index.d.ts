@@ -40,6 +40,9 @@ export declare class ReplayClient {
     regeneratedOps(): object[];
     /** Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076) on the final state. */
     findTile(startPos: number, tileLabel: string, preceding?: boolean): { pos: number; props?: Record<string, any> } | undefined;
+    /** Client.getStackContext(startPos, rangeLabels) (client.ts:946-948) on the final state: range
+     *  label -> its NestBegin / NestEnd markers, bottom to top. */
+    getStackContext(startPos: number, rangeLabels: string[]): Record<string, { pos: number; refType: number; props?: Record<string, any> }[]>;
     /** 0 = OK, else the MT_* status of the Error applyMsg would have thrown. */
     readonly status: number;
     readonly error: string | undefined;

@@ -294,6 +294,11 @@ class ReplayClient {
         const r = native().docFindTile(this.batch.h, this.index, startPos, tileLabel, preceding);
         return r === undefined ? undefined : { pos: r.pos, props: r.props ? JSON.parse(r.props) : undefined };
     }
+    // Client.getStackContext(startPos, rangeLabels) (client.ts:946-948; SharedSegmentSequence
+    // .getStackContext, sequence.ts:377): { label: [{ pos, refType, props }] }, stacks bottom to top
+    getStackContext(startPos, rangeLabels) {
+        return JSON.parse(native().docStackContext(this.batch.h, this.index, startPos, rangeLabels));
+    }
     get status() { return native().docStatus(this.batch.h, this.index); }
     get error() { const s = this.status; return s === 0 ? undefined : STATUS[s] || String(s); }
     getText() { return native().docText(this.batch.h, this.index); }

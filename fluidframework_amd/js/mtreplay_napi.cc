@@ -384,6 +384,26 @@ napi_value doc_find_tile(napi_env env, napi_callback_info info) {
     return r;
 }
 
+// docStackContext(h, doc, startPos, [rangeLabels]) -> JSON text of the stacks
+// (Client.getStackContext, client.ts:946-948, via mt_doc_stack_context)
+napi_value doc_stack_context(napi_env env, napi_callback_info info) {
+    auto a = args(env, info, 4);
+    mt_batch *b = batch_of(env, a[0]);
+    const int64_t doc = i64(env, a[1]), start = i64(env, a[2]);
+    const std::vector<std::string> labels = strs(env, a[3]);
+    std::vector<const char *> lp;
+    for (const auto &l : labels) lp.push_back(l.c_str());
+    int64_t n = 0;
+    MT_OK_OR_THROW(mt_doc_stack_context(b, doc, start, lp.data(), (int32_t)lp.size(), nullptr, 0, &n),
+                   "mt_doc_stack_context");
+    std::string out((size_t)n + 1, '\0');
+    MT_OK_OR_THROW(mt_doc_stack_context(b, doc, start, lp.data(), (int32_t)lp.size(), &out[0], n + 1, &n),
+                   "mt_doc_stack_context");
+    napi_value r;
+    NAPI_OK(napi_create_string_utf8(env, out.data(), (size_t)n, &r));
+    return r;
+}
+
 napi_value doc_digest(napi_env env, napi_callback_info info) {
     auto a = args(env, info, 2);
     uint64_t d = 0;
@@ -454,6 +474,7 @@ napi_value init(napi_env env, napi_value exports) {
         {"docSnapshotV1", nullptr, doc_snapshot, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docDigest", nullptr, doc_digest, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docFindTile", nullptr, doc_find_tile, nullptr, nullptr, nullptr, kMethod, nullptr},
+        {"docStackContext", nullptr, doc_stack_context, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docRegeneratedOps", nullptr, doc_regenerated_ops, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"deviceDigests", nullptr, device_digests, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"stats", nullptr, stats, nullptr, nullptr, nullptr, kMethod, nullptr},

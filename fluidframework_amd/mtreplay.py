@@ -44,6 +44,7 @@ EXPORTS = [
     "mt_packed_sizes", "mt_packed_arrays", "mt_packed_key", "mt_packed_value", "mt_packed_doc_clients",
     "mt_packed_client", "mt_batch_ingest_packed", "mt_batch_log_sizes_docs", "mt_batch_download_log_docs",
     "mt_build_id", "mt_doc_find_tile", "mt_doc_regenerated_ops", "mt_pack_json_gpu", "mt_batch_ingest_json_gpu",
+    "mt_doc_stack_context",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -201,6 +202,7 @@ def lib():
     L.mt_batch_snapshot_copy.argtypes = [vp, vp, i32]
     L.mt_batch_snapshot_digests.argtypes = [vp, vp, i32]
     L.mt_doc_find_tile.argtypes = [vp, i64, i64, cp, i32, P(i64), C.c_char_p, i64, P(i64)]
+    L.mt_doc_stack_context.argtypes = [vp, i64, i64, P(cp), i32, C.c_char_p, i64, P(i64)]
     _lib = L
     return L
 
@@ -341,6 +343,20 @@ class DocView:
         _chk(L.mt_doc_find_tile(*args, buf, n.value + 1, C.byref(n)), "mt_doc_find_tile")
         raw = buf.raw[: n.value].decode("utf-8")
         return {"pos": pos.value, "props": json.loads(raw) if raw else None}
+
+    def get_stack_context(self, start_pos: int, range_labels) -> dict:
+        """Client.getStackContext(startPos, rangeLabels) (client.ts:946-948; SharedSegmentSequence
+        .getStackContext, sequence.ts:377): {label: [{"pos", "refType"[, "props"]}, ...]}, each stack
+        bottom to top, keys in JS object order."""
+        L = lib()
+        labels = list(range_labels)
+        arr = (C.c_char_p * max(1, len(labels)))(*[l.encode("utf-8") for l in labels])
+        n = C.c_int64(0)
+        args = (self.batch.h, self.index, start_pos, arr, len(labels))
+        _chk(L.mt_doc_stack_context(*args, None, 0, C.byref(n)), "mt_doc_stack_context")
+        buf = C.create_string_buffer(n.value + 1)
+        _chk(L.mt_doc_stack_context(*args, buf, n.value + 1, C.byref(n)), "mt_doc_stack_context")
+        return json.loads(buf.raw[: n.value].decode("utf-8"))
 
     def regenerated_ops(self) -> list:
         """Client.regeneratePendingOp results of the log's reconnect (regenerate) records, in order."""

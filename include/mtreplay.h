@@ -19,6 +19,7 @@
  *   mt_doc_text                 SharedString.getText() (sequence/src/sharedString.ts:211-214 ->
  *                               MergeTreeTextHelper.getText, textSegment.ts:154-172)
  *   mt_doc_find_tile            Client.findTile(startPos, label, preceding) (client.ts:1073-1076)
+ *   mt_doc_stack_context        Client.getStackContext(startPos, rangeLabels) (client.ts:946-948)
  *   mt_doc_props_runs           Client.getPropertiesAtPosition(pos) for every pos (client.ts:1009-1023),
  *                               run-length encoded
  *   mt_doc_snapshot_v1/_blob    new SnapshotV1(mergeTree, logger).extractSync(); emit()
@@ -191,6 +192,15 @@ MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, i
    would be stale) or holds a label list other than an array of strings. */
 MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const char *label_utf8, int32_t preceding,
                             int64_t *tile_pos, char *props_buf, int64_t props_cap, int64_t *props_len);
+/* Client.getStackContext(startPos, rangeLabels) (merge-tree/src/client.ts:946-948 ->
+   mergeTree.ts:1750-1760; SharedSegmentSequence.getStackContext, sequence/src/sequence.ts:377) on
+   the document's final state: JSON {label: [{"pos": P, "refType": T[, "props": {...}]}, ...]} — the
+   range stacks of NestBegin / NestEnd markers (referenceRangeLabels), bottom to top, keys in JS
+   object order (size query with cap 0).  MT_UNSUPPORTED: the document annotates
+   referenceRangeLabels (the reference's block maps would be stale) or holds a label list other
+   than an array of strings. */
+MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, const char *const *labels_utf8,
+                                int32_t n_labels, char *buf, int64_t cap, int64_t *len);
 /* Client.regeneratePendingOp results (client.ts:855-893) of the document's MT_OP_REGENERATE
    records (a writer replica reconnecting), in order: a JSON array of the regenerated ops, one per
    reset message (a GROUP op when it regenerates to more or fewer than one op) */

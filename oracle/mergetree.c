@@ -43,6 +43,20 @@
 enum { SEG_TEXT = 0, SEG_MARKER = 1 };
 
 typedef struct Block Block;
+struct Seg;
+
+/* HierMergeBlock.rangeStacks (mergeTree.ts:49, 2755): String(label) -> Stack<ReferencePosition>, in
+   key creation order (each stack bottom to top) */
+typedef struct RStack {
+    unsigned short *key;
+    int klen;
+    struct Seg **items;
+    int n, cap;
+} RStack;
+struct RangeMap {
+    RStack *s;
+    int n, cap;
+};
 
 typedef struct Node {
     int is_leaf;
@@ -69,6 +83,7 @@ struct Block { /* MergeBlock / HierMergeBlock, mergeTree.ts:336-420 */
         struct Seg **segs;
         int n, cap;
     } rt, lt;
+    struct RangeMap rs; /* rangeStacks, rebuilt by the same blockUpdate */
 };
 
 typedef struct Group Group;
@@ -156,6 +171,9 @@ struct mto_doc {
     /* a Tile marker whose referenceTileLabels is not an array / string (for-of would throw in
        blockUpdate): tile queries report MTO_UNSUPPORTED */
     int tile_bad;
+    /* the same for a NestBegin / NestEnd marker's referenceRangeLabels: getStackContext reports
+       MTO_UNSUPPORTED */
+    int range_bad;
     /* local-client path: collabWindow.localSeq (mergeTree.ts:831) and MergeTree.pendingSegments,
        the FIFO of SegmentGroups awaiting their ack (mergeTree.ts:1093, 1261) */
     int local_seq;
@@ -1345,21 +1363,106 @@ static void add_tile_cb(void *vctx, const u16 *k, int kl, const jv *elem) {
     tm_set(&c->b->lt, k, kl, c->seg, 1); /* addTileIfNotPresent */
 }
 /* blockUpdate's rightmostTiles / leftmostTiles (mergeTree.ts:2751-2762 -> addNodeReferences) */
+/* ------------------------------------------------------------------ range stacks (getStackContext) */
+static void rm_clear(struct RangeMap *m) {
+    for (int i = 0; i < m->n; i++) {
+        free(m->s[i].key);
+        free(m->s[i].items);
+    }
+    m->n = 0;
+}
+static void rm_free(struct RangeMap *m) {
+    rm_clear(m);
+    free(m->s);
+    m->s = NULL;
+    m->cap = 0;
+}
+/* rangeStacks[label], created empty at the end of the key order when absent */
+static RStack *rm_get(struct RangeMap *m, const u16 *k, int kl) {
+    for (int i = 0; i < m->n; i++)
+        if (m->s[i].klen == kl && !memcmp(m->s[i].key, k, sizeof(u16) * (size_t)kl)) return &m->s[i];
+    if (m->n == m->cap) {
+        m->cap = m->cap ? 2 * m->cap : 4;
+        m->s = (RStack *)realloc(m->s, sizeof(RStack) * (size_t)m->cap);
+    }
+    RStack *st = &m->s[m->n++];
+    st->key = (u16 *)malloc(sizeof(u16) * (size_t)(kl + 1));
+    memcpy(st->key, k, sizeof(u16) * (size_t)kl);
+    st->klen = kl;
+    st->items = NULL;
+    st->n = st->cap = 0;
+    return st;
+}
+static void rs_push(RStack *st, Seg *x) {
+    if (st->n == st->cap) {
+        st->cap = st->cap ? 2 * st->cap : 4;
+        st->items = (Seg **)realloc(st->items, sizeof(Seg *) * (size_t)st->cap);
+    }
+    st->items[st->n++] = x;
+}
+/* applyRangeReference (mergeTree.ts:246-261): a NestBegin pushes; anything else (a NestEnd) pops a
+   NestBegin on top, else is pushed ("TODO: match end with begin": labels are not compared) */
+static void apply_range_ref(RStack *st, Seg *delta) {
+    if (delta->ref_type & 2) {
+        rs_push(st, delta);
+        return;
+    }
+    if (st->n > 0 && (st->items[st->n - 1]->ref_type & 2)) st->n--;
+    else rs_push(st, delta);
+}
+/* applyStackDelta (mergeTree.ts:229-244): every label of the delta with a non-empty stack, in the
+   delta's key order, its items bottom to top */
+static void apply_stack_delta(struct RangeMap *cur, const struct RangeMap *delta) {
+    for (int i = 0; i < delta->n; i++) {
+        const RStack *ds = &delta->s[i];
+        if (ds->n == 0) continue;
+        RStack *cs = rm_get(cur, ds->key, ds->klen);
+        for (int j = 0; j < ds->n; j++) apply_range_ref(cs, ds->items[j]);
+    }
+}
+/* refHasRangeLabels (mergeTree.ts:584-586): refType & (NestBegin | NestEnd) and a truthy
+   properties[referenceRangeLabels] */
+static const jv *range_labels(const Seg *s) {
+    if (s->kind != SEG_MARKER || !(s->ref_type & 6) || !s->props) return NULL;
+    const jv *v = jv_obj_get_ascii(s->props, "referenceRangeLabels");
+    return jv_truthy(v) ? v : NULL;
+}
+typedef struct {
+    Block *b;
+    Seg *seg;
+} AddRangeCtx;
+static void add_range_cb(void *vctx, const u16 *k, int kl, const jv *elem) {
+    (void)elem;
+    AddRangeCtx *c = (AddRangeCtx *)vctx;
+    apply_range_ref(rm_get(&c->b->rs, k, kl), c->seg); /* updateRangeInfo (mergeTree.ts:266-273) */
+}
+
 static void block_update_tiles(Block *b) {
     tm_clear(&b->rt);
     tm_clear(&b->lt);
+    rm_clear(&b->rs);
     for (int i = 0; i < b->child_count; i++) {
         Node *c = b->children[i];
         if (c->is_leaf) {
             Seg *sg = (Seg *)c;
             if (local_net_length(sg) > 0 && sg->kind == SEG_MARKER && (sg->ref_type & 1)) {
                 const jv *labels = tile_labels(sg);
-                if (!labels) continue; /* getTileLabels() -> [] */
-                AddTileCtx ctx = {b, sg};
-                if (!each_label(labels, add_tile_cb, &ctx) && b->doc) b->doc->tile_bad = 1;
+                if (labels) { /* getTileLabels() -> [] otherwise */
+                    AddTileCtx ctx = {b, sg};
+                    if (!each_label(labels, add_tile_cb, &ctx) && b->doc) b->doc->tile_bad = 1;
+                }
+            }
+            /* addNodeReferences (mergeTree.ts:289-293): NestBegin / NestEnd markers' range labels */
+            if (local_net_length(sg) > 0 && sg->kind == SEG_MARKER && (sg->ref_type & 6)) {
+                const jv *labels = range_labels(sg);
+                if (labels) {
+                    AddRangeCtx ctx = {b, sg};
+                    if (!each_label(labels, add_range_cb, &ctx) && b->doc) b->doc->range_bad = 1;
+                }
             }
         } else {
             const Block *cb = (const Block *)c;
+            apply_stack_delta(&b->rs, &cb->rs); /* (mergeTree.ts:312-316) */
             for (int j = 0; j < cb->rt.n; j++) tm_set(&b->rt, cb->rt.keys[j], cb->rt.klens[j], cb->rt.segs[j], 0);
             for (int j = 0; j < cb->lt.n; j++) tm_set(&b->lt, cb->lt.keys[j], cb->lt.klens[j], cb->lt.segs[j], 1);
         }
@@ -1469,6 +1572,142 @@ long mto_find_tile(mto_doc *d, int start_pos, const char *label_utf8, int preced
     return pos;
 }
 
+/* refHasRangeLabel (mergeTree.ts:599-608) */
+static int seg_has_range_label(mto_doc *d, const Seg *s, const u16 *label, int llen) {
+    const jv *labels = range_labels(s);
+    if (!labels) return 0;
+    HasLabelCtx ctx = {label, llen, 0};
+    if (!each_label(labels, has_label_cb, &ctx)) d->range_bad = 1;
+    return ctx.hit;
+}
+typedef struct {
+    u16 **labels;
+    int *llens;
+    int nl;
+    struct RangeMap out; /* searchInfo.stacks */
+} RangeSearch;
+/* applyLeafRangeMarker (mergeTree.ts:953-964): only the requested labels, in request order */
+static void apply_leaf_range_marker(mto_doc *d, Seg *m, RangeSearch *rs) {
+    for (int i = 0; i < rs->nl; i++)
+        if (seg_has_range_label(d, m, rs->labels[i], rs->llens[i])) apply_range_ref(rm_get(&rs->out, rs->labels[i], rs->llens[i]), m);
+}
+/* rangeShift (mergeTree.ts:978-994): a preceding leaf by its requested labels, a preceding block by
+   its whole rangeStacks delta (every label) */
+static void range_shift(mto_doc *d, Node *node, RangeSearch *rs) {
+    if (node->is_leaf) {
+        Seg *sg = (Seg *)node;
+        if (local_net_length(sg) > 0 && sg->kind == SEG_MARKER && (sg->ref_type & 6)) apply_leaf_range_marker(d, sg, rs);
+    } else {
+        apply_stack_delta(&rs->out, &((Block *)node)->rs);
+    }
+}
+/* searchBlock (mergeTree.ts:1797-1829) with { leaf: recordRangeLeaf (965-976), shift: rangeShift } */
+static void range_search_block(mto_doc *d, Block *block, int pos, RangeSearch *rs) {
+    for (int ci = 0; ci < block->child_count; ci++) {
+        Node *child = block->children[ci];
+        const int len = node_length(d, child, UNIVERSAL_SEQ, d->cw.client_id);
+        if (pos < len) {
+            if (!child->is_leaf) {
+                range_search_block(d, (Block *)child, pos, rs);
+            } else {
+                Seg *sg = (Seg *)child;
+                if (sg->kind == SEG_MARKER && (sg->ref_type & 6)) apply_leaf_range_marker(d, sg, rs);
+            }
+            return;
+        }
+        range_shift(d, child, rs);
+        pos -= len;
+    }
+}
+static long seg_position_local(mto_doc *d, Seg *s) { /* getPosition (mergeTree.ts:1586-1603), local view */
+    long pos = 0;
+    Node *node = &s->n;
+    for (Block *p = node->parent; p; node = &p->n, p = p->n.parent)
+        for (int i = 0; i < p->child_count && p->children[i] != node; i++)
+            pos += node_length(d, p->children[i], UNIVERSAL_SEQ, d->cw.client_id);
+    return pos;
+}
+/* canonical array index ("0", "17"; not "01"): JS object keys enumerate those first, ascending */
+static int u16_index_key(const u16 *k, int kl, unsigned long *v) {
+    if (kl < 1 || kl > 10 || (kl > 1 && k[0] == '0')) return 0;
+    unsigned long x = 0;
+    for (int i = 0; i < kl; i++) {
+        if (k[i] < '0' || k[i] > '9') return 0;
+        x = x * 10 + (unsigned long)(k[i] - '0');
+    }
+    if (x >= 4294967295ul) return 0;
+    *v = x;
+    return 1;
+}
+/* MergeTree.getStackContext(startPos, clientId, rangeLabels) (mergeTree.ts:1750-1760) via
+   Client.getStackContext (client.ts:946-948: the local client): JSON of searchInfo.stacks —
+   {label: [{"pos": P, "refType": T[, "props": {...}]}, ...]} in JS key order, each stack bottom to
+   top.  NULL with *status MTO_UNSUPPORTED when the document holds a range label list the reference
+   could not iterate. */
+char *mto_stack_context(mto_doc *d, int start_pos, const char *const *labels_utf8, int n_labels, int *status) {
+    RangeSearch rs;
+    memset(&rs, 0, sizeof rs);
+    rs.nl = n_labels;
+    rs.labels = (u16 **)calloc((size_t)(n_labels + 1), sizeof(u16 *));
+    rs.llens = (int *)calloc((size_t)(n_labels + 1), sizeof(int));
+    for (int i = 0; i < n_labels; i++) rs.labels[i] = utf8_to_u16(labels_utf8[i], &rs.llens[i]);
+    range_search_block(d, d->root, start_pos, &rs);
+    char *res = NULL;
+    *status = d->range_bad ? MTO_UNSUPPORTED : MTO_OK;
+    if (!d->range_bad) {
+        int *order = (int *)malloc(sizeof(int) * (size_t)(rs.out.n + 1));
+        int no = 0;
+        unsigned long iv[2];
+        /* integer-like keys ascending, then the others in creation order */
+        for (int i = 0; i < rs.out.n; i++)
+            if (u16_index_key(rs.out.s[i].key, rs.out.s[i].klen, &iv[0])) {
+                int j = no++;
+                while (j > 0 && (u16_index_key(rs.out.s[order[j - 1]].key, rs.out.s[order[j - 1]].klen, &iv[1]), iv[1] > iv[0])) {
+                    order[j] = order[j - 1];
+                    j--;
+                }
+                order[j] = i;
+            }
+        for (int i = 0; i < rs.out.n; i++)
+            if (!u16_index_key(rs.out.s[i].key, rs.out.s[i].klen, &iv[0])) order[no++] = i;
+        sb o;
+        sb_init(&o);
+        sb_putc(&o, '{');
+        for (int q = 0; q < no; q++) {
+            const RStack *st = &rs.out.s[order[q]];
+            if (q) sb_putc(&o, ',');
+            jv key;
+            memset(&key, 0, sizeof key);
+            key.kind = JV_STR;
+            key.s = st->key;
+            key.slen = st->klen;
+            jv_stringify(&key, &o);
+            sb_puts(&o, ":[");
+            for (int j = 0; j < st->n; j++) {
+                Seg *m = st->items[j];
+                char num[64];
+                snprintf(num, sizeof num, "%s{\"pos\":%ld,\"refType\":%d", j ? "," : "", seg_position_local(d, m), m->ref_type);
+                sb_puts(&o, num);
+                if (m->props) {
+                    sb_puts(&o, ",\"props\":");
+                    jv_stringify(m->props, &o);
+                }
+                sb_putc(&o, '}');
+            }
+            sb_putc(&o, ']');
+        }
+        sb_putc(&o, '}');
+        sb_putc(&o, 0);
+        res = o.p;
+        free(order);
+    }
+    for (int i = 0; i < n_labels; i++) free(rs.labels[i]);
+    free(rs.labels);
+    free(rs.llens);
+    rm_free(&rs.out);
+    return res;
+}
+
 /* ------------------------------------------------------------------ client */
 static int get_short_client_id(mto_doc *d, const char *long_id) {
     for (int i = 0; i < d->n_ids; i++)
@@ -1531,6 +1770,7 @@ void mto_free(mto_doc *d) {
         Block *n = b->all_next;
         tm_free(&b->rt);
         tm_free(&b->lt);
+        rm_free(&b->rs);
         free(b);
         b = n;
     }

@@ -19,6 +19,8 @@ for step in "$@"; do
     bench) run bench 900 python -u bench.py --steps 3 --warmup 1 ;;
     bench2) run bench2 600 python -u bench.py --config 2 --steps 3 --warmup 1 ;;
     bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
+    hbmphases) run hbmphases 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u tools/hbm_phases.py 100000 8 ;;
+    hbmrate) run hbmrate 600 python -u tools/hbm_phases.py 100000 8 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
@@ -39,6 +41,7 @@ for step in "$@"; do
     benchw2) run benchw2 600 python -u bench.py --config 2 --writers --steps 3 --warmup 1 ;;
     benchw3) run benchw3 900 python -u bench.py --config 3 --docs 8192 --writers --steps 2 --warmup 1 ;;
     bench2o) run bench2o 600 python -u bench.py --config 2 --steps 3 --warmup 1 --no-cpu ;;
+    bench3s_wpe4) run bench3s_wpe4 900 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_wpe4.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     bench3s) run bench3s 900 python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     writertests) run writertests 600 python -u -m pytest tests/test_gpu_writer.py tests/test_node_host.py -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     bench4s) run bench4s 600 python -u bench.py --config 4 --docs 4096 --ops 20000 --steps 1 --warmup 0 --no-cpu ;;

@@ -80,6 +80,8 @@ def lib():
     L.mto_find_tile.argtypes = [vp, i, cp, i, C.POINTER(C.c_void_p)]
     L.mto_find_tile.restype = l
     L.mto_free_string.argtypes = [vp]
+    L.mto_stack_context.argtypes = [vp, i, C.POINTER(cp), i, C.POINTER(i)]
+    L.mto_stack_context.restype = C.c_void_p
     L.mto_regenerate_pending_op_json.argtypes = [vp, cp, C.POINTER(C.c_void_p)]
     L.mto_regenerated_ops.argtypes = [vp, C.c_char_p, l]
     L.mto_regenerated_ops.restype = l
@@ -209,6 +211,22 @@ class Doc:
         if pos == -2:
             raise ValueError("unsupported tile labels")
         return None if pos < 0 else {"pos": pos, "props": props}
+
+    def stack_context(self, start_pos: int, labels) -> dict:
+        """MergeTree.getStackContext for the local client (client.ts:946-948): {label: [{"pos",
+        "refType"[, "props"]}, ...]} in JS key order; raises on a range label list the reference
+        could not iterate."""
+        import json as _json
+
+        arr = (C.c_char_p * max(1, len(labels)))(*[l.encode() for l in labels])
+        st = C.c_int(0)
+        p = self.L.mto_stack_context(self.h, start_pos, arr, len(labels), C.byref(st))
+        if not p:
+            raise ValueError("unsupported range labels")
+        try:
+            return _json.loads(C.string_at(p).decode(), object_pairs_hook=lambda kv: dict(kv))
+        finally:
+            self.L.mto_free_string(p)
 
     def length(self) -> int:
         return self.L.mto_get_length(self.h)

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parents[1]
 KATS = load_kats()
+GIANT, HBM = 2000000, 2097152  # mt_device.h kGiantSeg, kHbmSeg
 GEN_KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
 GEN_VALUES = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
 
@@ -448,9 +449,9 @@ def test_terminal_capacity_digests_are_defined():
     assert len(set(got[0].tolist())) == 8
 
 
-def test_segments_beyond_16_bit_lengths_move_to_the_hbm_class():
+def test_segments_beyond_16_bit_lengths_move_to_the_giant_class():
     """LDS classes keep segment lengths in 16 bits; a longer segment (one large insert, or zamboni
-    appending short inserts to a 65,530-unit run) re-runs the document from scratch in the HBM
+    appending short inserts to a 65,530-unit run) re-runs the document from scratch in the giant
     class with 32-bit lengths, bit-exact with the oracle."""
     big = "x" * 70000
     near = "y" * 65530
@@ -465,7 +466,7 @@ def test_segments_beyond_16_bit_lengths_move_to_the_hbm_class():
         b.ingest_messages(docs)
         b.run()
         classes = {li["seg_class"] for li in b.launches()}
-        assert 2097152 in classes, b.launches()
+        assert GIANT in classes, b.launches()
         for i in range(len(docs)):
             assert_doc_parity(b.doc(i), oracle[i])
         assert len(json.loads(b.doc(1).snapshot_v1()["header"])["segments"]) == 1  # merged past 65,535
@@ -473,8 +474,9 @@ def test_segments_beyond_16_bit_lengths_move_to_the_hbm_class():
 
 def test_giant_document_beyond_65k_segments():
     """A document far beyond the LDS classes and 16-bit ids (>= 100k live segments; SURVEY §8d
-    config 4's tail) escalates through the ladder into the HBM class (2M slots, 32-bit slot and
-    block ids, epoch-tagged overlay) and stays bit-exact with the oracle."""
+    config 4's tail) escalates through the ladder into the giant class (2M slots, 32-bit slot and
+    block ids, the top of the tree / overlay list / heap in the CU's LDS, the rest in HBM) and
+    stays bit-exact with the oracle."""
     p = O.gen_params(360000, pct_insert=50, pct_remove=15, seed=4096)  # 35% annotate: props keep segments apart
     ops, text, props, off = O.gen_batch(p, 1)
     t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
@@ -485,8 +487,8 @@ def test_giant_document_beyond_65k_segments():
         b.ingest(ops, off, text, props)
         b.run()
         c = b.counters()
-        hbm = [li for li in b.launches() if li["seg_class"] == 2097152]
-        print(f"max slots {int(c['max_slots'][0])}; HBM class: {hbm[0]['ops']} ops in {hbm[0]['ms']:.1f} ms = "
+        hbm = [li for li in b.launches() if li["seg_class"] == GIANT]
+        print(f"max slots {int(c['max_slots'][0])}; giant class: {hbm[0]['ops']} ops in {hbm[0]['ms']:.1f} ms = "
               f"{1e3 * hbm[0]['ms'] / max(1, hbm[0]['ops']):.2f} us/op")
         assert b.doc(0).status == st[0] == 0
         assert b.doc(0).digest() == int(dig[0])
@@ -495,6 +497,32 @@ def test_giant_document_beyond_65k_segments():
         od = O.replay_doc(ops.copy(), text, props, t, names)
         assert b.doc(0).get_text() == od.text()
         assert b.doc(0).snapshot_v1() == od.snapshot_v1()
+
+
+def test_wide_collab_window_passes_through_the_giant_class_to_the_hbm_class():
+    """A client that never advances its refSeq holds minSeq at 0, so every segment stays in the
+    overlay list: the list outgrows the LDS classes and the giant class's LDS list (kGiantUlist), and
+    the document continues in the HBM class (every table in HBM) — the checkpoint passes through
+    the giant class unchanged — bit-exact with the oracle."""
+    import random
+
+    rng = random.Random(11)
+    msgs = [_msg("B", 1, 0, {"type": 0, "pos1": 0, "seg": "start"})]
+    length = 5
+    for k in range(2, 3200):
+        pos = rng.randrange(length + 1)
+        msgs.append(_msg("A", k, k - 1, {"type": 0, "pos1": pos, "seg": "ab"}))
+        length += 2
+    docs = [msgs]
+    oracle = oracle_docs_from_messages(docs)
+    assert oracle[0].status == 0, oracle[0].error
+    with fa.ReplayBatch(1) as b:
+        b.ingest_messages(docs)
+        b.run()
+        classes = [li["seg_class"] for li in b.launches()]
+        assert GIANT in classes and HBM in classes, b.launches()
+        assert int(b.counters()["max_unsettled"][0]) > 2048
+        assert_doc_parity(b.doc(0), oracle[0])
 
 
 def test_combining_ops_match_oracle():

@@ -14,6 +14,7 @@ import pytest
 import oracle_ffi as O
 import fluidframework_amd as fa
 from writer_sim import farm, round_farm, writer_batch
+from test_gpu_parity import oracle_docs_from_messages
 
 pytestmark = pytest.mark.gpu
 
@@ -251,6 +252,91 @@ def test_find_tile_matches_oracle(mk):
                 for pos in range(0, n + 2):
                     for prec in (True, False):
                         assert dv.find_tile(pos, label, prec) == od.find_tile(pos, label, prec), (i, label, pos, prec)
+
+
+RANGE_QUERIES = (["row"], ["box", "row"], ["cell", "box", "row"], [])
+
+
+@pytest.mark.parametrize("mk", [lambda: round_farm(4, 30, 41, ranges=35), lambda: farm(5, 600, 42, ranges=30, markers=10)])
+def test_stack_context_matches_oracle(mk):
+    """Client.getStackContext (client.ts:946-948, mergeTree.ts:1750-1760) on every replica (writers
+    and observer) of farms with NestBegin / NestEnd markers carrying referenceRangeLabels: the
+    stacks the library rebuilds from the final table (leaves + the interior blocks each leaf block
+    closes) equal the oracle's block rangeStacks search at every position, for several label sets
+    (parity beyond beastTest's nesting check is unpinned: tests/test_oracle_ranges.py)."""
+    f = mk()
+    names = list(f.names)
+    docs = [f.events[n] for n in names]
+    with fa.ReplayBatch(len(docs) + 1) as b:
+        b.ingest_messages(docs + [list(f.log)], observer=names + ["readonly"])
+        b.run()
+        for i, od in enumerate([f.docs[n] for n in names] + [f.observer]):
+            dv = b.doc(i)
+            assert dv.digest() == od.digest()
+            for labels in RANGE_QUERIES:
+                for pos in range(0, od.length() + 2):
+                    assert dv.get_stack_context(pos, labels) == od.stack_context(pos, labels), (i, labels, pos)
+
+
+def test_stack_context_document_trees():
+    """beastTest.ts DocumentTree documents (rows / boxes / paragraphs, NestBegin / NestEnd markers):
+    replayed by an observer from the writer's sequenced messages, the GPU's getStackContext gives
+    the document's nesting at every text position (checkStacksAllPositions) and equals the
+    oracle everywhere; an annotate of referenceRangeLabels makes the query MT_UNSUPPORTED."""
+    import random
+
+    from test_oracle_ranges import DocTree, add_to_tree, check_stacks_all_positions, gen_content
+
+    class Rec:  # an oracle doc that records its local ops as sequenced messages of client "W"
+        def __init__(self):
+            self.d = O.Doc()
+            self.d.start_collab("W")
+            self.msgs = []
+
+        def local_op(self, op):
+            self.msgs.append({"clientId": "W", "sequenceNumber": len(self.msgs) + 1,
+                              "referenceSequenceNumber": len(self.msgs), "minimumSequenceNumber": len(self.msgs),
+                              "type": "op", "contents": op})
+            return self.d.local_op(op)
+
+        def __getattr__(self, k):
+            return getattr(self.d, k)
+
+    trees, logs = [], []
+    for seed in range(4):
+        rng = random.Random(100 + seed)
+        children = gen_content(rng, 0.6)
+        r = Rec()
+        st = {"pos": 0, "ids": {"box": 0, "row": 0}}
+        for c in children:
+            add_to_tree(r, c, st)
+        trees.append(children)
+        logs.append(r.msgs)
+    logs.append(logs[0] + [{"clientId": "W", "sequenceNumber": len(logs[0]) + 1, "referenceSequenceNumber": len(logs[0]),
+                            "minimumSequenceNumber": len(logs[0]), "type": "op",
+                            "contents": {"type": 2, "pos1": 0, "pos2": 1, "props": {"referenceRangeLabels": ["x"]}}}])
+    oracle = oracle_docs_from_messages(logs)
+    with fa.ReplayBatch(len(logs)) as b:
+        b.ingest_messages(logs)
+        b.run()
+        for i, children in enumerate(trees):
+            dv, od = b.doc(i), oracle[i]
+            assert dv.digest() == od.digest()
+            assert check_stacks_all_positions(_StackView(dv), children) == []
+            for labels in RANGE_QUERIES:
+                for pos in range(0, od.length() + 2):
+                    assert dv.get_stack_context(pos, labels) == od.stack_context(pos, labels), (i, labels, pos)
+        with pytest.raises(fa.MtError) as e:
+            b.doc(len(trees)).get_stack_context(0, ["row"])
+        assert e.value.code == fa.MT_UNSUPPORTED
+
+
+class _StackView:
+    def __init__(self, dv):
+        self.dv = dv
+
+    def stack_context(self, pos, labels):
+        return self.dv.get_stack_context(pos, labels)
 
 
 def test_regenerate_pending_ops_on_gpu():

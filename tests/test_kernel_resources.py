@@ -2,10 +2,11 @@
 by __graft_entry__.build()).
 
 The replay engine keeps every document's per-op control in registers; the class kernels run
-one wavefront per document and rely on 4 waves per SIMD (16 documents per CU, the config-2
-residency) — i.e. at most 128 VGPRs (512-entry register file / 4) — and must not spill to
-scratch.  A change that pushes a replay kernel past that silently halves residency (measured:
-22.3 ms -> 35 ms per config-2 launch), so it is pinned here."""
+one wavefront per document, and each class's kernel may use the registers its LDS residency leaves
+(16 documents per CU in the start class: 4 waves per SIMD, at most 128 VGPRs) and must not spill
+to scratch.  A change that pushes a replay kernel past its budget silently cuts residency
+(measured: 22.3 ms -> 35 ms per config-2 launch at 147 VGPRs in the 16-per-CU class), so it is
+pinned here."""
 import re
 import shutil
 import subprocess
@@ -38,15 +39,21 @@ def _kernels(notes: str) -> dict:
     return out
 
 
+# VGPR budget of each class's replay kernel: 512 / the waves per SIMD its LDS layout allows
+# (mt_device.h class_waves_per_eu: 16 documents per CU in class 363 -> 4 waves -> 128 VGPRs; 5 in
+# class 1376 -> 2 -> 256; 4 in class 1792 -> 1 -> 512)
+BUDGET = {363: 128, 423: 128, 1136: 256, 1376: 256, 1792: 512}
+
+
 @pytest.mark.skipif(not (LLVM / "llvm-readelf").exists() or not OBJ.exists(), reason="no build / ROCm llvm tools")
-@pytest.mark.parametrize("seg", [363, 423, 1136, 1376, 1792])
-def test_replay_kernel_fits_four_waves_per_simd(seg, tmp_path):
+@pytest.mark.parametrize("seg", sorted(BUDGET))
+def test_replay_kernel_fits_its_class_residency(seg, tmp_path):
     obj = OBJ / f"k{seg}.o"
     if not obj.exists():
         pytest.skip("class object not built")
     k = _kernels(_notes(obj, tmp_path))
     r = k[f"mt_replay_kernel_{seg}"]
-    assert r["vgpr_count"] <= 128, r
+    assert r["vgpr_count"] <= BUDGET[seg], r
     # no spill traffic: a real VGPR overflow spills hundreds of bytes and shows up as scratch
     # instructions; a few dwords of reserved (unused) private segment are tolerated
     assert r["private_segment_fixed_size"] <= 64, r
@@ -55,7 +62,7 @@ def test_replay_kernel_fits_four_waves_per_simd(seg, tmp_path):
     # the writer replay (local-client path) keeps the 4-waves-per-SIMD residency; its extra state
     # spills a few dwords (bounded here so growth is noticed)
     w = k[f"mt_writer_kernel_{seg}"]
-    assert w["vgpr_count"] <= 128, w
+    assert w["vgpr_count"] <= BUDGET[seg], w
     assert w["private_segment_fixed_size"] <= 512, w
 
 

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node
 
 FUNCS = {"createBatch", "setTables", "setClients", "ingest", "generate", "run", "runAsync", "docStatus", "docText",
          "docPropsRuns", "docSnapshotV1", "docDigest", "deviceDigests", "stats", "statusString", "ingestJson",
-         "docFindTile", "docRegeneratedOps"}
+         "docFindTile", "docRegeneratedOps", "docStackContext"}
 
 
 def _node(code):

@@ -34,13 +34,20 @@ def local_message(client: str, op: dict, ref: int) -> dict:
 
 
 TILE_LABELS = ("pg", "EOP", "cell")
+RANGE_LABELS = ("row", "box", "cell")
 
 
 def random_op(rng: random.Random, length: int, n_keys: int = 4, p_annotate: int = 15, p_remove: int = 30,
-              max_insert: int = 6, rewrite: int = 0, markers: int = 0) -> dict:
+              max_insert: int = 6, rewrite: int = 0, markers: int = 0, ranges: int = 0) -> dict:
     """An op drawn from a replica's local view (length = its getLength()).  markers: percentage of
-    inserts that are Tile / plain markers carrying referenceTileLabels."""
+    inserts that are Tile / plain markers carrying referenceTileLabels; ranges: percentage that are
+    NestBegin / NestEnd markers carrying referenceRangeLabels."""
     u = rng.randrange(100)
+    if ranges and (length == 0 or u >= p_annotate + p_remove) and rng.randrange(100) < ranges:
+        labels = rng.sample(RANGE_LABELS, 1 + rng.randrange(2))
+        return {"type": 0, "pos1": rng.randrange(length + 1),
+                "seg": {"marker": {"refType": rng.choice((2, 2, 4, 4, 3, 5, 6))},
+                        "props": {"referenceRangeLabels": labels}}}
     if markers and (length == 0 or u >= p_annotate + p_remove) and rng.randrange(100) < markers:
         labels = rng.sample(TILE_LABELS, 1 + rng.randrange(2))
         return {"type": 0, "pos1": rng.randrange(length + 1),
