@@ -170,10 +170,11 @@ constexpr bool is_giant_seg(int seg) { return seg == kGiantSeg; }
 // kGiantLdsLevel (0 = leaf blocks); lower levels (and high ones once the LDS ids run out) take
 // HBM ids [kGiantLdsBlocks, cap.blk).  The overlay list and the heap have LDS capacities: a
 // document short of them checkpoints into the HBM class.
-constexpr int kGiantLdsBlocks = 2560;
+constexpr int kGiantLdsBlocks = 2304;
 constexpr int kGiantLdsLevel = 3;
 constexpr int kGiantHeap = 1024;
-constexpr int kGiantUlist = 2048;
+constexpr int kGiantUlist = 1024;
+constexpr int kGiantChainRec = 4;  // HBM-resident blocks recorded per overlay list entry
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS class (16-bit lengths)
 
@@ -285,7 +286,8 @@ constexpr Layout make_glayout() {
     L.bslen = o;   o = lds_align(o + 4u * K);
     L.bacc = o;    o = lds_align(o + 4u * K);
     L.bep = o;     o = lds_align(o + 4u * K);
-    L.len = L.sr = L.meta = L.sblk = o;  // in HBM (make_layout)
+    L.sr = o;      o = lds_align(o + 4u * kGiantChainRec * kGiantUlist);  // the overlay's chain records
+    L.len = L.meta = L.sblk = o;  // in HBM (make_layout)
     L.bytes = o;
     return L;
 }

@@ -143,16 +143,43 @@ struct LWord {
 };
 
 // A block table.  In the giant class block ids [0, kGiantLdsBlocks) live in the CU's LDS (the
-// interior blocks near the root) and the rest in HBM: an access selects the base by id, so the
-// engine code is the same for both (flat loads / stores).  Every other class has one base.
-// kShift: log2 of the entries per block (b_child: 8).
+// interior blocks near the root) and the rest in HBM: an access branches on the id to an LDS
+// (ds_*) or a global (global_*) instruction — the pointers carry their address spaces, so no flat
+// access (which would make every LDS access wait for the wave's outstanding HBM traffic).  Every
+// other class has one base.  kShift: log2 of the entries per block (b_child: 8).
+#define MT_AS_LDS __attribute__((address_space(3)))
+#define MT_AS_GLOBAL __attribute__((address_space(1)))
 template <typename T, int kShift, bool kSplit>
-struct BArr {
-    T *lds;  // kSplit: entries of the LDS-resident ids
-    T *p;    // the table (giant class: indexed by the full id, ids below kGiantLdsBlocks unused)
-    MT_FI T &operator[](uint32_t i) const {
-        if constexpr (kSplit) return (i >> kShift) < (uint32_t)kGiantLdsBlocks ? lds[i] : p[i];
-        return p[i];
+struct BArr;
+template <typename T, int kShift>
+struct BArr<T, kShift, false> {
+    T *p;
+    MT_FI T &operator[](uint32_t i) const { return p[i]; }
+    MT_FI void add(uint32_t i, T v) const { __hip_atomic_fetch_add(&p[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
+};
+template <typename T, int kShift>
+struct BArr<T, kShift, true> {
+    MT_AS_LDS T *lds;   // entries of the LDS-resident ids
+    MT_AS_GLOBAL T *p;  // the HBM table, indexed by the full id (ids below kGiantLdsBlocks unused)
+    MT_FI static bool in_lds(uint32_t i) { return (i >> kShift) < (uint32_t)kGiantLdsBlocks; }
+    struct Ref {
+        const BArr &a;
+        uint32_t i;
+        MT_FI operator T() const {
+            if (in_lds(i)) return a.lds[i];
+            return a.p[i];
+        }
+        MT_FI Ref &operator=(T v) {
+            if (in_lds(i)) a.lds[i] = v;
+            else a.p[i] = v;
+            return *this;
+        }
+        MT_FI Ref &operator=(const Ref &o) { return *this = (T)o; }
+    };
+    MT_FI Ref operator[](uint32_t i) const { return Ref{*this, i}; }
+    MT_FI void add(uint32_t i, T v) const {
+        if (in_lds(i)) __hip_atomic_fetch_add(&lds[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        else __hip_atomic_fetch_add(&p[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 };
 
@@ -186,6 +213,11 @@ struct Engine {
     BA<uint32_t> b_slen, b_acc;
     BA<uint32_t> b_ep;   // HBM / giant class: the overlay epoch that last wrote b_acc[B] (no O(blocks) clear)
     uint32_t ov_epoch;
+    // giant class: the HBM-resident blocks the last overlay added into (kGiantChainRec per overlay
+    // list entry, kNoBlk-padded); their b_acc is zeroed before the next overlay, so HBM b_acc needs
+    // no epoch tags (a zero invariant between overlays) and the adds are fire-and-forget atomics
+    uint32_t *g_rec;
+    int32_t g_nrec;
     uint32_t *scratch;  // 128 words
     // ---- uniform scalars
     int32_t slot_top, free_head, free_n, blk_top, n_bfree, bfree_head, root, depth, hn, nu;
@@ -244,26 +276,27 @@ struct Engine {
         uint8_t *xb = kGiant ? lb : tb;  // the per-op state: in LDS for the giant class
         const Layout &xl = kGiant ? glay : lay;
         u_list = (Idx *)(xb + xl.ulist);
-        b_parent.p = (Idx *)(tb + lay.bparent);
-        b_child.p = (Idx *)(tb + lay.bchild);
-        b_count.p = (uint8_t *)(tb + lay.bcount);
-        b_leaf.p = (uint8_t *)(tb + lay.bleaf);
-        b_scour.p = (int8_t *)(tb + lay.bscour);
-        b_slen.p = (uint32_t *)(tb + lay.bslen);
-        b_acc.p = (uint32_t *)(tb + lay.bacc);
-        b_ep.p = (uint32_t *)(tb + lay.bep);
+        b_parent.p = (decltype(b_parent.p))(tb + lay.bparent);
+        b_child.p = (decltype(b_child.p))(tb + lay.bchild);
+        b_count.p = (decltype(b_count.p))(tb + lay.bcount);
+        b_leaf.p = (decltype(b_leaf.p))(tb + lay.bleaf);
+        b_scour.p = (decltype(b_scour.p))(tb + lay.bscour);
+        b_slen.p = (decltype(b_slen.p))(tb + lay.bslen);
+        b_acc.p = (decltype(b_acc.p))(tb + lay.bacc);
+        b_ep.p = (decltype(b_ep.p))(tb + lay.bep);
         if constexpr (kGiant) {
-            b_parent.lds = (Idx *)(lb + glay.bparent);
-            b_child.lds = (Idx *)(lb + glay.bchild);
-            b_count.lds = (uint8_t *)(lb + glay.bcount);
-            b_leaf.lds = (uint8_t *)(lb + glay.bleaf);
-            b_scour.lds = (int8_t *)(lb + glay.bscour);
-            b_slen.lds = (uint32_t *)(lb + glay.bslen);
-            b_acc.lds = (uint32_t *)(lb + glay.bacc);
-            b_ep.lds = (uint32_t *)(lb + glay.bep);
+            b_parent.lds = (MT_AS_LDS Idx *)(lb + glay.bparent);
+            b_child.lds = (MT_AS_LDS Idx *)(lb + glay.bchild);
+            b_count.lds = (MT_AS_LDS uint8_t *)(lb + glay.bcount);
+            b_leaf.lds = (MT_AS_LDS uint8_t *)(lb + glay.bleaf);
+            b_scour.lds = (MT_AS_LDS int8_t *)(lb + glay.bscour);
+            b_slen.lds = (MT_AS_LDS uint32_t *)(lb + glay.bslen);
+            b_acc.lds = (MT_AS_LDS uint32_t *)(lb + glay.bacc);
+            b_ep.lds = (MT_AS_LDS uint32_t *)(lb + glay.bep);
         }
         h_ent = (uint2 *)(xb + xl.heap);
         scratch = (uint32_t *)(xb + xl.scratch);
+        if constexpr (kGiant) g_rec = (uint32_t *)(lb + glay.sr);  // make_glayout: the chain records
         uint32_t *hw = (uint32_t *)(xb + xl.hdr);
         pay_end.p = hw + 0;
         arena_base.p = hw + 1;
@@ -464,7 +497,7 @@ struct Engine {
     MT_FI void chain_add(Arr &arr, bool act, uint32_t b, uint32_t v) {
         for (int32_t l = 0; l < depth; l++) {
             if (act && b != kNoBlk) {
-                lds_add(&arr[b], v);
+                arr.add(b, v);
                 b = b_parent[b];
             }
         }
@@ -501,14 +534,127 @@ struct Engine {
     }
     MT_FI void clear_epochs() {
         ov_epoch = 0;
-        if constexpr (kHbm) {  // once per launch: the tables are uninitialised device memory
+        if constexpr (kGiant) {  // once per launch: LDS epochs, and the zero invariant of HBM b_acc
+            for (int32_t i = lane; i < kGiantLdsBlocks; i += kWave) b_ep.lds[i] = 0xFFFFFFFFu;
+            g_nrec = 0;
+            giant_clear_acc(true);
+        } else if constexpr (kHbm) {  // once per launch: the tables are uninitialised device memory
             for (int32_t i = lane; i < cap.blk; i += kWave) b_ep[i] = 0xFFFFFFFFu;
             wsync();
         }
     }
     MT_FI uint32_t ov_acc(uint32_t b) const {
+        if constexpr (kGiant) {
+            if (b < (uint32_t)kGiantLdsBlocks) return b_ep.lds[b] == ov_epoch ? b_acc.lds[b] : 0u;
+            return b_acc.p[b];  // zero unless the current overlay added into it
+        }
         if constexpr (kHbm) return b_ep[b] == ov_epoch ? b_acc[b] : 0u;
         return b_acc[b];
+    }
+    // giant class: zero the HBM b_acc entries the last overlay wrote (and every one, once per
+    // launch, when `all`: the tables are uninitialised device memory)
+    MT_FI void giant_clear_acc(bool all) {
+        if (all) {
+            for (int32_t i = kGiantLdsBlocks + lane; i < cap.blk; i += kWave) b_acc.p[i] = 0u;
+        } else {
+            for (int32_t i = lane; i < g_nrec; i += kWave) {
+                const uint32_t r = g_rec[i];
+                if (r != kNoBlk) b_acc.p[r] = 0u;
+            }
+        }
+        g_nrec = 0;
+        wsync();
+    }
+
+    // giant class: the overlay of up to 4 x 64 list entries at once (their HBM loads — fields, leaf
+    // block, parents — overlap); LDS-resident blocks accumulate in LDS (epoch-tagged), HBM ones with
+    // fire-and-forget atomics on a zeroed b_acc, recorded for the next clear
+
+    MT_FI void overlay_giant(int32_t ref, uint32_t c) {
+        giant_clear_acc(false);
+        ov_epoch++;
+        ov_full = ref < min_seq;
+        if (ov_full) {  // a view below minSeq (outside valid logs): every segment — the HBM class
+            cap_fail(1);
+            return;
+        }
+        int32_t w = 0;
+        for (int32_t g0 = 0; g0 < nu; g0 += 4 * kWave) {
+            uint32_t slot[4], vlen[4], b[4], nh[4];
+            bool act[4];
+            int32_t wk[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int32_t j = g0 + k * kWave + lane;
+                slot[k] = j < nu ? (uint32_t)u_list[j] : 0xFFFFFFFFu;
+            }
+            uint32_t meta[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) meta[k] = slot[k] != 0xFFFFFFFFu ? s_meta[slot[k]] : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool valid = (meta[k] & kMetaUnsettled) && (meta[k] & kMetaLinked);
+                const uint64_t vm = ballot(valid);
+                wk[k] = valid ? w + __popcll(vm & ((1ull << lane) - 1ull)) : -1;
+                w += __popcll(vm);
+                act[k] = valid;
+            }
+            wsync();  // every read of this group's list entries is done: compact in place
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (act[k]) u_list[wk[k]] = (Idx)slot[k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                vlen[k] = 0;
+                b[k] = kNoBlk;
+                nh[k] = 0;
+                if (act[k]) {
+                    bool tie;
+                    view_of(slot[k], ref, c, vlen[k], tie);
+                    b[k] = s_blk[slot[k]];
+                }
+                act[k] = act[k] && vlen[k] > 0u;
+            }
+            for (int32_t l = 0; l < depth; l++) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (!act[k] || b[k] == kNoBlk) continue;
+                    if (b[k] < (uint32_t)kGiantLdsBlocks) {
+                        if (b_ep.lds[b[k]] != ov_epoch) {
+                            b_acc.lds[b[k]] = 0u;
+                            b_ep.lds[b[k]] = ov_epoch;
+                        }
+                    }
+                }
+                wsync();
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (!act[k] || b[k] == kNoBlk) continue;
+                    if (b[k] < (uint32_t)kGiantLdsBlocks) {
+                        __hip_atomic_fetch_add(&b_acc.lds[b[k]], vlen[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    } else {
+                        __hip_atomic_fetch_add(&b_acc.p[b[k]], vlen[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        if (nh[k] < (uint32_t)kGiantChainRec) g_rec[wk[k] * kGiantChainRec + nh[k]] = b[k];
+                        nh[k]++;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (act[k] && b[k] != kNoBlk) b[k] = b_parent[b[k]];
+            }
+            bool over = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (wk[k] >= 0)
+                    for (uint32_t q = act[k] ? nh[k] : 0u; q < (uint32_t)kGiantChainRec; q++) g_rec[wk[k] * kGiantChainRec + q] = kNoBlk;
+                over |= act[k] && nh[k] > (uint32_t)kGiantChainRec;
+            }
+            if (ballot(over)) cap_fail(1);  // more HBM blocks on a chain than recorded: the HBM class
+        }
+        nu = w;
+        g_nrec = w * kGiantChainRec;
+        ov_splits = splits;
+        wsync();
     }
 
     MT_FI void u_push(uint32_t slot) {
@@ -525,6 +671,10 @@ struct Engine {
     // B (or over all segments in full mode).  Also drops stale list entries.
     MT_FI void overlay(int32_t ref, uint32_t c) {
         PF_SCOPE(6);
+        if constexpr (kGiant) {
+            overlay_giant(ref, c);
+            return;
+        }
         wsync();
         if constexpr (kHbm) {
             ov_epoch++;  // blocks of other epochs read as 0 (giant documents: ~10^5 blocks)
@@ -635,8 +785,68 @@ struct Engine {
     // block the first leaf with pos < len or the leaf tie rule, else the block end.
     // strict mode (nodeMap's start < len, mergeTree.ts:2903-2965): first child whose cumulative
     // length exceeds pos; returns only the leaf block and its start position.
+    // giant class: the same walk with every child's row and count loaded in the round that loads
+    // the children's lengths (lane i: row entry i & 7 of child i >> 3), so an HBM level costs one
+    // dependent round trip instead of two; the chosen child's row moves to lanes 0-7 by a permute
+    MT_FI Walk descend_giant(uint32_t pos, int32_t ref, uint32_t c, bool strict) {
+        Walk W;
+        W.blk = -1;
+        W.k = 0;
+        W.n = 0;
+        W.base = 0;
+        W.excl = 0;
+        W.ok = 0;
+        int32_t N = root;
+        uint32_t base = 0;
+        const bool lanes8 = lane < kMaxNodes;
+        int32_t n = b_count[N];
+        uint32_t row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;
+        for (int32_t l = 0; l + 1 < depth; l++) {
+            const uint32_t myc = (uint32_t)__shfl((int)row, lane >> 3, kWave);
+            const bool cin = (lane >> 3) < n;
+            const uint32_t nrow = cin ? (uint32_t)b_child[myc * 8 + (lane & 7)] : 0u;
+            uint32_t v = 0, cnt = 0;
+            if (lane < n) {
+                v = ov_acc(row) + (ov_full ? 0u : b_slen[row]);
+                cnt = b_count[row];
+            }
+            const uint32_t incl = scan8(v) + base;
+            const uint64_t hb = ballot(lanes8 && lane < n && (strict ? incl > pos : incl >= pos));
+            if (!hb) return W;
+            const int f = first_lane(hb);
+            base = rdl(incl - v, f);
+            N = (int32_t)rdl(row, f);
+            n = (int32_t)rdl(cnt, f);
+            row = (uint32_t)__shfl((int)nrow, 8 * f + (lane & 7), kWave);
+            if (!lanes8) row = 0u;
+        }
+        W.blk = N;
+        W.n = n;
+        W.base = base;
+        if (strict) return W;
+        uint32_t vlen = 0;
+        bool tie = false;
+        if (lane < n) view_of(row, ref, c, vlen, tie);
+        const uint32_t incl = scan8(vlen) + base;
+        const uint32_t excl = incl - vlen;
+        const uint64_t cb = ballot(lanes8 && lane < n && (incl > pos || (excl == pos && vlen == 0u && tie)));
+        if (cb) {
+            const int f = first_lane(cb);
+            W.k = f;
+            W.excl = rdl(excl, f);
+            W.ok = 1;
+        } else {
+            const uint32_t end = n > 0 ? rdl(incl, n - 1) : base;
+            W.k = n;
+            W.excl = end;
+            W.ok = end == pos;
+        }
+        return W;
+    }
+
     MT_FI Walk descend(uint32_t pos, int32_t ref, uint32_t c, bool strict) {
         PF_SCOPE(1);
+        if constexpr (kGiant) return descend_giant(pos, ref, c, strict);
         Walk W;
         W.blk = -1;
         W.k = 0;
@@ -1895,7 +2105,7 @@ struct Engine {
             }
         }
         wsync();
-        if (in && sl) lds_add(&b_slen[nb], sl);
+        if (in && sl) b_slen.add(nb, sl);
         b_count[parent] = (uint8_t)cc;
         splits++;  // structure changed under the overlay
         wsync();
@@ -2914,8 +3124,8 @@ struct Engine {
         const uint32_t *ic = img + n;       // b_child rows
         const uint32_t *ik = img + 9 * n;   // count | leaf << 8 | scour << 16
         const uint32_t *is = img + 10 * n;  // b_slen (settled lengths)
-        uint32_t *tlev = b_ep.p + kGiantLdsBlocks;
-        uint32_t *tmap = b_acc.p + kGiantLdsBlocks;
+        MT_AS_GLOBAL uint32_t *tlev = b_ep.p + kGiantLdsBlocks;
+        MT_AS_GLOBAL uint32_t *tmap = b_acc.p + kGiantLdsBlocks;
         constexpr uint32_t kFree = 0xFFFFFFFFu;
         for (int32_t i = lane; i < n; i += kWave) tlev[i] = 0u;
         wsync();
