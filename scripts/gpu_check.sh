@@ -20,6 +20,7 @@ for step in "$@"; do
     bench2) run bench2 600 python -u bench.py --config 2 --steps 3 --warmup 1 ;;
     bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
     gianttests) run gianttests 600 python -u -m pytest tests/test_gpu_parity.py -k "giant or 16_bit or wide_collab or hbm_class or escalation" -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    giant1m) run giant1m 600 python -u -m pytest tests/test_gpu_parity.py -k "million_segments" -x -v -s --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     hbmphases) run hbmphases 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u tools/hbm_phases.py 100000 8 ;;
     hbmrate) run hbmrate 600 python -u tools/hbm_phases.py 100000 8 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;

@@ -499,6 +499,36 @@ def test_giant_document_beyond_65k_segments():
         assert b.doc(0).snapshot_v1() == od.snapshot_v1()
 
 
+def test_config4_largest_document_beyond_a_million_segments():
+    """BASELINE configs[3]'s largest Zipf document at full size: 2M ops of the config-4 mix (insert 50 /
+    remove 15 / annotate 35, so props keep neighbouring segments apart), generated on the GPU, grows
+    past 1,000,000 segment slots (about a million live segments at the end), escalates through the
+    LDS ladder into the giant class and replays bit-exact with the oracle on the downloaded log:
+    state digest, text and SnapshotV1.  Prints the giant class's microseconds per op."""
+    n_ops = 2000000
+    with fa.ReplayBatch(1) as b:
+        b.generate(fa.gen_params(n_ops, pct_insert=50, pct_remove=15, seed=4096), 0)
+        ops, off, text, props = b.download_log()
+        print("generated", flush=True)
+        b.run()
+        print("replayed", flush=True)
+        c = b.counters()
+        giant = [li for li in b.launches() if li["seg_class"] == GIANT]
+        print(f"max slots {int(c['max_slots'][0])}, out entries {int(c['n_entries'][0])}, depth {int(c['depth'][0])}; "
+              f"giant class: {giant[0]['ops']} ops in {giant[0]['ms']:.1f} ms = "
+              f"{1e3 * giant[0]['ms'] / max(1, giant[0]['ops']):.2f} us/op; launches "
+              f"{[(li['seg_class'], round(li['ms'], 1)) for li in b.launches()]}", flush=True)
+        assert b.doc(0).status == 0
+        assert giant and giant[0]["ops"] > n_ops // 2
+        assert int(c["max_slots"][0]) >= 1000000, int(c["max_slots"][0])
+        od = O.replay_doc(ops.copy(), text, props, O.gen_tables(), O.gen_client_names(8))
+        assert od.status == 0
+        dv = b.doc(0)
+        assert dv.digest() == od.digest()
+        assert dv.get_text() == od.text()
+        assert dv.snapshot_v1() == od.snapshot_v1()
+
+
 def test_wide_collab_window_passes_through_the_giant_class_to_the_hbm_class():
     """A client that never advances its refSeq holds minSeq at 0, so every segment stays in the
     overlay list: the list outgrows the LDS classes and the giant class's LDS list (kGiantUlist), and
