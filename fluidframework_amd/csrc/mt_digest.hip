@@ -8,6 +8,7 @@
 // is identical for a document whichever rank / launch / capacity class replayed it.
 #include <hip/hip_runtime.h>
 
+#include "../../include/mt_oplog.h"
 #include "mt_device.h"
 
 namespace mt {
@@ -25,6 +26,19 @@ __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
     return h * 0x100000001B3ull;
 }
 
+
+// the client ids and the Marker bit as one word: clientId | removedClientId << 8 | Marker << 16 in
+// the 8-bit encoding of the first engines (254 NonCollabClient, 255 none) for ids below 254, so the
+// digests of such documents are unchanged; the ids from 254 on add their high bits above bit 16
+__device__ __forceinline__ uint32_t id_enc(uint32_t id) {
+    if (id == MT_CLIENT_NONCOLLAB) return 254u;
+    if (id == kNoClient) return 255u;
+    return id < 254u ? id : ((id & 0xFFu) | 0x100u | ((id >> 8) << 9));
+}
+__device__ __forceinline__ uint32_t id_word(uint32_t cli, uint32_t rcli, bool marker) {
+    const uint32_t a = id_enc(cli), b = id_enc(rcli);
+    return (a & 0xFFu) | ((b & 0xFFu) << 8) | (marker ? 1u << 16 : 0u) | ((a >> 8) << 17) | ((b >> 8) << 22);
+}
 
 extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P) {
     const int64_t w = blockIdx.x;
@@ -48,7 +62,7 @@ extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P
             h = fnv(h, r.len);
             h = fnv(h, (uint32_t)r.seq);
             h = fnv(h, (uint32_t)r.rseq);
-            h = fnv(h, r.meta & (kMetaCli | (kMetaCli << kMetaRcliShift) | kMetaMarker));  // client ids, Marker
+            h = fnv(h, id_word(meta_cli(r.meta), meta_rcli(r.meta), (r.meta & kMetaMarker) != 0u));  // client ids, Marker
             // removedClientOverlap as a set (mask of clients < 31, or a pool list)
             uint64_t ov = 0;
             if (r.ovl & kOvlList) {

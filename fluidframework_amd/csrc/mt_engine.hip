@@ -3509,8 +3509,8 @@ MT_FI void generate_body(const ReplayParams &P) {
         if ((int32_t)len < g.min_len || (int32_t)u < g.pct_insert) type = MT_OP_INSERT;
         else if ((int32_t)u < g.pct_insert + g.pct_remove) type = MT_OP_REMOVE;
         else type = MT_OP_ANNOTATE;
-        op.type = (uint8_t)type;
-        op.client = (uint8_t)c;
+        op.type = (uint16_t)type;
+        op.client = (uint16_t)c;
         op.flags = 0;
         op.ref_seq = ref;
         op.msn = msn;

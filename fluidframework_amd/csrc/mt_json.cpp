@@ -456,7 +456,7 @@ struct LocalDoc {
     std::unordered_map<std::u16string, uint32_t> key_ids;
     std::unordered_map<std::string, uint32_t> value_ids;
     std::vector<std::u16string> names;
-    std::unordered_map<std::u16string, uint8_t> shortid;
+    std::unordered_map<std::u16string, uint16_t> shortid;
     int status = MT_OK;
     std::string err;
 };
@@ -652,8 +652,8 @@ struct Packer1 {
     int client_id(const std::u16string &name) {
         auto it = L.shortid.find(name);
         if (it != L.shortid.end()) return it->second;
-        if (L.names.size() >= MT_MAX_CLIENTS) return -1;  // 254, 255 are MT_CLIENT_NONCOLLAB / MT_CLIENT_NONE
-        const uint8_t c = (uint8_t)L.names.size();
+        if (L.names.size() >= MT_MAX_CLIENTS) return -1;  // 4094, 4095 are MT_CLIENT_NONCOLLAB / MT_CLIENT_NONE
+        const uint16_t c = (uint16_t)L.names.size();
         L.shortid.emplace(name, c);
         L.names.push_back(name);
         return c;
@@ -665,7 +665,7 @@ struct Packer1 {
         r.type = type;
         r.ref_seq = MT_SEQ_NONE;
         r.msn = (int32_t)MT_CLIENT_NONE;
-        r.client = (uint8_t)MT_CLIENT_NONCOLLAB;
+        r.client = MT_CLIENT_NONCOLLAB;
         const int32_t json = D.nodes[spec].type == J_OBJ ? D.member(spec, "json") : -1;
         int32_t seg = spec;
         if (json >= 0) {  // hasMergeInfo
@@ -675,15 +675,15 @@ struct Packer1 {
             if (cl >= 0) {
                 if (D.nodes[cl].type != J_STR) return fail(MT_BAD_INPUT, "client is not a string");
                 const int c = client_id(D.str_of(cl));
-                if (c < 0) return fail(MT_UNSUPPORTED, "more than 253 clients");
-                r.client = (uint8_t)c;
+                if (c < 0) return fail(MT_UNSUPPORTED, "more than 4093 clients");
+                r.client = (uint16_t)c;
             }
             if (sq >= 0) r.seq = as_int(D.nodes[sq]);
             if (rs >= 0) r.ref_seq = as_int(D.nodes[rs]);
             if (rc >= 0) {
                 if (D.nodes[rc].type != J_STR) return fail(MT_BAD_INPUT, "removedClient is not a string");
                 const int c = client_id(D.str_of(rc));
-                if (c < 0) return fail(MT_UNSUPPORTED, "more than 253 clients");
+                if (c < 0) return fail(MT_UNSUPPORTED, "more than 4093 clients");
                 r.msn = c;
             }
         }
@@ -817,8 +817,8 @@ struct Packer1 {
             const int32_t cid = D.member(m, "clientId");
             std::u16string name = cid >= 0 && D.nodes[cid].type == J_STR ? D.str_of(cid) : u"null";
             const int ci = client_id(name);
-            if (ci < 0) return fail(MT_UNSUPPORTED, "more than 253 clients");
-            const uint8_t c = (uint8_t)ci;
+            if (ci < 0) return fail(MT_UNSUPPORTED, "more than 4093 clients");
+            const uint16_t c = (uint16_t)ci;
             mt_op base{};
             base.client = c;
             const int32_t sq = D.member(m, "sequenceNumber"), rs = D.member(m, "referenceSequenceNumber"),
@@ -933,6 +933,17 @@ std::u16string from_utf8(const char *s) {
 namespace mt {
 void json_quote(std::string &o, const char16_t *s, size_t n) { quote(o, s, n); }
 void json_number(std::string &o, double v) { js_number(o, v); }
+bool json_canonical_value(const char *p, size_t n, std::string &out) {
+    Dom D;
+    D.p = p;
+    D.end = p + n;
+    const int32_t v = D.value(0);
+    D.ws();
+    if (v < 0 || D.p != D.end) return false;
+    out.clear();
+    js_stringify(D, v, out);
+    return true;
+}
 }  // namespace mt
 
 struct mt_packed {

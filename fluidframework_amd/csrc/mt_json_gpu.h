@@ -7,7 +7,7 @@
 // marker), remove, annotate (no combiningOp or rewrite), relative positions, or a one-level GROUP
 // of those, property values that are null / true / false / canonical integers / plain ASCII
 // strings / flat arrays of those in JSON.stringify form.  Anything else (writer replicas,
-// snapshots, escapes in keys or values, floats, objects as values, duplicate keys, > 253
+// snapshots, escapes in keys or values, floats, objects as values, duplicate keys, > 4093
 // clients, malformed JSON) is reported as "host parser needed"
 // (MT_UNSUPPORTED + the first such document): the caller runs mt_pack_json for that batch.
 #ifndef MT_JSON_GPU_H
@@ -23,6 +23,11 @@
 struct mt_packed;
 
 namespace mt {
+// JSON.stringify(JSON.parse(text)) of one JSON value with the host parser's JS semantics
+// (mt_json.cpp: Number::toString, JS key order, duplicate keys, lone surrogates); false when
+// [p, p + n) is not exactly one JSON value (surrounding whitespace allowed)
+bool json_canonical_value(const char *p, size_t n, std::string &out);
+
 namespace jg {
 
 struct Result {

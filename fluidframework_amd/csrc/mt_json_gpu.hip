@@ -42,8 +42,12 @@ namespace mt {
 namespace jg {
 
 constexpr uint32_t kNullSpan = 0xFFFFFFFFu;
+// on a prop value's span length: the source text is valid JSON but not in JSON.stringify form (a
+// float, an object, a nested array, whitespace, other string escapes); the host interns
+// JSON.stringify(JSON.parse(text)) for it (mt::json_canonical_value), so the tables stay the host
+// parser's and only the few unique values per document are formatted on the CPU
+constexpr uint32_t kSpanCanon = 0x80000000u;
 constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // mt_device.h: a RELPOS key the host cannot resolve
-constexpr int kClientSlots = 512;  // per-document client hash table (<= 253 distinct names)
 constexpr int kMaxProps = 16;      // keys per props object on the fast path
 
 // reasons a document leaves the fast path (Result::fail_bits)
@@ -52,7 +56,7 @@ enum : uint32_t {
     kFShape = 2,    // a message / op shape outside the fast path (markers, escapes, floats ...)
     kFRange = 4,    // an integer outside int32
     kFWriter = 8,   // a writer replica's log (local ops / own acks)
-    kFClients = 16, // more than 253 clients
+    kFClients = 16, // more than 4093 clients
     kFCap = 32      // more messages than the scan's per-document region holds
 };
 
@@ -78,9 +82,12 @@ struct Params {
     int32_t *sg_d0, *sg_d1;
     // per document
     uint32_t *d_nmsg, *d_fail, *d_nrec, *d_ntext, *d_nprop, *d_npropops, *d_nnames, *d_nuk, *d_nuv, *d_nval;
-    uint32_t *cl_ht;                 // kClientSlots per document
+    uint32_t *cl_ht;                 // per document cl_cap[d] slots from cl_base[d] (2 x its names + 1, a power of 2)
+    const uint64_t *cl_base;
+    const uint32_t *cl_cap;
+    const uint64_t *names_base;      // per document: first word of its names in `names`
     uint32_t *nm_off, *nm_len;       // per message region: client id k's span at index k - 1
-    uint32_t *names;                 // per document 256 x {off, len}: ids 1.. (compact, for the host)
+    uint32_t *names;                 // per document {off, len} of ids 1.. (compacted by jg_names_kernel)
     const uint8_t *obs;              // observer long id (UTF-8) + "null" at obs + 256
     uint32_t obs_len;
     // write
@@ -725,7 +732,7 @@ struct Ctx {  // write pass
     uint32_t gprop = 0;         // batch-global index of this message's first prop record
     uint32_t gval = 0;          // batch-global index of this message's first value event
     uint32_t *pk_off, *pk_len, *pv_off, *pv_len, *pe;  // keys per prop record, values per event
-    uint8_t cid = 0;
+    uint16_t cid = 0;
     bool install = false;
 };
 
@@ -901,19 +908,23 @@ __host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, uint3
             uint32_t so, sl;
             bool pl;
             if (!str_raw(r, so, sl, pl)) return kFSyntax;
-            if (!pl && !str_canonical(r, so, sl)) return kFShape;
             vl = sl + 2;  // a string already in JSON.stringify form: its source text
+            if (!pl && !str_canonical(r, so, sl)) vl |= kSpanCanon;  // other escapes: the host re-quotes
         } else if (c == '-' || is_digit(c)) {
             int64_t v;
             uint32_t nd;
             const int t = num_tok(r, v, nd);
-            if (t != 1) return t ? kFShape : kFSyntax;
-            if (nd > 15) return kFShape;  // Number::toString keeps <= 15 digits exactly
+            if (!t) return kFSyntax;
             vl = r.p - vo;
+            // a fraction / exponent, or more digits than Number::toString keeps exactly: the host
+            // formats the double (shortest round trip)
+            if (t != 1 || nd > 15) vl |= kSpanCanon;
         } else if (c == '[') {
             // a flat array already in JSON.stringify form (no whitespace, canonical elements:
-            // what a log written by JSON.stringify holds, e.g. referenceTileLabels ["pg"])
+            // what a log written by JSON.stringify holds, e.g. referenceTileLabels ["pg"]); any
+            // other array is validated here and formatted by the host's js_stringify
             r.p++;
+            bool canon = true;
             if (r.at() != ']') {
                 for (;;) {
                     const int e = r.at();
@@ -921,28 +932,40 @@ __host__ __device__ uint32_t props_obj(Rd &r, uint32_t &np, uint32_t gidx, uint3
                         uint32_t so, sl;
                         bool pl;
                         if (!str_raw(r, so, sl, pl)) return kFSyntax;
-                        if (!pl && !str_canonical(r, so, sl)) return kFShape;
+                        if (!pl && !str_canonical(r, so, sl)) canon = false;
                     } else if (e == '-' || is_digit(e)) {
                         int64_t v;
                         uint32_t nd;
                         const int t = num_tok(r, v, nd);
-                        if (t != 1) return t ? kFShape : kFSyntax;
-                        if (nd > 15) return kFShape;
+                        if (!t) return kFSyntax;
+                        if (t != 1 || nd > 15) canon = false;
                     } else if (!(r.lit("true", 4) || r.lit("false", 5) || r.lit("null", 4))) {
-                        return kFShape;  // nested containers / whitespace: the host's js_stringify
+                        canon = false;  // nested containers / whitespace
+                        break;
                     }
                     if (r.at() == ',') {
                         r.p++;
                         continue;
                     }
-                    if (r.at() == ']') break;
-                    return kFShape;
+                    if (r.at() != ']') canon = false;
+                    break;
                 }
             }
-            r.p++;
-            vl = r.p - vo;
+            if (canon) {
+                r.p++;
+                vl = r.p - vo;
+            } else {
+                r.p = vo;
+                if (!skip_value(r)) return kFSyntax;
+                vl = (r.p - vo) | kSpanCanon;
+            }
+        } else if (c == '{') {
+            // an object: validated here, formatted by the host's js_stringify (JS key order:
+            // array-index keys first, duplicate keys, whitespace)
+            if (!skip_value(r)) return kFSyntax;
+            vl = (r.p - vo) | kSpanCanon;
         } else {
-            return kFShape;  // objects: the host's js_stringify (JS key order, whitespace)
+            return kFSyntax;
         }
         if (W) {
             cx.pk_off[gidx + np] = ko;
@@ -1385,7 +1408,7 @@ __device__ void parse_chunk(const Params &P) {
         cx.pk_len = P.pk_len;
         cx.pv_off = P.pv_off;
         cx.pv_len = P.pv_len;
-        cx.cid = (uint8_t)P.m_cid[m];
+        cx.cid = (uint16_t)P.m_cid[m];
         cx.install = P.install != 0;
     }
     const uint32_t f = parse_msg<W>(s, len, P.m_start[m], mo, cx);
@@ -1452,7 +1475,7 @@ struct Spans {
     uint64_t base;             // index of entry 0
     const uint8_t *null4;
     __device__ const uint8_t *ptr(uint32_t i) const { return off[base + i] == kNullSpan ? null4 : s + off[base + i]; }
-    __device__ uint32_t n(uint32_t i) const { return off[base + i] == kNullSpan ? 4u : len[base + i]; }
+    __device__ uint32_t n(uint32_t i) const { return off[base + i] == kNullSpan ? 4u : len[base + i] & ~kSpanCanon; }
 };
 
 // insert entry i; returns false when the table is full
@@ -1541,20 +1564,28 @@ extern "C" __global__ __launch_bounds__(64) void jg_clients_kernel(Params P) {
         }
     }
     __syncthreads();
-    uint32_t *tab = P.cl_ht + (uint64_t)d * kClientSlots;
+    uint32_t *tab = P.cl_ht + P.cl_base[d];
     const uint32_t *cid = P.m_cid;
     auto is_obs = [&](uint32_t i) { return cid[mb + i] == 0u; };
-    const uint32_t cnt = intern(tab, kClientSlots, S, nmsg, 1u, P.m_cid, P.nm_off, P.nm_len, is_obs);
+    const uint32_t cnt = intern(tab, P.cl_cap[d], S, nmsg, 1u, P.m_cid, P.nm_off, P.nm_len, is_obs);
     for (int o = 32; o > 0; o >>= 1) fail |= __shfl_xor(fail, o, 64);
     if (cnt == 0xFFFFFFFFu || cnt + 1 > (uint32_t)MT_MAX_CLIENTS) fail |= kFClients;
-    __syncthreads();
-    for (uint32_t k = (uint32_t)lane; !fail && k < cnt; k += 64) {
-        P.names[(uint64_t)d * 512 + 2 * k] = P.nm_off[mb + k];
-        P.names[(uint64_t)d * 512 + 2 * k + 1] = P.nm_len[mb + k];
-    }
     if (lane == 0) {
         P.d_nnames[d] = cnt == 0xFFFFFFFFu ? 0u : cnt + 1;
         if (fail) P.d_fail[d] = fail;
+    }
+}
+
+// the documents' client-name spans (ids 1.., nm_off / nm_len of the message region) back to back
+// for the host: names_base from the host's prefix sum of the name counts
+extern "C" __global__ __launch_bounds__(64) void jg_names_kernel(Params P) {
+    const int64_t d = blockIdx.x;
+    if (d >= P.D) return;
+    const uint32_t nn = P.d_nnames[d];
+    const uint64_t mb = mregion(P.doc_off, d), nb = P.names_base[d];
+    for (uint32_t k = (uint32_t)lane_id(); k + 1 < nn; k += 64) {
+        P.names[nb + 2 * k] = P.nm_off[mb + k];
+        P.names[nb + 2 * k + 1] = P.nm_len[mb + k];
     }
 }
 
@@ -1753,9 +1784,6 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(hipMemsetAsync(P.d_ntext, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_nprop, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_npropops, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
-    JGCHK(B.get(&P.names, (size_t)D * 512));
-    JGCHK(B.get(&P.cl_ht, (size_t)D * kClientSlots));
-    JGCHK(hipMemsetAsync(P.cl_ht, 0, 4 * (size_t)D * kClientSlots, s));
     {
         uint8_t *o = nullptr;
         JGCHK(B.get(&o, 512));
@@ -1830,6 +1858,30 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(hipEventRecord(ev[1], s));
     if (cgrid) JGCHK(hipLaunchKernel((const void *)jg_count_kernel, dim3(cgrid), dim3(64), argc, 0, s));
     if (D) JGCHK(hipLaunchKernel((const void *)jg_offsets_kernel, dim3(grid), dim3(64), argc, 0, s));
+    // client hash tables: a power of two > 2 x the names a document can hold (its messages, at most
+    // MT_MAX_CLIENTS: a table too small for more names reports the document, kFClients)
+    {
+        std::vector<uint64_t> cl_base((size_t)D);
+        std::vector<uint32_t> cl_cap((size_t)D);
+        uint64_t csum = 0;
+        for (int64_t d = 0; d < D; d++) {
+            cl_cap[(size_t)d] = pow2_at_least(2ull * std::min<uint64_t>(nmsg[(size_t)d], MT_MAX_CLIENTS) + 1);
+            cl_base[(size_t)d] = csum;
+            csum += cl_cap[(size_t)d];
+        }
+        uint64_t *d_clb = nullptr;
+        uint32_t *d_clc = nullptr;
+        JGCHK(B.get(&P.cl_ht, (size_t)std::max<uint64_t>(csum, 1)));
+        JGCHK(hipMemsetAsync(P.cl_ht, 0, 4 * std::max<uint64_t>(csum, 1), s));
+        JGCHK(B.get(&d_clb, (size_t)D));
+        JGCHK(B.get(&d_clc, (size_t)D));
+        if (D) {
+            JGCHK(hipMemcpyAsync(d_clb, cl_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice, s));
+            JGCHK(hipMemcpyAsync(d_clc, cl_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice, s));
+        }
+        P.cl_base = d_clb;
+        P.cl_cap = d_clc;
+    }
     JGCHK(hipEventRecord(ev[2], s));
     if (D) JGCHK(hipLaunchKernel((const void *)jg_clients_kernel, dim3(grid), dim3(64), argc, 0, s));
     JGCHK(hipEventRecord(ev[3], s));
@@ -1952,8 +2004,23 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(dl(uvo, P.uv_off, (size_t)vp, s));
     JGCHK(dl(uvl, P.uv_len, (size_t)vp, s));
     JGCHK(dl(nnames, P.d_nnames, (size_t)D, s));
+    std::vector<uint64_t> names_base((size_t)D);
+    uint64_t nsum = 0;
+    for (int64_t d = 0; d < D; d++) {
+        names_base[(size_t)d] = nsum;
+        nsum += 2ull * (nnames[(size_t)d] > 0 ? nnames[(size_t)d] - 1 : 0);
+    }
     std::vector<uint32_t> names;
-    JGCHK(dl(names, P.names, (size_t)D * 512, s));  // jg_clients_kernel: names' spans by id - 1
+    {
+        uint64_t *d_nb = nullptr;
+        JGCHK(B.get(&P.names, (size_t)std::max<uint64_t>(nsum, 1)));
+        JGCHK(B.get(&d_nb, (size_t)D));
+        if (D) JGCHK(hipMemcpyAsync(d_nb, names_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice, s));
+        P.names_base = d_nb;
+        void *argn[] = {&P};
+        if (D) JGCHK(hipLaunchKernel((const void *)jg_names_kernel, dim3(grid), dim3(64), argn, 0, s));
+        JGCHK(dl(names, P.names, (size_t)nsum, s));  // names' spans by id - 1, document after document
+    }
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<uint32_t> kmap((size_t)std::max<uint64_t>(pp, 1)), vmap((size_t)std::max<uint64_t>(vp, 1));
     std::unordered_map<std::string, uint32_t> kid, vid{{"null", 0u}};
@@ -1973,7 +2040,17 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
         }
         const uint32_t vb = val_base[(size_t)d];
         for (uint32_t i = 0; i < nuv[(size_t)d]; i++) {
-            std::string v(js + uvo[vb + i], uvl[vb + i]);
+            std::string v(js + uvo[vb + i], uvl[vb + i] & ~kSpanCanon);
+            if (uvl[vb + i] & kSpanCanon) {  // not in JSON.stringify form: JSON.stringify(JSON.parse(v))
+                std::string cv;
+                if (!json_canonical_value(v.data(), v.size(), cv)) {
+                    res.status = MT_UNSUPPORTED;
+                    res.bad_doc = d;
+                    res.fail_bits = kFSyntax;
+                    return MT_UNSUPPORTED;
+                }
+                v.swap(cv);
+            }
             auto it = vid.find(v);
             if (it == vid.end()) {
                 it = vid.emplace(v, (uint32_t)res.values.size()).first;
@@ -1983,7 +2060,7 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
         }
         auto &nm = res.clients[(size_t)d];
         nm.assign(1, obs);
-        const uint32_t *nd = names.data() + (size_t)d * 512;
+        const uint32_t *nd = names.data() + names_base[(size_t)d];
         for (uint32_t i = 1; i < nnames[(size_t)d]; i++) {
             const uint32_t o = nd[2 * (i - 1)];
             nm.push_back(o == kNullSpan ? std::string("null") : std::string(js + o, nd[2 * (i - 1) + 1]));

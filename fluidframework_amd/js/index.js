@@ -169,8 +169,8 @@ class Packer {
             if (typeof msg === 'string') msg = JSON.parse(msg);
             let c = short.get(msg.clientId);
             if (c === undefined) {
-                // short ids 0..253 (include/mt_oplog.h MT_MAX_CLIENTS; 254 / 255 are sentinels)
-                if (names.length >= 254) throw new UnsupportedOp('more than 253 clients (short ids are 8-bit)');
+                // short ids 0..4093 (include/mt_oplog.h MT_MAX_CLIENTS; 4094 / 4095 are sentinels)
+                if (names.length >= 4094) throw new UnsupportedOp('more than 4093 clients (short ids are 12-bit)');
                 c = names.length;
                 short.set(msg.clientId, c);
                 names.push(msg.clientId);
@@ -229,8 +229,7 @@ class Packer {
         const ops = Buffer.alloc(32 * Math.max(1, this.recs.length));
         this.recs.forEach((r, i) => {
             const o = 32 * i;
-            ops.writeUInt8(r.type, o);
-            ops.writeUInt8(r.client, o + 1);
+            ops.writeUInt16LE((r.type & 15) | (r.client << 4), o);  // mt_op's type : 4, client : 12
             ops.writeUInt16LE(r.flags, o + 2);
             ops.writeInt32LE(r.seq, o + 4);
             ops.writeInt32LE(r.refSeq, o + 8);

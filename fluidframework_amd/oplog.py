@@ -31,8 +31,9 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+# "tc": the record type (bits 0-3) and the 12-bit short client id (bits 4-15), mt_op's bit-fields
 OP_DTYPE = np.dtype(
-    [("type", "u1"), ("client", "u1"), ("flags", "<u2"), ("seq", "<i4"), ("ref_seq", "<i4"),
+    [("tc", "<u2"), ("flags", "<u2"), ("seq", "<i4"), ("ref_seq", "<i4"),
      ("msn", "<i4"), ("pos1", "<i4"), ("pos2", "<i4"), ("payload", "<u4"), ("payload_len", "<u4")]
 )
 PROP_DTYPE = np.dtype([("key", "<u4"), ("value", "<u4")])
@@ -50,7 +51,28 @@ COMBINE_INCR, COMBINE_CONSENSUS, COMBINE_OTHER = 1, 2, 3
 KEY_COMBINE = VALUE_UNDEFINED = 0xFFFFFFFF
 
 
-MAX_CLIENTS = 254  # short ids 0..253 (include/mt_oplog.h MT_MAX_CLIENTS; 254 / 255 are sentinels)
+MAX_CLIENTS = 4094  # short ids 0..4093 (include/mt_oplog.h MT_MAX_CLIENTS; 4094 / 4095 are sentinels)
+CLIENT_NONCOLLAB, CLIENT_NONE = 4094, 4095
+
+
+def rec_type(a):
+    """record type(s) of an mt_op record / array (the low 4 bits of "tc")"""
+    return a["tc"] & 0xF
+
+
+def rec_client(a):
+    """short client id(s) of an mt_op record / array (the high 12 bits of "tc")"""
+    return a["tc"] >> 4
+
+
+def make_tc(t, c):
+    """the "tc" word of type t and short client id c (scalars or integer arrays)"""
+    return (np.asarray(t, np.uint32) & 0xF) | (np.asarray(c, np.uint32) << 4)
+
+
+def set_client(a, c):
+    """replace the short client id(s) of records, keeping their types"""
+    a["tc"] = make_tc(a["tc"] & 0xF, c).astype(np.uint16)
 
 
 class UnsupportedOp(ValueError):
@@ -220,7 +242,7 @@ class Packer:
                 cid = "null"
             if cid not in short:  # getOrAddShortClientId (client.ts:636-641)
                 if len(names) >= MAX_CLIENTS:
-                    raise UnsupportedOp(f"more than {MAX_CLIENTS - 1} clients (short ids are 8-bit)")
+                    raise UnsupportedOp(f"more than {MAX_CLIENTS - 1} clients (short ids are 12-bit)")
                 short[cid] = len(names)
                 names.append(cid)
             c = short[cid]
@@ -385,7 +407,10 @@ class Packer:
     def finish(self) -> PackedBatch:
         ops = np.zeros(len(self._ops), OP_DTYPE)
         for name in OP_DTYPE.names:
-            ops[name] = [r[name] for r in self._ops] if self._ops else []
+            if name == "tc":
+                ops[name] = [r["type"] | (r["client"] << 4) for r in self._ops] if self._ops else []
+            else:
+                ops[name] = [r[name] for r in self._ops] if self._ops else []
         text = np.concatenate(self._text) if self._text else np.zeros(0, np.uint16)
         props = np.array(self._props, PROP_DTYPE) if self._props else np.zeros(0, PROP_DTYPE)
         return PackedBatch(ops=ops, doc_op_off=np.array(self._off, np.int64), text=text.astype(np.uint16),
@@ -416,13 +441,13 @@ def writer_records(ops: np.ndarray, off: np.ndarray, writer_of: np.ndarray):
     doc = np.repeat(np.arange(D, dtype=np.int64), counts)
     idx = np.arange(len(ops), dtype=np.int64) - off[doc]
     w = np.asarray(writer_of, np.int64)[doc]
-    client = ops["client"].astype(np.int64)
+    client = rec_client(ops).astype(np.int64)
     mine = client == w
     orig = ops.copy()
-    orig["client"] = np.where(mine, 0, np.where(client == 0, w, client)).astype(np.uint8)
+    set_client(orig, np.where(mine, 0, np.where(client == 0, w, client)))
     loc = ops[mine].copy()
     loc["seq"] = -1
-    loc["client"] = 0
+    set_client(loc, 0)
     loc["msn"] = 0
     # order inside a document: original record i at 2i, a local copy with refSeq r at 2r - 1 (right
     # after the record with seq r, i.e. index r - 1); copies with the same refSeq in issue order
@@ -450,8 +475,8 @@ def records_to_json(ops: np.ndarray, off: np.ndarray, text: np.ndarray, props: n
     kq = [json.dumps(k) for k in keys]
     out = []
     shared = clients and isinstance(clients[0], str)
-    typ = ops["type"].tolist()
-    cli = ops["client"].tolist()
+    typ = rec_type(ops).tolist()
+    cli = rec_client(ops).tolist()
     flg = ops["flags"].tolist()
     seq = ops["seq"].tolist()
     ref = ops["ref_seq"].tolist()

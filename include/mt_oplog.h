@@ -69,9 +69,12 @@ enum mt_relpos_flags {
     MT_RELF_OFF1 = 0x100u,   /* relativePos1.offset is defined (payload)           */
     MT_RELF_OFF2 = 0x200u    /* relativePos2.offset is defined (payload_len)       */
 };
-#define MT_CLIENT_NONCOLLAB 254u /* NonCollabClient (constants.ts:15); long id "original" */
-#define MT_CLIENT_NONE 255u
-#define MT_MAX_CLIENTS 254      /* short ids 0 .. 253 per document (0 = the observer)          */
+/* short client ids are 12-bit: 0 .. 4093 per document (0 = the observer; Client.getOrAddShortClientId,
+   client.ts:636-660, numbers every long id a document's log names, and a real messages.json names a
+   new one on every reconnect), 4094 / 4095 are sentinels */
+#define MT_CLIENT_NONCOLLAB 4094u /* NonCollabClient (constants.ts:15); long id "original" */
+#define MT_CLIENT_NONE 4095u
+#define MT_MAX_CLIENTS 4094      /* short ids 0 .. 4093 per document (0 = the observer)          */
 #define MT_SEQ_NONE 0x7FFFFFFF
 #define MT_OP_IS_INSERT_LIKE(t) ((t) == MT_OP_INSERT || (t) == MT_OP_LOAD_HEADER || (t) == MT_OP_LOAD_BODY)
 
@@ -116,9 +119,12 @@ enum mt_combine_kind {
 #define MT_OPF_INTERNAL_ENDS_NL 0x8000u
 #define MT_OPF_INTERNAL (MT_OPF_INTERNAL_HAS_NL | MT_OPF_INTERNAL_ENDS_NL)
 
+/* The first 16-bit word holds the record type (bits 0-3) and the short client id (bits 4-15):
+   little-endian u16 `type | client << 4`.  C / C++ / HIP read both through the bit-fields below;
+   byte packers (Python, JS) write the word. */
 typedef struct mt_op {
-    uint8_t type;         /* enum mt_op_type                                             */
-    uint8_t client;       /* short client id (index in the doc's client table, 1..253; 0 is
+    uint16_t type : 4;    /* enum mt_op_type                                             */
+    uint16_t client : 12; /* short client id (index in the doc's client table, 1..4093; 0 is
                              the observer itself, as Client.startOrUpdateCollaboration
                              assigns it first: client.ts:1051-1062)                       */
     uint16_t flags;       /* enum mt_op_flags | nprops<<4                                  */

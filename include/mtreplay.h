@@ -55,7 +55,7 @@ enum mt_status_code {
     MT_INVALID_POS = 1,  /* "MergeTree insert failed" */
     MT_SEQ_ORDER = 2,    /* sequence number went backwards */
     MT_MSN_ORDER = 3,    /* minimumSequenceNumber went backwards / above seq */
-    MT_UNSUPPORTED = 4,  /* op outside the device model or limits (> 253 clients) */
+    MT_UNSUPPORTED = 4,  /* op outside the device model or limits (> 4093 clients) */
     MT_BAD_INPUT = 5,
     MT_CAPACITY = 6,     /* document exceeded the largest device capacity class */
     MT_INTERNAL = 7,

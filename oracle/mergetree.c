@@ -158,7 +158,7 @@ struct mto_doc {
     sb *blobs;
     int n_blobs;
     /* packed-op client index -> short id cache */
-    int pk_map[256];
+    int pk_map[MT_MAX_CLIENTS + 2];
     /* MergeTree.idToSegment (mergeTree.ts:1098): String(markerId) -> marker */
     u16 **id_keys;
     int *id_klens;
@@ -1737,7 +1737,7 @@ mto_doc *mto_new(void) {
     d->root->n.cached_length = 0;
     d->cw.client_id = LOCAL_CLIENT;
     heap_init(d);
-    for (int i = 0; i < 256; i++) d->pk_map[i] = -1;
+    for (int i = 0; i < MT_MAX_CLIENTS + 2; i++) d->pk_map[i] = -1;
     return d;
 }
 
@@ -3342,8 +3342,8 @@ int mto_gen_doc(const mt_gen_params *p, long doc, mt_op *ops_out, uint16_t *text
         if (len < p->min_len || (int)u < p->pct_insert) type = MT_OP_INSERT;
         else if ((int)u < p->pct_insert + p->pct_remove) type = MT_OP_REMOVE;
         else type = MT_OP_ANNOTATE;
-        op.type = (uint8_t)type;
-        op.client = (uint8_t)c;
+        op.type = (uint16_t)type;
+        op.client = (uint16_t)c;
         op.seq = seq;
         op.ref_seq = ref;
         op.msn = msn;

@@ -18,8 +18,7 @@ LIB_PATH = ORACLE_DIR / "build" / "liboracle.so"
 
 OP_DTYPE = np.dtype(
     [
-        ("type", "u1"),
-        ("client", "u1"),
+        ("tc", "<u2"),  # type (bits 0-3) | short client id << 4 (include/mt_oplog.h bit-fields)
         ("flags", "<u2"),
         ("seq", "<i4"),
         ("ref_seq", "<i4"),
@@ -325,9 +324,9 @@ def gen_batch(p: GenParams, n_docs: int, first_doc: int = 0, doc_ids=None, doc_o
             pj = GenParams(*[getattr(p, f) for f, _ in GenParams._fields_])
             pj.n_ops = int(doc_ops[j])
         ops, text, props = gen_doc(pj, int(dd))
-        ins = ops["type"] == 0
+        ins = (ops["tc"] & 0xF) == 0
         ops["payload"][ins] += t_base
-        ann = ops["type"] == 2
+        ann = (ops["tc"] & 0xF) == 2
         ops["payload"][ann] += p_base
         all_ops.append(ops)
         all_text.append(text)

@@ -25,7 +25,7 @@ def _messages(ops, text, props):
     vals = [json.loads(O.lib().mto_gen_value_json(v).decode()) for v in range(22)]
     out = []
     for o in ops:
-        t = int(o["type"])
+        t = int(o["tc"]) & 0xF
         if t == 0:
             s = text[o["payload"]:o["payload"] + o["payload_len"]]
             c = {"type": 0, "pos1": int(o["pos1"]), "seg": s.tobytes().decode("utf-16-le")}
@@ -35,7 +35,7 @@ def _messages(ops, text, props):
             pr = props[o["payload"]:o["payload"] + o["payload_len"]]
             c = {"type": 2, "pos1": int(o["pos1"]), "pos2": int(o["pos2"]),
                  "props": {keys[int(p["key"])]: vals[int(p["value"])] for p in pr}}
-        out.append({"clientId": NAMES[int(o["client"])], "sequenceNumber": int(o["seq"]),
+        out.append({"clientId": NAMES[int(o["tc"]) >> 4], "sequenceNumber": int(o["seq"]),
                     "referenceSequenceNumber": int(o["ref_seq"]), "minimumSequenceNumber": int(o["msn"]),
                     "type": "op", "contents": c})
     return out

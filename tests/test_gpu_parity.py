@@ -118,9 +118,9 @@ def test_gpu_generator_matches_oracle_generator():
         for d in range(n):
             o_ops, o_text, o_props = O.gen_doc(p, d)
             g_ops = ops[off[d]:off[d + 1]]
-            for f in ("type", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len"):
+            for f in ("tc", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len"):
                 assert (g_ops[f] == o_ops[f]).all(), (d, f)
-            ins = g_ops["type"] == 0
+            ins = (g_ops["tc"] & 0xF) == 0
             g_txt = np.concatenate([text[o["payload"]:o["payload"] + o["payload_len"]] for o in g_ops[ins]])
             assert (g_txt == o_text).all()
             od = O.replay_doc(o_ops, o_text, o_props, O.gen_tables(), O.gen_client_names(8))
@@ -180,23 +180,35 @@ def test_error_statuses_match_oracle():
         assert b.doc(3).get_text() == "fine"
 
 
-def _many_client_farm(n_clients, n_ops, seed, lag=24, hot=12):
+def _many_client_farm(n_clients, n_ops, seed, lag=24, hot=12, active=0):
     """A valid conflict-farm log of n_clients writers, generated against the oracle as the replica
     model (each op is drawn from its issuer's view getLength(refSeq, client), then applied):
     removes and annotates favour the first `hot` positions, so concurrent removes of the same
-    segments by many clients (removedClientOverlap with clients beyond the 31st) are common."""
+    segments by many clients (removedClientOverlap with clients beyond the 31st) are common.
+    active > 0: sessions — at most `active` clients are connected at once, each leaves after a few
+    ops and a new client id joins in its place (a reconnect is a new clientId in a real
+    messages.json), the MSN is the minimum over the connected ones; n_clients ids in all."""
     import random
 
     rnd = random.Random(seed)
-    names = [f"client-{i:03d}" for i in range(n_clients)]
+    names = [f"client-{i:04d}" for i in range(n_clients)]
     model = O.Doc()
     model.start_collab("readonly")
     short, last_ref, msgs = {}, {}, []
+    live, joined, floor = [], 0, 0
     for k in range(1, n_ops + 1):
-        c = names[rnd.randrange(n_clients)] if k > 1 else names[0]
+        if active:
+            while len(live) < active and joined < n_clients:
+                live.append(names[joined])
+                last_ref[names[joined]] = max(floor, k - 1)
+                joined += 1
+            c = live[rnd.randrange(len(live))]
+        else:
+            c = names[rnd.randrange(n_clients)] if k > 1 else names[0]
         ref = max(last_ref.get(c, 0), k - 1 - rnd.randrange(lag + 1))
         last_ref[c] = ref
-        msn = min(last_ref.values())
+        msn = max(floor, min(last_ref[x] for x in live)) if active else min(last_ref.values())
+        floor = msn
         sid = short.get(c, len(short) + 1)
         n = model.view_length(ref, sid)
         u = rnd.randrange(100)
@@ -214,14 +226,21 @@ def _many_client_farm(n_clients, n_ops, seed, lag=24, hot=12):
         assert model.apply_msg(json.dumps(m)) == 0, model.error()
         short.setdefault(c, len(short) + 1)
         msgs.append(m)
+        if active and rnd.random() < 0.15 and joined < n_clients:  # the client leaves: a new id joins
+            live.remove(c)
+            del last_ref[c]
     return msgs
 
 
 def test_many_clients_with_overlapping_removes():
-    """Short client ids are 8-bit (up to 253 writers per document, client.ts:636-660 assigns them
-    in first-appearance order): 150 writers with concurrent overlapping removes (overlap sets
-    beyond 31 clients are pool lists) replay bit-exact; more than 253 are flagged, not wrong."""
-    docs = [_many_client_farm(150, 2500, seed=11), _many_client_farm(200, 1500, seed=12, lag=60, hot=6)]
+    """Short client ids are 12-bit (up to 4,093 writers per document; client.ts:636-660 assigns them
+    in first-appearance order and a long-lived document's log names a new clientId on every
+    reconnect): 1,000 session ids over a 16-client window, and 300 writers with concurrent
+    overlapping removes (overlap sets beyond 31 clients are pool lists, mergeTree.ts:2544-2563)
+    replay bit-exact, also through checkpoint / resume; more than 4,093 are flagged, not wrong."""
+    docs = [_many_client_farm(1000, 7000, seed=13, active=16, hot=8),
+            _many_client_farm(300, 2500, seed=11), _many_client_farm(200, 1500, seed=12, lag=60, hot=6)]
+    assert len({m["clientId"] for m in docs[0]}) == 1000
     oracle = oracle_docs_from_messages(docs)
     with fa.ReplayBatch(len(docs)) as b:
         b.ingest_messages(docs)
@@ -236,7 +255,16 @@ def test_many_clients_with_overlapping_removes():
         b.ingest_messages(docs)
         b.run()
         assert (b.device_digests() == d0).all()
-    msgs = [_msg(f"c{i}", i + 1, i, {"type": 0, "pos1": 0, "seg": "x"}) for i in range(300)]
+    js = [json.dumps(d) for d in docs]
+    with fa.ReplayBatch(len(docs)) as b:  # the native JSON parsers (host threads, and the GPU's)
+        assert b.ingest_json(js, device="host")["path"] == "host"
+        b.run()
+        assert (b.device_digests() == d0).all()
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_json(js, device="gpu")
+        b.run()
+        assert (b.device_digests() == d0).all()
+    msgs = [_msg(f"c{i}", i + 1, i, {"type": 0, "pos1": 0, "seg": "x"}) for i in range(4100)]
     with fa.ReplayBatch(1) as b:
         with pytest.raises(oplog.UnsupportedOp):
             b.ingest_messages([msgs])
@@ -315,9 +343,9 @@ def test_mixed_size_batch_generate_docs_and_concurrent_classes():
         b.generate_docs(fa.gen_params(0, pct_insert=70, pct_remove=20, seed=0x21BF), ids, ops_n)
         gops, goff, gtext, gprops = b.download_log()
         assert (goff == off).all()
-        for f in ("type", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len"):
+        for f in ("tc", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len"):
             assert (gops[f] == ops[f]).all(), f
-        ins = gops["type"] == 0
+        ins = (gops["tc"] & 0xF) == 0
         g_txt = np.concatenate([gtext[o["payload"]:o["payload"] + o["payload_len"]] for o in gops[ins]])
         o_txt = np.concatenate([text[o["payload"]:o["payload"] + o["payload_len"]] for o in ops[ins]])
         assert (g_txt == o_txt).all()

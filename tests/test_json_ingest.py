@@ -56,7 +56,7 @@ def _farm_messages():
     vals = [json.loads(O.lib().mto_gen_value_json(v).decode()) for v in range(22)]
     out = []
     for o in ops:
-        t = int(o["type"])
+        t = int(o["tc"]) & 0xF
         if t == 0:
             c = {"type": 0, "pos1": int(o["pos1"]),
                  "seg": text[o["payload"]:o["payload"] + o["payload_len"]].tobytes().decode("utf-16-le")}
@@ -66,7 +66,7 @@ def _farm_messages():
             pr = props[o["payload"]:o["payload"] + o["payload_len"]]
             c = {"type": 2, "pos1": int(o["pos1"]), "pos2": int(o["pos2"]),
                  "props": {keys[int(q["key"])]: vals[int(q["value"])] for q in pr}}
-        out.append(_msg(names[int(o["client"])], int(o["seq"]), int(o["ref_seq"]), c, int(o["msn"])))
+        out.append(_msg(names[int(o["tc"]) >> 4], int(o["seq"]), int(o["ref_seq"]), c, int(o["msn"])))
     return out
 
 
@@ -196,7 +196,7 @@ def test_reconnect_streams_pack_identically():
     got = pj.arrays()
     pj.close()
     assert (got.ops == want.ops).all() and (got.props == want.props).all() and got.values == want.values
-    assert (got.ops["type"] == oplog.OP_REGENERATE).any()
+    assert (oplog.rec_type(got.ops) == oplog.OP_REGENERATE).any()
 
 
 def test_records_to_json_round_trips_generated_logs():

@@ -321,7 +321,7 @@ def test_writer_streams_of_generated_logs_replay():
         assert obs.status == 0
         for w in (1 + d % p.n_clients, 1 + (d + 3) % p.n_clients):
             recs, wn = writer_log(doc_ops, names, w)
-            assert (recs["seq"] == -1).sum() == (doc_ops["client"] == w).sum()
+            assert (recs["seq"] == -1).sum() == ((doc_ops["tc"] >> 4) == w).sum()
             wd = O.replay_doc(recs, text, props, t, wn)
             assert wd.status == 0, wd.error
             assert wd.pending_groups() == 0
@@ -357,7 +357,7 @@ def test_packed_writer_streams_replay_like_the_json_ones():
     t = O.Tables(pb.keys or ["_"], pb.values)
     for i, n in enumerate(f.names):
         recs = pb.ops[pb.doc_op_off[i]:pb.doc_op_off[i + 1]].copy()
-        assert (recs["seq"] == -1).any() and ((recs["client"] == 0) & (recs["seq"] > 0)).any()
+        assert (recs["seq"] == -1).any() and (((recs["tc"] >> 4) == 0) & (recs["seq"] > 0)).any()
         d = O.replay_doc(recs, pb.text, pb.props, t, pb.clients[i])
         assert d.status == 0, d.error
         assert d.digest() == f.docs[n].digest() and d.dump() == f.docs[n].dump()
@@ -380,6 +380,6 @@ def test_vectorized_writer_records_equal_writer_log():
         exp = recs.copy()
         order = [w] + [c for c in range(len(names)) if c != w]
         back = {new: old for new, old in enumerate(order)}
-        exp_client = np.array([0 if back[int(c)] == w else (w if back[int(c)] == 0 else back[int(c)]) for c in exp["client"]])
-        exp["client"] = exp_client
+        exp_client = np.array([0 if back[int(c)] == w else (w if back[int(c)] == 0 else back[int(c)]) for c in exp["tc"] >> 4])
+        oplog.set_client(exp, exp_client)
         assert mine.tobytes() == exp.tobytes(), d

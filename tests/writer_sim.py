@@ -207,21 +207,21 @@ def writer_log(ops: np.ndarray, names: list, w: int):
     issued = {}
     for m in msgs:
         r0 = ops[m[0]]
-        if int(r0["client"]) == w and int(r0["type"]) != 15:
+        if int(r0["tc"]) >> 4 == w and int(r0["tc"]) & 0xF != 15:
             local = ops[m].copy()
             local["seq"] = UNASSIGNED
-            local["client"] = 0
+            local["tc"] = local["tc"] & 0xF  # client 0
             local["msn"] = 0
             issued.setdefault(int(r0["ref_seq"]), []).append(local)
     # short ids: w first, the others keep their order (the packed client field indexes `names`)
     order = [w] + [c for c in range(len(names)) if c != w]
-    remap = np.zeros(256, np.int64)
+    remap = np.zeros(4096, np.int64)
     for new, old in enumerate(order):
         remap[old] = new
     out = list(issued.get(0, []))
     for m in msgs:
         rec = ops[m].copy()
-        rec["client"] = remap[rec["client"].astype(np.int64)]
+        rec["tc"] = (rec["tc"] & 0xF) | (remap[(rec["tc"] >> 4).astype(np.int64)] << 4).astype(np.uint16)
         out.append(rec)
         out.extend(issued.get(int(ops[m[0]]["seq"]), []))
     recs = np.concatenate(out) if out else ops[:0].copy()

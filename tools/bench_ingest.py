@@ -23,7 +23,7 @@ NAMES = ["readonly"] + [chr(ord("A") + i) for i in range(26)]
 def render(ops, off, text, props, d):
     out = []
     for o in ops[off[d]:off[d + 1]]:
-        t = int(o["type"])
+        t = int(o["tc"]) & 0xF
         if t == 0:
             c = {"type": 0, "pos1": int(o["pos1"]),
                  "seg": text[o["payload"]:o["payload"] + o["payload_len"]].tobytes().decode("utf-16-le")}
@@ -33,7 +33,7 @@ def render(ops, off, text, props, d):
             pr = props[o["payload"]:o["payload"] + o["payload_len"]]
             c = {"type": 2, "pos1": int(o["pos1"]), "pos2": int(o["pos2"]),
                  "props": {KEYS[int(q["key"])]: VALS[int(q["value"])] for q in pr}}
-        out.append({"clientId": NAMES[int(o["client"])], "sequenceNumber": int(o["seq"]),
+        out.append({"clientId": NAMES[int(o["tc"]) >> 4], "sequenceNumber": int(o["seq"]),
                     "referenceSequenceNumber": int(o["ref_seq"]), "minimumSequenceNumber": int(o["msn"]),
                     "type": "op", "contents": c})
     return json.dumps(out).encode()

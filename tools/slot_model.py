@@ -23,9 +23,9 @@ for n_ops, docs, pi, pr in CASES:
         ops, off, text, props = b.download_log()
         for d in range(docs):
             o = ops[off[d]:off[d + 1]]
-            ins = o["type"] == 0
-            rem = o["type"] == 1
-            ann = o["type"] == 2
+            ins = (o["tc"] & 0xF) == 0
+            rem = (o["tc"] & 0xF) == 1
+            ann = (o["tc"] & 0xF) == 2
             units = int(o["payload_len"][ins].sum())
             nl = sum(int((text[x["payload"]:x["payload"] + x["payload_len"]] == 10).sum()) for x in o[ins])
             removed = int((o["pos2"][rem] - o["pos1"][rem]).sum())
