@@ -182,11 +182,15 @@ constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS c
 // a pending-group region in HBM, persistent across launches (u32 words):
 //   [0] pending groups n   [1] id G of the oldest (groups are numbered in creation order)
 //   [2] first entry that may be live   [3] entries used
-//   [kPendDesc ..) per group G & 63: {type | flags << 16, prop-record offset, prop count, 0}
+//   [kPendDesc ..) per group G, at G mod kPendMaxGroups: {type | flags << 16, prop-record offset,
+//                  prop count, localSeq}
 //   [kPendEntries ..) entries {G, slot} in append order (the group's `segments` array order:
 //   members as the op reached them, split-off halves appended when the split happens)
 //   word 4: collabWindow.localSeq (one per applied local op); a group's desc .w = its localSeq
-constexpr int kPendMaxGroups = 64;  // unacked local ops at once (more: MT_UNSUPPORTED)
+// unacked local ops at once (more: MT_UNSUPPORTED).  A segment's groups are the bits G & 63 of a
+// 64-bit mask in its cold record: exact while at most 64 groups are pending; beyond, a bit stands
+// for every live group 64 apart and membership is decided by the groups' entry lists
+constexpr int kPendMaxGroups = 1024;
 constexpr int kPendDesc = 8;
 constexpr int kPendEntries = kPendDesc + 4 * kPendMaxGroups;
 constexpr int kCapPending = 9;  // DocOut.cap_kind: the pending-entry region is full (terminal)

@@ -1198,7 +1198,7 @@ struct Engine {
                 const uint64_t m = (uint64_t)rdl(pv, 6) | ((uint64_t)rdl(pv, 7) << 32);
                 const uint32_t head = pend_word(1);
                 for (int32_t i = 0; i < n_pend && !status; i++)
-                    if ((m >> ((head + (uint32_t)i) & 63u)) & 1ull) entry_append(head + (uint32_t)i, (uint32_t)ns);
+                    if (in_group(head + (uint32_t)i, slot, m)) entry_append(head + (uint32_t)i, (uint32_t)ns);
                 if (status) return -1;
             }
         }
@@ -1294,6 +1294,49 @@ struct Engine {
         s_meta[slot] = m ? (meta | kMetaPending) : (meta & ~kMetaPending);
         wsync();
     }
+    MT_FI uint32_t *pdesc(uint32_t G) const { return pend + kPendDesc + 4 * (G & (uint32_t)(kPendMaxGroups - 1)); }
+    // is `slot` (pending mask m) a member of the live group G?  The mask bit decides while at most 64
+    // groups are pending; beyond, groups 64 apart share a bit and G's entries decide
+    MT_FI bool in_group(uint32_t G, uint32_t slot, uint64_t m) {
+        if (!((m >> (G & 63u)) & 1ull)) return false;
+        return n_pend <= 64 || entry_has(G, slot);
+    }
+    MT_FI bool entry_has(uint32_t G, uint32_t slot) {
+        const uint32_t start = pend_word(2), n = pend_word(3);
+        const uint2 *E = (const uint2 *)(pend + kPendEntries);
+        for (uint32_t b0 = start; b0 < n; b0 += kWave) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            bool hit = false;
+            if (j < n) {
+                const uint2 e = E[j];
+                hit = e.x == G && e.y == slot;
+            }
+            if (ballot(hit)) return true;
+        }
+        return false;
+    }
+    // after `slot` leaves group G: may bit G & 63 go?  (not while another live group sharing it,
+    // other than `skip`, holds the segment)
+    MT_FI bool bit_free_after(uint32_t G, uint32_t slot, uint32_t head, uint32_t skip) {
+        if (n_pend <= 64) return true;
+        for (uint32_t o = (G - head) & 63u; o < (uint32_t)n_pend; o += 64u) {
+            const uint32_t H = head + o;
+            if (H != G && H != skip && entry_has(H, slot)) return false;
+        }
+        return true;
+    }
+    // localSeq of the live group of type T holding `slot` (0xFFFFFFFF: none)
+    MT_FI uint32_t group_lseq(uint32_t slot, uint64_t m, uint32_t T) {
+        const uint32_t head = pend_word(1);
+        for (int32_t i = 0; i < n_pend; i++) {
+            const uint32_t G = head + (uint32_t)i;
+            if (!((m >> (G & 63u)) & 1ull)) continue;
+            const uint32_t *dp = pdesc(G);
+            if ((rfl(dp[0]) & 0xFFu) != T) continue;
+            if (in_group(G, slot, m)) return rfl(dp[3]);
+        }
+        return 0xFFFFFFFFu;
+    }
     // live entries (of pending groups) move to the front, in order
     MT_FI void pend_compact() {
         const uint32_t head = pend_word(1), start = pend_word(2), n = pend_word(3);
@@ -1341,7 +1384,7 @@ struct Engine {
             cur_g = (int32_t)(pend_word(1) + (uint32_t)n_pend);
             const uint32_t lseq = pend_word(4);  // collabWindow.localSeq of this op
             if (lane == 0) {
-                *(uint4 *)(pend + kPendDesc + 4 * (cur_g & 63)) =
+                *(uint4 *)pdesc((uint32_t)cur_g) =
                     make_uint4((uint32_t)op.type | ((uint32_t)op.flags << 16), op.payload, op.payload_len, lseq);
                 pend[0] = (uint32_t)(n_pend + 1);
             }
@@ -1361,11 +1404,12 @@ struct Engine {
         pk = 0;
         prw = false;
         for (int32_t i = 0; i < n_pend; i++) {
-            const uint32_t b = (head + (uint32_t)i) & 63u;
-            if (!((m >> b) & 1ull)) continue;
-            const uint32_t *dp = pend + kPendDesc + 4 * b;
+            const uint32_t G = head + (uint32_t)i;
+            if (!((m >> (G & 63u)) & 1ull)) continue;
+            const uint32_t *dp = pdesc(G);
             const uint32_t tf = rfl(dp[0]), off = rfl(dp[1]), cnt = rfl(dp[2]);
             if ((tf & 0xFFu) != MT_OP_ANNOTATE) continue;
+            if (!in_group(G, slot, m)) continue;
             if ((tf >> 16) & MT_OPF_REWRITE) prw = true;
             for (uint32_t k = 0; k < cnt; k++) {
                 const uint32_t key = rfl(props_in[off + k].key);
@@ -1387,7 +1431,7 @@ struct Engine {
         if (n_pend > 0) {
             const uint32_t head = pend_word(1);
             const uint32_t b = head & 63u;
-            const uint32_t tf = rfl(pend[kPendDesc + 4 * b]);
+            const uint32_t tf = rfl(pdesc(head)[0]);
             if ((tf & 0xFFu) != op.type) {  // not the op this group was made by: the stream is corrupt
                 set_fail(ST_BAD_INPUT);
                 return;
@@ -1419,7 +1463,7 @@ struct Engine {
                             if (lane == 0) cold[2 * slot + 1].y = (uint32_t)op.seq;
                         }
                     }
-                    pend_set_mask(slot, pend_mask(slot) & ~(1ull << b));
+                    if (bit_free_after(head, slot, head, head)) pend_set_mask(slot, pend_mask(slot) & ~(1ull << b));
                     add_to_lru(rfl((int32_t)s_blk[slot]), slot, op.seq);
                     if (status) return;
                 }
@@ -2738,8 +2782,8 @@ struct Engine {
         }
         resolve_cold();
         const uint32_t head = pend_word(1), gb = head & 63u;
-        const uint32_t L = rfl(pend[kPendDesc + 4 * gb + 3]);
-        if ((rfl(pend[kPendDesc + 4 * gb]) & 0xFFu) != T) {
+        const uint32_t L = rfl(pdesc(head)[3]);
+        if ((rfl(pdesc(head)[0]) & 0xFFu) != T) {
             set_fail(ST_BAD_INPUT);
             return;
         }
@@ -2774,8 +2818,10 @@ struct Engine {
                     m = (uint64_t)q.z | ((uint64_t)q.w << 32);
                     member = (m >> gb) & 1ull;
                     for (uint64_t mm = m; mm; mm &= mm - 1) {
+                        // the live group of bit bi (exact while <= 64 are pending; else recomputed below)
                         const uint32_t bi = (uint32_t)__builtin_ctzll(mm);
-                        const uint32_t t = pend[kPendDesc + 4 * bi] & 0xFFu, ls = pend[kPendDesc + 4 * bi + 3];
+                        const uint32_t *dp = pdesc(head + ((bi - head) & 63u));
+                        const uint32_t t = dp[0] & 0xFFu, ls = dp[3];
                         if (t == MT_OP_INSERT) ins_l = ls;
                         if (t == MT_OP_REMOVE) rem_l = ls;
                     }
@@ -2784,6 +2830,26 @@ struct Engine {
                 const bool inserted = !pins || ins_l <= L;
                 const bool not_removed = !sr_removed(sr) || (prem && rem_l != 0xFFFFFFFFu && rem_l > L);
                 contrib = inserted && not_removed ? len : 0u;
+            }
+            if (n_pend > 64) {
+                // more than 64 groups pending: mask bits are shared by groups 64 apart, so the
+                // segment's insert / remove groups and membership come from the entry lists
+                uint64_t pm = ballot(lane < n && (meta & kMetaPending));
+                while (pm) {
+                    const int f = first_lane(pm);
+                    pm &= pm - 1;
+                    const uint32_t sl = rdl(slot, f);
+                    const uint64_t mf = (uint64_t)rdl((uint32_t)m, f) | ((uint64_t)rdl((uint32_t)(m >> 32), f) << 32);
+                    const uint32_t il = group_lseq(sl, mf, MT_OP_INSERT), rl = group_lseq(sl, mf, MT_OP_REMOVE);
+                    const bool mem = in_group(head, sl, mf);
+                    if (lane == f) {
+                        const bool pins = (sr & 0xFFFFu) == kSeq16Unassigned, prem = (sr >> 16) == kSeq16Unassigned;
+                        const bool inserted = !pins || il <= L;
+                        const bool not_removed = !sr_removed(sr) || (prem && rl != 0xFFFFFFFFu && rl > L);
+                        contrib = inserted && not_removed ? len : 0u;
+                        member = mem;
+                    }
+                }
             }
             const uint32_t incl = scan8(contrib) + base;
             const uint32_t excl = incl - contrib;
@@ -2817,7 +2883,7 @@ struct Engine {
                     w[4] = op.payload;
                     w[5] = op.payload_len;
                 }
-                uint64_t nm = mask & ~(1ull << gb);
+                uint64_t nm = bit_free_after(head, sl, head, head) ? mask & ~(1ull << gb) : mask;
                 if (made) {
                     const uint32_t words = kRegenOpWords + (np != 0xFFFFFFFFu ? 2u * np : 0u);
                     if (used + words > (uint32_t)regen_cap) {
@@ -2841,8 +2907,7 @@ struct Engine {
                     }
                     const uint32_t ng = head + (uint32_t)n_pend;
                     if (lane == 0) {
-                        *(uint4 *)(pend + kPendDesc + 4 * (ng & 63u)) =
-                            make_uint4(T | ((uint32_t)op.flags << 16), op.payload, op.payload_len, L);
+                        *(uint4 *)pdesc(ng) = make_uint4(T | ((uint32_t)op.flags << 16), op.payload, op.payload_len, L);
                         pend[0] = (uint32_t)(n_pend + 1);
                     }
                     n_pend++;

@@ -270,6 +270,28 @@ def test_many_clients_with_overlapping_removes():
             b.ingest_messages([msgs])
 
 
+def test_collab_window_beyond_16_bit_seqs_is_flagged():
+    """The tables keep sequence numbers relative to minSeq in 16 bits (s_sr): a document
+    whose collab window (currentSeq - minSeq, held open by a client that never advances its refSeq)
+    reaches 65,520 ops stops with MT_CAPACITY, cap_kind 5, in every class — flagged, never wrong
+    (DESIGN §7); a window just below the limit replays bit-exact."""
+    def doc(n_noops):
+        msgs = [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"})]
+        msgs += [{"clientId": "B", "sequenceNumber": k, "referenceSequenceNumber": 1, "minimumSequenceNumber": 0,
+                  "type": "noop", "contents": None} for k in range(2, 2 + n_noops)]
+        msgs.append(_msg("B", 2 + n_noops, 1, {"type": 0, "pos1": 1, "seg": "X"}))
+        msgs.append(_msg("A", 3 + n_noops, 1, {"type": 1, "pos1": 0, "pos2": 2}))
+        return msgs
+    docs = [doc(65400), doc(65600)]
+    oracle = oracle_docs_from_messages(docs)
+    assert oracle[1].status == 0
+    with fa.ReplayBatch(2) as b:
+        b.ingest_messages(docs)
+        b.run()
+        assert_doc_parity(b.doc(0), oracle[0])
+        assert b.doc(1).status == fa.MT_CAPACITY and int(b.counters()["cap_kind"][1]) == 5
+
+
 def test_empty_documents_and_empty_inserts():
     docs = [[], [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": ""}), _msg("A", 2, 1, {"type": 0, "pos1": 0, "seg": "k"})]]
     oracle = oracle_docs_from_messages(docs)

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 GEN_KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
 ST_BAD_INPUT = 5  # mt_device.h: an assert of the reference (here: in the ack path)
-PEND_MAX_GROUPS = 64  # unacked local ops a GPU replica holds at once (mt_device.h kPendMaxGroups)
+PEND_MAX_GROUPS = 1024  # unacked local ops a GPU replica holds at once (mt_device.h kPendMaxGroups)
 GEN_VALUES = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
 
 
@@ -73,20 +73,65 @@ def _farm_parity(f, **opts):
         b.ingest_messages(docs, observer=names)
         b.run()
         for i, n in enumerate(names):
-            if max_pending(n, docs[i]) > PEND_MAX_GROUPS:
-                # the device's pending-group window (mt_device.h kPendMaxGroups): flagged, never wrong
-                assert fa.status_string(b.doc(i).status) == fa.status_string(4), n
-                continue
             assert_same(b.doc(i), f.docs[n], n)
         return b.stats()
+
+
+@pytest.mark.parametrize("seg_cap", [0, 64])
+def test_writer_with_hundreds_of_pending_ops(seg_cap):
+    """An offline burst / reconnect storm: writer A issues 300 local ops (inserts, removes,
+    annotates, rewrites; splits of pending segments) before its first ack while B and C edit and
+    sequence concurrently, then A catches up.  Beyond 64 pending groups the segments' mask bits are
+    shared by groups 64 apart (mt_device.h kPendMaxGroups) and the entry lists decide membership:
+    every replica equals the oracle's, also through checkpoint / resume with the groups in flight."""
+    from writer_sim import Farm, random_op
+
+    f = Farm(3, 77)
+    for i in range(300):
+        f.local("A", random_op(f.rng, f.docs["A"].length(), rewrite=10))
+        if i % 4 == 0:
+            o = f.rng.choice(["B", "C"])
+            f.local(o, random_op(f.rng, f.docs[o].length()))
+            f.deliver(o, 1 + f.rng.randrange(3))
+    f.finish()
+    assert max_pending("A", f.events["A"]) > 250
+    _farm_parity(f, **({"seg_cap": seg_cap, "max_retries": 24} if seg_cap else {}))
 
 
 @pytest.mark.parametrize("seed,n_clients,steps,rewrite", [(1, 3, 400, 0), (2, 6, 900, 10), (3, 8, 1500, 25)])
 def test_free_running_farm_writers(seed, n_clients, steps, rewrite):
     """Writers at their own pace (deep pending windows, remote ops on pending segments, the #1213
-    race): every writer's replica on the GPU equals the oracle's.  (No initial text: a message
-    stream carries no pre-collaboration content; the snapshot-load path covers that start.)"""
+    race): every writer's replica on the GPU equals the oracle's.  (Pre-collaboration text starts
+    from a snapshot: test_writer_replicas_starting_from_a_snapshot.)"""
     _farm_parity(farm(n_clients, steps, seed, rewrite=rewrite))
+
+
+def test_writer_replicas_starting_from_a_snapshot():
+    """Pre-collaboration text (what commit afa32c4 took out of the free-running farms): every replica
+    of a farm held "hello world" before collaborating.  Each writer's GPU replica starts from the
+    SnapshotV1 of that state (snapshotLoader.ts:36-205, the host JSON parser's {"snapshot",
+    "messages"} form) and replays its own stream — local ops, acks, remote ops, rewrites — equal to
+    the oracle replica loaded the same way, whose text and digest equal the farm replica's (that
+    one inserted the text locally before startOrUpdateCollaboration)."""
+    d = O.Doc()
+    d.insert_local(0, json.dumps("hello world"))
+    blobs = d.snapshot_v1()
+    for f in (farm(4, 700, 31, initial="hello world", rewrite=10), round_farm(3, 25, 32, initial="hello world")):
+        for n in f.names:
+            od = O.Doc()
+            assert od.load_snapshot(blobs, n) == 0
+            for m in f.events[n]:
+                if m["sequenceNumber"] == -1:
+                    assert od.local_op(m["contents"]) == 0
+                elif od.apply_msg(json.dumps(m)) != 0:
+                    break
+            if f.docs[n].status == 0:
+                assert od.text() == f.docs[n].text() and od.digest() == f.docs[n].digest(), n
+            with fa.ReplayBatch(1) as b:
+                assert b.ingest_json([json.dumps({"snapshot": blobs, "messages": f.events[n]})], observer=n,
+                                     device="host")["path"] == "host"
+                b.run()
+                assert_same(b.doc(0), od, n)
 
 
 @pytest.mark.parametrize("seed,n_clients,rounds", [(5, 4, 40), (6, 8, 30)])
@@ -353,6 +398,49 @@ def test_regenerate_pending_ops_on_gpu():
             for i, n in enumerate(names):
                 assert_same(b.doc(i), docs[n], n)
                 assert b.doc(i).regenerated_ops() == docs[n].regenerated_ops(), n
+
+
+def test_regenerate_with_more_than_64_pending_groups():
+    """regeneratePendingOp over 130 pending local ops (reconnect with a deep queue): 110 inserts at
+    random places, removes and annotates over them, every one regenerated (each regenerated op a new
+    group with the original localSeq) and then acked — GPU == oracle on the regenerated ops and the
+    final state."""
+    import random
+
+    rng = random.Random(5)
+
+    def local(op):
+        return {"clientId": "W", "sequenceNumber": -1, "referenceSequenceNumber": 0,
+                "minimumSequenceNumber": 0, "type": "op", "contents": op}
+
+    def regen(op):
+        return {"clientId": "W", "sequenceNumber": -1, "type": "regenerate", "contents": op}
+
+    ops, length = [], 0
+    for i in range(130):
+        if i < 110 or length < 4:
+            op = {"type": 0, "pos1": rng.randrange(length + 1), "seg": "ab"[: 1 + rng.randrange(2)]}
+            length += len(op["seg"])
+        else:
+            a = rng.randrange(length - 1)
+            op = {"type": 1 + (i % 2), "pos1": a, "pos2": a + 1 + rng.randrange(3)}
+            if op["type"] == 2:
+                op["props"] = {"k": i}
+            else:
+                length -= op["pos2"] - a
+        ops.append(op)
+    ev = [local(o) for o in ops] + [regen(o) for o in ops]
+    od = oracle_replica("W", ev)
+    assert od.status == 0 and od.pending_groups() > 100
+    acks = [{"clientId": "W", "sequenceNumber": k + 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+             "type": "op", "contents": op} for k, op in enumerate(od.regenerated_ops())]
+    full = ev + acks
+    od2 = oracle_replica("W", full)
+    with fa.ReplayBatch(1) as b:
+        b.ingest_messages([full], observer=["W"])
+        b.run()
+        assert b.doc(0).regenerated_ops() == od.regenerated_ops()
+        assert_same(b.doc(0), od2, "regenerate")
 
 
 def test_reset_pending_segments_to_op_kats_on_gpu():
