@@ -23,6 +23,7 @@ for step in "$@"; do
     giant1m) run giant1m 600 python -u -m pytest tests/test_gpu_parity.py -k "million_segments" -x -v -s --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     hbmphases) run hbmphases 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u tools/hbm_phases.py 100000 8 ;;
     hbmrate) run hbmrate 600 python -u tools/hbm_phases.py 100000 8 ;;
+    hbmrate_nocache) run hbmrate_nocache 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_nocache.so python -u tools/hbm_phases.py 100000 8 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;

@@ -141,7 +141,7 @@ const docs = [[msg('A', 1, 0, { type: 0, pos1: 0, seg: 'hello world' }),
               [msg('C', 1, 0, { type: 0, pos1: 0, seg: { text: 'xyz', props: { k: 'v' } } })]];
 const g = new ReplayBatch(2), h = new ReplayBatch(2), f = new ReplayBatch(1);
 const pg = g.ingestJson(docs, 0, 'gpu'), ph = h.ingestJson(docs, 0, 'host');
-const pf = f.ingestJson([[msg('A', 1, 0, { type: 0, pos1: 0, seg: { text: 'a', props: { n: 1.5 } } })]]);
+const pf = f.ingestJson([[msg('A', 1, 0, { type: 0, pos1: 0, seg: { text: 'a', props: { '1': 1 } } })]]);  // an array-index key: JS key order, the host parser
 g.run(); h.run(); f.run();
 const dg = g.deviceDigests(), dh = h.deviceDigests();
 // a document count that differs from the batch's is refused by the wrapper and by the C ABI
