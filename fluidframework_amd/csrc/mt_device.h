@@ -291,8 +291,7 @@ constexpr Layout make_glayout() {
     L.bacc = o;    o = lds_align(o + 4u * K);
     L.bep = o;     o = lds_align(o + 4u * K);
     L.sr = o;      o = lds_align(o + 4u * kGiantChainRec * kGiantUlist);  // the overlay's chain records
-    L.meta = o;    o = lds_align(o + 4u * 4);  // the last descent's HBM path (chain hints)
-    L.len = L.sblk = o;  // in HBM (make_layout)
+    L.len = L.meta = L.sblk = o;  // in HBM (make_layout)
     L.bytes = o;
     return L;
 }

@@ -216,12 +216,8 @@ struct Engine {
     // giant class: the HBM-resident blocks the last overlay added into (kGiantChainRec per overlay
     // list entry, kNoBlk-padded); their b_acc is zeroed before the next overlay, so HBM b_acc needs
     // no epoch tags (a zero invariant between overlays) and the adds are fire-and-forget atomics
-    MT_AS_LDS uint32_t *g_rec;  // ds_* accesses: a flat one would wait for the wave's HBM traffic
+    uint32_t *g_rec;
     int32_t g_nrec;
-    // giant class: the HBM blocks on the last descent's path above its leaf block (leaf block,
-    // parent, grandparent while they have HBM ids; kNoBlk-padded) and `splits` at that time: the
-    // chain hint of a segment the op adds to the overlay list in that block
-    MT_AS_LDS uint32_t *g_path;
     uint32_t *scratch;  // 128 words
     // ---- uniform scalars
     int32_t slot_top, free_head, free_n, blk_top, n_bfree, bfree_head, root, depth, hn, nu;
@@ -300,10 +296,7 @@ struct Engine {
         }
         h_ent = (uint2 *)(xb + xl.heap);
         scratch = (uint32_t *)(xb + xl.scratch);
-        if constexpr (kGiant) {
-            g_rec = (MT_AS_LDS uint32_t *)(lb + glay.sr);  // make_glayout: the chain records
-            g_path = (MT_AS_LDS uint32_t *)(lb + glay.meta);
-        }
+        if constexpr (kGiant) g_rec = (uint32_t *)(lb + glay.sr);  // make_glayout: the chain records
         uint32_t *hw = (uint32_t *)(xb + xl.hdr);
         pay_end.p = hw + 0;
         arena_base.p = hw + 1;
@@ -543,7 +536,6 @@ struct Engine {
         ov_epoch = 0;
         if constexpr (kGiant) {  // once per launch: LDS epochs, and the zero invariant of HBM b_acc
             for (int32_t i = lane; i < kGiantLdsBlocks; i += kWave) b_ep.lds[i] = 0xFFFFFFFFu;
-            if (lane < 4) g_path[lane] = kNoBlk;  // no descent yet (splits is never 0xFFFFFFFF)
             g_nrec = 0;
             giant_clear_acc(true);
         } else if constexpr (kHbm) {  // once per launch: the tables are uninitialised device memory
@@ -566,8 +558,8 @@ struct Engine {
             for (int32_t i = kGiantLdsBlocks + lane; i < cap.blk; i += kWave) b_acc.p[i] = 0u;
         } else {
             for (int32_t i = lane; i < g_nrec; i += kWave) {
-                const uint32_t r = g_rec[i];  // a record may also hold a hint: only live HBM ids
-                if (r >= (uint32_t)kGiantLdsBlocks && r < (uint32_t)blk_top) b_acc.p[r] = 0u;
+                const uint32_t r = g_rec[i];
+                if (r != kNoBlk) b_acc.p[r] = 0u;
             }
         }
         g_nrec = 0;
@@ -589,16 +581,12 @@ struct Engine {
         int32_t w = 0;
         for (int32_t g0 = 0; g0 < nu; g0 += 4 * kWave) {
             uint32_t slot[4], vlen[4], b[4], nh[4];
-            uint4 rec[4];
             bool act[4];
             int32_t wk[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int32_t j = g0 + k * kWave + lane;
                 slot[k] = j < nu ? (uint32_t)u_list[j] : 0xFFFFFFFFu;
-                // the entry's chain record (the HBM blocks its last overlay added into, or a hint)
-                rec[k] = make_uint4(kNoBlk, kNoBlk, kNoBlk, kNoBlk);
-                if (j < nu) rec[k] = rec_load(j);
             }
             uint32_t meta[4];
 #pragma unroll
@@ -615,60 +603,17 @@ struct Engine {
 #pragma unroll
             for (int k = 0; k < 4; k++)
                 if (act[k]) u_list[wk[k]] = (Idx)slot[k];
-            // one round of independent HBM loads per entry: its fields, its leaf block and the
-            // parents of its recorded chain blocks; the record is the entry's chain when every link
-            // still holds (leaf block, then parent by parent up to an LDS block or the root)
-            uint32_t pq[4][4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 vlen[k] = 0;
                 b[k] = kNoBlk;
                 nh[k] = 0;
-                const uint32_t cq[4] = {rec[k].x, rec[k].y, rec[k].z, rec[k].w};
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-#ifdef MT_NO_CHAIN_CACHE
-                    const bool hbm = false;
-#else
-                    const bool hbm = cq[q] >= (uint32_t)kGiantLdsBlocks && cq[q] < (uint32_t)blk_top;
-#endif
-                    pq[k][q] = act[k] && hbm ? (uint32_t)b_parent.p[cq[q]] : kNoBlk;
-                }
                 if (act[k]) {
                     bool tie;
                     view_of(slot[k], ref, c, vlen[k], tie);
                     b[k] = s_blk[slot[k]];
                 }
                 act[k] = act[k] && vlen[k] > 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t cq[4] = {rec[k].x, rec[k].y, rec[k].z, rec[k].w};
-                uint32_t n = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (n == (uint32_t)q && cq[q] >= (uint32_t)kGiantLdsBlocks && cq[q] < (uint32_t)blk_top) n++;
-                bool ok = n > 0 && b[k] == cq[0];
-                uint32_t top = kNoBlk;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if ((uint32_t)q + 1 < n) ok = ok && pq[k][q] == cq[q + 1];
-                    if ((uint32_t)q + 1 == n) top = pq[k][q];
-                }
-                ok = ok && (top == kNoBlk || top < (uint32_t)kGiantLdsBlocks);
-#ifdef MT_NO_CHAIN_CACHE
-                ok = false;
-#endif
-                if (act[k] && ok) {
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        if ((uint32_t)q < n) {
-                            __hip_atomic_fetch_add(&b_acc.p[cq[q]], vlen[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                            g_rec[wk[k] * kGiantChainRec + q] = cq[q];
-                        }
-                    nh[k] = n;
-                    b[k] = top;  // the walk below continues in LDS
-                }
             }
             for (int32_t l = 0; l < depth; l++) {
 #pragma unroll
@@ -700,12 +645,8 @@ struct Engine {
             bool over = false;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                if (wk[k] >= 0 && !act[k]) {
-                    // invisible in this view (nothing added): the record stays as the next hint
-                    rec_store(wk[k], rec[k]);
-                } else if (wk[k] >= 0) {
-                    for (uint32_t q = nh[k]; q < (uint32_t)kGiantChainRec; q++) g_rec[wk[k] * kGiantChainRec + q] = kNoBlk;
-                }
+                if (wk[k] >= 0)
+                    for (uint32_t q = act[k] ? nh[k] : 0u; q < (uint32_t)kGiantChainRec; q++) g_rec[wk[k] * kGiantChainRec + q] = kNoBlk;
                 over |= act[k] && nh[k] > (uint32_t)kGiantChainRec;
             }
             if (ballot(over)) cap_fail(1);  // more HBM blocks on a chain than recorded: the HBM class
@@ -716,34 +657,14 @@ struct Engine {
         wsync();
     }
 
-    MT_FI uint4 rec_load(int32_t pos) const {
-        const MT_AS_LDS uint32_t *r = g_rec + pos * kGiantChainRec;
-        return make_uint4(r[0], r[1], r[2], r[3]);
-    }
-    MT_FI void rec_store(int32_t pos, uint4 v) {
-        MT_AS_LDS uint32_t *r = g_rec + pos * kGiantChainRec;
-        r[0] = v.x;
-        r[1] = v.y;
-        r[2] = v.z;
-        r[3] = v.w;
-    }
-    MT_FI void u_push(uint32_t slot, int32_t blk) {
+    MT_FI void u_push(uint32_t slot) {
         if (nu >= cap.ulist) {
             cap_fail(1);
             return;
         }
-        if constexpr (kGiant) chain_hint(nu, blk);
         u_list[nu] = (Idx)slot;
         nu++;
         if (nu > max_u) max_u = nu;
-    }
-    // giant class: the chain record of a new overlay-list entry at `pos` in leaf block blk — the
-    // last descent's path when it ended there and no block split since, else unknown (kNoBlk); the
-    // next overlay validates it either way.  Positions below g_nrec hold the dirty records.
-    MT_FI void chain_hint(int32_t pos, int32_t blk) {
-        if (pos * kGiantChainRec < g_nrec) return;
-        const bool ok = (uint32_t)blk == g_path[0] && (int32_t)g_path[3] == splits;
-        if (lane < kGiantChainRec) g_rec[pos * kGiantChainRec + lane] = ok && lane < 3 ? g_path[lane] : kNoBlk;
     }
 
     // Per-op overlay: b_acc[B] = sum of nodeLength(refSeq, c) over the unsettled segments under
@@ -812,17 +733,11 @@ struct Engine {
         PF_SCOPE(11);
         int32_t w = 0;
         const uint32_t m16 = (uint32_t)(min_seq - sbase);
-        // giant class: the overlay is recomputed after this (ov_splits = -1), so its HBM
-        // accumulators are zeroed now and the chain records move with their entries as hints
-        if constexpr (kGiant) giant_clear_acc(false);
         wsync();
         for (int32_t b0 = 0; b0 < nu; b0 += kWave) {
             const int32_t j = b0 + lane;
             const bool in = j < nu;
             const uint32_t slot = in ? (uint32_t)u_list[j] : 0u;
-            uint4 rec = make_uint4(kNoBlk, kNoBlk, kNoBlk, kNoBlk);
-            if constexpr (kGiant)
-                if (in) rec = rec_load(j);
             bool valid = false, elig = false;
             uint32_t meta = 0, add = 0, b = 0, sr = 0;
             if (in) {
@@ -841,7 +756,6 @@ struct Engine {
             wsync();
             if (keep) {
                 u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (Idx)slot;
-                if constexpr (kGiant) rec_store(w + __popcll(km & ((1ull << lane) - 1ull)), rec);
                 const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
                 uint32_t nq = q16 > m16 ? q16 - m16 : 0u;
                 uint32_t nr = r16 == kSeq16None ? kSeq16None : (r16 > m16 ? r16 - m16 : 0u);
@@ -887,10 +801,7 @@ struct Engine {
         const bool lanes8 = lane < kMaxNodes;
         int32_t n = b_count[N];
         uint32_t row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;
-        int32_t up1 = -1, up2 = -1;  // the path's two blocks above N
         for (int32_t l = 0; l + 1 < depth; l++) {
-            up2 = up1;
-            up1 = N;
             const uint32_t myc = (uint32_t)__shfl((int)row, lane >> 3, kWave);
             const bool cin = (lane >> 3) < n;
             const uint32_t nrow = cin ? (uint32_t)b_child[myc * 8 + (lane & 7)] : 0u;
@@ -912,13 +823,6 @@ struct Engine {
         W.blk = N;
         W.n = n;
         W.base = base;
-        {  // the chain hint: the HBM-id prefix of leaf block, parent, grandparent
-            const bool h0 = N >= kGiantLdsBlocks, h1 = h0 && up1 >= kGiantLdsBlocks, h2 = h1 && up2 >= kGiantLdsBlocks;
-            if (lane < 4)
-                g_path[lane] = lane == 0 ? (h0 ? (uint32_t)N : kNoBlk)
-                             : lane == 1 ? (h1 ? (uint32_t)up1 : kNoBlk)
-                             : lane == 2 ? (h2 ? (uint32_t)up2 : kNoBlk) : (uint32_t)splits;
-        }
         if (strict) return W;
         uint32_t vlen = 0;
         bool tie = false;
@@ -1285,7 +1189,7 @@ struct Engine {
         s_meta[ns] = meta;  // inherits ends-NL of the tail, linked, unsettled
         s_len[slot] = (Len)r;
         wsync();
-        if (meta & kMetaUnsettled) u_push((uint32_t)ns, blk);
+        if (meta & kMetaUnsettled) u_push((uint32_t)ns);
         if constexpr (kW) {
             // segmentGroups.copyTo (mergeTree.ts:560): the right half joins every group of the
             // segment, oldest first, at the end of each group's segments; its cold record (written
@@ -2011,7 +1915,6 @@ struct Engine {
         uint32_t meta = 0, len = 0, sr = 0;
         uint4 cr = make_uint4(0, 0, 0, 0);
         if (in) {
-            cr = cold[2 * slot];  // HBM: waited on only where props or merges need it
             sr = s_sr[slot];
             meta = s_meta[slot];
             len = s_len[slot];
@@ -2037,11 +1940,20 @@ struct Engine {
         uint64_t pairM = ballot(pair && noprops);
         const uint64_t withM = ballot(pair && !noprops);
         const uint64_t longM = ballot(in && len > kGranularity);
+        // the cold records (HBM) only of the leaves a candidate pair involves, both sides — every
+        // read below (prop sets, the append heads and tails) is of such a leaf; each record is its
+        // own 128-byte line (measured: 6 % of the replay's fetched bytes)
+        {
+            const uint64_t allP = pairM | withM;
+            if ((((allP | (allP >> 1)) >> lane) & 1ull) != 0ull) cr = cold[2 * slot];
+        }
         bool serial = false;
         if (withM) {
             const uint32_t props = cr.x, ph = props ? pool[props + 1] : 0u;
             // an irregular set (a value matching across structural classes) makes matchProperties
-            // intransitive: decide the chains serially against their heads, as scourNode does
+            // intransitive: decide the chains serially against their heads, as scourNode does (only
+            // leaves in a pair carry their set here: a chain without an irregular set merges the
+            // same pairwise as serially)
             serial = ballot(cand && props != 0u && !(ph & 1u)) != 0;
             if (!serial) {
                 const uint32_t pprev = __shfl_up(props, 1, kWave), hprev = __shfl_up(ph, 1, kWave);
@@ -2417,7 +2329,7 @@ struct Engine {
             }
             s_meta[slot] = meta;
             wsync();
-            if (!settled) u_push((uint32_t)slot, W.blk);
+            if (!settled) u_push((uint32_t)slot);
             int32_t blk = insert_leaf(W.blk, W.k, (uint32_t)slot);
             if (status) return;
             if (settled) {
@@ -2573,10 +2485,6 @@ struct Engine {
                 s_meta[slot] = meta | kMetaUnsettled;
                 u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (Idx)slot;
             }
-            if constexpr (kGiant) {
-                wsync();
-                for (uint64_t mm = um; mm; mm &= mm - 1) chain_hint(nu + __popcll(um & ((1ull << first_lane(mm)) - 1ull)), -1);
-            }
             nu += __popcll(um);
             if (nu > max_u) max_u = nu;
             chain_add(b_slen, add > 0u, b, add);
@@ -2615,27 +2523,13 @@ struct Engine {
         const int32_t ref = op.ref_seq;
         const uint32_t start = (uint32_t)op.pos1, end = (uint32_t)op.pos2;
         ov_splits = -1;
+        boundary(start, ref, c);
+        if (status) return;
+        boundary(end, ref, c);
+        if (status) return;
         // nodeMap visits leaves with vlen > 0 and E < end and P > start: none when end <= start
-        // (both boundaries were cut, so no leaf can straddle them).  Giant / HBM classes (every
-        // descent level a dependent HBM round trip, registers to spare): with no block split since
-        // the first boundary's walk, its leaf block and base still hold (a leaf split moves no block
-        // start) and the overlay is unchanged, so nodeMap's walk starts there — at the first block
-        // whose view length reaches start; the blocks before the strict descent's one end at start
-        // and hold no leaf the walk applies to
-        if constexpr (kHbm) {
-            const int32_t s0 = splits;
-            const Walk W1 = boundary(start, ref, c);
-            if (status) return;
-            boundary(end, ref, c);
-            if (status) return;
-            if (end > start) range_walk(op, start, end, splits == s0 && W1.blk >= 0 ? &W1 : nullptr);
-        } else {
-            boundary(start, ref, c);
-            if (status) return;
-            boundary(end, ref, c);
-            if (status) return;
-            if (end > start) range_walk(op, start, end, nullptr);
-        }
+        // (both boundaries were cut, so no leaf can straddle them)
+        if (end > start) range_walk(op, start, end);
         resolve_splits();
         if (kW && op.seq == kUnassignedSeq) return;  // a local op: no zamboni (mergeTree.ts:2600, 2713)
         zamboni();
@@ -2701,12 +2595,12 @@ struct Engine {
         }
     }
 
-    MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end, const Walk *from) {
+    MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end) {
         const uint32_t c = op.client;
         const int32_t ref = op.ref_seq;
         resolve_cold();  // the walk reads / updates cold records of split halves
         ensure_overlay(ref, c);
-        const Walk W = from ? *from : descend(start, ref, c, true);
+        Walk W = descend(start, ref, c, true);
         PF_SCOPE(4);
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = (op.flags & MT_OPF_REWRITE) != 0;
@@ -2763,10 +2657,6 @@ struct Engine {
                     if (newu) {
                         s_meta[slot] = meta | kMetaUnsettled;
                         u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (Idx)slot;
-                    }
-                    if constexpr (kGiant) {
-                        wsync();
-                        for (uint64_t mm = um; mm; mm &= mm - 1) chain_hint(nu + __popcll(um & ((1ull << first_lane(mm)) - 1ull)), blk);
                     }
                     nu += __popcll(um);
                     if (nu > max_u) max_u = nu;

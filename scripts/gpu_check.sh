@@ -23,6 +23,12 @@ for step in "$@"; do
     giant1m) run giant1m 600 python -u -m pytest tests/test_gpu_parity.py -k "million_segments" -x -v -s --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     hbmphases) run hbmphases 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u tools/hbm_phases.py 100000 8 ;;
     hbmrate) run hbmrate 600 python -u tools/hbm_phases.py 100000 8 ;;
+    hbmrate_base) run hbmrate_base 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_base.so python -u tools/hbm_phases.py 100000 8 ;;
+    hbmrate_rangeonly) run hbmrate_rangeonly 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_rangeonly.so python -u tools/hbm_phases.py 100000 8 ;;
+    b3s_lazy) run b3s_lazy 600 python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
+    b3s_eager) run b3s_eager 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_eagercold.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
+    f3s_lazy) run f3s_lazy 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/f3s_lazy -o run -- python3 -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
+    f3s_eager) run f3s_eager 180 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_eagercold.so rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/f3s_eager -o run -- python3 -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     hbmrate_nocache) run hbmrate_nocache 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_nocache.so python -u tools/hbm_phases.py 100000 8 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
