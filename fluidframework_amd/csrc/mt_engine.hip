@@ -123,6 +123,7 @@ struct Walk {
     uint32_t base;  // view position of the block start
     uint32_t excl;  // insert mode: view position before child k
     int32_t ok;     // insert mode: the walk found an insertion point
+    uint32_t slot;  // insert mode, giant class: the slot of child k (k < n), from the walk's leaf row
 };
 
 // A per-document scalar kept in LDS instead of a scalar register: the engine's rarely used state
@@ -796,6 +797,7 @@ struct Engine {
         W.base = 0;
         W.excl = 0;
         W.ok = 0;
+        W.slot = 0;
         int32_t N = root;
         uint32_t base = 0;
         const bool lanes8 = lane < kMaxNodes;
@@ -835,6 +837,7 @@ struct Engine {
             W.k = f;
             W.excl = rdl(excl, f);
             W.ok = 1;
+            W.slot = rdl(row, f);
         } else {
             const uint32_t end = n > 0 ? rdl(incl, n - 1) : base;
             W.k = n;
@@ -854,6 +857,7 @@ struct Engine {
         W.base = 0;
         W.excl = 0;
         W.ok = 0;
+        W.slot = 0;
         int32_t N = root;
         uint32_t base = 0;
         const bool lanes8 = lane < kMaxNodes;
@@ -1154,9 +1158,10 @@ struct Engine {
     // record is read now and written back in resolve_cold(); a second split of the same op
     // forwards the first one's pending records instead of reading HBM.
     // Returns the leaf block the right half landed in (-1: no split).
-    MT_FI int32_t split_at(int32_t blk, int32_t k, uint32_t r) {
+    MT_FI int32_t split_at(int32_t blk, int32_t k, uint32_t r, uint32_t slot_hint) {
         PF_SCOPE(2);
-        const uint32_t slot = rfl((uint32_t)b_child[blk * 8 + k]);
+        // the giant class takes the slot from the walk's leaf row (an HBM re-read otherwise)
+        const uint32_t slot = kGiant ? slot_hint : rfl((uint32_t)b_child[blk * 8 + k]);
         const uint32_t meta = s_meta[slot];
         if (meta & kMetaMarker) return -1;  // Marker.createSplitSegmentAt returns undefined
         // the slot's two cold records, lane-distributed (lane i < 8: word i)
@@ -1246,7 +1251,7 @@ struct Engine {
         Walk W = descend(pos, ref, c, false);
         if (W.blk >= 0 && W.ok && W.k < W.n && W.excl < pos) {
             const int32_t s0 = splits;
-            const int32_t nb = split_at(W.blk, W.k, pos - W.excl);
+            const int32_t nb = split_at(W.blk, W.k, pos - W.excl, W.slot);
             if (status) return W;
             if (splits == s0) {
                 // no block split: the left half ends at pos, the right half (k + 1) starts there
@@ -2233,9 +2238,13 @@ struct Engine {
             if (key == kHeapInvalid) continue;  // the segment was merged away / unlinked: parent undefined
             const uint32_t slot = key;
             const int32_t blk = s_blk[slot];
-            if (b_scour[blk] == kScourFalse) continue;
+            // the block's scour state, child count and row loaded together (one round in the giant
+            // class, whose leaf blocks are in HBM)
+            const int8_t sc = b_scour[blk];
             const int32_t cnt = b_count[blk];
-            const uint32_t cs = lane < cnt ? (uint32_t)b_child[blk * 8 + lane] : 0u;
+            const uint32_t row = lane < kMaxNodes ? (uint32_t)b_child[blk * 8 + lane] : 0u;
+            if (sc == kScourFalse) continue;
+            const uint32_t cs = lane < cnt ? row : 0u;
             uint32_t *hold = scratch;
             const int32_t nk = scour(cs, cnt, 1ull, hold);
             if (status) return;
