@@ -28,7 +28,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md: 8.0 TB/s spec)
-LDS_PEAK_GBS = 150000.0  # MI355X_MICROARCH.md §LDS: ~150 TB/s aggregate (256 B/clk/CU, 256 CUs, ~2.4 GHz)
+N_CUS, CLOCK_GHZ = 256, 2.4  # MI355X_MICROARCH.md: 256 CUs, ~2.4 GHz shader clock
 
 CONFIGS = {
     2: dict(docs=4096, ops=2000, n_clients=8, max_lag=32, pct_insert=60, pct_remove=40,
@@ -238,7 +238,7 @@ def main():
     achieved_gbs = first_bytes / (avg_first_ms * 1e-3) / 1e9
     kname = f"mt_{'writer' if args.writers else 'replay'}_kernel_{dom_class}"
     traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, kname)
-    lds = lds_roofline(args.config, n_docs, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
+    lds = lds_busy(args.config, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
@@ -285,7 +285,7 @@ def main():
                          "algorithmic_bytes_formula": "32 B/op record + 2 B/inserted code unit + 8 B/prop record "
                                                       "+ 32 B/final table entry (DESIGN.md §5)",
                          "ops_per_launch": int(sum(first_ops) / len(first_ops)),
-                         "lds": lds},
+                         "lds_busy": lds},
             "replay_ms_per_step": round(avg_kernel_ms, 3),
             "launches": b.launches(),
             "cpu_baseline": cpu,
@@ -429,12 +429,14 @@ def gather_summaries(b, torch, dist, world, rank, backend):
     return {"bytes": int(sum(int(r.numel()) for r in recv)), "ranks": len(recv), "rank0_roundtrip_equal": ok}
 
 
-def lds_roofline(config, n_docs, n_ops, kernel, avg_ms, ops_per_launch):
-    """LDS roofline of the dominant kernel from the committed rocprofv3 counter passes of this same
-    configuration (tools/pmc_counters.py -> profiles/pmc_counters_config<N>.json): LDS bytes moved
-    per op (SQ_INSTS_LDS wave-instructions x 256 B, the LDS width per array cycle, over the
-    LDS-array cycles actually used) over the launch time measured live here, against ~150 TB/s
-    (MI355X_MICROARCH.md §LDS: 256 B/clk/CU x 256 CUs x ~2.4 GHz).  None without a matching profile."""
+def lds_busy(config, n_ops, kernel, avg_ms, ops_per_launch):
+    """How busy the dominant kernel keeps the LDS arrays, from the committed rocprofv3 counter passes
+    of this same configuration (tools/pmc_counters.py -> profiles/pmc_counters_config<N>.json):
+    SQ_LDS_IDX_ACTIVE (LDS-array cycles, bank-conflict cycles included) per op x the ops of one
+    launch, over the launch time measured live here x 256 CUs x ~2.4 GHz.  A utilisation, not bytes
+    moved; the bank-conflict share is SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+    (MI355X_MICROARCH.md: BANK_CONFLICT = extra cycles, IDX_ACTIVE = all LDS-array cycles).
+    None without a matching profile."""
     path = ROOT / "profiles" / f"pmc_counters_config{config}.json"
     try:
         prof = json.loads(path.read_text())
@@ -443,13 +445,15 @@ def lds_roofline(config, n_docs, n_ops, kernel, avg_ms, ops_per_launch):
     k = prof.get("kernels", {}).get(kernel)
     if not k or prof.get("ops") != n_ops:
         return None
-    per_op = k.get("lds_bytes_per_op")
-    if not per_op:
+    per = k.get("per_op") or {}
+    act, conf = per.get("SQ_LDS_IDX_ACTIVE"), per.get("SQ_LDS_BANK_CONFLICT")
+    if not act:
         return None
-    ach = per_op * ops_per_launch / (avg_ms * 1e-3) / 1e9
-    return {"achieved": round(ach, 3), "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": round(ach / LDS_PEAK_GBS, 6),
-            "bytes_per_op": per_op, "source": str(path.relative_to(ROOT)),
-            "counters_per_op": k.get("per_op")}
+    cu_cycles = avg_ms * 1e-3 * CLOCK_GHZ * 1e9 * N_CUS
+    return {"frac": round(act * ops_per_launch / cu_cycles, 6), "lds_cycles_per_op": act,
+            "bank_conflict_cycles_per_op": conf,
+            "bank_conflict_share": round(conf / act, 4) if conf is not None else None,
+            "source": str(path.relative_to(ROOT)), "counters_per_op": per}
 
 
 if __name__ == "__main__":

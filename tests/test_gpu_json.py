@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import fluidframework_amd as fa
+import oracle_ffi as O
 from fluidframework_amd.mtreplay import NotOnGpuPath, PackedJson, PackedJsonGpu
 from kat_util import load_kats
 from test_json_ingest import _farm_messages, _msg
@@ -189,6 +190,41 @@ def test_gpu_ingest_replays_like_host_ingest():
         g.run()
         h.run()
         _replay_equal(g, h, len(docs))
+
+
+def test_gpu_ingest_replays_canonicalized_values_and_many_clients():
+    """Annotates whose values the host canonicalizes (floats, objects, escapes) and a document of
+    700 writers (client ids beyond 8 bits) replay on the GPU-ingested batch exactly like the
+    host-ingested one: same digests, text, property runs and snapshots."""
+    ins = ('{"clientId":"Z","sequenceNumber":1,"referenceSequenceNumber":0,"minimumSequenceNumber":0,'
+           '"type":"op","contents":{"type":0,"pos1":0,"seg":"abcdef"}}')
+    canon_msgs = [ins] + [_ANN.replace('"referenceSequenceNumber":0', '"referenceSequenceNumber":1') % (i + 2, v)
+                          for i, v in enumerate(CANON_VALUES)]
+    canon = "[" + ",".join(canon_msgs) + "]"
+    crowd = [_msg(f"writer-{i}", i + 1, i, {"type": 0, "pos1": i % (i + 1), "seg": chr(65 + i % 26)})
+             for i in range(700)]
+    crowd += [_msg(f"writer-{i}", 701 + k, 700 + k, {"type": 2, "pos1": i, "pos2": i + 2, "props": {"w": i * 0.5}})
+              for k, i in enumerate(range(0, 600, 7))]
+    texts = [canon, json.dumps(crowd), canon]
+    want = []
+    for msgs in (canon_msgs, [json.dumps(m) for m in crowd], canon_msgs):  # the oracle's JSON path
+        ref = O.Doc()
+        ref.start_collab("readonly")
+        for m in msgs:
+            assert ref.apply_msg(m) == 0, ref.error
+        want.append((ref.digest(), ref.props_runs()))
+    with fa.ReplayBatch(len(texts)) as g, fa.ReplayBatch(len(texts)) as h:
+        assert g.ingest_json(texts, device="gpu")["path"] == "gpu"
+        h.ingest_json(texts, device="host")
+        g.run()
+        h.run()
+        for d in range(len(texts)):
+            x, y = g.doc(d), h.doc(d)
+            assert x.status == y.status == 0, d
+            assert x.digest() == y.digest() == want[d][0]
+            assert x.get_text() == y.get_text()
+            assert x.props_runs() == y.props_runs() == want[d][1]
+            assert x.snapshot_v1() == y.snapshot_v1()
 
 
 def test_gpu_ingest_from_device_resident_json():
