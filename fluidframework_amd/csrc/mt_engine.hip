@@ -47,6 +47,15 @@ namespace mt {
 
 #define MT_FI __device__ __attribute__((always_inline)) inline
 
+// 1: the LDS classes also descend with descend_giant's walk (every child's row loaded in the round
+// that loads the children's lengths: one dependent LDS round trip per level instead of two).
+// Measured slower there (config 3, 8,192 documents, same box: 118.2M vs 122.5M ops/s — eight
+// times the LDS reads per level, and the row permute, outweigh the round trip saved in LDS), so
+// only the giant class, whose lower levels are HBM round trips, uses it.
+#ifndef MT_DESCENT_ONE_ROUND
+#define MT_DESCENT_ONE_ROUND 0
+#endif
+
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int32_t rfl(int32_t x) { return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)x); }
 __device__ __forceinline__ uint32_t rdl(uint32_t x, int l) { return __builtin_amdgcn_readlane(x, l); }
@@ -849,7 +858,7 @@ struct Engine {
 
     MT_FI Walk descend(uint32_t pos, int32_t ref, uint32_t c, bool strict) {
         PF_SCOPE(1);
-        if constexpr (kGiant) return descend_giant(pos, ref, c, strict);
+        if constexpr (kGiant || MT_DESCENT_ONE_ROUND) return descend_giant(pos, ref, c, strict);
         Walk W;
         W.blk = -1;
         W.k = 0;
@@ -2593,11 +2602,16 @@ struct Engine {
                 if (closes) *closes = up;
                 return -1;
             }
-            int32_t i = child_index(p, b);
-            if (i + 1 < (int32_t)b_count[p]) {
+            // child_index with the row kept: the next sibling comes from the same load
+            const int32_t n = b_count[p];
+            const uint32_t row = lane < n ? (uint32_t)b_child[p * 8 + lane] : kNoBlk;
+            const uint64_t hm = ballot(row == (uint32_t)b);
+            const int32_t i = hm ? first_lane(hm) : -1;
+            if (i + 1 < n) {
                 if (closes) *closes = up;
-                b = b_child[p * 8 + i + 1];
-                while (!b_leaf[b]) b = b_child[b * 8];
+                b = (int32_t)rdl(row, i + 1);
+                // every leaf is at depth 0: `up` levels down the left edge
+                for (int32_t d = 0; d < up; d++) b = b_child[b * 8];
                 return b;
             }
             b = p;

@@ -27,6 +27,8 @@ for step in "$@"; do
     hbmrate_rangeonly) run hbmrate_rangeonly 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_rangeonly.so python -u tools/hbm_phases.py 100000 8 ;;
     pmcGA) run pmcGA 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmcGA -o run -- python3 -u tools/hbm_phases.py 100000 8 ;;
     pmcGB) run pmcGB 200 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcGB -o run -- python3 -u tools/hbm_phases.py 100000 8 ;;
+    b3s) run b3s 600 python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
+    jsontests) run jsontests 600 python -u -m pytest tests/test_gpu_json.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     b3s_base) run b3s_base 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_base.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     b3s_lazy) run b3s_lazy 600 python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     b3s_eager) run b3s_eager 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_eagercold.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;

@@ -212,7 +212,7 @@ def test_gpu_ingest_replays_canonicalized_values_and_many_clients():
         ref.start_collab("readonly")
         for m in msgs:
             assert ref.apply_msg(m) == 0, ref.error
-        want.append((ref.digest(), ref.props_runs()))
+        want.append((ref.digest(), json.loads(ref.props_runs())))
     with fa.ReplayBatch(len(texts)) as g, fa.ReplayBatch(len(texts)) as h:
         assert g.ingest_json(texts, device="gpu")["path"] == "gpu"
         h.ingest_json(texts, device="host")
