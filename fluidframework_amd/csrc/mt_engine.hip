@@ -56,6 +56,13 @@ namespace mt {
 #define MT_DESCENT_ONE_ROUND 0
 #endif
 
+// 1: a scour's text appends of <= 64 code units are queued (up to 4) and issued together, so their
+// HBM loads overlap instead of each waiting for the previous copy (0 = one copy at a time); giant
+// class only (Engine::kTextBatch)
+#ifndef MT_TEXT_BATCH
+#define MT_TEXT_BATCH 1
+#endif
+
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int32_t rfl(int32_t x) { return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)x); }
 __device__ __forceinline__ uint32_t rdl(uint32_t x, int l) { return __builtin_amdgcn_readlane(x, l); }
@@ -206,6 +213,11 @@ struct Engine {
     static constexpr uint32_t kNoBlk = idx_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
     static constexpr bool kHbm = is_hbm_seg(SEG);
     static constexpr bool kGiant = is_giant_seg(SEG);
+    // batched text appends in the giant class only: measured on one box, config 3 at 8,192 documents
+    // with batching in the classes of <= 2 waves per SIMD 119.9M vs 122.0M ops/s (a scour rarely
+    // merges more than one leaf, so the queue only adds instructions; the 128-VGPR classes spill
+    // with it), the giant class 20.81 vs 21.24 us per op (profiles/r03_ab_experiments.json)
+    static constexpr bool kTextBatch = MT_TEXT_BATCH && kGiant;
     static constexpr Layout glay = make_glayout();
     template <typename T, int kShift = 0>
     using BA = BArr<T, kShift, kGiant>;
@@ -915,6 +927,22 @@ struct Engine {
     // lane-parallel copy of n code units inside the doc's text region
     MT_FI void text_copy(uint32_t dst, uint32_t src, uint32_t n) {
         for (uint32_t i = lane; i < n; i += kWave) text[dst + i] = text[src + i];
+    }
+    // the queued copies (lane i of dd / ds / dl: copy i, each <= 64 units): every load, then every
+    // store.  Their regions are disjoint: each destination is its head's free capacity, each source
+    // a merged leaf's own text (capacity regions of live segments never overlap).
+    static constexpr int kTextQ = 4;
+    MT_FI void text_flush(uint32_t dd, uint32_t ds, uint32_t dl, int32_t &nq) {
+        uint32_t v[kTextQ];
+#pragma unroll
+        for (int i = 0; i < kTextQ; i++) {
+            v[i] = 0u;
+            if (i < nq && (uint32_t)lane < rdl(dl, i)) v[i] = text[rdl(ds, i) + (uint32_t)lane];
+        }
+#pragma unroll
+        for (int i = 0; i < kTextQ; i++)
+            if (i < nq && (uint32_t)lane < rdl(dl, i)) text[rdl(dd, i) + (uint32_t)lane] = (uint16_t)v[i];
+        nq = 0;
     }
     // Bump allocation in the active text semispace; when it is full, live text moves to the
     // other semispace (text_gc) and the garbage left by reallocating merges is dropped.
@@ -2031,6 +2059,8 @@ struct Engine {
             int32_t h = -1;
             uint32_t hslot = 0, pl = 0, ptoff = 0, pcap = 0, hmeta = 0, hprops = 0, hov = 0;
             int32_t gcs0 = text_gcs;
+            uint32_t dd = 0, ds = 0, dl = 0;  // queued text copies (MT_TEXT_BATCH), lane i = copy i
+            int32_t nq = 0;
             while (m) {
                 const int k = first_lane(m);
                 m &= m - 1;
@@ -2056,23 +2086,27 @@ struct Engine {
                 }
                 const uint32_t need = pl + sl;
                 if (need > kMaxLen) {  // beyond 16-bit lengths: the document continues in the HBM class
+                    if (nq) text_flush(dd, ds, dl, nq);
                     cap_fail(kCapLongSeg);
                     return 0;
                 }
+                bool append = false;
                 if (pcap == pl && ptoff + pl == stoff) {
                     // texts already adjacent (split halves, consecutive payloads): take over the region
                     pcap = pl + stcap;
                 } else if (pcap >= need) {
-                    text_copy(ptoff + pl, stoff, sl);
+                    append = true;
                 } else if (ptoff >= arena_base && ptoff < arena_end && ptoff + pcap == arena_top &&
                            ptoff + 2u * need <= arena_end) {
                     // last allocation of the arena: grow in place
                     pcap = 2u * need;
                     arena_top = ptoff + pcap;
-                    text_copy(ptoff + pl, stoff, sl);
+                    append = true;
                 } else {
                     // reallocate; a compaction inside arena_alloc moves every text, so the head
-                    // is written back first and both offsets re-read afterwards
+                    // is written back first and both offsets re-read afterwards (the queued copies
+                    // land first: the head's text and the compaction read them)
+                    if (nq) text_flush(dd, ds, dl, nq);
                     s_len[hslot] = (Len)pl;
                     if (lane == 0) cold[2 * hslot] = make_uint4(hprops, hov, ptoff, pcap);
                     wsync();
@@ -2089,6 +2123,19 @@ struct Engine {
                     ptoff = dst;
                     pcap = (ncap + 1u) & ~1u;
                 }
+                if (append) {
+                    if (kTextBatch && sl <= (uint32_t)kWave) {
+                        if (nq == kTextQ) text_flush(dd, ds, dl, nq);
+                        if (lane == nq) {
+                            dd = ptoff + pl;
+                            ds = stoff;
+                            dl = sl;
+                        }
+                        nq++;
+                    } else {
+                        text_copy(ptoff + pl, stoff, sl);
+                    }
+                }
                 pl = need;
                 const uint32_t fm = rdl(meta, k);
                 hmeta = (hmeta & ~kMetaEndsNL) | (fm & (kMetaEndsNL | kMetaHasNL));
@@ -2097,6 +2144,7 @@ struct Engine {
                 s_meta[hslot] = hmeta;
                 wsync();
             }
+            if (nq) text_flush(dd, ds, dl, nq);
         }
         // unlink removed-below-minSeq leaves and appended ones; keep the rest in order
         const uint64_t freeM = freeR | mergeM;
