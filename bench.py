@@ -183,8 +183,9 @@ def main():
     for i in range(args.steps):
         sn, gathered = step()
         kernel_ms.append(b.stats()["kernel_ms"])
-        # the dominant kernel: the launch that applied the most ops (launch 0 in uniform batches)
-        l0 = max(b.launches(), key=lambda li: li["ops"])
+        # the dominant kernel: the launch that took the longest (config 4: the giant-class launch of
+        # the Zipf tail, not the class that applied the most ops)
+        l0 = max(b.launches(), key=lambda li: li["ms"])
         first_ms.append(l0["ms"])
         first_ops.append(l0["ops"])
         dom_class = l0["seg_class"]
@@ -239,6 +240,7 @@ def main():
     kname = f"mt_{'writer' if args.writers else 'replay'}_kernel_{dom_class}"
     traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, kname)
     lds = lds_busy(args.config, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
+    issue = issue_util(args.config, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
@@ -285,7 +287,9 @@ def main():
                          "algorithmic_bytes_formula": "32 B/op record + 2 B/inserted code unit + 8 B/prop record "
                                                       "+ 32 B/final table entry (DESIGN.md §5)",
                          "ops_per_launch": int(sum(first_ops) / len(first_ops)),
-                         "lds_busy": lds},
+                         "lds_busy": lds,
+                         "issue_frac": issue["frac"] if issue else None,
+                         "issue": issue},
             "replay_ms_per_step": round(avg_kernel_ms, 3),
             "launches": b.launches(),
             "cpu_baseline": cpu,
@@ -427,6 +431,43 @@ def gather_summaries(b, torch, dist, world, rank, backend):
         return None
     ok = bool(torch.equal(recv[0].to(buf.device), buf[:n]))
     return {"bytes": int(sum(int(r.numel()) for r in recv)), "ranks": len(recv), "rank0_roundtrip_equal": ok}
+
+
+INSTR_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH",
+                  "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR")
+
+
+def issue_util(config, n_ops, kernel, avg_ms, ops_per_launch):
+    """What bounds the dominant kernel when neither HBM nor LDS does: its instruction issue.
+    frac = instructions per op (the committed rocprofv3 SQ_INSTS_* passes of this configuration,
+    profiles/pmc_counters_config<N>.json) x the ops of one launch / (the launch time measured live
+    here x 256 CUs x 4 SIMDs x ~2.4 GHz), i.e. instructions per SIMD-cycle against one per cycle.
+    One wave alone issues at most one instruction per ~4 cycles (MI355X_MICROARCH.md, 'vector-
+    instruction ISSUE cost'), so `wave_frac` = 4 x instructions / SQ_WAVE_CYCLES-derived cycles per
+    op is how much of its own issue ceiling a document's wave uses; `wait_share` = SQ_WAIT_ANY /
+    SQ_WAVE_CYCLES, the share of wave time parked on s_waitcnt (memory latency)."""
+    path = ROOT / "profiles" / f"pmc_counters_config{config}.json"
+    try:
+        prof = json.loads(path.read_text())
+    except (OSError, ValueError):
+        return None
+    k = prof.get("kernels", {}).get(kernel)
+    if not k or prof.get("ops") != n_ops:
+        return None
+    per = k.get("per_op") or {}
+    if any(c not in per for c in INSTR_COUNTERS):
+        return None
+    inst = sum(per[c] for c in INSTR_COUNTERS)
+    simd_cycles = avg_ms * 1e-3 * CLOCK_GHZ * 1e9 * N_CUS * 4
+    out = {"frac": round(inst * ops_per_launch / simd_cycles, 6), "instructions_per_op": round(inst, 1),
+           "source": str(path.relative_to(ROOT))}
+    wc = per.get("SQ_WAVE_CYCLES")
+    if wc:  # SQ_WAVE_CYCLES counts in units of 4 cycles (quad-cycles) per wave
+        out["wave_cycles_per_op"] = round(4 * wc, 1)
+        out["wave_frac"] = round(4.0 * inst / (4.0 * wc), 4)  # 4 cycles per instruction / 4 cycles per quad
+        if per.get("SQ_WAIT_ANY"):
+            out["wait_share"] = round(per["SQ_WAIT_ANY"] / wc, 4)
+    return out
 
 
 def lds_busy(config, n_ops, kernel, avg_ms, ops_per_launch):

@@ -63,27 +63,32 @@ __device__ __forceinline__ int value_rel(uint32_t va, uint32_t vb, const uint32_
 // needsScour tri-state (mergeTree.ts:63, 1279, 1438)
 constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
 
-// segment meta word
+// OutRec meta word (the device's final table, mt_host.cpp, mt_snapshot.hip, mt_digest.hip) and the
+// canonical meta word of checkpoint images:
 //   [0,12)  clientId (short id)        [12,24) removedClientId (4095 = none)
 //   [24]    Marker                      [25]    text ends with '\n'
-//   [26]    linked (in the tree)        [27]    unsettled (in the overlay list, see mt_engine.hip)
+//   [26]    linked (in the tree)        [27]    (OutRec: 0)
 //   [28]    has a prop set              [29]    text contains a '\n' somewhere
 //   [30]    removedClientOverlap is non-empty (mask or list via the cold record)
+// The engine's per-slot LDS meta is narrower (mt_engine.hip SlotMeta): flags plus the index of the
+// slot's unsettled-overlay entry; client ids live in the cold record and in the overlay entry.
 constexpr uint32_t kMetaCli = 0xFFFu;
 constexpr uint32_t kMetaRcliShift = 12;
 constexpr uint32_t kMetaMarker = 1u << 24;
 constexpr uint32_t kMetaEndsNL = 1u << 25;
 constexpr uint32_t kMetaLinked = 1u << 26;
-constexpr uint32_t kMetaUnsettled = 1u << 27;
 constexpr uint32_t kMetaHasProps = 1u << 28;
 constexpr uint32_t kMetaHasNL = 1u << 29;
 constexpr uint32_t kMetaHasOvl = 1u << 30;
-//   [31]   in a pending (unacked) local segment group of a writer replica: its groups are the bits
-//          of the cold record's pending mask (cold[2 slot + 1].z / .w, bit G & 63 of group G)
-constexpr uint32_t kMetaPending = 1u << 31;
 __host__ __device__ constexpr uint32_t meta_cli(uint32_t m) { return m & kMetaCli; }
 __host__ __device__ constexpr uint32_t meta_rcli(uint32_t m) { return (m >> kMetaRcliShift) & kMetaCli; }
-// 16-bit window-relative sequence numbers in LDS (s_sr[slot] = seq16 | rseq16 << 16, see mt_engine.hip)
+// canonical slot meta of a checkpoint image: 7 flag bits at [24, 31), the overlay-entry index below
+// (kCanonNoEntry: settled).  Flag order: linked, Marker, ends-'\n', has props, has '\n', removed,
+// pending (a writer's unacked local segment group holds the slot)
+constexpr uint32_t kCanonNoEntry = 0xFFFFFFu;
+// a writer replica's pending-group membership: bit G & 31 of the 32-bit mask in the slot's cold
+// record (cold[2 slot + 1].w) for group G
+constexpr int kPendMaskBits = 32;
 constexpr uint32_t kSeq16None = 0xFFFFu;  // rseq16 of a segment that is not removed
 constexpr uint32_t kSeq16Unassigned = 0xFFFEu;  // seq16 / rseq16 of a pending local insert / remove
 constexpr int32_t kUnassignedSeq = -1;  // UnassignedSequenceNumber (constants.ts:11): real seqs of pending ops
@@ -159,7 +164,14 @@ struct Caps {
 // The replay kernel is latency bound, so a launch's rate grows with the documents per CU.
 constexpr int kGiantSeg = 2000000;
 constexpr int kHbmSeg = 2097152;
-constexpr int kClassSegs[] = {128, 363, 423, 483, 540, 600, 720, 840, 960, 1136, 1376, 1792, 2389, 3600, 7266, kGiantSeg, kHbmSeg};
+// the class list (X-macro: mt_host.cpp declares each class's kernels from it; __graft_entry__.py
+// builds one object per entry)
+#define MT_CLASS_LIST(X) \
+    X(128) X(416) X(499) X(579) X(659) X(743) X(904) X(1064) X(1229) X(1469) X(1792) X(2360) X(3168) X(3600) X(7280) \
+    X(2000000) X(2097152)
+#define MT_CLASS_SEG_(S) S,
+constexpr int kClassSegs[] = {MT_CLASS_LIST(MT_CLASS_SEG_)};
+static_assert(kClassSegs[15] == kGiantSeg && kClassSegs[16] == kHbmSeg, "spill classes last");
 constexpr int kNumClasses = 17;
 constexpr int kGiantClass = kNumClasses - 2;
 constexpr int kHbmClass = kNumClasses - 1;
@@ -187,8 +199,8 @@ constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS c
 //   [kPendEntries ..) entries {G, slot} in append order (the group's `segments` array order:
 //   members as the op reached them, split-off halves appended when the split happens)
 //   word 4: collabWindow.localSeq (one per applied local op); a group's desc .w = its localSeq
-// unacked local ops at once (more: MT_UNSUPPORTED).  A segment's groups are the bits G & 63 of a
-// 64-bit mask in its cold record: exact while at most 64 groups are pending; beyond, a bit stands
+// unacked local ops at once (more: MT_UNSUPPORTED).  A segment's groups are the bits G & 31 of a
+// 32-bit mask in its cold record: exact while at most 32 groups are pending; beyond, a bit stands
 // for every live group 64 apart and membership is decided by the groups' entry lists
 constexpr int kPendMaxGroups = 1024;
 constexpr int kPendDesc = 8;
@@ -206,20 +218,26 @@ constexpr int kRegenOpWords = 8;
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table
 constexpr int kCkHdr = 32;
 constexpr int64_t ck_words(int seg) { return 8ll * seg + 1024; }
-// cold records per slot in HBM: {props, ovl, toff, tcap} and {seq, rseq, 0, 0} (real seqs)
+// the words a checkpoint image uses: per slot len, canonical meta, block; per overlay entry slot,
+// seqs, clients; per block parent, 8 children, count | leaf | scour, settled length; the heap
+constexpr int64_t ck_used_words(int64_t slots, int64_t nu, int64_t blocks, int64_t hn) {
+    return kCkHdr + 3 * slots + 3 * nu + 11 * blocks + 2 * (hn + 1);
+}
+// cold records per slot in HBM: {props, ovl, toff, tcap} and {seq, rseq, clientId | removedClientId
+// << 16, pending-group mask (writers)} (the real seqs and client ids)
 constexpr int kColdPerSlot = 2;
 constexpr Caps class_caps(int seg) {
     // the overlay list (unsettled segments, ~100-200 at a lag <= 32) is sized to the collab window;
     // the largest classes, where a document with a wide window ends up, can hold half their slots
     if (is_giant_seg(seg))
         return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24 + kGiantLdsBlocks, kGiantHeap, kGiantUlist};
-    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg >= 3000 ? seg / 2 : seg / 8 + 224};
+    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg >= 3500 ? seg / 2 : seg / 16 + 160};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
-    uint32_t len, sr, meta, sblk, ulist;
-    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, bep, heap, scratch, hdr, bytes;
+    uint32_t len, meta, sblk, ulist, usr, ucm;
+    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, bep, heap, scratch, hdr, grec, bytes;
 };
 constexpr int kHdrWords = 24;  // per-document scalars kept in LDS (mt_engine.hip LWord)
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
@@ -229,6 +247,9 @@ constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
 constexpr bool is_hbm_seg(int seg) { return seg > 65000; }
 constexpr uint32_t len_bytes(int seg) { return is_hbm_seg(seg) ? 4u : 2u; }
 constexpr uint32_t idx_bytes(int seg) { return is_hbm_seg(seg) ? 4u : 2u; }
+// per-slot meta: 16 bits (7 flags + a 9-bit overlay-entry index) while the overlay list holds at most
+// 510 entries, else 32 bits (mt_engine.hip SlotMeta)
+constexpr uint32_t meta_bytes(int seg) { return !is_hbm_seg(seg) && class_caps(seg).ulist <= 510 ? 2u : 4u; }
 // The giant class: make_layout is its HBM image (slot tables and the blocks of HBM ids; the LDS-
 // resident parts get no room there) and make_glayout its LDS part.
 constexpr Layout make_layout(int seg) {
@@ -237,7 +258,6 @@ constexpr Layout make_layout(int seg) {
         Layout L{};
         uint32_t o = 0;
         L.len = o;     o = lds_align(o + 4u * c.seg);
-        L.sr = o;      o = lds_align(o + 4u * c.seg);
         L.meta = o;    o = lds_align(o + 4u * c.seg);
         L.sblk = o;    o = lds_align(o + 4u * c.seg);
         L.bparent = o; o = lds_align(o + 4u * c.blk);
@@ -248,17 +268,18 @@ constexpr Layout make_layout(int seg) {
         L.bslen = o;   o = lds_align(o + 4u * c.blk);
         L.bacc = o;    o = lds_align(o + 4u * c.blk);
         L.bep = o;     o = lds_align(o + 4u * c.blk);
-        L.ulist = L.heap = L.scratch = L.hdr = o;  // in LDS (make_glayout)
+        L.ulist = L.usr = L.ucm = L.heap = L.scratch = L.hdr = L.grec = o;  // in LDS (make_glayout)
         L.bytes = o;
         return L;
     }
     Layout L{};
     uint32_t o = 0;
     L.len = o;     o = lds_align(o + len_bytes(seg) * c.seg);
-    L.sr = o;      o = lds_align(o + 4u * c.seg);
-    L.meta = o;    o = lds_align(o + 4u * c.seg);
-    L.sblk = o;    o = lds_align(o + idx_bytes(seg) * c.seg);
+    L.meta = o;    o = lds_align(o + meta_bytes(seg) * c.seg);
+    L.sblk = o;    o = lds_align(o + idx_bytes(seg) * c.seg);   // a free slot's s_blk links the free list
     L.ulist = o;   o = lds_align(o + idx_bytes(seg) * c.ulist);
+    L.usr = o;     o = lds_align(o + 4u * c.ulist);
+    L.ucm = o;     o = lds_align(o + 4u * c.ulist);
     L.bparent = o; o = lds_align(o + idx_bytes(seg) * c.blk);  // a free block's b_parent links the free list
     L.bchild = o;  o = lds_align(o + 8u * idx_bytes(seg) * c.blk);
     L.bcount = o;  o = lds_align(o + 1u * c.blk);
@@ -270,6 +291,7 @@ constexpr Layout make_layout(int seg) {
     L.heap = o;    o = lds_align(o + 8u * (c.heap + 2));
     L.scratch = o; o = lds_align(o + 4u * 128);
     L.hdr = o;     o = lds_align(o + 4u * kHdrWords);
+    L.grec = o;
     L.bytes = o;
     return L;
 }
@@ -282,6 +304,8 @@ constexpr Layout make_glayout() {
     L.scratch = o; o = lds_align(o + 4u * 128);
     L.heap = o;    o = lds_align(o + 8u * (kGiantHeap + 2));
     L.ulist = o;   o = lds_align(o + 4u * kGiantUlist);
+    L.usr = o;     o = lds_align(o + 4u * kGiantUlist);
+    L.ucm = o;     o = lds_align(o + 4u * kGiantUlist);
     L.bparent = o; o = lds_align(o + 4u * K);
     L.bchild = o;  o = lds_align(o + 32u * K);
     L.bcount = o;  o = lds_align(o + 1u * K);
@@ -290,7 +314,7 @@ constexpr Layout make_glayout() {
     L.bslen = o;   o = lds_align(o + 4u * K);
     L.bacc = o;    o = lds_align(o + 4u * K);
     L.bep = o;     o = lds_align(o + 4u * K);
-    L.sr = o;      o = lds_align(o + 4u * kGiantChainRec * kGiantUlist);  // the overlay's chain records
+    L.grec = o;    o = lds_align(o + 4u * kGiantChainRec * kGiantUlist);  // the overlay's chain records
     L.len = L.meta = L.sblk = o;  // in HBM (make_layout)
     L.bytes = o;
     return L;

@@ -5,15 +5,16 @@
 // mergeTree.ts:334): leaf blocks list segment slots, interior blocks list blocks, every
 // child list is one 16-byte row that a wave reads with one lane per child.
 //
-//   s_*[slot]   the fields nodeLength reads (SoA): length, sequence numbers, client ids, flags;
-//               and the leaf block.  Sequence numbers are 16-bit, relative to a per-document base
-//               that follows minSeq (s_sr = seq16 | rseq16 << 16; a settled segment needs none:
-//               seq16 = 0, rseq16 = 0 if removed else kSeq16None), so a slot costs 14 B of LDS.
-//               The cold fields (prop-set id, removedClientOverlap — flagged in the meta word,
-//               read only when set —, text offset/capacity, and the real seq / removedSeq for
-//               output) live in a per-document HBM table `cold[2 * slot + {0,1}]` (2 x 16 B).
+//   s_*[slot]   length, flags + overlay-entry index (SlotMeta), leaf block: 6 B of LDS per slot.
+//               A settled segment (below) needs nothing else for nodeLength: every valid view sees
+//               its length, or 0 when removed.
+//   u_*[entry]  the unsettled segments (the collab window's "hot" set, ~100-250 per document):
+//               slot, 16-bit sequence numbers relative to a per-document base that follows minSeq
+//               (seq16 | rseq16 << 16), client ids and the has-overlap flag.
+//               The cold fields (prop-set id, removedClientOverlap, text offset/capacity, the real
+//               seq / removedSeq and client ids for output) live in a per-document HBM table
+//               `cold[2 * slot + {0,1}]` (2 x 16 B).
 //   b_*[block]  children[8], count, parent, needsScour, and the block's SETTLED length.
-//   u_list      the unsettled segments (the collab window's "hot" set).
 //   heap        the zamboni heap (collections.ts:213-265), in VGPRs.
 //
 // Position resolution (PartialSequenceLengths, partialLengths.ts, in the reference) is a
@@ -222,12 +223,23 @@ struct Engine {
     template <typename T, int kShift = 0>
     using BA = BArr<T, kShift, kGiant>;
     static constexpr uint32_t kMaxLen = len_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
+    // SlotMeta: 7 flags above a kUB-bit index of the slot's overlay entry (kUNone: settled)
+    using Meta = std::conditional_t<meta_bytes(SEG) == 2u, uint16_t, uint32_t>;
+    static constexpr int kUB = 8 * (int)sizeof(Meta) - 7;
+    static constexpr uint32_t kUNone = (1u << kUB) - 1u;
+    static constexpr uint32_t kFLinked = 1u << kUB, kFMarker = 2u << kUB, kFEndsNL = 4u << kUB,
+                              kFHasProps = 8u << kUB, kFHasNL = 16u << kUB, kFRemoved = 32u << kUB,
+                              kFPending = 64u << kUB;
+    static_assert(cap.ulist < (int32_t)kUNone, "overlay-entry index");
+    // u_cm: clientId | removedClientId << 12 | has-overlap
+    static constexpr uint32_t kCmOvl = 1u << 24;
     // ---- LDS state
     Len *s_len;
-    uint32_t *s_meta;
-    uint32_t *s_sr;  // seq16 | rseq16 << 16 (window-relative); of a free slot: the next free slot
-    Idx *s_blk;
-    Idx *u_list;  // exactly the unsettled slots (kMetaUnsettled), unordered
+    Meta *s_meta;  // flags | overlay-entry index; a free slot: kUNone
+    Idx *s_blk;    // leaf block; of a free slot: the next free slot (kNoBlk ends the list)
+    Idx *u_list;   // overlay entries: exactly the unsettled slots, unordered
+    uint32_t *u_sr;  // seq16 | rseq16 << 16, relative to sbase (kSeq16None: not removed)
+    uint32_t *u_cm;  // clientId | removedClientId << 12 | kCmOvl
     BA<Idx> b_parent;  // b_parent of a free block links the free block list
     BA<Idx, 3> b_child;
     BA<uint8_t> b_count, b_leaf;
@@ -247,7 +259,7 @@ struct Engine {
     // are the HBM ids, from kGiantLdsBlocks)
     int32_t lds_top, n_lfree, lfree_head;
     int32_t min_seq, cur_seq, status, settled_min;
-    int32_t sbase;  // sequence numbers in s_sr are relative to sbase (<= minSeq)
+    int32_t sbase;  // the overlay entries' 16-bit sequence numbers are relative to sbase (<= minSeq)
     int32_t splits;                 // leaf/interior block splits so far (overlay staleness)
     int32_t ov_splits, ov_full;     // overlay computed at `ov_splits`; full (refSeq < minSeq) mode
     uint32_t arena_top, pool_top;
@@ -292,12 +304,13 @@ struct Engine {
     // class's LDS part (make_glayout)
     MT_FI void carve(uint8_t *tb, uint8_t *lb) {
         s_len = (Len *)(tb + lay.len);
-        s_sr = (uint32_t *)(tb + lay.sr);
-        s_meta = (uint32_t *)(tb + lay.meta);
+        s_meta = (Meta *)(tb + lay.meta);
         s_blk = (Idx *)(tb + lay.sblk);
         uint8_t *xb = kGiant ? lb : tb;  // the per-op state: in LDS for the giant class
         const Layout &xl = kGiant ? glay : lay;
         u_list = (Idx *)(xb + xl.ulist);
+        u_sr = (uint32_t *)(xb + xl.usr);
+        u_cm = (uint32_t *)(xb + xl.ucm);
         b_parent.p = (decltype(b_parent.p))(tb + lay.bparent);
         b_child.p = (decltype(b_child.p))(tb + lay.bchild);
         b_count.p = (decltype(b_count.p))(tb + lay.bcount);
@@ -318,7 +331,7 @@ struct Engine {
         }
         h_ent = (uint2 *)(xb + xl.heap);
         scratch = (uint32_t *)(xb + xl.scratch);
-        if constexpr (kGiant) g_rec = (uint32_t *)(lb + glay.sr);  // make_glayout: the chain records
+        if constexpr (kGiant) g_rec = (uint32_t *)(lb + glay.grec);  // make_glayout: the chain records
         uint32_t *hw = (uint32_t *)(xb + xl.hdr);
         pay_end.p = hw + 0;
         arena_base.p = hw + 1;
@@ -401,7 +414,8 @@ struct Engine {
         int32_t s;
         if (free_head >= 0) {
             s = free_head;
-            free_head = (int32_t)rfl(s_sr[s]);
+            const uint32_t nx = rfl((uint32_t)s_blk[s]);
+            free_head = nx == kNoBlk ? -1 : (int32_t)nx;
             free_n--;
         } else {
             if (slot_top >= cap.seg) {
@@ -473,43 +487,84 @@ struct Engine {
         return hit;
     }
     // nodeLength of one leaf for (refSeq, clientId) + breakTie's leaf rule (mergeTree.ts:2248-2277).
-    // Valid views (refSeq >= minSeq >= sbase) compare the 16-bit relative seqs in LDS, where a
-    // settled leaf has seq16 = 0 and rseq16 = 0 (removed) / kSeq16None; a view below minSeq
-    // (outside valid logs) reads the real seqs from the cold records.
+    // Valid views (refSeq >= minSeq >= sbase): a settled leaf is seen whole (or not at all when
+    // removed) by every one of them; an unsettled leaf's overlay entry holds its 16-bit relative seqs
+    // and client ids.  A view below minSeq (outside valid logs) reads the real seqs and client ids from
+    // the cold records.
     __device__ __forceinline__ void view_of(uint32_t slot, int32_t ref, uint32_t c, uint32_t &vlen, bool &tie) const {
         const uint32_t meta = s_meta[slot];
         const uint32_t len = s_len[slot];
-        bool vis, rle;
+        bool vis, rle, rem;
         bool pending = false;  // writer: an unacked local insert (seq === UnassignedSequenceNumber)
         if (ref >= min_seq) {
-            const uint32_t sr = s_sr[slot];
+            const uint32_t ui = meta & kUNone;
+            if (ui == kUNone) {
+                const bool rm = (meta & kFRemoved) != 0u;
+                vlen = rm ? 0u : len;
+                tie = !rm;
+                return;
+            }
+            const uint32_t sr = u_sr[ui], cm = u_cm[ui];
             const uint32_t r16 = (uint32_t)(ref - sbase);
-            vis = (meta_cli(meta) == c) || ((sr & 0xFFFFu) <= r16);
+            vis = ((cm & kMetaCli) == c) || ((sr & 0xFFFFu) <= r16);
             rle = (sr >> 16) <= r16;
             if constexpr (kW) pending = (sr & 0xFFFFu) == kSeq16Unassigned;
+            rem = (((cm >> 12) & kMetaCli) == c) || rle;
+            if (!rem && (cm & kCmOvl)) rem = ovl_has(slot, c);
         } else {
             const uint4 q = cold[2 * slot + 1];
+            const uint32_t cli = q.z & kMetaCli, rcli = (q.z >> 16) & kMetaCli;
             if constexpr (kW) {
                 pending = (int32_t)q.x == kUnassignedSeq;
-                vis = (meta_cli(meta) == c) || (!pending && (int32_t)q.x <= ref);
+                vis = (cli == c) || (!pending && (int32_t)q.x <= ref);
                 rle = (int32_t)q.y != kUnassignedSeq && (int32_t)q.y <= ref;
             } else {
-                vis = (meta_cli(meta) == c) || ((int32_t)q.x <= ref);
+                vis = (cli == c) || ((int32_t)q.x <= ref);
                 rle = (int32_t)q.y <= ref;
             }
+            rem = (rcli == c) || rle;
+            if (!rem && (meta & kFRemoved)) rem = ovl_has(slot, c);
         }
-        bool rem = (meta_rcli(meta) == c) || rle;
-        if (!rem && (meta & kMetaHasOvl)) rem = ovl_has(slot, c);
         vlen = (vis && !rem) ? len : 0u;
         // breakTie's leaf rule: a remote op does not insert before a pending local segment; the
         // local client breaks every tie it reaches (mergeTree.ts:2263-2271)
         tie = !rle && (!kW || c == 0u || !pending);
     }
-    MT_FI static bool sr_removed(uint32_t sr) { return (sr >> 16) != kSeq16None; }
+    MT_FI static bool is_settled(uint32_t meta) { return (meta & kUNone) == kUNone; }
     // a leaf's contribution to the settled block sums
     __device__ __forceinline__ uint32_t settled_len(uint32_t slot) const {
-        uint32_t meta = s_meta[slot];
-        return (!(meta & kMetaUnsettled) && !sr_removed(s_sr[slot])) ? s_len[slot] : 0u;
+        const uint32_t meta = s_meta[slot];
+        return (is_settled(meta) && !(meta & kFRemoved)) ? s_len[slot] : 0u;
+    }
+    // canonical meta of a checkpoint image (mt_device.h kCanonNoEntry) and back
+    MT_FI static uint32_t meta_canon(uint32_t m) {
+        const uint32_t i = m & kUNone;
+        return (i == kUNone ? kCanonNoEntry : i) | ((m >> kUB) << 24);
+    }
+    MT_FI static uint32_t meta_uncanon(uint32_t c) {
+        const uint32_t i = c & kCanonNoEntry;
+        return (i == kCanonNoEntry ? kUNone : i) | ((c >> 24) << kUB);
+    }
+    // the OutRec meta word of a slot (client ids from the cold record)
+    MT_FI static uint32_t meta_out(uint32_t m, uint32_t clients, uint32_t ovl) {
+        uint32_t r = (clients & kMetaCli) | (((clients >> 16) & kMetaCli) << kMetaRcliShift);
+        if (m & kFMarker) r |= kMetaMarker;
+        if (m & kFEndsNL) r |= kMetaEndsNL;
+        if (m & kFLinked) r |= kMetaLinked;
+        if (m & kFHasProps) r |= kMetaHasProps;
+        if (m & kFHasNL) r |= kMetaHasNL;
+        if (ovl) r |= kMetaHasOvl;
+        return r;
+    }
+    // nodeLength of the unsettled segment of overlay entry j (slot) in a valid view (refSeq >= minSeq)
+    __device__ __forceinline__ uint32_t view_entry(uint32_t j, uint32_t slot, int32_t ref, uint32_t c) const {
+        const uint32_t sr = u_sr[j], cm = u_cm[j];
+        const uint32_t len = s_len[slot];
+        const uint32_t r16 = (uint32_t)(ref - sbase);
+        const bool vis = ((cm & kMetaCli) == c) || ((sr & 0xFFFFu) <= r16);
+        bool rem = (((cm >> 12) & kMetaCli) == c) || ((sr >> 16) <= r16);
+        if (!rem && (cm & kCmOvl)) rem = ovl_has(slot, c);
+        return (vis && !rem) ? len : 0u;
     }
 
     // ------------------------------------------------------------------ ancestor chains
@@ -600,7 +655,6 @@ struct Engine {
             cap_fail(1);
             return;
         }
-        int32_t w = 0;
         for (int32_t g0 = 0; g0 < nu; g0 += 4 * kWave) {
             uint32_t slot[4], vlen[4], b[4], nh[4];
             bool act[4];
@@ -608,31 +662,17 @@ struct Engine {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int32_t j = g0 + k * kWave + lane;
-                slot[k] = j < nu ? (uint32_t)u_list[j] : 0xFFFFFFFFu;
+                act[k] = j < nu;
+                wk[k] = act[k] ? j : -1;
+                slot[k] = act[k] ? (uint32_t)u_list[j] : 0u;
             }
-            uint32_t meta[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) meta[k] = slot[k] != 0xFFFFFFFFu ? s_meta[slot[k]] : 0u;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool valid = (meta[k] & kMetaUnsettled) && (meta[k] & kMetaLinked);
-                const uint64_t vm = ballot(valid);
-                wk[k] = valid ? w + __popcll(vm & ((1ull << lane) - 1ull)) : -1;
-                w += __popcll(vm);
-                act[k] = valid;
-            }
-            wsync();  // every read of this group's list entries is done: compact in place
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (act[k]) u_list[wk[k]] = (Idx)slot[k];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 vlen[k] = 0;
                 b[k] = kNoBlk;
                 nh[k] = 0;
                 if (act[k]) {
-                    bool tie;
-                    view_of(slot[k], ref, c, vlen[k], tie);
+                    vlen[k] = view_entry((uint32_t)wk[k], slot[k], ref, c);
                     b[k] = s_blk[slot[k]];
                 }
                 act[k] = act[k] && vlen[k] > 0u;
@@ -673,24 +713,41 @@ struct Engine {
             }
             if (ballot(over)) cap_fail(1);  // more HBM blocks on a chain than recorded: the HBM class
         }
-        nu = w;
-        g_nrec = w * kGiantChainRec;
+        g_nrec = nu * kGiantChainRec;
         ov_splits = splits;
         wsync();
     }
 
-    MT_FI void u_push(uint32_t slot) {
+    // a new segment's two cold records {props, no overlap, text offset, text capacity} and {seq,
+    // removedSeq, client ids, no pending groups}: one dword per lane 0-7, a single 32-byte store
+    MT_FI void cold_init(uint32_t slot, uint32_t props, uint32_t toff, uint32_t tcap, uint32_t seq, uint32_t rseq,
+                         uint32_t clients) {
+        uint32_t v = 0u;
+        v = lane == 0 ? props : v;
+        v = lane == 2 ? toff : v;
+        v = lane == 3 ? tcap : v;
+        v = lane == 4 ? seq : v;
+        v = lane == 5 ? rseq : v;
+        v = lane == 6 ? clients : v;
+        if (lane < 8) reinterpret_cast<uint32_t *>(cold + 2 * slot)[lane] = v;
+    }
+    // a new overlay entry for `slot` (its meta word gets the entry's index)
+    MT_FI void u_push(uint32_t slot, uint32_t sr, uint32_t cm) {
         if (nu >= cap.ulist) {
             cap_fail(1);
             return;
         }
         u_list[nu] = (Idx)slot;
+        u_sr[nu] = sr;
+        u_cm[nu] = cm;
+        s_meta[slot] = (Meta)((s_meta[slot] & ~kUNone) | (uint32_t)nu);
         nu++;
         if (nu > max_u) max_u = nu;
+        wsync();
     }
 
     // Per-op overlay: b_acc[B] = sum of nodeLength(refSeq, c) over the unsettled segments under
-    // B (or over all segments in full mode).  Also drops stale list entries.
+    // B (or over all segments in full mode).
     MT_FI void overlay(int32_t ref, uint32_t c) {
         PF_SCOPE(6);
         if constexpr (kGiant) {
@@ -706,33 +763,21 @@ struct Engine {
         wsync();
         ov_full = ref < min_seq;
         if (!ov_full) {
-            int32_t w = 0;
             for (int32_t base = 0; base < nu; base += kWave) {
                 const int32_t j = base + lane;
                 const bool in = j < nu;
-                const uint32_t slot = in ? (uint32_t)u_list[j] : 0u;
-                bool valid = false;
-                if (in) {
-                    uint32_t meta = s_meta[slot];
-                    valid = (meta & kMetaUnsettled) && (meta & kMetaLinked);
-                }
-                const uint64_t vm = ballot(valid);
-                wsync();
-                if (valid) u_list[w + __popcll(vm & ((1ull << lane) - 1ull))] = (Idx)slot;
-                w += __popcll(vm);
                 uint32_t vlen = 0, b = 0;
-                bool tie;
-                if (valid) {
-                    view_of(slot, ref, c, vlen, tie);
+                if (in) {
+                    const uint32_t slot = u_list[j];
+                    vlen = view_entry((uint32_t)j, slot, ref, c);
                     b = s_blk[slot];
                 }
-                ov_chain_add(valid && vlen > 0u, b, vlen);
+                ov_chain_add(in && vlen > 0u, b, vlen);
             }
-            nu = w;
         } else {
             for (int32_t base = 0; base < slot_top; base += kWave) {
                 const int32_t slot = base + lane;
-                bool live = slot < slot_top && (s_meta[slot] & kMetaLinked);
+                bool live = slot < slot_top && (s_meta[slot] & kFLinked);
                 uint32_t vlen = 0, b = 0;
                 bool tie;
                 if (live) {
@@ -750,7 +795,8 @@ struct Engine {
     }
 
     // settle every overlay entry that minSeq has caught up with (before zamboni scours), and
-    // rebase the 16-bit seqs of the rest on minSeq (a settled leaf's s_sr is base independent)
+    // rebase the 16-bit seqs of the rest on minSeq; the kept entries are compacted in order and
+    // their slots' meta words follow
     MT_FI void settle_all() {
         PF_SCOPE(11);
         int32_t w = 0;
@@ -759,25 +805,24 @@ struct Engine {
         for (int32_t b0 = 0; b0 < nu; b0 += kWave) {
             const int32_t j = b0 + lane;
             const bool in = j < nu;
-            const uint32_t slot = in ? (uint32_t)u_list[j] : 0u;
-            bool valid = false, elig = false;
-            uint32_t meta = 0, add = 0, b = 0, sr = 0;
+            uint32_t slot = 0, sr = 0, cm = 0, add = 0, b = 0;
+            bool elig = false;
             if (in) {
-                meta = s_meta[slot];
-                valid = (meta & kMetaUnsettled) && (meta & kMetaLinked);
-                if (valid) {
-                    sr = s_sr[slot];
-                    const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
-                    elig = q16 <= m16 && (r16 == kSeq16None || r16 <= m16);
-                    if (elig && r16 == kSeq16None) add = s_len[slot];
+                slot = u_list[j];
+                sr = u_sr[j];
+                cm = u_cm[j];
+                const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
+                elig = q16 <= m16 && (r16 == kSeq16None || r16 <= m16);
+                if (elig) {
+                    if (r16 == kSeq16None) add = s_len[slot];
                     b = s_blk[slot];
                 }
             }
-            const bool keep = valid && !elig;
+            const bool keep = in && !elig;
             const uint64_t km = ballot(keep);
+            const int32_t dst = w + __popcll(km & ((1ull << lane) - 1ull));
             wsync();
             if (keep) {
-                u_list[w + __popcll(km & ((1ull << lane) - 1ull))] = (Idx)slot;
                 const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
                 uint32_t nq = q16 > m16 ? q16 - m16 : 0u;
                 uint32_t nr = r16 == kSeq16None ? kSeq16None : (r16 > m16 ? r16 - m16 : 0u);
@@ -785,12 +830,12 @@ struct Engine {
                     if (q16 == kSeq16Unassigned) nq = kSeq16Unassigned;
                     if (r16 == kSeq16Unassigned) nr = kSeq16Unassigned;
                 }
-                s_sr[slot] = nq | (nr << 16);
+                u_list[dst] = (Idx)slot;
+                u_sr[dst] = nq | (nr << 16);
+                u_cm[dst] = cm;
+                if (dst != j) s_meta[slot] = (Meta)((s_meta[slot] & ~kUNone) | (uint32_t)dst);
             }
-            if (elig) {
-                s_meta[slot] = meta & ~kMetaUnsettled;
-                s_sr[slot] = ((sr >> 16) == kSeq16None ? kSeq16None : 0u) << 16;
-            }
+            if (elig) s_meta[slot] = (Meta)(s_meta[slot] | kUNone);
             w += __popcll(km);
             chain_add(b_slen, elig && add > 0u, b, add);
         }
@@ -800,7 +845,6 @@ struct Engine {
         ov_splits = -1;  // b_slen moved under the overlay
         wsync();
     }
-
     // ------------------------------------------------------------------ descent
     // insertingWalk (mergeTree.ts:2345-2474) in insert mode: at every interior level the first
     // child whose cumulative view length reaches pos (breakTie is true for blocks); in the leaf
@@ -972,7 +1016,7 @@ struct Engine {
             uint4 cr = make_uint4(0, 0, 0, 0);
             if (slot < slot_top) {
                 const uint32_t m = s_meta[slot];
-                if ((m & kMetaLinked) && !(m & kMetaMarker)) {
+                if ((m & kFLinked) && !(m & kFMarker)) {
                     cr = cold[2 * slot];
                     mv = cr.z >= arena_base && cr.z < arena_end;
                 }
@@ -1040,10 +1084,10 @@ struct Engine {
             uint32_t old = 0, ovl = 0;
             if (slot < slot_top) {
                 const uint32_t m = s_meta[slot];
-                if (m & kMetaLinked) {
+                if (m & kFLinked) {
                     const uint4 cr = cold[2 * slot];
-                    if (m & kMetaHasProps) old = cr.x;
-                    if ((m & kMetaHasOvl) && (cr.y & kOvlList)) ovl = cr.y & ~kOvlList;
+                    if (m & kFHasProps) old = cr.x;
+                    if (cr.y & kOvlList) ovl = cr.y & ~kOvlList;
                 }
             }
             uint64_t msk = ballot(old != 0u);
@@ -1200,7 +1244,7 @@ struct Engine {
         // the giant class takes the slot from the walk's leaf row (an HBM re-read otherwise)
         const uint32_t slot = kGiant ? slot_hint : rfl((uint32_t)b_child[blk * 8 + k]);
         const uint32_t meta = s_meta[slot];
-        if (meta & kMetaMarker) return -1;  // Marker.createSplitSegmentAt returns undefined
+        if (meta & kFMarker) return -1;  // Marker.createSplitSegmentAt returns undefined
         // the slot's two cold records, lane-distributed (lane i < 8: word i)
         uint32_t pv;
         if (pend_n > 0 && slot == ps0) {
@@ -1227,17 +1271,19 @@ struct Engine {
         }
         pend_n++;
         s_len[ns] = (Len)(len - r);
-        s_sr[ns] = s_sr[slot];
-        s_meta[ns] = meta;  // inherits ends-NL of the tail, linked, unsettled
+        s_meta[ns] = (Meta)(meta | kUNone);  // inherits ends-NL of the tail, linked, removed, pending
         s_len[slot] = (Len)r;
         wsync();
-        if (meta & kMetaUnsettled) u_push((uint32_t)ns);
+        if (!is_settled(meta)) {  // the right half gets a copy of the overlay entry
+            const uint32_t ui = meta & kUNone;
+            u_push((uint32_t)ns, u_sr[ui], u_cm[ui]);
+        }
         if constexpr (kW) {
             // segmentGroups.copyTo (mergeTree.ts:560): the right half joins every group of the
             // segment, oldest first, at the end of each group's segments; its cold record (written
             // by resolve_cold) carries the same pending mask
-            if (meta & kMetaPending) {
-                const uint64_t m = (uint64_t)rdl(pv, 6) | ((uint64_t)rdl(pv, 7) << 32);
+            if (meta & kFPending) {
+                const uint32_t m = rdl(pv, 7);
                 const uint32_t head = pend_word(1);
                 for (int32_t i = 0; i < n_pend && !status; i++)
                     if (in_group(head + (uint32_t)i, slot, m)) entry_append(head + (uint32_t)i, (uint32_t)ns);
@@ -1245,7 +1291,7 @@ struct Engine {
             }
         }
         const int32_t nb = insert_leaf(blk, k + 1, (uint32_t)ns);
-        if (meta & kMetaHasOvl) resolve_cold();  // view_of reads the halves' overlap masks from HBM
+        if (rdl(pv, 1)) resolve_cold();  // view_of reads the halves' overlap masks from HBM
         return nb;
     }
 
@@ -1260,7 +1306,7 @@ struct Engine {
             if (lane < 8)
                 reinterpret_cast<uint32_t *>(cold + 2 * ns)[lane] = pv + (lane == 2 ? r : 0u) - (lane == 3 ? r : 0u);
             // a text without any '\n' cannot end in one: no HBM read
-            const uint32_t ch = (s_meta[sl] & kMetaHasNL) ? (uint32_t)text[rdl(pv, 2) + r - 1] : 0u;
+            const uint32_t ch = (s_meta[sl] & kFHasNL) ? (uint32_t)text[rdl(pv, 2) + r - 1] : 0u;
             if (i) pch1 = ch;
             else pch0 = ch;
         }
@@ -1274,7 +1320,7 @@ struct Engine {
             const uint32_t sl = i ? ps1 : ps0;
             const uint32_t ch = i ? pch1 : pch0;
             const uint32_t m = s_meta[sl];
-            s_meta[sl] = ch == (uint32_t)'\n' ? (m | kMetaEndsNL) : (m & ~kMetaEndsNL);
+            s_meta[sl] = (Meta)(ch == (uint32_t)'\n' ? (m | kFEndsNL) : (m & ~kFEndsNL));
         }
         pend_n = 0;
         pend_cold = 0;
@@ -1323,25 +1369,20 @@ struct Engine {
     // MergeTree.pendingSegments / SegmentGroup (mergeTree.ts:1093, 1922-1929) in the document's HBM
     // region (mt_device.h kPendDesc / kPendEntries); lane 0 writes, every lane reads back.
     MT_FI uint32_t pend_word(int i) const { return rfl(pend[i]); }
-    MT_FI uint64_t pend_mask(uint32_t slot) const {
-        const uint4 q = cold[2 * slot + 1];
-        return (uint64_t)rfl(q.z) | ((uint64_t)rfl(q.w) << 32);
-    }
-    MT_FI void pend_set_mask(uint32_t slot, uint64_t m) {
-        if (lane == 0) {
-            cold[2 * slot + 1].z = (uint32_t)m;
-            cold[2 * slot + 1].w = (uint32_t)(m >> 32);
-        }
+    static constexpr uint32_t kPmb = (uint32_t)kPendMaskBits - 1u;  // group G's mask bit: G & kPmb
+    MT_FI uint32_t pend_mask(uint32_t slot) const { return rfl(cold[2 * slot + 1].w); }
+    MT_FI void pend_set_mask(uint32_t slot, uint32_t m) {
+        if (lane == 0) cold[2 * slot + 1].w = m;
         const uint32_t meta = s_meta[slot];
-        s_meta[slot] = m ? (meta | kMetaPending) : (meta & ~kMetaPending);
+        s_meta[slot] = (Meta)(m ? (meta | kFPending) : (meta & ~kFPending));
         wsync();
     }
     MT_FI uint32_t *pdesc(uint32_t G) const { return pend + kPendDesc + 4 * (G & (uint32_t)(kPendMaxGroups - 1)); }
-    // is `slot` (pending mask m) a member of the live group G?  The mask bit decides while at most 64
-    // groups are pending; beyond, groups 64 apart share a bit and G's entries decide
-    MT_FI bool in_group(uint32_t G, uint32_t slot, uint64_t m) {
-        if (!((m >> (G & 63u)) & 1ull)) return false;
-        return n_pend <= 64 || entry_has(G, slot);
+    // is `slot` (pending mask m) a member of the live group G?  The mask bit decides while at most 32
+    // groups are pending; beyond, groups 32 apart share a bit and G's entries decide
+    MT_FI bool in_group(uint32_t G, uint32_t slot, uint32_t m) {
+        if (!((m >> (G & kPmb)) & 1u)) return false;
+        return n_pend <= kPendMaskBits || entry_has(G, slot);
     }
     MT_FI bool entry_has(uint32_t G, uint32_t slot) {
         const uint32_t start = pend_word(2), n = pend_word(3);
@@ -1360,19 +1401,19 @@ struct Engine {
     // after `slot` leaves group G: may bit G & 63 go?  (not while another live group sharing it,
     // other than `skip`, holds the segment)
     MT_FI bool bit_free_after(uint32_t G, uint32_t slot, uint32_t head, uint32_t skip) {
-        if (n_pend <= 64) return true;
-        for (uint32_t o = (G - head) & 63u; o < (uint32_t)n_pend; o += 64u) {
+        if (n_pend <= kPendMaskBits) return true;
+        for (uint32_t o = (G - head) & kPmb; o < (uint32_t)n_pend; o += (uint32_t)kPendMaskBits) {
             const uint32_t H = head + o;
             if (H != G && H != skip && entry_has(H, slot)) return false;
         }
         return true;
     }
     // localSeq of the live group of type T holding `slot` (0xFFFFFFFF: none)
-    MT_FI uint32_t group_lseq(uint32_t slot, uint64_t m, uint32_t T) {
+    MT_FI uint32_t group_lseq(uint32_t slot, uint32_t m, uint32_t T) {
         const uint32_t head = pend_word(1);
         for (int32_t i = 0; i < n_pend; i++) {
             const uint32_t G = head + (uint32_t)i;
-            if (!((m >> (G & 63u)) & 1ull)) continue;
+            if (!((m >> (G & kPmb)) & 1u)) continue;
             const uint32_t *dp = pdesc(G);
             if ((rfl(dp[0]) & 0xFFu) != T) continue;
             if (in_group(G, slot, m)) return rfl(dp[3]);
@@ -1434,20 +1475,20 @@ struct Engine {
         }
         entry_append((uint32_t)cur_g, slot);
         if (status) return;
-        pend_set_mask(slot, pend_mask(slot) | (1ull << (cur_g & 63)));
+        pend_set_mask(slot, pend_mask(slot) | (1u << ((uint32_t)cur_g & kPmb)));
     }
     // the keys of the pending local annotates holding `slot` (lane j < npk: key j) and whether one of
     // them is a rewrite: SegmentPropertiesManager.pendingKeyUpdateCount / pendingRewriteCount
     // (segmentPropertiesManager.ts:12-14, 49-51, 56-63)
     MT_FI void pending_keys(uint32_t slot, uint32_t &pk, uint32_t &npk, bool &prw) {
-        const uint64_t m = pend_mask(slot);
+        const uint32_t m = pend_mask(slot);
         const uint32_t head = pend_word(1);
         npk = 0;
         pk = 0;
         prw = false;
         for (int32_t i = 0; i < n_pend; i++) {
             const uint32_t G = head + (uint32_t)i;
-            if (!((m >> (G & 63u)) & 1ull)) continue;
+            if (!((m >> (G & kPmb)) & 1u)) continue;
             const uint32_t *dp = pdesc(G);
             const uint32_t tf = rfl(dp[0]), off = rfl(dp[1]), cnt = rfl(dp[2]);
             if ((tf & 0xFFu) != MT_OP_ANNOTATE) continue;
@@ -1472,7 +1513,7 @@ struct Engine {
     MT_FI void op_ack(const mt_op &op) {
         if (n_pend > 0) {
             const uint32_t head = pend_word(1);
-            const uint32_t b = head & 63u;
+            const uint32_t b = head & kPmb;
             const uint32_t tf = rfl(pdesc(head)[0]);
             if ((tf & 0xFFu) != op.type) {  // not the op this group was made by: the stream is corrupt
                 set_fail(ST_BAD_INPUT);
@@ -1487,25 +1528,28 @@ struct Engine {
                 while (hm) {
                     const uint32_t slot = rdl(e.y, first_lane(hm));
                     hm &= hm - 1;
-                    const uint32_t sr = s_sr[slot];
+                    const uint32_t meta = rfl((uint32_t)s_meta[slot]);
+                    const uint32_t ui = meta & kUNone;
+                    const uint32_t sr = ui != kUNone ? rfl(u_sr[ui]) : (uint32_t)kSeq16None << 16;
                     if (op.type == MT_OP_INSERT) {
-                        if ((sr & 0xFFFFu) != kSeq16Unassigned) {
+                        if (ui == kUNone || (sr & 0xFFFFu) != kSeq16Unassigned) {
                             set_fail(ST_BAD_INPUT);
                             return;
                         }
-                        s_sr[slot] = (sr & 0xFFFF0000u) | rel16(op.seq);
+                        u_sr[ui] = (sr & 0xFFFF0000u) | rel16(op.seq);
                         if (lane == 0) cold[2 * slot + 1].x = (uint32_t)op.seq;
                     } else if (op.type == MT_OP_REMOVE) {
-                        if (!sr_removed(sr)) {
+                        if (!(meta & kFRemoved)) {
                             set_fail(ST_BAD_INPUT);
                             return;
                         }
-                        if ((sr >> 16) == kSeq16Unassigned) {
-                            s_sr[slot] = (sr & 0xFFFFu) | (rel16(op.seq) << 16);
+                        if (ui != kUNone && (sr >> 16) == kSeq16Unassigned) {
+                            u_sr[ui] = (sr & 0xFFFFu) | (rel16(op.seq) << 16);
                             if (lane == 0) cold[2 * slot + 1].y = (uint32_t)op.seq;
                         }
                     }
-                    if (bit_free_after(head, slot, head, head)) pend_set_mask(slot, pend_mask(slot) & ~(1ull << b));
+                    wsync();
+                    if (bit_free_after(head, slot, head, head)) pend_set_mask(slot, pend_mask(slot) & ~(1u << b));
                     add_to_lru(rfl((int32_t)s_blk[slot]), slot, op.seq);
                     if (status) return;
                 }
@@ -1540,15 +1584,15 @@ struct Engine {
             bool cont = false;
             for (int32_t b = nb; b >= 0; b = next_leaf_block(b)) {
                 const int32_t n = b_count[b];
-                uint32_t sr = 0;
-                bool live = false;
+                bool live = false, pins = false;
                 if (lane < n) {
-                    sr = s_sr[b_child[b * 8 + lane]];
-                    live = !sr_removed(sr);
+                    const uint32_t m = s_meta[b_child[b * 8 + lane]];
+                    live = !(m & kFRemoved);
+                    if (live && !is_settled(m)) pins = (u_sr[m & kUNone] & 0xFFFFu) == kSeq16Unassigned;
                 }
                 const uint64_t lm = ballot(live);
                 if (lm) {
-                    cont = (rdl(sr, first_lane(lm)) & 0xFFFFu) == kSeq16Unassigned;
+                    cont = (ballot(pins) >> first_lane(lm)) & 1ull;
                     break;
                 }
             }
@@ -1837,8 +1881,13 @@ struct Engine {
         }
         uint32_t ok_k = 0, ok_v = 0;
         if ((uint32_t)lane < nop) {
-            ok_k = op[lane].key;
-            ok_v = op[lane].value;
+            // the lane index through an empty asm: the address is formed here, not hoisted out of the
+            // op loop into a register the 128-VGPR classes would spill
+            uint32_t li = (uint32_t)lane;
+            asm volatile("" : "+v"(li));
+            const mt_prop pr = op[li];
+            ok_k = pr.key;
+            ok_v = pr.value;
         }
         wsync();
         if (ckind != MT_COMBINE_NONE && combine_values(ckind, op, nop, n, ok_k, ok_v)) {
@@ -1954,31 +2003,31 @@ struct Engine {
     MT_FI int32_t scour(uint32_t slot, int32_t n, uint64_t startM, uint32_t *hold) {
         PF_SCOPE(7);
         const bool in = lane < n;
-        uint32_t meta = 0, len = 0, sr = 0;
+        uint32_t meta = 0, len = 0;
         uint4 cr = make_uint4(0, 0, 0, 0);
         if (in) {
-            sr = s_sr[slot];
             meta = s_meta[slot];
             len = s_len[slot];
         }
-        // settle_all ran at this minSeq (sbase == minSeq): seq <= minSeq is seq16 == 0, a settled
-        // removal has rseq16 == 0
-        const bool rem = in && sr_removed(sr);
+        // settle_all ran at this minSeq: a settled leaf has seq <= minSeq, and removedSeq <= minSeq
+        // when removed; every other leaf is unsettled
+        const bool sett = in && is_settled(meta);
+        const bool rem = (meta & kFRemoved) != 0u;
         // writer: a segment in a pending group is held as is and breaks the append chain
         // (scourNode: segmentGroups not empty, mergeTree.ts:1295, 1353-1356)
-        const bool pend = kW && (meta & kMetaPending) != 0u;
-        const bool cand = in && !rem && !pend && (sr & 0xFFFFu) == 0u;
+        const bool pend = kW && (meta & kFPending) != 0u;
+        const bool cand = sett && !rem && !pend;
         const uint32_t mprev = __shfl_up(meta, 1, kWave);
         const uint64_t candM = ballot(cand);
-        const uint64_t freeR = ballot(rem && !pend && (sr >> 16) == 0u);
+        const uint64_t freeR = ballot(sett && rem && !pend);
         const uint64_t liveM = ballot(in);
         // lane k may append to the chain ending at lane k - 1 (TextSegment.canAppend without its
         // length rule, plus matchProperties): both candidates, same block, neither a Marker, the
         // tail not ending in '\n'
         const bool pair = lane > 0 && cand && ((candM >> (lane - 1)) & 1ull) && !((startM >> lane) & 1ull) &&
-                          !(meta & kMetaMarker) && !(mprev & kMetaMarker) && !(mprev & kMetaEndsNL);
+                          !(meta & kFMarker) && !(mprev & kFMarker) && !(mprev & kFEndsNL);
         // matchProperties: two leaves without prop sets match without reading HBM
-        const bool noprops = !((meta | mprev) & kMetaHasProps);
+        const bool noprops = !((meta | mprev) & kFHasProps);
         uint64_t pairM = ballot(pair && noprops);
         const uint64_t withM = ballot(pair && !noprops);
         const uint64_t longM = ballot(in && len > kGranularity);
@@ -2138,10 +2187,10 @@ struct Engine {
                 }
                 pl = need;
                 const uint32_t fm = rdl(meta, k);
-                hmeta = (hmeta & ~kMetaEndsNL) | (fm & (kMetaEndsNL | kMetaHasNL));
+                hmeta = (hmeta & ~kFEndsNL) | (fm & (kFEndsNL | kFHasNL));
                 s_len[hslot] = (Len)pl;
                 if (lane == 0) cold[2 * hslot] = make_uint4(hprops, hov, ptoff, pcap);
-                s_meta[hslot] = hmeta;
+                s_meta[hslot] = (Meta)hmeta;
                 wsync();
             }
             if (nq) text_flush(dd, ds, dl, nq);
@@ -2151,18 +2200,18 @@ struct Engine {
         const uint64_t holdM = liveM & ~freeM;
         const uint64_t below = (1ull << lane) - 1ull;
         wsync();
-        // freed slots are pushed on the free list, linked through s_sr in lane order
+        // freed slots are pushed on the free list, linked through s_blk in lane order
         const uint64_t above = ~((2ull << lane) - 1ull);
         const uint64_t nxtM = freeM & above;
         const int32_t nxt = __shfl((int)slot, nxtM ? first_lane(nxtM) : 0, kWave);
         if ((freeM >> lane) & 1ull) {
-            s_meta[slot] = 0u;  // unlinked
-            s_sr[slot] = (uint32_t)(nxtM ? nxt : free_head);
+            s_meta[slot] = (Meta)kUNone;  // unlinked
+            s_blk[slot] = (Idx)(nxtM ? (uint32_t)nxt : (free_head < 0 ? kNoBlk : (uint32_t)free_head));
         }
         if (freeM) {
             free_head = (int32_t)rdl(slot, first_lane(freeM));
             heap_forget(slot, freeM);
-            const uint64_t mkM = freeR & ballot((meta & kMetaMarker) != 0u);
+            const uint64_t mkM = freeR & ballot((meta & kFMarker) != 0u);
             if (mkM) idmap_forget(slot, mkM);
         }
         free_n += __popcll(freeM);
@@ -2380,26 +2429,28 @@ struct Engine {
             // a loaded segment below the collab window is settled: it joins the settled sums
             // after the leaf insert (while it moves through block splits it counts as unsettled)
             const bool settled = loaded && op.seq <= min_seq && (rseq == kNoneSeq || rseq <= min_seq);
-            uint32_t meta = kMetaLinked | kMetaUnsettled | (c & kMetaCli) | (rcli << kMetaRcliShift);
-            if (marker) meta |= kMetaMarker;
-            if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
-            if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
-            if (props) meta |= kMetaHasProps;
+            uint32_t meta = kFLinked | kUNone;
+            if (marker) meta |= kFMarker;
+            if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kFEndsNL;
+            if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kFHasNL;
+            if (props) meta |= kFHasProps;
+            if (rseq != kNoneSeq) meta |= kFRemoved;
             s_len[slot] = (Len)len;
-            s_sr[slot] = settled ? (rseq == kNoneSeq ? kSeq16None : 0u) << 16
-                                 : (local ? kSeq16Unassigned : rel16(op.seq)) |
-                                       ((rseq == kNoneSeq ? kSeq16None : rel16(rseq)) << 16);
-            if (lane == 0) {
-                cold[2 * slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
-                cold[2 * slot + 1] = make_uint4((uint32_t)op.seq, (uint32_t)rseq, 0u, 0u);
-            }
-            s_meta[slot] = meta;
+            const uint32_t sr = (local ? kSeq16Unassigned : rel16(op.seq)) |
+                                ((rseq == kNoneSeq ? kSeq16None : rel16(rseq)) << 16);
+            cold_init(slot, props, op.payload, marker ? 0u : len, (uint32_t)op.seq, (uint32_t)rseq, (c & kMetaCli) | (rcli << 16));
+            s_meta[slot] = (Meta)meta;
             wsync();
-            if (!settled) u_push((uint32_t)slot);
+            // (a settled loaded segment too, while it moves through block splits: it joins the
+            // settled sums after the leaf insert)
+            u_push((uint32_t)slot, sr, (c & kMetaCli) | (rcli << 12));
+            if (status) return;
             int32_t blk = insert_leaf(W.blk, W.k, (uint32_t)slot);
             if (status) return;
-            if (settled) {
-                s_meta[slot] = meta & ~kMetaUnsettled;
+            if (settled) {  // its entry is still the last one (leaf inserts push none)
+                nu--;
+                s_meta[slot] = (Meta)(s_meta[slot] | kUNone);
+                wsync();
                 if (rseq == kNoneSeq) chain_add_uniform(rfl((int32_t)s_blk[slot]), len);
             }
             // saveIfLocal (mergeTree.ts:2164-2179)
@@ -2440,18 +2491,16 @@ struct Engine {
         }
         const int32_t rseq = op.ref_seq;
         const uint32_t rcli = rseq != kNoneSeq ? ((uint32_t)op.msn & kMetaCli) : kNoClient;
-        uint32_t meta = kMetaLinked | (op.client & kMetaCli) | (rcli << kMetaRcliShift);
-        if (marker) meta |= kMetaMarker;
-        if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kMetaEndsNL;
-        if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kMetaHasNL;
-        if (props) meta |= kMetaHasProps;
+        uint32_t meta = kFLinked | kUNone;  // the overlay entries are made by op_collab from the real seqs
+        if (marker) meta |= kFMarker;
+        if (op.flags & MT_OPF_INTERNAL_ENDS_NL) meta |= kFEndsNL;
+        if (op.flags & MT_OPF_INTERNAL_HAS_NL) meta |= kFHasNL;
+        if (props) meta |= kFHasProps;
+        if (rseq != kNoneSeq) meta |= kFRemoved;
         s_len[slot] = (Len)len;
-        s_sr[slot] = 0u;  // set by op_collab from the real seqs in the cold record
-        if (lane == 0) {
-            cold[2 * slot] = make_uint4(props, 0u, op.payload, marker ? 0u : len);
-            cold[2 * slot + 1] = make_uint4((uint32_t)op.seq, (uint32_t)rseq, 0u, 0u);
-        }
-        s_meta[slot] = meta;
+        cold_init(slot, props, op.payload, marker ? 0u : len, (uint32_t)op.seq, (uint32_t)rseq,
+                  (op.client & kMetaCli) | (rcli << 16));
+        s_meta[slot] = (Meta)meta;
         wsync();
         // reloadFromSegments' blockUpdate maps the ids of markers with localNetLength > 0
         // (addNodeReferences, mergeTree.ts:270-285): not removed ones
@@ -2527,18 +2576,18 @@ struct Engine {
             const int32_t slot = base + lane;
             uint32_t meta = 0;
             bool live = false, sett = false;
-            uint32_t add = 0, b = 0;
+            uint32_t add = 0, b = 0, sr = 0, cm = 0;
             if (slot < slot_top) {
                 meta = s_meta[slot];
-                live = (meta & kMetaLinked) != 0;
+                live = (meta & kFLinked) != 0;
                 if (live) {
-                    const uint4 q = cold[2 * slot + 1];  // the loaded segment's real seqs
+                    const uint4 q = cold[2 * slot + 1];  // the loaded segment's real seqs and clients
                     const int32_t sq = (int32_t)q.x, rs = (int32_t)q.y;
                     sett = sq <= min_seq && (rs == kNoneSeq || rs <= min_seq);
                     if (sett && rs == kNoneSeq) add = s_len[slot];
                     b = s_blk[slot];
-                    s_sr[slot] = sett ? (rs == kNoneSeq ? kSeq16None : 0u) << 16
-                                      : rel16(sq) | ((rs == kNoneSeq ? kSeq16None : rel16(rs)) << 16);
+                    sr = rel16(sq) | ((rs == kNoneSeq ? kSeq16None : rel16(rs)) << 16);
+                    cm = (q.z & kMetaCli) | (((q.z >> 16) & kMetaCli) << 12);
                 }
             }
             const bool un = live && !sett;
@@ -2548,8 +2597,11 @@ struct Engine {
                 return;
             }
             if (un) {
-                s_meta[slot] = meta | kMetaUnsettled;
-                u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (Idx)slot;
+                const uint32_t e = (uint32_t)nu + (uint32_t)__popcll(um & ((1ull << lane) - 1ull));
+                s_meta[slot] = (Meta)((meta & ~kUNone) | e);
+                u_list[e] = (Idx)slot;
+                u_sr[e] = sr;
+                u_cm[e] = cm;
             }
             nu += __popcll(um);
             if (nu > max_u) max_u = nu;
@@ -2564,7 +2616,10 @@ struct Engine {
         for (int32_t base = 0; base < slot_top; base += kWave) {
             const int32_t slot = base + lane;
             uint32_t v = 0;
-            if (slot < slot_top && (s_meta[slot] & kMetaLinked) && !sr_removed(s_sr[slot])) v = s_len[slot];
+            if (slot < slot_top) {
+                const uint32_t m = s_meta[slot];
+                if ((m & kFLinked) && !(m & kFRemoved)) v = s_len[slot];
+            }
             sum += rdl(scan_incl(v), 63);
         }
         return sum;
@@ -2608,8 +2663,10 @@ struct Engine {
     MT_FI void ovl_add(uint32_t slot, uint64_t m, uint32_t c) {
         for (; m; m &= m - 1) {
             const uint32_t sl = rdl(slot, first_lane(m));
-            const bool had = (s_meta[sl] & kMetaHasOvl) != 0;
-            const uint32_t o = had ? rfl(cold[2 * sl].y) : 0u;
+            // a concurrently removed segment visible to the op: unsettled
+            const uint32_t ui = rfl((uint32_t)s_meta[sl]) & kUNone;
+            const uint32_t cm = rfl(u_cm[ui]);
+            const uint32_t o = (cm & kCmOvl) ? rfl(cold[2 * sl].y) : 0u;
             if (!(o & kOvlList) && c < kOvlMaskClients) {
                 if (lane == 0) cold[2 * sl].y = o | (1u << c);
             } else {
@@ -2637,7 +2694,7 @@ struct Engine {
                     cold[2 * sl].y = id | kOvlList;
                 }
             }
-            s_meta[sl] = s_meta[sl] | kMetaHasOvl;
+            u_cm[ui] = cm | kCmOvl;
             wsync();
         }
     }
@@ -2694,44 +2751,55 @@ struct Engine {
             const bool hit = lane < n && lane < kMaxNodes && vlen > 0u && excl < end && incl > start;
             uint64_t hb = ballot(hit);
             const uint32_t bend = n > 0 ? rdl(incl, n - 1) : base;
-            bool again = false;
-            if (is_remove && hit) {
-                const uint32_t sr = s_sr[slot];
-                if (sr_removed(sr) && !(kW && (sr >> 16) == kSeq16Unassigned)) {
-                    again = true;  // a concurrent remover: addOverlappingClient below
-                } else {
-                    // first remover; or (writer) a sequenced remove replacing a pending local one
-                    // (mergeTree.ts:2624-2630: its client and seq, no overlap entry)
-                    s_sr[slot] = (sr & 0xFFFFu) | ((local ? kSeq16Unassigned : rel16(op.seq)) << 16);
-                    s_meta[slot] = (s_meta[slot] & ~(kMetaCli << kMetaRcliShift)) | ((c & kMetaCli) << kMetaRcliShift);
-                    cold[2 * slot + 1].y = (uint32_t)op.seq;
-                }
-            }
-            const uint64_t againM = ballot(again);
-            if (againM) {
-                ovl_add(slot, againM, c);
-                if (status) return;
-            }
             if (is_remove) {
+                uint32_t meta = 0, ui = kUNone, sr = 0, cm = 0;
+                if (hit) {
+                    meta = s_meta[slot];
+                    ui = meta & kUNone;
+                    if (ui != kUNone) {
+                        sr = u_sr[ui];
+                        cm = u_cm[ui];
+                    }
+                }
+                // a visible leaf already removed is a concurrent removal (hence unsettled):
+                // addOverlappingClient below; a pending local removal is replaced instead
+                const bool again = hit && (meta & kFRemoved) && !(kW && (sr >> 16) == kSeq16Unassigned);
+                // first remover; or (writer) a sequenced remove replacing a pending local one
+                // (mergeTree.ts:2624-2630: its client and seq, no overlap entry)
+                const bool first = hit && !again;
+                const uint32_t r16 = local ? kSeq16Unassigned : rel16(op.seq);
                 // a settled leaf removed now leaves the settled sums and joins the overlay
-                // (a visible leaf already removed is concurrent, hence already unsettled)
-                uint32_t meta = hit ? s_meta[slot] : 0u;
-                const bool newu = hit && !(meta & kMetaUnsettled);
+                const bool newu = first && ui == kUNone;
                 const uint64_t um = ballot(newu);
+                if (um && nu + __popcll(um) > cap.ulist) {
+                    cap_fail(1);
+                    return;
+                }
+                const uint32_t lost = um ? rdl(sum8(newu ? s_len[slot] : 0u), 0) : 0u;
+                wsync();
+                if (first) {
+                    if (ui != kUNone) {
+                        u_sr[ui] = (sr & 0xFFFFu) | (r16 << 16);
+                        u_cm[ui] = (cm & ~(kMetaCli << 12)) | ((c & kMetaCli) << 12);
+                    } else {
+                        ui = (uint32_t)nu + (uint32_t)__popcll(um & ((1ull << lane) - 1ull));
+                        u_list[ui] = (Idx)slot;
+                        u_sr[ui] = r16 << 16;  // seq <= minSeq: seq16 0 (its clientId is never compared)
+                        u_cm[ui] = kNoClient | ((c & kMetaCli) << 12);
+                    }
+                    s_meta[slot] = (Meta)(((meta | kFRemoved) & ~kUNone) | ui);
+                    cold[2 * slot + 1].y = (uint32_t)op.seq;
+                    reinterpret_cast<uint16_t *>(&cold[2 * slot + 1].z)[1] = (uint16_t)(c & kMetaCli);
+                }
                 if (um) {
-                    if (nu + __popcll(um) > cap.ulist) {
-                        cap_fail(1);
-                        return;
-                    }
-                    const uint32_t lost = rdl(sum8(newu ? s_len[slot] : 0u), 0);
-                    wsync();
-                    if (newu) {
-                        s_meta[slot] = meta | kMetaUnsettled;
-                        u_list[nu + __popcll(um & ((1ull << lane) - 1ull))] = (Idx)slot;
-                    }
                     nu += __popcll(um);
                     if (nu > max_u) max_u = nu;
                     chain_add_uniform(blk, 0u - lost);
+                }
+                const uint64_t againM = ballot(again);
+                if (againM) {
+                    ovl_add(slot, againM, c);
+                    if (status) return;
                 }
             }
             wsync();
@@ -2755,7 +2823,7 @@ struct Engine {
                     uint64_t mb = ballot((uint32_t)lane < memo_n && memo_old == old);
                     uint32_t nid, nh;
                     bool pseg = false;
-                    if constexpr (kW) pseg = !local && (s_meta[sl] & kMetaPending);
+                    if constexpr (kW) pseg = !local && (s_meta[sl] & kFPending);
                     if (pseg) {
                         // a remote annotate of a segment with pending local annotates
                         // (segmentPropertiesManager.ts:48-92): nothing while a local rewrite is
@@ -2787,7 +2855,7 @@ struct Engine {
                         }
                     }
                     if (lane == 0) cold[2 * sl].x = nid;
-                    if (nid) s_meta[sl] = s_meta[sl] | kMetaHasProps;
+                    if (nid) s_meta[sl] = (Meta)(s_meta[sl] | kFHasProps);
                 }
                 if (local) pend_add(sl, op);
                 else add_to_lru(blk, sl, op.seq);
@@ -2860,7 +2928,7 @@ struct Engine {
             return;
         }
         resolve_cold();
-        const uint32_t head = pend_word(1), gb = head & 63u;
+        const uint32_t head = pend_word(1), gb = head & kPmb;
         const uint32_t L = rfl(pdesc(head)[3]);
         if ((rfl(pdesc(head)[0]) & 0xFFu) != T) {
             set_fail(ST_BAD_INPUT);
@@ -2882,24 +2950,24 @@ struct Engine {
         for (; blk >= 0 && !status; blk = next_leaf_block(blk)) {
             const int32_t n = b_count[blk];
             uint32_t slot = 0, meta = 0, len = 0, sr = 0;
-            uint64_t m = 0;
+            uint32_t m = 0;
             bool member = false;
             uint32_t contrib = 0;
             if (lane < n) {
                 slot = b_child[blk * 8 + lane];
                 meta = s_meta[slot];
                 len = s_len[slot];
-                sr = s_sr[slot];
+                // seq16 | rseq16 << 16 (a settled leaf: 0, and 0 or kSeq16None for the removal)
+                sr = !is_settled(meta) ? u_sr[meta & kUNone] : ((meta & kFRemoved) ? 0u : kSeq16None << 16);
                 // seg.localSeq / localRemovedSeq: the localSeq of its pending insert / remove group
                 uint32_t ins_l = 0xFFFFFFFFu, rem_l = 0xFFFFFFFFu;
-                if (meta & kMetaPending) {
-                    const uint4 q = cold[2 * slot + 1];
-                    m = (uint64_t)q.z | ((uint64_t)q.w << 32);
-                    member = (m >> gb) & 1ull;
-                    for (uint64_t mm = m; mm; mm &= mm - 1) {
-                        // the live group of bit bi (exact while <= 64 are pending; else recomputed below)
-                        const uint32_t bi = (uint32_t)__builtin_ctzll(mm);
-                        const uint32_t *dp = pdesc(head + ((bi - head) & 63u));
+                if (meta & kFPending) {
+                    m = cold[2 * slot + 1].w;
+                    member = (m >> gb) & 1u;
+                    for (uint32_t mm = m; mm; mm &= mm - 1) {
+                        // the live group of bit bi (exact while <= 32 are pending; else recomputed below)
+                        const uint32_t bi = (uint32_t)__builtin_ctz(mm);
+                        const uint32_t *dp = pdesc(head + ((bi - head) & kPmb));
                         const uint32_t t = dp[0] & 0xFFu, ls = dp[3];
                         if (t == MT_OP_INSERT) ins_l = ls;
                         if (t == MT_OP_REMOVE) rem_l = ls;
@@ -2907,24 +2975,24 @@ struct Engine {
                 }
                 const bool pins = (sr & 0xFFFFu) == kSeq16Unassigned, prem = (sr >> 16) == kSeq16Unassigned;
                 const bool inserted = !pins || ins_l <= L;
-                const bool not_removed = !sr_removed(sr) || (prem && rem_l != 0xFFFFFFFFu && rem_l > L);
+                const bool not_removed = !(meta & kFRemoved) || (prem && rem_l != 0xFFFFFFFFu && rem_l > L);
                 contrib = inserted && not_removed ? len : 0u;
             }
-            if (n_pend > 64) {
-                // more than 64 groups pending: mask bits are shared by groups 64 apart, so the
+            if (n_pend > kPendMaskBits) {
+                // more than 32 groups pending: mask bits are shared by groups 32 apart, so the
                 // segment's insert / remove groups and membership come from the entry lists
-                uint64_t pm = ballot(lane < n && (meta & kMetaPending));
+                uint64_t pm = ballot(lane < n && (meta & kFPending));
                 while (pm) {
                     const int f = first_lane(pm);
                     pm &= pm - 1;
                     const uint32_t sl = rdl(slot, f);
-                    const uint64_t mf = (uint64_t)rdl((uint32_t)m, f) | ((uint64_t)rdl((uint32_t)(m >> 32), f) << 32);
+                    const uint32_t mf = rdl(m, f);
                     const uint32_t il = group_lseq(sl, mf, MT_OP_INSERT), rl = group_lseq(sl, mf, MT_OP_REMOVE);
                     const bool mem = in_group(head, sl, mf);
                     if (lane == f) {
                         const bool pins = (sr & 0xFFFFu) == kSeq16Unassigned, prem = (sr >> 16) == kSeq16Unassigned;
                         const bool inserted = !pins || il <= L;
-                        const bool not_removed = !sr_removed(sr) || (prem && rl != 0xFFFFFFFFu && rl > L);
+                        const bool not_removed = !(meta & kFRemoved) || (prem && rl != 0xFFFFFFFFu && rl > L);
                         contrib = inserted && not_removed ? len : 0u;
                         member = mem;
                     }
@@ -2939,7 +3007,7 @@ struct Engine {
                 mb &= mb - 1;
                 const uint32_t sl = rdl(slot, f), pos = rdl(excl, f), ln = rdl(len, f), sr_f = rdl(sr, f);
                 const uint32_t mt_f = rdl(meta, f);
-                const uint64_t mask = (uint64_t)rdl((uint32_t)m, f) | ((uint64_t)rdl((uint32_t)(m >> 32), f) << 32);
+                const uint32_t mask = rdl(m, f);
                 bool made = true;
                 uint32_t w[kRegenOpWords] = {T, pos, pos + ln, 0u, 0u, 0u, 0u, 0u};
                 uint32_t props = 0, np = 0;
@@ -2949,10 +3017,10 @@ struct Engine {
                         return;
                     }
                     const uint4 cr = cold[2 * sl];
-                    w[3] = (mt_f & kMetaMarker) ? (1u | (rfl(cr.z) << 1)) : 0u;
-                    w[4] = (mt_f & kMetaMarker) ? 0u : rfl(cr.z);
+                    w[3] = (mt_f & kFMarker) ? (1u | (rfl(cr.z) << 1)) : 0u;
+                    w[4] = (mt_f & kFMarker) ? 0u : rfl(cr.z);
                     w[5] = ln;
-                    props = (mt_f & kMetaHasProps) ? rfl(cr.x) : 0u;
+                    props = (mt_f & kFHasProps) ? rfl(cr.x) : 0u;
                     np = props ? pool[props] : 0xFFFFFFFFu;
                     w[6] = np;
                 } else if (T == MT_OP_REMOVE) {
@@ -2962,7 +3030,7 @@ struct Engine {
                     w[4] = op.payload;
                     w[5] = op.payload_len;
                 }
-                uint64_t nm = bit_free_after(head, sl, head, head) ? mask & ~(1ull << gb) : mask;
+                uint32_t nm = bit_free_after(head, sl, head, head) ? mask & ~(1u << gb) : mask;
                 if (made) {
                     const uint32_t words = kRegenOpWords + (np != 0xFFFFFFFFu ? 2u * np : 0u);
                     if (used + words > (uint32_t)regen_cap) {
@@ -2992,7 +3060,7 @@ struct Engine {
                     n_pend++;
                     entry_append(ng, sl);
                     if (status) return;
-                    nm |= 1ull << (ng & 63u);
+                    nm |= 1u << (ng & kPmb);
                 }
                 pend_set_mask(sl, nm);
             }
@@ -3082,21 +3150,14 @@ struct Engine {
             for (int32_t base = 0; base < nu; base += kWave) {
                 const int32_t j = base + lane;
                 uint32_t vlen = 0;
-                if (j < nu) {
-                    const uint32_t slot = u_list[j];
-                    const uint32_t meta = s_meta[slot];
-                    if ((meta & kMetaUnsettled) && (meta & kMetaLinked)) {
-                        bool tie;
-                        view_of(slot, ref, c, vlen, tie);
-                    }
-                }
+                if (j < nu) vlen = view_entry((uint32_t)j, u_list[j], ref, c);
                 sum += rdl(scan_incl(vlen), 63);
             }
         } else {
             for (int32_t base = 0; base < slot_top; base += kWave) {
                 const int32_t slot = base + lane;
                 uint32_t vlen = 0;
-                if (slot < slot_top && (s_meta[slot] & kMetaLinked)) {
+                if (slot < slot_top && (s_meta[slot] & kFLinked)) {
                     bool tie;
                     view_of((uint32_t)slot, ref, c, vlen, tie);
                 }
@@ -3187,10 +3248,12 @@ struct Engine {
         }
         uint32_t *p = ck + kCkHdr;
         dump(p, s_len, slot_top);
-        dump(p, s_sr, slot_top);
-        dump(p, s_meta, slot_top);
-        dump(p, s_blk, slot_top);
+        for (int32_t i = lane; i < slot_top; i += kWave) p[i] = meta_canon(s_meta[i]);
+        p += slot_top;
+        dump_blk(p, s_blk, slot_top);  // (free slots: the free-list links)
         dump(p, u_list, nu);
+        dump(p, u_sr, nu);
+        dump(p, u_cm, nu);
         dump_blk(p, b_parent, blk_top);
         dump(p, b_child, 8 * blk_top);  // one word per child entry: the image is index-width independent
         for (int32_t i = lane; i < blk_top; i += kWave)
@@ -3234,10 +3297,12 @@ struct Engine {
         pool_end = pool_base + semi_p;
         const uint32_t *p = ck + kCkHdr;
         load(p, s_len, slot_top);
-        load(p, s_sr, slot_top);
-        load(p, s_meta, slot_top);
-        load(p, s_blk, slot_top);
+        for (int32_t i = lane; i < slot_top; i += kWave) s_meta[i] = (Meta)meta_uncanon(p[i]);
+        p += slot_top;
+        load_blk(p, s_blk, slot_top);
         load(p, u_list, nu);
+        load(p, u_sr, nu);
+        load(p, u_cm, nu);
         if constexpr (kGiant) {
             restore_giant_blocks(p, blk_top);
             p += 11 * (int64_t)rfl(ck[5]);
@@ -3327,7 +3392,7 @@ struct Engine {
         }
         for (int32_t b0 = 0; b0 < slot_top; b0 += kWave) {
             const int32_t sl = b0 + lane;
-            if (sl < slot_top && (s_meta[sl] & kMetaLinked)) s_blk[sl] = (Idx)tmap[(uint32_t)s_blk[sl]];
+            if (sl < slot_top && (s_meta[sl] & kFLinked)) s_blk[sl] = (Idx)tmap[(uint32_t)s_blk[sl]];
         }
         wsync();
         root = (int32_t)rfl(tmap[root]);
@@ -3367,8 +3432,8 @@ struct Engine {
                     r.len = s_len[slot];
                     r.seq = (int32_t)sq.x;
                     r.rseq = (int32_t)sq.y;
-                    r.meta = s_meta[slot] & (kMetaHasOvl * 2u - 1u) & ~kMetaUnsettled;
-                    r.ovl = (s_meta[slot] & kMetaHasOvl) ? cr.y : 0u;
+                    r.meta = meta_out(s_meta[slot], sq.z, cr.y);
+                    r.ovl = cr.y;
                     r.props = cr.x;
                     r.toff = cr.z;
                     r.blk = (uint32_t)blk;
@@ -3513,7 +3578,7 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
                 const int32_t hn = (int32_t)rfl(ck[9]), nu = (int32_t)rfl(ck[10]);
                 if (P.ck_out && (nu + 24 > E.cap.ulist || hn + 16 > E.cap.heap)) {
                     const int32_t st = (int32_t)rfl(ck[2]), bt = (int32_t)rfl(ck[5]);
-                    const int64_t words = kCkHdr + 4ll * st + nu + 11ll * bt + 2ll * (hn + 1);
+                    const int64_t words = ck_used_words(st, nu, bt, hn);
                     uint32_t *out = P.ck_out + w * ck_words(SEG);
                     for (int64_t i = E.lane; i < words; i += kWave) out[i] = ck[i];
                     for (int64_t i = E.lane; i < (int64_t)kColdPerSlot * st; i += kWave) E.cold[i] = cold_src[i];

@@ -34,23 +34,7 @@
     extern "C" __global__ void mt_writer_kernel_##S(mt::ReplayParams P);      \
     extern "C" __global__ void mt_load_kernel_##S(mt::ReplayParams P);        \
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);
-MT_DECLARE_CLASS(128)
-MT_DECLARE_CLASS(363)
-MT_DECLARE_CLASS(423)
-MT_DECLARE_CLASS(483)
-MT_DECLARE_CLASS(540)
-MT_DECLARE_CLASS(600)
-MT_DECLARE_CLASS(720)
-MT_DECLARE_CLASS(840)
-MT_DECLARE_CLASS(960)
-MT_DECLARE_CLASS(1136)
-MT_DECLARE_CLASS(1376)
-MT_DECLARE_CLASS(1792)
-MT_DECLARE_CLASS(2389)
-MT_DECLARE_CLASS(3600)
-MT_DECLARE_CLASS(7266)
-MT_DECLARE_CLASS(2000000)
-MT_DECLARE_CLASS(2097152)
+MT_CLASS_LIST(MT_DECLARE_CLASS)
 extern "C" __global__ void mt_digest_kernel(mt::DigestParams P);
 extern "C" __global__ void jg_markers_kernel(const mt_op *ops, const int64_t *op_off, mt_op *ops_w, const mt_prop *props,
                                              int64_t D, uint32_t mk_key, uint32_t tile_key, uint32_t range_key,
@@ -90,42 +74,10 @@ struct KernelClass {
     const void *load;
     const void *writer;  // replay + the local-client path (writer replicas)
 };
-static const KernelClass kKernels[mt::kNumClasses] = {
-    {128, (const void *)mt_replay_kernel_128, (const void *)mt_generate_kernel_128, (const void *)mt_load_kernel_128,
-     (const void *)mt_writer_kernel_128},
-    {363, (const void *)mt_replay_kernel_363, (const void *)mt_generate_kernel_363, (const void *)mt_load_kernel_363,
-     (const void *)mt_writer_kernel_363},
-    {423, (const void *)mt_replay_kernel_423, (const void *)mt_generate_kernel_423, (const void *)mt_load_kernel_423,
-     (const void *)mt_writer_kernel_423},
-    {483, (const void *)mt_replay_kernel_483, (const void *)mt_generate_kernel_483, (const void *)mt_load_kernel_483,
-     (const void *)mt_writer_kernel_483},
-    {540, (const void *)mt_replay_kernel_540, (const void *)mt_generate_kernel_540, (const void *)mt_load_kernel_540,
-     (const void *)mt_writer_kernel_540},
-    {600, (const void *)mt_replay_kernel_600, (const void *)mt_generate_kernel_600, (const void *)mt_load_kernel_600,
-     (const void *)mt_writer_kernel_600},
-    {720, (const void *)mt_replay_kernel_720, (const void *)mt_generate_kernel_720, (const void *)mt_load_kernel_720,
-     (const void *)mt_writer_kernel_720},
-    {840, (const void *)mt_replay_kernel_840, (const void *)mt_generate_kernel_840, (const void *)mt_load_kernel_840,
-     (const void *)mt_writer_kernel_840},
-    {960, (const void *)mt_replay_kernel_960, (const void *)mt_generate_kernel_960, (const void *)mt_load_kernel_960,
-     (const void *)mt_writer_kernel_960},
-    {1136, (const void *)mt_replay_kernel_1136, (const void *)mt_generate_kernel_1136, (const void *)mt_load_kernel_1136,
-     (const void *)mt_writer_kernel_1136},
-    {1376, (const void *)mt_replay_kernel_1376, (const void *)mt_generate_kernel_1376, (const void *)mt_load_kernel_1376,
-     (const void *)mt_writer_kernel_1376},
-    {1792, (const void *)mt_replay_kernel_1792, (const void *)mt_generate_kernel_1792, (const void *)mt_load_kernel_1792,
-     (const void *)mt_writer_kernel_1792},
-    {2389, (const void *)mt_replay_kernel_2389, (const void *)mt_generate_kernel_2389, (const void *)mt_load_kernel_2389,
-     (const void *)mt_writer_kernel_2389},
-    {3600, (const void *)mt_replay_kernel_3600, (const void *)mt_generate_kernel_3600, (const void *)mt_load_kernel_3600,
-     (const void *)mt_writer_kernel_3600},
-    {7266, (const void *)mt_replay_kernel_7266, (const void *)mt_generate_kernel_7266, (const void *)mt_load_kernel_7266,
-     (const void *)mt_writer_kernel_7266},
-    {2000000, (const void *)mt_replay_kernel_2000000, (const void *)mt_generate_kernel_2000000, (const void *)mt_load_kernel_2000000,
-     (const void *)mt_writer_kernel_2000000},
-    {2097152, (const void *)mt_replay_kernel_2097152, (const void *)mt_generate_kernel_2097152, (const void *)mt_load_kernel_2097152,
-     (const void *)mt_writer_kernel_2097152},
-};
+#define MT_KERNEL_CLASS_(S) {S, (const void *)mt_replay_kernel_##S, (const void *)mt_generate_kernel_##S, \
+                             (const void *)mt_load_kernel_##S, (const void *)mt_writer_kernel_##S},
+static const KernelClass kKernels[mt::kNumClasses] = {MT_CLASS_LIST(MT_KERNEL_CLASS_)};
+#undef MT_KERNEL_CLASS_
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
 
 struct Launch {
@@ -495,6 +447,7 @@ static const char kBuildId[] = MT_BUILD_ID;  // "MTBUILDID:" + 16 hex digits (bu
 extern "C" {
 
 MT_API const char *mt_build_id(void) { return kBuildId + 10; }
+MT_API int32_t mt_abi_version(void) { return MT_ABI_VERSION; }
 
 MT_API const char *mt_status_string(int code) {
     switch (code) {

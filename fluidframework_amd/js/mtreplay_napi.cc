@@ -459,6 +459,11 @@ constexpr napi_property_attributes kMethod =
     static_cast<napi_property_attributes>(napi_writable | napi_enumerable | napi_configurable);
 
 napi_value init(napi_env env, napi_value exports) {
+    // the library must speak this header's binary interface (struct layouts, signatures)
+    if (mt_abi_version() != MT_ABI_VERSION) {
+        napi_throw_error(env, nullptr, "libmtreplay.so: C ABI version differs from include/mtreplay.h");
+        return nullptr;
+    }
     const napi_property_descriptor d[] = {
         {"createBatch", nullptr, create_batch, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"setTables", nullptr, set_tables, nullptr, nullptr, nullptr, kMethod, nullptr},

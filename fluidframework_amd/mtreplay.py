@@ -28,6 +28,7 @@ import numpy as np
 from .oplog import OP_DTYPE, PROP_DTYPE, PackedBatch, Packer
 
 LIB_PATH = Path(os.environ.get("FLUIDFRAMEWORK_AMD_LIB") or Path(__file__).resolve().parent / "libmtreplay.so")
+ABI_VERSION = 4  # include/mtreplay.h MT_ABI_VERSION
 
 MT_OK, MT_INVALID_POS, MT_SEQ_ORDER, MT_MSN_ORDER, MT_UNSUPPORTED, MT_BAD_INPUT, MT_CAPACITY, MT_INTERNAL = range(8)
 MT_ERR_HIP, MT_ERR_ARG, MT_ERR_STATE, MT_ERR_NO_DEVICE = 100, 101, 102, 103
@@ -43,7 +44,7 @@ EXPORTS = [
     "mt_batch_snapshot_digests", "mt_batch_generate_docs", "mt_pack_json", "mt_packed_destroy", "mt_packed_error",
     "mt_packed_sizes", "mt_packed_arrays", "mt_packed_key", "mt_packed_value", "mt_packed_doc_clients",
     "mt_packed_client", "mt_batch_ingest_packed", "mt_batch_log_sizes_docs", "mt_batch_download_log_docs",
-    "mt_build_id", "mt_doc_find_tile", "mt_doc_regenerated_ops", "mt_pack_json_gpu", "mt_batch_ingest_json_gpu",
+    "mt_build_id", "mt_abi_version", "mt_doc_find_tile", "mt_doc_regenerated_ops", "mt_pack_json_gpu", "mt_batch_ingest_json_gpu",
     "mt_doc_stack_context",
 ]
 SNAP_MAX_BLOBS = 32
@@ -150,6 +151,10 @@ def lib():
         if got != want:
             raise RuntimeError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
                                "rebuild with __graft_entry__.build()")
+    L.mt_abi_version.argtypes = []
+    L.mt_abi_version.restype = C.c_int32
+    if L.mt_abi_version() != ABI_VERSION:  # struct layouts below are those of include/mtreplay.h v4
+        raise RuntimeError(f"{LIB_PATH}: C ABI version {L.mt_abi_version()}, this binding speaks {ABI_VERSION}")
     L.mt_status_string.argtypes = [C.c_int]
     L.mt_status_string.restype = cp
     L.mt_batch_create.argtypes = [P(vp), i64, P(BatchOptions)]

@@ -50,6 +50,13 @@ extern "C" {
 
 #define MT_API __attribute__((visibility("default")))
 
+/* Version of this header's binary interface: bumped on every change of a struct layout or an entry
+   point's signature, so a binding built against another header fails at load (mt_abi_version())
+   instead of passing fields at the wrong offsets.
+   4: round 3 dropped oe_cap / blk_cap / heap_cap from mt_batch_options and added n_docs to
+      mt_batch_ingest_json_gpu; round 4 added mt_abi_version. */
+#define MT_ABI_VERSION 4
+
 enum mt_status_code {
     MT_OK = 0,
     MT_INVALID_POS = 1,  /* "MergeTree insert failed" */
@@ -244,6 +251,8 @@ MT_API int mt_batch_download_log_docs(mt_batch *b, int64_t d0, int64_t d1, mt_op
                                       uint16_t *text, mt_prop *props);
 /* hash of the sources this library was built from (__graft_entry__.py SRC, sha256 hex prefix) */
 MT_API const char *mt_build_id(void);
+/* MT_ABI_VERSION of the header the library was built with */
+MT_API int32_t mt_abi_version(void);
 
 #ifdef __cplusplus
 }
