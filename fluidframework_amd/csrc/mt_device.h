@@ -89,10 +89,8 @@ constexpr uint32_t kCanonNoEntry = 0xFFFFFFu;
 // a writer replica's pending-group membership: bit G & 31 of the 32-bit mask in the slot's cold
 // record (cold[2 slot + 1].w) for group G
 constexpr int kPendMaskBits = 32;
-constexpr uint32_t kSeq16None = 0xFFFFu;  // rseq16 of a segment that is not removed
-constexpr uint32_t kSeq16Unassigned = 0xFFFEu;  // seq16 / rseq16 of a pending local insert / remove
 constexpr int32_t kUnassignedSeq = -1;  // UnassignedSequenceNumber (constants.ts:11): real seqs of pending ops
-constexpr int32_t kSeq16Span = 0xFFF0;    // cur_seq - base must stay below (else MT_CAPACITY, cap_kind 5)
+constexpr int32_t kSeq16Span = 0xFFF0;    // LDS classes: cur_seq - base must stay below (else cap_kind 8)
 constexpr uint32_t kHeapInvalid = 0xFFFFFFFFu;  // heap entry whose segment was merged away / unlinked
 constexpr uint16_t kNoBlock = 0xFFFFu;
 
@@ -127,10 +125,12 @@ struct DocOut {
     int32_t max_heap;
     int32_t fail_op;    // index of the op that failed (-1)
     int32_t cap_kind;   // ST_CAPACITY cause: 1 LDS tables, 2 text arena, 3 prop pool, 4 out records,
-                        // 5 collab window wider than kSeq16Span ops (16-bit relative seqs),
+                        // 5 (unused since round 4: a collab window wider than kSeq16Span ops
+                        //   re-runs in a spill class, cap_kind 8),
                         // 6 LDS headroom: state checkpointed before op ops_done (resumable),
-                        // 8 a segment longer than an LDS class's 16-bit lengths: re-run from
-                        //   scratch in the HBM class
+                        // 8 a segment longer than an LDS class's 16-bit lengths, or a collab
+                        //   window of kSeq16Span ops or more (16-bit relative seqs): re-run from
+                        //   scratch in a spill class (32-bit lengths and relative seqs)
     int32_t gen_text;   // generator: payload code units written
     int32_t gen_props;  // generator: prop records written
 };
@@ -188,7 +188,7 @@ constexpr int kGiantHeap = 1024;
 constexpr int kGiantUlist = 1024;
 constexpr int kGiantChainRec = 4;  // HBM-resident blocks recorded per overlay list entry
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
-constexpr int kCapLongSeg = 8;     // a segment length beyond 0xFFFF in an LDS class (16-bit lengths)
+constexpr int kCapLongSeg = 8;     // beyond an LDS class's 16-bit lengths or relative seqs: a spill class
 
 // Writer replicas (the local-client path, mergeTree.ts:1893-1929, client.ts:588-625): per document
 // a pending-group region in HBM, persistent across launches (u32 words):
@@ -217,11 +217,12 @@ constexpr int kRegenOpWords = 8;
 
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table
 constexpr int kCkHdr = 32;
-constexpr int64_t ck_words(int seg) { return 8ll * seg + 1024; }
+constexpr int64_t ck_words(int seg) { return 9ll * seg + 1024; }
 // the words a checkpoint image uses: per slot len, canonical meta, block; per overlay entry slot,
-// seqs, clients; per block parent, 8 children, count | leaf | scour, settled length; the heap
+// seq, removedSeq (32-bit relative), clients; per block parent, 8 children, count | leaf | scour,
+// settled length; the heap
 constexpr int64_t ck_used_words(int64_t slots, int64_t nu, int64_t blocks, int64_t hn) {
-    return kCkHdr + 3 * slots + 3 * nu + 11 * blocks + 2 * (hn + 1);
+    return kCkHdr + 3 * slots + 4 * nu + 11 * blocks + 2 * (hn + 1);
 }
 // cold records per slot in HBM: {props, ovl, toff, tcap} and {seq, rseq, clientId | removedClientId
 // << 16, pending-group mask (writers)} (the real seqs and client ids)
@@ -278,7 +279,7 @@ constexpr Layout make_layout(int seg) {
     L.meta = o;    o = lds_align(o + meta_bytes(seg) * c.seg);
     L.sblk = o;    o = lds_align(o + idx_bytes(seg) * c.seg);   // a free slot's s_blk links the free list
     L.ulist = o;   o = lds_align(o + idx_bytes(seg) * c.ulist);
-    L.usr = o;     o = lds_align(o + 4u * c.ulist);
+    L.usr = o;     o = lds_align(o + (is_hbm_seg(seg) ? 8u : 4u) * c.ulist);
     L.ucm = o;     o = lds_align(o + 4u * c.ulist);
     L.bparent = o; o = lds_align(o + idx_bytes(seg) * c.blk);  // a free block's b_parent links the free list
     L.bchild = o;  o = lds_align(o + 8u * idx_bytes(seg) * c.blk);
@@ -304,7 +305,7 @@ constexpr Layout make_glayout() {
     L.scratch = o; o = lds_align(o + 4u * 128);
     L.heap = o;    o = lds_align(o + 8u * (kGiantHeap + 2));
     L.ulist = o;   o = lds_align(o + 4u * kGiantUlist);
-    L.usr = o;     o = lds_align(o + 4u * kGiantUlist);
+    L.usr = o;     o = lds_align(o + 8u * kGiantUlist);
     L.ucm = o;     o = lds_align(o + 4u * kGiantUlist);
     L.bparent = o; o = lds_align(o + 4u * K);
     L.bchild = o;  o = lds_align(o + 32u * K);

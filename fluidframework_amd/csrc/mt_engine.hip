@@ -233,12 +233,23 @@ struct Engine {
     static_assert(cap.ulist < (int32_t)kUNone, "overlay-entry index");
     // u_cm: clientId | removedClientId << 12 | has-overlap
     static constexpr uint32_t kCmOvl = 1u << 24;
+    // an overlay entry's sequence numbers relative to sbase: seq | removedSeq << kRB, 16-bit each in
+    // the LDS classes (a collab window of kSeq16Span ops or more moves the document to a spill
+    // class), 32-bit in the giant and HBM classes (no window limit)
+    using USr = std::conditional_t<kHbm, uint64_t, uint32_t>;
+    static constexpr int kRB = kHbm ? 32 : 16;
+    static constexpr uint32_t kRMask = kHbm ? 0xFFFFFFFFu : 0xFFFFu;
+    static constexpr uint32_t kRNone = kRMask;             // removedSeq === undefined
+    static constexpr uint32_t kRUnassigned = kRMask - 1u;  // a pending local insert / remove
+    MT_FI static uint32_t us_q(USr x) { return (uint32_t)x & kRMask; }
+    MT_FI static uint32_t us_r(USr x) { return (uint32_t)(x >> kRB); }
+    MT_FI static USr us_make(uint32_t q, uint32_t r) { return (USr)q | ((USr)r << kRB); }
     // ---- LDS state
     Len *s_len;
     Meta *s_meta;  // flags | overlay-entry index; a free slot: kUNone
     Idx *s_blk;    // leaf block; of a free slot: the next free slot (kNoBlk ends the list)
     Idx *u_list;   // overlay entries: exactly the unsettled slots, unordered
-    uint32_t *u_sr;  // seq16 | rseq16 << 16, relative to sbase (kSeq16None: not removed)
+    USr *u_sr;       // seq | rseq << kRB, relative to sbase (kRNone: not removed)
     uint32_t *u_cm;  // clientId | removedClientId << 12 | kCmOvl
     BA<Idx> b_parent;  // b_parent of a free block links the free block list
     BA<Idx, 3> b_child;
@@ -309,7 +320,7 @@ struct Engine {
         uint8_t *xb = kGiant ? lb : tb;  // the per-op state: in LDS for the giant class
         const Layout &xl = kGiant ? glay : lay;
         u_list = (Idx *)(xb + xl.ulist);
-        u_sr = (uint32_t *)(xb + xl.usr);
+        u_sr = (USr *)(xb + xl.usr);
         u_cm = (uint32_t *)(xb + xl.ucm);
         b_parent.p = (decltype(b_parent.p))(tb + lay.bparent);
         b_child.p = (decltype(b_child.p))(tb + lay.bchild);
@@ -471,7 +482,7 @@ struct Engine {
 
     // ------------------------------------------------------------------ visibility
     // seq relative to sbase, clamped at 0 (a value below the base is <= every valid refSeq)
-    MT_FI uint32_t rel16(int32_t q) const {
+    MT_FI uint32_t rel(int32_t q) const {
         const int32_t d = q - sbase;
         return d <= 0 ? 0u : (uint32_t)d;
     }
@@ -504,11 +515,12 @@ struct Engine {
                 tie = !rm;
                 return;
             }
-            const uint32_t sr = u_sr[ui], cm = u_cm[ui];
-            const uint32_t r16 = (uint32_t)(ref - sbase);
-            vis = ((cm & kMetaCli) == c) || ((sr & 0xFFFFu) <= r16);
-            rle = (sr >> 16) <= r16;
-            if constexpr (kW) pending = (sr & 0xFFFFu) == kSeq16Unassigned;
+            const USr sr = u_sr[ui];
+            const uint32_t cm = u_cm[ui];
+            const uint32_t rr = (uint32_t)(ref - sbase);
+            vis = ((cm & kMetaCli) == c) || (us_q(sr) <= rr);
+            rle = us_r(sr) <= rr;
+            if constexpr (kW) pending = us_q(sr) == kRUnassigned;
             rem = (((cm >> 12) & kMetaCli) == c) || rle;
             if (!rem && (cm & kCmOvl)) rem = ovl_has(slot, c);
         } else {
@@ -536,6 +548,9 @@ struct Engine {
         const uint32_t meta = s_meta[slot];
         return (is_settled(meta) && !(meta & kFRemoved)) ? s_len[slot] : 0u;
     }
+    // canonical relative seq of a checkpoint image (32-bit; 0xFFFFFFFF none, 0xFFFFFFFE unassigned)
+    MT_FI static uint32_t canon_rel(uint32_t r) { return r >= kRUnassigned ? r - kRMask + 0xFFFFFFFFu : r; }
+    MT_FI static uint32_t uncanon_rel(uint32_t r) { return r >= 0xFFFFFFFEu ? r - 0xFFFFFFFFu + kRMask : r; }
     // canonical meta of a checkpoint image (mt_device.h kCanonNoEntry) and back
     MT_FI static uint32_t meta_canon(uint32_t m) {
         const uint32_t i = m & kUNone;
@@ -558,11 +573,12 @@ struct Engine {
     }
     // nodeLength of the unsettled segment of overlay entry j (slot) in a valid view (refSeq >= minSeq)
     __device__ __forceinline__ uint32_t view_entry(uint32_t j, uint32_t slot, int32_t ref, uint32_t c) const {
-        const uint32_t sr = u_sr[j], cm = u_cm[j];
+        const USr sr = u_sr[j];
+        const uint32_t cm = u_cm[j];
         const uint32_t len = s_len[slot];
-        const uint32_t r16 = (uint32_t)(ref - sbase);
-        const bool vis = ((cm & kMetaCli) == c) || ((sr & 0xFFFFu) <= r16);
-        bool rem = (((cm >> 12) & kMetaCli) == c) || ((sr >> 16) <= r16);
+        const uint32_t rr = (uint32_t)(ref - sbase);
+        const bool vis = ((cm & kMetaCli) == c) || (us_q(sr) <= rr);
+        bool rem = (((cm >> 12) & kMetaCli) == c) || (us_r(sr) <= rr);
         if (!rem && (cm & kCmOvl)) rem = ovl_has(slot, c);
         return (vis && !rem) ? len : 0u;
     }
@@ -732,7 +748,7 @@ struct Engine {
         if (lane < 8) reinterpret_cast<uint32_t *>(cold + 2 * slot)[lane] = v;
     }
     // a new overlay entry for `slot` (its meta word gets the entry's index)
-    MT_FI void u_push(uint32_t slot, uint32_t sr, uint32_t cm) {
+    MT_FI void u_push(uint32_t slot, USr sr, uint32_t cm) {
         if (nu >= cap.ulist) {
             cap_fail(1);
             return;
@@ -805,16 +821,17 @@ struct Engine {
         for (int32_t b0 = 0; b0 < nu; b0 += kWave) {
             const int32_t j = b0 + lane;
             const bool in = j < nu;
-            uint32_t slot = 0, sr = 0, cm = 0, add = 0, b = 0;
+            uint32_t slot = 0, cm = 0, add = 0, b = 0;
+            USr sr = 0;
             bool elig = false;
             if (in) {
                 slot = u_list[j];
                 sr = u_sr[j];
                 cm = u_cm[j];
-                const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
-                elig = q16 <= m16 && (r16 == kSeq16None || r16 <= m16);
+                const uint32_t q = us_q(sr), r = us_r(sr);
+                elig = q <= m16 && (r == kRNone || r <= m16);
                 if (elig) {
-                    if (r16 == kSeq16None) add = s_len[slot];
+                    if (r == kRNone) add = s_len[slot];
                     b = s_blk[slot];
                 }
             }
@@ -823,15 +840,15 @@ struct Engine {
             const int32_t dst = w + __popcll(km & ((1ull << lane) - 1ull));
             wsync();
             if (keep) {
-                const uint32_t q16 = sr & 0xFFFFu, r16 = sr >> 16;
-                uint32_t nq = q16 > m16 ? q16 - m16 : 0u;
-                uint32_t nr = r16 == kSeq16None ? kSeq16None : (r16 > m16 ? r16 - m16 : 0u);
+                const uint32_t q = us_q(sr), r = us_r(sr);
+                uint32_t nq = q > m16 ? q - m16 : 0u;
+                uint32_t nr = r == kRNone ? kRNone : (r > m16 ? r - m16 : 0u);
                 if constexpr (kW) {  // pending local ops keep their sentinel
-                    if (q16 == kSeq16Unassigned) nq = kSeq16Unassigned;
-                    if (r16 == kSeq16Unassigned) nr = kSeq16Unassigned;
+                    if (q == kRUnassigned) nq = kRUnassigned;
+                    if (r == kRUnassigned) nr = kRUnassigned;
                 }
                 u_list[dst] = (Idx)slot;
-                u_sr[dst] = nq | (nr << 16);
+                u_sr[dst] = us_make(nq, nr);
                 u_cm[dst] = cm;
                 if (dst != j) s_meta[slot] = (Meta)((s_meta[slot] & ~kUNone) | (uint32_t)dst);
             }
@@ -1530,21 +1547,22 @@ struct Engine {
                     hm &= hm - 1;
                     const uint32_t meta = rfl((uint32_t)s_meta[slot]);
                     const uint32_t ui = meta & kUNone;
-                    const uint32_t sr = ui != kUNone ? rfl(u_sr[ui]) : (uint32_t)kSeq16None << 16;
+                    const USr sr = ui != kUNone ? u_sr[ui] : us_make(0u, kRNone);
+                    const uint32_t sq = rfl(us_q(sr)), srr = rfl(us_r(sr));
                     if (op.type == MT_OP_INSERT) {
-                        if (ui == kUNone || (sr & 0xFFFFu) != kSeq16Unassigned) {
+                        if (ui == kUNone || sq != kRUnassigned) {
                             set_fail(ST_BAD_INPUT);
                             return;
                         }
-                        u_sr[ui] = (sr & 0xFFFF0000u) | rel16(op.seq);
+                        u_sr[ui] = us_make(rel(op.seq), srr);
                         if (lane == 0) cold[2 * slot + 1].x = (uint32_t)op.seq;
                     } else if (op.type == MT_OP_REMOVE) {
                         if (!(meta & kFRemoved)) {
                             set_fail(ST_BAD_INPUT);
                             return;
                         }
-                        if (ui != kUNone && (sr >> 16) == kSeq16Unassigned) {
-                            u_sr[ui] = (sr & 0xFFFFu) | (rel16(op.seq) << 16);
+                        if (ui != kUNone && srr == kRUnassigned) {
+                            u_sr[ui] = us_make(sq, rel(op.seq));
                             if (lane == 0) cold[2 * slot + 1].y = (uint32_t)op.seq;
                         }
                     }
@@ -1588,7 +1606,7 @@ struct Engine {
                 if (lane < n) {
                     const uint32_t m = s_meta[b_child[b * 8 + lane]];
                     live = !(m & kFRemoved);
-                    if (live && !is_settled(m)) pins = (u_sr[m & kUNone] & 0xFFFFu) == kSeq16Unassigned;
+                    if (live && !is_settled(m)) pins = us_q(u_sr[m & kUNone]) == kRUnassigned;
                 }
                 const uint64_t lm = ballot(live);
                 if (lm) {
@@ -2436,8 +2454,7 @@ struct Engine {
             if (props) meta |= kFHasProps;
             if (rseq != kNoneSeq) meta |= kFRemoved;
             s_len[slot] = (Len)len;
-            const uint32_t sr = (local ? kSeq16Unassigned : rel16(op.seq)) |
-                                ((rseq == kNoneSeq ? kSeq16None : rel16(rseq)) << 16);
+            const USr sr = us_make(local ? kRUnassigned : rel(op.seq), rseq == kNoneSeq ? kRNone : rel(rseq));
             cold_init(slot, props, op.payload, marker ? 0u : len, (uint32_t)op.seq, (uint32_t)rseq, (c & kMetaCli) | (rcli << 16));
             s_meta[slot] = (Meta)meta;
             wsync();
@@ -2565,8 +2582,8 @@ struct Engine {
         settled_min = min_seq;
         sbase = min_seq;
         ov_splits = -1;
-        if (cur_seq - sbase >= kSeq16Span) {
-            cap_fail(5);
+        if (!kHbm && cur_seq - sbase >= kSeq16Span) {  // 16-bit relative seqs: load in the HBM class
+            cap_fail(kCapLongSeg);
             return;
         }
         wsync();
@@ -2576,7 +2593,8 @@ struct Engine {
             const int32_t slot = base + lane;
             uint32_t meta = 0;
             bool live = false, sett = false;
-            uint32_t add = 0, b = 0, sr = 0, cm = 0;
+            uint32_t add = 0, b = 0, cm = 0;
+            USr sr = 0;
             if (slot < slot_top) {
                 meta = s_meta[slot];
                 live = (meta & kFLinked) != 0;
@@ -2586,7 +2604,7 @@ struct Engine {
                     sett = sq <= min_seq && (rs == kNoneSeq || rs <= min_seq);
                     if (sett && rs == kNoneSeq) add = s_len[slot];
                     b = s_blk[slot];
-                    sr = rel16(sq) | ((rs == kNoneSeq ? kSeq16None : rel16(rs)) << 16);
+                    sr = us_make(rel(sq), rs == kNoneSeq ? kRNone : rel(rs));
                     cm = (q.z & kMetaCli) | (((q.z >> 16) & kMetaCli) << 12);
                 }
             }
@@ -2752,7 +2770,8 @@ struct Engine {
             uint64_t hb = ballot(hit);
             const uint32_t bend = n > 0 ? rdl(incl, n - 1) : base;
             if (is_remove) {
-                uint32_t meta = 0, ui = kUNone, sr = 0, cm = 0;
+                uint32_t meta = 0, ui = kUNone, cm = 0;
+                USr sr = 0;
                 if (hit) {
                     meta = s_meta[slot];
                     ui = meta & kUNone;
@@ -2763,11 +2782,11 @@ struct Engine {
                 }
                 // a visible leaf already removed is a concurrent removal (hence unsettled):
                 // addOverlappingClient below; a pending local removal is replaced instead
-                const bool again = hit && (meta & kFRemoved) && !(kW && (sr >> 16) == kSeq16Unassigned);
+                const bool again = hit && (meta & kFRemoved) && !(kW && us_r(sr) == kRUnassigned);
                 // first remover; or (writer) a sequenced remove replacing a pending local one
                 // (mergeTree.ts:2624-2630: its client and seq, no overlap entry)
                 const bool first = hit && !again;
-                const uint32_t r16 = local ? kSeq16Unassigned : rel16(op.seq);
+                const uint32_t rq = local ? kRUnassigned : rel(op.seq);
                 // a settled leaf removed now leaves the settled sums and joins the overlay
                 const bool newu = first && ui == kUNone;
                 const uint64_t um = ballot(newu);
@@ -2779,12 +2798,12 @@ struct Engine {
                 wsync();
                 if (first) {
                     if (ui != kUNone) {
-                        u_sr[ui] = (sr & 0xFFFFu) | (r16 << 16);
+                        u_sr[ui] = us_make(us_q(sr), rq);
                         u_cm[ui] = (cm & ~(kMetaCli << 12)) | ((c & kMetaCli) << 12);
                     } else {
                         ui = (uint32_t)nu + (uint32_t)__popcll(um & ((1ull << lane) - 1ull));
                         u_list[ui] = (Idx)slot;
-                        u_sr[ui] = r16 << 16;  // seq <= minSeq: seq16 0 (its clientId is never compared)
+                        u_sr[ui] = us_make(0u, rq);  // seq <= minSeq: relative 0 (its clientId is never compared)
                         u_cm[ui] = kNoClient | ((c & kMetaCli) << 12);
                     }
                     s_meta[slot] = (Meta)(((meta | kFRemoved) & ~kUNone) | ui);
@@ -2949,7 +2968,8 @@ struct Engine {
         uint32_t base = 0;
         for (; blk >= 0 && !status; blk = next_leaf_block(blk)) {
             const int32_t n = b_count[blk];
-            uint32_t slot = 0, meta = 0, len = 0, sr = 0;
+            uint32_t slot = 0, meta = 0, len = 0;
+            USr sr = 0;
             uint32_t m = 0;
             bool member = false;
             uint32_t contrib = 0;
@@ -2957,8 +2977,8 @@ struct Engine {
                 slot = b_child[blk * 8 + lane];
                 meta = s_meta[slot];
                 len = s_len[slot];
-                // seq16 | rseq16 << 16 (a settled leaf: 0, and 0 or kSeq16None for the removal)
-                sr = !is_settled(meta) ? u_sr[meta & kUNone] : ((meta & kFRemoved) ? 0u : kSeq16None << 16);
+                // the relative seqs (a settled leaf: 0, and 0 or kRNone for the removal)
+                sr = !is_settled(meta) ? u_sr[meta & kUNone] : us_make(0u, (meta & kFRemoved) ? 0u : kRNone);
                 // seg.localSeq / localRemovedSeq: the localSeq of its pending insert / remove group
                 uint32_t ins_l = 0xFFFFFFFFu, rem_l = 0xFFFFFFFFu;
                 if (meta & kFPending) {
@@ -2973,7 +2993,7 @@ struct Engine {
                         if (t == MT_OP_REMOVE) rem_l = ls;
                     }
                 }
-                const bool pins = (sr & 0xFFFFu) == kSeq16Unassigned, prem = (sr >> 16) == kSeq16Unassigned;
+                const bool pins = us_q(sr) == kRUnassigned, prem = us_r(sr) == kRUnassigned;
                 const bool inserted = !pins || ins_l <= L;
                 const bool not_removed = !(meta & kFRemoved) || (prem && rem_l != 0xFFFFFFFFu && rem_l > L);
                 contrib = inserted && not_removed ? len : 0u;
@@ -2990,7 +3010,7 @@ struct Engine {
                     const uint32_t il = group_lseq(sl, mf, MT_OP_INSERT), rl = group_lseq(sl, mf, MT_OP_REMOVE);
                     const bool mem = in_group(head, sl, mf);
                     if (lane == f) {
-                        const bool pins = (sr & 0xFFFFu) == kSeq16Unassigned, prem = (sr >> 16) == kSeq16Unassigned;
+                        const bool pins = us_q(sr) == kRUnassigned, prem = us_r(sr) == kRUnassigned;
                         const bool inserted = !pins || il <= L;
                         const bool not_removed = !(meta & kFRemoved) || (prem && rl != 0xFFFFFFFFu && rl > L);
                         contrib = inserted && not_removed ? len : 0u;
@@ -3005,14 +3025,15 @@ struct Engine {
             while (mb && !status) {
                 const int f = first_lane(mb);
                 mb &= mb - 1;
-                const uint32_t sl = rdl(slot, f), pos = rdl(excl, f), ln = rdl(len, f), sr_f = rdl(sr, f);
+                const uint32_t sl = rdl(slot, f), pos = rdl(excl, f), ln = rdl(len, f);
+                const uint32_t sq_f = rdl(us_q(sr), f), sr_f = rdl(us_r(sr), f);
                 const uint32_t mt_f = rdl(meta, f);
                 const uint32_t mask = rdl(m, f);
                 bool made = true;
                 uint32_t w[kRegenOpWords] = {T, pos, pos + ln, 0u, 0u, 0u, 0u, 0u};
                 uint32_t props = 0, np = 0;
                 if (T == MT_OP_INSERT) {
-                    if ((sr_f & 0xFFFFu) != kSeq16Unassigned) {  // assert(segment.seq === UnassignedSequenceNumber)
+                    if (sq_f != kRUnassigned) {  // assert(segment.seq === UnassignedSequenceNumber)
                         set_fail(ST_BAD_INPUT);
                         return;
                     }
@@ -3024,7 +3045,7 @@ struct Engine {
                     np = props ? pool[props] : 0xFFFFFFFFu;
                     w[6] = np;
                 } else if (T == MT_OP_REMOVE) {
-                    made = (sr_f >> 16) == kSeq16Unassigned;  // only while the local remove is pending
+                    made = sr_f == kRUnassigned;  // only while the local remove is pending
                 } else {
                     w[3] = op.flags;
                     w[4] = op.payload;
@@ -3096,12 +3117,14 @@ struct Engine {
             set_fail(ST_UNSUPPORTED);
             return;
         }
-        // the 16-bit relative seqs in LDS need seq - sbase < kSeq16Span: rebase on minSeq, and a
-        // collab window wider than that stops the document (MT_CAPACITY, cap_kind 5)
-        if (op.seq - sbase >= kSeq16Span / 2 && min_seq > sbase) settle_all();
-        if (op.seq - sbase >= kSeq16Span) {
-            cap_fail(5);
-            return;
+        // the LDS classes' 16-bit relative seqs need seq - sbase < kSeq16Span: rebase on minSeq; a
+        // collab window wider than that re-runs the document in a spill class (32-bit relative seqs)
+        if constexpr (!kHbm) {
+            if (op.seq - sbase >= kSeq16Span / 2 && min_seq > sbase) settle_all();
+            if (op.seq - sbase >= kSeq16Span) {
+                cap_fail(kCapLongSeg);
+                return;
+            }
         }
         if constexpr (kW) {
             if (op.client == 0 && op.type != MT_OP_NOOP) {
@@ -3252,7 +3275,12 @@ struct Engine {
         p += slot_top;
         dump_blk(p, s_blk, slot_top);  // (free slots: the free-list links)
         dump(p, u_list, nu);
-        dump(p, u_sr, nu);
+        for (int32_t i = lane; i < nu; i += kWave) {  // canonical 32-bit relative seqs
+            const USr x = u_sr[i];
+            p[2 * i] = canon_rel(us_q(x));
+            p[2 * i + 1] = canon_rel(us_r(x));
+        }
+        p += 2 * nu;
         dump(p, u_cm, nu);
         dump_blk(p, b_parent, blk_top);
         dump(p, b_child, 8 * blk_top);  // one word per child entry: the image is index-width independent
@@ -3301,7 +3329,8 @@ struct Engine {
         p += slot_top;
         load_blk(p, s_blk, slot_top);
         load(p, u_list, nu);
-        load(p, u_sr, nu);
+        for (int32_t i = lane; i < nu; i += kWave) u_sr[i] = us_make(uncanon_rel(p[2 * i]), uncanon_rel(p[2 * i + 1]));
+        p += 2 * nu;
         load(p, u_cm, nu);
         if constexpr (kGiant) {
             restore_giant_blocks(p, blk_top);

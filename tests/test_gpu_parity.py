@@ -270,26 +270,34 @@ def test_many_clients_with_overlapping_removes():
             b.ingest_messages([msgs])
 
 
-def test_collab_window_beyond_16_bit_seqs_is_flagged():
-    """The tables keep sequence numbers relative to minSeq in 16 bits (s_sr): a document
-    whose collab window (currentSeq - minSeq, held open by a client that never advances its refSeq)
-    reaches 65,520 ops stops with MT_CAPACITY, cap_kind 5, in every class — flagged, never wrong
-    (DESIGN §7); a window just below the limit replays bit-exact."""
-    def doc(n_noops):
+def test_collab_window_beyond_16_bit_seqs():
+    """The LDS classes keep the overlay entries' sequence numbers relative to minSeq in 16 bits
+    (DESIGN §2): a document whose collab window (currentSeq - minSeq, held open by a client that never
+    advances its refSeq) reaches 65,520 ops re-runs from scratch in the giant class, whose relative
+    seqs are 32-bit (MergeTree keeps JS numbers, mergeTree.ts:1718-1736: no window limit), and from
+    there in the HBM class when its overlay list outgrows the giant class's LDS.  Windows below and
+    far beyond the 16-bit limit, with concurrent inserts spread through them, replay bit-exact."""
+    def doc(n_noops, every=0):
         msgs = [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "abc"})]
-        msgs += [{"clientId": "B", "sequenceNumber": k, "referenceSequenceNumber": 1, "minimumSequenceNumber": 0,
-                  "type": "noop", "contents": None} for k in range(2, 2 + n_noops)]
+        for k in range(2, 2 + n_noops):
+            if every and k % every == 0:  # C keeps up and inserts; B holds minSeq at 0
+                msgs.append(_msg("C", k, k - 1, {"type": 0, "pos1": 0, "seg": "q" + str(k % 7)}))
+            else:
+                msgs.append({"clientId": "B", "sequenceNumber": k, "referenceSequenceNumber": 1,
+                             "minimumSequenceNumber": 0, "type": "noop", "contents": None})
         msgs.append(_msg("B", 2 + n_noops, 1, {"type": 0, "pos1": 1, "seg": "X"}))
         msgs.append(_msg("A", 3 + n_noops, 1, {"type": 1, "pos1": 0, "pos2": 2}))
         return msgs
-    docs = [doc(65400), doc(65600)]
+    docs = [doc(65400), doc(65600), doc(65600, every=997), doc(140000, every=131)]
     oracle = oracle_docs_from_messages(docs)
-    assert oracle[1].status == 0
-    with fa.ReplayBatch(2) as b:
+    assert all(o.status == 0 for o in oracle)
+    with fa.ReplayBatch(len(docs)) as b:
         b.ingest_messages(docs)
         b.run()
-        assert_doc_parity(b.doc(0), oracle[0])
-        assert b.doc(1).status == fa.MT_CAPACITY and int(b.counters()["cap_kind"][1]) == 5
+        for d in range(len(docs)):
+            assert_doc_parity(b.doc(d), oracle[d])
+        classes = {li["seg_class"] for li in b.launches()}
+        assert max(classes) >= 2000000, classes  # the wide windows ran in a spill class
 
 
 def test_empty_documents_and_empty_inserts():
