@@ -389,6 +389,10 @@ struct ReplayParams {
     uint32_t *regen;              // regenerated ops (kRegenOpWords layout), per document
     const uint64_t *doc_regen_base;
     int32_t regen_cap;            // words per document
+    // batches whose annotates touch referenceTileLabels / referenceRangeLabels: per output record,
+    // the prop set a marker's leaf block last rebuilt its tile / range maps from (blockUpdate,
+    // mergeTree.ts:2748-2767; annotates do not run it, so those maps go stale), else null
+    uint32_t *lab_out;            // [n_docs * out_cap]
 };
 constexpr uint32_t kIdUnlinked = 0xFFFFFFFFu;
 constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // RELPOS key the host cannot resolve safely

@@ -305,6 +305,10 @@ struct Engine {
     const mt_prop *props_in;
     const ValueTables *vt;  // value flags / classes / exceptions (scalar loads where used)
     int lane;
+    // label tracking (ReplayParams.lab_out): a Marker's cold.w (its text capacity otherwise, unused
+    // by markers) holds the prop set its leaf block's last blockUpdate read the tile / range labels
+    // from; lab_refresh runs where the reference runs blockUpdate on a leaf block
+    bool lab;
     LWord<int32_t> cap_kind;
 #ifdef MT_PROF
     uint64_t pf[kProfSlots];
@@ -734,6 +738,17 @@ struct Engine {
         wsync();
     }
 
+    // blockUpdate of leaf block blk (mergeTree.ts:2748-2767): its markers' tile / range maps read the
+    // current labels (label tracking only)
+    MT_FI void lab_refresh(int32_t blk) {
+        if (!lab) return;
+        const int32_t n = b_count[blk];
+        if (lane < n) {
+            const uint32_t sl = b_child[blk * 8 + lane];
+            if (s_meta[sl] & kFMarker) cold[2 * sl].w = cold[2 * sl].x;
+        }
+        wsync();
+    }
     // a new segment's two cold records {props, no overlap, text offset, text capacity} and {seq,
     // removedSeq, client ids, no pending groups}: one dword per lane 0-7, a single 32-byte store
     MT_FI void cold_init(uint32_t slot, uint32_t props, uint32_t toff, uint32_t tcap, uint32_t seq, uint32_t rseq,
@@ -1098,13 +1113,14 @@ struct Engine {
         wsync();
         for (int32_t b0 = 0; b0 < slot_top; b0 += kWave) {
             const int32_t slot = b0 + lane;
-            uint32_t old = 0, ovl = 0;
+            uint32_t old = 0, ovl = 0, lw = 0;
             if (slot < slot_top) {
                 const uint32_t m = s_meta[slot];
                 if (m & kFLinked) {
                     const uint4 cr = cold[2 * slot];
                     if (m & kFHasProps) old = cr.x;
                     if (cr.y & kOvlList) ovl = cr.y & ~kOvlList;
+                    if (lab && (m & kFMarker)) lw = cr.w;  // the labels snapshot's prop set
                 }
             }
             uint64_t msk = ballot(old != 0u);
@@ -1123,6 +1139,15 @@ struct Engine {
                 const uint32_t nid = pool_forward(rdl(ovl, f), nb, top);
                 if (status) return;
                 if (lane == 0) cold[2 * (uint32_t)(b0 + f)].y = nid | kOvlList;
+                wsync();
+            }
+            msk = ballot(lw != 0u);
+            while (msk) {
+                const int f = first_lane(msk);
+                msk &= msk - 1;
+                const uint32_t nid = pool_forward(rdl(lw, f), nb, top);  // (already moved: forwarded)
+                if (status) return;
+                if (lane == 0) cold[2 * (uint32_t)(b0 + f)].w = nid;
                 wsync();
             }
         }
@@ -1245,8 +1270,12 @@ struct Engine {
         wsync();
         if (n + 1 >= kMaxNodes) {
             int32_t nb = split_leaf(blk);
+            lab_refresh(blk);  // MergeTree.split updates both halves
+            lab_refresh(nb);
             if (k >= kMaxNodes / 2) return nb;
+            return blk;
         }
+        lab_refresh(blk);  // insertingWalk's blockUpdateLength of the leaf block
         return blk;
     }
 
@@ -1569,6 +1598,7 @@ struct Engine {
                     wsync();
                     if (bit_free_after(head, slot, head, head)) pend_set_mask(slot, pend_mask(slot) & ~(1u << b));
                     add_to_lru(rfl((int32_t)s_blk[slot]), slot, op.seq);
+                    lab_refresh(rfl((int32_t)s_blk[slot]));  // blockUpdatePathLengths(segment.parent)
                     if (status) return;
                 }
             }
@@ -2347,6 +2377,8 @@ struct Engine {
         if (status) return;
         const int32_t cc = regroup(parent, pn, hold, nk, 1, 0);
         if (status) return;
+        if (lab)  // every packed block: nodeUpdateLengthNewStructure (mergeTree.ts:1404)
+            for (int32_t q = 0; q < cc; q++) lab_refresh(rfl((int32_t)b_child[parent * 8 + q]));
         if (cc < kMaxNodes / 2 && parent != root) pack_interior(parent);
     }
 
@@ -2380,6 +2412,7 @@ struct Engine {
                 splits++;
                 wsync();
                 if (nk < kMaxNodes / 2 && blk != root) pack_leaf(blk);
+                else lab_refresh(blk);  // blockUpdatePathLengths(block)
                 if (status) return;
             }
         }
@@ -2455,7 +2488,7 @@ struct Engine {
             if (rseq != kNoneSeq) meta |= kFRemoved;
             s_len[slot] = (Len)len;
             const USr sr = us_make(local ? kRUnassigned : rel(op.seq), rseq == kNoneSeq ? kRNone : rel(rseq));
-            cold_init(slot, props, op.payload, marker ? 0u : len, (uint32_t)op.seq, (uint32_t)rseq, (c & kMetaCli) | (rcli << 16));
+            cold_init(slot, props, op.payload, marker ? props : len, (uint32_t)op.seq, (uint32_t)rseq, (c & kMetaCli) | (rcli << 16));
             s_meta[slot] = (Meta)meta;
             wsync();
             // (a settled loaded segment too, while it moves through block splits: it joins the
@@ -2515,7 +2548,7 @@ struct Engine {
         if (props) meta |= kFHasProps;
         if (rseq != kNoneSeq) meta |= kFRemoved;
         s_len[slot] = (Len)len;
-        cold_init(slot, props, op.payload, marker ? 0u : len, (uint32_t)op.seq, (uint32_t)rseq,
+        cold_init(slot, props, op.payload, marker ? props : len, (uint32_t)op.seq, (uint32_t)rseq,
                   (op.client & kMetaCli) | (rcli << 16));
         s_meta[slot] = (Meta)meta;
         wsync();
@@ -2769,6 +2802,7 @@ struct Engine {
             const bool hit = lane < n && lane < kMaxNodes && vlen > 0u && excl < end && incl > start;
             uint64_t hb = ballot(hit);
             const uint32_t bend = n > 0 ? rdl(incl, n - 1) : base;
+            if (is_remove && hb) lab_refresh(blk);  // nodeMap's post action: afterMarkRemoved (mergeTree.ts:2660-2667)
             if (is_remove) {
                 uint32_t meta = 0, ui = kUNone, cm = 0;
                 USr sr = 0;
@@ -3436,7 +3470,8 @@ struct Engine {
 
     // ------------------------------------------------------------------ output
     // the leaves in document order, each leaf block closed by an end-marker record
-    MT_FI void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op) {
+    MT_FI void write_out(OutRec *out, int32_t out_cap, DocOut *dout, int32_t ops_done, int32_t fail_op,
+                         uint32_t *lab_out = nullptr) {
         resolve_splits();
         wsync();
         int32_t w = 0;
@@ -3466,6 +3501,7 @@ struct Engine {
                     r.props = cr.x;
                     r.toff = cr.z;
                     r.blk = (uint32_t)blk;
+                    if (lab_out) lab_out[j] = (s_meta[slot] & kFMarker) ? cr.w : 0u;
                 } else {
                     r.len = 0;
                     r.seq = 0;
@@ -3556,6 +3592,7 @@ MT_FI void engine_setup(Engine<SEG, kW> &E, const ReplayParams &P, int64_t w, in
     E.props_in = (const mt_prop *)P.props_in;
     E.vt = P.vt;
     E.idmap = P.idmap ? P.idmap + P.doc_idmap_base[d] : nullptr;
+    E.lab = P.lab_out != nullptr;
     if constexpr (kW) {
         E.pend = P.pend + P.doc_pend_base[d];
         E.pend_cap_e = P.pend_cap;
@@ -3677,7 +3714,8 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
         }
         cur = nxt;
     }
-    E.write_out(P.out + w * (int64_t)P.out_cap, P.out_cap, P.doc_out + w, done, fail_op);
+    E.write_out(P.out + w * (int64_t)P.out_cap, P.out_cap, P.doc_out + w, done, fail_op,
+                P.lab_out ? P.lab_out + w * (int64_t)P.out_cap : nullptr);
 #ifdef MT_PROF
     E.pf[0] = clock64() - t_kernel;
     if (P.prof && E.lane < kProfSlots) {

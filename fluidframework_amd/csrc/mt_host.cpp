@@ -86,6 +86,7 @@ struct Launch {
     Caps caps;
     int32_t out_cap = 0;
     OutRec *d_out = nullptr;
+    uint32_t *d_lab = nullptr;   // label tracking: per record, a marker's labels snapshot (ReplayParams.lab_out)
     DocOut *d_docout = nullptr;
     int32_t *d_list = nullptr;
     uint64_t *d_prof = nullptr;  // MT_PROF builds
@@ -313,7 +314,8 @@ struct mt_batch {
     int32_t max_ops_per_doc = 0;
     std::vector<int64_t> h_off;
     std::vector<int32_t> h_nload, h_nload_segs;  // leading SnapshotLoader records / segments per doc
-    std::vector<uint8_t> h_tile_annot;  // per doc: an annotate touches referenceTileLabels (findTile)
+    std::vector<uint8_t> h_tile_annot;  // per doc: an annotate touches referenceTileLabels (1) / referenceRangeLabels (2)
+    bool lab_track = false;             // some document's annotates touch them: the replay tracks labels snapshots
     std::vector<uint64_t> h_text_base, h_pool_base;
     std::vector<uint32_t> h_text_len, h_text_cap, h_pool_cap;
     // MT_OP_RELPOS records hold marker-id keys on the device (resolve_marker_ids); key_value[k] is a
@@ -353,6 +355,7 @@ struct mt_batch {
     // single-document result cache
     int64_t cached_doc = -1;
     std::vector<OutRec> c_recs;
+    std::vector<uint32_t> c_lab;  // label tracking: per record, the prop set of the labels snapshot
     std::vector<uint16_t> c_text;
     std::vector<uint32_t> c_pool;
     DocOut c_out{};
@@ -382,6 +385,7 @@ static void free_snap(mt_batch *b) {
 static void free_launches(mt_batch *b) {
     for (auto &L : b->launches) {
         (void)hipFree(L.d_out);
+        (void)hipFree(L.d_lab);
         (void)hipFree(L.d_docout);
         (void)hipFree(L.d_list);
         (void)hipFree(L.d_prof);
@@ -948,6 +952,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     b->h_nload = std::move(nload);
     b->h_nload_segs = std::move(nload_segs);
     b->h_tile_annot = std::move(tile_annot);
+    b->lab_track = std::any_of(b->h_tile_annot.begin(), b->h_tile_annot.end(), [](uint8_t t) { return t != 0; });
     b->payload_units = payload_units;
     b->prop_records = prop_records;
     b->text_words = tbase;
@@ -1248,6 +1253,7 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     b->h_nload_segs.assign((size_t)D, 0);
     b->h_tile_annot.assign((size_t)D, 0);
     for (int64_t d = 0; d < D; d++) b->h_tile_annot[(size_t)d] = (uint8_t)(tile[(size_t)d] & 3u);
+    b->lab_track = std::any_of(b->h_tile_annot.begin(), b->h_tile_annot.end(), [](uint8_t t) { return t != 0; });
     b->payload_units = (double)r.n_text;
     b->prop_records = (double)r.n_props;
     b->text_words = tb;
@@ -1383,6 +1389,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     L.out_cap = L.caps.oe;
     L.lds = class_lds(L.cls);
     HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
+    if (b->lab_track) HIPCHK(dalloc(&L.d_lab, (size_t)n * (size_t)L.out_cap));
     HIPCHK(dalloc(&L.d_docout, (size_t)n));
     HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg * mt::kColdPerSlot));
     if (class_state_bytes(L.cls)) HIPCHK(dalloc(&L.d_state, (size_t)n * class_state_bytes(L.cls)));
@@ -1400,6 +1407,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     }
     mt::ReplayParams P = base_params(b);
     P.out = L.d_out;
+    P.lab_out = L.d_lab;
     P.doc_out = L.d_docout;
     P.n_docs = n;
     P.doc_list = L.d_list;
@@ -1873,6 +1881,9 @@ static int load_doc(mt_batch *b, int64_t d) {
     if (b->c_out.n_out)
         HIPCHK(hipMemcpy(b->c_recs.data(), L.d_out + (size_t)w.idx * L.out_cap, sizeof(OutRec) * b->c_recs.size(),
                          hipMemcpyDeviceToHost));
+    b->c_lab.assign(L.d_lab ? b->c_recs.size() : 0, 0u);
+    if (L.d_lab && b->c_out.n_out)
+        HIPCHK(hipMemcpy(b->c_lab.data(), L.d_lab + (size_t)w.idx * L.out_cap, 4 * b->c_lab.size(), hipMemcpyDeviceToHost));
     uint32_t tt = std::min<uint32_t>(b->c_out.text_top, b->h_text_cap[d]);
     b->c_text.resize(tt);
     if (tt) HIPCHK(hipMemcpy(b->c_text.data(), b->d_text + b->h_text_base[d], 2ull * tt, hipMemcpyDeviceToHost));
@@ -2020,10 +2031,14 @@ MT_API int mt_doc_props_runs(mt_batch *b, int64_t doc, char *buf, int64_t cap, i
 // while the leaf test compares with ===).
 // (ref_labels_of: the same for the key `tk` of the ref types `type_mask` — Tile: referenceTileLabels;
 // NestBegin | NestEnd: referenceRangeLabels, refHasRangeLabels mergeTree.ts:584-586)
-static int ref_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, uint32_t type_mask, std::vector<std::u16string> &out) {
+// (props: the prop set to read, by default the record's current one)
+static int ref_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, uint32_t type_mask, std::vector<std::u16string> &out,
+                         uint32_t props = 0xFFFFFFFFu) {
     out.clear();
-    if (!(r.meta & mt::kMetaMarker) || !(r.toff & type_mask) || !r.props || tk == 0xFFFFFFFFu) return 0;
-    const uint32_t *p = b->c_pool.data() + r.props;
+    if (props == 0xFFFFFFFFu) props = r.props;
+    if (!(r.meta & mt::kMetaMarker) || !(r.toff & type_mask) || !props || tk == 0xFFFFFFFFu) return 0;
+    if ((size_t)props + 2 > b->c_pool.size()) return -1;
+    const uint32_t *p = b->c_pool.data() + props;
     uint32_t v = 0xFFFFFFFFu;
     for (uint32_t i = 0; i < p[0]; i++)
         if (p[2 + 2 * i] == tk) v = p[3 + 2 * i];
@@ -2058,14 +2073,81 @@ static int tile_labels_of(mt_batch *b, const OutRec &r, uint32_t tk, std::vector
     return ref_labels_of(b, r, tk, 1u, out);
 }
 
+// The document's block tree, rebuilt from its final table: the leaves in document order, each leaf
+// block closed by an end record naming the interior blocks that end with it (mt_engine.hip
+// write_out).  Level-0 nodes list leaves (indices into `leaves`), level l > 0 nodes list nodes.
+namespace {
+struct TNode {
+    int level;
+    std::vector<int64_t> kids;
+    int64_t len = 0;  // the local view's length (cachedLength)
+};
+}  // namespace
+static int64_t rebuild_tree(mt_batch *b, std::vector<TNode> &nodes, std::vector<const OutRec *> &leaves,
+                            std::vector<int64_t> &leaf_rec) {
+    const int D = std::max(1, b->c_out.depth);
+    std::vector<int64_t> open((size_t)D + 1, -1);
+    int64_t root = -1;
+    std::function<int64_t(int)> get_open = [&](int l) -> int64_t {
+        if (open[(size_t)l] >= 0) return open[(size_t)l];
+        nodes.push_back(TNode{l, {}, 0});
+        const int64_t n = (int64_t)nodes.size() - 1;
+        open[(size_t)l] = n;
+        if (l + 1 <= D - 1) {
+            const int64_t p = get_open(l + 1);
+            nodes[(size_t)p].kids.push_back(n);
+        } else {
+            root = n;
+        }
+        return n;
+    };
+    TNode cur{0, {}, 0};
+    for (size_t j = 0; j < b->c_recs.size(); j++) {
+        const OutRec &r = b->c_recs[j];
+        if (!rec_is_marker(r)) {
+            cur.kids.push_back((int64_t)leaves.size());
+            leaves.push_back(&r);
+            leaf_rec.push_back((int64_t)j);
+            continue;
+        }
+        nodes.push_back(std::move(cur));
+        cur = TNode{0, {}, 0};
+        const int64_t n = (int64_t)nodes.size() - 1;
+        if (D == 1) root = n;
+        else nodes[(size_t)get_open(1)].kids.push_back(n);
+        for (uint32_t l = 1; l <= r.toff && l < (uint32_t)D; l++) open[l] = -1;
+    }
+    // lengths, children before parents
+    std::function<void(int64_t)> sum = [&](int64_t n) {
+        TNode &t = nodes[(size_t)n];
+        t.len = 0;
+        for (int64_t k : t.kids) {
+            if (t.level == 0) {
+                t.len += rec_removed(*leaves[(size_t)k]) ? 0 : (int64_t)leaves[(size_t)k]->len;
+            } else {
+                sum(k);
+                t.len += nodes[(size_t)k].len;
+            }
+        }
+    };
+    if (root >= 0) sum(root);
+    return root;
+}
+// the prop set a leaf block's last blockUpdate read a marker's labels from: the device's labels
+// snapshot when the batch tracks them (annotates of referenceTileLabels / referenceRangeLabels leave
+// the block maps stale until the next blockUpdate), else the current one
+static uint32_t snap_props(mt_batch *b, const OutRec &r, int64_t rec) {
+    return b->c_lab.empty() ? r.props : b->c_lab[(size_t)rec];
+}
+
 // Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076 -> MergeTree.findTile,
 // mergeTree.ts:1763-1789) on the document's final table, in the replica's local view
-// (refSeq UniversalSequenceNumber).  With the block tile maps current (every path that changes a
-// marker's presence runs blockUpdate on its ancestors), search / backwardSearch reduce to:
-//   preceding:  the labelled tile marker containing startPos, else the last one (not removed)
-//               before it; past the end, the last one of the document;
-//   following:  startPos > length: none; the labelled tile containing startPos, else the first one
-//               (not removed) after it; startPos == length: the document's last leaf, if it is one.
+// (refSeq UniversalSequenceNumber): search (preceding, posPrecedesTile) or backwardSearch
+// (mergeTree.ts:1797-1870) with recordTileStart / tileShift (1000-1040) over the rebuilt tree, whose
+// blocks carry rightmostTiles / leftmostTiles as their last blockUpdate built them (2748-2767 ->
+// addNodeReferences 263-317: a leaf block reads its markers' labels at that time — an annotate of
+// referenceTileLabels does not run blockUpdate, so the maps keep the labels of the last one — and an
+// interior block extends its children's maps).  Leaves compare their current labels.
 MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const char *label_utf8, int32_t preceding,
                             int64_t *tile_pos, char *props_buf, int64_t props_cap, int64_t *props_len) {
     if (!b || !label_utf8 || !tile_pos) return MT_ERR_ARG;
@@ -2074,68 +2156,133 @@ MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const c
     *tile_pos = -1;
     if (props_len) *props_len = 0;
     if (b->c_out.status != MT_OK) return b->c_out.status;
-    if (b->h_tile_annot[(size_t)doc] & 1u) return MT_UNSUPPORTED;
     const std::vector<uint16_t> lu = utf8_to_utf16(std::string(label_utf8));
     const std::u16string label(lu.begin(), lu.end());
     uint32_t tk = 0xFFFFFFFFu;
     for (size_t k = 0; k < b->keys.size(); k++)
         if (b->keys[k] == "referenceTileLabels") tk = (uint32_t)k;
+    std::vector<TNode> nodes;
     std::vector<const OutRec *> leaves;
-    for (const OutRec &r : b->c_recs)
-        if (!rec_is_marker(r)) leaves.push_back(&r);
+    std::vector<int64_t> leaf_rec;
+    const int64_t root = rebuild_tree(b, nodes, leaves, leaf_rec);
+    if (root < 0) return MT_INTERNAL;
+    auto local_len = [](const OutRec &r) -> int64_t { return rec_removed(r) ? 0 : (int64_t)r.len; };
     std::vector<std::u16string> labels;
     bool bad = false;
-    auto labelled = [&](const OutRec &r) {
-        const int t = tile_labels_of(b, r, tk, labels);
+    // refHasTileLabel on the current labels (the leaf tests of recordTileStart / tileShift)
+    auto labelled = [&](int64_t k) {
+        const int t = tile_labels_of(b, *leaves[(size_t)k], tk, labels);
         if (t < 0) bad = true;
         if (t <= 0) return false;
         for (const auto &l : labels)
             if (l == label) return true;
         return false;
     };
-    auto local_len = [](const OutRec &r) -> int64_t { return rec_removed(r) ? 0 : (int64_t)r.len; };
-    int64_t total = 0;
-    for (const OutRec *r : leaves) total += local_len(*r);
+    // every block's maps for `label` (only that key is ever read): rightmost / leftmost leaf, -1 none
+    std::vector<int64_t> right(nodes.size(), -1), left(nodes.size(), -1);
+    std::function<void(int64_t)> update = [&](int64_t n) {
+        const TNode &t = nodes[(size_t)n];
+        for (int64_t k : t.kids) {
+            if (t.level == 0) {
+                const OutRec &r = *leaves[(size_t)k];
+                if (local_len(r) <= 0 || !(r.meta & mt::kMetaMarker) || !(r.toff & 1u)) continue;
+                const int tl = ref_labels_of(b, r, tk, 1u, labels, snap_props(b, r, leaf_rec[(size_t)k]));
+                if (tl < 0) bad = true;
+                if (tl <= 0) continue;
+                for (const auto &l : labels)
+                    if (l == label) {
+                        right[(size_t)n] = k;  // addTile
+                        if (left[(size_t)n] < 0) left[(size_t)n] = k;  // addTileIfNotPresent
+                    }
+            } else {
+                update(k);
+                if (right[(size_t)k] >= 0) right[(size_t)n] = right[(size_t)k];  // Properties.extend
+                if (left[(size_t)n] < 0) left[(size_t)n] = left[(size_t)k];     // extendIfUndefined
+            }
+        }
+    };
+    update(root);
     // every tile marker's labels are checked, so an unmodelled value anywhere is reported
-    for (const OutRec *r : leaves) (void)labelled(*r);
+    for (int64_t k = 0; k < (int64_t)leaves.size(); k++) (void)labelled(k);
     if (bad) return MT_UNSUPPORTED;
-    int64_t found = -1;  // leaf index
-    int64_t pos = 0, k = 0;
-    const int64_t n = (int64_t)leaves.size();
-    while (k < n && !(start_pos < pos + local_len(*leaves[(size_t)k]))) pos += local_len(*leaves[(size_t)k++]);
-    // k: the containing leaf (n: none)
-    if (preceding) {
-        if (k < n && labelled(*leaves[(size_t)k])) found = k;
-        else
-            for (int64_t i = (k < n ? k : n) - 1; i >= 0 && found < 0; i--)
-                if (local_len(*leaves[(size_t)i]) > 0 && labelled(*leaves[(size_t)i])) found = i;
-    } else if (start_pos < total) {
-        if (labelled(*leaves[(size_t)k])) found = k;
-        else
-            for (int64_t i = k + 1; i < n && found < 0; i++)
-                if (local_len(*leaves[(size_t)i]) > 0 && labelled(*leaves[(size_t)i])) found = i;
-    } else if (start_pos == total && n > 0) {
-        if (labelled(*leaves[(size_t)(n - 1)])) found = n - 1;
+    int64_t tile = -1;
+    if (preceding) {  // search -> searchBlock (1797-1829)
+        int64_t pos = start_pos;
+        for (int64_t n = root; n >= 0;) {
+            const TNode &t = nodes[(size_t)n];
+            int64_t next = -1;
+            bool hit = false;
+            for (int64_t k : t.kids) {
+                const int64_t len = t.level == 0 ? local_len(*leaves[(size_t)k]) : nodes[(size_t)k].len;
+                if (pos < len) {
+                    hit = true;
+                    if (t.level == 0) {
+                        if (labelled(k)) tile = k;  // recordTileStart
+                    } else {
+                        next = k;
+                    }
+                    break;
+                }
+                if (t.level == 0) {  // tileShift of a leaf
+                    if (len > 0 && labelled(k)) tile = k;
+                } else if (right[(size_t)k] >= 0) {  // tileShift of a block
+                    tile = right[(size_t)k];
+                }
+                pos -= len;
+            }
+            n = hit ? next : -1;
+        }
+    } else if (start_pos <= nodes[(size_t)root].len) {  // backwardSearch (1831-1870)
+        int64_t pos = start_pos, seg_end = nodes[(size_t)root].len;
+        for (int64_t n = root; n >= 0;) {
+            const TNode &t = nodes[(size_t)n];
+            int64_t next = -1;
+            bool hit = false;
+            for (size_t i = t.kids.size(); i-- > 0;) {
+                const int64_t k = t.kids[i];
+                const int64_t len = t.level == 0 ? local_len(*leaves[(size_t)k]) : nodes[(size_t)k].len;
+                const int64_t segpos = seg_end - len;
+                if (pos >= segpos) {
+                    hit = true;
+                    if (t.level == 0) {
+                        if (labelled(k)) tile = k;
+                    } else {
+                        next = k;
+                    }
+                    break;
+                }
+                if (t.level == 0) {
+                    if (len > 0 && labelled(k)) tile = k;
+                } else if (left[(size_t)k] >= 0) {
+                    tile = left[(size_t)k];
+                }
+                seg_end = segpos;
+            }
+            n = hit ? next : -1;
+        }
     }
-    if (found < 0) return MT_OK;
+    if (bad) return MT_UNSUPPORTED;
+    if (tile < 0) return MT_OK;
     int64_t tp = 0;
-    for (int64_t i = 0; i < found; i++) tp += local_len(*leaves[(size_t)i]);
+    for (int64_t i = 0; i < tile; i++) tp += local_len(*leaves[(size_t)i]);
     *tile_pos = tp;
     std::string pj;
-    if (leaves[(size_t)found]->props) props_json(b, leaves[(size_t)found]->props, pj);
+    if (leaves[(size_t)tile]->props) props_json(b, leaves[(size_t)tile]->props, pj);
     return out_str(pj, props_buf, props_cap, props_len);
 }
 
 // Client.getStackContext(startPos, rangeLabels) (client.ts:946-948 -> MergeTree.getStackContext,
 // mergeTree.ts:1750-1760; SharedSegmentSequence.getStackContext, sequence/src/sequence.ts:377) on the
-// document's final state in the replica's local view.  The final table lists the leaves in
-// document order and, per leaf block, the interior blocks that end with it, so the whole tree is
-// rebuilt here; every block's rangeStacks is the current one (blockUpdate runs on every path that
-// changes a marker's presence; a document annotating referenceRangeLabels is MT_UNSUPPORTED, its
-// maps would be stale).  The search is searchBlock with rangeShift / recordRangeLeaf
+// document's final state in the replica's local view, over the rebuilt tree.  Every block's
+// rangeStacks is the one its last blockUpdate built (addNodeReferences / applyStackDelta,
+// mergeTree.ts:229-317): a leaf block from its markers' labels at that time (the labels snapshot when
+// an annotate changed them since: stale maps, as in the reference), an interior block from its
+// children's deltas.  The search is searchBlock with rangeShift / recordRangeLeaf
 // (mergeTree.ts:953-994, 1797-1829): a preceding block applies its whole delta (every label),
-// preceding leaves of the containing leaf block and the containing leaf only the asked-for labels.
-// Output: {label: [{"pos":P,"refType":T[,"props":{..}]}, ..]} in JS key order, stacks bottom to top.
+// preceding leaves of the containing leaf block and the containing leaf only the asked-for labels
+// of their current labels.
+// Output (repo-defined shape): {label: [{"pos":P,"refType":T[,"props":{..}]}, ..]} in JS key order,
+// stacks bottom to top.
 namespace {
 struct RangeStacks {  // label -> stack of leaf indices, in key creation order
     std::vector<std::pair<std::u16string, std::vector<int64_t>>> s;
@@ -2155,7 +2302,6 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
     if (rc) return rc;
     if (len) *len = 0;
     if (b->c_out.status != MT_OK) return b->c_out.status;
-    if (b->h_tile_annot[(size_t)doc] & 2u) return MT_UNSUPPORTED;
     std::vector<std::u16string> want;
     for (int32_t i = 0; i < n_labels; i++) {
         if (!labels_utf8[i]) return MT_ERR_ARG;
@@ -2165,52 +2311,16 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
     uint32_t rk = 0xFFFFFFFFu;
     for (size_t k = 0; k < b->keys.size(); k++)
         if (b->keys[k] == "referenceRangeLabels") rk = (uint32_t)k;
-    // the tree: level-0 nodes list leaves (indices into `leaves`), level l > 0 nodes list nodes
-    struct TNode {
-        int level;
-        std::vector<int64_t> kids;
-        int64_t len = 0;
-        RangeStacks rs;
-    };
     std::vector<TNode> nodes;
     std::vector<const OutRec *> leaves;
-    const int D = std::max(1, b->c_out.depth);
-    std::vector<int64_t> open((size_t)D + 1, -1);
-    int64_t root = -1;
-    std::function<int64_t(int)> get_open = [&](int l) -> int64_t {
-        if (open[(size_t)l] >= 0) return open[(size_t)l];
-        nodes.push_back(TNode{l, {}, 0, {}});
-        const int64_t n = (int64_t)nodes.size() - 1;
-        open[(size_t)l] = n;
-        if (l + 1 <= D - 1) {
-            const int64_t p = get_open(l + 1);
-            nodes[(size_t)p].kids.push_back(n);
-        } else {
-            root = n;
-        }
-        return n;
-    };
-    {
-        TNode cur{0, {}, 0, {}};
-        for (const OutRec &r : b->c_recs) {
-            if (!rec_is_marker(r)) {
-                cur.kids.push_back((int64_t)leaves.size());
-                leaves.push_back(&r);
-                continue;
-            }
-            nodes.push_back(std::move(cur));
-            cur = TNode{0, {}, 0, {}};
-            const int64_t n = (int64_t)nodes.size() - 1;
-            if (D == 1) root = n;
-            else nodes[(size_t)get_open(1)].kids.push_back(n);
-            for (uint32_t l = 1; l <= r.toff && l < (uint32_t)D; l++) open[l] = -1;
-        }
-    }
+    std::vector<int64_t> leaf_rec;
+    const int64_t root = rebuild_tree(b, nodes, leaves, leaf_rec);
     if (root < 0) return MT_INTERNAL;
+    std::vector<RangeStacks> rs(nodes.size());
     auto local_len = [](const OutRec &r) -> int64_t { return rec_removed(r) ? 0 : (int64_t)r.len; };
     std::vector<std::u16string> labels;
     bool bad = false;
-    auto range_labels = [&](const OutRec &r) -> bool {  // refHasRangeLabels + getRangeLabels
+    auto range_labels = [&](const OutRec &r) -> bool {  // refHasRangeLabels + getRangeLabels (current)
         const int t = ref_labels_of(b, r, rk, 6u, labels);
         if (t < 0) bad = true;
         return t > 0;
@@ -2232,20 +2342,21 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
             for (int64_t x : e.second) apply_ref(c, x);
         }
     };
-    // blockUpdate's lengths and rangeStacks, children before parents (nodes were created parents
-    // before their later children, so a post-order walk from the root)
+    // blockUpdate's rangeStacks, children before parents: a leaf block reads its markers' labels as
+    // of its last blockUpdate (the labels snapshot)
     std::function<void(int64_t)> update = [&](int64_t n) {
-        TNode &t = nodes[(size_t)n];
+        const TNode &t = nodes[(size_t)n];
         for (int64_t k : t.kids) {
             if (t.level == 0) {
                 const OutRec &r = *leaves[(size_t)k];
-                t.len += local_len(r);
-                if (local_len(r) > 0 && (r.meta & mt::kMetaMarker) && (r.toff & 6u) && range_labels(r))
-                    for (const auto &l : labels) apply_ref(t.rs.get(l), k);  // updateRangeInfo
+                if (local_len(r) <= 0 || !(r.meta & mt::kMetaMarker) || !(r.toff & 6u)) continue;
+                const int tl = ref_labels_of(b, r, rk, 6u, labels, snap_props(b, r, leaf_rec[(size_t)k]));
+                if (tl < 0) bad = true;
+                if (tl > 0)
+                    for (const auto &l : labels) apply_ref(rs[(size_t)n].get(l), k);  // updateRangeInfo
             } else {
                 update(k);
-                t.len += nodes[(size_t)k].len;
-                apply_delta(t.rs, nodes[(size_t)k].rs);
+                apply_delta(rs[(size_t)n], rs[(size_t)k]);
             }
         }
     };
@@ -2282,7 +2393,7 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
                 const OutRec &r = *leaves[(size_t)k];
                 if (len > 0 && (r.meta & mt::kMetaMarker) && (r.toff & 6u)) leaf_marker(k);
             } else {  // rangeShift of a block
-                apply_delta(out, nodes[(size_t)k].rs);
+                apply_delta(out, rs[(size_t)k]);
             }
             pos -= len;
         }
@@ -3051,6 +3162,7 @@ static int generate_docs(mt_batch *b, const mt_gen_params *p, const std::vector<
     b->h_nload.assign(D, 0);
     b->h_nload_segs.assign(D, 0);
     b->h_tile_annot.assign(D, 0);
+    b->lab_track = false;
     int32_t max_ops = 0;
     for (int64_t d = 0; d < D; d++) {
         if (doc_ops[d] < 1) return MT_ERR_ARG;

@@ -38,10 +38,11 @@ RANGE_LABELS = ("row", "box", "cell")
 
 
 def random_op(rng: random.Random, length: int, n_keys: int = 4, p_annotate: int = 15, p_remove: int = 30,
-              max_insert: int = 6, rewrite: int = 0, markers: int = 0, ranges: int = 0) -> dict:
+              max_insert: int = 6, rewrite: int = 0, markers: int = 0, ranges: int = 0, label_annot: int = 0) -> dict:
     """An op drawn from a replica's local view (length = its getLength()).  markers: percentage of
     inserts that are Tile / plain markers carrying referenceTileLabels; ranges: percentage that are
-    NestBegin / NestEnd markers carrying referenceRangeLabels."""
+    NestBegin / NestEnd markers carrying referenceRangeLabels; label_annot: percentage of annotates
+    that set (or delete) referenceTileLabels / referenceRangeLabels (the block maps go stale)."""
     u = rng.randrange(100)
     if ranges and (length == 0 or u >= p_annotate + p_remove) and rng.randrange(100) < ranges:
         labels = rng.sample(RANGE_LABELS, 1 + rng.randrange(2))
@@ -62,8 +63,12 @@ def random_op(rng: random.Random, length: int, n_keys: int = 4, p_annotate: int 
     if u < p_remove:
         return {"type": 1, "pos1": start, "pos2": end}
     props = {}
-    for _ in range(1 + rng.randrange(2)):
-        props[f"k{rng.randrange(n_keys)}"] = None if rng.randrange(8) == 0 else rng.randrange(4)
+    if label_annot and rng.randrange(100) < label_annot:
+        key, pool = (("referenceTileLabels", TILE_LABELS) if rng.randrange(2) else ("referenceRangeLabels", RANGE_LABELS))
+        props[key] = None if rng.randrange(6) == 0 else rng.sample(pool, 1 + rng.randrange(2))
+    else:
+        for _ in range(1 + rng.randrange(2)):
+            props[f"k{rng.randrange(n_keys)}"] = None if rng.randrange(8) == 0 else rng.randrange(4)
     op = {"type": 2, "pos1": start, "pos2": end, "props": props}
     if rewrite and rng.randrange(100) < rewrite:
         op["combiningOp"] = {"name": "rewrite"}
