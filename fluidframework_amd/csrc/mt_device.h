@@ -6,6 +6,8 @@
 
 #include <stdint.h>
 
+#include "../../include/mt_oplog.h"
+
 namespace mt {
 
 // status codes (include/mtreplay.h MT_STATUS_*; the first six match the oracle's)
@@ -14,7 +16,7 @@ enum : int32_t {
     ST_INVALID_POS = 1,  // "MergeTree insert failed" (merge-tree/src/mergeTree.ts:2210-2216)
     ST_SEQ_ORDER = 2,    // client.ts:461-462, 824
     ST_MSN_ORDER = 3,    // client.ts:463-464, mergeTree.ts:1719-1722
-    ST_UNSUPPORTED = 4,  // outside the observer path / device limits (e.g. > 4093 clients)
+    ST_UNSUPPORTED = 4,  // outside the observer path / device limits (e.g. > 32765 clients)
     ST_BAD_INPUT = 5,
     ST_CAPACITY = 6,     // per-document LDS/HBM capacity exceeded: re-run with larger caps
     ST_INTERNAL = 7
@@ -24,11 +26,11 @@ constexpr int kWave = 64;
 constexpr int kMaxNodes = 8;            // MaxNodesInBlock, mergeTree.ts:334
 constexpr uint32_t kGranularity = 256;  // TextSegmentGranularity, mergeTree.ts:1059
 constexpr int kZamboniMax = 2;          // zamboniSegmentsMaxCount, mergeTree.ts:1061
-constexpr int kMaxClients = 4094;       // short client ids 0..4093 (4094 = NonCollabClient, 4095 = none)
+constexpr int kMaxClients = MT_MAX_CLIENTS;  // short client ids 0..32765 (0x7FFE NonCollabClient, 0x7FFF none)
 constexpr int32_t kNoneSeq = 0x7FFFFFFF;  // removedSeq === undefined
 constexpr uint32_t kOutBlockEnd = 0x80000000u;  // OutRec.blk of the entry that ends a leaf block
 __host__ __device__ constexpr bool out_is_end(uint32_t blk) { return (blk & kOutBlockEnd) != 0; }
-constexpr uint32_t kNoClient = 4095u;
+constexpr uint32_t kNoClient = MT_CLIENT_NONE;
 constexpr uint32_t kOvlMaskClients = 31u; // overlap sets of clients < 31 are a bit mask (see kOvlList)
 constexpr uint32_t kOvlList = 0x80000000u;  // cold.y with this bit: pool offset of an overlap-client list
 constexpr uint32_t kPoolOvlTag = 0x40000000u;  // header word of an overlap-list pool record: n | tag
@@ -63,23 +65,15 @@ __device__ __forceinline__ int value_rel(uint32_t va, uint32_t vb, const uint32_
 // needsScour tri-state (mergeTree.ts:63, 1279, 1438)
 constexpr int8_t kScourUndef = -1, kScourFalse = 0, kScourTrue = 1;
 
-// OutRec meta word (the device's final table, mt_host.cpp, mt_snapshot.hip, mt_digest.hip) and the
-// canonical meta word of checkpoint images:
-//   [0,12)  clientId (short id)        [12,24) removedClientId (4095 = none)
-//   [24]    Marker                      [25]    text ends with '\n'
-//   [26]    linked (in the tree)        [27]    (OutRec: 0)
-//   [28]    has a prop set              [29]    text contains a '\n' somewhere
-//   [30]    removedClientOverlap is non-empty (mask or list via the cold record)
+// OutRec meta word (the device's final table, mt_host.cpp, mt_snapshot.hip, mt_digest.hip):
+//   [0,15)  clientId (short id)        [15,30) removedClientId (kNoClient = none)
+//   [30]    Marker                      [31]    removedClientOverlap is non-empty
 // The engine's per-slot LDS meta is narrower (mt_engine.hip SlotMeta): flags plus the index of the
 // slot's unsettled-overlay entry; client ids live in the cold record and in the overlay entry.
-constexpr uint32_t kMetaCli = 0xFFFu;
-constexpr uint32_t kMetaRcliShift = 12;
-constexpr uint32_t kMetaMarker = 1u << 24;
-constexpr uint32_t kMetaEndsNL = 1u << 25;
-constexpr uint32_t kMetaLinked = 1u << 26;
-constexpr uint32_t kMetaHasProps = 1u << 28;
-constexpr uint32_t kMetaHasNL = 1u << 29;
-constexpr uint32_t kMetaHasOvl = 1u << 30;
+constexpr uint32_t kMetaCli = 0x7FFFu;
+constexpr uint32_t kMetaRcliShift = 15;
+constexpr uint32_t kMetaMarker = 1u << 30;
+constexpr uint32_t kMetaHasOvl = 1u << 31;
 __host__ __device__ constexpr uint32_t meta_cli(uint32_t m) { return m & kMetaCli; }
 __host__ __device__ constexpr uint32_t meta_rcli(uint32_t m) { return (m >> kMetaRcliShift) & kMetaCli; }
 // canonical slot meta of a checkpoint image: 7 flag bits at [24, 31), the overlay-entry index below
@@ -99,7 +93,7 @@ struct OutRec {
     uint32_t len;    // cachedLength (0 for a block marker)
     int32_t seq;
     int32_t rseq;    // kNoneSeq when not removed
-    uint32_t meta;   // segment meta word bits [0,31): client ids and flags (no kMetaPending)
+    uint32_t meta;   // client ids, Marker, has-overlap (kMetaCli, kMetaRcliShift, kMetaMarker, kMetaHasOvl)
     uint32_t ovl;    // removedClientOverlap: bit mask of clients < 31, or kOvlList | pool offset of
                      // a [n | kPoolOvlTag, 0, client x n] list
     uint32_t props;  // prop-set id in the doc's pool (0 = undefined)

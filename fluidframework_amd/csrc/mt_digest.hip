@@ -29,7 +29,7 @@ __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t w) {
 
 // the client ids and the Marker bit as one word: clientId | removedClientId << 8 | Marker << 16 in
 // the 8-bit encoding of the first engines (254 NonCollabClient, 255 none) for ids below 254, so the
-// digests of such documents are unchanged; the ids from 254 on add their high bits above bit 16
+// digests of such documents are unchanged; the ids from 254 to 4095 add their high bits above bit 16
 __device__ __forceinline__ uint32_t id_enc(uint32_t id) {
     if (id == MT_CLIENT_NONCOLLAB) return 254u;
     if (id == kNoClient) return 255u;
@@ -62,7 +62,13 @@ extern "C" __global__ __launch_bounds__(64) void mt_digest_kernel(DigestParams P
             h = fnv(h, r.len);
             h = fnv(h, (uint32_t)r.seq);
             h = fnv(h, (uint32_t)r.rseq);
-            h = fnv(h, id_word(meta_cli(r.meta), meta_rcli(r.meta), (r.meta & kMetaMarker) != 0u));  // client ids, Marker
+            const uint32_t ci = meta_cli(r.meta), ri = meta_rcli(r.meta);
+            h = fnv(h, id_word(ci, ri, (r.meta & kMetaMarker) != 0u));  // client ids, Marker
+            // 15-bit ids beyond the first engines' 12-bit range add a word (digests of documents with
+            // fewer clients are unchanged)
+            if ((ci >= 4096u && ci != MT_CLIENT_NONCOLLAB && ci != kNoClient) ||
+                (ri >= 4096u && ri != MT_CLIENT_NONCOLLAB && ri != kNoClient))
+                h = fnv(h, ci | ri << 16);
             // removedClientOverlap as a set (mask of clients < 31, or a pool list)
             uint64_t ov = 0;
             if (r.ovl & kOvlList) {

@@ -231,8 +231,9 @@ struct Engine {
                               kFHasProps = 8u << kUB, kFHasNL = 16u << kUB, kFRemoved = 32u << kUB,
                               kFPending = 64u << kUB;
     static_assert(cap.ulist < (int32_t)kUNone, "overlay-entry index");
-    // u_cm: clientId | removedClientId << 12 | has-overlap
-    static constexpr uint32_t kCmOvl = 1u << 24;
+    // u_cm: clientId | removedClientId << kCmR | has-overlap (15-bit short ids)
+    static constexpr int kCmR = 15;
+    static constexpr uint32_t kCmOvl = 1u << 30;
     // an overlay entry's sequence numbers relative to sbase: seq | removedSeq << kRB, 16-bit each in
     // the LDS classes (a collab window of kSeq16Span ops or more moves the document to a spill
     // class), 32-bit in the giant and HBM classes (no window limit)
@@ -250,7 +251,7 @@ struct Engine {
     Idx *s_blk;    // leaf block; of a free slot: the next free slot (kNoBlk ends the list)
     Idx *u_list;   // overlay entries: exactly the unsettled slots, unordered
     USr *u_sr;       // seq | rseq << kRB, relative to sbase (kRNone: not removed)
-    uint32_t *u_cm;  // clientId | removedClientId << 12 | kCmOvl
+    uint32_t *u_cm;  // clientId | removedClientId << kCmR | kCmOvl
     BA<Idx> b_parent;  // b_parent of a free block links the free block list
     BA<Idx, 3> b_child;
     BA<uint8_t> b_count, b_leaf;
@@ -525,7 +526,7 @@ struct Engine {
             vis = ((cm & kMetaCli) == c) || (us_q(sr) <= rr);
             rle = us_r(sr) <= rr;
             if constexpr (kW) pending = us_q(sr) == kRUnassigned;
-            rem = (((cm >> 12) & kMetaCli) == c) || rle;
+            rem = (((cm >> kCmR) & kMetaCli) == c) || rle;
             if (!rem && (cm & kCmOvl)) rem = ovl_has(slot, c);
         } else {
             const uint4 q = cold[2 * slot + 1];
@@ -568,10 +569,6 @@ struct Engine {
     MT_FI static uint32_t meta_out(uint32_t m, uint32_t clients, uint32_t ovl) {
         uint32_t r = (clients & kMetaCli) | (((clients >> 16) & kMetaCli) << kMetaRcliShift);
         if (m & kFMarker) r |= kMetaMarker;
-        if (m & kFEndsNL) r |= kMetaEndsNL;
-        if (m & kFLinked) r |= kMetaLinked;
-        if (m & kFHasProps) r |= kMetaHasProps;
-        if (m & kFHasNL) r |= kMetaHasNL;
         if (ovl) r |= kMetaHasOvl;
         return r;
     }
@@ -582,7 +579,7 @@ struct Engine {
         const uint32_t len = s_len[slot];
         const uint32_t rr = (uint32_t)(ref - sbase);
         const bool vis = ((cm & kMetaCli) == c) || (us_q(sr) <= rr);
-        bool rem = (((cm >> 12) & kMetaCli) == c) || (us_r(sr) <= rr);
+        bool rem = (((cm >> kCmR) & kMetaCli) == c) || (us_r(sr) <= rr);
         if (!rem && (cm & kCmOvl)) rem = ovl_has(slot, c);
         return (vis && !rem) ? len : 0u;
     }
@@ -1803,7 +1800,7 @@ struct Engine {
     // is passed on; both, and keys the host flagged, end the document as MT_UNSUPPORTED.
     MT_FI void op_relpos(const mt_op &op) {
         ov_splits = -1;
-        ensure_overlay(op.ref_seq, op.client);
+        ensure_overlay(op.ref_seq, MT_OP_CLIENT(op));
         int32_t pend = 0;
         for (int k = 0; k < 2; k++) {
             if (!(op.flags & (k ? MT_RELF_POS2 : MT_RELF_POS1))) continue;
@@ -1821,7 +1818,7 @@ struct Engine {
                 set_fail(ST_UNSUPPORTED);
                 return;
             }
-            int64_t pos = slot == kIdUnlinked ? 0 : (int64_t)get_position(slot, op.ref_seq, op.client);
+            int64_t pos = slot == kIdUnlinked ? 0 : (int64_t)get_position(slot, op.ref_seq, MT_OP_CLIENT(op));
             const int32_t off = (int32_t)(k ? op.payload_len : op.payload);
             if (!(op.flags & (k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1))) {
                 pos += 1;  // marker.cachedLength
@@ -2493,7 +2490,7 @@ struct Engine {
             wsync();
             // (a settled loaded segment too, while it moves through block splits: it joins the
             // settled sums after the leaf insert)
-            u_push((uint32_t)slot, sr, (c & kMetaCli) | (rcli << 12));
+            u_push((uint32_t)slot, sr, (c & kMetaCli) | (rcli << kCmR));
             if (status) return;
             int32_t blk = insert_leaf(W.blk, W.k, (uint32_t)slot);
             if (status) return;
@@ -2514,7 +2511,7 @@ struct Engine {
         if (local) return;  // no zamboni after a local op (mergeTree.ts:1994-1997)
         if (!loaded || !(op.flags & MT_OPF_GROUP_CONT)) zamboni();
     }
-    MT_FI void op_insert(const mt_op &op) { insert_one<false>(op, op.client, (uint32_t)op.pos1, op.ref_seq); }
+    MT_FI void op_insert(const mt_op &op) { insert_one<false>(op, MT_OP_CLIENT(op), (uint32_t)op.pos1, op.ref_seq); }
 
     // ------------------------------------------------------------------ SnapshotLoader
     // (snapshotLoader.ts:36-205) — the header chunk's segments, MergeTree.reloadFromSegments
@@ -2549,7 +2546,7 @@ struct Engine {
         if (rseq != kNoneSeq) meta |= kFRemoved;
         s_len[slot] = (Len)len;
         cold_init(slot, props, op.payload, marker ? props : len, (uint32_t)op.seq, (uint32_t)rseq,
-                  (op.client & kMetaCli) | (rcli << 16));
+                  (MT_OP_CLIENT(op) & kMetaCli) | (rcli << 16));
         s_meta[slot] = (Meta)meta;
         wsync();
         // reloadFromSegments' blockUpdate maps the ids of markers with localNetLength > 0
@@ -2638,7 +2635,7 @@ struct Engine {
                     if (sett && rs == kNoneSeq) add = s_len[slot];
                     b = s_blk[slot];
                     sr = us_make(rel(sq), rs == kNoneSeq ? kRNone : rel(rs));
-                    cm = (q.z & kMetaCli) | (((q.z >> 16) & kMetaCli) << 12);
+                    cm = (q.z & kMetaCli) | (((q.z >> 16) & kMetaCli) << kCmR);
                 }
             }
             const bool un = live && !sett;
@@ -2682,7 +2679,7 @@ struct Engine {
         const uint2 st = h_ent[0];  // {insert position, batch open}
         const uint32_t pos = rfl(st.y) ? rfl(st.x) : local_length();
         const uint32_t len = (op.flags & MT_OPF_MARKER) ? 1u : op.payload_len;
-        insert_one<true>(op, op.client, pos, 0);
+        insert_one<true>(op, MT_OP_CLIENT(op), pos, 0);
         wsync();
         if (lane == 0) h_ent[0] = make_uint2(pos + len, (op.flags & MT_OPF_GROUP_CONT) ? 1u : 0u);
         wsync();
@@ -2691,7 +2688,7 @@ struct Engine {
     // markRangeRemoved / annotateRange (mergeTree.ts:2565-2719): both boundaries, then the
     // nodeMap range walk leaf block by leaf block
     MT_FI void op_range(const mt_op &op) {
-        const uint32_t c = op.client;
+        const uint32_t c = MT_OP_CLIENT(op);
         const int32_t ref = op.ref_seq;
         const uint32_t start = (uint32_t)op.pos1, end = (uint32_t)op.pos2;
         ov_splits = -1;
@@ -2775,7 +2772,7 @@ struct Engine {
     }
 
     MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end) {
-        const uint32_t c = op.client;
+        const uint32_t c = MT_OP_CLIENT(op);
         const int32_t ref = op.ref_seq;
         resolve_cold();  // the walk reads / updates cold records of split halves
         ensure_overlay(ref, c);
@@ -2833,12 +2830,12 @@ struct Engine {
                 if (first) {
                     if (ui != kUNone) {
                         u_sr[ui] = us_make(us_q(sr), rq);
-                        u_cm[ui] = (cm & ~(kMetaCli << 12)) | ((c & kMetaCli) << 12);
+                        u_cm[ui] = (cm & ~(kMetaCli << kCmR)) | ((c & kMetaCli) << kCmR);
                     } else {
                         ui = (uint32_t)nu + (uint32_t)__popcll(um & ((1ull << lane) - 1ull));
                         u_list[ui] = (Idx)slot;
                         u_sr[ui] = us_make(0u, rq);  // seq <= minSeq: relative 0 (its clientId is never compared)
-                        u_cm[ui] = kNoClient | ((c & kMetaCli) << 12);
+                        u_cm[ui] = kNoClient | ((c & kMetaCli) << kCmR);
                     }
                     s_meta[slot] = (Meta)(((meta | kFRemoved) & ~kUNone) | ui);
                     cold[2 * slot + 1].y = (uint32_t)op.seq;
@@ -2924,8 +2921,9 @@ struct Engine {
     // SnapshotLoader records (mt_load_kernel only): no sequence checks, no updateSeqNumbers
     MT_FI void apply_load(const mt_op &op) {
         pend_n = 0;
-        const bool noncollab = op.client == MT_CLIENT_NONCOLLAB;
-        if (op.type != MT_OP_COLLAB && (op.client == 0 || (op.client >= (uint32_t)kMaxClients && !noncollab))) {
+        const uint32_t oc = MT_OP_CLIENT(op);
+        const bool noncollab = oc == MT_CLIENT_NONCOLLAB;
+        if (op.type != MT_OP_COLLAB && (oc == 0 || (oc >= (uint32_t)kMaxClients && !noncollab))) {
             set_fail(ST_UNSUPPORTED);
             return;
         }
@@ -2940,7 +2938,7 @@ struct Engine {
     // client, UnassignedSequenceNumber; 553-563).  getValidOpRange's local check (504-543): an
     // invalid range is logged (InvalidOpRange) and the op is not applied.
     MT_FI void op_local(mt_op op) {
-        if (op.client != 0u) {
+        if (MT_OP_CLIENT(op) != 0u) {
             set_fail(ST_BAD_INPUT);
             return;
         }
@@ -3147,7 +3145,7 @@ struct Engine {
                 return;
             }
         }
-        if (op.client >= (uint32_t)kMaxClients || (!kW && op.client == 0 && op.type != MT_OP_NOOP)) {
+        if (MT_OP_CLIENT(op) >= (uint32_t)kMaxClients || (!kW && MT_OP_CLIENT(op) == 0 && op.type != MT_OP_NOOP)) {
             set_fail(ST_UNSUPPORTED);
             return;
         }
@@ -3161,7 +3159,7 @@ struct Engine {
             }
         }
         if constexpr (kW) {
-            if (op.client == 0 && op.type != MT_OP_NOOP) {
+            if (MT_OP_CLIENT(op) == 0 && op.type != MT_OP_NOOP) {
                 // the replica's own sequenced message acks its oldest pending group (client.ts:
                 // 810-812; a GROUP acks one group per member); positions are not read
                 if (op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) == MT_COMBINE_CONSENSUS) {

@@ -904,7 +904,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     bool writer = false;
     for (int64_t d = 0; d < D && !writer; d++)
         for (int64_t i = h_off[d] + nload[d]; i < h_off[d + 1]; i++)
-            if (ops[i].seq == mt::kUnassignedSeq || (ops[i].client == 0 && ops[i].type != MT_OP_NOOP)) {
+            if (ops[i].seq == mt::kUnassignedSeq || (MT_OP_CLIENT(ops[i]) == 0 && ops[i].type != MT_OP_NOOP)) {
                 writer = true;
                 break;
             }

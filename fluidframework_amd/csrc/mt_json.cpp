@@ -589,7 +589,7 @@ struct Packer1 {
         }
         if (flags & (MT_RELF_POS1 | MT_RELF_POS2)) {
             r.type = MT_OP_RELPOS;
-            r.flags = (uint16_t)flags;
+            r.flags = (uint16_t)(flags | (base.flags & MT_OPF_CLIENT_HI_MASK));
         }
         return true;
     }
@@ -603,7 +603,7 @@ struct Packer1 {
         if (!D.is_null_or_absent(D.member(op, "register")))
             return fail(MT_UNSUPPORTED, "registers are not on the observer fast path");
         const double tv = t >= 0 && D.nodes[t].type == J_NUM ? D.nodes[t].num : -1;
-        r.flags = 0;
+        r.flags = (uint16_t)(base.flags & MT_OPF_CLIENT_HI_MASK);
         r.pos1 = p1 >= 0 ? as_int(D.nodes[p1]) : 0;
         r.pos2 = 0;
         r.payload = r.payload_len = 0;
@@ -648,12 +648,17 @@ struct Packer1 {
         }
         return true;
     }
+    // a record's short client id: the low 12 bits in `client`, the high 3 in flags bits 11-13
+    static void set_client(mt_op &r, uint32_t c) {
+        r.client = (uint16_t)(c & 0xFFFu);
+        r.flags = (uint16_t)((r.flags & ~MT_OPF_CLIENT_HI_MASK) | MT_OPF_CLIENT_HI(c));
+    }
     // getOrAddShortClientId (client.ts:636-641); -1 past MT_MAX_CLIENTS clients
     int client_id(const std::u16string &name) {
         auto it = L.shortid.find(name);
         if (it != L.shortid.end()) return it->second;
-        if (L.names.size() >= MT_MAX_CLIENTS) return -1;  // 4094, 4095 are MT_CLIENT_NONCOLLAB / MT_CLIENT_NONE
-        const uint16_t c = (uint16_t)L.names.size();
+        if (L.names.size() >= MT_MAX_CLIENTS) return -1;  // 0x7FFE, 0x7FFF are MT_CLIENT_NONCOLLAB / MT_CLIENT_NONE
+        const int c = (int)L.names.size();
         L.shortid.emplace(name, c);
         L.names.push_back(name);
         return c;
@@ -665,7 +670,7 @@ struct Packer1 {
         r.type = type;
         r.ref_seq = MT_SEQ_NONE;
         r.msn = (int32_t)MT_CLIENT_NONE;
-        r.client = MT_CLIENT_NONCOLLAB;
+        set_client(r, MT_CLIENT_NONCOLLAB);
         const int32_t json = D.nodes[spec].type == J_OBJ ? D.member(spec, "json") : -1;
         int32_t seg = spec;
         if (json >= 0) {  // hasMergeInfo
@@ -675,15 +680,15 @@ struct Packer1 {
             if (cl >= 0) {
                 if (D.nodes[cl].type != J_STR) return fail(MT_BAD_INPUT, "client is not a string");
                 const int c = client_id(D.str_of(cl));
-                if (c < 0) return fail(MT_UNSUPPORTED, "more than 4093 clients");
-                r.client = (uint16_t)c;
+                if (c < 0) return fail(MT_UNSUPPORTED, "more than 32765 clients");
+                set_client(r, (uint32_t)c);
             }
             if (sq >= 0) r.seq = as_int(D.nodes[sq]);
             if (rs >= 0) r.ref_seq = as_int(D.nodes[rs]);
             if (rc >= 0) {
                 if (D.nodes[rc].type != J_STR) return fail(MT_BAD_INPUT, "removedClient is not a string");
                 const int c = client_id(D.str_of(rc));
-                if (c < 0) return fail(MT_UNSUPPORTED, "more than 4093 clients");
+                if (c < 0) return fail(MT_UNSUPPORTED, "more than 32765 clients");
                 r.msn = c;
             }
         }
@@ -790,7 +795,7 @@ struct Packer1 {
             });
             if (!ok) return false;
         }
-        auto batchable = [](const mt_op &o) { return o.client == MT_CLIENT_NONCOLLAB && o.seq == 0; };
+        auto batchable = [](const mt_op &o) { return MT_OP_CLIENT(o) == MT_CLIENT_NONCOLLAB && o.seq == 0; };
         for (size_t i = body0; i + 1 < L.ops.size(); i++)
             if (batchable(L.ops[i]) && batchable(L.ops[i + 1])) L.ops[i].flags |= MT_OPF_GROUP_CONT;
         return true;
@@ -817,10 +822,10 @@ struct Packer1 {
             const int32_t cid = D.member(m, "clientId");
             std::u16string name = cid >= 0 && D.nodes[cid].type == J_STR ? D.str_of(cid) : u"null";
             const int ci = client_id(name);
-            if (ci < 0) return fail(MT_UNSUPPORTED, "more than 4093 clients");
-            const uint16_t c = (uint16_t)ci;
+            if (ci < 0) return fail(MT_UNSUPPORTED, "more than 32765 clients");
+            const uint32_t c = (uint32_t)ci;
             mt_op base{};
-            base.client = c;
+            set_client(base, c);
             const int32_t sq = D.member(m, "sequenceNumber"), rs = D.member(m, "referenceSequenceNumber"),
                           ms = D.member(m, "minimumSequenceNumber");
             if (sq < 0) return fail(MT_BAD_INPUT, "message without sequence numbers");

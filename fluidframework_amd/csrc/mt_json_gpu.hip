@@ -56,7 +56,7 @@ enum : uint32_t {
     kFShape = 2,    // a message / op shape outside the fast path (markers, escapes, floats ...)
     kFRange = 4,    // an integer outside int32
     kFWriter = 8,   // a writer replica's log (local ops / own acks)
-    kFClients = 16, // more than 4093 clients
+    kFClients = 16, // more than 32765 clients
     kFCap = 32      // more messages than the scan's per-document region holds
 };
 
@@ -1079,7 +1079,7 @@ __host__ __device__ uint32_t relpos_record(const uint8_t *s, uint32_t n, const O
         }
     }
     if (rflags & (MT_RELF_POS1 | MT_RELF_POS2)) {
-        rr.flags = (uint16_t)rflags;
+        rr.flags = (uint16_t)(rflags | (base.flags & MT_OPF_CLIENT_HI_MASK));
         if (W) cx.ops[mo.nrec] = rr;
         mo.nrec++;
         return 0;
@@ -1097,7 +1097,7 @@ __host__ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo 
         if (f) return f;
     }
     mt_op r = base;
-    r.flags = MT_OPF_GROUP_CONT;  // cleared on the message's last record
+    r.flags = (uint16_t)(MT_OPF_GROUP_CONT | (base.flags & MT_OPF_CLIENT_HI_MASK));  // GROUP_CONT: cleared on the message's last record
     r.pos1 = op.p1;
     r.pos2 = 0;
     r.payload = r.payload_len = 0;
@@ -1327,7 +1327,8 @@ __host__ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0
     if (is_op) mo.flags |= kMsgOp;
     mt_op base{};
     base.type = MT_OP_NOOP;
-    base.client = cx.cid;
+    base.client = (uint16_t)(cx.cid & 0xFFFu);  // the short id's high bits: flags 11-13 (mt_oplog.h)
+    base.flags = MT_OPF_CLIENT_HI(cx.cid);
     base.seq = (int32_t)seq;
     base.ref_seq = (int32_t)ref;
     base.msn = (int32_t)msn;

@@ -32,7 +32,8 @@ const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_REGENERATE = 7, OP_NOOP 
 const OPF_GROUP_CONT = 1, OPF_MARKER = 2, OPF_HAS_PROPS = 4, OPF_REWRITE = 8;
 const OP_RELPOS = 6, RELF_POS1 = 0x10, RELF_POS2 = 0x20, RELF_BEFORE1 = 0x40, RELF_BEFORE2 = 0x80, RELF_OFF1 = 0x100, RELF_OFF2 = 0x200;
 const COMBINE_INCR = 1, COMBINE_CONSENSUS = 2, COMBINE_OTHER = 3, KEY_COMBINE = 0xFFFFFFFF, VALUE_UNDEFINED = 0xFFFFFFFF;
-const MAX_INSERT_PROPS = 1023;
+const MAX_INSERT_PROPS = 127;  // include/mt_oplog.h MT_OPF_MAX_INSERT_PROPS (flags bits 4-10)
+const MAX_CLIENTS = 0x7FFE;      // short ids 0..32765 (MT_MAX_CLIENTS; 0x7FFE / 0x7FFF are sentinels)
 const STATUS = ['OK', 'INVALID_POS', 'SEQ_ORDER', 'MSN_ORDER', 'UNSUPPORTED', 'BAD_INPUT', 'CAPACITY', 'INTERNAL'];
 
 class UnsupportedOp extends Error {}
@@ -169,8 +170,7 @@ class Packer {
             if (typeof msg === 'string') msg = JSON.parse(msg);
             let c = short.get(msg.clientId);
             if (c === undefined) {
-                // short ids 0..4093 (include/mt_oplog.h MT_MAX_CLIENTS; 4094 / 4095 are sentinels)
-                if (names.length >= 4094) throw new UnsupportedOp('more than 4093 clients (short ids are 12-bit)');
+                if (names.length >= MAX_CLIENTS) throw new UnsupportedOp('more than 32765 clients (short ids are 15-bit)');
                 c = names.length;
                 short.set(msg.clientId, c);
                 names.push(msg.clientId);
@@ -229,8 +229,9 @@ class Packer {
         const ops = Buffer.alloc(32 * Math.max(1, this.recs.length));
         this.recs.forEach((r, i) => {
             const o = 32 * i;
-            ops.writeUInt16LE((r.type & 15) | (r.client << 4), o);  // mt_op's type : 4, client : 12
-            ops.writeUInt16LE(r.flags, o + 2);
+            // mt_op's type : 4, client : 12 (the id's low bits); its high 3 bits in flags 11-13
+            ops.writeUInt16LE((r.type & 15) | ((r.client & 0xFFF) << 4), o);
+            ops.writeUInt16LE(r.flags | (((r.client >> 12) & 7) << 11), o + 2);
             ops.writeInt32LE(r.seq, o + 4);
             ops.writeInt32LE(r.refSeq, o + 8);
             ops.writeInt32LE(r.msn, o + 12);

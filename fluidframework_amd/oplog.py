@@ -44,15 +44,16 @@ UNASSIGNED_SEQ = -1  # UnassignedSequenceNumber (merge-tree/src/constants.ts:11)
 # MT_OP_RELPOS flags (include/mt_oplog.h mt_relpos_flags)
 RELF_POS1, RELF_POS2, RELF_BEFORE1, RELF_BEFORE2, RELF_OFF1, RELF_OFF2 = 0x10, 0x20, 0x40, 0x80, 0x100, 0x200
 OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
-MAX_INSERT_PROPS = 1023
+MAX_INSERT_PROPS = 127  # include/mt_oplog.h MT_OPF_MAX_INSERT_PROPS (flags bits 4-10)
 # combiningOp other than "rewrite" (include/mt_oplog.h mt_combine_kind): annotate flags bits 4-5,
 # then three records {KEY_COMBINE, defaultValue}, {KEY_COMBINE, minValue}, {KEY_COMBINE, result slot}
 COMBINE_INCR, COMBINE_CONSENSUS, COMBINE_OTHER = 1, 2, 3
 KEY_COMBINE = VALUE_UNDEFINED = 0xFFFFFFFF
 
 
-MAX_CLIENTS = 4094  # short ids 0..4093 (include/mt_oplog.h MT_MAX_CLIENTS; 4094 / 4095 are sentinels)
-CLIENT_NONCOLLAB, CLIENT_NONE = 4094, 4095
+MAX_CLIENTS = 0x7FFE  # short ids 0..32765 (include/mt_oplog.h MT_MAX_CLIENTS; 0x7FFE / 0x7FFF are sentinels)
+CLIENT_NONCOLLAB, CLIENT_NONE = 0x7FFE, 0x7FFF
+OPF_CLIENT_HI_MASK = 0x3800  # the short id's high 3 bits live in flags bits 11-13 (mt_oplog.h)
 
 
 def rec_type(a):
@@ -61,8 +62,9 @@ def rec_type(a):
 
 
 def rec_client(a):
-    """short client id(s) of an mt_op record / array (the high 12 bits of "tc")"""
-    return a["tc"] >> 4
+    """short client id(s) of an mt_op record / array: the high 12 bits of "tc", and flags bits 11-13
+    above them (include/mt_oplog.h MT_OP_CLIENT)"""
+    return (np.asarray(a["tc"], np.uint32) >> 4) | (((np.asarray(a["flags"], np.uint32) >> 11) & 7) << 12)
 
 
 def make_tc(t, c):
@@ -71,8 +73,11 @@ def make_tc(t, c):
 
 
 def set_client(a, c):
-    """replace the short client id(s) of records, keeping their types"""
-    a["tc"] = make_tc(a["tc"] & 0xF, c).astype(np.uint16)
+    """replace the short client id(s) of records, keeping their types and other flags"""
+    c = np.asarray(c, np.uint32)
+    a["tc"] = make_tc(a["tc"] & 0xF, c & 0xFFF).astype(np.uint16)
+    a["flags"] = ((np.asarray(a["flags"], np.uint32) & ~np.uint32(OPF_CLIENT_HI_MASK)) |
+                  (((c >> 12) & 7) << 11)).astype(np.uint16)
 
 
 class UnsupportedOp(ValueError):
@@ -242,7 +247,7 @@ class Packer:
                 cid = "null"
             if cid not in short:  # getOrAddShortClientId (client.ts:636-641)
                 if len(names) >= MAX_CLIENTS:
-                    raise UnsupportedOp(f"more than {MAX_CLIENTS - 1} clients (short ids are 12-bit)")
+                    raise UnsupportedOp(f"more than {MAX_CLIENTS - 1} clients (short ids are 15-bit)")
                 short[cid] = len(names)
                 names.append(cid)
             c = short[cid]
@@ -408,7 +413,9 @@ class Packer:
         ops = np.zeros(len(self._ops), OP_DTYPE)
         for name in OP_DTYPE.names:
             if name == "tc":
-                ops[name] = [r["type"] | (r["client"] << 4) for r in self._ops] if self._ops else []
+                ops[name] = [r["type"] | ((r["client"] & 0xFFF) << 4) for r in self._ops] if self._ops else []
+            elif name == "flags":  # the short id's high bits in flags 11-13
+                ops[name] = [r["flags"] | (((r["client"] >> 12) & 7) << 11) for r in self._ops] if self._ops else []
             else:
                 ops[name] = [r[name] for r in self._ops] if self._ops else []
         text = np.concatenate(self._text) if self._text else np.zeros(0, np.uint16)

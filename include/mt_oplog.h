@@ -69,12 +69,16 @@ enum mt_relpos_flags {
     MT_RELF_OFF1 = 0x100u,   /* relativePos1.offset is defined (payload)           */
     MT_RELF_OFF2 = 0x200u    /* relativePos2.offset is defined (payload_len)       */
 };
-/* short client ids are 12-bit: 0 .. 4093 per document (0 = the observer; Client.getOrAddShortClientId,
+/* short client ids are 15-bit: 0 .. 32765 per document (0 = the observer; Client.getOrAddShortClientId,
    client.ts:636-660, numbers every long id a document's log names, and a real messages.json names a
-   new one on every reconnect), 4094 / 4095 are sentinels */
-#define MT_CLIENT_NONCOLLAB 4094u /* NonCollabClient (constants.ts:15); long id "original" */
-#define MT_CLIENT_NONE 4095u
-#define MT_MAX_CLIENTS 4094      /* short ids 0 .. 4093 per document (0 = the observer)          */
+   new one on every reconnect), 0x7FFE / 0x7FFF are sentinels.  A record's `client` bit-field holds
+   the low 12 bits, flags bits 11-13 the high 3 (MT_OP_CLIENT / MT_OPF_CLIENT_HI). */
+#define MT_CLIENT_NONCOLLAB 0x7FFEu /* NonCollabClient (constants.ts:15); long id "original" */
+#define MT_CLIENT_NONE 0x7FFFu
+#define MT_MAX_CLIENTS 0x7FFE      /* short ids 0 .. 32765 per document (0 = the observer)       */
+#define MT_OPF_CLIENT_HI_MASK 0x3800u
+#define MT_OPF_CLIENT_HI(c) ((uint16_t)((((uint32_t)(c) >> 12) & 7u) << 11))
+#define MT_OP_CLIENT(o) ((uint32_t)(o).client | ((((uint32_t)(o).flags >> 11) & 7u) << 12))
 #define MT_SEQ_NONE 0x7FFFFFFF
 #define MT_OP_IS_INSERT_LIKE(t) ((t) == MT_OP_INSERT || (t) == MT_OP_LOAD_HEADER || (t) == MT_OP_LOAD_BODY)
 
@@ -83,9 +87,9 @@ enum mt_relpos_flags {
    record of client 0 acks the oldest pending group (client.ts:797-819, mergeTree.ts:1893-1929). */
 #define MT_SEQ_LOCAL (-1)
 
-/* mt_op.flags: bits 0-3 public flags, bits 4-13 the prop count of an insert (<= 1023),
-   bits 14-15 are internal to the library (set at ingest: the insert's text contains a '\n' /
-   its last code unit is '\n') */
+/* mt_op.flags: bits 0-3 public flags, bits 4-10 the prop count of an insert (<= 127), bits 11-13
+   the short client id's high bits (every record type), bits 14-15 are internal to the library (set at
+   ingest: the insert's text contains a '\n' / its last code unit is '\n') */
 enum mt_op_flags {
     MT_OPF_GROUP_CONT = 1u, /* more members of the same GROUP message follow          */
     MT_OPF_MARKER = 2u,     /* insert of a Marker: payload = refType, payload_len = 1  */
@@ -112,21 +116,22 @@ enum mt_combine_kind {
 #define MT_KEY_COMBINE 0xFFFFFFFFu
 #define MT_VALUE_UNDEFINED 0xFFFFFFFFu
 #define MT_OPF_BITS(f) ((f) & 0xFu)
-#define MT_OPF_NPROPS(f) (((uint32_t)(f) >> 4) & 0x3FFu)
-#define MT_OPF_MAKE(bits, nprops) ((uint16_t)((((nprops) & 0x3FFu) << 4) | ((bits) & 0xFu)))
-#define MT_OPF_MAX_INSERT_PROPS 1023u
+#define MT_OPF_NPROPS(f) (((uint32_t)(f) >> 4) & 0x7Fu)
+#define MT_OPF_MAKE(bits, nprops) ((uint16_t)((((nprops) & 0x7Fu) << 4) | ((bits) & 0xFu)))
+#define MT_OPF_MAX_INSERT_PROPS 127u
 #define MT_OPF_INTERNAL_HAS_NL 0x4000u
 #define MT_OPF_INTERNAL_ENDS_NL 0x8000u
 #define MT_OPF_INTERNAL (MT_OPF_INTERNAL_HAS_NL | MT_OPF_INTERNAL_ENDS_NL)
 
-/* The first 16-bit word holds the record type (bits 0-3) and the short client id (bits 4-15):
-   little-endian u16 `type | client << 4`.  C / C++ / HIP read both through the bit-fields below;
-   byte packers (Python, JS) write the word. */
+/* The first 16-bit word holds the record type (bits 0-3) and the low 12 bits of the short client id
+   (bits 4-15): little-endian u16 `type | (client & 0xFFF) << 4`; the id's high 3 bits are flags bits
+   11-13.  C / C++ / HIP read them through the bit-fields below and MT_OP_CLIENT; byte packers
+   (Python, JS) write the words. */
 typedef struct mt_op {
     uint16_t type : 4;    /* enum mt_op_type                                             */
-    uint16_t client : 12; /* short client id (index in the doc's client table, 1..4093; 0 is
-                             the observer itself, as Client.startOrUpdateCollaboration
-                             assigns it first: client.ts:1051-1062)                       */
+    uint16_t client : 12; /* short client id, low 12 bits (index in the doc's client table;
+                             0 is the observer itself, as Client.startOrUpdateCollaboration
+                             assigns it first: client.ts:1051-1062); MT_OP_CLIENT            */
     uint16_t flags;       /* enum mt_op_flags | nprops<<4                                  */
     int32_t seq;          /* sequenceNumber                                                */
     int32_t ref_seq;      /* referenceSequenceNumber                                       */

@@ -54,15 +54,17 @@ extern "C" {
    point's signature, so a binding built against another header fails at load (mt_abi_version())
    instead of passing fields at the wrong offsets.
    4: round 3 dropped oe_cap / blk_cap / heap_cap from mt_batch_options and added n_docs to
-      mt_batch_ingest_json_gpu; round 4 added mt_abi_version. */
-#define MT_ABI_VERSION 4
+      mt_batch_ingest_json_gpu; round 4 added mt_abi_version.
+   5: 15-bit short client ids (mt_oplog.h: high bits in mt_op.flags 11-13, insert prop counts
+      <= 127, sentinels 0x7FFE / 0x7FFF); OutRec meta: clientId [0,15), removedClientId [15,30). */
+#define MT_ABI_VERSION 5
 
 enum mt_status_code {
     MT_OK = 0,
     MT_INVALID_POS = 1,  /* "MergeTree insert failed" */
     MT_SEQ_ORDER = 2,    /* sequence number went backwards */
     MT_MSN_ORDER = 3,    /* minimumSequenceNumber went backwards / above seq */
-    MT_UNSUPPORTED = 4,  /* op outside the device model or limits (> 4093 clients) */
+    MT_UNSUPPORTED = 4,  /* op outside the device model or limits (> 32765 clients) */
     MT_BAD_INPUT = 5,
     MT_CAPACITY = 6,     /* document exceeded the largest device capacity class */
     MT_INTERNAL = 7,

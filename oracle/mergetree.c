@@ -3160,11 +3160,12 @@ static void apply_local_packed(mto_doc *d, const mt_op *op, const uint16_t *text
 
 static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, const mt_prop *props,
                              const mto_tables *t, const char *const *client_names, int n_clients) {
-    if ((int)op->client >= n_clients) fail(d, MTO_BAD_INPUT, "client index out of range");
-    int sid = d->pk_map[op->client];
+    const int oc = (int)MT_OP_CLIENT(*op); /* 15-bit short id: high bits in flags 11-13 (mt_oplog.h) */
+    if (oc >= n_clients || oc >= MT_MAX_CLIENTS + 2) fail(d, MTO_BAD_INPUT, "client index out of range");
+    int sid = d->pk_map[oc];
     if (sid < 0) {
-        sid = get_or_add_short_client_id(d, client_names[op->client]); /* applyMsg registration */
-        d->pk_map[op->client] = sid;
+        sid = get_or_add_short_client_id(d, client_names[oc]); /* applyMsg registration */
+        d->pk_map[oc] = sid;
     }
     uint32_t bits = MT_OPF_BITS(op->flags);
     if (op->seq == UNASSIGNED_SEQ) { /* a local op of this replica (mt_oplog.h "local ops") */

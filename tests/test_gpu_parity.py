@@ -233,14 +233,17 @@ def _many_client_farm(n_clients, n_ops, seed, lag=24, hot=12, active=0):
 
 
 def test_many_clients_with_overlapping_removes():
-    """Short client ids are 12-bit (up to 4,093 writers per document; client.ts:636-660 assigns them
+    """Short client ids are 15-bit (up to 32,765 writers per document; client.ts:636-660 assigns them
     in first-appearance order and a long-lived document's log names a new clientId on every
-    reconnect): 1,000 session ids over a 16-client window, and 300 writers with concurrent
+    reconnect; the op record keeps the id's high bits in flags 11-13, mt_oplog.h): 5,000 and 1,000
+    session ids over a 16-client window with overlapping removes, and 300 writers with concurrent
     overlapping removes (overlap sets beyond 31 clients are pool lists, mergeTree.ts:2544-2563)
-    replay bit-exact, also through checkpoint / resume; more than 4,093 are flagged, not wrong."""
+    replay bit-exact, also through checkpoint / resume; more than 32,765 are flagged, not wrong."""
     docs = [_many_client_farm(1000, 7000, seed=13, active=16, hot=8),
-            _many_client_farm(300, 2500, seed=11), _many_client_farm(200, 1500, seed=12, lag=60, hot=6)]
+            _many_client_farm(300, 2500, seed=11), _many_client_farm(200, 1500, seed=12, lag=60, hot=6),
+            _many_client_farm(5000, 36000, seed=14, active=16, hot=8)]
     assert len({m["clientId"] for m in docs[0]}) == 1000
+    assert len({m["clientId"] for m in docs[3]}) == 5000
     oracle = oracle_docs_from_messages(docs)
     with fa.ReplayBatch(len(docs)) as b:
         b.ingest_messages(docs)
@@ -264,7 +267,7 @@ def test_many_clients_with_overlapping_removes():
         b.ingest_json(js, device="gpu")
         b.run()
         assert (b.device_digests() == d0).all()
-    msgs = [_msg(f"c{i}", i + 1, i, {"type": 0, "pos1": 0, "seg": "x"}) for i in range(4100)]
+    msgs = [_msg(f"c{i}", i + 1, i, {"type": 0, "pos1": 0, "seg": "x"}) for i in range(32770)]
     with fa.ReplayBatch(1) as b:
         with pytest.raises(oplog.UnsupportedOp):
             b.ingest_messages([msgs])
