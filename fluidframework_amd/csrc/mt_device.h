@@ -137,6 +137,8 @@ struct Caps {
     int32_t blk;   // blocks
     int32_t heap;  // zamboni heap entries
     int32_t ulist; // unsettled-overlay list entries
+    int32_t iblk;  // LDS classes: interior block ids [blk - iblk, blk), the only ones with settled /
+                   // overlay lengths (a leaf block's length is the sum over its leaves); 0: one pool
 };
 
 // Capacity classes are compile-time: each class is its own kernel instantiation
@@ -161,7 +163,7 @@ constexpr int kHbmSeg = 2097152;
 // the class list (X-macro: mt_host.cpp declares each class's kernels from it; __graft_entry__.py
 // builds one object per entry)
 #define MT_CLASS_LIST(X) \
-    X(128) X(416) X(499) X(579) X(659) X(743) X(904) X(1064) X(1229) X(1469) X(1792) X(2360) X(3168) X(3600) X(7280) \
+    X(128) X(480) X(569) X(664) X(756) X(847) X(1036) X(1216) X(1400) X(1679) X(2046) X(2688) X(3499) X(3937) X(7961) \
     X(2000000) X(2097152)
 #define MT_CLASS_SEG_(S) S,
 constexpr int kClassSegs[] = {MT_CLASS_LIST(MT_CLASS_SEG_)};
@@ -225,8 +227,12 @@ constexpr Caps class_caps(int seg) {
     // the overlay list (unsettled segments, ~100-200 at a lag <= 32) is sized to the collab window;
     // the largest classes, where a document with a wide window ends up, can hold half their slots
     if (is_giant_seg(seg))
-        return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24 + kGiantLdsBlocks, kGiantHeap, kGiantUlist};
-    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg >= 3500 ? seg / 2 : seg / 16 + 160};
+        return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24 + kGiantLdsBlocks, kGiantHeap, kGiantUlist, 0};
+    if (seg > 65000)  // the HBM class
+        return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg / 2, 0};
+    // leaf blocks ~0.23 per slot, interior ~0.05 (fan-out 4..7)
+    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg >= 3500 ? seg / 2 : seg / 16 + 160,
+                seg / 16 + 16};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
@@ -280,8 +286,8 @@ constexpr Layout make_layout(int seg) {
     L.bcount = o;  o = lds_align(o + 1u * c.blk);
     L.bleaf = o;   o = lds_align(o + 1u * c.blk);
     L.bscour = o;  o = lds_align(o + 1u * c.blk);
-    L.bslen = o;   o = lds_align(o + 4u * c.blk);
-    L.bacc = o;    o = lds_align(o + 4u * c.blk);
+    L.bslen = o;   o = lds_align(o + 4u * (c.iblk ? c.iblk : c.blk));  // interior blocks only (c.iblk)
+    L.bacc = o;    o = lds_align(o + 4u * (c.iblk ? c.iblk : c.blk));
     L.bep = o;     o = lds_align(o + (is_hbm_seg(seg) ? 4u * c.blk : 0u));
     L.heap = o;    o = lds_align(o + 8u * (c.heap + 2));
     L.scratch = o; o = lds_align(o + 4u * 128);

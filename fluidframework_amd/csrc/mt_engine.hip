@@ -223,6 +223,13 @@ struct Engine {
     template <typename T, int kShift = 0>
     using BA = BArr<T, kShift, kGiant>;
     static constexpr uint32_t kMaxLen = len_bytes(SEG) == 2u ? 0xFFFFu : 0xFFFFFFFFu;
+    // Block pools.  LDS classes: leaf blocks take ids [0, kLB), interior blocks [kLB, cap.blk); only
+    // interior blocks keep settled / overlay lengths (b_slen, b_acc indexed by si(id)) — a leaf
+    // block's length is the sum over its <= 7 leaves, evaluated where a walk needs it.  The giant and
+    // HBM classes keep full-size tables (leaf entries unused) and their own pools.
+    static constexpr bool kSplitPools = cap.iblk > 0;
+    static constexpr int32_t kLB = kSplitPools ? cap.blk - cap.iblk : 0;
+    MT_FI static uint32_t si(uint32_t b) { return kSplitPools ? b - (uint32_t)kLB : b; }
     // SlotMeta: 7 flags above a kUB-bit index of the slot's overlay entry (kUNone: settled)
     using Meta = std::conditional_t<meta_bytes(SEG) == 2u, uint16_t, uint32_t>;
     static constexpr int kUB = 8 * (int)sizeof(Meta) - 7;
@@ -445,7 +452,19 @@ struct Engine {
     // level: the block's height above the leaf blocks (0: a leaf block; a block's level never changes)
     MT_FI int32_t alloc_block(int leaf, int32_t level) {
         int32_t b;
-        if (kGiant && level >= kGiantLdsLevel && (n_lfree > 0 || lds_top < kGiantLdsBlocks)) {
+        if (kSplitPools && level >= 1) {  // the interior pool
+            if (n_lfree > 0) {
+                b = lfree_head;
+                lfree_head = (int32_t)rfl((uint32_t)b_parent[b]);
+                if (lfree_head == (int32_t)kNoBlk) lfree_head = -1;
+                n_lfree--;
+            } else if (lds_top < cap.iblk) {
+                b = kLB + lds_top++;
+            } else {
+                cap_fail(1);
+                return kLB;
+            }
+        } else if (kGiant && level >= kGiantLdsLevel && (n_lfree > 0 || lds_top < kGiantLdsBlocks)) {
             if (n_lfree > 0) {
                 b = lfree_head;
                 lfree_head = (int32_t)rfl((uint32_t)b_parent[b]);
@@ -460,7 +479,8 @@ struct Engine {
             if (bfree_head == (int32_t)kNoBlk) bfree_head = -1;
             n_bfree--;
         } else {
-            if (blk_top >= cap.blk || (uint32_t)blk_top >= kNoBlk) {
+            const int32_t top = kSplitPools ? kLB : cap.blk;
+            if (blk_top >= top || (uint32_t)blk_top >= kNoBlk) {
                 cap_fail(1);
                 return 0;
             }
@@ -470,11 +490,13 @@ struct Engine {
         b_count[b] = 0;
         b_scour[b] = kScourUndef;
         b_parent[b] = (Idx)kNoBlk;
-        b_slen[b] = 0;
+        if (!kSplitPools || !leaf) b_slen[si(b)] = 0;
         return b;
     }
+    // the second pool: interior ids (LDS classes) / LDS-resident ids (giant class)
+    MT_FI static bool in_second_pool(int32_t b) { return kSplitPools ? b >= kLB : (kGiant && b < kGiantLdsBlocks); }
     MT_FI void free_block(int32_t b) {
-        if (kGiant && b < kGiantLdsBlocks) {
+        if (in_second_pool(b)) {
             b_parent[b] = (Idx)(lfree_head < 0 ? (int32_t)kNoBlk : (int32_t)lfree_head);
             lfree_head = b;
             n_lfree++;
@@ -585,24 +607,26 @@ struct Engine {
     }
 
     // ------------------------------------------------------------------ ancestor chains
-    // every active lane adds v into arr[] on the chain leaf block b -> root (all leaves sit at
-    // depth - 1, so the walk is `depth` uniform steps)
+    // every active lane adds v into arr[si(B)] for the interior blocks B on the chain above leaf block
+    // b (all leaves sit at depth - 1, so the walk is depth - 1 uniform steps)
     template <typename Arr>
     MT_FI void chain_add(Arr &arr, bool act, uint32_t b, uint32_t v) {
-        for (int32_t l = 0; l < depth; l++) {
+        if (act) b = b_parent[b];
+        for (int32_t l = 1; l < depth; l++) {
             if (act && b != kNoBlk) {
-                arr.add(b, v);
+                arr.add(si(b), v);
                 b = b_parent[b];
             }
         }
     }
-    // uniform: b_slen += v on the chain b -> root
+    // uniform: b_slen += v on the interior chain above leaf block b
     MT_FI void chain_add_uniform(int32_t b, uint32_t v) {
         wsync();
+        b = b_parent[b];
         while (b != (int32_t)kNoBlk) {
-            uint32_t x = b_slen[b];
+            uint32_t x = b_slen[si(b)];
             int32_t p = b_parent[b];
-            b_slen[b] = x + v;
+            b_slen[si(b)] = x + v;
             b = p;
         }
         wsync();
@@ -612,8 +636,8 @@ struct Engine {
     // the adds (every lane of a shared block writes the same reset)
     MT_FI void ov_chain_add(bool act, uint32_t b, uint32_t v) {
         if constexpr (kHbm) {
-            uint32_t c = b;
-            for (int32_t l = 0; l < depth; l++) {
+            uint32_t c = act ? (uint32_t)b_parent[b] : kNoBlk;
+            for (int32_t l = 1; l < depth; l++) {
                 if (act && c != kNoBlk) {
                     if (b_ep[c] != ov_epoch) {
                         b_acc[c] = 0u;
@@ -637,14 +661,17 @@ struct Engine {
             wsync();
         }
     }
+    // an interior block's overlay length
     MT_FI uint32_t ov_acc(uint32_t b) const {
         if constexpr (kGiant) {
             if (b < (uint32_t)kGiantLdsBlocks) return b_ep.lds[b] == ov_epoch ? b_acc.lds[b] : 0u;
             return b_acc.p[b];  // zero unless the current overlay added into it
         }
         if constexpr (kHbm) return b_ep[b] == ov_epoch ? b_acc[b] : 0u;
-        return b_acc[b];
+        return b_acc[si(b)];
     }
+    // an interior block's view length (settled sum + overlay)
+    MT_FI uint32_t iview(uint32_t b) const { return ov_acc(b) + (ov_full ? 0u : b_slen[si(b)]); }
     // giant class: zero the HBM b_acc entries the last overlay wrote (and every one, once per
     // launch, when `all`: the tables are uninitialised device memory)
     MT_FI void giant_clear_acc(bool all) {
@@ -694,7 +721,10 @@ struct Engine {
                 }
                 act[k] = act[k] && vlen[k] > 0u;
             }
-            for (int32_t l = 0; l < depth; l++) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)  // the chain starts above the leaf block (interior blocks only)
+                if (act[k]) b[k] = b_parent[b[k]];
+            for (int32_t l = 1; l < depth; l++) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     if (!act[k] || b[k] == kNoBlk) continue;
@@ -786,7 +816,7 @@ struct Engine {
         if constexpr (kHbm) {
             ov_epoch++;  // blocks of other epochs read as 0 (giant documents: ~10^5 blocks)
         } else {
-            for (int32_t i = lane; i < blk_top; i += kWave) b_acc[i] = 0u;
+            for (int32_t i = lane; i < (kSplitPools ? lds_top : blk_top); i += kWave) b_acc[i] = 0u;
         }
         wsync();
         ov_full = ref < min_seq;
@@ -880,10 +910,14 @@ struct Engine {
     // block the first leaf with pos < len or the leaf tie rule, else the block end.
     // strict mode (nodeMap's start < len, mergeTree.ts:2903-2965): first child whose cumulative
     // length exceeds pos; returns only the leaf block and its start position.
-    // giant class: the same walk with every child's row and count loaded in the round that loads
-    // the children's lengths (lane i: row entry i & 7 of child i >> 3), so an HBM level costs one
-    // dependent round trip instead of two; the chosen child's row moves to lanes 0-7 by a permute
-    MT_FI Walk descend_giant(uint32_t pos, int32_t ref, uint32_t c, bool strict) {
+    // Levels whose children are interior blocks use their settled sums + overlay (giant class: every
+    // child's row loaded in the round that loads the children's lengths — lane i: row entry i & 7 of
+    // child i >> 3 — so an HBM level costs one dependent round trip; the chosen child's row moves to
+    // lanes 0-7 by a permute).  The level-1 block's children are leaf blocks, which keep no length: all
+    // their leaves are evaluated at once (lane = 8 x child + entry), the leaf blocks' lengths are
+    // group sums, and the chosen leaf block's leaves move to lanes 0-7 for the leaf rule.
+    MT_FI Walk descend(uint32_t pos, int32_t ref, uint32_t c, bool strict) {
+        PF_SCOPE(1);
         Walk W;
         W.blk = -1;
         W.k = 0;
@@ -897,13 +931,15 @@ struct Engine {
         const bool lanes8 = lane < kMaxNodes;
         int32_t n = b_count[N];
         uint32_t row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;
-        for (int32_t l = 0; l + 1 < depth; l++) {
-            const uint32_t myc = (uint32_t)__shfl((int)row, lane >> 3, kWave);
-            const bool cin = (lane >> 3) < n;
-            const uint32_t nrow = cin ? (uint32_t)b_child[myc * 8 + (lane & 7)] : 0u;
+        for (int32_t l = 0; l + 2 < depth; l++) {
+            uint32_t nrow = 0;
+            if constexpr (kGiant || MT_DESCENT_ONE_ROUND) {
+                const uint32_t myc = (uint32_t)__shfl((int)row, lane >> 3, kWave);
+                nrow = (lane >> 3) < n ? (uint32_t)b_child[myc * 8 + (lane & 7)] : 0u;
+            }
             uint32_t v = 0, cnt = 0;
             if (lane < n) {
-                v = ov_acc(row) + (ov_full ? 0u : b_slen[row]);
+                v = iview(row);
                 cnt = b_count[row];
             }
             const uint32_t incl = scan8(v) + base;
@@ -913,16 +949,47 @@ struct Engine {
             base = rdl(incl - v, f);
             N = (int32_t)rdl(row, f);
             n = (int32_t)rdl(cnt, f);
-            row = (uint32_t)__shfl((int)nrow, 8 * f + (lane & 7), kWave);
-            if (!lanes8) row = 0u;
+            if constexpr (kGiant || MT_DESCENT_ONE_ROUND) {
+                row = (uint32_t)__shfl((int)nrow, 8 * f + (lane & 7), kWave);
+                if (!lanes8) row = 0u;
+            } else {
+                row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;
+            }
         }
-        W.blk = N;
-        W.n = n;
-        W.base = base;
-        if (strict) return W;
         uint32_t vlen = 0;
         bool tie = false;
-        if (lane < n) view_of(row, ref, c, vlen, tie);
+        if (depth >= 2) {
+            const int32_t ci = lane >> 3, j = lane & 7;
+            const uint32_t cb = (uint32_t)__shfl((int)row, ci, kWave);
+            const bool cin = ci < n;
+            const uint32_t cn = cin ? (uint32_t)b_count[cb] : 0u;
+            const uint32_t sl = cin ? (uint32_t)b_child[cb * 8 + j] : 0u;
+            if (cin && (uint32_t)j < cn) view_of(sl, ref, c, vlen, tie);
+            const uint32_t gsum = sum8(vlen);
+            const uint32_t cl = (uint32_t)__shfl((int)gsum, 8 * lane, kWave);
+            const uint32_t incl = scan8(cl) + base;
+            const uint64_t hb = ballot(lanes8 && lane < n && (strict ? incl > pos : incl >= pos));
+            if (!hb) return W;
+            const int f = first_lane(hb);
+            base = rdl(incl - cl, f);
+            N = (int32_t)rdl(row, f);
+            n = (int32_t)rdl(cn, 8 * f);
+            W.blk = N;
+            W.n = n;
+            W.base = base;
+            if (strict) return W;
+            const int src = 8 * f + (lane & 7);
+            vlen = (uint32_t)__shfl((int)vlen, src, kWave);
+            tie = __shfl((int)tie, src, kWave) != 0;
+            row = (uint32_t)__shfl((int)sl, src, kWave);
+        } else {  // the root is the only (leaf) block
+            W.blk = N;
+            W.n = n;
+            W.base = base;
+            if (strict) return W;
+            if (lane < n) view_of(row, ref, c, vlen, tie);
+        }
+        if (lane >= n) vlen = 0u;
         const uint32_t incl = scan8(vlen) + base;
         const uint32_t excl = incl - vlen;
         const uint64_t cb = ballot(lanes8 && lane < n && (incl > pos || (excl == pos && vlen == 0u && tie)));
@@ -941,59 +1008,19 @@ struct Engine {
         return W;
     }
 
-    MT_FI Walk descend(uint32_t pos, int32_t ref, uint32_t c, bool strict) {
-        PF_SCOPE(1);
-        if constexpr (kGiant || MT_DESCENT_ONE_ROUND) return descend_giant(pos, ref, c, strict);
-        Walk W;
-        W.blk = -1;
-        W.k = 0;
-        W.n = 0;
-        W.base = 0;
-        W.excl = 0;
-        W.ok = 0;
-        W.slot = 0;
-        int32_t N = root;
-        uint32_t base = 0;
-        const bool lanes8 = lane < kMaxNodes;
-        for (int32_t l = 0; l + 1 < depth; l++) {
-            const int32_t n = b_count[N];
-            const uint32_t row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;  // issued with the count
-            uint32_t ch = 0, v = 0;
-            if (lane < n) {
-                ch = row;
-                v = ov_acc(ch) + (ov_full ? 0u : b_slen[ch]);
-            }
-            const uint32_t incl = scan8(v) + base;
-            const uint64_t hb = ballot(lanes8 && lane < n && (strict ? incl > pos : incl >= pos));
-            if (!hb) return W;
-            const int f = first_lane(hb);
-            base = rdl(incl - v, f);
-            N = (int32_t)rdl(ch, f);
-        }
-        const int32_t n = b_count[N];
-        W.blk = N;
-        W.n = n;
-        W.base = base;
-        if (strict) return W;
-        const uint32_t row = lanes8 ? (uint32_t)b_child[N * 8 + lane] : 0u;
-        uint32_t vlen = 0;
-        bool tie = false;
-        if (lane < n) view_of(row, ref, c, vlen, tie);
-        const uint32_t incl = scan8(vlen) + base;
-        const uint32_t excl = incl - vlen;
-        const uint64_t cb = ballot(lanes8 && lane < n && (incl > pos || (excl == pos && vlen == 0u && tie)));
-        if (cb) {
-            const int f = first_lane(cb);
-            W.k = f;
-            W.excl = rdl(excl, f);
-            W.ok = 1;
-        } else {
-            const uint32_t end = n > 0 ? rdl(incl, n - 1) : base;
-            W.k = n;
-            W.excl = end;
-            W.ok = end == pos;
-        }
-        return W;
+    // the settled length of a block: an interior block's b_slen, a leaf block's sum over its leaves
+    MT_FI uint32_t blk_settled(uint32_t b, bool leafb) {
+        if (!leafb) return b_slen[si(b)];
+        const int32_t n = b_count[b];
+        const uint32_t x = lane < n ? settled_len(b_child[b * 8 + lane]) : 0u;
+        return rdl(sum8(x), 0);
+    }
+    // per lane: the settled length of leaf block b (each lane its own block, <= 7 leaves)
+    MT_FI uint32_t leaf_block_settled(uint32_t b) {
+        const int32_t n = b_count[b];
+        uint32_t x = 0;
+        for (int32_t j = 0; j < n; j++) x += settled_len(b_child[b * 8 + j]);
+        return x;
     }
 
     // ------------------------------------------------------------------ text helpers
@@ -1168,10 +1195,12 @@ struct Engine {
     MT_FI void update_root(int32_t split_node) {
         int32_t nr = alloc_block(0, depth);  // the old root is at level depth - 1
         if (status) return;
+        const bool leafs = depth == 1;  // the old root and its split-off half are leaf blocks
+        const uint32_t sl = blk_settled((uint32_t)root, leafs) + blk_settled((uint32_t)split_node, leafs);
         b_child[nr * 8 + 0] = (Idx)root;
         b_child[nr * 8 + 1] = (Idx)split_node;
         b_count[nr] = 2;
-        b_slen[nr] = b_slen[root] + b_slen[split_node];
+        b_slen[si(nr)] = sl;
         b_parent[root] = (Idx)nr;
         b_parent[split_node] = (Idx)nr;
         root = nr;
@@ -1201,19 +1230,30 @@ struct Engine {
             if (status) return;
             splits++;
             wsync();
-            uint32_t sl = 0;
+            uint32_t moved;
+            if (level == 1) {  // p's children are leaf blocks: the moved settled length from their leaves
+                const int32_t ci = 4 + (lane >> 3), j = lane & 7;
+                uint32_t x = 0;
+                if (lane < 32) {
+                    const uint32_t cb = b_child[p * 8 + ci];
+                    if ((uint32_t)j < (uint32_t)b_count[cb]) x = settled_len(b_child[cb * 8 + j]);
+                }
+                moved = rdl(scan_incl(x), 63);
+            } else {
+                const uint32_t x = lane >= 4 && lane < 8 ? (uint32_t)b_slen[si(b_child[p * 8 + lane])] : 0u;
+                moved = rdl(sum8(x), 0);
+            }
+            wsync();
             if (lane >= 4 && lane < 8) {
                 Idx c = b_child[p * 8 + lane];
                 b_child[m * 8 + lane - 4] = c;
                 b_parent[c] = (Idx)m;
-                sl = b_slen[c];
             }
-            const uint32_t moved = rdl(sum8(lane >= 4 && lane < 8 ? sl : 0u), 0);
             wsync();
             b_count[m] = 4;
             b_count[p] = 4;
-            b_slen[m] = moved;
-            b_slen[p] = b_slen[p] - moved;
+            b_slen[si(m)] = moved;
+            b_slen[si(p)] = b_slen[si(p)] - moved;
             wsync();
             if (p == root) {
                 update_root(m);
@@ -1231,19 +1271,14 @@ struct Engine {
         if (status) return blk;
         splits++;
         wsync();
-        uint32_t sl = 0;
         if (lane >= 4 && lane < 8) {
             Idx c = b_child[blk * 8 + lane];
             b_child[nb * 8 + lane - 4] = c;
             s_blk[c] = (Idx)nb;
-            sl = settled_len(c);
         }
-        const uint32_t moved = rdl(sum8(lane >= 4 && lane < 8 ? sl : 0u), 0);
         wsync();
         b_count[nb] = 4;
-        b_count[blk] = 4;
-        b_slen[nb] = moved;
-        b_slen[blk] = b_slen[blk] - moved;
+        b_count[blk] = 4;  // (leaf blocks keep no length; the parent's settled sum is unchanged)
         wsync();
         if (blk == root) update_root(nb);
         else insert_child_after(b_parent[blk], blk, nb);
@@ -1773,25 +1808,30 @@ struct Engine {
     MT_FI uint32_t get_position(uint32_t slot, int32_t ref, uint32_t c) {
         int32_t B = (int32_t)rfl((uint32_t)s_blk[slot]);
         uint32_t pos = 0, child = slot;
-        bool leaf = true;
-        while (B != (int32_t)kNoBlk) {
+        for (int32_t level = 0; B != (int32_t)kNoBlk; level++) {
             const int32_t n = b_count[B];
             const uint32_t row = lane < n ? (uint32_t)b_child[B * 8 + lane] : kNoBlk;
             const uint64_t at = ballot(lane < n && row == child);
             const int32_t k = at ? first_lane(at) : n;
             uint32_t v = 0;
-            if (lane < k) {
-                if (leaf) {
+            if (level == 0) {  // the leaves before it
+                if (lane < k) {
                     bool tie;
                     view_of(row, ref, c, v, tie);
-                } else {
-                    v = ov_acc(row) + (ov_full ? 0u : b_slen[row]);
                 }
+            } else if (level == 1) {  // the leaf blocks before it: their leaves (lane = 8 x block + entry)
+                const int32_t ci = lane >> 3, j = lane & 7;
+                const uint32_t cb = (uint32_t)__shfl((int)row, ci, kWave);
+                if (ci < k && (uint32_t)j < (uint32_t)b_count[cb]) {
+                    bool tie;
+                    view_of(b_child[cb * 8 + j], ref, c, v, tie);
+                }
+            } else if (lane < k) {
+                v = iview(row);
             }
-            pos += rdl(sum8(v), 0);
+            pos += rdl(scan_incl(v), 63);
             child = (uint32_t)B;
             B = (int32_t)rfl((uint32_t)b_parent[B]);
-            leaf = false;
         }
         return pos;
     }
@@ -2289,7 +2329,7 @@ struct Engine {
             b_leaf[id] = (uint8_t)leaf;
             b_scour[id] = kScourUndef;
             b_parent[id] = (Idx)parent;
-            b_slen[id] = 0u;
+            if (!leaf) b_slen[si(id)] = 0u;
             b_count[id] = (uint8_t)(base + (lane < extra ? 1 : 0));
             b_child[parent * 8 + lane] = (Idx)id;
         }
@@ -2305,15 +2345,14 @@ struct Engine {
         if (in) {
             b_child[nb * 8 + p] = (Idx)c;
             if (leaf) {
-                s_blk[c] = (Idx)nb;
-                sl = settled_len(c);
+                s_blk[c] = (Idx)nb;  // (leaf blocks keep no length)
             } else {
                 b_parent[c] = (Idx)nb;
-                sl = b_slen[c];
+                sl = level == 1 ? leaf_block_settled(c) : (uint32_t)b_slen[si(c)];
             }
         }
         wsync();
-        if (in && sl) b_slen.add(nb, sl);
+        if (!leaf && in && sl) b_slen.add(si(nb), sl);
         b_count[parent] = (uint8_t)cc;
         splits++;  // structure changed under the overlay
         wsync();
@@ -2617,7 +2656,7 @@ struct Engine {
             return;
         }
         wsync();
-        for (int32_t i = lane; i < blk_top; i += kWave) b_slen[i] = 0u;
+        for (int32_t i = lane; i < (kSplitPools ? lds_top : blk_top); i += kWave) b_slen[i] = 0u;
         wsync();
         for (int32_t base = 0; base < slot_top; base += kWave) {
             const int32_t slot = base + lane;
@@ -3201,7 +3240,7 @@ struct Engine {
     MT_FI uint32_t view_length(int32_t ref, uint32_t c) {
         uint32_t sum = 0;
         if (ref >= min_seq) {
-            sum = b_slen[root];
+            sum = blk_settled((uint32_t)root, depth == 1);
             for (int32_t base = 0; base < nu; base += kWave) {
                 const int32_t j = base + lane;
                 uint32_t vlen = 0;
@@ -3228,6 +3267,10 @@ struct Engine {
     // resumed in a larger capacity class instead of failing mid-op.
     MT_FI bool low_headroom() const {
         const int32_t fs = cap.seg - slot_top + free_n;
+        if constexpr (kSplitPools) {
+            const int32_t fl = kLB - blk_top + n_bfree, fi = cap.iblk - lds_top + n_lfree;
+            return fs < 6 || fl < 16 || fi < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 24;
+        }
         const int32_t fb = cap.blk - blk_top + n_bfree;
         return fs < 6 || fb < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 24;
     }
@@ -3253,6 +3296,18 @@ struct Engine {
         for (int32_t i = lane; i < n; i += kWave) dst[i] = p[i] == 0xFFFFFFFFu ? (Idx)kNoBlk : (Idx)p[i];
         p += n;
     }
+    // Image block ids are dense and class independent: the first pool's ids [0, blk_top), then (split
+    // pools) the interior ids kLB + i as blk_top + i.  Both free lists keep their links (image ids).
+    MT_FI uint32_t img_id(uint32_t b) const {
+        if (b == kNoBlk) return 0xFFFFFFFFu;
+        if constexpr (kSplitPools) return b >= (uint32_t)kLB ? (uint32_t)blk_top + (b - (uint32_t)kLB) : b;
+        return b;
+    }
+    MT_FI uint32_t cls_id(uint32_t x, uint32_t nl) const {  // image id -> this class's id
+        if (x == 0xFFFFFFFFu) return kNoBlk;
+        if constexpr (kSplitPools) return x < nl ? x : (uint32_t)kLB + (x - nl);
+        return x;
+    }
     MT_FI void checkpoint(uint32_t *ck, int32_t ops_done) {
         resolve_splits();
         wsync();
@@ -3276,9 +3331,9 @@ struct Engine {
             ck[2] = (uint32_t)slot_top;
             ck[3] = (uint32_t)free_head;
             ck[4] = (uint32_t)free_n;
-            ck[5] = (uint32_t)blk_top;
+            ck[5] = (uint32_t)(blk_top + (kSplitPools ? lds_top : 0));  // image blocks
             ck[6] = (uint32_t)n_bfree;
-            ck[7] = (uint32_t)root;
+            ck[7] = img_id((uint32_t)root);
             ck[8] = (uint32_t)depth;
             ck[9] = (uint32_t)hn;
             ck[10] = (uint32_t)nu;
@@ -3295,11 +3350,14 @@ struct Engine {
             ck[21] = (uint32_t)max_heap;
             ck[22] = (uint32_t)max_u;
             ck[23] = (uint32_t)sbase;
-            ck[24] = (uint32_t)bfree_head;
+            ck[24] = bfree_head < 0 ? 0xFFFFFFFFu : img_id((uint32_t)bfree_head);
             ck[25] = (uint32_t)(int32_t)idmap_n;
             ck[26] = (uint32_t)(int32_t)rel_pend;
             ck[27] = (uint32_t)(int32_t)rel_p1;
             ck[28] = (uint32_t)(int32_t)rel_p2;
+            ck[29] = (uint32_t)blk_top;  // the first pool's image ids
+            ck[30] = kSplitPools ? (uint32_t)n_lfree : 0u;
+            ck[31] = kSplitPools && lfree_head >= 0 ? img_id((uint32_t)lfree_head) : 0xFFFFFFFFu;
         }
         uint32_t *p = ck + kCkHdr;
         dump(p, s_len, slot_top);
@@ -3314,12 +3372,21 @@ struct Engine {
         }
         p += 2 * nu;
         dump(p, u_cm, nu);
-        dump_blk(p, b_parent, blk_top);
-        dump(p, b_child, 8 * blk_top);  // one word per child entry: the image is index-width independent
-        for (int32_t i = lane; i < blk_top; i += kWave)
-            p[i] = (uint32_t)b_count[i] | ((uint32_t)b_leaf[i] << 8) | ((uint32_t)(uint8_t)b_scour[i] << 16);
-        p += blk_top;
-        dump(p, b_slen, blk_top);
+        // blocks in image order: parent, 8 child entries (interior rows as image ids; one word each, so
+        // the image is index-width independent), count | leaf | scour, settled length (0: leaf blocks)
+        const int32_t nimg = blk_top + (kSplitPools ? lds_top : 0);
+        for (int32_t i = lane; i < nimg; i += kWave) {
+            const uint32_t b = cls_id((uint32_t)i, (uint32_t)blk_top);
+            p[i] = img_id(b_parent[b]);
+            const uint32_t cnt = b_count[b], lf = b_leaf[b];
+            for (int32_t j = 0; j < 8; j++) {
+                const uint32_t x = b_child[b * 8 + j];
+                p[nimg + 8 * i + j] = (lf || (uint32_t)j >= cnt) ? x : img_id(x);
+            }
+            p[9 * nimg + i] = cnt | (lf << 8) | ((uint32_t)(uint8_t)b_scour[b] << 16);
+            p[10 * nimg + i] = (kSplitPools && lf) ? 0u : (uint32_t)b_slen[si(b)];
+        }
+        p += 11 * nimg;
         dump(p, (const uint32_t *)h_ent, 2 * (hn + 1));
     }
     // returns the number of ops the checkpoint had applied
@@ -3329,9 +3396,12 @@ struct Engine {
         slot_top = (int32_t)rfl(ck[2]);
         free_head = (int32_t)rfl(ck[3]);
         free_n = (int32_t)rfl(ck[4]);
-        blk_top = (int32_t)rfl(ck[5]);
+        const int32_t nimg = (int32_t)rfl(ck[5]);
+        const uint32_t nl = rfl(ck[29]);
+        blk_top = kSplitPools ? (int32_t)nl : nimg;
+        lds_top = kSplitPools ? nimg - (int32_t)nl : 0;
         n_bfree = (int32_t)rfl(ck[6]);
-        root = (int32_t)rfl(ck[7]);
+        root = (int32_t)cls_id(rfl(ck[7]), nl);
         depth = (int32_t)rfl(ck[8]);
         hn = (int32_t)rfl(ck[9]);
         nu = (int32_t)rfl(ck[10]);
@@ -3348,7 +3418,9 @@ struct Engine {
         max_heap = (int32_t)rfl(ck[21]);
         max_u = (int32_t)rfl(ck[22]);
         sbase = (int32_t)rfl(ck[23]);
-        bfree_head = (int32_t)rfl(ck[24]);
+        bfree_head = rfl(ck[24]) == 0xFFFFFFFFu ? -1 : (int32_t)cls_id(rfl(ck[24]), nl);
+        n_lfree = kSplitPools ? (int32_t)rfl(ck[30]) : 0;
+        lfree_head = kSplitPools && rfl(ck[31]) != 0xFFFFFFFFu ? (int32_t)cls_id(rfl(ck[31]), nl) : -1;
         idmap_n = (int32_t)rfl(ck[25]);
         rel_pend = (int32_t)rfl(ck[26]);
         rel_p1 = (int32_t)rfl(ck[27]);
@@ -3365,19 +3437,39 @@ struct Engine {
         p += 2 * nu;
         load(p, u_cm, nu);
         if constexpr (kGiant) {
-            restore_giant_blocks(p, blk_top);
-            p += 11 * (int64_t)rfl(ck[5]);
+            restore_giant_blocks(p, nimg, rfl(ck[31]), (int32_t)rfl(ck[30]));
+            p += 11 * (int64_t)nimg;
         } else {
-            load_blk(p, b_parent, blk_top);
-            load(p, b_child, 8 * blk_top);
-            for (int32_t i = lane; i < blk_top; i += kWave) {
-                const uint32_t v = p[i];
-                b_count[i] = (uint8_t)v;
-                b_leaf[i] = (uint8_t)(v >> 8);
-                b_scour[i] = (int8_t)(uint8_t)(v >> 16);
+            for (int32_t i = lane; i < nimg; i += kWave) {
+                const uint32_t b = cls_id((uint32_t)i, nl);
+                const uint32_t v = p[9 * nimg + i];
+                const uint32_t cnt = v & 0xFFu, lf = (v >> 8) & 0xFFu;
+                b_parent[b] = (Idx)cls_id(p[i], nl);
+                b_count[b] = (uint8_t)cnt;
+                b_leaf[b] = (uint8_t)lf;
+                b_scour[b] = (int8_t)(uint8_t)(v >> 16);
+                for (int32_t j = 0; j < 8; j++) {
+                    const uint32_t x = p[nimg + 8 * i + j];
+                    b_child[b * 8 + j] = (Idx)((lf || (uint32_t)j >= cnt) ? x : cls_id(x, nl));
+                }
+                if (!(kSplitPools && lf)) b_slen[si(b)] = p[10 * nimg + i];
             }
-            p += blk_top;
-            load(p, b_slen, blk_top);
+            p += 11 * (int64_t)nimg;
+            if constexpr (!kSplitPools) {  // one pool: the image's second free list joins the first
+                const int32_t n2 = (int32_t)rfl(ck[30]);
+                if (n2 > 0) {
+                    wsync();
+                    const int32_t h2 = (int32_t)cls_id(rfl(ck[31]), nl);
+                    if (n_bfree == 0) {
+                        bfree_head = h2;
+                    } else {
+                        int32_t t = bfree_head;
+                        for (int32_t k = 1; k < n_bfree; k++) t = (int32_t)rfl((uint32_t)b_parent[t]);
+                        b_parent[t] = (Idx)h2;
+                    }
+                    n_bfree += n2;
+                }
+            }
         }
         load(p, (uint32_t *)h_ent, 2 * (hn + 1));
         for (int32_t i = lane; i < kColdPerSlot * slot_top; i += kWave) cold[i] = cold_src[i];
@@ -3389,7 +3481,7 @@ struct Engine {
     // >= kGiantLdsLevel to LDS ids (while they last), the others to HBM ids from kGiantLdsBlocks —
     // and the image's free blocks are dropped.  Per image block, the HBM b_ep / b_acc entries of
     // ids kGiantLdsBlocks + i serve as temporaries (level, new id); clear_epochs() resets b_ep.
-    MT_FI void restore_giant_blocks(const uint32_t *img, int32_t n) {
+    MT_FI void restore_giant_blocks(const uint32_t *img, int32_t n, uint32_t free2_head, int32_t n_free2) {
         const uint32_t *ip = img;           // b_parent (0xFFFFFFFF: none; free blocks: the free list)
         const uint32_t *ic = img + n;       // b_child rows
         const uint32_t *ik = img + 9 * n;   // count | leaf << 8 | scour << 16
@@ -3399,9 +3491,14 @@ struct Engine {
         constexpr uint32_t kFree = 0xFFFFFFFFu;
         for (int32_t i = lane; i < n; i += kWave) tlev[i] = 0u;
         wsync();
-        {  // the image's free list (its links are b_parent)
+        {  // the image's free lists (their links are b_parent)
             int32_t t = bfree_head;
             for (int32_t k = 0; k < n_bfree && t >= 0 && t < n; k++) {
+                if (lane == 0) tlev[t] = kFree;
+                t = (int32_t)rfl(ip[t]);
+            }
+            t = free2_head == 0xFFFFFFFFu ? -1 : (int32_t)free2_head;
+            for (int32_t k = 0; k < n_free2 && t >= 0 && t < n; k++) {
                 if (lane == 0) tlev[t] = kFree;
                 t = (int32_t)rfl(ip[t]);
             }

@@ -417,8 +417,8 @@ def test_native_json_ingest_replays_like_the_packer():
 
 def test_config3_documents_at_full_size():
     """The north-star workload's documents at their own size: config-3 mix (55/35/10), 10k ops,
-    no seg_cap forcing, so documents run the natural capacity chain (class 416 -> 499 -> ... ->
-    1,469 -> 1,792) through checkpoint / resume.  Every digest equals the oracle's; every 8th
+    no seg_cap forcing, so documents run the natural capacity chain (class 480 -> 569 -> ... ->
+    1,679 -> 2,046) through checkpoint / resume.  Every digest equals the oracle's; every 8th
     document also text, property runs and SnapshotV1 (host and GPU serializers)."""
     n = 32
     p = O.gen_params(10000, pct_insert=55, pct_remove=35, seed=0xDEADBEEF)
