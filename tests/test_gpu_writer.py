@@ -387,6 +387,22 @@ def test_stack_context_document_trees():
                 assert dv.get_stack_context(pos, labels) == od.stack_context(pos, labels), (labels, pos)
 
 
+def test_stack_context_derived_kats_on_gpu():
+    """The hand-worked getStackContext cases (tests/test_oracle_ranges.py STACK_KATS, marked
+    derived) on a read-only GPU replica of each case's sequenced inserts."""
+    from test_oracle_ranges import STACK_KATS, stack_kat_messages
+
+    logs = [stack_kat_messages(k) for k in STACK_KATS]
+    with fa.ReplayBatch(len(logs)) as b:
+        b.ingest_messages(logs)
+        b.run()
+        for i, kat in enumerate(STACK_KATS):
+            dv = b.doc(i)
+            for pos, labels, want in kat["queries"]:
+                got = dv.get_stack_context(pos, labels)
+                assert got == want and list(got) == list(want), (kat["name"], pos, labels, got)
+
+
 class _StackView:
     def __init__(self, dv):
         self.dv = dv

@@ -136,3 +136,98 @@ def test_stack_context_quirks():
     first = d.stack_context(0, ["a"])  # the containing leaf is the first begin marker
     assert [it["props"]["markerId"] for it in first["a"]] == ["a0"]
     assert list(first) == ["a"]
+
+
+# Derived known-answer cases for getStackContext.  Nothing in the reference's tests pins these
+# values: they are worked by hand from the reference's rules and are marked "derived".
+#   applyRangeReference (mergeTree.ts:246-261): a NestBegin pushes; an end pops a NestBegin on top
+#     and is pushed otherwise (no label matching beyond the per-label stack).
+#   applyLeafRangeMarker (953-964): a leaf marker touches only the requested labels, in request
+#     order, creating a label's stack on first touch (it may end empty).
+#   applyStackDelta (229-244) via rangeShift (978-994): a preceding block applies its whole
+#     rangeStacks delta, every label, skipping labels whose delta stack is empty.
+#   split (2476-2489) at MaxNodesInBlock 8: appending segments one by one leaves segments 0..3 in
+#     the first leaf block for good once the 8th is inserted, so with >= 8 segments a query past
+#     segment 3 sees segments 0..3 only through that block's delta.
+# The output shape {label: [{pos, refType, props}, ...]} (stacks bottom to top, labels in the
+# order the search created them) is this repo's rendering of searchInfo.stacks, not the
+# reference's (a RangeStackMap of Stack<Marker>): INTEGRATION.md.
+def _mk(rt, labels, mid):
+    return {"marker": {"refType": rt}, "props": {"markerId": mid, "referenceRangeLabels": labels}}
+
+
+def _it(pos, rt, labels, mid):
+    return {"pos": pos, "refType": rt, "props": {"markerId": mid, "referenceRangeLabels": labels}}
+
+
+_E0, _AB, _EB = (NEST_END, ["a"], "e0"), (NEST_BEGIN, ["a", "b"], "ab"), (NEST_END, ["b"], "eb")
+_A0, _B0, _B0E, _C0E = (NEST_BEGIN, ["a"], "a0"), (NEST_BEGIN, ["b"], "b0"), (NEST_END, ["b"], "b0e"), (NEST_END, ["c"], "c0e")
+_AE = (NEST_END, ["a"], "ae")
+STACK_KATS = [
+    {   # one leaf block: every marker is a leaf the search visits, so only requested labels count
+        "name": "single_block",
+        "segs": [_mk(*_E0), _mk(*_AB), "xx", _mk(*_EB), "yy"],
+        "queries": [
+            (5, ["a", "b"], {"a": [_it(0, *_E0), _it(1, *_AB)], "b": []}),  # end on an empty stack is pushed; eb pops ab
+            (5, ["b"], {"b": []}),                                            # e0 has no "b": no "a" key
+            (0, ["a"], {"a": [_it(0, *_E0)]}),                                # the containing leaf applies too
+            (1, ["b", "a"], {"a": [_it(0, *_E0), _it(1, *_AB)], "b": [_it(1, *_AB)]}),  # keys in creation order
+            (2, ["a", "b"], {"a": [_it(0, *_E0), _it(1, *_AB)], "b": [_it(1, *_AB)]}),
+            (4, ["b"], {"b": []}),                                            # containing end pops the begin below
+            (6, [], {}),
+        ],
+    },
+    {   # markers in the first leaf block, queried from later blocks: the block delta carries every label
+        "name": "block_delta",
+        "segs": [_mk(*_A0), _mk(*_B0), _mk(*_B0E), _mk(*_C0E)] + ["t%02d" % i for i in range(20)],
+        "queries": [
+            (63, ["a"], {"a": [_it(0, *_A0)], "c": [_it(3, *_C0E)]}),  # "b" delta is empty: skipped
+            (4, [], {"a": [_it(0, *_A0)], "c": [_it(3, *_C0E)]}),
+            (3, ["a"], {"a": [_it(0, *_A0)]}),                          # same block: leaves, requested labels only
+            (3, ["b"], {"b": []}),
+            (3, ["c"], {"c": [_it(3, *_C0E)]}),
+        ],
+    },
+    {   # a begin in block 0 popped by the end in block 1's delta: the key stays with an empty stack
+        "name": "pop_across_blocks",
+        "segs": [_mk(*_A0), "t0", "t1", "t2", _mk(*_AE)] + ["u%02d" % i for i in range(16)],
+        "queries": [
+            (60, [], {"a": []}),
+            (4, ["a"], {"a": [_it(0, *_A0)]}),                          # in "t1": leaves of block 0
+            (7, ["a"], {"a": []}),                                      # on ae itself: block 0 delta, then ae pops
+            (8, ["b"], {"a": [_it(0, *_A0)]}),                          # ae is a leaf of this block, "a" not asked for
+            (20, ["b"], {"a": []}),                                     # past block 1: both block deltas
+        ],
+    },
+]
+
+
+def stack_kat_messages(kat, client="W"):
+    """The KAT's segments as one writer's sequenced inserts, appended in order; minimumSequenceNumber
+    stays 0 so no zamboni merges segments and the block shape is the append shape."""
+    msgs, pos = [], 0
+    for i, s in enumerate(kat["segs"]):
+        msgs.append({"clientId": client, "sequenceNumber": i + 1, "referenceSequenceNumber": i,
+                     "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 0, "pos1": pos, "seg": s}})
+        pos += 1 if isinstance(s, dict) else len(s)
+    return msgs
+
+
+@pytest.mark.parametrize("kat", STACK_KATS, ids=lambda k: k["name"])
+def test_stack_context_derived_kats(kat):
+    """derived (hand-worked, not reference fixtures): the writer's local view and a read-only
+    replica of its sequenced ops both give the worked stacks"""
+    import json
+
+    w = O.Doc()
+    w.start_collab("W")
+    obs = O.Doc()
+    obs.start_collab("readonly")
+    for m in stack_kat_messages(kat):
+        assert w.local_op(m["contents"]) == 0, w.error
+        assert obs.apply_msg(json.dumps(m)) == 0, obs.error
+    for d in (w, obs):
+        for pos, labels, want in kat["queries"]:
+            got = d.stack_context(pos, labels)
+            assert got == want, (kat["name"], pos, labels, got)
+            assert list(got) == list(want), (kat["name"], pos, labels)
