@@ -211,6 +211,17 @@ constexpr int64_t pend_words(int32_t cap) { return kPendEntries + 2ll * cap; }
 // annotate: a = flags, b / c = the reset op's prop records; remove: nothing more
 constexpr int kRegenOpWords = 8;
 
+// writer consensus (Client.annotateMarkerNotifyConsensus / updateConsensusProperty, client.ts:113-134,
+// 980-987), per document (u32 words), persistent across launches: [0] registered ids, [1] min-seq
+// listeners queued, [2] listeners fired, [3] id capacity, [4] listener capacity, [5..8) 0; from word
+// kConsHdr the pendingConsensus keys (raw value ids of marker ids), then per listener {raw id, seq,
+// registered, minSeq when it fired, seq of the message that fired it}.  The host sizes both parts from the log (one id per notify
+// record, one listener per consensus ack), so neither can overflow.
+constexpr int kConsHdr = 8;
+constexpr int kConsLis = 5;
+constexpr uint32_t kCombineConsensusAck = 4u;  // props_extend: updateConsensusProperty's re-combine
+constexpr int64_t cons_words(int64_t n_ids, int64_t n_lis) { return kConsHdr + n_ids + kConsLis * n_lis; }
+
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table
 constexpr int kCkHdr = 32;
 constexpr int64_t ck_words(int seg) { return 9ll * seg + 1024; }
@@ -389,6 +400,8 @@ struct ReplayParams {
     uint32_t *regen;              // regenerated ops (kRegenOpWords layout), per document
     const uint64_t *doc_regen_base;
     int32_t regen_cap;            // words per document
+    uint32_t *cons;               // consensus regions (cons_words layout), per document; null: none
+    const uint64_t *doc_cons_base;
     // batches whose annotates touch referenceTileLabels / referenceRangeLabels: per output record,
     // the prop set a marker's leaf block last rebuilt its tile / range maps from (blockUpdate,
     // mergeTree.ts:2748-2767; annotates do not run it, so those maps go stale), else null

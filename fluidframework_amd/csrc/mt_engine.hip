@@ -302,6 +302,12 @@ struct Engine {
     int32_t pend_cap_e, n_pend;
     uint32_t *regen;  // regenerated ops (mt_device.h kRegenOpWords), regen_cap words
     int32_t regen_cap;
+    // writer consensus: the document's region (mt_device.h kConsHdr; null: the batch has none), the
+    // seq of its oldest unfired min-seq listener (INT32_MAX: none), and the marker id a local notify
+    // RELPOS hands to the annotate after it
+    uint32_t *cons;
+    int32_t cons_next, ntf;
+    uint32_t ntf_raw;
     int32_t htop;
     uint2 *h_ent;
     // ---- global
@@ -1838,7 +1844,9 @@ struct Engine {
     // MT_OP_RELPOS: posFromRelativePos (mergeTree.ts:1942-1966) for the next record's pos1 / pos2
     // (client.ts:485-502).  An id with no marker gives -1 in the reference and a position below 0
     // is passed on; both, and keys the host flagged, end the document as MT_UNSUPPORTED.
-    MT_FI void op_relpos(const mt_op &op) {
+    // `local`: a writer's local op (getValidOpRange's local check follows): a position of -1 (no such
+    // marker) or below 0 reaches the check, which drops the op.
+    MT_FI void op_relpos(const mt_op &op, bool local = false) {
         ov_splits = -1;
         ensure_overlay(op.ref_seq, MT_OP_CLIENT(op));
         int32_t pend = 0;
@@ -1854,19 +1862,23 @@ struct Engine {
                 if (hm) slot = rdl(e.y, first_lane(hm));
                 found += __popcll(hm);
             }
-            if (key == 0u || key == kIdKeyUnsupported || found != 1u) {
+            if (key == kIdKeyUnsupported || found > 1u || (!local && (key == 0u || found != 1u))) {
                 set_fail(ST_UNSUPPORTED);
                 return;
             }
-            int64_t pos = slot == kIdUnlinked ? 0 : (int64_t)get_position(slot, op.ref_seq, MT_OP_CLIENT(op));
-            const int32_t off = (int32_t)(k ? op.payload_len : op.payload);
-            if (!(op.flags & (k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1))) {
-                pos += 1;  // marker.cachedLength
-                if (op.flags & (k ? MT_RELF_OFF2 : MT_RELF_OFF1)) pos += off;
-            } else if (op.flags & (k ? MT_RELF_OFF2 : MT_RELF_OFF1)) {
-                pos -= off;
+            int64_t pos = -1;
+            if (key != 0u && found == 1u) {
+                pos = slot == kIdUnlinked ? 0 : (int64_t)get_position(slot, op.ref_seq, MT_OP_CLIENT(op));
+                const int32_t off = (int32_t)(k ? op.payload_len : op.payload);
+                if (!(op.flags & (k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1))) {
+                    pos += 1;  // marker.cachedLength
+                    if (op.flags & (k ? MT_RELF_OFF2 : MT_RELF_OFF1)) pos += off;
+                } else if (op.flags & (k ? MT_RELF_OFF2 : MT_RELF_OFF1)) {
+                    pos -= off;
+                }
             }
-            if (pos < 0 || pos > 0x7FFFFFFF) {
+            if (local && pos < 0) pos = -1;
+            if (pos > 0x7FFFFFFF || (!local && pos < 0)) {
                 set_fail(ST_UNSUPPORTED);
                 return;
             }
@@ -1912,7 +1924,7 @@ struct Engine {
     // cannot reproduce it (incr of a string / object, consensus updating a shared object in place,
     // an undefined result): the document is MT_UNSUPPORTED.
     MT_FI bool combine_values(uint32_t ckind, const mt_prop *op, uint32_t nop, uint32_t n, uint32_t ok_k,
-                              uint32_t &ok_v) {
+                              uint32_t &ok_v, bool inplace = false) {
         // the result slot: value = an absent key's result, key = the NaN value for "incr"
         // (mt_host.cpp rc_resolve_combine)
         const mt_prop res = op[nop + 2];
@@ -1931,8 +1943,18 @@ struct Engine {
                 // concatenate "undefined" (not modelled on the device).  consensus of an object
                 // with seq === -1 would update a shared object in place.
                 bad = ckind == MT_COMBINE_INCR ? (!(f & kVNum) || res.key >= nv)
-                                               : (ckind == MT_COMBINE_CONSENSUS && (f & kVSeqM1));
+                                               : ((ckind == MT_COMBINE_CONSENSUS || ckind == kCombineConsensusAck) &&
+                                                  (f & kVSeqM1));
                 ok_v = ckind == MT_COMBINE_INCR ? res.key : ev;
+                // the { value: undefined, seq: -1 } this replica's local consensus made (the slot's
+                // key: mt_host.cpp rc_resolve_combine) is a marker's own object (markers never
+                // split): a sequenced consensus — updateConsensusProperty's re-combine at the ack,
+                // or a remote op while the local one is pending (`inplace`) — sets its seq in
+                // place, giving the value an absent key gets
+                if (ev == res.key && (ckind == kCombineConsensusAck || (ckind == MT_COMBINE_CONSENSUS && inplace))) {
+                    ok_v = res.value;
+                    bad = res.value != MT_VALUE_NULL && res.value >= nv;
+                }
             } else {
                 ok_v = res.value;
                 bad = res.value != MT_VALUE_NULL && res.value >= nv;
@@ -1951,7 +1973,7 @@ struct Engine {
     // Writer: pk / npk (lane j < npk: key j) are the keys of pending local annotates on the segment,
     // which a remote op leaves alone (shouldModifyKey, segmentPropertiesManager.ts:56-63).
     MT_FI uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout,
-                                uint32_t ckind = 0u, uint32_t pk = 0u, uint32_t npk = 0u) {
+                                uint32_t ckind = 0u, uint32_t pk = 0u, uint32_t npk = 0u, bool inplace = false) {
         uint32_t *keys = scratch;
         uint32_t *vals = scratch + 64;
         uint32_t n = old ? pool[old] : 0u;
@@ -1975,7 +1997,7 @@ struct Engine {
             ok_v = pr.value;
         }
         wsync();
-        if (ckind != MT_COMBINE_NONE && combine_values(ckind, op, nop, n, ok_k, ok_v)) {
+        if (ckind != MT_COMBINE_NONE && combine_values(ckind, op, nop, n, ok_k, ok_v, inplace)) {
             set_fail(ST_UNSUPPORTED);
             return 0;
         }
@@ -2472,6 +2494,9 @@ struct Engine {
         if (msn > min_seq) {
             min_seq = msn;
             zamboni();
+            if constexpr (kW) {
+                if (msn >= cons_next) consensus_fire();
+            }
         }
     }
 
@@ -2924,7 +2949,7 @@ struct Engine {
                         const uint32_t ck = MT_OPF_COMBINE(op.flags);
                         nid = prw ? old
                                   : props_extend(old, props_in + op.payload, op.payload_len, rewrite, nh, ck, pk,
-                                                 ck ? 0u : npk);
+                                                 ck ? 0u : npk, (rfl((uint32_t)s_meta[sl]) & kFMarker) != 0u);
                         if (status) return;
                     } else if (mb) {
                         int m = first_lane(mb);
@@ -2985,9 +3010,17 @@ struct Engine {
             op_regenerate(op);
             return;
         }
-        if (op.type == MT_OP_RELPOS || rel_pend ||
-            (op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) != MT_COMBINE_NONE)) {
-            set_fail(ST_UNSUPPORTED);  // relative positions / combiningOps in local ops: not modelled
+        if (op.type == MT_OP_RELPOS) {  // posFromRelativePos in the local view (client.ts:485-502)
+            ntf = (op.flags & MT_RELF_NOTIFY) ? 1 : 0;
+            ntf_raw = op.payload;
+            op.ref_seq = cur_seq;
+            op_relpos(op, true);
+            return;
+        }
+        const bool notify = ntf != 0;
+        ntf = 0;
+        if (notify && !(op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) == MT_COMBINE_CONSENSUS)) {
+            set_fail(ST_BAD_INPUT);
             return;
         }
         if (op.type != MT_OP_INSERT && op.type != MT_OP_REMOVE && op.type != MT_OP_ANNOTATE) {
@@ -3004,6 +3037,110 @@ struct Engine {
         if (lane == 0) pend[4] = pend_word(4) + 1u;  // ++collabWindow.localSeq (mergeTree.ts:1976, 2571, 2613)
         if (op.type == MT_OP_INSERT) insert_one<false>(op, 0u, (uint32_t)st, cur_seq);
         else op_range(op);
+        // annotateMarkerNotifyConsensus: pendingConsensus.set(marker.getId(), ...) once the
+        // annotate applied (client.ts:124-130)
+        if (notify && !status) consensus_register(ntf_raw);
+    }
+
+    // pendingConsensus.set(id, ...): the registered ids, each once (a Map key)
+    MT_FI void consensus_register(uint32_t raw) {
+        if (!cons) {
+            set_fail(ST_BAD_INPUT);
+            return;
+        }
+        const uint32_t nreg = rfl(cons[0]), capr = rfl(cons[3]);
+        bool have = false;
+        for (uint32_t b0 = 0; b0 < nreg; b0 += kWave) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            have |= ballot(j < nreg && cons[kConsHdr + j] == raw) != 0;
+        }
+        if (have) return;
+        if (nreg >= capr) {
+            set_fail(ST_BAD_INPUT);
+            return;
+        }
+        if (lane == 0) {
+            cons[kConsHdr + nreg] = raw;
+            cons[0] = nreg + 1u;
+        }
+    }
+
+    // Client.updateConsensusProperty (client.ts:980-987) after the ack of the replica's consensus
+    // annotate: pendingConsensus.get(op.relativePos1.id) (op.pos1: its raw value id) — when
+    // registered, the marker (idToSegment[id]: op.pos2) re-combines the op's keys with the sequenced
+    // seq and no collab window (segmentPropertiesManager.ts:35-111); either way a min-seq listener at
+    // seq is queued (mergeTree.ts:1701-1707), whose callback an unregistered id lacks.
+    MT_FI void consensus_ack(const mt_op &op) {
+        if (!cons) {
+            set_fail(ST_BAD_INPUT);
+            return;
+        }
+        const uint32_t raw = (uint32_t)op.pos1;
+        const uint32_t nreg = rfl(cons[0]), nlis = rfl(cons[1]), capr = rfl(cons[3]), capl = rfl(cons[4]);
+        bool reg = false;
+        for (uint32_t b0 = 0; raw && b0 < nreg; b0 += kWave) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            reg |= ballot(j < nreg && cons[kConsHdr + j] == raw) != 0;
+        }
+        if (reg) {
+            const uint32_t key = (uint32_t)op.pos2;
+            const int32_t n = idmap_n;
+            uint32_t found = 0, slot = kIdUnlinked;
+            for (int32_t j0 = 0; j0 < n; j0 += kWave) {
+                const int32_t j = j0 + lane;
+                const uint2 e = j < n ? idmap[j] : make_uint2(0u, 0u);
+                const uint64_t hm = ballot(j < n && e.x == key);
+                if (hm) slot = rdl(e.y, first_lane(hm));
+                found += __popcll(hm);
+            }
+            if (key == 0u || key == kIdKeyUnsupported || found != 1u) {
+                set_fail(ST_UNSUPPORTED);
+                return;
+            }
+            if (slot != kIdUnlinked) {
+                pool_reserve(2u + 2u * (64u + op.payload_len));
+                if (status) return;
+                const uint32_t old = rfl(cold[2 * slot].x);
+                uint32_t nh;
+                const uint32_t nid = props_extend(old, props_in + op.payload, op.payload_len, false, nh,
+                                                  kCombineConsensusAck);
+                if (status) return;
+                if (lane == 0) cold[2 * slot].x = nid;
+                if (nid) s_meta[slot] = (Meta)(s_meta[slot] | kFHasProps);
+                wsync();
+            }
+        }
+        if (nlis >= capl) {
+            set_fail(ST_BAD_INPUT);
+            return;
+        }
+        uint32_t *L = cons + kConsHdr + capr + kConsLis * nlis;
+        if (lane < kConsLis) L[lane] = lane == 0 ? raw : lane == 1 ? (uint32_t)op.seq : lane == 2 ? (uint32_t)reg : 0u;
+        if (lane == 0) cons[1] = nlis + 1u;
+        if (cons_next == INT32_MAX) cons_next = op.seq;
+    }
+
+    // notifyMinSeqListeners (mergeTree.ts:1709-1716) for the consensus listeners: those at seq <=
+    // minSeq fire in seq order (the host orders equal seqs as the reference's heap does); a
+    // listener without a registered id dereferences an undefined consensusInfo (a TypeError)
+    MT_FI void consensus_fire() {
+        const uint32_t nlis = rfl(cons[1]), capr = rfl(cons[3]);
+        uint32_t head = rfl(cons[2]);
+        uint32_t *L0 = cons + kConsHdr + capr;
+        for (; head < nlis; head++) {
+            const uint32_t s = rfl(L0[kConsLis * head + 1]);
+            if ((int32_t)s > min_seq) break;
+            if (!rfl(L0[kConsLis * head + 2])) {
+                set_fail(ST_UNSUPPORTED);
+                return;
+            }
+            if (lane == 0) {
+                L0[kConsLis * head + 3] = (uint32_t)min_seq;
+                L0[kConsLis * head + 4] = (uint32_t)cur_seq;
+            }
+        }
+        if (lane == 0) cons[2] = head;
+        cons_next = head < nlis ? (int32_t)rfl(L0[kConsLis * head + 1]) : INT32_MAX;
     }
 
     // Client.regeneratePendingOp(resetOp, oldest pending group) -> resetPendingDeltaToOps
@@ -3201,11 +3338,10 @@ struct Engine {
             if (MT_OP_CLIENT(op) == 0 && op.type != MT_OP_NOOP) {
                 // the replica's own sequenced message acks its oldest pending group (client.ts:
                 // 810-812; a GROUP acks one group per member); positions are not read
-                if (op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) == MT_COMBINE_CONSENSUS) {
-                    set_fail(ST_UNSUPPORTED);  // updateConsensusProperty (client.ts:596-600)
-                    return;
-                }
                 if (op.type != MT_OP_RELPOS) op_ack(op);
+                // updateConsensusProperty after the ack (client.ts:596-600)
+                if (op.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op.flags) == MT_COMBINE_CONSENSUS && !status)
+                    consensus_ack(op);
                 resolve_splits();
                 if (status) return;
                 if (!(op.flags & MT_OPF_GROUP_CONT)) update_seq_numbers(op.msn, op.seq);
@@ -3695,6 +3831,10 @@ MT_FI void engine_setup(Engine<SEG, kW> &E, const ReplayParams &P, int64_t w, in
         E.regen_cap = P.regen_cap;
         E.n_pend = 0;
         E.cur_g = -1;
+        E.cons = P.cons ? P.cons + P.doc_cons_base[d] : nullptr;
+        E.cons_next = INT32_MAX;
+        E.ntf = 0;
+        E.ntf_raw = 0;
     }
     E.init();
 }
@@ -3772,8 +3912,20 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
         uint32_t *rg = P.regen + P.doc_regen_base[d];
         rg[0] = 2u;
         rg[1] = 0u;
+        if (P.cons) {
+            uint32_t *cs = P.cons + P.doc_cons_base[d];
+            cs[0] = 0u;
+            cs[1] = 0u;
+            cs[2] = 0u;
+        }
     }
-    if constexpr (kW) E.n_pend = resumed ? (int32_t)E.pend_word(0) : 0;
+    if constexpr (kW) {
+        E.n_pend = resumed ? (int32_t)E.pend_word(0) : 0;
+        if (resumed && E.cons) {  // the oldest unfired listener of a resumed document
+            const uint32_t nl = rfl(E.cons[1]), hd = rfl(E.cons[2]);
+            E.cons_next = hd < nl ? (int32_t)rfl(E.cons[kConsHdr + rfl(E.cons[3]) + kConsLis * hd + 1]) : INT32_MAX;
+        }
+    }
     // ops stream through registers 64 at a time (coalesced 2 KiB loads), broadcast by readlane
     mt_op cur = load_op_lane(ops, b0 + done + E.lane, b1);
     for (int64_t base = b0 + done; base < b1 && E.status == ST_OK; base += kWave) {

@@ -306,6 +306,9 @@ struct mt_batch {
     int32_t regen_cap = 0;               // words per document of regenerated-op output
     uint32_t *d_regen = nullptr;
     uint64_t *d_regen_base = nullptr;
+    uint32_t *d_cons = nullptr;          // writer consensus regions (mt_device.h kConsHdr); null: none
+    uint64_t *d_cons_base = nullptr;
+    std::vector<uint64_t> h_cons_base;
     std::vector<mt_prop> h_props_all;    // the ingested prop records (regenerated annotates' props)
     std::vector<uint64_t> h_regen_base;
     uint32_t *d_pend = nullptr;
@@ -422,6 +425,11 @@ static void free_log(mt_batch *b) {
     (void)hipFree(b->d_regen_base);
     b->d_regen = nullptr;
     b->d_regen_base = nullptr;
+    (void)hipFree(b->d_cons);
+    (void)hipFree(b->d_cons_base);
+    b->d_cons = nullptr;
+    b->d_cons_base = nullptr;
+    b->h_cons_base.clear();
     b->writer = false;
     b->d_ops = nullptr;
     b->d_off = nullptr;
@@ -662,6 +670,12 @@ static int host_value_rel(const mt_batch *b, uint32_t va, uint32_t vb) {
 
 static uint32_t align16u(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
 
+// the replica's own sequenced consensus annotate (mt_oplog.h: updateConsensusProperty's inputs)
+static bool is_consensus_ack(const mt_op &o) {
+    return o.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(o.flags) == MT_COMBINE_CONSENSUS && MT_OP_CLIENT(o) == 0 &&
+           o.seq != mt::kUnassignedSeq;
+}
+
 // Marker ids and relative positions (idToSegment, posFromRelativePos: mergeTree.ts:1185,
 // 1942-1966).  Ids are object keys, so both sides are compared as String(value): every marker
 // insert / load record whose props give a truthy markerId gets that key's id (>= 1) in
@@ -715,6 +729,10 @@ static void resolve_marker_ids(mt_batch *b, std::vector<mt_op> &h_ops, const std
         }
         for (int64_t i = off[d]; i < off[d + 1]; i++) {
             mt_op &o = h_ops[(size_t)i];
+            if (is_consensus_ack(o)) {  // pos1: relativePos1.id's raw value id; pos2: its marker-id key
+                o.pos2 = (int32_t)(annot_mk ? mt::kIdKeyUnsupported : key_of((uint32_t)o.pos1));
+                continue;
+            }
             if (o.type != MT_OP_RELPOS) continue;
             o.pos1 = (int32_t)(annot_mk ? mt::kIdKeyUnsupported : key_of((uint32_t)o.pos1));
             o.pos2 = (int32_t)(annot_mk ? mt::kIdKeyUnsupported : key_of((uint32_t)o.pos2));
@@ -788,8 +806,11 @@ static void rc_resolve_combine(mt_batch *b, const mt_op *ops, int64_t N, const m
                 case mt::kCombineMin: u = x[1].value; break;
                 case mt::kCombineNaN: u = nan(); break;
                 case mt::kCombineConsensus: {
+                    // a local op's { value: undefined, seq: -1 } is updated in place by a later
+                    // consensus (kValSeqM1)
                     auto it = cons_ids.find(out);
-                    if (it == cons_ids.end()) it = cons_ids.emplace(out, append(out, mt::kValNever)).first;
+                    if (it == cons_ids.end())
+                        it = cons_ids.emplace(out, append(out, mt::kValNever | (o.seq == mt::kUnassignedSeq ? mt::kValSeqM1 : 0))).first;
                     u = it->second;
                     break;
                 }
@@ -797,6 +818,17 @@ static void rc_resolve_combine(mt_batch *b, const mt_op *ops, int64_t N, const m
                 default: break;
             }
             x[2].value = u;
+            // a sequenced consensus (the ack of the replica's own one: updateConsensusProperty, or a
+            // remote one): the slot's key names the { seq: -1 } object a local consensus made,
+            // which it updates in place on a marker
+            if (kind == MT_COMBINE_CONSENSUS && o.seq != mt::kUnassignedSeq) {
+                std::string lo;
+                if (mt::combine_absent((int)kind, def, mn, mt::kUnassignedSeq, lo) == mt::kCombineConsensus) {
+                    auto it = cons_ids.find(lo);
+                    if (it == cons_ids.end()) it = cons_ids.emplace(lo, append(lo, mt::kValNever | mt::kValSeqM1)).first;
+                    x[2].key = it->second;
+                }
+            }
         }
     }
     // the value tables are rebuilt (classes, flags) and uploaded again
@@ -908,6 +940,35 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
                 writer = true;
                 break;
             }
+    // writer consensus regions (mt_device.h kConsHdr): one id per notify RELPOS, one listener per ack
+    // of a consensus annotate
+    std::vector<uint64_t> cons_base((size_t)D + 1, 0);
+    std::vector<uint32_t> cons_img;
+    if (writer) {
+        uint64_t ct = 0;
+        for (int64_t d = 0; d < D; d++) {
+            cons_base[(size_t)d] = ct;
+            uint64_t ni = 0, nl = 0;
+            for (int64_t i = h_off[d]; i < h_off[d + 1]; i++) {
+                const mt_op &o = ops[i];
+                if (o.type == MT_OP_RELPOS && o.seq == mt::kUnassignedSeq && (o.flags & MT_RELF_NOTIFY)) {
+                    if (o.payload == 0 || o.payload >= b->n_user_values) return MT_ERR_ARG;
+                    ni++;
+                }
+                if (is_consensus_ack(o)) {
+                    if ((uint32_t)o.pos1 >= b->n_user_values) return MT_ERR_ARG;
+                    nl++;
+                }
+            }
+            if (ni + nl == 0) continue;
+            if (ni > 0x7FFFFFFF || nl > 0x7FFFFFFF) return MT_ERR_ARG;
+            cons_img.resize((size_t)(ct + (uint64_t)mt::cons_words((int64_t)ni, (int64_t)nl)), 0u);
+            cons_img[(size_t)ct + 3] = (uint32_t)ni;
+            cons_img[(size_t)ct + 4] = (uint32_t)nl;
+            ct += (uint64_t)mt::cons_words((int64_t)ni, (int64_t)nl);
+        }
+        cons_base[(size_t)D] = ct;
+    }
     // combiningOps: the value each one gives a key the segment does not have yet
     std::vector<mt_prop> h_props;
     rc_resolve_combine(b, ops, N, props, n_props, h_props);
@@ -1007,6 +1068,13 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         // per-document caps differ (2 words without REGENERATE records): the device checks
         // regen_cap only after a REGENERATE record, which only the large regions see
         b->h_regen_base = std::move(rbase);
+        if (!cons_img.empty()) {
+            HIPCHK(dalloc(&b->d_cons, cons_img.size()));
+            HIPCHK(hipMemcpy(b->d_cons, cons_img.data(), 4 * cons_img.size(), hipMemcpyHostToDevice));
+            HIPCHK(dalloc(&b->d_cons_base, (size_t)D + 1));
+            HIPCHK(hipMemcpy(b->d_cons_base, cons_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+            b->h_cons_base = std::move(cons_base);
+        }
         b->writer = true;
     }
     HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));
@@ -1380,6 +1448,8 @@ static mt::ReplayParams base_params(mt_batch *b) {
     P.regen = b->d_regen;
     P.doc_regen_base = b->d_regen_base;
     P.regen_cap = b->regen_cap;
+    P.cons = b->d_cons;
+    P.doc_cons_base = b->d_cons_base;
     return P;
 }
 
@@ -2535,6 +2605,73 @@ MT_API int mt_doc_regenerated_ops(mt_batch *b, int64_t doc, char *buf, int64_t c
                     o += "],\"type\":3}";
                 }
                 msg_ops.clear();
+            }
+        }
+    }
+    o.push_back(']');
+    return out_str(o, buf, cap, len);
+}
+
+// The consensus callbacks a writer replica's replay made, in call order: each
+// annotateMarkerNotifyConsensus whose ack registered a min-seq listener (client.ts:980-987) calls
+// consensusInfo.callback(marker) when minSeq reaches the ack's seq (notifyMinSeqListeners,
+// mergeTree.ts:1709-1716).  The device queues the listeners in seq order; equal seqs (one GROUP
+// message) pop in the order of the reference's binary heap (collections.ts:213-265), which is
+// replayed here from the registration and firing times.
+MT_API int mt_doc_consensus_events(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len) {
+    if (!b) return MT_ERR_ARG;
+    int rc = load_doc(b, doc);
+    if (rc) return rc;
+    std::string o = "[";
+    if (b->d_cons && !b->h_cons_base.empty()) {
+        const uint64_t a = b->h_cons_base[(size_t)doc], e = b->h_cons_base[(size_t)doc + 1];
+        std::vector<uint32_t> w((size_t)(e - a));
+        if (!w.empty()) HIPCHK(hipMemcpy(w.data(), b->d_cons + a, 4 * w.size(), hipMemcpyDeviceToHost));
+        if (w.size() >= (size_t)mt::kConsHdr) {
+            const uint32_t nl = std::min(w[1], w[4]), fired = std::min(w[2], nl);
+            const uint32_t *L = w.data() + mt::kConsHdr + w[3];
+            struct Lis {
+                uint32_t i;
+                int64_t s;
+            };
+            // timeline: registration at the ack's message, firing after that message's ack(s)
+            std::vector<std::pair<int64_t, int64_t>> ev;  // (time, index): time = 2 seq (+1: firing)
+            for (uint32_t i = 0; i < nl; i++) ev.push_back({2 * (int64_t)L[mt::kConsLis * i + 1], i});
+            for (uint32_t i = 0; i < fired; i++) ev.push_back({2 * (int64_t)L[mt::kConsLis * i + 4] + 1, -1 - (int64_t)i});
+            std::stable_sort(ev.begin(), ev.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+            std::vector<Lis> H(1, Lis{0, INT64_MIN});  // L[0]: comp.min
+            auto cmp = [&](size_t x, size_t y) { return H[x].s - H[y].s; };
+            std::vector<uint32_t> order;
+            int64_t last_fire = -1;
+            for (const auto &t : ev) {
+                if (t.second >= 0) {  // Heap.add: push + fixup
+                    H.push_back(Lis{(uint32_t)t.second, (int64_t)L[mt::kConsLis * t.second + 1]});
+                    for (size_t k = H.size() - 1; k > 1 && cmp(k >> 1, k) > 0; k >>= 1) std::swap(H[k >> 1], H[k]);
+                    continue;
+                }
+                if (t.first == last_fire) continue;  // one notifyMinSeqListeners per message
+                last_fire = t.first;
+                const int64_t msn = (int64_t)L[mt::kConsLis * (uint32_t)(-1 - t.second) + 3];
+                while (H.size() > 1 && H[1].s <= msn) {  // Heap.get: last to the root + fixdown
+                    order.push_back(H[1].i);
+                    H[1] = H.back();
+                    H.pop_back();
+                    const size_t n = H.size() - 1;
+                    for (size_t k = 1; (k << 1) <= n;) {
+                        size_t j = k << 1;
+                        if (j < n && cmp(j, j + 1) > 0) j++;
+                        if (cmp(k, j) <= 0) break;
+                        std::swap(H[k], H[j]);
+                        k = j;
+                    }
+                }
+            }
+            for (size_t q = 0; q < order.size(); q++) {
+                const uint32_t *r = L + mt::kConsLis * order[q];
+                if (q) o.push_back(',');
+                o += "{\"markerId\":";
+                o += r[0] < b->values.size() ? b->values[r[0]] : std::string("null");
+                o += ",\"seq\":" + std::to_string(r[1]) + ",\"minSeq\":" + std::to_string(r[3]) + "}";
             }
         }
     }

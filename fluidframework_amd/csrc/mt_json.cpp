@@ -594,6 +594,29 @@ struct Packer1 {
         return true;
     }
 
+    // the op Client.annotateMarkerNotifyConsensus makes (createAnnotateMarkerOp, opBuilder.ts:25-39,
+    // with combiningOp {name: "consensus"}): relativePos1 {id, before: true}, relativePos2 {id}; raw =
+    // the value id of the marker id it registers (client.ts:124-130)
+    bool notify_shape(int32_t op, uint32_t &raw) {
+        if (D.nodes[op].type != J_OBJ) return false;
+        const int32_t t = D.member(op, "type"), cop = D.member(op, "combiningOp");
+        if (t < 0 || D.nodes[t].type != J_NUM || D.nodes[t].num != 2) return false;
+        if (D.member(op, "pos1") >= 0 || D.member(op, "pos2") >= 0) return false;
+        if (cop < 0 || D.nodes[cop].type != J_OBJ) return false;
+        const int32_t nm = D.member(cop, "name");
+        if (nm < 0 || D.nodes[nm].type != J_STR || D.str_of(nm) != u"consensus") return false;
+        if (D.member(cop, "defaultValue") >= 0 || D.member(cop, "minValue") >= 0) return false;
+        const int32_t r1 = D.member(op, "relativePos1"), r2 = D.member(op, "relativePos2");
+        if (r1 < 0 || r2 < 0 || D.nodes[r1].type != J_OBJ || D.nodes[r2].type != J_OBJ) return false;
+        const int32_t i1 = D.member(r1, "id"), i2 = D.member(r2, "id");
+        const int32_t b1 = D.member(r1, "before"), b2 = D.member(r2, "before");
+        if (i1 < 0 || i2 < 0 || !truthy(D.nodes[i1]) || D.nodes[i1].type == J_OBJ || D.nodes[i1].type == J_ARR) return false;
+        if (b1 < 0 || !truthy(D.nodes[b1]) || (b2 >= 0 && truthy(D.nodes[b2]))) return false;
+        if (D.member(r1, "offset") >= 0 || D.member(r2, "offset") >= 0) return false;
+        raw = value(i1);
+        return value(i2) == raw;
+    }
+
     bool pack_op(int32_t op, const mt_op &base, mt_op &r) {
         r = base;
         if (D.nodes[op].type != J_OBJ) return fail(MT_UNSUPPORTED, "op must be an object");
@@ -891,19 +914,40 @@ struct Packer1 {
             std::vector<int32_t> members;
             const int32_t contents = D.member(m, "contents");
             if (contents >= 0) flatten(contents, members);
+            // {"notifyConsensus": true} on a local message: the op came from
+            // Client.annotateMarkerNotifyConsensus (a repo-defined field of the writer stream)
+            const int32_t nt = D.member(m, "notifyConsensus");
+            const bool notify = local && nt >= 0 && truthy(D.nodes[nt]);
+            uint32_t notify_raw = 0;
+            if (notify && !(members.size() == 1 && notify_shape(members[0], notify_raw)))
+                return fail(MT_UNSUPPORTED, "notifyConsensus on an op annotateMarkerNotifyConsensus does not make");
             for (size_t j = 0; j < members.size(); j++) {
                 mt_op r{};
                 if (!relpos(members[j], base, r)) return false;
                 if (r.type == MT_OP_RELPOS) {
-                    if (local) return fail(MT_UNSUPPORTED, "relative positions in a local op");
+                    if (notify) {
+                        r.flags |= MT_RELF_NOTIFY;
+                        r.payload = notify_raw;
+                    }
                     if (!ack) L.ops.push_back(r);  // an ack reads no positions
+                }
+                if (local && D.nodes[members[j]].type == J_OBJ) {
+                    // getValidOpRange validates an insert's end when one is given (client.ts:520-524)
+                    const int32_t t = D.member(members[j], "type"), rp2 = D.member(members[j], "relativePos2");
+                    if (t >= 0 && D.nodes[t].type == J_NUM && D.nodes[t].num == 0 &&
+                        (D.member(members[j], "pos2") >= 0 || (rp2 >= 0 && truthy(D.nodes[rp2]))))
+                        return fail(MT_UNSUPPORTED, "a local insert with an end position");
                 }
                 r = mt_op{};
                 if (!pack_op(members[j], base, r)) return false;
-                if (r.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(r.flags) != MT_COMBINE_NONE) {
-                    if (local) return fail(MT_UNSUPPORTED, "local combiningOp other than rewrite");
-                    if (ack && MT_OPF_COMBINE(r.flags) == MT_COMBINE_CONSENSUS)
-                        return fail(MT_UNSUPPORTED, "ack of a consensus annotate (updateConsensusProperty)");
+                if (ack && r.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(r.flags) == MT_COMBINE_CONSENSUS) {
+                    // updateConsensusProperty reads op.relativePos1.id (client.ts:981): a missing
+                    // relativePos1 throws; an id a Map lookup cannot match (none, an object) is 0
+                    const int32_t r1 = D.member(members[j], "relativePos1");
+                    if (r1 < 0 || D.nodes[r1].type == J_NULL)
+                        return fail(MT_UNSUPPORTED, "ack of a consensus annotate without relativePos1 (a TypeError)");
+                    const int32_t i1 = D.nodes[r1].type == J_OBJ ? D.member(r1, "id") : -1;
+                    r.pos1 = i1 >= 0 && D.nodes[i1].type != J_OBJ && D.nodes[i1].type != J_ARR ? (int32_t)value(i1) : 0;
                 }
                 if (j + 1 < members.size()) r.flags |= MT_OPF_GROUP_CONT;
                 L.ops.push_back(r);
@@ -1057,9 +1101,14 @@ MT_API int mt_pack_json(mt_packed **out, int64_t n_docs, const char *const *doc_
                 if (o.flags & MT_OPF_HAS_PROPS) o.pos2 += (int32_t)pbase;
             } else if (o.type == MT_OP_ANNOTATE || (o.type == MT_OP_REGENERATE && o.ref_seq == MT_OP_ANNOTATE)) {
                 o.payload += pbase;
+                // the replica's consensus ack: pos1 = relativePos1.id's value id (mt_oplog.h)
+                if (o.type == MT_OP_ANNOTATE && MT_OPF_COMBINE(o.flags) == MT_COMBINE_CONSENSUS &&
+                    MT_OP_CLIENT(o) == 0 && o.seq != -1)
+                    o.pos1 = (int32_t)vmap[(uint32_t)o.pos1];
             } else if (o.type == MT_OP_RELPOS) {  // relativePosN.id value ids
                 o.pos1 = (int32_t)vmap[(uint32_t)o.pos1];
                 o.pos2 = (int32_t)vmap[(uint32_t)o.pos2];
+                if (o.flags & MT_RELF_NOTIFY) o.payload = vmap[o.payload];
             }
             P->ops.push_back(o);
         }

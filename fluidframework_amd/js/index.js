@@ -31,6 +31,7 @@ function native() {
 const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_REGENERATE = 7, OP_NOOP = 15;
 const OPF_GROUP_CONT = 1, OPF_MARKER = 2, OPF_HAS_PROPS = 4, OPF_REWRITE = 8;
 const OP_RELPOS = 6, RELF_POS1 = 0x10, RELF_POS2 = 0x20, RELF_BEFORE1 = 0x40, RELF_BEFORE2 = 0x80, RELF_OFF1 = 0x100, RELF_OFF2 = 0x200;
+const RELF_NOTIFY = 0x2;  // a local RELPOS of Client.annotateMarkerNotifyConsensus (include/mt_oplog.h)
 const COMBINE_INCR = 1, COMBINE_CONSENSUS = 2, COMBINE_OTHER = 3, KEY_COMBINE = 0xFFFFFFFF, VALUE_UNDEFINED = 0xFFFFFFFF;
 const MAX_INSERT_PROPS = 127;  // include/mt_oplog.h MT_OPF_MAX_INSERT_PROPS (flags bits 4-10)
 const MAX_CLIENTS = 0x7FFE;      // short ids 0..32765 (MT_MAX_CLIENTS; 0x7FFE / 0x7FFF are sentinels)
@@ -81,6 +82,18 @@ class Packer {
         const off = this.props.length / 2;
         for (const k of Object.keys(props)) this.props.push(this.key(k), this.value(props[k]));
         return [off, this.props.length / 2 - off];
+    }
+    // the marker id a Client.annotateMarkerNotifyConsensus op registers (client.ts:113-134): the op
+    // createAnnotateMarkerOp makes (opBuilder.ts:25-39) with combiningOp {name: "consensus"}
+    notifyId(members) {
+        const op = members.length === 1 ? members[0] : null;
+        const r1 = op && op.relativePos1, r2 = op && op.relativePos2, cop = op && op.combiningOp;
+        const ok = op && op.type === OP_ANNOTATE && op.pos1 === undefined && op.pos2 === undefined &&
+            cop && typeof cop === 'object' && Object.keys(cop).length === 1 && cop.name === 'consensus' &&
+            r1 && r2 && typeof r1 === 'object' && typeof r2 === 'object' && r1.offset === undefined &&
+            r2.offset === undefined && r1.id && typeof r1.id !== 'object' && r2.id === r1.id && r1.before && !r2.before;
+        if (!ok) throw new UnsupportedOp('notifyConsensus on an op annotateMarkerNotifyConsensus does not make');
+        return this.value(r1.id);
     }
     static flatten(op) {
         if (op.type === 3) return (op.ops || []).reduce((a, m) => a.concat(Packer.flatten(m)), []);
@@ -207,15 +220,30 @@ class Packer {
                 continue;
             }
             const members = Packer.flatten(msg.contents);
+            // {notifyConsensus: true} on a local message: the op came from
+            // Client.annotateMarkerNotifyConsensus (a repo-defined field of the writer stream)
+            const notify = local && !!msg.notifyConsensus;
+            const notifyRaw = notify ? this.notifyId(members) : 0;
             members.forEach((op, j) => {
                 const cop = op.combiningOp;
-                if (local && cop && cop.name !== 'rewrite') throw new UnsupportedOp('local combiningOp other than rewrite');
-                if (ack && op.type === OP_ANNOTATE && cop && cop.name === 'consensus')
-                    throw new UnsupportedOp('ack of a consensus annotate (updateConsensusProperty)');
                 const rel = this.relPos(op, base);
-                if (rel && local) throw new UnsupportedOp('relative positions in a local op');
+                if (rel && notify) {
+                    rel.flags |= RELF_NOTIFY;
+                    rel.payload = notifyRaw;
+                }
                 if (rel && !ack) recs.push(rel);  // an ack reads no positions
+                // getValidOpRange validates an insert's end when one is given (client.ts:520-524)
+                if (local && op.type === OP_INSERT && (op.pos2 !== undefined || op.relativePos2))
+                    throw new UnsupportedOp('a local insert with an end position');
                 const r = this.packOp(op, base);
+                if (ack && op.type === OP_ANNOTATE && cop && cop.name === 'consensus') {
+                    // updateConsensusProperty reads op.relativePos1.id (client.ts:981): a missing
+                    // relativePos1 throws; an id a Map lookup cannot match (none, an object) is 0
+                    const rp = op.relativePos1;
+                    if (rp === undefined || rp === null) throw new UnsupportedOp('ack of a consensus annotate without relativePos1 (a TypeError)');
+                    const id = rp.id;
+                    r.pos1 = id === undefined || id === null || typeof id === 'object' ? 0 : this.value(id);
+                }
                 if (j + 1 < members.length) r.flags |= OPF_GROUP_CONT;
                 recs.push(r);
             });

@@ -45,7 +45,7 @@ EXPORTS = [
     "mt_packed_sizes", "mt_packed_arrays", "mt_packed_key", "mt_packed_value", "mt_packed_doc_clients",
     "mt_packed_client", "mt_batch_ingest_packed", "mt_batch_log_sizes_docs", "mt_batch_download_log_docs",
     "mt_build_id", "mt_abi_version", "mt_doc_find_tile", "mt_doc_regenerated_ops", "mt_pack_json_gpu", "mt_batch_ingest_json_gpu",
-    "mt_doc_stack_context",
+    "mt_doc_stack_context", "mt_doc_consensus_events",
 ]
 SNAP_MAX_BLOBS = 32
 SNAP_META = 1 + 3 * SNAP_MAX_BLOBS
@@ -189,7 +189,8 @@ def lib():
     L.mt_batch_algorithmic_bytes.argtypes = [vp, P(C.c_double)]
     L.mt_doc_status.argtypes = [vp, i64]
     L.mt_doc_status.restype = i32
-    for fn in ("mt_doc_text", "mt_doc_props_runs", "mt_doc_shape", "mt_doc_dump", "mt_doc_regenerated_ops"):
+    for fn in ("mt_doc_text", "mt_doc_props_runs", "mt_doc_shape", "mt_doc_dump", "mt_doc_regenerated_ops",
+               "mt_doc_consensus_events"):
         getattr(L, fn).argtypes = [vp, i64, C.c_char_p, i64, P(i64)]
     L.mt_doc_snapshot_v1.argtypes = [vp, i64, P(i32)]
     L.mt_doc_snapshot_blob.argtypes = [vp, i64, i32, C.c_char_p, i64, C.c_char_p, i64, P(i64)]
@@ -366,6 +367,11 @@ class DocView:
     def regenerated_ops(self) -> list:
         """Client.regeneratePendingOp results of the log's reconnect (regenerate) records, in order."""
         return json.loads(self._string(lib().mt_doc_regenerated_ops))
+
+    def consensus_events(self) -> list:
+        """The consensus callbacks of a writer replica (annotateMarkerNotifyConsensus), in call
+        order: [{"markerId", "seq", "minSeq"}, ...]."""
+        return json.loads(self._string(lib().mt_doc_consensus_events))
 
     def shape(self) -> str:
         return self._string(lib().mt_doc_shape)

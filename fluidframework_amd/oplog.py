@@ -43,6 +43,7 @@ OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_RELPOS, OP_REGENERATE, OP_NOOP = 0, 1, 2, 
 UNASSIGNED_SEQ = -1  # UnassignedSequenceNumber (merge-tree/src/constants.ts:11): a local, unacked op
 # MT_OP_RELPOS flags (include/mt_oplog.h mt_relpos_flags)
 RELF_POS1, RELF_POS2, RELF_BEFORE1, RELF_BEFORE2, RELF_OFF1, RELF_OFF2 = 0x10, 0x20, 0x40, 0x80, 0x100, 0x200
+RELF_NOTIFY = 0x2  # a local RELPOS of Client.annotateMarkerNotifyConsensus (include/mt_oplog.h)
 OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
 MAX_INSERT_PROPS = 127  # include/mt_oplog.h MT_OPF_MAX_INSERT_PROPS (flags bits 4-10)
 # combiningOp other than "rewrite" (include/mt_oplog.h mt_combine_kind): annotate flags bits 4-5,
@@ -287,20 +288,33 @@ class Packer:
                 continue
             ack = c == 0 and not local  # Client.applyMsg -> ackPendingSegment (client.ts:810-812)
             members = self._flatten(msg["contents"])
+            # {"notifyConsensus": true} on a local message: the op came from
+            # Client.annotateMarkerNotifyConsensus (a repo-defined field of the writer stream)
+            notify = local and js_truthy(msg.get("notifyConsensus"))
+            notify_raw = 0
+            if notify:
+                notify_raw = self._notify_id(members)
             for j, op in enumerate(members):
-                if local and (js_truthy(op.get("combiningOp")) and
-                              not (isinstance(op.get("combiningOp"), dict) and op["combiningOp"].get("name") == "rewrite")):
-                    raise UnsupportedOp("local combiningOp other than rewrite")
-                if ack and op.get("type") == 2 and isinstance(op.get("combiningOp"), dict) and \
-                        op["combiningOp"].get("name") == "consensus":
-                    raise UnsupportedOp("ack of a consensus annotate (updateConsensusProperty)")
                 rel = self._relpos(op, base)
                 if rel is not None:
-                    if local:
-                        raise UnsupportedOp("relative positions in a local op")
+                    if notify:
+                        rel["flags"] |= RELF_NOTIFY
+                        rel["payload"] = notify_raw
                     if not ack:  # an ack reads no positions
                         recs.append(rel)
+                if local and op.get("type") == 0 and ("pos2" in op or js_truthy(op.get("relativePos2"))):
+                    # getValidOpRange validates an insert's end when one is given (client.ts:520-524)
+                    raise UnsupportedOp("a local insert with an end position")
                 r = self._pack_op(op, base)
+                if ack and op.get("type") == 2 and isinstance(op.get("combiningOp"), dict) and \
+                        op["combiningOp"].get("name") == "consensus":
+                    # updateConsensusProperty reads op.relativePos1.id (client.ts:981): a missing
+                    # relativePos1 throws; an id a Map lookup cannot match (none, an object) is 0
+                    rp = op.get("relativePos1")
+                    if rp is None:
+                        raise UnsupportedOp("ack of a consensus annotate without relativePos1 (a TypeError)")
+                    rid = rp.get("id") if isinstance(rp, dict) else None
+                    r["pos1"] = self._value(rid) if rid is not None and not isinstance(rid, (dict, list)) else 0
                 if j + 1 < len(members):
                     r["flags"] |= OPF_GROUP_CONT
                 recs.append(r)
@@ -310,6 +324,21 @@ class Packer:
         self._off.append(self._off[-1] + len(recs))
         self._clients.append(names)
         return len(self._clients) - 1
+
+    def _notify_id(self, members: list) -> int:
+        """The marker id a Client.annotateMarkerNotifyConsensus op registers (client.ts:113-134): the
+        op createAnnotateMarkerOp makes (opBuilder.ts:25-39) with combiningOp {name: "consensus"}."""
+        op = members[0] if len(members) == 1 else None
+        ok = isinstance(op, dict) and op.get("type") == 2 and "pos1" not in op and "pos2" not in op and \
+            op.get("combiningOp") == {"name": "consensus"}
+        r1, r2 = (op.get("relativePos1"), op.get("relativePos2")) if ok else (None, None)
+        ok = ok and isinstance(r1, dict) and isinstance(r2, dict) and "offset" not in r1 and "offset" not in r2
+        mid = r1.get("id") if ok else None
+        ok = ok and js_truthy(mid) and not isinstance(mid, (dict, list)) and r2.get("id") == mid and \
+            type(r2.get("id")) is type(mid) and js_truthy(r1.get("before")) and not js_truthy(r2.get("before"))
+        if not ok:
+            raise UnsupportedOp("notifyConsensus on an op annotateMarkerNotifyConsensus does not make")
+        return self._value(mid)
 
     @staticmethod
     def _flatten(op) -> list:

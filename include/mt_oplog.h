@@ -67,8 +67,15 @@ enum mt_relpos_flags {
     MT_RELF_BEFORE1 = 0x40u, /* relativePos1.before is truthy                      */
     MT_RELF_BEFORE2 = 0x80u,
     MT_RELF_OFF1 = 0x100u,   /* relativePos1.offset is defined (payload)           */
-    MT_RELF_OFF2 = 0x200u    /* relativePos2.offset is defined (payload_len)       */
+    MT_RELF_OFF2 = 0x200u,   /* relativePos2.offset is defined (payload_len)       */
+    /* a local RELPOS of the replica's Client.annotateMarkerNotifyConsensus(marker, props, callback)
+       (client.ts:113-134): the annotate that follows registers pendingConsensus[marker id] when it
+       applies; payload = the raw value id of relativePos1.id (the op has no offsets) */
+    MT_RELF_NOTIFY = 0x2u
 };
+/* The replica's own sequenced consensus annotate (an ack; its positions are not read) carries in
+   pos1 the raw value id of relativePos1.id (0: none a Map lookup could match) for
+   updateConsensusProperty (client.ts:980-987); the library puts its marker-id key in pos2. */
 /* short client ids are 15-bit: 0 .. 32765 per document (0 = the observer; Client.getOrAddShortClientId,
    client.ts:636-660, numbers every long id a document's log names, and a real messages.json names a
    new one on every reconnect), 0x7FFE / 0x7FFF are sentinels.  A record's `client` bit-field holds

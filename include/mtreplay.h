@@ -214,6 +214,12 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
    records (a writer replica reconnecting), in order: a JSON array of the regenerated ops, one per
    reset message (a GROUP op when it regenerates to more or fewer than one op) */
 MT_API int mt_doc_regenerated_ops(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
+/* The consensus callbacks of a writer replica's replay, in call order: a JSON array of
+   {"markerId": id, "seq": S, "minSeq": M} — Client.annotateMarkerNotifyConsensus (client.ts:113-134;
+   a local message with "notifyConsensus": true) registered the marker id, the ack at seq S ran
+   updateConsensusProperty (980-987) and minSeq M >= S called consensusInfo.callback(marker)
+   (mergeTree.ts:1701-1716).  Listeners not yet called are not listed. */
+MT_API int mt_doc_consensus_events(mt_batch *b, int64_t doc, char *buf, int64_t cap, int64_t *len);
 MT_API int mt_doc_snapshot_v1(mt_batch *b, int64_t doc, int32_t *n_blobs);
 MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name, int64_t name_cap, char *buf,
                                 int64_t cap, int64_t *len);

@@ -137,6 +137,14 @@ struct mto_tables {
     int n_values;
 };
 
+/* a consensus ack's min-seq listener (MergeTree.addMinSeqListener, mergeTree.ts:1701-1707): the
+   closure holds the consensusInfo pendingConsensus gave at the ack (marker NULL: undefined) */
+typedef struct {
+    int min_required;
+    char *key; /* the marker id's JSON text */
+    Seg *marker;
+} ConsLis;
+
 struct mto_doc {
     Block *root;
     struct {
@@ -184,6 +192,19 @@ struct mto_doc {
        message's op (or group op), comma separated */
     sb regen_cur, regen_all;
     int regen_cur_n, regen_all_n;
+    /* Client.pendingConsensus (client.ts:66): marker id (its JSON text) -> the marker it was
+       registered with; MergeTree.minSeqListeners (mergeTree.ts:1101), a Heap with cons_lis[0] the
+       min sentinel and n_lis members; the callbacks made ([{markerId, seq, minSeq}], comma joined);
+       a packed notify RELPOS's id and marker for the local annotate after it */
+    char **cons_keys;
+    Seg **cons_marks;
+    int n_cons, cap_cons;
+    ConsLis *cons_lis;
+    int n_lis, cap_lis;
+    sb cons_events;
+    int cons_events_n;
+    char *ntf_key;
+    Seg *ntf_marker;
 };
 
 /* ------------------------------------------------------------------ errors */
@@ -1031,6 +1052,106 @@ static void zamboni_segments(mto_doc *d) {
     }
 }
 
+/* ------------------------------------------------------------------ consensus (writer) */
+static char *jv_json_text(const jv *v) {
+    sb o;
+    sb_init(&o);
+    jv_stringify(v, &o);
+    sb_putc(&o, 0);
+    return o.p;
+}
+static int cons_find(mto_doc *d, const char *key) {
+    for (int i = 0; i < d->n_cons; i++)
+        if (!strcmp(d->cons_keys[i], key)) return i;
+    return -1;
+}
+/* pendingConsensus.set(marker.getId(), {callback, marker}) (client.ts:124-130) */
+static void cons_register(mto_doc *d, const char *key, Seg *m) {
+    int i = cons_find(d, key);
+    if (i < 0) {
+        if (d->n_cons == d->cap_cons) {
+            d->cap_cons = d->cap_cons ? 2 * d->cap_cons : 8;
+            d->cons_keys = (char **)realloc(d->cons_keys, sizeof(char *) * (size_t)d->cap_cons);
+            d->cons_marks = (Seg **)realloc(d->cons_marks, sizeof(Seg *) * (size_t)d->cap_cons);
+        }
+        i = d->n_cons++;
+        d->cons_keys[i] = strdup(key);
+    }
+    d->cons_marks[i] = m;
+}
+/* Heap.add (collections.ts:236-248) with minListenerComparer (mergeTree.ts:1042-1045) */
+static void cons_lis_add(mto_doc *d, int min_required, char *key, Seg *m) {
+    if (d->n_lis + 2 > d->cap_lis) {
+        d->cap_lis = d->cap_lis ? 2 * d->cap_lis : 8;
+        d->cons_lis = (ConsLis *)realloc(d->cons_lis, sizeof(ConsLis) * (size_t)d->cap_lis);
+    }
+    int k = ++d->n_lis;
+    d->cons_lis[k] = (ConsLis){min_required, key, m};
+    ConsLis *L = d->cons_lis;
+    while (k > 1 && L[k >> 1].min_required - L[k].min_required > 0) {
+        ConsLis t = L[k >> 1];
+        L[k >> 1] = L[k];
+        L[k] = t;
+        k >>= 1;
+    }
+}
+/* Heap.get (collections.ts:228-234, 250-264) */
+static ConsLis cons_lis_get(mto_doc *d) {
+    ConsLis *L = d->cons_lis;
+    const ConsLis x = L[1];
+    L[1] = L[d->n_lis];
+    d->n_lis--;
+    const int n = d->n_lis;
+    for (int k = 1; (k << 1) <= n;) {
+        int j = k << 1;
+        if (j < n && L[j].min_required - L[j + 1].min_required > 0) j++;
+        if (L[k].min_required - L[j].min_required <= 0) break;
+        ConsLis t = L[k];
+        L[k] = L[j];
+        L[j] = t;
+        k = j;
+    }
+    return x;
+}
+/* notifyMinSeqListeners (mergeTree.ts:1709-1716): each listener at seq <= minSeq calls
+   consensusInfo.callback(consensusInfo.marker) (client.ts:986) — recorded as an event; an
+   unregistered id's consensusInfo is undefined (a TypeError) */
+static void cons_notify(mto_doc *d) {
+    while (d->n_lis > 0 && d->cons_lis[1].min_required <= d->cw.min_seq) {
+        ConsLis x = cons_lis_get(d);
+        if (!x.marker) {
+            free(x.key);
+            fail(d, MTO_UNSUPPORTED, "a consensus listener without pendingConsensus info (a TypeError)");
+        }
+        char num[96];
+        if (d->cons_events_n++) sb_putc(&d->cons_events, ',');
+        sb_puts(&d->cons_events, "{\"markerId\":");
+        sb_puts(&d->cons_events, x.key);
+        snprintf(num, sizeof num, ",\"seq\":%d,\"minSeq\":%d}", x.min_required, d->cw.min_seq);
+        sb_puts(&d->cons_events, num);
+        free(x.key);
+    }
+}
+static void seg_add_properties(mto_doc *d, Seg *s, const jv *new_props, int rewrite, const CombineOp *co,
+                               int seq, int collab);
+/* Client.updateConsensusProperty(op, msg) (client.ts:980-987) after the ack: `rel1` is
+   op.relativePos1 (NULL: undefined — reading .id throws) */
+static void update_consensus_property(mto_doc *d, const jv *rel1, const jv *props, const CombineOp *co, int seq) {
+    if (!rel1 || rel1->kind == JV_UNDEF || rel1->kind == JV_NULL)
+        fail(d, MTO_UNSUPPORTED, "updateConsensusProperty: relativePos1 is undefined (a TypeError)");
+    const jv *id = rel1->kind == JV_OBJ ? jv_obj_get_ascii(rel1, "id") : NULL;
+    char *key = NULL;
+    Seg *m = NULL;
+    if (id && id->kind != JV_UNDEF && id->kind != JV_OBJ && id->kind != JV_ARR) {
+        key = jv_json_text(id);
+        const int r = cons_find(d, key);
+        if (r >= 0) m = d->cons_marks[r];
+    }
+    /* consensusInfo.marker.addProperties(op.props, op.combiningOp, msg.sequenceNumber): no collab window */
+    if (m) seg_add_properties(d, m, props, 0, co, seq, 0);
+    cons_lis_add(d, seq, key ? key : strdup("null"), m);
+}
+
 /* setMinSeq, mergeTree.ts:1718-1736 */
 static void set_min_seq(mto_doc *d, int min_seq) {
     if (!(min_seq <= d->cw.current_seq)) fail(d, MTO_MSN_ORDER, "minSeq %d > currentSeq %d", min_seq, d->cw.current_seq);
@@ -1038,6 +1159,7 @@ static void set_min_seq(mto_doc *d, int min_seq) {
     if (min_seq > d->cw.min_seq) {
         d->cw.min_seq = min_seq;
         zamboni_segments(d);
+        if (d->n_lis) cons_notify(d);
     }
 }
 
@@ -1783,6 +1905,13 @@ void mto_free(mto_doc *d) {
     free(d->pend);
     sb_free(&d->regen_cur);
     sb_free(&d->regen_all);
+    for (int i = 0; i < d->n_cons; i++) free(d->cons_keys[i]);
+    free(d->cons_keys);
+    free(d->cons_marks);
+    for (int i = 1; i <= d->n_lis; i++) free(d->cons_lis[i].key);
+    free(d->cons_lis);
+    sb_free(&d->cons_events);
+    free(d->ntf_key);
     for (int i = 0; i < d->n_ids; i++) free(d->long_ids[i]);
     free(d->long_ids);
     for (int i = 0; i < d->n_ids_map; i++) free(d->id_keys[i]);
@@ -1924,6 +2053,32 @@ static void ack_pending_segment(mto_doc *d, int type, const jv *op_props, int re
     zamboni_segments(d);
 }
 
+/* an annotate's combiningOp (segmentPropertiesManager.ts:53-54): "rewrite" when op.name is
+   "rewrite", else any truthy combiningOp goes through Properties.combine */
+static void combine_of(const jv *op, int *rewrite, CombineOp *co) {
+    const jv *cop = jv_obj_get_ascii(op, "combiningOp");
+    *rewrite = 0;
+    co->kind = MT_COMBINE_NONE;
+    co->def = co->min = NULL;
+    if (!jv_truthy(cop)) return;
+    const jv *nm = cop->kind == JV_OBJ ? jv_obj_get_ascii(cop, "name") : NULL;
+    static const u16 RW[7] = {'r', 'e', 'w', 'r', 'i', 't', 'e'};
+    static const u16 INCR[4] = {'i', 'n', 'c', 'r'};
+    static const u16 CONS[9] = {'c', 'o', 'n', 's', 'e', 'n', 's', 'u', 's'};
+    const int str = nm && nm->kind == JV_STR;
+    if (str && u16_eq(nm->s, nm->slen, RW, 7)) {
+        *rewrite = 1;
+        return;
+    }
+    co->kind = str && u16_eq(nm->s, nm->slen, INCR, 4)   ? MT_COMBINE_INCR
+               : str && u16_eq(nm->s, nm->slen, CONS, 9) ? MT_COMBINE_CONSENSUS
+                                                         : MT_COMBINE_OTHER;
+    if (cop->kind == JV_OBJ) {
+        co->def = jv_obj_get_ascii(cop, "defaultValue");
+        co->min = jv_obj_get_ascii(cop, "minValue");
+    }
+}
+
 /* Client.applyRemoteOp (client.ts:768-795) */
 static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int ref_seq, int msn) {
     int type = -1;
@@ -1958,26 +2113,9 @@ static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int
             break;
         case 2: { /* applyAnnotateRangeOp, client.ts:358-386 */
             const jv *props = jv_obj_get_ascii(op, "props");
-            const jv *cop = jv_obj_get_ascii(op, "combiningOp");
             int rewrite = 0;
-            CombineOp co = {MT_COMBINE_NONE, NULL, NULL};
-            if (jv_truthy(cop)) { /* segmentPropertiesManager.ts:53-54 */
-                const jv *nm = cop->kind == JV_OBJ ? jv_obj_get_ascii(cop, "name") : NULL;
-                static const u16 RW[7] = {'r', 'e', 'w', 'r', 'i', 't', 'e'};
-                static const u16 INCR[4] = {'i', 'n', 'c', 'r'};
-                static const u16 CONS[9] = {'c', 'o', 'n', 's', 'e', 'n', 's', 'u', 's'};
-                const int str = nm && nm->kind == JV_STR;
-                if (str && u16_eq(nm->s, nm->slen, RW, 7)) rewrite = 1;
-                else {
-                    co.kind = str && u16_eq(nm->s, nm->slen, INCR, 4)   ? MT_COMBINE_INCR
-                              : str && u16_eq(nm->s, nm->slen, CONS, 9) ? MT_COMBINE_CONSENSUS
-                                                                        : MT_COMBINE_OTHER;
-                    if (cop->kind == JV_OBJ) {
-                        co.def = jv_obj_get_ascii(cop, "defaultValue");
-                        co.min = jv_obj_get_ascii(cop, "minValue");
-                    }
-                }
-            }
+            CombineOp co;
+            combine_of(op, &rewrite, &co);
             if (!has2) pos2 = 0;
             annotate_range(d, pos1, pos2, props, rewrite, co.kind ? &co : NULL, ref_seq, short_id, seq);
             complete_remote_op(d, seq, msn);
@@ -1993,15 +2131,6 @@ static void apply_remote_op(mto_doc *d, const jv *op, int short_id, int seq, int
     }
 }
 
-static int annotate_rewrite_of(mto_doc *d, const jv *op, int local) {
-    const jv *cop = jv_obj_get_ascii(op, "combiningOp");
-    if (!jv_truthy(cop)) return 0;
-    const jv *nm = cop->kind == JV_OBJ ? jv_obj_get_ascii(cop, "name") : NULL;
-    static const u16 RW[7] = {'r', 'e', 'w', 'r', 'i', 't', 'e'};
-    if (nm && nm->kind == JV_STR && u16_eq(nm->s, nm->slen, RW, 7)) return 1;
-    if (local) fail(d, MTO_UNSUPPORTED, "local combiningOp other than rewrite");
-    return 0;
-}
 /* Client.ackPendingSegment (client.ts:588-625): a GROUP acks each member */
 static void ack_op_json(mto_doc *d, const jv *op, int seq) {
     int type = -1;
@@ -2012,15 +2141,13 @@ static void ack_op_json(mto_doc *d, const jv *op, int seq) {
         for (int i = 0; i < ops->n; i++) ack_op_json(d, ops->vals[i], seq);
         return;
     }
-    if (type == 2 && jv_truthy(jv_obj_get_ascii(op, "combiningOp")) && !annotate_rewrite_of(d, op, 0)) {
-        const jv *cop = jv_obj_get_ascii(op, "combiningOp");
-        const jv *nm = cop->kind == JV_OBJ ? jv_obj_get_ascii(cop, "name") : NULL;
-        static const u16 CONS[9] = {'c', 'o', 'n', 's', 'e', 'n', 's', 'u', 's'};
-        if (nm && nm->kind == JV_STR && u16_eq(nm->s, nm->slen, CONS, 9))
-            fail(d, MTO_UNSUPPORTED, "ack of a consensus annotate (updateConsensusProperty)");
-    }
-    ack_pending_segment(d, type, type == 2 ? jv_obj_get_ascii(op, "props") : NULL,
-                        type == 2 ? annotate_rewrite_of(d, op, 0) : 0, seq);
+    int rewrite = 0;
+    CombineOp co = {MT_COMBINE_NONE, NULL, NULL};
+    if (type == 2) combine_of(op, &rewrite, &co);
+    ack_pending_segment(d, type, type == 2 ? jv_obj_get_ascii(op, "props") : NULL, rewrite, seq);
+    /* Client.ackPendingSegment -> updateConsensusProperty (client.ts:596-600) */
+    if (type == 2 && co.kind == MT_COMBINE_CONSENSUS)
+        update_consensus_property(d, jv_obj_get_ascii(op, "relativePos1"), jv_obj_get_ascii(op, "props"), &co, seq);
 }
 
 /* a local op of a collaborating replica: Client.insertSegmentLocal / removeRangeLocal /
@@ -2035,7 +2162,7 @@ static int local_range_valid(mto_doc *d, int type, int start, int has_end, int e
     }
     return 1;
 }
-static void apply_local_op_json(mto_doc *d, const jv *op) {
+static int apply_local_op_json(mto_doc *d, const jv *op) {
     int type = -1;
     if (!op || op->kind != JV_OBJ || !jv_int(jv_obj_get_ascii(op, "type"), &type)) fail(d, MTO_BAD_INPUT, "bad op");
     const int ref = d->cw.current_seq, cid = d->cw.client_id;
@@ -2043,14 +2170,24 @@ static void apply_local_op_json(mto_doc *d, const jv *op) {
     if (type == 3) {
         const jv *ops = jv_obj_get_ascii(op, "ops");
         if (!ops || ops->kind != JV_ARR) fail(d, MTO_BAD_INPUT, "group without ops");
-        for (int i = 0; i < ops->n; i++) apply_local_op_json(d, ops->vals[i]);
-        return;
+        int any = 0;
+        for (int i = 0; i < ops->n; i++) any |= apply_local_op_json(d, ops->vals[i]);
+        return any;
     }
     int pos1 = 0, pos2 = 0;
-    const int has1 = jv_int(jv_obj_get_ascii(op, "pos1"), &pos1);
-    const int has2 = jv_int(jv_obj_get_ascii(op, "pos2"), &pos2);
+    int has1 = jv_int(jv_obj_get_ascii(op, "pos1"), &pos1);
+    int has2 = jv_int(jv_obj_get_ascii(op, "pos2"), &pos2);
+    /* getValidOpRange (client.ts:485-502) in the local view: relative positions (-1: no marker) */
+    if (!jv_obj_get_ascii(op, "pos1") && jv_truthy(jv_obj_get_ascii(op, "relativePos1"))) {
+        pos1 = pos_from_relative_pos(d, jv_obj_get_ascii(op, "relativePos1"), ref, cid);
+        has1 = 1;
+    }
+    if (!jv_obj_get_ascii(op, "pos2") && jv_truthy(jv_obj_get_ascii(op, "relativePos2"))) {
+        pos2 = pos_from_relative_pos(d, jv_obj_get_ascii(op, "relativePos2"), ref, cid);
+        has2 = 1;
+    }
     if (!has1) fail(d, MTO_UNSUPPORTED, "local op without pos1");
-    if (!local_range_valid(d, type, pos1, has2, pos2)) return;
+    if (!local_range_valid(d, type, pos1, has2, pos2)) return 0;
     switch (type) {
         case 0: {
             const jv *segspec = jv_obj_get_ascii(op, "seg");
@@ -2061,22 +2198,74 @@ static void apply_local_op_json(mto_doc *d, const jv *op) {
         }
         case 1: mark_range_removed(d, pos1, pos2, ref, cid, seq); break;
         case 2: {
-            const int rewrite = annotate_rewrite_of(d, op, 1);
-            annotate_range(d, pos1, pos2, jv_obj_get_ascii(op, "props"), rewrite, NULL, ref, cid, seq);
+            int rewrite = 0;
+            CombineOp co;
+            combine_of(op, &rewrite, &co);
+            annotate_range(d, pos1, pos2, jv_obj_get_ascii(op, "props"), rewrite, co.kind ? &co : NULL, ref, cid, seq);
             break;
         }
         default: break;
     }
+    return 1;
 }
 
-int mto_local_op_json(mto_doc *d, const char *op_json) {
+int mto_local_op_json(mto_doc *d, const char *op_json) { return mto_local_op_notify_json(d, op_json, 0); }
+
+/* notify: Client.annotateMarkerNotifyConsensus(marker, props, callback) (client.ts:113-134) made
+   the op (createAnnotateMarkerOp: relativePos1 {id, before: true}); the marker is
+   getMarkerFromId(id), registered in pendingConsensus when the annotate applies */
+int mto_local_op_notify_json(mto_doc *d, const char *op_json, int notify) {
     GUARD(d);
     jv *op = jv_parse(op_json, strlen(op_json));
     if (!op) fail(d, MTO_BAD_INPUT, "op is not JSON");
-    apply_local_op_json(d, op);
+    char *key = NULL;
+    Seg *m = NULL;
+    if (notify) {
+        const jv *r1 = op->kind == JV_OBJ ? jv_obj_get_ascii(op, "relativePos1") : NULL;
+        const jv *id = r1 && r1->kind == JV_OBJ ? jv_obj_get_ascii(r1, "id") : NULL;
+        if (!jv_truthy(id) || id->kind == JV_OBJ || id->kind == JV_ARR) {
+            jv_unref(op);
+            fail(d, MTO_BAD_INPUT, "notifyConsensus without a marker id");
+        }
+        int kl;
+        u16 *k = js_key_of(id, &kl);
+        m = id_lookup(d, k, kl);
+        free(k);
+        key = jv_json_text(id);
+    }
+    const int applied = apply_local_op_json(d, op);
+    if (notify && applied && m) cons_register(d, key, m);
+    free(key);
     jv_unref(op);
     UNGUARD(d);
     return d->status;
+}
+
+/* test helper: the local position of the marker mapped to `id_json`'s key, -1 when there is none
+   or it is removed in the local view */
+int mto_local_marker_pos(mto_doc *d, const char *id_json) {
+    jv *id = jv_parse(id_json, strlen(id_json));
+    int pos = -1;
+    if (id && jv_truthy(id)) {
+        int kl;
+        u16 *k = js_key_of(id, &kl);
+        Seg *m = id_lookup(d, k, kl);
+        free(k);
+        if (m && m->n.parent && local_net_length(m) > 0) pos = get_position(d, &m->n, d->cw.current_seq, d->cw.client_id);
+    }
+    jv_unref(id);
+    return pos;
+}
+
+/* the consensus callbacks made so far, in call order: [{"markerId", "seq", "minSeq"}, ...] */
+char *mto_consensus_events(mto_doc *d) {
+    sb o;
+    sb_init(&o);
+    sb_putc(&o, '[');
+    if (d->cons_events.p) sb_putn(&o, d->cons_events.p, d->cons_events.n);
+    sb_puts(&o, "]");
+    sb_putc(&o, 0);
+    return o.p;
 }
 
 int mto_pending_groups(const mto_doc *d) { return d->pend_n; }
@@ -3100,12 +3289,74 @@ static jv *props_from_records(mto_doc *d, const mt_prop *p, uint32_t n, const mt
     return o;
 }
 
+/* an annotate record's combiningOp (mt_oplog.h: defaultValue / minValue records after the props) */
+static void combine_of_records(mto_doc *d, const mt_op *op, const mt_prop *props, const mto_tables *t, CombineOp *co) {
+    co->kind = (int)MT_OPF_COMBINE(op->flags);
+    co->def = co->min = NULL;
+    if (!co->kind) return;
+    const mt_prop *x = props + op->payload + op->payload_len;
+    if (x[0].key != MT_KEY_COMBINE || x[1].key != MT_KEY_COMBINE) fail(d, MTO_BAD_INPUT, "combiningOp records");
+    co->def = value_from_record(d, x[0].value, t);
+    co->min = value_from_record(d, x[1].value, t);
+}
+/* a packed RELPOS: posFromRelativePos of the next record's positions (client.ts:485-502) */
+static void relpos_packed(mto_doc *d, const mt_op *op, const mto_tables *t, int ref_seq, int client_id) {
+    d->rel_pending = 0;
+    for (int k = 0; k < 2; k++) {
+        const uint32_t f = op->flags;
+        if (!(f & (k ? MT_RELF_POS2 : MT_RELF_POS1))) continue;
+        const uint32_t idv = (uint32_t)(k ? op->pos2 : op->pos1);
+        jv *rel = jv_new(JV_OBJ);
+        if (idv) jv_obj_set_ascii(rel, "id", value_from_record(d, idv, t));
+        if (f & (k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1)) jv_obj_set_ascii(rel, "before", jv_new(JV_TRUE));
+        if (f & (k ? MT_RELF_OFF2 : MT_RELF_OFF1))
+            jv_obj_set_ascii(rel, "offset", jv_new_num((double)(int32_t)(k ? op->payload_len : op->payload)));
+        const int pos = pos_from_relative_pos(d, rel, ref_seq, client_id);
+        jv_unref(rel);
+        if (k) d->rel_pos2 = pos;
+        else d->rel_pos1 = pos;
+        d->rel_pending |= 1 << k;
+    }
+}
+
 /* a packed local op (seq == -1, client 0): see apply_local_op_json */
 static void apply_local_packed(mto_doc *d, const mt_op *op, const uint16_t *text, const mt_prop *props,
                                const mto_tables *t) {
     const uint32_t bits = MT_OPF_BITS(op->flags);
     const int ref = d->cw.current_seq, cid = d->cw.client_id;
-    if (d->rel_pending) fail(d, MTO_UNSUPPORTED, "relative positions in a local op");
+    if (op->type == MT_OP_RELPOS) {
+        relpos_packed(d, op, t, ref, cid);
+        free(d->ntf_key);
+        d->ntf_key = NULL;
+        d->ntf_marker = NULL;
+        if (op->flags & MT_RELF_NOTIFY) { /* annotateMarkerNotifyConsensus: getMarkerFromId(id) */
+            jv *id = value_from_record(d, op->payload, t);
+            if (!jv_truthy(id)) fail(d, MTO_BAD_INPUT, "notifyConsensus without a marker id");
+            int kl;
+            u16 *k = js_key_of(id, &kl);
+            d->ntf_marker = id_lookup(d, k, kl);
+            free(k);
+            d->ntf_key = jv_json_text(id);
+            jv_unref(id);
+        }
+        return;
+    }
+    char *ntf_key = d->ntf_key;
+    Seg *ntf_marker = d->ntf_marker;
+    d->ntf_key = NULL;
+    d->ntf_marker = NULL;
+    mt_op rop;
+    if (d->rel_pending) {
+        rop = *op;
+        if (d->rel_pending & 1) rop.pos1 = d->rel_pos1;
+        if (d->rel_pending & 2) rop.pos2 = d->rel_pos2;
+        d->rel_pending = 0;
+        op = &rop;
+    }
+    if (ntf_key && !(op->type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op->flags) == MT_COMBINE_CONSENSUS)) {
+        free(ntf_key);
+        fail(d, MTO_BAD_INPUT, "notifyConsensus on an op that is not a consensus annotate");
+    }
     switch (op->type) {
         case MT_OP_INSERT: {
             if (!local_range_valid(d, 0, op->pos1, 0, 0)) return;
@@ -3125,14 +3376,22 @@ static void apply_local_packed(mto_doc *d, const mt_op *op, const uint16_t *text
             mark_range_removed(d, op->pos1, op->pos2, ref, cid, UNASSIGNED_SEQ);
             break;
         case MT_OP_ANNOTATE: {
-            if (MT_OPF_COMBINE(op->flags)) fail(d, MTO_UNSUPPORTED, "local combiningOp other than rewrite");
-            if (!local_range_valid(d, 2, op->pos1, 1, op->pos2)) return;
+            if (!local_range_valid(d, 2, op->pos1, 1, op->pos2)) {
+                free(ntf_key);
+                return;
+            }
             jv *pr = props_from_records(d, props + op->payload, op->payload_len, t);
-            annotate_range(d, op->pos1, op->pos2, pr, (bits & MT_OPF_REWRITE) ? 1 : 0, NULL, ref, cid, UNASSIGNED_SEQ);
+            CombineOp co;
+            combine_of_records(d, op, props, t, &co);
+            annotate_range(d, op->pos1, op->pos2, pr, (bits & MT_OPF_REWRITE) ? 1 : 0, co.kind ? &co : NULL, ref, cid,
+                           UNASSIGNED_SEQ);
             jv_unref(pr);
+            jv_unref(co.def);
+            jv_unref(co.min);
+            if (ntf_key && ntf_marker) cons_register(d, ntf_key, ntf_marker);
+            free(ntf_key);
             break;
         }
-        case MT_OP_RELPOS: fail(d, MTO_UNSUPPORTED, "relative positions in a local op"); break;
         case MT_OP_REGENERATE: { /* regeneratePendingOp of one reset op (member) */
             jv *reset = jv_new(JV_OBJ);
             jv_obj_set_ascii(reset, "type", jv_new_num(op->ref_seq));
@@ -3177,12 +3436,19 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
         /* the replica's own sequenced message: ack (client.ts:810-812); positions are not read */
         if (op->type != MT_OP_RELPOS) {
             jv *pr = NULL;
-            if (op->type == MT_OP_ANNOTATE) {
-                if (MT_OPF_COMBINE(op->flags) == MT_COMBINE_CONSENSUS)
-                    fail(d, MTO_UNSUPPORTED, "ack of a consensus annotate (updateConsensusProperty)");
-                pr = props_from_records(d, props + op->payload, op->payload_len, t);
-            }
+            if (op->type == MT_OP_ANNOTATE) pr = props_from_records(d, props + op->payload, op->payload_len, t);
             ack_pending_segment(d, op->type, pr, op->type == MT_OP_ANNOTATE && (bits & MT_OPF_REWRITE), op->seq);
+            if (op->type == MT_OP_ANNOTATE && MT_OPF_COMBINE(op->flags) == MT_COMBINE_CONSENSUS) {
+                /* updateConsensusProperty: pos1 = relativePos1.id's value id (0: none to match) */
+                CombineOp co;
+                combine_of_records(d, op, props, t, &co);
+                jv *rel = jv_new(JV_OBJ);
+                if (op->pos1) jv_obj_set_ascii(rel, "id", value_from_record(d, (uint32_t)op->pos1, t));
+                update_consensus_property(d, rel, pr, &co, op->seq);
+                jv_unref(rel);
+                jv_unref(co.def);
+                jv_unref(co.min);
+            }
             jv_unref(pr);
         }
         if (!(bits & MT_OPF_GROUP_CONT)) update_seq_numbers(d, op->msn, op->seq);
@@ -3216,16 +3482,8 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
             break;
         case MT_OP_ANNOTATE: {
             jv *pr = props_from_records(d, props + op->payload, op->payload_len, t);
-            CombineOp co = {(int)MT_OPF_COMBINE(op->flags), NULL, NULL};
-            if (co.kind) { /* defaultValue, minValue records after the props (mt_oplog.h) */
-                const mt_prop *x = props + op->payload + op->payload_len;
-                if (x[0].key != MT_KEY_COMBINE || x[1].key != MT_KEY_COMBINE) {
-                    jv_unref(pr);
-                    fail(d, MTO_BAD_INPUT, "combiningOp records");
-                }
-                co.def = value_from_record(d, x[0].value, t);
-                co.min = value_from_record(d, x[1].value, t);
-            }
+            CombineOp co;
+            combine_of_records(d, op, props, t, &co);
             annotate_range(d, op->pos1, op->pos2, pr, (bits & MT_OPF_REWRITE) ? 1 : 0, co.kind ? &co : NULL,
                            op->ref_seq, sid, op->seq);
             jv_unref(pr);
@@ -3234,25 +3492,9 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
             complete_remote_op(d, op->seq, op->msn);
             break;
         }
-        case MT_OP_RELPOS: { /* getValidOpRange of the next record (client.ts:485-502) */
-            d->rel_pending = 0;
-            for (int k = 0; k < 2; k++) {
-                const uint32_t f = op->flags;
-                if (!(f & (k ? MT_RELF_POS2 : MT_RELF_POS1))) continue;
-                const uint32_t idv = (uint32_t)(k ? op->pos2 : op->pos1);
-                jv *rel = jv_new(JV_OBJ);
-                if (idv) jv_obj_set_ascii(rel, "id", value_from_record(d, idv, t));
-                if (f & (k ? MT_RELF_BEFORE2 : MT_RELF_BEFORE1)) jv_obj_set_ascii(rel, "before", jv_new(JV_TRUE));
-                if (f & (k ? MT_RELF_OFF2 : MT_RELF_OFF1))
-                    jv_obj_set_ascii(rel, "offset", jv_new_num((double)(int32_t)(k ? op->payload_len : op->payload)));
-                const int pos = pos_from_relative_pos(d, rel, op->ref_seq, sid);
-                jv_unref(rel);
-                if (k) d->rel_pos2 = pos;
-                else d->rel_pos1 = pos;
-                d->rel_pending |= 1 << k;
-            }
+        case MT_OP_RELPOS: /* getValidOpRange of the next record (client.ts:485-502) */
+            relpos_packed(d, op, t, op->ref_seq, sid);
             break;
-        }
         case MT_OP_NOOP: break;
         default: fail(d, MTO_BAD_INPUT, "op type %d", op->type);
     }

@@ -75,6 +75,10 @@ def lib():
     L.mto_annotate_local_json.argtypes = [vp, i, i, cp]
     L.mto_remove_local.argtypes = [vp, i, i]
     L.mto_local_op_json.argtypes = [vp, cp]
+    L.mto_local_op_notify_json.argtypes = [vp, cp, i]
+    L.mto_consensus_events.argtypes = [vp]
+    L.mto_consensus_events.restype = C.c_void_p
+    L.mto_local_marker_pos.argtypes = [vp, cp]
     L.mto_pending_groups.argtypes = [vp]
     L.mto_find_tile.argtypes = [vp, i, cp, i, C.POINTER(C.c_void_p)]
     L.mto_find_tile.restype = l
@@ -169,11 +173,29 @@ class Doc:
     def remove_local(self, start: int, end: int) -> int:
         return self.L.mto_remove_local(self.h, start, end)
 
-    def local_op(self, op) -> int:
-        """A local IMergeTreeOp of a collaborating replica (pending until its own message acks it)."""
+    def local_op(self, op, notify: bool = False) -> int:
+        """A local IMergeTreeOp of a collaborating replica (pending until its own message acks it);
+        notify: the op came from Client.annotateMarkerNotifyConsensus (registers its marker id)."""
         import json as _json
 
-        return self.L.mto_local_op_json(self.h, (op if isinstance(op, str) else _json.dumps(op)).encode())
+        return self.L.mto_local_op_notify_json(self.h, (op if isinstance(op, str) else _json.dumps(op)).encode(),
+                                               1 if notify else 0)
+
+    def local_marker_pos(self, marker_id) -> int:
+        """The local position of the marker `marker_id` names (-1: none, or removed locally)."""
+        import json as _json
+
+        return self.L.mto_local_marker_pos(self.h, _json.dumps(marker_id).encode())
+
+    def consensus_events(self) -> list:
+        """The consensus callbacks made so far, in call order: [{"markerId", "seq", "minSeq"}]."""
+        import json as _json
+
+        p = self.L.mto_consensus_events(self.h)
+        try:
+            return _json.loads(C.string_at(p).decode())
+        finally:
+            self.L.mto_free_string(p)
 
     def pending_groups(self) -> int:
         return self.L.mto_pending_groups(self.h)

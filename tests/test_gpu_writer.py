@@ -44,7 +44,7 @@ def oracle_replica(name, events, initial=""):
         if m.get("type") == "regenerate":
             d.regenerate(m["contents"])
         elif m["sequenceNumber"] == -1:
-            assert d.local_op(m["contents"]) == 0
+            assert d.local_op(m["contents"], bool(m.get("notifyConsensus"))) == 0
         elif d.apply_msg(json.dumps(m)) != 0:
             break
     return d
@@ -75,6 +75,40 @@ def _farm_parity(f, **opts):
         for i, n in enumerate(names):
             assert_same(b.doc(i), f.docs[n], n)
         return b.stats()
+
+
+@pytest.mark.parametrize("opts", [{}, {"seg_cap": 64, "max_retries": 24}], ids=["plain", "escalating"])
+def test_consensus_writers_and_local_relative_positions(opts):
+    """Writers calling annotateMarkerNotifyConsensus (client.ts:113-134) and issuing local ops
+    addressed by marker ids (client.ts:485-543) on free-running farms, plus the hand-worked cases
+    of tests/test_consensus.py: every replica on the GPU equals the oracle's — state, and the
+    consensus callbacks (updateConsensusProperty's re-combine at the ack, the min-seq listener
+    calls, client.ts:980-987) in call order."""
+    from test_consensus import _kat_registered, _kat_remote_first, _kat_unregistered, consensus_farms
+
+    farms = consensus_farms() + [round_farm(5, 50, 63, markers=35, consensus=45, rewrite=10)]
+    docs, names, want = [], [], []
+    for f in farms:
+        for n in f.names:
+            docs.append(f.events[n])
+            names.append(n)
+            want.append(f.docs[n])
+    kats = [_kat_registered()[0], _kat_remote_first()[0]] + list(_kat_unregistered())
+    for ev in kats:
+        docs.append(ev)
+        names.append("W")
+        want.append(oracle_replica("W", ev))
+    calls = 0
+    with fa.ReplayBatch(len(docs), **opts) as b:
+        b.ingest_messages(docs, observer=names)
+        b.run()
+        for i, od in enumerate(want):
+            dv = b.doc(i)
+            assert_same(dv, od, f"{i} {names[i]}")
+            if od.status == 0:
+                assert dv.consensus_events() == od.consensus_events(), i
+                calls += len(od.consensus_events())
+    assert want[-1].status != 0 and calls > 40
 
 
 @pytest.mark.parametrize("seg_cap", [0, 64])

@@ -75,6 +75,46 @@ def random_op(rng: random.Random, length: int, n_keys: int = 4, p_annotate: int 
     return op
 
 
+def id_op(rng: random.Random, ids: list, registered: set, live=None) -> tuple:
+    """An op addressed by a marker id (ids: markerIds inserted so far anywhere; registered: the ids
+    this replica's annotateMarkerNotifyConsensus calls registered): (op, notify).
+      * Client.annotateMarkerNotifyConsensus (client.ts:113-134): createAnnotateMarkerOp's shape
+        with combiningOp {name: "consensus"} (notify = True);
+      * annotateMarker with consensus on an id already registered (its ack re-combines too);
+      * local ops with relativePos1 / relativePos2 (client.ts:485-502): inserts, removes and
+        annotates at a marker, before / after it, with offsets.
+    live(id): the marker is present in the issuer's local view; only those are addressed.  (A
+    removed marker's position is its detached position once zamboni dropped it — 0 — so replicas
+    that zambonied at different times resolve it differently, and annotateMarkerNotifyConsensus on
+    it names the next segment: its { seq: -1 } object would land on text that may split later.)"""
+    u = rng.randrange(100)
+    cand = [i for i in (ids if u < 35 or u >= 45 else sorted(registered)) if live is None or live(i)]
+    if not cand:
+        return None, False
+    mid = rng.choice(cand)
+    cons = {"type": 2, "props": {f"v{rng.randrange(3)}": rng.randrange(5)}, "combiningOp": {"name": "consensus"},
+            "relativePos1": {"id": mid, "before": True}, "relativePos2": {"id": mid}}
+    if u < 35:
+        return cons, True
+    if u < 45:
+        return cons, False
+
+    def rel():
+        r = {"id": mid}
+        if rng.randrange(2):
+            r["before"] = True
+        if rng.randrange(3) == 0:
+            r["offset"] = rng.randrange(4)
+        return r
+
+    if u < 65:
+        return {"type": 0, "relativePos1": rel(), "seg": rng.choice(["x", "yz", "\n", "abc"])}, False
+    end = {"relativePos2": rel()} if rng.randrange(2) else {"pos2": 1 + rng.randrange(12)}
+    if u < 80:
+        return dict({"type": 1, "relativePos1": rel()}, **end), False
+    return dict({"type": 2, "relativePos1": rel(), "props": {"r": rng.randrange(3)}}, **end), False
+
+
 class Farm:
     """Writer replicas + an observer over one sequenced stream (all in the oracle)."""
 
@@ -95,22 +135,28 @@ class Farm:
         self.observer.start_collab("readonly")
         self.log = []        # sequenced messages
         self.cursor = {n: 0 for n in self.names}
+        self.ids = []        # markerIds inserted (step(consensus=...))
+        self.registered = {n: set() for n in self.names}
 
     def msn(self) -> int:
         live = [c for c in self.cursor.values() if c <= len(self.log)]
         return min(live) if live else len(self.log)
 
-    def local(self, name: str, op: dict):
+    def local(self, name: str, op: dict, notify: bool = False):
         d = self.docs[name]
         if d.status != 0:
             return
         ref = d.L.mto_current_seq(d.h)
         before = d.pending_groups()
-        assert d.local_op(op) == 0, d.error
+        assert d.local_op(op, notify) == 0, d.error
         msg = local_message(name, op, ref)
+        if notify:  # the op came from annotateMarkerNotifyConsensus (a repo-defined stream field)
+            msg["notifyConsensus"] = True
         self.events[name].append(msg)
         if d.pending_groups() == before:  # not applied (empty): nothing is submitted
             return
+        if notify:
+            self.registered[name].add(op["relativePos1"]["id"])
         seq = len(self.log) + 1
         self.log.append({"clientId": name, "sequenceNumber": seq, "referenceSequenceNumber": ref,
                          "minimumSequenceNumber": self.msn(), "type": "op", "contents": op})
@@ -131,11 +177,27 @@ class Farm:
                 self.cursor[name] = len(self.log) + 10 ** 9
                 return
 
+    def issue(self, name: str, consensus=0, **op_kw):
+        """One random local op of replica `name`.  consensus: percentage of local ops addressed
+        by marker ids (id_op) once markers with ids exist; marker inserts then carry a markerId."""
+        d = self.docs[name]
+        if consensus and self.ids and self.rng.randrange(100) < consensus:
+            op, notify = id_op(self.rng, self.ids, self.registered[name], lambda i: d.local_marker_pos(i) >= 0)
+            if op is not None:
+                self.local(name, op, notify)
+            return
+        op = random_op(self.rng, d.length(), **op_kw)
+        seg = op.get("seg")
+        if consensus and isinstance(seg, dict) and "marker" in seg:
+            mid = f"{name}{len(self.ids)}"
+            seg.setdefault("props", {})["markerId"] = mid
+            self.ids.append(mid)
+        self.local(name, op)
+
     def step(self, p_op=45, **op_kw):
         name = self.rng.choice(self.names)
         if self.rng.randrange(100) < p_op:
-            d = self.docs[name]
-            self.local(name, random_op(self.rng, d.length(), **op_kw))
+            self.issue(name, **op_kw)
         else:
             self.deliver(name, 1 + self.rng.randrange(4))
 
@@ -170,8 +232,7 @@ def round_farm(n_clients: int, n_rounds: int, seed: int, initial: str = "", max_
         s0 = len(f.log)
         ops = 1 + f.rng.randrange(max_ops)
         for _ in range(ops):
-            name = f.rng.choice(f.names)
-            f.local(name, random_op(f.rng, f.docs[name].length(), **kw))
+            f.issue(f.rng.choice(f.names), **kw)
         for m in f.log[s0:]:
             m["minimumSequenceNumber"] = s0
         for n in f.names:
