@@ -34,6 +34,13 @@ export declare class ReplayClient {
     insertMarkerLocal(pos: number, refType: number, props?: Record<string, any>): object;
     removeRangeLocal(start: number, end: number): object;
     annotateRangeLocal(start: number, end: number, props: Record<string, any>, combiningOp?: { name: string }): object;
+    /** Client.annotateMarkerNotifyConsensus(marker, props, callback) (client.ts:113-134) on the marker
+     *  with this id; the callback runs from runConsensusCallbacks() after run(). */
+    annotateMarkerNotifyConsensus(markerId: string, props: Record<string, any>,
+                                  callback?: (e: { markerId: any; seq: number; minSeq: number }) => void): object;
+    /** the consensus callbacks the replay made, in call order (after run()). */
+    consensusEvents(): { markerId: any; seq: number; minSeq: number }[];
+    runConsensusCallbacks(): void;
     /** Client.regeneratePendingOp(resetOp, oldest pending group) on reconnect (client.ts:855-893). */
     regeneratePendingOp(resetOp: object): void;
     /** the regenerated ops of every regeneratePendingOp call, in order (after run()). */

@@ -310,6 +310,30 @@ class ReplayClient {
         if (combiningOp) op.combiningOp = combiningOp;
         return this.localOp(op);
     }
+    // Client.annotateMarkerNotifyConsensus(marker, props, callback) (client.ts:113-134), the marker
+    // named by its id: createAnnotateMarkerOp's op queued as a local message marked
+    // notifyConsensus.  The replay records each callback the reference would make (the ack's
+    // updateConsensusProperty, then minSeq reaching its seq); runConsensusCallbacks() makes them,
+    // in order, after run(), with the marker id and the seq / minSeq of the call.
+    annotateMarkerNotifyConsensus(markerId, props, callback) {
+        const op = { combiningOp: { name: 'consensus' }, props, relativePos1: { id: markerId, before: true },
+            relativePos2: { id: markerId }, type: OP_ANNOTATE };
+        this.batch.queued = true;
+        this.messages.push({ clientId: this.longClientId, sequenceNumber: -1, referenceSequenceNumber: 0,
+            minimumSequenceNumber: 0, type: 'op', contents: op, notifyConsensus: true });
+        if (callback) {
+            if (!this.consensusCallbacks) this.consensusCallbacks = new Map();
+            this.consensusCallbacks.set(markerId, callback);  // pendingConsensus.set (client.ts:129)
+        }
+        return op;
+    }
+    consensusEvents() { return JSON.parse(native().docConsensusEvents(this.batch.h, this.index)); }
+    runConsensusCallbacks() {
+        for (const e of this.consensusEvents()) {
+            const cb = this.consensusCallbacks && this.consensusCallbacks.get(e.markerId);
+            if (cb) cb(e);
+        }
+    }
     // Client.regeneratePendingOp(resetOp, ...) on reconnect (client.ts:855-893): queued; the
     // regenerated ops come back from regeneratedOps() after run()
     regeneratePendingOp(resetOp) {

@@ -330,6 +330,9 @@ napi_value doc_text(napi_env env, napi_callback_info info) { return string_out(e
 napi_value doc_regenerated_ops(napi_env env, napi_callback_info info) {
     return string_out(env, info, mt_doc_regenerated_ops, "mt_doc_regenerated_ops");
 }
+napi_value doc_consensus_events(napi_env env, napi_callback_info info) {
+    return string_out(env, info, mt_doc_consensus_events, "mt_doc_consensus_events");
+}
 napi_value doc_props_runs(napi_env env, napi_callback_info info) {
     return string_out(env, info, mt_doc_props_runs, "mt_doc_props_runs");
 }
@@ -481,6 +484,7 @@ napi_value init(napi_env env, napi_value exports) {
         {"docFindTile", nullptr, doc_find_tile, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docStackContext", nullptr, doc_stack_context, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"docRegeneratedOps", nullptr, doc_regenerated_ops, nullptr, nullptr, nullptr, kMethod, nullptr},
+        {"docConsensusEvents", nullptr, doc_consensus_events, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"deviceDigests", nullptr, device_digests, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"stats", nullptr, stats, nullptr, nullptr, nullptr, kMethod, nullptr},
         {"statusString", nullptr, status_string, nullptr, nullptr, nullptr, kMethod, nullptr},

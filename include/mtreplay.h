@@ -56,8 +56,10 @@ extern "C" {
    4: round 3 dropped oe_cap / blk_cap / heap_cap from mt_batch_options and added n_docs to
       mt_batch_ingest_json_gpu; round 4 added mt_abi_version.
    5: 15-bit short client ids (mt_oplog.h: high bits in mt_op.flags 11-13, insert prop counts
-      <= 127, sentinels 0x7FFE / 0x7FFF); OutRec meta: clientId [0,15), removedClientId [15,30). */
-#define MT_ABI_VERSION 5
+      <= 127, sentinels 0x7FFE / 0x7FFF); OutRec meta: clientId [0,15), removedClientId [15,30).
+   6: writer consensus (mt_oplog.h MT_RELF_NOTIFY; a consensus ack's pos1 = relativePos1.id) and
+      relative positions in local ops; mt_doc_consensus_events. */
+#define MT_ABI_VERSION 6
 
 enum mt_status_code {
     MT_OK = 0,

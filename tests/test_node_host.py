@@ -21,7 +21,7 @@ pytestmark = pytest.mark.skipif(NODE is None or not ADDON.exists(), reason="node
 
 FUNCS = {"createBatch", "setTables", "setClients", "ingest", "generate", "run", "runAsync", "docStatus", "docText",
          "docPropsRuns", "docSnapshotV1", "docDigest", "deviceDigests", "stats", "statusString", "ingestJson",
-         "docFindTile", "docRegeneratedOps", "docStackContext"}
+         "docFindTile", "docRegeneratedOps", "docStackContext", "docConsensusEvents"}
 
 
 def _node(code):
@@ -125,6 +125,39 @@ const { ReplayBatch } = require('./fluidframework_amd/js');
     for pos, seg in ((0, mk), (0, "abc d"), (0, mk), (7, "ef"), (8, mk)):
         od.local_op({"type": 0, "pos1": pos, "seg": seg})
     assert int(got["cdigest"]) == od.digest()
+
+
+@pytest.mark.gpu
+def test_node_consensus_callbacks():
+    """Client.annotateMarkerNotifyConsensus through the JS client (client.ts:113-134): the
+    callback runs once minSeq reaches the ack's seq, and the marker holds the re-combined value —
+    the derived case of tests/test_consensus.py, equal to the oracle."""
+    from test_consensus import _kat_registered
+
+    ev, text, props, calls, _ = _kat_registered()
+    code = r"""
+const { ReplayBatch } = require('./fluidframework_amd/js');
+const ev = JSON.parse(process.argv[1]);
+(async () => {
+  const b = new ReplayBatch(1);
+  const w = b.client(0);
+  w.startOrUpdateCollaboration('W');
+  const seen = [];
+  for (const m of ev) {
+    if (m.sequenceNumber !== -1) w.applyMsg(m);
+    else if (m.notifyConsensus) w.annotateMarkerNotifyConsensus(m.contents.relativePos1.id, m.contents.props, (e) => seen.push(e));
+    else w.localOp(m.contents);
+  }
+  await b.runAsync();
+  w.runConsensusCallbacks();
+  process.stdout.write(JSON.stringify({ text: w.getText(), seen, props: w.propertyRuns() }));
+})().catch((e) => { console.error(e); process.exit(1); });
+"""
+    r = subprocess.run([NODE, "-e", code, json.dumps(ev)], capture_output=True, text=True, cwd=ROOT, timeout=60)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    assert got["text"] == text and got["seen"] == calls
+    assert [json.loads(x[2]) for x in got["props"] if x[2] and "markerId" in x[2]] == [props]
 
 
 @pytest.mark.gpu
