@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -357,6 +358,8 @@ struct mt_batch {
     std::chrono::steady_clock::time_point t_launch;
     // single-document result cache
     int64_t cached_doc = -1;
+    uint64_t load_gen = 0;         // bumped whenever load_doc loads a document's results
+    std::shared_ptr<void> qtree;   // the loaded document's rebuilt tree + query maps (DocTree)
     std::vector<OutRec> c_recs;
     std::vector<uint32_t> c_lab;  // label tracking: per record, the prop set of the labels snapshot
     std::vector<uint16_t> c_text;
@@ -1961,6 +1964,7 @@ static int load_doc(mt_batch *b, int64_t d) {
     b->c_pool.resize(pt);
     if (pt) HIPCHK(hipMemcpy(b->c_pool.data(), b->d_pool + b->h_pool_base[d], 4ull * pt, hipMemcpyDeviceToHost));
     b->cached_doc = d;
+    b->load_gen++;
     return MT_OK;
 }
 
@@ -2210,6 +2214,50 @@ static uint32_t snap_props(mt_batch *b, const OutRec &r, int64_t rec) {
     return b->c_lab.empty() ? r.props : b->c_lab[(size_t)rec];
 }
 
+namespace {
+struct RangeStacks {  // label -> stack of leaf indices, in key creation order
+    std::vector<std::pair<std::u16string, std::vector<int64_t>>> s;
+    std::vector<int64_t> &get(const std::u16string &k) {
+        for (auto &e : s)
+            if (e.first == k) return e.second;
+        s.push_back({k, {}});
+        return s.back().second;
+    }
+};
+using Labels = std::vector<std::u16string>;
+// The loaded document's tree and the maps its queries read, built once per load_doc: findTile /
+// getStackContext at every position (beastTest's checkStacksAllPositions) cost a descent each,
+// not a rebuild.  Tile maps are built per label on first use (a block's maps are only read for
+// the asked-for label); range stacks carry every label.
+struct DocTree {
+    uint64_t gen = 0;  // mt_batch.load_gen it was built for
+    std::vector<TNode> nodes;
+    std::vector<const OutRec *> leaves;
+    std::vector<int64_t> leaf_rec, lpos;  // lpos[i]: local position of leaf i (lpos[n]: the length)
+    int64_t root = -1;
+    bool tile_ready = false, tile_bad = false;
+    std::vector<Labels> tile_cur, tile_snap;  // current labels / as of the leaf block's last blockUpdate
+    std::unordered_map<std::u16string, std::pair<std::vector<int64_t>, std::vector<int64_t>>> tile_maps;
+    bool range_ready = false, range_bad = false;
+    std::vector<Labels> range_cur;
+    std::vector<RangeStacks> rs;
+};
+}  // namespace
+
+static DocTree &doc_tree(mt_batch *b) {
+    if (!b->qtree) b->qtree = std::make_shared<DocTree>();
+    DocTree &T = *(DocTree *)b->qtree.get();
+    if (T.gen != b->load_gen) {
+        T = DocTree();
+        T.gen = b->load_gen;
+        T.root = rebuild_tree(b, T.nodes, T.leaves, T.leaf_rec);
+        T.lpos.assign(T.leaves.size() + 1, 0);
+        for (size_t i = 0; i < T.leaves.size(); i++)
+            T.lpos[i + 1] = T.lpos[i] + (rec_removed(*T.leaves[i]) ? 0 : (int64_t)T.leaves[i]->len);
+    }
+    return T;
+}
+
 // Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076 -> MergeTree.findTile,
 // mergeTree.ts:1763-1789) on the document's final table, in the replica's local view
 // (refSeq UniversalSequenceNumber): search (preceding, posPrecedesTile) or backwardSearch
@@ -2231,50 +2279,56 @@ MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const c
     uint32_t tk = 0xFFFFFFFFu;
     for (size_t k = 0; k < b->keys.size(); k++)
         if (b->keys[k] == "referenceTileLabels") tk = (uint32_t)k;
-    std::vector<TNode> nodes;
-    std::vector<const OutRec *> leaves;
-    std::vector<int64_t> leaf_rec;
-    const int64_t root = rebuild_tree(b, nodes, leaves, leaf_rec);
-    if (root < 0) return MT_INTERNAL;
+    DocTree &T = doc_tree(b);
+    if (T.root < 0) return MT_INTERNAL;
+    const std::vector<TNode> &nodes = T.nodes;
+    const std::vector<const OutRec *> &leaves = T.leaves;
     auto local_len = [](const OutRec &r) -> int64_t { return rec_removed(r) ? 0 : (int64_t)r.len; };
-    std::vector<std::u16string> labels;
-    bool bad = false;
+    if (!T.tile_ready) {
+        // every tile marker's labels are parsed once, so an unmodelled value anywhere is reported
+        T.tile_cur.resize(leaves.size());
+        T.tile_snap.resize(leaves.size());
+        for (size_t k = 0; k < leaves.size(); k++) {
+            const OutRec &r = *leaves[k];
+            if (tile_labels_of(b, r, tk, T.tile_cur[k]) < 0) T.tile_bad = true;
+            if (local_len(r) > 0 && (r.meta & mt::kMetaMarker) && (r.toff & 1u) &&
+                ref_labels_of(b, r, tk, 1u, T.tile_snap[k], snap_props(b, r, T.leaf_rec[k])) < 0)
+                T.tile_bad = true;
+        }
+        T.tile_ready = true;
+    }
+    if (T.tile_bad) return MT_UNSUPPORTED;
     // refHasTileLabel on the current labels (the leaf tests of recordTileStart / tileShift)
     auto labelled = [&](int64_t k) {
-        const int t = tile_labels_of(b, *leaves[(size_t)k], tk, labels);
-        if (t < 0) bad = true;
-        if (t <= 0) return false;
-        for (const auto &l : labels)
+        for (const auto &l : T.tile_cur[(size_t)k])
             if (l == label) return true;
         return false;
     };
-    // every block's maps for `label` (only that key is ever read): rightmost / leftmost leaf, -1 none
-    std::vector<int64_t> right(nodes.size(), -1), left(nodes.size(), -1);
-    std::function<void(int64_t)> update = [&](int64_t n) {
-        const TNode &t = nodes[(size_t)n];
-        for (int64_t k : t.kids) {
-            if (t.level == 0) {
-                const OutRec &r = *leaves[(size_t)k];
-                if (local_len(r) <= 0 || !(r.meta & mt::kMetaMarker) || !(r.toff & 1u)) continue;
-                const int tl = ref_labels_of(b, r, tk, 1u, labels, snap_props(b, r, leaf_rec[(size_t)k]));
-                if (tl < 0) bad = true;
-                if (tl <= 0) continue;
-                for (const auto &l : labels)
-                    if (l == label) {
-                        right[(size_t)n] = k;  // addTile
-                        if (left[(size_t)n] < 0) left[(size_t)n] = k;  // addTileIfNotPresent
-                    }
-            } else {
-                update(k);
-                if (right[(size_t)k] >= 0) right[(size_t)n] = right[(size_t)k];  // Properties.extend
-                if (left[(size_t)n] < 0) left[(size_t)n] = left[(size_t)k];     // extendIfUndefined
+    auto mit = T.tile_maps.find(label);
+    if (mit == T.tile_maps.end()) {
+        // every block's maps for `label`: rightmost / leftmost leaf, -1 none
+        std::vector<int64_t> right(nodes.size(), -1), left(nodes.size(), -1);
+        std::function<void(int64_t)> update = [&](int64_t n) {
+            const TNode &t = nodes[(size_t)n];
+            for (int64_t k : t.kids) {
+                if (t.level == 0) {
+                    for (const auto &l : T.tile_snap[(size_t)k])
+                        if (l == label) {
+                            right[(size_t)n] = k;  // addTile
+                            if (left[(size_t)n] < 0) left[(size_t)n] = k;  // addTileIfNotPresent
+                        }
+                } else {
+                    update(k);
+                    if (right[(size_t)k] >= 0) right[(size_t)n] = right[(size_t)k];  // Properties.extend
+                    if (left[(size_t)n] < 0) left[(size_t)n] = left[(size_t)k];     // extendIfUndefined
+                }
             }
-        }
-    };
-    update(root);
-    // every tile marker's labels are checked, so an unmodelled value anywhere is reported
-    for (int64_t k = 0; k < (int64_t)leaves.size(); k++) (void)labelled(k);
-    if (bad) return MT_UNSUPPORTED;
+        };
+        update(T.root);
+        mit = T.tile_maps.emplace(label, std::make_pair(std::move(right), std::move(left))).first;
+    }
+    const std::vector<int64_t> &right = mit->second.first, &left = mit->second.second;
+    const int64_t root = T.root;
     int64_t tile = -1;
     if (preceding) {  // search -> searchBlock (1797-1829)
         int64_t pos = start_pos;
@@ -2331,11 +2385,8 @@ MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const c
             n = hit ? next : -1;
         }
     }
-    if (bad) return MT_UNSUPPORTED;
     if (tile < 0) return MT_OK;
-    int64_t tp = 0;
-    for (int64_t i = 0; i < tile; i++) tp += local_len(*leaves[(size_t)i]);
-    *tile_pos = tp;
+    *tile_pos = T.lpos[(size_t)tile];
     std::string pj;
     if (leaves[(size_t)tile]->props) props_json(b, leaves[(size_t)tile]->props, pj);
     return out_str(pj, props_buf, props_cap, props_len);
@@ -2353,17 +2404,6 @@ MT_API int mt_doc_find_tile(mt_batch *b, int64_t doc, int64_t start_pos, const c
 // of their current labels.
 // Output (repo-defined shape): {label: [{"pos":P,"refType":T[,"props":{..}]}, ..]} in JS key order,
 // stacks bottom to top.
-namespace {
-struct RangeStacks {  // label -> stack of leaf indices, in key creation order
-    std::vector<std::pair<std::u16string, std::vector<int64_t>>> s;
-    std::vector<int64_t> &get(const std::u16string &k) {
-        for (auto &e : s)
-            if (e.first == k) return e.second;
-        s.push_back({k, {}});
-        return s.back().second;
-    }
-};
-}  // namespace
 
 MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, const char *const *labels_utf8,
                                 int32_t n_labels, char *buf, int64_t cap, int64_t *len) {
@@ -2381,20 +2421,11 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
     uint32_t rk = 0xFFFFFFFFu;
     for (size_t k = 0; k < b->keys.size(); k++)
         if (b->keys[k] == "referenceRangeLabels") rk = (uint32_t)k;
-    std::vector<TNode> nodes;
-    std::vector<const OutRec *> leaves;
-    std::vector<int64_t> leaf_rec;
-    const int64_t root = rebuild_tree(b, nodes, leaves, leaf_rec);
-    if (root < 0) return MT_INTERNAL;
-    std::vector<RangeStacks> rs(nodes.size());
+    DocTree &T = doc_tree(b);
+    if (T.root < 0) return MT_INTERNAL;
+    const std::vector<TNode> &nodes = T.nodes;
+    const std::vector<const OutRec *> &leaves = T.leaves;
     auto local_len = [](const OutRec &r) -> int64_t { return rec_removed(r) ? 0 : (int64_t)r.len; };
-    std::vector<std::u16string> labels;
-    bool bad = false;
-    auto range_labels = [&](const OutRec &r) -> bool {  // refHasRangeLabels + getRangeLabels (current)
-        const int t = ref_labels_of(b, r, rk, 6u, labels);
-        if (t < 0) bad = true;
-        return t > 0;
-    };
     // applyRangeReference (mergeTree.ts:246-261): NestBegin pushes; an end pops a NestBegin on top
     auto apply_ref = [&](std::vector<int64_t> &st, int64_t leaf) {
         if (leaves[(size_t)leaf]->toff & 2u) {
@@ -2412,33 +2443,41 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
             for (int64_t x : e.second) apply_ref(c, x);
         }
     };
-    // blockUpdate's rangeStacks, children before parents: a leaf block reads its markers' labels as
-    // of its last blockUpdate (the labels snapshot)
-    std::function<void(int64_t)> update = [&](int64_t n) {
-        const TNode &t = nodes[(size_t)n];
-        for (int64_t k : t.kids) {
-            if (t.level == 0) {
-                const OutRec &r = *leaves[(size_t)k];
-                if (local_len(r) <= 0 || !(r.meta & mt::kMetaMarker) || !(r.toff & 6u)) continue;
-                const int tl = ref_labels_of(b, r, rk, 6u, labels, snap_props(b, r, leaf_rec[(size_t)k]));
-                if (tl < 0) bad = true;
-                if (tl > 0)
-                    for (const auto &l : labels) apply_ref(rs[(size_t)n].get(l), k);  // updateRangeInfo
-            } else {
-                update(k);
-                apply_delta(rs[(size_t)n], rs[(size_t)k]);
+    if (!T.range_ready) {
+        // every label list is parsed once (the reference's blockUpdate iterates them all); blockUpdate's
+        // rangeStacks, children before parents: a leaf block reads its markers' labels as of its last
+        // blockUpdate (the labels snapshot)
+        Labels labels;
+        T.range_cur.resize(leaves.size());
+        for (size_t k = 0; k < leaves.size(); k++)  // refHasRangeLabels + getRangeLabels (current)
+            if (ref_labels_of(b, *leaves[k], rk, 6u, T.range_cur[k]) < 0) T.range_bad = true;
+        T.rs.assign(nodes.size(), RangeStacks());
+        std::function<void(int64_t)> update = [&](int64_t n) {
+            const TNode &t = nodes[(size_t)n];
+            for (int64_t k : t.kids) {
+                if (t.level == 0) {
+                    const OutRec &r = *leaves[(size_t)k];
+                    if (local_len(r) <= 0 || !(r.meta & mt::kMetaMarker) || !(r.toff & 6u)) continue;
+                    const int tl = ref_labels_of(b, r, rk, 6u, labels, snap_props(b, r, T.leaf_rec[(size_t)k]));
+                    if (tl < 0) T.range_bad = true;
+                    if (tl > 0)
+                        for (const auto &l : labels) apply_ref(T.rs[(size_t)n].get(l), k);  // updateRangeInfo
+                } else {
+                    update(k);
+                    apply_delta(T.rs[(size_t)n], T.rs[(size_t)k]);
+                }
             }
-        }
-    };
-    update(root);
-    for (const OutRec *r : leaves) (void)range_labels(*r);  // every list is checked, as the reference's blockUpdate iterates them
-    if (bad) return MT_UNSUPPORTED;
+        };
+        update(T.root);
+        T.range_ready = true;
+    }
+    if (T.range_bad) return MT_UNSUPPORTED;
+    const std::vector<RangeStacks> &rs = T.rs;
+    const int64_t root = T.root;
     RangeStacks out;
     auto leaf_marker = [&](int64_t k) {  // applyLeafRangeMarker (953-964): the asked-for labels in order
-        const OutRec &r = *leaves[(size_t)k];
-        if (!range_labels(r)) return;
         for (const auto &w : want)
-            for (const auto &l : labels)
+            for (const auto &l : T.range_cur[(size_t)k])
                 if (l == w) {
                     apply_ref(out.get(w), k);
                     break;
@@ -2487,8 +2526,7 @@ MT_API int mt_doc_stack_context(mt_batch *b, int64_t doc, int64_t start_pos, con
         for (char16_t c : out.s[i].first) k8.push_back(c < 0x80 ? (char)c : '\x01');
         if (!array_index(k8, &v)) order.push_back(i);
     }
-    std::vector<int64_t> lpos(leaves.size() + 1, 0);
-    for (size_t i = 0; i < leaves.size(); i++) lpos[i + 1] = lpos[i] + local_len(*leaves[i]);
+    const std::vector<int64_t> &lpos = T.lpos;
     std::string o = "{";
     for (size_t q = 0; q < order.size(); q++) {
         const auto &e = out.s[order[q]];
