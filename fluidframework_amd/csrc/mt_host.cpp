@@ -42,6 +42,8 @@ extern "C" __global__ void jg_markers_kernel(const mt_op *ops, const int64_t *op
                                              const uint32_t *vkey,
                                              uint32_t n_values, uint32_t *n_ids, uint32_t *tile_annot);
 extern "C" __global__ void mt_snapshot_kernel(mt::SnapParams P);
+extern "C" __global__ void mt_snapshot_size_kernel(mt::SnapParams P);
+extern "C" __global__ void mt_snapshot_serial_kernel(mt::SnapParams P);
 extern "C" __global__ void mt_bytes_digest_kernel(const uint8_t *buf, const int64_t *off, const int64_t *len, int64_t n,
                                                   uint64_t *dst);
 
@@ -3017,7 +3019,12 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                 P.dst = b->d_snap;
                 P.dst_off = b->d_snap_off;
                 void *args[] = {&P};
-                if (hipLaunchKernel((const void *)mt_snapshot_kernel, dim3((unsigned)P.n), dim3(64), args, 0, s) !=
+                // the lane-parallel serializer (a sizing and a writing kernel); MT_SNAP_SERIAL=1: the
+                // record-at-a-time walker, both passes in one kernel
+                static const bool serial = getenv("MT_SNAP_SERIAL") && atoi(getenv("MT_SNAP_SERIAL")) > 0;
+                const void *kfn = serial ? (const void *)mt_snapshot_serial_kernel
+                                 : pass ? (const void *)mt_snapshot_kernel : (const void *)mt_snapshot_size_kernel;
+                if (hipLaunchKernel(kfn, dim3((unsigned)P.n), dim3(64), args, 0, s) !=
                     hipSuccess) {
                     fail(MT_ERR_HIP);
                     break;

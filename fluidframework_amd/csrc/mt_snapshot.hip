@@ -564,13 +564,563 @@ __device__ __forceinline__ void snapshot_doc(const SnapParams &P, int64_t w) {
     }
 }
 
+// ---------------------------------------------------------------- lane-parallel serializer
+// The same walk, re-organised so that HBM latency is paid per batch of 64, not per record:
+//   stage 1, per tile of 64 records: every lane loads its record, classifies it (skipped /
+//     settled / text / ends in '\n') and compares its properties with the previous kept
+//     record's (matchProperties; consecutive comparisons decide a run because matchProperties is
+//     an equivalence on decided pairs), then a register-only scalar loop applies the run rules
+//     (canAppend + TextSegmentGranularity, snapshotV1.ts:191-210) and queues segments;
+//   stage 2, per batch of 64 queued segments: lane j sizes segment j's JSON (a run's text escaped
+//     as one string, its props, a marker, or a standalone record with seq / client fields),
+//     a scalar loop places the segments in chunks (commas, headers, trailers: snapshotV1.ts:
+//     132-160) and, in the writing pass, lane j writes segment j at its offset.
+// Both passes rebuild the segments; pass 1 writes where pass 0 counted.
+enum : uint32_t { kSegRun = 0, kSegMarker = 1, kSegAlone = 2 };
+constexpr uint32_t kFSkip = 1, kFSettled = 2, kFText = 4, kFEndsNL = 8, kFMatch = 16, kFUndecided = 32;
+
+// one lane's output: its own segment, bytes counted (kWrite false) or stored at o[n]
+template <bool kWrite>
+struct LOut {
+    static constexpr bool kW = kWrite;
+    uint8_t *o;
+    uint32_t n;
+    __device__ __forceinline__ void put(uint32_t c) {
+        if (kWrite) o[n] = (uint8_t)c;
+        n++;
+    }
+    template <int N>
+    __device__ __forceinline__ void lit(const char (&s)[N]) {
+        if (kWrite) {
+#pragma nounroll
+            for (int i = 0; i < N - 1; i++) o[n + i] = (uint8_t)s[i];
+        }
+        n += N - 1;
+    }
+    __device__ __forceinline__ void bytes(const uint8_t *src, uint32_t len) {
+        if (kWrite)
+            for (uint32_t i = 0; i < len; i++) o[n + i] = src[i];
+        n += len;
+    }
+    // std::to_string of a 32-bit signed value
+    __device__ __forceinline__ void num(int32_t v) {
+        uint32_t u = (uint32_t)v;
+        if (v < 0) {
+            put('-');
+            u = 0u - u;
+        }
+        uint32_t nd = 1;
+        while (nd < 10 && u >= (uint32_t)kPow10[nd]) nd++;
+        if (kWrite)
+            for (uint32_t k = nd; k-- > 0;) {
+                o[n + k] = (uint8_t)('0' + u % 10u);
+                u /= 10u;
+            }
+        n += nd;
+    }
+    __device__ __forceinline__ void hex4(uint32_t c) {
+        if (kWrite) {
+            const char *hex = "0123456789abcdef";
+            o[n] = '\\';
+            o[n + 1] = 'u';
+            o[n + 2] = (uint8_t)hex[(c >> 12) & 15];
+            o[n + 3] = (uint8_t)hex[(c >> 8) & 15];
+            o[n + 4] = (uint8_t)hex[(c >> 4) & 15];
+            o[n + 5] = (uint8_t)hex[c & 15];
+        }
+        n += 6;
+    }
+    // JSON.stringify of one UTF-16 code unit that is not part of a surrogate pair
+    __device__ __forceinline__ void unit(uint32_t c) {
+        if (c == 0x22 || c == 0x5C || c == 0x08 || c == 0x0C || c == 0x0A || c == 0x0D || c == 0x09) {
+            if (kWrite) {
+                o[n] = '\\';
+                o[n + 1] = c == 0x22 ? '"' : c == 0x5C ? '\\' : c == 0x08 ? 'b' : c == 0x0C ? 'f' : c == 0x0A ? 'n'
+                                                                                    : c == 0x0D ? 'r' : 't';
+            }
+            n += 2;
+        } else if (c < 0x20 || (c >= 0xD800u && c <= 0xDFFFu)) {  // control / lone surrogate
+            hex4(c);
+        } else if (c < 0x80) {
+            put(c);
+        } else if (c < 0x800) {
+            if (kWrite) {
+                o[n] = (uint8_t)(0xC0 | (c >> 6));
+                o[n + 1] = (uint8_t)(0x80 | (c & 0x3F));
+            }
+            n += 2;
+        } else {
+            if (kWrite) {
+                o[n] = (uint8_t)(0xE0 | (c >> 12));
+                o[n + 1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+                o[n + 2] = (uint8_t)(0x80 | (c & 0x3F));
+            }
+            n += 3;
+        }
+    }
+    __device__ __forceinline__ void pair(uint32_t hi, uint32_t lo) {
+        if (kWrite) {
+            const uint32_t cp = 0x10000u + ((hi - 0xD800u) << 10) + (lo - 0xDC00u);
+            o[n] = (uint8_t)(0xF0 | (cp >> 18));
+            o[n + 1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+            o[n + 2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+            o[n + 3] = (uint8_t)(0x80 | (cp & 0x3F));
+        }
+        n += 4;
+    }
+    // the concatenated string, one unit at a time: a high surrogate waits for the next unit
+    __device__ __forceinline__ void text_unit(uint32_t c, uint32_t &hi) {
+        if (hi) {
+            if (is_lo(c)) {
+                pair(hi, c);
+                hi = 0;
+                return;
+            }
+            hex4(hi);
+            hi = 0;
+        }
+        if (is_hi(c)) hi = c;
+        else unit(c);
+    }
+};
+
+template <bool kWrite>
+struct LaneDoc {
+    const SnapParams P;  // by value: a reference to the kernel argument would copy it to scratch
+    const OutRec *rec;
+    const uint16_t *text;
+    const uint32_t *pool;
+    int32_t n_out, min_seq, cur_seq;
+    int32_t cli_first, cli_n;
+    Writer<kWrite> W;  // the wave's cursor: commas, headers, trailers
+    int32_t *mrow;
+    // chunking (as Doc)
+    int32_t nch = 0;
+    bool open = false;
+    int64_t ccount = 0, clen = 0, total_count = 0, total_len = 0;
+    int64_t seg_bytes_at_open = 0;
+    bool overflow = false;
+    int64_t all_len = 0, all_count = 0;
+    // the open run
+    bool have_prev = false, run_text = false, run_ends_nl = false;
+    int32_t run_first = 0, run_last = 0;
+    uint32_t run_len = 0, run_props = 0, run_ref = 0;
+    // queued segments, lane j = segment j: kind, first / last record, props, refType, chunk length
+    uint32_t sk = 0, sp = 0, sr = 0, sn = 0;
+    int32_t sf = 0, sl = 0;
+    int32_t nseg = 0;
+    // the last kept record of the previous tile: its props and whether it is settled text
+    uint32_t carry_props = 0;
+    bool carry_st = false;
+
+    __device__ LaneDoc(const SnapParams &p, const OutRec *r, const uint16_t *t, const uint32_t *pl, const DocOut &o,
+                       int32_t cf, int32_t cn, uint8_t *dst, int32_t *mr)
+        : P(p), rec(r), text(t), pool(pl), n_out(o.n_out), min_seq(o.min_seq), cur_seq(o.cur_seq), cli_first(cf),
+          cli_n(cn), W{dst, 0}, mrow(mr) {}
+
+    __device__ __forceinline__ uint32_t key_rank(uint32_t k) const { return k < (uint32_t)P.n_keys ? P.key_rank[k] : kNoRank; }
+    __device__ __forceinline__ bool skipped(uint32_t blk, int32_t seq, int32_t rseq) const {
+        return out_is_end(blk) || seq == kUnassignedSeq || (rseq != kNoneSeq && rseq <= min_seq);
+    }
+
+    // ---- per-lane pieces of a segment
+    template <class O>
+    __device__ __forceinline__ void str(O &w, const uint32_t *tab, uint32_t i) {
+        if (O::kW) w.bytes(P.strs + tab[2 * i], tab[2 * i + 1]);
+        else w.n += tab[2 * i + 1];
+    }
+    template <class O>
+    __device__ __forceinline__ void entry(O &w, uint32_t id, uint32_t e, bool &first) {
+        const uint32_t k = pool[id + 2 + 2 * e], v = pool[id + 3 + 2 * e];
+        if (!first) w.put(',');
+        first = false;
+        str(w, P.key_str, k < (uint32_t)P.n_keys ? k : (uint32_t)P.n_keys);
+        w.put(':');
+        str(w, P.val_str, v < (uint32_t)P.n_values ? v : 0u);
+    }
+    // JSON.stringify(properties): array-index keys ascending, then insertion order
+    template <class O>
+    __device__ __forceinline__ void props_json(O &w, uint32_t id) {
+        const uint32_t n = pool[id];
+        w.put('{');
+        bool first = true;
+        if (!O::kW) {  // the size does not depend on the order
+            for (uint32_t e = 0; e < n; e++) entry(w, id, e, first);
+            w.put('}');
+            return;
+        }
+        bool any = false;
+        for (uint32_t e = 0; e < n && !any; e++) any = key_rank(pool[id + 2 + 2 * e]) != kNoRank;
+        if (any) {
+            int64_t last = -1;
+            for (;;) {
+                uint32_t best = kNoRank, be = 0;
+                for (uint32_t e = 0; e < n; e++) {
+                    const uint32_t r = key_rank(pool[id + 2 + 2 * e]);
+                    if (r != kNoRank && (int64_t)r > last && r < best) {
+                        best = r;
+                        be = e;
+                    }
+                }
+                if (best == kNoRank) break;
+                entry(w, id, be, first);
+                last = best;
+            }
+        }
+        for (uint32_t e = 0; e < n; e++)
+            if (key_rank(pool[id + 2 + 2 * e]) == kNoRank) entry(w, id, e, first);
+        w.put('}');
+    }
+    template <class O>
+    __device__ __forceinline__ void marker(O &w, uint32_t ref, uint32_t props) {
+        w.lit("{\"marker\":{\"refType\":");
+        w.num((int32_t)ref);
+        w.put('}');
+        if (props) {
+            w.lit(",\"props\":");
+            props_json(w, props);
+        }
+        w.put('}');
+    }
+    template <class O>
+    __device__ __forceinline__ void client(O &w, uint32_t id) {
+        str(w, P.cli_str, id < (uint32_t)cli_n ? (uint32_t)cli_first + id : id == MT_CLIENT_NONCOLLAB ? 1u : 0u);
+    }
+    // the quoted text of records first..last (skipped ones left out), escaped as one string
+    template <class O>
+    __device__ __forceinline__ void text_run(O &w, int32_t first, int32_t last) {
+        w.put('"');
+        uint32_t hi = 0;
+        for (int32_t i = first; i <= last; i++) {
+            const uint4 a = reinterpret_cast<const uint4 *>(rec + i)[0];
+            const uint4 b = reinterpret_cast<const uint4 *>(rec + i)[1];
+            if (skipped(b.w, (int32_t)a.y, (int32_t)a.z)) continue;
+            const uint16_t *t = text + b.z;
+            const uint32_t len = a.x;
+            for (uint32_t k = 0; k < len; k += 8) {
+                // 8 loads in flight, then the units one at a time (packed two per word)
+                uint32_t c0, c1, c2, c3;
+                {
+                    uint32_t u[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) u[q] = k + q < len ? (uint32_t)t[k + q] : 0u;
+                    c0 = u[0] | u[1] << 16;
+                    c1 = u[2] | u[3] << 16;
+                    c2 = u[4] | u[5] << 16;
+                    c3 = u[6] | u[7] << 16;
+                }
+                const uint32_t m = min(8u, len - k);
+#pragma nounroll
+                for (uint32_t q = 0; q < m; q++) {
+                    const uint32_t wd = q < 2 ? c0 : q < 4 ? c1 : q < 6 ? c2 : c3;
+                    w.text_unit((q & 1) ? wd >> 16 : wd & 0xFFFFu, hi);
+                }
+            }
+        }
+        if (hi) w.hex4(hi);
+        w.put('"');
+    }
+    // segment (kind, first, last, props, ref) as JSON: returns its bytes (kW: stored at o)
+    template <bool kW>
+    __device__ __forceinline__ uint32_t emit(uint32_t kind, int32_t first, int32_t last, uint32_t props, uint32_t ref,
+                                             uint8_t *o) {
+        LOut<kW> w{o, 0};
+        if (kind == kSegRun) {
+            if (props) w.lit("{\"text\":");
+            text_run(w, first, last);
+            if (props) {
+                w.lit(",\"props\":");
+                props_json(w, props);
+                w.put('}');
+            }
+        } else if (kind == kSegMarker) {
+            marker(w, ref, props);
+        } else {
+            const uint4 a = reinterpret_cast<const uint4 *>(rec + first)[0];
+            const uint4 b = reinterpret_cast<const uint4 *>(rec + first)[1];
+            const int32_t seq = (int32_t)a.y, rseq = (int32_t)a.z;
+            const uint32_t meta = a.w, pr = b.y;
+            w.lit("{\"json\":");
+            if (!(meta & kMetaMarker)) {
+                if (pr) w.lit("{\"text\":");
+                text_run(w, first, first);
+                if (pr) {
+                    w.lit(",\"props\":");
+                    props_json(w, pr);
+                    w.put('}');
+                }
+            } else {
+                marker(w, b.z, pr);
+            }
+            if (seq > min_seq) {
+                w.lit(",\"seq\":");
+                w.num(seq);
+                w.lit(",\"client\":");
+                client(w, meta_cli(meta));
+            }
+            if (rseq != kNoneSeq) {
+                w.lit(",\"removedSeq\":");
+                w.num(rseq);
+                w.lit(",\"removedClient\":");
+                client(w, meta_rcli(meta));
+            }
+            w.put('}');
+        }
+        return w.n;
+    }
+
+    // matchProperties(a, c) by one lane: 1, 0, or -1 (undecided: the document goes to the host)
+    __device__ __forceinline__ int props_match_lane(uint32_t a, uint32_t c) const {
+        if (!a || !c) return a == c;
+        const uint32_t ha = pool[a + 1], hc = pool[c + 1];
+        if ((ha | hc) & kSetNever) return 0;
+        if (a == c) return 1;
+        const uint32_t na = pool[a], nc = pool[c];
+        if (na != nc) return 0;
+        if ((ha & hc & kSetRegular) && ha != hc) return 0;
+        for (uint32_t i = 0; i < na; i++) {
+            const uint32_t ka = pool[a + 2 + 2 * i], va = pool[a + 3 + 2 * i];
+            int rel = 0;
+            for (uint32_t j = 0; j < nc; j++)
+                if (pool[c + 2 + 2 * j] == ka)
+                    rel = value_rel(va, pool[c + 3 + 2 * j], P.value_class, P.value_flags, (uint32_t)P.n_values, P.exc,
+                                    P.n_exc);
+            if (rel != 1) return rel;
+        }
+        return 1;
+    }
+
+    // ---- chunks (as Doc)
+    template <class Wr>
+    __device__ __forceinline__ void header(Wr &w, int64_t count, int64_t length) {
+        w.lit("{\"version\":\"1\",\"segmentCount\":");
+        w.num(count);
+        w.lit(",\"length\":");
+        w.num(length);
+        w.lit(",\"segments\":[");
+    }
+    template <class Wr>
+    __device__ __forceinline__ void trailer(Wr &w, int32_t c, int64_t start, int32_t n_chunks, int64_t tlen,
+                                            int64_t tcount) {
+        w.lit("],\"startIndex\":");
+        w.num(start);
+        if (c == 0) {
+            w.lit(",\"headerMetadata\":{\"minSequenceNumber\":");
+            w.num(min_seq);
+            w.lit(",\"sequenceNumber\":");
+            w.num(cur_seq);
+            w.lit(",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+            for (int32_t bi = 1; bi < n_chunks; bi++) {
+                w.lit(",{\"id\":\"body_");
+                w.num(bi - 1);
+                w.lit("\"}");
+            }
+            w.lit("],\"totalLength\":");
+            w.num(tlen);
+            w.lit(",\"totalSegmentCount\":");
+            w.num(tcount);
+            w.byte('}');
+        }
+        w.byte('}');
+    }
+    __device__ __forceinline__ void open_chunk() {
+        open = true;
+        ccount = clen = 0;
+        if (kWrite) header(W, mrow[1 + 3 * nch], mrow[2 + 3 * nch]);
+        seg_bytes_at_open = W.pos;
+    }
+    __device__ __forceinline__ void close_chunk() {
+        if (nch >= kSnapMaxChunks) {
+            overflow = true;
+        } else if (kWrite) {
+            trailer(W, nch, total_count, mrow[0], all_len, all_count);
+        } else if (lane() == 0) {
+            mrow[1 + 3 * nch] = (int32_t)ccount;
+            mrow[2 + 3 * nch] = (int32_t)clen;
+            mrow[3 + 3 * nch] = (int32_t)(W.pos - seg_bytes_at_open);
+        }
+        total_count += ccount;
+        total_len += clen;
+        nch++;
+        open = false;
+    }
+
+    // ---- stage 2: place and write the queued segments
+    __device__ __forceinline__ void flush() {
+        if (nseg == 0 || overflow) return;
+        const bool mine = (int32_t)lane() < nseg;
+        uint32_t size = 0;
+        if (mine) size = emit<false>(sk, sf, sl, sp, sr, nullptr);
+        int64_t my_off = 0;
+        for (int32_t j = 0; j < nseg && !overflow; j++) {
+            const uint32_t sz = rl(size, (uint32_t)j), ln = rl(sn, (uint32_t)j);
+            if (!open) open_chunk();
+            else W.byte(',');
+            if ((int32_t)lane() == j) my_off = W.pos;
+            W.pos += sz;
+            ccount++;
+            clen += ln;
+            if (clen >= P.chunk_size) close_chunk();
+        }
+        if (kWrite && !overflow && mine) (void)emit<true>(sk, sf, sl, sp, sr, W.dst + my_off);
+        nseg = 0;
+    }
+    __device__ __forceinline__ void queue(uint32_t kind, int32_t first, int32_t last, uint32_t props, uint32_t ref,
+                                          uint32_t clen_) {
+        if ((int32_t)lane() == nseg) {
+            sk = kind;
+            sf = first;
+            sl = last;
+            sp = props;
+            sr = ref;
+            sn = clen_;
+        }
+        if (++nseg == 64) flush();
+    }
+    __device__ __forceinline__ void push_prev() {
+        if (!have_prev) return;
+        have_prev = false;
+        queue(run_text ? kSegRun : kSegMarker, run_first, run_last, run_props, run_ref, run_text ? run_len : 1u);
+    }
+
+    // ---- stage 1
+    __device__ __forceinline__ void walk() {
+        for (int32_t base = 0; base < n_out && !overflow; base += 64) {
+            const int32_t i = base + (int32_t)lane();
+            uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, kOutBlockEnd);
+            if (i < n_out) {
+                a = reinterpret_cast<const uint4 *>(rec + i)[0];
+                b = reinterpret_cast<const uint4 *>(rec + i)[1];
+            }
+            const uint32_t len = a.x, meta = a.w, props = b.y, toff = b.z;
+            const int32_t seq = (int32_t)a.y, rseq = (int32_t)a.z;
+            const bool skip = skipped(b.w, seq, rseq);
+            const bool txt = !(meta & kMetaMarker);
+            const bool settled = !skip && seq <= min_seq && rseq == kNoneSeq;
+            bool nl = false;
+            if (settled && txt && len > 0) nl = text[toff + len - 1] == 0x0Au;
+            // the previous kept record (this tile, or the previous tile's last)
+            const uint64_t kept = __ballot(!skip);
+            const uint64_t below = kept & ((1ull << lane()) - 1ull);
+            const int p = below ? 63 - __builtin_clzll(below) : 0;
+            const uint32_t pprops = (uint32_t)__shfl((int)props, p, 64);
+            const bool pst = (bool)__shfl((int)(settled && txt), p, 64);
+            const uint32_t prev_props = below ? pprops : carry_props;
+            const bool prev_st = below ? pst : carry_st;
+            int m = 0;
+            if (settled && txt && prev_st) m = props_match_lane(prev_props, props);
+            const uint32_t f = (skip ? kFSkip : 0u) | (settled ? kFSettled : 0u) | (txt ? kFText : 0u) |
+                               (nl ? kFEndsNL : 0u) | (m == 1 ? kFMatch : 0u) | (m < 0 ? kFUndecided : 0u);
+            if (kept) {
+                const uint32_t lk = 63u - (uint32_t)__builtin_clzll(kept);
+                carry_props = rl(props, lk);
+                carry_st = (rl(f, lk) & (kFSettled | kFText)) == (kFSettled | kFText);
+            }
+            const int32_t hi = min(64, n_out - base);
+            for (int32_t j = 0; j < hi && !overflow; j++) {
+                const uint32_t fj = rl(f, (uint32_t)j);
+                if (fj & kFSkip) continue;
+                const uint32_t lj = rl(len, (uint32_t)j), pj = rl(props, (uint32_t)j), tj = rl(toff, (uint32_t)j);
+                const int32_t idx = base + j;
+                if (fj & kFSettled) {
+                    if (have_prev) {
+                        const bool can = run_text && (fj & kFText) && !run_ends_nl &&
+                                         (run_len <= kGranularity || lj <= kGranularity);
+                        if (can && (fj & kFUndecided)) {
+                            overflow = true;
+                            break;
+                        }
+                        if (can && (fj & kFMatch)) {
+                            run_last = idx;
+                            run_len += lj;
+                            if (lj > 0) run_ends_nl = (fj & kFEndsNL) != 0;
+                            continue;
+                        }
+                        push_prev();
+                    }
+                    have_prev = true;  // set_prev
+                    run_text = (fj & kFText) != 0;
+                    run_first = run_last = idx;
+                    run_len = run_text ? lj : 0u;
+                    run_props = pj;
+                    run_ref = tj;
+                    run_ends_nl = (fj & kFEndsNL) != 0;
+                } else {
+                    push_prev();
+                    queue(kSegAlone, idx, idx, pj, tj, lj);
+                }
+            }
+        }
+        if (overflow) return;
+        push_prev();
+        flush();
+        if (!overflow && (open || nch == 0)) {
+            if (!open) open_chunk();
+            close_chunk();
+        }
+    }
+};
+
+template <bool kWrite>
+__device__ __forceinline__ void snapshot_doc_lanes(const SnapParams &P, int64_t w) {
+    const int64_t d = P.doc_list ? P.doc_list[w] : w;
+    if (kWrite && P.bytes[d] < 0) return;
+    const DocOut o = P.doc_out[w];
+    int32_t cf = P.cli_first, cn = P.cli_n;
+    if (P.doc_cli) {
+        cf = P.doc_cli[2 * d];
+        cn = P.doc_cli[2 * d + 1];
+    }
+    int32_t *mrow = P.meta + d * (int64_t)kSnapMeta;
+    LaneDoc<kWrite> D(P, P.out + w * (int64_t)P.out_cap, P.text + P.doc_text_base[d], P.pool + P.doc_pool_base[d], o,
+                      cf, cn, kWrite ? P.dst + P.dst_off[d] : nullptr, mrow);
+    if (kWrite)
+        for (int32_t c = 0; c < mrow[0]; c++) {
+            D.all_count += mrow[1 + 3 * c];
+            D.all_len += mrow[2 + 3 * c];
+        }
+    D.walk();
+    if (kWrite) return;
+    int64_t total = 0;
+    if (!D.overflow) {
+        Writer<false> f{nullptr, 0};
+        int64_t start = 0;
+        for (int32_t c = 0; c < D.nch; c++) {
+            const int64_t cnt = mrow[1 + 3 * c], len = mrow[2 + 3 * c];
+            f.pos = mrow[3 + 3 * c];
+            D.header(f, cnt, len);
+            D.trailer(f, c, start, D.nch, D.total_len, D.total_count);
+            if (lane() == 0) mrow[3 + 3 * c] = (int32_t)f.pos;
+            total += f.pos;
+            start += cnt;
+        }
+    }
+    if (lane() == 0) {
+        mrow[0] = D.overflow ? 0 : D.nch;
+        P.bytes[d] = D.overflow ? -1 : total;
+    }
+}
+
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mt_snapshot_kernel(SnapParams P) {
+// the serial walker (one record at a time across the wave): kept for A/B (MT_SNAP_SERIAL=1)
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mt_snapshot_serial_kernel(SnapParams P) {
     const int64_t w = blockIdx.x;
     if (w >= P.n || !P.final_mask[w]) return;
     if (P.pass) snapshot_doc<true>(P, w);
     else snapshot_doc<false>(P, w);
+}
+
+// pass 0 (sizes) and pass 1 (writes): separate kernels, each with its own register budget
+extern "C" __global__ __launch_bounds__(64) void mt_snapshot_size_kernel(SnapParams P) {
+    const int64_t w = blockIdx.x;
+    if (w >= P.n || !P.final_mask[w]) return;
+    snapshot_doc_lanes<false>(P, w);
+}
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mt_snapshot_kernel(SnapParams P) {
+    const int64_t w = blockIdx.x;
+    if (w >= P.n || !P.final_mask[w]) return;
+    snapshot_doc_lanes<true>(P, w);
 }
 
 }  // namespace mt
