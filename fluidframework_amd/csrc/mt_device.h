@@ -220,6 +220,7 @@ constexpr int kRegenOpWords = 8;
 constexpr int kConsHdr = 8;
 constexpr int kConsLis = 5;
 constexpr uint32_t kCombineConsensusAck = 4u;  // props_extend: updateConsensusProperty's re-combine
+constexpr uint32_t kCombineConsensusLocal = 5u;  // props_extend: a local consensus (seq -1)
 constexpr int64_t cons_words(int64_t n_ids, int64_t n_lis) { return kConsHdr + n_ids + kConsLis * n_lis; }
 
 // checkpoint image of one document (u32 words): header + the used prefix of every LDS table

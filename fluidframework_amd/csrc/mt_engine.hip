@@ -1942,6 +1942,7 @@ struct Engine {
                 // incr: `v += undefined` is NaN for a number / boolean; a string or object would
                 // concatenate "undefined" (not modelled on the device).  consensus of an object
                 // with seq === -1 would update a shared object in place.
+                // (a local consensus sets such an object's seq to -1: no change, kCombineConsensusLocal)
                 bad = ckind == MT_COMBINE_INCR ? (!(f & kVNum) || res.key >= nv)
                                                : ((ckind == MT_COMBINE_CONSENSUS || ckind == kCombineConsensusAck) &&
                                                   (f & kVSeqM1));
@@ -2956,8 +2957,9 @@ struct Engine {
                         nid = rdl(memo_new, m);
                         nh = rdl(memo_h, m);
                     } else {
+                        const uint32_t ck = MT_OPF_COMBINE(op.flags);
                         nid = props_extend(old, props_in + op.payload, op.payload_len, rewrite, nh,
-                                           MT_OPF_COMBINE(op.flags));
+                                           local && ck == MT_COMBINE_CONSENSUS ? kCombineConsensusLocal : ck);
                         if (status) return;
                         if (memo_n < 64u) {
                             if ((uint32_t)lane == memo_n) {

@@ -102,8 +102,15 @@ def test_consensus_writers_and_local_relative_positions(opts):
     with fa.ReplayBatch(len(docs), **opts) as b:
         b.ingest_messages(docs, observer=names)
         b.run()
+        cnt = b.counters()
         for i, od in enumerate(want):
             dv = b.doc(i)
+            if dv.status != od.status:  # name the record the device stopped at
+                from fluidframework_amd import oplog
+                p = oplog.Packer()
+                p.add_document(docs[i], names[i])
+                rec = p.finish().ops[int(cnt.fail_op[i])] if cnt.fail_op[i] >= 0 else None
+                assert False, (i, names[i], fa.status_string(dv.status), int(cnt.fail_op[i]), rec)
             assert_same(dv, od, f"{i} {names[i]}")
             if od.status == 0:
                 assert dv.consensus_events() == od.consensus_events(), i
