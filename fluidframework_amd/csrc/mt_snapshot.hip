@@ -577,29 +577,39 @@ __device__ __forceinline__ void snapshot_doc(const SnapParams &P, int64_t w) {
 //     132-160) and, in the writing pass, lane j writes segment j at its offset.
 // Both passes rebuild the segments; pass 1 writes where pass 0 counted.
 enum : uint32_t { kSegRun = 0, kSegMarker = 1, kSegAlone = 2 };
-constexpr uint32_t kFSkip = 1, kFSettled = 2, kFText = 4, kFEndsNL = 8, kFMatch = 16, kFUndecided = 32;
+constexpr uint32_t kFSkip = 1, kFSettled = 2, kFText = 4, kFEndsNL = 8, kFMatch = 16, kFUndecided = 32,
+                   kFFirstLo = 64, kFLastHi = 128;
 
 // one lane's output: its own segment, bytes counted (kWrite false) or stored at o[n]
-template <bool kWrite>
+// one lane's output: bytes counted, and stored at o[n] when o is set (the writing pass)
 struct LOut {
-    static constexpr bool kW = kWrite;
     uint8_t *o;
     uint32_t n;
     __device__ __forceinline__ void put(uint32_t c) {
-        if (kWrite) o[n] = (uint8_t)c;
+        if (o) o[n] = (uint8_t)c;
         n++;
     }
+    // a literal: its bytes are immediates (no loads), one store each
     template <int N>
     __device__ __forceinline__ void lit(const char (&s)[N]) {
-        if (kWrite) {
-#pragma nounroll
+        if (o) {
+#pragma unroll
             for (int i = 0; i < N - 1; i++) o[n + i] = (uint8_t)s[i];
         }
         n += N - 1;
     }
+    // a table string: eight loads in flight, then their stores (the source is read-only, but a
+    // byte store may alias it as far as the compiler knows)
     __device__ __forceinline__ void bytes(const uint8_t *src, uint32_t len) {
-        if (kWrite)
-            for (uint32_t i = 0; i < len; i++) o[n + i] = src[i];
+        if (o)
+            for (uint32_t i = 0; i < len; i += 8) {
+                uint32_t t[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) t[q] = i + q < len ? src[i + q] : 0u;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (i + q < len) o[n + i + q] = (uint8_t)t[q];
+            }
         n += len;
     }
     // std::to_string of a 32-bit signed value
@@ -609,80 +619,70 @@ struct LOut {
             put('-');
             u = 0u - u;
         }
-        uint32_t nd = 1;
-        while (nd < 10 && u >= (uint32_t)kPow10[nd]) nd++;
-        if (kWrite)
+        const uint32_t nd = 1u + (u >= 10u) + (u >= 100u) + (u >= 1000u) + (u >= 10000u) + (u >= 100000u) +
+                            (u >= 1000000u) + (u >= 10000000u) + (u >= 100000000u) + (u >= 1000000000u);
+        if (o)
             for (uint32_t k = nd; k-- > 0;) {
                 o[n + k] = (uint8_t)('0' + u % 10u);
                 u /= 10u;
             }
         n += nd;
     }
-    __device__ __forceinline__ void hex4(uint32_t c) {
-        if (kWrite) {
-            const char *hex = "0123456789abcdef";
-            o[n] = '\\';
-            o[n + 1] = 'u';
-            o[n + 2] = (uint8_t)hex[(c >> 12) & 15];
-            o[n + 3] = (uint8_t)hex[(c >> 8) & 15];
-            o[n + 4] = (uint8_t)hex[(c >> 4) & 15];
-            o[n + 5] = (uint8_t)hex[c & 15];
-        }
-        n += 6;
-    }
-    // JSON.stringify of one UTF-16 code unit that is not part of a surrogate pair
-    __device__ __forceinline__ void unit(uint32_t c) {
-        if (c == 0x22 || c == 0x5C || c == 0x08 || c == 0x0C || c == 0x0A || c == 0x0D || c == 0x09) {
-            if (kWrite) {
-                o[n] = '\\';
-                o[n + 1] = c == 0x22 ? '"' : c == 0x5C ? '\\' : c == 0x08 ? 'b' : c == 0x0C ? 'f' : c == 0x0A ? 'n'
-                                                                                    : c == 0x0D ? 'r' : 't';
-            }
-            n += 2;
-        } else if (c < 0x20 || (c >= 0xD800u && c <= 0xDFFFu)) {  // control / lone surrogate
-            hex4(c);
-        } else if (c < 0x80) {
-            put(c);
-        } else if (c < 0x800) {
-            if (kWrite) {
-                o[n] = (uint8_t)(0xC0 | (c >> 6));
-                o[n + 1] = (uint8_t)(0x80 | (c & 0x3F));
-            }
-            n += 2;
-        } else {
-            if (kWrite) {
-                o[n] = (uint8_t)(0xE0 | (c >> 12));
-                o[n + 1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
-                o[n + 2] = (uint8_t)(0x80 | (c & 0x3F));
-            }
-            n += 3;
-        }
-    }
-    __device__ __forceinline__ void pair(uint32_t hi, uint32_t lo) {
-        if (kWrite) {
-            const uint32_t cp = 0x10000u + ((hi - 0xD800u) << 10) + (lo - 0xDC00u);
-            o[n] = (uint8_t)(0xF0 | (cp >> 18));
-            o[n + 1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
-            o[n + 2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
-            o[n + 3] = (uint8_t)(0x80 | (cp & 0x3F));
-        }
-        n += 4;
-    }
-    // the concatenated string, one unit at a time: a high surrogate waits for the next unit
-    __device__ __forceinline__ void text_unit(uint32_t c, uint32_t &hi) {
-        if (hi) {
-            if (is_lo(c)) {
-                pair(hi, c);
-                hi = 0;
-                return;
-            }
-            hex4(hi);
-            hi = 0;
-        }
-        if (is_hi(c)) hi = c;
-        else unit(c);
-    }
 };
+
+// per-wave LDS of the batch text pass (one wave per workgroup): per record of a 64-record sub-tile
+// its escaped bytes / output offset / prefix of bytes before it; per segment of the batch its text
+// bytes (sizing) or its next free text byte (writing)
+__shared__ uint32_t s_rt[64], s_ro[64], s_rx[64], s_seg[64];
+
+// JSON bytes of code unit c of one record's text, given its neighbours in the record (0: none)
+__device__ __forceinline__ uint32_t unit_bytes(uint32_t c, uint32_t p, uint32_t nx) {
+    if (c == 0x22 || c == 0x5C || c == 0x08 || c == 0x0C || c == 0x0A || c == 0x0D || c == 0x09) return 2;
+    if (c < 0x20) return 6;
+    if (is_hi(c)) return is_lo(nx) ? 4 : 6;
+    if (is_lo(c)) return is_hi(p) ? 0 : 6;
+    return c < 0x80 ? 1 : c < 0x800 ? 2 : 3;
+}
+__device__ __forceinline__ void unit_write(uint8_t *o, uint32_t nb, uint32_t c, uint32_t nx) {
+    const char *hex = "0123456789abcdef";
+    if (nb == 2 && c < 0x80) {
+        o[0] = '\\';
+        o[1] = c == 0x22 ? '"' : c == 0x5C ? '\\' : c == 0x08 ? 'b' : c == 0x0C ? 'f' : c == 0x0A ? 'n' : c == 0x0D ? 'r' : 't';
+    } else if (nb == 6) {
+        o[0] = '\\';
+        o[1] = 'u';
+        o[2] = (uint8_t)hex[(c >> 12) & 15];
+        o[3] = (uint8_t)hex[(c >> 8) & 15];
+        o[4] = (uint8_t)hex[(c >> 4) & 15];
+        o[5] = (uint8_t)hex[c & 15];
+    } else if (nb == 4) {
+        const uint32_t cp = 0x10000u + ((c - 0xD800u) << 10) + (nx - 0xDC00u);
+        o[0] = (uint8_t)(0xF0 | (cp >> 18));
+        o[1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+        o[2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+        o[3] = (uint8_t)(0x80 | (cp & 0x3F));
+    } else if (nb == 1) {
+        o[0] = (uint8_t)c;
+    } else if (nb == 2) {
+        o[0] = (uint8_t)(0xC0 | (c >> 6));
+        o[1] = (uint8_t)(0x80 | (c & 0x3F));
+    } else if (nb == 3) {
+        o[0] = (uint8_t)(0xE0 | (c >> 12));
+        o[1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+        o[2] = (uint8_t)(0x80 | (c & 0x3F));
+    }
+}
+
+// MT_SNAP_PROF builds: cycles per phase of the lane-parallel serializer, per document, in the
+// tail of its meta row (pass 0 at [kSnapMeta-5, kSnapMeta), pass 1 at [kSnapMeta-10, kSnapMeta-5),
+// in units of 64 cycles): tile loads / flags, the record loop, segment framing, text, placement
+#ifdef MT_SNAP_PROF
+#define SNAP_T0() const uint64_t t0_ = __builtin_readcyclecounter()
+#define SNAP_ADD(k) pf[k] += __builtin_readcyclecounter() - t0_
+#else
+#define SNAP_T0()
+#define SNAP_ADD(k)
+#endif
 
 template <bool kWrite>
 struct LaneDoc {
@@ -702,7 +702,7 @@ struct LaneDoc {
     bool overflow = false;
     int64_t all_len = 0, all_count = 0;
     // the open run
-    bool have_prev = false, run_text = false, run_ends_nl = false;
+    bool have_prev = false, run_text = false, run_ends_nl = false, run_hi = false;
     int32_t run_first = 0, run_last = 0;
     uint32_t run_len = 0, run_props = 0, run_ref = 0;
     // queued segments, lane j = segment j: kind, first / last record, props, refType, chunk length
@@ -712,6 +712,9 @@ struct LaneDoc {
     // the last kept record of the previous tile: its props and whether it is settled text
     uint32_t carry_props = 0;
     bool carry_st = false;
+#ifdef MT_SNAP_PROF
+    uint64_t pf[5] = {0, 0, 0, 0, 0};
+#endif
 
     __device__ LaneDoc(const SnapParams &p, const OutRec *r, const uint16_t *t, const uint32_t *pl, const DocOut &o,
                        int32_t cf, int32_t cn, uint8_t *dst, int32_t *mr)
@@ -726,7 +729,7 @@ struct LaneDoc {
     // ---- per-lane pieces of a segment
     template <class O>
     __device__ __forceinline__ void str(O &w, const uint32_t *tab, uint32_t i) {
-        if (O::kW) w.bytes(P.strs + tab[2 * i], tab[2 * i + 1]);
+        if (w.o) w.bytes(P.strs + tab[2 * i], tab[2 * i + 1]);
         else w.n += tab[2 * i + 1];
     }
     template <class O>
@@ -744,7 +747,7 @@ struct LaneDoc {
         const uint32_t n = pool[id];
         w.put('{');
         bool first = true;
-        if (!O::kW) {  // the size does not depend on the order
+        if (!w.o) {  // the size does not depend on the order
             for (uint32_t e = 0; e < n; e++) entry(w, id, e, first);
             w.put('}');
             return;
@@ -786,72 +789,47 @@ struct LaneDoc {
     __device__ __forceinline__ void client(O &w, uint32_t id) {
         str(w, P.cli_str, id < (uint32_t)cli_n ? (uint32_t)cli_first + id : id == MT_CLIENT_NONCOLLAB ? 1u : 0u);
     }
-    // the quoted text of records first..last (skipped ones left out), escaped as one string
-    template <class O>
-    __device__ __forceinline__ void text_run(O &w, int32_t first, int32_t last) {
-        w.put('"');
-        uint32_t hi = 0;
-        for (int32_t i = first; i <= last; i++) {
-            const uint4 a = reinterpret_cast<const uint4 *>(rec + i)[0];
-            const uint4 b = reinterpret_cast<const uint4 *>(rec + i)[1];
-            if (skipped(b.w, (int32_t)a.y, (int32_t)a.z)) continue;
-            const uint16_t *t = text + b.z;
-            const uint32_t len = a.x;
-            for (uint32_t k = 0; k < len; k += 8) {
-                // 8 loads in flight, then the units one at a time (packed two per word)
-                uint32_t c0, c1, c2, c3;
-                {
-                    uint32_t u[8];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) u[q] = k + q < len ? (uint32_t)t[k + q] : 0u;
-                    c0 = u[0] | u[1] << 16;
-                    c1 = u[2] | u[3] << 16;
-                    c2 = u[4] | u[5] << 16;
-                    c3 = u[6] | u[7] << 16;
-                }
-                const uint32_t m = min(8u, len - k);
-#pragma nounroll
-                for (uint32_t q = 0; q < m; q++) {
-                    const uint32_t wd = q < 2 ? c0 : q < 4 ? c1 : q < 6 ? c2 : c3;
-                    w.text_unit((q & 1) ? wd >> 16 : wd & 0xFFFFu, hi);
-                }
-            }
-        }
-        if (hi) w.hex4(hi);
-        w.put('"');
-    }
-    // segment (kind, first, last, props, ref) as JSON: returns its bytes (kW: stored at o)
-    template <bool kW>
-    __device__ __forceinline__ uint32_t emit(uint32_t kind, int32_t first, int32_t last, uint32_t props, uint32_t ref,
-                                             uint8_t *o) {
-        LOut<kW> w{o, 0};
-        if (kind == kSegRun) {
-            if (props) w.lit("{\"text\":");
-            text_run(w, first, last);
-            if (props) {
-                w.lit(",\"props\":");
-                props_json(w, props);
-                w.put('}');
-            }
-        } else if (kind == kSegMarker) {
-            marker(w, ref, props);
-        } else {
+    // a segment's JSON around its text: `pre` bytes, the text (tb bytes: text_pass), `post` bytes
+    // (a marker: all `pre`, then a standalone one's seq / client fields in `post`).  o: the
+    // segment's first byte in the writing pass, null when sizing.
+    __device__ __forceinline__ void frame(uint32_t kind, int32_t first, uint32_t props, uint32_t ref, uint8_t *o,
+                                          uint32_t tb, uint32_t &pre, uint32_t &post) {
+        int32_t seq = 0, rseq = kNoneSeq;
+        uint32_t meta = 0;
+        const bool alone = kind == kSegAlone;
+        if (alone) {
             const uint4 a = reinterpret_cast<const uint4 *>(rec + first)[0];
             const uint4 b = reinterpret_cast<const uint4 *>(rec + first)[1];
-            const int32_t seq = (int32_t)a.y, rseq = (int32_t)a.z;
-            const uint32_t meta = a.w, pr = b.y;
-            w.lit("{\"json\":");
-            if (!(meta & kMetaMarker)) {
-                if (pr) w.lit("{\"text\":");
-                text_run(w, first, first);
-                if (pr) {
-                    w.lit(",\"props\":");
-                    props_json(w, pr);
-                    w.put('}');
-                }
-            } else {
-                marker(w, b.z, pr);
-            }
+            seq = (int32_t)a.y;
+            rseq = (int32_t)a.z;
+            meta = a.w;
+            props = b.y;
+            ref = b.z;
+        }
+        const bool txt = kind == kSegRun || (alone && !(meta & kMetaMarker));
+        LOut w{o, 0};
+        if (alone) w.lit("{\"json\":");
+        if (txt) {
+            if (props) w.lit("{\"text\":");
+            w.put('"');
+            pre = w.n;
+            w = LOut{o ? o + pre + tb : nullptr, 0};  // after the text
+            w.put('"');
+        } else {
+            w.lit("{\"marker\":{\"refType\":");
+            w.num((int32_t)ref);
+            w.put('}');
+        }
+        if (props) {
+            w.lit(",\"props\":");
+            props_json(w, props);
+        }
+        if (!txt || props) w.put('}');
+        if (!txt) {
+            pre = w.n;
+            w = LOut{o ? o + pre : nullptr, 0};
+        }
+        if (alone) {
             if (seq > min_seq) {
                 w.lit(",\"seq\":");
                 w.num(seq);
@@ -866,7 +844,91 @@ struct LaneDoc {
             }
             w.put('}');
         }
-        return w.n;
+        post = w.n;
+    }
+
+    // The text of the batch's records R0..R1, one 64-record sub-tile at a time, 64 code units per
+    // step across the wave (unit u of the sub-tile's concatenated texts: its record by a search of
+    // the records' unit offsets).  Sizing adds every record's escaped bytes to its segment
+    // (s_seg[j]); writing gives every record, in order, its segment's next text byte (s_seg[j]) and
+    // stores each unit there plus the bytes before it in the record.  Surrogate pairs are joined
+    // within a record; walk() sends a document whose run joins one across records to the host.
+    __device__ __forceinline__ void text_pass(int32_t R0, int32_t R1, bool kW) {
+        for (int32_t base = R0; base <= R1; base += 64) {
+            const int32_t i = base + (int32_t)lane();
+            uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, kOutBlockEnd);
+            if (i <= R1) {
+                a = reinterpret_cast<const uint4 *>(rec + i)[0];
+                b = reinterpret_cast<const uint4 *>(rec + i)[1];
+            }
+            int j = 0;  // the batch segment holding record i: the last j with sf_j <= i
+            for (int st = 32; st > 0; st >>= 1) {
+                const int c = j + st;
+                const int32_t f = __shfl(sf, c < 64 ? c : 63, 64);
+                if (c < nseg && f <= i) j = c;
+            }
+            const uint32_t kj = (uint32_t)__shfl((int)sk, j, 64);
+            const bool has = i <= R1 && !skipped(b.w, (int32_t)a.y, (int32_t)a.z) && !(a.w & kMetaMarker) &&
+                             kj != kSegMarker;
+            const uint32_t L = has ? a.x : 0u, toff = b.z;
+            uint32_t tot;
+            const uint32_t ex = wave_excl_scan(L, &tot);
+            s_rt[lane()] = 0u;
+            __syncthreads();
+#pragma nounroll
+            for (int pass = 0; pass < (kW ? 2 : 1); pass++) {
+                uint32_t G = 0;
+                for (uint32_t s0 = 0; s0 < tot; s0 += 64) {
+                    const uint32_t u = s0 + lane();
+                    int r = 0;  // the record of unit u: the last r with ex_r <= u
+                    for (int st = 32; st > 0; st >>= 1) {
+                        const int c = r + st;
+                        const uint32_t e = (uint32_t)__shfl((int)ex, c < 64 ? c : 63, 64);
+                        if (c < 64 && e <= u) r = c;
+                    }
+                    const uint32_t k = u - (uint32_t)__shfl((int)ex, r, 64);
+                    const uint32_t rt = (uint32_t)__shfl((int)toff, r, 64), rn = (uint32_t)__shfl((int)L, r, 64);
+                    uint32_t c = 0, p = 0, nx = 0, nb = 0;
+                    if (u < tot) {
+                        c = text[rt + k];
+                        if (k > 0) p = text[rt + k - 1];
+                        if (k + 1 < rn) nx = text[rt + k + 1];
+                        nb = unit_bytes(c, p, nx);
+                    }
+                    if (pass == 0) {
+                        if (u < tot) atomicAdd(&s_rt[r], nb);
+                    } else {
+                        uint32_t st;
+                        const uint32_t e = wave_excl_scan(nb, &st);
+                        if (nb) unit_write(W.dst + s_ro[r] + (G + e - s_rx[r]), nb, c, nx);
+                        G += st;
+                    }
+                }
+                __syncthreads();
+                if (pass == 0) {
+                    const uint32_t myrt = s_rt[lane()];
+                    if (!kW) {
+                        if (has) atomicAdd(&s_seg[j], myrt);
+                    } else {
+                        // record offsets, in record order: each takes its segment's next text byte
+                        // (the cursors lane-distributed: lane j holds segment j's)
+                        uint32_t cur = s_seg[lane()], ro = 0;
+                        for (uint64_t m = __ballot(has); m; m &= m - 1) {
+                            const uint32_t q = (uint32_t)__builtin_ctzll(m);
+                            const uint32_t jq = rl((uint32_t)j, q), t = rl(myrt, q);
+                            const uint32_t cq = rl(cur, jq);
+                            if (lane() == q) ro = cq;
+                            if (lane() == jq) cur = cq + t;
+                        }
+                        s_seg[lane()] = cur;
+                        uint32_t xt;
+                        s_ro[lane()] = ro;
+                        s_rx[lane()] = wave_excl_scan(myrt, &xt);
+                    }
+                    __syncthreads();
+                }
+            }
+        }
     }
 
     // matchProperties(a, c) by one lane: 1, 0, or -1 (undecided: the document goes to the host)
@@ -878,6 +940,33 @@ struct LaneDoc {
         const uint32_t na = pool[a], nc = pool[c];
         if (na != nc) return 0;
         if ((ha & hc & kSetRegular) && ha != hc) return 0;
+        if (na <= 8) {  // both sets' pairs loaded at once, compared in registers
+            uint32_t ka[8], va[8], kc[8], vc[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const bool in = (uint32_t)q < na;
+                ka[q] = in ? pool[a + 2 + 2 * q] : 0u;
+                va[q] = in ? pool[a + 3 + 2 * q] : 0u;
+                kc[q] = in ? pool[c + 2 + 2 * q] : 0u;
+                vc[q] = in ? pool[c + 3 + 2 * q] : 0u;
+            }
+            int res = 1;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                if ((uint32_t)q >= na || res != 1) continue;
+                uint32_t vb = 0xFFFFFFFFu;
+                bool found = false;
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+                    if ((uint32_t)r < nc && kc[r] == ka[q]) {
+                        vb = vc[r];
+                        found = true;
+                    }
+                res = found ? value_rel(va[q], vb, P.value_class, P.value_flags, (uint32_t)P.n_values, P.exc, P.n_exc)
+                            : 0;
+            }
+            return res;
+        }
         for (uint32_t i = 0; i < na; i++) {
             const uint32_t ka = pool[a + 2 + 2 * i], va = pool[a + 3 + 2 * i];
             int rel = 0;
@@ -949,20 +1038,41 @@ struct LaneDoc {
     __device__ __forceinline__ void flush() {
         if (nseg == 0 || overflow) return;
         const bool mine = (int32_t)lane() < nseg;
-        uint32_t size = 0;
-        if (mine) size = emit<false>(sk, sf, sl, sp, sr, nullptr);
+        const int32_t R0 = (int32_t)rl((uint32_t)sf, 0u), R1 = (int32_t)rl((uint32_t)sl, (uint32_t)(nseg - 1));
+        uint32_t pre = 0, post = 0, tb = 0;
         int64_t my_off = 0;
-        for (int32_t j = 0; j < nseg && !overflow; j++) {
-            const uint32_t sz = rl(size, (uint32_t)j), ln = rl(sn, (uint32_t)j);
-            if (!open) open_chunk();
-            else W.byte(',');
-            if ((int32_t)lane() == j) my_off = W.pos;
-            W.pos += sz;
-            ccount++;
-            clen += ln;
-            if (clen >= P.chunk_size) close_chunk();
+        // sizing, then (writing pass) the framing and the text at the placed offsets
+#pragma nounroll
+        for (int wr = 0; wr < (kWrite ? 2 : 1) && !overflow; wr++) {
+            {
+                SNAP_T0();
+                if (mine) frame(sk, sf, sp, sr, wr ? W.dst + my_off : nullptr, tb, pre, post);
+                __syncthreads();
+                SNAP_ADD(2);
+            }
+            s_seg[lane()] = wr && mine ? (uint32_t)(my_off + pre) : 0u;
+            __syncthreads();
+            {
+                SNAP_T0();
+                text_pass(R0, R1, wr != 0);
+                SNAP_ADD(3);
+            }
+            if (wr) break;
+            tb = mine ? s_seg[lane()] : 0u;
+            const uint32_t size = pre + tb + post;
+            SNAP_T0();
+            for (int32_t j = 0; j < nseg && !overflow; j++) {
+                const uint32_t sz = rl(size, (uint32_t)j), ln = rl(sn, (uint32_t)j);
+                if (!open) open_chunk();
+                else W.byte(',');
+                if ((int32_t)lane() == j) my_off = W.pos;
+                W.pos += sz;
+                ccount++;
+                clen += ln;
+                if (clen >= P.chunk_size) close_chunk();
+            }
+            SNAP_ADD(4);
         }
-        if (kWrite && !overflow && mine) (void)emit<true>(sk, sf, sl, sp, sr, W.dst + my_off);
         nseg = 0;
     }
     __device__ __forceinline__ void queue(uint32_t kind, int32_t first, int32_t last, uint32_t props, uint32_t ref,
@@ -975,7 +1085,7 @@ struct LaneDoc {
             sr = ref;
             sn = clen_;
         }
-        if (++nseg == 64) flush();
+        ++nseg;
     }
     __device__ __forceinline__ void push_prev() {
         if (!have_prev) return;
@@ -986,6 +1096,9 @@ struct LaneDoc {
     // ---- stage 1
     __device__ __forceinline__ void walk() {
         for (int32_t base = 0; base < n_out && !overflow; base += 64) {
+#ifdef MT_SNAP_PROF
+            const uint64_t tt_ = __builtin_readcyclecounter();
+#endif
             const int32_t i = base + (int32_t)lane();
             uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, kOutBlockEnd);
             if (i < n_out) {
@@ -997,8 +1110,13 @@ struct LaneDoc {
             const bool skip = skipped(b.w, seq, rseq);
             const bool txt = !(meta & kMetaMarker);
             const bool settled = !skip && seq <= min_seq && rseq == kNoneSeq;
-            bool nl = false;
-            if (settled && txt && len > 0) nl = text[toff + len - 1] == 0x0Au;
+            bool nl = false, flo = false, lhi = false;
+            if (settled && txt && len > 0) {
+                const uint32_t fc = text[toff], lc = text[toff + len - 1];
+                nl = lc == 0x0Au;
+                flo = is_lo(fc);
+                lhi = is_hi(lc);
+            }
             // the previous kept record (this tile, or the previous tile's last)
             const uint64_t kept = __ballot(!skip);
             const uint64_t below = kept & ((1ull << lane()) - 1ull);
@@ -1010,50 +1128,86 @@ struct LaneDoc {
             int m = 0;
             if (settled && txt && prev_st) m = props_match_lane(prev_props, props);
             const uint32_t f = (skip ? kFSkip : 0u) | (settled ? kFSettled : 0u) | (txt ? kFText : 0u) |
-                               (nl ? kFEndsNL : 0u) | (m == 1 ? kFMatch : 0u) | (m < 0 ? kFUndecided : 0u);
+                               (nl ? kFEndsNL : 0u) | (m == 1 ? kFMatch : 0u) | (m < 0 ? kFUndecided : 0u) |
+                               (flo ? kFFirstLo : 0u) | (lhi ? kFLastHi : 0u);
             if (kept) {
                 const uint32_t lk = 63u - (uint32_t)__builtin_clzll(kept);
                 carry_props = rl(props, lk);
                 carry_st = (rl(f, lk) & (kFSettled | kFText)) == (kFSettled | kFText);
             }
             const int32_t hi = min(64, n_out - base);
-            for (int32_t j = 0; j < hi && !overflow; j++) {
-                const uint32_t fj = rl(f, (uint32_t)j);
-                if (fj & kFSkip) continue;
-                const uint32_t lj = rl(len, (uint32_t)j), pj = rl(props, (uint32_t)j), tj = rl(toff, (uint32_t)j);
-                const int32_t idx = base + j;
-                if (fj & kFSettled) {
-                    if (have_prev) {
-                        const bool can = run_text && (fj & kFText) && !run_ends_nl &&
-                                         (run_len <= kGranularity || lj <= kGranularity);
-                        if (can && (fj & kFUndecided)) {
-                            overflow = true;
-                            break;
+            const bool last = base + 64 >= n_out;
+#ifdef MT_SNAP_PROF
+            pf[0] += __builtin_readcyclecounter() - tt_;
+            const uint64_t tl_ = __builtin_readcyclecounter();
+            const uint64_t fl_ = pf[2] + pf[3] + pf[4];
+#endif
+            // the records in order; the queue is flushed at one place (each record queues at most
+            // two segments), and after the last record the open run is pushed and flushed there too
+            bool pushed = false;
+            for (int32_t j = 0;;) {
+                for (; j < hi && nseg <= 62 && !overflow; j++) {
+                    const uint32_t fj = rl(f, (uint32_t)j);
+                    if (fj & kFSkip) continue;
+                    const uint32_t lj = rl(len, (uint32_t)j), pj = rl(props, (uint32_t)j), tj = rl(toff, (uint32_t)j);
+                    const int32_t idx = base + j;
+                    if (fj & kFSettled) {
+                        if (have_prev) {
+                            const bool can = run_text && (fj & kFText) && !run_ends_nl &&
+                                             (run_len <= kGranularity || lj <= kGranularity);
+                            if (can && (fj & kFUndecided)) {
+                                overflow = true;
+                                break;
+                            }
+                            if (can && (fj & kFMatch)) {
+                                run_last = idx;
+                                run_len += lj;
+                                if (lj > 0) {
+                                    run_ends_nl = (fj & kFEndsNL) != 0;
+                                    // a surrogate pair split across two records of the run: the text
+                                    // pass joins pairs within a record only, so the host serializes it
+                                    if (run_hi && (fj & kFFirstLo)) {
+                                        overflow = true;
+                                        break;
+                                    }
+                                    run_hi = (fj & kFLastHi) != 0;
+                                }
+                                continue;
+                            }
+                            push_prev();
                         }
-                        if (can && (fj & kFMatch)) {
-                            run_last = idx;
-                            run_len += lj;
-                            if (lj > 0) run_ends_nl = (fj & kFEndsNL) != 0;
-                            continue;
-                        }
+                        have_prev = true;  // set_prev
+                        run_text = (fj & kFText) != 0;
+                        run_first = run_last = idx;
+                        run_len = run_text ? lj : 0u;
+                        run_props = pj;
+                        run_ref = tj;
+                        run_ends_nl = (fj & kFEndsNL) != 0;
+                        run_hi = lj > 0 && (fj & kFLastHi) != 0;
+                    } else {
                         push_prev();
+                        queue(kSegAlone, idx, idx, pj, tj, lj);
                     }
-                    have_prev = true;  // set_prev
-                    run_text = (fj & kFText) != 0;
-                    run_first = run_last = idx;
-                    run_len = run_text ? lj : 0u;
-                    run_props = pj;
-                    run_ref = tj;
-                    run_ends_nl = (fj & kFEndsNL) != 0;
-                } else {
-                    push_prev();
-                    queue(kSegAlone, idx, idx, pj, tj, lj);
                 }
+                if (overflow) return;
+                const bool done = j >= hi;
+                if (done && last && !pushed && nseg <= 63) {
+                    push_prev();
+                    pushed = true;
+                }
+                if (nseg > 62 || (done && last && pushed)) flush();
+                if (overflow) return;
+                if (done && (!last || pushed)) break;
             }
+#ifdef MT_SNAP_PROF
+            pf[1] += (__builtin_readcyclecounter() - tl_) - (pf[2] + pf[3] + pf[4] - fl_);
+#endif
         }
         if (overflow) return;
-        push_prev();
-        flush();
+        if (n_out <= 0) {
+            push_prev();
+            flush();
+        }
         if (!overflow && (open || nch == 0)) {
             if (!open) open_chunk();
             close_chunk();
@@ -1080,6 +1234,10 @@ __device__ __forceinline__ void snapshot_doc_lanes(const SnapParams &P, int64_t 
             D.all_len += mrow[2 + 3 * c];
         }
     D.walk();
+#ifdef MT_SNAP_PROF
+    if (lane() == 0)
+        for (int k = 0; k < 5; k++) mrow[kSnapMeta - (kWrite ? 10 : 5) + k] = (int32_t)(D.pf[k] >> 6);
+#endif
     if (kWrite) return;
     int64_t total = 0;
     if (!D.overflow) {
