@@ -1747,6 +1747,9 @@ static int launch_on(mt_batch *b, Launch &&L, int *next_stream, std::vector<int>
     return MT_OK;
 }
 
+// escalating documents that a launch at class 1400 (~8 wave slots per CU) still runs concurrently
+static constexpr int64_t kTailDocs = 1024;
+
 MT_API int mt_batch_sync(mt_batch *b) {
     if (!b || b->launches.empty()) return MT_ERR_STATE;
     std::vector<int> pending;
@@ -1774,6 +1777,11 @@ MT_API int mt_batch_sync(mt_batch *b) {
         if (S.level >= b->opt.max_retries) continue;
         const int64_t n = launch_n(b->n_docs, S);
         std::map<int, Launch> groups;
+        int64_t n_ck = 0;
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
+            n_ck += b->docout[d].status == MT_CAPACITY && b->where[d].launch == li;
+        }
         for (int64_t i = 0; i < n; i++) {
             const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
             const DocOut &o = b->docout[d];
@@ -1783,6 +1791,15 @@ MT_API int mt_batch_sync(mt_batch *b) {
             else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg) src = -1;
             else continue;
             int cls = resume_class(S.cls);
+            // a tail document checkpointed for overlay-list room (a wide collab window; the list grows
+            // only by seg/16 per class) steps to the first class with ~64 entries to spare instead of one
+            // class at a time, each step a serial launch of its own.  Only in a tail (a launch too small
+            // to fill the chip at the bigger class): with many documents escalating, the smaller class's
+            // residency wins.
+            static const bool ulist_jump = !getenv("MT_ULIST_JUMP") || atoi(getenv("MT_ULIST_JUMP")) > 0;
+            if (ulist_jump && n_ck <= kTailDocs && o.cap_kind == mt::kCapCheckpoint && S.cls < mt::kLastLdsClass &&
+                o.max_oe + 24 > (int32_t)mt::class_caps(mt::kClassSegs[S.cls]).ulist)
+                while (cls < mt::kLastLdsClass && (int32_t)mt::class_caps(mt::kClassSegs[cls]).ulist < o.max_oe + 64) cls++;
             while (cls > S.cls + 1 && !class_usable(cls)) cls--;
             // a segment beyond 16-bit lengths: re-run from scratch in the giant class (32-bit lengths)
             if (o.cap_kind == mt::kCapLongSeg) cls = long_seg_class(S.cls);
