@@ -634,6 +634,9 @@ struct LOut {
 // its escaped bytes / output offset / prefix of bytes before it; per segment of the batch its text
 // bytes (sizing) or its next free text byte (writing)
 __shared__ uint32_t s_rt[64], s_ro[64], s_rx[64], s_seg[64];
+// segments a tile closes (lane-parallel run formation), in order, before they join the queue:
+// kind, first, last, props, ref, chunk length
+__shared__ uint32_t s_q[6][72];
 
 // JSON bytes of code unit c of one record's text, given its neighbours in the record (0: none)
 __device__ __forceinline__ uint32_t unit_bytes(uint32_t c, uint32_t p, uint32_t nx) {
@@ -910,20 +913,26 @@ struct LaneDoc {
                     if (!kW) {
                         if (has) atomicAdd(&s_seg[j], myrt);
                     } else {
-                        // record offsets, in record order: each takes its segment's next text byte
-                        // (the cursors lane-distributed: lane j holds segment j's)
-                        uint32_t cur = s_seg[lane()], ro = 0;
-                        for (uint64_t m = __ballot(has); m; m &= m - 1) {
-                            const uint32_t q = (uint32_t)__builtin_ctzll(m);
-                            const uint32_t jq = rl((uint32_t)j, q), t = rl(myrt, q);
-                            const uint32_t cq = rl(cur, jq);
-                            if (lane() == q) ro = cq;
-                            if (lane() == jq) cur = cq + t;
-                        }
-                        s_seg[lane()] = cur;
+                        // record offsets: each record takes its segment's next text byte (the
+                        // cursors lane-distributed: lane j holds segment j's); a segment's records
+                        // are consecutive lanes, so a record's offset is the cursor plus the bytes of
+                        // the segment's records before it in the sub-tile (an exclusive scan), and
+                        // the segment's last record in the sub-tile advances the cursor
+                        const bool inr = i <= R1;
+                        const uint32_t v = inr ? myrt : 0u;
                         uint32_t xt;
+                        const uint32_t X = wave_excl_scan(v, &xt);
+                        const int jp = __shfl_up(j, 1, 64), jn = __shfl_down(j, 1, 64);
+                        const bool inr_n = __shfl_down((int)inr, 1, 64) != 0;
+                        const uint64_t sM = __ballot(inr && (lane() == 0 || jp != j));
+                        const int fl = 63 - __builtin_clzll(sM & ((2ull << lane()) - 1ull) | 1ull);
+                        const uint32_t Xf = (uint32_t)__shfl((int)X, fl, 64);
+                        const uint32_t cj = (uint32_t)__shfl((int)s_seg[lane()], j, 64);
+                        const uint32_t ro = cj + X - Xf;
+                        __syncthreads();
+                        if (inr && (lane() == 63 || jn != j || !inr_n)) s_seg[j] = ro + v;
                         s_ro[lane()] = ro;
-                        s_rx[lane()] = wave_excl_scan(myrt, &xt);
+                        s_rx[lane()] = X;
                     }
                     __syncthreads();
                 }
@@ -1061,6 +1070,21 @@ struct LaneDoc {
             tb = mine ? s_seg[lane()] : 0u;
             const uint32_t size = pre + tb + post;
             SNAP_T0();
+            // a batch that closes no chunk (the open chunk stays below chunk_size): every segment
+            // follows a comma, its offset an exclusive scan of the sizes
+            uint32_t ltot;
+            wave_excl_scan(mine ? sn : 0u, &ltot);
+            if (open && clen + (int64_t)ltot < P.chunk_size) {
+                uint32_t stot;
+                const uint32_t ex = wave_excl_scan(mine ? size + 1u : 0u, &stot);
+                my_off = W.pos + ex + 1;
+                if (kWrite && mine) W.dst[my_off - 1] = (uint8_t)',';
+                W.pos += stot;
+                ccount += nseg;
+                clen += ltot;
+                SNAP_ADD(4);
+                continue;
+            }
             for (int32_t j = 0; j < nseg && !overflow; j++) {
                 const uint32_t sz = rl(size, (uint32_t)j), ln = rl(sn, (uint32_t)j);
                 if (!open) open_chunk();
@@ -1091,6 +1115,108 @@ struct LaneDoc {
         if (!have_prev) return;
         have_prev = false;
         queue(run_text ? kSegRun : kSegMarker, run_first, run_last, run_props, run_ref, run_text ? run_len : 1u);
+    }
+
+    // ---- stage 1, lane-parallel: a tile whose kept settled records are all 1..kGranularity long
+    // (canAppend's length rule always holds and every appended record sets the run's ends-NL and
+    // high-surrogate state) forms its runs from pairwise flags: a kept record continues the run of
+    // the kept record before it (or the open run) when both are settled text, the earlier does not
+    // end in '\n' and the properties match; every other kept record starts a segment.  The segments
+    // the tile closes are staged in order (the open run first) and join the queue 64 at a time; the
+    // tile's last run stays open.  Same segments, in the same order, as the record loop below.
+    __device__ __forceinline__ void tile_runs(uint32_t f, uint64_t kept, uint64_t below, bool prev_st, uint32_t len,
+                                              uint32_t props, uint32_t toff, int32_t base) {
+        const uint32_t L = lane();
+        const int pl = below ? 63 - __builtin_clzll(below) : 0;
+        const uint32_t fp = (uint32_t)__shfl((int)f, pl, 64);
+        const bool pnl = below ? (fp & kFEndsNL) != 0u : run_ends_nl;
+        const bool phi = below ? (fp & kFLastHi) != 0u : run_hi;
+        const bool cand = (f & (kFSkip | kFSettled | kFText)) == (kFSettled | kFText) && prev_st && !pnl;
+        const bool join = cand && (f & kFMatch);
+        // matchProperties undecided on the device, or a surrogate pair split across two records of
+        // a run (the text pass joins pairs within a record): the host serializes the document
+        if (__ballot((cand && (f & kFUndecided)) || (join && phi && (f & kFFirstLo)))) {
+            overflow = true;
+            return;
+        }
+        const uint64_t startM = kept & ~__ballot(join);
+        const uint32_t klen = (f & kFSkip) ? 0u : len;
+        uint32_t ltot;
+        const uint32_t lex = wave_excl_scan(klen, &ltot), lin = lex + klen;
+        // the kept records before the first start extend the open run (text, by construction)
+        const int s0 = startM ? __builtin_ctzll(startM) : 64;
+        const uint64_t pre = kept & (s0 < 64 ? (1ull << s0) - 1ull : ~0ull);
+        if (pre) {
+            const uint32_t lk = 63u - (uint32_t)__builtin_clzll(pre), fk = rl(f, lk);
+            run_last = base + (int32_t)lk;
+            run_len += rl(lin, lk);
+            run_ends_nl = (fk & kFEndsNL) != 0u;
+            run_hi = (fk & kFLastHi) != 0u;
+        }
+        if (!startM) return;
+        // per start lane: its segment runs to the next start, its last record the last kept before it
+        const uint64_t after = startM & ~((2ull << L) - 1ull);
+        const int t = after ? __builtin_ctzll(after) : 64;
+        const uint64_t upto = kept & (t < 64 ? (1ull << t) - 1ull : ~0ull);
+        const int lk = upto ? 63 - __builtin_clzll(upto) : (int)L;
+        const uint32_t rlen = (uint32_t)__shfl((int)lin, lk, 64) - lex;
+        const uint32_t flk = (uint32_t)__shfl((int)f, lk, 64);
+        const uint32_t sl_ = 63u - (uint32_t)__builtin_clzll(startM);
+        const bool last_alone = !(rl(f, sl_) & kFSettled);
+        const uint64_t qM = last_alone ? startM : startM & ~(1ull << sl_);
+        const int32_t c0 = have_prev ? 1 : 0;
+        const int32_t C = c0 + __popcll(qM);
+        if (have_prev && L == 0) {
+            s_q[0][0] = run_text ? kSegRun : kSegMarker;
+            s_q[1][0] = (uint32_t)run_first;
+            s_q[2][0] = (uint32_t)run_last;
+            s_q[3][0] = run_props;
+            s_q[4][0] = run_ref;
+            s_q[5][0] = run_text ? run_len : 1u;
+        }
+        if ((qM >> L) & 1ull) {
+            const uint32_t r = (uint32_t)c0 + (uint32_t)__popcll(qM & ((1ull << L) - 1ull));
+            const bool alone = !(f & kFSettled), txt = (f & kFText) != 0u;
+            s_q[0][r] = alone ? kSegAlone : txt ? kSegRun : kSegMarker;
+            s_q[1][r] = (uint32_t)(base + (int32_t)L);
+            s_q[2][r] = (uint32_t)(base + (alone ? (int32_t)L : lk));
+            s_q[3][r] = props;
+            s_q[4][r] = toff;
+            s_q[5][r] = alone ? len : txt ? rlen : 1u;
+        }
+        // the tile's last start: an open run, or (alone) none
+        if (last_alone) {
+            have_prev = false;
+        } else {
+            const uint32_t fs = rl(f, sl_), fl = rl(flk, sl_);
+            have_prev = true;
+            run_text = (fs & kFText) != 0u;
+            run_first = base + (int32_t)sl_;
+            run_last = base + (int32_t)rl((uint32_t)lk, sl_);
+            run_len = run_text ? rl(rlen, sl_) : 0u;
+            run_props = rl(props, sl_);
+            run_ref = rl(toff, sl_);
+            run_ends_nl = (fl & kFEndsNL) != 0u;
+            run_hi = (fl & kFLastHi) != 0u;
+        }
+        __syncthreads();
+        for (int32_t taken = 0; taken < C;) {
+            const int32_t k = min(C - taken, 64 - nseg);
+            if ((int32_t)L >= nseg && (int32_t)L < nseg + k) {
+                const int32_t q = taken + (int32_t)L - nseg;
+                sk = s_q[0][q];
+                sf = (int32_t)s_q[1][q];
+                sl = (int32_t)s_q[2][q];
+                sp = s_q[3][q];
+                sr = s_q[4][q];
+                sn = s_q[5][q];
+            }
+            nseg += k;
+            taken += k;
+            if (nseg == 64) flush();
+            if (overflow) return;
+        }
+        __syncthreads();
     }
 
     // ---- stage 1
@@ -1141,6 +1267,20 @@ struct LaneDoc {
             pf[0] += __builtin_readcyclecounter() - tt_;
             const uint64_t tl_ = __builtin_readcyclecounter();
             const uint64_t fl_ = pf[2] + pf[3] + pf[4];
+#endif
+#ifndef MT_SNAP_RECORD_LOOP
+            if (!__ballot(!skip && settled && (len > kGranularity || (txt && len == 0)))) {
+                tile_runs(f, kept, below, prev_st, len, props, toff, base);
+                if (last && !overflow) {  // the open run ends the document
+                    push_prev();
+                    flush();
+                }
+#ifdef MT_SNAP_PROF
+                pf[1] += (__builtin_readcyclecounter() - tl_) - (pf[2] + pf[3] + pf[4] - fl_);
+#endif
+                if (overflow) return;
+                continue;
+            }
 #endif
             // the records in order; the queue is flushed at one place (each record queues at most
             // two segments), and after the last record the open run is pushed and flushed there too
