@@ -2934,7 +2934,7 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
     uint32_t *d_key_str = nullptr, *d_key_rank = nullptr, *d_val_str = nullptr, *d_cli_str = nullptr;
     int32_t *d_doc_cli = nullptr;
     std::vector<uint8_t *> d_final(b->launches.size(), nullptr);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e_fork = nullptr, e_join[3] = {nullptr, nullptr, nullptr};
     int rc = MT_OK;
     auto fail = [&](int code) {
         rc = code;
@@ -2966,6 +2966,10 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
         }
         if (rc) break;
         if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
+            hipEventCreateWithFlags(&e_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e_join[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e_join[1], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e_join[2], hipEventDisableTiming) != hipSuccess ||
             hipEventRecord(e0, s) != hipSuccess) {
             fail(MT_ERR_HIP);
             break;
@@ -3001,8 +3005,27 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                     break;
                 }
             }
-            for (size_t li = 0; li < b->launches.size(); li++) {
+            // every launch's documents on a stream of their own (the escalated launches hold a few
+            // large documents each, whose serial walks otherwise follow the main launch)
+            if (hipEventRecord(e_fork, s) != hipSuccess) {
+                fail(MT_ERR_HIP);
+                break;
+            }
+            int n_aux = 0;
+            // the escalated launches first: their large documents' walks are the longest
+            for (size_t lo = 1; lo <= b->launches.size(); lo++) {
+                const size_t li = lo % b->launches.size();
                 const Launch &L = b->launches[li];
+                hipStream_t ls = s;
+                if (li > 0 && launch_n(b->n_docs, L) > 0) {
+                    hipStream_t &a = b->aux[n_aux++ % 3];
+                    if ((!a && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) ||
+                        hipStreamWaitEvent(a, e_fork, 0) != hipSuccess) {
+                        fail(MT_ERR_HIP);
+                        break;
+                    }
+                    ls = a;
+                }
                 mt::SnapParams P{};
                 P.out = L.d_out;
                 P.doc_out = L.d_docout;
@@ -3041,12 +3064,15 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                 static const bool serial = getenv("MT_SNAP_SERIAL") && atoi(getenv("MT_SNAP_SERIAL")) > 0;
                 const void *kfn = serial ? (const void *)mt_snapshot_serial_kernel
                                  : pass ? (const void *)mt_snapshot_kernel : (const void *)mt_snapshot_size_kernel;
-                if (hipLaunchKernel(kfn, dim3((unsigned)P.n), dim3(64), args, 0, s) !=
-                    hipSuccess) {
+                if (hipLaunchKernel(kfn, dim3((unsigned)P.n), dim3(64), args, 0, ls) != hipSuccess) {
                     fail(MT_ERR_HIP);
                     break;
                 }
             }
+            // join: the caller's stream waits for the aux streams
+            for (int k = 0; k < std::min(n_aux, 3) && !rc; k++)
+                if (hipEventRecord(e_join[k], b->aux[k]) != hipSuccess || hipStreamWaitEvent(s, e_join[k], 0) != hipSuccess)
+                    fail(MT_ERR_HIP);
         }
         if (rc) break;
         float ms = 0;
@@ -3069,6 +3095,9 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
     for (uint8_t *p : d_final) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
+    if (e_fork) (void)hipEventDestroy(e_fork);
+    for (hipEvent_t e : e_join)
+        if (e) (void)hipEventDestroy(e);
     return rc;
 }
 
