@@ -55,15 +55,30 @@ __device__ __constant__ uint64_t kPow10[20] = {1ull,
 __device__ __forceinline__ uint32_t lane() { return threadIdx.x; }
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+// wave-wide scans on DPP lane moves (no LDS round trips): within each row of 16 lanes row_shr 1, 2,
+// 4, 8 (a lane whose source is outside the row adds 0), then row 0's total into row 1 and row 2's
+// into row 3 (row_bcast:15), then rows 0-1's total into rows 2-3 (row_bcast:31)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane() >= (uint32_t)d) x += y;
-    }
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+    const uint32_t x = wave_incl_scan(v);
     *total = rl(x, 63);
     return x - v;
+}
+// the value of lane - 1 (lane 0: 0) and of lane + 1 (lane 63: 0): DPP wave_shr:1 / wave_shl:1
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
 }
 
 __device__ __forceinline__ bool is_hi(uint32_t c) { return c >= 0xD800u && c <= 0xDBFFu; }
@@ -881,32 +896,96 @@ struct LaneDoc {
 #pragma nounroll
             for (int pass = 0; pass < (kW ? 2 : 1); pass++) {
                 uint32_t G = 0;
-                for (uint32_t s0 = 0; s0 < tot; s0 += 64) {
-                    const uint32_t u = s0 + lane();
-                    int r = 0;  // the record of unit u: the last r with ex_r <= u
-                    for (int st = 32; st > 0; st >>= 1) {
-                        const int c = r + st;
-                        const uint32_t e = (uint32_t)__shfl((int)ex, c < 64 ? c : 63, 64);
-                        if (c < 64 && e <= u) r = c;
+                // two 64-unit windows per step (their text loads in flight together); the units'
+                // neighbours come from the adjacent lanes / window (a record's units are
+                // consecutive), only the step's last lane loads its right neighbour
+                uint32_t cprev = 0;  // the previous step's last unit
+#ifdef MT_SNAP_PROF_TEXT
+                const uint64_t tw_ = __builtin_readcyclecounter();
+#endif
+                for (uint32_t s0 = 0; s0 < tot; s0 += 128) {
+                    int r[2];
+                    uint32_t k[2], rt[2], rn[2], c[2];
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const uint32_t w0 = s0 + 64u * (uint32_t)q, u = w0 + lane();
+                        // the record of unit u (the last r with ex_r <= u): a scalar pass over the few
+                        // records overlapping the window, else a binary search
+                        const uint64_t ovM = __ballot(L > 0u && ex < w0 + 64u && ex + L > w0);
+                        int rq = 0;
+                        uint32_t er = 0, tq = 0, lq = 0;
+                        if (__popcll(ovM) <= 8) {
+                            for (uint64_t m = ovM; m; m &= m - 1) {
+                                const uint32_t x = (uint32_t)__builtin_ctzll(m), ex_x = rl(ex, x);
+                                const uint32_t t_x = rl(toff, x), l_x = rl(L, x);
+                                if (u >= ex_x) {
+                                    rq = (int)x;
+                                    er = ex_x;
+                                    tq = t_x;
+                                    lq = l_x;
+                                }
+                            }
+                        } else {
+                            for (int st = 32; st > 0; st >>= 1) {
+                                const int cc = rq + st;
+                                const uint32_t e = (uint32_t)__shfl((int)ex, cc < 64 ? cc : 63, 64);
+                                if (cc < 64 && e <= u) rq = cc;
+                            }
+                            er = (uint32_t)__shfl((int)ex, rq, 64);
+                            tq = (uint32_t)__shfl((int)toff, rq, 64);
+                            lq = (uint32_t)__shfl((int)L, rq, 64);
+                        }
+                        r[q] = rq;
+                        k[q] = u - er;
+                        rt[q] = tq;
+                        rn[q] = lq;
+                        c[q] = u < tot ? (uint32_t)text[tq + u - er] : 0u;
                     }
-                    const uint32_t k = u - (uint32_t)__shfl((int)ex, r, 64);
-                    const uint32_t rt = (uint32_t)__shfl((int)toff, r, 64), rn = (uint32_t)__shfl((int)L, r, 64);
-                    uint32_t c = 0, p = 0, nx = 0, nb = 0;
-                    if (u < tot) {
-                        c = text[rt + k];
-                        if (k > 0) p = text[rt + k - 1];
-                        if (k + 1 < rn) nx = text[rt + k + 1];
-                        nb = unit_bytes(c, p, nx);
+                    const uint32_t u1 = s0 + 64u + lane();
+                    uint32_t nxe = 0;
+                    if (lane() == 63 && u1 < tot && k[1] + 1 < rn[1]) nxe = text[rt[1] + k[1] + 1];
+                    const uint32_t c0_63 = rl(c[0], 63), c1_0 = rl(c[1], 0);
+                    uint32_t p[2], nx[2], nb[2];
+                    p[0] = from_prev_lane(c[0]);
+                    p[1] = from_prev_lane(c[1]);
+                    nx[0] = from_next_lane(c[0]);
+                    nx[1] = from_next_lane(c[1]);
+                    if (lane() == 0) {
+                        p[0] = cprev;
+                        p[1] = c0_63;
+                    }
+                    if (lane() == 63) {
+                        nx[0] = c1_0;
+                        nx[1] = nxe;
+                    }
+                    cprev = rl(c[1], 63);
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const uint32_t u = s0 + 64u * (uint32_t)q + lane();
+                        nb[q] = 0;
+                        if (u < tot) {
+                            if (k[q] == 0) p[q] = 0;
+                            if (k[q] + 1 >= rn[q]) nx[q] = 0;
+                            nb[q] = unit_bytes(c[q], p[q], nx[q]);
+                        }
                     }
                     if (pass == 0) {
-                        if (u < tot) atomicAdd(&s_rt[r], nb);
+#pragma unroll
+                        for (int q = 0; q < 2; q++)
+                            if (s0 + 64u * (uint32_t)q + lane() < tot) atomicAdd(&s_rt[r[q]], nb[q]);
                     } else {
-                        uint32_t st;
-                        const uint32_t e = wave_excl_scan(nb, &st);
-                        if (nb) unit_write(W.dst + s_ro[r] + (G + e - s_rx[r]), nb, c, nx);
-                        G += st;
+#pragma unroll
+                        for (int q = 0; q < 2; q++) {
+                            uint32_t st;
+                            const uint32_t e = wave_excl_scan(nb[q], &st);
+                            if (nb[q]) unit_write(W.dst + s_ro[r[q]] + (G + e - s_rx[r[q]]), nb[q], c[q], nx[q]);
+                            G += st;
+                        }
                     }
                 }
+#ifdef MT_SNAP_PROF_TEXT
+                pf[4] += __builtin_readcyclecounter() - tw_;
+#endif
                 __syncthreads();
                 if (pass == 0) {
                     const uint32_t myrt = s_rt[lane()];
@@ -1069,7 +1148,9 @@ struct LaneDoc {
             if (wr) break;
             tb = mine ? s_seg[lane()] : 0u;
             const uint32_t size = pre + tb + post;
+#ifndef MT_SNAP_PROF_TEXT
             SNAP_T0();
+#endif
             // a batch that closes no chunk (the open chunk stays below chunk_size): every segment
             // follows a comma, its offset an exclusive scan of the sizes
             uint32_t ltot;
@@ -1082,7 +1163,9 @@ struct LaneDoc {
                 W.pos += stot;
                 ccount += nseg;
                 clen += ltot;
+#ifndef MT_SNAP_PROF_TEXT
                 SNAP_ADD(4);
+#endif
                 continue;
             }
             for (int32_t j = 0; j < nseg && !overflow; j++) {
@@ -1095,7 +1178,9 @@ struct LaneDoc {
                 clen += ln;
                 if (clen >= P.chunk_size) close_chunk();
             }
+#ifndef MT_SNAP_PROF_TEXT
             SNAP_ADD(4);
+#endif
         }
         nseg = 0;
     }
@@ -1410,7 +1495,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4
 }
 
 // pass 0 (sizes) and pass 1 (writes): separate kernels, each with its own register budget
-extern "C" __global__ __launch_bounds__(64) void mt_snapshot_size_kernel(SnapParams P) {
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mt_snapshot_size_kernel(SnapParams P) {
     const int64_t w = blockIdx.x;
     if (w >= P.n || !P.final_mask[w]) return;
     snapshot_doc_lanes<false>(P, w);
