@@ -460,6 +460,12 @@ struct SnapParams {
     int64_t *bytes;             // [n_docs] total bytes of the document's blobs (-1: not on the GPU)
     uint8_t *dst;
     const int64_t *dst_off;     // [n_docs]
+    // per workgroup w, out_cap entries each: the sizing kernel stores every record's escaped text
+    // bytes (rec_bytes[w * out_cap + record]) and every queued segment's framing bytes before / after
+    // its text (seg_frame[2 * (w * out_cap + first record)] / [+1]); the writing kernel reads them
+    // instead of sizing again (null: both kernels size)
+    uint32_t *rec_bytes;
+    uint32_t *seg_frame;
 };
 
 }  // namespace mt

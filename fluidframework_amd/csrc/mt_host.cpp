@@ -375,6 +375,8 @@ struct mt_batch {
     int64_t *d_snap_bytes = nullptr, *d_snap_off = nullptr;
     uint8_t *d_snap = nullptr;
     size_t snap_cap = 0;
+    uint32_t *d_snap_scratch = nullptr;  // SnapParams.rec_bytes / seg_frame of every launch
+    size_t snap_scratch_cap = 0;         // (u32 words)
     std::vector<int64_t> h_snap_bytes, h_snap_off;
 };
 
@@ -383,6 +385,9 @@ static void free_snap(mt_batch *b) {
     (void)hipFree(b->d_snap_bytes);
     (void)hipFree(b->d_snap_off);
     (void)hipFree(b->d_snap);
+    (void)hipFree(b->d_snap_scratch);
+    b->d_snap_scratch = nullptr;
+    b->snap_scratch_cap = 0;
     b->d_snap_meta = nullptr;
     b->d_snap_bytes = b->d_snap_off = nullptr;
     b->d_snap = nullptr;
@@ -2965,6 +2970,21 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
             if (!up(&d_final[li], fm)) fail(MT_ERR_HIP);
         }
         if (rc) break;
+        // per launch: rec_bytes and seg_frame rows (out_cap entries per document; 3 words per entry)
+        std::vector<size_t> scr_off(b->launches.size() + 1, 0);
+        for (size_t li = 0; li < b->launches.size(); li++)
+            scr_off[li + 1] = scr_off[li] + 3 * (size_t)launch_n(b->n_docs, b->launches[li]) *
+                                                (size_t)std::max<int32_t>(0, b->launches[li].out_cap);
+        if (scr_off.back() > b->snap_scratch_cap) {
+            (void)hipFree(b->d_snap_scratch);
+            b->d_snap_scratch = nullptr;
+            b->snap_scratch_cap = 0;
+            if (dalloc(&b->d_snap_scratch, scr_off.back()) != hipSuccess) {
+                fail(MT_ERR_HIP);
+                break;
+            }
+            b->snap_scratch_cap = scr_off.back();
+        }
         if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
             hipEventCreateWithFlags(&e_fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e_join[0], hipEventDisableTiming) != hipSuccess ||
@@ -3058,6 +3078,12 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                 P.bytes = b->d_snap_bytes;
                 P.dst = b->d_snap;
                 P.dst_off = b->d_snap_off;
+                // MT_SNAP_RESIZE=1: the writing kernel sizes again (A/B)
+                static const bool resize = getenv("MT_SNAP_RESIZE") && atoi(getenv("MT_SNAP_RESIZE")) > 0;
+                if (!resize && b->d_snap_scratch) {
+                    P.rec_bytes = b->d_snap_scratch + scr_off[li];
+                    P.seg_frame = P.rec_bytes + (size_t)P.n * (size_t)P.out_cap;
+                }
                 void *args[] = {&P};
                 // the lane-parallel serializer (a sizing and a writing kernel); MT_SNAP_SERIAL=1: the
                 // record-at-a-time walker, both passes in one kernel

@@ -712,6 +712,7 @@ struct LaneDoc {
     int32_t cli_first, cli_n;
     Writer<kWrite> W;  // the wave's cursor: commas, headers, trailers
     int32_t *mrow;
+    uint32_t *rb, *sfr;  // this document's rows of P.rec_bytes / P.seg_frame (null: none)
     // chunking (as Doc)
     int32_t nch = 0;
     bool open = false;
@@ -737,7 +738,7 @@ struct LaneDoc {
     __device__ LaneDoc(const SnapParams &p, const OutRec *r, const uint16_t *t, const uint32_t *pl, const DocOut &o,
                        int32_t cf, int32_t cn, uint8_t *dst, int32_t *mr)
         : P(p), rec(r), text(t), pool(pl), n_out(o.n_out), min_seq(o.min_seq), cur_seq(o.cur_seq), cli_first(cf),
-          cli_n(cn), W{dst, 0}, mrow(mr) {}
+          cli_n(cn), W{dst, 0}, mrow(mr), rb(nullptr), sfr(nullptr) {}
 
     __device__ __forceinline__ uint32_t key_rank(uint32_t k) const { return k < (uint32_t)P.n_keys ? P.key_rank[k] : kNoRank; }
     __device__ __forceinline__ bool skipped(uint32_t blk, int32_t seq, int32_t rseq) const {
@@ -765,6 +766,16 @@ struct LaneDoc {
         const uint32_t n = pool[id];
         w.put('{');
         bool first = true;
+#ifdef MT_SNAP_PROF_NOPROPS  // timing experiment only: the props bytes are sized, not written
+        if (true) {
+            uint8_t *o_ = w.o;
+            w.o = nullptr;
+            for (uint32_t e = 0; e < n; e++) entry(w, id, e, first);
+            w.put('}');
+            w.o = o_;
+            return;
+        }
+#endif
         if (!w.o) {  // the size does not depend on the order
             for (uint32_t e = 0; e < n; e++) entry(w, id, e, first);
             w.put('}');
@@ -891,11 +902,16 @@ struct LaneDoc {
             const uint32_t L = has ? a.x : 0u, toff = b.z;
             uint32_t tot;
             const uint32_t ex = wave_excl_scan(L, &tot);
-            s_rt[lane()] = 0u;
-            __syncthreads();
+            // the writing kernel takes the records' escaped bytes from the sizing kernel
+            const bool stored = kWrite && rb != nullptr;
+            if (!stored) {
+                s_rt[lane()] = 0u;
+                __syncthreads();
+            }
 #pragma nounroll
             for (int pass = 0; pass < (kW ? 2 : 1); pass++) {
                 uint32_t G = 0;
+                if (!(pass == 0 && stored)) {
                 // two 64-unit windows per step (their text loads in flight together); the units'
                 // neighbours come from the adjacent lanes / window (a record's units are
                 // consecutive), only the step's last lane loads its right neighbour
@@ -986,9 +1002,11 @@ struct LaneDoc {
 #ifdef MT_SNAP_PROF_TEXT
                 pf[4] += __builtin_readcyclecounter() - tw_;
 #endif
+                }
                 __syncthreads();
                 if (pass == 0) {
-                    const uint32_t myrt = s_rt[lane()];
+                    const uint32_t myrt = stored ? (i <= R1 ? rb[i] : 0u) : s_rt[lane()];
+                    if (!kWrite && rb && i <= R1) rb[i] = myrt;
                     if (!kW) {
                         if (has) atomicAdd(&s_seg[j], myrt);
                     } else {
@@ -1134,7 +1152,18 @@ struct LaneDoc {
         for (int wr = 0; wr < (kWrite ? 2 : 1) && !overflow; wr++) {
             {
                 SNAP_T0();
-                if (mine) frame(sk, sf, sp, sr, wr ? W.dst + my_off : nullptr, tb, pre, post);
+                if (mine) {
+                    if (kWrite && !wr && sfr) {  // the sizing kernel's framing sizes
+                        pre = sfr[2 * sf];
+                        post = sfr[2 * sf + 1];
+                    } else {
+                        frame(sk, sf, sp, sr, wr ? W.dst + my_off : nullptr, tb, pre, post);
+                        if (!kWrite && sfr) {
+                            sfr[2 * sf] = pre;
+                            sfr[2 * sf + 1] = post;
+                        }
+                    }
+                }
                 __syncthreads();
                 SNAP_ADD(2);
             }
@@ -1453,6 +1482,10 @@ __device__ __forceinline__ void snapshot_doc_lanes(const SnapParams &P, int64_t 
     int32_t *mrow = P.meta + d * (int64_t)kSnapMeta;
     LaneDoc<kWrite> D(P, P.out + w * (int64_t)P.out_cap, P.text + P.doc_text_base[d], P.pool + P.doc_pool_base[d], o,
                       cf, cn, kWrite ? P.dst + P.dst_off[d] : nullptr, mrow);
+    if (P.rec_bytes) {
+        D.rb = P.rec_bytes + w * (int64_t)P.out_cap;
+        D.sfr = P.seg_frame + 2 * w * (int64_t)P.out_cap;
+    }
     if (kWrite)
         for (int32_t c = 0; c < mrow[0]; c++) {
             D.all_count += mrow[1 + 3 * c];
