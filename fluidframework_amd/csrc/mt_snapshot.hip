@@ -1533,7 +1533,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4
     if (w >= P.n || !P.final_mask[w]) return;
     snapshot_doc_lanes<false>(P, w);
 }
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mt_snapshot_kernel(SnapParams P) {
+#ifndef MT_SNAP_WRITE_WPE
+#define MT_SNAP_WRITE_WPE 4
+#endif
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MT_SNAP_WRITE_WPE))) void mt_snapshot_kernel(SnapParams P) {
     const int64_t w = blockIdx.x;
     if (w >= P.n || !P.final_mask[w]) return;
     snapshot_doc_lanes<true>(P, w);
