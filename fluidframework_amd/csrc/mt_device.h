@@ -466,6 +466,10 @@ struct SnapParams {
     // instead of sizing again (null: both kernels size)
     uint32_t *rec_bytes;
     uint32_t *seg_frame;
+    // chunks beyond the meta row's kSnapMaxChunks: per document d, (count, length, bytes) triples at
+    // chunk_ext[chunk_ext_off[d] ..chunk_ext_off[d + 1]) (null: kSnapMaxChunks at most)
+    int32_t *chunk_ext;
+    const int64_t *chunk_ext_off;
 };
 
 }  // namespace mt

@@ -377,6 +377,10 @@ struct mt_batch {
     size_t snap_cap = 0;
     uint32_t *d_snap_scratch = nullptr;  // SnapParams.rec_bytes / seg_frame of every launch
     size_t snap_scratch_cap = 0;         // (u32 words)
+    int32_t *d_chunk_ext = nullptr;      // chunk triples beyond the meta row (SnapParams.chunk_ext)
+    int64_t *d_chunk_ext_off = nullptr;
+    size_t chunk_ext_cap = 0, chunk_ext_off_n = 0;
+    std::vector<int64_t> h_chunk_ext_off;
     std::vector<int64_t> h_snap_bytes, h_snap_off;
 };
 
@@ -388,6 +392,12 @@ static void free_snap(mt_batch *b) {
     (void)hipFree(b->d_snap_scratch);
     b->d_snap_scratch = nullptr;
     b->snap_scratch_cap = 0;
+    (void)hipFree(b->d_chunk_ext);
+    (void)hipFree(b->d_chunk_ext_off);
+    b->d_chunk_ext = nullptr;
+    b->d_chunk_ext_off = nullptr;
+    b->chunk_ext_cap = b->chunk_ext_off_n = 0;
+    b->h_chunk_ext_off.clear();
     b->d_snap_meta = nullptr;
     b->d_snap_bytes = b->d_snap_off = nullptr;
     b->d_snap = nullptr;
@@ -2985,6 +2995,42 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
             }
             b->snap_scratch_cap = scr_off.back();
         }
+        // chunks beyond the meta row: a document's chunks hold at most its table's code units and
+        // markers (text_top + n_out) at chunk_size each, plus the last; a document that still runs
+        // out (it cannot) goes to the host serializer
+        b->h_chunk_ext_off.assign((size_t)b->n_docs + 1, 0);
+        const int64_t cs = std::max<int64_t>(1, b->opt.chunk_size);
+        for (int64_t d = 0; d < b->n_docs; d++) {
+            const mt::DocOut &o = b->docout[d];
+            const int64_t bound = ((int64_t)std::max<int64_t>(0, (int64_t)o.text_top) + std::max<int64_t>(0, (int64_t)o.n_out)) / cs + 2;
+            b->h_chunk_ext_off[d + 1] = b->h_chunk_ext_off[d] + 3 * std::max<int64_t>(0, bound - mt::kSnapMaxChunks);
+        }
+        const size_t ext_words = (size_t)b->h_chunk_ext_off.back();
+        if (ext_words > b->chunk_ext_cap) {
+            (void)hipFree(b->d_chunk_ext);
+            b->d_chunk_ext = nullptr;
+            b->chunk_ext_cap = 0;
+            if (dalloc(&b->d_chunk_ext, ext_words) != hipSuccess) {
+                fail(MT_ERR_HIP);
+                break;
+            }
+            b->chunk_ext_cap = ext_words;
+        }
+        if ((size_t)b->n_docs + 1 > b->chunk_ext_off_n) {
+            (void)hipFree(b->d_chunk_ext_off);
+            b->d_chunk_ext_off = nullptr;
+            b->chunk_ext_off_n = 0;
+            if (dalloc(&b->d_chunk_ext_off, (size_t)b->n_docs + 1) != hipSuccess) {
+                fail(MT_ERR_HIP);
+                break;
+            }
+            b->chunk_ext_off_n = (size_t)b->n_docs + 1;
+        }
+        if (hipMemcpyAsync(b->d_chunk_ext_off, b->h_chunk_ext_off.data(), 8 * b->h_chunk_ext_off.size(),
+                           hipMemcpyHostToDevice, s) != hipSuccess) {
+            fail(MT_ERR_HIP);
+            break;
+        }
         if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
             hipEventCreateWithFlags(&e_fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e_join[0], hipEventDisableTiming) != hipSuccess ||
@@ -3080,6 +3126,10 @@ MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_m
                 P.dst_off = b->d_snap_off;
                 // MT_SNAP_RESIZE=1: the writing kernel sizes again (A/B)
                 static const bool resize = getenv("MT_SNAP_RESIZE") && atoi(getenv("MT_SNAP_RESIZE")) > 0;
+                if (ext_words) {
+                    P.chunk_ext = b->d_chunk_ext;
+                    P.chunk_ext_off = b->d_chunk_ext_off;
+                }
                 if (!resize && b->d_snap_scratch) {
                     P.rec_bytes = b->d_snap_scratch + scr_off[li];
                     P.seg_frame = P.rec_bytes + (size_t)P.n * (size_t)P.out_cap;
@@ -3133,8 +3183,14 @@ MT_API int mt_doc_snapshot_v1_device(mt_batch *b, int64_t doc, int32_t *n_blobs)
     if (doc < 0 || doc >= b->n_docs) return MT_ERR_ARG;
     // documents beyond MT_SNAP_MAX_BLOBS blobs are serialized by the host path above
     if (b->h_snap_bytes[doc] < 0) return mt_doc_snapshot_v1(b, doc, n_blobs);
-    int32_t meta[mt::kSnapMeta];
-    HIPCHK(hipMemcpy(meta, b->d_snap_meta + doc * (int64_t)mt::kSnapMeta, sizeof meta, hipMemcpyDeviceToHost));
+    std::vector<int32_t> meta(mt::kSnapMeta);
+    HIPCHK(hipMemcpy(meta.data(), b->d_snap_meta + doc * (int64_t)mt::kSnapMeta, 4 * meta.size(), hipMemcpyDeviceToHost));
+    if (meta[0] > mt::kSnapMaxChunks) {  // the chunks beyond the row
+        const int64_t e0 = b->h_chunk_ext_off[doc], n_ext = 3 * (int64_t)(meta[0] - mt::kSnapMaxChunks);
+        if (n_ext > b->h_chunk_ext_off[doc + 1] - e0) return MT_INTERNAL;
+        meta.resize((size_t)(mt::kSnapMeta + n_ext));
+        HIPCHK(hipMemcpy(meta.data() + mt::kSnapMeta, b->d_chunk_ext + e0, 4 * (size_t)n_ext, hipMemcpyDeviceToHost));
+    }
     std::string all((size_t)b->h_snap_bytes[doc], '\0');
     if (!all.empty())
         HIPCHK(hipMemcpy(&all[0], b->d_snap + b->h_snap_off[doc], all.size(), hipMemcpyDeviceToHost));

@@ -713,6 +713,11 @@ struct LaneDoc {
     Writer<kWrite> W;  // the wave's cursor: commas, headers, trailers
     int32_t *mrow;
     uint32_t *rb, *sfr;  // this document's rows of P.rec_bytes / P.seg_frame (null: none)
+    int32_t *ext = nullptr;            // chunk triples beyond the meta row (P.chunk_ext)
+    int32_t max_ch = kSnapMaxChunks;   // chunks this document may hold on the GPU
+    __device__ __forceinline__ int32_t *cm(int32_t c) const {
+        return c < kSnapMaxChunks ? mrow + 1 + 3 * c : ext + 3 * (c - kSnapMaxChunks);
+    }
     // chunking (as Doc)
     int32_t nch = 0;
     bool open = false;
@@ -1121,18 +1126,19 @@ struct LaneDoc {
     __device__ __forceinline__ void open_chunk() {
         open = true;
         ccount = clen = 0;
-        if (kWrite) header(W, mrow[1 + 3 * nch], mrow[2 + 3 * nch]);
+        if (kWrite) header(W, cm(nch)[0], cm(nch)[1]);
         seg_bytes_at_open = W.pos;
     }
     __device__ __forceinline__ void close_chunk() {
-        if (nch >= kSnapMaxChunks) {
+        if (nch >= max_ch) {
             overflow = true;
         } else if (kWrite) {
             trailer(W, nch, total_count, mrow[0], all_len, all_count);
         } else if (lane() == 0) {
-            mrow[1 + 3 * nch] = (int32_t)ccount;
-            mrow[2 + 3 * nch] = (int32_t)clen;
-            mrow[3 + 3 * nch] = (int32_t)(W.pos - seg_bytes_at_open);
+            int32_t *t = cm(nch);
+            t[0] = (int32_t)ccount;
+            t[1] = (int32_t)clen;
+            t[2] = (int32_t)(W.pos - seg_bytes_at_open);
         }
         total_count += ccount;
         total_len += clen;
@@ -1486,10 +1492,14 @@ __device__ __forceinline__ void snapshot_doc_lanes(const SnapParams &P, int64_t 
         D.rb = P.rec_bytes + w * (int64_t)P.out_cap;
         D.sfr = P.seg_frame + 2 * w * (int64_t)P.out_cap;
     }
+    if (P.chunk_ext) {
+        D.ext = P.chunk_ext + P.chunk_ext_off[d];
+        D.max_ch = kSnapMaxChunks + (int32_t)((P.chunk_ext_off[d + 1] - P.chunk_ext_off[d]) / 3);
+    }
     if (kWrite)
         for (int32_t c = 0; c < mrow[0]; c++) {
-            D.all_count += mrow[1 + 3 * c];
-            D.all_len += mrow[2 + 3 * c];
+            D.all_count += D.cm(c)[0];
+            D.all_len += D.cm(c)[1];
         }
     D.walk();
 #ifdef MT_SNAP_PROF
@@ -1502,11 +1512,12 @@ __device__ __forceinline__ void snapshot_doc_lanes(const SnapParams &P, int64_t 
         Writer<false> f{nullptr, 0};
         int64_t start = 0;
         for (int32_t c = 0; c < D.nch; c++) {
-            const int64_t cnt = mrow[1 + 3 * c], len = mrow[2 + 3 * c];
-            f.pos = mrow[3 + 3 * c];
+            int32_t *t = D.cm(c);
+            const int64_t cnt = t[0], len = t[1];
+            f.pos = t[2];
             D.header(f, cnt, len);
             D.trailer(f, c, start, D.nch, D.total_len, D.total_count);
-            if (lane() == 0) mrow[3 + 3 * c] = (int32_t)f.pos;
+            if (lane() == 0) t[2] = (int32_t)f.pos;
             total += f.pos;
             start += cnt;
         }

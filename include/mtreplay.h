@@ -58,8 +58,10 @@ extern "C" {
    5: 15-bit short client ids (mt_oplog.h: high bits in mt_op.flags 11-13, insert prop counts
       <= 127, sentinels 0x7FFE / 0x7FFF); OutRec meta: clientId [0,15), removedClientId [15,30).
    6: writer consensus (mt_oplog.h MT_RELF_NOTIFY; a consensus ack's pos1 = relativePos1.id) and
-      relative positions in local ops; mt_doc_consensus_events. */
-#define MT_ABI_VERSION 6
+      relative positions in local ops; mt_doc_consensus_events.
+   7: mt_batch_snapshots keeps documents of more than MT_SNAP_MAX_BLOBS blobs on the GPU (their
+      meta row's n_blobs exceeds MT_SNAP_MAX_BLOBS; the row holds the first MT_SNAP_MAX_BLOBS). */
+#define MT_ABI_VERSION 7
 
 enum mt_status_code {
     MT_OK = 0,
@@ -227,13 +229,15 @@ MT_API int mt_doc_snapshot_blob(mt_batch *b, int64_t doc, int32_t i, char *name,
                                 int64_t cap, int64_t *len);
 /* SnapshotV1 of every document on the GPU (mt_snapshot.hip: a sizing pass, a host prefix sum of
    the bytes, a writing pass) into one device buffer of *total_bytes; *device_ms = both passes.
-   Blobs of a document lie back to back (header, body_0, ..) at doc_off[doc]; a document with more
-   than MT_SNAP_MAX_BLOBS blobs gets size 0 there and n_blobs 0 in its meta row. */
+   Blobs of a document lie back to back (header, body_0, ..) at doc_off[doc].  A meta row holds
+   n_blobs and the entries of the first MT_SNAP_MAX_BLOBS blobs (n_blobs may be larger: the device
+   keeps every blob; mt_doc_snapshot_v1_device returns them all); a document the device leaves to
+   the host serializer gets size 0 there and n_blobs 0. */
 #define MT_SNAP_MAX_BLOBS 32
 #define MT_SNAP_META (1 + 3 * MT_SNAP_MAX_BLOBS) /* n_blobs, then (segmentCount, length, bytes) */
 MT_API int mt_batch_snapshots(mt_batch *b, int64_t *total_bytes, float *device_ms);
 /* after mt_batch_snapshots: the GPU blobs of `doc` become what mt_doc_snapshot_blob returns
-   (documents over MT_SNAP_MAX_BLOBS blobs: the host serializer, as mt_doc_snapshot_v1) */
+   (a document the device left to the host: the host serializer, as mt_doc_snapshot_v1) */
 MT_API int mt_doc_snapshot_v1_device(mt_batch *b, int64_t doc, int32_t *n_blobs);
 /* doc_off[n_docs + 1] byte offsets; blob_meta[n_docs * MT_SNAP_META] (either may be NULL) */
 MT_API int mt_batch_snapshot_index(mt_batch *b, int64_t *doc_off, int32_t *blob_meta);

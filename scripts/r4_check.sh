@@ -15,6 +15,8 @@ for s in "$@"; do
     c5s) step c5s 600 python -u bench.py --config 5 --docs 32768 --steps 2 --warmup 1 --no-cpu ;;
     c5srec) step c5srec 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_recloop.so python -u bench.py --config 5 --docs 32768 --steps 2 --warmup 1 --no-cpu ;;
     snapphases) step snapphases 300 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_snapprof.so python -u tools/snap_phases.py 8192 2000 ;;
+    default) step default 600 python -u bench.py ;;
+    c5full) step c5full 900 python -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
     giant) step giant 600 python -u -m pytest tests/test_gpu_parity.py -k "giant or 16_bit or wide_collab or hbm_class or escalation or million" -x -v -s --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     *) echo "unknown $s"; exit 2 ;;
   esac

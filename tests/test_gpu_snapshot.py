@@ -80,11 +80,12 @@ def _check_batch(b, oracle=None, docs=None):
         if oracle is not None and oracle[i] is not None:
             assert gpu == oracle[i].snapshot_v1(), f"doc {i}: GPU SnapshotV1 differs from the oracle"
         n = meta[i, 0]
-        if n:  # the bulk buffer holds the same blobs back to back
-            assert buf[off[i]:off[i + 1]] == "".join(host.values()).encode("utf-8")
-            assert sum(meta[i, 3:3 + 3 * n:3]) == off[i + 1] - off[i]
-        else:  # more blobs than the device meta row: host path, nothing in the buffer
-            assert off[i + 1] == off[i] and len(host) > fa.mtreplay.SNAP_MAX_BLOBS
+        assert n == len(host), f"doc {i}: every blob on the GPU"
+        # the bulk buffer holds the same blobs back to back; the meta row the first SNAP_MAX_BLOBS
+        assert buf[off[i]:off[i + 1]] == "".join(host.values()).encode("utf-8")
+        m = min(n, fa.mtreplay.SNAP_MAX_BLOBS)
+        sizes = [len(v.encode("utf-8")) for v in host.values()]
+        assert list(meta[i, 3:3 + 3 * m:3]) == sizes[:m]
 
 
 def test_snapshot_kats_unicode_markers():
@@ -135,11 +136,13 @@ def test_snapshot_config3_shape_with_oracle():
         _check_batch(b, oracle)
 
 
-def test_snapshot_small_chunks_overflow_to_host():
-    # chunk_size 16 on 1500-op documents: more blobs than MT_SNAP_MAX_BLOBS -> host serializer
+def test_snapshot_more_blobs_than_the_meta_row():
+    # chunk_size 16 on 1500-op documents: hundreds of blobs, beyond MT_SNAP_MAX_BLOBS, stay on the GPU
     b, _ = _gen(O.gen_params(1500, n_clients=4, max_lag=8, pct_insert=70, pct_remove=20, seed=13), 32, chunk_size=16)
     with b:
         _check_batch(b)
+        _, meta = b.snapshot_index()
+        assert (meta[:, 0] > fa.mtreplay.SNAP_MAX_BLOBS).all()
 
 
 def test_snapshot_after_capacity_escalation():
