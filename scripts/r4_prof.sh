@@ -19,6 +19,10 @@ for s in "$@"; do
     pmcA5) step pmcA5 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA5 -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 1 --warmup 0 --no-cpu ;;
     pmcB5) step pmcB5 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB5 -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 1 --warmup 0 --no-cpu ;;
     pmcw5) step pmcw5 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw5 -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 1 --warmup 0 --no-cpu ;;
+    prof5f) step prof5f 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5f -o run -- python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
+    pmcA5f) step pmcA5f 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA5f -o run -- python3 -u bench.py --config 5 --steps 1 --warmup 0 --no-cpu ;;
+    pmcB5f) step pmcB5f 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB5f -o run -- python3 -u bench.py --config 5 --steps 1 --warmup 0 --no-cpu ;;
+    pmcw5f) step pmcw5f 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw5f -o run -- python3 -u bench.py --config 5 --steps 1 --warmup 0 --no-cpu ;;
     *) echo "unknown $s"; exit 2 ;;
   esac
 done
