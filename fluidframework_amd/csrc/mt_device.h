@@ -163,7 +163,7 @@ constexpr int kHbmSeg = 2097152;
 // the class list (X-macro: mt_host.cpp declares each class's kernels from it; __graft_entry__.py
 // builds one object per entry)
 #define MT_CLASS_LIST(X) \
-    X(128) X(480) X(569) X(664) X(756) X(847) X(1036) X(1216) X(1400) X(1679) X(2046) X(2688) X(3499) X(3937) X(7961) \
+    X(128) X(464) X(563) X(659) X(756) X(847) X(1036) X(1216) X(1400) X(1679) X(2046) X(2688) X(3499) X(3937) X(7961) \
     X(2000000) X(2097152)
 #define MT_CLASS_SEG_(S) S,
 constexpr int kClassSegs[] = {MT_CLASS_LIST(MT_CLASS_SEG_)};
@@ -242,9 +242,11 @@ constexpr Caps class_caps(int seg) {
         return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24 + kGiantLdsBlocks, kGiantHeap, kGiantUlist, 0};
     if (seg > 65000)  // the HBM class
         return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg / 2, 0};
-    // leaf blocks ~0.23 per slot, interior ~0.05 (fan-out 4..7)
-    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80, seg >= 3500 ? seg / 2 : seg / 16 + 160,
-                seg / 16 + 16};
+    // leaf blocks ~0.23 per slot, interior ~0.05 (fan-out 4..7); the overlay list holds at least 208
+    // entries, so a document whose collab window keeps ~180 segments unsettled (config 2's widest, with
+    // the 24-entry headroom) stays in the 16-per-CU class instead of finishing alone in a later launch
+    return Caps{seg, seg + seg * 3 / 10 + 24, seg * 3 / 10 + 24, seg / 16 + 80,
+                seg >= 3500 ? seg / 2 : (seg / 16 + 160 > 208 ? seg / 16 + 160 : 208), seg / 16 + 16};
 }
 
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
@@ -410,7 +412,7 @@ struct ReplayParams {
 };
 constexpr uint32_t kIdUnlinked = 0xFFFFFFFFu;
 constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // RELPOS key the host cannot resolve safely
-constexpr int kProfSlots = 12;
+constexpr int kProfSlots = 16;
 
 // mt_digest.hip: per-document device digest of one launch's results
 struct DigestParams {

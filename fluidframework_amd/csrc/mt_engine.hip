@@ -119,7 +119,8 @@ __device__ __forceinline__ uint32_t hash_pair(uint32_t k, uint32_t v) {
 }
 
 // Phase cycle counters (MT_PROF builds only): 0 kernel, 1 descents, 2 split, 3 insert,
-// 4 range walk, 5 zamboni, 6 overlay, 7 scour, 8 text, 9 heap, 10 pack, 11 settle
+// 4 range walk, 5 zamboni, 6 overlay, 7 scour, 8 text, 9 heap, 10 pack, 11 settle, 12 the scour's
+// wait for its cold records, 13 resolve_cold, 14 heap_forget, 15 unused
 #ifdef MT_PROF
 struct PfScope {
     uint64_t &acc;
@@ -1383,6 +1384,7 @@ struct Engine {
     // left half keeps its records with tcap = r, the right half gets (toff + r, tcap - r) and a
     // copy of the seq record
     MT_FI void resolve_cold() {
+        PF_SCOPE(13);
         for (int32_t i = pend_cold; i < pend_n; i++) {
             const uint32_t sl = i ? ps1 : ps0, ns = i ? pn1 : pn0, r = i ? pr1 : pr0;
             const uint32_t pv = i ? pv1 : pv0;
@@ -1775,7 +1777,7 @@ struct Engine {
     // entries naming them are invalidated, so a slot reused later is never scoured by an old
     // entry.  `slot` holds the lanes' slots, `freeM` the freed lanes.
     MT_FI void heap_forget(uint32_t slot, uint64_t freeM) {
-
+        PF_SCOPE(14);
         for (int32_t j0 = 1; j0 <= hn; j0 += kWave) {
             const int32_t j = j0 + lane;
             const uint32_t key = j <= hn ? h_ent[j].x : kHeapInvalid;
@@ -2145,6 +2147,12 @@ struct Engine {
         {
             const uint64_t allP = pairM | withM;
             if ((((allP | (allP >> 1)) >> lane) & 1ull) != 0ull) cr = cold[2 * slot];
+#ifdef MT_PROF
+            if (allP) {  // the wait for those records (and any earlier vector-memory traffic)
+                PF_SCOPE(12);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+#endif
         }
         bool serial = false;
         if (withM) {

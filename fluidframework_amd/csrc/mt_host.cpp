@@ -1709,7 +1709,8 @@ static int gather_launch(mt_batch *b, int li) {
                 if (k == 0 && (double)pf[(size_t)i * mt::kProfSlots] > mx) mx = (double)pf[(size_t)i * mt::kProfSlots];
             }
         fprintf(stderr, "MT_PROF launch %d docs %lld lds %zu: mean cycles/doc", li, (long long)n, L.lds);
-        static const char *nm[mt::kProfSlots] = {"kernel", "descend", "split", "insert", "range", "zamboni", "overlay", "scour", "text", "heap", "pack", "settle"};
+        static const char *nm[mt::kProfSlots] = {"kernel", "descend", "split", "insert", "range", "zamboni", "overlay", "scour", "text", "heap", "pack", "settle",
+                                                     "scold", "resolve", "hforget", "unused"};
         for (int k = 0; k < mt::kProfSlots; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (double)n);
         fprintf(stderr, " max_kernel=%.0f\n", mx);
     }

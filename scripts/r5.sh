@@ -1,0 +1,44 @@
+#!/bin/bash
+# round-5 GPU steps (each under its own time limit; stop at the first failure):
+#   tests            the -m gpu suite
+#   parity           tests/test_gpu_parity.py only
+#   c2 / c3s / c3    bench config 2 / config-3 slice (8,192 docs) / config 3 (default lib)
+#   c3s_q0 / c3s_z0 / c3s_q0z0  the config-3 slice with the deferred text queue off (MT_TEXT_QUEUE=0),
+#                    the zamboni prefetch off (MT_ZAMBONI_PREFETCH=0), both off
+#   c3s_base / c2_base  the same with fluidframework_amd/libmtreplay_base.so (the previous tree)
+#   phases3          MT_PROF phase profile of the config-3 slice (libmtreplay_prof.so)
+#   prof3            rocprofv3 kernel stats of the headline bench
+set -u
+mkdir -p gpurun_out
+step() {
+  local name=$1 lim=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 $lim "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"digest_xor": "[0-9a-f]*"\|"GB_per_s": [0-9.]*\|"host_match": [0-9]*\|"launches_per_step": [0-9]*\|[0-9]* passed\|[0-9]* failed' gpurun_out/$name.log | sort | uniq -c | tr '\n' ' ')"
+  if [ $rc -ne 0 ]; then tail -40 gpurun_out/$name.log; exit $rc; fi
+}
+BASE=fluidframework_amd/libmtreplay_base.so
+PROF=fluidframework_amd/libmtreplay_prof.so
+C3S="bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu"
+C2="bench.py --config 2 --steps 3 --warmup 1 --no-cpu"
+PT="-x -v --timeout 200 --timeout-method thread -p no:cacheprovider"
+for s in "$@"; do
+  case $s in
+    tests) step tests 900 python -u -m pytest tests -m gpu $PT ;;
+    parity) step parity 600 python -u -m pytest tests/test_gpu_parity.py -m gpu $PT ;;
+    writer) step writer 600 python -u -m pytest tests/test_gpu_writer.py -m gpu $PT ;;
+    smoke) step smoke 300 python -u __graft_entry__.py smoke ;;
+    c2) step c2 300 python -u $C2 ;;
+    c2_base) step c2_base 300 env FLUIDFRAMEWORK_AMD_LIB=$BASE python -u $C2 ;;
+    c3s) step c3s 400 python -u $C3S ;;
+    c3s_q0) step c3s_q0 400 env MT_TEXT_QUEUE=0 python -u $C3S ;;
+    c3s_base) step c3s_base 400 env FLUIDFRAMEWORK_AMD_LIB=$BASE python -u $C3S ;;
+    c3s_z0) step c3s_z0 400 env MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
+    c3s_q0z0) step c3s_q0z0 400 env MT_TEXT_QUEUE=0 MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
+    c3) step c3 600 python -u bench.py --steps 3 --warmup 1 ;;
+    phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
+    prof3) step prof3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
+    *) echo "unknown $s"; exit 2 ;;
+  esac
+done

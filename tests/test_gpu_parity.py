@@ -417,7 +417,7 @@ def test_native_json_ingest_replays_like_the_packer():
 
 def test_config3_documents_at_full_size():
     """The north-star workload's documents at their own size: config-3 mix (55/35/10), 10k ops,
-    no seg_cap forcing, so documents run the natural capacity chain (class 480 -> 569 -> ... ->
+    no seg_cap forcing, so documents run the natural capacity chain (class 464 -> 563 -> ... ->
     1,679 -> 2,046) through checkpoint / resume.  Every digest equals the oracle's; every 8th
     document also text, property runs and SnapshotV1 (host and GPU serializers)."""
     n = 32

@@ -232,25 +232,57 @@ def _gen_writer_parity(p, n_docs, full_every=4, **opts):
     ops, text, props, off = O.gen_batch(p, n_docs)
     t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
     wops, woff, wnames = writer_batch(ops, off, names, lambda d: 1 + d % p.n_clients)
+    stopped = []  # (doc, failing record)
     with fa.ReplayBatch(n_docs, **opts) as b:
         b.set_tables(GEN_KEYS, GEN_VALUES)
         for d in range(n_docs):
             b.set_clients(wnames[d], d)
         b.ingest(wops, woff, text, props)
         b.run()
+        fail_op = b.counters()["fail_op"]
         for d in range(n_docs):
             od = O.replay_doc(wops[woff[d]:woff[d + 1]].copy(), text, props, t, wnames[d])
             dv = b.doc(d)
             assert dv.status == od.status, (d, fa.status_string(dv.status), od.error)
             if od.status == ST_BAD_INPUT:
                 # a reference assert inside ackPendingSegment (the writer's local order diverged
-                # from the sequenced one, the #1213 family): the replica's state after the throw is
-                # not part of the contract, only that both stop there
+                # from the sequenced one, the #1213 family): both sides stop at the same record,
+                # and the states just before it are compared below
+                stopped.append((d, int(fail_op[d])))
                 continue
             assert dv.digest() == od.digest(), f"doc {d}"
             if d % full_every == 0:
                 assert_same(dv, od, f"doc {d}")
-        return b.stats()
+        stats = b.stats()
+    if stopped:
+        _stopped_writer_parity(wops, woff, wnames, text, props, t, stopped, **opts)
+    return stats
+
+
+def _stopped_writer_parity(wops, woff, wnames, text, props, t, stopped, **opts):
+    """A replica stopped by a reference assert: the oracle applies every record before the GPU's
+    failing one and stops exactly at that one (the same record on both sides), and the GPU replay of
+    the log cut before that record equals the oracle's state there (digest, shape, text, props,
+    SnapshotV1) — the state immediately before the throw."""
+    logs = []
+    for d, k in stopped:
+        log = wops[woff[d]:woff[d + 1]]
+        assert 0 <= k < len(log), (d, k)
+        assert O.replay_doc(log[:k + 1].copy(), text, props, t, wnames[d]).status == ST_BAD_INPUT, (d, k)
+        logs.append(log[:k].copy())
+    off = np.zeros(len(logs) + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in logs])
+    with fa.ReplayBatch(len(logs), **opts) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        for i, (d, _) in enumerate(stopped):
+            b.set_clients(wnames[d], i)
+        b.ingest(np.concatenate(logs) if len(logs) else wops[:0], off, text, props)
+        b.run()
+        for i, (d, k) in enumerate(stopped):
+            od = O.replay_doc(logs[i], text, props, t, wnames[d])
+            assert od.status == 0 and b.doc(i).status == 0, (d, k, od.error)
+            assert b.doc(i).digest() == od.digest(), f"doc {d} before record {k}"
+            assert_same(b.doc(i), od, f"doc {d} before record {k}")
 
 
 def test_generated_writer_logs_config2_shape():

@@ -40,9 +40,9 @@ def _kernels(notes: str) -> dict:
 
 
 # VGPR budget of each class's replay kernel: 512 / the waves per SIMD its LDS layout allows
-# (mt_device.h class_waves_per_eu: 16 documents per CU in class 480 -> 4 waves -> 128 VGPRs; 5 in
+# (mt_device.h class_waves_per_eu: 16 documents per CU in class 464 -> 4 waves -> 128 VGPRs; 5 in
 # class 2046 -> 2 -> 256; 4 in class 2688 -> 1 -> 512)
-BUDGET = {480: 128, 569: 128, 1400: 256, 2046: 256, 2688: 512}
+BUDGET = {464: 128, 563: 128, 1400: 256, 2046: 256, 2688: 512}
 
 
 @pytest.mark.skipif(not (LLVM / "llvm-readelf").exists() or not OBJ.exists(), reason="no build / ROCm llvm tools")
