@@ -2765,13 +2765,18 @@ struct Engine {
         const int32_t ref = op.ref_seq;
         const uint32_t start = (uint32_t)op.pos1, end = (uint32_t)op.pos2;
         ov_splits = -1;
-        boundary(start, ref, c);
+        const int32_t s0 = splits;
+        const Walk W = boundary(start, ref, c);
         if (status) return;
+        const bool wok = W.blk >= 0 && splits == s0;  // no block split: W.base is the block's start
         boundary(end, ref, c);
         if (status) return;
         // nodeMap visits leaves with vlen > 0 and E < end and P > start: none when end <= start
-        // (both boundaries were cut, so no leaf can straddle them)
-        if (end > start) range_walk(op, start, end);
+        // (both boundaries were cut, so no leaf can straddle them).  When neither boundary split a
+        // block, the walk starts at the first boundary's leaf block: every leaf before it ends
+        // before start (insertingWalk takes the first block reaching start), so the range walk
+        // from there visits exactly nodeMap's leaves, without a third descent.
+        if (end > start) range_walk(op, start, end, wok && splits == s0 ? W.blk : -1, W.base);
         resolve_splits();
         if (kW && op.seq == kUnassignedSeq) return;  // a local op: no zamboni (mergeTree.ts:2600, 2713)
         zamboni();
@@ -2844,12 +2849,19 @@ struct Engine {
         }
     }
 
-    MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end) {
+    // blk0 >= 0: start at leaf block blk0 (view position base0) instead of a strict descent
+    MT_FI void range_walk(const mt_op &op, uint32_t start, uint32_t end, int32_t blk0 = -1, uint32_t base0 = 0) {
         const uint32_t c = MT_OP_CLIENT(op);
         const int32_t ref = op.ref_seq;
         resolve_cold();  // the walk reads / updates cold records of split halves
         ensure_overlay(ref, c);
-        Walk W = descend(start, ref, c, true);
+        Walk W;
+        if (blk0 >= 0) {
+            W.blk = blk0;
+            W.base = base0;
+        } else {
+            W = descend(start, ref, c, true);
+        }
         PF_SCOPE(4);
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = (op.flags & MT_OPF_REWRITE) != 0;

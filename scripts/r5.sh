@@ -6,6 +6,7 @@
 #   c3s_q0 / c3s_z0 / c3s_q0z0  the config-3 slice with the deferred text queue off (MT_TEXT_QUEUE=0),
 #                    the zamboni prefetch off (MT_ZAMBONI_PREFETCH=0), both off
 #   c3s_base / c2_base  the same with fluidframework_amd/libmtreplay_base.so (the previous tree)
+#   c3s_a / c2_a     the same with fluidframework_amd/libmtreplay_r5a.so (an A/B reference build)
 #   phases3          MT_PROF phase profile of the config-3 slice (libmtreplay_prof.so)
 #   prof3            rocprofv3 kernel stats of the headline bench
 set -u
@@ -34,6 +35,8 @@ for s in "$@"; do
     c3s) step c3s 400 python -u $C3S ;;
     c3s_q0) step c3s_q0 400 env MT_TEXT_QUEUE=0 python -u $C3S ;;
     c3s_base) step c3s_base 400 env FLUIDFRAMEWORK_AMD_LIB=$BASE python -u $C3S ;;
+    c3s_a) step c3s_a 400 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5a.so python -u $C3S ;;
+    c2_a) step c2_a 300 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5a.so python -u $C2 ;;
     c3s_z0) step c3s_z0 400 env MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
     c3s_q0z0) step c3s_q0z0 400 env MT_TEXT_QUEUE=0 MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
     c3) step c3 600 python -u bench.py --steps 3 --warmup 1 ;;
