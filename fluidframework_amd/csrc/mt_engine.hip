@@ -1738,6 +1738,9 @@ struct Engine {
         if (hn > max_heap) max_heap = hn;
         wsync();
     }
+    // The sift-down reads three levels below the hole per LDS round trip (lanes 0-1: its children,
+    // 2-5: their children, 6-13: the next level), then compares level by level from registers: the
+    // same comparisons as one level per load, a third of the dependent round trips.
     MT_FI void heap_get(uint32_t &key, int32_t &seq) {
         PF_SCOPE(9);
         const uint2 top = h_ent[1];
@@ -1748,24 +1751,41 @@ struct Engine {
         hn--;
         int32_t k = 1;
         int32_t newtop = ls;
-        while ((k << 1) <= hn) {
-            const int32_t j0 = k << 1;
-            const uint4 pr = *(const uint4 *)&h_ent[j0];
-            int32_t j = j0;
-            uint32_t jk = pr.x;
-            int32_t sj = (int32_t)rfl(pr.y);
-            if (j0 < hn) {
-                const int32_t sj1 = (int32_t)rfl(pr.w);
-                if (sj - sj1 > 0) {
-                    j = j0 + 1;
-                    sj = sj1;
-                    jk = pr.z;
+        bool done = false;
+        while (!done && (k << 1) <= hn) {
+            const int32_t k0 = k;
+            // lane l < 14: level L = 1, 2, 3 below k0 (lanes 2^L - 2 .. 2^(L+1) - 3), entry 2^L k0 + (l - 2^L + 2)
+            const int32_t L = lane < 2 ? 1 : lane < 6 ? 2 : 3;
+            const int32_t idx = (k0 << L) + lane - ((1 << L) - 2);
+            uint2 e = make_uint2(0u, 0u);
+            if (lane < 14 && idx <= hn) e = h_ent[idx];
+#pragma unroll
+            for (int lv = 1; lv <= 3; lv++) {
+                const int32_t j0 = k << 1;
+                if (j0 > hn) {
+                    done = true;
+                    break;
                 }
+                const int l0 = ((1 << lv) - 2) + (j0 - (k0 << lv));
+                int32_t j = j0;
+                uint32_t jk = rdl(e.x, l0);
+                int32_t sj = (int32_t)rdl(e.y, l0);
+                if (j0 < hn) {
+                    const int32_t sj1 = (int32_t)rdl(e.y, l0 + 1);
+                    if (sj - sj1 > 0) {
+                        j = j0 + 1;
+                        sj = sj1;
+                        jk = rdl(e.x, l0 + 1);
+                    }
+                }
+                if (ls - sj <= 0) {
+                    done = true;
+                    break;
+                }
+                h_ent[k] = make_uint2(jk, (uint32_t)sj);
+                if (k == 1) newtop = sj;
+                k = j;
             }
-            if (ls - sj <= 0) break;
-            h_ent[k] = make_uint2(jk, (uint32_t)sj);
-            if (k == 1) newtop = sj;
-            k = j;
         }
         if (hn >= 1) h_ent[k] = last;
         htop = hn >= 1 ? newtop : kNoneSeq;
@@ -2223,7 +2243,7 @@ struct Engine {
             uint64_t m = mergeM;
             int32_t h = -1;
             uint32_t hslot = 0, pl = 0, ptoff = 0, pcap = 0, hmeta = 0, hprops = 0, hov = 0;
-            int32_t gcs0 = text_gcs;
+            bool gcd = false;  // a compaction (text_gc, only from arena_alloc below) moved the texts
             uint32_t dd = 0, ds = 0, dl = 0;  // queued text copies (MT_TEXT_BATCH), lane i = copy i
             int32_t nq = 0;
             while (m) {
@@ -2242,7 +2262,7 @@ struct Engine {
                 }
                 const uint32_t fslot = rdl(slot, k), sl = rdl(len, k);
                 uint32_t stoff = rdl(cr.z, k), stcap = rdl(cr.w, k);
-                if (text_gcs != gcs0) {  // a compaction moved texts: offsets are in HBM again
+                if (gcd) {  // a compaction moved texts: offsets are in HBM again
                     const uint4 hc = cold[2 * hslot], fc = cold[2 * fslot];
                     ptoff = hc.z;
                     pcap = hc.w;
@@ -2280,6 +2300,7 @@ struct Engine {
                     const uint32_t dst = arena_alloc(ncap);
                     if (status) return 0;
                     if (text_gcs != g0) {
+                        gcd = true;
                         ptoff = cold[2 * hslot].z;
                         stoff = cold[2 * fslot].z;
                     }
