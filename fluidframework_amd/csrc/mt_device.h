@@ -183,6 +183,12 @@ constexpr int kGiantLdsLevel = 3;
 constexpr int kGiantHeap = 1024;
 constexpr int kGiantUlist = 1024;
 constexpr int kGiantChainRec = 4;  // HBM-resident blocks recorded per overlay list entry
+// The giant class's replay workgroup holds a second wave that prefetches (mt_engine.hip
+// giant_prefetch): the replaying wave publishes in LDS words [0] the index of the op it applies,
+// [1] root, [2] depth, [7] kGiantRun / kGiantDone; word [6] is the prefetch wave's sink
+constexpr int kGiantPubWords = 8;
+constexpr uint32_t kGiantRun = 0x52554E21u, kGiantDone = 0x444F4E45u;
+constexpr int kGiantThreads = 128;
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapLongSeg = 8;     // beyond an LDS class's 16-bit lengths or relative seqs: a spill class
 
@@ -252,7 +258,7 @@ constexpr Caps class_caps(int seg) {
 // LDS layout of one document (byte offsets; every array 16-byte aligned)
 struct Layout {
     uint32_t len, meta, sblk, ulist, usr, ucm;
-    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, bep, heap, scratch, hdr, grec, bytes;
+    uint32_t bparent, bchild, bcount, bleaf, bscour, bslen, bacc, bep, heap, scratch, hdr, grec, pub, bytes;
 };
 constexpr int kHdrWords = 24;  // per-document scalars kept in LDS (mt_engine.hip LWord)
 constexpr uint32_t lds_align(uint32_t x) { return (x + 15u) & ~15u; }
@@ -330,6 +336,7 @@ constexpr Layout make_glayout() {
     L.bacc = o;    o = lds_align(o + 4u * K);
     L.bep = o;     o = lds_align(o + 4u * K);
     L.grec = o;    o = lds_align(o + 4u * kGiantChainRec * kGiantUlist);  // the overlay's chain records
+    L.pub = o;     o = lds_align(o + 4u * kGiantPubWords);  // the state the prefetch wave reads
     L.len = L.meta = L.sblk = o;  // in HBM (make_layout)
     L.bytes = o;
     return L;

@@ -3994,6 +3994,16 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
                     break;
                 }
                 mt_op op = bcast_op(cur, i);
+                if constexpr (is_giant_seg(SEG) && !kW) {
+                    // the prefetch wave's inputs (giant_prefetch): this op's index, the tree's root / depth
+                    if (!kLoad && E.lane == 0) {
+                        uint32_t *pub = (uint32_t *)((uint8_t *)E.scratch - make_glayout().scratch + make_glayout().pub);
+                        __hip_atomic_store(pub + 1, (uint32_t)E.root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(pub + 2, (uint32_t)E.depth, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(pub, (uint32_t)(base - b0 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(pub + 7, kGiantRun, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
                 E.apply(op);
             }
             if (E.status != ST_OK) {
@@ -4018,13 +4028,124 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
     return E.status == ST_CAPACITY && E.cap_kind == kCapCheckpoint;
 }
 
-// one workgroup per document (blockIdx.x)
+// The giant class's prefetch wave (the replay workgroup's second wave; it only reads).  A giant
+// document's lower tree levels, segment tables and cold records are in HBM, and every op walks
+// them with dependent loads (~30 per op).  While the replaying wave applies op k, this wave walks
+// the tree as it stands (racy reads: every id is bounds-checked and a wrong turn only wastes a
+// prefetch) towards op k + 1's positions, and to the leaf block of the zamboni heap's top segment,
+// loading what those walks read — block rows, lengths, the leaves' lengths / meta words and cold
+// records — so the replaying wave's dependent loads find the lines in the CU's L1 / the XCD's L2.
+// It stops when the replaying wave publishes kGiantDone, or after 10 s without a new op index.
+template <int SEG>
+MT_FI void giant_prefetch(const ReplayParams &P, int64_t w, int64_t d) {
+    if constexpr (is_giant_seg(SEG)) {
+        extern __shared__ __attribute__((aligned(16))) uint8_t gsmem[];
+        Engine<SEG> E;
+        E.lane = (int)threadIdx.x - kWave;
+        E.carve(tables<SEG>(P, w), gsmem);
+        E.cold = P.cold + w * (int64_t)SEG * kColdPerSlot;
+        const int lane = E.lane;
+        uint32_t *pub = (uint32_t *)(gsmem + make_glayout().pub);
+        const mt_op *ops = (const mt_op *)P.ops + P.doc_op_off[d];
+        const int64_t n_ops = P.doc_op_off[d + 1] - P.doc_op_off[d];
+        constexpr uint32_t kBlk = (uint32_t)E.cap.blk, kSeg = (uint32_t)SEG;
+        uint32_t sink = 0;
+        int32_t last = -1;
+        uint64_t t_prog = __builtin_amdgcn_s_memrealtime();
+        // touch the leaves of leaf block b: lengths, meta words, cold records
+        auto leaves = [&](uint32_t b, bool cold) {
+            if (b >= kBlk) return;
+            const uint32_t n = E.b_count[b];
+            const uint32_t s = lane < 8 && (uint32_t)lane < n ? (uint32_t)E.b_child[b * 8 + lane] : kSeg;
+            if (s < kSeg) {
+                sink += (uint32_t)E.s_len[s] + (uint32_t)E.s_meta[s];
+                if (cold) sink += E.cold[2 * s].x;
+            }
+        };
+        // the inserting walk's path towards pos (settled lengths only), then the leaf block's leaves
+        auto walk = [&](uint32_t root, int32_t depth, uint32_t pos) {
+            uint32_t N = root, base = 0;
+            for (int32_t l = 0; l + 2 < depth; l++) {
+                if (N >= kBlk) return;
+                const uint32_t n = E.b_count[N];
+                const uint32_t c = lane < 8 && (uint32_t)lane < n ? (uint32_t)E.b_child[N * 8 + lane] : kBlk;
+                const uint32_t v = c < kBlk ? (uint32_t)E.b_slen[c] : 0u;
+                const uint32_t incl = scan8(v) + base;
+                const uint64_t hb = ballot(lane < 8 && c < kBlk && incl >= pos);
+                const int f = hb ? first_lane(hb) : (n > 0 && n <= 8 ? (int)n - 1 : 0);
+                base = rdl(incl - v, f);
+                N = rdl(c, f);
+            }
+            if (N >= kBlk) return;
+            if (depth < 2) {
+                leaves(N, true);
+                return;
+            }
+            // the level-1 block: every leaf block's row and leaves (lane = 8 x leaf block + entry)
+            const uint32_t n = E.b_count[N];
+            const uint32_t ci = (uint32_t)lane >> 3, j = (uint32_t)lane & 7;
+            const uint32_t cb = ci < n && ci < 8 ? (uint32_t)E.b_child[N * 8 + ci] : kBlk;
+            const uint32_t cn = cb < kBlk ? (uint32_t)E.b_count[cb] : 0u;
+            const uint32_t s = j < cn && j < 8 ? (uint32_t)E.b_child[cb * 8 + j] : kSeg;
+            uint32_t len = 0;
+            if (s < kSeg) {
+                len = E.s_len[s];
+                sink += (uint32_t)E.s_meta[s];
+            }
+            const uint32_t gs = sum8(len);
+            const uint32_t cl = (uint32_t)__shfl((int)gs, 8 * lane, kWave);
+            const uint32_t incl = scan8(cl) + base;
+            const uint64_t hb = ballot(lane < 8 && (uint32_t)lane < n && incl >= pos);
+            if (hb) leaves(rdl(cb, 8 * first_lane(hb)), true);
+        };
+        for (;;) {
+            const uint32_t st = __hip_atomic_load(pub + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (st == kGiantDone) break;
+            const int32_t k = (int32_t)__hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (st != kGiantRun || k == last) {
+                if (now - t_prog > 1000000000ull) break;  // 10 s (100 MHz) without a new op
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            last = k;
+            t_prog = now;
+            const uint32_t root = rfl(__hip_atomic_load(pub + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            const int32_t depth = (int32_t)rfl(__hip_atomic_load(pub + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (root >= kBlk || depth < 1 || depth > 16) continue;
+            if (k >= 0 && k + 1 < n_ops) {
+                const mt_op op = ops[k + 1];
+                if (op.type <= MT_OP_ANNOTATE && op.pos1 >= 0) {
+                    walk(root, depth, (uint32_t)op.pos1);
+                    if (op.type != MT_OP_INSERT && op.pos2 > op.pos1) walk(root, depth, (uint32_t)op.pos2);
+                }
+            }
+            // the block zamboni pops next: the heap top's leaf block
+            const uint32_t key = rfl(E.h_ent[1].x);
+            if (key < kSeg) leaves((uint32_t)E.s_blk[key], true);
+        }
+        if (lane == 0) pub[6] = sink;  // (keeps the loads; the prefetch wave's own word)
+    }
+}
+
+// one workgroup per document (blockIdx.x); the giant class's observer replay adds the prefetch wave
 template <int SEG, bool kLoad, bool kW = false>
 MT_FI void replay_body(const ReplayParams &P) {
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
-    replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
+    if constexpr (is_giant_seg(SEG) && !kLoad && !kW) {
+        extern __shared__ __attribute__((aligned(16))) uint8_t gsmem[];
+        uint32_t *pub = (uint32_t *)(gsmem + make_glayout().pub);
+        if (threadIdx.x >= (unsigned)kWave) {
+            giant_prefetch<SEG>(P, w, d);
+            return;
+        }
+        replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
+        if (threadIdx.x == 0) __hip_atomic_store(pub + 7, kGiantDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
+    }
 }
 
 // Generator: draws each op from the issuer's view (include/mt_gen.h, DESIGN.md

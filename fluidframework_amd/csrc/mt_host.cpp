@@ -1522,7 +1522,9 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
                 (long long)n, (int)L.cksrc.size(), L.level, L.lds, (int)L.load);
     if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
     void *args[] = {&P};
-    HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(64), args, L.lds, s));
+    // the giant class's observer replay runs a prefetch wave beside the replaying one
+    const unsigned threads = (fn == kKernels[L.cls].replay && L.cls == mt::kGiantClass) ? (unsigned)mt::kGiantThreads : 64u;
+    HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(threads), args, L.lds, s));
     return MT_OK;
 }
 

@@ -24,7 +24,9 @@ constexpr int kWpe = mt::is_hbm_seg(MT_SEG) ? 1 : MT_WPE_UNIFORM;
 constexpr int kWpe = mt::class_waves_per_eu(MT_SEG);
 #endif
 
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void MT_CAT(mt_replay_kernel_, MT_SEG)(mt::ReplayParams P) {
+// the giant class's observer replay: the replaying wave plus its prefetch wave (mt_engine.hip giant_prefetch)
+constexpr int kReplayThreads = mt::is_giant_seg(MT_SEG) ? mt::kGiantThreads : 64;
+extern "C" __global__ __launch_bounds__(kReplayThreads) __attribute__((amdgpu_waves_per_eu(kWpe))) void MT_CAT(mt_replay_kernel_, MT_SEG)(mt::ReplayParams P) {
     mt::replay_body<MT_SEG, false>(P);
 }
 

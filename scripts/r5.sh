@@ -37,6 +37,11 @@ for s in "$@"; do
     c3s_base) step c3s_base 400 env FLUIDFRAMEWORK_AMD_LIB=$BASE python -u $C3S ;;
     c3s_a) step c3s_a 400 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5a.so python -u $C3S ;;
     c2_a) step c2_a 300 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5a.so python -u $C2 ;;
+    c3s_ilp) step c3s_ilp 400 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_ilp.so python -u $C3S ;;
+    c2_ilp) step c2_ilp 300 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_ilp.so python -u $C2 ;;
+    giant) step giant 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "giant or million or hbm_class or 16_bit or escalation" -x -v -s --timeout 600 --timeout-method thread -p no:cacheprovider ;;
+    grate) step grate 400 python -u tools/hbm_phases.py 100000 8 2000000 ;;
+    grate_a) step grate_a 400 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5a.so python -u tools/hbm_phases.py 100000 8 2000000 ;;
     c3s_z0) step c3s_z0 400 env MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
     c3s_q0z0) step c3s_q0z0 400 env MT_TEXT_QUEUE=0 MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
     c3) step c3 600 python -u bench.py --steps 3 --warmup 1 ;;
