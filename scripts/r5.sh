@@ -23,6 +23,8 @@ BASE=fluidframework_amd/libmtreplay_base.so
 PROF=fluidframework_amd/libmtreplay_prof.so
 C3S="bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu"
 C2="bench.py --config 2 --steps 3 --warmup 1 --no-cpu"
+B3="bench.py --config 3 --steps 1 --warmup 0 --no-cpu"
+B3S="bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu"
 PT="-x -v --timeout 200 --timeout-method thread -p no:cacheprovider"
 for s in "$@"; do
   case $s in
@@ -46,6 +48,18 @@ for s in "$@"; do
     c3s_q0z0) step c3s_q0z0 400 env MT_TEXT_QUEUE=0 MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
     c3) step c3 600 python -u bench.py --steps 3 --warmup 1 ;;
     phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
+    pmcA3) step pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u $B3 ;;
+    pmcB3) step pmcB3 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB3 -o run -- python3 -u $B3 ;;
+    pmcf3) step pmcf3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf3 -o run -- python3 -u $B3 ;;
+    pmcw3) step pmcw3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw3 -o run -- python3 -u $B3 ;;
+    b3s1) step b3s1 300 python -u $B3S ;;
+    b3c1) step b3c1 300 python -u $B3S --seg-cap 2046 ;;
+    pmcf3s) step pmcf3s 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf3s -o run -- python3 -u $B3S ;;
+    pmcw3s) step pmcw3s 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw3s -o run -- python3 -u $B3S ;;
+    pmcf3c) step pmcf3c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf3c -o run -- python3 -u $B3S --seg-cap 2046 ;;
+    pmcw3c) step pmcw3c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw3c -o run -- python3 -u $B3S --seg-cap 2046 ;;
+    bench3one) step bench3one 300 python -u $B3 ;;
+    driver) step driver 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof3) step prof3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     *) echo "unknown $s"; exit 2 ;;
   esac
