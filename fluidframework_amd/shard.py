@@ -76,9 +76,9 @@ def gather_results(digests, statuses, world: int, rank: int, snapshot_digests=No
         rec = rec.cpu()  # gloo gathers host tensors
     if counts is not None and max(counts) > rec.shape[0]:
         rec = torch.cat([rec, rec.new_zeros((max(counts) - rec.shape[0], rec.shape[1]))], 0)
-    if world == 1:
+    if world == 1 and not dist.is_initialized():
         parts = [rec]
-    else:
+    else:  # through the process group (also a one-rank RCCL group: the collective runs)
         parts = [torch.empty_like(rec) for _ in range(world)] if rank == 0 else None
         dist.gather(rec, parts, dst=0)
     if rank != 0:
@@ -100,7 +100,7 @@ def gather_bytes(buf, world: int, rank: int):
     import torch
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not dist.is_initialized():
         return [buf]
     n = torch.tensor([buf.numel()], dtype=torch.int64, device=buf.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]

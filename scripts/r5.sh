@@ -30,6 +30,7 @@ for s in "$@"; do
   case $s in
     tests) step tests 900 python -u -m pytest tests -m gpu $PT ;;
     parity) step parity 600 python -u -m pytest tests/test_gpu_parity.py -m gpu $PT ;;
+    shard) step shard 300 python -u -m pytest tests/test_gpu_shard.py -m gpu $PT ;;
     writer) step writer 600 python -u -m pytest tests/test_gpu_writer.py -m gpu $PT ;;
     smoke) step smoke 300 python -u __graft_entry__.py smoke ;;
     c2) step c2 300 python -u $C2 ;;

@@ -2,8 +2,9 @@
 gather over gloo): each rank generates and replays its shard of the global document space on the
 GPU (the same calls bench.py makes per rank), digests and statuses are gathered to rank 0 by
 fluidframework_amd/shard.py, and the union equals one process replaying every document and the
-oracle on the downloaded logs.  RCCL itself needs one GPU per rank, which the round's one-GPU box
-does not have; the gather code is the same for both backends (tensors on the device for "nccl")."""
+oracle on the downloaded logs.  RCCL needs one GPU per rank, which the one-GPU box does not have for
+two ranks: the RCCL test runs the same gathers through a one-rank "nccl" process group, so the
+collectives execute in RCCL on the device tensors."""
 import os
 import socket
 
@@ -61,3 +62,36 @@ def test_hip_ranks_gather_equals_single_process(tmp_path):
     assert len(set(one.tolist())) == WORLD * DOCS  # the shards are disjoint documents
     _, dig, st = O.replay_batch(ops, off, text, props, O.gen_tables(), O.gen_client_names(8))
     assert (st == 0).all() and (dig == host).all()
+
+
+def _rccl_rank(rank, port, out_path):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    with fa.ReplayBatch(DOCS) as b:
+        b.generate(fa.gen_params(OPS, **GEN), 0)
+        b.run()
+        dig_np = b.device_digests()
+        dig = torch.from_numpy(dig_np.view(np.int64)).cuda()
+        st = torch.from_numpy(b.counters()["status"].astype(np.int64)).cuda()
+        snap = b.doc(0).snapshot_v1()["header"].encode()
+    res = shard.gather_results(dig, st, 1, 0)
+    blobs = shard.gather_bytes(torch.tensor(list(snap), dtype=torch.uint8, device="cuda"), 1, 0)
+    np.savez(out_path, dig=np.asarray(res[0]), st=np.asarray(res[1]), local=dig_np,
+             blob=blobs[0].cpu().numpy(), snap=np.frombuffer(snap, np.uint8))
+    dist.destroy_process_group()
+
+
+def test_rccl_gathers_one_rank_group(tmp_path):
+    """shard.gather_results / gather_bytes through a one-rank "nccl" (RCCL) process group on the
+    device: the gathered digests, statuses and bytes equal the local ones."""
+    out = tmp_path / "rccl.npz"
+    mp.spawn(_rccl_rank, args=(_free_port(), str(out)), nprocs=1, join=True)
+    got = np.load(out)
+    assert (got["st"] == 0).all()
+    assert (got["dig"].view(np.uint64) == got["local"]).all()
+    assert got["blob"].tobytes() == got["snap"].tobytes()
