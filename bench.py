@@ -231,7 +231,7 @@ def main():
     value = ops_all * args.steps / t_max
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     alg_bytes = b.algorithmic_bytes()
-    # roofline of the dominant kernel (launch 0, mt_replay_kernel_<class>): the algorithmic bytes
+    # roofline of the dominant kernel (the longest launch, mt_replay_kernel_<class>): the algorithmic bytes
     # of the ops it applied (DESIGN.md "Roofline": per-op share of the batch's algorithmic bytes)
     # over its average launch duration (hipEvents on the run stream)
     avg_first_ms = sum(first_ms) / len(first_ms)

@@ -3906,6 +3906,7 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
 #ifdef MT_PROF
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
     const uint64_t t_kernel = clock64();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the launch's drain profile
 #endif
     engine_setup(E, P, w, d, smem);
     const mt_op *ops = (const mt_op *)P.ops;
@@ -4018,6 +4019,7 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
                 P.lab_out ? P.lab_out + w * (int64_t)P.out_cap : nullptr);
 #ifdef MT_PROF
     E.pf[0] = clock64() - t_kernel;
+    E.pf[kProfSlots - 1] = (rt_start << 32) | (__builtin_amdgcn_s_memrealtime() & 0xFFFFFFFFu);
     if (P.prof && E.lane < kProfSlots) {
         uint64_t v = E.pf[0];
         for (int k = 1; k < kProfSlots; k++)

@@ -104,6 +104,7 @@ struct Launch {
     int64_t ops = 0;            // ops applied by this launch (resumed documents: after their checkpoint)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int level = 0;              // escalation depth (0: a first launch)
+    int stream = 0;             // 0: the run stream, 1..3: aux stream k - 1
     bool load = false;          // SnapshotLoader launch (mt_load_kernel): LOAD records, then a checkpoint
 };
 
@@ -1653,9 +1654,23 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
         const int cls = g.first.first, src = g.first.second;
         std::vector<int32_t> &docs = g.second;
         if (groups.size() == 1 && !class_in_hbm(cls) && src < 0 && n_replay == b->n_docs) {
-            Launch L;
-            L.cls = cls;
-            b->launches.push_back(L);  // every document, in index order
+            // every document, in index order; split into `first_split` launches of contiguous
+            // documents, each escalating on its own as it completes, so one part's next class
+            // fills the CUs that another part's tail leaves idle
+            static const int64_t first_split = getenv("MT_FIRST_SPLIT") ? atoi(getenv("MT_FIRST_SPLIT")) : 1;
+            const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(first_split, 4));
+            if (parts == 1 || b->n_docs < 4096 * parts) {
+                Launch L;
+                L.cls = cls;
+                b->launches.push_back(L);
+                break;
+            }
+            for (int64_t q = 0; q < parts; q++) {
+                Launch L;
+                L.cls = cls;
+                for (int64_t d = b->n_docs * q / parts; d < b->n_docs * (q + 1) / parts; d++) L.docs.push_back((int32_t)d);
+                b->launches.push_back(std::move(L));
+            }
             break;
         }
         std::stable_sort(docs.begin(), docs.end(), [&](int32_t x, int32_t y) {
@@ -1677,7 +1692,8 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
         Launch &L = b->launches[i];
         hipStream_t ls = s;
         if (i > (size_t)b->first0) {
-            hipStream_t &a = b->aux[(i - (size_t)b->first0 - 1) % 3];
+            L.stream = 1 + (int)((i - (size_t)b->first0 - 1) % 3);
+            hipStream_t &a = b->aux[L.stream - 1];
             if (!a) HIPCHK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
             HIPCHK(hipStreamWaitEvent(a, b->ev0, 0));
             ls = a;
@@ -1711,10 +1727,37 @@ static int gather_launch(mt_batch *b, int li) {
                 if (k == 0 && (double)pf[(size_t)i * mt::kProfSlots] > mx) mx = (double)pf[(size_t)i * mt::kProfSlots];
             }
         fprintf(stderr, "MT_PROF launch %d docs %lld lds %zu: mean cycles/doc", li, (long long)n, L.lds);
-        static const char *nm[mt::kProfSlots] = {"kernel", "descend", "split", "insert", "range", "zamboni", "overlay", "scour", "text", "heap", "pack", "settle",
-                                                     "scold", "resolve", "hforget", "unused"};
-        for (int k = 0; k < mt::kProfSlots; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (double)n);
+        static const char *nm[mt::kProfSlots - 1] = {"kernel", "descend", "split", "insert", "range", "zamboni", "overlay", "scour",
+                                                     "text", "heap", "pack", "settle", "scold", "resolve", "hforget"};
+        for (int k = 0; k < mt::kProfSlots - 1; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (double)n);
         fprintf(stderr, " max_kernel=%.0f\n", mx);
+        // drain profile from each document's start / end on the 100 MHz realtime counter (the
+        // last slot: start << 32 | end, low 32 bits each): the launch's span, how many documents
+        // were resident at the peak and on average, and the tail after the last document started
+        std::vector<std::pair<int64_t, int>> ev;
+        ev.reserve(2 * (size_t)n);
+        const uint32_t ref = (uint32_t)(pf[mt::kProfSlots - 1] >> 32);
+        int64_t t_end = 0, last_start = 0, busy = 0, dmax = 0;
+        for (int64_t i = 0; i < n; i++) {
+            const uint64_t v = pf[(size_t)i * mt::kProfSlots + mt::kProfSlots - 1];
+            const int64_t a = (int32_t)((uint32_t)(v >> 32) - ref), e = (int32_t)((uint32_t)v - ref);
+            ev.push_back({a, 1});
+            ev.push_back({e, -1});
+            busy += e - a;
+            dmax = std::max(dmax, e - a);
+            last_start = std::max(last_start, a);
+            t_end = std::max(t_end, e);
+        }
+        std::sort(ev.begin(), ev.end());
+        const int64_t t0 = ev.front().first;
+        int cur = 0, peak = 0;
+        for (auto &x : ev) peak = std::max(peak, cur += x.second);
+        const double span = (double)(t_end - t0);
+        fprintf(stderr, "MT_PROF drain %d docs %lld: span_ms=%.3f mean_doc_ms=%.3f max_doc_ms=%.3f peak_resident=%d "
+                        "mean_resident=%.1f packing=%.4f last_start_ms=%.3f tail_ms=%.3f\n",
+                li, (long long)n, span * 1e-5, (double)busy / (double)n * 1e-5, (double)dmax * 1e-5, peak,
+                (double)busy / span, (double)busy / (span * peak), (double)(last_start - t0) * 1e-5,
+                (double)(t_end - last_start) * 1e-5);
     }
 #endif
     std::vector<DocOut> tmp((size_t)n);
@@ -1743,12 +1786,20 @@ static int gather_launch(mt_batch *b, int li) {
 // round trip to HBM).  When a launch finishes, its escalated documents are grouped by target
 // class and launched at once on the next of the run / aux streams, so a large document's chain
 // of classes never waits for unrelated launches (mixed-size batches, config 4).
-static int launch_on(mt_batch *b, Launch &&L, int *next_stream, std::vector<int> &pending) {
+// The launch goes on the stream with the fewest pending launches (ties: `prefer`, the stream of
+// the launch that just finished, which is idle): a stream still running an unrelated launch would
+// queue it behind that launch's tail.
+static int launch_on(mt_batch *b, Launch &&L, int prefer, std::vector<int> &pending) {
     if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) L.cksrc.clear();
+    int busy[4] = {0, 0, 0, 0};
+    for (int p : pending) busy[b->launches[(size_t)p].stream]++;
+    int k = prefer;
+    for (int j = 0; j < 4; j++)
+        if (busy[j] < busy[k]) k = j;
+    L.stream = k;
     b->launches.push_back(std::move(L));
     const int li = (int)b->launches.size() - 1;
     Launch &N = b->launches.back();
-    const int k = (*next_stream)++ % 4;
     hipStream_t s = b->run_stream;
     if (k > 0) {
         hipStream_t &a = b->aux[k - 1];
@@ -1772,7 +1823,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
     if (!b || b->launches.empty()) return MT_ERR_STATE;
     std::vector<int> pending;
     for (int li = b->first0; li < b->n_first; li++) pending.push_back(li);
-    int next_stream = 1, rc = MT_OK;
+    int rc = MT_OK;
     while (!pending.empty()) {
         size_t k = 0;
         for (;; std::this_thread::sleep_for(std::chrono::microseconds(20))) {
@@ -1841,7 +1892,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
                 const size_t e = std::min(G.docs.size(), at + chunk);
                 L.docs.assign(G.docs.begin() + (long)at, G.docs.begin() + (long)e);
                 L.cksrc.assign(G.cksrc.begin() + (long)at, G.cksrc.begin() + (long)e);
-                rc = launch_on(b, std::move(L), &next_stream, pending);
+                rc = launch_on(b, std::move(L), S.stream, pending);
                 if (rc) return rc;
             }
         }

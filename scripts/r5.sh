@@ -7,7 +7,8 @@
 #                    the zamboni prefetch off (MT_ZAMBONI_PREFETCH=0), both off
 #   c3s_base / c2_base  the same with fluidframework_amd/libmtreplay_base.so (the previous tree)
 #   c3s_a / c2_a     the same with fluidframework_amd/libmtreplay_r5a.so (an A/B reference build)
-#   phases3          MT_PROF phase profile of the config-3 slice (libmtreplay_prof.so)
+#   phases3 / phases3f  MT_PROF phase + drain profile of the config-3 slice / full config 3 (libmtreplay_prof.so)
+#   c4               bench config 4 (Zipf sizes, the giant class), one step
 #   prof3            rocprofv3 kernel stats of the headline bench
 set -u
 mkdir -p gpurun_out
@@ -48,6 +49,9 @@ for s in "$@"; do
     c3s_z0) step c3s_z0 400 env MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
     c3s_q0z0) step c3s_q0z0 400 env MT_TEXT_QUEUE=0 MT_ZAMBONI_PREFETCH=0 python -u $C3S ;;
     c3) step c3 600 python -u bench.py --steps 3 --warmup 1 ;;
+    phases3f) step phases3f 600 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
+    c3fs[1-4]*) n=${s#c3fs}; step $s 400 env MT_FIRST_SPLIT=${n%%_*} python -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
+    c4) step c4 1000 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     pmcA3) step pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u $B3 ;;
     pmcB3) step pmcB3 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB3 -o run -- python3 -u $B3 ;;
