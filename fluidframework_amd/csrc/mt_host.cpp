@@ -864,6 +864,49 @@ static void rc_resolve_combine(mt_batch *b, const mt_op *ops, int64_t N, const m
     b->d_vt = nullptr;
 }
 
+// The device regions of a writer batch (a log with local ops or acks): pending-group regions
+// (MT_PEND_CAP entries per document, default 4096: the live entries of at most kPendMaxGroups
+// unacked ops, compacted when full), regenerated-op output (MT_REGEN_CAP words per document with
+// MT_OP_REGENERATE records, default 16384, 2 for the others) and the consensus regions.
+static int writer_regions(mt_batch *b, int64_t D, const std::vector<uint8_t> &has_regen,
+                          std::vector<uint64_t> &cons_base, const std::vector<uint32_t> &cons_img) {
+    const char *e = getenv("MT_PEND_CAP");
+    b->pend_cap = e && atoi(e) > 0 ? atoi(e) : 4096;
+    const uint64_t words = (uint64_t)mt::pend_words(b->pend_cap);
+    std::vector<uint64_t> pbase_((size_t)D + 1);
+    for (int64_t d = 0; d <= D; d++) pbase_[(size_t)d] = (uint64_t)d * words;
+    HIPCHK(dalloc(&b->d_pend, (size_t)(words * (uint64_t)D)));
+    if (D > 0) HIPCHK(hipMemset(b->d_pend, 0, 4 * words * (uint64_t)D));
+    HIPCHK(dalloc(&b->d_pend_base, (size_t)D + 1));
+    HIPCHK(hipMemcpy(b->d_pend_base, pbase_.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+    const char *er = getenv("MT_REGEN_CAP");
+    const uint64_t rcap = er && atoi(er) > 0 ? (uint64_t)atoi(er) : 16384;
+    std::vector<uint64_t> rbase((size_t)D + 1, 0);
+    uint64_t rtot = 0;
+    for (int64_t d = 0; d < D; d++) {
+        rbase[(size_t)d] = rtot;
+        rtot += has_regen[(size_t)d] ? rcap : 2;
+    }
+    rbase[(size_t)D] = rtot;
+    b->regen_cap = (int32_t)rcap;
+    HIPCHK(dalloc(&b->d_regen, (size_t)std::max<uint64_t>(rtot, 2)));
+    HIPCHK(hipMemset(b->d_regen, 0, 4 * std::max<uint64_t>(rtot, 2)));
+    HIPCHK(dalloc(&b->d_regen_base, (size_t)D + 1));
+    HIPCHK(hipMemcpy(b->d_regen_base, rbase.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+    // per-document caps differ (2 words without REGENERATE records): the device checks
+    // regen_cap only after a REGENERATE record, which only the large regions see
+    b->h_regen_base = std::move(rbase);
+    if (!cons_img.empty()) {
+        HIPCHK(dalloc(&b->d_cons, cons_img.size()));
+        HIPCHK(hipMemcpy(b->d_cons, cons_img.data(), 4 * cons_img.size(), hipMemcpyHostToDevice));
+        HIPCHK(dalloc(&b->d_cons_base, (size_t)D + 1));
+        HIPCHK(hipMemcpy(b->d_cons_base, cons_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
+        b->h_cons_base = std::move(cons_base);
+    }
+    b->writer = true;
+    return MT_OK;
+}
+
 MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_off, const uint16_t *text,
                            int64_t n_text, const mt_prop *props, int64_t n_props) {
     if (!b || !ops || !doc_op_off || doc_op_off[0] != 0 || n_text < 0 || n_props < 0) return MT_ERR_ARG;
@@ -1056,47 +1099,12 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     HIPCHK(dalloc(&b->d_idmap_base, (size_t)D + 1));
     HIPCHK(hipMemcpy(b->d_idmap_base, idmap_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
     if (writer) {
-        // pending-group regions: MT_PEND_CAP entries per document (default 4096: the live entries
-        // of at most kPendMaxGroups unacked ops, compacted when full)
-        const char *e = getenv("MT_PEND_CAP");
-        b->pend_cap = e && atoi(e) > 0 ? atoi(e) : 4096;
-        const uint64_t words = (uint64_t)mt::pend_words(b->pend_cap);
-        std::vector<uint64_t> pbase_((size_t)D + 1);
-        for (int64_t d = 0; d <= D; d++) pbase_[(size_t)d] = (uint64_t)d * words;
-        HIPCHK(dalloc(&b->d_pend, (size_t)(words * (uint64_t)D)));
-        if (D > 0) HIPCHK(hipMemset(b->d_pend, 0, 4 * words * (uint64_t)D));
-        HIPCHK(dalloc(&b->d_pend_base, (size_t)D + 1));
-        HIPCHK(hipMemcpy(b->d_pend_base, pbase_.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
-        // regenerated-op output (MT_OP_REGENERATE records): MT_REGEN_CAP words per document that
-        // has such records (default 16384), 2 for the others
-        const char *er = getenv("MT_REGEN_CAP");
-        const uint64_t rcap = er && atoi(er) > 0 ? (uint64_t)atoi(er) : 16384;
-        std::vector<uint64_t> rbase((size_t)D + 1, 0);
-        uint64_t rtot = 0;
-        for (int64_t d = 0; d < D; d++) {
-            rbase[(size_t)d] = rtot;
-            bool has = false;
-            for (int64_t i = b->h_off[(size_t)d]; i < b->h_off[(size_t)d + 1] && !has; i++)
-                has = ops[i].type == MT_OP_REGENERATE;
-            rtot += has ? rcap : 2;
-        }
-        rbase[(size_t)D] = rtot;
-        b->regen_cap = (int32_t)rcap;
-        HIPCHK(dalloc(&b->d_regen, (size_t)std::max<uint64_t>(rtot, 2)));
-        HIPCHK(hipMemset(b->d_regen, 0, 4 * std::max<uint64_t>(rtot, 2)));
-        HIPCHK(dalloc(&b->d_regen_base, (size_t)D + 1));
-        HIPCHK(hipMemcpy(b->d_regen_base, rbase.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
-        // per-document caps differ (2 words without REGENERATE records): the device checks
-        // regen_cap only after a REGENERATE record, which only the large regions see
-        b->h_regen_base = std::move(rbase);
-        if (!cons_img.empty()) {
-            HIPCHK(dalloc(&b->d_cons, cons_img.size()));
-            HIPCHK(hipMemcpy(b->d_cons, cons_img.data(), 4 * cons_img.size(), hipMemcpyHostToDevice));
-            HIPCHK(dalloc(&b->d_cons_base, (size_t)D + 1));
-            HIPCHK(hipMemcpy(b->d_cons_base, cons_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
-            b->h_cons_base = std::move(cons_base);
-        }
-        b->writer = true;
+        std::vector<uint8_t> has_regen((size_t)D, 0);
+        for (int64_t d = 0; d < D; d++)
+            for (int64_t i = b->h_off[(size_t)d]; i < b->h_off[(size_t)d + 1] && !has_regen[(size_t)d]; i++)
+                has_regen[(size_t)d] = ops[i].type == MT_OP_REGENERATE;
+        const int rc2 = writer_regions(b, D, has_regen, cons_base, cons_img);
+        if (rc2) return rc2;
     }
     HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_off, b->h_off.data(), sizeof(int64_t) * (size_t)(D + 1), hipMemcpyHostToDevice));
@@ -1174,7 +1182,8 @@ MT_API int mt_pack_json_gpu(mt_packed **out, int64_t n_docs, const char *json, c
 
 // GPU parse straight into the replay's layout: per-document text arenas (payloads document-
 // relative, the '\n' flags set), the same host metadata as mt_batch_ingest for a log of the
-// observer fast path (no LOAD / RELPOS / REGENERATE records, markers, combiningOps or local ops)
+// GPU fast path (no LOAD / REGENERATE records, no combiningOps but rewrite, no consensus ids; a
+// writer replica's local ops and acks get mt_batch_ingest's writer regions)
 MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t *doc_off, int64_t n_docs,
                                     const void *d_json, const char *observer, int64_t *bad_doc,
                                     mt_json_gpu_stats *stats) {
@@ -1369,6 +1378,11 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     HIPCHK(hipMemcpy(b->d_text_cap, b->h_text_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_pool_base, b->h_pool_base.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(b->d_pool_cap, b->h_pool_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
+    if (r.writer) {
+        std::vector<uint64_t> cons_base((size_t)D + 1, 0);
+        rc = writer_regions(b, D, std::vector<uint8_t>((size_t)D, 0), cons_base, {});
+        if (rc) return rc;
+    }
     b->have_log = true;
     b->generated = false;
     json_gpu_stats(r, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
@@ -1657,9 +1671,14 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
             // every document, in index order; split into `first_split` launches of contiguous
             // documents, each escalating on its own as it completes, so one part's next class
             // fills the CUs that another part's tail leaves idle
-            static const int64_t first_split = getenv("MT_FIRST_SPLIT") ? atoi(getenv("MT_FIRST_SPLIT")) : 1;
+            // (2 parts: config 3 +2.1 %; 4 parts: -5 %, every stream busy so escalations queue behind
+            // unrelated tails).  Only batches that climb the ladder: at least 32,768
+            // documents (a few rounds of the chip's residency) of >= 4,096 ops on average (config
+            // 5's 2k-op documents finish in 1-2 classes and ran 2.5 % slower split).  MT_FIRST_SPLIT
+            // overrides the part count.
+            static const int64_t first_split = getenv("MT_FIRST_SPLIT") ? atoi(getenv("MT_FIRST_SPLIT")) : 2;
             const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(first_split, 4));
-            if (parts == 1 || b->n_docs < 4096 * parts) {
+            if (parts == 1 || b->n_docs < 32768 || (!getenv("MT_FIRST_SPLIT") && b->total_ops < 4096 * b->n_docs)) {
                 Launch L;
                 L.cls = cls;
                 b->launches.push_back(L);

@@ -34,6 +34,7 @@ struct Result {
     int status = 0;         // MT_OK, MT_UNSUPPORTED (host parser needed), MT_ERR_*
     int64_t bad_doc = -1;   // first document outside the GPU fast path
     uint32_t fail_bits = 0; // reasons (kF* in mt_json_gpu.hip) of bad_doc
+    bool writer = false;    // a writer replica's log (local ops / acks) in some document
     int64_t n_ops = 0, n_text = 0, n_props = 0, n_msgs = 0;
     std::vector<int64_t> doc_op_off;       // D + 1, batch-global record offsets
     std::vector<uint32_t> doc_text;        // code units per document

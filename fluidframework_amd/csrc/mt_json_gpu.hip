@@ -55,13 +55,14 @@ enum : uint32_t {
     kFSyntax = 1,   // not JSON the host parser accepts as is (it decides: maybe an error)
     kFShape = 2,    // a message / op shape outside the fast path (markers, escapes, floats ...)
     kFRange = 4,    // an integer outside int32
-    kFWriter = 8,   // a writer replica's log (local ops / own acks)
+    kFWriter = 8,   // a writer replica's message outside the fast path (regenerate, notifyConsensus,
+                    // an ack with relative positions, a local op of another client ...)
     kFClients = 16, // more than 32765 clients
     kFCap = 32      // more messages than the scan's per-document region holds
 };
 
-// message flags
-enum : uint32_t { kMsgOp = 1 };
+// message flags: an op message; a local (unsequenced) one; one with a RELPOS record
+enum : uint32_t { kMsgOp = 1, kMsgLocal = 2, kMsgRel = 4 };
 
 struct Params {
     const uint8_t *J;
@@ -82,6 +83,7 @@ struct Params {
     int32_t *sg_d0, *sg_d1;
     // per document
     uint32_t *d_nmsg, *d_fail, *d_nrec, *d_ntext, *d_nprop, *d_npropops, *d_nnames, *d_nuk, *d_nuv, *d_nval;
+    uint32_t *d_writer;  // per document: a writer replica's log (local ops or acks of its own)
     uint32_t *cl_ht;                 // per document cl_cap[d] slots from cl_base[d] (2 x its names + 1, a power of 2)
     const uint64_t *cl_base;
     const uint32_t *cl_cap;
@@ -1082,6 +1084,7 @@ __host__ __device__ uint32_t relpos_record(const uint8_t *s, uint32_t n, const O
         rr.flags = (uint16_t)(rflags | (base.flags & MT_OPF_CLIENT_HI_MASK));
         if (W) cx.ops[mo.nrec] = rr;
         mo.nrec++;
+        mo.flags |= kMsgRel;  // an ack reads no positions: the host parser drops it (clients stage)
         return 0;
     }
     return (op.seen & kOPos1) ? 0u : (uint32_t)kFShape;  // an op without a position
@@ -1092,6 +1095,8 @@ template <bool W>
 __host__ __device__ uint32_t emit_op(const uint8_t *s, uint32_t n, const OpInfo &op, const mt_op &base, MsgOut &mo,
                             const Ctx &cx) {
     if (!(op.seen & kOType)) return kFShape;
+    // a local insert with an end position fails in the host parser (getValidOpRange, client.ts:520-524)
+    if (base.seq == -1 && op.type == 0 && (op.seen & (kOPos2 | kORel2))) return kFWriter;
     {
         const uint32_t f = relpos_record<W>(s, n, op, base, mo, cx);
         if (f) return f;
@@ -1259,7 +1264,7 @@ __host__ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0
     enum { kCl = 1, kSeq = 2, kRef = 4, kMsn = 8, kTy = 16, kCo = 32 };
     uint32_t seen = 0, contents_p = 0;
     int64_t seq = 0, ref = 0, msn = 0;
-    bool is_op = false;
+    bool is_op = false, notify = false;
     r.ws();
     if (r.at() == '}') return kFShape;
     for (;;) {
@@ -1305,6 +1310,9 @@ __host__ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0
             is_op = l == 2 && r.b(o) == 'o' && r.b(o + 1) == 'p';
         } else {
             if (bit == kCo) contents_p = r.p;
+            // {"notifyConsensus": truthy} on a local message (Client.annotateMarkerNotifyConsensus):
+            // the host parser's; null / false are absent
+            if (!bit && r.is(ko, kl, "notifyConsensus") && !(r.lit("null", 4) || r.lit("false", 5))) notify = true;
             // clientId / type of another JSON type: "null" / not an op (the host's rules)
             if (!skip_value(r)) return kFSyntax;
         }
@@ -1322,8 +1330,17 @@ __host__ __device__ uint32_t parse_msg(const uint8_t *s, uint32_t n, uint32_t p0
     }
     r.ws();
     if (r.at() != ',' && r.at() != ']') return kFSyntax;
-    if ((seen & (kSeq | kRef | kMsn)) != (kSeq | kRef | kMsn)) return kFShape;
-    if (seq == -1) return kFWriter;  // a local op: the writer path
+    // a writer replica's own unsequenced message (sequenceNumber -1) is a local op: no refSeq / msn
+    // needed, msn 0 (mt_json.cpp Packer1::run); regenerate / non-op / notifyConsensus ones: host
+    const bool local = (seen & kSeq) && seq == -1;
+    if (local) {
+        if (!is_op || notify) return kFWriter;
+        if (!(seen & kRef)) ref = 0;
+        msn = 0;
+        mo.flags |= kMsgLocal;
+    } else if ((seen & (kSeq | kRef | kMsn)) != (kSeq | kRef | kMsn)) {
+        return kFShape;
+    }
     if (is_op) mo.flags |= kMsgOp;
     mt_op base{};
     base.type = MT_OP_NOOP;
@@ -1554,16 +1571,24 @@ extern "C" __global__ __launch_bounds__(64) void jg_clients_kernel(Params P) {
     const uint32_t nmsg = P.d_nmsg[d];
     Spans S{P.J + P.doc_off[d], P.m_cloff, P.m_cllen, mb, P.obs + 256};
     uint32_t fail = 0;
-    // the observer's own messages: short id 0 (an op of its own is an ack: the writer path)
+    // the observer's own messages: short id 0.  A local op or an op of its own (an ack) makes the
+    // document a writer replica's log; an ack with relative positions (whose RELPOS record the host
+    // parser drops) and a local op of another client (an error there) leave the fast path
+    uint32_t wr = 0;
     for (uint32_t i0 = 0; i0 < nmsg; i0 += 64) {
         const uint32_t i = i0 + (uint32_t)lane;
-        if (i < nmsg && span_eq(S.ptr(i), S.n(i), P.obs, P.obs_len)) {
+        if (i >= nmsg) continue;
+        const uint32_t fl = P.m_flags[mb + i];
+        if (span_eq(S.ptr(i), S.n(i), P.obs, P.obs_len)) {
             P.m_cid[mb + i] = 0;
-            if (P.m_flags[mb + i] & kMsgOp) fail |= kFWriter;
-        } else if (i < nmsg) {
+            if (fl & (kMsgOp | kMsgLocal)) wr = 1;
+            if ((fl & kMsgRel) && !(fl & kMsgLocal)) fail |= kFWriter;
+        } else {
             P.m_cid[mb + i] = 0xFFFFFFFFu;
+            if (fl & kMsgLocal) fail |= kFWriter;
         }
     }
+    for (int o = 32; o > 0; o >>= 1) wr |= __shfl_xor(wr, o, 64);
     __syncthreads();
     uint32_t *tab = P.cl_ht + P.cl_base[d];
     const uint32_t *cid = P.m_cid;
@@ -1572,6 +1597,7 @@ extern "C" __global__ __launch_bounds__(64) void jg_clients_kernel(Params P) {
     for (int o = 32; o > 0; o >>= 1) fail |= __shfl_xor(fail, o, 64);
     if (cnt == 0xFFFFFFFFu || cnt + 1 > (uint32_t)MT_MAX_CLIENTS) fail |= kFClients;
     if (lane == 0) {
+        P.d_writer[d] = wr;
         P.d_nnames[d] = cnt == 0xFFFFFFFFu ? 0u : cnt + 1;
         if (fail) P.d_fail[d] = fail;
     }
@@ -1779,9 +1805,10 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
                          &P.m_npops, &P.m_nval, &P.m_valoff};
     for (uint32_t **a : marr) JGCHK(B.get(a, M));
     uint32_t **darr[] = {&P.d_nmsg, &P.d_fail, &P.d_nrec, &P.d_ntext, &P.d_nprop, &P.d_npropops,
-                         &P.d_nnames, &P.d_nuk, &P.d_nuv, &P.d_nval};
+                         &P.d_nnames, &P.d_nuk, &P.d_nuv, &P.d_nval, &P.d_writer};
     for (uint32_t **a : darr) JGCHK(B.get(a, (size_t)D));
     JGCHK(hipMemsetAsync(P.d_nrec, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
+    JGCHK(hipMemsetAsync(P.d_writer, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_ntext, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_nprop, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
     JGCHK(hipMemsetAsync(P.d_npropops, 0, 4 * (size_t)std::max<int64_t>(D, 1), s));
@@ -2005,6 +2032,11 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     JGCHK(dl(uvo, P.uv_off, (size_t)vp, s));
     JGCHK(dl(uvl, P.uv_len, (size_t)vp, s));
     JGCHK(dl(nnames, P.d_nnames, (size_t)D, s));
+    {
+        std::vector<uint32_t> wr;
+        JGCHK(dl(wr, P.d_writer, (size_t)D, s));
+        res.writer = std::any_of(wr.begin(), wr.end(), [](uint32_t x) { return x != 0; });
+    }
     std::vector<uint64_t> names_base((size_t)D);
     uint64_t nsum = 0;
     for (int64_t d = 0; d < D; d++) {

@@ -31,6 +31,7 @@ for s in "$@"; do
   case $s in
     tests) step tests 900 python -u -m pytest tests -m gpu $PT ;;
     parity) step parity 600 python -u -m pytest tests/test_gpu_parity.py -m gpu $PT ;;
+    gjson) step gjson 400 python -u -m pytest tests/test_gpu_json.py -m gpu $PT ;;
     shard) step shard 300 python -u -m pytest tests/test_gpu_shard.py -m gpu $PT ;;
     writer) step writer 600 python -u -m pytest tests/test_gpu_writer.py -m gpu $PT ;;
     smoke) step smoke 300 python -u __graft_entry__.py smoke ;;
@@ -51,6 +52,9 @@ for s in "$@"; do
     c3) step c3 600 python -u bench.py --steps 3 --warmup 1 ;;
     phases3f) step phases3f 600 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
     c3fs[1-4]*) n=${s#c3fs}; step $s 400 env MT_FIRST_SPLIT=${n%%_*} python -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
+    c5) step c5 400 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
+    c5fs1) step c5fs1 400 env MT_FIRST_SPLIT=1 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
+    pcap) step pcap 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "beyond_64_keys" $PT ;;
     c4) step c4 1000 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     pmcA3) step pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u $B3 ;;

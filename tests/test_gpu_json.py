@@ -140,8 +140,12 @@ OUTSIDE = [  # (message, reason) — every one must be reported, never parsed di
                       "combiningOp": {"defaultValue": 1}}), "combiningOp without a name"),
     (_msg("A", 1, 0, {"type": 1, "relativePos1": {"id": "m", "offset": 1.5}, "pos2": 1}), "float offset"),
     (_msg("A", 1, 0, {"type": 1, "relativePos1": {"id": {"x": 1}}, "pos2": 1}), "object id"),
-    (_msg("A", -1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "local op"),
-    (_msg("readonly", 1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "own op (ack)"),
+    (_msg("A", -1, 0, {"type": 0, "pos1": 0, "seg": "a"}), "local op of another client"),
+    (_msg("readonly", -1, 0, {"type": 0, "pos1": 0, "pos2": 1, "seg": "a"}), "local insert with an end"),
+    (_msg("readonly", -1, 0, [{"type": 1, "pos1": 0, "pos2": 1}], type_="regenerate"), "regenerate"),
+    (dict(_msg("readonly", -1, 0, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1}}), notifyConsensus=True),
+     "notifyConsensus"),
+    (_msg("readonly", 1, 0, {"type": 1, "relativePos1": {"id": "m"}, "pos2": 1}), "ack with a relative position"),
     (_msg("A", 1, 0, {"type": 3, "ops": [{"type": 3, "ops": []}]}), "nested group"),
     (_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "a", "register": "r"}), "register"),
     (_msg("A", 2 ** 31, 0, {"type": 1, "pos1": 0, "pos2": 1}), "seq beyond int32"),
@@ -414,3 +418,41 @@ def test_string_values_with_escapes_and_unicode():
         doc = ('[{"clientId":"A","sequenceNumber":1,"referenceSequenceNumber":0,"minimumSequenceNumber":0,'
                '"type":"op","contents":{"type":2,"pos1":0,"pos2":1,"props":{"k":' + raw + '}}}]')
         _same(["[]", doc])
+
+
+def _writer_streams(n_docs=6, steps=400):
+    """Writer replica "A"'s stream of several conflict farms (local ops as sequenceNumber -1, its own
+    sequenced messages as acks; rewrites and markers included): one document per farm."""
+    from writer_sim import farm
+
+    return [farm(4, steps, 11 + k, rewrite=20, markers=10).events["A"] for k in range(n_docs)]
+
+
+def test_writer_streams_parse_identically():
+    """A writer replica's log stays on the GPU fast path: records (seq -1 local ops, acks), text,
+    props and tables equal the host parser's byte for byte."""
+    docs = _writer_streams()
+    assert any(m["sequenceNumber"] == -1 for m in docs[0])
+    st = _same([json.dumps(d) for d in docs], observer="A")
+    assert st["n_msgs"] == sum(len(d) for d in docs)
+    got = PackedJsonGpu([json.dumps(d) for d in docs], "A").arrays()
+    assert (got.ops["seq"] == -1).any()
+
+
+def test_gpu_ingested_writer_streams_replay_like_host_and_oracle():
+    """mt_batch_ingest_json_gpu of writer streams sets up the writer regions (pending groups) and
+    replays in the writer kernel exactly like the host-ingested batch and the oracle's replica."""
+    from test_gpu_writer import oracle_replica
+
+    docs = _writer_streams()
+    texts = [json.dumps(d) for d in docs]
+    with fa.ReplayBatch(len(docs)) as g, fa.ReplayBatch(len(docs)) as h:
+        assert g.ingest_json(texts, observer="A", device="gpu")["path"] == "gpu"
+        h.ingest_json(texts, observer="A", device="host")
+        g.run()
+        h.run()
+        _replay_equal(g, h, len(docs))
+        for d, ev in enumerate(docs):
+            ref = oracle_replica("A", ev)
+            assert g.doc(d).status == 0 and g.doc(d).digest() == ref.digest(), d
+            assert g.doc(d).get_text() == ref.text()

@@ -721,3 +721,30 @@ def test_relative_positions_outside_the_device_path_are_flagged():
         b.ingest_messages(docs)
         b.run()
         assert [b.doc(i).status for i in range(len(docs))] == [fa.MT_UNSUPPORTED] * len(docs)
+
+
+def test_prop_sets_beyond_64_keys_stop_with_capacity():
+    """A segment's property set holds at most 64 keys on the GPU (one key per lane, props_extend):
+    an insert with 100 props and an annotate that grows a set past 64 keys stop their document with
+    MT_CAPACITY (cap_kind 3, the prop pool) — never a silently different result — while a
+    64-key set next to them replays to the oracle's digest."""
+    def msg(s, contents):
+        return {"clientId": "A", "sequenceNumber": s, "referenceSequenceNumber": s - 1,
+                "minimumSequenceNumber": 0, "type": "op", "contents": contents}
+
+    ins = lambda n: msg(1, {"type": 0, "pos1": 0, "seg": {"text": "abc", "props": {f"k{i}": i for i in range(n)}}})
+    docs = [[ins(100)],
+            [ins(40), msg(2, {"type": 2, "pos1": 0, "pos2": 2, "props": {f"m{i}": i for i in range(30)}})],
+            [ins(64), msg(2, {"type": 1, "pos1": 1, "pos2": 2})]]
+    with fa.ReplayBatch(len(docs)) as b:
+        b.ingest_json([json.dumps(d) for d in docs], device="host")
+        b.run()
+        c = b.counters()
+        for d in (0, 1):
+            assert fa.status_string(b.doc(d).status) == fa.status_string(6) and int(c["cap_kind"][d]) == 3, d
+        assert b.doc(2).status == 0
+        ref = O.Doc()
+        ref.start_collab("readonly")
+        for m in docs[2]:
+            assert ref.apply_msg(json.dumps(m)) == 0, ref.error
+        assert b.doc(2).digest() == ref.digest()
