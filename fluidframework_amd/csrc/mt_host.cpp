@@ -1899,6 +1899,30 @@ MT_API int mt_batch_sync(mt_batch *b) {
             L.docs.push_back((int32_t)d);
             L.cksrc.push_back(src);
         }
+        // longest remaining replay first (LPT): workgroups dispatch roughly in index order, so the
+        // documents with the most ops left start first and the launch's tail is short (MT_LPT=0: the
+        // previous launch's order)
+        static const bool lpt = !getenv("MT_LPT") || atoi(getenv("MT_LPT")) > 0;
+        for (auto &kv : groups) {
+            Launch &G = kv.second;
+            if (!lpt) continue;
+            std::vector<std::pair<int64_t, size_t>> key(G.docs.size());
+            for (size_t k = 0; k < G.docs.size(); k++) {
+                const int32_t d = G.docs[k];
+                const int64_t n_ops = b->h_off[(size_t)d + 1] - b->h_off[(size_t)d];
+                key[k] = {G.cksrc[k] >= 0 ? n_ops - b->docout[(size_t)d].ops_done : n_ops, k};
+            }
+            std::stable_sort(key.begin(), key.end(), [](const std::pair<int64_t, size_t> &x, const std::pair<int64_t, size_t> &y) {
+                return x.first > y.first;
+            });
+            std::vector<int32_t> docs(G.docs.size()), cks(G.cksrc.size());
+            for (size_t k = 0; k < key.size(); k++) {
+                docs[k] = G.docs[key[k].second];
+                cks[k] = G.cksrc[key[k].second];
+            }
+            G.docs.swap(docs);
+            G.cksrc.swap(cks);
+        }
         for (auto &kv : groups) {
             Launch &G = kv.second;
             // the HBM class holds ~220 MB per document: bounded launches

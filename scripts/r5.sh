@@ -55,6 +55,7 @@ for s in "$@"; do
     c5) step c5 400 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
     c5fs1) step c5fs1 400 env MT_FIRST_SPLIT=1 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
     pcap) step pcap 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "beyond_64_keys" $PT ;;
+    c3lpt[01]*) v=${s#c3lpt}; step $s 400 env MT_LPT=${v%%_*} python -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
     c4) step c4 1000 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     pmcA3) step pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u $B3 ;;
