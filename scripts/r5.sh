@@ -56,6 +56,15 @@ for s in "$@"; do
     c5fs1) step c5fs1 400 env MT_FIRST_SPLIT=1 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
     pcap) step pcap 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "beyond_64_keys" $PT ;;
     c3lpt[01]*) v=${s#c3lpt}; step $s 400 env MT_LPT=${v%%_*} python -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
+    snap) step snap 600 python -u -m pytest tests/test_gpu_snapshot.py tests/test_gpu_snapshot_load.py -m gpu $PT ;;
+    c5b) step c5b 400 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5b.so python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
+    c5_*) step $s 400 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
+    c5b_*) step $s 400 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5b.so python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
+    prof5n) step prof5n 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5n -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 2 --warmup 1 --no-cpu ;;
+    prof5b) step prof5b 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_r5b.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5b -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 2 --warmup 1 --no-cpu ;;
+    pmcA5n) step pmcA5n 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA5n -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 1 --warmup 0 --no-cpu ;;
+    pmcB5n) step pmcB5n 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmcB5n -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 1 --warmup 0 --no-cpu ;;
+    pmcw5n) step pmcw5n 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw5n -o run -- python3 -u bench.py --config 5 --docs 32768 --steps 1 --warmup 0 --no-cpu ;;
     c4) step c4 1000 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     pmcA3) step pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u $B3 ;;
