@@ -140,8 +140,10 @@ MT_API int mt_batch_ingest_packed(mt_batch *b, const mt_packed *p);
 
 /* JSON op logs parsed on the GPU (fluidframework_amd/csrc/mt_json_gpu.hip): the same records,
    text and tables as mt_pack_json for the observer fast path — sequenced messages whose contents
-   are insert (text / {text, props}) / remove / annotate without combiningOp / a one-level group of
-   those, prop values null / booleans / integers / plain ASCII strings.  A batch with any other
+   are insert (text / {text, props} / markers) / remove / annotate (no combiningOp but rewrite) /
+   relative positions / a one-level group of those, and a writer replica's (observer's) local
+   messages (sequenceNumber -1) and acks — not regenerate events, notifyConsensus, a local insert
+   with an end, or an ack with relative positions.  A batch with any other
    document returns MT_UNSUPPORTED with *bad_doc set and nothing changed: parse it with
    mt_pack_json (the bindings' ingest_json does).  json: the documents back to back, document d =
    json[doc_off[d] .. doc_off[d+1]), doc_off has n_docs + 1 entries and n_docs must equal the
