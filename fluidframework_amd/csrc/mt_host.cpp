@@ -286,6 +286,11 @@ static uint64_t fnv_name(const std::string &s) {
 struct mt_batch {
     int device = 0;
     hipStream_t stream = nullptr;
+    // launch buffers of finished runs, by size, for the next run's launches (lbuf_alloc): a step
+    // replays the same launch shapes, and a hipMalloc of the GBs a class launch holds costs tens of
+    // ms of host time between a launch and its escalation
+    std::multimap<size_t, void *> buf_cache;
+    std::map<void *, size_t> buf_bytes;  // every cached-allocator buffer's size
     int64_t n_docs = 0;
     mt_batch_options opt{};
     // tables
@@ -406,17 +411,57 @@ static void free_snap(mt_batch *b) {
     b->snap_ready = false;
 }
 
+// launch buffers: a cached one of the size (within 1/8 above it), else hipMalloc (on failure the
+// cache is released and the allocation retried).  Every launch writes what it reads first, so a
+// reused buffer's old contents are never seen.
+static void lbuf_release(mt_batch *b) {
+    for (auto &kv : b->buf_cache) {
+        (void)hipFree(kv.second);
+        b->buf_bytes.erase(kv.second);
+    }
+    b->buf_cache.clear();
+}
+template <class T>
+static hipError_t lbuf_alloc(mt_batch *b, T **p, size_t n) {
+    const size_t bytes = (n ? n : 1) * sizeof(T);
+    auto it = b->buf_cache.lower_bound(bytes);
+    if (it != b->buf_cache.end() && it->first - bytes <= bytes / 8) {
+        *p = (T *)it->second;
+        b->buf_cache.erase(it);
+        return hipSuccess;
+    }
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess && !b->buf_cache.empty()) {
+        (void)hipGetLastError();
+        lbuf_release(b);
+        e = hipMalloc(&q, bytes);
+    }
+    if (e == hipSuccess) b->buf_bytes[q] = bytes;
+    *p = (T *)q;
+    return e;
+}
+static void lbuf_free(mt_batch *b, void *p) {
+    if (!p) return;
+    auto it = b->buf_bytes.find(p);
+    if (it == b->buf_bytes.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    b->buf_cache.emplace(it->second, p);
+}
+
 static void free_launches(mt_batch *b) {
     for (auto &L : b->launches) {
-        (void)hipFree(L.d_out);
-        (void)hipFree(L.d_lab);
-        (void)hipFree(L.d_docout);
-        (void)hipFree(L.d_list);
-        (void)hipFree(L.d_prof);
-        (void)hipFree(L.d_cold);
-        (void)hipFree(L.d_ck);
-        (void)hipFree(L.d_cksrc);
-        (void)hipFree(L.d_state);
+        lbuf_free(b, L.d_out);
+        lbuf_free(b, L.d_lab);
+        lbuf_free(b, L.d_docout);
+        lbuf_free(b, L.d_list);
+        lbuf_free(b, L.d_prof);
+        lbuf_free(b, L.d_cold);
+        lbuf_free(b, L.d_ck);
+        lbuf_free(b, L.d_cksrc);
+        lbuf_free(b, L.d_state);
         if (L.e0) (void)hipEventDestroy(L.e0);
         if (L.e1) (void)hipEventDestroy(L.e1);
     }
@@ -424,6 +469,7 @@ static void free_launches(mt_batch *b) {
 }
 
 static void free_log(mt_batch *b) {
+    lbuf_release(b);  // a new log: other launch shapes
     (void)hipFree(b->d_ops);
     (void)hipFree(b->d_off);
     (void)hipFree(b->d_text);
@@ -530,6 +576,7 @@ MT_API int mt_batch_create(mt_batch **out, int64_t n_docs, const mt_batch_option
 MT_API void mt_batch_destroy(mt_batch *b) {
     if (!b) return;
     free_launches(b);
+    lbuf_release(b);
     free_snap(b);
     (void)hipFree(b->d_digest);
     free_log(b);
@@ -1493,21 +1540,22 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     L.caps = mt::class_caps(mt::kClassSegs[L.cls]);
     L.out_cap = L.caps.oe;
     L.lds = class_lds(L.cls);
-    HIPCHK(dalloc(&L.d_out, (size_t)n * (size_t)L.out_cap));
-    if (b->lab_track) HIPCHK(dalloc(&L.d_lab, (size_t)n * (size_t)L.out_cap));
-    HIPCHK(dalloc(&L.d_docout, (size_t)n));
-    HIPCHK(dalloc(&L.d_cold, (size_t)n * (size_t)L.caps.seg * mt::kColdPerSlot));
+    HIPCHK(lbuf_alloc(b, &L.d_out, (size_t)n * (size_t)L.out_cap));
+    if (b->lab_track) HIPCHK(lbuf_alloc(b, &L.d_lab, (size_t)n * (size_t)L.out_cap));
+    HIPCHK(lbuf_alloc(b, &L.d_docout, (size_t)n));
+    HIPCHK(lbuf_alloc(b, &L.d_cold, (size_t)n * (size_t)L.caps.seg * mt::kColdPerSlot));
+    // (the HBM class's table images: fresh allocations, as before)
     if (class_state_bytes(L.cls)) HIPCHK(dalloc(&L.d_state, (size_t)n * class_state_bytes(L.cls)));
     if (!L.docs.empty()) {
-        HIPCHK(dalloc(&L.d_list, L.docs.size()));
+        HIPCHK(lbuf_alloc(b, &L.d_list, L.docs.size()));
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
     }
     // documents short of headroom checkpoint here unless this is the largest usable class
     const bool can_grow = (class_usable(L.cls + 1) && b->opt.max_retries != 0) || L.load;
-    if (can_grow) HIPCHK(dalloc(&L.d_ck, (size_t)n * (size_t)mt::ck_words(L.caps.seg)));
+    if (can_grow) HIPCHK(lbuf_alloc(b, &L.d_ck, (size_t)n * (size_t)mt::ck_words(L.caps.seg)));
     const Launch *prev = L.src >= 0 ? &b->launches[(size_t)L.src] : nullptr;
     if (!L.cksrc.empty()) {
-        HIPCHK(dalloc(&L.d_cksrc, L.cksrc.size()));
+        HIPCHK(lbuf_alloc(b, &L.d_cksrc, L.cksrc.size()));
         HIPCHK(hipMemcpyAsync(L.d_cksrc, L.cksrc.data(), 4 * L.cksrc.size(), hipMemcpyHostToDevice, s));
     }
     mt::ReplayParams P = base_params(b);
@@ -1528,7 +1576,7 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
         P.cold_in_seg = prev->caps.seg;
     }
 #ifdef MT_PROF
-    HIPCHK(dalloc(&L.d_prof, (size_t)n * mt::kProfSlots));
+    HIPCHK(lbuf_alloc(b, &L.d_prof, (size_t)n * mt::kProfSlots));
     P.prof = L.d_prof;
 #endif
     const void *fn = L.load ? kKernels[L.cls].load : b->writer ? kKernels[L.cls].writer : kKernels[L.cls].replay;
@@ -1805,15 +1853,16 @@ static int gather_launch(mt_batch *b, int li) {
 // round trip to HBM).  When a launch finishes, its escalated documents are grouped by target
 // class and launched at once on the next of the run / aux streams, so a large document's chain
 // of classes never waits for unrelated launches (mixed-size batches, config 4).
-// The launch goes on the stream with the fewest pending launches (ties: `prefer`, the stream of
-// the launch that just finished, which is idle): a stream still running an unrelated launch would
-// queue it behind that launch's tail.
+// The launch goes on the aux stream with the fewest pending launches (ties: `prefer`, the stream
+// of the launch that just finished, which is idle): a stream still running an unrelated launch
+// would queue it behind that launch's tail, and the run stream waits for every first launch
+// (mt_batch_launch's join), so an escalation there would wait for the slowest of them.
 static int launch_on(mt_batch *b, Launch &&L, int prefer, std::vector<int> &pending) {
     if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) L.cksrc.clear();
     int busy[4] = {0, 0, 0, 0};
     for (int p : pending) busy[b->launches[(size_t)p].stream]++;
-    int k = prefer;
-    for (int j = 0; j < 4; j++)
+    int k = prefer > 0 ? prefer : 1;
+    for (int j = 1; j < 4; j++)
         if (busy[j] < busy[k]) k = j;
     L.stream = k;
     b->launches.push_back(std::move(L));
@@ -1859,8 +1908,18 @@ MT_API int mt_batch_sync(mt_batch *b) {
             Launch &L = b->launches[(size_t)li];
             HIPCHK(hipEventElapsedTime(&L.ms, L.e0, L.e1));
         }
+        static const bool host_timing = getenv("MT_HOST_TIMING") != nullptr;
+        const auto th0 = std::chrono::steady_clock::now();
         rc = gather_launch(b, li);
         if (rc) return rc;
+        if (host_timing) {
+            float at = 0;
+            (void)hipEventElapsedTime(&at, b->ev0, b->launches[(size_t)li].e1);
+            fprintf(stderr, "MT_HOST launch %d (class %d) ended at %.1f ms; seen at %.1f ms host; gather %.2f ms\n", li,
+                    mt::kClassSegs[b->launches[(size_t)li].cls], at,
+                    std::chrono::duration<double, std::milli>(th0 - b->t_launch).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count());
+        }
         const Launch &S = b->launches[(size_t)li];
         if (S.level >= b->opt.max_retries) continue;
         const int64_t n = launch_n(b->n_docs, S);
@@ -1935,8 +1994,14 @@ MT_API int mt_batch_sync(mt_batch *b) {
                 const size_t e = std::min(G.docs.size(), at + chunk);
                 L.docs.assign(G.docs.begin() + (long)at, G.docs.begin() + (long)e);
                 L.cksrc.assign(G.cksrc.begin() + (long)at, G.cksrc.begin() + (long)e);
+                const auto tl0 = std::chrono::steady_clock::now();
                 rc = launch_on(b, std::move(L), S.stream, pending);
                 if (rc) return rc;
+                if (host_timing)
+                    fprintf(stderr, "MT_HOST   launch %d (class %d, %zu docs, stream %d) submitted at %.1f ms host (%.2f ms)\n",
+                            (int)b->launches.size() - 1, mt::kClassSegs[G.cls], e - at, b->launches.back().stream,
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count(),
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl0).count());
             }
         }
     }
