@@ -1853,16 +1853,17 @@ static int gather_launch(mt_batch *b, int li) {
 // round trip to HBM).  When a launch finishes, its escalated documents are grouped by target
 // class and launched at once on the next of the run / aux streams, so a large document's chain
 // of classes never waits for unrelated launches (mixed-size batches, config 4).
-// The launch goes on the aux stream with the fewest pending launches (ties: `prefer`, the stream
-// of the launch that just finished, which is idle): a stream still running an unrelated launch
-// would queue it behind that launch's tail, and the run stream waits for every first launch
-// (mt_batch_launch's join), so an escalation there would wait for the slowest of them.
+// The launch goes on the stream with the fewest pending launches (ties: `prefer`, the stream of
+// the launch that just finished, which is idle): a stream still running an unrelated launch would
+// queue it behind that launch's tail.  (Keeping escalations off the run stream, which joins every
+// first launch, measured +0.4 % but made rocprofv3's kernel trace serialize the two chains' aux
+// queues, so its kernel durations no longer matched the bench's)
 static int launch_on(mt_batch *b, Launch &&L, int prefer, std::vector<int> &pending) {
     if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) L.cksrc.clear();
     int busy[4] = {0, 0, 0, 0};
     for (int p : pending) busy[b->launches[(size_t)p].stream]++;
-    int k = prefer > 0 ? prefer : 1;
-    for (int j = 1; j < 4; j++)
+    int k = prefer;
+    for (int j = 0; j < 4; j++)
         if (busy[j] < busy[k]) k = j;
     L.stream = k;
     b->launches.push_back(std::move(L));
