@@ -70,6 +70,7 @@ for s in "$@"; do
     c3ht) step c3ht 400 env MT_HOST_TIMING=1 python -u bench.py --config 3 --steps 1 --warmup 1 --no-cpu ;;
     c3sf*) v=${s#c3sf}; step $s 400 env MT_SPLIT_FRAC=0.${v%%_*} python -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
     c3prio*) step $s 400 env MT_CHAIN_PRIO=1 python -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
+    fullpar) step fullpar 1100 python -u tools/full_parity.py 65536 8192 gpurun_out/full_parity_config3.json ;;
     c4) step c4 1000 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     pmcA3) step pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u $B3 ;;
