@@ -56,7 +56,8 @@ def main():
     for li in line["launches"]:
         ops_by_class[li["seg_class"]] += li["ops"]
     cnt = read_counters(a.csv)
-    res = {"config": a.config, "docs": line["config"]["docs_per_gpu"], "ops": line["config"]["ops_per_doc"],
+    opd = line["config"]["ops_per_doc"]  # config 4: {"min", "max", "lpt_loads"} (bench.py's n_ops is the max)
+    res = {"config": a.config, "docs": line["config"]["docs_per_gpu"], "ops": opd["max"] if isinstance(opd, dict) else opd,
            "command": "bench.py --config %d --docs %d --steps 1 --warmup 0 --no-cpu" % (a.config, line["config"]["docs_per_gpu"]),
            "units": "counters per dispatch summed over instances; per_op = / ops applied by the launch",
            "kernels": {}}
