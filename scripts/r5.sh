@@ -77,6 +77,8 @@ for s in "$@"; do
     pmcw4) step pmcw4 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw4 -o run -- python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu ;;
     c3v_*) v=${s#c3v_}; step $s 400 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_${v%%_*}.so python -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
     rehearse2) step rehearse2 600 env MT_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --docs 32768 --no-cpu ;;
+    c2w) step c2w 400 python -u bench.py --config 2 --writers --steps 3 --warmup 1 ;;
+    c2f) step c2f 300 python -u bench.py --config 2 --steps 3 --warmup 1 ;;
     c4) step c4 1000 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     phases3) step phases3 400 env FLUIDFRAMEWORK_AMD_LIB=$PROF python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;
     pmcA3) step pmcA3 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcA3 -o run -- python3 -u $B3 ;;
