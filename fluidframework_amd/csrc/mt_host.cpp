@@ -452,6 +452,9 @@ static void lbuf_free(mt_batch *b, void *p) {
 }
 
 static void free_launches(mt_batch *b) {
+    // what the cache still holds was not taken by the run that is ending: released, so the cache
+    // never holds more than one run's launch buffers
+    lbuf_release(b);
     for (auto &L : b->launches) {
         lbuf_free(b, L.d_out);
         lbuf_free(b, L.d_lab);
