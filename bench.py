@@ -61,22 +61,97 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seg-cap", type=int, default=0, help="first capacity class (default: from the op count)")
     ap.add_argument("--snapshot", action="store_true", help="serialize SnapshotV1 of every doc in each step")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rank layout + gather to rank 0 only, no replay (tests the --gpus N launcher on CPU)")
     ap.add_argument("--writers", action="store_true",
                     help="replay every document as one of its writers (local ops + acks, the local-client path)")
     return ap.parse_args()
 
 
-def main():
-    args = parse()
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without an outer launcher: start N rank processes of this same command
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as torch.distributed.run
+    would), before this process touches the GPU (it never does: children are started with Popen,
+    never exec).  Rank 0 writes the JSON line to the inherited stdout.  Returns 0 when every rank
+    succeeded, else the first failing rank's exit status (the other ranks are then stopped)."""
+    import subprocess
+
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"[bench] rank {procs.index(p)} exited with status {code}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def launch_check(world, rank, backend):
+    """--launch-check: the rank layout and the gather to rank 0 without a replay (the CPU suite's
+    test of `--gpus N`): every rank contributes a digest per document of a 4-document shard and rank
+    0 prints {"launch_check": ..., "n_gpus", "ranks_gathered", "digests_gathered"}."""
+    import numpy as np
     import torch
     import torch.distributed as dist
 
+    from fluidframework_amd import shard
+
+    if world > 1:
+        dist.init_process_group(backend)
+    dig = torch.arange(4, dtype=torch.int64) + 4 * rank
+    st = torch.zeros(4, dtype=torch.int64)
+    g = shard.gather_results(dig, st, world, rank)
+    ranks_gathered = dist.get_world_size() if dist.is_initialized() else 1
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_gathered": ranks_gathered,
+                          "digests_gathered": int(len(g[0])),
+                          "digests_in_order": bool((g[0].astype(np.int64) == np.arange(4 * world)).all())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # MT_BENCH_BACKEND=gloo rehearses the multi-rank path with ranks sharing GPUs (RCCL needs
     # one rank per device); the real runs use "nccl" (= RCCL) with one process per GPU
     backend = os.environ.get("MT_BENCH_BACKEND", "nccl")
+    if args.launch_check:
+        launch_check(world, rank, backend)
+        return
+    import torch
+    import torch.distributed as dist
+
+    if world > 1 and backend == "nccl" and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, {torch.cuda.device_count()} visible")
     dev = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -179,16 +254,24 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms, first_ms, first_ops, snap_ms, snap_bytes = [], [], [], [], 0
+    cls_span, cls_ops, cls_launches = [], [], []
     gathered = None
     for i in range(args.steps):
         sn, gathered = step()
         kernel_ms.append(b.stats()["kernel_ms"])
         # the dominant kernel: the launch that took the longest (config 4: the giant-class launch of
         # the Zipf tail, not the class that applied the most ops)
-        l0 = max(b.launches(), key=lambda li: li["ms"])
+        lis = b.launches()
+        l0 = max(lis, key=lambda li: li["ms"])
         first_ms.append(l0["ms"])
         first_ops.append(l0["ops"])
         dom_class = l0["seg_class"]
+        # the launches of that class share the chip (config 3: the two halves' launches run
+        # concurrently): their ops over the span from the first one's start to the last one's end
+        dom = [li for li in lis if li["seg_class"] == dom_class]
+        cls_span.append(max(li["start_ms"] + li["ms"] for li in dom) - min(li["start_ms"] for li in dom))
+        cls_ops.append(sum(li["ops"] for li in dom))
+        cls_launches.append(len(dom))
         if with_snap:
             snap_ms.append(sn["device_ms"])
             snap_bytes = sn["bytes"]
@@ -203,6 +286,8 @@ def main():
     if args.writers:  # the metric counts the log's sequenced messages, not the writers' local copies
         ops_done -= n_local
     ops_all = ops_done
+    alg_bytes = b.algorithmic_bytes()
+    alg_all = alg_bytes
     if world > 1:
         dev = "cuda" if backend == "nccl" else "cpu"
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -211,6 +296,10 @@ def main():
         o = torch.tensor([ops_done], device=dev, dtype=torch.int64)
         dist.all_reduce(o, op=dist.ReduceOp.SUM)
         ops_all = int(o.item())
+        a = torch.tensor([alg_bytes], device=dev, dtype=torch.float64)
+        dist.all_reduce(a, op=dist.ReduceOp.SUM)
+        alg_all = float(a.item())
+    ranks_gathered = dist.get_world_size() if dist.is_initialized() else 1
     summaries = None
     if with_snap:  # the SnapshotV1 bytes themselves to rank 0 (after the timed steps)
         summaries = gather_summaries(b, torch, dist, world, rank, backend)
@@ -230,17 +319,25 @@ def main():
     # applied ops); requested_ops_per_step is reported beside it
     value = ops_all * args.steps / t_max
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
-    alg_bytes = b.algorithmic_bytes()
     # roofline of the dominant kernel (the longest launch, mt_replay_kernel_<class>): the algorithmic bytes
     # of the ops it applied (DESIGN.md "Roofline": per-op share of the batch's algorithmic bytes)
-    # over its average launch duration (hipEvents on the run stream)
+    # over its average launch duration (hipEvents on the launch's stream)
     avg_first_ms = sum(first_ms) / len(first_ms)
-    first_bytes = alg_bytes * (sum(first_ops) / len(first_ops)) / max(1, ops_done)
+    ops_per_launch = sum(first_ops) / len(first_ops)
+    alg_per_op = alg_bytes / max(1, ops_done)
+    first_bytes = alg_per_op * ops_per_launch
     achieved_gbs = first_bytes / (avg_first_ms * 1e-3) / 1e9
+    # the class window: every launch of the dominant class (they run concurrently) over their span
+    avg_cls_span = sum(cls_span) / len(cls_span)
+    avg_cls_ops = sum(cls_ops) / len(cls_ops)
+    class_gbs = alg_per_op * avg_cls_ops / (avg_cls_span * 1e-3) / 1e9
+    # the whole step: every rank's algorithmic bytes over the max-over-ranks step time
+    step_gbs = alg_all * args.steps / t_max / 1e9
     kname = f"mt_{'writer' if args.writers else 'replay'}_kernel_{dom_class}"
-    traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, kname)
-    lds = lds_busy(args.config, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
-    issue = issue_util(args.config, n_ops, kname, avg_first_ms, sum(first_ops) / len(first_ops))
+    traffic, traffic_src = pmc_traffic(args.config, n_docs, n_ops, kname, ops_per_launch)
+    # issue / LDS utilisation over the chip time the class's concurrent launches share
+    lds = lds_busy(args.config, n_ops, kname, avg_cls_span, avg_cls_ops)
+    issue = issue_util(args.config, n_ops, kname, avg_cls_span, avg_cls_ops)
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
@@ -282,11 +379,20 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "traffic_source": traffic_src,
+                         "traffic_per": "launch (PMC HBM bytes per op of this kernel x ops_per_launch)",
                          "kernel": kname, "avg_launch_ms": round(avg_first_ms, 3),
                          "algorithmic_bytes_per_launch": int(first_bytes),
+                         "algorithmic_bytes_per_op": round(alg_per_op, 2),
                          "algorithmic_bytes_formula": "32 B/op record + 2 B/inserted code unit + 8 B/prop record "
                                                       "+ 32 B/final table entry (DESIGN.md §5)",
-                         "ops_per_launch": int(sum(first_ops) / len(first_ops)),
+                         "ops_per_launch": int(ops_per_launch),
+                         "class_window": {"launches": round(sum(cls_launches) / len(cls_launches), 2),
+                                          "span_ms": round(avg_cls_span, 3), "ops": int(avg_cls_ops),
+                                          "achieved": round(class_gbs, 3),
+                                          "frac": round(class_gbs / HBM_PEAK_GBS, 6)},
+                         "step": {"achieved": round(step_gbs, 3), "frac": round(step_gbs / HBM_PEAK_GBS, 6),
+                                  "algorithmic_bytes_per_step": int(alg_all)},
+                         "utilisation_window": "issue_frac / lds_busy: the class window's ops over its span x the chip",
                          "lds_busy": lds,
                          "issue_frac": issue["frac"] if issue else None,
                          "issue": issue},
@@ -301,6 +407,7 @@ def main():
             # parity.digest_match compares statuses too
             "docs_not_ok": not_ok,
             "digests_gathered": len(gathered[0]) if rank == 0 else None,
+            "ranks_gathered": ranks_gathered,
             "digest_xor": digest_xor,
             "snapshot_digest_xor": snap_xor,
             "ops_applied_per_step": ops_all,
@@ -316,22 +423,24 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(config, n_docs, n_ops, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+def pmc_traffic(config, n_docs, n_ops, kernel, ops_per_launch):
+    """HBM bytes of one launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
     of this same configuration (tools/pmc_counters.py -> profiles/pmc_counters_config<N>.json,
     scripts/gpu_check.sh pmcf<N> / pmcw<N>): (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per the guide's
-    gfx950 correction.  The counters cannot be read from inside this process, so the profile of the
-    current kernel build is committed under profiles/ and quoted here; None when no profile of
-    this configuration and kernel exists."""
+    gfx950 correction.  The profile sums every launch of the kernel in one step (config 3: two
+    concurrent launches of the dominant class), so its bytes per op times this run's ops per launch
+    is the per-launch figure that pairs with algorithmic_bytes_per_launch.  The counters cannot be
+    read from inside this process, so the profile of the current kernel build is committed under
+    profiles/ and quoted here; None when no profile of this configuration and kernel exists."""
     path = ROOT / "profiles" / f"pmc_counters_config{config}.json"
     try:
         prof = json.loads(path.read_text())
     except (OSError, ValueError):
         return None, None
     k = prof.get("kernels", {}).get(kernel)
-    if prof.get("docs") != n_docs or prof.get("ops") != n_ops or not k or "hbm_bytes" not in k:
+    if prof.get("docs") != n_docs or prof.get("ops") != n_ops or not k or "hbm_bytes" not in k or not k.get("ops"):
         return None, None
-    return int(k["hbm_bytes"]), str(path.relative_to(ROOT))
+    return int(k["hbm_bytes"] / k["ops"] * ops_per_launch), str(path.relative_to(ROOT))
 
 
 def log(rank, msg):
@@ -440,8 +549,9 @@ INSTR_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SM
 def issue_util(config, n_ops, kernel, avg_ms, ops_per_launch):
     """What bounds the dominant kernel when neither HBM nor LDS does: its instruction issue.
     frac = instructions per op (the committed rocprofv3 SQ_INSTS_* passes of this configuration,
-    profiles/pmc_counters_config<N>.json) x the ops of one launch / (the launch time measured live
-    here x 256 CUs x 4 SIMDs x ~2.4 GHz), i.e. instructions per SIMD-cycle against one per cycle.
+    profiles/pmc_counters_config<N>.json) x the ops the class's concurrent launches applied / (their
+    span measured live here x 256 CUs x 4 SIMDs x ~2.4 GHz), i.e. instructions per SIMD-cycle against
+    one per cycle.
     One wave alone issues at most one instruction per ~4 cycles (MI355X_MICROARCH.md, 'vector-
     instruction ISSUE cost'), so `wave_frac` = 4 x instructions / SQ_WAVE_CYCLES-derived cycles per
     op is how much of its own issue ceiling a document's wave uses; `wait_share` = SQ_WAIT_ANY /

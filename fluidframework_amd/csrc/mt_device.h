@@ -185,9 +185,12 @@ constexpr int kGiantUlist = 1024;
 constexpr int kGiantChainRec = 4;  // HBM-resident blocks recorded per overlay list entry
 // The giant class's replay workgroup holds a second wave that prefetches (mt_engine.hip
 // giant_prefetch): the replaying wave publishes in LDS words [0] the index of the op it applies,
-// [1] root, [2] depth, [7] kGiantRun / kGiantDone; word [6] is the prefetch wave's sink
+// [1] root, [2] depth, [7] giant_run(w) / giant_done(w); word [6] is the prefetch wave's sink.
+// The state words name the workgroup's document slot w: LDS keeps its contents between the
+// workgroups a CU runs, so a state left by an earlier document never matches a later one's.
 constexpr int kGiantPubWords = 8;
-constexpr uint32_t kGiantRun = 0x52554E21u, kGiantDone = 0x444F4E45u;
+__host__ __device__ constexpr uint32_t giant_run(int64_t w) { return 0x80000000u ^ (uint32_t)(2 * w); }
+__host__ __device__ constexpr uint32_t giant_done(int64_t w) { return 0x80000000u ^ (uint32_t)(2 * w + 1); }
 constexpr int kGiantThreads = 128;
 constexpr int kCapCheckpoint = 6;  // DocOut.cap_kind of a checkpointed (resumable) document
 constexpr int kCapLongSeg = 8;     // beyond an LDS class's 16-bit lengths or relative seqs: a spill class

@@ -879,6 +879,10 @@ struct Engine {
                 cm = u_cm[j];
                 const uint32_t q = us_q(sr), r = us_r(sr);
                 elig = q <= m16 && (r == kRNone || r <= m16);
+                // a diverged writer's group-free segment with seq -1, removed at or below minSeq
+                // (op_ack): length 0 to every view, unlinked by the next scour of its block
+                if constexpr (kW)
+                    elig = elig || (q == kRUnassigned && r <= m16 && !(s_meta[slot] & kFPending));
                 if (elig) {
                     if (r == kRNone) add = s_len[slot];
                     b = s_blk[slot];
@@ -1592,18 +1596,46 @@ struct Engine {
             }
         }
     }
+    // is `key` among the cnt prop records at props_in[off...]?  (wave-uniform)
+    MT_FI bool key_among(uint32_t off, uint32_t cnt, uint32_t key) const {
+        for (uint32_t k0 = 0; k0 < cnt; k0 += kWave) {
+            const uint32_t k = k0 + (uint32_t)lane;
+            if (ballot(k < cnt && props_in[off + k].key == key)) return true;
+        }
+        return false;
+    }
     // Client.ackPendingSegment -> MergeTree.ackPendingSegment (client.ts:588-625, mergeTree.ts:
-    // 1893-1920) with BaseSegment.ack (487-522): the oldest group's segments, in group order, get
-    // the op's sequence number (insert: seq; remove: removedSeq unless a sequenced remove replaced
-    // the local one; annotate: its keys stop being pending), each then addToLRUSet; then zamboni
+    // 1893-1920) with BaseSegment.ack (487-522): the oldest group's segments, in group order, are
+    // acked by the rules of the *incoming* op's type — whatever op made the group (a replica whose
+    // local op was dropped as an invalid range acks the next op's group with this one) — each then
+    // addToLRUSet; then zamboni.  insert: assert(seq === Unassigned), seq = the message's; remove:
+    // assert(removedSeq), removedSeq = the message's unless a sequenced remove replaced the local one;
+    // annotate: assert(propertyManager), ackPendingProperties(op) decrements the pending counts of the
+    // op's keys.  A failing assert stops the document (MT_BAD_INPUT) at this record, as the reference
+    // throws here.  The device derives a segment's pending keys from the annotate groups still
+    // holding it (pending_keys); an annotate ack whose literal decrements differ from dropping the
+    // group (another op's keys, a rewrite count off by one), or an ack that leaves a segment with an
+    // unassigned seq / removedSeq and no group, is a state the device does not model: MT_UNSUPPORTED.
     MT_FI void op_ack(const mt_op &op) {
         if (n_pend > 0) {
             const uint32_t head = pend_word(1);
             const uint32_t b = head & kPmb;
-            const uint32_t tf = rfl(pdesc(head)[0]);
-            if ((tf & 0xFFu) != op.type) {  // not the op this group was made by: the stream is corrupt
-                set_fail(ST_BAD_INPUT);
+            const uint32_t *dh = pdesc(head);
+            const uint32_t tf = rfl(dh[0]), g_off = rfl(dh[1]), g_cnt = rfl(dh[2]);
+            if (op.type != MT_OP_INSERT && op.type != MT_OP_REMOVE && op.type != MT_OP_ANNOTATE) {
+                set_fail(ST_BAD_INPUT);  // BaseSegment.ack: unrecognized operation type
                 return;
+            }
+            // annotate: does dropping the group change the pending keys exactly as the op's ack does?
+            const bool g_ann = (tf & 0xFFu) == MT_OP_ANNOTATE;
+            const bool g_rw = g_ann && (((tf >> 16) & MT_OPF_REWRITE) != 0u);
+            const bool o_rw = (op.flags & MT_OPF_REWRITE) != 0u;
+            const uint32_t o_off = (uint32_t)op.payload, o_cnt = (uint32_t)op.payload_len;
+            bool same = false;
+            if (op.type == MT_OP_ANNOTATE && g_ann && g_rw == o_rw) {
+                same = true;
+                for (uint32_t k = 0; same && k < o_cnt; k++) same = key_among(g_off, g_cnt, rfl(props_in[o_off + k].key));
+                for (uint32_t k = 0; same && k < g_cnt; k++) same = key_among(o_off, o_cnt, rfl(props_in[g_off + k].key));
             }
             const uint32_t start = pend_word(2), n = pend_word(3);
             const uint2 *E = (const uint2 *)(pend + kPendEntries);
@@ -1617,13 +1649,14 @@ struct Engine {
                     const uint32_t meta = rfl((uint32_t)s_meta[slot]);
                     const uint32_t ui = meta & kUNone;
                     const USr sr = ui != kUNone ? u_sr[ui] : us_make(0u, kRNone);
-                    const uint32_t sq = rfl(us_q(sr)), srr = rfl(us_r(sr));
+                    uint32_t sq = rfl(us_q(sr)), srr = rfl(us_r(sr));
                     if (op.type == MT_OP_INSERT) {
                         if (ui == kUNone || sq != kRUnassigned) {
                             set_fail(ST_BAD_INPUT);
                             return;
                         }
-                        u_sr[ui] = us_make(rel(op.seq), srr);
+                        sq = rel(op.seq);
+                        u_sr[ui] = us_make(sq, srr);
                         if (lane == 0) cold[2 * slot + 1].x = (uint32_t)op.seq;
                     } else if (op.type == MT_OP_REMOVE) {
                         if (!(meta & kFRemoved)) {
@@ -1631,12 +1664,53 @@ struct Engine {
                             return;
                         }
                         if (ui != kUNone && srr == kRUnassigned) {
-                            u_sr[ui] = us_make(sq, rel(op.seq));
+                            srr = rel(op.seq);
+                            u_sr[ui] = us_make(sq, srr);
                             if (lane == 0) cold[2 * slot + 1].y = (uint32_t)op.seq;
+                        }
+                    } else {
+                        if (!(meta & kFHasProps)) {  // assert(!!this.propertyManager)
+                            set_fail(ST_BAD_INPUT);
+                            return;
+                        }
+                        if (!same) {
+                            // literal: the op's keys that are pending lose one count (and a rewrite
+                            // one rewrite); derived: the group's keys (and its rewrite) go
+                            uint32_t pk, npk;
+                            bool prw;
+                            pending_keys(slot, pk, npk, prw);
+                            if (status) return;
+                            bool ok = o_rw == g_rw;
+                            for (uint32_t k = 0; ok && k < o_cnt; k++) {
+                                const uint32_t key = rfl(props_in[o_off + k].key);
+                                const bool pend_k = ballot((uint32_t)lane < npk && pk == key) != 0;
+                                ok = pend_k == (g_ann && key_among(g_off, g_cnt, key));
+                            }
+                            for (uint32_t k = 0; ok && g_ann && k < g_cnt; k++)
+                                ok = key_among(o_off, o_cnt, rfl(props_in[g_off + k].key));
+                            if (!ok) {
+                                set_fail(ST_UNSUPPORTED);
+                                return;
+                            }
                         }
                     }
                     wsync();
-                    if (bit_free_after(head, slot, head, head)) pend_set_mask(slot, pend_mask(slot) & ~(1u << b));
+                    if (bit_free_after(head, slot, head, head)) {
+                        const uint32_t m = pend_mask(slot) & ~(1u << b);
+                        pend_set_mask(slot, m);
+                        // no group left, yet an unassigned seq (a diverged replica's ack): scourNode
+                        // sees `seq <= minSeq` / `removedSeq <= minSeq` for -1 and the group-free test
+                        // passes.  A removed one is then view-independent (length 0 to every view):
+                        // it settles and is unlinked as the reference's scour does; other shapes are
+                        // not modelled.
+                        if (m == 0u && ui != kUNone && (sq == kRUnassigned || srr == kRUnassigned)) {
+                            if (sq == kRUnassigned && srr != kRUnassigned && srr != kRNone) settled_min = min_seq - 1;
+                            else {
+                                set_fail(ST_UNSUPPORTED);
+                                return;
+                            }
+                        }
+                    }
                     add_to_lru(rfl((int32_t)s_blk[slot]), slot, op.seq);
                     lab_refresh(rfl((int32_t)s_blk[slot]));  // blockUpdatePathLengths(segment.parent)
                     if (status) return;
@@ -2304,11 +2378,16 @@ struct Engine {
                         ptoff = cold[2 * hslot].z;
                         stoff = cold[2 * fslot].z;
                     }
+#ifndef MT_EXP_NOTEXT
                     text_copy(dst, ptoff, pl);
                     text_copy(dst + pl, stoff, sl);
+#endif
                     ptoff = dst;
                     pcap = (ncap + 1u) & ~1u;
                 }
+#ifdef MT_EXP_NOTEXT  // experiment: the merges' text copies skipped (an upper bound of hiding them)
+                append = false;
+#endif
                 if (append) {
                     if (kTextBatch && sl <= (uint32_t)kWave) {
                         if (nq == kTextQ) text_flush(dd, ds, dl, nq);
@@ -4002,7 +4081,7 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
                         __hip_atomic_store(pub + 1, (uint32_t)E.root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_store(pub + 2, (uint32_t)E.depth, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_store(pub, (uint32_t)(base - b0 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_store(pub + 7, kGiantRun, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(pub + 7, giant_run(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
                 E.apply(op);
@@ -4037,7 +4116,8 @@ MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) 
 // prefetch) towards op k + 1's positions, and to the leaf block of the zamboni heap's top segment,
 // loading what those walks read — block rows, lengths, the leaves' lengths / meta words and cold
 // records — so the replaying wave's dependent loads find the lines in the CU's L1 / the XCD's L2.
-// It stops when the replaying wave publishes kGiantDone, or after 10 s without a new op index.
+// It stops when the replaying wave publishes giant_done(w), or after 10 s without a new op index
+// (a state word left in LDS by an earlier workgroup names another w and is ignored).
 template <int SEG>
 MT_FI void giant_prefetch(const ReplayParams &P, int64_t w, int64_t d) {
     if constexpr (is_giant_seg(SEG)) {
@@ -4102,10 +4182,10 @@ MT_FI void giant_prefetch(const ReplayParams &P, int64_t w, int64_t d) {
         };
         for (;;) {
             const uint32_t st = __hip_atomic_load(pub + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (st == kGiantDone) break;
+            if (st == giant_done(w)) break;
             const int32_t k = (int32_t)__hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (st != kGiantRun || k == last) {
+            if (st != giant_run(w) || k == last) {
                 if (now - t_prog > 1000000000ull) break;  // 10 s (100 MHz) without a new op
                 __builtin_amdgcn_s_sleep(2);
                 continue;
@@ -4144,7 +4224,7 @@ MT_FI void replay_body(const ReplayParams &P) {
             return;
         }
         replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
-        if (threadIdx.x == 0) __hip_atomic_store(pub + 7, kGiantDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (threadIdx.x == 0) __hip_atomic_store(pub + 7, giant_done(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
         replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
     }

@@ -455,6 +455,10 @@ static void free_launches(mt_batch *b) {
     // what the cache still holds was not taken by the run that is ending: released, so the cache
     // never holds more than one run's launch buffers
     lbuf_release(b);
+    // a run that ended early (an error in mt_batch_sync, or a launch without a sync) may still have
+    // kernels in flight on the aux streams: their buffers are cached only once those have finished
+    for (auto &L : b->launches)
+        if (L.e1) (void)hipEventSynchronize(L.e1);
     for (auto &L : b->launches) {
         lbuf_free(b, L.d_out);
         lbuf_free(b, L.d_lab);
@@ -1548,7 +1552,15 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     HIPCHK(lbuf_alloc(b, &L.d_docout, (size_t)n));
     HIPCHK(lbuf_alloc(b, &L.d_cold, (size_t)n * (size_t)L.caps.seg * mt::kColdPerSlot));
     // (the HBM class's table images: fresh allocations, as before)
-    if (class_state_bytes(L.cls)) HIPCHK(dalloc(&L.d_state, (size_t)n * class_state_bytes(L.cls)));
+    if (class_state_bytes(L.cls)) {
+        hipError_t e = dalloc(&L.d_state, (size_t)n * class_state_bytes(L.cls));
+        if (e != hipSuccess && !b->buf_cache.empty()) {  // cached buffers first
+            (void)hipGetLastError();
+            lbuf_release(b);
+            e = dalloc(&L.d_state, (size_t)n * class_state_bytes(L.cls));
+        }
+        HIPCHK(e);
+    }
     if (!L.docs.empty()) {
         HIPCHK(lbuf_alloc(b, &L.d_list, L.docs.size()));
         HIPCHK(hipMemcpyAsync(L.d_list, L.docs.data(), 4 * L.docs.size(), hipMemcpyHostToDevice, s));
@@ -1589,7 +1601,10 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     if (L.lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds));
     void *args[] = {&P};
     // the giant class's observer replay runs a prefetch wave beside the replaying one
-    const unsigned threads = (fn == kKernels[L.cls].replay && L.cls == mt::kGiantClass) ? (unsigned)mt::kGiantThreads : 64u;
+    // (MT_GIANT_PREFETCH=0: the replaying wave alone, for A/B profiles of the prefetch)
+    static const bool giant_pf = !getenv("MT_GIANT_PREFETCH") || atoi(getenv("MT_GIANT_PREFETCH")) > 0;
+    const unsigned threads =
+        (giant_pf && fn == kKernels[L.cls].replay && L.cls == mt::kGiantClass) ? (unsigned)mt::kGiantThreads : 64u;
     HIPCHK(hipLaunchKernel(fn, dim3((unsigned)n), dim3(threads), args, L.lds, s));
     return MT_OK;
 }
@@ -1926,6 +1941,9 @@ MT_API int mt_batch_sync(mt_batch *b) {
         }
         const Launch &S = b->launches[(size_t)li];
         if (S.level >= b->opt.max_retries) continue;
+        // launch_on appends to b->launches, so S dangles after the first one: what the escalations
+        // need of it is copied here
+        const int prefer = S.stream;
         const int64_t n = launch_n(b->n_docs, S);
         std::map<int, Launch> groups;
         int64_t n_ck = 0;
@@ -1999,7 +2017,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
                 L.docs.assign(G.docs.begin() + (long)at, G.docs.begin() + (long)e);
                 L.cksrc.assign(G.cksrc.begin() + (long)at, G.cksrc.begin() + (long)e);
                 const auto tl0 = std::chrono::steady_clock::now();
-                rc = launch_on(b, std::move(L), S.stream, pending);
+                rc = launch_on(b, std::move(L), prefer, pending);
                 if (rc) return rc;
                 if (host_timing)
                     fprintf(stderr, "MT_HOST   launch %d (class %d, %zu docs, stream %d) submitted at %.1f ms host (%.2f ms)\n",
@@ -2018,6 +2036,9 @@ MT_API int mt_batch_sync(mt_batch *b) {
     b->kernel_ms = mx;
     b->total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count();
     b->ran = true;
+    // every launch of the run is submitted: cached buffers it did not take are released, so the
+    // cache never holds memory beside a run's own
+    lbuf_release(b);
     return MT_OK;
 }
 
@@ -2108,6 +2129,7 @@ MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *o) {
     o->resumed = (int32_t)std::count_if(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x >= 0; });
     o->lds_bytes = (int32_t)L.lds;
     o->ms = L.ms;
+    if (L.e0 && b->ev0) (void)hipEventElapsedTime(&o->start_ms, b->ev0, L.e0);
     o->ops = L.ops;
     return MT_OK;
 }

@@ -96,10 +96,10 @@ class BatchOptions(C.Structure):
 
 class LaunchInfo(C.Structure):
     _fields_ = [("seg_class", C.c_int32), ("n_docs", C.c_int32), ("resumed", C.c_int32), ("lds_bytes", C.c_int32),
-                ("ms", C.c_float), ("reserved", C.c_int32), ("ops", C.c_int64)]
+                ("ms", C.c_float), ("start_ms", C.c_float), ("ops", C.c_int64)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class BatchStats(C.Structure):

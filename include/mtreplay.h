@@ -184,8 +184,8 @@ typedef struct mt_launch_info {
     int32_t n_docs;         /* documents (workgroups) in the launch                           */
     int32_t resumed;        /* of them resumed from a checkpoint (the rest start from op 0)   */
     int32_t lds_bytes;      /* dynamic LDS per document (0: HBM class)                        */
-    float ms;               /* device time (hipEvents on the run stream)                      */
-    int32_t reserved;
+    float ms;               /* device time (hipEvents on the launch's stream)                 */
+    float start_ms;         /* its start, from the run's start (concurrent launches overlap)  */
     int64_t ops;            /* ops applied by this launch                                     */
 } mt_launch_info;
 MT_API int mt_batch_launch_info(mt_batch *b, int32_t i, mt_launch_info *out);

@@ -207,6 +207,81 @@ def test_issue_1213_writer_on_gpu():
         assert_same(b.doc(0), oracle_replica("1", events))
 
 
+def _diverged_writer_log(kind):
+    """Hand-built writer-"1" logs whose local order diverged from the sequenced one: local ops with
+    an invalid range are dropped (getValidOpRange, client.ts:504-543: no segment group), so the
+    acks of the sequenced copies dequeue the *next* op's group and BaseSegment.ack runs the
+    incoming op's rules on it (mergeTree.ts:487-522, 1893-1920).  Returns the messages and the
+    index of the message the reference throws on (None: it never throws)."""
+    m = lambda op, seq, c, ref, msn=0: {"clientId": c, "sequenceNumber": seq, "referenceSequenceNumber": ref,  # noqa
+                                        "minimumSequenceNumber": msn, "type": "op", "contents": op}
+    rm_bad, rm_bad2 = {"type": 1, "pos1": 5, "pos2": 6}, {"type": 1, "pos1": 7, "pos2": 8}
+    an_bad = {"type": 2, "pos1": 5, "pos2": 6, "props": {"color": "red"}}
+    ins, rem = {"type": 0, "pos1": 0, "seg": "abc"}, {"type": 1, "pos1": 0, "pos2": 3}
+    ins_p = {"type": 0, "pos1": 0, "seg": {"text": "abc", "props": {"bold": True}}}
+    tail = [m({"type": 0, "pos1": 0, "seg": "zz"}, 5, "2", 4, 4), m({"type": 0, "pos1": 1, "seg": "y"}, 6, "2", 5, 5),
+            m({"type": 0, "pos1": 0, "seg": "q"}, 7, "2", 6, 6)]
+    if kind in ("orphan_removed_unlinked", "orphan_removed_held"):
+        # two dropped removes: their acks run the remove rules on the insert's and the remove's
+        # groups; "abc" ends with seq -1, removedSeq 1 and no group, and scourNode unlinks it
+        # once minSeq reaches 1 (held while minSeq is 0)
+        ev = [m(rm_bad, -1, "1", 0), m(rm_bad2, -1, "1", 0), m(ins, -1, "1", 0), m(rem, -1, "1", 0),
+              m(rm_bad, 1, "1", 0), m(rm_bad2, 2, "1", 0), m(ins, 3, "1", 0), m(rem, 4, "1", 0)]
+        return (ev + tail if kind == "orphan_removed_unlinked" else ev), None
+    if kind == "insert_rules_on_remove_group":
+        # the dropped remove's ack removes "abc" at seq 1; the insert's ack gives it seq 2 via its
+        # remove group; the remove's ack finds no group
+        ev = [m(rm_bad, -1, "1", 0), m(ins, -1, "1", 0), m(rem, -1, "1", 0),
+              m(rm_bad, 1, "1", 0), m(ins, 2, "1", 0), m(rem, 3, "1", 0), m({"type": 0, "pos1": 0, "seg": "k"}, 4, "2", 3, 3)]
+        return ev + tail, None
+    if kind == "throws_later":
+        # ... and the remove's ack meets the later insert's group: assert(removalInfo) throws
+        ev = [m(rm_bad, -1, "1", 0), m(ins, -1, "1", 0), m(rem, -1, "1", 0), m({"type": 0, "pos1": 0, "seg": "de"}, -1, "1", 0),
+              m(rm_bad, 1, "1", 0), m(ins, 2, "1", 0), m(rem, 3, "1", 0), m({"type": 0, "pos1": 0, "seg": "de"}, 4, "1", 0)]
+        return ev + tail, 6
+    if kind == "annotate_without_property_manager":
+        ev = [m(an_bad, -1, "1", 0), m(ins, -1, "1", 0), m(an_bad, 1, "1", 0), m(ins, 2, "1", 0)]
+        return ev + tail, 2
+    if kind == "unassigned_insert_orphan":
+        # the annotate's ack acks the insert's group (the segment has props): "abc" keeps seq -1
+        # with no group — a state the device does not model (MT_UNSUPPORTED)
+        ev = [m(an_bad, -1, "1", 0), m(ins_p, -1, "1", 0), m(an_bad, 1, "1", 0), m(ins_p, 2, "1", 0)]
+        return ev + tail, None
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["orphan_removed_unlinked", "orphan_removed_held", "insert_rules_on_remove_group",
+                                  "throws_later", "annotate_without_property_manager", "unassigned_insert_orphan"])
+def test_acks_follow_the_incoming_op_type(kind):
+    """A diverged replica keeps going where the reference's does: the GPU runs every ack with the
+    incoming op's rules on whatever group is oldest, stops (MT_BAD_INPUT) on the record whose assert
+    throws in the reference, and equals the oracle's replica before it and at the end."""
+    ev, throws_at = _diverged_writer_log(kind)
+    od = oracle_replica("1", ev)
+    with fa.ReplayBatch(1) as b:
+        b.ingest_messages([ev], observer=["1"])
+        b.run()
+        dv = b.doc(0)
+        if kind == "unassigned_insert_orphan":
+            assert od.status == 0 and dv.status == fa.MT_UNSUPPORTED, (od.error, fa.status_string(dv.status))
+            return
+        if throws_at is None:
+            assert od.status == 0, od.error
+            assert_same(dv, od, kind)
+            if kind == "orphan_removed_unlinked":
+                assert "abc" not in od.dump() and dv.get_text() == "qzyz"
+            return
+        assert od.status == ST_BAD_INPUT and dv.status == ST_BAD_INPUT, (od.error, fa.status_string(dv.status))
+        assert int(b.counters()["fail_op"][0]) == throws_at
+    before = ev[:throws_at]
+    od = oracle_replica("1", before)
+    with fa.ReplayBatch(1) as b:
+        b.ingest_messages([before], observer=["1"])
+        b.run()
+        assert od.status == 0
+        assert_same(b.doc(0), od, kind + " before the throw")
+
+
 def test_pending_segments_in_snapshot_and_text():
     """A writer stopped with ops still pending: getText holds its unacked inserts, SnapshotV1 elides
     them and its pending removes (snapshotV1.ts:184-186)."""
@@ -260,20 +335,18 @@ def _gen_writer_parity(p, n_docs, full_every=4, **opts):
 
 
 def _stopped_writer_parity(wops, woff, wnames, text, props, t, stopped, **opts):
-    """A replica stopped by a reference assert: the oracle applies every record before the GPU's
-    failing one without an error, and the GPU replay of the log cut before that record equals the
-    oracle's state there (digest, shape, text, props, SnapshotV1) — the state immediately before the
-    throw.  The oracle stops at that same record, or — the one place the device is stricter — the
-    record is the replica's own sequenced message acking a pending group of another op type, which
-    the device refuses at once (mt_engine.hip op_ack) while the reference acks the group with the
-    wrong op's rules and throws later (mergeTree.ts:1893-1920)."""
+    """A replica stopped by a reference assert: the oracle stops at the GPU's failing record — it
+    applies every record before it without an error and throws on it (an ack of a pending group is
+    run with the incoming op's BaseSegment.ack rules whatever op made the group, mergeTree.ts:
+    487-522, 1893-1920, on both sides) — and the GPU replay of the log cut before that record
+    equals the oracle's state there (digest, shape, text, props, SnapshotV1): the state immediately
+    before the throw."""
     logs = []
     for d, k in stopped:
         log = wops[woff[d]:woff[d + 1]]
         assert 0 <= k < len(log), (d, k)
-        if O.replay_doc(log[:k + 1].copy(), text, props, t, wnames[d]).status != ST_BAD_INPUT:
-            r = log[k]
-            assert r["seq"] >= 0 and (int(r["tc"]) >> 4) == 0, (d, k, r)  # an own ack
+        od = O.replay_doc(log[:k + 1].copy(), text, props, t, wnames[d])
+        assert od.status == ST_BAD_INPUT, (d, k, od.status, od.error)
         logs.append(log[:k].copy())
     off = np.zeros(len(logs) + 1, np.int64)
     off[1:] = np.cumsum([len(x) for x in logs])

@@ -145,3 +145,37 @@ def test_summaries_gather_over_gloo(tmp_path):
                                .values()) for d in range(DOCS)).encode("utf-8")
         want = want[: len(want) - 37 * r]
         assert got[f"arr_{r}"].tobytes() == want
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` with no outer launcher starts two rank processes itself (RANK /
+    WORLD_SIZE / MASTER_* set, Popen, never exec); --launch-check runs the rank layout and the
+    gather to rank 0 over gloo without a replay, so the CPU suite can see n_gpus and the gather."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["MT_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--launch-check"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks_gathered"] == 2
+    assert line["digests_gathered"] == 8 and line["digests_in_order"]
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MT_BENCH_BACKEND="gloo")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "4", "--launch-check"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -16,7 +16,7 @@ rel = g.PKG / "build" / "release"
 out = g.PKG / "build" / f"q_{name}"
 out.mkdir(parents=True, exist_ok=True)
 base = [g._hipcc(), "-x", "hip", "-O3", "-std=c++17", f"--offload-arch={g.ARCH}", "-fPIC", "-fvisibility=hidden", *flags]
-procs = [subprocess.Popen(base + ["-c", f"-DMT_SEG={seg}", "-o", str(out / f"k{seg}.o"),
+procs = [subprocess.Popen(base + ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-c", f"-DMT_SEG={seg}", "-o", str(out / f"k{seg}.o"),
                                   str(g.PKG / "csrc" / "mt_kernels.hip")], cwd=ROOT) for seg in classes]
 host_flags = [f for f in flags if f == "-DMT_PROF"]
 if host_flags:  # the host object sees the same switches (MT_PROF: its report)
