@@ -212,6 +212,10 @@ constexpr int kPendDesc = 8;
 constexpr int kPendEntries = kPendDesc + 4 * kPendMaxGroups;
 constexpr int kCapPending = 9;  // DocOut.cap_kind: the pending-entry region is full (terminal)
 constexpr int kCapRegen = 10;   // DocOut.cap_kind: the regenerated-op output region is full (terminal)
+// DocOut.cap_kind: a property set or op past one pair per lane in an observer replay kernel of an LDS
+// class; the host re-runs the document from scratch in the class's mt_bigprops_kernel_<SEG>
+// (mt_engine.hip props_extend_big), and its later escalations stay in the bigprops kernels
+constexpr int kCapBigProps = 11;
 constexpr int64_t pend_words(int32_t cap) { return kPendEntries + 2ll * cap; }
 // regenerated ops of MT_OP_REGENERATE records, per document (u32 words): [0] words used (from 2),
 // [1] records; per record {GROUP_CONT flag, ops} then per op {type, pos1, pos2, a, b, c, nprops, 0}

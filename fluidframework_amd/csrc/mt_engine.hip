@@ -205,8 +205,13 @@ struct BArr<T, kShift, true> {
 // kW: a writer replica (the local-client path: local ops with UnassignedSequenceNumber, pending
 // segment groups acked by the replica's own sequenced messages); compiled as mt_writer_kernel_<SEG>
 // so the observer kernels carry none of it
-template <int SEG, bool kW = false>
+// kBig: property sets past one pair per lane (props_extend_big) — compiled into the writer, load
+// and mt_bigprops_kernel_<SEG> kernels and the spill classes; the observer replay kernels of the LDS
+// classes stop such a document with cap_kind kCapBigProps and the host re-runs it in the bigprops
+// kernel, so their op loop carries none of it (its registers are the replay's bound)
+template <int SEG, bool kW = false, bool kBigK = false>
 struct Engine {
+    static constexpr bool kBig = kW || kBigK || is_hbm_seg(SEG);
     static constexpr Caps cap = class_caps(SEG);
     static constexpr Layout lay = make_layout(SEG);
     using Len = std::conditional_t<len_bytes(SEG) == 2u, uint16_t, uint32_t>;
@@ -1998,18 +2003,40 @@ struct Engine {
         if ((ha & hb & kSetRegular) && ha != hb) return false;
         const uint32_t na = pool[a], nb = pool[b];
         if (na != nb) return false;
-        bool ok = true, unk = false;
-        if ((uint32_t)lane < na) {
-            const uint32_t k = pool[a + 2 + 2 * lane], va = pool[a + 3 + 2 * lane];
-            int rel = 0;
-            for (uint32_t i = 0; i < nb; i++)
-                if (pool[b + 2 + 2 * i] == k)
-                    rel = value_rel(va, pool[b + 3 + 2 * i], vt->cls, vt->flags, vt->n_values, vt->exc, vt->n_exc);
-            ok = rel == 1;
-            unk = rel < 0;
+        if constexpr (!kBig) {  // sets of at most 64 pairs: one of a's per lane
+            bool ok = true, unk = false;
+            if ((uint32_t)lane < na) {
+                const uint32_t k = pool[a + 2 + 2 * lane], va = pool[a + 3 + 2 * lane];
+                int rel = 0;
+                for (uint32_t i = 0; i < nb; i++)
+                    if (pool[b + 2 + 2 * i] == k)
+                        rel = value_rel(va, pool[b + 3 + 2 * i], vt->cls, vt->flags, vt->n_values, vt->exc, vt->n_exc);
+                ok = rel == 1;
+                unk = rel < 0;
+            }
+            if (ballot(unk)) set_fail(ST_UNSUPPORTED);  // an undecided structural compare (kVUnknown)
+            return ballot(!ok) == 0;
         }
-        if (ballot(unk)) set_fail(ST_UNSUPPORTED);  // an undecided structural compare (kVUnknown)
-        return ballot(!ok) == 0;
+        // one of a's pairs per lane, 64 at a time (sets of any size)
+        for (uint32_t b0 = 0; b0 < na; b0 += kWave) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            bool ok = true, unk = false;
+            if (j < na) {
+                const uint32_t k = pool[a + 2 + 2 * j], va = pool[a + 3 + 2 * j];
+                int rel = 0;
+                for (uint32_t i = 0; i < nb; i++)
+                    if (pool[b + 2 + 2 * i] == k)
+                        rel = value_rel(va, pool[b + 3 + 2 * i], vt->cls, vt->flags, vt->n_values, vt->exc, vt->n_exc);
+                ok = rel == 1;
+                unk = rel < 0;
+            }
+            if (ballot(unk)) {  // an undecided structural compare (kVUnknown)
+                set_fail(ST_UNSUPPORTED);
+                return false;
+            }
+            if (ballot(!ok)) return false;
+        }
+        return true;
     }
 
     // combiningOp (segmentPropertiesManager.ts:96-101, properties.ts:26-60) per key, lane-parallel
@@ -2019,18 +2046,24 @@ struct Engine {
     // holds key ok_k; keys / vals (scratch) hold the set's n pairs.  Returns true when the device
     // cannot reproduce it (incr of a string / object, consensus updating a shared object in place,
     // an undefined result): the document is MT_UNSUPPORTED.
+    // (big: the set's pairs are in the pool at big[2 j], big[2 j + 1] instead, any n)
     MT_FI bool combine_values(uint32_t ckind, const mt_prop *op, uint32_t nop, uint32_t n, uint32_t ok_k,
-                              uint32_t &ok_v, bool inplace = false) {
+                              uint32_t &ok_v, bool inplace = false, const uint32_t *big = nullptr) {
         // the result slot: value = an absent key's result, key = the NaN value for "incr"
         // (mt_host.cpp rc_resolve_combine)
         const mt_prop res = op[nop + 2];
         const uint32_t nv = vt->n_values;
-        // lane j < n: the set's pair j; lane i < nop finds its key among them
-        const uint32_t kj = (uint32_t)lane < n ? scratch[lane] : MT_KEY_COMBINE;
-        const uint32_t vj = (uint32_t)lane < n ? scratch[64 + lane] : MT_VALUE_NULL;
         uint32_t ev = MT_VALUE_NULL;
-        for (uint32_t j = 0; j < n; j++)
-            if (rdl(kj, (int)j) == ok_k) ev = rdl(vj, (int)j);
+        if (kBig && big) {
+            for (uint32_t j = 0; j < n; j++)
+                if (big[2 * j] == ok_k) ev = big[2 * j + 1];
+        } else {
+            // lane j < n: the set's pair j; lane i < nop finds its key among them
+            const uint32_t kj = (uint32_t)lane < n ? scratch[lane] : MT_KEY_COMBINE;
+            const uint32_t vj = (uint32_t)lane < n ? scratch[64 + lane] : MT_VALUE_NULL;
+            for (uint32_t j = 0; j < n; j++)
+                if (rdl(kj, (int)j) == ok_k) ev = rdl(vj, (int)j);
+        }
         bool bad = false;
         if ((uint32_t)lane < nop) {
             if (ev != MT_VALUE_NULL) {
@@ -2060,6 +2093,133 @@ struct Engine {
         return ballot(bad) != 0;
     }
 
+    // props_extend for a set that may outgrow one pair per lane (TextSegment.make / annotate copy
+    // any number of keys: properties.ts:95, textSegment.ts:23-28): the new set is built in place in
+    // the pool, 64 pairs at a time — the old pairs copied, rewrite's deletions compacted, then the
+    // op's pairs applied in order (delete: the pairs after it move down one) — with the semantics and
+    // the content hash of the lane path, so both give equal sets equal hashes.  A combiningOp over
+    // more than 64 keys is MT_UNSUPPORTED (its per-key results are held one per lane).
+    MT_FI uint32_t props_extend_big(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout,
+                                    uint32_t ckind, uint32_t pk, uint32_t npk, bool inplace) {
+        if constexpr (!kBig) return 0;
+        if (ckind != MT_COMBINE_NONE && nop > 64u) {
+            set_fail(ST_UNSUPPORTED);
+            return 0;
+        }
+        const uint32_t n0 = old ? rfl(pool[old]) : 0u;
+        if (pool_top + 2u + 2u * (n0 + nop) > pool_end) {
+            cap_fail(3);
+            return 0;
+        }
+        const uint32_t id = pool_top;
+        uint32_t *kv = pool + id + 2;  // pair j: kv[2 j] key, kv[2 j + 1] value
+        for (uint32_t i = (uint32_t)lane; i < 2u * n0; i += kWave) kv[i] = pool[old + 2 + i];
+        wsync();
+        uint32_t n = n0;
+        uint32_t ok_v = 0;  // a combiningOp's value for op key `lane`
+        if (ckind != MT_COMBINE_NONE) {
+            uint32_t ok_k = 0;
+            if ((uint32_t)lane < nop) {
+                ok_k = op[lane].key;
+                ok_v = op[lane].value;
+            }
+            if (combine_values(ckind, op, nop, n, ok_k, ok_v, inplace, kv)) {
+                set_fail(ST_UNSUPPORTED);
+                return 0;
+            }
+        }
+        if (rewrite) {  // delete existing keys whose new value is absent or falsy (segmentPropertiesManager.ts:70-80)
+            uint32_t w = 0;
+            for (uint32_t b0 = 0; b0 < n; b0 += kWave) {
+                const uint32_t j = b0 + (uint32_t)lane;
+                uint32_t k = 0, v = 0;
+                bool keep = false;
+                if (j < n) {
+                    k = kv[2 * j];
+                    v = kv[2 * j + 1];
+                    for (uint32_t i = 0; i < nop; i++) {
+                        const mt_prop q = op[i];
+                        if (q.key == k && q.value < vt->n_values && !(vt->flags[q.value] & 1u)) keep = true;
+                    }
+                    for (uint32_t i = 0; i < npk; i++) keep |= rdl(pk, (int)i) == k;
+                }
+                const uint64_t km = ballot(keep);
+                wsync();  // the chunk is read before it is compacted (destinations <= sources)
+                if (keep) {
+                    const uint32_t dst = w + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
+                    kv[2 * dst] = k;
+                    kv[2 * dst + 1] = v;
+                }
+                w += (uint32_t)__popcll(km);
+                wsync();
+            }
+            n = w;
+        }
+        for (uint32_t i = 0; i < nop; i++) {
+            const uint32_t k = rfl(op[i].key);
+            const uint32_t v = ckind != MT_COMBINE_NONE ? rdl(ok_v, (int)i) : rfl(op[i].value);
+            if (npk && ballot((uint32_t)lane < npk && pk == k)) continue;  // a pending local key
+            int32_t at = -1;
+            for (uint32_t b0 = 0; b0 < n && at < 0; b0 += kWave) {
+                const uint32_t j = b0 + (uint32_t)lane;
+                const uint64_t hb = ballot(j < n && kv[2 * j] == k);
+                if (hb) at = (int32_t)(b0 + (uint32_t)first_lane(hb));
+            }
+            if (v == MT_VALUE_NULL) {
+                if (at >= 0) {
+                    for (uint32_t b0 = (uint32_t)at + 1u; b0 < n; b0 += kWave) {
+                        const uint32_t j = b0 + (uint32_t)lane;
+                        uint32_t kk = 0, vv = 0;
+                        if (j < n) {
+                            kk = kv[2 * j];
+                            vv = kv[2 * j + 1];
+                        }
+                        wsync();
+                        if (j < n) {
+                            kv[2 * j - 2] = kk;
+                            kv[2 * j - 1] = vv;
+                        }
+                        wsync();
+                    }
+                    n--;
+                }
+            } else if (at >= 0) {
+                if (lane == 0) kv[2 * (uint32_t)at + 1] = v;
+                wsync();
+            } else {
+                if (lane == 0) {
+                    kv[2 * n] = k;
+                    kv[2 * n + 1] = v;
+                }
+                n++;
+                wsync();
+            }
+        }
+        uint32_t h = 0;
+        bool irr = false, never = false;
+        for (uint32_t b0 = 0; b0 < n; b0 += kWave) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            if (j < n) {
+                const uint32_t k = kv[2 * j], v = kv[2 * j + 1];
+                const bool known = v < vt->n_values;
+                const uint32_t f = known ? vt->flags[v] : 0u;
+                h += hash_pair(k, known ? vt->cls[v] : 0xFFFFFFFFu - v);
+                never |= (f & kVNever) != 0;
+                irr |= !known || (f & (kVIrregular | kVUnknown | kVNever));
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, kWave);
+        h = (rfl(h) & ~(kSetRegular | kSetNever)) | (ballot(irr) ? 0u : kSetRegular) | (ballot(never) ? kSetNever : 0u);
+        if (lane == 0) {
+            pool[id] = n;
+            pool[id + 1] = h;
+        }
+        pool_top = id + 2u + 2u * n;
+        hout = h;
+        wsync();
+        return id;
+    }
+
     // SegmentPropertiesManager.addProperties for a sequenced remote op (or insert-time props):
     // start from `old` (0 = undefined -> new empty map), apply rewrite then the op's pairs in
     // order (null deletes: properties.ts:95-116).  Returns the new set id (hash in hout).
@@ -2069,15 +2229,23 @@ struct Engine {
     // value, except that "incr" turns a number / boolean / NaN into NaN.
     // Writer: pk / npk (lane j < npk: key j) are the keys of pending local annotates on the segment,
     // which a remote op leaves alone (shouldModifyKey, segmentPropertiesManager.ts:56-63).
+    // Sets and ops of at most 64 pairs together are built in LDS, one pair per lane; larger ones
+    // in the pool itself (props_extend_big).  The caller reserved 2 + 2 (set size + nop) pool words.
     MT_FI uint32_t props_extend(uint32_t old, const mt_prop *op, uint32_t nop, bool rewrite, uint32_t &hout,
                                 uint32_t ckind = 0u, uint32_t pk = 0u, uint32_t npk = 0u, bool inplace = false) {
         uint32_t *keys = scratch;
         uint32_t *vals = scratch + 64;
         uint32_t n = old ? pool[old] : 0u;
-        if (n > 64u || nop > 64u) {
-            cap_fail(3);
+#ifdef MT_EXP_NOBIG
+        if (n + nop > 64u) { cap_fail(3); return 0; }
+#else
+        if constexpr (kBig) {
+            if (n + nop > 64u) return props_extend_big(old, op, nop, rewrite, hout, ckind, pk, npk, inplace);
+        } else if (n > 64u || nop > 64u) {
+            cap_fail(kCapBigProps);  // the bigprops kernel re-runs the document
             return 0;
         }
+#endif
         wsync();
         if ((uint32_t)lane < n) {
             keys[lane] = pool[old + 2 + 2 * lane];
@@ -2153,7 +2321,7 @@ struct Engine {
                 wsync();
             } else {
                 if (n >= 64u) {
-                    cap_fail(3);
+                    cap_fail(kCapBigProps);
                     return 0;
                 }
                 if (lane == 0) {
@@ -2640,9 +2808,15 @@ struct Engine {
             if (slot < 0) return;
             uint32_t props = 0, ph = 0;
             if (op.flags & MT_OPF_HAS_PROPS) {
-                pool_reserve(2u + 2u * MT_OPF_NPROPS(op.flags));
+                uint32_t p0 = 0;
+                const uint32_t np = mt_insert_props(&op, props_in, &p0);
+                if (!kBig && np > 64u) {
+                    cap_fail(kCapBigProps);
+                    return;
+                }
+                pool_reserve(2u + 2u * np);
                 if (status) return;
-                props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
+                props = props_extend(0, props_in + p0, np, false, ph);
                 if (status) return;
             }
             const int32_t rseq = loaded ? op.ref_seq : kNoneSeq;
@@ -2704,9 +2878,15 @@ struct Engine {
         if (slot < 0) return;
         uint32_t props = 0, ph = 0;
         if (op.flags & MT_OPF_HAS_PROPS) {
-            pool_reserve(2u + 2u * MT_OPF_NPROPS(op.flags));
+            uint32_t p0 = 0;
+            const uint32_t np = mt_insert_props(&op, props_in, &p0);
+            if (!kBig && np > 64u) {
+                cap_fail(kCapBigProps);
+                return;
+            }
+            pool_reserve(2u + 2u * np);
             if (status) return;
-            props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
+            props = props_extend(0, props_in + p0, np, false, ph);
             if (status) return;
         }
         const int32_t rseq = op.ref_seq;
@@ -3047,7 +3227,13 @@ struct Engine {
                 const uint32_t sl = rdl(slot, f);
                 if (!is_remove) {
                     int32_t g0 = pool_gcs;
-                    pool_reserve(2u + 2u * (64u + op.payload_len));
+                    if constexpr (kBig) {  // room for the largest set this op can make from the segment's
+                        const uint32_t o0 = rdl(oldp, f);
+                        const uint32_t n0 = o0 ? rfl(pool[o0]) : 0u;
+                        pool_reserve(2u + 2u * ((n0 > 64u ? n0 : 64u) + op.payload_len));
+                    } else {
+                        pool_reserve(2u + 2u * (64u + op.payload_len));
+                    }
                     if (status) return;
                     uint32_t old;
                     if (pool_gcs != g0) {  // ids moved
@@ -3220,7 +3406,11 @@ struct Engine {
                 return;
             }
             if (slot != kIdUnlinked) {
-                pool_reserve(2u + 2u * (64u + op.payload_len));
+                {
+                    const uint32_t o0 = rfl(cold[2 * slot].x);
+                    const uint32_t n0 = o0 ? rfl(pool[o0]) : 0u;
+                    pool_reserve(2u + 2u * ((n0 > 64u ? n0 : 64u) + op.payload_len));
+                }
                 if (status) return;
                 const uint32_t old = rfl(cold[2 * slot].x);
                 uint32_t nh;
@@ -3917,8 +4107,8 @@ __device__ __forceinline__ mt_op bcast_op(const mt_op &o, int l) {
     return r;
 }
 
-template <int SEG, bool kW>
-MT_FI void engine_setup(Engine<SEG, kW> &E, const ReplayParams &P, int64_t w, int64_t d, uint8_t *smem) {
+template <int SEG, bool kW, bool kBigK>
+MT_FI void engine_setup(Engine<SEG, kW, kBigK> &E, const ReplayParams &P, int64_t w, int64_t d, uint8_t *smem) {
     E.lane = threadIdx.x;
     if constexpr (is_giant_seg(SEG)) {
         extern __shared__ __attribute__((aligned(16))) uint8_t gsmem[];
@@ -3978,10 +4168,10 @@ MT_FI uint8_t *tables(const ReplayParams &P, int64_t w) {
 // Workgroup index w writes its results at w; document d; src >= 0: resume from the checkpoint
 // ck_in[src] (kSrcList: src = ck_src[w]).  Returns true if the document stopped at a checkpoint.
 constexpr int32_t kSrcList = -2;
-template <int SEG, bool kLoad, bool kW = false>
+template <int SEG, bool kLoad, bool kW = false, bool kBigK = false>
 MT_FI bool replay_one(const ReplayParams &P, int64_t w, int64_t d, int32_t src) {
     uint8_t *smem = tables<SEG>(P, w);
-    Engine<SEG, kW> E;
+    Engine<SEG, kW, kBigK || kLoad> E;
 #ifdef MT_PROF
     for (int k = 0; k < kProfSlots; k++) E.pf[k] = 0;
     const uint64_t t_kernel = clock64();
@@ -4211,22 +4401,22 @@ MT_FI void giant_prefetch(const ReplayParams &P, int64_t w, int64_t d) {
 }
 
 // one workgroup per document (blockIdx.x); the giant class's observer replay adds the prefetch wave
-template <int SEG, bool kLoad, bool kW = false>
+template <int SEG, bool kLoad, bool kW = false, bool kBigK = false>
 MT_FI void replay_body(const ReplayParams &P) {
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
-    if constexpr (is_giant_seg(SEG) && !kLoad && !kW) {
+    if constexpr (is_giant_seg(SEG) && !kLoad && !kW && !kBigK) {
         extern __shared__ __attribute__((aligned(16))) uint8_t gsmem[];
         uint32_t *pub = (uint32_t *)(gsmem + make_glayout().pub);
         if (threadIdx.x >= (unsigned)kWave) {
             giant_prefetch<SEG>(P, w, d);
             return;
         }
-        replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
+        replay_one<SEG, kLoad, kW, kBigK>(P, w, d, kSrcList);
         if (threadIdx.x == 0) __hip_atomic_store(pub + 7, giant_done(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
-        replay_one<SEG, kLoad, kW>(P, w, d, kSrcList);
+        replay_one<SEG, kLoad, kW, kBigK>(P, w, d, kSrcList);
     }
 }
 

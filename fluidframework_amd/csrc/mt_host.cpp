@@ -22,6 +22,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/mtreplay.h"
@@ -33,6 +34,7 @@
 #define MT_DECLARE_CLASS(S)                                                   \
     extern "C" __global__ void mt_replay_kernel_##S(mt::ReplayParams P);      \
     extern "C" __global__ void mt_writer_kernel_##S(mt::ReplayParams P);      \
+    extern "C" __global__ void mt_bigprops_kernel_##S(mt::ReplayParams P);    \
     extern "C" __global__ void mt_load_kernel_##S(mt::ReplayParams P);        \
     extern "C" __global__ void mt_generate_kernel_##S(mt::ReplayParams P);
 MT_CLASS_LIST(MT_DECLARE_CLASS)
@@ -75,10 +77,12 @@ struct KernelClass {
     const void *replay;
     const void *generate;
     const void *load;
-    const void *writer;  // replay + the local-client path (writer replicas)
+    const void *writer;    // replay + the local-client path (writer replicas)
+    const void *bigprops;  // the observer replay with property sets of any size (mt_device.h kCapBigProps)
 };
 #define MT_KERNEL_CLASS_(S) {S, (const void *)mt_replay_kernel_##S, (const void *)mt_generate_kernel_##S, \
-                             (const void *)mt_load_kernel_##S, (const void *)mt_writer_kernel_##S},
+                             (const void *)mt_load_kernel_##S, (const void *)mt_writer_kernel_##S,    \
+                             (const void *)mt_bigprops_kernel_##S},
 static const KernelClass kKernels[mt::kNumClasses] = {MT_CLASS_LIST(MT_KERNEL_CLASS_)};
 #undef MT_KERNEL_CLASS_
 constexpr size_t kGenStaticLds = 256;  // generate_body's lref[64]
@@ -106,6 +110,7 @@ struct Launch {
     int level = 0;              // escalation depth (0: a first launch)
     int stream = 0;             // 0: the run stream, 1..3: aux stream k - 1
     bool load = false;          // SnapshotLoader launch (mt_load_kernel): LOAD records, then a checkpoint
+    bool big = false;           // observer documents with large property sets: mt_bigprops_kernel_<SEG>
 };
 
 // workgroups (documents) of a launch
@@ -792,9 +797,12 @@ static void resolve_marker_ids(mt_batch *b, std::vector<mt_op> &h_ops, const std
             mt_op &o = h_ops[(size_t)i];
             if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
                 uint32_t id = 0;
-                if (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)
-                    for (uint32_t q = 0; q < MT_OPF_NPROPS(o.flags); q++)
-                        if ((int64_t)o.pos2 + q < n_props && props[o.pos2 + q].key == mk) id = key_of(props[o.pos2 + q].value);
+                if (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS) {
+                    uint32_t p0 = 0;
+                    const uint32_t np = mt_insert_props(&o, props, &p0);
+                    for (uint32_t q = 0; q < np; q++)
+                        if ((int64_t)p0 + q < n_props && props[p0 + q].key == mk) id = key_of(props[p0 + q].value);
+                }
                 o.payload_len = id;
                 if (id) total++;
             } else if (o.type == MT_OP_ANNOTATE) {
@@ -993,7 +1001,7 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         for (int64_t i = a + nload[d]; i < e; i++)  // LOAD records only lead a log
             if (ops[i].type == MT_OP_LOAD_HEADER || ops[i].type == MT_OP_LOAD_BODY || ops[i].type == MT_OP_COLLAB)
                 return MT_ERR_ARG;
-        uint64_t pay = 0, nprop_ops = 0;
+        uint64_t pay = 0, nprop_ops = 0, precs = 0;
         for (int64_t i = a; i < e; i++) {
             const mt_op &o = ops[i];
             if (MT_OP_IS_INSERT_LIKE(o.type) && !(MT_OPF_BITS(o.flags) & MT_OPF_MARKER)) {
@@ -1007,14 +1015,23 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
                     if (props[o.payload + o.payload_len + x].key != MT_KEY_COMBINE) return MT_ERR_ARG;
                 nprop_ops++;
                 prop_records += o.payload_len;
+                precs += o.payload_len;
             }
             if (o.type == MT_OP_REGENERATE && o.ref_seq == MT_OP_ANNOTATE &&
                 (int64_t)o.payload + (int64_t)o.payload_len > n_props)
                 return MT_ERR_ARG;
             if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
-                if (o.pos2 < 0 || (int64_t)o.pos2 + (int64_t)MT_OPF_NPROPS(o.flags) > n_props) return MT_ERR_ARG;
+                if (o.pos2 < 0 || o.pos2 >= n_props + (MT_OPF_NPROPS(o.flags) == MT_OPF_NPROPS_EXT ? 0 : 1))
+                    return MT_ERR_ARG;
+                uint32_t p0 = 0;
+                const uint32_t np = mt_insert_props(&o, props, &p0);
+                if ((int64_t)p0 + (int64_t)np > n_props) return MT_ERR_ARG;
+                if (MT_OPF_NPROPS(o.flags) == MT_OPF_NPROPS_EXT &&
+                    (props[o.pos2].key != MT_KEY_NPROPS || np <= MT_OPF_NPROPS_INLINE))
+                    return MT_ERR_ARG;
                 nprop_ops++;
-                prop_records += MT_OPF_NPROPS(o.flags);
+                prop_records += np;
+                precs += np;
             }
         }
         payload_units += (double)pay;
@@ -1024,7 +1041,25 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
         text_len[d] = (uint32_t)pay;
         text_cap[d] = (uint32_t)cap;
         tbase += align16u(cap);
-        uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * nprop_ops;
+        // prop sets of any size: besides the per-op allowance, room for the sets an op's records
+        // can make (a few live copies of the largest ones between collections)
+        uint64_t kd = 0;  // distinct keys of the document's prop records (sets of up to kd keys)
+        if (precs > 64) {
+            std::unordered_set<uint32_t> ks;
+            for (int64_t i = a; i < e; i++) {
+                const mt_op &o = ops[i];
+                uint32_t p0 = 0, np = 0;
+                if (o.type == MT_OP_ANNOTATE) {
+                    p0 = o.payload;
+                    np = o.payload_len;
+                } else if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
+                    np = mt_insert_props(&o, props, &p0);
+                }
+                for (uint32_t q = 0; q < np; q++) ks.insert(props[p0 + q].key);
+            }
+            kd = ks.size();
+        }
+        uint64_t pc = 1024 + (uint64_t)b->opt.pool_per_op * nprop_ops + (kd > 32 ? 8 * kd * kd + 8 * precs : 0);
         pool_base[d] = pbase;
         pool_cap[d] = (uint32_t)std::min<uint64_t>(pc, 0xFFFFFFF0ull);
         pbase += align16u(pc);
@@ -1594,7 +1629,10 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     HIPCHK(lbuf_alloc(b, &L.d_prof, (size_t)n * mt::kProfSlots));
     P.prof = L.d_prof;
 #endif
-    const void *fn = L.load ? kKernels[L.cls].load : b->writer ? kKernels[L.cls].writer : kKernels[L.cls].replay;
+    const void *fn = L.load     ? kKernels[L.cls].load
+                     : b->writer ? kKernels[L.cls].writer
+                     : L.big && !mt::is_hbm_seg(mt::kClassSegs[L.cls]) ? kKernels[L.cls].bigprops
+                                 : kKernels[L.cls].replay;
     if (getenv("MT_DEBUG_LAUNCHES"))
         fprintf(stderr, "mtreplay: launch class %d docs %lld resumed %d level %d lds %zu load %d\n", mt::kClassSegs[L.cls],
                 (long long)n, (int)L.cksrc.size(), L.level, L.lds, (int)L.load);
@@ -1944,8 +1982,9 @@ MT_API int mt_batch_sync(mt_batch *b) {
         // launch_on appends to b->launches, so S dangles after the first one: what the escalations
         // need of it is copied here
         const int prefer = S.stream;
+        const bool s_big = S.big;
         const int64_t n = launch_n(b->n_docs, S);
-        std::map<int, Launch> groups;
+        std::map<int, Launch> groups;  // by target class, x2 + 1 for the bigprops kernel
         int64_t n_ck = 0;
         for (int64_t i = 0; i < n; i++) {
             const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
@@ -1957,9 +1996,13 @@ MT_API int mt_batch_sync(mt_batch *b) {
             if (o.status != MT_CAPACITY || b->where[d].launch != li) continue;
             int32_t src;
             if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) src = (int32_t)i;
-            else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg) src = -1;
+            else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg || o.cap_kind == mt::kCapBigProps)
+                src = -1;
             else continue;
-            int cls = resume_class(S.cls);
+            // a large property set: the same class again, from scratch, in the bigprops kernel
+            const bool big = s_big || o.cap_kind == mt::kCapBigProps;
+            if (o.cap_kind == mt::kCapBigProps && s_big) continue;  // (the bigprops kernel never stops so)
+            int cls = o.cap_kind == mt::kCapBigProps ? S.cls : resume_class(S.cls);
             // a tail document checkpointed for overlay-list room (a wide collab window; the list grows
             // only by seg/16 per class) steps to the first class with ~64 entries to spare instead of one
             // class at a time, each step a serial launch of its own.  Only in a tail (a launch too small
@@ -1973,8 +2016,9 @@ MT_API int mt_batch_sync(mt_batch *b) {
             // a segment beyond 16-bit lengths: re-run from scratch in the giant class (32-bit lengths)
             if (o.cap_kind == mt::kCapLongSeg) cls = long_seg_class(S.cls);
             if (!class_usable(cls)) continue;  // largest class reached: the document keeps MT_CAPACITY
-            Launch &L = groups[cls];
+            Launch &L = groups[2 * cls + (big ? 1 : 0)];
             L.cls = cls;
+            L.big = big;
             L.src = li;
             L.level = S.level + 1;
             L.docs.push_back((int32_t)d);
@@ -2011,6 +2055,7 @@ MT_API int mt_batch_sync(mt_batch *b) {
             for (size_t at = 0; at < G.docs.size(); at += chunk) {
                 Launch L;
                 L.cls = G.cls;
+                L.big = G.big;
                 L.src = G.src;
                 L.level = G.level;
                 const size_t e = std::min(G.docs.size(), at + chunk);
@@ -3544,8 +3589,11 @@ static int64_t props_end(mt_batch *b, int64_t d0, int64_t d1, const mt_op *ops) 
     for (int64_t i = b->h_off[d0]; i < b->h_off[d1]; i++) {
         const mt_op &o = ops[i - base];
         if (o.type == MT_OP_ANNOTATE) end = std::max<int64_t>(end, (int64_t)o.payload + o.payload_len);
-        if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS))
+        if (MT_OP_IS_INSERT_LIKE(o.type) && (MT_OPF_BITS(o.flags) & MT_OPF_HAS_PROPS)) {
+            // an extended insert's count is in its first record (device memory): take everything
+            if (MT_OPF_NPROPS(o.flags) == MT_OPF_NPROPS_EXT) return b->total_props;
             end = std::max<int64_t>(end, (int64_t)o.pos2 + MT_OPF_NPROPS(o.flags));
+        }
     }
     return std::min(end, b->total_props);
 }

@@ -548,8 +548,9 @@ struct Packer1 {
         if (nonempty) {
             uint32_t off = 0, n = 0;
             if (!prop_records(props, &off, &n)) return false;
-            if (n > MT_OPF_MAX_INSERT_PROPS) return fail(MT_UNSUPPORTED, "too many insert props");
-            r.flags |= (uint16_t)(MT_OPF_HAS_PROPS | (n << 4));
+            if (n > MT_OPF_NPROPS_INLINE)  // any number of props: the count leads the records
+                L.props.insert(L.props.begin() + off, mt_prop{MT_KEY_NPROPS, n});
+            r.flags |= (uint16_t)(MT_OPF_HAS_PROPS | (MT_OPF_MAKE(0u, n) & 0x7F0u));
             r.pos2 = (int32_t)off;
         } else if (obj) {  // {}: an empty map is created
             r.flags |= MT_OPF_HAS_PROPS;
@@ -1113,9 +1114,14 @@ MT_API int mt_pack_json(mt_packed **out, int64_t n_docs, const char *const *doc_
             P->ops.push_back(o);
         }
         P->text.insert(P->text.end(), L.text.begin(), L.text.end());
-        for (const mt_prop &q : L.props)  // combiningOp records keep their sentinel key / undefined
+        for (const mt_prop &q : L.props) {  // combiningOp records keep their sentinel key / undefined
+            if (q.key == MT_KEY_NPROPS) {        // an extended insert's count record: not an id
+                P->props.push_back(q);
+                continue;
+            }
             P->props.push_back(mt_prop{q.key == MT_KEY_COMBINE ? q.key : kmap[q.key],
                                        q.value == MT_VALUE_UNDEFINED ? q.value : vmap[q.value]});
+        }
         P->off.push_back((int64_t)P->ops.size());
         std::vector<std::string> names;
         for (const auto &n : L.names) names.push_back(wtf8(n));

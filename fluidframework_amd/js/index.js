@@ -33,7 +33,9 @@ const OPF_GROUP_CONT = 1, OPF_MARKER = 2, OPF_HAS_PROPS = 4, OPF_REWRITE = 8;
 const OP_RELPOS = 6, RELF_POS1 = 0x10, RELF_POS2 = 0x20, RELF_BEFORE1 = 0x40, RELF_BEFORE2 = 0x80, RELF_OFF1 = 0x100, RELF_OFF2 = 0x200;
 const RELF_NOTIFY = 0x2;  // a local RELPOS of Client.annotateMarkerNotifyConsensus (include/mt_oplog.h)
 const COMBINE_INCR = 1, COMBINE_CONSENSUS = 2, COMBINE_OTHER = 3, KEY_COMBINE = 0xFFFFFFFF, VALUE_UNDEFINED = 0xFFFFFFFF;
-const MAX_INSERT_PROPS = 127;  // include/mt_oplog.h MT_OPF_MAX_INSERT_PROPS (flags bits 4-10)
+// an insert's prop count: flags bits 4-10 up to NPROPS_INLINE; beyond, NPROPS_EXT there and a first
+// record {KEY_NPROPS, count} (include/mt_oplog.h MT_OPF_NPROPS_EXT)
+const NPROPS_INLINE = 126, NPROPS_EXT = 127, KEY_NPROPS = 0xFFFFFFFE;
 const MAX_CLIENTS = 0x7FFE;      // short ids 0..32765 (MT_MAX_CLIENTS; 0x7FFE / 0x7FFF are sentinels)
 const STATUS = ['OK', 'INVALID_POS', 'SEQ_ORDER', 'MSN_ORDER', 'UNSUPPORTED', 'BAD_INPUT', 'CAPACITY', 'INTERNAL'];
 
@@ -143,8 +145,11 @@ class Packer {
             }
             if (Array.isArray(props)) throw new UnsupportedOp('array props');
             if (props && Object.keys(props).length) {  // TextSegment.make: `if (props) addProperties`
-                const [off, n] = this.propRecords(props);
-                if (n > MAX_INSERT_PROPS) throw new UnsupportedOp('too many insert props');
+                let [off, n] = this.propRecords(props);
+                if (n > NPROPS_INLINE) {  // any number of props: the count leads the records
+                    this.props.splice(2 * off, 0, KEY_NPROPS, n);
+                    n = NPROPS_EXT;
+                }
                 r.flags |= OPF_HAS_PROPS | (n << 4);
                 r.pos2 = off;
             } else if (props && typeof props === 'object') {  // {} is truthy: an empty map

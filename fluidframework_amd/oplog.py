@@ -45,7 +45,9 @@ UNASSIGNED_SEQ = -1  # UnassignedSequenceNumber (merge-tree/src/constants.ts:11)
 RELF_POS1, RELF_POS2, RELF_BEFORE1, RELF_BEFORE2, RELF_OFF1, RELF_OFF2 = 0x10, 0x20, 0x40, 0x80, 0x100, 0x200
 RELF_NOTIFY = 0x2  # a local RELPOS of Client.annotateMarkerNotifyConsensus (include/mt_oplog.h)
 OPF_GROUP_CONT, OPF_MARKER, OPF_HAS_PROPS, OPF_REWRITE = 1, 2, 4, 8
-MAX_INSERT_PROPS = 127  # include/mt_oplog.h MT_OPF_MAX_INSERT_PROPS (flags bits 4-10)
+# an insert's prop count: flags bits 4-10 up to NPROPS_INLINE; beyond, NPROPS_EXT there and a first
+# record {KEY_NPROPS, count} (include/mt_oplog.h MT_OPF_NPROPS_EXT)
+NPROPS_INLINE, NPROPS_EXT, KEY_NPROPS = 126, 127, 0xFFFFFFFE
 # combiningOp other than "rewrite" (include/mt_oplog.h mt_combine_kind): annotate flags bits 4-5,
 # then three records {KEY_COMBINE, defaultValue}, {KEY_COMBINE, minValue}, {KEY_COMBINE, result slot}
 COMBINE_INCR, COMBINE_CONSENSUS, COMBINE_OTHER = 1, 2, 3
@@ -405,8 +407,9 @@ class Packer:
                 raise UnsupportedOp("array props")
             if props:  # TextSegment.make: `if (props) addProperties(props)`
                 off, n = self._prop_records(props)
-                if n > MAX_INSERT_PROPS:
-                    raise UnsupportedOp("too many insert props")
+                if n > NPROPS_INLINE:  # any number of props: the count leads the records
+                    self._props.insert(off, (KEY_NPROPS, n))
+                    n = NPROPS_EXT
                 r["flags"] |= OPF_HAS_PROPS | (n << 4)
                 r["pos2"] = off
             elif isinstance(props, dict):  # {} is truthy: an empty map is created

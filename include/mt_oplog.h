@@ -94,9 +94,10 @@ enum mt_relpos_flags {
    record of client 0 acks the oldest pending group (client.ts:797-819, mergeTree.ts:1893-1929). */
 #define MT_SEQ_LOCAL (-1)
 
-/* mt_op.flags: bits 0-3 public flags, bits 4-10 the prop count of an insert (<= 127), bits 11-13
-   the short client id's high bits (every record type), bits 14-15 are internal to the library (set at
-   ingest: the insert's text contains a '\n' / its last code unit is '\n') */
+/* mt_op.flags: bits 0-3 public flags, bits 4-10 the prop count of an insert (0..126; 127 =
+   MT_OPF_NPROPS_EXT: the count is in the first prop record), bits 11-13 the short client id's high
+   bits (every record type), bits 14-15 are internal to the library (set at ingest: the insert's
+   text contains a '\n' / its last code unit is '\n') */
 enum mt_op_flags {
     MT_OPF_GROUP_CONT = 1u, /* more members of the same GROUP message follow          */
     MT_OPF_MARKER = 2u,     /* insert of a Marker: payload = refType, payload_len = 1  */
@@ -123,9 +124,19 @@ enum mt_combine_kind {
 #define MT_KEY_COMBINE 0xFFFFFFFFu
 #define MT_VALUE_UNDEFINED 0xFFFFFFFFu
 #define MT_OPF_BITS(f) ((f) & 0xFu)
+/* the raw 7-bit field; use mt_insert_props() to read an insert's prop records */
 #define MT_OPF_NPROPS(f) (((uint32_t)(f) >> 4) & 0x7Fu)
-#define MT_OPF_MAKE(bits, nprops) ((uint16_t)((((nprops) & 0x7Fu) << 4) | ((bits) & 0xFu)))
-#define MT_OPF_MAX_INSERT_PROPS 127u
+/* An insert (or LOAD record) with more than MT_OPF_NPROPS_INLINE props sets the field to
+   MT_OPF_NPROPS_EXT and its prop records start with {MT_KEY_NPROPS, count}: any number of props
+   (the reference's TextSegment.make / Marker.make copy every key, textSegment.ts:23-28,
+   properties.ts:95) */
+#define MT_OPF_NPROPS_INLINE 126u
+#define MT_OPF_NPROPS_EXT 127u
+#define MT_KEY_NPROPS 0xFFFFFFFEu
+#define MT_OPF_MAKE(bits, nprops) \
+    ((uint16_t)((((nprops) > MT_OPF_NPROPS_INLINE ? MT_OPF_NPROPS_EXT : ((nprops) & 0x7Fu)) << 4) | ((bits) & 0xFu)))
+/* prop records an insert of n props occupies (the count record of an extended one included) */
+#define MT_INSERT_PROP_RECORDS(n) ((n) > MT_OPF_NPROPS_INLINE ? (n) + 1u : (n))
 #define MT_OPF_INTERNAL_HAS_NL 0x4000u
 #define MT_OPF_INTERNAL_ENDS_NL 0x8000u
 #define MT_OPF_INTERNAL (MT_OPF_INTERNAL_HAS_NL | MT_OPF_INTERNAL_ENDS_NL)
@@ -156,6 +167,21 @@ typedef struct mt_prop {
 } mt_prop;
 
 #define MT_VALUE_NULL 0u
+
+/* An insert's prop records: *first = index of its first (key, value) record in `props`, returns
+   their count (the 7-bit flags field, or for MT_OPF_NPROPS_EXT the count record at op->pos2) */
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+static inline uint32_t mt_insert_props(const mt_op *op, const mt_prop *props, uint32_t *first) {
+    const uint32_t n = MT_OPF_NPROPS(op->flags);
+    if (n != MT_OPF_NPROPS_EXT) {
+        *first = (uint32_t)op->pos2;
+        return n;
+    }
+    *first = (uint32_t)op->pos2 + 1u;
+    return props[op->pos2].value;
+}
 
 #ifdef __cplusplus
 static_assert(sizeof(mt_op) == 32, "mt_op is 32 bytes");

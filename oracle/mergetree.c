@@ -3364,7 +3364,9 @@ static void apply_local_packed(mto_doc *d, const mt_op *op, const uint16_t *text
             if (bits & MT_OPF_MARKER) s = new_marker(d, (int)op->payload);
             else s = new_text_seg(d, text + op->payload, (int)op->payload_len);
             if (bits & MT_OPF_HAS_PROPS) {
-                jv *pr = props_from_records(d, props + op->pos2, MT_OPF_NPROPS(op->flags), t);
+                uint32_t p0 = 0;
+                const uint32_t np = mt_insert_props(op, props, &p0); /* MT_OPF_NPROPS_EXT: any count */
+                jv *pr = props_from_records(d, props + p0, (int)np, t);
                 seg_add_properties(d, s, pr, 0, NULL, 0, 0);
                 jv_unref(pr);
             }
@@ -3468,7 +3470,9 @@ static void apply_packed_one(mto_doc *d, const mt_op *op, const uint16_t *text, 
             if (bits & MT_OPF_MARKER) s = new_marker(d, (int)op->payload);
             else s = new_text_seg(d, text + op->payload, (int)op->payload_len);
             if (bits & MT_OPF_HAS_PROPS) {
-                jv *pr = props_from_records(d, props + op->pos2, MT_OPF_NPROPS(op->flags), t);
+                uint32_t p0 = 0;
+                const uint32_t np = mt_insert_props(op, props, &p0); /* MT_OPF_NPROPS_EXT: any count */
+                jv *pr = props_from_records(d, props + p0, (int)np, t);
                 seg_add_properties(d, s, pr, 0, NULL, 0, 0);
                 jv_unref(pr);
             }

@@ -37,6 +37,13 @@ for step in "$@"; do
     hbmrate_nocache) run hbmrate_nocache 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_nocache.so python -u tools/hbm_phases.py 100000 8 ;;
     bisect) run bisect 600 python -u tools/gpu_bisect.py ;;
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
+    b3s_notext) run b3s_notext 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_notext.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
+    b3s_var) run b3s_var 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_var.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
+    giantrate) run giantrate 600 python -u tools/hbm_phases.py 100000 8 2000000 ;;
+    giantrate_nopf) run giantrate_nopf 600 env MT_GIANT_PREFETCH=0 python -u tools/hbm_phases.py 100000 8 2000000 ;;
+    l2giant) run l2giant 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/l2giant -o run -- python3 -u tools/hbm_phases.py 100000 8 2000000 ;;
+    l2giant_nopf) run l2giant_nopf 300 env MT_GIANT_PREFETCH=0 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/l2giant_nopf -o run -- python3 -u tools/hbm_phases.py 100000 8 2000000 ;;
+    ptests) run ptests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_snapshot.py -k "any_size or combining or markers or kats or escalation" -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     phases) run phases 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --steps 1 --warmup 0 --no-cpu ;;
     phases3) run phases3 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_prof.so python -u bench.py --config 3 --docs 8192 --steps 1 --warmup 0 --no-cpu ;;

@@ -203,3 +203,60 @@ RELPOS_DOCS = [
      _msg("A", 4, 3, {"type": 0, "pos1": 0, "seg": "zz"}, 4),
      _msg("A", 5, 4, {"type": 0, "relativePos1": {"id": "gone"}, "seg": "!"}, 5)],
 ]
+
+
+def big_prop_docs():
+    """Property sets of any size (properties.ts:95 copies every key; textSegment.ts:23-28): an insert
+    of 500 props, a 130-prop insert (past the 126 a record's flags hold: MT_OPF_NPROPS_EXT), an
+    annotate chain that grows a set past 300 keys over concurrent, splitting annotates of two
+    clients (zamboni then merges neighbours whose big sets match), deletions, a rewrite with 80
+    keys, a 200-prop marker, and combiningOps over a 100-key set.  Every message is valid for its
+    view (positions within the refSeq view's length)."""
+    docs = []
+    big = {f"k{i}": i for i in range(500)}
+    d0 = [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "abcdef", "props": big}}),
+          _msg("B", 2, 1, {"type": 2, "pos1": 1, "pos2": 4, "props": {f"b{i}": "x" for i in range(20)}}),
+          _msg("A", 3, 2, {"type": 1, "pos1": 2, "pos2": 3}, msn=1),
+          _msg("B", 4, 3, {"type": 0, "pos1": 0, "seg": {"text": "XYZ", "props": {f"z{i}": True for i in range(130)}}}, msn=2),
+          _msg("A", 5, 4, {"type": 2, "pos1": 0, "pos2": 8, "props": {"k7": None, "k8": None, "q": 1}}, msn=3),
+          _msg("B", 6, 5, {"type": 0, "pos1": 8, "seg": "tail"}, msn=5),
+          _msg("A", 7, 6, {"type": 2, "pos1": 0, "pos2": 12, "props": {"last": [1, 2]}}, msn=6)]
+    docs.append(d0)
+    rnd = random.Random(11)
+    d1 = [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "0123456789", "props": {f"s{i}": i for i in range(40)}}})]
+    seq, length = 1, 10
+    for i in range(320):
+        seq += 1
+        c = "A" if i % 2 else "B"
+        msn = max(0, seq - 3)
+        if i == 150:
+            props = {f"s{j}": j for j in range(0, 80)}
+            d1.append(_msg(c, seq, seq - 1, {"type": 2, "pos1": 0, "pos2": length, "props": props,
+                                               "combiningOp": {"name": "rewrite"}}, msn=msn))
+            continue
+        if i == 200:
+            d1.append(_msg(c, seq, seq - 1, {"type": 0, "pos1": 5, "seg": {"marker": {"refType": 1},
+                                                                          "props": {f"mk{j}": j for j in range(200)}}}, msn=msn))
+            length += 1
+            continue
+        if i % 40 == 7:
+            d1.append(_msg(c, seq, seq - 1, {"type": 0, "pos1": rnd.randrange(length + 1), "seg": "ab"}, msn=msn))
+            length += 2
+            continue
+        a = rnd.randrange(0, 3)
+        b = length - rnd.randrange(0, 3)
+        props = {f"m{i}": i % 5}
+        if i % 7 == 0 and i >= 5:
+            props[f"m{i - 5}"] = None
+        if i % 11 == 0:
+            props.update({f"w{i}_{j}": "v" for j in range(70)})  # one op past 64 keys
+        d1.append(_msg(c, seq, seq - 2 if seq > 2 else 0, {"type": 2, "pos1": a, "pos2": b, "props": props}, msn=msn))
+    docs.append(d1)
+    d2 = [_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "numbers", "props": {f"n{i}": i for i in range(100)}}}),
+          _msg("B", 2, 1, {"type": 2, "pos1": 0, "pos2": 4, "props": {"n1": 5, "n2": 5, "fresh": 5},
+                           "combiningOp": {"name": "incr", "defaultValue": 1}}),
+          _msg("A", 3, 2, {"type": 2, "pos1": 2, "pos2": 7, "props": {"n3": 9, "other": 2},
+                           "combiningOp": {"name": "keep", "defaultValue": 7}}, msn=1),
+          _msg("B", 4, 3, {"type": 0, "pos1": 7, "seg": "!"}, msn=3)]
+    docs.append(d2)
+    return docs

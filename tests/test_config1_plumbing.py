@@ -121,6 +121,27 @@ def test_node_packer_combining_ops_byte_identical(tmp_path):
 
 
 @pytest.mark.skipif(NODE is None, reason="node not available")
+def test_node_packer_large_prop_sets_byte_identical(tmp_path):
+    """Inserts past 126 props (the extended count record, include/mt_oplog.h MT_OPF_NPROPS_EXT) and
+    annotates past 64 keys: the Node packer == the Python packer."""
+    from combine_logs import big_prop_docs
+
+    docs = big_prop_docs()
+    src = tmp_path / "msgs.json"
+    src.write_text(json.dumps(docs))
+    code = ("const {Packer}=require('./fluidframework_amd/js');const fs=require('fs');"
+            f"const docs=JSON.parse(fs.readFileSync({json.dumps(str(src))},'utf8'));const p=new Packer();"
+            "for(const d of docs)p.addDocument(d);const r=p.finish();"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'ops.bin'))},r.ops);"
+            f"fs.writeFileSync({json.dumps(str(tmp_path / 'props.bin'))},Buffer.from(r.props.buffer));")
+    r = subprocess.run([NODE, "-e", code], capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    pb = oplog.pack_documents(docs)
+    assert np.frombuffer((tmp_path / "ops.bin").read_bytes(), oplog.OP_DTYPE).tobytes() == pb.ops.tobytes()
+    assert np.frombuffer((tmp_path / "props.bin").read_bytes(), oplog.PROP_DTYPE).tobytes() == pb.props.tobytes()
+
+
+@pytest.mark.skipif(NODE is None, reason="node not available")
 def test_node_packer_writer_streams_byte_identical(tmp_path):
     """Writer replicas' streams (local ops, acks): the Node packer == the Python packer."""
     from writer_sim import farm as writer_farm

@@ -723,28 +723,42 @@ def test_relative_positions_outside_the_device_path_are_flagged():
         assert [b.doc(i).status for i in range(len(docs))] == [fa.MT_UNSUPPORTED] * len(docs)
 
 
-def test_prop_sets_beyond_64_keys_stop_with_capacity():
-    """A segment's property set holds at most 64 keys on the GPU (one key per lane, props_extend):
-    an insert with 100 props and an annotate that grows a set past 64 keys stop their document with
-    MT_CAPACITY (cap_kind 3, the prop pool) — never a silently different result — while a
-    64-key set next to them replays to the oracle's digest."""
-    def msg(s, contents):
-        return {"clientId": "A", "sequenceNumber": s, "referenceSequenceNumber": s - 1,
-                "minimumSequenceNumber": 0, "type": "op", "contents": contents}
+@pytest.mark.parametrize("path", ["packer", "json_host", "json_auto", "escalating"])
+def test_prop_sets_of_any_size(path):
+    """Property sets of any size (properties.ts:95, textSegment.ts:23-28): inserts of 500 and 130
+    props (the extended count record, include/mt_oplog.h MT_OPF_NPROPS_EXT), an annotate chain that
+    grows sets past 300 keys with concurrent splitting annotates of two clients (zamboni merges
+    neighbours whose large sets match), deletions, a rewrite with 80 keys, a 200-prop marker, and
+    combiningOps over a 100-key set.  Sets past one pair per lane are built in the pool
+    (mt_engine.hip props_extend_big).  Ingested by the Python packer, the host JSON parser, and the
+    automatic GPU / host choice (the GPU parser's fast path takes objects of up to 16 keys, so these
+    documents go to the host parser); "escalating" starts them in the smallest class, so they
+    re-run in the bigprops kernel (cap_kind 11) and escalate through checkpoints with their large
+    sets.  GPU == oracle on digest, text, props runs and SnapshotV1 (GPU and host serializers)."""
+    from combine_logs import big_prop_docs
 
-    ins = lambda n: msg(1, {"type": 0, "pos1": 0, "seg": {"text": "abc", "props": {f"k{i}": i for i in range(n)}}})
-    docs = [[ins(100)],
-            [ins(40), msg(2, {"type": 2, "pos1": 0, "pos2": 2, "props": {f"m{i}": i for i in range(30)}})],
-            [ins(64), msg(2, {"type": 1, "pos1": 1, "pos2": 2})]]
-    with fa.ReplayBatch(len(docs)) as b:
-        b.ingest_json([json.dumps(d) for d in docs], device="host")
+    docs = big_prop_docs()
+    opts = {"seg_cap": 64, "max_retries": 24} if path == "escalating" else {}
+    with fa.ReplayBatch(len(docs), **opts) as b:
+        if path in ("packer", "escalating"):
+            b.ingest_messages(docs)
+        else:
+            info = b.ingest_json([json.dumps(d) for d in docs], device="host" if path == "json_host" else "auto")
+            assert info["path"] == "host"
         b.run()
-        c = b.counters()
-        for d in (0, 1):
-            assert fa.status_string(b.doc(d).status) == fa.status_string(6) and int(c["cap_kind"][d]) == 3, d
-        assert b.doc(2).status == 0
-        ref = O.Doc()
-        ref.start_collab("readonly")
-        for m in docs[2]:
-            assert ref.apply_msg(json.dumps(m)) == 0, ref.error
-        assert b.doc(2).digest() == ref.digest()
+        b.snapshots()
+        for i, msgs in enumerate(docs):
+            ref = O.Doc()
+            ref.start_collab("readonly")
+            for m in msgs:
+                assert ref.apply_msg(json.dumps(m)) == 0, ref.error
+            dv = b.doc(i)
+            assert dv.status == 0, (i, fa.status_string(dv.status), int(b.counters()["cap_kind"][i]))
+            assert dv.digest() == ref.digest(), i
+            assert dv.get_text() == ref.text(), i
+            assert dv.props_runs() == json.loads(ref.props_runs()), i
+            assert dv.snapshot_v1() == ref.snapshot_v1(), i
+            assert dv.snapshot_v1(device=True) == ref.snapshot_v1(), i
+        # the largest set the replay built
+        assert max(len(json.loads(x[2])) for i in range(len(docs)) for x in b.doc(i).props_runs()
+                   if isinstance(x[2], str)) > 300

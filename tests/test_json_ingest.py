@@ -216,3 +216,26 @@ def test_records_to_json_round_trips_generated_logs():
             assert od.apply_msg(json.dumps(m)) == 0, od.error
         assert od.text() == ref.text() and od.props_runs() == ref.props_runs()
     _assert_same([json.loads(js) for js in texts])
+
+
+def test_large_prop_sets_pack_identically():
+    """Inserts of any number of props (past 126: the count leads the records, include/mt_oplog.h
+    MT_OPF_NPROPS_EXT) and annotates of more than 64 keys: mt_pack_json == the Python packer, and
+    the oracle's packed path replays them like its JSON path (properties.ts:95, textSegment.ts:23-28)."""
+    from combine_logs import big_prop_docs
+
+    docs = big_prop_docs()
+    _assert_same(docs, n_threads=2)
+    pb = oplog.pack_documents(docs)
+    ext = [(int(o["flags"]) >> 4) & 0x7F for o in pb.ops if (int(o["tc"]) & 0xF) == 0 and int(o["flags"]) & 4]
+    assert oplog.NPROPS_EXT in ext  # the 500- and 130-prop inserts use the extended count
+    t = O.Tables(pb.keys, pb.values)
+    for i, msgs in enumerate(docs):
+        ref = O.Doc()
+        ref.start_collab("readonly")
+        for m in msgs:
+            assert ref.apply_msg(json.dumps(m)) == 0, ref.error
+        a, e = pb.doc_op_off[i], pb.doc_op_off[i + 1]
+        got = O.replay_doc(pb.ops[a:e].copy(), pb.text, pb.props, t, pb.clients[i])
+        assert got.status == 0, got.error
+        assert got.digest() == ref.digest() and got.props_runs() == ref.props_runs()

@@ -16,8 +16,9 @@ rel = g.PKG / "build" / "release"
 out = g.PKG / "build" / f"q_{name}"
 out.mkdir(parents=True, exist_ok=True)
 base = [g._hipcc(), "-x", "hip", "-O3", "-std=c++17", f"--offload-arch={g.ARCH}", "-fPIC", "-fvisibility=hidden", *flags]
-procs = [subprocess.Popen(base + ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-c", f"-DMT_SEG={seg}", "-o", str(out / f"k{seg}.o"),
-                                  str(g.PKG / "csrc" / "mt_kernels.hip")], cwd=ROOT) for seg in classes]
+procs = [subprocess.Popen(base + ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-c", f"-DMT_SEG={seg}", "-DMT_PART=1",
+                                  "-o", str(out / f"k{seg}_1.o"), str(g.PKG / "csrc" / "mt_kernels.hip")], cwd=ROOT)
+         for seg in classes]
 host_flags = [f for f in flags if f == "-DMT_PROF"]
 if host_flags:  # the host object sees the same switches (MT_PROF: its report)
     procs.append(subprocess.Popen(base + ["-c", '-DMT_BUILD_ID="MTBUILDID:variant000000000"', "-o", str(out / "host.o"),
@@ -26,8 +27,9 @@ for p in procs:
     if p.wait() != 0:
         sys.exit(1)
 objs = []
-for seg in g.CLASSES:
-    objs.append(str(out / f"k{seg}.o") if seg in classes else str(rel / f"k{seg}.o"))
+for seg in g.CLASSES:  # (the observer replay objects of `classes` rebuilt; the rest from the release build)
+    objs.append(str(out / f"k{seg}_1.o") if seg in classes else str(rel / f"k{seg}_1.o"))
+    objs.append(str(rel / f"k{seg}_2.o"))
 for o in ("host", "digest", "snapshot", "json", "json_gpu", "values"):
     objs.append(str(out / f"{o}.o") if (out / f"{o}.o").exists() and o == "host" and host_flags else str(rel / f"{o}.o"))
 lib = g.PKG / f"libmtreplay_{name}.so"
