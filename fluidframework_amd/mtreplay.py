@@ -28,7 +28,7 @@ import numpy as np
 from .oplog import OP_DTYPE, PROP_DTYPE, PackedBatch, Packer
 
 LIB_PATH = Path(os.environ.get("FLUIDFRAMEWORK_AMD_LIB") or Path(__file__).resolve().parent / "libmtreplay.so")
-ABI_VERSION = 7  # include/mtreplay.h MT_ABI_VERSION
+ABI_VERSION = 8  # include/mtreplay.h MT_ABI_VERSION
 
 MT_OK, MT_INVALID_POS, MT_SEQ_ORDER, MT_MSN_ORDER, MT_UNSUPPORTED, MT_BAD_INPUT, MT_CAPACITY, MT_INTERNAL = range(8)
 MT_ERR_HIP, MT_ERR_ARG, MT_ERR_STATE, MT_ERR_NO_DEVICE = 100, 101, 102, 103
@@ -153,7 +153,7 @@ def lib():
                                "rebuild with __graft_entry__.build()")
     L.mt_abi_version.argtypes = []
     L.mt_abi_version.restype = C.c_int32
-    if L.mt_abi_version() != ABI_VERSION:  # struct layouts below are those of include/mtreplay.h v7
+    if L.mt_abi_version() != ABI_VERSION:  # struct layouts below are those of include/mtreplay.h v8
         raise RuntimeError(f"{LIB_PATH}: C ABI version {L.mt_abi_version()}, this binding speaks {ABI_VERSION}")
     L.mt_status_string.argtypes = [C.c_int]
     L.mt_status_string.restype = cp

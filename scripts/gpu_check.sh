@@ -17,6 +17,7 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 300 python -u __graft_entry__.py smoke ;;
     bench) run bench 900 python -u bench.py --steps 3 --warmup 1 ;;
+    benchfinal) run benchfinal 600 python -u bench.py --steps 20 --warmup 5 ;;
     bench2) run bench2 600 python -u bench.py --config 2 --steps 3 --warmup 1 ;;
     bench3) run bench3 900 python -u bench.py --config 3 --docs 2048 --steps 2 --warmup 1 ;;
     gianttests) run gianttests 600 python -u -m pytest tests/test_gpu_parity.py -k "giant or 16_bit or wide_collab or hbm_class or escalation" -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;

@@ -533,6 +533,46 @@ def test_segments_beyond_16_bit_lengths_move_to_the_giant_class():
         assert len(json.loads(b.doc(1).snapshot_v1()["header"])["segments"]) == 1  # merged past 65,535
 
 
+def test_one_launch_escalating_into_several_classes():
+    """One first launch whose documents escalate into different classes at once — checkpoints into
+    the next LDS class, a long segment into the giant class, a large property set into the bigprops
+    kernel — so the host submits several launches while scheduling that launch's escalations
+    (mt_host.cpp mt_batch_sync: every target group gets its own launch); all equal the oracle."""
+    from combine_logs import big_prop_docs
+
+    p = O.gen_params(900, pct_insert=55, pct_remove=35, seed=0xE5C)
+    docs = [[_msg("A", 1, 0, {"type": 0, "pos1": 0, "seg": "x" * 70000})],
+            big_prop_docs()[0]]
+    # generated logs as messages (growing documents that checkpoint out of the small first class)
+    keys = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
+    vals = [json.loads(O.lib().mto_gen_value_json(v).decode()) for v in range(22)]
+    names = O.gen_client_names(p.n_clients)
+    for d in range(6):
+        o_ops, o_text, o_props = O.gen_doc(p, d)
+        msgs = []
+        for o in o_ops:
+            t = int(o["tc"]) & 0xF
+            c = {"type": t, "pos1": int(o["pos1"])}
+            if t == 0:
+                c["seg"] = "".join(chr(x) for x in o_text[int(o["payload"]):int(o["payload"]) + int(o["payload_len"])])
+            else:
+                c["pos2"] = int(o["pos2"])
+            if t == 2:
+                c["props"] = {keys[int(q["key"])]: vals[int(q["value"])]
+                              for q in o_props[int(o["payload"]):int(o["payload"]) + int(o["payload_len"])]}
+            msgs.append(_msg(names[int(o["tc"]) >> 4], int(o["seq"]), int(o["ref_seq"]), c, int(o["msn"])))
+        docs.append(msgs)
+    oracle = oracle_docs_from_messages(docs)
+    with fa.ReplayBatch(len(docs), seg_cap=128, max_retries=24) as b:
+        b.ingest_messages(docs)
+        b.run()
+        launches = b.launches()
+        classes = [li["seg_class"] for li in launches]
+        assert GIANT in classes and len(set(classes)) >= 3, launches
+        for i in range(len(docs)):
+            assert_doc_parity(b.doc(i), oracle[i])
+
+
 def test_giant_document_beyond_65k_segments():
     """A document far beyond the LDS classes and 16-bit ids (>= 100k live segments; SURVEY §8d
     config 4's tail) escalates through the ladder into the giant class (2M slots, 32-bit slot and
