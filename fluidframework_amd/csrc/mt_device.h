@@ -212,10 +212,12 @@ constexpr int kPendDesc = 8;
 constexpr int kPendEntries = kPendDesc + 4 * kPendMaxGroups;
 constexpr int kCapPending = 9;  // DocOut.cap_kind: the pending-entry region is full (terminal)
 constexpr int kCapRegen = 10;   // DocOut.cap_kind: the regenerated-op output region is full (terminal)
-// DocOut.cap_kind: a property set or op past one pair per lane in an observer replay kernel of an LDS
-// class; the host re-runs the document from scratch in the class's mt_bigprops_kernel_<SEG>
-// (mt_engine.hip props_extend_big), and its later escalations stay in the bigprops kernels
-constexpr int kCapBigProps = 11;
+// DocOut.cap_kind 3 (the prop pool) from an observer replay kernel of an LDS class: a property set or
+// op past one pair per lane there, or a full pool.  The host re-runs the document from scratch in the
+// class's mt_bigprops_kernel_<SEG> (mt_engine.hip props_extend_big), and its later escalations stay in
+// the bigprops kernels; a full pool stops it there again (terminal).  (A kind of its own measured
+// worse: the distinct constant alone moved class 756's SGPR spills from 182 to 260.)
+constexpr int kCapPool = 3;
 constexpr int64_t pend_words(int32_t cap) { return kPendEntries + 2ll * cap; }
 // regenerated ops of MT_OP_REGENERATE records, per document (u32 words): [0] words used (from 2),
 // [1] records; per record {GROUP_CONT flag, ops} then per op {type, pos1, pos2, a, b, c, nprops, 0}

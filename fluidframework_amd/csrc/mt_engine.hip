@@ -207,7 +207,7 @@ struct BArr<T, kShift, true> {
 // so the observer kernels carry none of it
 // kBig: property sets past one pair per lane (props_extend_big) — compiled into the writer, load
 // and mt_bigprops_kernel_<SEG> kernels and the spill classes; the observer replay kernels of the LDS
-// classes stop such a document with cap_kind kCapBigProps and the host re-runs it in the bigprops
+// classes stop such a document with cap_kind 3 (kCapPool) and the host re-runs it in the bigprops
 // kernel, so their op loop carries none of it (its registers are the replay's bound)
 template <int SEG, bool kW = false, bool kBigK = false>
 struct Engine {
@@ -2242,7 +2242,7 @@ struct Engine {
         if constexpr (kBig) {
             if (n + nop > 64u) return props_extend_big(old, op, nop, rewrite, hout, ckind, pk, npk, inplace);
         } else if (n > 64u || nop > 64u) {
-            cap_fail(kCapBigProps);  // the bigprops kernel re-runs the document
+            cap_fail(kCapPool);  // the bigprops kernel re-runs the document
             return 0;
         }
 #endif
@@ -2321,7 +2321,7 @@ struct Engine {
                 wsync();
             } else {
                 if (n >= 64u) {
-                    cap_fail(kCapBigProps);
+                    cap_fail(kCapPool);
                     return 0;
                 }
                 if (lane == 0) {
@@ -2808,15 +2808,19 @@ struct Engine {
             if (slot < 0) return;
             uint32_t props = 0, ph = 0;
             if (op.flags & MT_OPF_HAS_PROPS) {
-                uint32_t p0 = 0;
-                const uint32_t np = mt_insert_props(&op, props_in, &p0);
-                if (!kBig && np > 64u) {
-                    cap_fail(kCapBigProps);
-                    return;
+                if constexpr (kBig) {
+                    uint32_t p0 = 0;
+                    const uint32_t np = mt_insert_props(&op, props_in, &p0);
+                    pool_reserve(2u + 2u * np);
+                    if (status) return;
+                    props = props_extend(0, props_in + p0, np, false, ph);
+                } else {
+                    // (an extended count, MT_OPF_NPROPS_EXT = 127 > 64, stops in props_extend with
+                    // kCapPool before any record is read: the bigprops kernel re-runs the document)
+                    pool_reserve(2u + 2u * MT_OPF_NPROPS(op.flags));
+                    if (status) return;
+                    props = props_extend(0, props_in + op.pos2, MT_OPF_NPROPS(op.flags), false, ph);
                 }
-                pool_reserve(2u + 2u * np);
-                if (status) return;
-                props = props_extend(0, props_in + p0, np, false, ph);
                 if (status) return;
             }
             const int32_t rseq = loaded ? op.ref_seq : kNoneSeq;
@@ -2880,8 +2884,8 @@ struct Engine {
         if (op.flags & MT_OPF_HAS_PROPS) {
             uint32_t p0 = 0;
             const uint32_t np = mt_insert_props(&op, props_in, &p0);
-            if (!kBig && np > 64u) {
-                cap_fail(kCapBigProps);
+            if (!kBig && np > 64u) {  // (LOAD records: the load kernel is kBig)
+                cap_fail(kCapPool);
                 return;
             }
             pool_reserve(2u + 2u * np);

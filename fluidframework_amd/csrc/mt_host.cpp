@@ -78,7 +78,7 @@ struct KernelClass {
     const void *generate;
     const void *load;
     const void *writer;    // replay + the local-client path (writer replicas)
-    const void *bigprops;  // the observer replay with property sets of any size (mt_device.h kCapBigProps)
+    const void *bigprops;  // the observer replay with property sets of any size (mt_device.h kCapPool)
 };
 #define MT_KERNEL_CLASS_(S) {S, (const void *)mt_replay_kernel_##S, (const void *)mt_generate_kernel_##S, \
                              (const void *)mt_load_kernel_##S, (const void *)mt_writer_kernel_##S,    \
@@ -1996,13 +1996,17 @@ MT_API int mt_batch_sync(mt_batch *b) {
             if (o.status != MT_CAPACITY || b->where[d].launch != li) continue;
             int32_t src;
             if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) src = (int32_t)i;
-            else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg || o.cap_kind == mt::kCapBigProps)
+            else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg ||
+                     (o.cap_kind == mt::kCapPool && !s_big))
                 src = -1;
             else continue;
             // a large property set: the same class again, from scratch, in the bigprops kernel
-            const bool big = s_big || o.cap_kind == mt::kCapBigProps;
-            if (o.cap_kind == mt::kCapBigProps && s_big) continue;  // (the bigprops kernel never stops so)
-            int cls = o.cap_kind == mt::kCapBigProps ? S.cls : resume_class(S.cls);
+            // (the observer kernels of the LDS classes stop on large sets with kCapPool; the writer,
+            // load and spill-class kernels hold them, so there it is a full pool: terminal)
+            const bool to_big = o.cap_kind == mt::kCapPool;
+            if (to_big && (s_big || b->writer || S.load || mt::is_hbm_seg(mt::kClassSegs[S.cls]))) continue;
+            const bool big = s_big || to_big;
+            int cls = to_big ? S.cls : resume_class(S.cls);
             // a tail document checkpointed for overlay-list room (a wide collab window; the list grows
             // only by seg/16 per class) steps to the first class with ~64 entries to spare instead of one
             // class at a time, each step a serial launch of its own.  Only in a tail (a launch too small

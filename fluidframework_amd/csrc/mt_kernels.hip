@@ -46,7 +46,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(k
 }
 
 // the observer replay with property sets of any size (props_extend_big): documents whose sets outgrow
-// one pair per lane re-run here (cap_kind kCapBigProps), so the replay kernels above carry none of it
+// one pair per lane re-run here (cap_kind 3, mt_device.h kCapPool), so the replay kernels above carry none of it
 // (the spill classes' replay kernels hold sets of any size themselves: the host never launches
 // their bigprops kernel, whose body is empty)
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void MT_CAT(mt_bigprops_kernel_, MT_SEG)(mt::ReplayParams P) {

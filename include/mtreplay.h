@@ -62,8 +62,7 @@ extern "C" {
    7: mt_batch_snapshots keeps documents of more than MT_SNAP_MAX_BLOBS blobs on the GPU (their
       meta row's n_blobs exceeds MT_SNAP_MAX_BLOBS; the row holds the first MT_SNAP_MAX_BLOBS).
    8: inserts of any number of props (mt_oplog.h MT_OPF_NPROPS_EXT: a leading {MT_KEY_NPROPS,
-      count} record past 126); mt_launch_info.start_ms (was reserved); cap_kind 11 is internal (a
-      document re-run in the bigprops kernel), never a final status. */
+      count} record past 126); mt_launch_info.start_ms (was reserved). */
 #define MT_ABI_VERSION 8
 
 enum mt_status_code {
