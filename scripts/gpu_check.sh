@@ -40,6 +40,8 @@ for step in "$@"; do
     bisect3) run bisect3 600 python -u tools/gpu_bisect.py --ops 1500 --docs 32 --ins 55 --rem 35 --seed 0xBADC0DE ;;
     b3s_notext) run b3s_notext 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_notext.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     b3s_var) run b3s_var 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_var.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
+    b3full) run b3full 600 python -u bench.py --steps 3 --warmup 1 --no-cpu ;;
+    b3full_var) run b3full_var 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_var.so python -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     b3s_old) run b3s_old 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_old.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     giantrate) run giantrate 600 python -u tools/hbm_phases.py 100000 8 2000000 ;;
     giantrate_nopf) run giantrate_nopf 600 env MT_GIANT_PREFETCH=0 python -u tools/hbm_phases.py 100000 8 2000000 ;;

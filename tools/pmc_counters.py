@@ -3,8 +3,9 @@
 Input: the counter_collection CSVs of separate `rocprofv3 --pmc ...` passes over the same
 `bench.py --config N --steps 1 --warmup 0 --no-cpu` command (scripts/gpu_check.sh pmcA/pmcB/pmcf/
 pmcw<N>), and that command's bench log (its JSON line gives the ops each replay launch applied).
-Counters are summed over the instances (XCD / SE) of one dispatch; a kernel dispatched once per
-pass (one step, no warmup) gives one value per counter.
+Counters are summed over the instances (XCD / SE) of a dispatch and over the dispatches of the
+kernel in the profiled step (one step, no warmup: config 3 launches each class twice, one launch
+per half), and divided by the ops all of those launches applied.
 
 Derived per kernel:
   per_op[c]         counter / ops applied by the launch
@@ -33,7 +34,9 @@ def read_counters(paths):
     per = collections.defaultdict(lambda: collections.defaultdict(list))  # kernel -> counter -> [per dispatch]
     for (k, _, c), v in acc.items():
         per[k][c].append(v)
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
+    # every dispatch of the profiled step (config 3: the two halves' launches of a class) summed,
+    # pairing with the ops all of the class's launches applied (bench line)
+    return {k: {c: sum(v) for c, v in cs.items()} for k, cs in per.items()}
 
 
 def bench_line(path):
@@ -59,7 +62,7 @@ def main():
     opd = line["config"]["ops_per_doc"]  # config 4: {"min", "max", "lpt_loads"} (bench.py's n_ops is the max)
     res = {"config": a.config, "docs": line["config"]["docs_per_gpu"], "ops": opd["max"] if isinstance(opd, dict) else opd,
            "command": "bench.py --config %d --docs %d --steps 1 --warmup 0 --no-cpu" % (a.config, line["config"]["docs_per_gpu"]),
-           "units": "counters per dispatch summed over instances; per_op = / ops applied by the launch",
+           "units": "counters summed over instances and over the step's dispatches of the kernel; per_op = / ops its launches applied",
            "kernels": {}}
     for k, cs in sorted(cnt.items()):
         m = re.match(r"mt_replay_kernel_(\d+)", k)

@@ -2,6 +2,7 @@
 release objects of the others into fluidframework_amd/libmtreplay_<name>.so (loaded through
 FLUIDFRAMEWORK_AMD_LIB, which skips the source-stamp check).
 python tools/quick_variant.py NAME "CLASS,CLASS,..." [-DFLAG ...]"""
+import os
 import shutil
 import subprocess
 import sys
@@ -16,7 +17,11 @@ rel = g.PKG / "build" / "release"
 out = g.PKG / "build" / f"q_{name}"
 out.mkdir(parents=True, exist_ok=True)
 base = [g._hipcc(), "-x", "hip", "-O3", "-std=c++17", f"--offload-arch={g.ARCH}", "-fPIC", "-fvisibility=hidden", *flags]
-procs = [subprocess.Popen(base + ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-c", f"-DMT_SEG={seg}", "-DMT_PART=1",
+# QV_SCHED: the machine scheduler of the rebuilt classes (default max-ilp, as the release build;
+# "default": the compiler's own)
+sched = os.environ.get("QV_SCHED", "max-ilp")
+sflags = [] if sched == "default" else ["-mllvm", f"-amdgpu-sched-strategy={sched}"]
+procs = [subprocess.Popen(base + sflags + ["-c", f"-DMT_SEG={seg}", "-DMT_PART=1",
                                   "-o", str(out / f"k{seg}_1.o"), str(g.PKG / "csrc" / "mt_kernels.hip")], cwd=ROOT)
          for seg in classes]
 host_flags = [f for f in flags if f == "-DMT_PROF"]
