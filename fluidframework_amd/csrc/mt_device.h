@@ -173,6 +173,9 @@ constexpr int kGiantClass = kNumClasses - 2;
 constexpr int kHbmClass = kNumClasses - 1;
 constexpr int kLastLdsClass = kGiantClass - 1;
 constexpr int kReplayStartClass = 1;  // replay starts documents in at most the 16-per-CU class
+// the kernels that append early-escalation notices (ReplayParams.notice): those of the classes a
+// first replay launch runs in
+__host__ __device__ constexpr bool notice_class(int seg) { return seg <= kClassSegs[kReplayStartClass]; }
 constexpr bool is_giant_seg(int seg) { return seg == kGiantSeg; }
 // giant class: block ids [0, kGiantLdsBlocks) are LDS-resident and given to blocks of level >=
 // kGiantLdsLevel (0 = leaf blocks); lower levels (and high ones once the LDS ids run out) take
@@ -425,6 +428,13 @@ struct ReplayParams {
     // the prop set a marker's leaf block last rebuilt its tile / range maps from (blockUpdate,
     // mergeTree.ts:2748-2767; annotates do not run it, so those maps go stale), else null
     uint32_t *lab_out;            // [n_docs * out_cap]
+    // early escalation (a launch whose documents are expected to finish in its class): a document
+    // that stops short of capacity anyway appends {workgroup + 1, launch | cap_kind << 24, ops_done,
+    // max_oe} to this host-visible ring (slot from notice_count, device memory) once everything it
+    // wrote is past its XCD's L2, so the host starts its next class while the launch still runs
+    uint32_t *notice;             // host memory (4 words per entry), or null
+    uint32_t *notice_count;
+    int32_t launch_id;
 };
 constexpr uint32_t kIdUnlinked = 0xFFFFFFFFu;
 constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // RELPOS key the host cannot resolve safely

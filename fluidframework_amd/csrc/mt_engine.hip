@@ -4404,6 +4404,26 @@ MT_FI void giant_prefetch(const ReplayParams &P, int64_t w, int64_t d) {
     }
 }
 
+// Early escalation (ReplayParams.notice, mt_host.cpp mt_batch_sync): a document that ends with
+// MT_CAPACITY tells the host at once.  The agent-scope release makes everything the wave wrote — the
+// checkpoint image, cold records, text arena, prop pool, per-document regions — visible past this
+// XCD's L2 before the ring entry (system scope, host memory) is; the next class's launch, which
+// the host starts after reading the entry, acquires at its dispatch.
+MT_FI void escalation_notice(const ReplayParams &P, int64_t w) {
+    wsync();  // the DocOut row this wave just stored
+    if (threadIdx.x != 0) return;
+    const DocOut o = P.doc_out[w];
+    if (o.status != ST_CAPACITY) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t slot = __hip_atomic_fetch_add(P.notice_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t *e = P.notice + 4ull * slot;
+    __hip_atomic_store(e + 1, (uint32_t)P.launch_id | ((uint32_t)o.cap_kind << 24), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(e + 2, (uint32_t)o.ops_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(e + 3, (uint32_t)o.max_oe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(e, (uint32_t)w + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // one workgroup per document (blockIdx.x); the giant class's observer replay adds the prefetch wave
 template <int SEG, bool kLoad, bool kW = false, bool kBigK = false>
 MT_FI void replay_body(const ReplayParams &P) {
@@ -4422,6 +4442,9 @@ MT_FI void replay_body(const ReplayParams &P) {
     } else {
         replay_one<SEG, kLoad, kW, kBigK>(P, w, d, kSrcList);
     }
+    // (first launches only: the classes replay starts documents in; the larger classes keep their codegen)
+    if constexpr (!kLoad && notice_class(SEG))
+        if (P.notice) escalation_notice(P, w);
 }
 
 // Generator: draws each op from the issuer's view (include/mt_gen.h, DESIGN.md

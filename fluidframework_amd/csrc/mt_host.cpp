@@ -23,6 +23,7 @@
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
+#include <atomic>
 #include <vector>
 
 #include "../../include/mtreplay.h"
@@ -108,9 +109,12 @@ struct Launch {
     int64_t ops = 0;            // ops applied by this launch (resumed documents: after their checkpoint)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int level = 0;              // escalation depth (0: a first launch)
-    int stream = 0;             // 0: the run stream, 1..3: aux stream k - 1
+    int stream = 0;             // 0: the run stream, 1..3: aux stream k - 1, 4..5: early stream k - 4
     bool load = false;          // SnapshotLoader launch (mt_load_kernel): LOAD records, then a checkpoint
     bool big = false;           // observer documents with large property sets: mt_bigprops_kernel_<SEG>
+    bool notice = false;        // appends early-escalation entries (mt_batch.h_notice)
+    bool gathered = false;      // its results are gathered: later entries of it are not taken
+    int64_t early_ops = 0;      // ops of its documents that escalated early (poll_notices)
 };
 
 // workgroups (documents) of a launch
@@ -360,6 +364,7 @@ struct mt_batch {
     std::vector<DocOut> docout;  // gathered per doc
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};  // concurrent first launches of mixed-size batches
+    hipStream_t early_s[2] = {nullptr, nullptr};        // early escalations (Launch.stream 4, 5)
     hipStream_t cstream = nullptr;  // result gathers (never queued behind a running launch)
     hipEvent_t ev_user = nullptr;
     uint64_t *d_digest = nullptr;  // mt_batch_device_digests
@@ -369,6 +374,15 @@ struct mt_batch {
                                   // the SnapshotLoader launches, after them the escalations
     hipStream_t run_stream = nullptr;
     std::chrono::steady_clock::time_point t_launch;
+    // early escalation (poll_notices): a ring of 4-word entries in coherent host memory the first
+    // launches append to (ReplayParams.notice), its device-side counter, the host's read cursor,
+    // the documents taken from their source launch, and early groups waiting for an idle stream
+    uint32_t *h_notice = nullptr;
+    uint32_t *d_notice = nullptr;       // device alias of h_notice
+    uint32_t *d_notice_count = nullptr;
+    int64_t notice_cap = 0, notice_read = 0, notice_alloc = 0;
+    std::vector<uint8_t> taken;
+    std::map<int, std::map<int, Launch>> early_groups;  // by source launch, then target (cls x2 + big)
     // single-document result cache
     int64_t cached_doc = -1;
     uint64_t load_gen = 0;         // bumped whenever load_doc loads a document's results
@@ -592,6 +606,8 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     free_snap(b);
     (void)hipFree(b->d_digest);
     free_log(b);
+    if (b->h_notice) (void)hipHostFree(b->h_notice);
+    (void)hipFree(b->d_notice_count);
     (void)hipFree(b->d_vflags);
     (void)hipFree(b->d_vclass);
     (void)hipFree(b->d_vexc);
@@ -599,6 +615,8 @@ MT_API void mt_batch_destroy(mt_batch *b) {
     if (b->ev0) (void)hipEventDestroy(b->ev0);
     if (b->ev1) (void)hipEventDestroy(b->ev1);
     for (hipStream_t a : b->aux)
+        if (a) (void)hipStreamDestroy(a);
+    for (hipStream_t a : b->early_s)
         if (a) (void)hipStreamDestroy(a);
     if (b->cstream) (void)hipStreamDestroy(b->cstream);
     if (b->ev_user) (void)hipEventDestroy(b->ev_user);
@@ -1618,6 +1636,11 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.cold = L.d_cold;
     P.hbm_state = L.d_state;
     P.ck_out = L.d_ck;
+    if (L.notice) {
+        P.notice = b->d_notice;
+        P.notice_count = b->d_notice_count;
+        P.launch_id = (int32_t)(&L - b->launches.data());
+    }
     if (!L.cksrc.empty() && prev) {
         P.ck_in = prev->d_ck;
         P.ck_src = L.d_cksrc;
@@ -1811,6 +1834,42 @@ MT_API int mt_batch_launch(mt_batch *b, void *hip_stream) {
             b->launches.push_back(std::move(L));
         }
     }
+    // early escalation (poll_notices) for first launches that most of their documents are expected
+    // to fit (>= 90 % by the op-count estimate): the few that outgrow the class start their next
+    // launch while it runs.  Not for batches that climb the ladder (config 3), whose mass escalation
+    // the two first launches schedule.  MT_EARLY_ESCALATION=0: off; 2: every first launch.
+    b->taken.assign((size_t)b->n_docs, 0);
+    b->early_groups.clear();
+    b->notice_cap = b->notice_read = 0;
+    {
+        static const int early = getenv("MT_EARLY_ESCALATION") ? atoi(getenv("MT_EARLY_ESCALATION")) : 1;
+        for (size_t i = (size_t)b->first0; i < b->launches.size() && early > 0 && b->opt.max_retries != 0; i++) {
+            Launch &L = b->launches[i];
+            if (class_in_hbm(L.cls) || !class_usable(L.cls + 1) || !mt::notice_class(mt::kClassSegs[L.cls])) continue;
+            const int64_t n = launch_n(b->n_docs, L);
+            int64_t fit = 0;
+            for (int64_t k = 0; k < n; k++) {
+                const int64_t d = L.docs.empty() ? k : L.docs[(size_t)k];
+                fit += (b->h_off[(size_t)d + 1] - b->h_off[(size_t)d]) / 12 + 64 <= mt::kClassSegs[L.cls];
+            }
+            L.notice = early >= 2 || 10 * fit >= 9 * n;
+            if (L.notice) b->notice_cap += n;
+        }
+        if (b->notice_cap > b->notice_alloc) {
+            if (b->h_notice) (void)hipHostFree(b->h_notice);
+            b->h_notice = nullptr;
+            HIPCHK(hipHostMalloc((void **)&b->h_notice, 16 * (size_t)b->notice_cap, hipHostMallocCoherent | hipHostMallocMapped));
+            HIPCHK(hipHostGetDevicePointer((void **)&b->d_notice, b->h_notice, 0));
+            b->notice_alloc = b->notice_cap;
+        }
+        if (b->notice_cap && !b->d_notice_count) HIPCHK(hipMalloc((void **)&b->d_notice_count, 4));
+        if (b->notice_cap) {
+            // (the previous run's kernels have all finished: free_launches waited for them)
+            memset(b->h_notice, 0, 16 * (size_t)b->notice_cap);
+            HIPCHK(hipMemsetAsync(b->d_notice_count, 0, 4, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+    }
     for (size_t i = (size_t)b->first0; i < b->launches.size(); i++) {
         Launch &L = b->launches[i];
         hipStream_t ls = s;
@@ -1891,15 +1950,17 @@ static int gather_launch(mt_batch *b, int li) {
         b->docout.assign((size_t)b->n_docs, DocOut{});
         b->where.assign((size_t)b->n_docs, DocRes{});
     }
-    L.ops = 0;
+    L.ops = L.early_ops;
     for (int64_t i = 0; i < n; i++) {
         int64_t d = L.docs.empty() ? i : L.docs[i];
+        if (L.notice && b->taken[(size_t)d]) continue;  // escalated early: its results are another launch's
         const bool resumed = !L.cksrc.empty() && L.cksrc[(size_t)i] >= 0;
         L.ops += tmp[i].ops_done - (resumed ? b->docout[d].ops_done : 0);
         b->docout[d] = tmp[i];
         b->where[d].launch = li;
         b->where[d].idx = (int32_t)i;
     }
+    L.gathered = true;
     return MT_OK;
 }
 
@@ -1916,17 +1977,25 @@ static int gather_launch(mt_batch *b, int li) {
 // queues, so its kernel durations no longer matched the bench's)
 static int launch_on(mt_batch *b, Launch &&L, int prefer, std::vector<int> &pending) {
     if (std::all_of(L.cksrc.begin(), L.cksrc.end(), [](int32_t x) { return x < 0; })) L.cksrc.clear();
-    int busy[4] = {0, 0, 0, 0};
+    int busy[6] = {0, 0, 0, 0, 0, 0};
     for (int p : pending) busy[b->launches[(size_t)p].stream]++;
     int k = prefer;
-    for (int j = 0; j < 4; j++)
-        if (busy[j] < busy[k]) k = j;
+    if (k < 4)  // (4, 5: the early-escalation streams, chosen by poll_notices)
+        for (int j = 0; j < 4; j++)
+            if (busy[j] < busy[k]) k = j;
     L.stream = k;
     b->launches.push_back(std::move(L));
     const int li = (int)b->launches.size() - 1;
     Launch &N = b->launches.back();
     hipStream_t s = b->run_stream;
-    if (k > 0) {
+    if (k >= 4) {
+        // early escalations: two streams of their own, so a normal escalation never queues behind one
+        // (a stream of the highest priority measured the same: the dispatcher still fills the CUs the
+        // running launch frees with its own smaller workgroups first)
+        hipStream_t &a = b->early_s[k - 4];
+        if (!a) HIPCHK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+        s = a;
+    } else if (k > 0) {
         hipStream_t &a = b->aux[k - 1];
         if (!a) HIPCHK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
         s = a;
@@ -1944,6 +2013,172 @@ static int launch_on(mt_batch *b, Launch &&L, int prefer, std::vector<int> &pend
 // escalating documents that a launch at class 1400 (~8 wave slots per CU) still runs concurrently
 static constexpr int64_t kTailDocs = 1024;
 
+// The next launch of an escalating document of launch S (workgroup i, results o): its class, kernel
+// and checkpoint source (i: resume; -1: from scratch).  False: nothing to escalate to (the document
+// keeps its status).  n_ck: how many of S's documents checkpointed (a tail below kTailDocs).
+static bool escalation_target(const mt_batch *b, const Launch &S, const DocOut &o, int64_t n_ck, int32_t i, int *cls_out,
+                              bool *big_out, int32_t *src_out) {
+    int32_t src;
+    if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) src = i;
+    else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg || (o.cap_kind == mt::kCapPool && !S.big))
+        src = -1;
+    else return false;
+    // a large property set: the same class again, from scratch, in the bigprops kernel
+    // (the observer kernels of the LDS classes stop on large sets with kCapPool; the writer,
+    // load and spill-class kernels hold them, so there it is a full pool: terminal)
+    const bool to_big = o.cap_kind == mt::kCapPool;
+    if (to_big && (S.big || b->writer || S.load || mt::is_hbm_seg(mt::kClassSegs[S.cls]))) return false;
+    int cls = to_big ? S.cls : resume_class(S.cls);
+    // a tail document checkpointed for overlay-list room (a wide collab window; the list grows
+    // only by seg/16 per class) steps to the first class with ~64 entries to spare instead of one
+    // class at a time, each step a serial launch of its own.  Only in a tail (a launch too small
+    // to fill the chip at the bigger class): with many documents escalating, the smaller class's
+    // residency wins.
+    static const bool ulist_jump = !getenv("MT_ULIST_JUMP") || atoi(getenv("MT_ULIST_JUMP")) > 0;
+    if (ulist_jump && n_ck <= kTailDocs && o.cap_kind == mt::kCapCheckpoint && S.cls < mt::kLastLdsClass &&
+        o.max_oe + 24 > (int32_t)mt::class_caps(mt::kClassSegs[S.cls]).ulist)
+        while (cls < mt::kLastLdsClass && (int32_t)mt::class_caps(mt::kClassSegs[cls]).ulist < o.max_oe + 64) cls++;
+    while (cls > S.cls + 1 && !class_usable(cls)) cls--;
+    // a segment beyond 16-bit lengths: re-run from scratch in the giant class (32-bit lengths)
+    if (o.cap_kind == mt::kCapLongSeg) cls = long_seg_class(S.cls);
+    if (!class_usable(cls)) return false;  // largest class reached: the document keeps MT_CAPACITY
+    *cls_out = cls;
+    *big_out = S.big || to_big;
+    *src_out = src;
+    return true;
+}
+
+// Submit escalation groups (keyed by target class x2 + bigprops): longest remaining replay first
+// (LPT: workgroups dispatch roughly in index order, so the documents with the most ops left start
+// first and the launch's tail is short; MT_LPT=0: the source launch's order), the HBM class in
+// bounded chunks.
+static int submit_groups(mt_batch *b, std::map<int, Launch> &groups, int prefer, std::vector<int> &pending) {
+    static const bool host_timing = getenv("MT_HOST_TIMING") != nullptr;
+    static const bool lpt = !getenv("MT_LPT") || atoi(getenv("MT_LPT")) > 0;
+    for (auto &kv : groups) {
+        Launch &G = kv.second;
+        if (!lpt) continue;
+        std::vector<std::pair<int64_t, size_t>> key(G.docs.size());
+        for (size_t k = 0; k < G.docs.size(); k++) {
+            const int32_t d = G.docs[k];
+            const int64_t n_ops = b->h_off[(size_t)d + 1] - b->h_off[(size_t)d];
+            key[k] = {G.cksrc[k] >= 0 ? n_ops - b->docout[(size_t)d].ops_done : n_ops, k};
+        }
+        std::stable_sort(key.begin(), key.end(), [](const std::pair<int64_t, size_t> &x, const std::pair<int64_t, size_t> &y) {
+            return x.first > y.first;
+        });
+        std::vector<int32_t> docs(G.docs.size()), cks(G.cksrc.size());
+        for (size_t k = 0; k < key.size(); k++) {
+            docs[k] = G.docs[key[k].second];
+            cks[k] = G.cksrc[key[k].second];
+        }
+        G.docs.swap(docs);
+        G.cksrc.swap(cks);
+    }
+    for (auto &kv : groups) {
+        Launch &G = kv.second;
+        // the HBM class holds ~220 MB per document: bounded launches
+        const size_t chunk = launch_chunk(G.cls, G.docs.size());
+        for (size_t at = 0; at < G.docs.size(); at += chunk) {
+            Launch L;
+            L.cls = G.cls;
+            L.big = G.big;
+            L.src = G.src;
+            L.level = G.level;
+            const size_t e = std::min(G.docs.size(), at + chunk);
+            L.docs.assign(G.docs.begin() + (long)at, G.docs.begin() + (long)e);
+            L.cksrc.assign(G.cksrc.begin() + (long)at, G.cksrc.begin() + (long)e);
+            const auto tl0 = std::chrono::steady_clock::now();
+            const int rc = launch_on(b, std::move(L), prefer, pending);
+            if (rc) return rc;
+            if (host_timing)
+                fprintf(stderr, "MT_HOST   launch %d (class %d, %zu docs, stream %d) submitted at %.1f ms host (%.2f ms)\n",
+                        (int)b->launches.size() - 1, mt::kClassSegs[G.cls], e - at, b->launches.back().stream,
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count(),
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl0).count());
+        }
+    }
+    groups.clear();
+    return MT_OK;
+}
+
+// Early escalation (ReplayParams.notice): read the ring entries the running launches appended — a
+// document that stopped with MT_CAPACITY, everything it wrote already visible beyond its XCD — and
+// start their next launches on an idle aux stream while their source launches still run, so a
+// handful of documents outgrowing a class that fits the rest (writer config 2, config 5) no longer
+// replay alone after it.  Entries whose source launch has no idle stream yet wait in early_groups;
+// the source launch's completion submits what is left (flush_src).
+static int poll_notices(mt_batch *b, std::vector<int> &pending, int flush_src) {
+    while (b->notice_read < b->notice_cap) {
+        volatile uint32_t *e = b->h_notice + 4 * b->notice_read;
+        const uint32_t w1 = e[0];
+        if (!w1) break;
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const uint32_t lw = e[1];
+        const int li = (int)(lw & 0xFFFFFFu);
+        DocOut o{};
+        o.status = MT_CAPACITY;
+        o.cap_kind = (int32_t)(lw >> 24);
+        o.ops_done = (int32_t)e[2];
+        o.max_oe = (int32_t)e[3];
+        b->notice_read++;
+        if (li < 0 || li >= (int)b->launches.size()) return MT_INTERNAL;
+        Launch &S = b->launches[(size_t)li];
+        // an entry read after its launch's gather (the ring is read in slot order, and a slot a
+        // running launch reserved but has not written yet holds back the ones after it): the
+        // completion path escalated that document already
+        if (S.gathered) continue;
+        const int32_t i = (int32_t)w1 - 1;
+        if (i < 0 || i >= (int32_t)launch_n(b->n_docs, S)) return MT_INTERNAL;
+        const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
+        int cls = 0;
+        bool big = false;
+        int32_t src = -1;
+        if (S.level >= b->opt.max_retries || !escalation_target(b, S, o, 1, i, &cls, &big, &src)) continue;
+        b->docout[(size_t)d] = o;  // (the fields the escalation reads; the final launch's gather fills the rest)
+        b->where[(size_t)d] = DocRes{li, i};
+        b->taken[(size_t)d] = 1;
+        S.early_ops += o.ops_done;  // (a first launch: no resumed documents)
+        Launch &G = b->early_groups[li][2 * cls + (big ? 1 : 0)];
+        G.cls = cls;
+        G.big = big;
+        G.src = li;
+        G.level = S.level + 1;
+        G.docs.push_back((int32_t)d);
+        G.cksrc.push_back(src);
+    }
+    for (auto it = b->early_groups.begin(); it != b->early_groups.end();) {
+        int idle = -1;
+        if (it->first != flush_src) {
+            int busy[6] = {0, 0, 0, 0, 0, 0};
+            for (int p : pending) busy[b->launches[(size_t)p].stream]++;
+            for (int k = 4; k < 6 && idle < 0; k++)
+                if (!busy[k]) idle = k;
+            if (idle < 0) {
+                ++it;
+                continue;
+            }
+        } else {
+            idle = b->launches[(size_t)it->first].stream;
+        }
+        const int rc = submit_groups(b, it->second, idle, pending);
+        if (rc) return rc;
+        it = b->early_groups.erase(it);
+    }
+    return MT_OK;
+}
+
+// Capacity escalation, scheduled as launches complete: a checkpointed document resumes, a
+// document that overflowed mid-op re-runs from scratch, both in the next class with >= 1.2x the
+// slots (docs per CU matter more than the number of resumes: each resume costs one LDS image
+// round trip to HBM).  When a launch finishes, its escalated documents are grouped by target
+// class and launched at once on the next of the run / aux streams, so a large document's chain
+// of classes never waits for unrelated launches (mixed-size batches, config 4).
+// The launch goes on the stream with the fewest pending launches (ties: `prefer`, the stream of
+// the launch that just finished, which is idle): a stream still running an unrelated launch would
+// queue it behind that launch's tail.  (Keeping escalations off the run stream, which joins every
+// first launch, measured +0.4 % but made rocprofv3's kernel trace serialize the two chains' aux
+// queues, so its kernel durations no longer matched the bench's)
 MT_API int mt_batch_sync(mt_batch *b) {
     if (!b || b->launches.empty()) return MT_ERR_STATE;
     std::vector<int> pending;
@@ -1958,12 +2193,20 @@ MT_API int mt_batch_sync(mt_batch *b) {
                 if (q != hipErrorNotReady) HIPCHK(q);
             }
             if (k < pending.size()) break;
+            if (b->notice_cap) {
+                rc = poll_notices(b, pending, -1);
+                if (rc) return rc;
+            }
         }
         const int li = pending[k];
         pending.erase(pending.begin() + (long)k);
         {
             Launch &L = b->launches[(size_t)li];
             HIPCHK(hipEventElapsedTime(&L.ms, L.e0, L.e1));
+        }
+        if (b->notice_cap && b->launches[(size_t)li].notice) {  // its last entries, and what waits of it
+            rc = poll_notices(b, pending, li);
+            if (rc) return rc;
         }
         static const bool host_timing = getenv("MT_HOST_TIMING") != nullptr;
         const auto th0 = std::chrono::steady_clock::now();
@@ -1982,100 +2225,46 @@ MT_API int mt_batch_sync(mt_batch *b) {
         // launch_on appends to b->launches, so S dangles after the first one: what the escalations
         // need of it is copied here
         const int prefer = S.stream;
-        const bool s_big = S.big;
+        const Launch Sc = [&] {
+            Launch c;
+            c.cls = S.cls;
+            c.big = S.big;
+            c.load = S.load;
+            c.d_ck = S.d_ck;
+            c.level = S.level;
+            return c;
+        }();
         const int64_t n = launch_n(b->n_docs, S);
+        std::vector<int32_t> sdocs = S.docs;
+        // documents poll_notices took from this launch (a launch's escalated documents are not)
+        const bool notice = S.notice;
         std::map<int, Launch> groups;  // by target class, x2 + 1 for the bigprops kernel
+        auto doc_of = [&](int64_t i) { return sdocs.empty() ? i : (int64_t)sdocs[(size_t)i]; };
         int64_t n_ck = 0;
         for (int64_t i = 0; i < n; i++) {
-            const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
-            n_ck += b->docout[d].status == MT_CAPACITY && b->where[d].launch == li;
+            const int64_t d = doc_of(i);
+            n_ck += b->docout[d].status == MT_CAPACITY && b->where[d].launch == li && !(notice && b->taken[(size_t)d]);
         }
         for (int64_t i = 0; i < n; i++) {
-            const int64_t d = S.docs.empty() ? i : S.docs[(size_t)i];
+            const int64_t d = doc_of(i);
             const DocOut &o = b->docout[d];
-            if (o.status != MT_CAPACITY || b->where[d].launch != li) continue;
-            int32_t src;
-            if (o.cap_kind == mt::kCapCheckpoint && S.d_ck) src = (int32_t)i;
-            else if (o.cap_kind == 1 || o.cap_kind == 4 || o.cap_kind == mt::kCapLongSeg ||
-                     (o.cap_kind == mt::kCapPool && !s_big))
-                src = -1;
-            else continue;
-            // a large property set: the same class again, from scratch, in the bigprops kernel
-            // (the observer kernels of the LDS classes stop on large sets with kCapPool; the writer,
-            // load and spill-class kernels hold them, so there it is a full pool: terminal)
-            const bool to_big = o.cap_kind == mt::kCapPool;
-            if (to_big && (s_big || b->writer || S.load || mt::is_hbm_seg(mt::kClassSegs[S.cls]))) continue;
-            const bool big = s_big || to_big;
-            int cls = to_big ? S.cls : resume_class(S.cls);
-            // a tail document checkpointed for overlay-list room (a wide collab window; the list grows
-            // only by seg/16 per class) steps to the first class with ~64 entries to spare instead of one
-            // class at a time, each step a serial launch of its own.  Only in a tail (a launch too small
-            // to fill the chip at the bigger class): with many documents escalating, the smaller class's
-            // residency wins.
-            static const bool ulist_jump = !getenv("MT_ULIST_JUMP") || atoi(getenv("MT_ULIST_JUMP")) > 0;
-            if (ulist_jump && n_ck <= kTailDocs && o.cap_kind == mt::kCapCheckpoint && S.cls < mt::kLastLdsClass &&
-                o.max_oe + 24 > (int32_t)mt::class_caps(mt::kClassSegs[S.cls]).ulist)
-                while (cls < mt::kLastLdsClass && (int32_t)mt::class_caps(mt::kClassSegs[cls]).ulist < o.max_oe + 64) cls++;
-            while (cls > S.cls + 1 && !class_usable(cls)) cls--;
-            // a segment beyond 16-bit lengths: re-run from scratch in the giant class (32-bit lengths)
-            if (o.cap_kind == mt::kCapLongSeg) cls = long_seg_class(S.cls);
-            if (!class_usable(cls)) continue;  // largest class reached: the document keeps MT_CAPACITY
+            if (o.status != MT_CAPACITY || b->where[d].launch != li || (notice && b->taken[(size_t)d])) continue;
+            int cls = 0;
+            bool big = false;
+            int32_t src = -1;
+            if (!escalation_target(b, Sc, o, n_ck, (int32_t)i, &cls, &big, &src)) continue;
             Launch &L = groups[2 * cls + (big ? 1 : 0)];
             L.cls = cls;
             L.big = big;
             L.src = li;
-            L.level = S.level + 1;
+            L.level = Sc.level + 1;
             L.docs.push_back((int32_t)d);
             L.cksrc.push_back(src);
         }
-        // longest remaining replay first (LPT): workgroups dispatch roughly in index order, so the
-        // documents with the most ops left start first and the launch's tail is short (MT_LPT=0: the
-        // previous launch's order)
-        static const bool lpt = !getenv("MT_LPT") || atoi(getenv("MT_LPT")) > 0;
-        for (auto &kv : groups) {
-            Launch &G = kv.second;
-            if (!lpt) continue;
-            std::vector<std::pair<int64_t, size_t>> key(G.docs.size());
-            for (size_t k = 0; k < G.docs.size(); k++) {
-                const int32_t d = G.docs[k];
-                const int64_t n_ops = b->h_off[(size_t)d + 1] - b->h_off[(size_t)d];
-                key[k] = {G.cksrc[k] >= 0 ? n_ops - b->docout[(size_t)d].ops_done : n_ops, k};
-            }
-            std::stable_sort(key.begin(), key.end(), [](const std::pair<int64_t, size_t> &x, const std::pair<int64_t, size_t> &y) {
-                return x.first > y.first;
-            });
-            std::vector<int32_t> docs(G.docs.size()), cks(G.cksrc.size());
-            for (size_t k = 0; k < key.size(); k++) {
-                docs[k] = G.docs[key[k].second];
-                cks[k] = G.cksrc[key[k].second];
-            }
-            G.docs.swap(docs);
-            G.cksrc.swap(cks);
-        }
-        for (auto &kv : groups) {
-            Launch &G = kv.second;
-            // the HBM class holds ~220 MB per document: bounded launches
-            const size_t chunk = launch_chunk(G.cls, G.docs.size());
-            for (size_t at = 0; at < G.docs.size(); at += chunk) {
-                Launch L;
-                L.cls = G.cls;
-                L.big = G.big;
-                L.src = G.src;
-                L.level = G.level;
-                const size_t e = std::min(G.docs.size(), at + chunk);
-                L.docs.assign(G.docs.begin() + (long)at, G.docs.begin() + (long)e);
-                L.cksrc.assign(G.cksrc.begin() + (long)at, G.cksrc.begin() + (long)e);
-                const auto tl0 = std::chrono::steady_clock::now();
-                rc = launch_on(b, std::move(L), prefer, pending);
-                if (rc) return rc;
-                if (host_timing)
-                    fprintf(stderr, "MT_HOST   launch %d (class %d, %zu docs, stream %d) submitted at %.1f ms host (%.2f ms)\n",
-                            (int)b->launches.size() - 1, mt::kClassSegs[G.cls], e - at, b->launches.back().stream,
-                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b->t_launch).count(),
-                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl0).count());
-            }
-        }
+        rc = submit_groups(b, groups, prefer, pending);
+        if (rc) return rc;
     }
+    if (!b->early_groups.empty()) return MT_INTERNAL;  // (flushed when their source launch completed)
     // device wall time: from the first launch to the last completion
     float ms = 0, mx = 0;
     for (const Launch &L : b->launches) {

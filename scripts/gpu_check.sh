@@ -42,6 +42,13 @@ for step in "$@"; do
     b3s_var) run b3s_var 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_var.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     b3full) run b3full 600 python -u bench.py --steps 3 --warmup 1 --no-cpu ;;
     b3full_var) run b3full_var 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_var.so python -u bench.py --steps 3 --warmup 1 --no-cpu ;;
+    c2) run c2 600 python -u bench.py --config 2 --steps 5 --warmup 2 ;;
+    earlytest) run earlytest 300 python -u -m pytest tests/test_gpu_parity.py -k "early_escalation or several_classes or escalation" -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    c2w) run c2w 600 python -u bench.py --config 2 --writers --steps 3 --warmup 1 ;;
+    c2wne) run c2wne 600 env MT_EARLY_ESCALATION=0 python -u bench.py --config 2 --writers --steps 3 --warmup 1 --no-cpu ;;
+    c5ne) run c5ne 900 env MT_EARLY_ESCALATION=0 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
+    c5) run c5 900 python -u bench.py --config 5 --steps 3 --warmup 1 ;;
+    c4) run c4 900 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     b3s_old) run b3s_old 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_old.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     giantrate) run giantrate 600 python -u tools/hbm_phases.py 100000 8 2000000 ;;
     giantrate_nopf) run giantrate_nopf 600 env MT_GIANT_PREFETCH=0 python -u tools/hbm_phases.py 100000 8 2000000 ;;

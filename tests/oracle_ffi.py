@@ -334,9 +334,10 @@ def gen_doc(p: GenParams, doc: int):
     return ops, text[: tl.value].copy(), props[: npr.value].copy()
 
 
-def gen_batch(p: GenParams, n_docs: int, first_doc: int = 0, doc_ids=None, doc_ops=None):
+def gen_batch(p: GenParams, n_docs: int, first_doc: int = 0, doc_ids=None, doc_ops=None, doc_params=None):
     """Concatenate generated docs with absolute offsets (the C-ABI batch layout).  doc_ids /
-    doc_ops: per-document global indices and op counts (mt_batch_generate_docs)."""
+    doc_ops: per-document global indices and op counts (mt_batch_generate_docs); doc_params:
+    per-document GenParams (mixed batches)."""
     all_ops, all_text, all_props, off = [], [], [], [0]
     t_base = p_base = 0
     ids = list(doc_ids) if doc_ids is not None else list(range(first_doc, first_doc + n_docs))
@@ -345,6 +346,8 @@ def gen_batch(p: GenParams, n_docs: int, first_doc: int = 0, doc_ids=None, doc_o
         if doc_ops is not None:
             pj = GenParams(*[getattr(p, f) for f, _ in GenParams._fields_])
             pj.n_ops = int(doc_ops[j])
+        if doc_params is not None:
+            pj = doc_params[j]
         ops, text, props = gen_doc(pj, int(dd))
         ins = (ops["tc"] & 0xF) == 0
         ops["payload"][ins] += t_base

@@ -573,6 +573,39 @@ def test_one_launch_escalating_into_several_classes():
             assert_doc_parity(b.doc(i), oracle[i])
 
 
+def test_early_escalation_while_the_first_launch_runs():
+    """A batch whose first launch fits nearly every document (2,048 of 1,500 ops in class 464) and a
+    few wide-window documents (refSeq lag up to 1,500: the overlay list outgrows the class within
+    a few hundred ops).  Those append an early-escalation notice (mt_engine.hip escalation_notice)
+    and the host starts their next launch while the first one still runs (mt_host.cpp
+    poll_notices); every document equals the oracle, and the first launch's ops exclude the
+    escalated documents' resumed part exactly once."""
+    n_small, wide_at = 2048, (5, 700, 1400, 2047)
+    small = O.gen_params(1500, pct_insert=55, pct_remove=35, seed=0xEA51)
+    wide = O.gen_params(1500, max_lag=1500, pct_insert=55, pct_remove=35, seed=0xEA52)
+    params = [wide if d in wide_at else small for d in range(n_small)]
+    ops, text, props, off = O.gen_batch(small, n_small, doc_params=params)
+    t, names = O.gen_tables(), O.gen_client_names(small.n_clients)
+    _, dig, st = O.replay_batch(ops, off, text, props, t, names)
+    with fa.ReplayBatch(n_small) as b:
+        b.set_tables(GEN_KEYS, GEN_VALUES)
+        b.set_clients(names)
+        b.ingest(ops, off, text, props)
+        b.run()
+        launches = b.launches()
+        first = launches[0]
+        assert first["seg_class"] == 464 and first["n_docs"] == n_small, launches
+        early = [li for li in launches[1:] if li["start_ms"] < first["start_ms"] + first["ms"]]
+        assert early, launches
+        # (a document re-run from scratch counts its first partial replay too)
+        if all(li["resumed"] == li["n_docs"] for li in launches[1:]):
+            assert sum(li["ops"] for li in launches) == len(ops), launches
+        for d in range(n_small):
+            dv = b.doc(d)
+            assert dv.status == st[d] == 0, d
+            assert dv.digest() == int(dig[d]), d
+
+
 def test_giant_document_beyond_65k_segments():
     """A document far beyond the LDS classes and 16-bit ids (>= 100k live segments; SURVEY §8d
     config 4's tail) escalates through the ladder into the giant class (2M slots, 32-bit slot and
