@@ -435,6 +435,10 @@ struct ReplayParams {
     uint32_t *notice;             // host memory (4 words per entry), or null
     uint32_t *notice_count;
     int32_t launch_id;
+    // writer replicas escalated early (mt_host.cpp poll_notices): their waves raise their issue
+    // priority, so a replica outgrowing its first class replays beside that launch's waves at close
+    // to its rate alone instead of becoming the step's tail
+    int32_t urgent;
 };
 constexpr uint32_t kIdUnlinked = 0xFFFFFFFFu;
 constexpr uint32_t kIdKeyUnsupported = 0xFFFFFFFFu;  // RELPOS key the host cannot resolve safely

@@ -3716,15 +3716,19 @@ struct Engine {
     // ------------------------------------------------------------------ checkpoint / resume
     // LDS headroom for one more op (two splits + an insert, a split cascade per leaf insert,
     // a range op's heap / overlay pushes, a pack); below it the document is checkpointed and
-    // resumed in a larger capacity class instead of failing mid-op.
+    // resumed in a larger capacity class instead of failing mid-op.  (The overlay list keeps 16
+    // entries, as the heap does: an op pushes one per segment it makes unsettled, and one that
+    // pushes more fails with cap_kind 1 and re-runs from scratch in the next class.  24 sent a
+    // writer replica of config 2 that peaks at 187 of class 464's 208 entries into a second launch
+    // of its own, the step's tail)
     MT_FI bool low_headroom() const {
         const int32_t fs = cap.seg - slot_top + free_n;
         if constexpr (kSplitPools) {
             const int32_t fl = kLB - blk_top + n_bfree, fi = cap.iblk - lds_top + n_lfree;
-            return fs < 6 || fl < 16 || fi < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 24;
+            return fs < 6 || fl < 16 || fi < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 16;
         }
         const int32_t fb = cap.blk - blk_top + n_bfree;
-        return fs < 6 || fb < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 24;
+        return fs < 6 || fb < 2 * depth + 10 || cap.heap - hn < 16 || cap.ulist - nu < 16;
     }
     template <typename A>
     MT_FI void dump(uint32_t *&p, const A &src, int32_t n) {
@@ -4430,6 +4434,8 @@ MT_FI void replay_body(const ReplayParams &P) {
     const int64_t w = (int64_t)blockIdx.x;
     if (w >= P.n_docs) return;
     const int64_t d = P.doc_list ? (int64_t)P.doc_list[w] : w;
+    if constexpr (kW && !notice_class(SEG))  // (an early escalation runs in a later class)
+        if (P.urgent) __builtin_amdgcn_s_setprio(3);
     if constexpr (is_giant_seg(SEG) && !kLoad && !kW && !kBigK) {
         extern __shared__ __attribute__((aligned(16))) uint8_t gsmem[];
         uint32_t *pub = (uint32_t *)(gsmem + make_glayout().pub);

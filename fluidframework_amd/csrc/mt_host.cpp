@@ -114,6 +114,7 @@ struct Launch {
     bool big = false;           // observer documents with large property sets: mt_bigprops_kernel_<SEG>
     bool notice = false;        // appends early-escalation entries (mt_batch.h_notice)
     bool gathered = false;      // its results are gathered: later entries of it are not taken
+    bool urgent = false;        // an early escalation (ReplayParams.urgent)
     int64_t early_ops = 0;      // ops of its documents that escalated early (poll_notices)
 };
 
@@ -1636,6 +1637,8 @@ static int launch_replay(mt_batch *b, hipStream_t s, Launch &L) {
     P.cold = L.d_cold;
     P.hbm_state = L.d_state;
     P.ck_out = L.d_ck;
+    static const bool urgent_ok = !getenv("MT_EARLY_SETPRIO") || atoi(getenv("MT_EARLY_SETPRIO")) > 0;
+    P.urgent = L.urgent && urgent_ok ? 1 : 0;
     if (L.notice) {
         P.notice = b->d_notice;
         P.notice_count = b->d_notice_count;
@@ -2036,7 +2039,7 @@ static bool escalation_target(const mt_batch *b, const Launch &S, const DocOut &
     // residency wins.
     static const bool ulist_jump = !getenv("MT_ULIST_JUMP") || atoi(getenv("MT_ULIST_JUMP")) > 0;
     if (ulist_jump && n_ck <= kTailDocs && o.cap_kind == mt::kCapCheckpoint && S.cls < mt::kLastLdsClass &&
-        o.max_oe + 24 > (int32_t)mt::class_caps(mt::kClassSegs[S.cls]).ulist)
+        o.max_oe + 16 > (int32_t)mt::class_caps(mt::kClassSegs[S.cls]).ulist)
         while (cls < mt::kLastLdsClass && (int32_t)mt::class_caps(mt::kClassSegs[cls]).ulist < o.max_oe + 64) cls++;
     while (cls > S.cls + 1 && !class_usable(cls)) cls--;
     // a segment beyond 16-bit lengths: re-run from scratch in the giant class (32-bit lengths)
@@ -2086,6 +2089,7 @@ static int submit_groups(mt_batch *b, std::map<int, Launch> &groups, int prefer,
             L.src = G.src;
             L.level = G.level;
             const size_t e = std::min(G.docs.size(), at + chunk);
+            L.urgent = G.urgent;
             L.docs.assign(G.docs.begin() + (long)at, G.docs.begin() + (long)e);
             L.cksrc.assign(G.cksrc.begin() + (long)at, G.cksrc.begin() + (long)e);
             const auto tl0 = std::chrono::steady_clock::now();
@@ -2144,6 +2148,7 @@ static int poll_notices(mt_batch *b, std::vector<int> &pending, int flush_src) {
         G.big = big;
         G.src = li;
         G.level = S.level + 1;
+        G.urgent = true;
         G.docs.push_back((int32_t)d);
         G.cksrc.push_back(src);
     }

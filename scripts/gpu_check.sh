@@ -45,6 +45,7 @@ for step in "$@"; do
     c2) run c2 600 python -u bench.py --config 2 --steps 5 --warmup 2 ;;
     earlytest) run earlytest 300 python -u -m pytest tests/test_gpu_parity.py -k "early_escalation or several_classes or escalation" -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     c2w) run c2w 600 python -u bench.py --config 2 --writers --steps 3 --warmup 1 ;;
+    c2wnsp) run c2wnsp 600 env MT_EARLY_SETPRIO=0 python -u bench.py --config 2 --writers --steps 3 --warmup 1 --no-cpu ;;
     c2wne) run c2wne 600 env MT_EARLY_ESCALATION=0 python -u bench.py --config 2 --writers --steps 3 --warmup 1 --no-cpu ;;
     c5ne) run c5ne 900 env MT_EARLY_ESCALATION=0 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
     c5) run c5 900 python -u bench.py --config 5 --steps 3 --warmup 1 ;;
