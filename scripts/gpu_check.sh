@@ -49,6 +49,7 @@ for step in "$@"; do
     c2wne) run c2wne 600 env MT_EARLY_ESCALATION=0 python -u bench.py --config 2 --writers --steps 3 --warmup 1 --no-cpu ;;
     c5ne) run c5ne 900 env MT_EARLY_ESCALATION=0 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu ;;
     c5) run c5 900 python -u bench.py --config 5 --steps 3 --warmup 1 ;;
+    fullpar) run fullpar 900 python -u tools/full_parity.py 65536 8192 gpurun_out/full_parity_config3.json ;;
     c4) run c4 900 python -u bench.py --config 4 --steps 1 --warmup 0 ;;
     b3s_old) run b3s_old 600 env FLUIDFRAMEWORK_AMD_LIB=fluidframework_amd/libmtreplay_old.so python -u bench.py --config 3 --docs 8192 --steps 2 --warmup 1 --no-cpu ;;
     giantrate) run giantrate 600 python -u tools/hbm_phases.py 100000 8 2000000 ;;
