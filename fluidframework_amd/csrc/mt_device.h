@@ -202,17 +202,20 @@ constexpr int kCapLongSeg = 8;     // beyond an LDS class's 16-bit lengths or re
 // a pending-group region in HBM, persistent across launches (u32 words):
 //   [0] pending groups n   [1] id G of the oldest (groups are numbered in creation order)
 //   [2] first entry that may be live   [3] entries used
-//   [kPendDesc ..) per group G, at G mod kPendMaxGroups: {type | flags << 16, prop-record offset,
+//   [kPendDesc ..) per group G, at G mod pend_groups(cap): {type | flags << 16, prop-record offset,
 //                  prop count, localSeq}
-//   [kPendEntries ..) entries {G, slot} in append order (the group's `segments` array order:
-//   members as the op reached them, split-off halves appended when the split happens)
+//   [pend_entries(cap) ..) `cap` entries {G, slot} in append order (the group's `segments` array
+//   order: members as the op reached them, split-off halves appended when the split happens)
 //   word 4: collabWindow.localSeq (one per applied local op); a group's desc .w = its localSeq
-// unacked local ops at once (more: MT_UNSUPPORTED).  A segment's groups are the bits G & 31 of a
-// 32-bit mask in its cold record: exact while at most 32 groups are pending; beyond, a bit stands
-// for every live group 64 apart and membership is decided by the groups' entry lists
-constexpr int kPendMaxGroups = 1024;
+// `cap` (ReplayParams.pend_cap) is a power of two the host sizes from the log (mt_host.cpp
+// writer_regions: 4 entries per group of the most unacked local ops any replica holds, at least
+// 4,096); cap / 4 groups may be pending at once (more: MT_UNSUPPORTED, only if the log's own count
+// was exceeded).  A segment's groups are the bits G & 31 of a 32-bit mask in its cold record: exact
+// while at most 32 groups are pending; beyond, a bit stands for every live group 32 apart and
+// membership is decided by the groups' entry lists
 constexpr int kPendDesc = 8;
-constexpr int kPendEntries = kPendDesc + 4 * kPendMaxGroups;
+__host__ __device__ constexpr uint32_t pend_groups(int32_t cap) { return (uint32_t)cap >> 2; }
+__host__ __device__ constexpr uint32_t pend_entries(int32_t cap) { return (uint32_t)kPendDesc + 4u * pend_groups(cap); }
 constexpr int kCapPending = 9;  // DocOut.cap_kind: the pending-entry region is full (terminal)
 constexpr int kCapRegen = 10;   // DocOut.cap_kind: the regenerated-op output region is full (terminal)
 // DocOut.cap_kind 3 (the prop pool) from an observer replay kernel of an LDS class: a property set or
@@ -221,7 +224,7 @@ constexpr int kCapRegen = 10;   // DocOut.cap_kind: the regenerated-op output re
 // the bigprops kernels; a full pool stops it there again (terminal).  (A kind of its own measured
 // worse: the distinct constant alone moved class 756's SGPR spills from 182 to 260.)
 constexpr int kCapPool = 3;
-constexpr int64_t pend_words(int32_t cap) { return kPendEntries + 2ll * cap; }
+constexpr int64_t pend_words(int32_t cap) { return (int64_t)pend_entries(cap) + 2ll * cap; }
 // regenerated ops of MT_OP_REGENERATE records, per document (u32 words): [0] words used (from 2),
 // [1] records; per record {GROUP_CONT flag, ops} then per op {type, pos1, pos2, a, b, c, nprops, 0}
 // + nprops (key, value) pairs.  insert: a = 1 | refType << 1 for a Marker (else 0), b = text offset

@@ -302,7 +302,7 @@ struct Engine {
     // marker ids (idToSegment) and the positions an MT_OP_RELPOS record resolved for the next op
     LWord<int32_t> idmap_n, rel_pend, rel_p1, rel_p2;
     uint2 *idmap;
-    // writer replicas: the document's pending-group region (mt_device.h kPendDesc / kPendEntries)
+    // writer replicas: the document's pending-group region (mt_device.h kPendDesc / pend_entries)
     // and its group count (kept in HBM word 0 as well, so checkpoints carry it)
     uint32_t *pend;
     int32_t pend_cap_e, n_pend;
@@ -1462,7 +1462,7 @@ struct Engine {
 
     // ------------------------------------------------------------------ writer: pending segment groups
     // MergeTree.pendingSegments / SegmentGroup (mergeTree.ts:1093, 1922-1929) in the document's HBM
-    // region (mt_device.h kPendDesc / kPendEntries); lane 0 writes, every lane reads back.
+    // region (mt_device.h kPendDesc / pend_entries); lane 0 writes, every lane reads back.
     MT_FI uint32_t pend_word(int i) const { return rfl(pend[i]); }
     static constexpr uint32_t kPmb = (uint32_t)kPendMaskBits - 1u;  // group G's mask bit: G & kPmb
     MT_FI uint32_t pend_mask(uint32_t slot) const { return rfl(cold[2 * slot + 1].w); }
@@ -1472,7 +1472,7 @@ struct Engine {
         s_meta[slot] = (Meta)(m ? (meta | kFPending) : (meta & ~kFPending));
         wsync();
     }
-    MT_FI uint32_t *pdesc(uint32_t G) const { return pend + kPendDesc + 4 * (G & (uint32_t)(kPendMaxGroups - 1)); }
+    MT_FI uint32_t *pdesc(uint32_t G) const { return pend + kPendDesc + 4 * (G & (pend_groups(pend_cap_e) - 1u)); }
     // is `slot` (pending mask m) a member of the live group G?  The mask bit decides while at most 32
     // groups are pending; beyond, groups 32 apart share a bit and G's entries decide
     MT_FI bool in_group(uint32_t G, uint32_t slot, uint32_t m) {
@@ -1481,7 +1481,7 @@ struct Engine {
     }
     MT_FI bool entry_has(uint32_t G, uint32_t slot) {
         const uint32_t start = pend_word(2), n = pend_word(3);
-        const uint2 *E = (const uint2 *)(pend + kPendEntries);
+        const uint2 *E = (const uint2 *)(pend + pend_entries(pend_cap_e));
         for (uint32_t b0 = start; b0 < n; b0 += kWave) {
             const uint32_t j = b0 + (uint32_t)lane;
             bool hit = false;
@@ -1518,7 +1518,7 @@ struct Engine {
     // live entries (of pending groups) move to the front, in order
     MT_FI void pend_compact() {
         const uint32_t head = pend_word(1), start = pend_word(2), n = pend_word(3);
-        uint2 *E = (uint2 *)(pend + kPendEntries);
+        uint2 *E = (uint2 *)(pend + pend_entries(pend_cap_e));
         uint32_t w = 0;
         for (uint32_t b0 = start; b0 < n; b0 += kWave) {
             const uint32_t j = b0 + (uint32_t)lane;
@@ -1545,7 +1545,7 @@ struct Engine {
             }
         }
         if (lane == 0) {
-            ((uint2 *)(pend + kPendEntries))[n] = make_uint2(G, slot);
+            ((uint2 *)(pend + pend_entries(pend_cap_e)))[n] = make_uint2(G, slot);
             pend[3] = n + 1u;
         }
     }
@@ -1555,7 +1555,7 @@ struct Engine {
     MT_FI void pend_add(uint32_t slot, const mt_op &op) {
         resolve_cold();  // the split halves' cold records (pending masks) are in HBM
         if (cur_g < 0) {
-            if (n_pend >= kPendMaxGroups) {
+            if (n_pend >= (int32_t)pend_groups(pend_cap_e)) {
                 set_fail(ST_UNSUPPORTED);
                 return;
             }
@@ -1643,7 +1643,7 @@ struct Engine {
                 for (uint32_t k = 0; same && k < g_cnt; k++) same = key_among(o_off, o_cnt, rfl(props_in[g_off + k].key));
             }
             const uint32_t start = pend_word(2), n = pend_word(3);
-            const uint2 *E = (const uint2 *)(pend + kPendEntries);
+            const uint2 *E = (const uint2 *)(pend + pend_entries(pend_cap_e));
             for (uint32_t b0 = start; b0 < n; b0 += kWave) {
                 const uint32_t j = b0 + (uint32_t)lane;
                 const uint2 e = j < n ? E[j] : make_uint2(head + 1u, 0u);
@@ -3593,7 +3593,7 @@ struct Engine {
                     used += words;
                     nops++;
                     // the new group of this segment alone (same localSeq), queued last
-                    if (n_pend >= kPendMaxGroups) {
+                    if (n_pend >= (int32_t)pend_groups(pend_cap_e)) {
                         set_fail(ST_UNSUPPORTED);
                         return;
                     }

@@ -946,13 +946,18 @@ static void rc_resolve_combine(mt_batch *b, const mt_op *ops, int64_t N, const m
 }
 
 // The device regions of a writer batch (a log with local ops or acks): pending-group regions
-// (MT_PEND_CAP entries per document, default 4096: the live entries of at most kPendMaxGroups
-// unacked ops, compacted when full), regenerated-op output (MT_REGEN_CAP words per document with
-// MT_OP_REGENERATE records, default 16384, 2 for the others) and the consensus regions.
+// (a power of two of entries per document, mt_device.h pend_groups: at least 4,096 or MT_PEND_CAP,
+// and 4 per group of `max_pending`, the most unacked local ops any replica of the log holds —
+// the live entries, compacted when full), regenerated-op output (MT_REGEN_CAP words per document
+// with MT_OP_REGENERATE records, default 16384, 2 for the others) and the consensus regions.
 static int writer_regions(mt_batch *b, int64_t D, const std::vector<uint8_t> &has_regen,
-                          std::vector<uint64_t> &cons_base, const std::vector<uint32_t> &cons_img) {
+                          std::vector<uint64_t> &cons_base, const std::vector<uint32_t> &cons_img,
+                          int64_t max_pending = 0) {
     const char *e = getenv("MT_PEND_CAP");
-    b->pend_cap = e && atoi(e) > 0 ? atoi(e) : 4096;
+    int64_t want = std::max<int64_t>(e && atoi(e) > 0 ? atoi(e) : 4096, 4 * (max_pending + 64));
+    int64_t cap = 4096;
+    while (cap < want && cap < (int64_t)1 << 28) cap <<= 1;
+    b->pend_cap = (int32_t)cap;
     const uint64_t words = (uint64_t)mt::pend_words(b->pend_cap);
     std::vector<uint64_t> pbase_((size_t)D + 1);
     for (int64_t d = 0; d <= D; d++) pbase_[(size_t)d] = (uint64_t)d * words;
@@ -1208,10 +1213,18 @@ MT_API int mt_batch_ingest(mt_batch *b, const mt_op *ops, const int64_t *doc_op_
     HIPCHK(hipMemcpy(b->d_idmap_base, idmap_base.data(), 8 * ((size_t)D + 1), hipMemcpyHostToDevice));
     if (writer) {
         std::vector<uint8_t> has_regen((size_t)D, 0);
-        for (int64_t d = 0; d < D; d++)
-            for (int64_t i = b->h_off[(size_t)d]; i < b->h_off[(size_t)d + 1] && !has_regen[(size_t)d]; i++)
-                has_regen[(size_t)d] = ops[i].type == MT_OP_REGENERATE;
-        const int rc2 = writer_regions(b, D, has_regen, cons_base, cons_img);
+        // the most groups a replica can hold pending: local records less the acks (its own
+        // sequenced records) before them, at the peak (an upper bound; a regenerate replaces groups)
+        int64_t max_pending = 0;
+        for (int64_t d = 0; d < D; d++) {
+            int64_t pend = 0;
+            for (int64_t i = b->h_off[(size_t)d]; i < b->h_off[(size_t)d + 1]; i++) {
+                has_regen[(size_t)d] |= ops[i].type == MT_OP_REGENERATE;
+                if (ops[i].seq == MT_SEQ_LOCAL) max_pending = std::max(max_pending, ++pend);
+                else if (ops[i].seq > 0 && MT_OP_CLIENT(ops[i]) == 0 && pend > 0) pend--;
+            }
+        }
+        const int rc2 = writer_regions(b, D, has_regen, cons_base, cons_img, max_pending);
         if (rc2) return rc2;
     }
     HIPCHK(hipMemcpy(b->d_ops, h_ops.data(), sizeof(mt_op) * (size_t)N, hipMemcpyHostToDevice));

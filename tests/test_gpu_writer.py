@@ -20,7 +20,6 @@ pytestmark = pytest.mark.gpu
 
 GEN_KEYS = [O.lib().mto_gen_key_name(k).decode() for k in range(4)]
 ST_BAD_INPUT = 5  # mt_device.h: an assert of the reference (here: in the ack path)
-PEND_MAX_GROUPS = 1024  # unacked local ops a GPU replica holds at once (mt_device.h kPendMaxGroups)
 GEN_VALUES = [O.lib().mto_gen_value_json(v).decode() for v in range(22)]
 
 
@@ -123,7 +122,7 @@ def test_writer_with_hundreds_of_pending_ops(seg_cap):
     """An offline burst / reconnect storm: writer A issues 300 local ops (inserts, removes,
     annotates, rewrites; splits of pending segments) before its first ack while B and C edit and
     sequence concurrently, then A catches up.  Beyond 64 pending groups the segments' mask bits are
-    shared by groups 64 apart (mt_device.h kPendMaxGroups) and the entry lists decide membership:
+    shared by groups 32 apart (mt_device.h pend_groups) and the entry lists decide membership:
     every replica equals the oracle's, also through checkpoint / resume with the groups in flight."""
     from writer_sim import Farm, random_op
 
@@ -137,6 +136,25 @@ def test_writer_with_hundreds_of_pending_ops(seg_cap):
     f.finish()
     assert max_pending("A", f.events["A"]) > 250
     _farm_parity(f, **({"seg_cap": seg_cap, "max_retries": 24} if seg_cap else {}))
+
+
+def test_writer_beyond_1024_pending_ops():
+    """More unacked local ops than round 5's fixed 1,024-group region: writer A issues 1,500 local
+    ops before its first ack while B and C edit concurrently.  The host sizes the pending-group
+    region from the log (mt_host.cpp writer_regions: the replica's peak of local records less acks,
+    mt_device.h pend_groups) and the replica equals the oracle's."""
+    from writer_sim import Farm, random_op
+
+    f = Farm(3, 1501)
+    for i in range(1500):
+        f.local("A", random_op(f.rng, f.docs["A"].length(), rewrite=5))
+        if i % 10 == 0:
+            o = f.rng.choice(["B", "C"])
+            f.local(o, random_op(f.rng, f.docs[o].length()))
+            f.deliver(o, 1 + f.rng.randrange(3))
+    f.finish()
+    assert max_pending("A", f.events["A"]) > 1024
+    _farm_parity(f)
 
 
 @pytest.mark.parametrize("seed,n_clients,steps,rewrite", [(1, 3, 400, 0), (2, 6, 900, 10), (3, 8, 1500, 25)])
