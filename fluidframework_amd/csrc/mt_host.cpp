@@ -1501,7 +1501,10 @@ MT_API int mt_batch_ingest_json_gpu(mt_batch *b, const char *json, const int64_t
     HIPCHK(hipMemcpy(b->d_pool_cap, b->h_pool_cap.data(), 4 * (size_t)D, hipMemcpyHostToDevice));
     if (r.writer) {
         std::vector<uint64_t> cons_base((size_t)D + 1, 0);
-        rc = writer_regions(b, D, std::vector<uint8_t>((size_t)D, 0), cons_base, {});
+        int64_t max_pending = 0;
+        rc = mt::jg::pending_peak(b->d_ops, b->d_off, D, b->stream, &max_pending);
+        if (rc) return rc;
+        rc = writer_regions(b, D, std::vector<uint8_t>((size_t)D, 0), cons_base, {}, max_pending);
         if (rc) return rc;
     }
     b->have_log = true;

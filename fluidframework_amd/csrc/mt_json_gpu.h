@@ -59,6 +59,9 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
           void *stream, const TextLayout *install, mt_op **d_ops, uint16_t **d_text, uint64_t *text_words,
           mt_prop **d_props, Result &res);
 
+// the most unacked local ops any writer replica of a parsed log holds (mt_host.cpp writer_regions)
+int pending_peak(const mt_op *d_ops, const int64_t *d_off, int64_t D, void *stream, int64_t *out);
+
 }  // namespace jg
 }  // namespace mt
 

@@ -2120,5 +2120,39 @@ int parse(const char *h_json, const int64_t *doc_off, int64_t D, const uint8_t *
     return MT_OK;
 }
 
+// Writer logs parsed here: the most unacked local ops any replica holds (its local records less
+// the acks, its own sequenced records, before them, at the peak), for the pending-group region
+// (mt_host.cpp writer_regions).  One lane per document, serial over its records.
+extern "C" __global__ __launch_bounds__(64) void jg_pending_peak_kernel(const mt_op *ops, const int64_t *off, int64_t D,
+                                                                        unsigned long long *peak) {
+    const int64_t d = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (d >= D) return;
+    int64_t pend = 0, mx = 0;
+    for (int64_t i = off[d]; i < off[d + 1]; i++) {
+        const mt_op o = ops[i];
+        if (o.seq == MT_SEQ_LOCAL) mx = max(mx, ++pend);
+        else if (o.seq > 0 && MT_OP_CLIENT(o) == 0 && pend > 0) pend--;
+    }
+    if (mx) atomicMax(peak, (unsigned long long)mx);
+}
+
+int pending_peak(const mt_op *d_ops, const int64_t *d_off, int64_t D, void *stream, int64_t *out) {
+    *out = 0;
+    if (D <= 0) return MT_OK;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long *d_peak = nullptr, h = 0;
+    JGCHK(hipMalloc(&d_peak, 8));
+    int rc = MT_OK;
+    const unsigned grid = (unsigned)((D + 63) / 64);
+    void *args[] = {&d_ops, &d_off, &D, &d_peak};
+    if (hipMemsetAsync(d_peak, 0, 8, s) != hipSuccess ||
+        hipLaunchKernel((const void *)jg_pending_peak_kernel, dim3(grid), dim3(64), args, 0, s) != hipSuccess ||
+        hipMemcpyAsync(&h, d_peak, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        rc = MT_ERR_HIP;
+    (void)hipFree(d_peak);
+    *out = (int64_t)h;
+    return rc;
+}
+
 }  // namespace jg
 }  // namespace mt

@@ -456,3 +456,33 @@ def test_gpu_ingested_writer_streams_replay_like_host_and_oracle():
             ref = oracle_replica("A", ev)
             assert g.doc(d).status == 0 and g.doc(d).digest() == ref.digest(), d
             assert g.doc(d).get_text() == ref.text()
+
+
+def test_gpu_ingested_writer_beyond_1024_pending_ops():
+    """A writer stream with 1,500 unacked local ops parsed on the GPU: the device counts the
+    replica's peak of pending groups (mt_json_gpu.hip jg_pending_peak_kernel) and the pending
+    region is sized from it, so the replica equals the host-ingested batch and the oracle's."""
+    from test_gpu_writer import max_pending, oracle_replica
+    from writer_sim import Farm, random_op
+
+    f = Farm(3, 1501)
+    for i in range(1500):
+        f.local("A", random_op(f.rng, f.docs["A"].length()))
+        if i % 10 == 0:
+            o = f.rng.choice(["B", "C"])
+            f.local(o, random_op(f.rng, f.docs[o].length()))
+            f.deliver(o, 1 + f.rng.randrange(3))
+    f.finish()
+    ev = f.events["A"]
+    assert max_pending("A", ev) > 1024
+    texts = [json.dumps(ev)]
+    with fa.ReplayBatch(1) as g, fa.ReplayBatch(1) as h:
+        assert g.ingest_json(texts, observer="A", device="gpu")["path"] == "gpu"
+        h.ingest_json(texts, observer="A", device="host")
+        g.run()
+        h.run()
+        _replay_equal(g, h, 1)
+        ref = oracle_replica("A", ev)
+        assert g.doc(0).status == ref.status == 0, (g.doc(0).status, ref.status)
+        assert g.doc(0).digest() == ref.digest()
+        assert g.doc(0).get_text() == ref.text()
