@@ -41,7 +41,12 @@ extern "C" __global__ __launch_bounds__(64) void MT_CAT(mt_generate_kernel_, MT_
 #if !defined(MT_PART) || MT_PART == 2
 // writer replicas: the same replay plus the local-client path (local ops, pending segment groups,
 // acks by the replica's own sequenced messages)
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void MT_CAT(mt_writer_kernel_, MT_SEG)(mt::ReplayParams P) {
+#ifdef MT_WRITER_WPE  // (A/B: the writer kernels' own register budget)
+constexpr int kWriterWpe = kWpe > MT_WRITER_WPE ? MT_WRITER_WPE : kWpe;
+#else
+constexpr int kWriterWpe = kWpe;
+#endif
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWriterWpe))) void MT_CAT(mt_writer_kernel_, MT_SEG)(mt::ReplayParams P) {
     mt::replay_body<MT_SEG, false, true>(P);
 }
 
