@@ -322,8 +322,8 @@ def test_pending_segments_in_snapshot_and_text():
             assert_same(b.doc(i), od, n)
 
 
-def _gen_writer_parity(p, n_docs, full_every=4, **opts):
-    ops, text, props, off = O.gen_batch(p, n_docs)
+def _gen_writer_parity(p, n_docs, full_every=4, doc_params=None, launches=None, **opts):
+    ops, text, props, off = O.gen_batch(p, n_docs, doc_params=doc_params)
     t, names = O.gen_tables(), O.gen_client_names(p.n_clients)
     wops, woff, wnames = writer_batch(ops, off, names, lambda d: 1 + d % p.n_clients)
     stopped = []  # (doc, failing record)
@@ -348,6 +348,8 @@ def _gen_writer_parity(p, n_docs, full_every=4, **opts):
             if d % full_every == 0:
                 assert_same(dv, od, f"doc {d}")
         stats = b.stats()
+        if launches is not None:
+            launches.extend(b.launches())
     if stopped:
         _stopped_writer_parity(wops, woff, wnames, text, props, t, stopped, **opts)
     return stats
@@ -398,6 +400,23 @@ def test_generated_writer_logs_wide_windows():
     reference's replica would (insert failed / an ack assert), the GPU at the same record."""
     _gen_writer_parity(O.gen_params(1200, n_clients=24, max_lag=200, pct_insert=50, pct_remove=40, min_len=0,
                                     max_insert=3, seed=77), 16)
+
+
+def test_generated_writer_logs_early_escalation():
+    """1,024 writers of config-2-shaped logs that fit class 464 and 4 whose collab window (lag up to
+    400) outgrows its overlay list within a few hundred records: the first launch reports those
+    while it runs and their next class starts beside it (mt_host.cpp poll_notices; writer waves of
+    such launches raise their priority); every replica equals the oracle's."""
+    small = O.gen_params(1500, seed=0xEA53)
+    wide = O.gen_params(1500, max_lag=400, seed=0xEA54)
+    n, wide_at = 1024, (3, 300, 700, 1023)
+    launches = []
+    _gen_writer_parity(small, n, full_every=64, doc_params=[wide if d in wide_at else small for d in range(n)],
+                       launches=launches)
+    first = launches[0]
+    assert first["seg_class"] == 464 and first["n_docs"] == n, launches
+    print([(li["seg_class"], li["n_docs"], round(li["start_ms"], 2), round(li["ms"], 2)) for li in launches])
+    assert any(li["start_ms"] < first["start_ms"] + first["ms"] for li in launches[1:]), launches
 
 
 def test_observer_logs_still_run_the_observer_kernel():
